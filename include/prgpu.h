@@ -1,0 +1,152 @@
+/*
+ * prgpu.h — C-ABI of libprgpu.so, the MI355X (gfx950) implementation of
+ * proovread's hot path.  Plain pointers and sizes only; no torch / HIP types.
+ *
+ * Two stages of the reference become HIP kernels behind this ABI:
+ *
+ *  1. Consensus (pileup): what one `bam2cns` worker process does for a chunk
+ *     of long reads (bin/bam2cns:332-365 per-read loop, 375-455
+ *     generate_consensus, 461-491 detect_chimera) using the Sam::Seq engine
+ *     (lib/Sam/Seq.pm: add_aln_by_score 582-614, State_matrix 232-467,
+ *     state_matrix_consensus 1568-1654, chimera 774-889).
+ *     REPLACES: the `xargs -P T perl bam2cns ...` fan-out of
+ *     bin/proovread:1596-1619 (correct_sr_mt) — one pr_cns_run() call per
+ *     chunk (or per GPU shard of chunks).  The class globals of Sam::Seq
+ *     (Seq.pm:114-128, set at bam2cns:227-237) become pr_cns_params.
+ *
+ *  2. Seed extension + CIGAR (SW): the ksw_extend2 / ksw_global2 stage inside
+ *     `bwa-proovread mem` (called from bin/proovread:1313 run_bwa) for a batch
+ *     of (short read, long read, seed) tasks.  REPLACES: the extension and
+ *     CIGAR-generation inner loops of the absent bwa-proovread binary
+ *     (SURVEY.md §8a A2/A3), see pr_sw_run().
+ *
+ * Conventions: every function returns 0 (PR_OK) on success or a negative
+ * PR_ERR_* code; pr_last_error() returns a thread-local message.  Callers own
+ * all input buffers (copied before the call returns); output buffers are
+ * owned by the caller too (sizes are given by the *_bounds helpers).
+ * Handles are not thread-safe; use one pr_ctx per thread / device.
+ */
+#ifndef PRGPU_H
+#define PRGPU_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    PR_OK = 0,
+    PR_ERR_ARG = -1,          /* bad argument / shape                                   */
+    PR_ERR_HIP = -2,          /* HIP runtime failure (no device, OOM, launch failure)   */
+    PR_ERR_SAM = -3,          /* malformed record (CIGAR query length != SEQ length ...) */
+    PR_ERR_NOSEQ = -4,        /* SEQ '*' (bam2cns:347 "Cannot handle ... without seq")  */
+    PR_ERR_BIN_RANGE = -5,    /* alignment centre beyond last bin (Perl dies, Seq.pm:606) */
+    PR_ERR_DIV0 = -6,         /* zero-length scored alignment (Perl "Illegal division") */
+    PR_ERR_CIGAR = -7,        /* unknown CIGAR op in a kept alignment (Seq.pm:348/378/430) */
+    PR_ERR_BEYOND_REF = -8,   /* kept alignment extends past the long read end            */
+    PR_ERR_CAPACITY = -9,     /* an on-chip table overflowed (see DESIGN.md limits)       */
+    PR_ERR_UNSUPPORTED = -10, /* option not implemented on the GPU path                   */
+};
+
+const char *pr_last_error(void);
+const char *pr_version(void);
+
+/* ------------------------------------------------------------------ */
+/* device context                                                      */
+typedef struct pr_ctx pr_ctx;
+/* device: HIP device ordinal (one process per GPU; -1 = current device) */
+int pr_ctx_create(int device, pr_ctx **out);
+void pr_ctx_destroy(pr_ctx *ctx);
+int pr_device_count(int *n);
+
+/* ------------------------------------------------------------------ */
+/* consensus stage                                                     */
+
+/* Sam::Seq class globals (Seq.pm:114-128) + consensus() options.          */
+typedef struct pr_cns_params {
+    double max_coverage;      /* --coverage (bam2cns:230); proovread passes min(cov,task)*0.75 */
+    double bin_size;          /* BinSize; bam2cns always uses 20 (bam2cns:186 quirk)     */
+    int32_t trim;             /* Sam::Seq->Trim (cfg sr-trim)                            */
+    int32_t indel_taboo_length; /* cfg sr-indel-taboo-length (7); 0 => use indel_taboo    */
+    double indel_taboo;       /* cfg sr-indel-taboo (0.1)                                */
+    int32_t min_aln_length;   /* StateMatrixMinAlnLength (50)                            */
+    int32_t max_ins_length;   /* --max-ins-length                                        */
+    int32_t fallback_phred;   /* FallbackPhred (1)                                       */
+    int32_t phred_offset;     /* Sam::Seq PhredOffset (33) — consensus quality output    */
+    int32_t ref_phred_offset; /* phred offset of the reference FASTQ (--qv-offset)       */
+    int32_t use_ref_qual;     /* --[no-]use-ref-qual                                     */
+    int32_t qual_weighted;    /* --qual-weighted (not on the GPU path: PR_ERR_UNSUPPORTED) */
+    int32_t detect_chimera;   /* --detect-chimera                                        */
+    int32_t invert_scores;    /* --invert-scores (Alignment.pm InvertScores)             */
+} pr_cns_params;
+
+void pr_cns_params_default(pr_cns_params *p);
+
+/* A batch = a set of long reads (a bam2cns chunk or a GPU shard) with their
+ * alignments in BAM order.  CIGAR ops are BAM-encoded: len<<4 | op with
+ * op in {M=0,I=1,D=2,N=3,S=4,H=5,P=6,'='=7,X=8}.                          */
+enum { PR_ALN_HAS_SCORE = 1, PR_ALN_NO_QUAL = 2, PR_ALN_NO_SEQ = 4 };
+
+typedef struct pr_cns_batch {
+    int32_t n_lr;
+    const int64_t *lr_off;    /* [n_lr+1] prefix of long-read lengths                    */
+    const uint8_t *ref_seq;   /* concatenated long-read sequences (lr_off) or NULL (no --ref) */
+    const uint8_t *ref_qual;  /* concatenated qualities (lr_off) or NULL                 */
+    const int64_t *ign_off;   /* [n_lr+1] prefix into ign, or NULL (no MCR ranges)       */
+    const int32_t *ign;       /* (offset,length) pairs: MCRn:off,len tags (bam2cns:384)  */
+    const int64_t *aln_off;   /* [n_lr+1] prefix of alignment counts                     */
+    const int32_t *aln_pos;   /* 1-based POS                                             */
+    const double *aln_score;  /* AS:i value (valid if PR_ALN_HAS_SCORE)                  */
+    const uint8_t *aln_flags; /* PR_ALN_*                                                */
+    const int64_t *aln_seq_off; /* offset of SEQ (and QUAL) in seq_pool / qual_pool      */
+    const int32_t *aln_lseq;
+    const int64_t *aln_cig_off;
+    const int32_t *aln_ncig;
+    const uint8_t *seq_pool;
+    const uint8_t *qual_pool;
+    const uint32_t *cig_pool;
+    int64_t seq_pool_len, cig_pool_len;
+} pr_cns_batch;
+
+/* Output capacities for a batch (all in elements).                        */
+typedef struct pr_cns_bounds {
+    int64_t seq_cap;          /* bytes for consensus seq (and qual, and trace, cigar ops) */
+    int64_t chim_cap;         /* chimera records                                         */
+} pr_cns_bounds;
+int pr_cns_bounds_of(const pr_cns_batch *b, pr_cns_bounds *out);
+
+typedef struct pr_cns_out {
+    /* per long read, offsets into the pools are out_off[i] (from the bounds) */
+    int64_t *out_off;         /* [n_lr+1] capacity prefix (filled by the library)       */
+    int32_t *status;          /* [n_lr] PR_OK or PR_ERR_* for that read                 */
+    int32_t *seq_len;         /* [n_lr] consensus length (= qual length)                */
+    int32_t *trace_len;       /* [n_lr]                                                  */
+    int32_t *ncigar;          /* [n_lr] consensus CIGAR ops (Trace2cigar)                */
+    int32_t *nchim;           /* [n_lr] chimera records                                  */
+    uint8_t *seq;             /* [seq_cap]                                               */
+    uint8_t *qual;            /* [seq_cap] phred+phred_offset chars                      */
+    uint8_t *trace;           /* [seq_cap] M/D/I                                         */
+    uint32_t *cigar;          /* [seq_cap] len<<4|op (M=0,I=1,D=2)                      */
+    int64_t *chim_off;        /* [n_lr+1] capacity prefix of chim records                */
+    int32_t *chim;            /* [chim_cap*4] (from, to, n_pos, n_cols) per record        */
+    uint8_t *kept;            /* [n_alns] 1 if kept after binning (may be NULL)          */
+    int64_t *bin_bases;       /* optional: per-read bin fill (Seq.pm _bin_bases), reads
+                                 concatenated, int(L/bin_size)+1 bins each (may be NULL)  */
+} pr_cns_out;
+
+/* One-shot: upload, run, download (synchronous). */
+int pr_cns_run(pr_ctx *ctx, const pr_cns_params *p, const pr_cns_batch *b, pr_cns_out *o);
+
+/* Resident-batch API (bench / pipelined drivers): inputs stay in HBM. */
+int pr_cns_upload(pr_ctx *ctx, const pr_cns_batch *b);
+int pr_cns_launch(pr_ctx *ctx, const pr_cns_params *p);     /* async on ctx stream */
+int pr_cns_download(pr_ctx *ctx, pr_cns_out *o);            /* syncs               */
+/* milliseconds of the last launch's dominant (pileup) kernel, HIP events on ctx stream */
+int pr_cns_last_timing(pr_ctx *ctx, double *ms_prep, double *ms_pileup);
+/* number of columns (sum of long-read lengths) and algorithmic bytes of the resident batch
+ * (SURVEY.md §8d pileup byte model) */
+int pr_cns_resident_stats(pr_ctx *ctx, int64_t *columns, int64_t *alg_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

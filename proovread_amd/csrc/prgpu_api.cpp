@@ -1,0 +1,439 @@
+// Host side of libprgpu.so: the C-ABI declared in include/prgpu.h.
+// Device memory, one HIP stream per context, HIP events for kernel timing.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/prgpu.h"
+#include "cns_dev.h"
+#include "sw_dev.h"
+
+using namespace prgpu;
+
+static thread_local std::string g_err;
+static int set_error(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIPCHK(x)                                                                        \
+    do {                                                                                 \
+        hipError_t e_ = (x);                                                             \
+        if (e_ != hipSuccess)                                                            \
+            return set_error(PR_ERR_HIP, "%s failed: %s", #x, hipGetErrorString(e_));    \
+    } while (0)
+
+extern "C" const char *pr_last_error(void) { return g_err.c_str(); }
+extern "C" const char *pr_version(void) { return "prgpu 0.1.0 (gfx950)"; }
+
+// ---------------------------------------------------------------------------
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes ? bytes : 16;
+        if (hipMalloc(&p, want) != hipSuccess) return set_error(PR_ERR_HIP, "hipMalloc(%zu) failed", want);
+        cap = want;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+enum CnsBufId {
+    CB_LR_OFF, CB_REF_SEQ, CB_REF_QUAL, CB_IGN_OFF, CB_IGN, CB_ALN_OFF, CB_POS, CB_SCORE, CB_AFLAGS,
+    CB_SEQ_OFF, CB_LSEQ, CB_CIG_OFF, CB_NCIG, CB_SEQ, CB_CIG,
+    CB_A_ST, CB_A_LEN, CB_A_NC, CB_A_BIN, CB_A_CB, CB_A_CE, CB_A_SB, CB_A_RPOS, CB_A_END,
+    CB_SORTED, CB_LST_SCORE, CB_LST_ALN, CB_KEPT, CB_BIN_OFF, CB_BIN_BASES, CB_WORK,
+    CB_OUT_OFF, CB_CHIM_OFF, CB_STATUS, CB_SEQ_LEN, CB_TRACE_LEN, CB_NCIGAR, CB_NCHIM,
+    CB_O_SEQ, CB_O_QUAL, CB_O_TRACE, CB_O_CIG, CB_O_CHIM,
+    CB_COUNT
+};
+
+struct pr_ctx {
+    int device = 0;
+    int n_cu = 256;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[4] = {};
+    // consensus resident batch
+    DevBuf cb[CB_COUNT];
+    bool cns_loaded = false;
+    int32_t n_lr = 0;
+    int64_t n_aln = 0, total_cols = 0, n_bins = 0, seq_cap = 0, chim_cap = 0;
+    int64_t alg_bytes = 0;
+    bool has_ref = false, has_qual = false, has_ign = false;
+    std::vector<int64_t> out_off, chim_off, bin_off;
+    float last_ms = 0.f;
+    // SW resident batch
+    SwResident sw;
+};
+
+extern "C" int pr_device_count(int *n) {
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *n = c;
+    return 0;
+}
+
+extern "C" int pr_ctx_create(int device, pr_ctx **out) {
+    if (!out) return set_error(PR_ERR_ARG, "null out");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return set_error(PR_ERR_HIP, "no HIP device visible (libprgpu needs an MI355X)");
+    if (device < 0) HIPCHK(hipGetDevice(&device));
+    if (device >= n) return set_error(PR_ERR_ARG, "device %d >= count %d", device, n);
+    HIPCHK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_error(PR_ERR_HIP, "device %d is %s, libprgpu is built for gfx950", device, prop.gcnArchName);
+    pr_ctx *c = new pr_ctx();
+    c->device = device;
+    c->n_cu = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return set_error(PR_ERR_HIP, "hipStreamCreate failed");
+    }
+    for (auto &e : c->ev) (void)hipEventCreate(&e);
+    *out = c;
+    return 0;
+}
+
+extern "C" void pr_ctx_destroy(pr_ctx *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    for (auto &b : c->cb) b.release();
+    sw_release(c->sw);
+    for (auto &e : c->ev) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+// ---------------------------------------------------------------------------
+// consensus
+extern "C" void pr_cns_params_default(pr_cns_params *p) {
+    p->max_coverage = 50.0;  // Seq.pm:116 default; proovread passes --coverage
+    p->bin_size = 20.0;
+    p->trim = 1;
+    p->indel_taboo_length = 7;
+    p->indel_taboo = 0.1;
+    p->min_aln_length = 50;
+    p->max_ins_length = 0;
+    p->fallback_phred = 1;
+    p->phred_offset = 33;
+    p->ref_phred_offset = 33;
+    p->use_ref_qual = 1;
+    p->qual_weighted = 0;
+    p->detect_chimera = 0;
+    p->invert_scores = 0;
+}
+
+static int validate_batch(const pr_cns_batch *b) {
+    if (!b || b->n_lr < 0) return set_error(PR_ERR_ARG, "null batch");
+    if (b->n_lr == 0) return 0;
+    if (!b->lr_off || !b->aln_off) return set_error(PR_ERR_ARG, "lr_off/aln_off required");
+    if (b->lr_off[0] != 0 || b->aln_off[0] != 0) return set_error(PR_ERR_ARG, "offsets must start at 0");
+    for (int i = 0; i < b->n_lr; ++i) {
+        if (b->lr_off[i + 1] < b->lr_off[i] || b->aln_off[i + 1] < b->aln_off[i])
+            return set_error(PR_ERR_ARG, "offsets not monotone at %d", i);
+        if (b->ign_off && b->ign_off[i + 1] < b->ign_off[i]) return set_error(PR_ERR_ARG, "ign_off not monotone");
+    }
+    const int64_t na = b->aln_off[b->n_lr];
+    if (na && (!b->aln_pos || !b->aln_score || !b->aln_flags || !b->aln_seq_off || !b->aln_lseq ||
+               !b->aln_cig_off || !b->aln_ncig || !b->cig_pool))
+        return set_error(PR_ERR_ARG, "alignment arrays required");
+    for (int64_t a = 0; a < na; ++a) {
+        if (b->aln_cig_off[a] < 0 || b->aln_ncig[a] < 0 || b->aln_cig_off[a] + b->aln_ncig[a] > b->cig_pool_len)
+            return set_error(PR_ERR_ARG, "cigar out of pool at alignment %lld", (long long)a);
+        if (!(b->aln_flags[a] & PR_ALN_NO_SEQ) &&
+            (b->aln_seq_off[a] < 0 || b->aln_lseq[a] < 0 || b->aln_seq_off[a] + b->aln_lseq[a] > b->seq_pool_len))
+            return set_error(PR_ERR_ARG, "seq out of pool at alignment %lld", (long long)a);
+    }
+    return 0;
+}
+
+extern "C" int pr_cns_bounds_of(const pr_cns_batch *b, pr_cns_bounds *out) {
+    int rc = validate_batch(b);
+    if (rc) return rc;
+    int64_t sc = 0, cc = 0;
+    for (int i = 0; i < b->n_lr; ++i) {
+        const int64_t L = b->lr_off[i + 1] - b->lr_off[i];
+        int64_t ins = 0;
+        for (int64_t a = b->aln_off[i]; a < b->aln_off[i + 1]; ++a)
+            for (int k = 0; k < b->aln_ncig[a]; ++k) {
+                const uint32_t c = b->cig_pool[b->aln_cig_off[a] + k];
+                if ((c & 15u) == 1u) ins += c >> 4;
+            }
+        sc += L + ins + 1;
+        cc += (int64_t)((double)L / 20.0) / 2 + 2;
+    }
+    out->seq_cap = sc;
+    out->chim_cap = cc;
+    return 0;
+}
+
+template <class T>
+static int upload(DevBuf &d, const T *h, size_t n, hipStream_t s) {
+    int rc = d.ensure(n * sizeof(T));
+    if (rc) return rc;
+    if (n && h) HIPCHK(hipMemcpyAsync(d.p, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+    return 0;
+}
+
+extern "C" int pr_cns_upload(pr_ctx *c, const pr_cns_batch *b) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    int rc = validate_batch(b);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int n = b->n_lr;
+    const int64_t na = n ? b->aln_off[n] : 0;
+    const int64_t tl = n ? b->lr_off[n] : 0;
+    c->n_lr = n;
+    c->n_aln = na;
+    c->total_cols = tl;
+    c->has_ref = b->ref_seq != nullptr;
+    c->has_qual = b->ref_qual != nullptr;
+    c->has_ign = b->ign_off != nullptr;
+    // output / bin offsets
+    c->out_off.assign(n + 1, 0);
+    c->chim_off.assign(n + 1, 0);
+    c->bin_off.assign(n + 1, 0);
+    int64_t in_bytes = 0;
+    for (int i = 0; i < n; ++i) {
+        const int64_t L = b->lr_off[i + 1] - b->lr_off[i];
+        int64_t ins = 0;
+        for (int64_t a = b->aln_off[i]; a < b->aln_off[i + 1]; ++a) {
+            in_bytes += (b->aln_flags[a] & PR_ALN_NO_SEQ ? 0 : b->aln_lseq[a]) + 4 * (int64_t)b->aln_ncig[a] + 16;
+            for (int k = 0; k < b->aln_ncig[a]; ++k) {
+                const uint32_t cc = b->cig_pool[b->aln_cig_off[a] + k];
+                if ((cc & 15u) == 1u) ins += cc >> 4;
+            }
+        }
+        const int64_t nb = (int64_t)((double)L / 20.0) + 1;
+        c->out_off[i + 1] = c->out_off[i] + L + ins + 1;
+        c->chim_off[i + 1] = c->chim_off[i] + nb / 2 + 2;
+    }
+    c->seq_cap = c->out_off[n];
+    c->chim_cap = c->chim_off[n];
+    // SURVEY.md §8d pileup byte model: alignments in + ref seq/qual in + consensus out + state counts
+    c->alg_bytes = in_bytes + tl * 2 + tl * 2 + tl * 6 * 4 * 2;
+
+    DevBuf *B = c->cb;
+    if ((rc = upload(B[CB_LR_OFF], b->lr_off, n + 1, s))) return rc;
+    if ((rc = upload(B[CB_REF_SEQ], b->ref_seq, b->ref_seq ? tl : 0, s))) return rc;
+    if ((rc = upload(B[CB_REF_QUAL], b->ref_qual, b->ref_qual ? tl : 0, s))) return rc;
+    if (b->ign_off) {
+        if ((rc = upload(B[CB_IGN_OFF], b->ign_off, n + 1, s))) return rc;
+        if ((rc = upload(B[CB_IGN], b->ign, 2 * b->ign_off[n], s))) return rc;
+    }
+    if ((rc = upload(B[CB_ALN_OFF], b->aln_off, n + 1, s))) return rc;
+    if ((rc = upload(B[CB_POS], b->aln_pos, na, s))) return rc;
+    if ((rc = upload(B[CB_SCORE], b->aln_score, na, s))) return rc;
+    if ((rc = upload(B[CB_AFLAGS], b->aln_flags, na, s))) return rc;
+    if ((rc = upload(B[CB_SEQ_OFF], b->aln_seq_off, na, s))) return rc;
+    if ((rc = upload(B[CB_LSEQ], b->aln_lseq, na, s))) return rc;
+    if ((rc = upload(B[CB_CIG_OFF], b->aln_cig_off, na, s))) return rc;
+    if ((rc = upload(B[CB_NCIG], b->aln_ncig, na, s))) return rc;
+    if ((rc = upload(B[CB_SEQ], b->seq_pool, b->seq_pool_len, s))) return rc;
+    if ((rc = upload(B[CB_CIG], b->cig_pool, b->cig_pool_len, s))) return rc;
+    // per-alignment scratch
+    const size_t na1 = (size_t)na + 1;
+    if ((rc = B[CB_A_ST].ensure(na1 * 4)) || (rc = B[CB_A_LEN].ensure(na1 * 4)) ||
+        (rc = B[CB_A_NC].ensure(na1 * 8)) || (rc = B[CB_A_BIN].ensure(na1 * 4)) ||
+        (rc = B[CB_A_CB].ensure(na1 * 4)) || (rc = B[CB_A_CE].ensure(na1 * 4)) ||
+        (rc = B[CB_A_SB].ensure(na1 * 4)) || (rc = B[CB_A_RPOS].ensure(na1 * 4)) ||
+        (rc = B[CB_A_END].ensure(na1 * 4)) || (rc = B[CB_SORTED].ensure(na1 * 4)) ||
+        (rc = B[CB_LST_SCORE].ensure(na1 * 8)) || (rc = B[CB_LST_ALN].ensure(na1 * 4)) ||
+        (rc = B[CB_KEPT].ensure(na1)))
+        return rc;
+    if ((rc = B[CB_WORK].ensure(64))) return rc;
+    if ((rc = upload(B[CB_OUT_OFF], c->out_off.data(), n + 1, s))) return rc;
+    if ((rc = upload(B[CB_CHIM_OFF], c->chim_off.data(), n + 1, s))) return rc;
+    const size_t n1 = (size_t)n + 1;
+    if ((rc = B[CB_STATUS].ensure(n1 * 4)) || (rc = B[CB_SEQ_LEN].ensure(n1 * 4)) ||
+        (rc = B[CB_TRACE_LEN].ensure(n1 * 4)) || (rc = B[CB_NCIGAR].ensure(n1 * 4)) ||
+        (rc = B[CB_NCHIM].ensure(n1 * 4)))
+        return rc;
+    const size_t sc = (size_t)c->seq_cap + 1;
+    if ((rc = B[CB_O_SEQ].ensure(sc)) || (rc = B[CB_O_QUAL].ensure(sc)) || (rc = B[CB_O_TRACE].ensure(sc)) ||
+        (rc = B[CB_O_CIG].ensure(sc * 4)) || (rc = B[CB_O_CHIM].ensure(((size_t)c->chim_cap + 1) * 16)))
+        return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    c->cns_loaded = true;
+    return 0;
+}
+
+extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
+    if (!c || !p) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->cns_loaded) return set_error(PR_ERR_ARG, "no resident consensus batch (pr_cns_upload first)");
+    if (p->qual_weighted)
+        return set_error(PR_ERR_UNSUPPORTED, "--qual-weighted (ccseq/utg modes) is not implemented on the GPU path");
+    if (!(p->bin_size >= 1.0)) return set_error(PR_ERR_ARG, "bin_size must be >= 1");
+    HIPCHK(hipSetDevice(c->device));
+    CnsParamsDev P;
+    P.max_coverage = p->max_coverage;
+    P.bin_size = p->bin_size;
+    P.bin_max_bases = p->bin_size * p->max_coverage;   // Seq.pm:517
+    P.indel_taboo = p->indel_taboo;
+    P.trim = p->trim;
+    P.indel_taboo_length = p->indel_taboo_length;
+    P.min_aln_length = p->min_aln_length;
+    P.max_ins_length = p->max_ins_length;
+    P.fallback_phred = p->fallback_phred;
+    P.phred_offset = p->phred_offset;
+    P.ref_phred_offset = p->ref_phred_offset;
+    P.use_ref_qual = p->use_ref_qual;
+    P.detect_chimera = p->detect_chimera;
+    P.invert_scores = p->invert_scores;
+    DevBuf *B = c->cb;
+    CnsDev D;
+    std::memset(&D, 0, sizeof D);
+    D.n_lr = c->n_lr;
+    D.n_aln = c->n_aln;
+    D.lr_off = B[CB_LR_OFF].as<int64_t>();
+    D.ref_seq = c->has_ref ? B[CB_REF_SEQ].as<uint8_t>() : nullptr;
+    D.ref_qual = c->has_qual ? B[CB_REF_QUAL].as<uint8_t>() : nullptr;
+    D.ign_off = c->has_ign ? B[CB_IGN_OFF].as<int64_t>() : nullptr;
+    D.ign = c->has_ign ? B[CB_IGN].as<int32_t>() : nullptr;
+    D.aln_off = B[CB_ALN_OFF].as<int64_t>();
+    D.pos = B[CB_POS].as<int32_t>();
+    D.score = B[CB_SCORE].as<double>();
+    D.aflags = B[CB_AFLAGS].as<uint8_t>();
+    D.seq_off = B[CB_SEQ_OFF].as<int64_t>();
+    D.lseq = B[CB_LSEQ].as<int32_t>();
+    D.cig_off = B[CB_CIG_OFF].as<int64_t>();
+    D.ncig = B[CB_NCIG].as<int32_t>();
+    D.seq = B[CB_SEQ].as<uint8_t>();
+    D.cig = B[CB_CIG].as<uint32_t>();
+    D.a_st = B[CB_A_ST].as<uint32_t>();
+    D.a_len = B[CB_A_LEN].as<int32_t>();
+    D.a_nc = B[CB_A_NC].as<double>();
+    D.a_bin = B[CB_A_BIN].as<int32_t>();
+    D.a_cb = B[CB_A_CB].as<int32_t>();
+    D.a_ce = B[CB_A_CE].as<int32_t>();
+    D.a_sb = B[CB_A_SB].as<int32_t>();
+    D.a_rpos = B[CB_A_RPOS].as<int32_t>();
+    D.a_end = B[CB_A_END].as<int32_t>();
+    D.sorted = B[CB_SORTED].as<int32_t>();
+    D.lst_score = B[CB_LST_SCORE].as<double>();
+    D.lst_aln = B[CB_LST_ALN].as<int32_t>();
+    D.kept = B[CB_KEPT].as<uint8_t>();
+    D.bin_off = B[CB_BIN_OFF].as<int64_t>();
+    D.bin_bases = B[CB_BIN_BASES].as<int64_t>();
+    D.work = B[CB_WORK].as<int32_t>();
+    D.out_off = B[CB_OUT_OFF].as<int64_t>();
+    D.chim_off = B[CB_CHIM_OFF].as<int64_t>();
+    D.status = B[CB_STATUS].as<int32_t>();
+    D.seq_len = B[CB_SEQ_LEN].as<int32_t>();
+    D.trace_len = B[CB_TRACE_LEN].as<int32_t>();
+    D.ncigar = B[CB_NCIGAR].as<int32_t>();
+    D.nchim = B[CB_NCHIM].as<int32_t>();
+    D.o_seq = B[CB_O_SEQ].as<uint8_t>();
+    D.o_qual = B[CB_O_QUAL].as<uint8_t>();
+    D.o_trace = B[CB_O_TRACE].as<uint8_t>();
+    D.o_cig = B[CB_O_CIG].as<uint32_t>();
+    D.o_chim = B[CB_O_CHIM].as<int32_t>();
+    if (c->n_lr == 0) return 0;
+    {
+        // bins per read with this bin size (Seq.pm:1437-1444 _init_read_bins)
+        std::vector<int64_t> lr(c->n_lr + 1);
+        HIPCHK(hipMemcpy(lr.data(), B[CB_LR_OFF].p, (c->n_lr + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+        c->bin_off.assign(c->n_lr + 1, 0);
+        for (int i = 0; i < c->n_lr; ++i)
+            c->bin_off[i + 1] = c->bin_off[i] + (int64_t)((double)(lr[i + 1] - lr[i]) / p->bin_size) + 1;
+        int rc;
+        if ((rc = upload(B[CB_BIN_OFF], c->bin_off.data(), c->n_lr + 1, c->stream))) return rc;
+        if ((rc = B[CB_BIN_BASES].ensure((size_t)(c->bin_off[c->n_lr] + 1) * 8))) return rc;
+        D.bin_off = B[CB_BIN_OFF].as<int64_t>();
+        D.bin_bases = B[CB_BIN_BASES].as<int64_t>();
+    }
+    HIPCHK(hipMemsetAsync(D.work, 0, 64, c->stream));
+    const int grid = c->n_lr < c->n_cu * 2 ? c->n_lr : c->n_cu * 2;
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    int e = cns_launch(D, P, grid, (void *)c->stream);
+    if (e != 0) return set_error(PR_ERR_HIP, "cns kernel launch failed: %s", hipGetErrorString((hipError_t)e));
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    return 0;
+}
+
+template <class T>
+static int download(T *h, const DevBuf &d, size_t n, hipStream_t s) {
+    if (h && n) HIPCHK(hipMemcpyAsync(h, d.p, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    return 0;
+}
+
+extern "C" int pr_cns_download(pr_ctx *c, pr_cns_out *o) {
+    if (!c || !o) return set_error(PR_ERR_ARG, "null arg");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+    float ms = 0.f;
+    if (c->n_lr && hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->last_ms = ms;
+    const int n = c->n_lr;
+    DevBuf *B = c->cb;
+    int rc;
+    if (o->out_off) std::memcpy(o->out_off, c->out_off.data(), (n + 1) * sizeof(int64_t));
+    if (o->chim_off) std::memcpy(o->chim_off, c->chim_off.data(), (n + 1) * sizeof(int64_t));
+    if ((rc = download(o->status, B[CB_STATUS], n, s)) || (rc = download(o->seq_len, B[CB_SEQ_LEN], n, s)) ||
+        (rc = download(o->trace_len, B[CB_TRACE_LEN], n, s)) || (rc = download(o->ncigar, B[CB_NCIGAR], n, s)) ||
+        (rc = download(o->nchim, B[CB_NCHIM], n, s)) || (rc = download(o->seq, B[CB_O_SEQ], c->seq_cap, s)) ||
+        (rc = download(o->qual, B[CB_O_QUAL], c->seq_cap, s)) ||
+        (rc = download(o->trace, B[CB_O_TRACE], c->seq_cap, s)) ||
+        (rc = download(o->cigar, B[CB_O_CIG], c->seq_cap, s)) ||
+        (rc = download(o->chim, B[CB_O_CHIM], c->chim_cap * 4, s)) ||
+        (rc = download(o->kept, B[CB_KEPT], c->n_aln, s)))
+        return rc;
+    if (o->bin_bases && c->bin_off.size() == (size_t)n + 1)
+        if ((rc = download(o->bin_bases, B[CB_BIN_BASES], c->bin_off[n], s))) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" int pr_cns_run(pr_ctx *c, const pr_cns_params *p, const pr_cns_batch *b, pr_cns_out *o) {
+    int rc = pr_cns_upload(c, b);
+    if (rc) return rc;
+    if ((rc = pr_cns_launch(c, p))) return rc;
+    return pr_cns_download(c, o);
+}
+
+extern "C" int pr_cns_last_timing(pr_ctx *c, double *ms_prep, double *ms_pileup) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    if (ms_prep) *ms_prep = 0.0;
+    if (ms_pileup) *ms_pileup = c->last_ms;
+    return 0;
+}
+
+extern "C" int pr_cns_resident_stats(pr_ctx *c, int64_t *columns, int64_t *alg_bytes) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    if (columns) *columns = c->total_cols;
+    if (alg_bytes) *alg_bytes = c->alg_bytes;
+    return 0;
+}
+
+// SW stage entry points are in sw_api.cpp (they share pr_ctx through this accessor)
+SwResident &ctx_sw(pr_ctx *c) { return c->sw; }
+hipStream_t ctx_stream(pr_ctx *c) { return c->stream; }
+int ctx_device(pr_ctx *c) { return c->device; }
+int ctx_ncu(pr_ctx *c) { return c->n_cu; }
+hipEvent_t ctx_event(pr_ctx *c, int i) { return c->ev[i]; }
+int pr_set_error(int code, const char *msg) { return set_error(code, "%s", msg); }
