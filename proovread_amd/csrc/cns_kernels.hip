@@ -311,6 +311,10 @@ constexpr int CNS_LDS_BYTES = OFF_B + SZ_B;
 static_assert(CNS_LDS_BYTES <= 81920, "two workgroups per CU");
 constexpr int MAX_BINS_LDS = (SZ_A - CNS_THREADS * 4) / 8;
 
+// per-column descriptor: flag bits above the 11-bit state-table slot
+constexpr uint32_t DESC_FIXED = 1u << 16;
+constexpr uint32_t DESC_INS = 1u << 17;
+
 struct Ctrl {
     int lr;
     int err_code;
@@ -704,13 +708,13 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                         }
                     }
                     if (!any || !(maxf != 0.0)) {
-                        olen = 1; desc = 0x100u | (D.ref_seq ? D.ref_seq[r0 + col] : (uint8_t)'n'); ph = 0;
+                        olen = 1; desc = DESC_FIXED | (D.ref_seq ? D.ref_seq[r0 + col] : (uint8_t)'n'); ph = 0;
                     } else if (idx == 4) {
                         olen = 0; desc = 0; ph = 0;
                     } else if (idx < 6) {
-                        olen = 1; desc = 0x100u | (uint8_t)("ATGC-N"[idx]); ph = (uint8_t)freq2phred(maxf);
+                        olen = 1; desc = DESC_FIXED | (uint8_t)("ATGC-N"[idx]); ph = (uint8_t)freq2phred(maxf);
                     } else {
-                        olen = (uint16_t)(T.exem[best_slot] >> 40); desc = 0x200u | (uint32_t)best_slot;
+                        olen = (uint16_t)(T.exem[best_slot] >> 40); desc = DESC_INS | (uint32_t)best_slot;
                         ph = (uint8_t)freq2phred(maxf);
                     }
                 }
@@ -744,7 +748,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     if (ol == 0) {
                         D.o_trace[o0 + to] = 'I';
                         to += 1;
-                    } else if (d & 0x100u) {
+                    } else if (d & DESC_FIXED) {
                         D.o_seq[o0 + so] = (uint8_t)(d & 0xFFu);
                         D.o_qual[o0 + so] = qc;
                         D.o_trace[o0 + to] = 'M';
@@ -927,7 +931,8 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 long long tp, tt;
                 block_scan_excl(npos, scan, &tp);
                 block_scan_excl(ntot, scan, &tt);
-                if (tid == 0 && tt > 0) {
+                if (tid == 0 && tt > 0 && C->nchim >= (int)(D.chim_off[lr + 1] - c_off)) C->flag = 1;
+                else if (tid == 0 && tt > 0) {
                     int32_t *rec = D.o_chim + 4 * (c_off + C->nchim);
                     rec[0] = mf + bs; rec[1] = mt - bs; rec[2] = (int32_t)tp; rec[3] = (int32_t)tt;
                     C->nchim += 1;

@@ -170,23 +170,39 @@ static int validate_batch(const pr_cns_batch *b) {
     return 0;
 }
 
+// Output capacities per long read (shared by pr_cns_bounds_of and the upload):
+// consensus bytes <= L + inserted bases of all its alignments (+1); chimera
+// records <= bins/2 + 2 (bins at the smallest bin size bam2cns uses, 20).
+static void cns_caps(const pr_cns_batch *b, std::vector<int64_t> &out_off, std::vector<int64_t> &chim_off,
+                     int64_t *in_bytes) {
+    const int n = b->n_lr;
+    out_off.assign(n + 1, 0);
+    chim_off.assign(n + 1, 0);
+    int64_t ib = 0;
+    for (int i = 0; i < n; ++i) {
+        const int64_t L = b->lr_off[i + 1] - b->lr_off[i];
+        int64_t ins = 0;
+        for (int64_t a = b->aln_off[i]; a < b->aln_off[i + 1]; ++a) {
+            ib += (b->aln_flags[a] & PR_ALN_NO_SEQ ? 0 : b->aln_lseq[a]) + 4 * (int64_t)b->aln_ncig[a] + 16;
+            for (int k = 0; k < b->aln_ncig[a]; ++k) {
+                const uint32_t cc = b->cig_pool[b->aln_cig_off[a] + k];
+                if ((cc & 15u) == 1u) ins += cc >> 4;
+            }
+        }
+        const int64_t nb = (int64_t)((double)L / 20.0) + 1;
+        out_off[i + 1] = out_off[i] + L + ins + 1;
+        chim_off[i + 1] = chim_off[i] + nb / 2 + 2;
+    }
+    if (in_bytes) *in_bytes = ib;
+}
+
 extern "C" int pr_cns_bounds_of(const pr_cns_batch *b, pr_cns_bounds *out) {
     int rc = validate_batch(b);
     if (rc) return rc;
-    int64_t sc = 0, cc = 0;
-    for (int i = 0; i < b->n_lr; ++i) {
-        const int64_t L = b->lr_off[i + 1] - b->lr_off[i];
-        int64_t ins = 0;
-        for (int64_t a = b->aln_off[i]; a < b->aln_off[i + 1]; ++a)
-            for (int k = 0; k < b->aln_ncig[a]; ++k) {
-                const uint32_t c = b->cig_pool[b->aln_cig_off[a] + k];
-                if ((c & 15u) == 1u) ins += c >> 4;
-            }
-        sc += L + ins + 1;
-        cc += (int64_t)((double)L / 20.0) / 2 + 2;
-    }
-    out->seq_cap = sc;
-    out->chim_cap = cc;
+    std::vector<int64_t> oo, co;
+    cns_caps(b, oo, co, nullptr);
+    out->seq_cap = oo.back();
+    out->chim_cap = co.back();
     return 0;
 }
 
@@ -213,25 +229,8 @@ extern "C" int pr_cns_upload(pr_ctx *c, const pr_cns_batch *b) {
     c->has_ref = b->ref_seq != nullptr;
     c->has_qual = b->ref_qual != nullptr;
     c->has_ign = b->ign_off != nullptr;
-    // output / bin offsets
-    c->out_off.assign(n + 1, 0);
-    c->chim_off.assign(n + 1, 0);
-    c->bin_off.assign(n + 1, 0);
     int64_t in_bytes = 0;
-    for (int i = 0; i < n; ++i) {
-        const int64_t L = b->lr_off[i + 1] - b->lr_off[i];
-        int64_t ins = 0;
-        for (int64_t a = b->aln_off[i]; a < b->aln_off[i + 1]; ++a) {
-            in_bytes += (b->aln_flags[a] & PR_ALN_NO_SEQ ? 0 : b->aln_lseq[a]) + 4 * (int64_t)b->aln_ncig[a] + 16;
-            for (int k = 0; k < b->aln_ncig[a]; ++k) {
-                const uint32_t cc = b->cig_pool[b->aln_cig_off[a] + k];
-                if ((cc & 15u) == 1u) ins += cc >> 4;
-            }
-        }
-        const int64_t nb = (int64_t)((double)L / 20.0) + 1;
-        c->out_off[i + 1] = c->out_off[i] + L + ins + 1;
-        c->chim_off[i + 1] = c->chim_off[i] + nb / 2 + 2;
-    }
+    cns_caps(b, c->out_off, c->chim_off, &in_bytes);
     c->seq_cap = c->out_off[n];
     c->chim_cap = c->chim_off[n];
     // SURVEY.md §8d pileup byte model: alignments in + ref seq/qual in + consensus out + state counts

@@ -1,0 +1,9 @@
+#!/bin/bash
+# GPU-box check: parity tests then smoke; stops at the first failing GPU step.
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/gpu_tests.log 2>&1
+rc=$?; echo "pytest rc=$rc" >> gpurun_out/gpu_tests.log
+case $rc in 124|134|137|139) exit $rc;; esac
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc2=$?; echo "smoke rc=$rc2" >> gpurun_out/smoke.log
+exit $(( rc != 0 ? rc : rc2 ))
