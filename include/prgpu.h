@@ -146,6 +146,65 @@ int pr_cns_last_timing(pr_ctx *ctx, double *ms_prep, double *ms_pileup);
  * (SURVEY.md §8d pileup byte model) */
 int pr_cns_resident_stats(pr_ctx *ctx, int64_t *columns, int64_t *alg_bytes);
 
+
+/* ------------------------------------------------------------------ */
+/* seed-extension stage (ksw_extend2 / ksw_global2 of bwa-proovread mem) */
+
+/* bwa mem scoring / band options (proovread.cfg:320-333, 343-365).        */
+typedef struct pr_sw_opts {
+    int32_t a, b;                  /* -A match, -B mismatch                        */
+    int32_t o_del, e_del;          /* -O d / -E d                                   */
+    int32_t o_ins, e_ins;          /* -O ,i / -E ,i                                 */
+    int32_t w;                     /* -w band width                                 */
+    int32_t pen_clip5, pen_clip3;  /* -L 5,3 clipping penalties                     */
+    int32_t zdrop;                 /* -d (bwa default 100)                          */
+    double min_score_per_base;     /* -T "per-base-score" (cfg:324; semantics unpinned) */
+} pr_sw_opts;
+/* finish = 0: bwa-sr iterations (-A5 -B11 -O2,1 -E4,3 -w40 -T2.5 -L30,30);
+ * finish = 1: bwa-sr-finish (-A5 -B13 -O15,19 -E3,3 -w30 -T4 -L30,30)            */
+void pr_sw_opts_default(pr_sw_opts *o, int finish);
+
+/* A batch of extension tasks.  Sequences are nt4-coded (A0 C1 G2 T3 N4, as
+ * bwa's nst_nt4_table).  A task is one exact-match seed of short read t_sr
+ * on long read t_lr: t_strand 1 = the short read aligns to the reverse
+ * complement; t_rbeg is in that strand's coordinates (reverse: L-1-x). This
+ * replaces bwa-proovread's mem_chain2aln/mem_reg2aln for single-seed chains
+ * (bwamem.c), i.e. one alignment per (short read, long read, strand).      */
+typedef struct pr_sw_batch {
+    int32_t n_sr;
+    const int64_t *sr_off;          /* [n_sr+1]                                      */
+    const uint8_t *sr_seq;
+    int32_t n_lr;
+    const int64_t *lr_off;          /* [n_lr+1]                                      */
+    const uint8_t *lr_seq;
+    int64_t n_task;
+    const int32_t *t_sr, *t_lr;
+    const uint8_t *t_strand;
+    const int32_t *t_qbeg, *t_rbeg, *t_slen;
+} pr_sw_batch;
+
+#define PR_SW_MAXCIG 128
+typedef struct pr_sw_out {          /* per task (any pointer may be NULL)              */
+    int32_t *qb, *qe;               /* aligned query interval                          */
+    int32_t *rb, *re;               /* reference interval (strand coordinates)         */
+    int32_t *score;                 /* AS:i (local extension score)                    */
+    int32_t *truesc;                /* mem_alnreg_t truesc                             */
+    int32_t *pos;                   /* 0-based leftmost forward position (SAM POS-1)   */
+    int32_t *ncigar;
+    uint32_t *cigar;                /* [n_task * PR_SW_MAXCIG] BAM ops M0 I1 D2 S4       */
+    uint8_t *pass;                  /* score >= T * (qe - qb)                          */
+    int32_t *status;                /* 0 or PR_ERR_CAPACITY (CIGAR > PR_SW_MAXCIG ops) */
+} pr_sw_out;
+
+int pr_sw_run(pr_ctx *ctx, const pr_sw_opts *o, const pr_sw_batch *b, pr_sw_out *out);
+int pr_sw_upload(pr_ctx *ctx, const pr_sw_batch *b);
+int pr_sw_launch(pr_ctx *ctx, const pr_sw_opts *o);   /* async on ctx stream */
+int pr_sw_download(pr_ctx *ctx, pr_sw_out *out);      /* syncs               */
+/* kernel milliseconds of the last launch (HIP events on the ctx stream) */
+int pr_sw_last_timing(pr_ctx *ctx, double *ms_extend, double *ms_global);
+/* canonical DP cells of the last launch (unpruned band, final width) */
+int pr_sw_last_cells(pr_ctx *ctx, int64_t *cells_extend, int64_t *cells_global);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,249 @@
+// Host side of the SW stage C-ABI (include/prgpu.h pr_sw_*).
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "../../include/prgpu.h"
+#include "sw_dev.h"
+
+using namespace prgpu;
+
+// accessors defined in prgpu_api.cpp
+SwResident &ctx_sw(pr_ctx *c);
+hipStream_t ctx_stream(pr_ctx *c);
+int ctx_device(pr_ctx *c);
+int ctx_ncu(pr_ctx *c);
+hipEvent_t ctx_event(pr_ctx *c, int i);
+int pr_set_error(int code, const char *msg);
+
+#define HIPCHK(x)                                                                 \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            std::string m_ = std::string(#x) + " failed: " + hipGetErrorString(e_); \
+            return pr_set_error(PR_ERR_HIP, m_.c_str());                          \
+        }                                                                         \
+    } while (0)
+
+enum SwBuf {
+    SB_SR, SB_SR_OFF, SB_LR, SB_LR_OFF, SB_T_SR, SB_T_LR, SB_T_STRAND, SB_T_QBEG, SB_T_RBEG, SB_T_SLEN,
+    SB_QB, SB_QE, SB_RB, SB_RE, SB_SCORE, SB_TRUESC, SB_W, SB_PASS, SB_GSCORE, SB_POS, SB_NCIG, SB_STATUS,
+    SB_CIG, SB_Z
+};
+static const int SB_CELLS = 24;
+
+namespace prgpu {
+void sw_release(SwResident &r) {
+    for (int i = 0; i < 32; ++i) {
+        if (r.buf[i]) (void)hipFree(r.buf[i]);
+        r.buf[i] = nullptr;
+        r.cap[i] = 0;
+    }
+    r.loaded = false;
+}
+}  // namespace prgpu
+
+static int ensure(SwResident &r, int id, size_t bytes) {
+    if (r.buf[id] && r.cap[id] >= bytes) return 0;
+    if (r.buf[id]) (void)hipFree(r.buf[id]);
+    r.buf[id] = nullptr;
+    r.cap[id] = 0;
+    const size_t want = bytes ? bytes : 16;
+    if (hipMalloc(&r.buf[id], want) != hipSuccess) return pr_set_error(PR_ERR_HIP, "hipMalloc failed (SW)");
+    r.cap[id] = want;
+    return 0;
+}
+template <class T>
+static int up(SwResident &r, int id, const T *h, size_t n, hipStream_t s) {
+    int rc = ensure(r, id, n * sizeof(T));
+    if (rc) return rc;
+    if (n && h) HIPCHK(hipMemcpyAsync(r.buf[id], h, n * sizeof(T), hipMemcpyHostToDevice, s));
+    return 0;
+}
+
+extern "C" void pr_sw_opts_default(pr_sw_opts *o, int finish) {
+    o->a = 5;
+    o->pen_clip5 = o->pen_clip3 = 30;
+    o->zdrop = 100;
+    if (finish) {
+        o->b = 13; o->o_del = 15; o->o_ins = 19; o->e_del = 3; o->e_ins = 3; o->w = 30;
+        o->min_score_per_base = 4.0;
+    } else {
+        o->b = 11; o->o_del = 2; o->o_ins = 1; o->e_del = 4; o->e_ins = 3; o->w = 40;
+        o->min_score_per_base = 2.5;
+    }
+}
+
+extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
+    if (!c || !b) return pr_set_error(PR_ERR_ARG, "null arg");
+    if (b->n_sr < 0 || b->n_lr < 0 || b->n_task < 0) return pr_set_error(PR_ERR_ARG, "negative sizes");
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    SwResident &r = ctx_sw(c);
+    hipStream_t s = ctx_stream(c);
+    int qmax = 1;
+    for (int i = 0; i < b->n_sr; ++i) {
+        const int64_t l = b->sr_off[i + 1] - b->sr_off[i];
+        if (l < 0) return pr_set_error(PR_ERR_ARG, "sr_off not monotone");
+        if (l > 1000) return pr_set_error(PR_ERR_ARG, "short read longer than 1000 (proovread:457 limit)");
+        if (l > qmax) qmax = (int)l;
+    }
+    for (int i = 0; i < b->n_lr; ++i)
+        if (b->lr_off[i + 1] < b->lr_off[i] || b->lr_off[i + 1] - b->lr_off[i] > (1 << 30))
+            return pr_set_error(PR_ERR_ARG, "lr_off not monotone");
+    for (int64_t t = 0; t < b->n_task; ++t) {
+        const int sr = b->t_sr[t], lr = b->t_lr[t];
+        if (sr < 0 || sr >= b->n_sr || lr < 0 || lr >= b->n_lr)
+            return pr_set_error(PR_ERR_ARG, "task references a missing read");
+        const int64_t lq = b->sr_off[sr + 1] - b->sr_off[sr], L = b->lr_off[lr + 1] - b->lr_off[lr];
+        if (b->t_slen[t] <= 0 || b->t_qbeg[t] < 0 || b->t_qbeg[t] + b->t_slen[t] > lq || b->t_rbeg[t] < 0 ||
+            b->t_rbeg[t] + b->t_slen[t] > L)
+            return pr_set_error(PR_ERR_ARG, "seed outside its reads");
+    }
+    const int64_t nt = b->n_task;
+    int rc;
+    if ((rc = up(r, SB_SR, b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
+        (rc = up(r, SB_SR_OFF, b->sr_off, (size_t)b->n_sr + 1, s)) ||
+        (rc = up(r, SB_LR, b->lr_seq, (size_t)b->lr_off[b->n_lr], s)) ||
+        (rc = up(r, SB_LR_OFF, b->lr_off, (size_t)b->n_lr + 1, s)) || (rc = up(r, SB_T_SR, b->t_sr, nt, s)) ||
+        (rc = up(r, SB_T_LR, b->t_lr, nt, s)) || (rc = up(r, SB_T_STRAND, b->t_strand, nt, s)) ||
+        (rc = up(r, SB_T_QBEG, b->t_qbeg, nt, s)) || (rc = up(r, SB_T_RBEG, b->t_rbeg, nt, s)) ||
+        (rc = up(r, SB_T_SLEN, b->t_slen, nt, s)))
+        return rc;
+    const size_t n4 = (size_t)(nt + 1) * 4;
+    for (int id : {SB_QB, SB_QE, SB_RB, SB_RE, SB_SCORE, SB_TRUESC, SB_W, SB_GSCORE, SB_POS, SB_NCIG, SB_STATUS})
+        if ((rc = ensure(r, id, n4))) return rc;
+    if ((rc = ensure(r, SB_PASS, (size_t)nt + 1)) || (rc = ensure(r, SB_CIG, (size_t)(nt + 1) * SW_MAXCIG * 4)) ||
+        (rc = ensure(r, SB_CELLS, 64)))
+        return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    r.loaded = true;
+    r.n_task = nt;
+    r.n_sr = b->n_sr;
+    r.n_lr = b->n_lr;
+    r.qmax = qmax;
+    return 0;
+}
+
+extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
+    if (!c || !o) return pr_set_error(PR_ERR_ARG, "null arg");
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch (pr_sw_upload first)");
+    if (o->a <= 0 || o->b < 0 || o->e_del <= 0 || o->e_ins <= 0 || o->w <= 0)
+        return pr_set_error(PR_ERR_ARG, "bad scoring options");
+    if ((long)o->a * 2 * r.qmax >= 16384)
+        return pr_set_error(PR_ERR_ARG, "a * 2 * max read length must stay below 16384 (14-bit LDS words)");
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    hipStream_t s = ctx_stream(c);
+    SwOptsDev O;
+    O.a = o->a; O.b = o->b; O.o_del = o->o_del; O.e_del = o->e_del; O.o_ins = o->o_ins; O.e_ins = o->e_ins;
+    O.w = o->w; O.pen_clip5 = o->pen_clip5; O.pen_clip3 = o->pen_clip3; O.zdrop = o->zdrop;
+    O.min_score_per_base = o->min_score_per_base;
+    SwDev D;
+    std::memset(&D, 0, sizeof D);
+    D.n_task = r.n_task;
+    D.qmax = r.qmax;
+    D.tmax = r.qmax + 4 * o->w + 4;
+    D.sr = (const uint8_t *)r.buf[SB_SR];
+    D.sr_off = (const int64_t *)r.buf[SB_SR_OFF];
+    D.lr = (const uint8_t *)r.buf[SB_LR];
+    D.lr_off = (const int64_t *)r.buf[SB_LR_OFF];
+    D.t_sr = (const int32_t *)r.buf[SB_T_SR];
+    D.t_lr = (const int32_t *)r.buf[SB_T_LR];
+    D.t_strand = (const uint8_t *)r.buf[SB_T_STRAND];
+    D.t_qbeg = (const int32_t *)r.buf[SB_T_QBEG];
+    D.t_rbeg = (const int32_t *)r.buf[SB_T_RBEG];
+    D.t_slen = (const int32_t *)r.buf[SB_T_SLEN];
+    D.o_qb = (int32_t *)r.buf[SB_QB];
+    D.o_qe = (int32_t *)r.buf[SB_QE];
+    D.o_rb = (int32_t *)r.buf[SB_RB];
+    D.o_re = (int32_t *)r.buf[SB_RE];
+    D.o_score = (int32_t *)r.buf[SB_SCORE];
+    D.o_truesc = (int32_t *)r.buf[SB_TRUESC];
+    D.o_w = (int32_t *)r.buf[SB_W];
+    D.o_pass = (uint8_t *)r.buf[SB_PASS];
+    D.o_gscore = (int32_t *)r.buf[SB_GSCORE];
+    D.o_pos = (int32_t *)r.buf[SB_POS];
+    D.o_ncig = (int32_t *)r.buf[SB_NCIG];
+    D.o_status = (int32_t *)r.buf[SB_STATUS];
+    D.o_cig = (uint32_t *)r.buf[SB_CIG];
+    D.cells = (unsigned long long *)r.buf[SB_CELLS];
+    D.work = (int32_t *)((char *)r.buf[SB_CELLS] + 32);
+    // LDS: extension = (qmax+1) words per lane; global = same + lane-major query bytes
+    const int lds_ext = (r.qmax + 1) * SW_WAVE * 4;
+    const int qpad = (r.qmax + 4) & ~3;
+    const int lds_glob = lds_ext + SW_WAVE * qpad;
+    if (lds_glob > 160 * 1024) return pr_set_error(PR_ERR_ARG, "short reads too long for the LDS layout");
+    const int blocks_per_cu = (160 * 1024) / (lds_glob + 64) > 0 ? (160 * 1024) / (lds_glob + 64) : 1;
+    const int grid_g = ctx_ncu(c) * (blocks_per_cu < 8 ? blocks_per_cu : 8);
+    D.z_slab = (int64_t)D.tmax * r.qmax * SW_WAVE;
+    int rc;
+    if ((rc = ensure(r, SB_Z, (size_t)D.z_slab * grid_g))) return rc;
+    D.z = (uint8_t *)r.buf[SB_Z];
+    HIPCHK(hipMemsetAsync(r.buf[SB_CELLS], 0, 64, s));
+    if (r.n_task == 0) return 0;
+    const int grid_e = (int)((r.n_task + SW_WAVE - 1) / SW_WAVE);
+    HIPCHK(hipEventRecord(ctx_event(c, 2), s));
+    int e = sw_launch_extend(D, O, grid_e, lds_ext, (void *)s);
+    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    HIPCHK(hipEventRecord(ctx_event(c, 3), s));
+    e = sw_launch_global(D, O, grid_g, lds_glob, (void *)s);
+    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    HIPCHK(hipEventRecord(ctx_event(c, 0), s));
+    return 0;
+}
+
+template <class T>
+static int down(T *h, const SwResident &r, int id, size_t n, hipStream_t s) {
+    if (h && n) HIPCHK(hipMemcpyAsync(h, r.buf[id], n * sizeof(T), hipMemcpyDeviceToHost, s));
+    return 0;
+}
+
+extern "C" int pr_sw_download(pr_ctx *c, pr_sw_out *o) {
+    if (!c || !o) return pr_set_error(PR_ERR_ARG, "null arg");
+    SwResident &r = ctx_sw(c);
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    hipStream_t s = ctx_stream(c);
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+    if (r.n_task) {
+        float a = 0.f, b = 0.f;
+        if (hipEventElapsedTime(&a, ctx_event(c, 2), ctx_event(c, 3)) == hipSuccess) r.ms_ext = a;
+        if (hipEventElapsedTime(&b, ctx_event(c, 3), ctx_event(c, 0)) == hipSuccess) r.ms_glob = b;
+    }
+    HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 16, hipMemcpyDeviceToHost));
+    const size_t n = (size_t)r.n_task;
+    int rc;
+    if ((rc = down(o->qb, r, SB_QB, n, s)) || (rc = down(o->qe, r, SB_QE, n, s)) ||
+        (rc = down(o->rb, r, SB_RB, n, s)) || (rc = down(o->re, r, SB_RE, n, s)) ||
+        (rc = down(o->score, r, SB_SCORE, n, s)) || (rc = down(o->truesc, r, SB_TRUESC, n, s)) ||
+        (rc = down(o->pos, r, SB_POS, n, s)) || (rc = down(o->ncigar, r, SB_NCIG, n, s)) ||
+        (rc = down(o->cigar, r, SB_CIG, n * SW_MAXCIG, s)) || (rc = down(o->pass, r, SB_PASS, n, s)) ||
+        (rc = down(o->status, r, SB_STATUS, n, s)))
+        return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" int pr_sw_run(pr_ctx *c, const pr_sw_opts *o, const pr_sw_batch *b, pr_sw_out *out) {
+    int rc = pr_sw_upload(c, b);
+    if (rc) return rc;
+    if ((rc = pr_sw_launch(c, o))) return rc;
+    return pr_sw_download(c, out);
+}
+
+extern "C" int pr_sw_last_timing(pr_ctx *c, double *ms_extend, double *ms_global) {
+    if (!c) return pr_set_error(PR_ERR_ARG, "null ctx");
+    SwResident &r = ctx_sw(c);
+    if (ms_extend) *ms_extend = r.ms_ext;
+    if (ms_global) *ms_global = r.ms_glob;
+    return 0;
+}
+
+extern "C" int pr_sw_last_cells(pr_ctx *c, int64_t *ce, int64_t *cg) {
+    if (!c) return pr_set_error(PR_ERR_ARG, "null ctx");
+    SwResident &r = ctx_sw(c);
+    if (ce) *ce = (int64_t)r.cells[0];
+    if (cg) *cg = (int64_t)r.cells[1];
+    return 0;
+}

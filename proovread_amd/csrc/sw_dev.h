@@ -3,8 +3,49 @@
 #include <stdint.h>
 
 namespace prgpu {
+
+constexpr int SW_MAXCIG = 128;   // CIGAR ops per task (PR_SW_MAXCIG)
+constexpr int SW_WAVE = 64;
+
+struct SwOptsDev {
+    int a, b, o_del, e_del, o_ins, e_ins, w, pen_clip5, pen_clip3, zdrop;
+    double min_score_per_base;
+};
+
+struct SwDev {
+    int64_t n_task;
+    int qmax;                  // longest short read in the batch
+    int tmax;                  // bound on reference window rows (qmax + 4w)
+    const uint8_t *sr;         // nt4 short reads
+    const int64_t *sr_off;
+    const uint8_t *lr;         // nt4 long reads (forward)
+    const int64_t *lr_off;
+    const int32_t *t_sr, *t_lr, *t_qbeg, *t_rbeg, *t_slen;
+    const uint8_t *t_strand;
+    // extension results (inputs of the global kernel)
+    int32_t *o_qb, *o_qe, *o_rb, *o_re, *o_score, *o_truesc, *o_w;
+    uint8_t *o_pass;
+    // global / CIGAR results
+    int32_t *o_gscore, *o_pos, *o_ncig, *o_status;
+    uint32_t *o_cig;           // n_task * SW_MAXCIG
+    uint8_t *z;                // direction-matrix slabs, one per resident block
+    int64_t z_slab;            // bytes per slab
+    unsigned long long *cells; // [2] canonical DP cells (extension, global)
+    int32_t *work;             // dequeue counter for the global kernel
+};
+
 struct SwResident {
     bool loaded = false;
+    int64_t n_task = 0, n_sr = 0, n_lr = 0;
+    int qmax = 0;
+    void *buf[32] = {};
+    size_t cap[32] = {};
+    float ms_ext = 0.f, ms_glob = 0.f;
+    unsigned long long cells[2] = {0, 0};
 };
-inline void sw_release(SwResident &) {}
+
+int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
+int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
+void sw_release(SwResident &r);
+
 }  // namespace prgpu

@@ -123,3 +123,78 @@ def run_case(case):
         out["bin_bases"] = [R.bin_bases[i] for i in range(R.nbins)]
     L.ocns_free(C.byref(R))
     return out
+
+
+# ---------------------------------------------------------------------------
+# SW oracle (oracle/sw_oracle.c)
+class OswOpts(C.Structure):
+    _fields_ = [("a", C.c_int), ("b", C.c_int), ("o_del", C.c_int), ("o_ins", C.c_int),
+                ("e_del", C.c_int), ("e_ins", C.c_int), ("w", C.c_int), ("pen_clip5", C.c_int),
+                ("pen_clip3", C.c_int), ("zdrop", C.c_int), ("min_score_per_base", C.c_double)]
+
+
+class OswResult(C.Structure):
+    _fields_ = [("qb", C.c_int), ("qe", C.c_int), ("rb", C.c_int), ("re", C.c_int),
+                ("score", C.c_int), ("truesc", C.c_int), ("w", C.c_int), ("global_score", C.c_int),
+                ("w2", C.c_int), ("pos", C.c_int), ("n_cigar", C.c_int), ("cigar", C.c_uint32 * 512),
+                ("pass", C.c_int)]
+
+
+def sw_opts(task="bwa-sr"):
+    """proovread.cfg:320-333 (bwa-sr / bwa-sr-finish); zdrop = bwa default 100."""
+    o = OswOpts()
+    if task == "bwa-sr-finish":
+        o.a, o.b, o.o_del, o.o_ins, o.e_del, o.e_ins, o.w = 5, 13, 15, 19, 3, 3, 30
+        o.min_score_per_base = 4.0
+    else:
+        o.a, o.b, o.o_del, o.o_ins, o.e_del, o.e_ins, o.w = 5, 11, 2, 1, 4, 3, 40
+        o.min_score_per_base = 2.5
+    o.pen_clip5 = o.pen_clip3 = 30
+    o.zdrop = 100
+    return o
+
+
+_sw_set = False
+
+
+def sw_lib():
+    global _sw_set
+    L = lib()
+    if not _sw_set:
+        L.osw_task.argtypes = [C.POINTER(OswOpts), C.POINTER(C.c_uint8), C.c_int, C.POINTER(C.c_uint8),
+                               C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(OswResult)]
+        L.osw_extend.argtypes = [C.c_int, C.POINTER(C.c_uint8), C.c_int, C.POINTER(C.c_uint8), C.c_int,
+                                 C.POINTER(C.c_int8), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_int, C.c_int] + [C.POINTER(C.c_int)] * 5
+        L.osw_global.argtypes = [C.c_int, C.POINTER(C.c_uint8), C.c_int, C.POINTER(C.c_uint8), C.c_int,
+                                 C.POINTER(C.c_int8), C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.POINTER(C.c_int), C.POINTER(C.c_uint32), C.c_int]
+        L.osw_fill_scmat.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_int8)]
+        _sw_set = True
+    return L
+
+
+NT4 = {c: i for i, c in enumerate("ACGT")}
+
+
+def nt4(s):
+    return (C.c_uint8 * max(1, len(s)))(*[NT4.get(c, 4) for c in s.upper()])
+
+
+def sw_task(opts, q, ref, strand, qbeg, rbeg, slen):
+    L = sw_lib()
+    r = OswResult()
+    rc = L.osw_task(C.byref(opts), nt4(q), len(q), nt4(ref), len(ref), strand, qbeg, rbeg, slen, C.byref(r))
+    assert rc == 0
+    cig = "".join(f"{x >> 4}{'MIDNSHP=X'[x & 15]}" for x in r.cigar[:r.n_cigar])
+    return r, cig
+
+
+def sw_extend(q, t, h0, w=40, a=5, b=11, o_del=2, e_del=4, o_ins=1, e_ins=3, end_bonus=30, zdrop=100):
+    L = sw_lib()
+    mat = (C.c_int8 * 25)()
+    L.osw_fill_scmat(a, b, mat)
+    outs = [C.c_int() for _ in range(5)]
+    sc = L.osw_extend(len(q), nt4(q), len(t), nt4(t), 5, mat, o_del, e_del, o_ins, e_ins, w, end_bonus,
+                      zdrop, h0, *[C.byref(x) for x in outs])
+    return sc, [x.value for x in outs]   # qle, tle, gtle, gscore, max_off
