@@ -205,6 +205,23 @@ int pr_sw_last_timing(pr_ctx *ctx, double *ms_extend, double *ms_global);
 /* canonical DP cells of the last launch (unpruned band, final width) */
 int pr_sw_last_cells(pr_ctx *ctx, int64_t *cells_extend, int64_t *cells_global);
 
+/* ------------------------------------------------------------------ */
+/* one correction iteration on the device: SW -> assemble -> consensus  */
+/* (bin/proovread:835-869 for one task: run_bwa, create_sorted_bam and
+ * correct_sr_mt without the SAM/BAM round trip; the hand-off sorts the
+ * reported alignments of every long read into samtools coordinate order)   */
+typedef struct pr_iter_batch {
+    pr_sw_batch sw;               /* tasks grouped by long read                        */
+    const int64_t *task_lr_off;   /* [sw.n_lr+1]: tasks of read i are [off[i],off[i+1]) */
+    const uint8_t *lr_qual;       /* phred+33 qualities of the long reads (lr_off), or NULL */
+} pr_iter_batch;
+int pr_iter_upload(pr_ctx *ctx, const pr_iter_batch *b);
+int pr_iter_launch(pr_ctx *ctx, const pr_sw_opts *o, const pr_cns_params *p);   /* async */
+int pr_iter_download(pr_ctx *ctx, pr_cns_out *out);   /* consensus outputs, syncs */
+int pr_iter_bounds(pr_ctx *ctx, int32_t *n_lr, int64_t *n_task, pr_cns_bounds *bd);
+int pr_iter_last_timing(pr_ctx *ctx, double *ms_sw_extend, double *ms_sw_global, double *ms_assemble,
+                        double *ms_consensus);
+
 #ifdef __cplusplus
 }
 #endif

@@ -52,6 +52,8 @@ struct CnsDev {
     const int32_t *ncig;
     const uint8_t *seq;
     const uint32_t *cig;
+    int seq_nt4;           // seq pool holds nt4 codes (GPU pipeline) instead of ASCII
+    int ref_nt4;           // reference pool holds nt4 codes
     // prep outputs (per alignment)
     uint32_t *a_st;
     int32_t *a_len;

@@ -61,21 +61,64 @@ __device__ __forceinline__ int code5(uint8_t c) {
 }
 // injective key for insertion-state strings of <=19 chars over ACGTN, else a
 // 63-bit FNV-1a hash with the top bit set (collision note)
-__device__ __forceinline__ uint64_t state_key(const uint8_t *s, int n) {
+// Read-only view of an alignment's SEQ as SAM prints it: the stored bytes are
+// ASCII or nt4 codes (0-4, bwa's nst_nt4_table); `rc` means SEQ is the reverse
+// complement of the stored read (GPU pipeline: bwa prints reverse-strand hits
+// reverse-complemented, bwamem.c mem_aln2sam).
+struct SeqV {
+    const uint8_t *p;
+    int n;
+    bool rc, nt4;
+    __device__ __forceinline__ uint8_t operator[](int s) const {
+        uint8_t c = rc ? p[n - 1 - s] : p[s];
+        if (nt4) {
+            if (c > 4) c = 4;
+            if (rc && c < 4) c = (uint8_t)(3 - c);
+            return (uint8_t)"ACGTN"[c];
+        }
+        if (rc) {
+            switch (c) {
+                case 'A': return 'T';
+                case 'C': return 'G';
+                case 'G': return 'C';
+                case 'T': return 'A';
+                default: return c;
+            }
+        }
+        return c;
+    }
+};
+__device__ __forceinline__ uint64_t state_key(const SeqV &v, int off, int n) {
     if (n <= 19) {
         uint64_t k = (uint64_t)n << 57;
         bool ok = true;
         for (int i = 0; i < n; ++i) {
-            int c = code5(s[i]);
+            int c = code5(v[off + i]);
             ok &= (c != 0);
             k |= (uint64_t)c << (3 * i);
         }
         if (ok) return k;
     }
     uint64_t h = 1469598103934665603ULL;
-    for (int i = 0; i < n; ++i) { h ^= s[i]; h *= 1099511628211ULL; }
+    for (int i = 0; i < n; ++i) { h ^= v[off + i]; h *= 1099511628211ULL; }
     h ^= (uint64_t)n; h *= 1099511628211ULL;
     return h | (1ULL << 63);
+}
+// exemplar of a state-table entry: len<<48 | SEQ offset<<32 | alignment index
+__device__ __forceinline__ int ex_len(uint64_t e) { return (int)(e >> 48); }
+__device__ __forceinline__ int ex_off(uint64_t e) { return (int)((e >> 32) & 0xFFFFu); }
+__device__ __forceinline__ int64_t ex_aln(uint64_t e) { return (int64_t)(e & 0xFFFFFFFFu); }
+__device__ __forceinline__ SeqV seq_view(const CnsDev &D, int64_t g) {
+    SeqV v;
+    v.p = D.seq + D.seq_off[g];
+    v.n = D.lseq[g];
+    v.rc = (D.aflags[g] & 8) != 0;
+    v.nt4 = D.seq_nt4 != 0;
+    return v;
+}
+__device__ __forceinline__ uint8_t ref_base(const CnsDev &D, int64_t i) {
+    const uint8_t c = D.ref_seq[i];
+    return D.ref_nt4 ? (uint8_t)"ACGTN"[c > 4 ? 4 : c] : c;
 }
 __device__ __forceinline__ uint32_t key_slot_hash(uint64_t k) {
     k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL; k ^= k >> 33;
@@ -337,7 +380,7 @@ struct STab {
     unsigned long long *key;  // TCAP
     unsigned int *ord_cns;    // TCAP (min order of non-ignored occurrences)
     unsigned int *ord_all;    // TCAP (min order of all occurrences)
-    unsigned long long *exem; // TCAP  len<<40 | global seq offset
+    unsigned long long *exem; // TCAP  len<<48 | SEQ offset<<32 | alignment index
 };
 __device__ __forceinline__ int stab_find(const STab &T, uint64_t k) {
     uint32_t h = key_slot_hash(k) & (TCAP - 1);
@@ -587,13 +630,15 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         for (int i = tid; i < na; i += CNS_THREADS) {
             const int64_t g = a0 + i;
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
-            const uint8_t *sq = D.seq + D.seq_off[g] + D.a_sb[g];
-            const int64_t sqoff = D.seq_off[g] + D.a_sb[g];
+            const SeqV sv = seq_view(D, g);
+            const int sb = D.a_sb[g];
             const uint32_t *cg = D.cig + D.cig_off[g];
             walk_states<true>(cg, D.a_cb[g], D.a_ce[g], D.a_rpos[g], 0, 0x7fffffff,
                               [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                  const uint64_t k = state_key(sq + qoff, qlen);
-                                  const int h = stab_insert(T, k, ((uint64_t)qlen << 40) | (uint64_t)(sqoff + qoff));
+                                  const uint64_t k = state_key(sv, sb + qoff, qlen);
+                                  if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
+                                  const int h = stab_insert(T, k, ((uint64_t)qlen << 48) |
+                                                                      ((uint64_t)(sb + qoff) << 32) | (uint64_t)g);
                                   if (h < 0) { C->flag = 1; return; }
                                   const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
                                   atomicMin(&T.ord_all[h], ord);
@@ -632,15 +677,16 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
                 const int rp = D.a_rpos[g];
                 if (rp >= w0 + wn || D.a_end[g] <= w0) continue;
-                const uint8_t *sq = D.seq + D.seq_off[g] + D.a_sb[g];
+                const SeqV sv = seq_view(D, g);
+                const int sb = D.a_sb[g];
                 const uint32_t *cg = D.cig + D.cig_off[g];
                 walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, (int)w0, (int)(w0 + wn),
                                    [&](int col, int sidx, int kind, int qoff, int qlen) {
                                        if (nig && in_ign(ig, nig, col)) return;
                                        const int c = col - (int)w0;
                                        if (kind == 1) { atomicAdd(&cnt6[c * 6 + 4], 1u); return; }
-                                       if (qlen == 1) { atomicAdd(&cnt6[c * 6 + fixed_idx(sq[qoff])], 1u); return; }
-                                       const int h = stab_find(T, state_key(sq + qoff, qlen));
+                                       if (qlen == 1) { atomicAdd(&cnt6[c * 6 + fixed_idx(sv[sb + qoff])], 1u); return; }
+                                       const int h = stab_find(T, state_key(sv, sb + qoff, qlen));
                                        if (h < 0 || wtab_add(wkey, wcnt, ((uint32_t)(c + 1) << 11) | (uint32_t)h) < 0)
                                            C->flag = 1;
                                    });
@@ -681,7 +727,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     if (use_rq) {
                         const double fr = phred2freq((int)D.ref_qual[r0 + col] - P.ref_phred_offset);
                         if (fr != 0.0) {
-                            const int rs = fixed_idx(D.ref_seq[r0 + col]);
+                            const int rs = fixed_idx(ref_base(D, r0 + col));
                             double v = fr;   // ref freq is added first, then +1 per alignment
                             for (uint32_t k = 0; k < f6[rs]; ++k) v = __dadd_rn(v, 1.0);
                             val[rs] = v; def[rs] = true; any = true;
@@ -699,7 +745,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     for (int k = 0; k < ne; ++k) {
                         const int e = elist[colst[c] + k];
                         const int slot = (int)(wkey[e] & 2047u);
-                        const int slen = (int)(T.exem[slot] >> 40);
+                        const int slen = ex_len(T.exem[slot]);
                         if (P.max_ins_length && slen > P.max_ins_length) continue;
                         const double v = (double)wcnt[e];
                         const unsigned int o = T.ord_cns[slot];
@@ -708,13 +754,13 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                         }
                     }
                     if (!any || !(maxf != 0.0)) {
-                        olen = 1; desc = DESC_FIXED | (D.ref_seq ? D.ref_seq[r0 + col] : (uint8_t)'n'); ph = 0;
+                        olen = 1; desc = DESC_FIXED | (D.ref_seq ? ref_base(D, r0 + col) : (uint8_t)'n'); ph = 0;
                     } else if (idx == 4) {
                         olen = 0; desc = 0; ph = 0;
                     } else if (idx < 6) {
                         olen = 1; desc = DESC_FIXED | (uint8_t)("ATGC-N"[idx]); ph = (uint8_t)freq2phred(maxf);
                     } else {
-                        olen = (uint16_t)(T.exem[best_slot] >> 40); desc = DESC_INS | (uint32_t)best_slot;
+                        olen = (uint16_t)ex_len(T.exem[best_slot]); desc = DESC_INS | (uint32_t)best_slot;
                         ph = (uint8_t)freq2phred(maxf);
                     }
                 }
@@ -739,7 +785,12 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 int so = C->run_seq + (int)(base & 0xffffffffLL);
                 int to = C->run_trace + (int)(base >> 32);
                 const uint8_t qch_off = (uint8_t)P.phred_offset;
-                for (int k = 0; k < per; ++k) {
+                // output capacity of this read (always sufficient for pr_cns_run batches,
+                // a guard for pipeline batches whose capacity is estimated)
+                const long long cap = D.out_off[lr + 1] - o0;
+                const bool fits = (long long)C->run_trace + (tot >> 32) <= cap;
+                if (!fits && tid == 0) C->flag = 1;
+                for (int k = 0; k < per && fits; ++k) {
                     const int c = tid * per + k;
                     if (c >= wn) break;
                     const int ol = cout_[c];
@@ -756,9 +807,10 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     } else {
                         const int slot = (int)(d & 2047u);
                         const uint64_t ex = T.exem[slot];
-                        const uint8_t *src = D.seq + (ex & ((1ULL << 40) - 1));
+                        const SeqV src = seq_view(D, ex_aln(ex));
+                        const int eo = ex_off(ex);
                         for (int q = 0; q < ol; ++q) {
-                            D.o_seq[o0 + so + q] = src[q];
+                            D.o_seq[o0 + so + q] = src[eo + q];
                             D.o_qual[o0 + so + q] = qc;
                             D.o_trace[o0 + to + q] = q ? 'D' : 'M';
                         }
@@ -869,7 +921,8 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     if (rp > mt || D.a_end[g] <= mf) continue;
                     const int bin = D.a_bin[g];
                     const bool inl = bin >= fl && bin <= tl, inr = bin >= fr && bin <= tr;
-                    const uint8_t *sq = D.seq + D.seq_off[g] + D.a_sb[g];
+                    const SeqV sv = seq_view(D, g);
+                    const int sb = D.a_sb[g];
                     const uint32_t *cg = D.cig + D.cig_off[g];
                     walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, mf, mt + 1,
                                        [&](int col, int sidx, int kind, int qoff, int qlen) {
@@ -877,8 +930,8 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                                            f6a[c] = 1u;
                                            int fi = -1, slot = -1;
                                            if (kind == 1) fi = 4;
-                                           else if (qlen == 1) fi = fixed_idx(sq[qoff]);
-                                           else slot = stab_find(T, state_key(sq + qoff, qlen));
+                                           else if (qlen == 1) fi = fixed_idx(sv[sb + qoff]);
+                                           else slot = stab_find(T, state_key(sv, sb + qoff, qlen));
                                            for (int side = 0; side < 2; ++side) {
                                                if (side == 0 ? !inl : !inr) continue;
                                                uint32_t *f6 = side == 0 ? f6l : f6r;

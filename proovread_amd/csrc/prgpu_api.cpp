@@ -12,8 +12,10 @@
 #include "../../include/prgpu.h"
 #include "cns_dev.h"
 #include "sw_dev.h"
+#include "pipe_dev.h"
 
 using namespace prgpu;
+int sw_get_ptrs(pr_ctx *c, SwPtrs *p);
 
 static thread_local std::string g_err;
 static int set_error(int code, const char *fmt, ...) {
@@ -72,7 +74,7 @@ struct pr_ctx {
     int device = 0;
     int n_cu = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[4] = {};
+    hipEvent_t ev[8] = {};
     // consensus resident batch
     DevBuf cb[CB_COUNT];
     bool cns_loaded = false;
@@ -80,8 +82,13 @@ struct pr_ctx {
     int64_t n_aln = 0, total_cols = 0, n_bins = 0, seq_cap = 0, chim_cap = 0;
     int64_t alg_bytes = 0;
     bool has_ref = false, has_qual = false, has_ign = false;
-    std::vector<int64_t> out_off, chim_off, bin_off;
+    std::vector<int64_t> out_off, chim_off, bin_off, lr_off_host;
     float last_ms = 0.f;
+    // SW -> consensus pipeline (pr_iter_*)
+    bool pipe = false;
+    int pipe_sort_cap = 0;
+    DevBuf pb[4];           // task_off, cnt, err, (spare)
+    float ms_pipe = 0.f, ms_cns = 0.f;
     // SW resident batch
     SwResident sw;
 };
@@ -226,6 +233,8 @@ extern "C" int pr_cns_upload(pr_ctx *c, const pr_cns_batch *b) {
     c->n_lr = n;
     c->n_aln = na;
     c->total_cols = tl;
+    c->pipe = false;
+    c->lr_off_host.assign(b->lr_off, b->lr_off + n + 1);
     c->has_ref = b->ref_seq != nullptr;
     c->has_qual = b->ref_qual != nullptr;
     c->has_ign = b->ign_off != nullptr;
@@ -354,8 +363,7 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
     if (c->n_lr == 0) return 0;
     {
         // bins per read with this bin size (Seq.pm:1437-1444 _init_read_bins)
-        std::vector<int64_t> lr(c->n_lr + 1);
-        HIPCHK(hipMemcpy(lr.data(), B[CB_LR_OFF].p, (c->n_lr + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+        const std::vector<int64_t> &lr = c->lr_off_host;
         c->bin_off.assign(c->n_lr + 1, 0);
         for (int i = 0; i < c->n_lr; ++i)
             c->bin_off[i + 1] = c->bin_off[i] + (int64_t)((double)(lr[i + 1] - lr[i]) / p->bin_size) + 1;
@@ -365,12 +373,24 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         D.bin_off = B[CB_BIN_OFF].as<int64_t>();
         D.bin_bases = B[CB_BIN_BASES].as<int64_t>();
     }
+    if (c->pipe) {
+        // consensus reads the SW batch in place: long reads and short reads as
+        // nt4, CIGARs from the SW output (stride SW_MAXCIG)
+        SwPtrs sp;
+        int rc = sw_get_ptrs(c, &sp);
+        if (rc) return rc;
+        D.ref_seq = sp.lr;
+        D.ref_nt4 = 1;
+        D.seq = sp.sr;
+        D.seq_nt4 = 1;
+        D.cig = sp.cig;
+    }
     HIPCHK(hipMemsetAsync(D.work, 0, 64, c->stream));
     const int grid = c->n_lr < c->n_cu * 2 ? c->n_lr : c->n_cu * 2;
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(hipEventRecord(c->ev[4], c->stream));
     int e = cns_launch(D, P, grid, (void *)c->stream);
     if (e != 0) return set_error(PR_ERR_HIP, "cns kernel launch failed: %s", hipGetErrorString((hipError_t)e));
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    HIPCHK(hipEventRecord(c->ev[5], c->stream));
     return 0;
 }
 
@@ -387,7 +407,8 @@ extern "C" int pr_cns_download(pr_ctx *c, pr_cns_out *o) {
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipGetLastError());
     float ms = 0.f;
-    if (c->n_lr && hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->last_ms = ms;
+    if (c->n_lr && hipEventElapsedTime(&ms, c->ev[4], c->ev[5]) == hipSuccess) c->last_ms = ms;
+    if (c->pipe && c->n_lr && hipEventElapsedTime(&ms, c->ev[0], c->ev[4]) == hipSuccess) c->ms_pipe = ms;
     const int n = c->n_lr;
     DevBuf *B = c->cb;
     int rc;
@@ -426,6 +447,144 @@ extern "C" int pr_cns_resident_stats(pr_ctx *c, int64_t *columns, int64_t *alg_b
     if (!c) return set_error(PR_ERR_ARG, "null ctx");
     if (columns) *columns = c->total_cols;
     if (alg_bytes) *alg_bytes = c->alg_bytes;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// one iteration on the device: SW -> assemble -> consensus (pr_iter_*)
+extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
+    if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
+    const pr_sw_batch &sb = b->sw;
+    const int n = sb.n_lr;
+    if (!b->task_lr_off || b->task_lr_off[0] != 0 || b->task_lr_off[n] != sb.n_task)
+        return set_error(PR_ERR_ARG, "task_lr_off must partition the tasks");
+    int maxt = 1;
+    for (int i = 0; i < n; ++i) {
+        if (b->task_lr_off[i + 1] < b->task_lr_off[i]) return set_error(PR_ERR_ARG, "task_lr_off not monotone");
+        for (int64_t t = b->task_lr_off[i]; t < b->task_lr_off[i + 1]; ++t)
+            if (sb.t_lr[t] != i) return set_error(PR_ERR_ARG, "tasks must be grouped by long read");
+        const int64_t k = b->task_lr_off[i + 1] - b->task_lr_off[i];
+        if (k > maxt) maxt = (int)k;
+    }
+    if (maxt > 16384) return set_error(PR_ERR_CAPACITY, "more than 16384 tasks on one long read");
+    int rc = pr_sw_upload(c, &sb);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    c->n_lr = n;
+    c->n_aln = sb.n_task;
+    c->total_cols = sb.lr_off[n];
+    c->has_ref = true;
+    c->has_qual = b->lr_qual != nullptr;
+    c->has_ign = false;
+    c->lr_off_host.assign(sb.lr_off, sb.lr_off + n + 1);
+    c->out_off.assign(n + 1, 0);
+    c->chim_off.assign(n + 1, 0);
+    for (int i = 0; i < n; ++i) {
+        const int64_t L = sb.lr_off[i + 1] - sb.lr_off[i];
+        const int64_t nb = (int64_t)((double)L / 20.0) + 1;
+        c->out_off[i + 1] = c->out_off[i] + 2 * L + 1024;   // guarded in the kernel
+        c->chim_off[i + 1] = c->chim_off[i] + nb / 2 + 2;
+    }
+    c->seq_cap = c->out_off[n];
+    c->chim_cap = c->chim_off[n];
+    c->alg_bytes = 0;
+    int sc = 1;
+    while (sc < maxt) sc <<= 1;
+    c->pipe_sort_cap = sc;
+    DevBuf *B = c->cb;
+    const size_t na1 = (size_t)sb.n_task + 1, n1 = (size_t)n + 1;
+    if ((rc = upload(B[CB_LR_OFF], sb.lr_off, n1, s))) return rc;
+    if (b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)sb.lr_off[n], s))) return rc;
+    if ((rc = upload(c->pb[0], b->task_lr_off, n1, s))) return rc;
+    if ((rc = c->pb[1].ensure(n1 * 4)) || (rc = c->pb[2].ensure(n1 * 4))) return rc;
+    if ((rc = B[CB_ALN_OFF].ensure(n1 * 8)) || (rc = B[CB_POS].ensure(na1 * 4)) ||
+        (rc = B[CB_SCORE].ensure(na1 * 8)) || (rc = B[CB_AFLAGS].ensure(na1)) ||
+        (rc = B[CB_SEQ_OFF].ensure(na1 * 8)) || (rc = B[CB_LSEQ].ensure(na1 * 4)) ||
+        (rc = B[CB_CIG_OFF].ensure(na1 * 8)) || (rc = B[CB_NCIG].ensure(na1 * 4)))
+        return rc;
+    if ((rc = B[CB_A_ST].ensure(na1 * 4)) || (rc = B[CB_A_LEN].ensure(na1 * 4)) ||
+        (rc = B[CB_A_NC].ensure(na1 * 8)) || (rc = B[CB_A_BIN].ensure(na1 * 4)) ||
+        (rc = B[CB_A_CB].ensure(na1 * 4)) || (rc = B[CB_A_CE].ensure(na1 * 4)) ||
+        (rc = B[CB_A_SB].ensure(na1 * 4)) || (rc = B[CB_A_RPOS].ensure(na1 * 4)) ||
+        (rc = B[CB_A_END].ensure(na1 * 4)) || (rc = B[CB_SORTED].ensure(na1 * 4)) ||
+        (rc = B[CB_LST_SCORE].ensure(na1 * 8)) || (rc = B[CB_LST_ALN].ensure(na1 * 4)) ||
+        (rc = B[CB_KEPT].ensure(na1)) || (rc = B[CB_WORK].ensure(64)))
+        return rc;
+    if ((rc = upload(B[CB_OUT_OFF], c->out_off.data(), n1, s))) return rc;
+    if ((rc = upload(B[CB_CHIM_OFF], c->chim_off.data(), n1, s))) return rc;
+    if ((rc = B[CB_STATUS].ensure(n1 * 4)) || (rc = B[CB_SEQ_LEN].ensure(n1 * 4)) ||
+        (rc = B[CB_TRACE_LEN].ensure(n1 * 4)) || (rc = B[CB_NCIGAR].ensure(n1 * 4)) ||
+        (rc = B[CB_NCHIM].ensure(n1 * 4)))
+        return rc;
+    const size_t scap = (size_t)c->seq_cap + 1;
+    if ((rc = B[CB_O_SEQ].ensure(scap)) || (rc = B[CB_O_QUAL].ensure(scap)) || (rc = B[CB_O_TRACE].ensure(scap)) ||
+        (rc = B[CB_O_CIG].ensure(scap * 4)) || (rc = B[CB_O_CHIM].ensure(((size_t)c->chim_cap + 1) * 16)))
+        return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    c->cns_loaded = true;
+    c->pipe = true;
+    return 0;
+}
+
+extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_params *p) {
+    if (!c || !o || !p) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->pipe) return set_error(PR_ERR_ARG, "no resident iteration batch (pr_iter_upload first)");
+    int rc = pr_sw_launch(c, o);   // records ev[2], ev[3], ev[0]
+    if (rc) return rc;
+    SwPtrs sp;
+    if ((rc = sw_get_ptrs(c, &sp))) return rc;
+    DevBuf *B = c->cb;
+    PipeDev P;
+    P.n_lr = c->n_lr;
+    P.sort_cap = c->pipe_sort_cap;
+    P.maxcig = SW_MAXCIG;
+    P.task_off = c->pb[0].as<int64_t>();
+    P.t_sr = sp.t_sr;
+    P.strand = sp.strand;
+    P.pass = sp.pass;
+    P.status = sp.status;
+    P.pos = sp.pos;
+    P.score = sp.score;
+    P.ncig = sp.ncig;
+    P.sr_off = sp.sr_off;
+    P.cnt = c->pb[1].as<int32_t>();
+    P.aln_off = B[CB_ALN_OFF].as<int64_t>();
+    P.err = c->pb[2].as<int32_t>();
+    P.a_pos = B[CB_POS].as<int32_t>();
+    P.a_score = B[CB_SCORE].as<double>();
+    P.a_flags = B[CB_AFLAGS].as<uint8_t>();
+    P.a_seq_off = B[CB_SEQ_OFF].as<int64_t>();
+    P.a_lseq = B[CB_LSEQ].as<int32_t>();
+    P.a_cig_off = B[CB_CIG_OFF].as<int64_t>();
+    P.a_ncig = B[CB_NCIG].as<int32_t>();
+    if (c->n_lr == 0) return 0;
+    const int grid = c->n_lr < c->n_cu * 4 ? c->n_lr : c->n_cu * 4;
+    int e = pipe_launch(P, grid, (void *)c->stream, c->pipe_sort_cap * 8);
+    if (e) return set_error(PR_ERR_HIP, "pipe kernels: %s", hipGetErrorString((hipError_t)e));
+    return pr_cns_launch(c, p);
+}
+
+extern "C" int pr_iter_download(pr_ctx *c, pr_cns_out *o) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    return pr_cns_download(c, o);
+}
+
+extern "C" int pr_iter_last_timing(pr_ctx *c, double *ms_sw_extend, double *ms_sw_global, double *ms_assemble,
+                                   double *ms_consensus) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    if (ms_sw_extend) *ms_sw_extend = c->sw.ms_ext;
+    if (ms_sw_global) *ms_sw_global = c->sw.ms_glob;
+    if (ms_assemble) *ms_assemble = c->ms_pipe;
+    if (ms_consensus) *ms_consensus = c->last_ms;
+    return 0;
+}
+
+extern "C" int pr_iter_bounds(pr_ctx *c, int32_t *n_lr, int64_t *n_task, pr_cns_bounds *bd) {
+    if (!c || !c->pipe) return set_error(PR_ERR_ARG, "no resident iteration batch");
+    if (n_lr) *n_lr = c->n_lr;
+    if (n_task) *n_task = c->n_aln;
+    if (bd) { bd->seq_cap = c->seq_cap; bd->chim_cap = c->chim_cap; }
     return 0;
 }
 

@@ -247,3 +247,26 @@ extern "C" int pr_sw_last_cells(pr_ctx *c, int64_t *ce, int64_t *cg) {
     if (cg) *cg = (int64_t)r.cells[1];
     return 0;
 }
+
+// for the SW -> consensus pipeline (prgpu_api.cpp)
+int sw_get_ptrs(pr_ctx *c, SwPtrs *p) {
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
+    p->sr = (const uint8_t *)r.buf[SB_SR];
+    p->lr = (const uint8_t *)r.buf[SB_LR];
+    p->strand = (const uint8_t *)r.buf[SB_T_STRAND];
+    p->pass = (const uint8_t *)r.buf[SB_PASS];
+    p->sr_off = (const int64_t *)r.buf[SB_SR_OFF];
+    p->lr_off = (const int64_t *)r.buf[SB_LR_OFF];
+    p->t_sr = (const int32_t *)r.buf[SB_T_SR];
+    p->t_lr = (const int32_t *)r.buf[SB_T_LR];
+    p->status = (const int32_t *)r.buf[SB_STATUS];
+    p->pos = (const int32_t *)r.buf[SB_POS];
+    p->score = (const int32_t *)r.buf[SB_SCORE];
+    p->ncig = (const int32_t *)r.buf[SB_NCIG];
+    p->cig = (const uint32_t *)r.buf[SB_CIG];
+    p->n_task = r.n_task;
+    p->n_sr = (int)r.n_sr;
+    p->n_lr = (int)r.n_lr;
+    return 0;
+}

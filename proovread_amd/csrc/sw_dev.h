@@ -44,6 +44,16 @@ struct SwResident {
     unsigned long long cells[2] = {0, 0};
 };
 
+// device pointers of a resident SW batch (for the SW -> consensus pipeline)
+struct SwPtrs {
+    const uint8_t *sr, *lr, *strand, *pass;
+    const int64_t *sr_off, *lr_off;
+    const int32_t *t_sr, *t_lr, *status, *pos, *score, *ncig;
+    const uint32_t *cig;
+    int64_t n_task;
+    int n_sr, n_lr;
+};
+
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
 void sw_release(SwResident &r);

@@ -1,0 +1,111 @@
+"""One proovread correction iteration on the GPU (pr_iter_* of libprgpu.so):
+seed extension + CIGAR for every (short read, long read) task, the device-side
+hand-off into samtools coordinate order, and the consensus of every long read
+— bin/proovread:835-869 for one task (run_bwa 1254-1322, create_sorted_bam
+1330-1355, correct_sr_mt 1528-1721) without the SAM/BAM files in between."""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional
+
+import numpy as np
+
+from . import _abi, cns, sw
+
+
+class IterBatch(C.Structure):
+    _fields_ = [("sw", sw.SwBatch), ("task_lr_off", _abi.P64), ("lr_qual", _abi.PU8)]
+
+
+def _setup(L):
+    if getattr(L, "_iter_ready", False):
+        return
+    sw._setup(L)
+    L.pr_iter_upload.argtypes = [C.c_void_p, C.POINTER(IterBatch)]
+    L.pr_iter_launch.argtypes = [C.c_void_p, C.POINTER(sw.SwOpts), C.POINTER(_abi.CnsParams)]
+    L.pr_iter_download.argtypes = [C.c_void_p, C.POINTER(_abi.CnsOut)]
+    L.pr_iter_bounds.argtypes = [C.c_void_p, _abi.P32, _abi.P64, C.POINTER(_abi.CnsBounds)]
+    L.pr_iter_last_timing.argtypes = [C.c_void_p, _abi.PD, _abi.PD, _abi.PD, _abi.PD]
+    L._iter_ready = True
+
+
+class Iteration:
+    """A resident iteration batch on one GPU (upload once, launch many)."""
+
+    def __init__(self, d, lr_qual: Optional[np.ndarray] = None, ctx: Optional[_abi.Context] = None):
+        self.L = _abi.lib()
+        _setup(self.L)
+        self.ctx = ctx or _abi.default_context()
+        self.d = d
+        self.inp = d.sw_input()
+        n_lr = len(d.lr_off) - 1
+        self.task_lr_off = np.zeros(n_lr + 1, np.int64)
+        np.cumsum(np.bincount(d.t_lr, minlength=n_lr), out=self.task_lr_off[1:])
+        if lr_qual is None:
+            lr_qual = np.full(int(d.lr_off[-1]), ord("$"), np.uint8)   # raw CLR reads: phred 3
+        self.lr_qual = lr_qual
+        b = IterBatch()
+        b.sw = self.inp.c_batch()
+        b.task_lr_off = _abi.ptr(self.task_lr_off, C.c_int64)
+        b.lr_qual = _abi.ptr(self.lr_qual, C.c_uint8)
+        self._b = b
+        _abi.check(self.L.pr_iter_upload(self.ctx.h, C.byref(b)), "pr_iter_upload")
+        nl, nt, bd = C.c_int32(), C.c_int64(), _abi.CnsBounds()
+        _abi.check(self.L.pr_iter_bounds(self.ctx.h, C.byref(nl), C.byref(nt), C.byref(bd)), "pr_iter_bounds")
+        self.n_lr, self.n_task, self.bounds = nl.value, nt.value, bd
+        self.out = None
+
+    def launch(self, sw_opts: sw.SwOpts, params: cns.CnsParams):
+        self._pc = params.to_c()
+        self._so = sw_opts
+        _abi.check(self.L.pr_iter_launch(self.ctx.h, C.byref(sw_opts), C.byref(self._pc)), "pr_iter_launch")
+
+    def _out_buffers(self, bin_size=20.0):
+        n = self.n_lr
+        lens = np.diff(self.d.lr_off)
+        nb = np.floor(lens / bin_size).astype(np.int64) + 1
+        a = dict(out_off=np.zeros(n + 1, np.int64), status=np.zeros(n, np.int32), seq_len=np.zeros(n, np.int32),
+                 trace_len=np.zeros(n, np.int32), ncigar=np.zeros(n, np.int32), nchim=np.zeros(n, np.int32),
+                 seq=np.zeros(self.bounds.seq_cap + 1, np.uint8), qual=np.zeros(self.bounds.seq_cap + 1, np.uint8),
+                 trace=np.zeros(self.bounds.seq_cap + 1, np.uint8),
+                 cigar=np.zeros(self.bounds.seq_cap + 1, np.uint32), chim_off=np.zeros(n + 1, np.int64),
+                 chim=np.zeros(4 * (self.bounds.chim_cap + 1), np.int32),
+                 kept=np.zeros(self.n_task + 1, np.uint8), bin_bases=np.zeros(int(nb.sum()) + 1, np.int64))
+        o = _abi.CnsOut()
+        P = _abi.ptr
+        for k, ct in (("out_off", C.c_int64), ("status", C.c_int32), ("seq_len", C.c_int32),
+                      ("trace_len", C.c_int32), ("ncigar", C.c_int32), ("nchim", C.c_int32), ("seq", C.c_uint8),
+                      ("qual", C.c_uint8), ("trace", C.c_uint8), ("cigar", C.c_uint32), ("chim_off", C.c_int64),
+                      ("chim", C.c_int32), ("kept", C.c_uint8), ("bin_bases", C.c_int64)):
+            setattr(o, k, P(a[k], ct))
+        return a, o
+
+    def download(self, with_arrays: bool = True):
+        if self.out is None:
+            self.out = self._out_buffers()
+        a, o = self.out
+        _abi.check(self.L.pr_iter_download(self.ctx.h, C.byref(o)), "pr_iter_download")
+        return a
+
+    def timing(self):
+        v = [C.c_double() for _ in range(4)]
+        self.L.pr_iter_last_timing(self.ctx.h, *[C.byref(x) for x in v])
+        return [x.value for x in v]
+
+    def results(self) -> List[cns.ReadResult]:
+        a = self.download()
+        out = []
+        for i in range(self.n_lr):
+            st = int(a["status"][i])
+            r = cns.ReadResult(f"lr{i}", st)
+            if st == 0:
+                o = int(a["out_off"][i])
+                sl, tl, nc = int(a["seq_len"][i]), int(a["trace_len"][i]), int(a["ncigar"][i])
+                r.seq = a["seq"][o:o + sl].tobytes().decode("latin-1")
+                r.qual = a["qual"][o:o + sl].tobytes().decode("latin-1")
+                r.trace = a["trace"][o:o + tl].tobytes().decode("latin-1")
+                r.cigar = [(int(x >> 4), "MID"[int(x & 15)]) for x in a["cigar"][o:o + nc]]
+                c0, nch = int(a["chim_off"][i]), int(a["nchim"][i])
+                r.chim = [tuple(int(v) for v in row) for row in a["chim"][4 * c0:4 * (c0 + nch)].reshape(-1, 4)]
+            out.append(r)
+        return out

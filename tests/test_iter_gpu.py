@@ -1,0 +1,37 @@
+"""End-to-end parity of one GPU iteration (pr_iter_*: SW -> device hand-off ->
+consensus) against the CPU chain SW oracle -> SAM -> coordinate sort ->
+consensus oracle, on seeded synthetic long/short reads.  Bar: byte-exact
+corrected reads (sequence and qualities), traces and chimera records."""
+import numpy as np
+import pytest
+
+import oracle_bind as ob
+from pipeline_oracle import consensus_cases, sam_for_tasks
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("finish", [False, True])
+def test_iteration_matches_cpu_chain(finish):
+    from proovread_amd import cns, iteration, sw, synth
+    d = synth.simulate(31 + finish, 40000, 40, 2500, 15, sr_frac=1.0)
+    task = "bwa-sr-finish" if finish else "bwa-sr"
+    params = {"coverage": "22.5" if finish else "11.25", "use_ref_qual": "0" if finish else "1",
+              "detect_chimera": "1" if finish else "0"}
+    it = iteration.Iteration(d)
+    cp = cns.CnsParams(coverage=float(params["coverage"]), use_ref_qual=params["use_ref_qual"] == "1",
+                       detect_chimera=params["detect_chimera"] == "1")
+    it.launch(sw.default_opts(finish=finish), cp)
+    got = it.results()
+    sams = sam_for_tasks(d, task)
+    cases = consensus_cases(d, sams, params)
+    n_checked = 0
+    for c, g in zip(cases, got):
+        want = ob.run_case(c)
+        assert want["rc"] == 0
+        assert g.status == 0, (c.name, g.status)
+        assert g.fastq == want["fastq"], c.name
+        assert g.trace == want["trace"], c.name
+        assert "".join(l + "\n" for l in g.chim_lines()) == want["chim"], c.name
+        n_checked += 1
+    assert n_checked == d.n_lr
