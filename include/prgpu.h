@@ -57,6 +57,8 @@ typedef struct pr_ctx pr_ctx;
 int pr_ctx_create(int device, pr_ctx **out);
 void pr_ctx_destroy(pr_ctx *ctx);
 int pr_device_count(int *n);
+/* wait for everything enqueued on the context's stream */
+int pr_ctx_sync(pr_ctx *ctx);
 
 /* ------------------------------------------------------------------ */
 /* consensus stage                                                     */
@@ -219,8 +221,15 @@ int pr_iter_upload(pr_ctx *ctx, const pr_iter_batch *b);
 int pr_iter_launch(pr_ctx *ctx, const pr_sw_opts *o, const pr_cns_params *p);   /* async */
 int pr_iter_download(pr_ctx *ctx, pr_cns_out *out);   /* consensus outputs, syncs */
 int pr_iter_bounds(pr_ctx *ctx, int32_t *n_lr, int64_t *n_task, pr_cns_bounds *bd);
+/* reported alignments of the last iteration: count, total CIGAR ops, total SEQ bytes (syncs) */
+int pr_iter_alignment_stats(pr_ctx *ctx, int64_t *n_aln, int64_t *sum_ncig, int64_t *sum_lseq);
 int pr_iter_last_timing(pr_ctx *ctx, double *ms_sw_extend, double *ms_sw_global, double *ms_assemble,
                         double *ms_consensus);
+/* enqueue (ctx stream) the per-iteration statistic of the resident consensus:
+ * dev_out[0] = corrected bases, dev_out[1] = bases with phred >= min_phred.
+ * dev_out is DEVICE memory (e.g. a tensor gathered with RCCL all_reduce across
+ * GPUs: the global masked-fraction input of mask_shortcut_frac, proovread:2026) */
+int pr_iter_stats(pr_ctx *ctx, int32_t min_phred, int64_t *dev_out);
 
 #ifdef __cplusplus
 }

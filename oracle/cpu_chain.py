@@ -1,0 +1,105 @@
+"""ORACLE — TEST / BASELINE INFRASTRUCTURE ONLY.
+
+CPU restatement of one proovread correction iteration, used as the checker of
+the GPU pipeline and as bench.py's cpu_baseline leg (kind "port"): for every
+seed-extension task the SW oracle (oracle/sw_oracle.c, restatement of
+bwa-proovread's ksw stage), SAM records with AS:i, the per-long-read
+coordinate order samtools would produce, and the consensus oracle
+(oracle/cns_oracle.c, restatement of bam2cns / Sam::Seq, pinned to the
+reference's Perl engine).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import multiprocessing as mp
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE.parent / "tests"))
+import oracle_bind as ob  # noqa: E402
+
+_ASCII = np.frombuffer(b"ACGTN", np.uint8)
+_D = None        # dataset shared with forked workers
+_OPTS = None
+_PARAMS = None
+
+
+def _lr_chain(lr: int):
+    """SW oracle for all tasks of long read `lr`, then its consensus."""
+    d = _D
+    L = ob.sw_lib()
+    t0, t1 = int(d._task_off[lr]), int(d._task_off[lr + 1])
+    lr_ptr = d.lr_seq.ctypes.data + int(d.lr_off[lr])
+    Llen = int(d.lr_off[lr + 1] - d.lr_off[lr])
+    recs = []
+    r = ob.OswResult()
+    for t in range(t0, t1):
+        sid = int(d.t_sr[t])
+        so = int(d.sr_off[sid])
+        lq = int(d.sr_off[sid + 1]) - so
+        rc = L.osw_task(C.byref(_OPTS), C.cast(d.sr_seq.ctypes.data + so, C.POINTER(C.c_uint8)), lq,
+                        C.cast(lr_ptr, C.POINTER(C.c_uint8)), Llen, int(d.t_strand[t]), int(d.t_qbeg[t]),
+                        int(d.t_rbeg[t]), int(d.t_slen[t]), C.byref(r))
+        if rc or not getattr(r, "pass"):
+            continue
+        strand = int(d.t_strand[t])
+        q = d.sr_seq[so:so + lq]
+        seq = (_ASCII[np.where(q < 4, 3 - q, 4)][::-1] if strand else _ASCII[q]).tobytes().decode()
+        cg = "".join(f"{x >> 4}{'MIDNSHP=X'[x & 15]}" for x in r.cigar[:r.n_cigar])
+        recs.append((r.pos, strand, t, f"sr{sid}\t{16 if strand else 0}\tlr{lr}\t{r.pos + 1}\t60\t{cg}\t*\t0\t0\t"
+                                       f"{seq}\t*\tAS:i:{r.score}"))
+    recs.sort(key=lambda x: (x[0], x[1], x[2]))
+    lines = [x[3].encode() for x in recs]
+    arr = (C.c_char_p * (len(lines) + 1))(*lines)
+    ref = _ASCII[d.lr_seq[int(d.lr_off[lr]):int(d.lr_off[lr + 1])]].tobytes()
+    res = ob.OcnsResult()
+    rc = ob.lib().ocns_run(C.byref(_PARAMS), f"lr{lr}".encode(), ref, b"$" * len(ref), len(ref), arr, len(lines),
+                           None, 0, C.byref(res))
+    out = (rc, res.fastq.decode() if rc == 0 else "")
+    ob.lib().ocns_free(C.byref(res))
+    return out
+
+
+def _init_worker():
+    ob.sw_lib()
+
+
+def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers=None):
+    """Run the CPU chain on long reads `lrs`; returns (wall seconds, bases, results, workers)."""
+    global _D, _OPTS, _PARAMS
+    _D = d
+    if not hasattr(d, "_task_off"):
+        d._task_off = np.zeros(d.n_lr + 1, np.int64)
+        np.cumsum(np.bincount(d.t_lr, minlength=d.n_lr), out=d._task_off[1:])
+    _OPTS = ob.sw_opts(task)
+    _PARAMS = ob.OcnsParams()
+    _PARAMS.max_coverage = coverage
+    _PARAMS.bin_size = 20.0
+    _PARAMS.trim = 1
+    _PARAMS.indel_taboo_length = 7
+    _PARAMS.indel_taboo = 0.1
+    _PARAMS.min_aln_length = 50
+    _PARAMS.max_ins_length = 0
+    _PARAMS.fallback_phred = 1
+    _PARAMS.phred_offset = 33
+    _PARAMS.ref_phred_offset = 33
+    _PARAMS.use_ref_qual = int(use_ref_qual)
+    _PARAMS.qual_weighted = 0
+    _PARAMS.detect_chimera = 0
+    _PARAMS.invert_scores = 0
+    ob.build() if not ob.LIB.exists() else None
+    ob.sw_lib()
+    workers = workers or min(16, os.cpu_count() or 1)
+    bases = int(sum(int(d.lr_off[i + 1] - d.lr_off[i]) for i in lrs))
+    t = time.perf_counter()
+    if workers == 1:
+        res = [_lr_chain(i) for i in lrs]
+    else:
+        with mp.get_context("fork").Pool(workers, initializer=_init_worker) as pool:
+            res = pool.map(_lr_chain, list(lrs), chunksize=1)
+    return time.perf_counter() - t, bases, res, workers

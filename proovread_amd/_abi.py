@@ -87,10 +87,6 @@ def lib():
     L.pr_cns_download.argtypes = [C.c_void_p, C.POINTER(CnsOut)]
     L.pr_cns_last_timing.argtypes = [C.c_void_p, PD, PD]
     L.pr_cns_resident_stats.argtypes = [C.c_void_p, P64, P64]
-    for name in ("pr_sw_upload", "pr_sw_launch", "pr_sw_download", "pr_sw_run", "pr_sw_last_timing",
-                 "pr_sw_resident_stats"):
-        if not hasattr(L, name):
-            continue
     _lib = L
     return L
 

@@ -28,5 +28,7 @@ struct PipeDev {
 };
 
 int pipe_launch(const PipeDev &P, int grid, void *stream, int lds_sort);
+int iter_stats_launch(const int64_t *out_off, const int32_t *status, const int32_t *seq_len, const uint8_t *qual,
+                      int n_lr, int min_char, unsigned long long *out, void *stream);
 
 }  // namespace prgpu

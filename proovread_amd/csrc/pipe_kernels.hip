@@ -116,6 +116,38 @@ __global__ void __launch_bounds__(PIPE_THREADS) pipe_sort_kernel(PipeDev P) {
     }
 }
 
+// per-iteration statistic gathered across GPUs (proovread:1702-1720 computes
+// bpN/bpt with SeqFilter --phred-mask; here: corrected bases and bases with
+// phred >= min_phred, summed into out[0..1] on the device)
+__global__ void __launch_bounds__(256) iter_stats_kernel(const int64_t *out_off, const int32_t *status,
+                                                         const int32_t *seq_len, const uint8_t *qual, int n_lr,
+                                                         int min_char, unsigned long long *out) {
+    unsigned long long tot = 0, hq = 0;
+    for (int lr = blockIdx.x; lr < n_lr; lr += gridDim.x) {
+        if (status[lr] != 0) continue;
+        const int64_t o = out_off[lr];
+        const int n = seq_len[lr];
+        if (threadIdx.x == 0) tot += (unsigned long long)n;
+        for (int i = threadIdx.x; i < n; i += 256) hq += qual[o + i] >= min_char ? 1ull : 0ull;
+    }
+    for (int o = 32; o > 0; o >>= 1) { tot += __shfl_down(tot, o, 64); hq += __shfl_down(hq, o, 64); }
+    if ((threadIdx.x & 63) == 0) {
+        if (tot) atomicAdd(&out[0], tot);
+        if (hq) atomicAdd(&out[1], hq);
+    }
+}
+
+int iter_stats_launch(const int64_t *out_off, const int32_t *status, const int32_t *seq_len, const uint8_t *qual,
+                      int n_lr, int min_char, unsigned long long *out, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(out, 0, 16, s);
+    if (e != hipSuccess) return (int)e;
+    const int grid = n_lr < 2048 ? (n_lr > 0 ? n_lr : 1) : 2048;
+    hipLaunchKernelGGL(iter_stats_kernel, dim3(grid), dim3(256), 0, s, out_off, status, seq_len, qual, n_lr,
+                       min_char, out);
+    return (int)hipGetLastError();
+}
+
 int pipe_launch(const PipeDev &P, int grid, void *stream, int lds_sort) {
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(pipe_count_kernel, dim3(grid), dim3(PIPE_THREADS), 0, s, P);

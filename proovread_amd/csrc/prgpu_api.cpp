@@ -572,11 +572,38 @@ extern "C" int pr_iter_download(pr_ctx *c, pr_cns_out *o) {
 
 extern "C" int pr_iter_last_timing(pr_ctx *c, double *ms_sw_extend, double *ms_sw_global, double *ms_assemble,
                                    double *ms_consensus) {
+    // HIP events of the last pr_iter_launch (the caller has synchronised):
+    // ev2 | SW extend | ev3 | SW global | ev0 | hand-off | ev4 | consensus | ev5
     if (!c) return set_error(PR_ERR_ARG, "null ctx");
-    if (ms_sw_extend) *ms_sw_extend = c->sw.ms_ext;
-    if (ms_sw_global) *ms_sw_global = c->sw.ms_glob;
-    if (ms_assemble) *ms_assemble = c->ms_pipe;
-    if (ms_consensus) *ms_consensus = c->last_ms;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    const int pairs[4][2] = {{2, 3}, {3, 0}, {0, 4}, {4, 5}};
+    for (int k = 0; k < 4; ++k)
+        if (hipEventElapsedTime(&v[k], c->ev[pairs[k][0]], c->ev[pairs[k][1]]) != hipSuccess) v[k] = 0.f;
+    if (ms_sw_extend) *ms_sw_extend = v[0];
+    if (ms_sw_global) *ms_sw_global = v[1];
+    if (ms_assemble) *ms_assemble = v[2];
+    if (ms_consensus) *ms_consensus = v[3];
+    return 0;
+}
+
+extern "C" int pr_iter_alignment_stats(pr_ctx *c, int64_t *n_aln, int64_t *sum_ncig, int64_t *sum_lseq) {
+    // reported alignments of the last iteration (for the SURVEY.md §8d pileup byte model)
+    if (!c || !c->pipe) return set_error(PR_ERR_ARG, "no resident iteration batch");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int64_t na = 0;
+    HIPCHK(hipMemcpy(&na, c->cb[CB_ALN_OFF].as<int64_t>() + c->n_lr, 8, hipMemcpyDeviceToHost));
+    std::vector<int32_t> v((size_t)na + 1);
+    int64_t sc = 0, sl = 0;
+    if (na) {
+        HIPCHK(hipMemcpy(v.data(), c->cb[CB_NCIG].p, (size_t)na * 4, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < na; ++i) sc += v[i];
+        HIPCHK(hipMemcpy(v.data(), c->cb[CB_LSEQ].p, (size_t)na * 4, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < na; ++i) sl += v[i];
+    }
+    if (n_aln) *n_aln = na;
+    if (sum_ncig) *sum_ncig = sc;
+    if (sum_lseq) *sum_lseq = sl;
     return 0;
 }
 
@@ -585,6 +612,26 @@ extern "C" int pr_iter_bounds(pr_ctx *c, int32_t *n_lr, int64_t *n_task, pr_cns_
     if (n_lr) *n_lr = c->n_lr;
     if (n_task) *n_task = c->n_aln;
     if (bd) { bd->seq_cap = c->seq_cap; bd->chim_cap = c->chim_cap; }
+    return 0;
+}
+
+extern "C" int pr_ctx_sync(pr_ctx *c) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+extern "C" int pr_iter_stats(pr_ctx *c, int32_t min_phred, int64_t *dev_out) {
+    if (!c || !dev_out) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->cns_loaded) return set_error(PR_ERR_ARG, "no resident consensus batch");
+    HIPCHK(hipSetDevice(c->device));
+    DevBuf *B = c->cb;
+    int e = iter_stats_launch(B[CB_OUT_OFF].as<int64_t>(), B[CB_STATUS].as<int32_t>(), B[CB_SEQ_LEN].as<int32_t>(),
+                              B[CB_O_QUAL].as<uint8_t>(), c->n_lr, min_phred + 33,
+                              reinterpret_cast<unsigned long long *>(dev_out), (void *)c->stream);
+    if (e) return set_error(PR_ERR_HIP, "stats kernel: %s", hipGetErrorString((hipError_t)e));
     return 0;
 }
 

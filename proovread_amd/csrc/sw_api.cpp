@@ -243,6 +243,11 @@ extern "C" int pr_sw_last_timing(pr_ctx *c, double *ms_extend, double *ms_global
 extern "C" int pr_sw_last_cells(pr_ctx *c, int64_t *ce, int64_t *cg) {
     if (!c) return pr_set_error(PR_ERR_ARG, "null ctx");
     SwResident &r = ctx_sw(c);
+    if (r.loaded && r.buf[SB_CELLS]) {
+        HIPCHK(hipSetDevice(ctx_device(c)));
+        HIPCHK(hipStreamSynchronize(ctx_stream(c)));
+        HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 16, hipMemcpyDeviceToHost));
+    }
     if (ce) *ce = (int64_t)r.cells[0];
     if (cg) *cg = (int64_t)r.cells[1];
     return 0;

@@ -26,6 +26,9 @@ def _setup(L):
     L.pr_iter_download.argtypes = [C.c_void_p, C.POINTER(_abi.CnsOut)]
     L.pr_iter_bounds.argtypes = [C.c_void_p, _abi.P32, _abi.P64, C.POINTER(_abi.CnsBounds)]
     L.pr_iter_last_timing.argtypes = [C.c_void_p, _abi.PD, _abi.PD, _abi.PD, _abi.PD]
+    L.pr_iter_stats.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+    L.pr_ctx_sync.argtypes = [C.c_void_p]
+    L.pr_iter_alignment_stats.argtypes = [C.c_void_p, _abi.P64, _abi.P64, _abi.P64]
     L._iter_ready = True
 
 
@@ -60,6 +63,13 @@ class Iteration:
         self._so = sw_opts
         _abi.check(self.L.pr_iter_launch(self.ctx.h, C.byref(sw_opts), C.byref(self._pc)), "pr_iter_launch")
 
+    def sync(self):
+        _abi.check(self.L.pr_ctx_sync(self.ctx.h), "pr_ctx_sync")
+
+    def stats_to(self, dev_ptr: int, min_phred: int = 20):
+        """Enqueue {corrected bases, bases >= min_phred} into device memory dev_ptr (int64[2])."""
+        _abi.check(self.L.pr_iter_stats(self.ctx.h, min_phred, C.c_void_p(dev_ptr)), "pr_iter_stats")
+
     def _out_buffers(self, bin_size=20.0):
         n = self.n_lr
         lens = np.diff(self.d.lr_off)
@@ -86,6 +96,11 @@ class Iteration:
         a, o = self.out
         _abi.check(self.L.pr_iter_download(self.ctx.h, C.byref(o)), "pr_iter_download")
         return a
+
+    def alignment_stats(self):
+        v = [C.c_int64() for _ in range(3)]
+        _abi.check(self.L.pr_iter_alignment_stats(self.ctx.h, *[C.byref(x) for x in v]), "alignment_stats")
+        return [x.value for x in v]
 
     def timing(self):
         v = [C.c_double() for _ in range(4)]
