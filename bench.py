@@ -129,6 +129,7 @@ def main():
     ms /= max(args.steps, 1)
     me, mg, ce, cg = sw.last_timing(ctx)
     a = it.download()
+    cns_phases = it.cns_phase_ms()
     ok = int((a["status"] == 0).sum())
     hq = stats.cpu().tolist()
     if rank != 0:
@@ -171,6 +172,7 @@ def main():
         "sw_gcups": round(cells / ((ms[0] + ms[1]) * 1e-3) / 1e9, 2),
         "stage_ms": {"sw_extend": round(ms[0], 3), "sw_global_cigar": round(ms[1], 3),
                      "handoff_sort": round(ms[2], 3), "consensus": round(ms[3], 3)},
+        "consensus_phase_ms_summed_over_workgroups": {k: round(v, 1) for k, v in cns_phases.items()},
         "roofline": {
             "kernel": "sw_extend_kernel (ksw_extend2, one task per lane)",
             "bound": "valu",

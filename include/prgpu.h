@@ -146,6 +146,10 @@ int pr_cns_download(pr_ctx *ctx, pr_cns_out *o);            /* syncs            
 int pr_cns_last_timing(pr_ctx *ctx, double *ms_prep, double *ms_pileup);
 /* number of columns (sum of long-read lengths) and algorithmic bytes of the resident batch
  * (SURVEY.md §8d pileup byte model) */
+/* Diagnostics: wall-clock ticks (100 MHz) the consensus workgroups spent per phase in the
+ * last launch, summed over workgroups: [prep, binning, state table, pileup scatter,
+ * argmax+write, Trace2cigar, chimera, dequeue/idle]; n must be >= 8. */
+int pr_cns_phase_ticks(pr_ctx *ctx, uint64_t *ticks, int n);
 int pr_cns_resident_stats(pr_ctx *ctx, int64_t *columns, int64_t *alg_bytes);
 
 

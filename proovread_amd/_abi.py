@@ -86,6 +86,7 @@ def lib():
     L.pr_cns_launch.argtypes = [C.c_void_p, C.POINTER(CnsParams)]
     L.pr_cns_download.argtypes = [C.c_void_p, C.POINTER(CnsOut)]
     L.pr_cns_last_timing.argtypes = [C.c_void_p, PD, PD]
+    L.pr_cns_phase_ticks.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]
     L.pr_cns_resident_stats.argtypes = [C.c_void_p, P64, P64]
     _lib = L
     return L

@@ -68,6 +68,7 @@ struct CnsDev {
     int64_t *bin_off;    // [n_lr+1] prefix of bins
     int64_t *bin_bases;  // per bin
     int32_t *work;       // [1] dequeue counter
+    unsigned long long *prof;  // [CNS_NPHASE] summed wall-clock ticks per phase (may be null)
     // outputs
     const int64_t *out_off;  // [n_lr+1]
     const int64_t *chim_off; // [n_lr+1]
@@ -89,5 +90,6 @@ constexpr int WCOLS = 512;       // columns per pileup window
 constexpr int WCAP = 1024;       // (column, insertion state) pairs per window
 constexpr int CHIM_MAXCOLS = 128;
 constexpr int CHIM_TCAP = 256;
+constexpr int CNS_NPHASE = 8;    // prep, binning, state table, scatter, argmax+write, cigar, chimera, idle
 
 }  // namespace prgpu

@@ -432,52 +432,72 @@ __device__ __forceinline__ unsigned long long chim_order(const STab &T, int slot
     return oc != 0xFFFFFFFFu ? (unsigned long long)oc : (1ULL << 32) | T.ord_all[slot];
 }
 
-__device__ void chim_hx(const uint32_t *f6, const uint32_t *ik, const uint32_t *ic, int ni,
-                        const STab &T, const uint32_t *f6b, const uint32_t *ikb, const uint32_t *icb,
-                        int nib, double *out) {
-    // Hx (Seq.pm:188-197) of a column given as fixed counts + insertion (slot,count)
-    // pairs, optionally summed with a second column (combined column, Seq.pm:857-865).
-    // Terms are visited in state-index order.
-    uint32_t slots[64];
-    uint32_t cnts[64];
-    int m = 0;
-    for (int i = 0; i < ni && m < 64; ++i) { slots[m] = ik[i]; cnts[m] = ic[i]; ++m; }
-    if (f6b) {
-        for (int i = 0; i < nib; ++i) {
-            int j = 0;
-            for (; j < m; ++j) if (slots[j] == ikb[i]) break;
-            if (j < m) cnts[j] += icb[i];
-            else if (m < 64) { slots[m] = ikb[i]; cnts[m] = icb[i]; ++m; }
-        }
+// count of (column c, slot) in a chimera side table (0 if absent)
+__device__ __forceinline__ uint32_t chim_count(const uint32_t *tk, const uint32_t *tc, uint32_t key) {
+    uint32_t h = (key * 2654435761u) >> 24;
+    for (int p = 0; p < CHIM_TCAP; ++p) {
+        const uint32_t x = tk[h];
+        if (x == key) return tc[h];
+        if (x == 0u) return 0u;
+        h = (h + 1) & (CHIM_TCAP - 1);
     }
-    // sort insertion entries by chimera index order (insertion sort; few entries)
-    for (int i = 1; i < m; ++i) {
-        uint32_t s = slots[i], c = cnts[i];
-        unsigned long long o = chim_order(T, (int)s);
-        int j = i - 1;
-        while (j >= 0 && chim_order(T, (int)slots[j]) > o) { slots[j + 1] = slots[j]; cnts[j + 1] = cnts[j]; --j; }
-        slots[j + 1] = s; cnts[j + 1] = c;
-    }
+    return 0u;
+}
+
+// Hx (Seq.pm:188-197) of column c of the left matrix (side 0), the right matrix
+// (side 1) or their element-wise sum (side 2, the combined column of
+// Seq.pm:857-865).  Fixed states first, then insertion states in state-index
+// order (selection over the LDS tables: no per-thread arrays).
+__device__ double chim_hx(int side, int c, const uint32_t *f6l, const uint32_t *f6r, const uint32_t *tkl,
+                          const uint32_t *tcl, const uint32_t *tkr, const uint32_t *tcr, const STab &T) {
+    const double l2 = log(2.0);
     double total = 0.0;
     for (int s = 0; s < 6; ++s) {
-        const uint32_t v = f6[s] + (f6b ? f6b[s] : 0u);
+        const uint32_t v = (side != 1 ? f6l[c * 6 + s] : 0u) + (side != 0 ? f6r[c * 6 + s] : 0u);
         if (v) total += (double)v;
     }
-    for (int i = 0; i < m; ++i) if (cnts[i]) total += (double)cnts[i];
+    // pass 0: total over insertion states; pass 1: entropy terms
     double h = 0.0;
-    const double l2 = log(2.0);
-    for (int s = 0; s < 6; ++s) {
-        const uint32_t v = f6[s] + (f6b ? f6b[s] : 0u);
-        if (!v) continue;
-        const double p = (double)v / total;
-        h -= p * (log(p) / l2);
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1) {
+            for (int s = 0; s < 6; ++s) {
+                const uint32_t v = (side != 1 ? f6l[c * 6 + s] : 0u) + (side != 0 ? f6r[c * 6 + s] : 0u);
+                if (!v) continue;
+                const double p = (double)v / total;
+                h -= p * (log(p) / l2);
+            }
+        }
+        unsigned long long prev = 0;
+        bool first = true;
+        for (;;) {
+            unsigned long long best = ~0ULL;
+            int bslot = -1;
+            for (int t = 0; t < 2; ++t) {
+                if ((t == 0 && side == 1) || (t == 1 && side == 0)) continue;
+                const uint32_t *tk = t == 0 ? tkl : tkr;
+                for (int e = 0; e < CHIM_TCAP; ++e) {
+                    const uint32_t k = tk[e];
+                    if (!k || (int)(k >> 11) - 1 != c) continue;
+                    const int slot = (int)(k & 2047u);
+                    const unsigned long long o = chim_order(T, slot);
+                    if ((first || o > prev) && o < best) { best = o; bslot = slot; }
+                }
+            }
+            if (bslot < 0) break;
+            const uint32_t key = ((uint32_t)(c + 1) << 11) | (uint32_t)bslot;
+            const uint32_t v = (side != 1 ? chim_count(tkl, tcl, key) : 0u) + (side != 0 ? chim_count(tkr, tcr, key) : 0u);
+            if (v) {
+                if (pass == 0) total += (double)v;
+                else {
+                    const double p = (double)v / total;
+                    h -= p * (log(p) / l2);
+                }
+            }
+            prev = best;
+            first = false;
+        }
     }
-    for (int i = 0; i < m; ++i) {
-        if (!cnts[i]) continue;
-        const double p = (double)cnts[i] / total;
-        h -= p * (log(p) / l2);
-    }
-    *out = h;
+    return h;
 }
 
 // ---------------------------------------------------------------------------
@@ -488,6 +508,17 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
     uint8_t *A = smem + OFF_A;
     uint8_t *B = smem + OFF_B;
     const int tid = threadIdx.x;
+    // phase clock (thread 0, 100 MHz wall clock): ticks per phase summed over workgroups
+    unsigned long long pt[CNS_NPHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tlast = wall_clock64();
+#define CNS_TICK(ph)                                                      \
+    do {                                                                  \
+        if (D.prof && tid == 0) {                                         \
+            const unsigned long long t_ = wall_clock64();                 \
+            pt[ph] += t_ - tlast;                                         \
+            tlast = t_;                                                   \
+        }                                                                 \
+    } while (0)
 
     for (;;) {
         if (tid == 0) {
@@ -500,6 +531,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         }
         __syncthreads();
         const int lr = C->lr;
+        CNS_TICK(7);
         if (lr >= D.n_lr) break;
         const int64_t a0 = D.aln_off[lr];
         const int na = (int)(D.aln_off[lr + 1] - a0);
@@ -523,6 +555,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         }
         if (nbins > MAX_BINS_LDS && tid == 0) set_err(C, 0, PR_ERR_CODE_CAP);
         __syncthreads();
+        CNS_TICK(0);
         if (C->err_first != ~0ULL) {
             if (tid == 0) {
                 D.status[lr] = -(int)(C->err_first & 0xFF);
@@ -597,6 +630,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             }
             __syncthreads();
         }
+        CNS_TICK(1);
         // kept alignments that State_matrix would die on (Seq.pm:313/348/430)
         for (int i = tid; i < na; i += CNS_THREADS) {
             if (!D.kept[a0 + i]) continue;
@@ -655,6 +689,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             continue;
         }
 
+        CNS_TICK(2);
         // ---- 4. windowed pileup + argmax (Seq.pm:438-461, 1568-1654)
         uint32_t *cnt6 = reinterpret_cast<uint32_t *>(B + B_CNT6);
         uint32_t *wkey = reinterpret_cast<uint32_t *>(B + B_WKEY);
@@ -692,6 +727,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                                    });
             }
             __syncthreads();
+            CNS_TICK(3);
             // per-column lists of insertion entries (counting sort)
             for (int e = tid; e < WCAP; e += CNS_THREADS)
                 if (wkey[e]) atomicAdd(&colcnt[(wkey[e] >> 11) - 1], 1);
@@ -722,16 +758,23 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     double val[6];
                     bool def[6];
                     bool any = false;
-#pragma unroll
-                    for (int s = 0; s < 6; ++s) { val[s] = (double)f6[s]; def[s] = f6[s] != 0u; any |= def[s]; }
+                    int rs = -1;
+                    double vref = 0.0;
                     if (use_rq) {
                         const double fr = phred2freq((int)D.ref_qual[r0 + col] - P.ref_phred_offset);
                         if (fr != 0.0) {
-                            const int rs = fixed_idx(ref_base(D, r0 + col));
-                            double v = fr;   // ref freq is added first, then +1 per alignment
-                            for (uint32_t k = 0; k < f6[rs]; ++k) v = __dadd_rn(v, 1.0);
-                            val[rs] = v; def[rs] = true; any = true;
+                            rs = fixed_idx(ref_base(D, r0 + col));
+                            vref = fr;   // ref freq is added first, then +1 per alignment
+                            const uint32_t n = f6[rs];
+                            for (uint32_t k = 0; k < n; ++k) vref = __dadd_rn(vref, 1.0);
                         }
+                    }
+#pragma unroll
+                    for (int s = 0; s < 6; ++s) {
+                        const uint32_t n = f6[s];
+                        val[s] = s == rs ? vref : (double)n;
+                        def[s] = (n != 0u) || (s == rs);
+                        any |= def[s];
                     }
                     const int ne = colcnt[c];
                     any |= ne > 0;
@@ -824,6 +867,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 }
                 __syncthreads();
             }
+            CNS_TICK(4);
         }
         if (C->flag) {
             if (tid == 0) {
@@ -867,6 +911,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             }
         }
 
+        CNS_TICK(5);
         // ---- 6. chimera (Seq.pm:774-889) + detect_chimera (bam2cns:461-491)
         int nch = 0;
         if (P.detect_chimera && nbins > 20) {
@@ -964,19 +1009,16 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 if (empty) continue;
                 int npos = 0, ntot = 0;
                 for (int c = tid; c < ncol; c += CNS_THREADS) {
-                    uint32_t ikl[64], icl[64], ikr[64], icr[64];
-                    int nl = 0, nr = 0;
-                    for (int h = 0; h < CHIM_TCAP; ++h) {
-                        if (tkl[h] && (int)(tkl[h] >> 11) - 1 == c && nl < 64) { ikl[nl] = tkl[h] & 2047u; icl[nl] = tcl[h]; ++nl; }
-                        if (tkr[h] && (int)(tkr[h] >> 11) - 1 == c && nr < 64) { ikr[nr] = tkr[h] & 2047u; icr[nr] = tcr[h]; ++nr; }
-                    }
-                    bool nel = nl > 0, ner = nr > 0;
+                    bool nel = false, ner = false;
                     for (int s = 0; s < 6; ++s) { nel |= f6l[c * 6 + s] != 0u; ner |= f6r[c * 6 + s] != 0u; }
+                    for (int e = 0; e < CHIM_TCAP; ++e) {
+                        nel |= tkl[e] != 0u && (int)(tkl[e] >> 11) - 1 == c;
+                        ner |= tkr[e] != 0u && (int)(tkr[e] >> 11) - 1 == c;
+                    }
                     if (!nel || !ner) continue;
-                    double hr, hl, hc;
-                    chim_hx(f6r + c * 6, ikr, icr, nr, T, nullptr, nullptr, nullptr, 0, &hr);
-                    chim_hx(f6l + c * 6, ikl, icl, nl, T, nullptr, nullptr, nullptr, 0, &hl);
-                    chim_hx(f6l + c * 6, ikl, icl, nl, T, f6r + c * 6, ikr, icr, nr, &hc);
+                    const double hr = chim_hx(1, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
+                    const double hl = chim_hx(0, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
+                    const double hc = chim_hx(2, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
                     const double hgt = hr > hl ? hr : hl;
                     ++ntot;
                     if (hc - hgt > 0.7) ++npos;
@@ -1021,6 +1063,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 __syncthreads();
             }
         }
+        CNS_TICK(6);
         if (tid == 0) {
             if (!C->flag) D.status[lr] = 0;
             D.seq_len[lr] = C->run_seq;
@@ -1030,6 +1073,9 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         }
         __syncthreads();
     }
+    if (D.prof && tid == 0)
+        for (int k = 0; k < CNS_NPHASE; ++k) atomicAdd(&D.prof[k], pt[k]);
+#undef CNS_TICK
 }
 
 }  // namespace prgpu

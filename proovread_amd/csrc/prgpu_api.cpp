@@ -66,7 +66,7 @@ enum CnsBufId {
     CB_A_ST, CB_A_LEN, CB_A_NC, CB_A_BIN, CB_A_CB, CB_A_CE, CB_A_SB, CB_A_RPOS, CB_A_END,
     CB_SORTED, CB_LST_SCORE, CB_LST_ALN, CB_KEPT, CB_BIN_OFF, CB_BIN_BASES, CB_WORK,
     CB_OUT_OFF, CB_CHIM_OFF, CB_STATUS, CB_SEQ_LEN, CB_TRACE_LEN, CB_NCIGAR, CB_NCHIM,
-    CB_O_SEQ, CB_O_QUAL, CB_O_TRACE, CB_O_CIG, CB_O_CHIM,
+    CB_O_SEQ, CB_O_QUAL, CB_O_TRACE, CB_O_CIG, CB_O_CHIM, CB_PROF,
     CB_COUNT
 };
 
@@ -274,6 +274,7 @@ extern "C" int pr_cns_upload(pr_ctx *c, const pr_cns_batch *b) {
         (rc = B[CB_KEPT].ensure(na1)))
         return rc;
     if ((rc = B[CB_WORK].ensure(64))) return rc;
+    if ((rc = B[CB_PROF].ensure(CNS_NPHASE * 8))) return rc;
     if ((rc = upload(B[CB_OUT_OFF], c->out_off.data(), n + 1, s))) return rc;
     if ((rc = upload(B[CB_CHIM_OFF], c->chim_off.data(), n + 1, s))) return rc;
     const size_t n1 = (size_t)n + 1;
@@ -348,6 +349,7 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
     D.bin_off = B[CB_BIN_OFF].as<int64_t>();
     D.bin_bases = B[CB_BIN_BASES].as<int64_t>();
     D.work = B[CB_WORK].as<int32_t>();
+    D.prof = B[CB_PROF].as<unsigned long long>();
     D.out_off = B[CB_OUT_OFF].as<int64_t>();
     D.chim_off = B[CB_CHIM_OFF].as<int64_t>();
     D.status = B[CB_STATUS].as<int32_t>();
@@ -386,6 +388,7 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         D.cig = sp.cig;
     }
     HIPCHK(hipMemsetAsync(D.work, 0, 64, c->stream));
+    HIPCHK(hipMemsetAsync(D.prof, 0, CNS_NPHASE * 8, c->stream));
     const int grid = c->n_lr < c->n_cu * 2 ? c->n_lr : c->n_cu * 2;
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
     int e = cns_launch(D, P, grid, (void *)c->stream);
@@ -440,6 +443,15 @@ extern "C" int pr_cns_last_timing(pr_ctx *c, double *ms_prep, double *ms_pileup)
     if (!c) return set_error(PR_ERR_ARG, "null ctx");
     if (ms_prep) *ms_prep = 0.0;
     if (ms_pileup) *ms_pileup = c->last_ms;
+    return 0;
+}
+
+extern "C" int pr_cns_phase_ticks(pr_ctx *c, uint64_t *ticks, int n) {
+    if (!c || !ticks || n < CNS_NPHASE) return set_error(PR_ERR_ARG, "need ctx and %d ticks", CNS_NPHASE);
+    if (!c->cns_loaded || !c->cb[CB_PROF].p) return set_error(PR_ERR_ARG, "no consensus launch yet");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(ticks, c->cb[CB_PROF].p, CNS_NPHASE * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -509,7 +521,8 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
         (rc = B[CB_A_SB].ensure(na1 * 4)) || (rc = B[CB_A_RPOS].ensure(na1 * 4)) ||
         (rc = B[CB_A_END].ensure(na1 * 4)) || (rc = B[CB_SORTED].ensure(na1 * 4)) ||
         (rc = B[CB_LST_SCORE].ensure(na1 * 8)) || (rc = B[CB_LST_ALN].ensure(na1 * 4)) ||
-        (rc = B[CB_KEPT].ensure(na1)) || (rc = B[CB_WORK].ensure(64)))
+        (rc = B[CB_KEPT].ensure(na1)) || (rc = B[CB_WORK].ensure(64)) ||
+        (rc = B[CB_PROF].ensure(CNS_NPHASE * 8)))
         return rc;
     if ((rc = upload(B[CB_OUT_OFF], c->out_off.data(), n1, s))) return rc;
     if ((rc = upload(B[CB_CHIM_OFF], c->chim_off.data(), n1, s))) return rc;

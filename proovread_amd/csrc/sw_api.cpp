@@ -1,6 +1,7 @@
 // Host side of the SW stage C-ABI (include/prgpu.h pr_sw_*).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -32,6 +33,8 @@ enum SwBuf {
     SB_CIG, SB_Z
 };
 static const int SB_CELLS = 24;
+static const int SB_PERM = 25;
+static const int SB_BUCKET = 26;
 
 namespace prgpu {
 void sw_release(SwResident &r) {
@@ -113,6 +116,8 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
     const size_t n4 = (size_t)(nt + 1) * 4;
     for (int id : {SB_QB, SB_QE, SB_RB, SB_RE, SB_SCORE, SB_TRUESC, SB_W, SB_GSCORE, SB_POS, SB_NCIG, SB_STATUS})
         if ((rc = ensure(r, id, n4))) return rc;
+    if ((rc = ensure(r, SB_PERM, (size_t)(nt + 1) * 4)) || (rc = ensure(r, SB_BUCKET, (SW_NBUCKET + 1) * 4)))
+        return rc;
     if ((rc = ensure(r, SB_PASS, (size_t)nt + 1)) || (rc = ensure(r, SB_CIG, (size_t)(nt + 1) * SW_MAXCIG * 4)) ||
         (rc = ensure(r, SB_CELLS, 64)))
         return rc;
@@ -131,14 +136,15 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch (pr_sw_upload first)");
     if (o->a <= 0 || o->b < 0 || o->e_del <= 0 || o->e_ins <= 0 || o->w <= 0)
         return pr_set_error(PR_ERR_ARG, "bad scoring options");
-    if ((long)o->a * 2 * r.qmax >= 16384)
-        return pr_set_error(PR_ERR_ARG, "a * 2 * max read length must stay below 16384 (14-bit LDS words)");
+    if ((long)o->a * r.qmax >= 8192)
+        return pr_set_error(PR_ERR_ARG, "a * max read length must stay below 8192 (13-bit LDS words)");
     HIPCHK(hipSetDevice(ctx_device(c)));
     hipStream_t s = ctx_stream(c);
     SwOptsDev O;
     O.a = o->a; O.b = o->b; O.o_del = o->o_del; O.e_del = o->e_del; O.o_ins = o->o_ins; O.e_ins = o->e_ins;
     O.w = o->w; O.pen_clip5 = o->pen_clip5; O.pen_clip3 = o->pen_clip3; O.zdrop = o->zdrop;
     O.min_score_per_base = o->min_score_per_base;
+    O.debug = getenv("PRGPU_SW_DEBUG") ? atoi(getenv("PRGPU_SW_DEBUG")) : 0;
     SwDev D;
     std::memset(&D, 0, sizeof D);
     D.n_task = r.n_task;
@@ -169,14 +175,16 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.o_cig = (uint32_t *)r.buf[SB_CIG];
     D.cells = (unsigned long long *)r.buf[SB_CELLS];
     D.work = (int32_t *)((char *)r.buf[SB_CELLS] + 32);
+    D.perm = (int32_t *)r.buf[SB_PERM];
+    D.bucket = (int32_t *)r.buf[SB_BUCKET];
     // LDS: extension = (qmax+1) words per lane; global = same + lane-major query bytes
     const int lds_ext = (r.qmax + 1) * SW_WAVE * 4;
-    const int qpad = (r.qmax + 4) & ~3;
+    const int qpad = (r.qmax + 8) & ~3;
     const int lds_glob = lds_ext + SW_WAVE * qpad;
     if (lds_glob > 160 * 1024) return pr_set_error(PR_ERR_ARG, "short reads too long for the LDS layout");
     const int blocks_per_cu = (160 * 1024) / (lds_glob + 64) > 0 ? (160 * 1024) / (lds_glob + 64) : 1;
     const int grid_g = ctx_ncu(c) * (blocks_per_cu < 8 ? blocks_per_cu : 8);
-    D.z_slab = (int64_t)D.tmax * r.qmax * SW_WAVE;
+    D.z_slab = (int64_t)D.tmax * ((r.qmax + 3) / 4) * 4 * SW_WAVE;
     int rc;
     if ((rc = ensure(r, SB_Z, (size_t)D.z_slab * grid_g))) return rc;
     D.z = (uint8_t *)r.buf[SB_Z];
@@ -184,7 +192,9 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if (r.n_task == 0) return 0;
     const int grid_e = (int)((r.n_task + SW_WAVE - 1) / SW_WAVE);
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
-    int e = sw_launch_extend(D, O, grid_e, lds_ext, (void *)s);
+    int e = sw_launch_order(D, (void *)s);
+    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    e = sw_launch_extend(D, O, grid_e, lds_ext, (void *)s);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
     e = sw_launch_global(D, O, grid_g, lds_glob, (void *)s);

@@ -6,10 +6,12 @@ namespace prgpu {
 
 constexpr int SW_MAXCIG = 128;   // CIGAR ops per task (PR_SW_MAXCIG)
 constexpr int SW_WAVE = 64;
+constexpr int SW_NBUCKET = 1 << 15;   // (left extension length, right extension length / 8) keys
 
 struct SwOptsDev {
     int a, b, o_del, e_del, o_ins, e_ins, w, pen_clip5, pen_clip3, zdrop;
     double min_score_per_base;
+    int debug;   // timing ablations only (PRGPU_SW_DEBUG): 1 = skip backtrack, 2 = skip z stores
 };
 
 struct SwDev {
@@ -31,6 +33,8 @@ struct SwDev {
     uint8_t *z;                // direction-matrix slabs, one per resident block
     int64_t z_slab;            // bytes per slab
     unsigned long long *cells; // [2] canonical DP cells (extension, global)
+    int32_t *perm;             // lane -> task order (tasks bucketed by extension lengths)
+    int32_t *bucket;           // [SW_NBUCKET + 1] counting-sort scratch
     int32_t *work;             // dequeue counter for the global kernel
 };
 
@@ -54,6 +58,7 @@ struct SwPtrs {
     int n_sr, n_lr;
 };
 
+int sw_launch_order(const SwDev &D, void *stream);
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
 void sw_release(SwResident &r);

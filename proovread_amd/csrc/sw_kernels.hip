@@ -27,13 +27,26 @@ __device__ __forceinline__ int sw_score(int t, int q, int a, int b) {
     return (t > 3 || q > 3) ? -1 : (t == q ? a : -b);
 }
 
-// ---- extension: packed word = h[0,14) | e[14,28) | q[28,31)
-__device__ __forceinline__ uint32_t pk(int h, int e, int q) {
-    return (uint32_t)h | ((uint32_t)e << 14) | ((uint32_t)q << 28);
+// ---- extension: packed LDS word = h[0,13) | e[13,26) | 8*q[26,32)
+// (H and E of ksw_extend2 are >= 0 and bounded by a * read length < 8192;
+// the query base is stored pre-multiplied by 8 to index the row score table)
+__device__ __forceinline__ uint32_t pk(int h, int e, uint32_t q8) {
+    return (uint32_t)h | ((uint32_t)e << 13) | (q8 << 26);
 }
-__device__ __forceinline__ int pk_h(uint32_t w) { return (int)(w & 0x3FFFu); }
-__device__ __forceinline__ int pk_e(uint32_t w) { return (int)((w >> 14) & 0x3FFFu); }
-__device__ __forceinline__ int pk_q(uint32_t w) { return (int)(w >> 28); }
+constexpr uint32_t PK_HE = (1u << 26) - 1u;
+__device__ __forceinline__ int imax3(int a, int b, int c) { return max(max(a, b), c); }
+// bwa_fill_scmat row for target base tc as bytes q = 0..4 (N row / column = -1)
+__device__ __forceinline__ uint64_t score_row(int tc, int a, int b) {
+    uint32_t lo;
+    if (tc > 3) {
+        lo = 0xFFFFFFFFu;
+    } else {
+        const uint32_t mm = (uint32_t)(uint8_t)(int8_t)(-b);
+        lo = mm * 0x01010101u;
+        lo = (lo & ~(0xFFu << (8 * tc))) | ((uint32_t)(uint8_t)a << (8 * tc));
+    }
+    return ((uint64_t)0xFFu << 32) | lo;
+}
 
 struct ExtIO {
     int qle, tle, gtle, gscore, max_off;
@@ -60,8 +73,8 @@ __device__ int ksw_extend_lane(uint32_t *eh, const uint8_t *Q, int qb, int qs, i
                 h = alive ? hp - e_ins : 0;
             }
             hp = h;
-            const int q = j < qlen ? (int)Q[qb + qs * j] : 0;
-            eh[j * SW_WAVE] = pk(h, 0, q);
+            const uint32_t q = j < qlen ? (uint32_t)Q[qb + qs * j] : 0u;
+            eh[j * SW_WAVE] = pk(h, 0, q << 3);
         }
     }
     int max_ins = (int)((double)(qlen * a + end_bonus - o_ins) / e_ins + 1.);
@@ -94,31 +107,28 @@ __device__ int ksw_extend_lane(uint32_t *eh, const uint8_t *Q, int qb, int qs, i
             if (h1 < 0) h1 = 0;
         } else
             h1 = 0;
+        const uint64_t srow = score_row(tc, a, b);
         int j;
+        uint32_t wd = eh[beg * SW_WAVE];
         for (j = beg; j < end; ++j) {
-            const uint32_t wd = eh[j * SW_WAVE];
-            int M = pk_h(wd), e = pk_e(wd);
-            const int qc = pk_q(wd);
-            const int hprev = h1;
-            M = M ? M + sw_score(tc, qc, a, b) : 0;
-            int h = M > e ? M : e;
-            h = h > f ? h : f;
-            h1 = h;
+            const uint32_t wn = eh[(j + 1) * SW_WAVE];   // prefetch: column j+1 is not written at j
+            const int Mr = (int)(wd & 0x1FFFu);
+            const int e0 = (int)((wd >> 13) & 0x1FFFu);
+            const uint32_t q8 = wd >> 26;
+            const int sc = (int)(int8_t)(uint8_t)(srow >> q8);
+            const int M = Mr ? Mr + sc : 0;   // separating H and M (ksw: no 100M3I3D20M)
+            const int h = imax3(M, e0, f);
             mj = m > h ? mj : j;
             m = m > h ? m : h;
-            int t = M - oe_del;
-            t = t > 0 ? t : 0;
-            e -= e_del;
-            e = e > t ? e : t;
-            t = M - oe_ins;
-            t = t > 0 ? t : 0;
-            f -= e_ins;
-            f = f > t ? f : t;
-            eh[j * SW_WAVE] = pk(hprev, e, qc);
+            const int e = imax3(e0 - e_del, M - oe_del, 0);
+            f = imax3(f - e_ins, M - oe_ins, 0);
+            eh[j * SW_WAVE] = pk(h1, e, q8);
+            h1 = h;
+            wd = wn;
         }
         {
-            const uint32_t wd = eh[end * SW_WAVE];
-            eh[end * SW_WAVE] = pk(h1, 0, pk_q(wd));
+            const uint32_t w2 = eh[end * SW_WAVE];
+            eh[end * SW_WAVE] = pk(h1, 0, w2 >> 26);
         }
         if (j == qlen) {
             max_ie = gscore > h1 ? max_ie : i;
@@ -136,9 +146,9 @@ __device__ int ksw_extend_lane(uint32_t *eh, const uint8_t *Q, int qb, int qs, i
                 if (max - m - ((mj - max_j) - (i - max_i)) * e_ins > O.zdrop) break;
             }
         }
-        for (j = beg; j < end && (eh[j * SW_WAVE] & 0x0FFFFFFFu) == 0u; ++j);
+        for (j = beg; j < end && (eh[j * SW_WAVE] & PK_HE) == 0u; ++j);
         beg = j;
-        for (j = end; j >= beg && (eh[j * SW_WAVE] & 0x0FFFFFFFu) == 0u; --j);
+        for (j = end; j >= beg && (eh[j * SW_WAVE] & PK_HE) == 0u; --j);
         end = j + 2 < qlen ? j + 2 : qlen;
     }
     io.qle = max_j + 1;
@@ -160,9 +170,10 @@ __device__ __forceinline__ int cal_max_gap(const SwOptsDev &O, int qlen) {
 __global__ void __launch_bounds__(SW_WAVE) sw_extend_kernel(SwDev D, SwOptsDev O) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_eh[];
     const int lane = threadIdx.x;
-    const int64_t t = (int64_t)blockIdx.x * SW_WAVE + lane;
+    const int64_t slot = (int64_t)blockIdx.x * SW_WAVE + lane;
     unsigned long long cells = 0;
-    if (t < D.n_task) {
+    if (slot < D.n_task) {
+        const int64_t t = D.perm[slot];
         uint32_t *eh = lds_eh + lane;
         const int sid = D.t_sr[t], lid = D.t_lr[t];
         const uint8_t *Q = D.sr + D.sr_off[sid];
@@ -262,10 +273,12 @@ __device__ __forceinline__ int infer_bw(int l1, int l2, int score, int a, int q,
     return w;
 }
 
-// ksw_global2 for one lane; direction bytes into the block's slab.
-__device__ int ksw_global_lane(uint32_t *eh, const uint8_t *qv /* lane query, LDS */, int qlen,
+// ksw_global2 for one lane.  Direction bytes (h-source | e-bit<<2 | f-bit<<5,
+// exactly ksw_global2's) are packed four per dword into the block's slab:
+// dword index ((row * nc4 + col/4) * 64 + lane), byte col%4.  qv holds 8*q.
+__device__ int ksw_global_lane(uint32_t *eh, const uint8_t *qv /* lane query (8*q), LDS */, int qlen,
                                const uint8_t *Lr, long tb, int ts, bool comp, int tlen,
-                               const SwOptsDev &O, int w, uint8_t *zl /* slab + lane */, int ncmax,
+                               const SwOptsDev &O, int w, uint32_t *zl /* slab + lane */, int nc4,
                                unsigned long long &cells) {
     const int a = O.a, b = O.b, o_del = O.o_del, e_del = O.e_del, o_ins = O.o_ins, e_ins = O.e_ins;
     const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
@@ -276,32 +289,43 @@ __device__ int ksw_global_lane(uint32_t *eh, const uint8_t *qv /* lane query, LD
     for (int i = 0; i < tlen; ++i) {
         int tc = (int)Lr[tb + (long)ts * i];
         if (comp && tc < 4) tc = 3 - tc;
+        const uint64_t srow = score_row(tc, a, b);
         const int beg = i > w ? i - w : 0;
         const int end = i + w + 1 < qlen ? i + w + 1 : qlen;
         int f = G_NEG;
         int h1 = beg == 0 ? -(o_del + e_del * (i + 1)) : G_NEG;
-        uint8_t *zi = zl + (long)i * ncmax * SW_WAVE;
+        uint32_t *zi = zl + (long)i * nc4 * SW_WAVE;
         cells += (unsigned long long)(end > beg ? end - beg : 0);
+        uint32_t wd = eh[beg * SW_WAVE];
+        uint32_t qn = qv[beg];
+        uint32_t dacc = 0;
         for (j = beg; j < end; ++j) {
-            const uint32_t wd = eh[j * SW_WAVE];
+            const uint32_t wn = eh[(j + 1) * SW_WAVE];   // prefetch (column j+1 is not written at j)
+            const uint32_t qc = qn;
+            qn = qv[j + 1];
             int m = gh(wd), e = ge(wd);
-            const int hprev = h1;
-            m += sw_score(tc, (int)qv[j], a, b);
+            m += (int)(int8_t)(uint8_t)(srow >> qc);
             uint32_t d = m >= e ? 0u : 1u;
             int h = m >= e ? m : e;
             d = h >= f ? d : 2u;
             h = h >= f ? h : f;
-            h1 = h;
-            int t = m - oe_del;
+            const int t1 = m - oe_del;
             e -= e_del;
-            d |= e > t ? 4u : 0u;
-            e = e > t ? e : t;
-            t = m - oe_ins;
+            d |= e > t1 ? 4u : 0u;
+            e = e > t1 ? e : t1;
+            const int t2 = m - oe_ins;
             f -= e_ins;
-            d |= f > t ? 32u : 0u;
-            f = f > t ? f : t;
-            eh[j * SW_WAVE] = gpk(hprev, e);
-            zi[(long)(j - beg) * SW_WAVE] = (uint8_t)d;
+            d |= f > t2 ? 32u : 0u;
+            f = f > t2 ? f : t2;
+            eh[j * SW_WAVE] = gpk(h1, e);
+            h1 = h;
+            wd = wn;
+            const int jj = j - beg;
+            dacc |= d << ((jj & 3) << 3);
+            if ((jj & 3) == 3 || j + 1 == end) {
+                if (!(O.debug & 2)) zi[(long)(jj >> 2) * SW_WAVE] = dacc;
+                dacc = 0;
+            }
         }
         eh[end * SW_WAVE] = gpk(h1, G_NEG);
     }
@@ -322,11 +346,11 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_g[];
     __shared__ int s_task;
     const int lane = threadIdx.x;
-    const int qpad = (D.qmax + 4) & ~3;
+    const int qpad = (D.qmax + 8) & ~3;
     uint32_t *eh = lds_g + lane;
     uint8_t *qv = reinterpret_cast<uint8_t *>(lds_g + (D.qmax + 1) * SW_WAVE) + lane * qpad;
-    uint8_t *zl = D.z + (int64_t)blockIdx.x * D.z_slab + lane;
-    const int ncmax = D.qmax;
+    const int nc4 = (D.qmax + 3) >> 2;
+    uint32_t *zl = reinterpret_cast<uint32_t *>(D.z + (int64_t)blockIdx.x * D.z_slab) + lane;
     unsigned long long cells = 0;
     for (;;) {
         if (lane == 0) s_task = atomicAdd(D.work, 1);
@@ -334,8 +358,9 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
         const int64_t t0 = (int64_t)s_task * SW_WAVE;
         __syncthreads();
         if (t0 >= D.n_task) break;
-        const int64_t t = t0 + lane;
-        if (t < D.n_task) {
+        const int64_t slot = t0 + lane;
+        if (slot < D.n_task) {
+            const int64_t t = D.perm[slot];
             const int sid = D.t_sr[t], lid = D.t_lr[t];
             const uint8_t *Q = D.sr + D.sr_off[sid];
             const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
@@ -346,7 +371,8 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
             const int truesc = D.o_truesc[t];
             const int lqq = qe - qb, rlen = re - rb;
             // query (reversed for the reverse strand: indels leftmost on the forward strand)
-            for (int j = 0; j < lqq; ++j) qv[j] = rev ? Q[qe - 1 - j] : Q[qb + j];
+            for (int j = 0; j < lqq; ++j) qv[j] = (uint8_t)((rev ? Q[qe - 1 - j] : Q[qb + j]) << 3);
+            qv[lqq] = 0;
             // reference rows: forward strand rb.., reverse strand comp(L[L-re+i])
             const long tb = rev ? (long)L - re : (long)rb;
             int tmpw = infer_bw(lqq, rlen, truesc, O.a, O.o_del, O.e_del);
@@ -368,7 +394,7 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
                     for (int i = 0; i < lqq; ++i) {
                         int tc = (int)Lr[tb + i];
                         if (rev && tc < 4) tc = 3 - tc;
-                        gsc += sw_score(tc, (int)qv[i], O.a, O.b);
+                        gsc += sw_score(tc, (int)(qv[i] >> 3), O.a, O.b);
                     }
                     ww = 0;
                 } else {
@@ -384,7 +410,7 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
                     const int min_w = dl + 3;
                     ww = ww > min_w ? ww : min_w;
                     cpass = 0;
-                    gsc = ksw_global_lane(eh, qv, lqq, Lr, tb, 1, rev, rlen, O, ww, zl, ncmax, cpass);
+                    gsc = ksw_global_lane(eh, qv, lqq, Lr, tb, 1, rev, rlen, O, ww, zl, nc4, cpass);
                 }
                 if (gsc == last_sc || w2 == O.w << 2) break;
                 last_sc = gsc;
@@ -395,14 +421,15 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
             int n = 0;
             if (ww < 0) {
                 n = 0;
-            } else if (nogap) {
+            } else if (nogap || (O.debug & 1)) {
                 cg[0] = ((uint32_t)lqq << 4);
                 n = 1;
             } else {
                 int i = rlen - 1, k = (i + ww + 1 < lqq ? i + ww + 1 : lqq) - 1, which = 0;
                 while (i >= 0 && k >= 0 && n >= 0) {
                     const int jj = k - (i > ww ? i - ww : 0);
-                    which = (zl[((long)i * ncmax + jj) * SW_WAVE] >> (which << 1)) & 3;
+                    const uint32_t zw = zl[((long)i * nc4 + (jj >> 2)) * SW_WAVE];
+                    which = ((zw >> ((jj & 3) << 3)) >> (which << 1)) & 3;
                     if (which == 0) n = push_op(cg, n, 0, 1), --i, --k;
                     else if (which == 1) n = push_op(cg, n, 2, 1), --i;
                     else n = push_op(cg, n, 1, 1), --k;
@@ -449,6 +476,60 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
     }
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
     if (lane == 0 && cells) atomicAdd(&D.cells[1], cells);
+}
+
+// ---------------------------------------------------------------------------
+// Task ordering: lanes of a wave run in lock-step, so tasks are bucketed by
+// (left extension length = qbeg, right extension length / 8) before the DP
+// kernels (counting sort; the order inside a bucket does not affect results).
+__device__ __forceinline__ int sw_task_key(const SwDev &D, int64_t t) {
+    const int sid = D.t_sr[t];
+    const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
+    const int qbeg = D.t_qbeg[t];
+    int right = (lq - qbeg - D.t_slen[t]) >> 3;
+    right = right < 31 ? right : 31;
+    const int left = qbeg < 1023 ? qbeg : 1023;
+    return (left << 5) | right;
+}
+__global__ void sw_order_count(SwDev D) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x)
+        atomicAdd(&D.bucket[sw_task_key(D, t)], 1);
+}
+__global__ void __launch_bounds__(1024) sw_order_scan(int32_t *b) {
+    __shared__ int part[1024];
+    const int tid = threadIdx.x, per = SW_NBUCKET / 1024;
+    int s = 0;
+    for (int k = 0; k < per; ++k) s += b[tid * per + k];
+    part[tid] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int base = part[tid] - s;
+    for (int k = 0; k < per; ++k) {
+        const int c = b[tid * per + k];
+        b[tid * per + k] = base;
+        base += c;
+    }
+}
+__global__ void sw_order_scatter(SwDev D) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x)
+        D.perm[atomicAdd(&D.bucket[sw_task_key(D, t)], 1)] = (int32_t)t;
+}
+
+int sw_launch_order(const SwDev &D, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(D.bucket, 0, (SW_NBUCKET + 1) * sizeof(int32_t), s);
+    if (e != hipSuccess) return (int)e;
+    int grid = (int)((D.n_task + 255) / 256);
+    grid = grid < 4096 ? (grid > 0 ? grid : 1) : 4096;
+    hipLaunchKernelGGL(sw_order_count, dim3(grid), dim3(256), 0, s, D);
+    hipLaunchKernelGGL(sw_order_scan, dim3(1), dim3(1024), 0, s, D.bucket);
+    hipLaunchKernelGGL(sw_order_scatter, dim3(grid), dim3(256), 0, s, D);
+    return (int)hipGetLastError();
 }
 
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream) {

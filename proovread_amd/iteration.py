@@ -107,6 +107,13 @@ class Iteration:
         self.L.pr_iter_last_timing(self.ctx.h, *[C.byref(x) for x in v])
         return [x.value for x in v]
 
+    def cns_phase_ms(self):
+        """Consensus workgroup time per phase (ms summed over workgroups) of the last launch."""
+        t = (C.c_uint64 * 8)()
+        _abi.check(self.L.pr_cns_phase_ticks(self.ctx.h, t, 8), "pr_cns_phase_ticks")
+        names = ["prep", "binning", "state_table", "scatter", "argmax_write", "cigar", "chimera", "idle"]
+        return {k: t[i] / 1e5 for i, k in enumerate(names)}
+
     def results(self) -> List[cns.ReadResult]:
         a = self.download()
         out = []

@@ -16,7 +16,7 @@ b = d.sw_input().c_batch()
 opts = sw.default_opts()
 _abi.check(L.pr_sw_upload(ctx.h, C.byref(b)), "upload")
 res = sw.SwResult(len(d.t_sr))
-for it in range(3):
+for it in range(2):
     t = time.time()
     _abi.check(L.pr_sw_launch(ctx.h, C.byref(opts)), "launch")
     _abi.check(L.pr_sw_download(ctx.h, C.byref(res.c)), "download")
