@@ -1,5 +1,6 @@
 // Device-side structures shared by the consensus kernels and the host API.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace prgpu {
@@ -68,6 +69,11 @@ struct CnsDev {
     int64_t *bin_off;    // [n_lr+1] prefix of bins
     int64_t *bin_bases;  // per bin
     int32_t *work;       // [1] dequeue counter
+    // expanded pileup (per resident workgroup): one state code per (alignment, column)
+    uint32_t *e_pool;    // [grid * e_cap]  code 0-5 fixed state (A T G C - N), 8+slot insertion state
+    int64_t e_cap;
+    int4 *k_pool;        // [grid * k_cap]  kept alignments by start window: {rpos, end, E offset, -}
+    int32_t k_cap;
     unsigned long long *prof;  // [CNS_NPHASE] summed wall-clock ticks per phase (may be null)
     // outputs
     const int64_t *out_off;  // [n_lr+1]
@@ -90,6 +96,8 @@ constexpr int WCOLS = 512;       // columns per pileup window
 constexpr int WCAP = 1024;       // (column, insertion state) pairs per window
 constexpr int CHIM_MAXCOLS = 128;
 constexpr int CHIM_TCAP = 256;
+constexpr int WLCAP = 512;       // window candidates staged in LDS per pass
+constexpr int WBCAP = 1024;      // start-window buckets (long reads up to WBCAP-1 windows)
 constexpr int CNS_NPHASE = 8;    // prep, binning, state table, scatter, argmax+write, cigar, chimera, idle
 
 }  // namespace prgpu

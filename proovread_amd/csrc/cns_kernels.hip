@@ -59,6 +59,8 @@ __device__ __forceinline__ int code5(uint8_t c) {
         default: return 0;
     }
 }
+// nt4 code (0-4) -> 'A','C','G','T','N' without a memory table
+__device__ __forceinline__ uint8_t nt4_ascii(uint32_t c) { return (uint8_t)(0x4E54474341ULL >> (8 * c)); }
 // injective key for insertion-state strings of <=19 chars over ACGTN, else a
 // 63-bit FNV-1a hash with the top bit set (collision note)
 // Read-only view of an alignment's SEQ as SAM prints it: the stored bytes are
@@ -74,7 +76,7 @@ struct SeqV {
         if (nt4) {
             if (c > 4) c = 4;
             if (rc && c < 4) c = (uint8_t)(3 - c);
-            return (uint8_t)"ACGTN"[c];
+            return nt4_ascii(c);
         }
         if (rc) {
             switch (c) {
@@ -118,7 +120,7 @@ __device__ __forceinline__ SeqV seq_view(const CnsDev &D, int64_t g) {
 }
 __device__ __forceinline__ uint8_t ref_base(const CnsDev &D, int64_t i) {
     const uint8_t c = D.ref_seq[i];
-    return D.ref_nt4 ? (uint8_t)"ACGTN"[c > 4 ? 4 : c] : c;
+    return D.ref_nt4 ? nt4_ascii(c > 4 ? 4 : c) : c;
 }
 __device__ __forceinline__ uint32_t key_slot_hash(uint64_t k) {
     k ^= k >> 33; k *= 0xff51afd7ed558ccdULL; k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL; k ^= k >> 33;
@@ -340,7 +342,11 @@ constexpr int OFF_SCAN = 256;                     // 256 x 8 B scan scratch
 constexpr int OFF_A = OFF_SCAN + 2048;            // region A: bin arrays, then state table
 constexpr int SZ_A = TCAP * 24;
 constexpr int OFF_B = OFF_A + SZ_A;               // region B: window / chimera buffers
-constexpr int B_CNT6 = 0;                                   // u32 [WCOLS*6]
+constexpr int B_CNT6 = 0;                                   // u32 [WCOLS*6] (scatter fallback)
+constexpr int B_WL = B_CNT6;                                // int4 [WLCAP]   (expanded path, aliases CNT6)
+constexpr int B_WBEG = B_WL + WLCAP * 16;                   // i32 [WBCAP]    (expanded path)
+static_assert(WLCAP * 16 + WBCAP * 4 <= WCOLS * 6 * 4, "window staging fits the CNT6 area");
+static_assert(WCOLS == 2 * CNS_THREADS, "two pileup columns per thread");
 constexpr int B_WKEY = B_CNT6 + WCOLS * 6 * 4;              // u32 [WCAP]
 constexpr int B_WCNT = B_WKEY + WCAP * 4;                   // u32 [WCAP]
 constexpr int B_COLCNT = B_WCNT + WCAP * 4;                 // i32 [WCOLS]
@@ -366,7 +372,8 @@ struct Ctrl {
     int cand_b0, cand_b1;
     int nchim;
     int flag;
-    int pad[6];
+    unsigned long long ne;          // expanded entries: total, then running offset
+    int nk, maxspan, fast, pad;
 };
 
 __device__ __forceinline__ bool in_ign(const int32_t *ig, int nig, int col) {
@@ -651,7 +658,8 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             continue;
         }
 
-        // ---- 3. insertion-state table: first-seen order (Seq.pm:446-448)
+        // ---- 3. insertion-state table: first-seen order (Seq.pm:446-448), and (expanded
+        //         path) every kept alignment's states written once as one code per column
         STab T;
         T.key = reinterpret_cast<unsigned long long *>(A);
         T.exem = T.key + TCAP;
@@ -660,24 +668,89 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         for (int h = tid; h < TCAP; h += CNS_THREADS) {
             T.key[h] = 0ULL; T.exem[h] = 0ULL; T.ord_cns[h] = 0xFFFFFFFFu; T.ord_all[h] = 0xFFFFFFFFu;
         }
+        int4 *WL = reinterpret_cast<int4 *>(B + B_WL);
+        int32_t *wbeg = reinterpret_cast<int32_t *>(B + B_WBEG);
+        int32_t *wcur = reinterpret_cast<int32_t *>(B + B_COLCNT);   // colcnt+colst: WBCAP ints
+        const int nwin = (int)((L + WCOLS - 1) / WCOLS);
+        uint32_t *E = D.e_pool ? D.e_pool + (int64_t)blockIdx.x * D.e_cap : nullptr;
+        int4 *K = D.k_pool ? D.k_pool + (int64_t)blockIdx.x * D.k_cap : nullptr;
+        if (tid == 0) { C->ne = 0ULL; C->nk = 0; C->maxspan = 0; }
+        for (int x = tid; x < WBCAP; x += CNS_THREADS) wcur[x] = 0;
         __syncthreads();
         for (int i = tid; i < na; i += CNS_THREADS) {
             const int64_t g = a0 + i;
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
-            const SeqV sv = seq_view(D, g);
-            const int sb = D.a_sb[g];
-            const uint32_t *cg = D.cig + D.cig_off[g];
-            walk_states<true>(cg, D.a_cb[g], D.a_ce[g], D.a_rpos[g], 0, 0x7fffffff,
-                              [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                  const uint64_t k = state_key(sv, sb + qoff, qlen);
-                                  if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
-                                  const int h = stab_insert(T, k, ((uint64_t)qlen << 48) |
-                                                                      ((uint64_t)(sb + qoff) << 32) | (uint64_t)g);
-                                  if (h < 0) { C->flag = 1; return; }
-                                  const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
-                                  atomicMin(&T.ord_all[h], ord);
-                                  if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
-                              });
+            const int rp = D.a_rpos[g], span = D.a_end[g] - rp;
+            atomicAdd(&C->ne, (unsigned long long)span);
+            atomicAdd(&C->nk, 1);
+            atomicMax(&C->maxspan, span);
+            const int win = rp / WCOLS;
+            if (win < WBCAP) atomicAdd(&wcur[win], 1);
+        }
+        __syncthreads();
+        const bool fast = E && K && nwin + 1 <= WBCAP && C->nk <= D.k_cap && C->ne <= (unsigned long long)D.e_cap;
+        if (fast) {
+            // start-window buckets: wbeg = exclusive scan of counts (4 windows per thread)
+            long long sc = 0;
+            for (int k = 0; k < 4; ++k) { const int w = tid * 4 + k; if (w < nwin) sc += wcur[w]; }
+            long long tot;
+            long long base = block_scan_excl(sc, scan, &tot);
+            for (int k = 0; k < 4; ++k) {
+                const int w = tid * 4 + k;
+                if (w < nwin) { wbeg[w] = (int32_t)base; base += wcur[w]; wcur[w] = 0; }
+            }
+            if (tid == 0) { wbeg[nwin] = (int32_t)tot; C->ne = 0ULL; }
+            __syncthreads();
+            for (int i = tid; i < na; i += CNS_THREADS) {
+                const int64_t g = a0 + i;
+                if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
+                const int rp = D.a_rpos[g], en = D.a_end[g];
+                const int win = rp / WCOLS;
+                const int kpos = wbeg[win] + atomicAdd(&wcur[win], 1);
+                const int eoff = (int)atomicAdd(&C->ne, (unsigned long long)(en - rp));
+                K[kpos] = make_int4(rp, en, eoff, 0);
+                uint32_t *Ea = E + eoff;
+                const SeqV sv = seq_view(D, g);
+                const int sb = D.a_sb[g];
+                const uint32_t *cg = D.cig + D.cig_off[g];
+                walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, 0, 0x7fffffff,
+                                   [&](int col, int sidx, int kind, int qoff, int qlen) {
+                                       uint32_t code;
+                                       if (kind == 1) code = 4u;
+                                       else if (qlen == 1) code = (uint32_t)fixed_idx(sv[sb + qoff]);
+                                       else {
+                                           const uint64_t k = state_key(sv, sb + qoff, qlen);
+                                           if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
+                                           const int h = stab_insert(T, k, ((uint64_t)qlen << 48) |
+                                                                               ((uint64_t)(sb + qoff) << 32) | (uint64_t)g);
+                                           if (h < 0) { C->flag = 1; return; }
+                                           const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
+                                           atomicMin(&T.ord_all[h], ord);
+                                           if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
+                                           code = 8u + (uint32_t)h;
+                                       }
+                                       Ea[sidx] = code;
+                                   });
+            }
+        } else {
+            for (int i = tid; i < na; i += CNS_THREADS) {
+                const int64_t g = a0 + i;
+                if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
+                const SeqV sv = seq_view(D, g);
+                const int sb = D.a_sb[g];
+                const uint32_t *cg = D.cig + D.cig_off[g];
+                walk_states<true>(cg, D.a_cb[g], D.a_ce[g], D.a_rpos[g], 0, 0x7fffffff,
+                                  [&](int col, int sidx, int kind, int qoff, int qlen) {
+                                      const uint64_t k = state_key(sv, sb + qoff, qlen);
+                                      if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
+                                      const int h = stab_insert(T, k, ((uint64_t)qlen << 48) |
+                                                                          ((uint64_t)(sb + qoff) << 32) | (uint64_t)g);
+                                      if (h < 0) { C->flag = 1; return; }
+                                      const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
+                                      atomicMin(&T.ord_all[h], ord);
+                                      if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
+                                  });
+            }
         }
         __syncthreads();
         if (C->flag) {
@@ -688,6 +761,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             __syncthreads();
             continue;
         }
+        const int wback = (C->maxspan + WCOLS - 1) / WCOLS;   // windows an alignment can reach back
 
         CNS_TICK(2);
         // ---- 4. windowed pileup + argmax (Seq.pm:438-461, 1568-1654)
@@ -703,29 +777,71 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         const bool use_rq = P.use_ref_qual && D.ref_seq && D.ref_qual;
         for (long w0 = 0; w0 < L; w0 += WCOLS) {
             const int wn = (L - w0) < WCOLS ? (int)(L - w0) : WCOLS;
-            for (int x = tid; x < WCOLS * 6; x += CNS_THREADS) cnt6[x] = 0u;
+            uint32_t cnt0[6], cnt1[6];
+#pragma unroll
+            for (int s = 0; s < 6; ++s) { cnt0[s] = 0u; cnt1[s] = 0u; }
+            if (!fast)
+                for (int x = tid; x < WCOLS * 6; x += CNS_THREADS) cnt6[x] = 0u;
             for (int x = tid; x < WCAP; x += CNS_THREADS) { wkey[x] = 0u; wcnt[x] = 0u; }
-            for (int x = tid; x < WCOLS; x += CNS_THREADS) colcnt[x] = 0;
             __syncthreads();
-            for (int i = tid; i < na; i += CNS_THREADS) {
-                const int64_t g = a0 + i;
-                if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
-                const int rp = D.a_rpos[g];
-                if (rp >= w0 + wn || D.a_end[g] <= w0) continue;
-                const SeqV sv = seq_view(D, g);
-                const int sb = D.a_sb[g];
-                const uint32_t *cg = D.cig + D.cig_off[g];
-                walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, (int)w0, (int)(w0 + wn),
-                                   [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                       if (nig && in_ign(ig, nig, col)) return;
-                                       const int c = col - (int)w0;
-                                       if (kind == 1) { atomicAdd(&cnt6[c * 6 + 4], 1u); return; }
-                                       if (qlen == 1) { atomicAdd(&cnt6[c * 6 + fixed_idx(sv[sb + qoff])], 1u); return; }
-                                       const int h = stab_find(T, state_key(sv, sb + qoff, qlen));
-                                       if (h < 0 || wtab_add(wkey, wcnt, ((uint32_t)(c + 1) << 11) | (uint32_t)h) < 0)
-                                           C->flag = 1;
-                                   });
+            if (fast) {
+                // column-parallel: each thread owns columns tid and tid+256 and reads the
+                // codes of every candidate alignment (consecutive columns -> coalesced)
+                const int wi = (int)(w0 / WCOLS);
+                const int kb = wbeg[wi - wback > 0 ? wi - wback : 0], ke = wbeg[wi + 1];
+                for (int c0 = kb; c0 < ke; c0 += WLCAP) {
+                    const int n = (ke - c0) < WLCAP ? (ke - c0) : WLCAP;
+                    for (int x = tid; x < n; x += CNS_THREADS) WL[x] = K[c0 + x];
+                    __syncthreads();
+                    auto accumulate = [&](const int c, uint32_t (&f6)[6]) {
+                        const int col = (int)w0 + c;
+                        if (c < wn && !(nig && in_ign(ig, nig, col))) {
+                            unsigned long long acc = 0ULL;   // six 10-bit counters (n <= 512)
+                            for (int j = 0; j < n; ++j) {
+                                const int4 e = WL[j];
+                                if (col >= e.x && col < e.y) {
+                                    const uint32_t code = E[e.z + col - e.x];
+                                    if (code < 8u) acc += 1ULL << (10u * code);
+                                    else if (wtab_add(wkey, wcnt, ((uint32_t)(c + 1) << 11) | (code - 8u)) < 0)
+                                        C->flag = 1;
+                                }
+                            }
+#pragma unroll
+                            for (int s = 0; s < 6; ++s) f6[s] += (uint32_t)(acc >> (10 * s)) & 1023u;
+                        }
+                    };
+                    accumulate(tid, cnt0);
+                    accumulate(tid + CNS_THREADS, cnt1);
+                    __syncthreads();
+                }
+            } else {
+                for (int i = tid; i < na; i += CNS_THREADS) {
+                    const int64_t g = a0 + i;
+                    if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
+                    const int rp = D.a_rpos[g];
+                    if (rp >= w0 + wn || D.a_end[g] <= w0) continue;
+                    const SeqV sv = seq_view(D, g);
+                    const int sb = D.a_sb[g];
+                    const uint32_t *cg = D.cig + D.cig_off[g];
+                    walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, (int)w0, (int)(w0 + wn),
+                                       [&](int col, int sidx, int kind, int qoff, int qlen) {
+                                           if (nig && in_ign(ig, nig, col)) return;
+                                           const int c = col - (int)w0;
+                                           if (kind == 1) { atomicAdd(&cnt6[c * 6 + 4], 1u); return; }
+                                           if (qlen == 1) { atomicAdd(&cnt6[c * 6 + fixed_idx(sv[sb + qoff])], 1u); return; }
+                                           const int h = stab_find(T, state_key(sv, sb + qoff, qlen));
+                                           if (h < 0 || wtab_add(wkey, wcnt, ((uint32_t)(c + 1) << 11) | (uint32_t)h) < 0)
+                                               C->flag = 1;
+                                       });
+                }
+                __syncthreads();
+#pragma unroll
+                for (int s = 0; s < 6; ++s) {
+                    cnt0[s] = cnt6[tid * 6 + s];
+                    cnt1[s] = cnt6[(tid + CNS_THREADS) * 6 + s];
+                }
             }
+            for (int x = tid; x < WCOLS; x += CNS_THREADS) colcnt[x] = 0;
             __syncthreads();
             CNS_TICK(3);
             // per-column lists of insertion entries (counting sort)
@@ -747,14 +863,13 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     elist[colst[c] + atomicAdd(&colcnt[c], 1)] = (uint16_t)e;
                 }
             __syncthreads();
-            // argmax per column
-            for (int c = tid; c < WCOLS; c += CNS_THREADS) {
+            // argmax per column (the thread's two columns; counts stay in registers)
+            auto argmax_col = [&](const int c, const uint32_t (&f6)[6]) {
                 uint16_t olen = 0;
                 uint32_t desc = 0;
                 uint8_t ph = 0;
                 if (c < wn) {
                     const long col = w0 + c;
-                    const uint32_t *f6 = cnt6 + c * 6;
                     double val[6];
                     bool def[6];
                     bool any = false;
@@ -765,8 +880,10 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                         if (fr != 0.0) {
                             rs = fixed_idx(ref_base(D, r0 + col));
                             vref = fr;   // ref freq is added first, then +1 per alignment
-                            const uint32_t n = f6[rs];
-                            for (uint32_t k = 0; k < n; ++k) vref = __dadd_rn(vref, 1.0);
+                            uint32_t n = 0;
+#pragma unroll
+                            for (int s = 0; s < 6; ++s) n = s == rs ? f6[s] : n;
+                            for (uint32_t kk = 0; kk < n; ++kk) vref = __dadd_rn(vref, 1.0);
                         }
                     }
 #pragma unroll
@@ -785,8 +902,8 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
 #pragma unroll
                     for (int s = 0; s < 6; ++s)
                         if (def[s] && val[s] > maxf) { maxf = val[s]; idx = s; }
-                    for (int k = 0; k < ne; ++k) {
-                        const int e = elist[colst[c] + k];
+                    for (int x = 0; x < ne; ++x) {
+                        const int e = elist[colst[c] + x];
                         const int slot = (int)(wkey[e] & 2047u);
                         const int slen = ex_len(T.exem[slot]);
                         if (P.max_ins_length && slen > P.max_ins_length) continue;
@@ -801,7 +918,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     } else if (idx == 4) {
                         olen = 0; desc = 0; ph = 0;
                     } else if (idx < 6) {
-                        olen = 1; desc = DESC_FIXED | (uint8_t)("ATGC-N"[idx]); ph = (uint8_t)freq2phred(maxf);
+                        olen = 1; desc = DESC_FIXED | (uint8_t)(0x4E2D43475441ULL >> (8 * idx)); ph = (uint8_t)freq2phred(maxf);
                     } else {
                         olen = (uint16_t)ex_len(T.exem[best_slot]); desc = DESC_INS | (uint32_t)best_slot;
                         ph = (uint8_t)freq2phred(maxf);
@@ -810,7 +927,9 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 cout_[c] = olen;
                 cdesc[c] = desc;
                 cphr[c] = ph;
-            }
+            };
+            argmax_col(tid, cnt0);
+            argmax_col(tid + CNS_THREADS, cnt1);
             __syncthreads();
             // block scan of (seq len, trace len) over the window's columns, then write
             {

@@ -59,3 +59,18 @@ def test_gpu_matches_reference_batched():
             _check(c, r)
             n += 1
     assert n > 20
+
+
+def test_gpu_scatter_fallback_path_matches_reference(monkeypatch):
+    """The in-kernel scatter path (taken when a read's expanded pileup exceeds the
+    per-workgroup scratch) forced for every read: same bytes as the reference."""
+    from proovread_amd import cns
+    monkeypatch.setenv("PRGPU_CNS_SCATTER", "1")
+    n = 0
+    for c in CASES:
+        lr, alns, params = case_inputs(c)
+        if params.qual_weighted:
+            continue
+        _check(c, cns.run_chunk([lr], [alns], params)[0])
+        n += 1
+    assert n > 50
