@@ -70,9 +70,10 @@ struct CnsDev {
     int64_t *bin_bases;  // per bin
     int32_t *work;       // [1] dequeue counter
     // expanded pileup (per resident workgroup): one state code per (alignment, column)
-    uint32_t *e_pool;    // [grid * e_cap]  code 0-5 fixed state (A T G C - N), 8+slot insertion state
+    uint32_t *e_pool;    // [grid * e_cap]  SEQ position of a single-base state, E_DEL, E_INS|slot
     int64_t e_cap;
-    int4 *k_pool;        // [grid * k_cap]  kept alignments by start window: {rpos, end, E offset, -}
+    int4 *k_pool;        // [grid * k_cap * 2] kept alignments by start window:
+                         //   {rpos, end, E offset, lseq | rc<<31}, {seq_off lo, seq_off hi, -, -}
     int32_t k_cap;
     unsigned long long *prof;  // [CNS_NPHASE] summed wall-clock ticks per phase (may be null)
     // outputs
@@ -96,7 +97,7 @@ constexpr int WCOLS = 512;       // columns per pileup window
 constexpr int WCAP = 1024;       // (column, insertion state) pairs per window
 constexpr int CHIM_MAXCOLS = 128;
 constexpr int CHIM_TCAP = 256;
-constexpr int WLCAP = 512;       // window candidates staged in LDS per pass
+constexpr int WLCAP = 256;       // window candidates staged in LDS per pass
 constexpr int WBCAP = 1024;      // start-window buckets (long reads up to WBCAP-1 windows)
 constexpr int CNS_NPHASE = 8;    // prep, binning, state table, scatter, argmax+write, cigar, chimera, idle
 

@@ -343,9 +343,9 @@ constexpr int OFF_A = OFF_SCAN + 2048;            // region A: bin arrays, then 
 constexpr int SZ_A = TCAP * 24;
 constexpr int OFF_B = OFF_A + SZ_A;               // region B: window / chimera buffers
 constexpr int B_CNT6 = 0;                                   // u32 [WCOLS*6] (scatter fallback)
-constexpr int B_WL = B_CNT6;                                // int4 [WLCAP]   (expanded path, aliases CNT6)
-constexpr int B_WBEG = B_WL + WLCAP * 16;                   // i32 [WBCAP]    (expanded path)
-static_assert(WLCAP * 16 + WBCAP * 4 <= WCOLS * 6 * 4, "window staging fits the CNT6 area");
+constexpr int B_WL = B_CNT6;                                // int4 [2*WLCAP] (expanded path, aliases CNT6)
+constexpr int B_WBEG = B_WL + WLCAP * 32;                   // i32 [WBCAP]    (expanded path)
+static_assert(WLCAP * 32 + WBCAP * 4 <= WCOLS * 6 * 4, "window staging fits the CNT6 area");
 static_assert(WCOLS == 2 * CNS_THREADS, "two pileup columns per thread");
 constexpr int B_WKEY = B_CNT6 + WCOLS * 6 * 4;              // u32 [WCAP]
 constexpr int B_WCNT = B_WKEY + WCAP * 4;                   // u32 [WCAP]
@@ -363,6 +363,9 @@ constexpr int MAX_BINS_LDS = (SZ_A - CNS_THREADS * 4) / 8;
 // per-column descriptor: flag bits above the 11-bit state-table slot
 constexpr uint32_t DESC_FIXED = 1u << 16;
 constexpr uint32_t DESC_INS = 1u << 17;
+// expanded pileup codes (per alignment and column)
+constexpr uint32_t E_INS = 0x80000000u;   // | state-table slot
+constexpr uint32_t E_DEL = 0xFFFFFFFFu;
 
 struct Ctrl {
     int lr;
@@ -673,7 +676,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         int32_t *wcur = reinterpret_cast<int32_t *>(B + B_COLCNT);   // colcnt+colst: WBCAP ints
         const int nwin = (int)((L + WCOLS - 1) / WCOLS);
         uint32_t *E = D.e_pool ? D.e_pool + (int64_t)blockIdx.x * D.e_cap : nullptr;
-        int4 *K = D.k_pool ? D.k_pool + (int64_t)blockIdx.x * D.k_cap : nullptr;
+        int4 *K = D.k_pool ? D.k_pool + (int64_t)blockIdx.x * D.k_cap * 2 : nullptr;
         if (tid == 0) { C->ne = 0ULL; C->nk = 0; C->maxspan = 0; }
         for (int x = tid; x < WBCAP; x += CNS_THREADS) wcur[x] = 0;
         __syncthreads();
@@ -708,16 +711,20 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 const int win = rp / WCOLS;
                 const int kpos = wbeg[win] + atomicAdd(&wcur[win], 1);
                 const int eoff = (int)atomicAdd(&C->ne, (unsigned long long)(en - rp));
-                K[kpos] = make_int4(rp, en, eoff, 0);
-                uint32_t *Ea = E + eoff;
                 const SeqV sv = seq_view(D, g);
+                const int64_t so = D.seq_off[g];
+                K[2 * kpos] = make_int4(rp, en, eoff, sv.n | (sv.rc ? (int)0x80000000 : 0));
+                K[2 * kpos + 1] = make_int4((int)(so & 0xFFFFFFFF), (int)(so >> 32), 0, 0);
+                uint32_t *Ea = E + eoff;
                 const int sb = D.a_sb[g];
                 const uint32_t *cg = D.cig + D.cig_off[g];
+                // codes: SEQ position of a single-base state (the base is read later, in the
+                // coalesced pileup), E_DEL for '-', E_INS|slot for an insertion state
                 walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, 0, 0x7fffffff,
                                    [&](int col, int sidx, int kind, int qoff, int qlen) {
                                        uint32_t code;
-                                       if (kind == 1) code = 4u;
-                                       else if (qlen == 1) code = (uint32_t)fixed_idx(sv[sb + qoff]);
+                                       if (kind == 1) code = E_DEL;
+                                       else if (qlen == 1) code = (uint32_t)(sb + qoff);
                                        else {
                                            const uint64_t k = state_key(sv, sb + qoff, qlen);
                                            if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
@@ -727,7 +734,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                                            const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
                                            atomicMin(&T.ord_all[h], ord);
                                            if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
-                                           code = 8u + (uint32_t)h;
+                                           code = E_INS | (uint32_t)h;
                                        }
                                        Ea[sidx] = code;
                                    });
@@ -791,19 +798,30 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 const int kb = wbeg[wi - wback > 0 ? wi - wback : 0], ke = wbeg[wi + 1];
                 for (int c0 = kb; c0 < ke; c0 += WLCAP) {
                     const int n = (ke - c0) < WLCAP ? (ke - c0) : WLCAP;
-                    for (int x = tid; x < n; x += CNS_THREADS) WL[x] = K[c0 + x];
+                    for (int x = tid; x < 2 * n; x += CNS_THREADS) WL[x] = K[2 * c0 + x];
                     __syncthreads();
                     auto accumulate = [&](const int c, uint32_t (&f6)[6]) {
                         const int col = (int)w0 + c;
                         if (c < wn && !(nig && in_ign(ig, nig, col))) {
-                            unsigned long long acc = 0ULL;   // six 10-bit counters (n <= 512)
+                            unsigned long long acc = 0ULL;   // six 10-bit counters (n <= WLCAP)
+#pragma unroll 4
                             for (int j = 0; j < n; ++j) {
-                                const int4 e = WL[j];
+                                const int4 e = WL[2 * j];
                                 if (col >= e.x && col < e.y) {
-                                    const uint32_t code = E[e.z + col - e.x];
-                                    if (code < 8u) acc += 1ULL << (10u * code);
-                                    else if (wtab_add(wkey, wcnt, ((uint32_t)(c + 1) << 11) | (code - 8u)) < 0)
+                                    const uint32_t v = E[e.z + col - e.x];
+                                    if (v < E_INS) {
+                                        const int4 e2 = WL[2 * j + 1];
+                                        SeqV sv;
+                                        sv.p = D.seq + (((int64_t)e2.y << 32) | (uint32_t)e2.x);
+                                        sv.n = e.w & 0x7FFFFFFF;
+                                        sv.rc = e.w < 0;
+                                        sv.nt4 = D.seq_nt4 != 0;
+                                        acc += 1ULL << (10u * (uint32_t)fixed_idx(sv[(int)v]));
+                                    } else if (v == E_DEL) {
+                                        acc += 1ULL << 40;
+                                    } else if (wtab_add(wkey, wcnt, ((uint32_t)(c + 1) << 11) | (v & 2047u)) < 0) {
                                         C->flag = 1;
+                                    }
                                 }
                             }
 #pragma unroll

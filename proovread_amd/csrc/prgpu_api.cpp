@@ -406,7 +406,7 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         int64_t kc = c->k_need < 64 ? 64 : c->k_need;
         if (kc > (1 << 20)) kc = 1 << 20;
         int rc;
-        if ((rc = B[CB_E].ensure((size_t)grid * ec * 4)) || (rc = B[CB_K].ensure((size_t)grid * kc * 16))) return rc;
+        if ((rc = B[CB_E].ensure((size_t)grid * ec * 4)) || (rc = B[CB_K].ensure((size_t)grid * kc * 32))) return rc;
         D.e_pool = B[CB_E].as<uint32_t>();
         D.e_cap = ec;
         D.k_pool = B[CB_K].as<int4>();
