@@ -35,6 +35,9 @@ enum SwBuf {
 static const int SB_CELLS = 24;
 static const int SB_PERM = 25;
 static const int SB_BUCKET = 26;
+static const int SB_X = 27;
+static const int SB_XTRY = 28;
+static const int SB_LIST = 29;
 
 namespace prgpu {
 void sw_release(SwResident &r) {
@@ -116,7 +119,9 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
     const size_t n4 = (size_t)(nt + 1) * 4;
     for (int id : {SB_QB, SB_QE, SB_RB, SB_RE, SB_SCORE, SB_TRUESC, SB_W, SB_GSCORE, SB_POS, SB_NCIG, SB_STATUS})
         if ((rc = ensure(r, id, n4))) return rc;
-    if ((rc = ensure(r, SB_PERM, (size_t)(nt + 1) * 4)) || (rc = ensure(r, SB_BUCKET, (SW_NBUCKET + 1) * 4)))
+    if ((rc = ensure(r, SB_PERM, (size_t)(nt + 1) * 4)) || (rc = ensure(r, SB_BUCKET, (SW_NBUCKET + 1) * 4)) ||
+        (rc = ensure(r, SB_X, (size_t)(nt + 1) * 4 * 12)) || (rc = ensure(r, SB_XTRY, (size_t)nt + 1)) ||
+        (rc = ensure(r, SB_LIST, (size_t)(nt + 1) * 4)))
         return rc;
     if ((rc = ensure(r, SB_PASS, (size_t)nt + 1)) || (rc = ensure(r, SB_CIG, (size_t)(nt + 1) * SW_MAXCIG * 4)) ||
         (rc = ensure(r, SB_CELLS, 64)))
@@ -137,7 +142,9 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if (o->a <= 0 || o->b < 0 || o->e_del <= 0 || o->e_ins <= 0 || o->w <= 0)
         return pr_set_error(PR_ERR_ARG, "bad scoring options");
     if ((long)o->a * r.qmax >= 8192)
-        return pr_set_error(PR_ERR_ARG, "a * max read length must stay below 8192 (13-bit LDS words)");
+        return pr_set_error(PR_ERR_ARG, "a * max read length must stay below 8192 (13-bit DP words)");
+    if (o->w > 40) return pr_set_error(PR_ERR_UNSUPPORTED, "band width w > 40 (register ring holds 2*80+2 columns)");
+    if (o->a > 15 || o->b > 16) return pr_set_error(PR_ERR_UNSUPPORTED, "match score > 15 or mismatch penalty > 16");
     HIPCHK(hipSetDevice(ctx_device(c)));
     hipStream_t s = ctx_stream(c);
     SwOptsDev O;
@@ -177,7 +184,11 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.work = (int32_t *)((char *)r.buf[SB_CELLS] + 32);
     D.perm = (int32_t *)r.buf[SB_PERM];
     D.bucket = (int32_t *)r.buf[SB_BUCKET];
-    // LDS: extension = (qmax+1) words per lane; global = same + lane-major query bytes
+    D.x = (int32_t *)r.buf[SB_X];
+    D.x_try = (uint8_t *)r.buf[SB_XTRY];
+    D.list = (int32_t *)r.buf[SB_LIST];
+    D.list_n = D.bucket + SW_NBUCKET;
+    // LDS of the CIGAR kernel: (qmax+1) H/E words per lane + lane-major query bytes
     const int lds_ext = (r.qmax + 1) * SW_WAVE * 4;
     const int qpad = (r.qmax + 8) & ~3;
     const int lds_glob = lds_ext + SW_WAVE * qpad;
@@ -185,19 +196,21 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     const int blocks_per_cu = (160 * 1024) / (lds_glob + 64) > 0 ? (160 * 1024) / (lds_glob + 64) : 1;
     const int grid_g = ctx_ncu(c) * (blocks_per_cu < 8 ? blocks_per_cu : 8);
     D.z_slab = (int64_t)D.tmax * ((r.qmax + 3) / 4) * 4 * SW_WAVE;
+    const int grid_w = ctx_ncu(c) * 12;                       // ring kernels: 3 waves per SIMD
+    D.z_ring_slab = (int64_t)D.tmax * ((2 * 80 + 2 + 7) / 8) * SW_WAVE;
+    const size_t zb = (size_t)D.z_slab * grid_g > (size_t)D.z_ring_slab * 4 * grid_w
+                          ? (size_t)D.z_slab * grid_g : (size_t)D.z_ring_slab * 4 * grid_w;
     int rc;
-    if ((rc = ensure(r, SB_Z, (size_t)D.z_slab * grid_g))) return rc;
+    if ((rc = ensure(r, SB_Z, zb))) return rc;
     D.z = (uint8_t *)r.buf[SB_Z];
     HIPCHK(hipMemsetAsync(r.buf[SB_CELLS], 0, 64, s));
     if (r.n_task == 0) return 0;
-    const int grid_e = (int)((r.n_task + SW_WAVE - 1) / SW_WAVE);
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
-    int e = sw_launch_order(D, (void *)s);
+    int e = sw_launch_extend(D, O, ctx_ncu(c) * 16, (void *)s);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
-    e = sw_launch_extend(D, O, grid_e, lds_ext, (void *)s);
-    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
-    e = sw_launch_global(D, O, grid_g, lds_glob, (void *)s);
+    e = sw_launch_global(D, O, grid_w, grid_g, lds_glob, (void *)s);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     HIPCHK(hipEventRecord(ctx_event(c, 0), s));
     return 0;

@@ -1,5 +1,6 @@
 // Device-side structures of the SW (seed extension + CIGAR) stage.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 namespace prgpu {
@@ -31,11 +32,16 @@ struct SwDev {
     int32_t *o_gscore, *o_pos, *o_ncig, *o_status;
     uint32_t *o_cig;           // n_task * SW_MAXCIG
     uint8_t *z;                // direction-matrix slabs, one per resident block
-    int64_t z_slab;            // bytes per slab
+    int64_t z_slab;            // bytes per slab (LDS kernel)
+    int64_t z_ring_slab;       // dwords per slab (register-ring kernels: rows x words x 64 lanes)
     unsigned long long *cells; // [2] canonical DP cells (extension, global)
     int32_t *perm;             // lane -> task order (tasks bucketed by extension lengths)
     int32_t *bucket;           // [SW_NBUCKET + 1] counting-sort scratch
     int32_t *work;             // dequeue counter for the global kernel
+    int32_t *x;                // extension scratch: 2 sides x XF fields x n_task
+    uint8_t *x_try;            // bit side: that side needs the second band try
+    int32_t *list;             // task list of the current extension phase
+    const int32_t *list_n;     // its length (device)
 };
 
 struct SwResident {
@@ -58,9 +64,9 @@ struct SwPtrs {
     int n_sr, n_lr;
 };
 
-int sw_launch_order(const SwDev &D, void *stream);
-int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
-int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
+int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out, void *stream);
+int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *stream);
+int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_lds, int lds, void *stream);
 void sw_release(SwResident &r);
 
 }  // namespace prgpu

@@ -3,9 +3,10 @@
 // window, seed) task per lane, rows of the banded DP walked in lock-step by the
 // 64 lanes of a wave.
 //
-//   sw_extend_kernel : mem_chain2aln for a single-seed chain — left and right
-//                      ksw_extend2 (band pruning, z-drop, to-end gscore) with
-//                      MAX_BAND_TRY=2 band doubling and the -L clip decision.
+//   sw_ext_phase_kernel<WB> : mem_chain2aln for a single-seed chain — left and
+//                      right ksw_extend2 (band pruning, z-drop, to-end gscore),
+//                      the DP row in registers; MAX_BAND_TRY=2 band doubling as
+//                      separate compacted phases; sw_*_finish: the -L clip decision.
 //   sw_global_kernel : mem_reg2aln / bwa_gen_cigar2 — infer_bw, up to three
 //                      ksw_global2 passes, backtrack, D-squeeze, soft clips.
 //
@@ -19,6 +20,7 @@
 #include <stdint.h>
 
 #include "sw_dev.h"
+#include "sw_ring.h"
 
 namespace prgpu {
 
@@ -48,115 +50,15 @@ __device__ __forceinline__ uint64_t score_row(int tc, int a, int b) {
     return ((uint64_t)0xFFu << 32) | lo;
 }
 
-struct ExtIO {
-    int qle, tle, gtle, gscore, max_off;
-};
-
-// ksw_extend2 for one lane.  eh: this lane's column 0 in LDS (stride 64 words).
-// Query column j is Q[qb + qs*j]; target row i is comp?(L[tb + ts*i]).
-__device__ int ksw_extend_lane(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen,
-                               const uint8_t *Lr, long tb, int ts, bool comp, int tlen,
-                               const SwOptsDev &O, int w, int end_bonus, int h0, ExtIO &io,
-                               unsigned long long &cells) {
-    const int a = O.a, b = O.b, o_del = O.o_del, e_del = O.e_del, o_ins = O.o_ins, e_ins = O.e_ins;
-    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
-    // first row + query bases
-    {
-        int hp = h0;
-        bool alive = true;
-        for (int j = 0; j <= qlen; ++j) {
-            int h;
-            if (j == 0) h = h0;
-            else if (j == 1) h = h0 > oe_ins ? h0 - oe_ins : 0;
-            else {
-                alive = alive && hp > e_ins;
-                h = alive ? hp - e_ins : 0;
-            }
-            hp = h;
-            const uint32_t q = j < qlen ? (uint32_t)Q[qb + qs * j] : 0u;
-            eh[j * SW_WAVE] = pk(h, 0, q << 3);
-        }
-    }
-    int max_ins = (int)((double)(qlen * a + end_bonus - o_ins) / e_ins + 1.);
-    max_ins = max_ins > 1 ? max_ins : 1;
-    w = w < max_ins ? w : max_ins;
-    int max_del = (int)((double)(qlen * a + end_bonus - o_del) / e_del + 1.);
-    max_del = max_del > 1 ? max_del : 1;
-    w = w < max_del ? w : max_del;
-    // canonical unpruned band cell count
-    {
-        unsigned long long c = 0;
-        for (int i = 0; i < tlen; ++i) {
-            const int lo = i - w > 0 ? i - w : 0;
-            const int hi = i + w + 1 < qlen ? i + w + 1 : qlen;
-            if (hi > lo) c += (unsigned long long)(hi - lo);
-        }
-        cells += c;
-    }
-    int max = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
-    int beg = 0, end = qlen;
+// canonical unpruned band cells of one ksw_extend2 call
+__device__ __forceinline__ unsigned long long band_cells(int tlen, int qlen, int w) {
+    unsigned long long c = 0;
     for (int i = 0; i < tlen; ++i) {
-        int f = 0, h1, m = 0, mj = -1;
-        int tc = (int)Lr[tb + (long)ts * i];
-        if (comp && tc < 4) tc = 3 - tc;
-        if (beg < i - w) beg = i - w;
-        if (end > i + w + 1) end = i + w + 1;
-        if (end > qlen) end = qlen;
-        if (beg == 0) {
-            h1 = h0 - (o_del + e_del * (i + 1));
-            if (h1 < 0) h1 = 0;
-        } else
-            h1 = 0;
-        const uint64_t srow = score_row(tc, a, b);
-        int j;
-        uint32_t wd = eh[beg * SW_WAVE];
-        for (j = beg; j < end; ++j) {
-            const uint32_t wn = eh[(j + 1) * SW_WAVE];   // prefetch: column j+1 is not written at j
-            const int Mr = (int)(wd & 0x1FFFu);
-            const int e0 = (int)((wd >> 13) & 0x1FFFu);
-            const uint32_t q8 = wd >> 26;
-            const int sc = (int)(int8_t)(uint8_t)(srow >> q8);
-            const int M = Mr ? Mr + sc : 0;   // separating H and M (ksw: no 100M3I3D20M)
-            const int h = imax3(M, e0, f);
-            mj = m > h ? mj : j;
-            m = m > h ? m : h;
-            const int e = imax3(e0 - e_del, M - oe_del, 0);
-            f = imax3(f - e_ins, M - oe_ins, 0);
-            eh[j * SW_WAVE] = pk(h1, e, q8);
-            h1 = h;
-            wd = wn;
-        }
-        {
-            const uint32_t w2 = eh[end * SW_WAVE];
-            eh[end * SW_WAVE] = pk(h1, 0, w2 >> 26);
-        }
-        if (j == qlen) {
-            max_ie = gscore > h1 ? max_ie : i;
-            gscore = gscore > h1 ? gscore : h1;
-        }
-        if (m == 0) break;
-        if (m > max) {
-            max = m, max_i = i, max_j = mj;
-            const int d = mj - i < 0 ? i - mj : mj - i;
-            max_off = max_off > d ? max_off : d;
-        } else if (O.zdrop > 0) {
-            if (i - max_i > mj - max_j) {
-                if (max - m - ((i - max_i) - (mj - max_j)) * e_del > O.zdrop) break;
-            } else {
-                if (max - m - ((mj - max_j) - (i - max_i)) * e_ins > O.zdrop) break;
-            }
-        }
-        for (j = beg; j < end && (eh[j * SW_WAVE] & PK_HE) == 0u; ++j);
-        beg = j;
-        for (j = end; j >= beg && (eh[j * SW_WAVE] & PK_HE) == 0u; --j);
-        end = j + 2 < qlen ? j + 2 : qlen;
+        const int lo = i - w > 0 ? i - w : 0;
+        const int hi = i + w + 1 < qlen ? i + w + 1 : qlen;
+        if (hi > lo) c += (unsigned long long)(hi - lo);
     }
-    io.qle = max_j + 1;
-    io.tle = max_i + 1;
-    io.gtle = max_ie + 1;
-    io.gscore = gscore;
-    io.max_off = max_off;
-    return max;
+    return c;
 }
 
 __device__ __forceinline__ int cal_max_gap(const SwOptsDev &O, int qlen) {
@@ -167,93 +69,175 @@ __device__ __forceinline__ int cal_max_gap(const SwOptsDev &O, int qlen) {
     return l < O.w << 1 ? l : O.w << 1;
 }
 
-__global__ void __launch_bounds__(SW_WAVE) sw_extend_kernel(SwDev D, SwOptsDev O) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds_eh[];
+// mem_chain2aln geometry of a single-seed task
+struct TaskGeo {
+    const uint8_t *Q, *Lr;
+    int lq, L, qbeg, rbeg, slen;
+    bool rev;
+    long rmax0, rmax1;
+};
+__device__ __forceinline__ TaskGeo task_geo(const SwDev &D, const SwOptsDev &O, int64_t t) {
+    TaskGeo g;
+    const int sid = D.t_sr[t], lid = D.t_lr[t];
+    g.Q = D.sr + D.sr_off[sid];
+    g.lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
+    g.Lr = D.lr + D.lr_off[lid];
+    g.L = (int)(D.lr_off[lid + 1] - D.lr_off[lid]);
+    g.rev = D.t_strand[t] != 0;
+    g.qbeg = D.t_qbeg[t];
+    g.rbeg = D.t_rbeg[t];
+    g.slen = D.t_slen[t];
+    g.rmax0 = (long)g.rbeg - (g.qbeg + cal_max_gap(O, g.qbeg));
+    g.rmax1 = (long)g.rbeg + g.slen + ((g.lq - g.qbeg - g.slen) + cal_max_gap(O, g.lq - g.qbeg - g.slen));
+    if (g.rmax0 < 0) g.rmax0 = 0;
+    if (g.rmax1 > g.L) g.rmax1 = g.L;
+    return g;
+}
+
+// per-task extension scratch: field f of side s at x[(s * XF + f) * n_task + t]
+enum { XF_SCORE, XF_QLE, XF_TLE, XF_GTLE, XF_GSCORE, XF_MAXOFF, XF };
+__device__ __forceinline__ int32_t &xref(const SwDev &D, int side, int f, int64_t t) {
+    return D.x[((int64_t)(side * XF + f)) * D.n_task + t];
+}
+
+// One extension phase: side 0 = left (query reversed from qbeg-1), 1 = right;
+// band try `tryi` (w = O.w << tryi, mem_chain2aln's MAX_BAND_TRY loop).  Lanes
+// take tasks from the phase's list (bucketed by query length).
+template <int WB>
+__global__ void __launch_bounds__(SW_WAVE) sw_ext_phase_kernel(SwDev D, SwOptsDev O, int side, int tryi) {
     const int lane = threadIdx.x;
-    const int64_t slot = (int64_t)blockIdx.x * SW_WAVE + lane;
-    unsigned long long cells = 0;
-    if (slot < D.n_task) {
-        const int64_t t = D.perm[slot];
-        uint32_t *eh = lds_eh + lane;
-        const int sid = D.t_sr[t], lid = D.t_lr[t];
-        const uint8_t *Q = D.sr + D.sr_off[sid];
-        const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
-        const uint8_t *Lr = D.lr + D.lr_off[lid];
-        const int L = (int)(D.lr_off[lid + 1] - D.lr_off[lid]);
-        const bool rev = D.t_strand[t] != 0;
-        const int qbeg = D.t_qbeg[t], rbeg = D.t_rbeg[t], slen = D.t_slen[t];
-        // mem_chain2aln: max possible span
-        long rmax0 = (long)rbeg - (qbeg + cal_max_gap(O, qbeg));
-        long rmax1 = (long)rbeg + slen + ((lq - qbeg - slen) + cal_max_gap(O, lq - qbeg - slen));
-        if (rmax0 < 0) rmax0 = 0;
-        if (rmax1 > L) rmax1 = L;
-        int aw0 = O.w, aw1 = O.w;
-        int score = -1, truesc = -1, qb, qe, rb, re;
-        ExtIO io;
-        if (qbeg) {
-            const int tlen = (int)(rbeg - rmax0);
-            // left: query Q[qbeg-1-j], target strand position rbeg-1-i
-            const long tb = rev ? (long)L - rbeg : (long)rbeg - 1;
-            const int ts = rev ? 1 : -1;
-            unsigned long long c = 0;
-            for (int i = 0; i < 2; ++i) {
-                const int prev = score;
-                aw0 = O.w << i;
-                c = 0;
-                score = ksw_extend_lane(eh, Q, qbeg - 1, -1, qbeg, Lr, tb, ts, rev, tlen, O, aw0,
-                                        O.pen_clip5, slen * O.a, io, c);
-                if (score == prev || io.max_off < (aw0 >> 1) + (aw0 >> 2)) break;
+    const int n = D.list_n[0];
+    for (int64_t c0 = (int64_t)blockIdx.x * SW_WAVE; c0 < n; c0 += (int64_t)gridDim.x * SW_WAVE) {
+        const int64_t slot = c0 + lane;
+        int64_t t = -1;
+        TaskGeo g;
+        const uint8_t *Q = D.sr;
+        const uint8_t *Lr = D.lr;
+        int qb = 0, qs = 1, qlen = 0, tlen = 0, ts = 1, end_bonus = 0, h0 = 0;
+        long tb = 0;
+        bool comp = false;
+        if (slot < n) {
+            t = D.list[slot];
+            g = task_geo(D, O, t);
+            Q = g.Q;
+            Lr = g.Lr;
+            comp = g.rev;
+            if (side == 0) {
+                qb = g.qbeg - 1; qs = -1; qlen = g.qbeg;
+                tlen = (int)(g.rbeg - g.rmax0);
+                tb = g.rev ? (long)g.L - g.rbeg : (long)g.rbeg - 1;
+                ts = g.rev ? 1 : -1;
+                end_bonus = O.pen_clip5;
+                h0 = g.slen * O.a;
+            } else {
+                const int qe0 = g.qbeg + g.slen;
+                const int re0 = (int)(g.rbeg + g.slen - g.rmax0);
+                qb = qe0; qs = 1; qlen = g.lq - qe0;
+                tlen = (int)(g.rmax1 - g.rmax0 - re0);
+                tb = g.rev ? (long)g.L - 1 - g.rbeg - g.slen : (long)g.rbeg + g.slen;
+                ts = g.rev ? -1 : 1;
+                end_bonus = O.pen_clip3;
+                h0 = D.o_score[t];   // left result (sc0)
             }
-            cells += c;
-            if (io.gscore <= 0 || io.gscore <= score - O.pen_clip5) {
-                qb = qbeg - io.qle, rb = rbeg - io.tle;
+        }
+        ExtIO io;
+        const int aw = O.w << tryi;
+        const int score = ext_ring<WB>(Q, qb, qs, qlen, Lr, tb, ts, comp, tlen, O, aw, end_bonus, h0, io);
+        if (t >= 0) {
+            xref(D, side, XF_SCORE, t) = score;
+            xref(D, side, XF_QLE, t) = io.qle;
+            xref(D, side, XF_TLE, t) = io.tle;
+            xref(D, side, XF_GTLE, t) = io.gtle;
+            xref(D, side, XF_GSCORE, t) = io.gscore;
+            xref(D, side, XF_MAXOFF, t) = io.max_off;
+            if (tryi == 0) {
+                const int prev = side == 0 ? -1 : h0;
+                const bool stop = score == prev || io.max_off < (aw >> 1) + (aw >> 2);
+                D.x_try[t] = (uint8_t)(D.x_try[t] | (stop ? 0 : (1 << side)));
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ int band_w(const SwOptsDev &O, int w, int qlen, int end_bonus) {
+    int max_ins = (int)((double)(qlen * O.a + end_bonus - O.o_ins) / O.e_ins + 1.);
+    max_ins = max_ins > 1 ? max_ins : 1;
+    w = w < max_ins ? w : max_ins;
+    int max_del = (int)((double)(qlen * O.a + end_bonus - O.o_del) / O.e_del + 1.);
+    max_del = max_del > 1 ? max_del : 1;
+    return w < max_del ? w : max_del;
+}
+
+// after the left phases: qb, rb, score, truesc (mem_chain2aln); o_w holds aw[0]
+__global__ void sw_left_finish_kernel(SwDev D, SwOptsDev O) {
+    unsigned long long cells = 0;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const TaskGeo g = task_geo(D, O, t);
+        int score, truesc, qb, rb, aw0 = O.w;
+        if (g.qbeg) {
+            const int tr = (D.x_try[t] & 1) ? 1 : 0;
+            aw0 = O.w << tr;
+            score = xref(D, 0, XF_SCORE, t);
+            const int gs = xref(D, 0, XF_GSCORE, t);
+            if (gs <= 0 || gs <= score - O.pen_clip5) {
+                qb = g.qbeg - xref(D, 0, XF_QLE, t), rb = g.rbeg - xref(D, 0, XF_TLE, t);
                 truesc = score;
             } else {
-                qb = 0, rb = rbeg - io.gtle;
-                truesc = io.gscore;
+                qb = 0, rb = g.rbeg - xref(D, 0, XF_GTLE, t);
+                truesc = gs;
             }
+            cells += band_cells((int)(g.rbeg - g.rmax0), g.qbeg, band_w(O, aw0, g.qbeg, O.pen_clip5));
         } else {
-            score = truesc = slen * O.a, qb = 0, rb = rbeg;
-        }
-        if (qbeg + slen != lq) {
-            const int sc0 = score;
-            const int qe0 = qbeg + slen;
-            const int re0 = (int)(rbeg + slen - rmax0);
-            const int tlen = (int)(rmax1 - rmax0 - re0);
-            const long tb = rev ? (long)L - 1 - rbeg - slen : (long)rbeg + slen;
-            const int ts = rev ? -1 : 1;
-            unsigned long long c = 0;
-            for (int i = 0; i < 2; ++i) {
-                const int prev = score;
-                aw1 = O.w << i;
-                c = 0;
-                score = ksw_extend_lane(eh, Q, qe0, 1, lq - qe0, Lr, tb, ts, rev, tlen, O, aw1,
-                                        O.pen_clip3, sc0, io, c);
-                if (score == prev || io.max_off < (aw1 >> 1) + (aw1 >> 2)) break;
-            }
-            cells += c;
-            if (io.gscore <= 0 || io.gscore <= score - O.pen_clip3) {
-                qe = qe0 + io.qle, re = (int)(rmax0 + re0 + io.tle);
-                truesc += score - sc0;
-            } else {
-                qe = lq, re = (int)(rmax0 + re0 + io.gtle);
-                truesc += io.gscore - sc0;
-            }
-        } else {
-            qe = lq, re = rbeg + slen;
+            score = truesc = g.slen * O.a, qb = 0, rb = g.rbeg;
         }
         D.o_qb[t] = qb;
-        D.o_qe[t] = qe;
         D.o_rb[t] = rb;
+        D.o_score[t] = score;
+        D.o_truesc[t] = truesc;
+        D.o_w[t] = aw0;
+    }
+    for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
+    if ((threadIdx.x & 63) == 0 && cells) atomicAdd(&D.cells[0], cells);
+}
+
+// after the right phases: qe, re, score, truesc, w, pass
+__global__ void sw_right_finish_kernel(SwDev D, SwOptsDev O) {
+    unsigned long long cells = 0;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task;
+         t += (int64_t)gridDim.x * blockDim.x) {
+        const TaskGeo g = task_geo(D, O, t);
+        int score = D.o_score[t], truesc = D.o_truesc[t], qe, re, aw1 = O.w;
+        const int qb = D.o_qb[t];
+        if (g.qbeg + g.slen != g.lq) {
+            const int sc0 = score;
+            const int qe0 = g.qbeg + g.slen;
+            const int re0 = (int)(g.rbeg + g.slen - g.rmax0);
+            const int tr = (D.x_try[t] & 2) ? 1 : 0;
+            aw1 = O.w << tr;
+            score = xref(D, 1, XF_SCORE, t);
+            const int gs = xref(D, 1, XF_GSCORE, t);
+            if (gs <= 0 || gs <= score - O.pen_clip3) {
+                qe = qe0 + xref(D, 1, XF_QLE, t), re = (int)(g.rmax0 + re0 + xref(D, 1, XF_TLE, t));
+                truesc += score - sc0;
+            } else {
+                qe = g.lq, re = (int)(g.rmax0 + re0 + xref(D, 1, XF_GTLE, t));
+                truesc += gs - sc0;
+            }
+            cells += band_cells((int)(g.rmax1 - g.rmax0 - re0), g.lq - qe0, band_w(O, aw1, g.lq - qe0, O.pen_clip3));
+        } else {
+            qe = g.lq, re = g.rbeg + g.slen;
+        }
+        const int aw0 = D.o_w[t];
+        D.o_qe[t] = qe;
         D.o_re[t] = re;
         D.o_score[t] = score;
         D.o_truesc[t] = truesc;
         D.o_w[t] = aw0 > aw1 ? aw0 : aw1;
         D.o_pass[t] = (double)score >= O.min_score_per_base * (double)(qe - qb) ? 1 : 0;
     }
-    // one atomic per wave for the cell counter
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
-    if (lane == 0 && cells) atomicAdd(&D.cells[0], cells);
+    if ((threadIdx.x & 63) == 0 && cells) atomicAdd(&D.cells[0], cells);
 }
 
 // ---------------------------------------------------------------------------
@@ -342,6 +326,74 @@ __device__ __forceinline__ int push_op(uint32_t *cg, int n, int op, int len) {
     return n + 1;
 }
 
+// mem_reg2aln after ksw_global2: position, leading/trailing D squeeze, soft clips
+__device__ __forceinline__ void glob_emit(const SwDev &D, int64_t t, uint32_t *cg, int n, int status, int gsc,
+                                          bool rev, int lq, int L, int qb, int qe, int rb, int re) {
+    int pos = rev ? L - re : rb;
+    if (n > 0) {
+        if ((cg[0] & 0xFu) == 2u) {
+            pos += (int)(cg[0] >> 4);
+            for (int x = 0; x + 1 < n; ++x) cg[x] = cg[x + 1];
+            --n;
+        } else if ((cg[n - 1] & 0xFu) == 2u) {
+            --n;
+        }
+    }
+    if (qb != 0 || qe != lq) {
+        const int clip5 = rev ? lq - qe : qb;
+        const int clip3 = rev ? qb : lq - qe;
+        if (n + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > SW_MAXCIG) {
+            status = -9;
+        } else {
+            if (clip5) {
+                for (int x = n; x > 0; --x) cg[x] = cg[x - 1];
+                cg[0] = ((uint32_t)clip5 << 4) | 4u;
+                ++n;
+            }
+            if (clip3) cg[n++] = ((uint32_t)clip3 << 4) | 4u;
+        }
+    }
+    D.o_gscore[t] = gsc;
+    D.o_pos[t] = pos;
+    D.o_ncig[t] = n;
+    D.o_status[t] = status;
+}
+
+// band of one ksw_global2 pass (mem_reg2aln/bwa_gen_cigar2); -1: empty query or
+// reference, 0 with nogap: equal lengths and w2 == 0 (no DP)
+__device__ __forceinline__ int glob_pass_w(const SwOptsDev &O, int lqq, int rlen, int w2, bool &nogap) {
+    nogap = false;
+    if (lqq <= 0 || rlen <= 0) return -1;
+    if (lqq == rlen && w2 == 0) { nogap = true; return 0; }
+    const int mn = lqq < rlen ? lqq : rlen;
+    const int max_ins = (int)((double)(mn * O.a - O.o_ins) / O.e_ins + 1.);
+    const int max_del = (int)((double)(mn * O.a - O.o_del) / O.e_del + 1.);
+    int max_gap = max_ins > max_del ? max_ins : max_del;
+    max_gap = max_gap > 1 ? max_gap : 1;
+    const int dl = rlen > lqq ? rlen - lqq : lqq - rlen;
+    int ww = (max_gap + dl + 1) >> 1;
+    ww = ww < w2 ? ww : w2;
+    const int min_w = dl + 3;
+    return ww > min_w ? ww : min_w;
+}
+// first-pass w2 of a task (after the extension)
+__device__ __forceinline__ int glob_w2(const SwDev &D, const SwOptsDev &O, int64_t t, int lqq, int rlen) {
+    const int truesc = D.o_truesc[t];
+    int tmpw = infer_bw(lqq, rlen, truesc, O.a, O.o_del, O.e_del);
+    int w2 = infer_bw(lqq, rlen, truesc, O.a, O.o_ins, O.e_ins);
+    w2 = w2 > tmpw ? w2 : tmpw;
+    const int wreg = D.o_w[t];
+    if (w2 > O.w) w2 = w2 < wreg ? w2 : wreg;
+    return w2 < O.w << 2 ? w2 : O.w << 2;
+}
+// band class of the first pass: 0 -> ring<40>, 1 -> ring<80>, 2 -> LDS kernel
+__device__ __forceinline__ int glob_class(const SwDev &D, const SwOptsDev &O, int64_t t) {
+    const int lqq = D.o_qe[t] - D.o_qb[t], rlen = D.o_re[t] - D.o_rb[t];
+    bool nogap;
+    const int ww = glob_pass_w(O, lqq, rlen, glob_w2(D, O, t, lqq, rlen), nogap);
+    return ww <= 40 ? 0 : (ww <= 80 ? 1 : 2);
+}
+
 __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_g[];
     __shared__ int s_task;
@@ -357,10 +409,11 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
         __syncthreads();
         const int64_t t0 = (int64_t)s_task * SW_WAVE;
         __syncthreads();
-        if (t0 >= D.n_task) break;
+        const int nl = D.list_n[0];
+        if (t0 >= nl) break;
         const int64_t slot = t0 + lane;
-        if (slot < D.n_task) {
-            const int64_t t = D.perm[slot];
+        if (slot < nl) {
+            const int64_t t = D.list[slot];
             const int sid = D.t_sr[t], lid = D.t_lr[t];
             const uint8_t *Q = D.sr + D.sr_off[sid];
             const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
@@ -443,57 +496,118 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
                     cg[n - 1 - x] = tmp;
                 }
             }
-            // mem_reg2aln: position, D squeeze, clipping
-            int pos = rev ? L - re : rb;
-            if (n > 0) {
-                if ((cg[0] & 0xFu) == 2u) {
-                    pos += (int)(cg[0] >> 4);
-                    for (int x = 0; x + 1 < n; ++x) cg[x] = cg[x + 1];
-                    --n;
-                } else if ((cg[n - 1] & 0xFu) == 2u) {
-                    --n;
-                }
-            }
-            if (qb != 0 || qe != lq) {
-                const int clip5 = rev ? lq - qe : qb;
-                const int clip3 = rev ? qb : lq - qe;
-                if (n + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > SW_MAXCIG) {
-                    status = -9;
-                } else {
-                    if (clip5) {
-                        for (int x = n; x > 0; --x) cg[x] = cg[x - 1];
-                        cg[0] = ((uint32_t)clip5 << 4) | 4u;
-                        ++n;
-                    }
-                    if (clip3) cg[n++] = ((uint32_t)clip3 << 4) | 4u;
-                }
-            }
-            D.o_gscore[t] = gsc;
-            D.o_pos[t] = pos;
-            D.o_ncig[t] = n;
-            D.o_status[t] = status;
+            glob_emit(D, t, cg, n, status, gsc, rev, lq, L, qb, qe, rb, re);
         }
     }
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
     if (lane == 0 && cells) atomicAdd(&D.cells[1], cells);
 }
 
+
+// ksw_global2 pass 1 with the DP row in registers (band class WB); a task whose
+// loop would run a second pass is left to the LDS kernel (x_try bit 2).
+template <int WB>
+__global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOptsDev O) {
+    constexpr int NW = (2 * WB + 2 + 7) / 8;
+    const int lane = threadIdx.x;
+    uint32_t *zl = reinterpret_cast<uint32_t *>(D.z) + (int64_t)blockIdx.x * D.z_ring_slab + lane;
+    unsigned long long cells = 0;
+    const int n = D.list_n[0];
+    for (int64_t c0 = (int64_t)blockIdx.x * SW_WAVE; c0 < n; c0 += (int64_t)gridDim.x * SW_WAVE) {
+        const int64_t slot = c0 + lane;
+        int64_t t = -1;
+        const uint8_t *Q = D.sr, *Lr = D.lr;
+        int lq = 0, L = 0, qb = 0, qe = 0, rb = 0, re = 0, lqq = 0, rlen = 0, w2 = 0, ww = -1, truesc = 0;
+        bool rev = false, nogap = false;
+        long tb = 0;
+        if (slot < n) {
+            t = D.list[slot];
+            const int sid = D.t_sr[t], lid = D.t_lr[t];
+            Q = D.sr + D.sr_off[sid];
+            lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
+            Lr = D.lr + D.lr_off[lid];
+            L = (int)(D.lr_off[lid + 1] - D.lr_off[lid]);
+            rev = D.t_strand[t] != 0;
+            qb = D.o_qb[t], qe = D.o_qe[t], rb = D.o_rb[t], re = D.o_re[t];
+            truesc = D.o_truesc[t];
+            lqq = qe - qb, rlen = re - rb;
+            tb = rev ? (long)L - re : (long)rb;
+            w2 = glob_w2(D, O, t, lqq, rlen);
+            ww = glob_pass_w(O, lqq, rlen, w2, nogap);
+        }
+        const bool dp = t >= 0 && ww > 0 && !nogap;
+        // query reversed on the reverse strand (indels leftmost on the forward strand)
+        const int qbase = rev ? qe - 1 : qb, qstep = rev ? -1 : 1;
+        int gsc = glob_ring<WB>(Q, qbase, qstep, dp ? lqq : 0, Lr, tb, 1, rev, dp ? rlen : 0, O, dp ? ww : 0, zl, SW_WAVE);
+        if (t < 0) continue;
+        if (ww < 0) gsc = 0;
+        if (nogap) {
+            gsc = 0;
+            for (int i = 0; i < lqq; ++i) {
+                int tc = (int)Lr[tb + i];
+                if (rev && tc < 4) tc = 3 - tc;
+                gsc += sw_score(tc, (int)Q[qbase + qstep * i], O.a, O.b);
+            }
+        }
+        // bwa_gen_cigar2's loop after pass 1: stop when w2 hit its cap or the score is close
+        // enough; otherwise the LDS kernel reruns the whole loop for this task
+        if (dp && w2 != O.w << 2 && gsc < truesc - O.a) {
+            D.x_try[t] = (uint8_t)(D.x_try[t] | 4);
+            continue;
+        }
+        uint32_t *cg = D.o_cig + t * SW_MAXCIG;
+        int nc = 0, status = 0;
+        if (ww < 0) {
+            nc = 0;
+        } else if (!dp || (O.debug & 1)) {
+            cg[0] = ((uint32_t)lqq << 4);
+            nc = 1;
+        } else {
+            cells += band_cells(rlen, lqq, ww);
+            nc = glob_backtrack<WB>(zl, SW_WAVE, rlen, lqq, ww, cg, SW_MAXCIG);
+            if (nc < 0) { status = -9; nc = 0; }
+            for (int x = 0; x < nc >> 1; ++x) {
+                const uint32_t tmp = cg[x];
+                cg[x] = cg[nc - 1 - x];
+                cg[nc - 1 - x] = tmp;
+            }
+        }
+        glob_emit(D, t, cg, nc, status, gsc, rev, lq, L, qb, qe, rb, re);
+    }
+    for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
+    if (lane == 0 && cells) atomicAdd(&D.cells[1], cells);
+}
+
 // ---------------------------------------------------------------------------
-// Task ordering: lanes of a wave run in lock-step, so tasks are bucketed by
-// (left extension length = qbeg, right extension length / 8) before the DP
-// kernels (counting sort; the order inside a bucket does not affect results).
-__device__ __forceinline__ int sw_task_key(const SwDev &D, int64_t t) {
+// Task ordering: lanes of a wave run in lock-step, so every DP launch takes its
+// tasks bucketed by query length (counting sort; the order inside a bucket does
+// not affect results).  Phase keys: 0/1 left extension try 0/1 (qbeg), 2/3
+// right extension try 0/1 (right length), 4 CIGAR pass (left<<5 | right/8).
+__device__ __forceinline__ int sw_phase_key(const SwDev &D, const SwOptsDev &O, int64_t t, int phase) {
     const int sid = D.t_sr[t];
     const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
     const int qbeg = D.t_qbeg[t];
-    int right = (lq - qbeg - D.t_slen[t]) >> 3;
-    right = right < 31 ? right : 31;
-    const int left = qbeg < 1023 ? qbeg : 1023;
-    return (left << 5) | right;
+    const int right = lq - qbeg - D.t_slen[t];
+    switch (phase) {
+        case 0: return qbeg > 0 ? qbeg : -1;
+        case 1: return (D.x_try[t] & 1) ? qbeg : -1;
+        case 2: return right > 0 ? right : -1;
+        case 3: return (D.x_try[t] & 2) ? right : -1;
+        case 5: return glob_class(D, O, t) == 0 ? D.o_qe[t] - D.o_qb[t] : -1;
+        case 6: return glob_class(D, O, t) == 1 ? D.o_qe[t] - D.o_qb[t] : -1;
+        case 7: return (glob_class(D, O, t) == 2 || (D.x_try[t] & 4)) ? D.o_qe[t] - D.o_qb[t] : -1;
+        default: {
+            const int r8 = (right >> 3) < 31 ? (right >> 3) : 31;
+            const int l = qbeg < 1023 ? qbeg : 1023;
+            return (l << 5) | r8;
+        }
+    }
 }
-__global__ void sw_order_count(SwDev D) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x)
-        atomicAdd(&D.bucket[sw_task_key(D, t)], 1);
+__global__ void sw_order_count(SwDev D, SwOptsDev O, int phase) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+        const int k = sw_phase_key(D, O, t, phase);
+        if (k >= 0) atomicAdd(&D.bucket[k], 1);
+    }
 }
 __global__ void __launch_bounds__(1024) sw_order_scan(int32_t *b) {
     __shared__ int part[1024];
@@ -514,37 +628,64 @@ __global__ void __launch_bounds__(1024) sw_order_scan(int32_t *b) {
         b[tid * per + k] = base;
         base += c;
     }
+    if (tid == 1023) b[SW_NBUCKET] = part[1023];   // list length
 }
-__global__ void sw_order_scatter(SwDev D) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x)
-        D.perm[atomicAdd(&D.bucket[sw_task_key(D, t)], 1)] = (int32_t)t;
+__global__ void sw_order_scatter(SwDev D, SwOptsDev O, int phase, int32_t *out) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+        const int k = sw_phase_key(D, O, t, phase);
+        if (k >= 0) out[atomicAdd(&D.bucket[k], 1)] = (int32_t)t;
+    }
 }
 
-int sw_launch_order(const SwDev &D, void *stream) {
+int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(D.bucket, 0, (SW_NBUCKET + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
     int grid = (int)((D.n_task + 255) / 256);
     grid = grid < 4096 ? (grid > 0 ? grid : 1) : 4096;
-    hipLaunchKernelGGL(sw_order_count, dim3(grid), dim3(256), 0, s, D);
+    hipLaunchKernelGGL(sw_order_count, dim3(grid), dim3(256), 0, s, D, O, phase);
     hipLaunchKernelGGL(sw_order_scan, dim3(1), dim3(1024), 0, s, D.bucket);
-    hipLaunchKernelGGL(sw_order_scatter, dim3(grid), dim3(256), 0, s, D);
+    hipLaunchKernelGGL(sw_order_scatter, dim3(grid), dim3(256), 0, s, D, O, phase, out);
     return (int)hipGetLastError();
 }
 
-int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream) {
-    hipError_t e = hipFuncSetAttribute((const void *)sw_extend_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+// the four extension phases + the two finish passes (mem_chain2aln)
+int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    int fgrid = (int)((D.n_task + 255) / 256);
+    fgrid = fgrid < 8192 ? (fgrid > 0 ? fgrid : 1) : 8192;
+    hipError_t e = hipMemsetAsync(D.x_try, 0, (size_t)D.n_task + 1, s);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(sw_extend_kernel, dim3(grid), dim3(SW_WAVE), lds, (hipStream_t)stream, D, O);
+    for (int side = 0; side < 2; ++side) {
+        for (int tryi = 0; tryi < 2; ++tryi) {
+            int rc = sw_launch_order(D, O, side * 2 + tryi, D.list, stream);
+            if (rc) return rc;
+            const int wb = O.w << tryi;
+            if (wb <= 32) hipLaunchKernelGGL(sw_ext_phase_kernel<32>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
+            else if (wb <= 40) hipLaunchKernelGGL(sw_ext_phase_kernel<40>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
+            else if (wb <= 64) hipLaunchKernelGGL(sw_ext_phase_kernel<64>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
+            else if (wb <= 80) hipLaunchKernelGGL(sw_ext_phase_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
+            else return (int)hipErrorInvalidValue;   // checked on the host (w <= 40)
+            if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+        }
+        if (side == 0) hipLaunchKernelGGL(sw_left_finish_kernel, dim3(fgrid), dim3(256), 0, s, D, O);
+        else hipLaunchKernelGGL(sw_right_finish_kernel, dim3(fgrid), dim3(256), 0, s, D, O);
+    }
     return (int)hipGetLastError();
 }
-int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream) {
-    hipError_t e = hipFuncSetAttribute((const void *)sw_global_kernel,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_lds, int lds, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    int rc;
+    if ((rc = sw_launch_order(D, O, 5, D.list, stream))) return rc;
+    hipLaunchKernelGGL(sw_global_ring_kernel<40>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
+    if ((rc = sw_launch_order(D, O, 6, D.list, stream))) return rc;
+    hipLaunchKernelGGL(sw_global_ring_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
+    if ((rc = sw_launch_order(D, O, 7, D.list, stream))) return rc;
+    hipError_t e = hipFuncSetAttribute((const void *)sw_global_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(sw_global_kernel, dim3(grid), dim3(SW_WAVE), lds, (hipStream_t)stream, D, O);
+    hipLaunchKernelGGL(sw_global_kernel, dim3(grid_lds), dim3(SW_WAVE), lds, s, D, O);
     return (int)hipGetLastError();
 }
+
 
 }  // namespace prgpu
