@@ -7,7 +7,7 @@ namespace prgpu {
 
 constexpr int SW_MAXCIG = 128;   // CIGAR ops per task (PR_SW_MAXCIG)
 constexpr int SW_WAVE = 64;
-constexpr int SW_NBUCKET = 1 << 15;   // (left extension length, right extension length / 8) keys
+constexpr int SW_NBUCKET = 1024;      // task-ordering keys (query lengths <= 1000)
 
 struct SwOptsDev {
     int a, b, o_del, e_del, o_ins, e_ins, w, pen_clip5, pen_clip3, zdrop;

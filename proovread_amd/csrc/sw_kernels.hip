@@ -582,7 +582,8 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
 // Task ordering: lanes of a wave run in lock-step, so every DP launch takes its
 // tasks bucketed by query length (counting sort; the order inside a bucket does
 // not affect results).  Phase keys: 0/1 left extension try 0/1 (qbeg), 2/3
-// right extension try 0/1 (right length), 4 CIGAR pass (left<<5 | right/8).
+// right extension try 0/1 (right length), 5/6 CIGAR pass 1 in the register
+// ring (band <= 40 / <= 80), 7 CIGAR passes in the LDS kernel (query length).
 __device__ __forceinline__ int sw_phase_key(const SwDev &D, const SwOptsDev &O, int64_t t, int phase) {
     const int sid = D.t_sr[t];
     const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
@@ -596,18 +597,21 @@ __device__ __forceinline__ int sw_phase_key(const SwDev &D, const SwOptsDev &O, 
         case 5: return glob_class(D, O, t) == 0 ? D.o_qe[t] - D.o_qb[t] : -1;
         case 6: return glob_class(D, O, t) == 1 ? D.o_qe[t] - D.o_qb[t] : -1;
         case 7: return (glob_class(D, O, t) == 2 || (D.x_try[t] & 4)) ? D.o_qe[t] - D.o_qb[t] : -1;
-        default: {
-            const int r8 = (right >> 3) < 31 ? (right >> 3) : 31;
-            const int l = qbeg < 1023 ? qbeg : 1023;
-            return (l << 5) | r8;
-        }
+        default: return -1;
     }
 }
-__global__ void sw_order_count(SwDev D, SwOptsDev O, int phase) {
+// block-local histograms in LDS, one global atomic per (block, key)
+__global__ void __launch_bounds__(256) sw_order_count(SwDev D, SwOptsDev O, int phase) {
+    __shared__ int hist[SW_NBUCKET];
+    for (int k = threadIdx.x; k < SW_NBUCKET; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
         const int k = sw_phase_key(D, O, t, phase);
-        if (k >= 0) atomicAdd(&D.bucket[k], 1);
+        if (k >= 0) atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1);
     }
+    __syncthreads();
+    for (int k = threadIdx.x; k < SW_NBUCKET; k += blockDim.x)
+        if (hist[k]) atomicAdd(&D.bucket[k], hist[k]);
 }
 __global__ void __launch_bounds__(1024) sw_order_scan(int32_t *b) {
     __shared__ int part[1024];
@@ -630,10 +634,23 @@ __global__ void __launch_bounds__(1024) sw_order_scan(int32_t *b) {
     }
     if (tid == 1023) b[SW_NBUCKET] = part[1023];   // list length
 }
-__global__ void sw_order_scatter(SwDev D, SwOptsDev O, int phase, int32_t *out) {
+// same grid and task partition as sw_order_count: each block reserves its
+// per-key ranges with one atomic each, then places its tasks
+__global__ void __launch_bounds__(256) sw_order_scatter(SwDev D, SwOptsDev O, int phase, int32_t *out) {
+    __shared__ int hist[SW_NBUCKET];
+    for (int k = threadIdx.x; k < SW_NBUCKET; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
         const int k = sw_phase_key(D, O, t, phase);
-        if (k >= 0) out[atomicAdd(&D.bucket[k], 1)] = (int32_t)t;
+        if (k >= 0) atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < SW_NBUCKET; k += blockDim.x)
+        if (hist[k]) hist[k] = atomicAdd(&D.bucket[k], hist[k]);
+    __syncthreads();
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+        const int k = sw_phase_key(D, O, t, phase);
+        if (k >= 0) out[atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1)] = (int32_t)t;
     }
 }
 
@@ -642,7 +659,7 @@ int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out,
     hipError_t e = hipMemsetAsync(D.bucket, 0, (SW_NBUCKET + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
     int grid = (int)((D.n_task + 255) / 256);
-    grid = grid < 4096 ? (grid > 0 ? grid : 1) : 4096;
+    grid = grid < 2048 ? (grid > 0 ? grid : 1) : 2048;
     hipLaunchKernelGGL(sw_order_count, dim3(grid), dim3(256), 0, s, D, O, phase);
     hipLaunchKernelGGL(sw_order_scan, dim3(1), dim3(1024), 0, s, D.bucket);
     hipLaunchKernelGGL(sw_order_scatter, dim3(grid), dim3(256), 0, s, D, O, phase, out);
