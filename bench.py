@@ -30,10 +30,11 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
-# VALU int32 peak: 256 CUs x 4 SIMD x 32 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md:
-# SIMD-32, a wave64 VALU op issues over 2 cycles; FP32 vector peak 157.3 TF = the same
-# lane rate x 2 flops per FMA).  Confirmed by tools/valu_peak.py (profiles/).
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# INT32 VALU peak: 256 CUs x 64 lanes per clock x 2.4 GHz = 39.3 Tops/s.
+# Measured with tools/valu_peak.hip (16 independent v_add_u32/v_max_i32 chains per lane,
+# 32 waves/CU): 37.0 Tops/s = 94 % of it (profiles/valu_peak_r01.json) -- integer ops do not
+# get the 2-cycle wave64 issue of FP32 (MI355X_MICROARCH.md), so 39.3 is the ceiling.
+VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 OPS_PER_CELL = 14   # SURVEY.md §8d canonical int ops per DP cell
 
@@ -110,9 +111,13 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ms = np.zeros(4)
+    dom_ms, dom_cells = 0.0, 0
     for _ in range(args.steps):
         step()
         ms += np.array(it.timing())
+        dm, dc = sw.dominant_kernel(ctx)
+        dom_ms += dm
+        dom_cells = dc
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -138,7 +143,8 @@ def main():
         return
     value = total_bases * args.steps / el / 1e6
     cells = ce + cg
-    ext_tops = ce * OPS_PER_CELL / (ms[0] * 1e-3) / 1e12
+    dom_ms /= max(args.steps, 1)
+    dom_tops = dom_cells * OPS_PER_CELL / (dom_ms * 1e-3) / 1e12
     # pileup kernel: algorithmic bytes (SURVEY.md §8d model) / kernel time
     n_aln, sum_ncig, sum_lseq = it.alignment_stats()
     cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + lr_bases * (2 + 2 + 6 * 4 * 2)
@@ -146,7 +152,7 @@ def main():
     traffic = None
     if prof.exists():
         try:
-            traffic = json.loads(prof.read_text()).get("sw_extend_kernel", {}).get("hbm_bytes_per_launch")
+            traffic = json.loads(prof.read_text()).get("sw_global_ring_kernel<40>", {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {
@@ -174,14 +180,15 @@ def main():
                      "handoff_sort": round(ms[2], 3), "consensus": round(ms[3], 3)},
         "consensus_phase_ms_summed_over_workgroups": {k: round(v, 1) for k, v in cns_phases.items()},
         "roofline": {
-            "kernel": "sw_extend_kernel (ksw_extend2, one task per lane)",
+            "kernel": "sw_global_ring_kernel<40> (ksw_global2 CIGAR pass, DP row in registers, one task per lane)",
             "bound": "valu",
-            "achieved": round(ext_tops, 3),
+            "achieved": round(dom_tops, 3),
             "peak": round(VALU_PEAK_TOPS, 2),
             "unit": "TOP/s (int32)",
-            "frac": round(ext_tops / VALU_PEAK_TOPS, 4),
+            "frac": round(dom_tops / VALU_PEAK_TOPS, 4),
             "traffic": traffic,
-            "cells_per_launch": int(ce),
+            "launch_ms": round(dom_ms, 3),
+            "cells_per_launch": int(dom_cells),
             "ops_per_cell": OPS_PER_CELL,
         },
         "roofline_consensus": {

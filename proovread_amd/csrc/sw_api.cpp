@@ -210,7 +210,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
 
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
-    e = sw_launch_global(D, O, grid_w, grid_g, lds_glob, (void *)s);
+    e = sw_launch_global(D, O, grid_w, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6), (void *)ctx_event(c, 7));
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     HIPCHK(hipEventRecord(ctx_event(c, 0), s));
     return 0;
@@ -233,8 +233,9 @@ extern "C" int pr_sw_download(pr_ctx *c, pr_sw_out *o) {
         float a = 0.f, b = 0.f;
         if (hipEventElapsedTime(&a, ctx_event(c, 2), ctx_event(c, 3)) == hipSuccess) r.ms_ext = a;
         if (hipEventElapsedTime(&b, ctx_event(c, 3), ctx_event(c, 0)) == hipSuccess) r.ms_glob = b;
+        if (hipEventElapsedTime(&b, ctx_event(c, 6), ctx_event(c, 7)) == hipSuccess) r.ms_glob_ring = b;
     }
-    HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 16, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 24, hipMemcpyDeviceToHost));
     const size_t n = (size_t)r.n_task;
     int rc;
     if ((rc = down(o->qb, r, SB_QB, n, s)) || (rc = down(o->qe, r, SB_QE, n, s)) ||
@@ -269,10 +270,26 @@ extern "C" int pr_sw_last_cells(pr_ctx *c, int64_t *ce, int64_t *cg) {
     if (r.loaded && r.buf[SB_CELLS]) {
         HIPCHK(hipSetDevice(ctx_device(c)));
         HIPCHK(hipStreamSynchronize(ctx_stream(c)));
-        HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 16, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 24, hipMemcpyDeviceToHost));
     }
     if (ce) *ce = (int64_t)r.cells[0];
     if (cg) *cg = (int64_t)r.cells[1];
+    return 0;
+}
+
+extern "C" int pr_sw_dominant_kernel(pr_ctx *c, double *ms, int64_t *cells) {
+    // the CIGAR pass's register-ring launch (band <= 40): HIP events around that
+    // launch alone on the SW stream, and the DP cells it computed
+    if (!c) return pr_set_error(PR_ERR_ARG, "null ctx");
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    HIPCHK(hipStreamSynchronize(ctx_stream(c)));
+    float b = 0.f;
+    if (r.n_task && hipEventElapsedTime(&b, ctx_event(c, 6), ctx_event(c, 7)) == hipSuccess) r.ms_glob_ring = b;
+    HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 24, hipMemcpyDeviceToHost));
+    if (ms) *ms = r.ms_glob_ring;
+    if (cells) *cells = (int64_t)r.cells[2];
     return 0;
 }
 

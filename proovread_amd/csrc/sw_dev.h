@@ -34,7 +34,7 @@ struct SwDev {
     uint8_t *z;                // direction-matrix slabs, one per resident block
     int64_t z_slab;            // bytes per slab (LDS kernel)
     int64_t z_ring_slab;       // dwords per slab (register-ring kernels: rows x words x 64 lanes)
-    unsigned long long *cells; // [2] canonical DP cells (extension, global)
+    unsigned long long *cells; // [3] canonical DP cells (extension, global, global ring<40> launch)
     int32_t *perm;             // lane -> task order (tasks bucketed by extension lengths)
     int32_t *bucket;           // [SW_NBUCKET + 1] counting-sort scratch
     int32_t *work;             // dequeue counter for the global kernel
@@ -51,7 +51,8 @@ struct SwResident {
     void *buf[32] = {};
     size_t cap[32] = {};
     float ms_ext = 0.f, ms_glob = 0.f;
-    unsigned long long cells[2] = {0, 0};
+    unsigned long long cells[3] = {0, 0, 0};
+    float ms_glob_ring = 0.f;
 };
 
 // device pointers of a resident SW batch (for the SW -> consensus pipeline)
@@ -66,7 +67,8 @@ struct SwPtrs {
 
 int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out, void *stream);
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *stream);
-int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_lds, int lds, void *stream);
+int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_lds, int lds, void *stream,
+                     void *ev_a, void *ev_b);
 void sw_release(SwResident &r);
 
 }  // namespace prgpu

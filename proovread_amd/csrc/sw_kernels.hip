@@ -575,7 +575,10 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
         glob_emit(D, t, cg, nc, status, gsc, rev, lq, L, qb, qe, rb, re);
     }
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
-    if (lane == 0 && cells) atomicAdd(&D.cells[1], cells);
+    if (lane == 0 && cells) {
+        atomicAdd(&D.cells[1], cells);
+        if (WB == 40) atomicAdd(&D.cells[2], cells);   // the dominant launch's own cells (bench roofline)
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -690,11 +693,14 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *s
     }
     return (int)hipGetLastError();
 }
-int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_lds, int lds, void *stream) {
+int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_lds, int lds, void *stream,
+                     void *ev_a, void *ev_b) {
     hipStream_t s = (hipStream_t)stream;
     int rc;
     if ((rc = sw_launch_order(D, O, 5, D.list, stream))) return rc;
+    if (ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
     hipLaunchKernelGGL(sw_global_ring_kernel<40>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
+    if (ev_b) (void)hipEventRecord((hipEvent_t)ev_b, s);
     if ((rc = sw_launch_order(D, O, 6, D.list, stream))) return rc;
     hipLaunchKernelGGL(sw_global_ring_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
     if ((rc = sw_launch_order(D, O, 7, D.list, stream))) return rc;

@@ -54,6 +54,7 @@ def _setup(L):
     L.pr_sw_download.argtypes = [C.c_void_p, C.POINTER(SwOut)]
     L.pr_sw_last_timing.argtypes = [C.c_void_p, _abi.PD, _abi.PD]
     L.pr_sw_last_cells.argtypes = [C.c_void_p, _abi.P64, _abi.P64]
+    L.pr_sw_dominant_kernel.argtypes = [C.c_void_p, _abi.PD, _abi.P64]
     L._sw_ready = True
 
 
@@ -140,3 +141,12 @@ def last_timing(ctx: _abi.Context):
     ce, cg = C.c_int64(), C.c_int64()
     L.pr_sw_last_cells(ctx.h, C.byref(ce), C.byref(cg))
     return a.value, b.value, ce.value, cg.value
+
+
+def dominant_kernel(ctx: _abi.Context):
+    """(ms, cells) of the last launch's CIGAR-pass register-ring kernel (band <= 40)."""
+    L = _abi.lib()
+    _setup(L)
+    ms, cells = C.c_double(), C.c_int64()
+    _abi.check(L.pr_sw_dominant_kernel(ctx.h, C.byref(ms), C.byref(cells)), "pr_sw_dominant_kernel")
+    return ms.value, cells.value
