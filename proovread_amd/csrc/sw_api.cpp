@@ -7,6 +7,7 @@
 
 #include "../../include/prgpu.h"
 #include "sw_dev.h"
+#include "sw_pk.h"
 
 using namespace prgpu;
 
@@ -119,9 +120,9 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
     const size_t n4 = (size_t)(nt + 1) * 4;
     for (int id : {SB_QB, SB_QE, SB_RB, SB_RE, SB_SCORE, SB_TRUESC, SB_W, SB_GSCORE, SB_POS, SB_NCIG, SB_STATUS})
         if ((rc = ensure(r, id, n4))) return rc;
-    if ((rc = ensure(r, SB_PERM, (size_t)(nt + 1) * 4)) || (rc = ensure(r, SB_BUCKET, (SW_NBUCKET + 1) * 4)) ||
+    if ((rc = ensure(r, SB_PERM, (size_t)(nt + 1) * 4)) || (rc = ensure(r, SB_BUCKET, (SW_NBUCKET + 16 + PK_SCAN + 1) * 4)) ||
         (rc = ensure(r, SB_X, (size_t)(nt + 1) * 4 * 12)) || (rc = ensure(r, SB_XTRY, (size_t)nt + 1)) ||
-        (rc = ensure(r, SB_LIST, (size_t)(nt + 1) * 4)))
+        (rc = ensure(r, SB_LIST, (size_t)(nt + 1 + (int64_t)PK_NB * PK_SEG) * 4)))
         return rc;
     if ((rc = ensure(r, SB_PASS, (size_t)nt + 1)) || (rc = ensure(r, SB_CIG, (size_t)(nt + 1) * SW_MAXCIG * 4)) ||
         (rc = ensure(r, SB_CELLS, 64)))
@@ -151,6 +152,8 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     O.a = o->a; O.b = o->b; O.o_del = o->o_del; O.e_del = o->e_del; O.o_ins = o->o_ins; O.e_ins = o->e_ins;
     O.w = o->w; O.pen_clip5 = o->pen_clip5; O.pen_clip3 = o->pen_clip3; O.zdrop = o->zdrop;
     O.min_score_per_base = o->min_score_per_base;
+    // the packed kernel's int16 frame holds |values| < 9000 for these penalties (sw_pk.h)
+    O.pk = (o->o_del <= 32 && o->o_ins <= 32 && o->e_del <= 32 && o->e_ins <= 32 && !getenv("PRGPU_SW_NOPK")) ? 1 : 0;
     O.debug = getenv("PRGPU_SW_DEBUG") ? atoi(getenv("PRGPU_SW_DEBUG")) : 0;
     SwDev D;
     std::memset(&D, 0, sizeof D);
@@ -188,6 +191,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.x_try = (uint8_t *)r.buf[SB_XTRY];
     D.list = (int32_t *)r.buf[SB_LIST];
     D.list_n = D.bucket + SW_NBUCKET;
+    D.pk_bucket = D.bucket + SW_NBUCKET + 16;
     // LDS of the CIGAR kernel: (qmax+1) H/E words per lane + lane-major query bytes
     const int lds_ext = (r.qmax + 1) * SW_WAVE * 4;
     const int qpad = (r.qmax + 8) & ~3;
@@ -198,8 +202,11 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.z_slab = (int64_t)D.tmax * ((r.qmax + 3) / 4) * 4 * SW_WAVE;
     const int grid_w = ctx_ncu(c) * 12;                       // ring kernels: 3 waves per SIMD
     D.z_ring_slab = (int64_t)D.tmax * ((2 * 80 + 2 + 7) / 8) * SW_WAVE;
-    const size_t zb = (size_t)D.z_slab * grid_g > (size_t)D.z_ring_slab * 4 * grid_w
-                          ? (size_t)D.z_slab * grid_g : (size_t)D.z_ring_slab * 4 * grid_w;
+    const int grid_pk = ctx_ncu(c) * 8;                       // packed kernel: ~200 VGPRs, 2 waves per SIMD
+    D.z_pk_slab = (int64_t)PK_TMAX * pk_npair(40) * SW_WAVE;
+    size_t zb = (size_t)D.z_slab * grid_g > (size_t)D.z_ring_slab * 4 * grid_w
+                    ? (size_t)D.z_slab * grid_g : (size_t)D.z_ring_slab * 4 * grid_w;
+    if ((size_t)D.z_pk_slab * sizeof(PkDir) * grid_pk > zb) zb = (size_t)D.z_pk_slab * sizeof(PkDir) * grid_pk;
     int rc;
     if ((rc = ensure(r, SB_Z, zb))) return rc;
     D.z = (uint8_t *)r.buf[SB_Z];
@@ -210,7 +217,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
 
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
-    e = sw_launch_global(D, O, grid_w, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6), (void *)ctx_event(c, 7));
+    e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6), (void *)ctx_event(c, 7));
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     HIPCHK(hipEventRecord(ctx_event(c, 0), s));
     return 0;

@@ -8,10 +8,14 @@ namespace prgpu {
 constexpr int SW_MAXCIG = 128;   // CIGAR ops per task (PR_SW_MAXCIG)
 constexpr int SW_WAVE = 64;
 constexpr int SW_NBUCKET = 1024;      // task-ordering keys (query lengths <= 1000)
+constexpr int PK_NB = 41 * 256;       // packed-kernel keys: band (<= 40) x query length (<= 255)
+constexpr int PK_SCAN = 11 * 1024;    // scanned key range (PK_NB rounded up to the scan's 1024 x 11)
+constexpr int PK_SEG = 128;           // tasks per wave (two per lane)
 
 struct SwOptsDev {
     int a, b, o_del, e_del, o_ins, e_ins, w, pen_clip5, pen_clip3, zdrop;
     double min_score_per_base;
+    int pk;      // 1: the packed two-tasks-per-lane CIGAR kernel may take tasks (penalties fit its int16 frame)
     int debug;   // timing ablations only (PRGPU_SW_DEBUG): 1 = skip backtrack, 2 = skip z stores
 };
 
@@ -34,6 +38,7 @@ struct SwDev {
     uint8_t *z;                // direction-matrix slabs, one per resident block
     int64_t z_slab;            // bytes per slab (LDS kernel)
     int64_t z_ring_slab;       // dwords per slab (register-ring kernels: rows x words x 64 lanes)
+    int64_t z_pk_slab;         // PkDir entries per slab (packed kernel: rows x chunks x 64 lanes)
     unsigned long long *cells; // [3] canonical DP cells (extension, global, global ring<40> launch)
     int32_t *perm;             // lane -> task order (tasks bucketed by extension lengths)
     int32_t *bucket;           // [SW_NBUCKET + 1] counting-sort scratch
@@ -42,6 +47,7 @@ struct SwDev {
     uint8_t *x_try;            // bit side: that side needs the second band try
     int32_t *list;             // task list of the current extension phase
     const int32_t *list_n;     // its length (device)
+    int32_t *pk_bucket;        // [PK_SCAN + 1] packed-kernel key counts -> padded offsets; [PK_SCAN] = list length
 };
 
 struct SwResident {
@@ -67,8 +73,8 @@ struct SwPtrs {
 
 int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out, void *stream);
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *stream);
-int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_lds, int lds, void *stream,
-                     void *ev_a, void *ev_b);
+int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
+                     void *stream, void *ev_a, void *ev_b);
 void sw_release(SwResident &r);
 
 }  // namespace prgpu

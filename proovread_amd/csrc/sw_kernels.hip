@@ -21,6 +21,7 @@
 
 #include "sw_dev.h"
 #include "sw_ring.h"
+#include "sw_pk.h"
 
 namespace prgpu {
 
@@ -393,6 +394,17 @@ __device__ __forceinline__ int glob_class(const SwDev &D, const SwOptsDev &O, in
     const int ww = glob_pass_w(O, lqq, rlen, glob_w2(D, O, t, lqq, rlen), nogap);
     return ww <= 40 ? 0 : (ww <= 80 ? 1 : 2);
 }
+// packed-kernel key (band * 256 + query length) of a task whose first pass runs a
+// DP with band <= 40 inside the kernel's int16 frame; -1 otherwise
+__device__ __forceinline__ int pk_key(const SwDev &D, const SwOptsDev &O, int64_t t) {
+    if (!O.pk) return -1;
+    const int lqq = D.o_qe[t] - D.o_qb[t], rlen = D.o_re[t] - D.o_rb[t];
+    if (lqq > PK_QMAX || rlen > PK_TMAX) return -1;
+    bool nogap;
+    const int ww = glob_pass_w(O, lqq, rlen, glob_w2(D, O, t, lqq, rlen), nogap);
+    if (ww <= 0 || nogap || ww > 40) return -1;
+    return ww * 256 + lqq;
+}
 
 __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_g[];
@@ -577,8 +589,181 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
     if (lane == 0 && cells) {
         atomicAdd(&D.cells[1], cells);
-        if (WB == 40) atomicAdd(&D.cells[2], cells);   // the dominant launch's own cells (bench roofline)
+        if (WB == 40 && !O.pk) atomicAdd(&D.cells[2], cells);   // the dominant launch's own cells (bench roofline)
     }
+}
+
+// ---------------------------------------------------------------------------
+// ksw_global2 pass 1 for two tasks per lane (sw_pk.h).  Wave k takes the 128-task
+// segment list[128k, 128k + 128) of one (band, query length) key: lane l runs
+// tasks list[128k + l] (low halves) and list[128k + 64 + l] (high halves).
+// Tasks that meet an N, or whose loop would run a second pass, are left to the
+// LDS kernel (x_try bit 2).
+
+template <int WB>
+__global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOptsDev O) {
+    // query masks during the DP ([half][bit][word][lane]), backtrack windows after it
+    __shared__ __attribute__((aligned(16))) uint32_t lsh[2 * 8 * SW_WAVE * 4];
+    static_assert(2 * 2 * PK_NQW <= 2 * 8 * 4, "mask words fit the backtrack window area");
+    const int lane = threadIdx.x;
+    uint32_t *lm = lsh;
+    PkDir *lw = reinterpret_cast<PkDir *>(lsh) + lane;
+    PkDir *zl = reinterpret_cast<PkDir *>(D.z) + (int64_t)blockIdx.x * D.z_pk_slab + lane;
+    unsigned long long cells = 0;
+    const int nseg = D.pk_bucket[PK_SCAN] / PK_SEG;
+    for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+        const int64_t tt[2] = {D.list[(int64_t)seg * PK_SEG + lane], D.list[(int64_t)seg * PK_SEG + 64 + lane]};
+        // the segment's key (its first task is never padding)
+        const int key = __builtin_amdgcn_readfirstlane(pk_key(D, O, D.list[(int64_t)seg * PK_SEG]));
+        const int ww = key >> 8, lqq = key & 255;
+        PkHalf H[2];
+        int nrow = 0, qn = 0;
+        __syncthreads();   // the previous segment's backtrack windows are done with the LDS
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t t = tt[h];
+            H[h] = PkHalf{D.lr, 0, false};
+            const uint8_t *Q = D.sr;
+            int qbase = 0, qstep = 1, ql = 0;
+            if (t >= 0) {
+                const int sid = D.t_sr[t], lid = D.t_lr[t];
+                const bool rev = D.t_strand[t] != 0;
+                const int qb = D.o_qb[t], qe = D.o_qe[t], rb = D.o_rb[t], re = D.o_re[t];
+                const int L = (int)(D.lr_off[lid + 1] - D.lr_off[lid]);
+                H[h] = PkHalf{D.lr + D.lr_off[lid] + (rev ? (long)L - re : (long)rb), re - rb, rev};
+                Q = D.sr + D.sr_off[sid];
+                qbase = rev ? qe - 1 : qb;
+                qstep = rev ? -1 : 1;
+                ql = lqq;
+            }
+            if (pk_build_mask(Q, qbase, qstep, ql, lm + (h * 2 * PK_NQW) * SW_WAVE + lane, SW_WAVE)) qn |= 1 << h;
+            nrow = nrow > H[h].tlen ? nrow : H[h].tlen;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const int v = __shfl_xor(nrow, o, 64);
+            nrow = nrow > v ? nrow : v;
+        }
+        nrow = __builtin_amdgcn_readfirstlane(nrow);
+        const int npair = pk_npair(ww);
+        int sc[2] = {0, 0}, nflag = 0;
+        glob_pk<WB>(H[0], H[1], lqq, ww, nrow, O, lm + lane, lm + 2 * PK_NQW * SW_WAVE + lane, SW_WAVE, zl,
+                    SW_WAVE, sc[0], sc[1], nflag);
+        nflag |= qn;
+        __syncthreads();   // masks dead: the LDS becomes the backtrack windows
+        uint32_t *cg[2] = {nullptr, nullptr};
+        int tl[2] = {0, 0};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t t = tt[h];
+            if (t < 0) continue;
+            const int rlen = H[h].tlen;
+            const int w2 = glob_w2(D, O, t, lqq, rlen);
+            if ((nflag >> h) & 1 || (w2 != O.w << 2 && sc[h] < D.o_truesc[t] - O.a)) {
+                D.x_try[t] = (uint8_t)(D.x_try[t] | 4);
+                continue;
+            }
+            cg[h] = D.o_cig + t * SW_MAXCIG;
+            tl[h] = rlen;
+        }
+        int nc[2] = {0, 0};
+        if (O.debug & 1) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (cg[h]) cg[h][0] = ((uint32_t)lqq << 4), nc[h] = 1;
+        } else {
+            pk_backtrack2(zl, SW_WAVE, npair, tl, lqq, ww, cg, nc, lw, SW_WAVE, SW_MAXCIG);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!cg[h]) continue;
+            const int64_t t = tt[h];
+            int status = 0, m = nc[h];
+            if (m < 0) { status = -9; m = 0; }
+            if (!(O.debug & 1))
+                for (int x = 0; x < m >> 1; ++x) {
+                    const uint32_t tmp = cg[h][x];
+                    cg[h][x] = cg[h][m - 1 - x];
+                    cg[h][m - 1 - x] = tmp;
+                }
+            const int sid = D.t_sr[t], lid = D.t_lr[t];
+            const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
+            const int L = (int)(D.lr_off[lid + 1] - D.lr_off[lid]);
+            cells += band_cells(tl[h], lqq, ww);
+            glob_emit(D, t, cg[h], m, status, sc[h], H[h].comp, lq, L, D.o_qb[t], D.o_qe[t], D.o_rb[t], D.o_re[t]);
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
+    if (lane == 0 && cells) {
+        atomicAdd(&D.cells[1], cells);
+        atomicAdd(&D.cells[2], cells);   // the dominant launch's own cells (bench roofline)
+    }
+}
+
+// ordering of the packed kernel's tasks: counting sort by key, every key's run
+// padded to a multiple of 128 (padding entries -1)
+__global__ void __launch_bounds__(256) pk_order_count(SwDev D, SwOptsDev O) {
+    __shared__ int hist[PK_NB];
+    for (int k = threadIdx.x; k < PK_NB; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+        const int k = pk_key(D, O, t);
+        if (k >= 0) atomicAdd(&hist[k], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < PK_NB; k += blockDim.x)
+        if (hist[k]) atomicAdd(&D.pk_bucket[k], hist[k]);
+}
+__global__ void __launch_bounds__(1024) pk_order_scan(int32_t *b) {
+    __shared__ int part[1024];
+    constexpr int per = PK_SCAN / 1024;
+    const int tid = threadIdx.x;
+    int s = 0;
+    for (int k = 0; k < per; ++k) s += (b[tid * per + k] + PK_SEG - 1) / PK_SEG * PK_SEG;
+    part[tid] = s;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int base = part[tid] - s;
+    for (int k = 0; k < per; ++k) {
+        const int c = (b[tid * per + k] + PK_SEG - 1) / PK_SEG * PK_SEG;
+        b[tid * per + k] = base;
+        base += c;
+    }
+    if (tid == 1023) b[PK_SCAN] = part[1023];   // padded list length
+}
+__global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O) {
+    __shared__ int hist[PK_NB];
+    for (int k = threadIdx.x; k < PK_NB; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+        const int k = pk_key(D, O, t);
+        if (k >= 0) atomicAdd(&hist[k], 1);
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < PK_NB; k += blockDim.x)
+        if (hist[k]) hist[k] = atomicAdd(&D.pk_bucket[k], hist[k]);
+    __syncthreads();
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+        const int k = pk_key(D, O, t);
+        if (k >= 0) D.list[atomicAdd(&hist[k], 1)] = (int32_t)t;
+    }
+}
+int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(D.pk_bucket, 0, (PK_SCAN + 1) * sizeof(int32_t), s);
+    if (e != hipSuccess) return (int)e;
+    e = hipMemsetAsync(D.list, 0xFF, (size_t)(D.n_task + (int64_t)PK_NB * PK_SEG + 1) * sizeof(int32_t), s);
+    if (e != hipSuccess) return (int)e;
+    int grid = (int)((D.n_task + 255) / 256);
+    grid = grid < 2048 ? (grid > 0 ? grid : 1) : 2048;
+    hipLaunchKernelGGL(pk_order_count, dim3(grid), dim3(256), 0, s, D, O);
+    hipLaunchKernelGGL(pk_order_scan, dim3(1), dim3(1024), 0, s, D.pk_bucket);
+    hipLaunchKernelGGL(pk_order_scatter, dim3(grid), dim3(256), 0, s, D, O);
+    return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -597,7 +782,7 @@ __device__ __forceinline__ int sw_phase_key(const SwDev &D, const SwOptsDev &O, 
         case 1: return (D.x_try[t] & 1) ? qbeg : -1;
         case 2: return right > 0 ? right : -1;
         case 3: return (D.x_try[t] & 2) ? right : -1;
-        case 5: return glob_class(D, O, t) == 0 ? D.o_qe[t] - D.o_qb[t] : -1;
+        case 5: return (glob_class(D, O, t) == 0 && pk_key(D, O, t) < 0) ? D.o_qe[t] - D.o_qb[t] : -1;
         case 6: return glob_class(D, O, t) == 1 ? D.o_qe[t] - D.o_qb[t] : -1;
         case 7: return (glob_class(D, O, t) == 2 || (D.x_try[t] & 4)) ? D.o_qe[t] - D.o_qb[t] : -1;
         default: return -1;
@@ -693,14 +878,20 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *s
     }
     return (int)hipGetLastError();
 }
-int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_lds, int lds, void *stream,
-                     void *ev_a, void *ev_b) {
+int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
+                     void *stream, void *ev_a, void *ev_b) {
     hipStream_t s = (hipStream_t)stream;
     int rc;
+    if (O.pk) {
+        if ((rc = sw_launch_pk_order(D, O, stream))) return rc;
+        if (ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
+        hipLaunchKernelGGL(sw_global_pk_kernel<40>, dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O);
+        if (ev_b) (void)hipEventRecord((hipEvent_t)ev_b, s);
+    }
     if ((rc = sw_launch_order(D, O, 5, D.list, stream))) return rc;
-    if (ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
+    if (!O.pk && ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
     hipLaunchKernelGGL(sw_global_ring_kernel<40>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
-    if (ev_b) (void)hipEventRecord((hipEvent_t)ev_b, s);
+    if (!O.pk && ev_b) (void)hipEventRecord((hipEvent_t)ev_b, s);
     if ((rc = sw_launch_order(D, O, 6, D.list, stream))) return rc;
     hipLaunchKernelGGL(sw_global_ring_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
     if ((rc = sw_launch_order(D, O, 7, D.list, stream))) return rc;

@@ -1,0 +1,413 @@
+// ksw_global2 for TWO tasks per lane in packed 16-bit arithmetic (device code,
+// also compiled for the host by tests/native/ring_host.cpp and checked against
+// the oracle there).
+//
+// Every 32-bit register holds one DP value of task A (low half) and of task B
+// (high half); one v_pk_* instruction advances both.  The two tasks of a lane,
+// and all 64 lanes of a wave, share the band w and the query length (the
+// ordering kernel groups tasks by (w, qlen) in 128-task segments), so the band
+// geometry of every row is wave-uniform and only the sequences differ.
+//
+// Slot scheme.  Slot s of row i holds query column c = i - w + s (the band of
+// row i starts at slot max(0, w - i)); NS = 2*WB + 2 slots.  The word read by
+// slot s is ring word s+1 (ksw_global2's eh[c]: H(i-1, c-1), E(i, c)), the new
+// eh[c] goes to ring word s: every column moves down one slot per row.
+// Columns left of the band are not masked out: columns < 0 carry NEG words and
+// column -1 carries E(i,-1) = -(o_del + e_del*(i+1)), so its cell yields
+// ksw_global2's H(i,-1) boundary naturally and the left edge needs no select.
+// Columns right of the band end are dead; the end column's E is set to NEG by
+// a per-row fixup (ksw_global2's eh[end].e = KSW_NEG_INF).
+//
+// Biased frame.  Values of row i carry the bias beta_i = (i+1)*b, so the score
+// step is M = Hdiag + (a+b)*[match] (no separate mismatch add); E is stored
+// pre-biased for the next row (its constants absorb the +b), F lives within the
+// row.  The final score is H - tlen*b.  All finite values stay within
+// (-7000, 9000) for the routed tasks (qlen <= 255, tlen <= 320, penalties <= 32);
+// NEG = -18000 (KSW_NEG_INF stand-in, only ever compared with finite values).
+//
+// Direction bits per cell (ksw_global2's): D1 = M < E, D2 = max(M,E) < F,
+// D3 = E-continue, D4 = F-continue, from the sign bits of packed differences;
+// v_perm_b32 turns the signs of two differences into four 0x00/0xFF bytes and
+// one v_bfi_b32 drops the slot's bit into them.  Per 8-slot chunk a lane
+// accumulates two dwords x = [A.D1, B.D1, A.D2, B.D2], y = [A.D3, B.D3, A.D4,
+// B.D4] (byte per task and bit, bit k = slot 8c+k) and stores them per row as
+// 16-byte pairs of chunks (one coalesced 1 KB store per wave).
+//
+// Match bits come from two bit masks per task (bit 0 / bit 1 of the 2-bit base
+// code over the query positions, 64-bit left pad), windowed per row with
+// v_alignbit_b32 and interleaved into 16-slot groups with v_perm_b32.  Tasks
+// with an N in the query or the target window are flagged and recomputed by
+// the general kernel (exact N scoring).
+#pragma once
+#include <stdint.h>
+
+#include "sw_ring.h"
+
+namespace prgpu {
+
+constexpr int PK_NQW = 13;        // mask words per (task, bit): 64-bit pad + 255 bases + 96-bit window
+constexpr int PK_QMAX = 255;      // routed query lengths
+constexpr int PK_TMAX = 320;      // routed reference lengths
+constexpr int PK_NEG = -18000;
+
+#ifndef SW_RING_HOST
+typedef short pk_v __attribute__((ext_vector_type(2)));
+SW_RING_FN pk_v PV(uint32_t u) { return __builtin_bit_cast(pk_v, u); }
+SW_RING_FN uint32_t PU(pk_v v) { return __builtin_bit_cast(uint32_t, v); }
+SW_RING_FN uint32_t pk_add(uint32_t a, uint32_t b) { return PU(PV(a) + PV(b)); }
+SW_RING_FN uint32_t pk_sub(uint32_t a, uint32_t b) { return PU(PV(a) - PV(b)); }
+SW_RING_FN uint32_t pk_max(uint32_t a, uint32_t b) { return PU(__builtin_elementwise_max(PV(a), PV(b))); }
+SW_RING_FN uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) { return PU(PV(a) * PV(b) + PV(c)); }
+SW_RING_FN uint32_t pk_shl(uint32_t a, int k) { return PU(PV(a) << pk_v{(short)k, (short)k}); }
+SW_RING_FN uint32_t pk_asr15(uint32_t a) { return PU(PV(a) >> pk_v{15, 15}); }
+SW_RING_FN uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) { return __builtin_amdgcn_perm(s0, s1, sel); }
+SW_RING_FN uint32_t align_b32(uint32_t hi, uint32_t lo, uint32_t sh) { return __builtin_amdgcn_alignbit(hi, lo, sh); }
+#else
+SW_RING_FN int16_t pk_lo(uint32_t a) { return (int16_t)(a & 0xFFFFu); }
+SW_RING_FN int16_t pk_hi(uint32_t a) { return (int16_t)(a >> 16); }
+SW_RING_FN uint32_t pk_mk(int lo, int hi) { return (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16); }
+SW_RING_FN uint32_t pk_add(uint32_t a, uint32_t b) { return pk_mk(pk_lo(a) + pk_lo(b), pk_hi(a) + pk_hi(b)); }
+SW_RING_FN uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_mk(pk_lo(a) - pk_lo(b), pk_hi(a) - pk_hi(b)); }
+SW_RING_FN uint32_t pk_max(uint32_t a, uint32_t b) {
+    return pk_mk(pk_lo(a) > pk_lo(b) ? pk_lo(a) : pk_lo(b), pk_hi(a) > pk_hi(b) ? pk_hi(a) : pk_hi(b));
+}
+SW_RING_FN uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
+    return pk_mk(pk_lo(a) * pk_lo(b) + pk_lo(c), pk_hi(a) * pk_hi(b) + pk_hi(c));
+}
+SW_RING_FN uint32_t pk_shl(uint32_t a, int k) { return pk_mk((uint16_t)(a << k), (uint16_t)((a >> 16) << k)); }
+SW_RING_FN uint32_t pk_asr15(uint32_t a) { return pk_mk(pk_lo(a) >> 15, pk_hi(a) >> 15); }
+SW_RING_FN uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {
+    const uint64_t d = ((uint64_t)s0 << 32) | s1;
+    uint32_t r = 0;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t v = (sel >> (8 * k)) & 0xFFu;
+        uint32_t byte;
+        if (v >= 13) byte = 0xFFu;
+        else if (v == 12) byte = 0u;
+        else if (v >= 8) byte = ((d >> (16 * (v - 8) + 15)) & 1u) ? 0xFFu : 0u;
+        else byte = (uint32_t)(d >> (8 * v)) & 0xFFu;
+        r |= byte << (8 * k);
+    }
+    return r;
+}
+SW_RING_FN uint32_t align_b32(uint32_t hi, uint32_t lo, uint32_t sh) {
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (sh & 31u));
+}
+#endif
+SW_RING_FN uint32_t pk_dup(int v) { return (uint32_t)(uint16_t)v * 0x10001u; }
+
+// One half (task) of a lane pair as glob_pk sees it.
+struct PkHalf {
+    const uint8_t *T;   // first reference base of the window in the forward long read (nt4)
+    int tlen;           // rows; 0 = empty half
+    bool comp;          // reverse strand: complement the reference bases
+};
+
+// Query bit masks of one task: m[(bit * PK_NQW + k) * MS], bit 0 / 1 of the base code
+// at bit 64 + j of the 416-bit string; returns true if the query holds an N.
+// (The byte loads of a word are unrolled so that they are all in flight together.)
+SW_RING_FN bool pk_build_mask(const uint8_t *Q, int qbase, int qstep, int qlen, uint32_t *m, int MS) {
+    bool has_n = false;
+    for (int k = 0; k < PK_NQW; ++k) {
+        uint32_t b0 = 0u, b1 = 0u;
+        const int j0 = 32 * k - 64;
+        if (j0 + 32 > 0 && j0 < qlen) {
+            uint32_t q[32];
+#pragma unroll
+            for (int x = 0; x < 32; ++x) {
+                const int j = j0 + x;
+                q[x] = (j >= 0 && j < qlen) ? (uint32_t)Q[qbase + qstep * j] : 0u;
+            }
+#pragma unroll
+            for (int x = 0; x < 32; ++x) {
+                has_n |= q[x] > 3u;
+                b0 |= (q[x] & 1u) << x;
+                b1 |= ((q[x] >> 1) & 1u) << x;
+            }
+        }
+        m[k * MS] = b0;
+        m[(PK_NQW + k) * MS] = b1;
+    }
+    return has_n;
+}
+
+// match bits of one task for the 96 columns from (p - 64): bit x of win[g] = column p - 64 + 32g + x
+SW_RING_FN void pk_window(const uint32_t *m, int MS, int p, int t, uint32_t win[3]) {
+    const int k = p >> 5;
+    const uint32_t sh = (uint32_t)(p & 31);
+    const uint32_t t0 = (t & 1) ? 0xFFFFFFFFu : 0u, t1 = (t & 2) ? 0xFFFFFFFFu : 0u;
+    uint32_t a[4], c[4];
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+        a[x] = m[(k + x) * MS];
+        c[x] = m[(PK_NQW + k + x) * MS];
+    }
+#pragma unroll
+    for (int g = 0; g < 3; ++g) {
+        const uint32_t q0 = align_b32(a[g + 1], a[g], sh), q1 = align_b32(c[g + 1], c[g], sh);
+        win[g] = ~((q0 ^ t0) | (q1 ^ t1));
+    }
+}
+
+// bitfield insert: bits of v where mask is set, of acc elsewhere (one v_bfi_b32)
+#ifndef SW_RING_HOST
+SW_RING_FN uint32_t bfi_b32(uint32_t mask, uint32_t v, uint32_t acc) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(v), "v"(acc));
+    return r;
+}
+// keeps a wave-uniform conditional block a real branch (a volatile asm cannot be
+// speculated), so skipped chunks cost a scalar branch instead of per-slot selects
+#define PK_BRANCH_BARRIER() asm volatile("")
+#else
+SW_RING_FN uint32_t bfi_b32(uint32_t mask, uint32_t v, uint32_t acc) { return (mask & v) | (~mask & acc); }
+#define PK_BRANCH_BARRIER() ((void)0)
+#endif
+
+// Direction words of one (row, 16-slot pair of chunks): chunk 2p in x0/y0, 2p+1 in x1/y1.
+struct PkDir {
+    uint32_t x0, y0, x1, y1;
+};
+constexpr int pk_npair(int w) { return (2 * w + 2 + 15) >> 4; }
+
+// The DP of both tasks.  mA/mB: their query masks; nrows = wave max of tlen;
+// z: direction words of this lane, (row, pair) at z[(i * npair + p) * ZS];
+// scA/scB: ksw_global2 scores; nflag gets bit 0 / 1 set if task A / B met an N
+// in its reference window.  w and qlen must be wave-uniform.
+template <int WB>
+SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int nrows, const SwOptsDev &O,
+                        const uint32_t *mA, const uint32_t *mB, int MS, PkDir *z, int ZS, int &scA, int &scB,
+                        int &nflag) {
+    constexpr int NS = 2 * WB + 2;
+    constexpr int CH = 8;
+    constexpr int NCH = (NS + CH - 1) / CH;
+    const int b = O.b;
+    const int npair = pk_npair(w);
+    const uint32_t NEG = pk_dup(PK_NEG);
+    const uint32_t NAB = pk_dup(-(O.a + b));               // m = -1 on a match: M = Hd + (a + b)
+    const uint32_t cE = pk_dup(O.e_del - b);               // E' = e0 - e_del (+ b: next row's bias)
+    const uint32_t cT1 = pk_dup(O.o_del + O.e_del - b);    // t1 = M - oe_del (+ b)
+    const uint32_t cD3 = pk_dup(O.o_del);                  // t1 - E' = D1 - o_del
+    const uint32_t cF = pk_dup(O.e_ins);
+    const uint32_t cT2 = pk_dup(O.o_ins + O.e_ins);
+    uint32_t RH[NS], RE[NS];
+    // row -1 (bias 0 for H, b for the stored E): eh[c] for c = s - w - 1
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+        const int c = s - w - 1;
+        int h = PK_NEG, e = PK_NEG;
+        if (c == -1) e = -(O.o_del + O.e_del) + b;
+        else if (c == 0) h = 0;
+        else if (c > 0 && c <= w && c <= qlen) h = -(O.o_ins + O.e_ins * c);
+        RH[s] = pk_dup(h);
+        RE[s] = pk_dup(e);
+    }
+    int tA = A.tlen > 0 ? (int)A.T[0] : 0, tB = B.tlen > 0 ? (int)B.T[0] : 0;
+    int hlA = 0, hlB = 0;
+    for (int i = 0; i < nrows; ++i) {
+        // reference bases of row i (prefetched one row ahead)
+        int ca = tA, cb = tB;
+        if (i + 1 < A.tlen) tA = (int)A.T[i + 1];
+        if (i + 1 < B.tlen) tB = (int)B.T[i + 1];
+        if (A.comp && ca < 4) ca = 3 - ca;
+        if (B.comp && cb < 4) cb = 3 - cb;
+        if (i < A.tlen && ca > 3) nflag |= 1;
+        if (i < B.tlen && cb > 3) nflag |= 2;
+        // match groups: slot s <-> bit s & 15 of G[s >> 4] (low half A, high half B)
+        uint32_t wa[3], wb[3], G[6];
+        pk_window(mA, MS, i - w + 64, ca & 3, wa);
+        pk_window(mB, MS, i - w + 64, cb & 3, wb);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            G[2 * g] = perm_b32(wb[g], wa[g], 0x05040100u);
+            G[2 * g + 1] = perm_b32(wb[g], wa[g], 0x07060302u);
+        }
+        const int beta = (i + 1) * b;
+        uint32_t h1 = i == w ? pk_dup(-(O.o_del + O.e_del * (i + 1)) + beta) : NEG;
+        uint32_t f = NEG;
+        const int se = (2 * w + 1 < qlen - i + w) ? 2 * w + 1 : qlen - i + w;   // slot of column end
+        const int lo = w - i - 2;                                                 // slot of column -2
+        const int cse = se >> 3;
+        PkDir *zi = z + (long)i * npair * ZS;
+        uint32_t hl = 0u, px = 0u, py = 0u;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if (c * CH > se || (c + 1) * CH - 1 < lo) continue;   // dead chunk (wave-uniform)
+            PK_BRANCH_BARRIER();
+            uint32_t ax = 0u, ay = 0u;
+#pragma unroll
+            for (int s = c * CH; s < (c + 1) * CH && s < NS; ++s) {
+                const uint32_t Hd = s + 1 < NS ? RH[s + 1] : NEG;
+                const uint32_t e0 = s + 1 < NS ? RE[s + 1] : NEG;
+                const uint32_t mm = pk_asr15(pk_shl(G[s >> 4], 15 - (s & 15)));
+                const uint32_t M = pk_mad(mm, NAB, Hd);
+                const uint32_t hme = pk_max(M, e0);
+                const uint32_t h = pk_max(hme, f);
+                const uint32_t D1 = pk_sub(M, e0);
+                const uint32_t D2 = pk_sub(hme, f);
+                const uint32_t Ep = pk_sub(e0, cE);
+                const uint32_t t1 = pk_sub(M, cT1);
+                RE[s] = pk_max(Ep, t1);
+                const uint32_t D3 = pk_sub(D1, cD3);
+                const uint32_t Fp = pk_sub(f, cF);
+                const uint32_t t2 = pk_sub(M, cT2);
+                f = pk_max(Fp, t2);
+                const uint32_t D4 = pk_sub(t2, Fp);
+                RH[s] = h1;
+                h1 = h;
+                const uint32_t bit = 0x01010101u << (s - c * CH);
+                ax = bfi_b32(bit, perm_b32(D2, D1, 0x0B0A0908u), ax);
+                ay = bfi_b32(bit, perm_b32(D4, D3, 0x0B0A0908u), ay);
+            }
+            if (c & 1) {
+                if (!(O.debug & 2)) zi[(c >> 1) * ZS] = PkDir{px, py, ax, ay};
+            } else if (c == cse || c + 1 == NCH) {
+                if (!(O.debug & 2)) zi[(c >> 1) * ZS] = PkDir{ax, ay, 0u, 0u};
+            } else {
+                px = ax, py = ay;
+            }
+            // eh[end]: E = NEG; its H (= H(i, end-1)) is the score once end == qlen.  A real
+            // (wave-uniform) branch: the 8 selects run in one chunk per row, not in all.
+            if (c == cse) {
+                PK_BRANCH_BARRIER();
+#pragma unroll
+                for (int s = c * CH; s < (c + 1) * CH && s < NS; ++s)
+                    if (s == se) {
+                        RE[s] = NEG;
+                        hl = RH[s];
+                    }
+            }
+        }
+        if (i == A.tlen - 1) hlA = (int)(int16_t)(hl & 0xFFFFu) - beta;
+        if (i == B.tlen - 1) hlB = (int)(int16_t)(hl >> 16) - beta;
+    }
+    scA = hlA;
+    scB = hlB;
+}
+
+// direction nibble (D1 | D2 << 1 | D3 << 2 | D4 << 3) of half hb at (row i, slot s)
+SW_RING_FN int pk_nib(const PkDir &v, int s, int hb) {
+    const uint32_t x = (s & 8) ? v.x1 : v.x0, y = (s & 8) ? v.y1 : v.y0;
+    const int bt = (s & 7) + 8 * hb;
+    return (int)(((x >> bt) & 1u) | (((x >> (bt + 16)) & 1u) << 1) | (((y >> bt) & 1u) << 2) |
+                 (((y >> (bt + 16)) & 1u) << 3));
+}
+// ksw_global2's state step: h source (M 0, E 1, F 2) from state 0, continue bits otherwise
+SW_RING_FN int pk_which(int which, int nib) {
+    if (which == 0) return (nib & 2) ? 2 : (nib & 1);
+    if (which == 1) return (nib >> 2) & 1;
+    return ((nib >> 3) & 1) * 2;
+}
+
+// ksw_global2's backtrack for half `hb` (0 = A, 1 = B) over glob_pk's direction
+// words: ops (0 M, 1 I, 2 D) pushed in reverse order; returns the count or -1.
+SW_RING_FN int glob_pk_backtrack(const PkDir *z, int ZS, int npair, int hb, int tlen, int qlen, int w, uint32_t *cg,
+                                 int maxcig) {
+    int n = 0;
+    auto push = [&](int op, int len) {
+        if (n < 0) return;
+        if (n > 0 && (int)(cg[n - 1] & 0xFu) == op) {
+            cg[n - 1] += (uint32_t)len << 4;
+            return;
+        }
+        if (n >= maxcig) { n = -1; return; }
+        cg[n++] = ((uint32_t)len << 4) | (uint32_t)op;
+    };
+    int i = tlen - 1, k = (i + w + 1 < qlen ? i + w + 1 : qlen) - 1, which = 0;
+    while (i >= 0 && k >= 0 && n >= 0) {
+        const int s = k - i + w;
+        which = pk_which(which, pk_nib(z[((long)i * npair + (s >> 4)) * ZS], s, hb));
+        if (which == 0) push(0, 1), --i, --k;
+        else if (which == 1) push(2, 1), --i;
+        else push(1, 1), --k;
+    }
+    if (n >= 0 && i >= 0) push(2, i + 1);
+    if (n >= 0 && k >= 0) push(1, k + 1);
+    return n;
+}
+
+// Backtrack of both halves of a lane (glob_pk_backtrack's walk, ops pushed in
+// reverse order; the kernel's version: glob_pk_backtrack is the plain reference).  The walk mostly keeps its slot (diagonal moves), so it reads
+// a window of 8 rows x one 16-slot pair: the 8 loads of a window are issued
+// together and staged in LDS (lw: [half][row][lane]); a half reloads only when
+// it leaves its window.  Both halves advance in the same loop.  The current op
+// run stays in registers.  n[h] = op count or -1 (more than maxcig).
+SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, const int tl[2], int qlen, int w,
+                              uint32_t *const cg[2], int n[2], PkDir *lw, int LS, int maxcig) {
+    int i[2], k[2], which[2] = {0, 0}, rop[2] = {-1, -1}, rln[2] = {0, 0}, wr[2] = {-1, -1}, wp[2] = {-1, -1};
+    bool live[2];
+    // ksw's push with the last op kept in registers: false when the op count would exceed maxcig
+    auto push = [&](int h, int op, int len) -> bool {
+        if (op == rop[h]) {
+            rln[h] += len;
+            return true;
+        }
+        if (rop[h] >= 0) {
+            if (n[h] + 1 >= maxcig) return false;
+            cg[h][n[h]++] = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
+        }
+        rop[h] = op;
+        rln[h] = len;
+        return true;
+    };
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        i[h] = tl[h] - 1;
+        k[h] = (i[h] + w + 1 < qlen ? i[h] + w + 1 : qlen) - 1;
+        n[h] = 0;
+        live[h] = cg[h] != nullptr && i[h] >= 0 && k[h] >= 0;
+    }
+    while (live[0] || live[1]) {
+        PkDir buf[2][8];
+        bool need[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int sp = (k[h] - i[h] + w) >> 4;
+            need[h] = live[h] && !(i[h] <= wr[h] && i[h] > wr[h] - 8 && sp == wp[h]);
+            if (need[h]) {
+#pragma unroll
+                for (int d = 0; d < 8; ++d) {
+                    const int r = i[h] - d;
+                    buf[h][d] = r >= 0 ? zl[((long)r * npair + sp) * ZS] : PkDir{0u, 0u, 0u, 0u};
+                }
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (need[h]) {
+#pragma unroll
+                for (int d = 0; d < 8; ++d) lw[(h * 8 + d) * LS] = buf[h][d];
+                wr[h] = i[h];
+                wp[h] = (k[h] - i[h] + w) >> 4;
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!live[h]) continue;
+            const int sl = k[h] - i[h] + w;
+            which[h] = pk_which(which[h], pk_nib(lw[(h * 8 + (wr[h] - i[h])) * LS], sl, h));
+            const int op = which[h] == 0 ? 0 : (which[h] == 1 ? 2 : 1);
+            if (!push(h, op, 1)) {
+                n[h] = -1;
+                live[h] = false;
+                continue;
+            }
+            if (which[h] == 0) --i[h], --k[h];
+            else if (which[h] == 1) --i[h];
+            else --k[h];
+            live[h] = i[h] >= 0 && k[h] >= 0;
+        }
+    }
+    // leading D / I remainders (ksw's pushes after the walk), then the last run
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        if (cg[h] == nullptr || n[h] < 0) continue;
+        bool ok = true;
+        if (i[h] >= 0) ok = push(h, 2, i[h] + 1);
+        if (ok && k[h] >= 0) ok = push(h, 1, k[h] + 1);
+        if (!ok) n[h] = -1;
+        else if (rop[h] >= 0) cg[h][n[h]++] = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
+    }
+}
+
+}  // namespace prgpu

@@ -50,3 +50,49 @@ extern "C" int ring_global(int wb, int a, int b, int o_del, int e_del, int o_ins
     *n_cigar = n;
     return sc;
 }
+
+// ksw_global2 + backtrack for a lane pair in the packed kernel's arithmetic
+// (proovread_amd/csrc/sw_pk.h): two tasks with the same query length and band,
+// their own queries/targets; scores to sc[2], CIGARs (bwa order) to cig[h * max_cigar ..].
+#include <algorithm>
+#include <vector>
+#include "../../proovread_amd/csrc/sw_pk.h"
+extern "C" int pk_global(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int qlen, int w,
+                         const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb, const uint8_t *tb,
+                         int *sc, int *ncig, uint32_t *cig, int max_cigar, int nrow_min) {
+    SwOptsDev O{};
+    O.a = a; O.b = b; O.o_del = o_del; O.e_del = e_del; O.o_ins = o_ins; O.e_ins = e_ins;
+    uint32_t m[2][2 * PK_NQW];
+    int qn = 0;
+    if (pk_build_mask(qa, 0, 1, tla >= 0 ? qlen : 0, m[0], 1)) qn |= 1;
+    if (pk_build_mask(qb, 0, 1, tlb >= 0 ? qlen : 0, m[1], 1)) qn |= 2;
+    PkHalf A{ta, tla > 0 ? tla : 0, false}, B{tb, tlb > 0 ? tlb : 0, false};
+    int nrow = A.tlen > B.tlen ? A.tlen : B.tlen;
+    if (nrow < nrow_min) nrow = nrow_min;   // other lanes of the wave may run longer
+    const int npair = pk_npair(w);
+    PkDir *z = new PkDir[(size_t)(nrow + 1) * npair + 1]();
+    int s2[2] = {0, 0}, nflag = 0;
+    glob_pk<40>(A, B, qlen, w, nrow, O, m[0], m[1], 1, z, 1, s2[0], s2[1], nflag);
+    // the kernel's windowed two-half backtrack, checked against the plain one
+    PkDir lw[16];
+    const int tl2[2] = {A.tlen, B.tlen};
+    uint32_t *cg2[2] = {A.tlen > 0 ? cig : nullptr, B.tlen > 0 ? cig + max_cigar : nullptr};
+    int n2[2] = {0, 0};
+    pk_backtrack2(z, 1, npair, tl2, qlen, w, cg2, n2, lw, 1, max_cigar);
+    for (int h = 0; h < 2; ++h) {
+        const int tl = h ? B.tlen : A.tlen;
+        uint32_t *cg = cig + (size_t)h * max_cigar;
+        std::vector<uint32_t> ref(max_cigar + 1);
+        int n = tl > 0 ? glob_pk_backtrack(z, 1, npair, h, tl, qlen, w, ref.data(), max_cigar) : 0;
+        if (tl > 0 && (n != n2[h] || (n > 0 && !std::equal(ref.begin(), ref.begin() + n, cg)))) {
+            delete[] z;
+            return -1000 - h;   // windowed walk disagrees with the plain walk
+        }
+        if (n > 0)
+            for (int x = 0; x < n / 2; ++x) { uint32_t t = cg[x]; cg[x] = cg[n - 1 - x]; cg[n - 1 - x] = t; }
+        ncig[h] = n;
+        sc[h] = s2[h];
+    }
+    delete[] z;
+    return nflag | (qn << 2);
+}

@@ -98,3 +98,50 @@ def test_global_ring_matches_oracle(ring, seed):
             assert (sc2, list(cig2[:nc2.value])) == (sc, list(cig[:nc.value])), (q, t, w, wb)
             n += 1
     assert n > 600
+
+
+@pytest.mark.parametrize("seed", [31, 32, 33])
+def test_global_pk_matches_oracle(ring, seed):
+    """ksw_global2 + backtrack of the packed two-tasks-per-lane kernel (sw_pk.h), host
+    emulation of its int16 arithmetic, vs oracle osw_global: scores and CIGARs of both
+    halves, shared query length and band, independent sequences and target lengths."""
+    L = ob.sw_lib()
+    rng = random.Random(seed)
+    n = 0
+    for _ in range(300):
+        lq = rng.choice([1, 2, 5, 10, 30, 60, 100, 149, 150, 151, 200, 255])
+        qs = ["".join(rng.choice("ACGT") for _ in range(lq)) for _ in range(2)]
+        ts = [(_mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])).replace("N", "A") or "A") for q in qs]
+        if rng.random() < 0.15:
+            ts[1] = ""      # empty partner half
+        dls = [abs(len(t) - lq) for t in ts if t]
+        if max(dls) + 3 > 40 or any(len(t) > 320 for t in ts):
+            continue
+        w = rng.randint(max(dls) + 3, 40)
+        nrow = rng.choice([0, lq + w - 3])   # the wave's longest reference window bounds the rows
+        for a, b, od, ed, oi, ei, _ in SCORING[:2]:
+            sc, nc, cig = (C.c_int * 2)(), (C.c_int * 2)(), (C.c_uint32 * 8192)()
+            fl = ring.pk_global(a, b, od, ed, oi, ei, lq, w, _nt4(qs[0]), _nt4(qs[1]), len(ts[0]), _nt4(ts[0]),
+                                len(ts[1]) if ts[1] else -1, _nt4(ts[1] or "A"), sc, nc, cig, 4096, nrow)
+            assert fl == 0
+            for h in range(2):
+                if not ts[h]:
+                    continue
+                mat = (C.c_int8 * 25)()
+                L.osw_fill_scmat(a, b, mat)
+                nco, cigo = C.c_int(), (C.c_uint32 * 4096)()
+                so = L.osw_global(lq, _nt4(qs[h]), len(ts[h]), _nt4(ts[h]), 5, mat, od, ed, oi, ei, w,
+                                  C.byref(nco), cigo, 4096)
+                got = (sc[h], list(cig[h * 4096:h * 4096 + nc[h]]))
+                assert got == (so, list(cigo[:nco.value])), (h, qs[h], ts[h], w, (a, b, od, ed, oi, ei))
+                n += 1
+    assert n > 600
+
+
+def test_global_pk_flags_n(ring):
+    """An N in the query or the target window is flagged (the task goes to the exact kernel)."""
+    q, t = "ACGTNACGTA", "ACGTAACGTA"
+    sc, nc, cig = (C.c_int * 2)(), (C.c_int * 2)(), (C.c_uint32 * 256)()
+    fl = ring.pk_global(5, 11, 2, 4, 1, 3, 10, 5, _nt4(q), _nt4(t), 10, _nt4(t), 10, _nt4("ACGTANCGTA"),
+                        sc, nc, cig, 128, 0)
+    assert fl == (1 << 2) | 2
