@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the configs[1] workload per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-lrs-per-worker", type=int, default=96)
+    ap.add_argument("--cpu-lrs-per-worker", type=int, default=256)
     return ap.parse_args()
 
 

@@ -213,7 +213,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     HIPCHK(hipMemsetAsync(r.buf[SB_CELLS], 0, 64, s));
     if (r.n_task == 0) return 0;
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
-    int e = sw_launch_extend(D, O, ctx_ncu(c) * 16, (void *)s);
+    int e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
 
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));

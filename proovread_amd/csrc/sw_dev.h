@@ -72,7 +72,7 @@ struct SwPtrs {
 };
 
 int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out, void *stream);
-int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *stream);
+int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream);
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
                      void *stream, void *ev_a, void *ev_b);
 void sw_release(SwResident &r);

@@ -95,6 +95,16 @@ __device__ __forceinline__ TaskGeo task_geo(const SwDev &D, const SwOptsDev &O, 
     return g;
 }
 
+// packed extension key (mode 1 = left, 2 = right side, first band try): the side's
+// query length, for tasks whose scores fit the kernel's int16 frame; -1 otherwise
+__device__ __forceinline__ int pk_ext_key(const SwDev &D, const SwOptsDev &O, int64_t t, int side) {
+    if (!O.pk || O.w > 40) return -1;
+    const int sid = D.t_sr[t];
+    const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
+    const int ql = side == 0 ? D.t_qbeg[t] : lq - D.t_qbeg[t] - D.t_slen[t];
+    if (ql <= 0 || ql > PK_QMAX || O.a * lq > 2047) return -1;
+    return ql;
+}
 // per-task extension scratch: field f of side s at x[(s * XF + f) * n_task + t]
 enum { XF_SCORE, XF_QLE, XF_TLE, XF_GTLE, XF_GSCORE, XF_MAXOFF, XF };
 __device__ __forceinline__ int32_t &xref(const SwDev &D, int side, int f, int64_t t) {
@@ -167,6 +177,77 @@ __device__ __forceinline__ int band_w(const SwOptsDev &O, int w, int qlen, int e
     int max_del = (int)((double)(qlen * O.a + end_bonus - O.o_del) / O.e_del + 1.);
     max_del = max_del > 1 ? max_del : 1;
     return w < max_del ? w : max_del;
+}
+
+// First band try of one extension side for two tasks per lane (sw_pk.h ext_pk):
+// wave k takes the 128-task segment of one side query length (so qlen and the
+// capped band are wave-uniform); lane l runs list[128k + l] and list[128k + 64 + l].
+// Tasks that meet an N are flagged (x_try bit 3 + side) for sw_ext_phase_kernel.
+template <int WB>
+__global__ void __launch_bounds__(SW_WAVE, 2) sw_ext_pk_kernel(SwDev D, SwOptsDev O, int side) {
+    __shared__ __attribute__((aligned(16))) uint32_t lm[2 * 2 * PK_NQW * SW_WAVE];
+    const int lane = threadIdx.x;
+    const int nseg = D.pk_bucket[PK_SCAN] / PK_SEG;
+    const int end_bonus = side == 0 ? O.pen_clip5 : O.pen_clip3;
+    for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+        const int64_t tt[2] = {D.list[(int64_t)seg * PK_SEG + lane], D.list[(int64_t)seg * PK_SEG + 64 + lane]};
+        const int qlen = __builtin_amdgcn_readfirstlane(pk_ext_key(D, O, D.list[(int64_t)seg * PK_SEG], side));
+        const int w = __builtin_amdgcn_readfirstlane(band_w(O, O.w, qlen, end_bonus));
+        PkExtHalf H[2];
+        int nrow = 0, nflag = 0;
+        __syncthreads();
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t t = tt[h];
+            H[h] = PkExtHalf{D.lr, 1, false, 0, 0};
+            const uint8_t *Q = D.sr;
+            int qb = 0, qs = 1, ql = 0;
+            if (t >= 0) {
+                const TaskGeo g = task_geo(D, O, t);
+                Q = g.Q;
+                ql = qlen;
+                if (side == 0) {
+                    qb = g.qbeg - 1; qs = -1;
+                    const long tb = g.rev ? (long)g.L - g.rbeg : (long)g.rbeg - 1;
+                    H[h] = PkExtHalf{g.Lr + tb, g.rev ? 1 : -1, g.rev, (int)(g.rbeg - g.rmax0), g.slen * O.a};
+                } else {
+                    const int qe0 = g.qbeg + g.slen;
+                    const int re0 = (int)(g.rbeg + g.slen - g.rmax0);
+                    qb = qe0; qs = 1;
+                    const long tb = g.rev ? (long)g.L - 1 - g.rbeg - g.slen : (long)g.rbeg + g.slen;
+                    H[h] = PkExtHalf{g.Lr + tb, g.rev ? -1 : 1, g.rev, (int)(g.rmax1 - g.rmax0 - re0), D.o_score[t]};
+                }
+            }
+            if (pk_build_mask(Q, qb, qs, ql, lm + (h * 2 * PK_NQW) * SW_WAVE + lane, SW_WAVE)) nflag |= 1 << h;
+            nrow = nrow > H[h].tlen ? nrow : H[h].tlen;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const int v = __shfl_xor(nrow, o, 64);
+            nrow = nrow > v ? nrow : v;
+        }
+        nrow = __builtin_amdgcn_readfirstlane(nrow);
+        PkExtOut out[2];
+        ext_pk<WB>(H[0], H[1], qlen, w, nrow, O, lm + lane, lm + 2 * PK_NQW * SW_WAVE + lane, SW_WAVE, out, nflag);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t t = tt[h];
+            if (t < 0) continue;
+            if ((nflag >> h) & 1) {
+                D.x_try[t] = (uint8_t)(D.x_try[t] | (8 << side));
+                continue;
+            }
+            xref(D, side, XF_SCORE, t) = out[h].score;
+            xref(D, side, XF_QLE, t) = out[h].qle;
+            xref(D, side, XF_TLE, t) = out[h].tle;
+            xref(D, side, XF_GTLE, t) = out[h].gtle;
+            xref(D, side, XF_GSCORE, t) = out[h].gscore;
+            xref(D, side, XF_MAXOFF, t) = out[h].max_off;
+            const int aw = O.w;
+            const int prev = side == 0 ? -1 : H[h].h0;
+            const bool stop = out[h].score == prev || out[h].max_off < (aw >> 1) + (aw >> 2);
+            D.x_try[t] = (uint8_t)(D.x_try[t] | (stop ? 0 : (1 << side)));
+        }
+    }
 }
 
 // after the left phases: qb, rb, score, truesc (mem_chain2aln); o_w holds aw[0]
@@ -701,12 +782,15 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
 
 // ordering of the packed kernel's tasks: counting sort by key, every key's run
 // padded to a multiple of 128 (padding entries -1)
-__global__ void __launch_bounds__(256) pk_order_count(SwDev D, SwOptsDev O) {
+__device__ __forceinline__ int pk_mode_key(const SwDev &D, const SwOptsDev &O, int64_t t, int mode) {
+    return mode == 0 ? pk_key(D, O, t) : pk_ext_key(D, O, t, mode - 1);
+}
+__global__ void __launch_bounds__(256) pk_order_count(SwDev D, SwOptsDev O, int mode) {
     __shared__ int hist[PK_NB];
     for (int k = threadIdx.x; k < PK_NB; k += blockDim.x) hist[k] = 0;
     __syncthreads();
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
-        const int k = pk_key(D, O, t);
+        const int k = pk_mode_key(D, O, t, mode);
         if (k >= 0) atomicAdd(&hist[k], 1);
     }
     __syncthreads();
@@ -735,12 +819,12 @@ __global__ void __launch_bounds__(1024) pk_order_scan(int32_t *b) {
     }
     if (tid == 1023) b[PK_SCAN] = part[1023];   // padded list length
 }
-__global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O) {
+__global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O, int mode) {
     __shared__ int hist[PK_NB];
     for (int k = threadIdx.x; k < PK_NB; k += blockDim.x) hist[k] = 0;
     __syncthreads();
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
-        const int k = pk_key(D, O, t);
+        const int k = pk_mode_key(D, O, t, mode);
         if (k >= 0) atomicAdd(&hist[k], 1);
     }
     __syncthreads();
@@ -748,11 +832,11 @@ __global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O) {
         if (hist[k]) hist[k] = atomicAdd(&D.pk_bucket[k], hist[k]);
     __syncthreads();
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
-        const int k = pk_key(D, O, t);
+        const int k = pk_mode_key(D, O, t, mode);
         if (k >= 0) D.list[atomicAdd(&hist[k], 1)] = (int32_t)t;
     }
 }
-int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, void *stream) {
+int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(D.pk_bucket, 0, (PK_SCAN + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
@@ -760,9 +844,9 @@ int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, void *stream) {
     if (e != hipSuccess) return (int)e;
     int grid = (int)((D.n_task + 255) / 256);
     grid = grid < 2048 ? (grid > 0 ? grid : 1) : 2048;
-    hipLaunchKernelGGL(pk_order_count, dim3(grid), dim3(256), 0, s, D, O);
+    hipLaunchKernelGGL(pk_order_count, dim3(grid), dim3(256), 0, s, D, O, mode);
     hipLaunchKernelGGL(pk_order_scan, dim3(1), dim3(1024), 0, s, D.pk_bucket);
-    hipLaunchKernelGGL(pk_order_scatter, dim3(grid), dim3(256), 0, s, D, O);
+    hipLaunchKernelGGL(pk_order_scatter, dim3(grid), dim3(256), 0, s, D, O, mode);
     return (int)hipGetLastError();
 }
 
@@ -778,9 +862,9 @@ __device__ __forceinline__ int sw_phase_key(const SwDev &D, const SwOptsDev &O, 
     const int qbeg = D.t_qbeg[t];
     const int right = lq - qbeg - D.t_slen[t];
     switch (phase) {
-        case 0: return qbeg > 0 ? qbeg : -1;
+        case 0: return (qbeg > 0 && (pk_ext_key(D, O, t, 0) < 0 || (D.x_try[t] & 8))) ? qbeg : -1;
         case 1: return (D.x_try[t] & 1) ? qbeg : -1;
-        case 2: return right > 0 ? right : -1;
+        case 2: return (right > 0 && (pk_ext_key(D, O, t, 1) < 0 || (D.x_try[t] & 16))) ? right : -1;
         case 3: return (D.x_try[t] & 2) ? right : -1;
         case 5: return (glob_class(D, O, t) == 0 && pk_key(D, O, t) < 0) ? D.o_qe[t] - D.o_qb[t] : -1;
         case 6: return glob_class(D, O, t) == 1 ? D.o_qe[t] - D.o_qb[t] : -1;
@@ -854,8 +938,10 @@ int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out,
     return (int)hipGetLastError();
 }
 
+int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *stream);
+
 // the four extension phases + the two finish passes (mem_chain2aln)
-int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *stream) {
+int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     int fgrid = (int)((D.n_task + 255) / 256);
     fgrid = fgrid < 8192 ? (fgrid > 0 ? fgrid : 1) : 8192;
@@ -863,6 +949,12 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, void *s
     if (e != hipSuccess) return (int)e;
     for (int side = 0; side < 2; ++side) {
         for (int tryi = 0; tryi < 2; ++tryi) {
+            if (tryi == 0 && O.pk && O.w <= 40) {
+                int rc = sw_launch_pk_order(D, O, 1 + side, stream);
+                if (rc) return rc;
+                hipLaunchKernelGGL(sw_ext_pk_kernel<40>, dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, side);
+                if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+            }
             int rc = sw_launch_order(D, O, side * 2 + tryi, D.list, stream);
             if (rc) return rc;
             const int wb = O.w << tryi;
@@ -883,7 +975,7 @@ int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
     hipStream_t s = (hipStream_t)stream;
     int rc;
     if (O.pk) {
-        if ((rc = sw_launch_pk_order(D, O, stream))) return rc;
+        if ((rc = sw_launch_pk_order(D, O, 0, stream))) return rc;
         if (ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
         hipLaunchKernelGGL(sw_global_pk_kernel<40>, dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O);
         if (ev_b) (void)hipEventRecord((hipEvent_t)ev_b, s);

@@ -57,6 +57,7 @@ SW_RING_FN uint32_t PU(pk_v v) { return __builtin_bit_cast(uint32_t, v); }
 SW_RING_FN uint32_t pk_add(uint32_t a, uint32_t b) { return PU(PV(a) + PV(b)); }
 SW_RING_FN uint32_t pk_sub(uint32_t a, uint32_t b) { return PU(PV(a) - PV(b)); }
 SW_RING_FN uint32_t pk_max(uint32_t a, uint32_t b) { return PU(__builtin_elementwise_max(PV(a), PV(b))); }
+SW_RING_FN uint32_t pk_min(uint32_t a, uint32_t b) { return PU(__builtin_elementwise_min(PV(a), PV(b))); }
 SW_RING_FN uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) { return PU(PV(a) * PV(b) + PV(c)); }
 SW_RING_FN uint32_t pk_shl(uint32_t a, int k) { return PU(PV(a) << pk_v{(short)k, (short)k}); }
 SW_RING_FN uint32_t pk_asr15(uint32_t a) { return PU(PV(a) >> pk_v{15, 15}); }
@@ -70,6 +71,9 @@ SW_RING_FN uint32_t pk_add(uint32_t a, uint32_t b) { return pk_mk(pk_lo(a) + pk_
 SW_RING_FN uint32_t pk_sub(uint32_t a, uint32_t b) { return pk_mk(pk_lo(a) - pk_lo(b), pk_hi(a) - pk_hi(b)); }
 SW_RING_FN uint32_t pk_max(uint32_t a, uint32_t b) {
     return pk_mk(pk_lo(a) > pk_lo(b) ? pk_lo(a) : pk_lo(b), pk_hi(a) > pk_hi(b) ? pk_hi(a) : pk_hi(b));
+}
+SW_RING_FN uint32_t pk_min(uint32_t a, uint32_t b) {
+    return pk_mk(pk_lo(a) < pk_lo(b) ? pk_lo(a) : pk_lo(b), pk_hi(a) < pk_hi(b) ? pk_hi(a) : pk_hi(b));
 }
 SW_RING_FN uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
     return pk_mk(pk_lo(a) * pk_lo(b) + pk_lo(c), pk_hi(a) * pk_hi(b) + pk_hi(c));
@@ -156,10 +160,14 @@ SW_RING_FN uint32_t bfi_b32(uint32_t mask, uint32_t v, uint32_t acc) {
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(v), "v"(acc));
     return r;
 }
+// (a plain expression: the compiler emits v_bfi_b32 / v_bitop3_b32 and, unlike for an
+// inline asm, knows its hazards)
 // keeps a wave-uniform conditional block a real branch (a volatile asm cannot be
 // speculated), so skipped chunks cost a scalar branch instead of per-slot selects
+SW_RING_FN uint32_t bfi_b32v(uint32_t mask, uint32_t v, uint32_t acc) { return (mask & v) | (~mask & acc); }
 #define PK_BRANCH_BARRIER() asm volatile("")
 #else
+SW_RING_FN uint32_t bfi_b32v(uint32_t mask, uint32_t v, uint32_t acc) { return (mask & v) | (~mask & acc); }
 SW_RING_FN uint32_t bfi_b32(uint32_t mask, uint32_t v, uint32_t acc) { return (mask & v) | (~mask & acc); }
 #define PK_BRANCH_BARRIER() ((void)0)
 #endif
@@ -283,6 +291,219 @@ SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int n
     }
     scA = hlA;
     scB = hlB;
+}
+
+
+// ---------------------------------------------------------------------------
+// ksw_extend2 for two tasks per lane in packed 16-bit arithmetic.
+//
+// Same slot scheme as glob_pk (slot s of row i = query column i - w + s; the
+// 64 lanes of a wave share qlen and w).  Left edge: negative columns and the
+// columns that the band pruning drops on the left hold zero words, which the
+// DP keeps at zero (no select, no effect on the row maximum); ksw_extend2's
+// first-column H(i,-1) = max(h0 - oe_del - e_del*i, 0) only ever enters as the
+// H part of column 0's word, written by a per-row fixup at the (wave-uniform)
+// slot of column 0 while i <= w.  Right edge, per
+// task: slot se = end - i + w.  Cells at s >= se are dead: the end word gets
+// E = 0 (eh[end] = {h1, 0}) and words above it are carried down unchanged
+// (ksw_extend2 reads such stale words when the pruned end grows again), with
+// the masks GE_s = [s >= se] (per half, from a sign) and GT_s = GE_{s-1}.
+// Row maximum and its last column: per 16-slot group the packed max of
+// h * 16 + (s & 15) (h <= 2047 for the routed tasks).  Pruned end: the last
+// word eh[j] != 0 is one past the last column with H > 0 (E(i+1,j) > 0 implies
+// H(i,j) > 0), tracked as a packed max of [h > 0] * (s + 1).
+// Tasks that meet an N are flagged for the exact kernel.
+struct PkExtHalf {
+    const uint8_t *T;   // first reference base of the side's window
+    int ts;             // +1 / -1: reference step
+    bool comp;          // reverse strand: complement the reference bases
+    int tlen;           // rows (0 = empty half)
+    int h0;             // start score
+};
+struct PkExtOut {
+    int score, qle, tle, gtle, gscore, max_off;
+};
+
+template <int WB>
+SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, int nrows, const SwOptsDev &O,
+                       const uint32_t *mA, const uint32_t *mB, int MS, PkExtOut out[2], int &nflag) {
+    constexpr int NS = 2 * WB + 2;
+    constexpr int CH = 8;
+    constexpr int NCH = (NS + CH - 1) / CH;
+    constexpr int NG = (NS + 15) / 16;
+    const int b = O.b, oe_del = O.o_del + O.e_del, oe_ins = O.o_ins + O.e_ins;
+    const uint32_t NAB = pk_dup(-(O.a + b)), BD = pk_dup(b);
+    const uint32_t cOD = pk_dup(oe_del), cED = pk_dup(O.e_del), cOI = pk_dup(oe_ins), cEI = pk_dup(O.e_ins);
+    const PkExtHalf *Hh[2] = {&A, &B};
+    uint32_t RH[NS], RE[NS];
+    {
+        int h1v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int h0 = Hh[h]->h0;
+            h1v[h] = h0 > oe_ins ? h0 - oe_ins : 0;
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            const int c = s - w - 1;
+            int hv[2] = {0, 0}, ev[2] = {0, 0};
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (c == 0) hv[h] = Hh[h]->h0;
+                else if (c > 0 && c <= qlen) {
+                    const int v = h1v[h] - O.e_ins * (c - 1);
+                    hv[h] = v > 0 ? v : 0;
+                }
+            }
+            RH[s] = (uint32_t)(uint16_t)hv[0] | ((uint32_t)(uint16_t)hv[1] << 16);
+            RE[s] = (uint32_t)(uint16_t)ev[0] | ((uint32_t)(uint16_t)ev[1] << 16);
+        }
+    }
+    int end[2] = {qlen, qlen}, mx[2], max_i[2] = {-1, -1}, max_j[2] = {-1, -1}, max_ie[2] = {-1, -1};
+    int gscore[2] = {-1, -1}, max_off[2] = {0, 0};
+    bool live[2];
+    int tc[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        mx[h] = Hh[h]->h0;
+        live[h] = Hh[h]->tlen > 0;
+        tc[h] = live[h] ? (int)Hh[h]->T[0] : 0;
+    }
+    for (int i = 0; i < nrows; ++i) {
+        int cb[2];
+        uint32_t sev = 0u, bnd = 0u;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            int c = tc[h];
+            if (i + 1 < Hh[h]->tlen) tc[h] = (int)Hh[h]->T[(long)Hh[h]->ts * (i + 1)];
+            if (Hh[h]->comp && c < 4) c = 3 - c;
+            if (live[h] && i >= Hh[h]->tlen) live[h] = false;
+            if (live[h] && c > 3) {
+                nflag |= 1 << h;
+                live[h] = false;
+            }
+            cb[h] = c & 3;
+            if (end[h] > i + w + 1) end[h] = i + w + 1;
+            if (end[h] > qlen) end[h] = qlen;
+            sev |= (uint32_t)(uint16_t)(end[h] - i + w - 1) << (16 * h);   // se - 1
+            int bd = Hh[h]->h0 - (O.o_del + O.e_del * (i + 1));
+            bnd |= (uint32_t)(uint16_t)(bd > 0 ? bd : 0) << (16 * h);
+        }
+        uint32_t wa[3], wb[3], G[6];
+        pk_window(mA, MS, i - w + 64, cb[0], wa);
+        pk_window(mB, MS, i - w + 64, cb[1], wb);
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            G[2 * g] = perm_b32(wb[g], wa[g], 0x05040100u);
+            G[2 * g + 1] = perm_b32(wb[g], wa[g], 0x07060302u);
+        }
+        // the column entering at the top slot still holds its row -1 word (H only)
+        uint32_t qin = 0u;
+        {
+            const int cin = i - w + NS;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                int v = 0;
+                if (cin == 0) v = Hh[h]->h0;
+                else if (cin > 0 && cin <= qlen) {
+                    const int h0 = Hh[h]->h0;
+                    v = (h0 > oe_ins ? h0 - oe_ins : 0) - O.e_ins * (cin - 1);
+                    v = v > 0 ? v : 0;
+                }
+                qin |= (uint32_t)(uint16_t)v << (16 * h);
+            }
+        }
+        uint32_t h1 = 0u, f = 0u, gt = 0u, lp = 0u;
+        uint32_t gm[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g) gm[g] = 0u;
+        const int stop = qlen - i + w;   // slot of column qlen (wave-uniform)
+        const int sbl = w - i;           // slot of column 0 (wave-uniform)
+        const int lo = w - i - 2;        // slot of column -2
+        uint32_t hl = 0u;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            if (c * CH > stop || (c + 1) * CH - 1 < lo) continue;   // dead chunk (wave-uniform)
+            PK_BRANCH_BARRIER();
+#pragma unroll
+            for (int s = c * CH; s < (c + 1) * CH && s < NS; ++s) {
+                const uint32_t Hd = s + 1 < NS ? RH[s + 1] : qin;
+                const uint32_t e0 = s + 1 < NS ? RE[s + 1] : 0u;
+                const uint32_t mm = pk_asr15(pk_shl(G[s >> 4], 15 - (s & 15)));
+                // M = H(i-1,j-1) ? H(i-1,j-1) + S : 0 (a negative M acts as 0 below)
+                const uint32_t M = pk_min(pk_shl(Hd, 4), pk_mad(mm, NAB, pk_sub(Hd, BD)));
+                const uint32_t h = pk_max(pk_max(M, e0), f);
+                const uint32_t en = pk_max(pk_sub(e0, cED), pk_max(pk_sub(M, cOD), 0u));
+                const uint32_t fn = pk_max(pk_sub(f, cEI), pk_max(pk_sub(M, cOI), 0u));
+                const uint32_t ge = perm_b32(0u, pk_sub(sev, pk_dup(s)), 0x09090808u);   // s >= se
+                RH[s] = bfi_b32v(gt, Hd, h1);
+                RE[s] = bfi_b32v(gt, e0, bfi_b32v(ge, 0u, en));
+                const uint32_t hm = bfi_b32v(ge, 0u, h);
+                gm[s >> 4] = pk_max(gm[s >> 4], pk_mad(hm, pk_dup(16), pk_dup(s & 15)));
+                lp = pk_max(lp, pk_mad(pk_min(hm, pk_dup(1)), pk_dup(s + 1), 0u));
+                h1 = h;
+                f = fn;
+                gt = ge;
+            }
+            if (c == (sbl >> 3) && sbl >= 0) {   // column 0's word: H(i,-1), the first-column score
+                PK_BRANCH_BARRIER();
+#pragma unroll
+                for (int s = c * CH; s < (c + 1) * CH && s < NS; ++s)
+                    if (s == sbl) RH[s] = bnd;
+            }
+            if (c == (stop >> 3)) {   // eh[qlen].h = H(i, qlen-1) when the band reaches the query end
+                PK_BRANCH_BARRIER();
+#pragma unroll
+                for (int s = c * CH; s < (c + 1) * CH && s < NS; ++s)
+                    if (s == stop) hl = RH[s];
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!live[h]) continue;
+            if (end[h] == qlen) {
+                const int v = (int)((hl >> (16 * h)) & 0xFFFFu);
+                max_ie[h] = gscore[h] > v ? max_ie[h] : i;
+                gscore[h] = gscore[h] > v ? gscore[h] : v;
+            }
+            int best = -1;
+#pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const int kv = (int)((gm[g] >> (16 * h)) & 0xFFFFu);
+                const int cand = ((kv >> 4) << 8) | (g * 16 + (kv & 15));
+                best = best > cand ? best : cand;
+            }
+            const int m = best >> 8;
+            if (m == 0) {
+                live[h] = false;
+                continue;
+            }
+            const int mj = i - w + (best & 255);
+            if (m > mx[h]) {
+                mx[h] = m, max_i[h] = i, max_j[h] = mj;
+                const int d = mj - i < 0 ? i - mj : mj - i;
+                max_off[h] = max_off[h] > d ? max_off[h] : d;
+            } else if (O.zdrop > 0) {
+                if (i - max_i[h] > mj - max_j[h]) {
+                    if (mx[h] - m - ((i - max_i[h]) - (mj - max_j[h])) * O.e_del > O.zdrop) { live[h] = false; continue; }
+                } else {
+                    if (mx[h] - m - ((mj - max_j[h]) - (i - max_i[h])) * O.e_ins > O.zdrop) { live[h] = false; continue; }
+                }
+            }
+            const int jl = i - w + (int)((lp >> (16 * h)) & 0xFFFFu);   // last column whose word is non-zero
+            end[h] = jl + 2 < qlen ? jl + 2 : qlen;
+        }
+        if (!SW_RING_ANY(live[0] || live[1])) break;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        out[h].score = mx[h];
+        out[h].qle = max_j[h] + 1;
+        out[h].tle = max_i[h] + 1;
+        out[h].gtle = max_ie[h] + 1;
+        out[h].gscore = gscore[h];
+        out[h].max_off = max_off[h];
+    }
 }
 
 // direction nibble (D1 | D2 << 1 | D3 << 2 | D4 << 3) of half hb at (row i, slot s)

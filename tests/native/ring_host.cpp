@@ -96,3 +96,27 @@ extern "C" int pk_global(int a, int b, int o_del, int e_del, int o_ins, int e_in
     delete[] z;
     return nflag | (qn << 2);
 }
+
+// ksw_extend2 for a lane pair in the packed kernel's arithmetic (sw_pk.h ext_pk):
+// two tasks with the same query length and band; out[12] = (score, qle, tle, gtle,
+// gscore, max_off) per half; returns the N flags.
+extern "C" int pk_extend(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int zdrop, int qlen, int w,
+                         const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb,
+                         const uint8_t *tb, int h0a, int h0b, int nrow_min, int *out) {
+    SwOptsDev O{};
+    O.a = a; O.b = b; O.o_del = o_del; O.e_del = e_del; O.o_ins = o_ins; O.e_ins = e_ins; O.zdrop = zdrop;
+    uint32_t m[2][2 * PK_NQW];
+    int nflag = 0;
+    if (pk_build_mask(qa, 0, 1, qlen, m[0], 1)) nflag |= 4;
+    if (pk_build_mask(qb, 0, 1, qlen, m[1], 1)) nflag |= 8;
+    PkExtHalf A{ta, 1, false, tla, h0a}, B{tb, 1, false, tlb, h0b};
+    int nrow = tla > tlb ? tla : tlb;
+    if (nrow < nrow_min) nrow = nrow_min;
+    PkExtOut o[2];
+    ext_pk<40>(A, B, qlen, w, nrow, O, m[0], m[1], 1, o, nflag);
+    for (int h = 0; h < 2; ++h) {
+        out[6 * h + 0] = o[h].score; out[6 * h + 1] = o[h].qle; out[6 * h + 2] = o[h].tle;
+        out[6 * h + 3] = o[h].gtle; out[6 * h + 4] = o[h].gscore; out[6 * h + 5] = o[h].max_off;
+    }
+    return nflag;
+}

@@ -145,3 +145,44 @@ def test_global_pk_flags_n(ring):
     fl = ring.pk_global(5, 11, 2, 4, 1, 3, 10, 5, _nt4(q), _nt4(t), 10, _nt4(t), 10, _nt4("ACGTANCGTA"),
                         sc, nc, cig, 128, 0)
     assert fl == (1 << 2) | 2
+
+
+def _band_w(lq, a, od, ed, oi, ei, eb, w):
+    """ksw_extend2's band cap (max_ins / max_del) for a query of length lq."""
+    mi = max(int((lq * a + eb - oi) / ei + 1.0), 1)
+    md = max(int((lq * a + eb - od) / ed + 1.0), 1)
+    return min(w, mi, md)
+
+
+@pytest.mark.parametrize("seed", [41, 42, 43])
+def test_extend_pk_matches_oracle(ring, seed):
+    """ksw_extend2 of the packed two-tasks-per-lane kernel (sw_pk.h ext_pk), host
+    emulation of its int16 arithmetic, vs oracle osw_extend: score, qle, tle, gtle,
+    gscore, max_off of both halves (shared query length and band, own sequences,
+    target lengths and start scores); z-drop on/off, both scoring sets."""
+    rng = random.Random(seed)
+    n = 0
+    for _ in range(250):
+        L = rng.choice([1, 2, 5, 10, 20, 40, 60, 75, 100, 150, 200])
+        qs = ["".join(rng.choice("ACGT") for _ in range(L)) for _ in range(2)]
+        ts = []
+        for q in qs:
+            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])).replace("N", "C") + \
+                "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 60)))
+            if rng.random() < 0.2:
+                t = "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 200)))
+            ts.append(t[:300])
+        h0s = [rng.choice([0, 5, 30, 100, 400, 750]) for _ in range(2)]
+        eb = rng.choice([30, 0, 5])
+        for a, b, od, ed, oi, ei, zd in SCORING[:2]:
+            w = _band_w(L, a, od, ed, oi, ei, eb, 40)
+            out = (C.c_int * 12)()
+            fl = ring.pk_extend(a, b, od, ed, oi, ei, zd, L, w, _nt4(qs[0]), _nt4(qs[1]), len(ts[0]), _nt4(ts[0] or "A"),
+                                len(ts[1]), _nt4(ts[1] or "A"), h0s[0], h0s[1], rng.choice([0, 300]), out)
+            assert fl == 0
+            for h in range(2):
+                sc, outs = ob.sw_extend(qs[h], ts[h], h0s[h], w=w, a=a, b=b, o_del=od, e_del=ed, o_ins=oi,
+                                        e_ins=ei, end_bonus=eb, zdrop=zd)
+                assert list(out[6 * h:6 * h + 6]) == [sc] + list(outs), (h, qs[h], ts[h], w, h0s[h], eb, (a, b, od, ed, oi, ei, zd))
+                n += 1
+    assert n == 1000
