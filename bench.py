@@ -133,6 +133,7 @@ def main():
         total_bases = lr_bases
     ms /= max(args.steps, 1)
     me, mg, ce, cg = sw.last_timing(ctx)
+    pc = sw.phase_cycles(ctx)
     a = it.download()
     cns_phases = it.cns_phase_ms()
     ok = int((a["status"] == 0).sum())
@@ -178,6 +179,8 @@ def main():
         "sw_gcups": round(cells / ((ms[0] + ms[1]) * 1e-3) / 1e9, 2),
         "stage_ms": {"sw_extend": round(ms[0], 3), "sw_global_cigar": round(ms[1], 3),
                      "handoff_sort": round(ms[2], 3), "consensus": round(ms[3], 3)},
+        "cigar_kernel_phase_share": {k: round(v / max(sum(pc), 1), 3) for k, v in
+                                     zip(("masks", "dp", "backtrack", "emit"), pc)},
         "consensus_phase_ms_summed_over_workgroups": {k: round(v, 1) for k, v in cns_phases.items()},
         "roofline": {
             "kernel": "sw_global_ring_kernel<40> (ksw_global2 CIGAR pass, DP row in registers, one task per lane)",

@@ -214,6 +214,9 @@ int pr_sw_last_cells(pr_ctx *ctx, int64_t *cells_extend, int64_t *cells_global);
  * launch's dominant kernel, the CIGAR pass register-ring launch (band <= 40), and the
  * DP cells it computed. */
 int pr_sw_dominant_kernel(pr_ctx *ctx, double *ms, int64_t *cells);
+/* Diagnostics: shader-clock cycles summed over waves of the packed CIGAR kernel's
+ * phases in the last launch: [0] query masks, [1] DP, [2] backtrack, [3] CIGAR emit. */
+int pr_sw_phase_cycles(pr_ctx *ctx, int64_t *out4);
 
 /* ------------------------------------------------------------------ */
 /* one correction iteration on the device: SW -> assemble -> consensus  */

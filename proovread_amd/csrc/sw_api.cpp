@@ -34,6 +34,10 @@ enum SwBuf {
     SB_CIG, SB_Z
 };
 static const int SB_CELLS = 24;
+// layout of the SB_CELLS buffer (zeroed per launch): [0,24) canonical DP cells, [24,56)
+// packed CIGAR kernel phase cycles, [64,68) the LDS CIGAR kernel's dequeue counter
+static const size_t CELLS_BYTES = 128;
+static const size_t CELLS_WORK_OFF = 64;
 static const int SB_PERM = 25;
 static const int SB_BUCKET = 26;
 static const int SB_X = 27;
@@ -125,7 +129,7 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
         (rc = ensure(r, SB_LIST, (size_t)(nt + 1 + (int64_t)PK_NB * PK_SEG) * 4)))
         return rc;
     if ((rc = ensure(r, SB_PASS, (size_t)nt + 1)) || (rc = ensure(r, SB_CIG, (size_t)(nt + 1) * SW_MAXCIG * 4)) ||
-        (rc = ensure(r, SB_CELLS, 64)))
+        (rc = ensure(r, SB_CELLS, CELLS_BYTES)))
         return rc;
     HIPCHK(hipStreamSynchronize(s));
     r.loaded = true;
@@ -184,7 +188,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.o_status = (int32_t *)r.buf[SB_STATUS];
     D.o_cig = (uint32_t *)r.buf[SB_CIG];
     D.cells = (unsigned long long *)r.buf[SB_CELLS];
-    D.work = (int32_t *)((char *)r.buf[SB_CELLS] + 32);
+    D.work = (int32_t *)((char *)r.buf[SB_CELLS] + CELLS_WORK_OFF);
     D.perm = (int32_t *)r.buf[SB_PERM];
     D.bucket = (int32_t *)r.buf[SB_BUCKET];
     D.x = (int32_t *)r.buf[SB_X];
@@ -210,7 +214,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     int rc;
     if ((rc = ensure(r, SB_Z, zb))) return rc;
     D.z = (uint8_t *)r.buf[SB_Z];
-    HIPCHK(hipMemsetAsync(r.buf[SB_CELLS], 0, 64, s));
+    HIPCHK(hipMemsetAsync(r.buf[SB_CELLS], 0, CELLS_BYTES, s));
     if (r.n_task == 0) return 0;
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
     int e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s);
@@ -320,5 +324,18 @@ int sw_get_ptrs(pr_ctx *c, SwPtrs *p) {
     p->n_task = r.n_task;
     p->n_sr = (int)r.n_sr;
     p->n_lr = (int)r.n_lr;
+    return 0;
+}
+
+extern "C" int pr_sw_phase_cycles(pr_ctx *c, int64_t *out4) {
+    // wave-cycle totals of the packed CIGAR kernel's phases (masks, DP, backtrack, emit)
+    if (!c || !out4) return pr_set_error(PR_ERR_ARG, "null arg");
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    HIPCHK(hipStreamSynchronize(ctx_stream(c)));
+    unsigned long long v[7];
+    HIPCHK(hipMemcpy(v, r.buf[SB_CELLS], sizeof v, hipMemcpyDeviceToHost));
+    for (int q = 0; q < 4; ++q) out4[q] = (int64_t)v[3 + q];
     return 0;
 }

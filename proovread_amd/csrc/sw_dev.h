@@ -39,7 +39,7 @@ struct SwDev {
     int64_t z_slab;            // bytes per slab (LDS kernel)
     int64_t z_ring_slab;       // dwords per slab (register-ring kernels: rows x words x 64 lanes)
     int64_t z_pk_slab;         // PkDir entries per slab (packed kernel: rows x chunks x 64 lanes)
-    unsigned long long *cells; // [3] canonical DP cells (extension, global, global ring<40> launch)
+    unsigned long long *cells; // [3] canonical DP cells (extension, global, dominant launch), [3..6] pk phase cycles
     int32_t *perm;             // lane -> task order (tasks bucketed by extension lengths)
     int32_t *bucket;           // [SW_NBUCKET + 1] counting-sort scratch
     int32_t *work;             // dequeue counter for the global kernel

@@ -683,23 +683,23 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
 
 template <int WB>
 __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOptsDev O) {
-    // query masks during the DP ([half][bit][word][lane]), backtrack windows after it
-    __shared__ __attribute__((aligned(16))) uint32_t lsh[2 * 8 * SW_WAVE * 4];
-    static_assert(2 * 2 * PK_NQW <= 2 * 8 * 4, "mask words fit the backtrack window area");
+    // query masks ([half][bit][word][lane])
+    __shared__ __attribute__((aligned(16))) uint32_t lsh[2 * 2 * PK_NQW * SW_WAVE];
     const int lane = threadIdx.x;
     uint32_t *lm = lsh;
-    PkDir *lw = reinterpret_cast<PkDir *>(lsh) + lane;
     PkDir *zl = reinterpret_cast<PkDir *>(D.z) + (int64_t)blockIdx.x * D.z_pk_slab + lane;
     unsigned long long cells = 0;
     const int nseg = D.pk_bucket[PK_SCAN] / PK_SEG;
+    unsigned long long ph[4] = {0, 0, 0, 0};   // wave cycles: masks, DP, backtrack, emit
     for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+        unsigned long long c0 = clock64();
         const int64_t tt[2] = {D.list[(int64_t)seg * PK_SEG + lane], D.list[(int64_t)seg * PK_SEG + 64 + lane]};
         // the segment's key (its first task is never padding)
         const int key = __builtin_amdgcn_readfirstlane(pk_key(D, O, D.list[(int64_t)seg * PK_SEG]));
         const int ww = key >> 8, lqq = key & 255;
         PkHalf H[2];
         int nrow = 0, qn = 0;
-        __syncthreads();   // the previous segment's backtrack windows are done with the LDS
+        __syncthreads();   // the previous segment is done with the masks
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int64_t t = tt[h];
@@ -727,10 +727,12 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
         nrow = __builtin_amdgcn_readfirstlane(nrow);
         const int npair = pk_npair(ww);
         int sc[2] = {0, 0}, nflag = 0;
+        unsigned long long c1 = clock64();
+        ph[0] += c1 - c0;
         glob_pk<WB>(H[0], H[1], lqq, ww, nrow, O, lm + lane, lm + 2 * PK_NQW * SW_WAVE + lane, SW_WAVE, zl,
                     SW_WAVE, sc[0], sc[1], nflag);
         nflag |= qn;
-        __syncthreads();   // masks dead: the LDS becomes the backtrack windows
+        // (the masks are dead from here on)
         uint32_t *cg[2] = {nullptr, nullptr};
         int tl[2] = {0, 0};
 #pragma unroll
@@ -747,32 +749,59 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
             tl[h] = rlen;
         }
         int nc[2] = {0, 0};
+        uint32_t fst[2] = {0u, 0u}, lst[2] = {0u, 0u};
+        unsigned long long c2 = clock64();
+        ph[1] += c2 - c1;
         if (O.debug & 1) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                if (cg[h]) cg[h][0] = ((uint32_t)lqq << 4), nc[h] = 1;
+                if (cg[h]) cg[h][SW_MAXCIG - 1] = fst[h] = lst[h] = ((uint32_t)lqq << 4), nc[h] = 1;
         } else {
-            pk_backtrack2(zl, SW_WAVE, npair, tl, lqq, ww, cg, nc, lw, SW_WAVE, SW_MAXCIG);
+            pk_backtrack2(zl, SW_WAVE, npair, nrow, tl, lqq, ww, cg, nc, fst, lst, SW_MAXCIG);
         }
+        unsigned long long c3 = clock64();
+        ph[2] += c3 - c2;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (!cg[h]) continue;
             const int64_t t = tt[h];
-            int status = 0, m = nc[h];
-            if (m < 0) { status = -9; m = 0; }
-            if (!(O.debug & 1))
-                for (int x = 0; x < m >> 1; ++x) {
-                    const uint32_t tmp = cg[h][x];
-                    cg[h][x] = cg[h][m - 1 - x];
-                    cg[h][m - 1 - x] = tmp;
-                }
             const int sid = D.t_sr[t], lid = D.t_lr[t];
             const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
             const int L = (int)(D.lr_off[lid + 1] - D.lr_off[lid]);
+            const int qb = D.o_qb[t], qe = D.o_qe[t], rb = D.o_rb[t], re = D.o_re[t];
+            const bool rev = H[h].comp;
+            // mem_reg2aln after ksw_global2 (glob_emit's rules) on the forward-ordered ops at the slots' end
+            int status = 0, m = nc[h], src = SW_MAXCIG - nc[h];
+            int pos = rev ? L - re : rb;
+            if (m < 0) { status = -9; m = 0; src = SW_MAXCIG; }
+            if (m > 0) {
+                if ((fst[h] & 0xFu) == 2u) {
+                    pos += (int)(fst[h] >> 4);
+                    ++src, --m;
+                } else if ((lst[h] & 0xFu) == 2u) {
+                    --m;
+                }
+            }
+            int clip5 = 0, clip3 = 0;
+            if (qb != 0 || qe != lq) {
+                clip5 = rev ? lq - qe : qb;
+                clip3 = rev ? qb : lq - qe;
+                if (m + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > SW_MAXCIG) status = -9, clip5 = clip3 = 0;
+            }
+            const int d0 = clip5 ? 1 : 0;
+            pk_cig_move(cg[h], d0, src, m);
+            if (clip5) cg[h][0] = ((uint32_t)clip5 << 4) | 4u;
+            if (clip3) cg[h][d0 + m] = ((uint32_t)clip3 << 4) | 4u;
             cells += band_cells(tl[h], lqq, ww);
-            glob_emit(D, t, cg[h], m, status, sc[h], H[h].comp, lq, L, D.o_qb[t], D.o_qe[t], D.o_rb[t], D.o_re[t]);
+            D.o_gscore[t] = sc[h];
+            D.o_pos[t] = pos;
+            D.o_ncig[t] = d0 + m + (clip3 ? 1 : 0);
+            D.o_status[t] = status;
         }
+        ph[3] += clock64() - c3;
     }
+    if (lane == 0)
+        for (int q = 0; q < 4; ++q) atomicAdd(&D.cells[3 + q], ph[q]);
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
     if (lane == 0 && cells) {
         atomicAdd(&D.cells[1], cells);

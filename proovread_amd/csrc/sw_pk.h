@@ -99,6 +99,13 @@ SW_RING_FN uint32_t align_b32(uint32_t hi, uint32_t lo, uint32_t sh) {
 }
 #endif
 SW_RING_FN uint32_t pk_dup(int v) { return (uint32_t)(uint16_t)v * 0x10001u; }
+#ifdef SW_RING_HOST
+// host test builds: every direction-word read is checked against the slab the test allocated
+extern long pk_host_zlen;
+#define PK_ZCHECK(idx) do { if ((idx) < 0 || (idx) >= pk_host_zlen) __builtin_trap(); } while (0)
+#else
+#define PK_ZCHECK(idx) ((void)0)
+#endif
 
 // One half (task) of a lane pair as glob_pk sees it.
 struct PkHalf {
@@ -547,16 +554,29 @@ SW_RING_FN int glob_pk_backtrack(const PkDir *z, int ZS, int npair, int hb, int 
     return n;
 }
 
-// Backtrack of both halves of a lane (glob_pk_backtrack's walk, ops pushed in
-// reverse order; the kernel's version: glob_pk_backtrack is the plain reference).  The walk mostly keeps its slot (diagonal moves), so it reads
-// a window of 8 rows x one 16-slot pair: the 8 loads of a window are issued
-// together and staged in LDS (lw: [half][row][lane]); a half reloads only when
-// it leaves its window.  Both halves advance in the same loop.  The current op
-// run stays in registers.  n[h] = op count or -1 (more than maxcig).
-SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, const int tl[2], int qlen, int w,
-                              uint32_t *const cg[2], int n[2], PkDir *lw, int LS, int maxcig) {
-    int i[2], k[2], which[2] = {0, 0}, rop[2] = {-1, -1}, rln[2] = {0, 0}, wr[2] = {-1, -1}, wp[2] = {-1, -1};
+// Backtrack of both halves of a lane (glob_pk_backtrack's walk; the plain
+// version above is its reference), in row lockstep across the wave: every
+// walk leaves a row only by an M or D step, so all lanes can sweep the rows
+// together from the wave's last row down.  Windows of 16 rows are loaded at
+// each half's current 16-slot pair (the walks hug the band centre, so the 64
+// lanes mostly read the same pair: the loads are coalesced rows of the
+// [row][pair][lane] slab), the half's direction bytes are picked out with
+// v_perm_b32 into registers (wave-uniform row index: static register
+// indexing); a step whose slot left the loaded pair reads its word directly.
+// The current op run stays in registers and every finished run is stored once,
+// from the END of the task's CIGAR slots backwards: the ops land in final
+// (forward) order at cg[maxcig - n, maxcig).  n[h] = op count or -1 (more than
+// maxcig); first[h] / last[h] = the first / last op of the forward CIGAR.
+SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, const int tl[2], int qlen, int w,
+                              uint32_t *const cg[2], int n[2], uint32_t first[2], uint32_t last[2], int maxcig) {
+    int i[2], k[2], which[2] = {0, 0}, rop[2] = {-1, -1}, rln[2] = {0, 0};
     bool live[2];
+    auto flush = [&](int h) {
+        const uint32_t v = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
+        if (n[h] == 0) last[h] = v;
+        first[h] = v;
+        cg[h][maxcig - 1 - n[h]++] = v;
+    };
     // ksw's push with the last op kept in registers: false when the op count would exceed maxcig
     auto push = [&](int h, int op, int len) -> bool {
         if (op == rop[h]) {
@@ -565,58 +585,74 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, const int tl[2
         }
         if (rop[h] >= 0) {
             if (n[h] + 1 >= maxcig) return false;
-            cg[h][n[h]++] = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
+            flush(h);
         }
         rop[h] = op;
         rln[h] = len;
         return true;
+    };
+    // the half's direction bytes of a (row, pair) word: x = D1|D2 of both chunks, y = D3|D4
+    auto pick = [&](const PkDir &v, int h, uint32_t &x, uint32_t &y) {
+        const uint32_t sel = h ? 0x07050301u : 0x06040200u;
+        x = perm_b32(v.x1, v.x0, sel);
+        y = perm_b32(v.y1, v.y0, sel);
     };
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         i[h] = tl[h] - 1;
         k[h] = (i[h] + w + 1 < qlen ? i[h] + w + 1 : qlen) - 1;
         n[h] = 0;
+        first[h] = last[h] = 0u;
         live[h] = cg[h] != nullptr && i[h] >= 0 && k[h] >= 0;
     }
-    while (live[0] || live[1]) {
-        PkDir buf[2][8];
-        bool need[2];
+    for (int R = nrows - 1; R >= 0 && SW_RING_ANY(live[0] || live[1]); R -= 16) {
+        uint32_t bx[2][16], by[2][16];
+        int p[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            const int sp = (k[h] - i[h] + w) >> 4;
-            need[h] = live[h] && !(i[h] <= wr[h] && i[h] > wr[h] - 8 && sp == wp[h]);
-            if (need[h]) {
+            p[h] = (k[h] - i[h] + w) >> 4;
+            PkDir v[16];
 #pragma unroll
-                for (int d = 0; d < 8; ++d) {
-                    const int r = i[h] - d;
-                    buf[h][d] = r >= 0 ? zl[((long)r * npair + sp) * ZS] : PkDir{0u, 0u, 0u, 0u};
+            for (int d = 0; d < 16; ++d) {
+                v[d] = PkDir{0u, 0u, 0u, 0u};
+                if (live[h] && R - d >= 0 && R - d <= i[h]) {
+                    const long ix = ((long)(R - d) * npair + p[h]) * ZS;
+                    PK_ZCHECK(ix);
+                    v[d] = zl[ix];
                 }
             }
+#pragma unroll
+            for (int d = 0; d < 16; ++d) pick(v[d], h, bx[h][d], by[h][d]);
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (need[h]) {
+        for (int d = 0; d < 16; ++d) {
+            const int r = R - d;
 #pragma unroll
-                for (int d = 0; d < 8; ++d) lw[(h * 8 + d) * LS] = buf[h][d];
-                wr[h] = i[h];
-                wp[h] = (k[h] - i[h] + w) >> 4;
+            for (int h = 0; h < 2; ++h) {
+                while (live[h] && i[h] == r) {
+                    const int sl = k[h] - r + w;
+                    uint32_t X = bx[h][d], Y = by[h][d];
+                    if ((sl >> 4) != p[h]) {
+                        const long ix = ((long)r * npair + (sl >> 4)) * ZS;
+                        PK_ZCHECK(ix);
+                        pick(zl[ix], h, X, Y);
+                    }
+                    const int bt = ((sl >> 3) & 1) * 16 + (sl & 7);
+                    const int nib = (int)(((X >> bt) & 1u) | (((X >> (bt + 8)) & 1u) << 1) |
+                                          (((Y >> bt) & 1u) << 2) | (((Y >> (bt + 8)) & 1u) << 3));
+                    which[h] = pk_which(which[h], nib);
+                    const int op = which[h] == 0 ? 0 : (which[h] == 1 ? 2 : 1);
+                    if (!push(h, op, 1)) {
+                        n[h] = -1;
+                        live[h] = false;
+                        break;
+                    }
+                    if (which[h] == 0) --i[h], --k[h];
+                    else if (which[h] == 1) --i[h];
+                    else --k[h];
+                    live[h] = i[h] >= 0 && k[h] >= 0;
+                }
             }
-        }
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!live[h]) continue;
-            const int sl = k[h] - i[h] + w;
-            which[h] = pk_which(which[h], pk_nib(lw[(h * 8 + (wr[h] - i[h])) * LS], sl, h));
-            const int op = which[h] == 0 ? 0 : (which[h] == 1 ? 2 : 1);
-            if (!push(h, op, 1)) {
-                n[h] = -1;
-                live[h] = false;
-                continue;
-            }
-            if (which[h] == 0) --i[h], --k[h];
-            else if (which[h] == 1) --i[h];
-            else --k[h];
-            live[h] = i[h] >= 0 && k[h] >= 0;
         }
     }
     // leading D / I remainders (ksw's pushes after the walk), then the last run
@@ -627,7 +663,19 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, const int tl[2
         if (i[h] >= 0) ok = push(h, 2, i[h] + 1);
         if (ok && k[h] >= 0) ok = push(h, 1, k[h] + 1);
         if (!ok) n[h] = -1;
-        else if (rop[h] >= 0) cg[h][n[h]++] = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
+        else if (rop[h] >= 0) flush(h);
+    }
+}
+
+// Forward copy of n ops from cg[src] to cg[dst] (dst <= src), 8 independent loads at a time.
+SW_RING_FN void pk_cig_move(uint32_t *cg, int dst, int src, int n) {
+    for (int x = 0; x < n; x += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int y = 0; y < 8; ++y) v[y] = x + y < n ? cg[src + x + y] : 0u;
+#pragma unroll
+        for (int y = 0; y < 8; ++y)
+            if (x + y < n) cg[dst + x + y] = v[y];
     }
 }
 

@@ -55,6 +55,7 @@ def _setup(L):
     L.pr_sw_last_timing.argtypes = [C.c_void_p, _abi.PD, _abi.PD]
     L.pr_sw_last_cells.argtypes = [C.c_void_p, _abi.P64, _abi.P64]
     L.pr_sw_dominant_kernel.argtypes = [C.c_void_p, _abi.PD, _abi.P64]
+    L.pr_sw_phase_cycles.argtypes = [C.c_void_p, _abi.P64]
     L._sw_ready = True
 
 
@@ -150,3 +151,12 @@ def dominant_kernel(ctx: _abi.Context):
     ms, cells = C.c_double(), C.c_int64()
     _abi.check(L.pr_sw_dominant_kernel(ctx.h, C.byref(ms), C.byref(cells)), "pr_sw_dominant_kernel")
     return ms.value, cells.value
+
+
+def phase_cycles(ctx: _abi.Context):
+    """Wave-cycle totals of the packed CIGAR kernel's phases (masks, DP, backtrack, emit)."""
+    L = _abi.lib()
+    _setup(L)
+    out = (C.c_int64 * 4)()
+    _abi.check(L.pr_sw_phase_cycles(ctx.h, out), "pr_sw_phase_cycles")
+    return list(out)

@@ -57,6 +57,7 @@ extern "C" int ring_global(int wb, int a, int b, int o_del, int e_del, int o_ins
 #include <algorithm>
 #include <vector>
 #include "../../proovread_amd/csrc/sw_pk.h"
+namespace prgpu { long pk_host_zlen = 0; }
 extern "C" int pk_global(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int qlen, int w,
                          const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb, const uint8_t *tb,
                          int *sc, int *ncig, uint32_t *cig, int max_cigar, int nrow_min) {
@@ -71,14 +72,21 @@ extern "C" int pk_global(int a, int b, int o_del, int e_del, int o_ins, int e_in
     if (nrow < nrow_min) nrow = nrow_min;   // other lanes of the wave may run longer
     const int npair = pk_npair(w);
     PkDir *z = new PkDir[(size_t)(nrow + 1) * npair + 1]();
+    pk_host_zlen = (long)nrow * npair;   // rows [0, nrow) x pairs
     int s2[2] = {0, 0}, nflag = 0;
     glob_pk<40>(A, B, qlen, w, nrow, O, m[0], m[1], 1, z, 1, s2[0], s2[1], nflag);
     // the kernel's windowed two-half backtrack, checked against the plain one
-    PkDir lw[16];
     const int tl2[2] = {A.tlen, B.tlen};
     uint32_t *cg2[2] = {A.tlen > 0 ? cig : nullptr, B.tlen > 0 ? cig + max_cigar : nullptr};
     int n2[2] = {0, 0};
-    pk_backtrack2(z, 1, npair, tl2, qlen, w, cg2, n2, lw, 1, max_cigar);
+    uint32_t fst[2], lst[2];
+    pk_backtrack2(z, 1, npair, nrow, tl2, qlen, w, cg2, n2, fst, lst, max_cigar);
+    for (int h = 0; h < 2; ++h)   // forward order at the slots' end -> reverse order at the start (plain walk's)
+        if (cg2[h] && n2[h] > 0) {
+            if (fst[h] != cg2[h][max_cigar - n2[h]] || lst[h] != cg2[h][max_cigar - 1]) { delete[] z; return -2000 - h; }
+            pk_cig_move(cg2[h], 0, max_cigar - n2[h], n2[h]);
+            std::reverse(cg2[h], cg2[h] + n2[h]);
+        }
     for (int h = 0; h < 2; ++h) {
         const int tl = h ? B.tlen : A.tlen;
         uint32_t *cg = cig + (size_t)h * max_cigar;
