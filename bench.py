@@ -153,7 +153,7 @@ def main():
     traffic = None
     if prof.exists():
         try:
-            traffic = json.loads(prof.read_text()).get("sw_global_ring_kernel<40>", {}).get("hbm_bytes_per_launch")
+            traffic = json.loads(prof.read_text()).get("sw_global_pk_kernel<40>", {}).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     out = {
@@ -183,7 +183,7 @@ def main():
                                      zip(("masks", "dp", "backtrack", "emit"), pc)},
         "consensus_phase_ms_summed_over_workgroups": {k: round(v, 1) for k, v in cns_phases.items()},
         "roofline": {
-            "kernel": "sw_global_ring_kernel<40> (ksw_global2 CIGAR pass, DP row in registers, one task per lane)",
+            "kernel": "sw_global_pk_kernel<40> (ksw_global2 CIGAR pass + backtrack, packed int16, two tasks per lane)",
             "bound": "valu",
             "achieved": round(dom_tops, 3),
             "peak": round(VALU_PEAK_TOPS, 2),
@@ -193,6 +193,8 @@ def main():
             "launch_ms": round(dom_ms, 3),
             "cells_per_launch": int(dom_cells),
             "ops_per_cell": OPS_PER_CELL,
+            "peak_packed_int16": round(2 * VALU_PEAK_TOPS, 2),
+            "frac_of_packed_int16_peak": round(dom_tops / (2 * VALU_PEAK_TOPS), 4),
         },
         "roofline_consensus": {
             "kernel": "cns_lr_kernel (bin cap + pileup + argmax, one long read per workgroup)", "bound": "hbm",

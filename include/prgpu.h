@@ -211,8 +211,8 @@ int pr_sw_last_timing(pr_ctx *ctx, double *ms_extend, double *ms_global);
 /* canonical DP cells of the last launch (unpruned band, final width) */
 int pr_sw_last_cells(pr_ctx *ctx, int64_t *cells_extend, int64_t *cells_global);
 /* Diagnostics for the roofline: duration (HIP events on the SW stream) of the last
- * launch's dominant kernel, the CIGAR pass register-ring launch (band <= 40), and the
- * DP cells it computed. */
+ * launch's dominant kernel, the CIGAR pass's packed launch (the band <= 40 ring launch
+ * when the packed kernel is off), and the DP cells it computed. */
 int pr_sw_dominant_kernel(pr_ctx *ctx, double *ms, int64_t *cells);
 /* Diagnostics: shader-clock cycles summed over waves of the packed CIGAR kernel's
  * phases in the last launch: [0] query masks, [1] DP, [2] backtrack, [3] CIGAR emit. */

@@ -145,7 +145,7 @@ def last_timing(ctx: _abi.Context):
 
 
 def dominant_kernel(ctx: _abi.Context):
-    """(ms, cells) of the last launch's CIGAR-pass register-ring kernel (band <= 40)."""
+    """(ms, cells) of the last launch's dominant kernel: the CIGAR pass's packed launch."""
     L = _abi.lib()
     _setup(L)
     ms, cells = C.c_double(), C.c_int64()
