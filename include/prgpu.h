@@ -219,6 +219,50 @@ int pr_sw_dominant_kernel(pr_ctx *ctx, double *ms, int64_t *cells);
 int pr_sw_phase_cycles(pr_ctx *ctx, int64_t *out4);
 
 /* ------------------------------------------------------------------ */
+/* host seeding front end: `bwa-proovread index` + the seeding / chaining part
+ * of `bwa-proovread mem` (bin/proovread:1270, 1313), producing the pr_sw_batch
+ * task list.  Restates upstream bwa's mem_collect_intv (SMEMs, re-seeding, the
+ * -y third round), mem_chain / test_and_merge, mem_chain_flt and the seed choice
+ * of mem_chain2aln over an exact 12-mer index of the long reads (both strands).
+ * Parity with the absent bwa-proovread is unpinned.              */
+typedef struct pr_seed_opts {
+    int min_seed_len;        /* -k (>= 12)                                    */
+    int min_chain_weight;    /* -W                                            */
+    int w;                   /* -w: chaining diagonal tolerance, window gaps  */
+    double split_factor;     /* -r                                            */
+    int split_width;         /* bwa default 10                                */
+    int max_mem_intv;        /* -y                                            */
+    int max_occ;             /* -c (bwa default 500)                          */
+    double drop_ratio;       /* -D                                            */
+    int max_chain_gap;       /* bwa default 10000                             */
+    double mask_level;       /* bwa default 0.5                               */
+    int a, o_del, e_del, o_ins, e_ins;   /* scoring, for the chain window (cal_max_gap) */
+} pr_seed_opts;
+typedef struct pr_seed_task {
+    int32_t sr, lr;          /* short read, long read                         */
+    int32_t strand;          /* 1: the read aligns to the long read's reverse complement */
+    int32_t qbeg, rbeg, slen;/* seed: read offset, long-read offset in strand coordinates, length */
+    int32_t rmax0, rmax1;    /* the chain's reference window (strand coordinates) */
+    int32_t weight, nseed;   /* chain weight and seed count                   */
+} pr_seed_task;
+typedef struct pr_seed_tasks {
+    int64_t n;
+    pr_seed_task *t;         /* library-owned; pr_seed_tasks_free              */
+} pr_seed_tasks;
+typedef struct pr_seed_index pr_seed_index;
+void pr_seed_opts_default(pr_seed_opts *o, int finish);   /* bwa-sr / bwa-sr-finish (proovread.cfg:318-333) */
+int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off, int n_lr, pr_seed_index **out);
+void pr_seed_index_free(pr_seed_index *h);
+/* seeds of every read, in read order and chain order (n_threads <= 0: all cores) */
+int pr_seed_map(const pr_seed_index *h, const pr_seed_opts *o, const uint8_t *sr_seq, const int64_t *sr_off,
+                int n_sr, int n_threads, pr_seed_tasks *out);
+void pr_seed_tasks_free(pr_seed_tasks *t);
+/* diagnostics (tests): occurrences of a string (both strands), and bwt_smem1a's SMEMs at x */
+int pr_seed_index_occ(const pr_seed_index *h, const uint8_t *s, int n, int64_t *count);
+int pr_seed_smem(const pr_seed_index *h, const uint8_t *q, int len, int x, int64_t min_intv, int32_t *start,
+                 int32_t *end, int64_t *occ, int cap, int *n_out);
+
+/* ------------------------------------------------------------------ */
 /* one correction iteration on the device: SW -> assemble -> consensus  */
 /* (bin/proovread:835-869 for one task: run_bwa, create_sorted_bam and
  * correct_sr_mt without the SAM/BAM round trip; the hand-off sorts the

@@ -1,0 +1,118 @@
+"""Host seeding front end (C-ABI pr_seed_*): `bwa-proovread index` + the seeding and
+chaining part of `bwa-proovread mem` (bin/proovread:1270, 1313), which produce the
+seed-extension task list of the SW stage.  See include/prgpu.h and DESIGN.md
+(parity with bwa-proovread unpinned)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+
+
+class SeedOpts(C.Structure):
+    _fields_ = [("min_seed_len", C.c_int), ("min_chain_weight", C.c_int), ("w", C.c_int),
+                ("split_factor", C.c_double), ("split_width", C.c_int), ("max_mem_intv", C.c_int),
+                ("max_occ", C.c_int), ("drop_ratio", C.c_double), ("max_chain_gap", C.c_int),
+                ("mask_level", C.c_double), ("a", C.c_int), ("o_del", C.c_int), ("e_del", C.c_int),
+                ("o_ins", C.c_int), ("e_ins", C.c_int)]
+
+
+class SeedTask(C.Structure):
+    _fields_ = [(k, C.c_int32) for k in ("sr", "lr", "strand", "qbeg", "rbeg", "slen", "rmax0", "rmax1",
+                                          "weight", "nseed")]
+
+
+class SeedTasks(C.Structure):
+    _fields_ = [("n", C.c_int64), ("t", C.POINTER(SeedTask))]
+
+
+TASK_DTYPE = np.dtype([(k, np.int32) for k, _ in SeedTask._fields_])
+_done = False
+
+
+def _setup(L):
+    global _done
+    if _done:
+        return
+    L.pr_seed_opts_default.argtypes = [C.POINTER(SeedOpts), C.c_int]
+    L.pr_seed_opts_default.restype = None
+    L.pr_seed_index_build.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+    L.pr_seed_index_free.argtypes = [C.c_void_p]
+    L.pr_seed_index_free.restype = None
+    L.pr_seed_map.argtypes = [C.c_void_p, C.POINTER(SeedOpts), C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                              C.POINTER(SeedTasks)]
+    L.pr_seed_tasks_free.argtypes = [C.POINTER(SeedTasks)]
+    L.pr_seed_tasks_free.restype = None
+    L.pr_seed_index_occ.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int64)]
+    L.pr_seed_smem.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
+                               C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    _done = True
+
+
+def default_opts(finish: bool = False) -> SeedOpts:
+    L = _abi.lib()
+    _setup(L)
+    o = SeedOpts()
+    L.pr_seed_opts_default(C.byref(o), 1 if finish else 0)
+    return o
+
+
+class SeedIndex:
+    """Index of a long-read shard (nt4 pool + offsets), both strands."""
+
+    def __init__(self, lr_seq: np.ndarray, lr_off: np.ndarray):
+        self.L = _abi.lib()
+        _setup(self.L)
+        self._seq = np.ascontiguousarray(lr_seq, np.uint8)
+        self._off = np.ascontiguousarray(lr_off, np.int64)
+        h = C.c_void_p()
+        _abi.check(self.L.pr_seed_index_build(self._seq.ctypes.data, self._off.ctypes.data, len(self._off) - 1,
+                                              C.byref(h)), "pr_seed_index_build")
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.L.pr_seed_index_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def occ(self, s: np.ndarray) -> int:
+        s = np.ascontiguousarray(s, np.uint8)
+        n = C.c_int64()
+        _abi.check(self.L.pr_seed_index_occ(self.h, s.ctypes.data, len(s), C.byref(n)), "pr_seed_index_occ")
+        return n.value
+
+    def smem(self, q: np.ndarray, x: int, min_intv: int = 1):
+        q = np.ascontiguousarray(q, np.uint8)
+        cap = len(q) + 1
+        st, en, oc = np.zeros(cap, np.int32), np.zeros(cap, np.int32), np.zeros(cap, np.int64)
+        n = C.c_int()
+        ret = self.L.pr_seed_smem(self.h, q.ctypes.data, len(q), x, min_intv, st.ctypes.data, en.ctypes.data,
+                                  oc.ctypes.data, cap, C.byref(n))
+        if ret < 0:
+            _abi.check(ret, "pr_seed_smem")
+        return [(int(st[i]), int(en[i]), int(oc[i])) for i in range(n.value)], ret
+
+    def map(self, sr_seq: np.ndarray, sr_off: np.ndarray, opts: SeedOpts | None = None, threads: int = 0):
+        """Seed-extension tasks (structured array, TASK_DTYPE) in read order, chain order."""
+        opts = opts or default_opts()
+        sr_seq = np.ascontiguousarray(sr_seq, np.uint8)
+        sr_off = np.ascontiguousarray(sr_off, np.int64)
+        out = SeedTasks()
+        _abi.check(self.L.pr_seed_map(self.h, C.byref(opts), sr_seq.ctypes.data, sr_off.ctypes.data,
+                                      len(sr_off) - 1, threads, C.byref(out)), "pr_seed_map")
+        try:
+            n = int(out.n)
+            if n == 0:
+                return np.zeros(0, TASK_DTYPE)
+            buf = C.cast(out.t, C.POINTER(C.c_int32 * (10 * n))).contents
+            return np.frombuffer(bytes(buf), dtype=TASK_DTYPE).copy()
+        finally:
+            self.L.pr_seed_tasks_free(C.byref(out))
