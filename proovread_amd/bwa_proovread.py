@@ -1,0 +1,231 @@
+"""`bwa-proovread`-compatible mapper: the SW-stage drop-in of SURVEY.md §8(b).
+
+proovread calls (bin/proovread:1270, 1313; options from proovread.cfg:318-333):
+
+    bwa-proovread index REF PREFIX
+    bwa-proovread mem -b BIN -l LEN -a -Y -A 5 -B 11 -O 2,1 -E 4,3 -T 2.5 \\
+        -k 12 -W 20 -w 40 -r 1 -D 0 -y 20 -L 30,30 [-t N] REF /dev/fd/0 > SAM
+
+`index` checks the long-read file and records it (the seed index is rebuilt in
+memory by `mem`, in about a second per 15 Mb).  `mem` reads the long reads
+(FASTA/FASTQ), the short reads (FASTA/FASTQ, a file, `-` or /dev/fd/0), seeds and
+chains them on the host (libprgpu.so pr_seed_map, restating bwa's
+mem_collect_intv / mem_chain / mem_chain_flt), runs seed extension + CIGAR on
+the GPU (pr_sw_run: ksw_extend2 / ksw_global2 / mem_reg2aln, bit-exact to the
+SW oracle) and prints SAM: `QNAME FLAG RNAME POS MAPQ CIGAR * 0 0 SEQ QUAL
+AS:i:score` for every chain whose alignment passes -T (AS >= T * aligned query
+length, cfg:324 "per-base-score"), with SEQ/QUAL printed for secondary hits too
+(bam2cns:347 needs them).  Per read the best AS is primary (MAPQ 60), others
+secondary (flag 0x100, MAPQ 0).  Logs go to stderr; errors exit 1 (proovread
+prints the log, proovread:1320).
+
+Not restated (parity unpinned): bwa-proovread's -b/-l bin filter
+(accepted and ignored: bam2cns applies the same coverage binning downstream),
+mem_sort_dedup_patch, bwa's MAPQ model.
+"""
+from __future__ import annotations
+
+import argparse
+import gzip
+import os
+import sys
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
+
+from . import seed, sw
+
+_ASCII = np.frombuffer(b"ACGTN", np.uint8)
+
+
+def read_fastx(path: str) -> Tuple[List[str], List[bytes], List[Optional[bytes]]]:
+    """FASTA/FASTQ (optionally gzipped) -> names (first word), sequences, qualities (None for FASTA)."""
+    if path in ("-", "/dev/fd/0", "/dev/stdin"):
+        fh = sys.stdin.buffer
+    elif path.endswith(".gz"):
+        fh = gzip.open(path, "rb")
+    else:
+        fh = open(path, "rb")
+    names, seqs, quals = [], [], []
+    try:
+        first = fh.readline()
+        while first and not first.strip():
+            first = fh.readline()
+        if not first:
+            return names, seqs, quals
+        if first.startswith(b">"):
+            name, buf = first, []
+            for line in fh:
+                if line.startswith(b">"):
+                    names.append(name[1:].split()[0].decode())
+                    seqs.append(b"".join(buf))
+                    quals.append(None)
+                    name, buf = line, []
+                else:
+                    buf.append(line.strip())
+            names.append(name[1:].split()[0].decode())
+            seqs.append(b"".join(buf))
+            quals.append(None)
+        elif first.startswith(b"@"):
+            line = first
+            while line:
+                if not line.strip():
+                    line = fh.readline()
+                    continue
+                s = fh.readline().strip()
+                fh.readline()
+                q = fh.readline().strip()
+                names.append(line[1:].split()[0].decode())
+                seqs.append(s)
+                quals.append(q)
+                line = fh.readline()
+        else:
+            raise ValueError(f"{path}: neither FASTA nor FASTQ")
+    finally:
+        if fh is not sys.stdin.buffer:
+            fh.close()
+    return names, seqs, quals
+
+
+def _pool(seqs: List[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    off = np.zeros(len(seqs) + 1, np.int64)
+    np.cumsum([len(s) for s in seqs], out=off[1:])
+    pool = sw.NT4[np.frombuffer(b"".join(seqs), np.uint8)] if seqs else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(pool, np.uint8), off
+
+
+def _pair(s: str, cast=int) -> Tuple:
+    v = [cast(x) for x in s.split(",")]
+    return (v[0], v[1] if len(v) > 1 else v[0])
+
+
+def parse_mem(argv: List[str]):
+    ap = argparse.ArgumentParser(prog="bwa-proovread mem", add_help=False)
+    ap.add_argument("-b", type=int, default=0)
+    ap.add_argument("-l", type=float, default=0)
+    ap.add_argument("-a", action="store_true")
+    ap.add_argument("-Y", action="store_true")
+    ap.add_argument("-e", action="store_true")
+    ap.add_argument("-A", type=int, default=1)
+    ap.add_argument("-B", type=int, default=4)
+    ap.add_argument("-O", default="6,6")
+    ap.add_argument("-E", default="1,1")
+    ap.add_argument("-L", default="5,5")
+    ap.add_argument("-T", type=float, default=30)
+    ap.add_argument("-k", type=int, default=19)
+    ap.add_argument("-W", type=int, default=0)
+    ap.add_argument("-w", type=int, default=100)
+    ap.add_argument("-r", type=float, default=1.5)
+    ap.add_argument("-D", type=float, default=0.5)
+    ap.add_argument("-y", type=int, default=20)
+    ap.add_argument("-c", type=int, default=500)
+    ap.add_argument("-d", type=int, default=100)
+    ap.add_argument("-t", type=int, default=1)
+    ap.add_argument("ref")
+    ap.add_argument("reads")
+    return ap.parse_args(argv)
+
+
+def options(a) -> Tuple[seed.SeedOpts, sw.SwOpts]:
+    so = seed.default_opts(False)
+    so.min_seed_len, so.w, so.split_factor, so.max_mem_intv = a.k, a.w, a.r, a.y
+    so.max_occ, so.drop_ratio = a.c, a.D
+    # bwa: -W defaults to the minimum seed length
+    so.min_chain_weight = a.W if a.W > 0 else a.k
+    o_del, o_ins = _pair(a.O)
+    e_del, e_ins = _pair(a.E)
+    so.a, so.o_del, so.e_del, so.o_ins, so.e_ins = a.A, o_del, e_del, o_ins, e_ins
+    wo = sw.default_opts(False)
+    wo.a, wo.b, wo.o_del, wo.e_del, wo.o_ins, wo.e_ins = a.A, a.B, o_del, e_del, o_ins, e_ins
+    wo.w, wo.zdrop = a.w, a.d
+    wo.pen_clip5, wo.pen_clip3 = _pair(a.L)
+    wo.min_score_per_base = a.T
+    return so, wo
+
+
+SwRunner = Callable[[sw.SwInput, sw.SwOpts], "sw.SwResult"]
+
+
+def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=None) -> int:
+    out = out or sys.stdout
+    log = log or sys.stderr
+    a = parse_mem(argv)
+    if a.b or a.l:
+        print(f"[bwa-proovread] -b {a.b} -l {a.l}: bin filter not applied (bam2cns bins downstream)", file=log)
+    so, wo = options(a)
+    lr_names, lr_seqs, _ = read_fastx(a.ref)
+    sr_names, sr_seqs, sr_quals = read_fastx(a.reads)
+    lr_pool, lr_off = _pool(lr_seqs)
+    sr_pool, sr_off = _pool(sr_seqs)
+    ix = seed.SeedIndex(lr_pool, lr_off)
+    tasks = ix.map(sr_pool, sr_off, so, threads=a.t)
+    ix.close()
+    print(f"[bwa-proovread] {len(sr_seqs)} reads, {len(lr_seqs)} long reads, {len(tasks)} chains", file=log)
+    inp = sw.SwInput(sr_off, sr_pool, lr_off, lr_pool, tasks["sr"].astype(np.int32), tasks["lr"].astype(np.int32),
+                     tasks["strand"].astype(np.uint8), tasks["qbeg"].astype(np.int32),
+                     tasks["rbeg"].astype(np.int32), tasks["slen"].astype(np.int32))
+    res = (sw_runner or sw.run)(inp, wo)
+    out.write("@HD\tVN:1.5\tSO:unsorted\n")
+    for n, s in zip(lr_names, lr_seqs):
+        out.write(f"@SQ\tSN:{n}\tLN:{len(s)}\n")
+    out.write("@PG\tID:bwa-proovread\tPN:bwa-proovread\tVN:prgpu\tCL:bwa-proovread mem " + " ".join(argv) + "\n")
+    st, ps, sc, pos = res["status"], res["pass"], res["score"], res["pos"]
+    t = 0
+    nt = len(tasks)
+    while t < nt:
+        r = int(tasks["sr"][t])
+        e = t
+        while e < nt and int(tasks["sr"][e]) == r:
+            e += 1
+        hits = [x for x in range(t, e) if st[x] == 0 and ps[x]]
+        if hits:
+            best = max(hits, key=lambda x: (int(sc[x]), -x))
+            q = sr_seqs[r]
+            qual = sr_quals[r]
+            for x in hits:
+                strand = int(tasks["strand"][x])
+                if strand:
+                    codes = sw.NT4[np.frombuffer(q, np.uint8)]
+                    seqs = _ASCII[np.where(codes < 4, 3 - codes, 4)][::-1].tobytes().decode()
+                    quals = qual[::-1].decode() if qual is not None else "*"
+                else:
+                    seqs = q.decode().upper()
+                    quals = qual.decode() if qual is not None else "*"
+                flag = (16 if strand else 0) | (0 if x == best else 256)
+                mapq = 60 if x == best else 0
+                out.write(f"{sr_names[r]}\t{flag}\t{lr_names[int(tasks['lr'][x])]}\t{int(pos[x]) + 1}\t{mapq}\t"
+                          f"{res.cigar_str(x)}\t*\t0\t0\t{seqs}\t{quals}\tAS:i:{int(sc[x])}\n")
+        t = e
+    return 0
+
+
+def index(argv: List[str], log=None) -> int:
+    log = log or sys.stderr
+    if not argv:
+        raise ValueError("usage: bwa-proovread index REF [PREFIX]")
+    ref = argv[0]
+    prefix = argv[1] if len(argv) > 1 else ref
+    names, seqs, _ = read_fastx(ref)
+    with open(prefix + ".prgpu", "w") as fh:
+        fh.write(f"{os.path.abspath(ref)}\t{len(names)}\t{sum(len(s) for s in seqs)}\n")
+    print(f"[bwa-proovread] index: {len(names)} sequences, {sum(len(s) for s in seqs)} bp (built at mem time)",
+          file=log)
+    return 0
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    if not argv or argv[0] not in ("index", "mem"):
+        print("usage: bwa-proovread index REF [PREFIX] | mem [options] REF READS", file=sys.stderr)
+        return 1
+    try:
+        return index(argv[1:]) if argv[0] == "index" else mem(argv[1:])
+    except SystemExit as e:   # argparse
+        return 1 if e.code else 0
+    except Exception as e:   # bwa exits non-zero, proovread prints the log (proovread:1320)
+        print(f"[bwa-proovread] error: {e}", file=sys.stderr)
+        return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
