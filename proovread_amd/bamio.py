@@ -1,0 +1,537 @@
+"""BAM / BGZF I/O for the file-level drop-in pipeline: what
+proovread asks samtools for — `view -bS` (SAM -> BAM, bin/proovread:1313),
+`sort` and `index` (create_sorted_bam, bin/proovread:1330-1355), `merge`
+(bin/proovread:1692), and bam2cns's header and per-long-read region reads
+(bin/bam2cns:224, 336).  Pure Python + zlib, following the SAM/BAM format
+specification (BGZF blocks with the BC extra field and the EOF marker, binary
+records, the BAI binning + 16 kb linear index), so the files stay readable by
+samtools.
+
+Coordinate order is samtools sort's: (reference id, POS, reverse flag), input
+order on ties, unmapped records last.
+"""
+from __future__ import annotations
+
+import dataclasses
+import heapq
+import os
+import struct
+import zlib
+from typing import BinaryIO, Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
+
+EOF_BLOCK = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+_NT16 = "=ACMGRSVTWYHKDBN"
+_NT16_IDX = {c: i for i, c in enumerate(_NT16)}
+_OPS = "MIDNSHP=X"
+_AUX_FMT = {"c": "<b", "C": "<B", "s": "<h", "S": "<H", "i": "<i", "I": "<I", "f": "<f"}
+_BLOCK_DATA = 0xFF00
+
+
+# ---------------------------------------------------------------------------
+# BGZF
+class BgzfWriter:
+    """BGZF writer; `tell()` is the virtual offset (compressed block start << 16 | in-block offset)."""
+
+    def __init__(self, fh: BinaryIO, level: int = 6):
+        self.fh = fh
+        self.level = level
+        self.buf = bytearray()
+        self.coff = 0
+
+    def tell(self) -> int:
+        return (self.coff << 16) | len(self.buf)
+
+    def _flush_block(self, data: bytes):
+        c = zlib.compressobj(self.level, zlib.DEFLATED, -15)
+        comp = c.compress(data) + c.flush()
+        bsize = len(comp) + 25
+        blk = struct.pack("<BBBBIBBHBBHH", 31, 139, 8, 4, 0, 0, 255, 6, 66, 67, 2, bsize) + comp + \
+            struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data))
+        self.fh.write(blk)
+        self.coff += len(blk)
+
+    def write(self, data: bytes):
+        self.buf += data
+        while len(self.buf) >= _BLOCK_DATA:
+            self._flush_block(bytes(self.buf[:_BLOCK_DATA]))
+            del self.buf[:_BLOCK_DATA]
+
+    def flush_block(self):
+        """End the current block (records written next start a new one)."""
+        if self.buf:
+            self._flush_block(bytes(self.buf))
+            self.buf = bytearray()
+
+    def close(self):
+        self.flush_block()
+        self.fh.write(EOF_BLOCK)
+        self.fh.flush()
+
+
+class BgzfReader:
+    """Sequential / seekable BGZF reader with virtual offsets."""
+
+    def __init__(self, fh: BinaryIO):
+        self.fh = fh
+        self.block = b""
+        self.bpos = 0
+        self.coff = 0       # compressed offset of the current block
+        self.next_coff = 0
+
+    def _load(self, coff: int) -> bool:
+        self.fh.seek(coff)
+        hdr = self.fh.read(18)
+        if len(hdr) < 18:
+            self.block, self.bpos, self.coff, self.next_coff = b"", 0, coff, coff
+            return False
+        if hdr[:4] != b"\x1f\x8b\x08\x04":
+            raise ValueError("not a BGZF block")
+        xlen = struct.unpack("<H", hdr[10:12])[0]
+        extra = hdr[12:12 + xlen] if xlen <= 6 else hdr[12:18] + self.fh.read(xlen - 6)
+        bsize = None
+        o = 0
+        while o < len(extra):
+            si1, si2, sl = extra[o], extra[o + 1], struct.unpack("<H", extra[o + 2:o + 4])[0]
+            if si1 == 66 and si2 == 67:
+                bsize = struct.unpack("<H", extra[o + 4:o + 6])[0]
+            o += 4 + sl
+        if bsize is None:
+            raise ValueError("BGZF block without BC field")
+        self.fh.seek(coff + 12 + xlen)
+        comp = self.fh.read(bsize + 1 - 12 - xlen - 8)
+        self.block = zlib.decompress(comp, -15)
+        self.fh.read(8)
+        self.coff = coff
+        self.next_coff = coff + bsize + 1
+        self.bpos = 0
+        return True
+
+    def seek(self, voff: int):
+        self._load(voff >> 16)
+        self.bpos = voff & 0xFFFF
+
+    def tell(self) -> int:
+        if self.bpos >= len(self.block):
+            return self.next_coff << 16
+        return (self.coff << 16) | self.bpos
+
+    def read(self, n: int) -> bytes:
+        out = bytearray()
+        while len(out) < n:
+            if self.bpos >= len(self.block):
+                if not self._load(self.next_coff):
+                    break
+                if not self.block:
+                    continue
+            take = min(n - len(out), len(self.block) - self.bpos)
+            out += self.block[self.bpos:self.bpos + take]
+            self.bpos += take
+        return bytes(out)
+
+
+# ---------------------------------------------------------------------------
+# records
+@dataclasses.dataclass
+class Header:
+    text: str
+    refs: List[Tuple[str, int]]
+
+    def index(self) -> Dict[str, int]:
+        return {n: i for i, (n, _) in enumerate(self.refs)}
+
+    @classmethod
+    def from_sam_text(cls, text: str) -> "Header":
+        refs = []
+        for line in text.splitlines():
+            if line.startswith("@SQ"):
+                f = dict(x.split(":", 1) for x in line.split("\t")[1:] if ":" in x)
+                refs.append((f["SN"], int(f["LN"])))
+        return cls(text, refs)
+
+
+def reg2bin(beg: int, end: int) -> int:
+    end -= 1
+    for shift, off in ((14, 4681), (17, 585), (20, 73), (23, 9), (26, 1)):
+        if beg >> shift == end >> shift:
+            return off + (beg >> shift)
+    return 0
+
+
+def reg2bins(beg: int, end: int) -> List[int]:
+    end -= 1
+    out = [0]
+    for shift, off in ((26, 1), (23, 9), (20, 73), (17, 585), (14, 4681)):
+        out += range(off + (beg >> shift), off + (end >> shift) + 1)
+    return out
+
+
+def cigar_ops(cig: str) -> List[int]:
+    if cig == "*":
+        return []
+    out, num = [], ""
+    for ch in cig:
+        if ch.isdigit():
+            num += ch
+        else:
+            out.append((int(num) << 4) | _OPS.index(ch))
+            num = ""
+    return out
+
+
+def ref_span(ops: Sequence[int]) -> int:
+    return sum(o >> 4 for o in ops if (o & 15) in (0, 2, 3, 7, 8))
+
+
+def _aux_encode(tags: Sequence[str]) -> bytes:
+    out = bytearray()
+    for t in tags:
+        tag, typ, val = t.split(":", 2)
+        if typ == "i":
+            v = int(val)
+            for c, (lo, hi) in (("c", (-128, 127)), ("C", (0, 255)), ("s", (-32768, 32767)), ("S", (0, 65535)),
+                                ("i", (-2 ** 31, 2 ** 31 - 1)), ("I", (0, 2 ** 32 - 1))):
+                if lo <= v <= hi:
+                    out += tag.encode() + c.encode() + struct.pack(_AUX_FMT[c], v)
+                    break
+        elif typ == "f":
+            out += tag.encode() + b"f" + struct.pack("<f", float(val))
+        elif typ == "A":
+            out += tag.encode() + b"A" + val[:1].encode()
+        elif typ == "B":
+            parts = val.split(",")
+            st, vals = parts[0], parts[1:]
+            out += tag.encode() + b"B" + st.encode() + struct.pack("<i", len(vals))
+            out += b"".join(struct.pack(_AUX_FMT[st], float(x) if st == "f" else int(x)) for x in vals)
+        else:   # Z, H
+            out += tag.encode() + typ.encode() + val.encode() + b"\0"
+    return bytes(out)
+
+
+def _aux_decode(r: bytes, o: int) -> List[str]:
+    tags = []
+    while o < len(r):
+        tag = r[o:o + 2].decode()
+        t = chr(r[o + 2])
+        o += 3
+        if t in ("c", "C", "s", "S", "i", "I"):
+            sz = struct.calcsize(_AUX_FMT[t])
+            tags.append(f"{tag}:i:{struct.unpack(_AUX_FMT[t], r[o:o + sz])[0]}")
+            o += sz
+        elif t == "f":
+            tags.append(f"{tag}:f:{struct.unpack('<f', r[o:o + 4])[0]:g}")
+            o += 4
+        elif t == "A":
+            tags.append(f"{tag}:A:{chr(r[o])}")
+            o += 1
+        elif t in ("Z", "H"):
+            e = r.index(b"\0", o)
+            tags.append(f"{tag}:{t}:{r[o:e].decode()}")
+            o = e + 1
+        elif t == "B":
+            st = chr(r[o])
+            cnt = struct.unpack("<i", r[o + 1:o + 5])[0]
+            sz = struct.calcsize(_AUX_FMT[st])
+            vals = [struct.unpack(_AUX_FMT[st], r[o + 5 + i * sz:o + 5 + (i + 1) * sz])[0] for i in range(cnt)]
+            tags.append(f"{tag}:B:{st}," + ",".join(f"{v:g}" if st == "f" else str(v) for v in vals))
+            o += 5 + cnt * sz
+        else:
+            raise ValueError(f"bad BAM aux type {t}")
+    return tags
+
+
+def sam_to_record(line: str, ref_index: Dict[str, int]) -> bytes:
+    """One SAM text line -> a BAM record (with its block_size prefix)."""
+    f = line.rstrip("\r\n").split("\t")
+    qname, flag, rname, pos, mapq, cig = f[0], int(f[1]), f[2], int(f[3]), int(f[4]), f[5]
+    rnext, pnext, tlen, seq, qual = f[6], int(f[7]), int(f[8]), f[9], f[10]
+    ops = cigar_ops(cig)
+    rid = ref_index.get(rname, -1) if rname != "*" else -1
+    nid = rid if rnext == "=" else (ref_index.get(rnext, -1) if rnext != "*" else -1)
+    beg = pos - 1
+    end = beg + (ref_span(ops) or 1)
+    l_seq = 0 if seq == "*" else len(seq)
+    sb = bytearray((l_seq + 1) // 2)
+    for i in range(l_seq):
+        sb[i >> 1] |= _NT16_IDX.get(seq[i].upper(), 15) << (4 * (1 - (i & 1)))
+    qb = bytes([0xFF] * l_seq) if qual == "*" else bytes(ord(c) - 33 for c in qual[:l_seq])
+    rn = qname.encode() + b"\0"
+    body = struct.pack("<iiBBHHHiiii", rid, beg, len(rn), mapq, reg2bin(beg, end) if beg >= 0 else 4680,
+                       len(ops), flag, l_seq, nid, pnext - 1, tlen)
+    body += rn + struct.pack(f"<{len(ops)}I", *ops) + bytes(sb) + qb + _aux_encode(f[11:])
+    return struct.pack("<i", len(body)) + body
+
+
+def record_to_sam(r: bytes, names: Sequence[str]) -> str:
+    """A BAM record (without block_size) -> SAM text (no newline)."""
+    rid, pos, l_rn, mapq, _bin, n_cig, flag, l_seq, nid, npos, tlen = struct.unpack("<iiBBHHHiiii", r[:32])
+    o = 32
+    qname = r[o:o + l_rn - 1].decode()
+    o += l_rn
+    ops = struct.unpack(f"<{n_cig}I", r[o:o + 4 * n_cig])
+    o += 4 * n_cig
+    cig = "".join(f"{x >> 4}{_OPS[x & 15]}" for x in ops) or "*"
+    sb = r[o:o + (l_seq + 1) // 2]
+    o += (l_seq + 1) // 2
+    seq = "".join(_NT16[(sb[i >> 1] >> (4 * (1 - (i & 1)))) & 15] for i in range(l_seq)) or "*"
+    qb = r[o:o + l_seq]
+    o += l_seq
+    qual = "*" if (l_seq == 0 or qb[0] == 0xFF) else "".join(chr(x + 33) for x in qb)
+    rname = names[rid] if rid >= 0 else "*"
+    rnext = "*" if nid < 0 else ("=" if nid == rid else names[nid])
+    f = [qname, str(flag), rname, str(pos + 1), str(mapq), cig, rnext, str(npos + 1), str(tlen), seq, qual]
+    return "\t".join(f + _aux_decode(r, o))
+
+
+def record_key(r: bytes) -> Tuple[int, int, int]:
+    """samtools sort's coordinate key: (reference id, POS, reverse flag), unmapped last."""
+    rid, pos = struct.unpack("<ii", r[:8])
+    flag = struct.unpack("<H", r[14:16])[0]
+    return ((rid if rid >= 0 else 1 << 31), pos + 1 if rid >= 0 else 0, (flag >> 4) & 1)
+
+
+# ---------------------------------------------------------------------------
+# files
+class BamWriter:
+    def __init__(self, path_or_fh, header: Header):
+        self._own = isinstance(path_or_fh, str)
+        self.fh = open(path_or_fh, "wb") if self._own else path_or_fh
+        self.w = BgzfWriter(self.fh)
+        self.header = header
+        text = header.text.encode()
+        raw = b"BAM\x01" + struct.pack("<i", len(text)) + text + struct.pack("<i", len(header.refs))
+        for n, l in header.refs:
+            raw += struct.pack("<i", len(n) + 1) + n.encode() + b"\0" + struct.pack("<i", l)
+        self.w.write(raw)
+        self.w.flush_block()   # records start in a fresh block (index-friendly)
+
+    def write_record(self, rec: bytes):
+        """rec includes its block_size prefix."""
+        self.w.write(rec)
+
+    def close(self):
+        self.w.close()
+        if self._own:
+            self.fh.close()
+
+
+class BamReader:
+    def __init__(self, path: str):
+        self.path = path
+        self.fh = open(path, "rb")
+        self.r = BgzfReader(self.fh)
+        if self.r.read(4) != b"BAM\x01":
+            raise ValueError(f"{path}: not a BAM file")
+        l_text = struct.unpack("<i", self.r.read(4))[0]
+        text = self.r.read(l_text).rstrip(b"\0").decode()
+        n_ref = struct.unpack("<i", self.r.read(4))[0]
+        refs = []
+        for _ in range(n_ref):
+            ln = struct.unpack("<i", self.r.read(4))[0]
+            name = self.r.read(ln).rstrip(b"\0").decode()
+            refs.append((name, struct.unpack("<i", self.r.read(4))[0]))
+        self.header = Header(text, refs)
+        self.names = [n for n, _ in refs]
+        self.first_voff = self.r.tell()
+
+    def records(self) -> Iterator[Tuple[int, bytes, int]]:
+        """(virtual offset, record without block_size, end virtual offset) from the current position."""
+        while True:
+            v = self.r.tell()
+            b = self.r.read(4)
+            if len(b) < 4:
+                return
+            n = struct.unpack("<i", b)[0]
+            yield v, self.r.read(n), self.r.tell()
+
+    def rewind(self):
+        self.r.seek(self.first_voff)
+
+    def close(self):
+        self.fh.close()
+
+
+def write_bam_from_sam(lines: Iterable[str], out_path: str, header_text: Optional[str] = None) -> Header:
+    """`samtools view -bS`: SAM text (header lines first) -> BAM, records in input order."""
+    hdr_lines, recs = [], []
+    it = iter(lines)
+    for line in it:
+        if line.startswith("@"):
+            hdr_lines.append(line.rstrip("\r\n"))
+            continue
+        if line.strip():
+            recs.append(line)
+        break
+    h = Header.from_sam_text(header_text if header_text is not None else "\n".join(hdr_lines) + "\n")
+    idx = h.index()
+    w = BamWriter(out_path, h)
+    for line in recs:
+        w.write_record(sam_to_record(line, idx))
+    for line in it:
+        if line.strip() and not line.startswith("@"):
+            w.write_record(sam_to_record(line, idx))
+    w.close()
+    return h
+
+
+def _set_sort_order(text: str, so: str) -> str:
+    lines = text.splitlines()
+    if lines and lines[0].startswith("@HD"):
+        f = [x for x in lines[0].split("\t") if not x.startswith("SO:")]
+        lines[0] = "\t".join(f + [f"SO:{so}"])
+    else:
+        lines.insert(0, f"@HD\tVN:1.6\tSO:{so}")
+    return "\n".join(lines) + "\n"
+
+
+def sort_bam(in_path: str, out_path: str):
+    """`samtools sort` (coordinate): stable in input order on equal keys."""
+    rd = BamReader(in_path)
+    recs = [r for _, r, _ in rd.records()]
+    rd.close()
+    order = sorted(range(len(recs)), key=lambda i: (record_key(recs[i]), i))
+    w = BamWriter(out_path, Header(_set_sort_order(rd.header.text, "coordinate"), rd.header.refs))
+    for i in order:
+        w.write_record(struct.pack("<i", len(recs[i])) + recs[i])
+    w.close()
+
+
+def merge_bams(out_path: str, in_paths: Sequence[str]):
+    """`samtools merge` of coordinate-sorted BAMs with identical reference lists."""
+    readers = [BamReader(p) for p in in_paths]
+    refs = readers[0].header.refs
+    for r in readers[1:]:
+        if r.header.refs != refs:
+            raise ValueError("merge: reference lists differ")
+    w = BamWriter(out_path, Header(_set_sort_order(readers[0].header.text, "coordinate"), refs))
+    def keyed(k, r):
+        for n, (_, rec, _) in enumerate(r.records()):
+            yield (record_key(rec), k, n), rec
+    for _, rec in heapq.merge(*[keyed(k, r) for k, r in enumerate(readers)]):
+        w.write_record(struct.pack("<i", len(rec)) + rec)
+    w.close()
+    for r in readers:
+        r.close()
+
+
+def index_bam(path: str, out_path: Optional[str] = None):
+    """`samtools index`: BAI (bins with chunks, 16 kb linear index, pseudo-bin 37450 with counts)."""
+    rd = BamReader(path)
+    n_ref = len(rd.header.refs)
+    bins: List[Dict[int, List[List[int]]]] = [dict() for _ in range(n_ref)]
+    lin: List[List[int]] = [[] for _ in range(n_ref)]
+    meta = [[None, 0, 0, 0] for _ in range(n_ref)]   # off_beg, off_end, mapped, unmapped
+    n_no_coor = 0
+    last = (-1, -1)
+    for v, r, ve in rd.records():
+        rid, pos = struct.unpack("<ii", r[:8])
+        bin_, n_cig, flag = struct.unpack("<HHH", r[10:16])
+        if rid < 0:
+            n_no_coor += 1
+            continue
+        if (rid, pos) < last:
+            raise ValueError(f"{path}: not coordinate-sorted")
+        last = (rid, pos)
+        l_rn = r[8]
+        ops = struct.unpack(f"<{n_cig}I", r[32 + l_rn:32 + l_rn + 4 * n_cig])
+        end = pos + (ref_span(ops) or 1)
+        ch = bins[rid].setdefault(bin_, [])
+        if ch and ch[-1][1] == v:
+            ch[-1][1] = ve
+        else:
+            ch.append([v, ve])
+        for wdw in range(pos >> 14, ((end - 1) >> 14) + 1):
+            while len(lin[rid]) <= wdw:
+                lin[rid].append(0)
+            if lin[rid][wdw] == 0:
+                lin[rid][wdw] = v
+        m = meta[rid]
+        if m[0] is None:
+            m[0] = v
+        m[1] = ve
+        if flag & 4:
+            m[3] += 1
+        else:
+            m[2] += 1
+    rd.close()
+    out = bytearray(b"BAI\x01" + struct.pack("<i", n_ref))
+    for rid in range(n_ref):
+        b = bins[rid]
+        n_bin = len(b) + (1 if meta[rid][0] is not None else 0)
+        out += struct.pack("<i", n_bin)
+        for bn in sorted(b):
+            out += struct.pack("<Ii", bn, len(b[bn]))
+            for beg, end in b[bn]:
+                out += struct.pack("<QQ", beg, end)
+        if meta[rid][0] is not None:
+            out += struct.pack("<Ii", 37450, 2) + struct.pack("<QQQQ", meta[rid][0], meta[rid][1], meta[rid][2],
+                                                               meta[rid][3])
+        li = lin[rid]
+        for i in range(len(li)):   # empty windows take the next filled window's offset (samtools: previous)
+            if li[i] == 0 and i > 0:
+                li[i] = li[i - 1]
+        out += struct.pack("<i", len(li)) + b"".join(struct.pack("<Q", x) for x in li)
+    out += struct.pack("<Q", n_no_coor)
+    with open(out_path or path + ".bai", "wb") as fh:
+        fh.write(bytes(out))
+
+
+def read_bai(path: str):
+    with open(path, "rb") as fh:
+        d = fh.read()
+    if d[:4] != b"BAI\x01":
+        raise ValueError(f"{path}: not a BAI index")
+    n_ref = struct.unpack("<i", d[4:8])[0]
+    o = 8
+    refs = []
+    for _ in range(n_ref):
+        n_bin = struct.unpack("<i", d[o:o + 4])[0]
+        o += 4
+        bins = {}
+        for _ in range(n_bin):
+            bn, n_chunk = struct.unpack("<Ii", d[o:o + 8])
+            o += 8
+            bins[bn] = [struct.unpack("<QQ", d[o + 16 * k:o + 16 * k + 16]) for k in range(n_chunk)]
+            o += 16 * n_chunk
+        n_intv = struct.unpack("<i", d[o:o + 4])[0]
+        o += 4
+        lin = list(struct.unpack(f"<{n_intv}Q", d[o:o + 8 * n_intv]))
+        o += 8 * n_intv
+        refs.append((bins, lin))
+    return refs
+
+
+def region_records(path: str, ref: str, beg: int = 0, end: int = 1 << 29) -> Iterator[bytes]:
+    """Records of reference `ref` overlapping [beg, end) (0-based), through the .bai index when present
+    (`samtools view BAM "ref:"`, bin/bam2cns:336); in file order."""
+    rd = BamReader(path)
+    try:
+        if ref not in rd.names:
+            return
+        rid = rd.names.index(ref)
+        chunks = None
+        if os.path.exists(path + ".bai"):
+            bins, lin = read_bai(path + ".bai")[rid]
+            minoff = lin[beg >> 14] if (beg >> 14) < len(lin) else 0
+            chunks = sorted((b, e) for bn in reg2bins(beg, end) if bn in bins for b, e in bins[bn] if e > minoff)
+        if chunks is None:
+            chunks = [(rd.first_voff, 1 << 62)]
+        seen = set()
+        for cb, ce in chunks:
+            rd.r.seek(cb)
+            for v, r, _ in rd.records():
+                if v >= ce:
+                    break
+                if v in seen:
+                    continue
+                rrid, pos = struct.unpack("<ii", r[:8])
+                if rrid != rid:
+                    if chunks[0][1] == 1 << 62 and rrid > rid:
+                        break
+                    continue
+                l_rn, n_cig = r[8], struct.unpack("<H", r[12:14])[0]
+                ops = struct.unpack(f"<{n_cig}I", r[32 + l_rn:32 + l_rn + 4 * n_cig])
+                if pos < end and pos + (ref_span(ops) or 1) > beg:
+                    seen.add(v)
+                    yield r
+    finally:
+        rd.close()

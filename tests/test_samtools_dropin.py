@@ -1,0 +1,141 @@
+"""BAM I/O and the samtools drop-in (proovread_amd/bamio.py, proovread_amd/samtools.py)
+for the commands proovread / bam2cns run: view -bS / -H / region, sort, index, merge,
+--version.  Checked by round trips (SAM -> BAM -> SAM field-identical), the coordinate
+order samtools sort defines ((ref id, POS, reverse flag), input order on ties,
+unmapped last), region reads through the BAI index against a full scan, merge against
+sort, and readability by the bam2cns drop-in's own BAM parser."""
+import io
+import random
+import re
+
+import pytest
+
+from proovread_amd import bam2cns, bamio, samtools
+
+REFS = [("lr0", 5000), ("lr1", 120000), ("lr2", 300)]
+
+
+def _records(n, seed=3):
+    rng = random.Random(seed)
+    out = []
+    for i in range(n):
+        r = rng.randrange(len(REFS) + 1)
+        if r == len(REFS):
+            out.append(f"u{i}\t4\t*\t0\t0\t*\t*\t0\t0\tACGTN\t*")
+            continue
+        name, L = REFS[r]
+        ln = rng.randint(20, 150)
+        pos = rng.randint(1, max(1, L - ln))
+        d = rng.randint(0, 3)
+        ins = rng.randint(0, 3)
+        s5 = rng.randint(0, 5)
+        cig = (f"{s5}S" if s5 else "") + f"{ln - d - ins - s5}M{d}D{ins}I" if ln - d - ins - s5 > 0 else f"{ln}M"
+        cig = cig.replace("0D", "").replace("0I", "")
+        seq = "".join(rng.choice("ACGT") for _ in range(ln))
+        qual = "".join(chr(33 + rng.randint(0, 40)) for _ in range(ln)) if rng.random() < 0.7 else "*"
+        flag = rng.choice([0, 16, 256, 272])
+        tags = [f"AS:i:{rng.randint(-5, 700)}", "XA:Z:lr1,+5,10M,0", f"XF:f:{rng.random():g}", "XC:A:q"]
+        out.append(f"r{i}\t{flag}\t{name}\t{pos}\t{rng.choice([0, 60])}\t{cig}\t*\t0\t0\t{seq}\t{qual}\t" + "\t".join(tags))
+    return out
+
+
+HEADER = "@HD\tVN:1.5\tSO:unsorted\n" + "".join(f"@SQ\tSN:{n}\tLN:{l}\n" for n, l in REFS)
+
+
+def _sam_file(tmp_path, recs):
+    p = tmp_path / "in.sam"
+    p.write_text(HEADER + "\n".join(recs) + "\n")
+    return p
+
+
+def _norm(line):
+    f = line.split("\t")
+    return f[:11] + sorted(f[11:])
+
+
+def test_view_bS_round_trip(tmp_path):
+    recs = _records(3000)
+    sam = _sam_file(tmp_path, recs)
+    assert samtools.main(["view", "-@", "4", "-bS", str(sam), "-o", str(tmp_path / "a.bam")]) == 0
+    out = io.StringIO()
+    assert samtools.view([str(tmp_path / "a.bam")], out=out) == 0
+    got = out.getvalue().splitlines()
+    assert [_norm(x) for x in got] == [_norm(x) for x in recs]
+    out = io.StringIO()
+    samtools.view(["-H", str(tmp_path / "a.bam")], out=out)
+    assert out.getvalue() == HEADER
+
+
+def _key(line):
+    f = line.split("\t")
+    if f[2] == "*":
+        return (len(REFS), 0, 0)
+    return ([n for n, _ in REFS].index(f[2]), int(f[3]), (int(f[1]) >> 4) & 1)
+
+
+def test_sort_index_region(tmp_path):
+    recs = _records(4000, seed=5)
+    sam = _sam_file(tmp_path, recs)
+    samtools.main(["view", "-bS", str(sam), "-o", str(tmp_path / "u.bam")])
+    assert samtools.main(["sort", "-m", "2G", "-@", "3", "-T", str(tmp_path / "tmp"), "-o", str(tmp_path / "s.bam"),
+                          str(tmp_path / "u.bam")]) == 0
+    out = io.StringIO()
+    samtools.view([str(tmp_path / "s.bam")], out=out)
+    got = out.getvalue().splitlines()
+    want = [r for _, r in sorted(((_key(r), i), r) for i, r in enumerate(recs))]
+    assert [_norm(x) for x in got] == [_norm(x) for x in want]
+    assert samtools.main(["index", str(tmp_path / "s.bam")]) == 0
+    assert (tmp_path / "s.bam.bai").exists()
+    # region reads through the index == a scan
+    for ref, beg, end in [("lr0", None, None), ("lr1", None, None), ("lr2", None, None), ("lr1", 30000, 31000),
+                          ("lr1", 1, 17000), ("lr0", 4990, 5000)]:
+        region = f"{ref}:" if beg is None else f"{ref}:{beg}-{end}"
+        out = io.StringIO()
+        samtools.view([str(tmp_path / "s.bam"), region], out=out)
+        b0 = 0 if beg is None else beg - 1
+        e0 = 1 << 29 if end is None else end
+        scan = []
+        for r in want:
+            f = r.split("\t")
+            if f[2] != ref:
+                continue
+            p = int(f[3]) - 1
+            span = bamio.ref_span(bamio.cigar_ops(f[5])) or 1
+            if p < e0 and p + span > b0:
+                scan.append(r)
+        assert [_norm(x) for x in out.getvalue().splitlines()] == [_norm(x) for x in scan], region
+
+
+def test_merge_equals_sort(tmp_path):
+    recs = _records(2000, seed=9)
+    parts = [recs[:700], recs[700:]]
+    for k, p in enumerate(parts):
+        s = tmp_path / f"p{k}.sam"
+        s.write_text(HEADER + "\n".join(p) + "\n")
+        samtools.main(["view", "-bS", str(s), "-o", str(tmp_path / f"p{k}u.bam")])
+        samtools.main(["sort", "-o", str(tmp_path / f"p{k}.bam"), str(tmp_path / f"p{k}u.bam")])
+    assert samtools.main(["merge", str(tmp_path / "m.bam"), str(tmp_path / "p0.bam"), str(tmp_path / "p1.bam")]) == 0
+    out = io.StringIO()
+    samtools.view([str(tmp_path / "m.bam")], out=out)
+    want = [r for _, r in sorted(((_key(r), i), r) for i, r in enumerate(recs))]
+    assert [_norm(x) for x in out.getvalue().splitlines()] == [_norm(x) for x in want]
+
+
+def test_bam2cns_reader_reads_dropin_bam(tmp_path):
+    recs = [r for r in _records(500, seed=11) if "\t*\t0\t0\t" not in r.split("\t", 2)[2][:10]]
+    sam = _sam_file(tmp_path, recs)
+    samtools.main(["view", "-bS", str(sam), "-o", str(tmp_path / "c.bam")])
+    hdr, it = bam2cns.bam_records(str(tmp_path / "c.bam"))
+    assert hdr == dict(REFS)
+    got = list(it)
+    mapped = [r for r in recs if r.split("\t")[2] != "*"]
+    assert len(got) == len(mapped)
+    for g, r in zip(got, mapped):
+        f = r.split("\t")
+        assert (g.rname, g.pos, g.seq) == (f[2], int(f[3]), f[9])
+        assert g.score == float(f[11][5:])
+
+
+def test_version_satisfies_proovread_check():
+    v = re.search(r"([0-9\.]+)", samtools.VERSION).group(1)
+    assert tuple(int(x) for x in v.split(".")) >= (1, 1)
