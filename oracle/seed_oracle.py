@@ -14,7 +14,7 @@ unknown, .gitmodules:4-6 — parity unpinned):
   bwt.c     bwt_smem1a (max_intv = 0), bwt_seed_strategy1
 over the same index definition as the library: forward long reads then the
 reverse complement of their concatenation (bwa's forward-reverse coordinates),
-contigs separated, N never matching, occurrences of a seed in suffix order.
+contigs separated, N never matching, occurrences of a seed in text-position order.
 """
 from __future__ import annotations
 
@@ -83,11 +83,6 @@ class Index:
             return self.lr_off[ci] + off, ci
         rid = 2 * self.n_lr - 1 - ci
         return self.l_pac + (self.l_pac - self.lr_off[rid + 1]) + off, rid
-
-    def suffix_key(self, ci, off):
-        # suffix order of the library's text: codes A<C<G<T<N<separator, then text position
-        order = {"A": 0, "C": 1, "G": 2, "T": 3, "N": 4}
-        return [order[c] for c in self.contigs[ci][off:]] + [5], ci, off
 
 
 def _qs(q, a, b):
@@ -230,7 +225,7 @@ def map_read(I: Index, O: Opts, q, sid=0):
     chains = []   # sorted by pos (insertion after equal keys, like the library's multimap)
     keys = []
     for (a, b, _) in collect_intv(I, O, q):
-        pos = sorted(I.positions(_qs(q, a, b)), key=lambda p: I.suffix_key(*p))
+        pos = I.positions(_qs(q, a, b))   # text order: contig-major, then offset
         npos = len(pos)
         step = npos // O.max_occ if npos > O.max_occ else 1
         k = count = 0

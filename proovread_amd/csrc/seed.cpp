@@ -6,7 +6,7 @@
 // upstream bwa's published algorithms over an index of the long reads:
 //   mem_collect_intv   SMEMs (bwt_smem1a) >= -k, re-seeding of long SMEMs
 //                      with <= split_width hits (-r), LAST-like third round (-y)
-//   mem_chain          occurrences (<= -c per SMEM, sampled in suffix order),
+//   mem_chain          occurrences (<= -c per SMEM, sampled in text order),
 //                      chains grown by test_and_merge (-w, max_chain_gap)
 //   mem_chain_flt      chain weight, -W minimum, -D drop ratio (mask_level .5)
 //   mem_chain2aln      the chain's best seed (highest score, last on ties)
@@ -19,7 +19,8 @@
 // differences: contigs are separated (bwa's concatenated pac lets a
 // match run across a contig or strand boundary; such seeds are discarded there
 // anyway, but they can shadow SMEMs), an N never matches (bwa substitutes random
-// bases), ties in the chain weight sort are stable, seeds other than the best
+// bases), a seed's occurrences are visited in text-position order (bwa: suffix-array
+// order), ties in the chain weight sort are stable, seeds other than the best
 // one of a chain are not extended.
 #include <algorithm>
 #include <atomic>
@@ -204,19 +205,6 @@ int chain_weight(const Chain &c) {
     return w < (1 << 30) ? w : (1 << 30) - 1;
 }
 
-// suffix order of text positions (the order of an SA interval): lexicographic, codes
-// 0-3 < N < SEP, then position
-bool suffix_less(const Index &I, uint32_t a, uint32_t b) {
-    const uint8_t *T = I.text.data();
-    const int64_t n = (int64_t)I.text.size();
-    for (int64_t x = 0;; ++x) {
-        if (a + x >= n || b + x >= n) return a < b;
-        const uint8_t ca = T[a + x], cb = T[b + x];
-        if (ca != cb) return ca < cb;
-        if (ca == SEP) return a < b;
-    }
-}
-
 struct ReadOut {
     std::vector<pr_seed_task> tasks;
 };
@@ -269,8 +257,7 @@ void map_read(const Index &I, const pr_seed_opts &O, const uint8_t *q, int len, 
     std::vector<uint32_t> pos;
     for (const Iv &p : mems) {
         const int slen = p.end - p.start;
-        occ(I, q, p.start, p.end, &pos);
-        std::sort(pos.begin(), pos.end(), [&](uint32_t a, uint32_t b) { return suffix_less(I, a, b); });
+        occ(I, q, p.start, p.end, &pos);   // text-position order (12-mer lists are position-sorted)
         const int64_t np = (int64_t)pos.size();
         const int64_t step = np > O.max_occ ? np / O.max_occ : 1;
         int64_t count = 0;
