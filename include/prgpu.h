@@ -286,6 +286,43 @@ int pr_iter_last_timing(pr_ctx *ctx, double *ms_sw_extend, double *ms_sw_global,
  * GPUs: the global masked-fraction input of mask_shortcut_frac, proovread:2026) */
 int pr_iter_stats(pr_ctx *ctx, int32_t min_phred, int64_t *dev_out);
 
+/* ------------------------------------------------------------------ */
+/* masking: `SeqFilter --phred-mask <hcr-mask> --base-content N` after every
+ * iteration (bin/proovread:1701-1716).  High-confidence regions of the
+ * corrected reads (quality runs in [phred_min, phred_max]) become N, minus
+ * sticky ends, with read-end and gap rules (sam2cns:806-951, the in-tree
+ * predecessor of SeqFilter's masking; mapping of the hcr-mask fields in
+ * DESIGN.md, parity with the absent SeqFilter unpinned).  The masked reads are
+ * the next iteration's bwa reference (.masked.fa, proovread:850), bpN/bpt the
+ * mask_shortcut_frac input (proovread:1711-1716, 2026-2047).                 */
+typedef struct pr_mask_params {
+    int32_t phred_min, phred_max;  /* hcr-mask fields 0-1                              */
+    int32_t mask_min_len;          /* field 2 (scaled to the short-read length)     */
+    int32_t unmask_min_len;        /* field 3 (scaled)                              */
+    int32_t mask_reduce;           /* field 4: bases unmasked at each HCR end       */
+    double end_ratio;              /* field 5                                       */
+    int32_t phred_offset;          /* --phred-offset (33)                           */
+} pr_mask_params;
+void pr_mask_params_default(pr_mask_params *p);   /* proovread.cfg:235 at 100 bp   */
+/* "20,41,80,130,60,0.7" scaled to min_sr_length as proovread:1702-1705 does */
+int pr_mask_params_parse(const char *hcr_mask, int32_t min_sr_length, pr_mask_params *out);
+/* MCR capacity (pairs) of a batch of reads with offsets off[n+1] */
+int pr_mask_bound(const pr_mask_params *p, int32_t n, const int64_t *off, int64_t *mcr_cap);
+/* One-shot masking of n reads (ASCII seq, phred+offset qual, offsets off[n+1]):
+ * out_seq[off[n]] masked bases; mcr_off[n+1] (filled) capacity prefix into mcr;
+ * mcr (offset, length) pairs of read i at mcr[2*mcr_off[i]], n_mcr[i] of them;
+ * stats[0] = bases, stats[1] = N bases (bpt, bpN).  Output pointers may be NULL. */
+int pr_mask_run(pr_ctx *ctx, const pr_mask_params *p, int32_t n, const int64_t *off, const uint8_t *seq,
+                const uint8_t *qual, uint8_t *out_seq, int64_t *mcr_off, int32_t *mcr, int32_t *n_mcr,
+                int64_t *stats);
+/* Mask the resident consensus of the last pr_iter_launch / pr_cns_launch (async,
+ * ctx stream).  dev_stats is DEVICE int64[2] = {bases, N bases} of the reads with
+ * status 0 (RCCL-reducible, like pr_iter_stats). */
+int pr_iter_mask(pr_ctx *ctx, const pr_mask_params *p, int64_t *dev_stats);
+/* the masked consensus of the last pr_iter_mask: seq_cap bytes laid out like
+ * pr_cns_out.seq (syncs; PR_ERR_CAPACITY if a run list overflowed) */
+int pr_iter_mask_download(pr_ctx *ctx, uint8_t *masked);
+
 #ifdef __cplusplus
 }
 #endif

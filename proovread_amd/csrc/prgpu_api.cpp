@@ -14,6 +14,7 @@
 #include "cns_dev.h"
 #include "sw_dev.h"
 #include "pipe_dev.h"
+#include "mask_dev.h"
 
 using namespace prgpu;
 int sw_get_ptrs(pr_ctx *c, SwPtrs *p);
@@ -71,6 +72,9 @@ enum CnsBufId {
     CB_COUNT
 };
 
+// masking buffers (pr_mask_run inputs / outputs, pr_iter_mask output and run lists)
+enum MaskBufId { MB_OFF, MB_SEQ, MB_QUAL, MB_OUT, MB_RUN_OFF, MB_RUNS, MB_TMP, MB_NRUNS, MB_ERR, MB_STATS, MB_COUNT };
+
 struct pr_ctx {
     int device = 0;
     int n_cu = 256;
@@ -93,6 +97,10 @@ struct pr_ctx {
     float ms_pipe = 0.f, ms_cns = 0.f;
     // SW resident batch
     SwResident sw;
+    // masking
+    DevBuf mb[MB_COUNT];
+    bool iter_masked = false;
+    bool cns_launched = false;   // a consensus launch filled the CB_O_* outputs
 };
 
 extern "C" int pr_device_count(int *n) {
@@ -130,6 +138,7 @@ extern "C" void pr_ctx_destroy(pr_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (auto &b : c->cb) b.release();
+    for (auto &b : c->mb) b.release();
     sw_release(c->sw);
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -233,6 +242,8 @@ extern "C" int pr_cns_upload(pr_ctx *c, const pr_cns_batch *b) {
     if (!c) return set_error(PR_ERR_ARG, "null ctx");
     int rc = validate_batch(b);
     if (rc) return rc;
+    c->cns_launched = false;
+    c->iter_masked = false;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const int n = b->n_lr;
@@ -370,7 +381,10 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
     D.o_trace = B[CB_O_TRACE].as<uint8_t>();
     D.o_cig = B[CB_O_CIG].as<uint32_t>();
     D.o_chim = B[CB_O_CHIM].as<int32_t>();
-    if (c->n_lr == 0) return 0;
+    if (c->n_lr == 0) {
+        c->cns_launched = true;
+        return 0;
+    }
     {
         // bins per read with this bin size (Seq.pm:1437-1444 _init_read_bins)
         const std::vector<int64_t> &lr = c->lr_off_host;
@@ -417,6 +431,7 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
     int e = cns_launch(D, P, grid, (void *)c->stream);
     if (e != 0) return set_error(PR_ERR_HIP, "cns kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     HIPCHK(hipEventRecord(c->ev[5], c->stream));
+    c->cns_launched = true;
     return 0;
 }
 
@@ -505,6 +520,8 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
     int rc = pr_sw_upload(c, &sb);
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
+    c->cns_launched = false;
+    c->iter_masked = false;
     hipStream_t s = c->stream;
     c->n_lr = n;
     c->n_aln = sb.n_task;
@@ -670,6 +687,180 @@ extern "C" int pr_iter_stats(pr_ctx *c, int32_t min_phred, int64_t *dev_out) {
                               B[CB_O_QUAL].as<uint8_t>(), c->n_lr, min_phred + 33,
                               reinterpret_cast<unsigned long long *>(dev_out), (void *)c->stream);
     if (e) return set_error(PR_ERR_HIP, "stats kernel: %s", hipGetErrorString((hipError_t)e));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// masking (SeqFilter --phred-mask of bin/proovread:1701-1716; mask_core.h)
+extern "C" void pr_mask_params_default(pr_mask_params *p) {
+    p->phred_min = 20;        // proovread.cfg:235 "20,41,80,130,60,0.7" at 100 bp short reads
+    p->phred_max = 41;
+    p->mask_min_len = 80;
+    p->unmask_min_len = 130;
+    p->mask_reduce = 60;
+    p->end_ratio = 0.7;
+    p->phred_offset = 33;
+}
+
+extern "C" int pr_mask_params_parse(const char *hcr_mask, int32_t min_sr_length, pr_mask_params *out) {
+    if (!hcr_mask || !out || min_sr_length <= 0) return set_error(PR_ERR_ARG, "hcr_mask, out and min_sr_length > 0");
+    double f[6];
+    const char *q = hcr_mask;
+    for (int i = 0; i < 6; ++i) {
+        char *e = nullptr;
+        f[i] = std::strtod(q, &e);
+        if (e == q || (i < 5 && *e != ',') || (i == 5 && *e && *e != '\n'))
+            return set_error(PR_ERR_ARG, "hcr-mask '%s': want phred-min,phred-max,mask-min-len,unmask-min-len,"
+                             "mask-reduce,mask-end-ratio", hcr_mask);
+        q = e + 1;
+    }
+    pr_mask_params_default(out);
+    out->phred_min = (int32_t)f[0];
+    out->phred_max = (int32_t)f[1];
+    // proovread:1703-1704: int(x * min_sr_length / 100 + .5)
+    out->mask_min_len = (int32_t)(f[2] * min_sr_length / 100.0 + .5);
+    out->unmask_min_len = (int32_t)(f[3] * min_sr_length / 100.0 + .5);
+    out->mask_reduce = (int32_t)f[4];
+    out->end_ratio = f[5];
+    return 0;
+}
+
+static int mask_cfg(const pr_mask_params *p, MaskCfg *c) {
+    if (!p) return set_error(PR_ERR_ARG, "null params");
+    if (p->mask_min_len < 1 || p->mask_reduce < 0 || p->unmask_min_len < 0 || p->phred_min > p->phred_max)
+        return set_error(PR_ERR_ARG, "mask params: need mask_min_len >= 1, mask_reduce >= 0, unmask_min_len >= 0, "
+                         "phred_min <= phred_max");
+    c->lo_char = p->phred_min + p->phred_offset;
+    c->hi_char = p->phred_max + p->phred_offset;
+    c->lcs_min = p->mask_min_len + 2 * p->mask_reduce;
+    c->hcr_min = p->mask_min_len;
+    c->lcr_min = p->unmask_min_len;
+    c->sticky = p->mask_reduce;
+    c->end_ratio = p->end_ratio;
+    return 0;
+}
+
+static void mask_run_offsets(const int64_t *off, int32_t n, int32_t lcs_min, std::vector<int64_t> &ro) {
+    ro.assign((size_t)n + 1, 0);
+    for (int32_t i = 0; i < n; ++i) ro[i + 1] = ro[i] + mask_run_cap(off[i + 1] - off[i], lcs_min);
+}
+
+extern "C" int pr_mask_bound(const pr_mask_params *p, int32_t n, const int64_t *off, int64_t *mcr_cap) {
+    MaskCfg mc;
+    int rc = mask_cfg(p, &mc);
+    if (rc) return rc;
+    if (n < 0 || (n && !off) || !mcr_cap) return set_error(PR_ERR_ARG, "bad batch");
+    std::vector<int64_t> ro;
+    mask_run_offsets(off, n, mc.lcs_min, ro);
+    *mcr_cap = ro[n];
+    return 0;
+}
+
+static int mask_enqueue(pr_ctx *c, MaskDev &D, const std::vector<int64_t> &ro) {
+    DevBuf *M = c->mb;
+    hipStream_t s = c->stream;
+    const int64_t nr = ro.back();
+    int rc;
+    if ((rc = upload(M[MB_RUN_OFF], ro.data(), ro.size(), s)) || (rc = M[MB_RUNS].ensure((size_t)nr * 8)) ||
+        (rc = M[MB_TMP].ensure((size_t)nr * 8)) || (rc = M[MB_NRUNS].ensure((size_t)(D.n > 0 ? D.n : 1) * 4)) ||
+        (rc = M[MB_ERR].ensure(4)) || (rc = M[MB_STATS].ensure(16)))
+        return rc;
+    D.run_off = M[MB_RUN_OFF].as<int64_t>();
+    D.runs = M[MB_RUNS].as<MaskRun>();
+    D.tmp = M[MB_TMP].as<MaskRun>();
+    D.n_runs = M[MB_NRUNS].as<int32_t>();
+    D.err = M[MB_ERR].as<int32_t>();
+    if (!D.stats) D.stats = M[MB_STATS].as<unsigned long long>();
+    const int e = mask_launch(D, c->n_cu, (void *)s);
+    if (e) return set_error(PR_ERR_HIP, "mask kernel: %s", hipGetErrorString((hipError_t)e));
+    return 0;
+}
+
+static int mask_check_err(pr_ctx *c) {
+    int32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&err, c->mb[MB_ERR].p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (err) return set_error(PR_ERR_CAPACITY, "masking: HCR list exceeded its run capacity");
+    return 0;
+}
+
+extern "C" int pr_mask_run(pr_ctx *c, const pr_mask_params *p, int32_t n, const int64_t *off, const uint8_t *seq,
+                           const uint8_t *qual, uint8_t *out_seq, int64_t *mcr_off, int32_t *mcr, int32_t *n_mcr,
+                           int64_t *stats) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    MaskCfg mc;
+    int rc = mask_cfg(p, &mc);
+    if (rc) return rc;
+    if (n < 0 || (n && (!off || !seq || !qual))) return set_error(PR_ERR_ARG, "bad batch");
+    if (n && off[0] != 0) return set_error(PR_ERR_ARG, "offsets must start at 0");
+    for (int32_t i = 0; i < n; ++i)
+        if (off[i + 1] < off[i]) return set_error(PR_ERR_ARG, "offsets not monotone at %d", i);
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const int64_t nb = n ? off[n] : 0;
+    DevBuf *M = c->mb;
+    if ((rc = upload(M[MB_OFF], off, (size_t)n + 1, s)) || (rc = upload(M[MB_SEQ], seq, (size_t)nb, s)) ||
+        (rc = upload(M[MB_QUAL], qual, (size_t)nb, s)) || (rc = M[MB_OUT].ensure((size_t)nb)))
+        return rc;
+    std::vector<int64_t> ro;
+    mask_run_offsets(n ? off : nullptr, n, mc.lcs_min, ro);
+    MaskDev D{};
+    D.n = n;
+    D.off = M[MB_OFF].as<int64_t>();
+    D.seq = M[MB_SEQ].as<uint8_t>();
+    D.qual = M[MB_QUAL].as<uint8_t>();
+    D.out = M[MB_OUT].as<uint8_t>();
+    D.cfg = mc;
+    if ((rc = mask_enqueue(c, D, ro))) return rc;
+    if ((rc = mask_check_err(c))) return rc;
+    unsigned long long st[2] = {0, 0};
+    if ((rc = download(out_seq, M[MB_OUT], (size_t)nb, s)) || (rc = download(n_mcr, M[MB_NRUNS], (size_t)n, s)) ||
+        (rc = download(reinterpret_cast<MaskRun *>(mcr), M[MB_RUNS], (size_t)ro[n], s)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(st, M[MB_STATS].p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (mcr_off) std::memcpy(mcr_off, ro.data(), ro.size() * sizeof(int64_t));
+    if (stats) {
+        stats[0] = (int64_t)st[0];
+        stats[1] = (int64_t)st[1];
+    }
+    return 0;
+}
+
+extern "C" int pr_iter_mask(pr_ctx *c, const pr_mask_params *p, int64_t *dev_stats) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    if (!c->cns_loaded || !c->cns_launched) return set_error(PR_ERR_ARG, "no consensus launch to mask");
+    MaskCfg mc;
+    int rc = mask_cfg(p, &mc);
+    if (rc) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    DevBuf *B = c->cb;
+    if ((rc = c->mb[MB_OUT].ensure((size_t)(c->seq_cap > 0 ? c->seq_cap : 1)))) return rc;
+    std::vector<int64_t> ro;
+    mask_run_offsets(c->out_off.data(), c->n_lr, mc.lcs_min, ro);
+    MaskDev D{};
+    D.n = c->n_lr;
+    D.off = B[CB_OUT_OFF].as<int64_t>();
+    D.len = B[CB_SEQ_LEN].as<int32_t>();
+    D.status = B[CB_STATUS].as<int32_t>();
+    D.seq = B[CB_O_SEQ].as<uint8_t>();
+    D.qual = B[CB_O_QUAL].as<uint8_t>();
+    D.out = c->mb[MB_OUT].as<uint8_t>();
+    D.stats = reinterpret_cast<unsigned long long *>(dev_stats);
+    D.cfg = mc;
+    if ((rc = mask_enqueue(c, D, ro))) return rc;
+    c->iter_masked = true;
+    return 0;
+}
+
+extern "C" int pr_iter_mask_download(pr_ctx *c, uint8_t *masked) {
+    if (!c || !masked) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->iter_masked) return set_error(PR_ERR_ARG, "no pr_iter_mask launch yet");
+    HIPCHK(hipSetDevice(c->device));
+    int rc = mask_check_err(c);
+    if (rc) return rc;
+    if ((rc = download(masked, c->mb[MB_OUT], (size_t)c->seq_cap, c->stream))) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
 

@@ -70,6 +70,25 @@ class Iteration:
         """Enqueue {corrected bases, bases >= min_phred} into device memory dev_ptr (int64[2])."""
         _abi.check(self.L.pr_iter_stats(self.ctx.h, min_phred, C.c_void_p(dev_ptr)), "pr_iter_stats")
 
+    def mask_to(self, dev_ptr: int, p):
+        """Enqueue the masking of the resident consensus (SeqFilter --phred-mask, proovread:1706);
+        {bases, N bases} (bpt, bpN) go to device memory dev_ptr (int64[2])."""
+        from . import mask
+        mask._setup(self.L)
+        self._mp = p
+        _abi.check(self.L.pr_iter_mask(self.ctx.h, C.byref(p), C.c_void_p(dev_ptr)), "pr_iter_mask")
+
+    def masked(self) -> List[bytes]:
+        """Masked consensus of the last mask_to, one bytes object per long read (status 0 reads)."""
+        a = self.download()
+        buf = np.zeros(self.bounds.seq_cap + 1, np.uint8)
+        _abi.check(self.L.pr_iter_mask_download(self.ctx.h, buf.ctypes.data), "pr_iter_mask_download")
+        out = []
+        for i in range(self.n_lr):
+            o, sl = int(a["out_off"][i]), int(a["seq_len"][i])
+            out.append(buf[o:o + sl].tobytes() if a["status"][i] == 0 else b"")
+        return out
+
     def _out_buffers(self, bin_size=20.0):
         n = self.n_lr
         lens = np.diff(self.d.lr_off)

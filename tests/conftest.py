@@ -6,6 +6,15 @@ sys.path.insert(0, str(HERE))
 sys.path.insert(0, str(HERE / "golden"))
 sys.path.insert(0, str(HERE.parent))
 
+# GPU test modules whose kernels have not yet run on an MI355X run after the rest
+# of the suite, so that under `pytest -x` a failure there cannot hide the results
+# of the validated kernels.
+RUN_LAST = ("test_mask_gpu.py",)
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libprgpu.so on the device)")
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=lambda it: Path(str(it.fspath)).name in RUN_LAST)
