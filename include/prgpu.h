@@ -323,6 +323,26 @@ int pr_iter_mask(pr_ctx *ctx, const pr_mask_params *p, int64_t *dev_stats);
  * pr_cns_out.seq (syncs; PR_ERR_CAPACITY if a run list overflowed) */
 int pr_iter_mask_download(pr_ctx *ctx, uint8_t *masked);
 
+/* ------------------------------------------------------------------ */
+/* final quality trimming: the windows `SeqFilter --trim-win mean,min` keeps
+ * (proovread.cfg:152-155; bin/proovread:919-943), i.e. Fastq::Seq::qual_window
+ * (lib/Fastq/Seq.pm:1064-1160).  Host code (once per job), threads over reads. */
+typedef struct pr_trim_params {
+    int32_t size;          /* Qual_window_size (10)                               */
+    int32_t soft;          /* Qual_window_min_score_soft: window mean (25; --trim-win field 0) */
+    int32_t hard;          /* Qual_window_min_score_hard: any position (3; field 1) */
+    int32_t min_len;       /* Qual_window_min_stretch_length (10)                 */
+    int32_t phred_offset;  /* 33                                                   */
+} pr_trim_params;
+void pr_trim_params_default(pr_trim_params *p);
+int pr_trim_params_parse(const char *trim_win, pr_trim_params *p);   /* "12,5" */
+/* window capacity (pairs) of a batch */
+int pr_trim_bound(const pr_trim_params *p, int32_t n, const int64_t *off, int64_t *win_cap);
+/* windows of read i: (offset, length) pairs at win[2*win_off[i]], n_win[i] of them, in
+ * read order; win_off[n+1] is filled (capacity prefix).  n_threads <= 0: all cores. */
+int pr_trim_windows(const pr_trim_params *p, int32_t n, const int64_t *off, const uint8_t *qual, int64_t *win_off,
+                    int32_t *win, int32_t *n_win, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,25 +19,22 @@ Pure-Python restatement of proovread's read post-processing (SURVEY.md §8f.2,
                   mask-reduce         -> hcr_sticky_length (per side)
                   mask-end-ratio      -> lcr_end_ratio
                   Qual_lcs_min_length = hcr_min + 2 * sticky (sam2cns:434).
-                The restatement is pinned to that Perl (tests/golden/
-                gen_seqfilter_golden.pl); the mapping onto SeqFilter's fields is
-                unpinned (DESIGN.md).
+                Pinning: the HCR search (qual_lcs) is checked against the
+                reference module's own output (tests/golden/seqfilter_expected.txt,
+                gen_seqfilter_golden.pl).  The sticky / end / gap rounds are
+                restated from reading the commented-out sub, which cannot be run
+                without extracting its text (not done); they and the
+                field mapping onto SeqFilter are parity unpinned.
   qual_window   Fastq::Seq::qual_window and its _qw_slide_* helpers (Seq.pm:
                 1064-1160), the windows `SeqFilter --trim-win mean,min` keeps
                 (proovread.cfg:152-155), including the Perl quirks (low-slide
                 window update subtracts X[I-W+1]; `A || B && return` precedence).
-  chim_filter   bin/ChimeraToSeqFilter.pl:171-201 (the header line is skipped,
-                the first line of each read is never added, the last read is never
-                flushed, --trim-length is unused).
-  seqfilter_*   the SeqFilter glue proovread relies on (substr by chimera
-                coordinates, trim windows, --min-length): unpinned.
 """
 from __future__ import annotations
 
 import copy
 import dataclasses
-import re
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import List, Sequence, Tuple
 
 
 # ---------------------------------------------------------------- masking
@@ -250,84 +247,3 @@ def qual_window(phreds: Sequence[int], P: WinParams) -> List[Tuple[int, int]]:
         if h:
             out.append(h)
     return out
-
-
-# ---------------------------------------------------------------- chimera filter
-
-def chim_filter(lines: Sequence[str], min_score: float = 0.01) -> List[str]:
-    """bin/ChimeraToSeqFilter.pl:171-201 on the lines of a bam2cns .chim.tsv -> output lines."""
-    out = []
-    rid, coords = "", []
-    for raw in list(lines)[1:]:   # :176 first line is a header
-        f = raw.rstrip("\n").split("\t")
-        id_, fr, to, score = (f + ["", "", "", ""])[:4]
-        if id_ != rid:
-            if coords:
-                c = ["0"] + coords
-                i = 0
-                while i < len(c) - 1:
-                    out.append(f"{rid}\t{c[i]}\t{c[i + 1]}")
-                    i += 2
-                out.append(f"{rid}\t{c[i]}")
-            rid, coords = id_, []
-        else:
-            if _perl_num(score) >= min_score:
-                coords += [fr, to]
-    return out
-
-
-def _perl_num(s: str) -> float:
-    m = re.match(r"\s*([+-]?(?:\d+\.?\d*(?:[eE][+-]?\d+)?|\.\d+(?:[eE][+-]?\d+)?))", s)
-    return float(m.group(1)) if m else 0.0
-
-
-# ---------------------------------------------------------------- SeqFilter glue (unpinned)
-
-def parse_substr(lines: Sequence[str]) -> Dict[str, List[Tuple[int, Optional[int]]]]:
-    """ChimeraToSeqFilter output -> id: [(start, end or None)] (end None = to the read end)."""
-    d: Dict[str, List[Tuple[int, Optional[int]]]] = {}
-    for ln in lines:
-        f = ln.rstrip("\n").split("\t")
-        if len(f) < 2 or not f[0]:
-            continue
-        d.setdefault(f[0], []).append((int(f[1]), int(f[2]) if len(f) > 2 and f[2] != "" else None))
-    return d
-
-
-def substr_pieces(L: int, ranges: Sequence[Tuple[int, Optional[int]]]) -> List[Tuple[int, int]]:
-    out = []
-    for s, e in ranges:
-        e = L if e is None else min(e, L)
-        s = max(0, min(s, L))
-        out.append((s, max(0, e - s)))
-    return out
-
-
-def seqfilter_trim(records, P: WinParams, min_length: int, substr=None, phred_offset: int = 33):
-    """records: [(id, desc, seq, qual)] -> trimmed records, the order SeqFilter writes them.
-
-    Per read: pieces from --substr (one piece keeps the id, several become id.1, id.2 ...
-    like Fastq::Seq::substr_seq, Seq.pm:813-876), then the --trim-win windows of every
-    piece (same naming), then --min-length.  Descriptions gain SUBSTR:offset,length."""
-    out = []
-    for rid, desc, seq, qual in records:
-        pieces = [(rid, desc, seq, qual)]
-        if substr and rid in substr:
-            pieces = _split(rid, desc, seq, qual, substr_pieces(len(seq), substr[rid]))
-        for pid, pdesc, ps, pq in pieces:
-            wins = qual_window([c - phred_offset for c in pq], P)
-            for wid, wdesc, ws, wq in _split(pid, pdesc, ps, pq, wins):
-                if len(ws) >= min_length:
-                    out.append((wid, wdesc, ws, wq))
-    return out
-
-
-def _split(rid, desc, seq, qual, ranges):
-    if not ranges:
-        return []
-    res = []
-    many = len(ranges) > 1
-    for k, (o, l) in enumerate(ranges, 1):
-        d = f"SUBSTR:{o},{l}"
-        res.append((f"{rid}.{k}" if many else rid, f"{desc} {d}" if desc else d, seq[o:o + l], qual[o:o + l]))
-    return res
