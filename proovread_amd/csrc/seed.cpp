@@ -26,13 +26,14 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
-#include <map>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/prgpu.h"
+#include "seed_core.h"
+
+namespace seedc = prgpu::seedc;
 
 int pr_set_error(int code, const char *msg);
 
@@ -115,125 +116,6 @@ struct IndexOcc {
     void positions(int a, int b, std::vector<uint32_t> &pos) const { occ(I, q, a, b, &pos); }
 };
 
-// Per-read occurrence table (the seeding path): for every start a of the read, the
-// 12-mer hits of q[a, a+12) with their exact match length ml = LCP(q[a..], T[p..])
-// (>= 12).  occ(q[a, b)) for b - a >= 12 is #{hits of a: ml >= b - a}: a per-start
-// table ge[a][t] = #{ml >= 12 + t} for t < HB, a scan of the start's hits beyond;
-// shorter strings use the j-mer count tables.  Match lengths follow diagonals (when
-// p-1 is a hit of a-1 with ml >= 13, p is a hit of a with ml - 1); a new diagonal
-// compares the KX bases stored after the hit (kext, contiguous with kpos) and only
-// goes on in the text after a full KX-base match.  Same counts as IndexOcc, one pass
-// over the hits per read; the buffers are reused across the reads of a thread.
-constexpr int HB = 20;
-
-struct ReadOcc {
-    const Index *I = nullptr;
-    const uint8_t *q = nullptr;
-    int len = 0;
-    std::vector<int32_t> hoff;    // [len + 1]
-    std::vector<uint32_t> hpos;   // hits of start a at [hoff[a], hoff[a+1]), text order
-    std::vector<uint16_t> hml;    // their match lengths
-    std::vector<uint64_t> qext;   // per start a: pack_ext of q[a+12, a+12+KX)
-    std::vector<int32_t> ge;      // [len * HB]
-    std::vector<int64_t> codes;   // 12-mer code per start, -1 with N
-
-    void build(const Index &I_, const uint8_t *q_, int len_) {
-        I = &I_;
-        q = q_;
-        len = len_;
-        hoff.assign((size_t)len + 1, 0);
-        qext.assign((size_t)len + 1, 0);
-        hpos.clear();
-        hml.clear();
-        ge.assign((size_t)len * HB, 0);
-        for (int a = 0; a + KI <= len; ++a) {
-            const int n = len - a - KI;
-            qext[a] = pack_ext(q + a + KI, n < KX ? n : KX);
-        }
-        const uint8_t *T = I->text.data();
-        uint32_t code = 0;
-        int run = 0;
-        int32_t prev0 = 0, prev1 = 0;   // hits of start a-1
-        // 12-mer code of every start (-1: contains N), then software prefetch of the
-        // random koff / kpos / kext lines a few starts ahead (the loop is latency bound)
-        codes.assign((size_t)len + 1, -1);
-        for (int e = 0; e < len; ++e) {
-            if (q[e] > 3) {
-                run = 0;
-                code = 0;
-            } else {
-                code = ((code << 2) | q[e]) & (NK - 1);
-                ++run;
-            }
-            if (e - KI + 1 >= 0 && run >= KI) codes[e - KI + 1] = (int64_t)code;
-        }
-        constexpr int PF_OFF = 24, PF_POS = 12;
-        for (int a = 0; a < PF_OFF && a < len; ++a)
-            if (codes[a] >= 0) __builtin_prefetch(&I->koff[(size_t)codes[a]]);
-        for (int e = KI - 1; e < len; ++e) {   // e = last base of the 12-mer starting at a = e - 11
-            const int a = e - KI + 1;
-            if (a + PF_OFF < len && codes[a + PF_OFF] >= 0) __builtin_prefetch(&I->koff[(size_t)codes[a + PF_OFF]]);
-            if (a + PF_POS < len && codes[a + PF_POS] >= 0) {
-                const uint32_t r0 = I->koff[(size_t)codes[a + PF_POS]];
-                __builtin_prefetch(&I->kpos[r0]);
-                __builtin_prefetch(&I->kext[r0]);
-                __builtin_prefetch(&I->kext[r0] + 8);
-            }
-            run = codes[a] >= 0 ? KI : 0;
-            code = codes[a] >= 0 ? (uint32_t)codes[a] : 0;
-            hoff[a] = (int32_t)hpos.size();
-            if (run >= KI) {
-                int32_t k = prev0;
-                int32_t *g = ge.data() + (size_t)a * HB;
-                for (uint32_t r = I->koff[code]; r < I->koff[code + 1]; ++r) {
-                    const uint32_t p = I->kpos[r];
-                    while (k < prev1 && hpos[k] + 1 < p) ++k;
-                    int ml;
-                    if (k < prev1 && hpos[k] + 1 == p && hml[k] > KI) {
-                        ml = hml[k] - 1;
-                    } else {
-                        const uint64_t ex = I->kext[r];
-                        const uint64_t qe = qext[a];
-                        const int le = (int)(ex >> 56), lq = (int)(qe >> 56);
-                        const uint64_t x = (ex ^ qe) & KX_MASK;
-                        int m = x ? __builtin_ctzll(x) >> 1 : KX;
-                        m = m < le ? m : le;
-                        m = m < lq ? m : lq;
-                        ml = KI + m;
-                        if (m == KX)
-                            while (a + ml < len && q[a + ml] < 4 && T[p + ml] == q[a + ml]) ++ml;
-                    }
-                    hpos.push_back(p);
-                    hml.push_back((uint16_t)(ml < 65535 ? ml : 65535));
-                    ++g[ml - KI < HB - 1 ? ml - KI : HB - 1];
-                }
-                for (int t = HB - 2; t >= 0; --t) g[t] += g[t + 1];
-            }
-            prev0 = hoff[a];
-            prev1 = (int32_t)hpos.size();
-        }
-        for (int a = len - KI + 1 < 0 ? 0 : len - KI + 1; a <= len; ++a) hoff[a] = (int32_t)hpos.size();
-    }
-    int64_t operator()(int a, int b) const {
-        const int n = b - a;
-        if (n < KI) {
-            uint32_t code = 0;
-            for (int x = a; x < b; ++x) code = (code << 2) | q[x];
-            return I->cnt[n - 1][code];
-        }
-        if (n - KI < HB) return ge[(size_t)a * HB + (n - KI)];
-        int64_t c = 0;
-        for (int32_t k = hoff[a]; k < hoff[a + 1]; ++k) c += hml[k] >= n;
-        return c;
-    }
-    void positions(int a, int b, std::vector<uint32_t> &pos) const {
-        pos.clear();
-        const int n = b - a;
-        for (int32_t k = hoff[a]; k < hoff[a + 1]; ++k)
-            if (hml[k] >= n) pos.push_back(hpos[k]);
-    }
-};
-
 // bwt_smem1a (max_intv = 0): SMEMs covering x with >= min_intv occurrences, sorted by start;
 // returns the end of the longest forward match from x (the next x of the caller)
 template <class Occ>
@@ -299,263 +181,88 @@ int seed_strategy1(const Occ &occ, const uint8_t *q, int len, int x, int min_len
     return len;
 }
 
-struct Seed {
-    int64_t rbeg;   // forward-reverse coordinate (bwa): reverse strand >= l_pac
-    int qbeg, len;
-};
-// A chain's seeds are a linked list in the read's seed pool (seeds are only ever
-// appended), so chaining allocates nothing per chain.
-struct Chain {
-    int64_t pos;
-    int rid;
-    int32_t head, tail, n;   // first / last seed in the pool, seed count
-    int w, kept, first;
-};
-struct SeedPool {
-    std::vector<Seed> s;
-    std::vector<int32_t> next;
-    int32_t add(const Seed &x) {
-        s.push_back(x);
-        next.push_back(-1);
-        return (int32_t)s.size() - 1;
-    }
-    void append(Chain &c, const Seed &x) {
-        const int32_t k = add(x);
-        next[c.tail] = k;
-        c.tail = k;
-        ++c.n;
-    }
-};
-
-// text position -> bwa forward-reverse coordinate and contig (long read) id
-inline void text_to_fr(const Index &I, uint32_t p, int64_t &fr, int &rid) {
-    const int c = contig_of(I, p);
-    const int64_t o = (int64_t)p - I.cstart[c];
-    if (c < I.n_lr) {
-        rid = c;
-        fr = I.lr_off[c] + o;
-    } else {
-        rid = 2 * I.n_lr - 1 - c;   // reverse half holds the long reads in reverse order
-        fr = I.l_pac + (I.l_pac - I.lr_off[rid + 1]) + o;
-    }
+// Host path: the shared core (seed_core.h) over a view of this index, with scratch
+// that grows when a read outgrows it (the device path flags such reads instead).
+seedc::IndexView view_of(const Index &I) {
+    seedc::IndexView v{};
+    v.text = I.text.data();
+    v.n_text = (int64_t)I.text.size();
+    v.cstart = I.cstart.data();
+    v.n_contig = (int32_t)I.cstart.size();
+    v.cblk = I.cblk.data();
+    v.lr_off = I.lr_off.data();
+    v.n_lr = I.n_lr;
+    v.l_pac = I.l_pac;
+    v.koff = I.koff.data();
+    v.kpos = I.kpos.data();
+    v.kext = I.kext.data();
+    for (int j = 0; j < KI - 1; ++j) v.cnt[j] = I.cnt[j].data();
+    return v;
 }
 
-bool test_and_merge(const pr_seed_opts &O, int64_t l_pac, SeedPool &P, Chain &c, const Seed &p, int rid) {
-    const Seed &last = P.s[c.tail];
-    const Seed &first = P.s[c.head];
-    const int64_t qend = last.qbeg + last.len, rend = last.rbeg + last.len;
-    if (rid != c.rid) return false;
-    if (p.qbeg >= first.qbeg && p.qbeg + p.len <= qend && p.rbeg >= first.rbeg && p.rbeg + p.len <= rend)
-        return true;   // contained seed
-    if ((last.rbeg < l_pac || first.rbeg < l_pac) && p.rbeg >= l_pac) return false;   // other strand
-    const int64_t x = p.qbeg - last.qbeg, y = p.rbeg - last.rbeg;
-    if (y >= 0 && x - y <= O.w && y - x <= O.w && x - last.len < O.max_chain_gap && y - last.len < O.max_chain_gap) {
-        P.append(c, p);
-        return true;
-    }
-    return false;
-}
+struct HostScratch {
+    std::vector<int32_t> hoff, codes;
+    std::vector<uint64_t> qext;
+    std::vector<uint32_t> ge, hpos;
+    std::vector<uint16_t> hml;
+    std::vector<seedc::Iv> mems, m1, curr, prev;
+    std::vector<seedc::Seed> seeds;
+    std::vector<int32_t> next, ord, kept;
+    std::vector<seedc::Chain> cv, ch;
+    std::vector<pr_seed_task> out;
+    seedc::Scratch S{};
+    int lmax = 0, hits = 1 << 14, iv = 256, mems_cap = 1024, seeds_cap = 4096, chains = 2048, out_cap = 512;
 
-int chain_weight(const SeedPool &P, const Chain &c) {
-    int64_t end = 0;
-    int w = 0;
-    for (int32_t k = c.head; k >= 0; k = P.next[k]) {
-        const Seed &s = P.s[k];
-        if (s.qbeg >= end) w += s.len;
-        else if (s.qbeg + s.len > end) w += (int)(s.qbeg + s.len - end);
-        end = end > s.qbeg + s.len ? end : s.qbeg + s.len;
+    void size(int len) {
+        lmax = len > lmax ? len : lmax;
+        hoff.resize((size_t)lmax + 1);
+        codes.resize((size_t)lmax + 1);
+        qext.resize((size_t)lmax + 1);
+        ge.resize((size_t)lmax * seedc::HB + 1);
+        hpos.resize((size_t)hits);
+        hml.resize((size_t)hits);
+        mems.resize((size_t)mems_cap);
+        m1.resize((size_t)iv);
+        curr.resize((size_t)iv);
+        prev.resize((size_t)iv);
+        seeds.resize((size_t)seeds_cap);
+        next.resize((size_t)seeds_cap);
+        cv.resize((size_t)chains);
+        ch.resize((size_t)chains);
+        ord.resize((size_t)chains);
+        kept.resize((size_t)chains);
+        out.resize((size_t)out_cap);
+        S = seedc::Scratch{lmax,        hoff.data(),  qext.data(), codes.data(), ge.data(),   hpos.data(),
+                           hml.data(),  hits,         mems.data(), mems_cap,     m1.data(),   curr.data(),
+                           prev.data(), iv,           seeds.data(), next.data(), seeds_cap,   cv.data(),
+                           ch.data(),   ord.data(),   kept.data(), chains};
     }
-    const int tmp = w;
-    w = 0;
-    end = 0;
-    for (int32_t k = c.head; k >= 0; k = P.next[k]) {
-        const Seed &s = P.s[k];
-        if (s.rbeg >= end) w += s.len;
-        else if (s.rbeg + s.len > end) w += (int)(s.rbeg + s.len - end);
-        end = end > s.rbeg + s.len ? end : s.rbeg + s.len;
+    void grow(int err) {
+        if (err & seedc::SC_OVER_HITS) hits *= 2;
+        if (err & seedc::SC_OVER_IV) iv *= 2;
+        if (err & seedc::SC_OVER_MEMS) mems_cap *= 2;
+        if (err & seedc::SC_OVER_SEEDS) seeds_cap *= 2;
+        if (err & seedc::SC_OVER_CHAINS) chains *= 2;
+        if (err & seedc::SC_OVER_OUT) out_cap *= 2;
     }
-    w = w < tmp ? w : tmp;
-    return w < (1 << 30) ? w : (1 << 30) - 1;
-}
+};
 
 struct ReadOut {
     std::vector<pr_seed_task> tasks;
 };
 
-inline int cal_max_gap(const pr_seed_opts &O, int qlen) {
-    int l_del = (int)((double)(qlen * O.a - O.o_del) / O.e_del + 1.);
-    int l_ins = (int)((double)(qlen * O.a - O.o_ins) / O.e_ins + 1.);
-    int l = l_del > l_ins ? l_del : l_ins;
-    l = l > 1 ? l : 1;
-    return l < O.w << 1 ? l : O.w << 1;
-}
-
-std::vector<uint32_t> &tl_pos() {
-    static thread_local std::vector<uint32_t> v;
-    return v;
-}
-std::vector<Chain> &tl_chains() {
-    static thread_local std::vector<Chain> v;
-    return v;
-}
-
-void map_read(const Index &I, const pr_seed_opts &O, const uint8_t *q, int len, int sid, ReadOut &out) {
-    static thread_local ReadOcc R;
-    static thread_local SeedPool P;
-    static thread_local std::vector<Chain> cv;     // chains, creation order
-    static thread_local std::vector<int32_t> ord;  // chain ids sorted by pos (mem_chain's btree order)
-    R.build(I, q, len);
-    // mem_collect_intv
-    std::vector<Iv> mems, m1;
-    for (int x = 0; x < len;) {
-        if (q[x] < 4) {
-            x = smem1(R, q, len, x, 1, m1);
-            for (const Iv &p : m1)
-                if (p.end - p.start >= O.min_seed_len) mems.push_back(p);
-        } else {
-            ++x;
+void map_read(const seedc::IndexView &V, const pr_seed_opts &O, const uint8_t *q, int len, int sid, ReadOut &res) {
+    static thread_local HostScratch H;
+    if (len > H.lmax || H.S.hoff == nullptr) H.size(len);
+    for (;;) {
+        int n = 0;
+        const int err = seedc::map_read(V, O, H.S, q, len, sid, H.out.data(), H.out_cap, &n);
+        if (!err) {
+            res.tasks.assign(H.out.begin(), H.out.begin() + n);
+            return;
         }
-    }
-    const int split_len = (int)(O.min_seed_len * O.split_factor + .499);
-    const size_t n1 = mems.size();
-    for (size_t k = 0; k < n1; ++k) {
-        const Iv p = mems[k];
-        if (p.end - p.start < split_len || p.occ > O.split_width) continue;
-        smem1(R, q, len, (p.start + p.end) >> 1, p.occ + 1, m1);
-        for (const Iv &r : m1)
-            if (r.end - r.start >= O.min_seed_len) mems.push_back(r);
-    }
-    if (O.max_mem_intv > 0) {
-        for (int x = 0; x < len;) {
-            if (q[x] < 4) {
-                Iv m;
-                x = seed_strategy1(R, q, len, x, O.min_seed_len, O.max_mem_intv, m);
-                if (m.occ > 0) mems.push_back(m);
-            } else {
-                ++x;
-            }
-        }
-    }
-    std::stable_sort(mems.begin(), mems.end(), [](const Iv &a, const Iv &b) {
-        return a.start != b.start ? a.start < b.start : a.end < b.end;
-    });
-    // mem_chain: every occurrence is merged into the chain with the largest pos <= its
-    // rbeg, else it opens a chain inserted after the chains of equal pos (btree order)
-    P.s.clear();
-    P.next.clear();
-    cv.clear();
-    ord.clear();
-    std::vector<uint32_t> &pos = tl_pos();
-    for (const Iv &p : mems) {
-        const int slen = p.end - p.start;
-        R.positions(p.start, p.end, pos);   // text-position order (12-mer lists are position-sorted)
-        const int64_t np = (int64_t)pos.size();
-        const int64_t step = np > O.max_occ ? np / O.max_occ : 1;
-        int64_t count = 0;
-        for (int64_t k = 0; k < np && count < O.max_occ; k += step, ++count) {
-            Seed s;
-            int rid;
-            text_to_fr(I, pos[k], s.rbeg, rid);
-            s.qbeg = p.start;
-            s.len = slen;
-            // first chain with pos > rbeg
-            size_t lo = 0, hi = ord.size();
-            while (lo < hi) {
-                const size_t mid = (lo + hi) >> 1;
-                if (cv[ord[mid]].pos <= s.rbeg) lo = mid + 1;
-                else hi = mid;
-            }
-            if (lo > 0 && test_and_merge(O, I.l_pac, P, cv[ord[lo - 1]], s, rid)) continue;
-            Chain c;
-            c.pos = s.rbeg;
-            c.rid = rid;
-            c.head = c.tail = P.add(s);
-            c.n = 1;
-            c.w = c.kept = 0;
-            c.first = -1;
-            cv.push_back(c);
-            ord.insert(ord.begin() + (ptrdiff_t)lo, (int32_t)cv.size() - 1);
-        }
-    }
-    std::vector<Chain> &ch = tl_chains();
-    ch.clear();
-    for (int32_t id : ord) ch.push_back(cv[id]);
-    // mem_chain_flt
-    {
-        size_t k = 0;
-        for (size_t i = 0; i < ch.size(); ++i) {
-            ch[i].w = chain_weight(P, ch[i]);
-            if (ch[i].w >= O.min_chain_weight) {
-                if (k != i) ch[k] = ch[i];
-                ++k;
-            }
-        }
-        ch.resize(k);
-    }
-    if (!ch.empty()) {
-        std::stable_sort(ch.begin(), ch.end(), [](const Chain &a, const Chain &b) { return a.w > b.w; });
-        auto cbeg = [&](const Chain &c) { return P.s[c.head].qbeg; };
-        auto cend = [&](const Chain &c) { return P.s[c.tail].qbeg + P.s[c.tail].len; };
-        std::vector<int> kept_idx{0};
-        ch[0].kept = 3;
-        for (size_t i = 1; i < ch.size(); ++i) {
-            int large = 0;
-            size_t k;
-            for (k = 0; k < kept_idx.size(); ++k) {
-                Chain &cj = ch[kept_idx[k]];
-                const int bmax = cbeg(cj) > cbeg(ch[i]) ? cbeg(cj) : cbeg(ch[i]);
-                const int emin = cend(cj) < cend(ch[i]) ? cend(cj) : cend(ch[i]);
-                if (emin > bmax) {
-                    const int li = cend(ch[i]) - cbeg(ch[i]), lj = cend(cj) - cbeg(cj);
-                    const int minl = li < lj ? li : lj;
-                    if (emin - bmax >= minl * O.mask_level && minl < O.max_chain_gap) {
-                        large = 1;
-                        if (cj.first < 0) cj.first = (int)i;
-                        if (ch[i].w < cj.w * O.drop_ratio && cj.w - ch[i].w >= O.min_seed_len << 1) break;
-                    }
-                }
-            }
-            if (k == kept_idx.size()) {
-                kept_idx.push_back((int)i);
-                ch[i].kept = large ? 2 : 3;
-            }
-        }
-        for (int j : kept_idx)
-            if (ch[j].first >= 0) ch[ch[j].first].kept = 1;
-    }
-    // mem_chain2aln: the best seed of every kept chain, and the chain's reference window
-    for (const Chain &c : ch) {
-        if (c.kept == 0) continue;
-        int32_t best = c.head;
-        for (int32_t k = P.next[c.head]; k >= 0; k = P.next[k])
-            if (P.s[k].len >= P.s[best].len) best = k;   // srt order: (score, index), last wins
-        const Seed &s = P.s[best];
-        const bool rev = s.rbeg >= I.l_pac;
-        const int64_t L = I.lr_off[c.rid + 1] - I.lr_off[c.rid];
-        // strand coordinates: forward long read, or its reverse complement
-        const int64_t cs = rev ? I.l_pac + (I.l_pac - I.lr_off[c.rid + 1]) : I.lr_off[c.rid];
-        int64_t r0 = INT64_MAX, r1 = INT64_MIN;
-        for (int32_t k = c.head; k >= 0; k = P.next[k]) {
-            const Seed &t = P.s[k];
-            const int64_t b = t.rbeg - (t.qbeg + cal_max_gap(O, t.qbeg));
-            const int64_t e = t.rbeg + t.len + ((len - t.qbeg - t.len) + cal_max_gap(O, len - t.qbeg - t.len));
-            r0 = r0 < b ? r0 : b;
-            r1 = r1 > e ? r1 : e;
-        }
-        r0 -= cs;
-        r1 -= cs;
-        pr_seed_task t;
-        t.sr = sid;
-        t.lr = c.rid;
-        t.strand = rev ? 1 : 0;
-        t.qbeg = s.qbeg;
-        t.rbeg = (int32_t)(s.rbeg - cs);
-        t.slen = s.len;
-        t.rmax0 = (int32_t)(r0 > 0 ? r0 : 0);
-        t.rmax1 = (int32_t)(r1 < L ? r1 : L);
-        t.weight = c.w;
-        t.nseed = c.n;
-        out.tasks.push_back(t);
+        H.grow(err);
+        H.size(len);
     }
 }
 
@@ -719,6 +426,7 @@ extern "C" int pr_seed_map(const pr_seed_index *h, const pr_seed_opts *o, const 
     int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
     nt = nt < 1 ? 1 : (nt > 256 ? 256 : nt);
     std::vector<ReadOut> res(n_sr);
+    const seedc::IndexView V = view_of(h->I);
     std::atomic<int> next{0};
     auto work = [&]() {
         std::vector<uint8_t> q;
@@ -729,7 +437,7 @@ extern "C" int pr_seed_map(const pr_seed_index *h, const pr_seed_opts *o, const 
                 const int len = (int)(sr_off[i + 1] - sr_off[i]);
                 q.assign(sr_seq + sr_off[i], sr_seq + sr_off[i + 1]);
                 for (auto &c : q) c = c < 4 ? c : 4;
-                if (len > 0) map_read(h->I, *o, q.data(), len, i, res[i]);
+                if (len > 0) map_read(V, *o, q.data(), len, i, res[i]);
             }
         }
     };

@@ -1,0 +1,573 @@
+// Seeding and chaining of one short read: the part of
+// `bwa-proovread mem` that turns a read into seed-extension tasks.  One
+// implementation for the host path (seed.cpp, scratch that grows on demand)
+// and the device path (seed_kernels.hip, one lane per read, fixed scratch per
+// lane; a read that outgrows it is flagged, never silently changed).
+//
+// Restates upstream bwa (absent submodule, .gitmodules:4-6; parity unpinned,
+// DESIGN.md) over the index of seed.cpp:
+//   mem_collect_intv  bwt_smem1a SMEMs >= -k, re-seeding of long SMEMs with
+//                     <= split_width hits (-r), bwt_seed_strategy1 (-y)
+//   mem_chain         occurrences (<= -c per SMEM, sampled in text order), each
+//                     merged into the chain with the largest pos <= its rbeg by
+//                     test_and_merge or opening a new chain after the chains of
+//                     equal pos (the btree order)
+//   mem_chain_flt     chain weight, -W minimum, stable sort, -D / mask_level
+//   mem_chain2aln     the chain's best seed (longest, last on ties) and the
+//                     chain's reference window (cal_max_gap over its seeds)
+// Occurrence counts come from a per-read table: for every start a, the hits of
+// the 12-mer q[a, a+12) with their exact match length ml = LCP(q[a..], T[p..]);
+// occ(q[a, b)) = #{hits of a with ml >= b - a} (a per-start count table for
+// ml < 12 + HB), j-mer count tables below 12.  Match lengths follow diagonals
+// (p-1 a hit of a-1 with ml >= 13 -> p a hit of a with ml - 1); a new diagonal
+// compares the KX bases the index stores after the hit (kext) and reads the
+// text only after a full KX-base match.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/prgpu.h"
+
+#if defined(__HIPCC__)
+#define SC_HD __host__ __device__ inline
+#else
+#define SC_HD inline
+#endif
+
+namespace prgpu {
+namespace seedc {
+
+constexpr int KI = 12;                        // indexed k-mer length
+constexpr uint32_t NK = 1u << (2 * KI);       // 4^12
+constexpr int KX = 28;                        // bases stored after each hit
+constexpr uint64_t KX_MASK = (1ull << (2 * KX)) - 1;
+constexpr int HB = 20;                        // per-start count table width
+constexpr int CB_SHIFT = 12;                  // contig block table granularity
+
+// Device- or host-resident index, plain pointers (built by seed.cpp).
+struct IndexView {
+    const uint8_t *text;       // forward long reads, then rc of their concatenation, SEP (5) after each
+    int64_t n_text;
+    const int64_t *cstart;     // [n_contig] text offset of contig c
+    int32_t n_contig;          // 2 * n_lr
+    const int32_t *cblk;       // contig at the start of every 2^CB_SHIFT text block
+    const int64_t *lr_off;     // [n_lr + 1] forward long-read offsets
+    int32_t n_lr;
+    int64_t l_pac;
+    const uint32_t *koff;      // [NK + 1]
+    const uint32_t *kpos;      // 12-mer hits, text order within a k-mer
+    const uint64_t *kext;      // per hit: KX bases after it (2 bits each) | count << 56
+    const uint32_t *cnt[KI - 1];   // cnt[j-1][code]: occurrences of the j-mer `code`, j = 1..11
+};
+
+struct Iv {
+    int32_t start, end;
+    int64_t occ;
+};
+struct Seed {
+    int64_t rbeg;   // forward-reverse coordinate (bwa): reverse strand >= l_pac
+    int32_t qbeg, len;
+};
+struct Chain {
+    int64_t pos;
+    int32_t rid, head, tail, n;   // seeds: a linked list in the pool (only ever appended)
+    int32_t w, kept, first;
+};
+
+enum {
+    SC_OVER_LEN = 1, SC_OVER_HITS = 2, SC_OVER_IV = 4, SC_OVER_MEMS = 8, SC_OVER_SEEDS = 16,
+    SC_OVER_CHAINS = 32, SC_OVER_OUT = 64
+};
+
+// Scratch of one read (host: vectors; device: a lane's slice of a global buffer).
+struct Scratch {
+    int32_t lmax;                              // longest read the per-start arrays hold
+    int32_t *hoff;                             // [lmax + 1]
+    uint64_t *qext;                            // [lmax + 1]
+    int32_t *codes;                            // [lmax + 1]
+    uint32_t *ge;                              // [lmax * HB]
+    uint32_t *hpos;                            // [cap_hits]
+    uint16_t *hml;                             // [cap_hits]
+    int32_t cap_hits;
+    Iv *mems;                                  // [cap_mems]
+    int32_t cap_mems;
+    Iv *m1, *curr, *prev;                      // [cap_iv] each
+    int32_t cap_iv;
+    Seed *seeds;                               // [cap_seeds]
+    int32_t *next;                             // [cap_seeds]
+    int32_t cap_seeds;
+    Chain *cv, *ch;                            // [cap_chains] each
+    int32_t *ord, *kept;                       // [cap_chains] each
+    int32_t cap_chains;
+};
+
+SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
+    uint64_t v = 0;
+    int k = 0;
+    for (; k < n && s[k] < 4; ++k) v |= (uint64_t)s[k] << (2 * k);
+    return v | ((uint64_t)k << 56);
+}
+
+SC_HD int ctz64(uint64_t x) { return __builtin_ctzll(x); }
+
+// ---------------------------------------------------------------- occurrence table
+struct Occ {
+    const IndexView *I;
+    const Scratch *S;
+    const uint8_t *q;
+    int len;
+
+    SC_HD int64_t operator()(int a, int b) const {
+        const int n = b - a;
+        if (n < KI) {
+            uint32_t code = 0;
+            for (int x = a; x < b; ++x) code = (code << 2) | q[x];
+            return I->cnt[n - 1][code];
+        }
+        if (n - KI < HB) return S->ge[(int64_t)a * HB + (n - KI)];
+        int64_t c = 0;
+        for (int32_t k = S->hoff[a]; k < S->hoff[a + 1]; ++k) c += S->hml[k] >= n;
+        return c;
+    }
+};
+
+// -> 0 or SC_OVER_*
+SC_HD int build_occ(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
+    if (len > S.lmax) return SC_OVER_LEN;
+    for (int a = 0; a <= len; ++a) {
+        S.hoff[a] = 0;
+        S.codes[a] = -1;
+        S.qext[a] = 0;
+    }
+    for (int64_t k = 0; k < (int64_t)len * HB; ++k) S.ge[k] = 0;
+    for (int a = 0; a + KI <= len; ++a) {
+        const int n = len - a - KI;
+        S.qext[a] = pack_ext(q + a + KI, n < KX ? n : KX);
+    }
+    {
+        uint32_t code = 0;
+        int run = 0;
+        for (int e = 0; e < len; ++e) {
+            if (q[e] > 3) {
+                run = 0;
+                code = 0;
+            } else {
+                code = ((code << 2) | q[e]) & (NK - 1);
+                ++run;
+            }
+            if (e - KI + 1 >= 0 && run >= KI) S.codes[e - KI + 1] = (int32_t)code;
+        }
+    }
+    const uint8_t *T = I.text;
+    int32_t nh = 0, prev0 = 0, prev1 = 0;   // hits of start a-1: [prev0, prev1)
+    for (int a = 0; a + KI <= len; ++a) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+        constexpr int PF_OFF = 24, PF_POS = 12;   // latency-bound on the host: prefetch ahead
+        if (a + PF_OFF < len && S.codes[a + PF_OFF] >= 0) __builtin_prefetch(&I.koff[S.codes[a + PF_OFF]]);
+        if (a + PF_POS < len && S.codes[a + PF_POS] >= 0) {
+            const uint32_t r0 = I.koff[S.codes[a + PF_POS]];
+            __builtin_prefetch(&I.kpos[r0]);
+            __builtin_prefetch(&I.kext[r0]);
+            __builtin_prefetch(&I.kext[r0] + 8);
+        }
+#endif
+        S.hoff[a] = nh;
+        if (S.codes[a] >= 0) {
+            const uint32_t code = (uint32_t)S.codes[a];
+            const uint32_t r0 = I.koff[code], r1 = I.koff[code + 1];
+            if ((int64_t)nh + (r1 - r0) > S.cap_hits) return SC_OVER_HITS;
+            uint32_t *g = S.ge + (int64_t)a * HB;
+            int32_t k = prev0;
+            for (uint32_t r = r0; r < r1; ++r) {
+                const uint32_t p = I.kpos[r];
+                while (k < prev1 && S.hpos[k] + 1 < p) ++k;
+                int ml;
+                if (k < prev1 && S.hpos[k] + 1 == p && S.hml[k] > KI) {
+                    ml = S.hml[k] - 1;
+                } else {
+                    const uint64_t ex = I.kext[r];
+                    const uint64_t qe = S.qext[a];
+                    const int le = (int)(ex >> 56), lq = (int)(qe >> 56);
+                    const uint64_t x = (ex ^ qe) & KX_MASK;
+                    int m = x ? ctz64(x) >> 1 : KX;
+                    m = m < le ? m : le;
+                    m = m < lq ? m : lq;
+                    ml = KI + m;
+                    if (m == KX)
+                        while (a + ml < len && q[a + ml] < 4 && T[p + ml] == q[a + ml]) ++ml;
+                }
+                S.hpos[nh] = p;
+                S.hml[nh] = (uint16_t)(ml < 65535 ? ml : 65535);
+                ++nh;
+                ++g[ml - KI < HB - 1 ? ml - KI : HB - 1];
+            }
+            for (int t = HB - 2; t >= 0; --t) g[t] += g[t + 1];
+        }
+        prev0 = S.hoff[a];
+        prev1 = nh;
+    }
+    for (int a = len - KI + 1 < 0 ? 0 : len - KI + 1; a <= len; ++a) S.hoff[a] = nh;
+    return 0;
+}
+
+// ---------------------------------------------------------------- SMEMs
+SC_HD void iv_reverse(Iv *v, int n) {
+    for (int i = 0, j = n - 1; i < j; ++i, --j) {
+        const Iv t = v[i];
+        v[i] = v[j];
+        v[j] = t;
+    }
+}
+
+// bwt_smem1a (max_intv = 0): SMEMs covering x with >= min_intv occurrences, sorted by
+// start, into mem[0, *nmem); returns the end of the longest forward match from x.
+SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int x, int64_t min_intv, Iv *mem,
+                int &nmem, int &err) {
+    nmem = 0;
+    if (q[x] > 3) return x + 1;
+    if (min_intv < 1) min_intv = 1;
+    Iv *curr = S.curr, *prev = S.prev;
+    const int cap = S.cap_iv;
+    int nc = 0, np = 0;
+    Iv ik{x, x + 1, occ(x, x + 1)};
+    int i;
+    for (i = x + 1; i < len; ++i) {
+        if (q[i] < 4) {
+            const int64_t o = occ(x, i + 1);
+            if (o != ik.occ) {
+                if (nc >= cap) { err |= SC_OVER_IV; return len; }
+                curr[nc++] = ik;
+                if (o < min_intv) break;
+            }
+            ik = Iv{x, i + 1, o};
+        } else {
+            if (nc >= cap) { err |= SC_OVER_IV; return len; }
+            curr[nc++] = ik;
+            break;
+        }
+    }
+    if (i == len) {
+        if (nc >= cap) { err |= SC_OVER_IV; return len; }
+        curr[nc++] = ik;
+    }
+    iv_reverse(curr, nc);   // longer matches first
+    const int ret = curr[0].end;
+    {
+        Iv *t = prev;
+        prev = curr;
+        curr = t;
+        np = nc;
+    }
+    for (i = x - 1; i >= -1; --i) {
+        const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
+        nc = 0;
+        for (int k = 0; k < np; ++k) {
+            const Iv p = prev[k];
+            const int64_t o = c >= 0 ? occ(i, p.end) : 0;
+            if (c < 0 || o < min_intv) {
+                if (nc == 0 && (nmem == 0 || i + 1 < mem[nmem - 1].start)) {
+                    if (nmem >= cap) { err |= SC_OVER_IV; return len; }
+                    mem[nmem++] = Iv{i + 1, p.end, p.occ};
+                }
+            } else if (nc == 0 || o != curr[nc - 1].occ) {
+                curr[nc++] = Iv{i, p.end, o};   // nc <= np <= cap
+            }
+        }
+        if (nc == 0) break;
+        Iv *t = prev;
+        prev = curr;
+        curr = t;
+        np = nc;
+    }
+    iv_reverse(mem, nmem);
+    return ret;
+}
+
+// bwt_seed_strategy1: the shortest match from x longer than min_len with < max_intv hits
+SC_HD int seed_strategy1(const Occ &occ, const uint8_t *q, int len, int x, int min_len, int64_t max_intv, Iv &m) {
+    m = Iv{0, 0, 0};
+    if (q[x] > 3) return x + 1;
+    for (int i = x + 1; i < len; ++i) {
+        if (q[i] > 3) return i + 1;
+        if (i - x >= min_len) {
+            const int64_t o = occ(x, i + 1);
+            if (o < max_intv) {
+                m = Iv{x, i + 1, o};
+                return i + 1;
+            }
+        }
+    }
+    return len;
+}
+
+// mem_collect_intv -> S.mems[0, return) sorted by (start, end), stable
+SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const uint8_t *q, int len, int &err) {
+    int nm = 0, n1 = 0;
+    auto push = [&](const Iv &v) {
+        if (nm >= S.cap_mems) {
+            err |= SC_OVER_MEMS;
+            return;
+        }
+        S.mems[nm++] = v;
+    };
+    for (int x = 0; x < len && !err;) {
+        if (q[x] < 4) {
+            x = smem1(occ, S, q, len, x, 1, S.m1, n1, err);
+            for (int k = 0; k < n1; ++k)
+                if (S.m1[k].end - S.m1[k].start >= O.min_seed_len) push(S.m1[k]);
+        } else {
+            ++x;
+        }
+    }
+    const int split_len = (int)(O.min_seed_len * O.split_factor + .499);
+    const int nfirst = nm;
+    for (int k = 0; k < nfirst && !err; ++k) {
+        const Iv p = S.mems[k];
+        if (p.end - p.start < split_len || p.occ > O.split_width) continue;
+        smem1(occ, S, q, len, (p.start + p.end) >> 1, p.occ + 1, S.m1, n1, err);
+        for (int j = 0; j < n1; ++j)
+            if (S.m1[j].end - S.m1[j].start >= O.min_seed_len) push(S.m1[j]);
+    }
+    if (O.max_mem_intv > 0) {
+        for (int x = 0; x < len && !err;) {
+            if (q[x] < 4) {
+                Iv m;
+                x = seed_strategy1(occ, q, len, x, O.min_seed_len, O.max_mem_intv, m);
+                if (m.occ > 0) push(m);
+            } else {
+                ++x;
+            }
+        }
+    }
+    // stable insertion sort by (start, end)
+    for (int i = 1; i < nm; ++i) {
+        const Iv v = S.mems[i];
+        int j = i - 1;
+        while (j >= 0 && (S.mems[j].start > v.start || (S.mems[j].start == v.start && S.mems[j].end > v.end))) {
+            S.mems[j + 1] = S.mems[j];
+            --j;
+        }
+        S.mems[j + 1] = v;
+    }
+    return nm;
+}
+
+// ---------------------------------------------------------------- chaining
+SC_HD int contig_of(const IndexView &I, int64_t p) {
+    int c = I.cblk[p >> CB_SHIFT];
+    while (c + 1 < I.n_contig && I.cstart[c + 1] <= p) ++c;
+    return c;
+}
+
+SC_HD void text_to_fr(const IndexView &I, uint32_t p, int64_t &fr, int &rid) {
+    const int c = contig_of(I, p);
+    const int64_t o = (int64_t)p - I.cstart[c];
+    if (c < I.n_lr) {
+        rid = c;
+        fr = I.lr_off[c] + o;
+    } else {
+        rid = 2 * I.n_lr - 1 - c;   // the reverse half holds the long reads in reverse order
+        fr = I.l_pac + (I.l_pac - I.lr_off[rid + 1]) + o;
+    }
+}
+
+// -> 1 merged, 0 not, -1 pool full
+SC_HD int test_and_merge(const pr_seed_opts &O, int64_t l_pac, Scratch &S, int32_t &ns, Chain &c, const Seed &p,
+                         int rid) {
+    const Seed &last = S.seeds[c.tail];
+    const Seed &first = S.seeds[c.head];
+    const int64_t qend = last.qbeg + last.len, rend = last.rbeg + last.len;
+    if (rid != c.rid) return 0;
+    if (p.qbeg >= first.qbeg && p.qbeg + p.len <= qend && p.rbeg >= first.rbeg && p.rbeg + p.len <= rend)
+        return 1;   // contained seed
+    if ((last.rbeg < l_pac || first.rbeg < l_pac) && p.rbeg >= l_pac) return 0;   // other strand
+    const int64_t x = p.qbeg - last.qbeg, y = p.rbeg - last.rbeg;
+    if (y >= 0 && x - y <= O.w && y - x <= O.w && x - last.len < O.max_chain_gap && y - last.len < O.max_chain_gap) {
+        if (ns >= S.cap_seeds) return -1;
+        S.seeds[ns] = p;
+        S.next[ns] = -1;
+        S.next[c.tail] = ns;
+        c.tail = ns++;
+        ++c.n;
+        return 1;
+    }
+    return 0;
+}
+
+SC_HD int chain_weight(const Scratch &S, const Chain &c) {
+    int64_t end = 0;
+    int w = 0;
+    for (int32_t k = c.head; k >= 0; k = S.next[k]) {
+        const Seed &s = S.seeds[k];
+        if (s.qbeg >= end) w += s.len;
+        else if (s.qbeg + s.len > end) w += (int)(s.qbeg + s.len - end);
+        end = end > s.qbeg + s.len ? end : s.qbeg + s.len;
+    }
+    const int tmp = w;
+    w = 0;
+    end = 0;
+    for (int32_t k = c.head; k >= 0; k = S.next[k]) {
+        const Seed &s = S.seeds[k];
+        if (s.rbeg >= end) w += s.len;
+        else if (s.rbeg + s.len > end) w += (int)(s.rbeg + s.len - end);
+        end = end > s.rbeg + s.len ? end : s.rbeg + s.len;
+    }
+    w = w < tmp ? w : tmp;
+    return w < (1 << 30) ? w : (1 << 30) - 1;
+}
+
+SC_HD int cal_max_gap(const pr_seed_opts &O, int qlen) {
+    int l_del = (int)((double)(qlen * O.a - O.o_del) / O.e_del + 1.);
+    int l_ins = (int)((double)(qlen * O.a - O.o_ins) / O.e_ins + 1.);
+    int l = l_del > l_ins ? l_del : l_ins;
+    l = l > 1 ? l : 1;
+    return l < O.w << 1 ? l : O.w << 1;
+}
+
+// The whole read: tasks into out[0, *n_out) (chain order after mem_chain_flt).
+// Returns 0 or an SC_OVER_* mask (then the read's output is not valid).
+SC_HD int map_read(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
+                   pr_seed_task *out, int cap_out, int *n_out) {
+    *n_out = 0;
+    int err = build_occ(I, S, q, len);
+    if (err) return err;
+    const Occ occ{&I, &S, q, len};
+    const int nm = collect_intv(occ, S, O, q, len, err);
+    if (err) return err;
+    // mem_chain
+    int32_t ns = 0, ncv = 0;
+    for (int mi = 0; mi < nm; ++mi) {
+        const Iv p = S.mems[mi];
+        const int slen = p.end - p.start;
+        const int32_t h0 = S.hoff[p.start], h1 = S.hoff[p.start + 1];
+        int64_t np = 0;
+        for (int32_t k = h0; k < h1; ++k) np += S.hml[k] >= slen;
+        const int64_t step = np > O.max_occ ? np / O.max_occ : 1;
+        int64_t fidx = 0, take = 0, count = 0;
+        for (int32_t k = h0; k < h1 && count < O.max_occ; ++k) {
+            if (S.hml[k] < slen) continue;   // text-position order: the 12-mer lists are sorted
+            const bool use = fidx == take;
+            ++fidx;
+            if (!use) continue;
+            take += step;
+            ++count;
+            Seed s;
+            int rid;
+            text_to_fr(I, S.hpos[k], s.rbeg, rid);
+            s.qbeg = p.start;
+            s.len = slen;
+            int lo = 0, hi = ncv;   // first chain with pos > rbeg
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (S.cv[S.ord[mid]].pos <= s.rbeg) lo = mid + 1;
+                else hi = mid;
+            }
+            if (lo > 0) {
+                const int r = test_and_merge(O, I.l_pac, S, ns, S.cv[S.ord[lo - 1]], s, rid);
+                if (r < 0) return SC_OVER_SEEDS;
+                if (r) continue;
+            }
+            if (ncv >= S.cap_chains) return SC_OVER_CHAINS;
+            if (ns >= S.cap_seeds) return SC_OVER_SEEDS;
+            S.seeds[ns] = s;
+            S.next[ns] = -1;
+            Chain c;
+            c.pos = s.rbeg;
+            c.rid = rid;
+            c.head = c.tail = ns++;
+            c.n = 1;
+            c.w = c.kept = 0;
+            c.first = -1;
+            S.cv[ncv] = c;
+            for (int j = ncv; j > lo; --j) S.ord[j] = S.ord[j - 1];
+            S.ord[lo] = ncv++;
+        }
+    }
+    // mem_chain_flt
+    int nch = 0;
+    for (int j = 0; j < ncv; ++j) {
+        Chain c = S.cv[S.ord[j]];
+        c.w = chain_weight(S, c);
+        if (c.w >= O.min_chain_weight) S.ch[nch++] = c;
+    }
+    for (int i = 1; i < nch; ++i) {   // stable sort by weight, descending
+        const Chain v = S.ch[i];
+        int j = i - 1;
+        while (j >= 0 && S.ch[j].w < v.w) {
+            S.ch[j + 1] = S.ch[j];
+            --j;
+        }
+        S.ch[j + 1] = v;
+    }
+    if (nch > 0) {
+        int nk = 1;
+        S.kept[0] = 0;
+        S.ch[0].kept = 3;
+        for (int i = 1; i < nch; ++i) {
+            int large = 0, k;
+            const int bi = S.seeds[S.ch[i].head].qbeg;
+            const int ei = S.seeds[S.ch[i].tail].qbeg + S.seeds[S.ch[i].tail].len;
+            for (k = 0; k < nk; ++k) {
+                Chain &cj = S.ch[S.kept[k]];
+                const int bj = S.seeds[cj.head].qbeg;
+                const int ej = S.seeds[cj.tail].qbeg + S.seeds[cj.tail].len;
+                const int bmax = bj > bi ? bj : bi;
+                const int emin = ej < ei ? ej : ei;
+                if (emin > bmax) {
+                    const int li = ei - bi, lj = ej - bj;
+                    const int minl = li < lj ? li : lj;
+                    if (emin - bmax >= minl * O.mask_level && minl < O.max_chain_gap) {
+                        large = 1;
+                        if (cj.first < 0) cj.first = i;
+                        if (S.ch[i].w < cj.w * O.drop_ratio && cj.w - S.ch[i].w >= O.min_seed_len << 1) break;
+                    }
+                }
+            }
+            if (k == nk) {
+                S.kept[nk++] = i;
+                S.ch[i].kept = large ? 2 : 3;
+            }
+        }
+        for (int k = 0; k < nk; ++k)
+            if (S.ch[S.kept[k]].first >= 0) S.ch[S.ch[S.kept[k]].first].kept = 1;
+    }
+    // mem_chain2aln: the best seed of every kept chain and the chain's reference window
+    int no = 0;
+    for (int ci = 0; ci < nch; ++ci) {
+        const Chain &c = S.ch[ci];
+        if (c.kept == 0) continue;
+        int32_t best = c.head;
+        for (int32_t k = S.next[c.head]; k >= 0; k = S.next[k])
+            if (S.seeds[k].len >= S.seeds[best].len) best = k;   // srt order: (score, index), last wins
+        const Seed &s = S.seeds[best];
+        const bool rev = s.rbeg >= I.l_pac;
+        const int64_t L = I.lr_off[c.rid + 1] - I.lr_off[c.rid];
+        const int64_t cs = rev ? I.l_pac + (I.l_pac - I.lr_off[c.rid + 1]) : I.lr_off[c.rid];
+        int64_t r0 = INT64_MAX, r1 = INT64_MIN;
+        for (int32_t k = c.head; k >= 0; k = S.next[k]) {
+            const Seed &t = S.seeds[k];
+            const int64_t b = t.rbeg - (t.qbeg + cal_max_gap(O, t.qbeg));
+            const int64_t e = t.rbeg + t.len + ((len - t.qbeg - t.len) + cal_max_gap(O, len - t.qbeg - t.len));
+            r0 = r0 < b ? r0 : b;
+            r1 = r1 > e ? r1 : e;
+        }
+        r0 -= cs;
+        r1 -= cs;
+        if (no >= cap_out) return SC_OVER_OUT;
+        pr_seed_task &t = out[no++];
+        t.sr = sid;
+        t.lr = c.rid;
+        t.strand = rev ? 1 : 0;
+        t.qbeg = s.qbeg;
+        t.rbeg = (int32_t)(s.rbeg - cs);
+        t.slen = s.len;
+        t.rmax0 = (int32_t)(r0 > 0 ? r0 : 0);
+        t.rmax1 = (int32_t)(r1 < L ? r1 : L);
+        t.weight = c.w;
+        t.nseed = c.n;
+    }
+    *n_out = no;
+    return 0;
+}
+
+}  // namespace seedc
+}  // namespace prgpu
