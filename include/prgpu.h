@@ -261,6 +261,20 @@ void pr_seed_tasks_free(pr_seed_tasks *t);
 int pr_seed_index_occ(const pr_seed_index *h, const uint8_t *s, int n, int64_t *count);
 int pr_seed_smem(const pr_seed_index *h, const uint8_t *q, int len, int x, int64_t min_intv, int32_t *start,
                  int32_t *end, int64_t *occ, int cap, int *n_out);
+/* The GPU seeding path (seed_kernels.hip: the same per-read core, one lane per read,
+ * fixed scratch per lane).  pr_seed_gpu_upload copies a built index into the context's
+ * HBM; pr_seed_gpu_map seeds n_sr reads (nt4 codes) into library-owned tasks in read
+ * order; status[i] (may be NULL) is 0 or the overflow flags of a read whose work
+ * outgrew the lane scratch (it then has no tasks, and the call returns PR_ERR_CAPACITY
+ * after filling everything else). */
+int pr_seed_gpu_upload(pr_ctx *ctx, const pr_seed_index *h);
+int pr_seed_gpu_map(pr_ctx *ctx, const pr_seed_opts *o, const uint8_t *sr_seq, const int64_t *sr_off, int n_sr,
+                    pr_seed_tasks *out, int32_t *status);
+/* milliseconds of the last pr_seed_gpu_map kernel (HIP events on the ctx stream) */
+int pr_seed_gpu_last_ms(pr_ctx *ctx, double *ms);
+/* diagnostics (tests): the device path's core and capacities run on the host */
+int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opts *o, const uint8_t *sr_seq,
+                            const int64_t *sr_off, int n_sr, int n_threads, pr_seed_tasks *out, int32_t *status);
 
 /* ------------------------------------------------------------------ */
 /* one correction iteration on the device: SW -> assemble -> consensus  */

@@ -10,7 +10,7 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 SRC = PKG / "csrc"
 OUT = PKG / "libprgpu.so"
-SOURCES = ["cns_kernels.hip", "sw_kernels.hip", "pipe_kernels.hip", "mask_kernels.hip", "sw_api.cpp", "prgpu_api.cpp", "seed.cpp", "trim.cpp"]
+SOURCES = ["cns_kernels.hip", "sw_kernels.hip", "pipe_kernels.hip", "mask_kernels.hip", "seed_kernels.hip", "sw_api.cpp", "prgpu_api.cpp", "seed.cpp", "trim.cpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17", "-pthread",
          # exact IEEE double semantics of the reference Perl arithmetic
          "-ffp-contract=off", "-fno-fast-math",

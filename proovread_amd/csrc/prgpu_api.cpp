@@ -15,6 +15,7 @@
 #include "sw_dev.h"
 #include "pipe_dev.h"
 #include "mask_dev.h"
+#include "seed_dev.h"
 
 using namespace prgpu;
 int sw_get_ptrs(pr_ctx *c, SwPtrs *p);
@@ -74,12 +75,17 @@ enum CnsBufId {
 
 // masking buffers (pr_mask_run inputs / outputs, pr_iter_mask output and run lists)
 enum MaskBufId { MB_OFF, MB_SEQ, MB_QUAL, MB_OUT, MB_RUN_OFF, MB_RUNS, MB_TMP, MB_NRUNS, MB_ERR, MB_STATS, MB_COUNT };
+// device seeding: the index copy (SI_*) and per-call buffers (SB_*)
+enum SeedBufId {
+    SI_TEXT, SI_CSTART, SI_CBLK, SI_LROFF, SI_KOFF, SI_KPOS, SI_KEXT, SI_CNT0,
+    SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SD_COUNT
+};
 
 struct pr_ctx {
     int device = 0;
     int n_cu = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[10] = {};   // 0-7: SW, consensus, pipeline; 8-9: seeding
     // consensus resident batch
     DevBuf cb[CB_COUNT];
     bool cns_loaded = false;
@@ -99,6 +105,11 @@ struct pr_ctx {
     SwResident sw;
     // masking
     DevBuf mb[MB_COUNT];
+    // seeding
+    DevBuf sd[SD_COUNT];
+    bool seed_loaded = false;
+    seedc::IndexView seed_view{};
+    float ms_seed = 0.f;
     bool iter_masked = false;
     bool cns_launched = false;   // a consensus launch filled the CB_O_* outputs
 };
@@ -139,6 +150,7 @@ extern "C" void pr_ctx_destroy(pr_ctx *c) {
     (void)hipSetDevice(c->device);
     for (auto &b : c->cb) b.release();
     for (auto &b : c->mb) b.release();
+    for (auto &b : c->sd) b.release();
     sw_release(c->sw);
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -861,6 +873,115 @@ extern "C" int pr_iter_mask_download(pr_ctx *c, uint8_t *masked) {
     if (rc) return rc;
     if ((rc = download(masked, c->mb[MB_OUT], (size_t)c->seq_cap, c->stream))) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// seeding on the device (seed_kernels.hip over seed_core.h)
+extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
+    if (!c || !h) return set_error(PR_ERR_ARG, "null arg");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const seedc::IndexView hv = seed_index_view(h);
+    const SeedIndexSizes z = seed_index_sizes(h);
+    DevBuf *D = c->sd;
+    int rc;
+    if ((rc = upload(D[SI_TEXT], hv.text, (size_t)z.text, s)) || (rc = upload(D[SI_CSTART], hv.cstart, (size_t)z.cstart, s)) ||
+        (rc = upload(D[SI_CBLK], hv.cblk, (size_t)z.cblk, s)) || (rc = upload(D[SI_LROFF], hv.lr_off, (size_t)z.lr_off, s)) ||
+        (rc = upload(D[SI_KOFF], hv.koff, (size_t)z.koff, s)) || (rc = upload(D[SI_KPOS], hv.kpos, (size_t)z.kpos, s)) ||
+        (rc = upload(D[SI_KEXT], hv.kext, (size_t)z.kpos, s)))
+        return rc;
+    seedc::IndexView v = hv;
+    for (int j = 0; j < seedc::KI - 1; ++j) {
+        if ((rc = upload(D[SI_CNT0 + j], hv.cnt[j], (size_t)z.cnt[j], s))) return rc;
+        v.cnt[j] = D[SI_CNT0 + j].as<uint32_t>();
+    }
+    v.text = D[SI_TEXT].as<uint8_t>();
+    v.cstart = D[SI_CSTART].as<int64_t>();
+    v.cblk = D[SI_CBLK].as<int32_t>();
+    v.lr_off = D[SI_LROFF].as<int64_t>();
+    v.koff = D[SI_KOFF].as<uint32_t>();
+    v.kpos = D[SI_KPOS].as<uint32_t>();
+    v.kext = D[SI_KEXT].as<uint64_t>();
+    HIPCHK(hipStreamSynchronize(s));
+    c->seed_view = v;
+    c->seed_loaded = true;
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *sr_seq, const int64_t *sr_off, int n_sr,
+                               pr_seed_tasks *out, int32_t *status) {
+    if (!c || !o || !out || n_sr < 0 || (n_sr && (!sr_seq || !sr_off))) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->seed_loaded) return set_error(PR_ERR_ARG, "no seed index on the device (pr_seed_gpu_upload)");
+    if (o->min_seed_len < seedc::KI) return set_error(PR_ERR_UNSUPPORTED, "min seed length below the 12-mer index");
+    if (o->max_occ <= 0 || o->w < 0) return set_error(PR_ERR_ARG, "bad seeding options");
+    out->n = 0;
+    out->t = nullptr;
+    if (n_sr && sr_off[0] != 0) return set_error(PR_ERR_ARG, "sr_off must start at 0");
+    for (int i = 0; i < n_sr; ++i)
+        if (sr_off[i + 1] < sr_off[i]) return set_error(PR_ERR_ARG, "sr_off not monotone");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    DevBuf *D = c->sd;
+    const seedc::Caps caps = seedc::device_caps();
+    SeedDev K{};
+    K.V = c->seed_view;
+    K.O = *o;
+    K.n_sr = n_sr;
+    K.caps = caps;
+    K.stride = seedc::scratch_bytes(caps);
+    // lanes: two resident 64-lane waves per CU, bounded by the scratch (~0.45 MB per lane,
+    // ~15 GB at 256 CUs)
+    int64_t lanes = (int64_t)c->n_cu * 64 * 2;
+    if (lanes > n_sr) lanes = ((int64_t)n_sr + 63) / 64 * 64;
+    if (lanes < 64) lanes = 64;
+    K.n_lanes = lanes;
+    const int64_t nb = n_sr ? sr_off[n_sr] : 0;
+    int rc;
+    if ((rc = upload(D[SB_SEQ], sr_seq, (size_t)nb, s)) || (rc = upload(D[SB_OFF], sr_off, (size_t)n_sr + 1, s)) ||
+        (rc = D[SB_SCRATCH].ensure((size_t)(lanes * K.stride))) ||
+        (rc = D[SB_OUT].ensure((size_t)n_sr * caps.out * sizeof(pr_seed_task) + 16)) ||
+        (rc = D[SB_NOUT].ensure((size_t)n_sr * 4 + 16)) || (rc = D[SB_STATUS].ensure((size_t)n_sr * 4 + 16)))
+        return rc;
+    K.sr_seq = D[SB_SEQ].as<uint8_t>();
+    K.sr_off = D[SB_OFF].as<int64_t>();
+    K.scratch = D[SB_SCRATCH].as<uint8_t>();
+    K.out = D[SB_OUT].as<pr_seed_task>();
+    K.n_out = D[SB_NOUT].as<int32_t>();
+    K.status = D[SB_STATUS].as<int32_t>();
+    HIPCHK(hipEventRecord(c->ev[8], s));
+    const int e = seed_launch(K, (void *)s);
+    if (e) return set_error(PR_ERR_HIP, "seed kernel: %s", hipGetErrorString((hipError_t)e));
+    HIPCHK(hipEventRecord(c->ev[9], s));
+    std::vector<int32_t> nout((size_t)n_sr), st((size_t)n_sr);
+    if ((rc = download(nout.data(), D[SB_NOUT], (size_t)n_sr, s)) || (rc = download(st.data(), D[SB_STATUS], (size_t)n_sr, s)))
+        return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0.f;
+    if (n_sr && hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_seed = ms;
+    int64_t total = 0, bad = 0;
+    for (int i = 0; i < n_sr; ++i) {
+        if (nout[i] < 0 || nout[i] > caps.out) return set_error(PR_ERR_HIP, "seed kernel: bad task count");
+        total += nout[i];
+        bad += st[i] != 0;
+    }
+    std::vector<pr_seed_task> slots((size_t)n_sr * caps.out);
+    if ((rc = download(slots.data(), D[SB_OUT], slots.size(), s))) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    out->t = (pr_seed_task *)std::malloc(sizeof(pr_seed_task) * (size_t)(total > 0 ? total : 1));
+    if (!out->t) return set_error(PR_ERR_ARG, "out of host memory");
+    int64_t k = 0;
+    for (int i = 0; i < n_sr; ++i)
+        for (int j = 0; j < nout[i]; ++j) out->t[k++] = slots[(size_t)i * caps.out + j];
+    out->n = total;
+    if (status) std::memcpy(status, st.data(), (size_t)n_sr * 4);
+    if (bad) return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags)", (long long)bad);
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_last_ms(pr_ctx *c, double *ms) {
+    if (!c || !ms) return set_error(PR_ERR_ARG, "null arg");
+    *ms = c->ms_seed;
     return 0;
 }
 

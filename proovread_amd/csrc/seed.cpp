@@ -32,6 +32,7 @@
 
 #include "../../include/prgpu.h"
 #include "seed_core.h"
+#include "seed_dev.h"
 
 namespace seedc = prgpu::seedc;
 
@@ -272,6 +273,22 @@ struct pr_seed_index {
     Index I;
 };
 
+namespace prgpu {
+seedc::IndexView seed_index_view(const pr_seed_index *h) { return view_of(h->I); }
+SeedIndexSizes seed_index_sizes(const pr_seed_index *h) {
+    const Index &I = h->I;
+    SeedIndexSizes z{};
+    z.text = (int64_t)I.text.size();
+    z.cstart = (int64_t)I.cstart.size();
+    z.cblk = (int64_t)I.cblk.size();
+    z.lr_off = (int64_t)I.lr_off.size();
+    z.koff = (int64_t)I.koff.size();
+    z.kpos = (int64_t)I.kpos.size();
+    for (int j = 0; j < KI - 1; ++j) z.cnt[j] = (int64_t)I.cnt[j].size();
+    return z;
+}
+}  // namespace prgpu
+
 extern "C" void pr_seed_opts_default(pr_seed_opts *o, int finish) {
     std::memset(o, 0, sizeof *o);
     // bwa mem defaults + proovread.cfg bwa-sr (-k 12 -W 20 -w 40 -r 1 -D 0 -y 20) /
@@ -459,4 +476,51 @@ extern "C" int pr_seed_map(const pr_seed_index *h, const pr_seed_opts *o, const 
 extern "C" void pr_seed_tasks_free(pr_seed_tasks *t) {
     if (t && t->t) std::free(t->t);
     if (t) t->t = nullptr, t->n = 0;
+}
+
+// The device path's arithmetic on the host: seed_core.h with the device's fixed
+// scratch capacities (seedc::device_caps), so tests can check which reads the GPU
+// kernel flags and that every other read gets the host path's tasks.
+extern "C" int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opts *o, const uint8_t *sr_seq,
+                                       const int64_t *sr_off, int n_sr, int n_threads, pr_seed_tasks *out,
+                                       int32_t *status) {
+    if (!h || !o || !out || !status || n_sr < 0 || (n_sr && (!sr_seq || !sr_off)))
+        return pr_set_error(PR_ERR_ARG, "null arg");
+    if (o->min_seed_len < KI) return pr_set_error(PR_ERR_UNSUPPORTED, "min seed length below the 12-mer index");
+    out->n = 0;
+    out->t = nullptr;
+    const seedc::IndexView V = view_of(h->I);
+    const seedc::Caps caps = seedc::device_caps();
+    const int64_t bytes = seedc::scratch_bytes(caps);
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : (nt > 64 ? 64 : nt);
+    std::vector<ReadOut> res(n_sr);
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        std::vector<uint64_t> slab((size_t)(bytes / 8 + 1));
+        seedc::Scratch S = seedc::carve(reinterpret_cast<uint8_t *>(slab.data()), caps);
+        std::vector<pr_seed_task> buf((size_t)caps.out);
+        for (;;) {
+            const int i = next.fetch_add(1);
+            if (i >= n_sr) break;
+            const int len = (int)(sr_off[i + 1] - sr_off[i]);
+            int n = 0, err = 0;
+            if (len > 0) err = seedc::map_read(V, *o, S, sr_seq + sr_off[i], len, i, buf.data(), caps.out, &n);
+            status[i] = err;
+            if (!err) res[i].tasks.assign(buf.begin(), buf.begin() + n);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    int64_t total = 0;
+    for (auto &r : res) total += (int64_t)r.tasks.size();
+    out->t = (pr_seed_task *)std::malloc(sizeof(pr_seed_task) * (size_t)(total > 0 ? total : 1));
+    if (!out->t) return pr_set_error(PR_ERR_ARG, "out of host memory");
+    int64_t k = 0;
+    for (auto &r : res)
+        for (auto &t : r.tasks) out->t[k++] = t;
+    out->n = total;
+    return 0;
 }

@@ -571,3 +571,69 @@ SC_HD int map_read(const IndexView &I, const pr_seed_opts &O, Scratch &S, const 
 
 }  // namespace seedc
 }  // namespace prgpu
+
+namespace prgpu {
+namespace seedc {
+
+// Fixed scratch capacities of the device path (one lane per read).  Reads that
+// need more are flagged with the SC_OVER_* bit of the array that overflowed.
+struct Caps {
+    int32_t lmax, hits, iv, mems, seeds, chains, out;
+};
+SC_HD Caps device_caps() { return Caps{1024, 8192, 256, 1024, 4096, 2048, 128}; }
+
+SC_HD int64_t align8(int64_t x) { return (x + 7) & ~(int64_t)7; }
+
+// bytes of one lane's scratch slice
+SC_HD int64_t scratch_bytes(const Caps &c) {
+    int64_t b = 0;
+    b += align8(4 * (int64_t)(c.lmax + 1));              // hoff
+    b += align8(8 * (int64_t)(c.lmax + 1));              // qext
+    b += align8(4 * (int64_t)(c.lmax + 1));              // codes
+    b += align8(4 * (int64_t)c.lmax * HB);               // ge
+    b += align8(4 * (int64_t)c.hits);                    // hpos
+    b += align8(2 * (int64_t)c.hits);                    // hml
+    b += align8((int64_t)sizeof(Iv) * c.mems);           // mems
+    b += 3 * align8((int64_t)sizeof(Iv) * c.iv);         // m1, curr, prev
+    b += align8((int64_t)sizeof(Seed) * c.seeds);        // seeds
+    b += align8(4 * (int64_t)c.seeds);                   // next
+    b += 2 * align8((int64_t)sizeof(Chain) * c.chains);  // cv, ch
+    b += 2 * align8(4 * (int64_t)c.chains);              // ord, kept
+    return b;
+}
+
+// lay a Scratch over an 8-byte aligned slice of scratch_bytes(c) bytes
+SC_HD Scratch carve(uint8_t *p, const Caps &c) {
+    Scratch S{};
+    auto take = [&p](int64_t bytes) {
+        uint8_t *r = p;
+        p += align8(bytes);
+        return r;
+    };
+    S.lmax = c.lmax;
+    S.hoff = (int32_t *)take(4 * (int64_t)(c.lmax + 1));
+    S.qext = (uint64_t *)take(8 * (int64_t)(c.lmax + 1));
+    S.codes = (int32_t *)take(4 * (int64_t)(c.lmax + 1));
+    S.ge = (uint32_t *)take(4 * (int64_t)c.lmax * HB);
+    S.hpos = (uint32_t *)take(4 * (int64_t)c.hits);
+    S.hml = (uint16_t *)take(2 * (int64_t)c.hits);
+    S.cap_hits = c.hits;
+    S.mems = (Iv *)take((int64_t)sizeof(Iv) * c.mems);
+    S.cap_mems = c.mems;
+    S.m1 = (Iv *)take((int64_t)sizeof(Iv) * c.iv);
+    S.curr = (Iv *)take((int64_t)sizeof(Iv) * c.iv);
+    S.prev = (Iv *)take((int64_t)sizeof(Iv) * c.iv);
+    S.cap_iv = c.iv;
+    S.seeds = (Seed *)take((int64_t)sizeof(Seed) * c.seeds);
+    S.next = (int32_t *)take(4 * (int64_t)c.seeds);
+    S.cap_seeds = c.seeds;
+    S.cv = (Chain *)take((int64_t)sizeof(Chain) * c.chains);
+    S.ch = (Chain *)take((int64_t)sizeof(Chain) * c.chains);
+    S.ord = (int32_t *)take(4 * (int64_t)c.chains);
+    S.kept = (int32_t *)take(4 * (int64_t)c.chains);
+    S.cap_chains = c.chains;
+    return S;
+}
+
+}  // namespace seedc
+}  // namespace prgpu

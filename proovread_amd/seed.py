@@ -1,4 +1,4 @@
-"""Host seeding front end (C-ABI pr_seed_*): `bwa-proovread index` + the seeding and
+"""Seeding front end (C-ABI pr_seed_*: host path, and the GPU path pr_seed_gpu_*): `bwa-proovread index` + the seeding and
 chaining part of `bwa-proovread mem` (bin/proovread:1270, 1313), which produce the
 seed-extension task list of the SW stage.  See include/prgpu.h and DESIGN.md
 (parity with bwa-proovread unpinned)."""
@@ -48,6 +48,12 @@ def _setup(L):
     L.pr_seed_index_occ.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int64)]
     L.pr_seed_smem.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
                                C.c_void_p, C.c_int, C.POINTER(C.c_int)]
+    L.pr_seed_map_device_caps.argtypes = [C.c_void_p, C.POINTER(SeedOpts), C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                          C.POINTER(SeedTasks), C.c_void_p]
+    L.pr_seed_gpu_upload.argtypes = [C.c_void_p, C.c_void_p]
+    L.pr_seed_gpu_map.argtypes = [C.c_void_p, C.POINTER(SeedOpts), C.c_void_p, C.c_void_p, C.c_int,
+                                  C.POINTER(SeedTasks), C.c_void_p]
+    L.pr_seed_gpu_last_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     _done = True
 
 
@@ -108,6 +114,48 @@ class SeedIndex:
         out = SeedTasks()
         _abi.check(self.L.pr_seed_map(self.h, C.byref(opts), sr_seq.ctypes.data, sr_off.ctypes.data,
                                       len(sr_off) - 1, threads, C.byref(out)), "pr_seed_map")
+        return self._take(out)
+
+    def map_device_caps(self, sr_seq: np.ndarray, sr_off: np.ndarray, opts: SeedOpts | None = None,
+                        threads: int = 0):
+        """The GPU path's core and fixed scratch capacities run on the host -> (tasks, status per read)."""
+        opts = opts or default_opts()
+        sr_seq = np.ascontiguousarray(sr_seq, np.uint8)
+        sr_off = np.ascontiguousarray(sr_off, np.int64)
+        st = np.zeros(max(1, len(sr_off) - 1), np.int32)
+        out = SeedTasks()
+        _abi.check(self.L.pr_seed_map_device_caps(self.h, C.byref(opts), sr_seq.ctypes.data, sr_off.ctypes.data,
+                                                  len(sr_off) - 1, threads, C.byref(out), st.ctypes.data),
+                   "pr_seed_map_device_caps")
+        return self._take(out), st[:len(sr_off) - 1]
+
+    def to_gpu(self, ctx: "_abi.Context"):
+        """Copy the index into the context's HBM (pr_seed_gpu_upload)."""
+        _abi.check(self.L.pr_seed_gpu_upload(ctx.h, self.h), "pr_seed_gpu_upload")
+        self._ctx = ctx
+
+    def map_gpu(self, sr_seq: np.ndarray, sr_off: np.ndarray, opts: SeedOpts | None = None,
+                allow_flagged: bool = False):
+        """Seeding on the GPU -> (tasks, status per read).  Reads flagged with a scratch overflow
+        have no tasks; unless allow_flagged, that raises."""
+        opts = opts or default_opts()
+        sr_seq = np.ascontiguousarray(sr_seq, np.uint8)
+        sr_off = np.ascontiguousarray(sr_off, np.int64)
+        st = np.zeros(max(1, len(sr_off) - 1), np.int32)
+        out = SeedTasks()
+        rc = self.L.pr_seed_gpu_map(self._ctx.h, C.byref(opts), sr_seq.ctypes.data, sr_off.ctypes.data,
+                                    len(sr_off) - 1, C.byref(out), st.ctypes.data)
+        if rc != 0 and not (allow_flagged and rc == -9):
+            self.L.pr_seed_tasks_free(C.byref(out))
+            _abi.check(rc, "pr_seed_gpu_map")
+        return self._take(out), st[:len(sr_off) - 1]
+
+    def gpu_ms(self) -> float:
+        v = C.c_double()
+        _abi.check(self.L.pr_seed_gpu_last_ms(self._ctx.h, C.byref(v)), "pr_seed_gpu_last_ms")
+        return v.value
+
+    def _take(self, out: SeedTasks):
         try:
             n = int(out.n)
             if n == 0:
