@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the configs[1] workload per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-lrs-per-worker", type=int, default=256)
+    ap.add_argument("--seeds", choices=("truth", "host", "gpu"), default="truth",
+                    help="task list: simulation truth, or the seeding front end (host path / GPU path), "
+                         "computed before the timed region")
     return ap.parse_args()
 
 
@@ -69,6 +72,31 @@ def main():
     d = synth.simulate(seed, gl, n_lr, 10_000, 50.0, sr_frac=0.3)
     gen_s = time.perf_counter() - t
     lr_bases = int(d.lr_off[-1])
+    seed_info = None
+
+    def seed_front_end(ctx=None):
+        """The front end (bwa-proovread mem seeding + chaining) on this rank's reads, outside
+        the timed region: the step measures the iteration from resident tasks."""
+        from proovread_amd import seed as seeding
+        t = time.perf_counter()
+        ix = seeding.SeedIndex(d.lr_seq, d.lr_off)
+        t_ix = time.perf_counter() - t
+        t = time.perf_counter()
+        if ctx is None:
+            tasks = ix.map(d.sr_seq, d.sr_off, seeding.default_opts(False), threads=min(16, os.cpu_count() or 1))
+            ms = None
+        else:
+            ix.to_gpu(ctx)
+            tasks, _ = ix.map_gpu(d.sr_seq, d.sr_off, seeding.default_opts(False))
+            ms = ix.gpu_ms()
+        t_map = time.perf_counter() - t
+        ix.close()
+        info = {"path": "gpu" if ctx is not None else "host", "index_s": round(t_ix, 2), "map_s": round(t_map, 2),
+                "reads_per_s": round(d.n_sr / t_map, 1), "kernel_ms": ms, "tasks": int(len(tasks))}
+        return synth.with_seeded_tasks(d, tasks), info
+
+    if args.seeds == "host":   # before the CPU baseline, which then runs on the same tasks
+        d, seed_info = seed_front_end()
 
     # CPU baseline (rank 0, N=1): the oracle chain on a bounded sample of the same
     # workload, before this process touches the GPU (the pool forks).
@@ -92,6 +120,10 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
     ctx = _abi.Context(local)
+    if args.seeds == "gpu":   # after the CPU baseline (its worker pool forks before any GPU use)
+        d, seed_info = seed_front_end(ctx)
+        if cpu is not None:
+            cpu["sample"] += " (simulation-truth tasks)"
     it = iteration.Iteration(d, ctx=ctx)
     opts = sw.default_opts(finish=False)
     params = cns.CnsParams(coverage=min(50.0, 15.0) * 0.75, use_ref_qual=True)   # proovread:1540-1541
@@ -168,7 +200,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic: iid genome, CLR-like long reads, 150 bp short reads, seeds from the simulation truth",
+        "data": "synthetic: iid genome, CLR-like long reads, 150 bp short reads, seeds from "
+                + ("the simulation truth" if args.seeds == "truth" else f"the {args.seeds} seeding path"),
         "config": {
             "workload": "configs[1] per GPU: 4.6 Mb genome, 13,800 x 10 kb long reads (30x, 15% error), "
                         "50x 2x150 short reads sampled to 15x for one bwa-sr iteration",
@@ -203,6 +236,7 @@ def main():
             "alignments": int(n_aln),
         },
         "cpu_baseline": cpu,
+        "seeding": seed_info,
         "gen_s": round(gen_s, 1),
         "reads_ok": ok,
         "iteration_stat": {"corrected_bases": hq[0], "phred_ge20_bases": hq[1]},

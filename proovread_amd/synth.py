@@ -175,3 +175,15 @@ def simulate(seed: int, genome_len: int, n_lr: int, lr_len: int, sr_cov: float,
     return Dataset(genome, lr_seq, lr_off, lr_start, sr_seq, sr_off, sr_start, sr_strand,
                    p_sr[order].astype(np.int32), p_lr[order].astype(np.int32), strand[order].astype(np.uint8),
                    qbeg[order].astype(np.int32), rbeg[order].astype(np.int32), best_len[order].astype(np.int32))
+
+
+def with_seeded_tasks(d: Dataset, tasks: np.ndarray) -> Dataset:
+    """The same reads with the task list of the seeding front end (seed.TASK_DTYPE records,
+    pr_seed_map / pr_seed_gpu_map) in place of the simulation truth: grouped by long read
+    (stable, so a long read's tasks stay in read order, then chain order) as the iteration
+    hand-off expects."""
+    order = np.argsort(tasks["lr"], kind="stable")
+    t = tasks[order]
+    return dataclasses.replace(d, t_sr=t["sr"].astype(np.int32), t_lr=t["lr"].astype(np.int32),
+                               t_strand=t["strand"].astype(np.uint8), t_qbeg=t["qbeg"].astype(np.int32),
+                               t_rbeg=t["rbeg"].astype(np.int32), t_slen=t["slen"].astype(np.int32))

@@ -134,3 +134,20 @@ def test_seeds_are_exact_matches(data, index):
         q = r[t["qbeg"]:t["qbeg"] + t["slen"]]
         assert q == ref[t["rbeg"]:t["rbeg"] + t["slen"]]
         assert t["slen"] >= 12 and 0 <= t["rmax0"] <= t["rbeg"] and t["rbeg"] + t["slen"] <= t["rmax1"] <= len(lr)
+
+
+def test_with_seeded_tasks_groups_by_long_read():
+    """bench --seeds host|gpu: the front end's tasks replace the simulation truth, grouped by
+    long read (the hand-off's layout), a long read's tasks kept in read / chain order."""
+    from proovread_amd import seed as seeding, synth
+    d = synth.simulate(9, 60_000, 60, 4000, 30.0, sr_frac=0.5)
+    ix = seeding.SeedIndex(d.lr_seq, d.lr_off)
+    tasks = ix.map(d.sr_seq, d.sr_off)
+    d2 = synth.with_seeded_tasks(d, tasks)
+    assert len(d2.t_lr) == len(tasks) > 0
+    assert np.all(np.diff(d2.t_lr) >= 0)
+    for lr in np.unique(d2.t_lr)[:20]:
+        sel = tasks[tasks["lr"] == lr]
+        m = d2.t_lr == lr
+        assert np.array_equal(d2.t_sr[m], sel["sr"]) and np.array_equal(d2.t_rbeg[m], sel["rbeg"])
+    assert d2.sr_seq is d.sr_seq and d2.lr_seq is d.lr_seq
