@@ -348,23 +348,53 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
             I.cblk[(size_t)b] = c;
         }
     }
-    std::vector<uint32_t> kc(NK, 0);
-    auto for_kmers = [&](auto f) {
+    // k-mers starting in [p0, p1) (a k-mer may read past p1)
+    auto for_kmers = [&](int64_t p0, int64_t p1, auto f) {
         uint32_t code = 0;
         int run = 0;
-        for (int64_t p = 0; p < n; ++p) {
+        int64_t p = p0 - (KI - 1) > 0 ? p0 - (KI - 1) : 0;
+        for (; p < p1 + KI - 1 && p < n; ++p) {
             if (T[p] > 3) { run = 0; code = 0; continue; }
             code = ((code << 2) | T[p]) & (NK - 1);
-            if (++run >= KI) f(code, (uint32_t)(p - KI + 1));
+            if (++run >= KI && p - KI + 1 >= p0) f(code, (uint32_t)(p - KI + 1));
         }
     };
-    for_kmers([&](uint32_t c, uint32_t) { ++kc[c]; });
+    // counting and filling split over text chunks; chunk t's positions of a k-mer go
+    // after those of chunks < t, so every list stays in ascending text order
+    int nt = (int)std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);
+    if (n < (int64_t)1 << 22) nt = 1;
+    auto run_threads = [&](auto body) {
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(body, t);
+        body(0);
+        for (auto &x : th) x.join();
+    };
+    std::vector<std::vector<uint32_t>> tc((size_t)nt, std::vector<uint32_t>(NK, 0));
+    run_threads([&](int t) {
+        std::vector<uint32_t> &c = tc[(size_t)t];
+        for_kmers(n * t / nt, n * (t + 1) / nt, [&](uint32_t k, uint32_t) { ++c[k]; });
+    });
+    std::vector<uint32_t> kc(NK, 0);
     I.koff.assign(NK + 1, 0);
-    for (uint32_t k = 0; k < NK; ++k) I.koff[k + 1] = I.koff[k] + kc[k];
+    for (uint32_t k = 0; k < NK; ++k) {
+        uint32_t sum = 0;
+        for (int t = 0; t < nt; ++t) {
+            const uint32_t v = tc[(size_t)t][k];
+            tc[(size_t)t][k] = I.koff[k] + sum;   // chunk t's first slot for k-mer k
+            sum += v;
+        }
+        kc[k] = sum;
+        I.koff[k + 1] = I.koff[k] + sum;
+    }
     I.kpos.resize(I.koff[NK]);
     I.kext.resize(I.koff[NK]);
-    std::vector<uint32_t> fill(I.koff.begin(), I.koff.end() - 1);
-    for_kmers([&](uint32_t c, uint32_t p) { I.kpos[fill[c]++] = p; });
+    run_threads([&](int t) {
+        std::vector<uint32_t> &fill = tc[(size_t)t];
+        for_kmers(n * t / nt, n * (t + 1) / nt, [&](uint32_t k, uint32_t p) { I.kpos[fill[k]++] = p; });
+    });
+    tc.clear();
+    tc.shrink_to_fit();
     {   // bases after every hit, in kpos order (random text reads: spread over threads)
         const int64_t nk = (int64_t)I.kpos.size();
         int nt = (int)std::thread::hardware_concurrency();
