@@ -19,13 +19,22 @@ length, cfg:324 "per-base-score"), with SEQ/QUAL printed for secondary hits too
 secondary (flag 0x100, MAPQ 0).  Logs go to stderr; errors exit 1 (proovread
 prints the log, proovread:1320).
 
-Not restated (parity unpinned): bwa-proovread's -b/-l bin filter
-(accepted and ignored: bam2cns applies the same coverage binning downstream),
+`-b BIN -l LEN` (proovread:1302-1313: BIN = bin-size, LEN = BIN x min(coverage,
+task coverage)) is bwa-proovread's proovread.[ch] bin filter, "reporting of
+alignments is determined by score-comparison within bins" (README.org:228-236).
+Its source is absent; it is restated here as the binning proovread itself uses
+(Sam::Seq add_aln_by_score, Seq.pm:582-614, the B4 row of the consensus engine):
+per long read, bin = int((POS + length/2) / BIN) with Sam::Alignment's length
+rule (Alignment.pm:417-431), ncscore = AS/length * length/(40+length); a bin
+holding more than LEN bases admits a record only if it beats the bin's lowest
+ncscore, which it then evicts.  Records pass through it in output order and the
+survivors are printed in that order (parity unpinned).  Not restated:
 mem_sort_dedup_patch, bwa's MAPQ model.
 """
 from __future__ import annotations
 
 import argparse
+import re
 import gzip
 import os
 import sys
@@ -146,12 +155,51 @@ def options(a) -> Tuple[seed.SeedOpts, sw.SwOpts]:
 SwRunner = Callable[[sw.SwInput, sw.SwOpts], "sw.SwResult"]
 
 
+def aln_length(cigar: str, seq_len: int) -> int:
+    """Sam::Alignment::length (Alignment.pm:417-431): M+D if SEQ is '*' or the CIGAR starts
+    or ends with S, else the SEQ length."""
+    ops = [(int(n), o) for n, o in re.findall(r"(\d+)([MIDNSHP=X])", cigar)]
+    if seq_len == 0 or (ops and (ops[0][1] == "S" or ops[-1][1] == "S")):
+        return sum(n for n, o in ops if o in "MD")
+    return seq_len
+
+
+class BinFilter:
+    """-b/-l score binning over the records of one run (see the module docstring)."""
+
+    def __init__(self, bin_size: int, bin_bases: float):
+        self.b, self.cap = float(bin_size), float(bin_bases)
+        self.bins = {}     # (lr, bin) -> [bases, [(ncscore, rid)] descending, stable]
+        self.alive = []
+
+    def add(self, lr: int, pos1: int, length: int, score: float) -> int:
+        rid = len(self.alive)
+        self.alive.append(False)
+        if length <= 0:
+            return rid
+        nc = (score / length) * (length / (40 + length))
+        key = (lr, int((pos1 + length / 2.0) / self.b))
+        ent = self.bins.setdefault(key, [0, []])
+        lst = ent[1]
+        if ent[0] > self.cap:
+            if nc <= lst[-1][0]:
+                return rid
+            _, old, olen = lst.pop()
+            self.alive[old] = False
+            ent[0] -= olen
+        ent[0] += length
+        i = len(lst) - 1
+        while i >= 0 and nc > lst[i][0]:
+            i -= 1
+        lst.insert(i + 1, (nc, rid, length))
+        self.alive[rid] = True
+        return rid
+
+
 def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=None) -> int:
     out = out or sys.stdout
     log = log or sys.stderr
     a = parse_mem(argv)
-    if a.b or a.l:
-        print(f"[bwa-proovread] -b {a.b} -l {a.l}: bin filter not applied (bam2cns bins downstream)", file=log)
     so, wo = options(a)
     lr_names, lr_seqs, _ = read_fastx(a.ref)
     sr_names, sr_seqs, sr_quals = read_fastx(a.reads)
@@ -170,6 +218,8 @@ def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=Non
         out.write(f"@SQ\tSN:{n}\tLN:{len(s)}\n")
     out.write("@PG\tID:bwa-proovread\tPN:bwa-proovread\tVN:prgpu\tCL:bwa-proovread mem " + " ".join(argv) + "\n")
     st, ps, sc, pos = res["status"], res["pass"], res["score"], res["pos"]
+    filt = BinFilter(a.b, a.l) if a.b > 0 and a.l > 0 else None
+    records = []
     t = 0
     nt = len(tasks)
     while t < nt:
@@ -193,9 +243,17 @@ def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=Non
                     quals = qual.decode() if qual is not None else "*"
                 flag = (16 if strand else 0) | (0 if x == best else 256)
                 mapq = 60 if x == best else 0
-                out.write(f"{sr_names[r]}\t{flag}\t{lr_names[int(tasks['lr'][x])]}\t{int(pos[x]) + 1}\t{mapq}\t"
-                          f"{res.cigar_str(x)}\t*\t0\t0\t{seqs}\t{quals}\tAS:i:{int(sc[x])}\n")
+                cig = res.cigar_str(x)
+                rec = (f"{sr_names[r]}\t{flag}\t{lr_names[int(tasks['lr'][x])]}\t{int(pos[x]) + 1}\t{mapq}\t"
+                       f"{cig}\t*\t0\t0\t{seqs}\t{quals}\tAS:i:{int(sc[x])}\n")
+                if filt is not None:
+                    filt.add(int(tasks["lr"][x]), int(pos[x]) + 1, aln_length(cig, len(q)), float(sc[x]))
+                records.append(rec)
         t = e
+    if filt is not None:
+        records = [rec for rec, keep in zip(records, filt.alive) if keep]
+        print(f"[bwa-proovread] -b {a.b} -l {a.l}: {len(records)} of {len(filt.alive)} records kept", file=log)
+    out.write("".join(records))
     return 0
 
 

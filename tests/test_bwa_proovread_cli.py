@@ -130,3 +130,31 @@ def test_cli_options_map_to_proovread_cfg():
 
 def test_cli_rejects_unknown_option(capsys):
     assert bp.main(["mem", "--bogus", "ref", "reads"]) == 1
+
+
+def test_bin_filter_reproduces_reference_binning():
+    """-b/-l (row A4, semantics unpinned): the filter is restated as Sam::Seq's
+    add_aln_by_score (Seq.pm:582-614).  On the consensus goldens (SAM records per
+    long read, made by the reference Perl engine), BinFilter with -b 20 -l 20*coverage
+    keeps exactly the alignments the reference keeps after binning."""
+    import casefmt
+    from pathlib import Path
+    from proovread_amd.bwa_proovread import BinFilter, aln_length
+    gold = Path(__file__).resolve().parent / "golden"
+    cases = casefmt.read_cases(gold / "cns_cases.txt")
+    exp = casefmt.read_expect(gold / "cns_expected.txt")
+    n = 0
+    for c in cases:
+        e = exp[c.name]
+        if e.error or not e.kept or c.p("noref") == "1":
+            continue
+        recs = [l.split("\t") for l in c.sam]
+        if any(not any(x.startswith("AS:i:") for x in r[11:]) or r[9] == "*" for r in recs):
+            continue
+        f = BinFilter(20, 20 * float(c.p("coverage")))
+        for r in recs:
+            sc = float([x for x in r[11:] if x.startswith("AS:i:")][0][5:])
+            f.add(0, int(r[3]), aln_length(r[5], len(r[9])), sc)
+        assert "".join("1" if k else "0" for k in f.alive) == e.kept, c.name
+        n += 1
+    assert n > 10
