@@ -357,6 +357,18 @@ int pr_trim_bound(const pr_trim_params *p, int32_t n, const int64_t *off, int64_
 int pr_trim_windows(const pr_trim_params *p, int32_t n, const int64_t *off, const uint8_t *qual, int64_t *win_off,
                     int32_t *win, int32_t *n_win, int n_threads);
 
+/* ------------------------------------------------------------------ */
+/* BAM I/O for the samtools drop-in (`samtools view -bS`, bin/proovread:1313): host code.
+ * pr_sam_encode: SAM text (header lines skipped) -> concatenated BAM records (each with its
+ * block_size prefix), reference ids from ref_names[n_ref]; PR_ERR_SAM on a malformed line.
+ * pr_bgzf_compress: BGZF blocks of 0xFF00 input bytes (raw deflate at `level`, BC field,
+ * CRC32, ISIZE), no EOF marker.  Outputs are library-allocated: pr_buffer_free.
+ * n_threads <= 0: all cores.                                                     */
+int pr_sam_encode(const char *text, int64_t len, const char *const *ref_names, int32_t n_ref, int n_threads,
+                  uint8_t **out, int64_t *out_len, int64_t *n_records);
+int pr_bgzf_compress(const uint8_t *data, int64_t len, int level, int n_threads, uint8_t **out, int64_t *out_len);
+void pr_buffer_free(void *p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -350,8 +350,13 @@ class BamReader:
         self.fh.close()
 
 
-def write_bam_from_sam(lines: Iterable[str], out_path: str, header_text: Optional[str] = None) -> Header:
-    """`samtools view -bS`: SAM text (header lines first) -> BAM, records in input order."""
+def write_bam_from_sam(lines: Iterable[str], out_path: str, header_text: Optional[str] = None,
+                       native: bool = True, threads: int = 0) -> Header:
+    """`samtools view -bS`: SAM text (header lines first) -> BAM, records in input order.
+
+    native: records encoded and BGZF-compressed by libprgpu (pr_sam_encode /
+    pr_bgzf_compress, threads over lines and blocks); byte-identical to the pure-Python
+    path (sam_to_record + BgzfWriter), which native=False keeps."""
     hdr_lines, recs = [], []
     it = iter(lines)
     for line in it:
@@ -362,8 +367,17 @@ def write_bam_from_sam(lines: Iterable[str], out_path: str, header_text: Optiona
             recs.append(line)
         break
     h = Header.from_sam_text(header_text if header_text is not None else "\n".join(hdr_lines) + "\n")
-    idx = h.index()
     w = BamWriter(out_path, h)
+    if native:
+        body = "".join(x if x.endswith("\n") else x + "\n" for x in recs)
+        body += "".join(x if x.endswith("\n") else x + "\n" for x in it)
+        w.w.fh.write(_native_bgzf(_native_encode(body, [n for n, _ in h.refs], threads), w.w.level, threads))
+        w.w.fh.write(EOF_BLOCK)
+        w.w.fh.flush()
+        if w._own:
+            w.fh.close()
+        return h
+    idx = h.index()
     for line in recs:
         w.write_record(sam_to_record(line, idx))
     for line in it:
@@ -371,6 +385,47 @@ def write_bam_from_sam(lines: Iterable[str], out_path: str, header_text: Optiona
             w.write_record(sam_to_record(line, idx))
     w.close()
     return h
+
+
+def _codec():
+    import ctypes as C
+    from . import _abi
+    L = _abi.lib()
+    if not getattr(L, "_bam_ready", False):
+        L.pr_sam_encode.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_char_p), C.c_int32, C.c_int,
+                                    C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.pr_bgzf_compress.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_void_p),
+                                       C.POINTER(C.c_int64)]
+        L.pr_buffer_free.argtypes = [C.c_void_p]
+        L.pr_buffer_free.restype = None
+        L._bam_ready = True
+    return L, C, _abi
+
+
+def _take(L, C, p, n) -> bytes:
+    try:
+        return C.string_at(p.value, n.value) if n.value else b""
+    finally:
+        L.pr_buffer_free(p)
+
+
+def _native_encode(text: str, names: Sequence[str], threads: int = 0) -> bytes:
+    """SAM record lines -> BAM records (block_size prefixed), libprgpu pr_sam_encode."""
+    L, C, _abi = _codec()
+    raw = text.encode()
+    arr = (C.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
+    p, n, nr = C.c_void_p(), C.c_int64(), C.c_int64()
+    _abi.check(L.pr_sam_encode(raw, len(raw), arr, len(names), threads, C.byref(p), C.byref(n), C.byref(nr)),
+               "pr_sam_encode")
+    return _take(L, C, p, n)
+
+
+def _native_bgzf(data: bytes, level: int = 6, threads: int = 0) -> bytes:
+    """BGZF blocks of data (no EOF marker), libprgpu pr_bgzf_compress."""
+    L, C, _abi = _codec()
+    p, n = C.c_void_p(), C.c_int64()
+    _abi.check(L.pr_bgzf_compress(data, len(data), level, threads, C.byref(p), C.byref(n)), "pr_bgzf_compress")
+    return _take(L, C, p, n)
 
 
 def _set_sort_order(text: str, so: str) -> str:

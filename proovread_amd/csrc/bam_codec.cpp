@@ -1,0 +1,311 @@
+// SAM text -> BAM records and BGZF compression for the samtools drop-in (SURVEY.md
+// §8f.3: `samtools view -bS` after bwa-proovread, bin/proovread:1313).  Host code,
+// threads over line ranges / BGZF blocks.  Byte-identical to proovread_amd/bamio.py
+// (sam_to_record, BgzfWriter): same record layout (SAM/BAM spec), smallest-fitting
+// integer tag type in the order c, C, s, S, i, I, and the same zlib raw-deflate
+// parameters per 0xFF00-byte block.
+#include <stdint.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/prgpu.h"
+
+int pr_set_error(int code, const char *msg);
+
+namespace {
+
+const char OPS[] = "MIDNSHP=X";
+
+int nt16(char c) {
+    switch (c >= 'a' && c <= 'z' ? c - 32 : c) {
+        case '=': return 0;
+        case 'A': return 1;
+        case 'C': return 2;
+        case 'M': return 3;
+        case 'G': return 4;
+        case 'R': return 5;
+        case 'S': return 6;
+        case 'V': return 7;
+        case 'T': return 8;
+        case 'W': return 9;
+        case 'Y': return 10;
+        case 'H': return 11;
+        case 'K': return 12;
+        case 'D': return 13;
+        case 'B': return 14;
+        default: return 15;
+    }
+}
+
+int reg2bin(int64_t beg, int64_t end) {
+    --end;
+    if (beg >> 14 == end >> 14) return (int)(((1 << 15) - 1) / 7 + (beg >> 14));
+    if (beg >> 17 == end >> 17) return (int)(((1 << 12) - 1) / 7 + (beg >> 17));
+    if (beg >> 20 == end >> 20) return (int)(((1 << 9) - 1) / 7 + (beg >> 20));
+    if (beg >> 23 == end >> 23) return (int)(((1 << 6) - 1) / 7 + (beg >> 23));
+    if (beg >> 26 == end >> 26) return (int)(((1 << 3) - 1) / 7 + (beg >> 26));
+    return 0;
+}
+
+template <class T>
+void put(std::string &o, T v) {
+    o.append(reinterpret_cast<const char *>(&v), sizeof v);
+}
+
+bool parse_i64(const char *s, const char *e, int64_t &v) {
+    std::string t(s, e);
+    char *end = nullptr;
+    v = std::strtoll(t.c_str(), &end, 10);
+    return end && *end == 0 && !t.empty();
+}
+
+// One SAM line [s, e) -> record (block_size prefix included) appended to o; false if malformed.
+bool encode_line(const char *s, const char *e, const std::unordered_map<std::string, int> &ref, std::string &o) {
+    std::vector<std::pair<const char *, const char *>> f;
+    const char *p = s;
+    for (const char *q = s; q <= e; ++q)
+        if (q == e || *q == '\t') {
+            f.emplace_back(p, q);
+            p = q + 1;
+        }
+    if (f.size() < 11) return false;
+    auto str = [&](int i) { return std::string(f[i].first, f[i].second); };
+    int64_t flag, pos, mapq, pnext, tlen;
+    if (!parse_i64(f[1].first, f[1].second, flag) || !parse_i64(f[3].first, f[3].second, pos) ||
+        !parse_i64(f[4].first, f[4].second, mapq) || !parse_i64(f[7].first, f[7].second, pnext) ||
+        !parse_i64(f[8].first, f[8].second, tlen))
+        return false;
+    // CIGAR
+    std::vector<uint32_t> ops;
+    const std::string cig = str(5);
+    if (cig != "*") {
+        int64_t num = 0;
+        bool have = false;
+        for (char c : cig) {
+            if (c >= '0' && c <= '9') {
+                num = num * 10 + (c - '0');
+                have = true;
+            } else {
+                const char *k = std::strchr(OPS, c);
+                if (!k || !*k || !have) return false;
+                ops.push_back((uint32_t)(num << 4) | (uint32_t)(k - OPS));
+                num = 0;
+                have = false;
+            }
+        }
+    }
+    int64_t span = 0;
+    for (uint32_t x : ops) {
+        const int op = x & 15;
+        if (op == 0 || op == 2 || op == 3 || op == 7 || op == 8) span += x >> 4;
+    }
+    const std::string rname = str(2), rnext = str(6), qname = str(0);
+    auto rid_of = [&](const std::string &n) {
+        auto it = ref.find(n);
+        return it == ref.end() ? -1 : it->second;
+    };
+    const int32_t rid = rname != "*" ? rid_of(rname) : -1;
+    const int32_t nid = rnext == "=" ? rid : (rnext != "*" ? rid_of(rnext) : -1);
+    const int64_t beg = pos - 1;
+    const int64_t end = beg + (span ? span : 1);
+    const std::string seq = str(9), qual = str(10);
+    const int32_t l_seq = seq == "*" ? 0 : (int32_t)seq.size();
+    std::string body;
+    put<int32_t>(body, rid);
+    put<int32_t>(body, (int32_t)beg);
+    put<uint8_t>(body, (uint8_t)(qname.size() + 1));
+    put<uint8_t>(body, (uint8_t)mapq);
+    put<uint16_t>(body, (uint16_t)(beg >= 0 ? reg2bin(beg, end) : 4680));
+    put<uint16_t>(body, (uint16_t)ops.size());
+    put<uint16_t>(body, (uint16_t)flag);
+    put<int32_t>(body, l_seq);
+    put<int32_t>(body, nid);
+    put<int32_t>(body, (int32_t)(pnext - 1));
+    put<int32_t>(body, (int32_t)tlen);
+    body += qname;
+    body.push_back('\0');
+    for (uint32_t x : ops) put<uint32_t>(body, x);
+    std::string sb((size_t)(l_seq + 1) / 2, '\0');
+    for (int32_t i = 0; i < l_seq; ++i) sb[(size_t)i >> 1] = (char)(sb[(size_t)i >> 1] | (nt16(seq[i]) << (4 * (1 - (i & 1)))));
+    body += sb;
+    if (qual == "*") {
+        body.append((size_t)l_seq, (char)0xFF);
+    } else {
+        const size_t nq = std::min(qual.size(), (size_t)l_seq);
+        for (size_t i = 0; i < nq; ++i) body.push_back((char)(qual[i] - 33));
+    }
+    // optional fields
+    for (size_t k = 11; k < f.size(); ++k) {
+        const std::string t = str((int)k);
+        if (t.size() < 5 || t[2] != ':' || t[4] != ':') return false;
+        const std::string tag = t.substr(0, 2), val = t.substr(5);
+        const char typ = t[3];
+        if (typ == 'i') {
+            int64_t v;
+            if (!parse_i64(val.data(), val.data() + val.size(), v)) return false;
+            body += tag;
+            if (v >= -128 && v <= 127) { body.push_back('c'); put<int8_t>(body, (int8_t)v); }
+            else if (v >= 0 && v <= 255) { body.push_back('C'); put<uint8_t>(body, (uint8_t)v); }
+            else if (v >= -32768 && v <= 32767) { body.push_back('s'); put<int16_t>(body, (int16_t)v); }
+            else if (v >= 0 && v <= 65535) { body.push_back('S'); put<uint16_t>(body, (uint16_t)v); }
+            else if (v >= INT32_MIN && v <= INT32_MAX) { body.push_back('i'); put<int32_t>(body, (int32_t)v); }
+            else if (v >= 0 && v <= (int64_t)UINT32_MAX) { body.push_back('I'); put<uint32_t>(body, (uint32_t)v); }
+            else return false;
+        } else if (typ == 'f') {
+            body += tag;
+            body.push_back('f');
+            put<float>(body, (float)std::strtod(val.c_str(), nullptr));
+        } else if (typ == 'A') {
+            body += tag;
+            body.push_back('A');
+            if (!val.empty()) body.push_back(val[0]);
+        } else if (typ == 'B') {
+            if (val.empty()) return false;
+            const char st = val[0];
+            std::vector<std::string> xs;
+            size_t a = 2;
+            while (a <= val.size() && val.size() > 1) {
+                size_t b = val.find(',', a);
+                if (b == std::string::npos) b = val.size();
+                xs.push_back(val.substr(a, b - a));
+                a = b + 1;
+            }
+            body += tag;
+            body.push_back('B');
+            body.push_back(st);
+            put<int32_t>(body, (int32_t)xs.size());
+            for (const std::string &x : xs) {
+                if (st == 'f') { put<float>(body, (float)std::strtod(x.c_str(), nullptr)); continue; }
+                int64_t v;
+                if (!parse_i64(x.data(), x.data() + x.size(), v)) return false;
+                switch (st) {
+                    case 'c': put<int8_t>(body, (int8_t)v); break;
+                    case 'C': put<uint8_t>(body, (uint8_t)v); break;
+                    case 's': put<int16_t>(body, (int16_t)v); break;
+                    case 'S': put<uint16_t>(body, (uint16_t)v); break;
+                    case 'i': put<int32_t>(body, (int32_t)v); break;
+                    case 'I': put<uint32_t>(body, (uint32_t)v); break;
+                    default: return false;
+                }
+            }
+        } else {   // Z, H
+            body += tag;
+            body.push_back(typ);
+            body += val;
+            body.push_back('\0');
+        }
+    }
+    put<int32_t>(o, (int32_t)body.size());
+    o += body;
+    return true;
+}
+
+uint8_t *take(const std::string &s, int64_t *len) {
+    uint8_t *p = (uint8_t *)std::malloc(s.size() ? s.size() : 1);
+    if (p && !s.empty()) std::memcpy(p, s.data(), s.size());
+    *len = (int64_t)s.size();
+    return p;
+}
+
+}  // namespace
+
+extern "C" int pr_sam_encode(const char *text, int64_t len, const char *const *ref_names, int32_t n_ref, int n_threads,
+                             uint8_t **out, int64_t *out_len, int64_t *n_records) {
+    if (!out || !out_len || (len && !text) || n_ref < 0 || (n_ref && !ref_names)) return pr_set_error(PR_ERR_ARG, "null arg");
+    std::unordered_map<std::string, int> ref;
+    for (int i = 0; i < n_ref; ++i) ref[ref_names[i]] = i;   // a repeated name maps to its last entry, like the dict
+    // line starts (header lines '@' and empty lines skipped)
+    std::vector<std::pair<int64_t, int64_t>> lines;
+    for (int64_t i = 0; i < len;) {
+        int64_t j = i;
+        while (j < len && text[j] != '\n') ++j;
+        int64_t e = j;
+        if (e > i && text[e - 1] == '\r') --e;
+        if (e > i && text[i] != '@') lines.emplace_back(i, e);
+        i = j + 1;
+    }
+    const int64_t n = (int64_t)lines.size();
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min(nt, 64));
+    if (n < 4096) nt = 1;
+    std::vector<std::string> part((size_t)nt);
+    std::vector<int64_t> bad((size_t)nt, -1);
+    auto work = [&](int t) {
+        for (int64_t k = n * t / nt; k < n * (t + 1) / nt; ++k)
+            if (!encode_line(text + lines[k].first, text + lines[k].second, ref, part[t])) {
+                bad[t] = k;
+                return;
+            }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+    for (int t = 0; t < nt; ++t)
+        if (bad[t] >= 0) return pr_set_error(PR_ERR_SAM, "malformed SAM record");
+    std::string all;
+    size_t tot = 0;
+    for (auto &p : part) tot += p.size();
+    all.reserve(tot);
+    for (auto &p : part) all += p;
+    *out = take(all, out_len);
+    if (n_records) *n_records = n;
+    return *out ? 0 : pr_set_error(PR_ERR_ARG, "out of host memory");
+}
+
+extern "C" int pr_bgzf_compress(const uint8_t *data, int64_t len, int level, int n_threads, uint8_t **out,
+                                int64_t *out_len) {
+    if (!out || !out_len || (len && !data)) return pr_set_error(PR_ERR_ARG, "null arg");
+    const int64_t BS = 0xFF00;
+    const int64_t nb = (len + BS - 1) / BS;
+    std::vector<std::string> blk((size_t)nb);
+    std::vector<int> fail((size_t)(nb ? nb : 1), 0);
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min(nt, 64));
+    if (nb < 2) nt = 1;
+    auto work = [&](int t) {
+        std::vector<uint8_t> buf(compressBound(BS) + 64);
+        for (int64_t b = t; b < nb; b += nt) {
+            const uint8_t *src = data + b * BS;
+            const uInt n = (uInt)std::min(BS, len - b * BS);
+            z_stream z;
+            std::memset(&z, 0, sizeof z);
+            if (deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) { fail[b] = 1; continue; }
+            z.next_in = const_cast<Bytef *>(src);
+            z.avail_in = n;
+            z.next_out = buf.data();
+            z.avail_out = (uInt)buf.size();
+            const int rc = deflate(&z, Z_FINISH);
+            const size_t clen = buf.size() - z.avail_out;
+            deflateEnd(&z);
+            if (rc != Z_STREAM_END || clen + 25 > 65536) { fail[b] = 1; continue; }
+            std::string &o = blk[(size_t)b];
+            const uint8_t hdr[18] = {31, 139, 8, 4, 0, 0, 0, 0, 0, 255, 6, 0, 66, 67, 2, 0,
+                                     (uint8_t)((clen + 25) & 0xFF), (uint8_t)((clen + 25) >> 8)};
+            o.append(reinterpret_cast<const char *>(hdr), 18);
+            o.append(reinterpret_cast<const char *>(buf.data()), clen);
+            const uint32_t crc = (uint32_t)crc32(crc32(0L, Z_NULL, 0), src, n);
+            put<uint32_t>(o, crc);
+            put<uint32_t>(o, (uint32_t)n);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+    for (int64_t b = 0; b < nb; ++b)
+        if (fail[b]) return pr_set_error(PR_ERR_ARG, "deflate failed");
+    std::string all;
+    for (auto &b : blk) all += b;
+    *out = take(all, out_len);
+    return *out ? 0 : pr_set_error(PR_ERR_ARG, "out of host memory");
+}
+
+extern "C" void pr_buffer_free(void *p) { std::free(p); }
