@@ -47,9 +47,9 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the configs[1] workload per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-lrs-per-worker", type=int, default=256)
-    ap.add_argument("--seeds", choices=("truth", "host", "gpu"), default="truth",
-                    help="task list: simulation truth, or the seeding front end (host path / GPU path), "
-                         "computed before the timed region")
+    ap.add_argument("--seeds", choices=("truth", "host", "gpu"), default="host",
+                    help="task list: the product's seeding front end (host path / GPU path; bwa mem seeding "
+                         "+ chaining restated), or the simulation truth; computed before the timed region")
     return ap.parse_args()
 
 

@@ -1,7 +1,9 @@
 """End-to-end parity of one GPU iteration (pr_iter_*: SW -> device hand-off ->
 consensus) against the CPU chain SW oracle -> SAM -> coordinate sort ->
 consensus oracle, on seeded synthetic long/short reads.  Bar: byte-exact
-corrected reads (sequence and qualities), traces and chimera records."""
+corrected reads (sequence and qualities), traces and chimera records.  The task
+list is either the simulation truth or the product's own seeding front end
+(pr_seed_map, bwa mem seeding + chaining restated), as bench.py uses it."""
 import numpy as np
 import pytest
 
@@ -11,10 +13,16 @@ from pipeline_oracle import consensus_cases, sam_for_tasks
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("seeds", ["truth", "host"])
 @pytest.mark.parametrize("finish", [False, True])
-def test_iteration_matches_cpu_chain(finish):
-    from proovread_amd import cns, iteration, sw, synth
+def test_iteration_matches_cpu_chain(finish, seeds):
+    from proovread_amd import cns, iteration, seed, sw, synth
     d = synth.simulate(31 + finish, 40000, 40, 2500, 15, sr_frac=1.0)
+    if seeds == "host":
+        ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+        d = synth.with_seeded_tasks(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(finish), threads=4))
+        ix.close()
+        assert len(d.t_sr) > 10 * d.n_lr
     task = "bwa-sr-finish" if finish else "bwa-sr"
     params = {"coverage": "22.5" if finish else "11.25", "use_ref_qual": "0" if finish else "1",
               "detect_chimera": "1" if finish else "0"}
