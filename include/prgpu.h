@@ -285,6 +285,11 @@ typedef struct pr_iter_batch {
     pr_sw_batch sw;               /* tasks grouped by long read                        */
     const int64_t *task_lr_off;   /* [sw.n_lr+1]: tasks of read i are [off[i],off[i+1]) */
     const uint8_t *lr_qual;       /* phred+33 qualities of the long reads (lr_off), or NULL */
+    const uint8_t *ref_seq;       /* ASCII bases of the consensus reference (bam2cns --ref, the
+                                   * previous iteration's .fq; lr_off layout), or NULL: the SW long
+                                   * reads (sw.lr_seq, nt4) are the reference.  Differs from the
+                                   * mapping reference after masking (proovread:848-858: bwa maps
+                                   * to .masked.fa, bam2cns reads the unmasked .fq)             */
 } pr_iter_batch;
 int pr_iter_upload(pr_ctx *ctx, const pr_iter_batch *b);
 int pr_iter_launch(pr_ctx *ctx, const pr_sw_opts *o, const pr_cns_params *p);   /* async */

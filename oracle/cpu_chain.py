@@ -27,6 +27,9 @@ _ASCII = np.frombuffer(b"ACGTN", np.uint8)
 _D = None        # dataset shared with forked workers
 _OPTS = None
 _PARAMS = None
+_REF = None      # optional ASCII consensus reference pool (lr_off layout), else the mapped reads
+_QUAL = None     # optional reference qualities (phred+33), else '$'
+_FULL = False    # return (rc, fastq, trace, chim) instead of (rc, fastq)
 
 
 def _lr_chain(lr: int):
@@ -56,11 +59,17 @@ def _lr_chain(lr: int):
     recs.sort(key=lambda x: (x[0], x[1], x[2]))
     lines = [x[3].encode() for x in recs]
     arr = (C.c_char_p * (len(lines) + 1))(*lines)
-    ref = _ASCII[d.lr_seq[int(d.lr_off[lr]):int(d.lr_off[lr + 1])]].tobytes()
+    a, b = int(d.lr_off[lr]), int(d.lr_off[lr + 1])
+    ref = _REF[a:b].tobytes() if _REF is not None else _ASCII[d.lr_seq[a:b]].tobytes()
+    qual = _QUAL[a:b].tobytes() if _QUAL is not None else b"$" * len(ref)
+    name = d.lr_names[lr] if hasattr(d, "lr_names") else f"lr{lr}"
     res = ob.OcnsResult()
-    rc = ob.lib().ocns_run(C.byref(_PARAMS), f"lr{lr}".encode(), ref, b"$" * len(ref), len(ref), arr, len(lines),
+    rc = ob.lib().ocns_run(C.byref(_PARAMS), name.encode(), ref, qual, len(ref), arr, len(lines),
                            None, 0, C.byref(res))
-    out = (rc, res.fastq.decode() if rc == 0 else "")
+    if _FULL:
+        out = (rc, res.fastq.decode(), res.trace.decode(), res.chim.decode()) if rc == 0 else (rc, "", "", "")
+    else:
+        out = (rc, res.fastq.decode() if rc == 0 else "")
     ob.lib().ocns_free(C.byref(res))
     return out
 
@@ -69,10 +78,18 @@ def _init_worker():
     ob.sw_lib()
 
 
-def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers=None):
-    """Run the CPU chain on long reads `lrs`; returns (wall seconds, bases, results, workers)."""
-    global _D, _OPTS, _PARAMS
+def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers=None, ref_seq=None,
+               ref_qual=None, detect_chimera=False, full=False):
+    """Run the CPU chain on long reads `lrs`; returns (wall seconds, bases, results, workers).
+
+    ref_seq / ref_qual: ASCII consensus reference and its qualities in the long reads' layout
+    (bam2cns --ref, the previous iteration's .fq) when it differs from the mapped reads;
+    full: per read (rc, fastq, trace, chim lines) instead of (rc, fastq)."""
+    global _D, _OPTS, _PARAMS, _REF, _QUAL, _FULL
     _D = d
+    _REF = None if ref_seq is None else np.ascontiguousarray(ref_seq, np.uint8)
+    _QUAL = None if ref_qual is None else np.ascontiguousarray(ref_qual, np.uint8)
+    _FULL = bool(full)
     if not hasattr(d, "_task_off"):
         d._task_off = np.zeros(d.n_lr + 1, np.int64)
         np.cumsum(np.bincount(d.t_lr, minlength=d.n_lr), out=d._task_off[1:])
@@ -90,7 +107,7 @@ def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers
     _PARAMS.ref_phred_offset = 33
     _PARAMS.use_ref_qual = int(use_ref_qual)
     _PARAMS.qual_weighted = 0
-    _PARAMS.detect_chimera = 0
+    _PARAMS.detect_chimera = int(detect_chimera)
     _PARAMS.invert_scores = 0
     ob.build() if not ob.LIB.exists() else None
     ob.sw_lib()

@@ -1,0 +1,274 @@
+"""proovread's sr correction loop in one process, on one GPU.
+
+bin/proovread runs the tasks of its mode (proovread.cfg:105-127; `sr-noccs`:
+read-long, bwa-sr-1 .. bwa-sr-6, bwa-sr-finish) as separate programs joined by
+files.  This module runs the same loop with the reads held in memory and the
+hot stages on the device:
+
+  read-long        (proovread:1368-1524) stubby long reads dropped, upper case,
+                   IUPAC -> N, natural (`byfile`) id order; the mapping reference
+                   is the read itself (`.masked.fa` with --lower-case: same codes)
+  bwa-sr-k         (proovread:835-869) short reads sampled with SeqChunker
+                   (cov2seqchunker, proovread:2085-2102), seeded against the
+                   previous iteration's masked reads (bwa-proovread mem front end,
+                   seed.SeedIndex), seed extension + CIGAR + hand-off + consensus on
+                   the GPU (pr_iter_*) with the previous iteration's unmasked .fq as
+                   bam2cns --ref (sequence and qualities, use_ref_qual), then
+                   SeqFilter --phred-mask on the GPU (pr_mask_run) -> the next
+                   mapping reference and bpN/bpt for mask_shortcut_frac
+                   (proovread:1700-1720, 2026-2047)
+  bwa-sr-finish    (proovread:838-850, 1572-1577) 30x sampling, finish scoring,
+                   unmasked reference, --no-use-ref-qual, --max-ins-length 0,
+                   --detect-chimera
+
+The device stages are behind `GpuStages` (the product; it fails loudly without
+libprgpu.so and a gfx950 device).  Tests drive the same loop with the CPU oracle
+chain in place of the stages (tests/loop_oracle.py) to check the GPU loop
+byte-for-byte.  Deliberate scope: one GPU, the whole read set resident (at
+configs[1] size ~17 GB of device buffers, far below 288 GB); bwa-proovread's
+-b/-l bin filter is not applied (the consensus' own binning follows).
+"""
+from __future__ import annotations
+
+import dataclasses
+import functools
+from types import SimpleNamespace
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import control, seqchunker
+
+NT4 = np.full(256, 4, np.uint8)
+for _i, _c in enumerate(b"ACGT"):
+    NT4[_c] = _i
+    NT4[_c + 32] = _i
+
+# proovread.cfg:119 (the sr-noccs task list) and the per-task values the loop reads
+SR_NOCCS_TASKS = ("read-long", "bwa-sr-1", "bwa-sr-2", "bwa-sr-3", "bwa-sr-4", "bwa-sr-5", "bwa-sr-6",
+                  "bwa-sr-finish")
+HCR_MASK_DEF = "20,41,80,130,60,0.7"                      # proovread.cfg:234-242
+HCR_MASK_LATE = "20,41,80,130,60,0.3"                     # bwa-sr-4 .. bwa-sr-6
+
+
+def hcr_mask_for(task: str) -> str:
+    return HCR_MASK_LATE if task in ("bwa-sr-4", "bwa-sr-5", "bwa-sr-6") else HCR_MASK_DEF
+
+
+def sr_coverage_for(task: str) -> float:
+    return 30.0 if task.endswith("-finish") else 15.0       # proovread.cfg:188-192
+
+
+@dataclasses.dataclass
+class LoopConfig:
+    coverage: float = 50.0                 # --coverage (proovread.cfg:48)
+    coverage_scale_factor: float = 0.75    # proovread.cfg:256
+    mask_shortcut_frac: float = 0.92       # proovread.cfg:246
+    mask_min_gain_frac: float = 0.03       # proovread.cfg:249
+    sampling: bool = True                  # --no-sampling turns it off
+    min_sr_length: Optional[int] = None    # proovread:530-532 (None: shortest short read)
+    lr_min_length: Optional[int] = None    # cfg lr-min-length (None: 2 * min_sr_length)
+    tasks: Tuple[str, ...] = SR_NOCCS_TASKS
+    seed_threads: int = 0
+
+
+@dataclasses.dataclass
+class LongReads:
+    """The current long-read set: the .fq of the last task (ids, sequences, qualities)."""
+    ids: List[str]
+    seqs: List[bytes]
+    quals: List[bytes]
+
+    def pool(self, which: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+        off = np.zeros(len(which) + 1, np.int64)
+        np.cumsum([len(s) for s in which], out=off[1:])
+        buf = np.frombuffer(b"".join(which), np.uint8).copy() if which else np.zeros(0, np.uint8)
+        return buf, off
+
+    def fastq(self) -> str:
+        return "".join(f"@{i}\n{s.decode()}\n+\n{q.decode()}\n" for i, s, q in zip(self.ids, self.seqs, self.quals))
+
+
+@dataclasses.dataclass
+class TaskLog:
+    task: str
+    n_sr: int = 0
+    n_tasks: int = 0
+    bpt: int = 0
+    bpn: int = 0
+    masked_frac: Optional[float] = None
+    shortcut: str = ""
+
+
+@dataclasses.dataclass
+class LoopResult:
+    reads: LongReads
+    chim: List[str]                        # .chim.tsv lines of the finish task (id from to score)
+    ignored: List[str]                     # .ignored.tsv lines (stubby reads)
+    log: List[TaskLog]
+    masked: Optional[List[bytes]] = None   # the last regular iteration's masked reads
+
+
+# ---------------------------------------------------------------------------- read-long
+def read_long(records: Sequence[Tuple[str, bytes, Optional[bytes]]], stubby_length: int) -> Tuple[LongReads, List[str]]:
+    """proovread:1368-1524 on (id, seq, qual or None) records: FASTA reads get '$'
+    qualities, reads shorter than stubby_length go to .ignored.tsv, sequences are
+    upper-cased with every non-ACGTN char -> N, ids in `byfile` order."""
+    from .bam2cns import byfile_cmp
+    keep: Dict[str, Tuple[bytes, bytes]] = {}
+    ignored = []
+    for rid, seq, qual in records:
+        if len(seq) < stubby_length:
+            ignored.append(f"{rid}\tstubby")
+            continue
+        if rid in keep:
+            raise ValueError(f"Non-unique long read id ({rid})")
+        s = seq.upper()
+        s = bytes(c if c in b"ACGTN" else ord("N") for c in s)
+        keep[rid] = (s, qual if qual is not None else b"$" * len(s))
+    ids = sorted(keep, key=functools.cmp_to_key(byfile_cmp))
+    return LongReads(ids, [keep[i][0] for i in ids], [keep[i][1] for i in ids]), ignored
+
+
+# ---------------------------------------------------------------------------- short reads
+class ShortReads:
+    """The short-read input as one byte stream (`cat $or_files`, proovread:1293) with its
+    FASTQ/FASTA records, sampled per task like SeqChunker."""
+
+    def __init__(self, data: bytes, chunk_number: int = 1000):
+        self.data = data
+        self.n_chunks, self.chunks = seqchunker.chunk(data, n_chunks=chunk_number)
+        self.spans = [r for c in self.chunks for r in c]
+        self.lengths = [len(self._seq(s, e)) for s, e in self.spans]
+
+    def _seq(self, s: int, e: int) -> bytes:
+        rec = self.data[s:e]
+        if rec[:1] == b">":
+            return b"".join(rec.split(b"\n")[1:]).strip()
+        return rec.split(b"\n")[1].strip()
+
+    def sample(self, sc: Optional[Dict[str, int]]) -> Tuple[np.ndarray, np.ndarray]:
+        """nt4 pool of the records SeqChunker writes for cov2seqchunker's parameters
+        (None: every record), in stream order."""
+        if sc is None:
+            spans = self.spans
+        else:
+            ks = seqchunker.select(self.n_chunks, sc["--first-chunk"], sc["--chunk-step"], sc["--chunks-per-step"])
+            spans = [r for k in ks for r in self.chunks[k - 1]]
+        seqs = [self._seq(s, e) for s, e in spans]
+        off = np.zeros(len(seqs) + 1, np.int64)
+        np.cumsum([len(x) for x in seqs], out=off[1:])
+        pool = NT4[np.frombuffer(b"".join(seqs), np.uint8)] if seqs else np.zeros(0, np.uint8)
+        return np.ascontiguousarray(pool), off
+
+
+# ---------------------------------------------------------------------------- device stages
+class GpuStages:
+    """The product's device stages: pr_iter_* (SW + hand-off + consensus) and pr_mask_run."""
+
+    def __init__(self, ctx=None):
+        from . import _abi
+        self.ctx = ctx or _abi.default_context()
+
+    def iteration(self, d, ref_seq: np.ndarray, ref_qual: np.ndarray, finish: bool, params) -> List[tuple]:
+        """-> per long read (status, seq, qual, chim lines with id `lr<i>`)."""
+        from . import iteration, sw
+        it = iteration.Iteration(d, lr_qual=ref_qual, ctx=self.ctx, ref_seq=ref_seq)
+        it.launch(sw.default_opts(finish=finish), params)
+        return [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
+
+    def mask(self, seqs: List[bytes], quals: List[bytes], hcr_mask: str, min_sr_length: int):
+        """-> (masked reads, bpt, bpN)."""
+        from . import mask
+        masked, _, (bpt, bpn) = mask.run(seqs, quals, mask.params(hcr_mask, min_sr_length), ctx=self.ctx)
+        return masked, bpt, bpn
+
+
+def _tasks_dataset(lr_map: np.ndarray, lr_off: np.ndarray, sr: np.ndarray, sr_off: np.ndarray, tasks: np.ndarray):
+    from .sw import SwInput
+    order = np.argsort(tasks["lr"], kind="stable")
+    t = tasks[order]
+    d = SimpleNamespace(lr_seq=lr_map, lr_off=lr_off, sr_seq=sr, sr_off=sr_off, n_lr=len(lr_off) - 1,
+                        n_sr=len(sr_off) - 1, t_sr=t["sr"].astype(np.int32), t_lr=t["lr"].astype(np.int32),
+                        t_strand=t["strand"].astype(np.uint8), t_qbeg=t["qbeg"].astype(np.int32),
+                        t_rbeg=t["rbeg"].astype(np.int32), t_slen=t["slen"].astype(np.int32))
+    d.sw_input = lambda: SwInput(d.sr_off, d.sr_seq, d.lr_off, d.lr_seq, d.t_sr, d.t_lr, d.t_strand, d.t_qbeg,
+                                 d.t_rbeg, d.t_slen)
+    return d
+
+
+def _rename(lines: List[str], rid: str) -> List[str]:
+    return [rid + "\t" + ln.split("\t", 1)[1] for ln in lines]
+
+
+# ---------------------------------------------------------------------------- the loop
+def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes, cfg: Optional[LoopConfig] = None,
+        stages=None) -> LoopResult:
+    """The sr-noccs loop (bin/proovread:705-905) from long-read records and the short-read
+    FASTQ/FASTA stream; returns the finish task's reads and chimera lines and a log per task."""
+    from . import cns, seed
+    cfg = cfg or LoopConfig()
+    stages = stages or GpuStages()
+    srs = ShortReads(sr_data)
+    min_sr = cfg.min_sr_length or (min(srs.lengths) if srs.lengths else 200)
+    stubby = cfg.lr_min_length if cfg.lr_min_length is not None else 2 * min_sr
+    sampler = control.Sampler(sampling=cfg.sampling)
+    tasks = list(cfg.tasks)
+    fracs: List[float] = []
+    log: List[TaskLog] = []
+    reads, ignored = None, []
+    mapped: List[bytes] = []          # the mapping reference of the next task (.masked.fa)
+    chim: List[str] = []
+    last_masked = None
+    tc = 0
+    while tc < len(tasks):   # proovread:705 (tasks may shrink: mask_shortcut_frac splices)
+        task = tasks[tc]
+        if task == "read-long":
+            reads, ignored = read_long(lr_records, stubby)
+            mapped = list(reads.seqs)
+            log.append(TaskLog(task))
+            tc += 1
+            continue
+        if not task.startswith("bwa-sr"):
+            raise ValueError(f"task {task} is outside the sr-noccs loop")
+        finish = task.endswith("-finish")
+        ent = TaskLog(task)
+        task_cov = sr_coverage_for(task)
+        sr, sr_off = srs.sample(sampler.cov2seqchunker(cfg.coverage, task_cov))
+        ent.n_sr = len(sr_off) - 1
+        ref_map = reads.seqs if finish else mapped     # finish maps to the unmasked .fq (proovread:838-850)
+        lr_map, lr_off = reads.pool(ref_map)
+        lr_map = NT4[lr_map]
+        ix = seed.SeedIndex(lr_map, lr_off)
+        try:
+            tk = ix.map(sr, sr_off, seed.default_opts(finish), threads=cfg.seed_threads)
+        finally:
+            ix.close()
+        ent.n_tasks = int(len(tk))
+        d = _tasks_dataset(lr_map, lr_off, sr, sr_off, tk)
+        ref_seq, _ = reads.pool(reads.seqs)
+        ref_qual, _ = reads.pool(reads.quals)
+        max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541
+        params = cns.CnsParams(coverage=max_cov, use_ref_qual=not finish, detect_chimera=finish,
+                               max_ins_length=0)
+        out = stages.iteration(d, ref_seq, ref_qual, finish, params)
+        seqs, quals = [], []
+        for i, (st, s, q, ch) in enumerate(out):
+            if st != 0:
+                raise RuntimeError(f"{task}: consensus of {reads.ids[i]} failed with status {st}")
+            seqs.append(s)
+            quals.append(q)
+            if finish:
+                chim += _rename(ch, reads.ids[i])
+        reads = LongReads(reads.ids, seqs, quals)
+        if not finish:
+            masked, bpt, bpn = stages.mask(seqs, quals, hcr_mask_for(task), min_sr)
+            mapped = masked
+            last_masked = masked
+            ent.bpt, ent.bpn = bpt, bpn
+            ent.masked_frac = control.masked_fraction(bpt, bpn) if bpt else 0.0
+            ent.shortcut = control.mask_shortcut(tasks, tc, ent.masked_frac, fracs, cfg.mask_shortcut_frac,
+                                                 cfg.mask_min_gain_frac)
+        log.append(ent)
+        tc += 1
+    return LoopResult(reads, chim, ignored, log, last_masked)

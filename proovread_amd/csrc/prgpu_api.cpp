@@ -98,6 +98,7 @@ struct pr_ctx {
     float last_ms = 0.f;
     // SW -> consensus pipeline (pr_iter_*)
     bool pipe = false;
+    bool pipe_ref_ascii = false;   // pr_iter_batch.ref_seq given: consensus reference in CB_REF_SEQ
     int pipe_sort_cap = 0;
     DevBuf pb[4];           // task_off, cnt, err, (spare)
     float ms_pipe = 0.f, ms_cns = 0.f;
@@ -415,8 +416,13 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         SwPtrs sp;
         int rc = sw_get_ptrs(c, &sp);
         if (rc) return rc;
-        D.ref_seq = sp.lr;
-        D.ref_nt4 = 1;
+        if (c->pipe_ref_ascii) {   // bam2cns --ref differs from the mapping reference (masked HCRs)
+            D.ref_seq = B[CB_REF_SEQ].as<uint8_t>();
+            D.ref_nt4 = 0;
+        } else {
+            D.ref_seq = sp.lr;
+            D.ref_nt4 = 1;
+        }
         D.seq = sp.sr;
         D.seq_nt4 = 1;
         D.cig = sp.cig;
@@ -539,6 +545,7 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
     c->n_aln = sb.n_task;
     c->total_cols = sb.lr_off[n];
     c->has_ref = true;
+    c->pipe_ref_ascii = b->ref_seq != nullptr;
     c->has_qual = b->lr_qual != nullptr;
     c->has_ign = false;
     c->lr_off_host.assign(sb.lr_off, sb.lr_off + n + 1);
@@ -562,6 +569,7 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
     const size_t na1 = (size_t)sb.n_task + 1, n1 = (size_t)n + 1;
     if ((rc = upload(B[CB_LR_OFF], sb.lr_off, n1, s))) return rc;
     if (b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)sb.lr_off[n], s))) return rc;
+    if (b->ref_seq && (rc = upload(B[CB_REF_SEQ], b->ref_seq, (size_t)sb.lr_off[n], s))) return rc;
     if ((rc = upload(c->pb[0], b->task_lr_off, n1, s))) return rc;
     if ((rc = c->pb[1].ensure(n1 * 4)) || (rc = c->pb[2].ensure(n1 * 4))) return rc;
     if ((rc = B[CB_ALN_OFF].ensure(n1 * 8)) || (rc = B[CB_POS].ensure(na1 * 4)) ||

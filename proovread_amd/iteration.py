@@ -14,7 +14,7 @@ from . import _abi, cns, sw
 
 
 class IterBatch(C.Structure):
-    _fields_ = [("sw", sw.SwBatch), ("task_lr_off", _abi.P64), ("lr_qual", _abi.PU8)]
+    _fields_ = [("sw", sw.SwBatch), ("task_lr_off", _abi.P64), ("lr_qual", _abi.PU8), ("ref_seq", _abi.PU8)]
 
 
 def _setup(L):
@@ -35,7 +35,11 @@ def _setup(L):
 class Iteration:
     """A resident iteration batch on one GPU (upload once, launch many)."""
 
-    def __init__(self, d, lr_qual: Optional[np.ndarray] = None, ctx: Optional[_abi.Context] = None):
+    def __init__(self, d, lr_qual: Optional[np.ndarray] = None, ctx: Optional[_abi.Context] = None,
+                 ref_seq: Optional[np.ndarray] = None):
+        """d: reads + tasks (synth.Dataset fields); lr_qual: the reference qualities (phred+33,
+        default '$'); ref_seq: ASCII consensus reference when it differs from the mapped long
+        reads d.lr_seq (iterations after the first map to the masked consensus)."""
         self.L = _abi.lib()
         _setup(self.L)
         self.ctx = ctx or _abi.default_context()
@@ -47,10 +51,17 @@ class Iteration:
         if lr_qual is None:
             lr_qual = np.full(int(d.lr_off[-1]), ord("$"), np.uint8)   # raw CLR reads: phred 3
         self.lr_qual = lr_qual
+        if ref_seq is not None:
+            ref_seq = np.ascontiguousarray(ref_seq, np.uint8)
+            if len(ref_seq) != int(d.lr_off[-1]):
+                raise ValueError("ref_seq must have the long reads' layout (lr_off)")
+        self.ref_seq = ref_seq
         b = IterBatch()
         b.sw = self.inp.c_batch()
         b.task_lr_off = _abi.ptr(self.task_lr_off, C.c_int64)
         b.lr_qual = _abi.ptr(self.lr_qual, C.c_uint8)
+        if ref_seq is not None:
+            b.ref_seq = _abi.ptr(self.ref_seq, C.c_uint8)
         self._b = b
         _abi.check(self.L.pr_iter_upload(self.ctx.h, C.byref(b)), "pr_iter_upload")
         nl, nt, bd = C.c_int32(), C.c_int64(), _abi.CnsBounds()

@@ -9,7 +9,7 @@ sys.path.insert(0, str(HERE.parent))
 # GPU test modules whose kernels have not yet run on an MI355X run after the rest
 # of the suite, so that under `pytest -x` a failure there cannot hide the results
 # of the validated kernels.
-RUN_LAST = ("test_fantasticus_cns.py", "test_mask_gpu.py", "test_seed_gpu.py")
+RUN_LAST = ("test_fantasticus_cns.py", "test_mask_gpu.py", "test_seed_gpu.py", "test_correct_loop.py")
 
 
 def pytest_configure(config):
@@ -17,4 +17,7 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(session, config, items):
-    items.sort(key=lambda it: Path(str(it.fspath)).name in RUN_LAST)
+    def rank(it):
+        name = Path(str(it.fspath)).name
+        return RUN_LAST.index(name) + 1 if name in RUN_LAST else 0
+    items.sort(key=rank)

@@ -1,0 +1,102 @@
+"""The in-process sr-noccs loop (proovread_amd.correct; bin/proovread:705-905).
+
+CPU: read-long preprocessing (stubby reads, IUPAC -> N, byfile order), SeqChunker
+sampling equal to the SeqChunker drop-in's output, and the whole loop driven by
+the oracle stages (tests/loop_oracle.py): the reads get corrected, the masked
+fraction grows, mask_shortcut_frac decides like proovread.
+GPU: the loop on the device stages (pr_iter_* with the previous .fq as consensus
+reference, pr_mask_run) equals the oracle loop byte-for-byte at every task:
+corrected reads, qualities, chimera lines, masked fractions and the task list."""
+import io
+
+import numpy as np
+import pytest
+
+from proovread_amd import correct, seqchunker, synth
+
+ACGT = np.frombuffer(b"ACGT", np.uint8)
+
+
+def _inputs(seed=5, gl=24000, n_lr=10, lr_len=2400, sr_cov=40.0):
+    d = synth.simulate(seed, gl, n_lr, lr_len, sr_cov, sr_frac=1.0)
+    lrs = [(f"lr_{i}", ACGT[np.minimum(d.lr_seq[d.lr_off[i]:d.lr_off[i + 1]], 3)].tobytes(), None)
+           for i in range(d.n_lr)]
+    sr = io.BytesIO()
+    for i in range(d.n_sr):
+        s = ACGT[np.minimum(d.sr_seq[d.sr_off[i]:d.sr_off[i + 1]], 3)].tobytes()
+        sr.write(b"@sr%d\n%s\n+\n%s\n" % (i, s, b"I" * len(s)))
+    return d, lrs, sr.getvalue()
+
+
+def _kmers(g, k=20):
+    s = ACGT[g].tobytes()
+    rc = s[::-1].translate(bytes.maketrans(b"ACGT", b"TGCA"))
+    return {t[i:i + k] for t in (s, rc) for i in range(len(t) - k + 1)}
+
+
+def _exact(s, km, k=20):
+    n = len(s) - k + 1
+    return sum(s[i:i + k] in km for i in range(n)) / max(n, 1)
+
+
+def test_read_long_preprocessing():
+    recs = [("r10", b"acgtRYacgt" * 30, None), ("r9", b"ACGT" * 80, b"#" * 320), ("r1", b"ACGT" * 10, None)]
+    reads, ign = correct.read_long(recs, 300)
+    assert reads.ids == ["r9", "r10"]                  # byfile: 9 < 10; r1 is stubby
+    assert ign == ["r1\tstubby"]
+    assert reads.seqs[1] == b"ACGTNNACGT" * 30 and reads.quals[1] == b"$" * 300
+    assert reads.quals[0] == b"#" * 320
+    with pytest.raises(ValueError):
+        correct.read_long([("a", b"A" * 10, None), ("a", b"C" * 10, None)], 1)
+
+
+def test_short_read_sampling_matches_seqchunker():
+    _, _, data = _inputs()
+    srs = correct.ShortReads(data)
+    sc = {"--chunk-number": 1000, "--chunk-step": 20, "--chunks-per-step": 6, "--first-chunk": 3}
+    pool, off = srs.sample(sc)
+    out = io.BytesIO()
+    import tempfile
+    with tempfile.NamedTemporaryFile(suffix=".fq") as f:
+        f.write(data)
+        f.flush()
+        args = [x for k, v in sc.items() for x in (k, str(v))] + [f.name]
+        assert seqchunker.main(args, stdout=out) == 0
+    recs = out.getvalue().split(b"\n")[1::4]
+    assert len(recs) == len(off) - 1 and 0 < len(recs) < len(srs.lengths)
+    got = [ACGT[np.minimum(pool[off[i]:off[i + 1]], 3)].tobytes() for i in range(len(off) - 1)]
+    assert got == recs
+
+
+def test_loop_on_oracle_stages():
+    import loop_oracle
+    d, lrs, srd = _inputs()
+    res = correct.run(lrs, srd, correct.LoopConfig(coverage=40.0, seed_threads=2), stages=loop_oracle.OracleStages(4))
+    tasks = [e.task for e in res.log]
+    assert tasks[0] == "read-long" and tasks[-1] == "bwa-sr-finish"
+    fr = [e.masked_frac for e in res.log[1:-1]]
+    assert fr[0] > 0.05 and fr == sorted(fr)
+    if len(tasks) < 8:                                 # shortcut taken: by proovread's rule
+        assert res.log[len(tasks) - 2].shortcut == "skip"
+    km = _kmers(d.genome)
+    raw = np.mean([_exact(s, km) for _, s, _ in lrs])
+    cor = np.mean([_exact(s, km) for s in res.reads.seqs])
+    assert raw < 0.3 and cor > 0.85, (raw, cor)
+    assert all(len(s) == len(q) for s, q in zip(res.reads.seqs, res.reads.quals))
+    for ln in res.chim:
+        assert ln.split("\t")[0] in res.reads.ids
+
+
+@pytest.mark.gpu
+def test_gpu_loop_matches_oracle_loop():
+    import loop_oracle
+    _, lrs, srd = _inputs(seed=6)
+    cfg = correct.LoopConfig(coverage=40.0, seed_threads=4)
+    want = correct.run(lrs, srd, cfg, stages=loop_oracle.OracleStages(8))
+    got = correct.run(lrs, srd, cfg)
+    assert [e.task for e in got.log] == [e.task for e in want.log]
+    for g, w in zip(got.log, want.log):
+        assert (g.n_sr, g.n_tasks, g.bpt, g.bpn, g.shortcut) == (w.n_sr, w.n_tasks, w.bpt, w.bpn, w.shortcut), g.task
+    assert got.reads.seqs == want.reads.seqs
+    assert got.reads.quals == want.reads.quals
+    assert got.chim == want.chim
