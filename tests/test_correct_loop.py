@@ -100,3 +100,46 @@ def test_gpu_loop_matches_oracle_loop():
     assert got.reads.seqs == want.reads.seqs
     assert got.reads.quals == want.reads.quals
     assert got.chim == want.chim
+
+
+# ---------------------------------------------------------------- configs[0]: the bundled sample
+def _sample_inputs():
+    from test_fantasticus_chain import FX, simulate_sr
+    from proovread_amd import bwa_proovread as bp, sw
+    names, seqs, quals = bp.read_fastx(str(FX / "F.antasticus_long_error.fq"))
+    _, gs, _ = bp.read_fastx(str(FX / "F.antasticus_genome.fa"))
+    G = sw.NT4[np.frombuffer(gs[0], np.uint8)]
+    sr, off = simulate_sr(G, 50)
+    buf = io.BytesIO()
+    for i in range(len(off) - 1):
+        s = ACGT[sr[off[i]:off[i + 1]]].tobytes()
+        buf.write(b"@sr%d\n%s\n+\n%s\n" % (i, s, b"I" * len(s)))
+    return G, list(zip(names, seqs, quals)), buf.getvalue()
+
+
+def test_loop_on_sample_oracle_stages():
+    """configs[0] through the whole sr-noccs loop on the oracle stages: every genomic
+    read ends >= 95 % genome-exact (20-mers), the contamination read does not."""
+    import loop_oracle
+    G, lrs, srd = _sample_inputs()
+    res = correct.run(lrs, srd, correct.LoopConfig(coverage=50.0, seed_threads=4), stages=loop_oracle.OracleStages(4))
+    assert res.log[-1].task == "bwa-sr-finish" and len(res.reads.ids) == len(lrs)
+    km = _kmers(G)
+    for rid, s in zip(res.reads.ids, res.reads.seqs):
+        f = _exact(s, km)
+        if rid.startswith("long_contamination"):
+            assert f < 0.5, rid
+        else:
+            assert f >= 0.95, (rid, f)
+
+
+@pytest.mark.gpu
+def test_gpu_loop_on_sample_matches_oracle_loop():
+    import loop_oracle
+    _, lrs, srd = _sample_inputs()
+    cfg = correct.LoopConfig(coverage=50.0, seed_threads=4)
+    want = correct.run(lrs, srd, cfg, stages=loop_oracle.OracleStages(8))
+    got = correct.run(lrs, srd, cfg)
+    assert [(e.task, e.n_tasks, e.bpn) for e in got.log] == [(e.task, e.n_tasks, e.bpn) for e in want.log]
+    assert got.reads.fastq() == want.reads.fastq()
+    assert got.chim == want.chim
