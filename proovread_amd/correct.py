@@ -201,12 +201,93 @@ def _rename(lines: List[str], rid: str) -> List[str]:
     return [rid + "\t" + ln.split("\t", 1)[1] for ln in lines]
 
 
+# ---------------------------------------------------------------------------- multi-rank
+class Comm:
+    """The collectives of the multi-rank loop over torch.distributed (RCCL on GPUs with
+    device tensors, gloo on CPU).  Layout: SURVEY.md §8e's exact-parity option
+    (exact_shard.py): every rank keeps the whole read set and its index, seeds a
+    contiguous shard of the sampled short reads, sends each task to the owner of its
+    long read (one all-to-all), corrects and masks the long reads it owns; the corrected
+    and masked reads are then all-gathered for the next task's index and consensus
+    reference, and bpt/bpN all-reduced so every rank takes the same mask_shortcut
+    decision (the north star's per-iteration statistics gather)."""
+
+    def __init__(self, group=None, device: Optional[str] = None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = device
+
+    def _dev(self):
+        import torch
+        return torch.device(self.device) if self.device else torch.device("cpu")
+
+    def allreduce_ints(self, vals: Sequence[int]) -> List[int]:
+        import torch
+        t = torch.tensor(list(vals), dtype=torch.int64, device=self._dev())
+        self.dist.all_reduce(t, group=self.group)
+        return [int(x) for x in t.cpu().tolist()]
+
+    def allgather_bytes(self, blob: bytes) -> List[bytes]:
+        import torch
+        n = self.world
+        size = torch.tensor([len(blob)], dtype=torch.int64, device=self._dev())
+        sizes = [torch.zeros_like(size) for _ in range(n)]
+        self.dist.all_gather(sizes, size, group=self.group)
+        sz = [int(x.item()) for x in sizes]
+        cap = max(max(sz), 1)
+        buf = torch.zeros(cap, dtype=torch.uint8)
+        if blob:
+            buf[:len(blob)] = torch.from_numpy(np.frombuffer(blob, np.uint8).copy())
+        buf = buf.to(self._dev())
+        outs = [torch.empty(cap, dtype=torch.uint8, device=self._dev()) for _ in range(n)]
+        self.dist.all_gather(outs, buf, group=self.group)
+        return [outs[r][:sz[r]].cpu().numpy().tobytes() for r in range(n)]
+
+    def allgather_lists(self, items: List[bytes]) -> List[bytes]:
+        """Concatenation over ranks (rank order) of per-rank lists of byte strings."""
+        lens = np.array([len(x) for x in items], np.int64).tobytes()
+        parts = self.allgather_bytes(np.int64(len(items)).tobytes() + lens + b"".join(items))
+        out: List[bytes] = []
+        for p in parts:
+            k = int(np.frombuffer(p[:8], np.int64)[0])
+            ln = np.frombuffer(p[8:8 + 8 * k], np.int64)
+            o = 8 + 8 * k
+            for x in ln:
+                out.append(p[o:o + int(x)])
+                o += int(x)
+        return out
+
+
+def _seed_tasks(lr_map, lr_off, sr, sr_off, finish, threads, comm: Optional[Comm]):
+    """Tasks of the long reads this rank corrects (global ids), in the single run's order,
+    and the [lo, hi) long-read range it owns."""
+    from . import exact_shard as ex, seed
+    ix = seed.SeedIndex(lr_map, lr_off)
+    try:
+        if comm is None or comm.world == 1:
+            return ix.map(sr, sr_off, seed.default_opts(finish), threads=threads), 0, len(lr_off) - 1
+        s, e = ex.sr_range(len(sr_off) - 1, comm.world, comm.rank)
+        tk = ix.map(sr[sr_off[s]:sr_off[e]], sr_off[s:e + 1] - sr_off[s], seed.default_opts(finish), threads=threads)
+    finally:
+        ix.close()
+    tk["sr"] += s
+    b = ex.lr_bounds(lr_off, comm.world)
+    got = ex.group_by_lr(ex.exchange_tasks(tk, b, device=comm.device, group=comm.group))
+    return got, int(b[comm.rank]), int(b[comm.rank + 1])
+
+
+# ---------------------------------------------------------------------------- the loop
 # ---------------------------------------------------------------------------- the loop
 def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes, cfg: Optional[LoopConfig] = None,
-        stages=None) -> LoopResult:
+        stages=None, comm: Optional[Comm] = None) -> LoopResult:
     """The sr-noccs loop (bin/proovread:705-905) from long-read records and the short-read
-    FASTQ/FASTA stream; returns the finish task's reads and chimera lines and a log per task."""
-    from . import cns, seed
+    FASTQ/FASTA stream; returns the finish task's reads and chimera lines and a log per task.
+    With `comm` (world > 1) every rank calls run() on the same inputs and gets the same
+    result; the work is split as Comm describes.  n_tasks in the log is the rank's share."""
+    from . import cns
     cfg = cfg or LoopConfig()
     stages = stages or GpuStages()
     srs = ShortReads(sr_data)
@@ -239,30 +320,42 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         ref_map = reads.seqs if finish else mapped     # finish maps to the unmasked .fq (proovread:838-850)
         lr_map, lr_off = reads.pool(ref_map)
         lr_map = NT4[lr_map]
-        ix = seed.SeedIndex(lr_map, lr_off)
-        try:
-            tk = ix.map(sr, sr_off, seed.default_opts(finish), threads=cfg.seed_threads)
-        finally:
-            ix.close()
+        tk, lo, hi = _seed_tasks(lr_map, lr_off, sr, sr_off, finish, cfg.seed_threads, comm)
         ent.n_tasks = int(len(tk))
+        if hi - lo < len(reads.ids):   # this rank's long reads only
+            tk = tk.copy()
+            tk["lr"] -= lo
+            lr_map = lr_map[lr_off[lo]:lr_off[hi]]
+            lr_off = lr_off[lo:hi + 1] - lr_off[lo]
         d = _tasks_dataset(lr_map, lr_off, sr, sr_off, tk)
-        ref_seq, _ = reads.pool(reads.seqs)
-        ref_qual, _ = reads.pool(reads.quals)
+        ids = reads.ids[lo:hi]
+        ref_seq, _ = reads.pool(reads.seqs[lo:hi])
+        ref_qual, _ = reads.pool(reads.quals[lo:hi])
         max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541
         params = cns.CnsParams(coverage=max_cov, use_ref_qual=not finish, detect_chimera=finish,
                                max_ins_length=0)
-        out = stages.iteration(d, ref_seq, ref_qual, finish, params)
-        seqs, quals = [], []
+        out = stages.iteration(d, ref_seq, ref_qual, finish, params) if hi > lo else []
+        seqs, quals, lines = [], [], []
         for i, (st, s, q, ch) in enumerate(out):
             if st != 0:
-                raise RuntimeError(f"{task}: consensus of {reads.ids[i]} failed with status {st}")
+                raise RuntimeError(f"{task}: consensus of {ids[i]} failed with status {st}")
             seqs.append(s)
             quals.append(q)
             if finish:
-                chim += _rename(ch, reads.ids[i])
+                lines += _rename(ch, ids[i])
+        masked, bpt, bpn = [], 0, 0
+        if not finish and seqs:
+            masked, bpt, bpn = stages.mask(seqs, quals, hcr_mask_for(task), min_sr)
+        if comm is not None and comm.world > 1:
+            seqs, quals = comm.allgather_lists(seqs), comm.allgather_lists(quals)
+            if finish:
+                lines = [x.decode() for x in comm.allgather_lists([x.encode() for x in lines])]
+            else:
+                masked = comm.allgather_lists(masked)
+                bpt, bpn = comm.allreduce_ints([bpt, bpn])
+        chim += lines
         reads = LongReads(reads.ids, seqs, quals)
         if not finish:
-            masked, bpt, bpn = stages.mask(seqs, quals, hcr_mask_for(task), min_sr)
             mapped = masked
             last_masked = masked
             ent.bpt, ent.bpn = bpt, bpn
@@ -272,3 +365,61 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         log.append(ent)
         tc += 1
     return LoopResult(reads, chim, ignored, log, last_masked)
+
+
+# ---------------------------------------------------------------------------- command line
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    """python -m proovread_amd.correct -l LR.fq -s SR.fq [-s ...] --pre OUT [--coverage C]
+
+    Writes OUT.fq (the finish task's corrected reads), OUT.chim.tsv and OUT.ignored.tsv.
+    Launched with torch.distributed.run (one rank per GPU), the ranks split the work as
+    Comm describes and rank 0 writes the files."""
+    import argparse
+    import os
+    import sys
+    from .bwa_proovread import read_fastx
+    ap = argparse.ArgumentParser(prog="proovread_amd.correct")
+    ap.add_argument("-l", "--long-reads", action="append", required=True)
+    ap.add_argument("-s", "--short-reads", action="append", required=True)
+    ap.add_argument("-p", "--pre", required=True)
+    ap.add_argument("--coverage", type=float, default=50.0)
+    ap.add_argument("--no-sampling", action="store_true")
+    ap.add_argument("-t", "--threads", type=int, default=0)
+    a = ap.parse_args(argv)
+    lrs = []
+    for f in a.long_reads:
+        names, seqs, quals = read_fastx(f)
+        lrs += list(zip(names, seqs, quals))
+    sr_data = b"".join(open(f, "rb").read() for f in a.short_reads)
+    cfg = LoopConfig(coverage=a.coverage, sampling=not a.no_sampling, seed_threads=a.threads)
+    comm, rank = None, 0
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch
+        import torch.distributed as dist
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        comm = Comm(device=f"cuda:{local}")
+        rank = comm.rank
+        from . import _abi
+        stages = GpuStages(_abi.Context(local))
+    else:
+        stages = GpuStages()
+    res = run(lrs, sr_data, cfg, stages=stages, comm=comm)
+    if rank == 0:
+        with open(a.pre + ".fq", "w") as f:
+            f.write(res.reads.fastq())
+        with open(a.pre + ".chim.tsv", "w") as f:
+            f.write("#id\tfrom\tto\tscore\n" + "".join(ln + "\n" for ln in res.chim))
+        with open(a.pre + ".ignored.tsv", "w") as f:
+            f.write("".join(ln + "\n" for ln in res.ignored))
+        for e in res.log:
+            if e.masked_frac is not None:
+                print(f"{e.task}: {e.n_sr} short reads, masked {100 * e.masked_frac:.1f}% {e.shortcut}", file=sys.stderr)
+    if comm is not None:
+        comm.dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

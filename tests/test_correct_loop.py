@@ -143,3 +143,42 @@ def test_gpu_loop_on_sample_matches_oracle_loop():
     assert [(e.task, e.n_tasks, e.bpn) for e in got.log] == [(e.task, e.n_tasks, e.bpn) for e in want.log]
     assert got.reads.fastq() == want.reads.fastq()
     assert got.chim == want.chim
+
+
+# ---------------------------------------------------------------- multi-rank (exact layout)
+def _loop_rank(rank, world, port, outdir):
+    import json
+    import os
+    import torch.distributed as dist
+    import loop_oracle
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _, lrs, srd = _inputs(seed=7)
+    res = correct.run(lrs, srd, correct.LoopConfig(coverage=40.0, seed_threads=2),
+                      stages=loop_oracle.OracleStages(1), comm=correct.Comm())
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as f:
+        json.dump({"fastq": res.reads.fastq(), "chim": res.chim, "n_tasks": [e.n_tasks for e in res.log],
+                   "log": [(e.task, e.n_sr, e.bpt, e.bpn, e.shortcut) for e in res.log]}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_loop_two_ranks_equals_single_process(tmp_path):
+    """world_size-2 gloo run of the loop (short-read shards, task all-to-all to the long-read
+    owners, all-gather of corrected and masked reads, all-reduce of bpt/bpN) gives exactly
+    the single-process loop's reads, chimera lines and task decisions on both ranks."""
+    import json
+    import torch.multiprocessing as tmp
+    import loop_oracle
+    from test_exact_shard import _free_port
+    world = 2
+    tmp.spawn(_loop_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    _, lrs, srd = _inputs(seed=7)
+    want = correct.run(lrs, srd, correct.LoopConfig(coverage=40.0, seed_threads=2), stages=loop_oracle.OracleStages(2))
+    got = [json.loads((tmp_path / f"r{r}.json").read_text()) for r in range(world)]
+    for g in got:
+        assert g["fastq"] == want.reads.fastq()
+        assert g["chim"] == want.chim
+        assert [tuple(x) for x in g["log"]] == [(e.task, e.n_sr, e.bpt, e.bpn, e.shortcut) for e in want.log]
+    assert [a + b for a, b in zip(got[0]["n_tasks"], got[1]["n_tasks"])] == [e.n_tasks for e in want.log]
+    assert min(got[0]["n_tasks"][1:]) > 0 and min(got[1]["n_tasks"][1:]) > 0
