@@ -367,11 +367,35 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
     return LoopResult(reads, chim, ignored, log, last_masked)
 
 
+# ---------------------------------------------------------------------------- outputs
+def write_outputs(res: LoopResult, pre: str, min_length: int = 500, trim_win: str = "12,5") -> None:
+    """The files of bin/proovread:905-958 (without siamaera, which needs BLAST):
+    PRE.untrimmed.fq, PRE.chim.tsv (ChimeraToSeqFilter of the finish task's chimera lines),
+    PRE.trimmed.fq (SeqFilter --trim-win 12,5 --min-length 500 --substr PRE.chim.tsv,
+    proovread.cfg:152-155) and PRE.trimmed.fa; also PRE.ignored.tsv."""
+    import os
+    from . import chimera_filter, seqfilter
+    with open(pre + ".untrimmed.fq", "w") as f:
+        f.write(res.reads.fastq())
+    raw = ["#id\tfrom\tto\tscore"] + res.chim          # correct_sr_mt's header (proovread:1679)
+    with open(pre + ".chim.tsv", "w") as f:
+        f.write("".join(x + "\n" for x in chimera_filter.convert(raw)))
+    with open(pre + ".ignored.tsv", "w") as f:
+        f.write("".join(ln + "\n" for ln in res.ignored))
+    rc = seqfilter.run(["--trim-win", trim_win, "--min-length", str(min_length), "--substr", pre + ".chim.tsv",
+                        "--in", pre + ".untrimmed.fq", "--out", pre + ".trimmed.fq", "--phred-offset", "33"])
+    if rc:
+        raise RuntimeError("SeqFilter trimming failed")
+    if os.path.getsize(pre + ".trimmed.fq"):   # proovread:947
+        seqfilter.run(["--in", pre + ".trimmed.fq", "--out", pre + ".trimmed.fa", "--fasta", "--phred-offset", "33"])
+
+
 # ---------------------------------------------------------------------------- command line
 def main(argv: Optional[Sequence[str]] = None) -> int:
     """python -m proovread_amd.correct -l LR.fq -s SR.fq [-s ...] --pre OUT [--coverage C]
 
-    Writes OUT.fq (the finish task's corrected reads), OUT.chim.tsv and OUT.ignored.tsv.
+    Writes write_outputs' files (OUT.untrimmed.fq, OUT.trimmed.fq/.fa, OUT.chim.tsv,
+    OUT.ignored.tsv).
     Launched with torch.distributed.run (one rank per GPU), the ranks split the work as
     Comm describes and rank 0 writes the files."""
     import argparse
@@ -407,12 +431,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         stages = GpuStages()
     res = run(lrs, sr_data, cfg, stages=stages, comm=comm)
     if rank == 0:
-        with open(a.pre + ".fq", "w") as f:
-            f.write(res.reads.fastq())
-        with open(a.pre + ".chim.tsv", "w") as f:
-            f.write("#id\tfrom\tto\tscore\n" + "".join(ln + "\n" for ln in res.chim))
-        with open(a.pre + ".ignored.tsv", "w") as f:
-            f.write("".join(ln + "\n" for ln in res.ignored))
+        write_outputs(res, a.pre)
         for e in res.log:
             if e.masked_frac is not None:
                 print(f"{e.task}: {e.n_sr} short reads, masked {100 * e.masked_frac:.1f}% {e.shortcut}", file=sys.stderr)

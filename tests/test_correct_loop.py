@@ -182,3 +182,25 @@ def test_loop_two_ranks_equals_single_process(tmp_path):
         assert [tuple(x) for x in g["log"]] == [(e.task, e.n_sr, e.bpt, e.bpn, e.shortcut) for e in want.log]
     assert [a + b for a, b in zip(got[0]["n_tasks"], got[1]["n_tasks"])] == [e.n_tasks for e in want.log]
     assert min(got[0]["n_tasks"][1:]) > 0 and min(got[1]["n_tasks"][1:]) > 0
+
+
+def test_loop_outputs_on_sample(tmp_path):
+    """write_outputs: untrimmed = the loop's reads; trimmed reads are >= 500 bp pieces of them
+    cut at the chimera breakpoints and quality windows (SeqFilter drop-in), FASTA mirrors FASTQ."""
+    import loop_oracle
+    from proovread_amd.seqfilter import read_records
+    G, lrs, srd = _sample_inputs()
+    res = correct.run(lrs, srd, correct.LoopConfig(coverage=50.0, seed_threads=4), stages=loop_oracle.OracleStages(4))
+    pre = str(tmp_path / "out")
+    correct.write_outputs(res, pre)
+    un = read_records(pre + ".untrimmed.fq")
+    assert [r[2] for r in un] == res.reads.seqs
+    tr = read_records(pre + ".trimmed.fq")
+    fa = read_records(pre + ".trimmed.fa")
+    assert len(tr) >= 100 and [r[2] for r in tr] == [r[2] for r in fa]
+    full = dict(zip(res.reads.ids, res.reads.seqs))
+    for r in tr:
+        rid = r[0].split()[0]
+        base = rid.rsplit(".", 1)[0] if rid not in full else rid
+        assert len(r[2]) >= 500 and r[2] in full[base], rid
+    assert (tmp_path / "out.chim.tsv").exists() and (tmp_path / "out.ignored.tsv").read_text() == ""
