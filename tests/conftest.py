@@ -9,7 +9,8 @@ sys.path.insert(0, str(HERE.parent))
 # GPU test modules whose kernels have not yet run on an MI355X run after the rest
 # of the suite, so that under `pytest -x` a failure there cannot hide the results
 # of the validated kernels.
-RUN_LAST = ("test_fantasticus_cns.py", "test_mask_gpu.py", "test_seed_gpu.py", "test_correct_loop.py")
+RUN_LAST = ("test_fantasticus_cns.py", "test_mask_gpu.py", "test_seed_gpu.py", "test_correct_loop.py",
+            "test_sw_edge_gpu.py")
 
 
 def pytest_configure(config):
