@@ -47,13 +47,6 @@ constexpr int KX = 28;                       // bases stored after each 12-mer h
 constexpr uint64_t KX_MASK = (1ull << (2 * KX)) - 1;
 
 // 2-bit pack of s[0, n) (n <= KX), base i at bits 2i; stops at the first non-ACGT
-inline uint64_t pack_ext(const uint8_t *s, int n) {
-    uint64_t v = 0;
-    int k = 0;
-    for (; k < n && s[k] < 4; ++k) v |= (uint64_t)s[k] << (2 * k);
-    return v | ((uint64_t)k << 56);
-}
-
 struct Index {
     // text: forward long reads, then the reverse complement of their concatenation
     // (bwa's forward-reverse layout), each contig followed by SEP
@@ -359,8 +352,7 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
             if (++run >= KI && p - KI + 1 >= p0) f(code, (uint32_t)(p - KI + 1));
         }
     };
-    // counting and filling split over text chunks; chunk t's positions of a k-mer go
-    // after those of chunks < t, so every list stays in ascending text order
+    // counting split over text chunks (per-chunk counts, then the table offsets)
     int nt = (int)std::thread::hardware_concurrency();
     nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);
     if (n < (int64_t)1 << 22) nt = 1;
@@ -379,38 +371,95 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     I.koff.assign(NK + 1, 0);
     for (uint32_t k = 0; k < NK; ++k) {
         uint32_t sum = 0;
-        for (int t = 0; t < nt; ++t) {
-            const uint32_t v = tc[(size_t)t][k];
-            tc[(size_t)t][k] = I.koff[k] + sum;   // chunk t's first slot for k-mer k
-            sum += v;
-        }
+        for (int t = 0; t < nt; ++t) sum += tc[(size_t)t][k];
         kc[k] = sum;
         I.koff[k + 1] = I.koff[k] + sum;
     }
     I.kpos.resize(I.koff[NK]);
     I.kext.resize(I.koff[NK]);
-    run_threads([&](int t) {
-        std::vector<uint32_t> &fill = tc[(size_t)t];
-        for_kmers(n * t / nt, n * (t + 1) / nt, [&](uint32_t k, uint32_t p) { I.kpos[fill[k]++] = p; });
-    });
-    tc.clear();
-    tc.shrink_to_fit();
-    {   // bases after every hit, in kpos order (random text reads: spread over threads)
-        const int64_t nk = (int64_t)I.kpos.size();
-        int nt = (int)std::thread::hardware_concurrency();
-        nt = nt < 1 ? 1 : (nt > 32 ? 32 : nt);
-        auto work = [&](int t) {
-            for (int64_t r = nk * t / nt; r < nk * (t + 1) / nt; ++r) {
-                const uint32_t p = I.kpos[r];
-                const int64_t n_after = n - ((int64_t)p + KI);   // the text ends with SEP: pack_ext stops there
-                I.kext[r] = pack_ext(T + p + KI, n_after < KX ? (int)n_after : KX);
+    // Fill in two cache-friendly passes instead of one scatter over the whole table:
+    //  1. every thread walks its text chunk once, computing the k-mer code and the KX bases
+    //     after it with rolling windows (sequential reads), and appends (pos, low k-mer bits,
+    //     ext) to one of NB buckets by the high k-mer bits (NB sequential write streams);
+    //  2. every bucket (a contiguous koff range, ~1/NB of the table) is counting-sorted by
+    //     the low bits into kpos / kext, writes staying inside the bucket's region.
+    // A bucket holds thread 0's records, then thread 1's ..., each in text order, and pass 2
+    // is stable, so every k-mer's positions stay in ascending text order.
+    constexpr int LB = 12;                    // low k-mer bits sorted in pass 2
+    constexpr uint32_t NB = NK >> LB;         // buckets
+    struct Rec {
+        uint32_t pos, low;
+        uint64_t ext;
+    };
+    std::vector<Rec> tmp(I.koff[NK]);
+    {
+        // per-thread bucket cursors: bucket b starts at koff[b << LB]; thread t after threads < t
+        std::vector<std::vector<uint64_t>> cur((size_t)nt, std::vector<uint64_t>(NB, 0));
+        for (uint32_t b = 0; b < NB; ++b) {
+            uint64_t o = I.koff[b << LB];
+            for (int t = 0; t < nt; ++t) {
+                cur[(size_t)t][b] = o;
+                uint64_t sz = 0;
+                for (uint32_t k = b << LB; k < ((b + 1) << LB); ++k) sz += tc[(size_t)t][k];
+                o += sz;
             }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
-        work(0);
-        for (auto &x : th) x.join();
+        }
+        tc.clear();
+        tc.shrink_to_fit();
+        run_threads([&](int t) {
+            const int64_t p0 = n * t / nt, p1 = n * (t + 1) / nt;
+            uint64_t *c = cur[(size_t)t].data();
+            Rec *R = tmp.data();
+            uint32_t code = 0;
+            int run = 0;
+            int64_t p = p0 - (KI - 1) > 0 ? p0 - (KI - 1) : 0;
+            // w: bases T[p+1 .. p+1+KX) two bits each (non-bases as 0); nb: first index >= p+1
+            // holding N / SEP (the text ends with SEP, so nb < n always exists)
+            uint64_t w = 0;
+            for (int j = KX - 1; j >= 0; --j) w = (w << 2) | (p + 1 + j < n ? (uint64_t)(T[p + 1 + j] & 3) : 0);
+            int64_t nb = p + 1;
+            while (nb < n && T[nb] <= 3) ++nb;
+            for (bool first = true; p < p1 + KI - 1 && p < n; ++p, first = false) {
+                if (!first) {   // slide the windows from p-1 to p
+                    const int64_t q = p + KX;
+                    w = (w >> 2) | ((q < n ? (uint64_t)(T[q] & 3) : 0) << (2 * (KX - 1)));
+                    if (nb < p + 1) {
+                        nb = p + 1;
+                        while (nb < n && T[nb] <= 3) ++nb;
+                    }
+                }
+                if (T[p] > 3) { run = 0; code = 0; continue; }
+                code = ((code << 2) | T[p]) & (NK - 1);
+                if (++run >= KI && p - KI + 1 >= p0) {
+                    int64_t m = nb - (p + 1);
+                    if (m > KX) m = KX;
+                    const uint64_t ext = (m ? (w & ((1ull << (2 * m)) - 1)) : 0) | ((uint64_t)m << 56);
+                    Rec &r = R[c[code >> LB]++];
+                    r.pos = (uint32_t)(p - KI + 1);
+                    r.low = code & ((1u << LB) - 1);
+                    r.ext = ext;
+                }
+            }
+        });
     }
+    {
+        std::atomic<uint32_t> next{0};
+        run_threads([&](int) {
+            std::vector<uint32_t> fill((size_t)1 << LB);
+            for (uint32_t b; (b = next.fetch_add(1)) < NB;) {
+                const uint32_t k0 = b << LB;
+                for (uint32_t j = 0; j < (1u << LB); ++j) fill[j] = I.koff[k0 + j];
+                for (uint64_t i = I.koff[k0]; i < I.koff[k0 + (1u << LB)]; ++i) {
+                    const Rec &r = tmp[i];
+                    const uint32_t slot = fill[r.low]++;
+                    I.kpos[slot] = r.pos;
+                    I.kext[slot] = r.ext;
+                }
+            }
+        });
+    }
+    tmp.clear();
+    tmp.shrink_to_fit();
     // j-mer counts for j < 12: C_j(x) = sum_c C_{j+1}(4x + c) + #(j-mers x ending a run of bases),
     // a run being a maximal stretch without N / SEP (an occurrence is either followed by another
     // base of its run, then it prefixes a (j+1)-mer occurrence, or it ends the run)
