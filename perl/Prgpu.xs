@@ -1,0 +1,220 @@
+/* Perl XS binding of libprgpu's consensus stage (include/prgpu.h).
+ *
+ * This is the in-process replacement a proovread maintainer binds where bin/proovread's
+ * correct_sr_mt (bin/proovread:1528-1721) fans bam2cns out over `xargs -P`
+ * (bin/proovread:1596-1619): one cns_run call processes a whole chunk of long reads
+ * (bam2cns:332-365 for every read) on the GPU.  The Sam::Seq class globals that bam2cns
+ * sets (bam2cns:227-237) arrive as a hash; the chunk arrives as the SoA buffers of
+ * pr_cns_batch, packed on the Perl side (lib/Prgpu.pm) with pack().
+ *
+ * The binding is thin on purpose: it checks that every packed buffer holds what the
+ * batch's counts say it must (so the library never reads past a Perl string), calls
+ * pr_cns_run, and hands the output pools back as packed strings.  Library errors croak
+ * with pr_last_error(), as bam2cns dies through Verbose->exit (Verbose.pm:454).
+ */
+#define PERL_NO_GET_CONTEXT
+#include "EXTERN.h"
+#include "perl.h"
+#include "XSUB.h"
+
+#include <stdint.h>
+#include <string.h>
+
+#include "prgpu.h"
+
+/* a packed batch field holding at least `need` bytes (NULL if optional and absent) */
+static const char *field(pTHX_ HV *b, const char *key, size_t need, int optional, STRLEN *got) {
+    SV **sv = hv_fetch(b, key, (I32)strlen(key), 0);
+    STRLEN len = 0;
+    const char *p;
+    if (!sv || !SvOK(*sv)) {
+        if (optional) {
+            if (got) *got = 0;
+            return NULL;
+        }
+        croak("Prgpu::cns_run: batch field '%s' missing", key);
+    }
+    p = SvPVbyte(*sv, len);
+    if (len < need)
+        croak("Prgpu::cns_run: batch field '%s' holds %lu bytes, %lu needed", key, (unsigned long)len,
+              (unsigned long)need);
+    if (got) *got = len;
+    return p;
+}
+
+static double num(pTHX_ HV *h, const char *key, double dflt) {
+    SV **sv = hv_fetch(h, key, (I32)strlen(key), 0);
+    return (sv && SvOK(*sv)) ? SvNV(*sv) : dflt;
+}
+
+static int32_t inum(pTHX_ HV *h, const char *key, int32_t dflt) {
+    SV **sv = hv_fetch(h, key, (I32)strlen(key), 0);
+    return (sv && SvOK(*sv)) ? (int32_t)SvIV(*sv) : dflt;
+}
+
+/* an int64 element of a packed buffer (Perl strings are not 8-byte aligned in general) */
+static int64_t i64_at(const char *p, int64_t i) {
+    int64_t v;
+    memcpy(&v, p + 8 * i, 8);
+    return v;
+}
+
+MODULE = Prgpu  PACKAGE = Prgpu
+
+PROTOTYPES: DISABLE
+
+const char *
+version()
+  CODE:
+    RETVAL = pr_version();
+  OUTPUT:
+    RETVAL
+
+const char *
+last_error()
+  CODE:
+    RETVAL = pr_last_error();
+  OUTPUT:
+    RETVAL
+
+int
+device_count()
+  CODE:
+    int n = 0;
+    if (pr_device_count(&n) != 0) n = 0;
+    RETVAL = n;
+  OUTPUT:
+    RETVAL
+
+IV
+ctx_create(int device)
+  CODE:
+    pr_ctx *c = NULL;
+    int rc = pr_ctx_create(device, &c);
+    if (rc != 0) croak("Prgpu: pr_ctx_create: %s (%d)", pr_last_error(), rc);
+    RETVAL = PTR2IV(c);
+  OUTPUT:
+    RETVAL
+
+void
+ctx_destroy(IV ctx)
+  CODE:
+    if (ctx) pr_ctx_destroy(INT2PTR(pr_ctx *, ctx));
+
+SV *
+cns_run(IV ctx, HV *params, HV *batch)
+  CODE:
+    pr_cns_params p;
+    pr_cns_batch b;
+    pr_cns_bounds bd;
+    pr_cns_out o;
+    const char *lr_off, *aln_off, *ign_off;
+    STRLEN seq_len = 0, qual_len = 0, cig_len = 0;
+    int64_t n, na, nbases, nign = 0, i;
+    int rc;
+    HV *res;
+    /* Sam::Seq class globals (Seq.pm:114-128) as bam2cns sets them (bam2cns:227-237) */
+    pr_cns_params_default(&p);
+    p.max_coverage = num(aTHX_ params, "coverage", p.max_coverage);
+    p.bin_size = num(aTHX_ params, "bin_size", p.bin_size);
+    p.trim = inum(aTHX_ params, "trim", p.trim);
+    p.indel_taboo_length = inum(aTHX_ params, "indel_taboo_length", p.indel_taboo_length);
+    p.indel_taboo = num(aTHX_ params, "indel_taboo", p.indel_taboo);
+    p.min_aln_length = inum(aTHX_ params, "min_aln_length", p.min_aln_length);
+    p.max_ins_length = inum(aTHX_ params, "max_ins_length", p.max_ins_length);
+    p.fallback_phred = inum(aTHX_ params, "fallback_phred", p.fallback_phred);
+    p.phred_offset = inum(aTHX_ params, "phred_offset", p.phred_offset);
+    p.ref_phred_offset = inum(aTHX_ params, "qv_offset", p.ref_phred_offset);
+    p.use_ref_qual = inum(aTHX_ params, "use_ref_qual", p.use_ref_qual);
+    p.qual_weighted = inum(aTHX_ params, "qual_weighted", p.qual_weighted);
+    p.detect_chimera = inum(aTHX_ params, "detect_chimera", p.detect_chimera);
+    p.invert_scores = inum(aTHX_ params, "invert_scores", p.invert_scores);
+
+    /* the batch: every buffer checked against the counts before the library sees it */
+    memset(&b, 0, sizeof b);
+    n = (int64_t)inum(aTHX_ batch, "n_lr", -1);
+    if (n < 0) croak("Prgpu::cns_run: batch field 'n_lr' missing or negative");
+    b.n_lr = (int32_t)n;
+    lr_off = field(aTHX_ batch, "lr_off", 8 * (size_t)(n + 1), 0, NULL);
+    aln_off = field(aTHX_ batch, "aln_off", 8 * (size_t)(n + 1), 0, NULL);
+    nbases = i64_at(lr_off, n);
+    na = i64_at(aln_off, n);
+    if (nbases < 0 || na < 0 || i64_at(lr_off, 0) != 0 || i64_at(aln_off, 0) != 0)
+        croak("Prgpu::cns_run: lr_off / aln_off must start at 0 and end non-negative");
+    b.lr_off = (const int64_t *)lr_off;
+    b.aln_off = (const int64_t *)aln_off;
+    b.ref_seq = (const uint8_t *)field(aTHX_ batch, "ref_seq", (size_t)nbases, 1, NULL);
+    b.ref_qual = (const uint8_t *)field(aTHX_ batch, "ref_qual", (size_t)nbases, 1, NULL);
+    ign_off = field(aTHX_ batch, "ign_off", 8 * (size_t)(n + 1), 1, NULL);
+    if (ign_off) {
+        nign = i64_at(ign_off, n);
+        if (nign < 0 || i64_at(ign_off, 0) != 0) croak("Prgpu::cns_run: ign_off must start at 0");
+        b.ign_off = (const int64_t *)ign_off;
+        b.ign = (const int32_t *)field(aTHX_ batch, "ign", 8 * (size_t)nign, 0, NULL);
+    }
+    b.aln_pos = (const int32_t *)field(aTHX_ batch, "aln_pos", 4 * (size_t)na, na == 0, NULL);
+    b.aln_score = (const double *)field(aTHX_ batch, "aln_score", 8 * (size_t)na, na == 0, NULL);
+    b.aln_flags = (const uint8_t *)field(aTHX_ batch, "aln_flags", (size_t)na, na == 0, NULL);
+    b.aln_seq_off = (const int64_t *)field(aTHX_ batch, "aln_seq_off", 8 * (size_t)na, na == 0, NULL);
+    b.aln_lseq = (const int32_t *)field(aTHX_ batch, "aln_lseq", 4 * (size_t)na, na == 0, NULL);
+    b.aln_cig_off = (const int64_t *)field(aTHX_ batch, "aln_cig_off", 8 * (size_t)na, na == 0, NULL);
+    b.aln_ncig = (const int32_t *)field(aTHX_ batch, "aln_ncig", 4 * (size_t)na, na == 0, NULL);
+    b.seq_pool = (const uint8_t *)field(aTHX_ batch, "seq_pool", 0, 1, &seq_len);
+    b.qual_pool = (const uint8_t *)field(aTHX_ batch, "qual_pool", 0, 1, &qual_len);
+    b.cig_pool = (const uint32_t *)field(aTHX_ batch, "cig_pool", 0, 1, &cig_len);
+    if (qual_len < seq_len) croak("Prgpu::cns_run: qual_pool shorter than seq_pool");
+    b.seq_pool_len = (int64_t)seq_len;
+    b.cig_pool_len = (int64_t)(cig_len / 4);
+    for (i = 0; i < n; ++i) {
+        int64_t l0 = i64_at(lr_off, i), l1 = i64_at(lr_off, i + 1);
+        int64_t a0 = i64_at(aln_off, i), a1 = i64_at(aln_off, i + 1);
+        if (l1 < l0 || a1 < a0 || l1 > nbases || a1 > na) croak("Prgpu::cns_run: lr_off / aln_off not monotone");
+        if (ign_off && (i64_at(ign_off, i + 1) < i64_at(ign_off, i) || i64_at(ign_off, i + 1) > nign))
+            croak("Prgpu::cns_run: ign_off not monotone");
+    }
+
+    rc = pr_cns_bounds_of(&b, &bd);
+    if (rc != 0) croak("Prgpu: pr_cns_bounds_of: %s (%d)", pr_last_error(), rc);
+    {
+        /* output pools, one Perl string each, returned as packed data */
+        SV *s_off = newSV(8 * (n + 1) + 1), *s_st = newSV(4 * n + 1), *s_sl = newSV(4 * n + 1),
+           *s_tl = newSV(4 * n + 1), *s_nc = newSV(4 * n + 1), *s_nch = newSV(4 * n + 1),
+           *s_seq = newSV(bd.seq_cap + 1), *s_qual = newSV(bd.seq_cap + 1), *s_tr = newSV(bd.seq_cap + 1),
+           *s_cig = newSV(4 * bd.seq_cap + 1), *s_choff = newSV(8 * (n + 1) + 1),
+           *s_ch = newSV(16 * bd.chim_cap + 1), *s_kept = newSV(na + 1);
+        SV *all[] = {s_off, s_st, s_sl, s_tl, s_nc, s_nch, s_seq, s_qual, s_tr, s_cig, s_choff, s_ch, s_kept};
+        const STRLEN lens[] = {8 * (n + 1), 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, bd.seq_cap, bd.seq_cap, bd.seq_cap,
+                               4 * bd.seq_cap, 8 * (n + 1), 16 * bd.chim_cap, na};
+        const char *keys[] = {"out_off", "status", "seq_len", "trace_len", "ncigar", "nchim", "seq", "qual",
+                              "trace", "cigar", "chim_off", "chim", "kept"};
+        unsigned k;
+        for (k = 0; k < sizeof all / sizeof all[0]; ++k) {
+            SvPOK_on(all[k]);
+            memset(SvPVX(all[k]), 0, lens[k] + 1);
+            SvCUR_set(all[k], lens[k]);
+        }
+        memset(&o, 0, sizeof o);
+        o.out_off = (int64_t *)SvPVX(s_off);
+        o.status = (int32_t *)SvPVX(s_st);
+        o.seq_len = (int32_t *)SvPVX(s_sl);
+        o.trace_len = (int32_t *)SvPVX(s_tl);
+        o.ncigar = (int32_t *)SvPVX(s_nc);
+        o.nchim = (int32_t *)SvPVX(s_nch);
+        o.seq = (uint8_t *)SvPVX(s_seq);
+        o.qual = (uint8_t *)SvPVX(s_qual);
+        o.trace = (uint8_t *)SvPVX(s_tr);
+        o.cigar = (uint32_t *)SvPVX(s_cig);
+        o.chim_off = (int64_t *)SvPVX(s_choff);
+        o.chim = (int32_t *)SvPVX(s_ch);
+        o.kept = (uint8_t *)SvPVX(s_kept);
+        rc = pr_cns_run(INT2PTR(pr_ctx *, ctx), &p, &b, &o);
+        if (rc != 0) {
+            for (k = 0; k < sizeof all / sizeof all[0]; ++k) SvREFCNT_dec(all[k]);
+            croak("Prgpu: pr_cns_run: %s (%d)", pr_last_error(), rc);
+        }
+        res = newHV();
+        for (k = 0; k < sizeof all / sizeof all[0]; ++k) hv_store(res, keys[k], (I32)strlen(keys[k]), all[k], 0);
+    }
+    RETVAL = newRV_noinc((SV *)res);
+  OUTPUT:
+    RETVAL

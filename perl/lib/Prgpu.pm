@@ -1,0 +1,209 @@
+package Prgpu;
+
+# Perl side of the XS binding (perl/Prgpu.xs) of libprgpu's consensus stage.
+#
+# What a proovread maintainer calls instead of fanning bam2cns out over xargs
+# (bin/proovread:1596-1619): one Prgpu::run_chunk per chunk of long reads, with the
+# reads' SAM records in BAM order.  The record fields read here are the ones the
+# Sam::Seq engine reads (Sam/Alignment.pm:87-110: POS, CIGAR, SEQ, QUAL, AS:i); the
+# chunk is flattened into the SoA buffers of pr_cns_batch (include/prgpu.h) with pack,
+# the same layout proovread_amd/cns.py:pack_chunk builds.
+#
+#   my $ctx = Prgpu::Context->new(0);
+#   my @res = Prgpu::run_chunk($ctx, {coverage => 11.25, use_ref_qual => 1},
+#                              [{id => 'r1', seq => $seq, qual => $qual, desc => $desc}],
+#                              [[@sam_lines_of_r1]]);
+#   print Prgpu::fastq($_) for @res;            # bam2cns:453
+#   print Prgpu::chim_lines($_) for @res;       # bam2cns:488
+#
+# There is no CPU fallback: without a gfx950 device Context->new dies.
+
+use strict;
+use warnings;
+
+our $VERSION = '0.1';
+
+require XSLoader;
+XSLoader::load('Prgpu', $VERSION);
+
+# status codes of include/prgpu.h
+our %ERRORS = (0 => 'PR_OK', -1 => 'PR_ERR_ARG', -2 => 'PR_ERR_HIP', -3 => 'PR_ERR_SAM',
+               -4 => 'PR_ERR_NOSEQ', -5 => 'PR_ERR_BIN_RANGE', -6 => 'PR_ERR_DIV0',
+               -7 => 'PR_ERR_CIGAR', -8 => 'PR_ERR_BEYOND_REF', -9 => 'PR_ERR_CAPACITY',
+               -10 => 'PR_ERR_UNSUPPORTED');
+
+my %CIGAR_OP = (M => 0, I => 1, D => 2, N => 3, S => 4, H => 5, P => 6, '=' => 7, X => 8);
+use constant { ALN_HAS_SCORE => 1, ALN_NO_QUAL => 2, ALN_NO_SEQ => 4 };
+
+package Prgpu::Context;
+
+sub new {
+    my ($class, $device) = @_;
+    my $h = Prgpu::ctx_create(defined $device ? $device : 0);
+    return bless {h => $h}, $class;
+}
+
+sub handle { $_[0]{h} }
+
+sub DESTROY {
+    my $self = shift;
+    Prgpu::ctx_destroy($self->{h}) if $self->{h};
+    $self->{h} = 0;
+}
+
+package Prgpu;
+
+# CIGAR string -> BAM-coded ops (len<<4 | op); dies on a malformed string like
+# Sam::Alignment's cigar parsing would produce garbage for
+sub cigar_ops {
+    my ($cig) = @_;
+    return () if $cig eq '*';
+    my @ops;
+    my $rest = $cig;
+    while ($rest =~ s/^(\d+)([MIDNSHP=X])//) {
+        push @ops, ($1 << 4) | $CIGAR_OP{$2};
+    }
+    die "Prgpu: bad CIGAR '$cig'\n" if length $rest;
+    return @ops;
+}
+
+# Flatten reads + SAM records into the packed fields of pr_cns_batch.
+sub pack_chunk {
+    my ($reads, $alns) = @_;
+    my $n = @$reads;
+    my %b = (n_lr => $n);
+    my $has_ref = $n > 0;
+    for my $r (@$reads) { $has_ref = 0 unless defined $r->{seq} }
+    my (@lr_off, @ign_off, @ign) = (0);
+    my ($ref_seq, $ref_qual) = ('', '');
+    my $any_ign = 0;
+    @ign_off = (0);
+    for my $r (@$reads) {
+        my $len = defined $r->{seq} ? length($r->{seq}) : $r->{length};
+        push @lr_off, $lr_off[-1] + $len;
+        if ($has_ref) {
+            $ref_seq .= $r->{seq};
+            # a quality string shorter than the sequence contributes nothing past its end
+            # (Seq.pm:262 `next unless $freqs[$i]`): pad with phred 0
+            my $q = defined $r->{qual} ? substr($r->{qual}, 0, $len) : '';
+            $ref_qual .= $q . ('!' x ($len - length $q));
+            # bam2cns:382-391: MCRn:off,len tags of the reference description
+            my @m = (($r->{desc} // '') =~ /MCR\d+:(\d+),(\d+)/g);
+            $any_ign ||= @m;
+            push @ign, @m;
+        }
+        push @ign_off, @ign / 2;
+    }
+    $b{lr_off} = pack('q<*', @lr_off);
+    if ($has_ref) {
+        $b{ref_seq} = $ref_seq;
+        $b{ref_qual} = $ref_qual;
+    }
+    if ($any_ign) {
+        $b{ign_off} = pack('q<*', @ign_off);
+        $b{ign} = pack('l<*', @ign);
+    }
+    my (@aln_off, @pos, @score, @flags, @seq_off, @lseq, @cig_off, @ncig, @cig) = (0);
+    my ($seq_pool, $qual_pool) = ('', '');
+    for my $list (@$alns) {
+        for my $line (@$list) {
+            chomp(my $l = $line);
+            my @f = split /\t/, $l, 12;
+            die "Prgpu: SAM line with < 11 fields\n" if @f < 11;
+            my $fl = 0;
+            my $sc = 0;
+            if (@f == 12) {
+                for my $t (split /\t/, $f[11]) {
+                    if (substr($t, 0, 2) eq 'AS') {
+                        no warnings 'numeric';
+                        $sc = 0 + substr($t, 5);   # Perl's own numification, as Sam::Alignment
+                        $fl |= ALN_HAS_SCORE;
+                    }
+                }
+            }
+            my $s = $f[9] eq '*' ? '' : $f[9];
+            $fl |= ALN_NO_SEQ if $f[9] eq '*';
+            my $q;
+            if ($f[10] eq '*') {
+                $fl |= ALN_NO_QUAL;
+                $q = '!' x length $s;
+            } else {
+                $q = substr($f[10], 0, length $s);
+                $q .= '!' x (length($s) - length $q);
+            }
+            my @ops = cigar_ops($f[5]);
+            push @pos, $f[3];
+            push @score, $sc;
+            push @flags, $fl;
+            push @seq_off, length $seq_pool;
+            push @lseq, length $s;
+            push @cig_off, scalar @cig;
+            push @ncig, scalar @ops;
+            push @cig, @ops;
+            $seq_pool .= $s;
+            $qual_pool .= $q;
+        }
+        push @aln_off, scalar @pos;
+    }
+    $b{aln_off} = pack('q<*', @aln_off);
+    $b{aln_pos} = pack('l<*', @pos);
+    $b{aln_score} = pack('d<*', @score);
+    $b{aln_flags} = pack('C*', @flags);
+    $b{aln_seq_off} = pack('q<*', @seq_off);
+    $b{aln_lseq} = pack('l<*', @lseq);
+    $b{aln_cig_off} = pack('q<*', @cig_off);
+    $b{aln_ncig} = pack('l<*', @ncig);
+    $b{seq_pool} = $seq_pool;
+    $b{qual_pool} = $qual_pool;
+    $b{cig_pool} = pack('L<*', @cig);
+    return \%b;
+}
+
+# One bam2cns chunk on the GPU (bam2cns:332-365 for every read).  Returns one hash per
+# read: id, status (0 or a PR_ERR_* code), seq, qual, trace, cigar (string), chim
+# ([from, to, n_pos, n_cols] records).
+sub run_chunk {
+    my ($ctx, $params, $reads, $alns) = @_;
+    die "Prgpu::run_chunk: reads and alignment lists differ in length\n" unless @$reads == @$alns;
+    my $b = pack_chunk($reads, $alns);
+    my $o = cns_run(ref $ctx ? $ctx->handle : $ctx, $params, $b);
+    my $n = @$reads;
+    my @off = unpack('q<*', $o->{out_off});
+    my @st = unpack('l<*', $o->{status});
+    my @sl = unpack('l<*', $o->{seq_len});
+    my @tl = unpack('l<*', $o->{trace_len});
+    my @nc = unpack('l<*', $o->{ncigar});
+    my @nch = unpack('l<*', $o->{nchim});
+    my @choff = unpack('q<*', $o->{chim_off});
+    my @res;
+    for my $i (0 .. $n - 1) {
+        my %r = (id => $reads->[$i]{id}, status => $st[$i]);
+        if ($st[$i] == 0) {
+            my $p = $off[$i];
+            $r{seq} = substr($o->{seq}, $p, $sl[$i]);
+            $r{qual} = substr($o->{qual}, $p, $sl[$i]);
+            $r{trace} = substr($o->{trace}, $p, $tl[$i]);
+            $r{cigar} = join '', map { ($_ >> 4) . substr('MID', $_ & 15, 1) }
+                unpack('L<*', substr($o->{cigar}, 4 * $p, 4 * $nc[$i]));
+            my @c = unpack('l<*', substr($o->{chim}, 16 * $choff[$i], 16 * $nch[$i]));
+            $r{chim} = [map { [@c[4 * $_ .. 4 * $_ + 3]] } 0 .. $nch[$i] - 1];
+        }
+        push @res, \%r;
+    }
+    return @res;
+}
+
+# the FASTQ record bam2cns prints (bam2cns:453, Fastq::Seq string)
+sub fastq {
+    my ($r) = @_;
+    return "\@$r->{id}\n$r->{seq}\n+\n$r->{qual}\n";
+}
+
+# the .chim.tsv lines (bam2cns:488: printf "%s\t%d\t%d\t%s\n", score in Perl's own
+# number stringification)
+sub chim_lines {
+    my ($r) = @_;
+    return map { sprintf("%s\t%d\t%d\t%s\n", $r->{id}, $_->[0], $_->[1], $_->[2] / $_->[3]) } @{$r->{chim} || []};
+}
+
+1;
