@@ -259,6 +259,9 @@ int pr_seed_map(const pr_seed_index *h, const pr_seed_opts *o, const uint8_t *sr
 void pr_seed_tasks_free(pr_seed_tasks *t);
 /* diagnostics (tests): occurrences of a string (both strands), and bwt_smem1a's SMEMs at x */
 int pr_seed_index_occ(const pr_seed_index *h, const uint8_t *s, int n, int64_t *count);
+/* order-sensitive digests of the index tables (text, koff, kpos, kext, j-mer counts,
+   contig tables): a test hook proving that build changes leave the tables identical */
+int pr_seed_index_digest(const pr_seed_index *h, uint64_t *out6);
 int pr_seed_smem(const pr_seed_index *h, const uint8_t *q, int len, int x, int64_t min_intv, int32_t *start,
                  int32_t *end, int64_t *occ, int cap, int *n_out);
 /* The GPU seeding path (seed_kernels.hip: the same per-read core, one lane per read,

@@ -28,7 +28,10 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <utility>
 #include <vector>
+
+#include <sys/mman.h>
 
 #include "../../include/prgpu.h"
 #include "seed_core.h"
@@ -47,18 +50,56 @@ constexpr int KX = 28;                       // bases stored after each 12-mer h
 constexpr uint64_t KX_MASK = (1ull << (2 * KX)) - 1;
 
 // 2-bit pack of s[0, n) (n <= KX), base i at bits 2i; stops at the first non-ACGT
+// Allocator for the index's big tables: no value-initialisation on resize (the build
+// writes every element, from many threads, so the pages are first touched in parallel
+// instead of being zeroed by one thread), and transparent huge pages for big blocks.
+template <class T>
+struct BigAlloc {
+    using value_type = T;
+    static constexpr size_t kHuge = (size_t)32 << 20;
+    BigAlloc() = default;
+    template <class U>
+    BigAlloc(const BigAlloc<U> &) {}
+    T *allocate(size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes >= kHuge) {
+            void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (p == MAP_FAILED) throw std::bad_alloc();
+            madvise(p, bytes, MADV_HUGEPAGE);
+            return static_cast<T *>(p);
+        }
+        return static_cast<T *>(::operator new(bytes));
+    }
+    void deallocate(T *p, size_t n) {
+        const size_t bytes = n * sizeof(T);
+        if (bytes >= kHuge) munmap(p, bytes);
+        else ::operator delete(p);
+    }
+    template <class U, class... A>
+    void construct(U *p, A &&...a) {
+        if constexpr (sizeof...(A) == 0) ::new ((void *)p) U;
+        else ::new ((void *)p) U(std::forward<A>(a)...);
+    }
+    template <class U>
+    bool operator==(const BigAlloc<U> &) const { return true; }
+    template <class U>
+    bool operator!=(const BigAlloc<U> &) const { return false; }
+};
+template <class T>
+using BigVec = std::vector<T, BigAlloc<T>>;
+
 struct Index {
     // text: forward long reads, then the reverse complement of their concatenation
     // (bwa's forward-reverse layout), each contig followed by SEP
-    std::vector<uint8_t> text;
+    BigVec<uint8_t> text;
     std::vector<int64_t> cstart;   // text offset of contig c (2*n_lr contigs in text order)
     std::vector<int32_t> cblk;     // contig containing text position (b << CB_SHIFT), per block
     std::vector<int64_t> lr_off;   // forward long-read offsets (n_lr + 1), l_pac = lr_off[n_lr]
     int n_lr = 0;
     int64_t l_pac = 0;
     std::vector<uint32_t> koff;    // [NK + 1] offsets into kpos
-    std::vector<uint32_t> kpos;    // text positions of every valid 12-mer, grouped by k-mer, ascending
-    std::vector<uint64_t> kext;    // per kpos entry: the next KX bases after the 12-mer (2 bits each,
+    BigVec<uint32_t> kpos;         // text positions of every valid 12-mer, grouped by k-mer, ascending
+    BigVec<uint64_t> kext;         // per kpos entry: the next KX bases after the 12-mer (2 bits each,
                                    // base i at bits 2i) and their count before N / SEP (bits 56..61)
     std::vector<uint32_t> cnt[KI]; // cnt[j][code] = occurrences of the (j+1)-mer `code` (j < KI-1)
 };
@@ -317,17 +358,40 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     I.l_pac = l_pac;
     I.lr_off.assign(n_lr + 1, 0);
     for (int i = 0; i <= n_lr; ++i) I.lr_off[i] = lr_off[i] - lr_off[0];
-    I.text.reserve(2 * l_pac + 2 * n_lr);
+    int nt = (int)std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);
+    if (l_pac < (int64_t)1 << 21) nt = 1;
+    auto run_threads = [&](auto body) {
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) th.emplace_back(body, t);
+        body(0);
+        for (auto &x : th) x.join();
+    };
+    // text: forward read i at lr_off[i] + i; the reverse strand holds read n_lr-1-k as
+    // contig n_lr+k, i.e. read i reverse-complemented at l_pac + n_lr + (l_pac - lr_off[i+1]) + (n_lr-1-i)
+    const int64_t n_text = 2 * l_pac + 2 * (int64_t)n_lr;
+    I.text.resize((size_t)n_text);
+    I.cstart.assign(2 * (size_t)n_lr, 0);
     for (int i = 0; i < n_lr; ++i) {
-        I.cstart.push_back((int64_t)I.text.size());
-        for (int64_t p = lr_off[i]; p < lr_off[i + 1]; ++p) I.text.push_back(lr_seq[p] < 4 ? lr_seq[p] : 4);
-        I.text.push_back(SEP);
+        I.cstart[i] = I.lr_off[i] + i;
+        I.cstart[2 * (size_t)n_lr - 1 - i] = l_pac + n_lr + (l_pac - I.lr_off[i + 1]) + (n_lr - 1 - i);
     }
-    for (int i = n_lr - 1; i >= 0; --i) {
-        I.cstart.push_back((int64_t)I.text.size());
-        for (int64_t p = lr_off[i + 1] - 1; p >= lr_off[i]; --p) I.text.push_back(lr_seq[p] < 4 ? (uint8_t)(3 - lr_seq[p]) : 4);
-        I.text.push_back(SEP);
-    }
+    run_threads([&](int t) {
+        uint8_t *X = I.text.data();
+        for (int i = (int)((int64_t)n_lr * t / nt); i < (int)((int64_t)n_lr * (t + 1) / nt); ++i) {
+            const uint8_t *r = lr_seq + lr_off[i];
+            const int64_t len = lr_off[i + 1] - lr_off[i];
+            uint8_t *f = X + I.cstart[i];
+            uint8_t *b = X + I.cstart[2 * (size_t)n_lr - 1 - i];
+            for (int64_t p = 0; p < len; ++p) {
+                const uint8_t c = r[p];
+                f[p] = c < 4 ? c : 4;
+                b[len - 1 - p] = c < 4 ? (uint8_t)(3 - c) : 4;
+            }
+            f[len] = SEP;
+            b[len] = SEP;
+        }
+    });
     // 12-mer table (positions ascending within a k-mer)
     const uint8_t *T = I.text.data();
     const int64_t n = (int64_t)I.text.size();
@@ -352,29 +416,35 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
             if (++run >= KI && p - KI + 1 >= p0) f(code, (uint32_t)(p - KI + 1));
         }
     };
-    // counting split over text chunks (per-chunk counts, then the table offsets)
-    int nt = (int)std::thread::hardware_concurrency();
-    nt = nt < 1 ? 1 : (nt > 16 ? 16 : nt);
-    if (n < (int64_t)1 << 22) nt = 1;
-    auto run_threads = [&](auto body) {
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) th.emplace_back(body, t);
-        body(0);
-        for (auto &x : th) x.join();
-    };
-    std::vector<std::vector<uint32_t>> tc((size_t)nt, std::vector<uint32_t>(NK, 0));
+    // counting split over text chunks (per-chunk counts, each thread zeroing and filling
+    // its own table), then the table offsets summed over k-mer ranges in parallel
+    std::vector<std::vector<uint32_t>> tc((size_t)nt);
     run_threads([&](int t) {
         std::vector<uint32_t> &c = tc[(size_t)t];
+        c.assign(NK, 0);
         for_kmers(n * t / nt, n * (t + 1) / nt, [&](uint32_t k, uint32_t) { ++c[k]; });
     });
-    std::vector<uint32_t> kc(NK, 0);
+    std::vector<uint32_t> kc(NK);
     I.koff.assign(NK + 1, 0);
-    for (uint32_t k = 0; k < NK; ++k) {
-        uint32_t sum = 0;
-        for (int t = 0; t < nt; ++t) sum += tc[(size_t)t][k];
-        kc[k] = sum;
-        I.koff[k + 1] = I.koff[k] + sum;
-    }
+    std::vector<uint64_t> part((size_t)nt + 1, 0);
+    run_threads([&](int t) {
+        const uint32_t k0 = (uint32_t)((uint64_t)NK * t / nt), k1 = (uint32_t)((uint64_t)NK * (t + 1) / nt);
+        uint64_t run = 0;
+        for (uint32_t k = k0; k < k1; ++k) {
+            uint32_t sum = 0;
+            for (int u = 0; u < nt; ++u) sum += tc[(size_t)u][k];
+            kc[k] = sum;
+            run += sum;
+            I.koff[k + 1] = (uint32_t)run;   // range-local prefix, shifted below
+        }
+        part[(size_t)t + 1] = run;
+    });
+    for (int t = 0; t < nt; ++t) part[(size_t)t + 1] += part[(size_t)t];
+    run_threads([&](int t) {
+        const uint32_t k0 = (uint32_t)((uint64_t)NK * t / nt), k1 = (uint32_t)((uint64_t)NK * (t + 1) / nt);
+        const uint32_t base = (uint32_t)part[(size_t)t];
+        for (uint32_t k = k0; k < k1; ++k) I.koff[k + 1] += base;
+    });
     I.kpos.resize(I.koff[NK]);
     I.kext.resize(I.koff[NK]);
     // Fill in two cache-friendly passes instead of one scatter over the whole table:
@@ -391,19 +461,21 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
         uint32_t pos, low;
         uint64_t ext;
     };
-    std::vector<Rec> tmp(I.koff[NK]);
+    BigVec<Rec> tmp(I.koff[NK]);
     {
         // per-thread bucket cursors: bucket b starts at koff[b << LB]; thread t after threads < t
         std::vector<std::vector<uint64_t>> cur((size_t)nt, std::vector<uint64_t>(NB, 0));
-        for (uint32_t b = 0; b < NB; ++b) {
-            uint64_t o = I.koff[b << LB];
-            for (int t = 0; t < nt; ++t) {
-                cur[(size_t)t][b] = o;
-                uint64_t sz = 0;
-                for (uint32_t k = b << LB; k < ((b + 1) << LB); ++k) sz += tc[(size_t)t][k];
-                o += sz;
+        run_threads([&](int u) {
+            for (uint32_t b = (uint32_t)((uint64_t)NB * u / nt); b < (uint32_t)((uint64_t)NB * (u + 1) / nt); ++b) {
+                uint64_t o = I.koff[b << LB];
+                for (int t = 0; t < nt; ++t) {
+                    cur[(size_t)t][b] = o;
+                    uint64_t sz = 0;
+                    for (uint32_t k = b << LB; k < ((b + 1) << LB); ++k) sz += tc[(size_t)t][k];
+                    o += sz;
+                }
             }
-        }
+        });
         tc.clear();
         tc.shrink_to_fit();
         run_threads([&](int t) {
@@ -465,9 +537,16 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     // base of its run, then it prefixes a (j+1)-mer occurrence, or it ends the run)
     std::vector<std::vector<uint32_t>> tail(KI);
     {
+        std::vector<std::vector<int64_t>> stops((size_t)nt);   // non-base positions, per text chunk
+        run_threads([&](int t) {
+            for (int64_t p = n * t / nt; p < n * (t + 1) / nt; ++p)
+                if (T[p] > 3) stops[(size_t)t].push_back(p);
+        });
+        std::vector<int64_t> ends;
+        for (auto &v : stops) ends.insert(ends.end(), v.begin(), v.end());
+        ends.push_back(n);
         int64_t s0 = 0;
-        for (int64_t p = 0; p <= n; ++p) {
-            if (p < n && T[p] <= 3) continue;
+        for (const int64_t p : ends) {
             for (int j = 1; j < KI && p - j >= s0; ++j) {   // run [s0, p)
                 uint32_t code = 0;
                 for (int64_t e = p - j; e < p; ++e) code = (code << 2) | T[e];
@@ -489,6 +568,34 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
 }
 
 extern "C" void pr_seed_index_free(pr_seed_index *h) { delete h; }
+
+// order-sensitive 64-bit digests of the index tables (test hook: a faster build must
+// produce identical tables)
+template <class T>
+static uint64_t digest_of(const T *p, size_t n) {
+    uint64_t h = 1469598103934665603ull ^ (uint64_t)n;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= (uint64_t)p[i];
+        h *= 1099511628211ull;
+        h ^= h >> 29;
+    }
+    return h;
+}
+
+extern "C" int pr_seed_index_digest(const pr_seed_index *h, uint64_t *out6) {
+    if (!h || !out6) return pr_set_error(PR_ERR_ARG, "null arg");
+    const Index &I = h->I;
+    out6[0] = digest_of(I.text.data(), I.text.size());
+    out6[1] = digest_of(I.koff.data(), I.koff.size());
+    out6[2] = digest_of(I.kpos.data(), I.kpos.size());
+    out6[3] = digest_of(I.kext.data(), I.kext.size());
+    uint64_t c = 0;
+    for (int j = 0; j < KI; ++j) c = c * 31 + digest_of(I.cnt[j].data(), I.cnt[j].size());
+    out6[4] = c;
+    out6[5] = digest_of(I.cstart.data(), I.cstart.size()) * 31 + digest_of(I.cblk.data(), I.cblk.size()) * 7 +
+              digest_of(I.lr_off.data(), I.lr_off.size());
+    return 0;
+}
 
 extern "C" int pr_seed_index_occ(const pr_seed_index *h, const uint8_t *s, int n, int64_t *count) {
     if (!h || !s || !count || n <= 0) return pr_set_error(PR_ERR_ARG, "bad arg");

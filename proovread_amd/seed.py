@@ -45,6 +45,7 @@ def _setup(L):
                               C.POINTER(SeedTasks)]
     L.pr_seed_tasks_free.argtypes = [C.POINTER(SeedTasks)]
     L.pr_seed_tasks_free.restype = None
+    L.pr_seed_index_digest.argtypes = [C.c_void_p, C.c_void_p]
     L.pr_seed_index_occ.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_int64)]
     L.pr_seed_smem.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int64, C.c_void_p, C.c_void_p,
                                C.c_void_p, C.c_int, C.POINTER(C.c_int)]
@@ -88,6 +89,12 @@ class SeedIndex:
             self.close()
         except Exception:
             pass
+
+    def digest(self) -> tuple:
+        """Digests of the index tables (pr_seed_index_digest)."""
+        out = np.zeros(6, np.uint64)
+        _abi.check(self.L.pr_seed_index_digest(self.h, out.ctypes.data), "pr_seed_index_digest")
+        return tuple(int(x) for x in out)
 
     def occ(self, s: np.ndarray) -> int:
         s = np.ascontiguousarray(s, np.uint8)

@@ -151,3 +151,35 @@ def test_with_seeded_tasks_groups_by_long_read():
         m = d2.t_lr == lr
         assert np.array_equal(d2.t_sr[m], sel["sr"]) and np.array_equal(d2.t_rbeg[m], sel["rbeg"])
     assert d2.sr_seq is d.sr_seq and d2.lr_seq is d.lr_seq
+
+
+# Digests of the index tables (pr_seed_index_digest) recorded with the single-threaded-fill
+# build of round 1 (before the parallel text / count / tail passes and the uninitialised
+# big tables): every later build must reproduce them exactly.
+INDEX_DIGESTS = {"edge": [3546541225710248283, 8536593745191129070, 10635058001152306152, 10887004318922434826, 17265816249920140396, 10474070083008801549], "s3": [5932085080177065250, 12668374040756329347, 3287268347065411532, 15991074188727081827, 10713618094517999836, 13382138088525873941], "s4": [4197478436865662894, 6759494015559495109, 12608834300269571323, 13333961972377079611, 10616757141662657057, 560078664211191469]}
+
+
+def _edge_shard():
+    rng = np.random.default_rng(7)
+    reads = [rng.integers(0, 4, n).astype(np.uint8) for n in (0, 5, 11, 12, 13, 40, 1000, 5000)]
+    r = rng.integers(0, 4, 3000).astype(np.uint8)
+    r[100:130] = 4
+    r[2000] = 4
+    reads.append(r)
+    off = np.zeros(len(reads) + 1, np.int64)
+    np.cumsum([len(x) for x in reads], out=off[1:])
+    return np.concatenate(reads), off
+
+
+@pytest.mark.parametrize("name", ["edge", "s3", "s4"])
+def test_index_tables_unchanged(name):
+    from proovread_amd import seed, synth
+    if name == "edge":
+        s, o = _edge_shard()
+    else:
+        sd, gl, n = {"s3": (3, 200_000, 200), "s4": (4, 1_000_000, 1500)}[name]
+        d = synth.simulate(sd, gl, n, 5000, 10.0, sr_frac=0.1)
+        s, o = d.lr_seq, d.lr_off
+    ix = seed.SeedIndex(s, o)
+    assert ix.digest() == tuple(INDEX_DIGESTS[name])
+    ix.close()
