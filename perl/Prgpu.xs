@@ -7,6 +7,11 @@
  * sets (bam2cns:227-237) arrive as a hash; the chunk arrives as the SoA buffers of
  * pr_cns_batch, packed on the Perl side (lib/Prgpu.pm) with pack().
  *
+ * The seed-extension stage is bound the same way (seed_index_build / seed_map / sw_run):
+ * what bin/proovread's run_bwa (bin/proovread:1254-1322) gets from a `bwa-proovread mem`
+ * process, minus the SAM text round trip; lib/Prgpu.pm turns the results into the SAM
+ * records bwa-proovread prints.
+ *
  * The binding is thin on purpose: it checks that every packed buffer holds what the
  * batch's counts say it must (so the library never reads past a Perl string), calls
  * pr_cns_run, and hands the output pools back as packed strings.  Library errors croak
@@ -57,6 +62,29 @@ static int64_t i64_at(const char *p, int64_t i) {
     int64_t v;
     memcpy(&v, p + 8 * i, 8);
     return v;
+}
+
+/* a packed buffer argument holding at least `need` bytes */
+static const char *arg_buf(pTHX_ SV *sv, const char *what, size_t need, STRLEN *got) {
+    STRLEN len = 0;
+    const char *p;
+    if (!SvOK(sv)) croak("Prgpu: %s undefined", what);
+    p = SvPVbyte(sv, len);
+    if (len < need) croak("Prgpu: %s holds %lu bytes, %lu needed", what, (unsigned long)len, (unsigned long)need);
+    if (got) *got = len;
+    return p;
+}
+
+/* offsets packed as int64: n+1 entries from 0, monotone, ending within a pool of `pool` bytes */
+static int64_t check_off(pTHX_ const char *off, STRLEN off_len, STRLEN pool, const char *what) {
+    int64_t n, i;
+    if (off_len < 8 || off_len % 8) croak("Prgpu: %s must hold n+1 int64 offsets", what);
+    n = (int64_t)(off_len / 8) - 1;
+    if (i64_at(off, 0) != 0) croak("Prgpu: %s must start at 0", what);
+    for (i = 0; i < n; ++i)
+        if (i64_at(off, i + 1) < i64_at(off, i)) croak("Prgpu: %s not monotone", what);
+    if (i64_at(off, n) > (int64_t)pool) croak("Prgpu: %s ends past its sequence pool", what);
+    return n;
 }
 
 MODULE = Prgpu  PACKAGE = Prgpu
@@ -211,6 +239,138 @@ cns_run(IV ctx, HV *params, HV *batch)
         if (rc != 0) {
             for (k = 0; k < sizeof all / sizeof all[0]; ++k) SvREFCNT_dec(all[k]);
             croak("Prgpu: pr_cns_run: %s (%d)", pr_last_error(), rc);
+        }
+        res = newHV();
+        for (k = 0; k < sizeof all / sizeof all[0]; ++k) hv_store(res, keys[k], (I32)strlen(keys[k]), all[k], 0);
+    }
+    RETVAL = newRV_noinc((SV *)res);
+  OUTPUT:
+    RETVAL
+
+IV
+seed_index_build(SV *lr_seq, SV *lr_off)
+  CODE:
+    STRLEN ls = 0, lo = 0;
+    const char *seq = arg_buf(aTHX_ lr_seq, "lr_seq", 0, &ls);
+    const char *off = arg_buf(aTHX_ lr_off, "lr_off", 8, &lo);
+    const int64_t n = check_off(aTHX_ off, lo, ls, "lr_off");
+    pr_seed_index *h = NULL;
+    int rc = pr_seed_index_build((const uint8_t *)seq, (const int64_t *)off, (int)n, &h);
+    if (rc != 0) croak("Prgpu: pr_seed_index_build: %s (%d)", pr_last_error(), rc);
+    RETVAL = PTR2IV(h);
+  OUTPUT:
+    RETVAL
+
+void
+seed_index_free(IV ix)
+  CODE:
+    if (ix) pr_seed_index_free(INT2PTR(pr_seed_index *, ix));
+
+SV *
+seed_map(IV ix, HV *opts, SV *sr_seq, SV *sr_off, int threads)
+  CODE:
+    /* bwa mem seeding + chaining options (bin/proovread:1313, proovread.cfg:318-333) */
+    pr_seed_opts o;
+    pr_seed_tasks t;
+    STRLEN ls = 0, lo = 0;
+    const char *seq = arg_buf(aTHX_ sr_seq, "sr_seq", 0, &ls);
+    const char *off = arg_buf(aTHX_ sr_off, "sr_off", 8, &lo);
+    const int64_t n = check_off(aTHX_ off, lo, ls, "sr_off");
+    int rc;
+    if (!ix) croak("Prgpu::seed_map: no index");
+    pr_seed_opts_default(&o, inum(aTHX_ opts, "finish", 0));
+    o.min_seed_len = inum(aTHX_ opts, "min_seed_len", o.min_seed_len);
+    o.min_chain_weight = inum(aTHX_ opts, "min_chain_weight", o.min_chain_weight);
+    o.w = inum(aTHX_ opts, "w", o.w);
+    o.split_factor = num(aTHX_ opts, "split_factor", o.split_factor);
+    o.split_width = inum(aTHX_ opts, "split_width", o.split_width);
+    o.max_mem_intv = inum(aTHX_ opts, "max_mem_intv", o.max_mem_intv);
+    o.max_occ = inum(aTHX_ opts, "max_occ", o.max_occ);
+    o.drop_ratio = num(aTHX_ opts, "drop_ratio", o.drop_ratio);
+    o.a = inum(aTHX_ opts, "a", o.a);
+    o.o_del = inum(aTHX_ opts, "o_del", o.o_del);
+    o.e_del = inum(aTHX_ opts, "e_del", o.e_del);
+    o.o_ins = inum(aTHX_ opts, "o_ins", o.o_ins);
+    o.e_ins = inum(aTHX_ opts, "e_ins", o.e_ins);
+    rc = pr_seed_map(INT2PTR(const pr_seed_index *, ix), &o, (const uint8_t *)seq, (const int64_t *)off, (int)n,
+                     threads, &t);
+    if (rc != 0) croak("Prgpu: pr_seed_map: %s (%d)", pr_last_error(), rc);
+    RETVAL = newSVpvn(t.n ? (const char *)t.t : "", (STRLEN)(t.n * sizeof(pr_seed_task)));
+    pr_seed_tasks_free(&t);
+  OUTPUT:
+    RETVAL
+
+SV *
+sw_run(IV ctx, HV *opts, HV *batch)
+  CODE:
+    /* ksw_extend2 + ksw_global2 over the task list (bwa mem -A -B -O -E -w -L -d -T) */
+    pr_sw_opts o;
+    pr_sw_batch b;
+    pr_sw_out out;
+    STRLEN lss = 0, lso = 0, lls = 0, llo = 0;
+    const char *ss, *so, *ls_, *lo_;
+    int64_t nt;
+    int rc;
+    HV *res;
+    pr_sw_opts_default(&o, inum(aTHX_ opts, "finish", 0));
+    o.a = inum(aTHX_ opts, "a", o.a);
+    o.b = inum(aTHX_ opts, "b", o.b);
+    o.o_del = inum(aTHX_ opts, "o_del", o.o_del);
+    o.e_del = inum(aTHX_ opts, "e_del", o.e_del);
+    o.o_ins = inum(aTHX_ opts, "o_ins", o.o_ins);
+    o.e_ins = inum(aTHX_ opts, "e_ins", o.e_ins);
+    o.w = inum(aTHX_ opts, "w", o.w);
+    o.pen_clip5 = inum(aTHX_ opts, "pen_clip5", o.pen_clip5);
+    o.pen_clip3 = inum(aTHX_ opts, "pen_clip3", o.pen_clip3);
+    o.zdrop = inum(aTHX_ opts, "zdrop", o.zdrop);
+    o.min_score_per_base = num(aTHX_ opts, "min_score_per_base", o.min_score_per_base);
+    memset(&b, 0, sizeof b);
+    ss = field(aTHX_ batch, "sr_seq", 0, 0, &lss);
+    so = field(aTHX_ batch, "sr_off", 8, 0, &lso);
+    ls_ = field(aTHX_ batch, "lr_seq", 0, 0, &lls);
+    lo_ = field(aTHX_ batch, "lr_off", 8, 0, &llo);
+    b.n_sr = (int32_t)check_off(aTHX_ so, lso, lss, "sr_off");
+    b.n_lr = (int32_t)check_off(aTHX_ lo_, llo, lls, "lr_off");
+    b.sr_seq = (const uint8_t *)ss;
+    b.sr_off = (const int64_t *)so;
+    b.lr_seq = (const uint8_t *)ls_;
+    b.lr_off = (const int64_t *)lo_;
+    nt = (int64_t)num(aTHX_ batch, "n_task", -1);
+    if (nt < 0) croak("Prgpu::sw_run: batch field 'n_task' missing or negative");
+    b.n_task = nt;
+    b.t_sr = (const int32_t *)field(aTHX_ batch, "t_sr", 4 * (size_t)nt, 0, NULL);
+    b.t_lr = (const int32_t *)field(aTHX_ batch, "t_lr", 4 * (size_t)nt, 0, NULL);
+    b.t_strand = (const uint8_t *)field(aTHX_ batch, "t_strand", (size_t)nt, 0, NULL);
+    b.t_qbeg = (const int32_t *)field(aTHX_ batch, "t_qbeg", 4 * (size_t)nt, 0, NULL);
+    b.t_rbeg = (const int32_t *)field(aTHX_ batch, "t_rbeg", 4 * (size_t)nt, 0, NULL);
+    b.t_slen = (const int32_t *)field(aTHX_ batch, "t_slen", 4 * (size_t)nt, 0, NULL);
+    {
+        /* outputs, one Perl string each (PR_SW_MAXCIG ops per task for the CIGARs) */
+        SV *s_pos = newSV(4 * nt + 1), *s_sc = newSV(4 * nt + 1), *s_nc = newSV(4 * nt + 1),
+           *s_cig = newSV(4 * (size_t)PR_SW_MAXCIG * nt + 1), *s_pass = newSV(nt + 1), *s_st = newSV(4 * nt + 1),
+           *s_qb = newSV(4 * nt + 1), *s_qe = newSV(4 * nt + 1);
+        SV *all[] = {s_pos, s_sc, s_nc, s_cig, s_pass, s_st, s_qb, s_qe};
+        const STRLEN lens[] = {4 * nt, 4 * nt, 4 * nt, 4 * (size_t)PR_SW_MAXCIG * nt, nt, 4 * nt, 4 * nt, 4 * nt};
+        const char *keys[] = {"pos", "score", "ncigar", "cigar", "pass", "status", "qb", "qe"};
+        unsigned k;
+        for (k = 0; k < sizeof all / sizeof all[0]; ++k) {
+            SvPOK_on(all[k]);
+            memset(SvPVX(all[k]), 0, lens[k] + 1);
+            SvCUR_set(all[k], lens[k]);
+        }
+        memset(&out, 0, sizeof out);
+        out.pos = (int32_t *)SvPVX(s_pos);
+        out.score = (int32_t *)SvPVX(s_sc);
+        out.ncigar = (int32_t *)SvPVX(s_nc);
+        out.cigar = (uint32_t *)SvPVX(s_cig);
+        out.pass = (uint8_t *)SvPVX(s_pass);
+        out.status = (int32_t *)SvPVX(s_st);
+        out.qb = (int32_t *)SvPVX(s_qb);
+        out.qe = (int32_t *)SvPVX(s_qe);
+        rc = pr_sw_run(INT2PTR(pr_ctx *, ctx), &o, &b, &out);
+        if (rc != 0) {
+            for (k = 0; k < sizeof all / sizeof all[0]; ++k) SvREFCNT_dec(all[k]);
+            croak("Prgpu: pr_sw_run: %s (%d)", pr_last_error(), rc);
         }
         res = newHV();
         for (k = 0; k < sizeof all / sizeof all[0]; ++k) hv_store(res, keys[k], (I32)strlen(keys[k]), all[k], 0);

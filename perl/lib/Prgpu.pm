@@ -193,6 +193,160 @@ sub run_chunk {
     return @res;
 }
 
+# ------------------------------------------------------------------ seed-extension stage
+#
+# What bin/proovread's run_bwa (bin/proovread:1254-1322) gets from a `bwa-proovread mem -a -Y`
+# process: SAM records of every short read against the long reads, here from the library's
+# seeding front end (seed_index_build / seed_map, host) and the GPU seed extension (sw_run),
+# with the records written the way proovread_amd/bwa_proovread.py:mem writes them.
+
+my @NT = ('A', 'C', 'G', 'T', 'N');
+my $CIGAR_CHARS = 'MIDNSHP=X';
+
+# bwa's nst_nt4_table: A C G T (either case) -> 0..3, everything else -> 4
+sub nt4 {
+    my ($s) = @_;
+    $s =~ tr/ACGTacgt/\x04/c;
+    $s =~ tr/ACGTacgt/\x00\x01\x02\x03\x00\x01\x02\x03/;
+    return $s;
+}
+
+# sequences -> (nt4 pool, packed int64 offsets)
+sub pool {
+    my ($seqs) = @_;
+    my @off = (0);
+    push @off, $off[-1] + length $_ for @$seqs;
+    return (nt4(join '', @$seqs), pack('q<*', @off));
+}
+
+use constant TASK_BYTES => 40;   # pr_seed_task: 10 x int32
+
+# SW results of a packed sw_run output for tasks 0..n-1
+sub sw_unpack {
+    my ($o, $n) = @_;
+    my @nc = unpack('l<*', $o->{ncigar});
+    my @cig;
+    for my $t (0 .. $n - 1) {
+        my @ops = unpack('L<*', substr($o->{cigar}, 4 * 128 * $t, 4 * $nc[$t]));
+        push @cig, join '', map { ($_ >> 4) . substr($CIGAR_CHARS, $_ & 15, 1) } @ops;
+    }
+    return {pos => [unpack('l<*', $o->{pos})], score => [unpack('l<*', $o->{score})],
+            pass => [unpack('C*', $o->{pass})], status => [unpack('l<*', $o->{status})], cigar => \@cig};
+}
+
+# Sam::Alignment::length (Alignment.pm:417-431): M+D if SEQ is empty or the CIGAR starts or
+# ends with S, else the SEQ length
+sub aln_length {
+    my ($cig, $seq_len) = @_;
+    my @ops = $cig =~ /(\d+)([MIDNSHP=X])/g;
+    if ($seq_len == 0 || (@ops && ($ops[1] eq 'S' || $ops[-1] eq 'S'))) {
+        my $l = 0;
+        for (my $i = 0; $i < @ops; $i += 2) { $l += $ops[$i] if $ops[$i + 1] eq 'M' || $ops[$i + 1] eq 'D' }
+        return $l;
+    }
+    return $seq_len;
+}
+
+# mem(%a) -> (header lines, record lines): the output of `bwa-proovread mem`.
+#   ctx        Prgpu::Context (or a sw_runner coderef taking the task batch hash and
+#              returning {pos, score, pass, status, cigar} arrays — the tests inject the oracle)
+#   seed_opts, sw_opts  option hashes for seed_map / sw_run ({finish => 0|1, ...})
+#   b, l       the -b/-l bin filter (0: off)
+#   threads    host seeding threads
+#   lr_names, lr_seqs, sr_names, sr_seqs, sr_quals (undef entries for FASTA reads)
+#   cl         the command line for @PG
+sub mem {
+    my (%a) = @_;
+    my ($lr_pool, $lr_off) = pool($a{lr_seqs});
+    my ($sr_pool, $sr_off) = pool($a{sr_seqs});
+    my $ix = seed_index_build($lr_pool, $lr_off);
+    my $packed = eval { seed_map($ix, $a{seed_opts} || {}, $sr_pool, $sr_off, $a{threads} || 0) };
+    my $err = $@;
+    seed_index_free($ix);
+    die $err if $err;
+    my $nt = length($packed) / TASK_BYTES;
+    my (@t_sr, @t_lr, @t_strand, @t_qbeg, @t_rbeg, @t_slen);
+    for my $t (0 .. $nt - 1) {
+        my @f = unpack('l<10', substr($packed, TASK_BYTES * $t, TASK_BYTES));
+        push @t_sr, $f[0];
+        push @t_lr, $f[1];
+        push @t_strand, $f[2];
+        push @t_qbeg, $f[3];
+        push @t_rbeg, $f[4];
+        push @t_slen, $f[5];
+    }
+    my %batch = (sr_seq => $sr_pool, sr_off => $sr_off, lr_seq => $lr_pool, lr_off => $lr_off, n_task => $nt,
+                 t_sr => pack('l<*', @t_sr), t_lr => pack('l<*', @t_lr), t_strand => pack('C*', @t_strand),
+                 t_qbeg => pack('l<*', @t_qbeg), t_rbeg => pack('l<*', @t_rbeg), t_slen => pack('l<*', @t_slen));
+    my $res = ref $a{ctx} eq 'CODE' ? $a{ctx}->(\%batch)
+            : sw_unpack(sw_run(ref $a{ctx} ? $a{ctx}->handle : $a{ctx}, $a{sw_opts} || {}, \%batch), $nt);
+
+    my @head = ("\@HD\tVN:1.5\tSO:unsorted\n");
+    push @head, "\@SQ\tSN:$a{lr_names}[$_]\tLN:" . length($a{lr_seqs}[$_]) . "\n" for 0 .. $#{$a{lr_names}};
+    push @head, "\@PG\tID:bwa-proovread\tPN:bwa-proovread\tVN:prgpu\tCL:bwa-proovread mem " . ($a{cl} // '') . "\n";
+
+    # -b/-l binning: Sam::Seq add_aln_by_score over the run's records (bwa_proovread.py BinFilter)
+    my (%bins, @alive);
+    my $filter = ($a{b} || 0) > 0 && ($a{l} || 0) > 0;
+    my $bin_add = sub {
+        my ($lr, $pos1, $len, $score) = @_;
+        my $rid = @alive;
+        push @alive, 0;
+        return if $len <= 0;
+        my $nc = ($score / $len) * ($len / (40 + $len));
+        my $ent = $bins{$lr, int(($pos1 + $len / 2.0) / $a{b})} ||= [0, []];
+        my $lst = $ent->[1];
+        if ($ent->[0] > $a{l}) {
+            return if $nc <= $lst->[-1][0];
+            my $old = pop @$lst;
+            $alive[$old->[1]] = 0;
+            $ent->[0] -= $old->[2];
+        }
+        $ent->[0] += $len;
+        my $i = $#$lst;
+        --$i while $i >= 0 && $nc > $lst->[$i][0];
+        splice @$lst, $i + 1, 0, [$nc, $rid, $len];
+        $alive[$rid] = 1;
+    };
+
+    my @rec;
+    my ($pos, $sc, $ps, $st, $cg) = @$res{qw(pos score pass status cigar)};
+    my $t = 0;
+    while ($t < $nt) {
+        my $r = $t_sr[$t];
+        my $e = $t;
+        ++$e while $e < $nt && $t_sr[$e] == $r;
+        my @hits = grep { $st->[$_] == 0 && $ps->[$_] } $t .. $e - 1;
+        if (@hits) {
+            my $best = $hits[0];
+            for my $x (@hits) { $best = $x if $sc->[$x] > $sc->[$best] }   # highest score, first on ties
+            my $q = $a{sr_seqs}[$r];
+            my $qual = $a{sr_quals}[$r];
+            for my $x (@hits) {
+                my $strand = $t_strand[$x];
+                my ($s, $qq);
+                if ($strand) {
+                    ($s = $q) =~ tr/ACGTacgt/N/c;
+                    $s =~ tr/ACGTacgt/TGCATGCA/;
+                    $s = reverse $s;
+                    $qq = defined $qual ? scalar reverse($qual) : '*';
+                } else {
+                    $s = uc $q;
+                    $qq = defined $qual ? $qual : '*';
+                }
+                my $flag = ($strand ? 16 : 0) | ($x == $best ? 0 : 256);
+                my $mapq = $x == $best ? 60 : 0;
+                push @rec, join("\t", $a{sr_names}[$r], $flag, $a{lr_names}[$t_lr[$x]], $pos->[$x] + 1, $mapq,
+                                $cg->[$x], '*', 0, 0, $s, $qq, "AS:i:$sc->[$x]") . "\n";
+                $bin_add->($t_lr[$x], $pos->[$x] + 1, aln_length($cg->[$x], length $q), $sc->[$x]) if $filter;
+            }
+        }
+        $t = $e;
+    }
+    @rec = @rec[grep { $alive[$_] } 0 .. $#rec] if $filter;
+    return (\@head, \@rec);
+}
+
 # the FASTQ record bam2cns prints (bam2cns:453, Fastq::Seq string)
 sub fastq {
     my ($r) = @_;

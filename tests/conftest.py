@@ -10,7 +10,7 @@ sys.path.insert(0, str(HERE.parent))
 # of the suite, so that under `pytest -x` a failure there cannot hide the results
 # of the validated kernels.
 RUN_LAST = ("test_fantasticus_cns.py", "test_mask_gpu.py", "test_seed_gpu.py", "test_correct_loop.py",
-            "test_sw_edge_gpu.py", "test_perl_xs.py")
+            "test_sw_edge_gpu.py", "test_perl_xs.py", "test_perl_xs_mem.py")
 
 
 def pytest_configure(config):

@@ -4,6 +4,10 @@
 #
 #   perl_cns_helper.pl pack IN.json  -> {field: hex of the packed pr_cns_batch buffer}
 #   perl_cns_helper.pl run  IN.json  -> [{id, status, seq, qual, trace, cigar, chim}] (GPU)
+#   perl_cns_helper.pl mem  IN.json  -> {head, rec, batch}: Prgpu::mem (the bwa-proovread
+#       mem output) with host seeding, and the SW results either injected from IN.json's
+#       `sw` (the tests' CPU oracle; `batch` is then the hex of the task arrays handed to it)
+#       or from sw_run on the GPU
 use strict;
 use warnings;
 use FindBin;
@@ -26,6 +30,19 @@ if ($mode eq 'pack') {
     my @res = Prgpu::run_chunk($ctx, $in->{params}, $in->{reads}, $in->{alns});
     for my $r (@res) { $r->{chim_lines} = [Prgpu::chim_lines($r)]; $r->{fastq} = $r->{status} ? '' : Prgpu::fastq($r) }
     print $json->encode(\@res), "\n";
+} elsif ($mode eq 'mem') {
+    my %batch_hex;
+    my $ctx = $in->{sw} ? sub {
+        my ($b) = @_;
+        %batch_hex = map { $_ => ($_ eq 'n_task' ? $b->{$_} : unpack('H*', $b->{$_})) } keys %$b;
+        return $in->{sw};
+    } : Prgpu::Context->new(0);
+    my ($head, $rec) = Prgpu::mem(ctx => $ctx, seed_opts => $in->{seed_opts}, sw_opts => $in->{sw_opts},
+                                  b => $in->{b}, l => $in->{l}, threads => $in->{threads}, cl => $in->{cl},
+                                  lr_names => $in->{lr_names}, lr_seqs => $in->{lr_seqs},
+                                  sr_names => $in->{sr_names}, sr_seqs => $in->{sr_seqs},
+                                  sr_quals => $in->{sr_quals});
+    print $json->encode({head => $head, rec => $rec, batch => \%batch_hex}), "\n";
 } else {
-    die "usage: perl_cns_helper.pl pack|run IN.json\n";
+    die "usage: perl_cns_helper.pl pack|run|mem IN.json\n";
 }
