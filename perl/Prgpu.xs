@@ -378,3 +378,76 @@ sw_run(IV ctx, HV *opts, HV *batch)
     RETVAL = newRV_noinc((SV *)res);
   OUTPUT:
     RETVAL
+
+SV *
+mask_params(const char *hcr_mask, int min_sr_length)
+  CODE:
+    /* proovread.cfg:235 hcr-mask scaled to the short-read length (bin/proovread:1702-1705) */
+    pr_mask_params p;
+    HV *h = newHV();
+    int rc = pr_mask_params_parse(hcr_mask, min_sr_length, &p);
+    if (rc != 0) {
+        SvREFCNT_dec((SV *)h);
+        croak("Prgpu: pr_mask_params_parse: %s (%d)", pr_last_error(), rc);
+    }
+    hv_store(h, "phred_min", 9, newSViv(p.phred_min), 0);
+    hv_store(h, "phred_max", 9, newSViv(p.phred_max), 0);
+    hv_store(h, "mask_min_len", 12, newSViv(p.mask_min_len), 0);
+    hv_store(h, "unmask_min_len", 14, newSViv(p.unmask_min_len), 0);
+    hv_store(h, "mask_reduce", 11, newSViv(p.mask_reduce), 0);
+    hv_store(h, "end_ratio", 9, newSVnv(p.end_ratio), 0);
+    hv_store(h, "phred_offset", 12, newSViv(p.phred_offset), 0);
+    RETVAL = newRV_noinc((SV *)h);
+  OUTPUT:
+    RETVAL
+
+SV *
+mask_run(IV ctx, HV *params, SV *seq, SV *qual, SV *off)
+  CODE:
+    /* SeqFilter --phred-mask on the GPU (bin/proovread:1706): masked bases, the MCRs and
+       (bpt, bpN) of reads packed as ASCII seq / phred+offset qual pools with int64 offsets */
+    pr_mask_params p;
+    STRLEN ls = 0, lq = 0, lo = 0;
+    const char *s = arg_buf(aTHX_ seq, "seq", 0, &ls);
+    const char *q = arg_buf(aTHX_ qual, "qual", 0, &lq);
+    const char *o = arg_buf(aTHX_ off, "off", 8, &lo);
+    const int64_t n = check_off(aTHX_ o, lo, ls, "off");
+    int64_t cap = 0;
+    int rc;
+    HV *res;
+    if (lq < ls) croak("Prgpu::mask_run: qual shorter than seq");
+    pr_mask_params_default(&p);
+    p.phred_min = inum(aTHX_ params, "phred_min", p.phred_min);
+    p.phred_max = inum(aTHX_ params, "phred_max", p.phred_max);
+    p.mask_min_len = inum(aTHX_ params, "mask_min_len", p.mask_min_len);
+    p.unmask_min_len = inum(aTHX_ params, "unmask_min_len", p.unmask_min_len);
+    p.mask_reduce = inum(aTHX_ params, "mask_reduce", p.mask_reduce);
+    p.end_ratio = num(aTHX_ params, "end_ratio", p.end_ratio);
+    p.phred_offset = inum(aTHX_ params, "phred_offset", p.phred_offset);
+    rc = pr_mask_bound(&p, (int32_t)n, (const int64_t *)o, &cap);
+    if (rc != 0) croak("Prgpu: pr_mask_bound: %s (%d)", pr_last_error(), rc);
+    {
+        SV *s_out = newSV(ls + 1), *s_moff = newSV(8 * (n + 1) + 1), *s_mcr = newSV(8 * cap + 1),
+           *s_nm = newSV(4 * n + 1), *s_st = newSV(16 + 1);
+        SV *all[] = {s_out, s_moff, s_mcr, s_nm, s_st};
+        const STRLEN lens[] = {ls, 8 * (n + 1), 8 * cap, 4 * n, 16};
+        const char *keys[] = {"seq", "mcr_off", "mcr", "n_mcr", "stats"};
+        unsigned k;
+        for (k = 0; k < sizeof all / sizeof all[0]; ++k) {
+            SvPOK_on(all[k]);
+            memset(SvPVX(all[k]), 0, lens[k] + 1);
+            SvCUR_set(all[k], lens[k]);
+        }
+        rc = pr_mask_run(INT2PTR(pr_ctx *, ctx), &p, (int32_t)n, (const int64_t *)o, (const uint8_t *)s,
+                         (const uint8_t *)q, (uint8_t *)SvPVX(s_out), (int64_t *)SvPVX(s_moff),
+                         (int32_t *)SvPVX(s_mcr), (int32_t *)SvPVX(s_nm), (int64_t *)SvPVX(s_st));
+        if (rc != 0) {
+            for (k = 0; k < sizeof all / sizeof all[0]; ++k) SvREFCNT_dec(all[k]);
+            croak("Prgpu: pr_mask_run: %s (%d)", pr_last_error(), rc);
+        }
+        res = newHV();
+        for (k = 0; k < sizeof all / sizeof all[0]; ++k) hv_store(res, keys[k], (I32)strlen(keys[k]), all[k], 0);
+    }
+    RETVAL = newRV_noinc((SV *)res);
+  OUTPUT:
+    RETVAL

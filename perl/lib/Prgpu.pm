@@ -347,6 +347,33 @@ sub mem {
     return (\@head, \@rec);
 }
 
+# ------------------------------------------------------------------ masking
+#
+# `SeqFilter --phred-mask <hcr-mask> --base-content N` after every iteration (bin/proovread:1701-1716)
+# on the GPU: mask($ctx, hcr_mask => '20,41,80,130,60,0.7', min_sr_length => 150,
+# seqs => [...], quals => [...]) -> (\@masked, \@mcrs ([[off, len], ...] per read), [bpt, bpN]);
+# bpN / bpt is the input of mask_shortcut_frac (bin/proovread:2026-2047).
+sub mask {
+    my ($ctx, %a) = @_;
+    my $p = mask_params($a{hcr_mask} // '20,41,80,130,60,0.7', $a{min_sr_length} // 100);
+    $p->{phred_offset} = $a{phred_offset} if defined $a{phred_offset};
+    my ($seqs, $quals) = @a{qw(seqs quals)};
+    die "Prgpu::mask: every read needs a quality string of its length\n"
+        if @$seqs != @$quals || grep { length $seqs->[$_] != length $quals->[$_] } 0 .. $#$seqs;
+    my @off = (0);
+    push @off, $off[-1] + length $_ for @$seqs;
+    my $o = mask_run(ref $ctx ? $ctx->handle : $ctx, $p, join('', @$seqs), join('', @$quals), pack('q<*', @off));
+    my @moff = unpack('q<*', $o->{mcr_off});
+    my @nm = unpack('l<*', $o->{n_mcr});
+    my (@masked, @mcrs);
+    for my $i (0 .. $#$seqs) {
+        push @masked, substr($o->{seq}, $off[$i], $off[$i + 1] - $off[$i]);
+        my @v = unpack('l<*', substr($o->{mcr}, 8 * $moff[$i], 8 * $nm[$i]));
+        push @mcrs, [map { [@v[2 * $_, 2 * $_ + 1]] } 0 .. $nm[$i] - 1];
+    }
+    return (\@masked, \@mcrs, [unpack('q<2', $o->{stats})]);
+}
+
 # the FASTQ record bam2cns prints (bam2cns:453, Fastq::Seq string)
 sub fastq {
     my ($r) = @_;

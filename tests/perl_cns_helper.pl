@@ -8,6 +8,8 @@
 #       mem output) with host seeding, and the SW results either injected from IN.json's
 #       `sw` (the tests' CPU oracle; `batch` is then the hex of the task arrays handed to it)
 #       or from sw_run on the GPU
+#   perl_cns_helper.pl mask IN.json  -> {params, masked, mcrs, stats}: Prgpu::mask_params, and
+#       Prgpu::mask on the GPU when IN.json has reads
 use strict;
 use warnings;
 use FindBin;
@@ -43,6 +45,13 @@ if ($mode eq 'pack') {
                                   sr_names => $in->{sr_names}, sr_seqs => $in->{sr_seqs},
                                   sr_quals => $in->{sr_quals});
     print $json->encode({head => $head, rec => $rec, batch => \%batch_hex}), "\n";
+} elsif ($mode eq 'mask') {
+    my $p = Prgpu::mask_params($in->{hcr_mask}, $in->{min_sr_length});
+    my ($masked, $mcrs, $st) = $in->{seqs}
+        ? Prgpu::mask(Prgpu::Context->new(0), hcr_mask => $in->{hcr_mask}, min_sr_length => $in->{min_sr_length},
+                      seqs => $in->{seqs}, quals => $in->{quals})
+        : ([], [], []);
+    print $json->encode({params => $p, masked => $masked, mcrs => $mcrs, stats => $st}), "\n";
 } else {
-    die "usage: perl_cns_helper.pl pack|run|mem IN.json\n";
+    die "usage: perl_cns_helper.pl pack|run|mem|mask IN.json\n";
 }

@@ -118,3 +118,54 @@ def test_perl_mem_equals_python_mem_on_gpu(tmp_path):
     got = _perl_mem(js, tmp_path)
     assert got["head"] == head
     assert got["rec"] == rec and len(rec) > 40
+
+
+# ---- masking (SeqFilter --phred-mask) through XS
+
+def _perl_mask(js, tmp_path):
+    p = tmp_path / "mask.json"
+    p.write_text(json.dumps(js))
+    r = subprocess.run(["perl", str(HELPER), "mask", str(p)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+@pytest.mark.parametrize("spec,srl", [("20,41,80,130,60,0.7", 150), ("20,41,80,130,60,0.3", 101),
+                                      ("15,40,75,125,30,0.5", 250)])
+def test_perl_mask_params_equal_python(tmp_path, spec, srl):
+    from proovread_amd import mask
+    got = _perl_mask({"hcr_mask": spec, "min_sr_length": srl}, tmp_path)["params"]
+    p = mask.params(spec, srl)
+    for k in ("phred_min", "phred_max", "mask_min_len", "unmask_min_len", "mask_reduce", "phred_offset"):
+        assert got[k] == getattr(p, k), k
+    assert got["end_ratio"] == p.end_ratio
+
+
+def test_perl_mask_without_device_dies(tmp_path):
+    p = tmp_path / "mask.json"
+    p.write_text(json.dumps({"hcr_mask": "20,41,80,130,60,0.7", "min_sr_length": 150, "seqs": ["ACGT"],
+                             "quals": ["IIII"]}))
+    r = subprocess.run(["perl", str(HELPER), "mask", str(p)], capture_output=True, text=True)
+    assert r.returncode != 0 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_perl_mask_equals_python_mask_on_gpu(tmp_path):
+    import random
+    from proovread_amd import mask
+    rng = random.Random(9)
+    seqs, quals = [], []
+    for _ in range(40):
+        L = rng.choice([0, 1, 64, 500, 3000, 10000])
+        q, hi = [], rng.random() < 0.6
+        while len(q) < L:
+            q += [rng.randint(53, 74) if hi else rng.randint(33, 52)] * rng.randint(1, 400)
+            hi = not hi
+        quals.append(bytes(q[:L]).decode())
+        seqs.append("".join(rng.choice("ACGT") for _ in range(L)))
+    spec, srl = "20,41,80,130,60,0.7", 150
+    got = _perl_mask({"hcr_mask": spec, "min_sr_length": srl, "seqs": seqs, "quals": quals}, tmp_path)
+    want, wmcrs, wst = mask.run([s.encode() for s in seqs], [q.encode() for q in quals], mask.params(spec, srl))
+    assert got["masked"] == [w.decode() for w in want]
+    assert got["mcrs"] == wmcrs
+    assert tuple(got["stats"]) == wst and wst[1] > 0
