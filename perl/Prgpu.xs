@@ -87,6 +87,105 @@ static int64_t check_off(pTHX_ const char *off, STRLEN off_len, STRLEN pool, con
     return n;
 }
 
+/* Sam::Seq class globals (Seq.pm:114-128) as bam2cns sets them (bam2cns:227-237) */
+static void fill_cns_params(pTHX_ HV *params, pr_cns_params *p) {
+    pr_cns_params_default(p);
+    p->max_coverage = num(aTHX_ params, "coverage", p->max_coverage);
+    p->bin_size = num(aTHX_ params, "bin_size", p->bin_size);
+    p->trim = inum(aTHX_ params, "trim", p->trim);
+    p->indel_taboo_length = inum(aTHX_ params, "indel_taboo_length", p->indel_taboo_length);
+    p->indel_taboo = num(aTHX_ params, "indel_taboo", p->indel_taboo);
+    p->min_aln_length = inum(aTHX_ params, "min_aln_length", p->min_aln_length);
+    p->max_ins_length = inum(aTHX_ params, "max_ins_length", p->max_ins_length);
+    p->fallback_phred = inum(aTHX_ params, "fallback_phred", p->fallback_phred);
+    p->phred_offset = inum(aTHX_ params, "phred_offset", p->phred_offset);
+    p->ref_phred_offset = inum(aTHX_ params, "qv_offset", p->ref_phred_offset);
+    p->use_ref_qual = inum(aTHX_ params, "use_ref_qual", p->use_ref_qual);
+    p->qual_weighted = inum(aTHX_ params, "qual_weighted", p->qual_weighted);
+    p->detect_chimera = inum(aTHX_ params, "detect_chimera", p->detect_chimera);
+    p->invert_scores = inum(aTHX_ params, "invert_scores", p->invert_scores);
+}
+
+/* bwa mem scoring / band options (proovread.cfg:320-333) over the bwa-sr / finish defaults */
+static void fill_sw_opts(pTHX_ HV *opts, pr_sw_opts *o) {
+    pr_sw_opts_default(o, inum(aTHX_ opts, "finish", 0));
+    o->a = inum(aTHX_ opts, "a", o->a);
+    o->b = inum(aTHX_ opts, "b", o->b);
+    o->o_del = inum(aTHX_ opts, "o_del", o->o_del);
+    o->e_del = inum(aTHX_ opts, "e_del", o->e_del);
+    o->o_ins = inum(aTHX_ opts, "o_ins", o->o_ins);
+    o->e_ins = inum(aTHX_ opts, "e_ins", o->e_ins);
+    o->w = inum(aTHX_ opts, "w", o->w);
+    o->pen_clip5 = inum(aTHX_ opts, "pen_clip5", o->pen_clip5);
+    o->pen_clip3 = inum(aTHX_ opts, "pen_clip3", o->pen_clip3);
+    o->zdrop = inum(aTHX_ opts, "zdrop", o->zdrop);
+    o->min_score_per_base = num(aTHX_ opts, "min_score_per_base", o->min_score_per_base);
+}
+
+/* consensus output pools as Perl strings (13 of them, returned as a hash of packed data) */
+#define CNS_NOUT 13
+static void cns_out_alloc(pTHX_ int64_t n, int64_t na, const pr_cns_bounds *bd, SV **all, pr_cns_out *o) {
+    const STRLEN lens[CNS_NOUT] = {8 * (n + 1), 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, bd->seq_cap, bd->seq_cap,
+                                   bd->seq_cap, 4 * bd->seq_cap, 8 * (n + 1), 16 * bd->chim_cap, na};
+    unsigned k;
+    for (k = 0; k < CNS_NOUT; ++k) {
+        all[k] = newSV(lens[k] + 1);
+        SvPOK_on(all[k]);
+        memset(SvPVX(all[k]), 0, lens[k] + 1);
+        SvCUR_set(all[k], lens[k]);
+    }
+    memset(o, 0, sizeof *o);
+    o->out_off = (int64_t *)SvPVX(all[0]);
+    o->status = (int32_t *)SvPVX(all[1]);
+    o->seq_len = (int32_t *)SvPVX(all[2]);
+    o->trace_len = (int32_t *)SvPVX(all[3]);
+    o->ncigar = (int32_t *)SvPVX(all[4]);
+    o->nchim = (int32_t *)SvPVX(all[5]);
+    o->seq = (uint8_t *)SvPVX(all[6]);
+    o->qual = (uint8_t *)SvPVX(all[7]);
+    o->trace = (uint8_t *)SvPVX(all[8]);
+    o->cigar = (uint32_t *)SvPVX(all[9]);
+    o->chim_off = (int64_t *)SvPVX(all[10]);
+    o->chim = (int32_t *)SvPVX(all[11]);
+    o->kept = (uint8_t *)SvPVX(all[12]);
+}
+
+static SV *cns_out_hash(pTHX_ SV **all) {
+    static const char *keys[CNS_NOUT] = {"out_off", "status", "seq_len", "trace_len", "ncigar", "nchim", "seq",
+                                         "qual", "trace", "cigar", "chim_off", "chim", "kept"};
+    HV *res = newHV();
+    unsigned k;
+    for (k = 0; k < CNS_NOUT; ++k) hv_store(res, keys[k], (I32)strlen(keys[k]), all[k], 0);
+    return newRV_noinc((SV *)res);
+}
+
+/* the SW batch fields of a batch hash (nt4 pools, offsets, task columns), checked */
+static void fill_sw_batch(pTHX_ HV *batch, pr_sw_batch *b) {
+    STRLEN lss = 0, lso = 0, lls = 0, llo = 0;
+    const char *ss, *so, *ls_, *lo_;
+    int64_t nt;
+    memset(b, 0, sizeof *b);
+    ss = field(aTHX_ batch, "sr_seq", 0, 0, &lss);
+    so = field(aTHX_ batch, "sr_off", 8, 0, &lso);
+    ls_ = field(aTHX_ batch, "lr_seq", 0, 0, &lls);
+    lo_ = field(aTHX_ batch, "lr_off", 8, 0, &llo);
+    b->n_sr = (int32_t)check_off(aTHX_ so, lso, lss, "sr_off");
+    b->n_lr = (int32_t)check_off(aTHX_ lo_, llo, lls, "lr_off");
+    b->sr_seq = (const uint8_t *)ss;
+    b->sr_off = (const int64_t *)so;
+    b->lr_seq = (const uint8_t *)ls_;
+    b->lr_off = (const int64_t *)lo_;
+    nt = (int64_t)num(aTHX_ batch, "n_task", -1);
+    if (nt < 0) croak("Prgpu: batch field 'n_task' missing or negative");
+    b->n_task = nt;
+    b->t_sr = (const int32_t *)field(aTHX_ batch, "t_sr", 4 * (size_t)nt, 0, NULL);
+    b->t_lr = (const int32_t *)field(aTHX_ batch, "t_lr", 4 * (size_t)nt, 0, NULL);
+    b->t_strand = (const uint8_t *)field(aTHX_ batch, "t_strand", (size_t)nt, 0, NULL);
+    b->t_qbeg = (const int32_t *)field(aTHX_ batch, "t_qbeg", 4 * (size_t)nt, 0, NULL);
+    b->t_rbeg = (const int32_t *)field(aTHX_ batch, "t_rbeg", 4 * (size_t)nt, 0, NULL);
+    b->t_slen = (const int32_t *)field(aTHX_ batch, "t_slen", 4 * (size_t)nt, 0, NULL);
+}
+
 MODULE = Prgpu  PACKAGE = Prgpu
 
 PROTOTYPES: DISABLE
@@ -140,23 +239,7 @@ cns_run(IV ctx, HV *params, HV *batch)
     STRLEN seq_len = 0, qual_len = 0, cig_len = 0;
     int64_t n, na, nbases, nign = 0, i;
     int rc;
-    HV *res;
-    /* Sam::Seq class globals (Seq.pm:114-128) as bam2cns sets them (bam2cns:227-237) */
-    pr_cns_params_default(&p);
-    p.max_coverage = num(aTHX_ params, "coverage", p.max_coverage);
-    p.bin_size = num(aTHX_ params, "bin_size", p.bin_size);
-    p.trim = inum(aTHX_ params, "trim", p.trim);
-    p.indel_taboo_length = inum(aTHX_ params, "indel_taboo_length", p.indel_taboo_length);
-    p.indel_taboo = num(aTHX_ params, "indel_taboo", p.indel_taboo);
-    p.min_aln_length = inum(aTHX_ params, "min_aln_length", p.min_aln_length);
-    p.max_ins_length = inum(aTHX_ params, "max_ins_length", p.max_ins_length);
-    p.fallback_phred = inum(aTHX_ params, "fallback_phred", p.fallback_phred);
-    p.phred_offset = inum(aTHX_ params, "phred_offset", p.phred_offset);
-    p.ref_phred_offset = inum(aTHX_ params, "qv_offset", p.ref_phred_offset);
-    p.use_ref_qual = inum(aTHX_ params, "use_ref_qual", p.use_ref_qual);
-    p.qual_weighted = inum(aTHX_ params, "qual_weighted", p.qual_weighted);
-    p.detect_chimera = inum(aTHX_ params, "detect_chimera", p.detect_chimera);
-    p.invert_scores = inum(aTHX_ params, "invert_scores", p.invert_scores);
+    fill_cns_params(aTHX_ params, &p);
 
     /* the batch: every buffer checked against the counts before the library sees it */
     memset(&b, 0, sizeof b);
@@ -204,46 +287,16 @@ cns_run(IV ctx, HV *params, HV *batch)
     rc = pr_cns_bounds_of(&b, &bd);
     if (rc != 0) croak("Prgpu: pr_cns_bounds_of: %s (%d)", pr_last_error(), rc);
     {
-        /* output pools, one Perl string each, returned as packed data */
-        SV *s_off = newSV(8 * (n + 1) + 1), *s_st = newSV(4 * n + 1), *s_sl = newSV(4 * n + 1),
-           *s_tl = newSV(4 * n + 1), *s_nc = newSV(4 * n + 1), *s_nch = newSV(4 * n + 1),
-           *s_seq = newSV(bd.seq_cap + 1), *s_qual = newSV(bd.seq_cap + 1), *s_tr = newSV(bd.seq_cap + 1),
-           *s_cig = newSV(4 * bd.seq_cap + 1), *s_choff = newSV(8 * (n + 1) + 1),
-           *s_ch = newSV(16 * bd.chim_cap + 1), *s_kept = newSV(na + 1);
-        SV *all[] = {s_off, s_st, s_sl, s_tl, s_nc, s_nch, s_seq, s_qual, s_tr, s_cig, s_choff, s_ch, s_kept};
-        const STRLEN lens[] = {8 * (n + 1), 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, bd.seq_cap, bd.seq_cap, bd.seq_cap,
-                               4 * bd.seq_cap, 8 * (n + 1), 16 * bd.chim_cap, na};
-        const char *keys[] = {"out_off", "status", "seq_len", "trace_len", "ncigar", "nchim", "seq", "qual",
-                              "trace", "cigar", "chim_off", "chim", "kept"};
+        SV *all[CNS_NOUT];
         unsigned k;
-        for (k = 0; k < sizeof all / sizeof all[0]; ++k) {
-            SvPOK_on(all[k]);
-            memset(SvPVX(all[k]), 0, lens[k] + 1);
-            SvCUR_set(all[k], lens[k]);
-        }
-        memset(&o, 0, sizeof o);
-        o.out_off = (int64_t *)SvPVX(s_off);
-        o.status = (int32_t *)SvPVX(s_st);
-        o.seq_len = (int32_t *)SvPVX(s_sl);
-        o.trace_len = (int32_t *)SvPVX(s_tl);
-        o.ncigar = (int32_t *)SvPVX(s_nc);
-        o.nchim = (int32_t *)SvPVX(s_nch);
-        o.seq = (uint8_t *)SvPVX(s_seq);
-        o.qual = (uint8_t *)SvPVX(s_qual);
-        o.trace = (uint8_t *)SvPVX(s_tr);
-        o.cigar = (uint32_t *)SvPVX(s_cig);
-        o.chim_off = (int64_t *)SvPVX(s_choff);
-        o.chim = (int32_t *)SvPVX(s_ch);
-        o.kept = (uint8_t *)SvPVX(s_kept);
+        cns_out_alloc(aTHX_ n, na, &bd, all, &o);
         rc = pr_cns_run(INT2PTR(pr_ctx *, ctx), &p, &b, &o);
         if (rc != 0) {
-            for (k = 0; k < sizeof all / sizeof all[0]; ++k) SvREFCNT_dec(all[k]);
+            for (k = 0; k < CNS_NOUT; ++k) SvREFCNT_dec(all[k]);
             croak("Prgpu: pr_cns_run: %s (%d)", pr_last_error(), rc);
         }
-        res = newHV();
-        for (k = 0; k < sizeof all / sizeof all[0]; ++k) hv_store(res, keys[k], (I32)strlen(keys[k]), all[k], 0);
+        RETVAL = cns_out_hash(aTHX_ all);
     }
-    RETVAL = newRV_noinc((SV *)res);
   OUTPUT:
     RETVAL
 
@@ -307,43 +360,12 @@ sw_run(IV ctx, HV *opts, HV *batch)
     pr_sw_opts o;
     pr_sw_batch b;
     pr_sw_out out;
-    STRLEN lss = 0, lso = 0, lls = 0, llo = 0;
-    const char *ss, *so, *ls_, *lo_;
     int64_t nt;
     int rc;
     HV *res;
-    pr_sw_opts_default(&o, inum(aTHX_ opts, "finish", 0));
-    o.a = inum(aTHX_ opts, "a", o.a);
-    o.b = inum(aTHX_ opts, "b", o.b);
-    o.o_del = inum(aTHX_ opts, "o_del", o.o_del);
-    o.e_del = inum(aTHX_ opts, "e_del", o.e_del);
-    o.o_ins = inum(aTHX_ opts, "o_ins", o.o_ins);
-    o.e_ins = inum(aTHX_ opts, "e_ins", o.e_ins);
-    o.w = inum(aTHX_ opts, "w", o.w);
-    o.pen_clip5 = inum(aTHX_ opts, "pen_clip5", o.pen_clip5);
-    o.pen_clip3 = inum(aTHX_ opts, "pen_clip3", o.pen_clip3);
-    o.zdrop = inum(aTHX_ opts, "zdrop", o.zdrop);
-    o.min_score_per_base = num(aTHX_ opts, "min_score_per_base", o.min_score_per_base);
-    memset(&b, 0, sizeof b);
-    ss = field(aTHX_ batch, "sr_seq", 0, 0, &lss);
-    so = field(aTHX_ batch, "sr_off", 8, 0, &lso);
-    ls_ = field(aTHX_ batch, "lr_seq", 0, 0, &lls);
-    lo_ = field(aTHX_ batch, "lr_off", 8, 0, &llo);
-    b.n_sr = (int32_t)check_off(aTHX_ so, lso, lss, "sr_off");
-    b.n_lr = (int32_t)check_off(aTHX_ lo_, llo, lls, "lr_off");
-    b.sr_seq = (const uint8_t *)ss;
-    b.sr_off = (const int64_t *)so;
-    b.lr_seq = (const uint8_t *)ls_;
-    b.lr_off = (const int64_t *)lo_;
-    nt = (int64_t)num(aTHX_ batch, "n_task", -1);
-    if (nt < 0) croak("Prgpu::sw_run: batch field 'n_task' missing or negative");
-    b.n_task = nt;
-    b.t_sr = (const int32_t *)field(aTHX_ batch, "t_sr", 4 * (size_t)nt, 0, NULL);
-    b.t_lr = (const int32_t *)field(aTHX_ batch, "t_lr", 4 * (size_t)nt, 0, NULL);
-    b.t_strand = (const uint8_t *)field(aTHX_ batch, "t_strand", (size_t)nt, 0, NULL);
-    b.t_qbeg = (const int32_t *)field(aTHX_ batch, "t_qbeg", 4 * (size_t)nt, 0, NULL);
-    b.t_rbeg = (const int32_t *)field(aTHX_ batch, "t_rbeg", 4 * (size_t)nt, 0, NULL);
-    b.t_slen = (const int32_t *)field(aTHX_ batch, "t_slen", 4 * (size_t)nt, 0, NULL);
+    fill_sw_opts(aTHX_ opts, &o);
+    fill_sw_batch(aTHX_ batch, &b);
+    nt = b.n_task;
     {
         /* outputs, one Perl string each (PR_SW_MAXCIG ops per task for the CIGARs) */
         SV *s_pos = newSV(4 * nt + 1), *s_sc = newSV(4 * nt + 1), *s_nc = newSV(4 * nt + 1),
@@ -449,5 +471,54 @@ mask_run(IV ctx, HV *params, SV *seq, SV *qual, SV *off)
         for (k = 0; k < sizeof all / sizeof all[0]; ++k) hv_store(res, keys[k], (I32)strlen(keys[k]), all[k], 0);
     }
     RETVAL = newRV_noinc((SV *)res);
+  OUTPUT:
+    RETVAL
+
+SV *
+iter_run(IV ctx, HV *sw_opts, HV *params, HV *batch)
+  CODE:
+    /* One correction iteration on the device (bin/proovread:835-869 for one task: run_bwa,
+       create_sorted_bam and correct_sr_mt without the SAM/BAM files): seed extension + CIGAR
+       of every task, the hand-off into samtools coordinate order, the consensus of every long
+       read.  Tasks grouped by long read (task_lr_off); lr_qual / ref_seq optional. */
+    pr_sw_opts o;
+    pr_cns_params p;
+    pr_iter_batch b;
+    pr_cns_bounds bd;
+    pr_cns_out out;
+    int32_t n_lr = 0;
+    int64_t n_task = 0, nbases, i;
+    const char *tlo;
+    int rc;
+    fill_sw_opts(aTHX_ sw_opts, &o);
+    fill_cns_params(aTHX_ params, &p);
+    memset(&b, 0, sizeof b);
+    fill_sw_batch(aTHX_ batch, &b.sw);
+    nbases = i64_at((const char *)b.sw.lr_off, b.sw.n_lr);
+    tlo = field(aTHX_ batch, "task_lr_off", 8 * (size_t)(b.sw.n_lr + 1), 0, NULL);
+    if (i64_at(tlo, 0) != 0 || i64_at(tlo, b.sw.n_lr) != b.sw.n_task)
+        croak("Prgpu::iter_run: task_lr_off must run from 0 to n_task");
+    for (i = 0; i < b.sw.n_lr; ++i)
+        if (i64_at(tlo, i + 1) < i64_at(tlo, i)) croak("Prgpu::iter_run: task_lr_off not monotone");
+    b.task_lr_off = (const int64_t *)tlo;
+    b.lr_qual = (const uint8_t *)field(aTHX_ batch, "lr_qual", (size_t)nbases, 1, NULL);
+    b.ref_seq = (const uint8_t *)field(aTHX_ batch, "ref_seq", (size_t)nbases, 1, NULL);
+    if ((rc = pr_iter_upload(INT2PTR(pr_ctx *, ctx), &b)) != 0)
+        croak("Prgpu: pr_iter_upload: %s (%d)", pr_last_error(), rc);
+    if ((rc = pr_iter_bounds(INT2PTR(pr_ctx *, ctx), &n_lr, &n_task, &bd)) != 0)
+        croak("Prgpu: pr_iter_bounds: %s (%d)", pr_last_error(), rc);
+    if ((rc = pr_iter_launch(INT2PTR(pr_ctx *, ctx), &o, &p)) != 0)
+        croak("Prgpu: pr_iter_launch: %s (%d)", pr_last_error(), rc);
+    {
+        SV *all[CNS_NOUT];
+        unsigned k;
+        cns_out_alloc(aTHX_ n_lr, n_task, &bd, all, &out);
+        rc = pr_iter_download(INT2PTR(pr_ctx *, ctx), &out);
+        if (rc != 0) {
+            for (k = 0; k < CNS_NOUT; ++k) SvREFCNT_dec(all[k]);
+            croak("Prgpu: pr_iter_download: %s (%d)", pr_last_error(), rc);
+        }
+        RETVAL = cns_out_hash(aTHX_ all);
+    }
   OUTPUT:
     RETVAL

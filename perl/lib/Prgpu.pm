@@ -1,8 +1,10 @@
 package Prgpu;
 
-# Perl side of the XS binding (perl/Prgpu.xs) of libprgpu's consensus stage.
+# Perl side of the XS binding (perl/Prgpu.xs) of libprgpu: the consensus stage
+# (run_chunk), the seed-extension stage (mem), one whole iteration (iteration) and the
+# per-iteration masking (mask).
 #
-# What a proovread maintainer calls instead of fanning bam2cns out over xargs
+# Consensus: what a proovread maintainer calls instead of fanning bam2cns out over xargs
 # (bin/proovread:1596-1619): one Prgpu::run_chunk per chunk of long reads, with the
 # reads' SAM records in BAM order.  The record fields read here are the ones the
 # Sam::Seq engine reads (Sam/Alignment.pm:87-110: POS, CIGAR, SEQ, QUAL, AS:i); the
@@ -167,7 +169,13 @@ sub run_chunk {
     die "Prgpu::run_chunk: reads and alignment lists differ in length\n" unless @$reads == @$alns;
     my $b = pack_chunk($reads, $alns);
     my $o = cns_run(ref $ctx ? $ctx->handle : $ctx, $params, $b);
-    my $n = @$reads;
+    return cns_results($o, [map { $_->{id} } @$reads]);
+}
+
+# per-read results of a packed consensus output (cns_run / iter_run)
+sub cns_results {
+    my ($o, $ids) = @_;
+    my $n = @$ids;
     my @off = unpack('q<*', $o->{out_off});
     my @st = unpack('l<*', $o->{status});
     my @sl = unpack('l<*', $o->{seq_len});
@@ -177,7 +185,7 @@ sub run_chunk {
     my @choff = unpack('q<*', $o->{chim_off});
     my @res;
     for my $i (0 .. $n - 1) {
-        my %r = (id => $reads->[$i]{id}, status => $st[$i]);
+        my %r = (id => $ids->[$i], status => $st[$i]);
         if ($st[$i] == 0) {
             my $p = $off[$i];
             $r{seq} = substr($o->{seq}, $p, $sl[$i]);
@@ -247,15 +255,9 @@ sub aln_length {
     return $seq_len;
 }
 
-# mem(%a) -> (header lines, record lines): the output of `bwa-proovread mem`.
-#   ctx        Prgpu::Context (or a sw_runner coderef taking the task batch hash and
-#              returning {pos, score, pass, status, cigar} arrays — the tests inject the oracle)
-#   seed_opts, sw_opts  option hashes for seed_map / sw_run ({finish => 0|1, ...})
-#   b, l       the -b/-l bin filter (0: off)
-#   threads    host seeding threads
-#   lr_names, lr_seqs, sr_names, sr_seqs, sr_quals (undef entries for FASTA reads)
-#   cl         the command line for @PG
-sub mem {
+# Host seeding of sr_seqs against lr_seqs (seed_index_build / seed_map) -> the pr_sw_batch
+# fields (nt4 pools, offsets, task columns in read order, chain order) and the task columns.
+sub seed_batch {
     my (%a) = @_;
     my ($lr_pool, $lr_off) = pool($a{lr_seqs});
     my ($sr_pool, $sr_off) = pool($a{sr_seqs});
@@ -278,6 +280,27 @@ sub mem {
     my %batch = (sr_seq => $sr_pool, sr_off => $sr_off, lr_seq => $lr_pool, lr_off => $lr_off, n_task => $nt,
                  t_sr => pack('l<*', @t_sr), t_lr => pack('l<*', @t_lr), t_strand => pack('C*', @t_strand),
                  t_qbeg => pack('l<*', @t_qbeg), t_rbeg => pack('l<*', @t_rbeg), t_slen => pack('l<*', @t_slen));
+    return (\%batch, {sr => \@t_sr, lr => \@t_lr, strand => \@t_strand, qbeg => \@t_qbeg, rbeg => \@t_rbeg,
+                      slen => \@t_slen});
+}
+
+# mem(%a) -> (header lines, record lines): the output of `bwa-proovread mem`.
+#   ctx        Prgpu::Context (or a sw_runner coderef taking the task batch hash and
+#              returning {pos, score, pass, status, cigar} arrays — the tests inject the oracle)
+#   seed_opts, sw_opts  option hashes for seed_map / sw_run ({finish => 0|1, ...})
+#   b, l       the -b/-l bin filter (0: off)
+#   threads    host seeding threads
+#   lr_names, lr_seqs, sr_names, sr_seqs, sr_quals (undef entries for FASTA reads)
+#   cl         the command line for @PG
+sub mem {
+    my (%a) = @_;
+    my ($bt, $tc) = seed_batch(%a);
+    my %batch = %$bt;
+    my $nt = $batch{n_task};
+    my ($t_sr, $t_lr, $t_strand) = @$tc{qw(sr lr strand)};
+    my @t_sr = @$t_sr;
+    my @t_lr = @$t_lr;
+    my @t_strand = @$t_strand;
     my $res = ref $a{ctx} eq 'CODE' ? $a{ctx}->(\%batch)
             : sw_unpack(sw_run(ref $a{ctx} ? $a{ctx}->handle : $a{ctx}, $a{sw_opts} || {}, \%batch), $nt);
 
@@ -345,6 +368,40 @@ sub mem {
     }
     @rec = @rec[grep { $alive[$_] } 0 .. $#rec] if $filter;
     return (\@head, \@rec);
+}
+
+# ------------------------------------------------------------------ one iteration in one call
+#
+# iteration(%a): one proovread correction task (bin/proovread:835-869: bwa-proovread mem,
+# samtools sort, the bam2cns fan-out) on the device without SAM/BAM files: host seeding of
+# sr_seqs against lr_seqs, then iter_run (seed extension + CIGAR, hand-off in samtools
+# coordinate order, consensus of every long read).  Returns run_chunk-style per-read results.
+#   ctx, seed_opts, sw_opts, threads   as for mem
+#   params     consensus options as for run_chunk
+#   lr_ids, lr_seqs (the mapping reference: the previous task's .masked.fa from the second
+#   iteration on), lr_quals (default phred 3 '$', raw CLR reads), ref_seqs (the consensus
+#   reference, the previous task's unmasked .fq; default lr_seqs), sr_seqs
+sub iteration {
+    my (%a) = @_;
+    my ($bt, $tc) = seed_batch(%a);
+    my %batch = %$bt;
+    my $nt = $batch{n_task};
+    my @ord = sort { $tc->{lr}[$a] <=> $tc->{lr}[$b] || $a <=> $b } 0 .. $nt - 1;   # grouped by long read, stable
+    for my $k (qw(sr lr qbeg rbeg slen)) { $batch{"t_$k"} = pack('l<*', @{$tc->{$k}}[@ord]) }
+    $batch{t_strand} = pack('C*', @{$tc->{strand}}[@ord]);
+    my @cnt = (0) x @{$a{lr_seqs}};
+    ++$cnt[$_] for @{$tc->{lr}};
+    my @tlo = (0);
+    push @tlo, $tlo[-1] + $_ for @cnt;
+    $batch{task_lr_off} = pack('q<*', @tlo);
+    $batch{lr_qual} = join '', map {
+        my $q = $a{lr_quals} ? $a{lr_quals}[$_] : undef;
+        defined $q ? $q : '$' x length $a{lr_seqs}[$_]
+    } 0 .. $#{$a{lr_seqs}};
+    $batch{ref_seq} = join '', @{$a{ref_seqs}} if $a{ref_seqs};
+    my $o = ref $a{ctx} eq 'CODE' ? $a{ctx}->(\%batch)
+          : iter_run(ref $a{ctx} ? $a{ctx}->handle : $a{ctx}, $a{sw_opts} || {}, $a{params} || {}, \%batch);
+    return cns_results($o, $a{lr_ids});
 }
 
 # ------------------------------------------------------------------ masking

@@ -8,6 +8,8 @@
 #       mem output) with host seeding, and the SW results either injected from IN.json's
 #       `sw` (the tests' CPU oracle; `batch` is then the hex of the task arrays handed to it)
 #       or from sw_run on the GPU
+#   perl_cns_helper.pl iter IN.json  -> {batch, res}: Prgpu::iteration (host seeding + iter_run on
+#       the GPU), or with `inject` the batch it would hand to iter_run (CPU)
 #   perl_cns_helper.pl mask IN.json  -> {params, masked, mcrs, stats}: Prgpu::mask_params, and
 #       Prgpu::mask on the GPU when IN.json has reads
 use strict;
@@ -45,6 +47,21 @@ if ($mode eq 'pack') {
                                   sr_names => $in->{sr_names}, sr_seqs => $in->{sr_seqs},
                                   sr_quals => $in->{sr_quals});
     print $json->encode({head => $head, rec => $rec, batch => \%batch_hex}), "\n";
+} elsif ($mode eq 'iter') {
+    # inject: capture the batch handed to iter_run and return an all-failed output (CPU)
+    my %batch_hex;
+    my $n = @{$in->{lr_seqs}};
+    my $ctx = $in->{inject} ? sub {
+        my ($b) = @_;
+        %batch_hex = map { $_ => ($_ eq 'n_task' ? $b->{$_} : unpack('H*', $b->{$_})) } keys %$b;
+        return {map({ $_ => '' } qw(seq qual trace cigar chim kept)), out_off => pack('q<*', (0) x ($n + 1)),
+                chim_off => pack('q<*', (0) x ($n + 1)), status => pack('l<*', (-1) x $n),
+                map({ $_ => pack('l<*', (0) x $n) } qw(seq_len trace_len ncigar nchim))};
+    } : Prgpu::Context->new(0);
+    my @res = Prgpu::iteration(ctx => $ctx, seed_opts => $in->{seed_opts}, sw_opts => $in->{sw_opts},
+                               params => $in->{params}, threads => 2, lr_ids => $in->{lr_ids},
+                               lr_seqs => $in->{lr_seqs}, lr_quals => $in->{lr_quals}, sr_seqs => $in->{sr_seqs});
+    print $json->encode({batch => \%batch_hex, res => \@res}), "\n";
 } elsif ($mode eq 'mask') {
     my $p = Prgpu::mask_params($in->{hcr_mask}, $in->{min_sr_length});
     my ($masked, $mcrs, $st) = $in->{seqs}
@@ -53,5 +70,5 @@ if ($mode eq 'pack') {
         : ([], [], []);
     print $json->encode({params => $p, masked => $masked, mcrs => $mcrs, stats => $st}), "\n";
 } else {
-    die "usage: perl_cns_helper.pl pack|run|mem|mask IN.json\n";
+    die "usage: perl_cns_helper.pl pack|run|mem|iter|mask IN.json\n";
 }

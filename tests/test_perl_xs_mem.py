@@ -169,3 +169,63 @@ def test_perl_mask_equals_python_mask_on_gpu(tmp_path):
     assert got["masked"] == [w.decode() for w in want]
     assert got["mcrs"] == wmcrs
     assert tuple(got["stats"]) == wst and wst[1] > 0
+
+
+# ---- one iteration in one call (Prgpu::iteration -> iter_run -> pr_iter_*)
+
+def _iter_inputs():
+    from proovread_amd import synth
+    d = synth.simulate(31, 60_000, 30, 3000, 40.0, sr_frac=0.3)
+    asc = np.frombuffer(b"ACGTN", np.uint8)
+    lr = [asc[d.lr_seq[d.lr_off[i]:d.lr_off[i + 1]]].tobytes().decode() for i in range(d.n_lr)]
+    sr = [asc[d.sr_seq[d.sr_off[i]:d.sr_off[i + 1]]].tobytes().decode() for i in range(d.n_sr)]
+    js = {"lr_ids": [f"lr{i}" for i in range(d.n_lr)], "lr_seqs": lr, "lr_quals": None, "sr_seqs": sr,
+          "seed_opts": {"finish": 0}, "sw_opts": {"finish": 0}, "params": {"coverage": 11.25, "use_ref_qual": 1}}
+    return d, js
+
+
+def _perl_iter(js, tmp_path):
+    p = tmp_path / "iter.json"
+    p.write_text(json.dumps(js))
+    r = subprocess.run(["perl", str(HELPER), "iter", str(p)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout)
+
+
+def test_perl_iteration_batch_equals_python_iteration_batch(tmp_path):
+    """The batch Prgpu::iteration hands to iter_run: host-seeded tasks grouped by long read
+    (stable) exactly as synth.with_seeded_tasks groups them for iteration.Iteration."""
+    from proovread_amd import seed, synth
+    d, js = _iter_inputs()
+    js["inject"] = 1
+    got = _perl_iter(js, tmp_path)
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    dd = synth.with_seeded_tasks(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=2))
+    b = got["batch"]
+    assert int(b["n_task"]) == len(dd.t_sr) > 1000
+    for k in ("t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen"):
+        assert bytes.fromhex(b[k]) == np.asarray(getattr(dd, k)).tobytes(), k
+    tlo = np.zeros(d.n_lr + 1, np.int64)
+    np.cumsum(np.bincount(dd.t_lr, minlength=d.n_lr), out=tlo[1:])
+    assert bytes.fromhex(b["task_lr_off"]) == tlo.tobytes()
+    assert bytes.fromhex(b["lr_qual"]) == b"$" * int(d.lr_off[-1])
+    assert bytes.fromhex(b["lr_seq"]) == np.asarray(d.lr_seq, np.uint8).tobytes()
+    assert [r["status"] for r in got["res"]] == [-1] * d.n_lr
+
+
+@pytest.mark.gpu
+def test_perl_iteration_equals_python_iteration_on_gpu(tmp_path):
+    from proovread_amd import cns, iteration, seed, sw, synth
+    d, js = _iter_inputs()
+    got = _perl_iter(js, tmp_path)["res"]
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    dd = synth.with_seeded_tasks(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=2))
+    it = iteration.Iteration(dd)
+    it.launch(sw.default_opts(False), cns.CnsParams(coverage=11.25, use_ref_qual=True))
+    want = it.results()
+    assert len(got) == len(want) == d.n_lr
+    for g, w in zip(got, want):
+        assert g["status"] == w.status
+        if w.status == 0:
+            assert (g["seq"], g["qual"], g["trace"], g["cigar"]) == (w.seq, w.qual, w.trace, w.cigar_str)
+            assert [tuple(c) for c in g["chim"]] == list(w.chim)
