@@ -375,6 +375,13 @@ int pr_trim_windows(const pr_trim_params *p, int32_t n, const int64_t *off, cons
 int pr_sam_encode(const char *text, int64_t len, const char *const *ref_names, int32_t n_ref, int n_threads,
                   uint8_t **out, int64_t *out_len, int64_t *n_records);
 int pr_bgzf_compress(const uint8_t *data, int64_t len, int level, int n_threads, uint8_t **out, int64_t *out_len);
+/* samtools sort (bin/proovread:1338) on the host.  pr_bgzf_decompress: BGZF bytes -> the
+ * uncompressed stream (blocks inflated in parallel).  pr_bam_sort_records: a stream of
+ * block_size-prefixed BAM records (what follows the BAM header) in samtools coordinate
+ * order — (reference id, unmapped last; POS; reverse flag), stable on equal keys.      */
+int pr_bgzf_decompress(const uint8_t *data, int64_t len, int n_threads, uint8_t **out, int64_t *out_len);
+int pr_bam_sort_records(const uint8_t *recs, int64_t len, int n_threads, uint8_t **out, int64_t *out_len,
+                        int64_t *n_records);
 void pr_buffer_free(void *p);
 
 #ifdef __cplusplus

@@ -396,6 +396,10 @@ def _codec():
                                     C.POINTER(C.c_void_p), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.pr_bgzf_compress.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_void_p),
                                        C.POINTER(C.c_int64)]
+        L.pr_bgzf_decompress.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.POINTER(C.c_void_p),
+                                         C.POINTER(C.c_int64)]
+        L.pr_bam_sort_records.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.POINTER(C.c_void_p),
+                                          C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.pr_buffer_free.argtypes = [C.c_void_p]
         L.pr_buffer_free.restype = None
         L._bam_ready = True
@@ -438,8 +442,58 @@ def _set_sort_order(text: str, so: str) -> str:
     return "\n".join(lines) + "\n"
 
 
-def sort_bam(in_path: str, out_path: str):
-    """`samtools sort` (coordinate): stable in input order on equal keys."""
+def _native_inflate(data: bytes, threads: int = 0) -> bytes:
+    """BGZF bytes -> uncompressed stream, libprgpu pr_bgzf_decompress."""
+    L, C, _abi = _codec()
+    p, n = C.c_void_p(), C.c_int64()
+    _abi.check(L.pr_bgzf_decompress(data, len(data), threads, C.byref(p), C.byref(n)), "pr_bgzf_decompress")
+    return _take(L, C, p, n)
+
+
+def _native_sort(recs: bytes, threads: int = 0) -> bytes:
+    """block_size-prefixed BAM records in samtools coordinate order, libprgpu pr_bam_sort_records."""
+    L, C, _abi = _codec()
+    p, n, nr = C.c_void_p(), C.c_int64(), C.c_int64()
+    _abi.check(L.pr_bam_sort_records(recs, len(recs), threads, C.byref(p), C.byref(n), C.byref(nr)),
+               "pr_bam_sort_records")
+    return _take(L, C, p, n)
+
+
+def _parse_header(stream: bytes) -> Tuple[Header, int]:
+    """The header of an uncompressed BAM stream (as BamReader reads it) and where records start."""
+    if stream[:4] != b"BAM\x01":
+        raise ValueError("not a BAM file")
+    l_text = struct.unpack_from("<i", stream, 4)[0]
+    text = stream[8:8 + l_text].rstrip(b"\0").decode()
+    o = 8 + l_text
+    n_ref = struct.unpack_from("<i", stream, o)[0]
+    o += 4
+    refs = []
+    for _ in range(n_ref):
+        ln = struct.unpack_from("<i", stream, o)[0]
+        name = stream[o + 4:o + 4 + ln].rstrip(b"\0").decode()
+        refs.append((name, struct.unpack_from("<i", stream, o + 4 + ln)[0]))
+        o += 8 + ln
+    return Header(text, refs), o
+
+
+def sort_bam(in_path: str, out_path: str, native: bool = True, threads: int = 0):
+    """`samtools sort` (coordinate): stable in input order on equal keys.
+
+    native: BGZF inflate, record sort and BGZF deflate in libprgpu (threads); byte-identical
+    to the pure-Python path (native=False)."""
+    if native:
+        with open(in_path, "rb") as fh:
+            stream = _native_inflate(fh.read(), threads)
+        h, o = _parse_header(stream)
+        body = _native_sort(stream[o:], threads)
+        w = BamWriter(out_path, Header(_set_sort_order(h.text, "coordinate"), h.refs))
+        w.w.fh.write(_native_bgzf(body, w.w.level, threads))
+        w.w.fh.write(EOF_BLOCK)
+        w.w.fh.flush()
+        if w._own:
+            w.fh.close()
+        return
     rd = BamReader(in_path)
     recs = [r for _, r, _ in rd.records()]
     rd.close()

@@ -308,4 +308,138 @@ extern "C" int pr_bgzf_compress(const uint8_t *data, int64_t len, int level, int
     return *out ? 0 : pr_set_error(PR_ERR_ARG, "out of host memory");
 }
 
+// BGZF bytes -> the uncompressed stream.  Block boundaries are found by one serial walk
+// over the BC extra fields (BSIZE) and each block's ISIZE trailer, then the blocks are
+// inflated in parallel straight into their place in the output (samtools sort's input side,
+// bin/proovread:1338).
+extern "C" int pr_bgzf_decompress(const uint8_t *data, int64_t len, int n_threads, uint8_t **out, int64_t *out_len) {
+    if (!out || !out_len || (len && !data)) return pr_set_error(PR_ERR_ARG, "null arg");
+    struct Blk {
+        int64_t src, clen, dst;
+        uint32_t isize;
+    };
+    std::vector<Blk> bl;
+    int64_t o = 0, tot = 0;
+    while (o < len) {
+        if (len - o < 18 || data[o] != 31 || data[o + 1] != 139 || data[o + 2] != 8 || !(data[o + 3] & 4))
+            return pr_set_error(PR_ERR_ARG, "not a BGZF block");
+        const int xlen = data[o + 10] | (data[o + 11] << 8);
+        if (o + 12 + xlen > len) return pr_set_error(PR_ERR_ARG, "truncated BGZF header");
+        int bsize = -1;
+        for (int e = 0; e + 4 <= xlen;) {
+            const uint8_t *x = data + o + 12 + e;
+            const int sl = x[2] | (x[3] << 8);
+            if (x[0] == 66 && x[1] == 67 && sl == 2 && e + 6 <= xlen) bsize = x[4] | (x[5] << 8);
+            e += 4 + sl;
+        }
+        if (bsize < 0) return pr_set_error(PR_ERR_ARG, "BGZF block without BC field");
+        const int64_t end = o + bsize + 1;
+        if (end > len || bsize + 1 < 12 + xlen + 8) return pr_set_error(PR_ERR_ARG, "truncated BGZF block");
+        const uint8_t *t = data + end - 4;
+        const uint32_t isize = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+        bl.push_back(Blk{o + 12 + xlen, bsize + 1 - 12 - xlen - 8, tot, isize});
+        tot += isize;
+        o = end;
+    }
+    uint8_t *buf = (uint8_t *)std::malloc((size_t)(tot > 0 ? tot : 1));
+    if (!buf) return pr_set_error(PR_ERR_ARG, "out of host memory");
+    const int64_t nb = (int64_t)bl.size();
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min(nt, 64));
+    if (nb < 2) nt = 1;
+    std::vector<int> fail((size_t)(nb ? nb : 1), 0);
+    auto work = [&](int th) {
+        for (int64_t b = th; b < nb; b += nt) {
+            const Blk &k = bl[(size_t)b];
+            if (k.isize == 0) continue;
+            z_stream z;
+            std::memset(&z, 0, sizeof z);
+            if (inflateInit2(&z, -15) != Z_OK) { fail[b] = 1; continue; }
+            z.next_in = const_cast<Bytef *>(data + k.src);
+            z.avail_in = (uInt)k.clen;
+            z.next_out = buf + k.dst;
+            z.avail_out = k.isize;
+            const int rc = inflate(&z, Z_FINISH);
+            if (rc != Z_STREAM_END || z.avail_out != 0) fail[b] = 1;
+            inflateEnd(&z);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto &x : th) x.join();
+    for (int64_t b = 0; b < nb; ++b)
+        if (fail[b]) {
+            std::free(buf);
+            return pr_set_error(PR_ERR_ARG, "inflate failed (corrupt BGZF block)");
+        }
+    *out = buf;
+    *out_len = tot;
+    return 0;
+}
+
+// samtools sort (coordinate) of a BAM record stream (block_size-prefixed records, the
+// part of an uncompressed BAM after its header): key (reference id with unmapped last,
+// POS+1 or 0 when unmapped, reverse flag), stable in input order on equal keys — the
+// order of proovread_amd/bamio.py:record_key + sort_bam.
+extern "C" int pr_bam_sort_records(const uint8_t *recs, int64_t len, int n_threads, uint8_t **out, int64_t *out_len,
+                                   int64_t *n_records) {
+    if (!out || !out_len || (len && !recs)) return pr_set_error(PR_ERR_ARG, "null arg");
+    std::vector<int64_t> off;
+    for (int64_t o = 0; o < len;) {
+        if (len - o < 4) return pr_set_error(PR_ERR_ARG, "truncated BAM record");
+        int32_t bs;
+        std::memcpy(&bs, recs + o, 4);
+        if (bs < 32 || o + 4 + bs > len) return pr_set_error(PR_ERR_ARG, "bad BAM record size");
+        off.push_back(o);
+        o += 4 + (int64_t)bs;
+    }
+    const int64_t n = (int64_t)off.size();
+    struct Key {
+        uint64_t hi, lo;   // reference id (unmapped: 2^31), then (POS+1) << 1 | reverse
+        int64_t i;         // input index: stable on equal keys
+        bool operator<(const Key &o) const {
+            return hi != o.hi ? hi < o.hi : (lo != o.lo ? lo < o.lo : i < o.i);
+        }
+    };
+    std::vector<Key> key((size_t)n);
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t *r = recs + off[(size_t)i] + 4;
+        int32_t rid, pos;
+        uint16_t flag;
+        std::memcpy(&rid, r, 4);
+        std::memcpy(&pos, r + 4, 4);
+        std::memcpy(&flag, r + 14, 2);
+        const uint64_t k0 = rid >= 0 ? (uint64_t)rid : (uint64_t)1 << 31;
+        const uint64_t k1 = rid >= 0 ? (uint64_t)(uint32_t)(pos + 1) : 0;
+        key[(size_t)i] = Key{k0, (k1 << 1) | ((flag >> 4) & 1u), i};
+    }
+    std::sort(key.begin(), key.end());
+    uint8_t *buf = (uint8_t *)std::malloc((size_t)(len > 0 ? len : 1));
+    if (!buf) return pr_set_error(PR_ERR_ARG, "out of host memory");
+    std::vector<int64_t> dst((size_t)n + 1, 0);
+    for (int64_t j = 0; j < n; ++j) {
+        const int64_t i = key[(size_t)j].i;
+        const int64_t sz = (i + 1 < n ? off[(size_t)i + 1] : len) - off[(size_t)i];
+        dst[(size_t)j + 1] = dst[(size_t)j] + sz;
+    }
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min(nt, 64));
+    if (n < 4096) nt = 1;
+    auto copy = [&](int t) {
+        for (int64_t j = n * t / nt; j < n * (t + 1) / nt; ++j) {
+            const int64_t i = key[(size_t)j].i;
+            std::memcpy(buf + dst[(size_t)j], recs + off[(size_t)i], (size_t)(dst[(size_t)j + 1] - dst[(size_t)j]));
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(copy, t);
+    copy(0);
+    for (auto &x : th) x.join();
+    *out = buf;
+    *out_len = len;
+    if (n_records) *n_records = n;
+    return 0;
+}
+
 extern "C" void pr_buffer_free(void *p) { std::free(p); }
