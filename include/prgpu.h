@@ -382,6 +382,25 @@ int pr_bgzf_compress(const uint8_t *data, int64_t len, int level, int n_threads,
 int pr_bgzf_decompress(const uint8_t *data, int64_t len, int n_threads, uint8_t **out, int64_t *out_len);
 int pr_bam_sort_records(const uint8_t *recs, int64_t len, int n_threads, uint8_t **out, int64_t *out_len,
                         int64_t *n_records);
+/* bam2cns's BAM reader (bam2cns:336 region reads, restated as one pass): every record of a
+ * BAM record stream decoded into the pr_cns_batch alignment columns — rid (-1 unmapped),
+ * POS (1-based), AS:i/f/Z value and PR_ALN_* flags, SEQ as SAM prints it, QUAL phred+33
+ * ('!' x l_seq when absent), BAM CIGAR ops; pools and offsets library-owned.          */
+typedef struct pr_bam_alns {
+    int64_t n;
+    int32_t *rid, *pos1;
+    double *score;
+    uint8_t *flags;
+    int64_t *seq_off;
+    int32_t *lseq;
+    int64_t *cig_off;
+    int32_t *ncig;
+    uint8_t *seq, *qual;
+    uint32_t *cig;
+    int64_t seq_len, cig_len;
+} pr_bam_alns;
+int pr_bam_decode_alns(const uint8_t *recs, int64_t len, int n_threads, pr_bam_alns *out);
+void pr_bam_alns_free(pr_bam_alns *a);
 void pr_buffer_free(void *p);
 
 #ifdef __cplusplus

@@ -17,6 +17,7 @@ order).  Errors exit with status 255 like Verbose->exit (Verbose.pm:454).
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import dataclasses
 import functools
 import glob
@@ -27,7 +28,9 @@ import struct
 import sys
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
-from . import cns
+import numpy as np
+
+from . import bamio, cns
 
 
 def _perl_split_digits(s: str) -> List[str]:
@@ -219,6 +222,85 @@ def bam_records(path: str) -> Tuple[Dict[str, int], Iterator[cns.SamRecord]]:
     return hdr, it()
 
 
+class _BamAlns(C.Structure):
+    _fields_ = [("n", C.c_int64), ("rid", C.c_void_p), ("pos1", C.c_void_p), ("score", C.c_void_p),
+                ("flags", C.c_void_p), ("seq_off", C.c_void_p), ("lseq", C.c_void_p), ("cig_off", C.c_void_p),
+                ("ncig", C.c_void_p), ("seq", C.c_void_p), ("qual", C.c_void_p), ("cig", C.c_void_p),
+                ("seq_len", C.c_int64), ("cig_len", C.c_int64)]
+
+
+def bam_alns_native(path: str, threads: int = 0) -> Tuple[List[str], Dict[str, np.ndarray]]:
+    """Every record of a BAM decoded by libprgpu (pr_bgzf_decompress + pr_bam_decode_alns):
+    reference names and the pr_cns_batch alignment columns (rid, pos1, score, flags, seq_off,
+    lseq, cig_off, ncig) with their pools (seq, qual, cig) — what bam_records yields, as arrays."""
+    from . import _abi
+    L, _, _ = bamio._codec()
+    if not getattr(L, "_bam_alns_ready", False):
+        L.pr_bam_decode_alns.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.POINTER(_BamAlns)]
+        L.pr_bam_alns_free.argtypes = [C.POINTER(_BamAlns)]
+        L.pr_bam_alns_free.restype = None
+        L._bam_alns_ready = True
+    with open(path, "rb") as fh:
+        stream = bamio._native_inflate(fh.read(), threads)
+    h, o = bamio._parse_header(stream)
+    body = stream[o:]
+    a = _BamAlns()
+    _abi.check(L.pr_bam_decode_alns(body, len(body), threads, C.byref(a)), "pr_bam_decode_alns")
+    try:
+        n = a.n
+        def take(ptr, ct, cnt):
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ct)), shape=(max(cnt, 1),))[:cnt].copy()
+        cols = {"rid": take(a.rid, C.c_int32, n), "pos1": take(a.pos1, C.c_int32, n),
+                "score": take(a.score, C.c_double, n), "flags": take(a.flags, C.c_uint8, n),
+                "seq_off": take(a.seq_off, C.c_int64, n), "lseq": take(a.lseq, C.c_int32, n),
+                "cig_off": take(a.cig_off, C.c_int64, n), "ncig": take(a.ncig, C.c_int32, n),
+                "seq": take(a.seq, C.c_uint8, a.seq_len), "qual": take(a.qual, C.c_uint8, a.seq_len),
+                "cig": take(a.cig, C.c_uint32, a.cig_len)}
+    finally:
+        L.pr_bam_alns_free(C.byref(a))
+    return [nm for nm, _ in h.refs], cols
+
+
+def pack_bam_chunk(reads: Sequence[cns.LongRead], names: Sequence[str], A: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+    """pr_cns_batch for a chunk from natively decoded BAM columns: each read gets the records
+    whose RNAME is its id, in file order (a repeated id gets the same records, samtools view
+    "id:"); the pools stay as decoded, the columns point into them."""
+    want: Dict[str, int] = {}
+    for i, r in enumerate(reads):
+        want.setdefault(r.id, i)
+    lut = np.array([want.get(nm, -1) for nm in names] + [-1], np.int64)
+    ridx = lut[A["rid"]] if len(A["rid"]) else np.zeros(0, np.int64)   # rid -1 -> lut[-1] = -1
+    sel = np.nonzero(ridx >= 0)[0]
+    if (A["flags"][sel] & _abi_flag("PR_ALN_NO_SEQ")).any():
+        die("Cannot handle BAM secondary alignments without seq/qual")
+    order = sel[np.argsort(ridx[sel], kind="stable")]
+    counts = np.bincount(ridx[sel], minlength=len(reads))
+    start = np.zeros(len(reads) + 1, np.int64)
+    np.cumsum(counts, out=start[1:])
+    canon = [want[r.id] for r in reads]
+    if all(c == i for i, c in enumerate(canon)):
+        idx = order
+    else:
+        idx = np.concatenate([order[start[c]:start[c + 1]] for c in canon] or [np.zeros(0, np.int64)])
+    d = cns.pack_reads(reads)
+    aln_off = np.zeros(len(reads) + 1, np.int64)
+    np.cumsum([counts[c] for c in canon], out=aln_off[1:])
+    d.update(aln_off=aln_off, aln_pos=A["pos1"][idx], aln_score=A["score"][idx], aln_flags=A["flags"][idx],
+             aln_seq_off=A["seq_off"][idx], aln_lseq=A["lseq"][idx], aln_cig_off=A["cig_off"][idx],
+             aln_ncig=A["ncig"][idx])
+    d["seq_pool"] = A["seq"] if len(A["seq"]) else np.zeros(1, np.uint8)
+    d["qual_pool"] = A["qual"] if len(A["qual"]) else np.zeros(1, np.uint8)
+    d["cig_pool"] = A["cig"] if len(A["cig"]) else np.zeros(1, np.uint32)
+    d["_seq_pool_len"] = np.array([len(A["seq"])], np.int64)
+    d["_cig_pool_len"] = np.array([len(A["cig"])], np.int64)
+    return d
+
+
+def _abi_flag(name: str) -> int:
+    from . import _abi
+    return getattr(_abi, name)
+
+
 # ---------------------------------------------------------------------------
 def parse_args(argv):
     ap = argparse.ArgumentParser(prog="bam2cns", allow_abbrev=False)
@@ -366,6 +448,18 @@ def execute(jobs: Sequence[Job]) -> None:
         groups.setdefault((j.aln_path, j.aln_fmt, dataclasses.astuple(j.params)), []).append(j)
     for (path, fmt, _), js in groups.items():
         reads = [r for j in js for r in j.reads]
+        if fmt == "bam" and reads and not os.environ.get("PRGPU_BAM2CNS_PYREADER"):
+            # one native pass over the BAM (inflate + decode in libprgpu), columns into pr_cns_batch
+            try:
+                names, cols = bam_alns_native(path)
+            except (OSError, ValueError, RuntimeError) as e:
+                die(f"{path}: {e}")
+            res = cns.run_packed(reads, pack_bam_chunk(reads, names, cols), js[0].params)
+            k = 0
+            for j in js:
+                write_outputs(j, res[k:k + len(j.reads)])
+                k += len(j.reads)
+            continue
         want: Dict[str, int] = {}
         for i, r in enumerate(reads):
             want.setdefault(r.id, i)

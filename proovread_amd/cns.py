@@ -169,6 +169,13 @@ class SamRecord:
 
 def pack_chunk(reads: Sequence[LongRead], alns: Sequence[Sequence[SamRecord]]) -> Dict[str, np.ndarray]:
     """Flatten a chunk into the SoA arrays of pr_cns_batch."""
+    d = pack_reads(reads)
+    d.update(pack_alns(alns))
+    return d
+
+
+def pack_reads(reads: Sequence[LongRead]) -> Dict[str, np.ndarray]:
+    """The long-read part of pr_cns_batch: lengths, reference seq / qual, MCR ranges."""
     n = len(reads)
     lens = np.array([r.len for r in reads], dtype=np.int64)
     lr_off = np.zeros(n + 1, np.int64)
@@ -190,6 +197,13 @@ def pack_chunk(reads: Sequence[LongRead], alns: Sequence[Sequence[SamRecord]]) -
         np.cumsum([len(x) for x in ign], out=ig_off[1:])
         d["ign_off"] = ig_off
         d["ign"] = np.array([v for x in ign for rg in x for v in rg] or [0], np.int32)
+    return d
+
+
+def pack_alns(alns: Sequence[Sequence[SamRecord]]) -> Dict[str, np.ndarray]:
+    """The alignment part of pr_cns_batch: every read's SAM records in BAM order."""
+    d: Dict[str, np.ndarray] = {}
+    n = len(alns)
     counts = [len(a) for a in alns]
     aln_off = np.zeros(n + 1, np.int64)
     np.cumsum(counts, out=aln_off[1:])
@@ -335,8 +349,13 @@ class OutBuffers:
 def run_chunk(reads: Sequence[LongRead], alns: Sequence[Sequence[SamRecord]], params: CnsParams,
               ctx: Optional[_abi.Context] = None, raise_on_error: bool = False) -> List[ReadResult]:
     """One bam2cns chunk on the GPU (bin/bam2cns:332-365 for every read)."""
+    return run_packed(reads, pack_chunk(reads, alns), params, ctx, raise_on_error)
+
+
+def run_packed(reads: Sequence[LongRead], d: Dict[str, np.ndarray], params: CnsParams,
+               ctx: Optional[_abi.Context] = None, raise_on_error: bool = False) -> List[ReadResult]:
+    """run_chunk on an already packed batch (pack_reads + the alignment columns)."""
     ctx = ctx or _abi.default_context()
-    d = pack_chunk(reads, alns)
     cb = make_c_batch(d)
     ob = OutBuffers(d, cb, params.bin_size)
     pc = params.to_c()

@@ -442,4 +442,192 @@ extern "C" int pr_bam_sort_records(const uint8_t *recs, int64_t len, int n_threa
     return 0;
 }
 
+// Perl's numification of an AS:Z string as proovread_amd/cns.py:parse_perl_number reads
+// it: optional spaces, then [+-]?(digits[.digits][e[+-]digits] | .digits[e[+-]digits]), else 0
+static double perl_number(const char *s, const char *e) {
+    const char *p = s;
+    while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r' || *p == '\f' || *p == '\v')) ++p;
+    const char *b = p;
+    if (p < e && (*p == '+' || *p == '-')) ++p;
+    const char *d0 = p;
+    while (p < e && *p >= '0' && *p <= '9') ++p;
+    bool ok = p > d0;
+    if (ok) {
+        if (p < e && *p == '.') {
+            ++p;
+            while (p < e && *p >= '0' && *p <= '9') ++p;
+        }
+    } else if (p + 1 < e && *p == '.' && p[1] >= '0' && p[1] <= '9') {
+        ++p;
+        while (p < e && *p >= '0' && *p <= '9') ++p;
+        ok = true;
+    }
+    if (!ok) return 0.0;
+    if (p < e && (*p == 'e' || *p == 'E')) {
+        const char *q = p + 1;
+        if (q < e && (*q == '+' || *q == '-')) ++q;
+        const char *q0 = q;
+        while (q < e && *q >= '0' && *q <= '9') ++q;
+        if (q > q0) p = q;
+    }
+    return std::strtod(std::string(b, p).c_str(), nullptr);
+}
+
+// BAM record stream -> the per-alignment arrays of the consensus stage (bam2cns's BAM
+// reader, proovread_amd/bam2cns.py:bam_records + cns.py:pack_chunk): POS, AS, flags, SEQ as
+// printed ("=ACMGRSVTWYHKDBN"), QUAL as phred+33 ('!' for a missing one), CIGAR ops.
+// Records are walked once for their sizes, then decoded in parallel into the pools.
+extern "C" int pr_bam_decode_alns(const uint8_t *recs, int64_t len, int n_threads, pr_bam_alns *out) {
+    if (!out || (len && !recs)) return pr_set_error(PR_ERR_ARG, "null arg");
+    std::memset(out, 0, sizeof *out);
+    std::vector<int64_t> off;
+    std::vector<int64_t> so(1, 0), co(1, 0);
+    for (int64_t o = 0; o < len;) {
+        if (len - o < 4) return pr_set_error(PR_ERR_ARG, "truncated BAM record");
+        int32_t bs, l_seq;
+        std::memcpy(&bs, recs + o, 4);
+        if (bs < 32 || o + 4 + bs > len) return pr_set_error(PR_ERR_ARG, "bad BAM record size");
+        const uint8_t *r = recs + o + 4;
+        uint16_t n_cig;
+        std::memcpy(&n_cig, r + 12, 2);
+        std::memcpy(&l_seq, r + 16, 4);
+        const int64_t need = 32 + (int64_t)r[8] + 4 * (int64_t)n_cig + (l_seq + 1) / 2 + l_seq;
+        if (l_seq < 0 || need > bs) return pr_set_error(PR_ERR_ARG, "BAM record fields exceed its size");
+        off.push_back(o);
+        so.push_back(so.back() + l_seq);
+        co.push_back(co.back() + n_cig);
+        o += 4 + (int64_t)bs;
+    }
+    const int64_t n = (int64_t)off.size();
+    auto alloc = [](size_t b) { return std::malloc(b ? b : 1); };
+    out->n = n;
+    out->rid = (int32_t *)alloc(4 * (size_t)n);
+    out->pos1 = (int32_t *)alloc(4 * (size_t)n);
+    out->score = (double *)alloc(8 * (size_t)n);
+    out->flags = (uint8_t *)alloc((size_t)n);
+    out->seq_off = (int64_t *)alloc(8 * (size_t)n);
+    out->lseq = (int32_t *)alloc(4 * (size_t)n);
+    out->cig_off = (int64_t *)alloc(8 * (size_t)n);
+    out->ncig = (int32_t *)alloc(4 * (size_t)n);
+    out->seq = (uint8_t *)alloc((size_t)so.back());
+    out->qual = (uint8_t *)alloc((size_t)so.back());
+    out->cig = (uint32_t *)alloc(4 * (size_t)co.back());
+    out->seq_len = so.back();
+    out->cig_len = co.back();
+    if (!out->rid || !out->pos1 || !out->score || !out->flags || !out->seq_off || !out->lseq || !out->cig_off ||
+        !out->ncig || !out->seq || !out->qual || !out->cig) {
+        pr_bam_alns_free(out);
+        return pr_set_error(PR_ERR_ARG, "out of host memory");
+    }
+    static const char NT16[] = "=ACMGRSVTWYHKDBN";
+    std::vector<int> bad((size_t)(n ? n : 1), 0);
+    auto work = [&](int64_t i0, int64_t i1) {
+        for (int64_t i = i0; i < i1; ++i) {
+            const uint8_t *r = recs + off[(size_t)i] + 4;
+            int32_t bs, rid, pos, l_seq;
+            uint16_t n_cig;
+            std::memcpy(&bs, recs + off[(size_t)i], 4);
+            std::memcpy(&rid, r, 4);
+            std::memcpy(&pos, r + 4, 4);
+            std::memcpy(&n_cig, r + 12, 2);
+            std::memcpy(&l_seq, r + 16, 4);
+            const uint8_t *end = r + bs;
+            const uint8_t *c = r + 32 + r[8];
+            out->rid[i] = rid;
+            out->pos1[i] = pos + 1;
+            out->seq_off[i] = so[(size_t)i];
+            out->lseq[i] = l_seq;
+            out->cig_off[i] = co[(size_t)i];
+            out->ncig[i] = n_cig;
+            std::memcpy(out->cig + co[(size_t)i], c, 4 * (size_t)n_cig);
+            const uint8_t *sb = c + 4 * n_cig;
+            uint8_t *sd = out->seq + so[(size_t)i];
+            for (int32_t k = 0; k < l_seq; ++k) sd[k] = (uint8_t)NT16[(sb[k >> 1] >> (4 * (1 - (k & 1)))) & 15];
+            const uint8_t *qb = sb + (l_seq + 1) / 2;
+            uint8_t *qd = out->qual + so[(size_t)i];
+            uint8_t fl = l_seq == 0 ? PR_ALN_NO_SEQ : 0;
+            if (l_seq && qb[0] == 0xFF) {
+                fl |= PR_ALN_NO_QUAL;
+                std::memset(qd, '!', (size_t)l_seq);
+            } else {
+                for (int32_t k = 0; k < l_seq; ++k) qd[k] = (uint8_t)(qb[k] + 33);
+            }
+            double score = 0.0;
+            const uint8_t *a = qb + l_seq;
+            while (a < end) {   // aux fields: the last AS tag wins
+                if (end - a < 3) { bad[(size_t)i] = 1; break; }
+                const bool as = a[0] == 'A' && a[1] == 'S';
+                const char t = (char)a[2];
+                a += 3;
+                int64_t v = 0;
+                int sz = 0;
+                switch (t) {
+                    case 'c': sz = 1; v = (int8_t)a[0]; break;
+                    case 'C': sz = 1; v = a[0]; break;
+                    case 's': { sz = 2; int16_t x; std::memcpy(&x, a, 2); v = x; break; }
+                    case 'S': { sz = 2; uint16_t x; std::memcpy(&x, a, 2); v = x; break; }
+                    case 'i': { sz = 4; int32_t x; std::memcpy(&x, a, 4); v = x; break; }
+                    case 'I': { sz = 4; uint32_t x; std::memcpy(&x, a, 4); v = x; break; }
+                    default: break;
+                }
+                if (sz) {
+                    if (a + sz > end) { bad[(size_t)i] = 1; break; }
+                    if (as) { score = (double)v; fl |= PR_ALN_HAS_SCORE; }
+                    a += sz;
+                } else if (t == 'A' || t == 'f') {
+                    const int w = t == 'A' ? 1 : 4;
+                    if (a + w > end) { bad[(size_t)i] = 1; break; }
+                    if (as && t == 'f') {
+                        float f;
+                        std::memcpy(&f, a, 4);
+                        score = (double)f;
+                        fl |= PR_ALN_HAS_SCORE;
+                    }
+                    a += w;
+                } else if (t == 'Z' || t == 'H') {
+                    const uint8_t *z = a;
+                    while (z < end && *z) ++z;
+                    if (z >= end) { bad[(size_t)i] = 1; break; }
+                    if (as) { score = perl_number((const char *)a, (const char *)z); fl |= PR_ALN_HAS_SCORE; }
+                    a = z + 1;
+                } else if (t == 'B') {
+                    if (end - a < 5) { bad[(size_t)i] = 1; break; }
+                    const char st = (char)a[0];
+                    int32_t cnt;
+                    std::memcpy(&cnt, a + 1, 4);
+                    const int es = (st == 'c' || st == 'C') ? 1 : (st == 's' || st == 'S') ? 2 :
+                                   (st == 'i' || st == 'I' || st == 'f') ? 4 : 0;
+                    if (!es || cnt < 0 || a + 5 + (int64_t)cnt * es > end) { bad[(size_t)i] = 1; break; }
+                    a += 5 + (int64_t)cnt * es;
+                } else {
+                    bad[(size_t)i] = 1;
+                    break;
+                }
+            }
+            out->score[i] = score;
+            out->flags[i] = fl;
+        }
+    };
+    int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
+    nt = std::max(1, std::min(nt, 64));
+    if (n < 4096) nt = 1;
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(work, n * t / nt, n * (t + 1) / nt);
+    work(0, n / nt);
+    for (auto &x : th) x.join();
+    for (int64_t i = 0; i < n; ++i)
+        if (bad[(size_t)i]) {
+            pr_bam_alns_free(out);
+            return pr_set_error(PR_ERR_SAM, "bad BAM aux field");
+        }
+    return 0;
+}
+
+extern "C" void pr_bam_alns_free(pr_bam_alns *a) {
+    if (!a) return;
+    void *p[] = {a->rid, a->pos1, a->score, a->flags, a->seq_off, a->lseq, a->cig_off, a->ncig, a->seq, a->qual, a->cig};
+    for (void *x : p) std::free(x);
+    std::memset(a, 0, sizeof *a);
+}
+
 extern "C" void pr_buffer_free(void *p) { std::free(p); }

@@ -129,3 +129,33 @@ def test_cli_matches_reference_golden(tmp_path, fmt):
     assert Path(pre + ".ignored.tsv").read_text() == ""
     trace = Path(pre + ".debug.trace").read_text().split("\n")
     assert trace[4] == EXPECT[order(cases[:half])[0].name].trace
+
+
+def test_native_bam_columns_equal_python_reader(tmp_path):
+    """bam2cns's native BAM path (pr_bgzf_decompress + pr_bam_decode_alns + pack_bam_chunk)
+    hands pr_cns_run the same alignments, field for field, as the Python reader + pack_chunk
+    (POS, AS, flags, SEQ, QUAL, CIGAR per read in file order), including a repeated read id."""
+    import numpy as np
+    from proovread_amd import cns
+    p, cases = _golden_group()
+    cases = [c for c in cases if not any(ch.islower() for l in c.sam for ch in l.split("\t")[9])]
+    _write_inputs(tmp_path, cases)
+    names, cols = bam2cns.bam_alns_native(str(tmp_path / "x.bam"))
+    _, recs = bam2cns.bam_records(str(tmp_path / "x.bam"))
+    recs = list(recs)
+    ids = [c.ref_id for c in cases] + [cases[0].ref_id]
+    lrs = [cns.LongRead(i, None, None, "", 100000) for i in ids]
+    d = bam2cns.pack_bam_chunk(lrs, names, cols)
+    want = cns.pack_chunk(lrs, [[r for r in recs if r.rname == i] for i in ids])
+
+    def per_aln(d):
+        out = []
+        for k in range(int(d["aln_off"][-1])):
+            so, ls = int(d["aln_seq_off"][k]), int(d["aln_lseq"][k])
+            co, nc = int(d["aln_cig_off"][k]), int(d["aln_ncig"][k])
+            out.append((int(d["aln_pos"][k]), float(d["aln_score"][k]), int(d["aln_flags"][k]),
+                        d["seq_pool"][so:so + ls].tobytes(), d["qual_pool"][so:so + ls].tobytes(),
+                        d["cig_pool"][co:co + nc].tolist()))
+        return out
+    assert np.array_equal(d["aln_off"], want["aln_off"]) and int(d["aln_off"][-1]) > 100
+    assert per_aln(d) == per_aln(want)
