@@ -401,6 +401,10 @@ typedef struct pr_bam_alns {
 } pr_bam_alns;
 int pr_bam_decode_alns(const uint8_t *recs, int64_t len, int n_threads, pr_bam_alns *out);
 void pr_bam_alns_free(pr_bam_alns *a);
+/* `samtools index` (bin/proovread:1343-1355): the BAI bytes of a coordinate-sorted BAM file
+ * (bins + chunks, pseudo-bin 37450, 16 kb linear index, no-coordinate count);
+ * PR_ERR_ARG if the file is not coordinate-sorted.                                     */
+int pr_bam_index(const uint8_t *data, int64_t len, int n_threads, uint8_t **out, int64_t *out_len);
 void pr_buffer_free(void *p);
 
 #ifdef __cplusplus

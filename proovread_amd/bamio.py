@@ -400,6 +400,7 @@ def _codec():
                                          C.POINTER(C.c_int64)]
         L.pr_bam_sort_records.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.POINTER(C.c_void_p),
                                           C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.pr_bam_index.argtypes = [C.c_char_p, C.c_int64, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_int64)]
         L.pr_buffer_free.argtypes = [C.c_void_p]
         L.pr_buffer_free.restype = None
         L._bam_ready = True
@@ -522,8 +523,23 @@ def merge_bams(out_path: str, in_paths: Sequence[str]):
         r.close()
 
 
-def index_bam(path: str, out_path: Optional[str] = None):
-    """`samtools index`: BAI (bins with chunks, 16 kb linear index, pseudo-bin 37450 with counts)."""
+def index_bam(path: str, out_path: Optional[str] = None, native: bool = True, threads: int = 0):
+    """`samtools index`: BAI (bins with chunks, 16 kb linear index, pseudo-bin 37450 with counts).
+
+    native: built by libprgpu (pr_bam_index: parallel inflate, one pass over the records);
+    byte-identical to the pure-Python path (native=False)."""
+    if native:
+        L, C, _abi = _codec()
+        with open(path, "rb") as fh:
+            data = fh.read()
+        p, n = C.c_void_p(), C.c_int64()
+        rc = L.pr_bam_index(data, len(data), threads, C.byref(p), C.byref(n))
+        if rc != 0:
+            raise ValueError(f"{path}: {_abi.lib().pr_last_error().decode()}")
+        bai = _take(L, C, p, n)
+        with open(out_path or path + ".bai", "wb") as fh:
+            fh.write(bai)
+        return
     rd = BamReader(path)
     n_ref = len(rd.header.refs)
     bins: List[Dict[int, List[List[int]]]] = [dict() for _ in range(n_ref)]

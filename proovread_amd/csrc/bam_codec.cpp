@@ -9,6 +9,8 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <map>
+#include <memory>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -628,6 +630,156 @@ extern "C" void pr_bam_alns_free(pr_bam_alns *a) {
     void *p[] = {a->rid, a->pos1, a->score, a->flags, a->seq_off, a->lseq, a->cig_off, a->ncig, a->seq, a->qual, a->cig};
     for (void *x : p) std::free(x);
     std::memset(a, 0, sizeof *a);
+}
+
+// `samtools index` (bin/proovread:1343-1355) of a coordinate-sorted BAM file: the BAI of
+// proovread_amd/bamio.py:index_bam — per reference the bins with their chunks (virtual
+// offsets, adjacent chunks of one bin merged), the pseudo-bin 37450 (first/last offset,
+// mapped/unmapped counts), the 16 kb linear index (empty windows take the previous one), and
+// the count of records without coordinates.  Virtual offsets follow the BGZF reader: a
+// position at the end of a block is the start of the next block.
+extern "C" int pr_bam_index(const uint8_t *data, int64_t len, int n_threads, uint8_t **out, int64_t *out_len) {
+    if (!out || !out_len || (len && !data)) return pr_set_error(PR_ERR_ARG, "null arg");
+    // block table (compressed offset, uncompressed start) of the file
+    std::vector<int64_t> coff, ustart;
+    int64_t tot = 0;
+    for (int64_t o = 0; o < len;) {
+        if (len - o < 18 || data[o] != 31 || data[o + 1] != 139) return pr_set_error(PR_ERR_ARG, "not a BGZF block");
+        const int xlen = data[o + 10] | (data[o + 11] << 8);
+        int bsize = -1;
+        for (int e = 0; e + 4 <= xlen && o + 12 + e + 4 <= len;) {
+            const uint8_t *x = data + o + 12 + e;
+            const int sl = x[2] | (x[3] << 8);
+            if (x[0] == 66 && x[1] == 67 && sl == 2) bsize = x[4] | (x[5] << 8);
+            e += 4 + sl;
+        }
+        if (bsize < 0 || o + bsize + 1 > len) return pr_set_error(PR_ERR_ARG, "bad BGZF block");
+        const uint8_t *t = data + o + bsize + 1 - 4;
+        coff.push_back(o);
+        ustart.push_back(tot);
+        tot += (int64_t)((uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24));
+        o += bsize + 1;
+    }
+    coff.push_back(len);
+    ustart.push_back(tot);
+    uint8_t *u = nullptr;
+    int64_t ulen = 0;
+    int rc = pr_bgzf_decompress(data, len, n_threads, &u, &ulen);
+    if (rc) return rc;
+    std::unique_ptr<uint8_t, void (*)(void *)> hold(u, std::free);
+    // virtual offset of stream position p (monotone queries: block cursor)
+    const size_t nblk = coff.size() - 1;   // real blocks; coff[nblk] = file length
+    size_t cb = 0;
+    auto voff = [&](int64_t p) -> uint64_t {
+        while (cb < nblk && ustart[cb + 1] < p) ++cb;   // skip blocks that end before p
+        if (cb < nblk && ustart[cb + 1] == p && ustart[cb + 1] > ustart[cb])
+            return (uint64_t)coff[cb + 1] << 16;       // the end of a block reads as the next block's start
+        return ((uint64_t)coff[cb] << 16) | (uint64_t)(p - ustart[cb]);
+    };
+    if (ulen < 12 || std::memcmp(u, "BAM\1", 4) != 0) return pr_set_error(PR_ERR_ARG, "not a BAM file");
+    int32_t l_text, n_ref;
+    std::memcpy(&l_text, u + 4, 4);
+    int64_t p = 8 + (int64_t)l_text;
+    if (l_text < 0 || p + 4 > ulen) return pr_set_error(PR_ERR_ARG, "truncated BAM header");
+    std::memcpy(&n_ref, u + p, 4);
+    p += 4;
+    for (int32_t r = 0; r < n_ref; ++r) {
+        int32_t ln;
+        if (p + 4 > ulen) return pr_set_error(PR_ERR_ARG, "truncated BAM header");
+        std::memcpy(&ln, u + p, 4);
+        p += 8 + (int64_t)ln;
+    }
+    if (n_ref < 0 || p > ulen) return pr_set_error(PR_ERR_ARG, "truncated BAM header");
+    struct Meta {
+        bool any = false;
+        uint64_t beg = 0, end = 0, mapped = 0, unmapped = 0;
+    };
+    std::vector<std::map<uint32_t, std::vector<std::pair<uint64_t, uint64_t>>>> bins((size_t)n_ref);
+    std::vector<std::vector<uint64_t>> lin((size_t)n_ref);
+    std::vector<Meta> meta((size_t)n_ref);
+    uint64_t n_no_coor = 0;
+    int32_t last_rid = -1, last_pos = -1;
+    while (p < ulen) {
+        if (ulen - p < 4) return pr_set_error(PR_ERR_ARG, "truncated BAM record");
+        int32_t bs;
+        std::memcpy(&bs, u + p, 4);
+        if (bs < 32 || p + 4 + bs > ulen) return pr_set_error(PR_ERR_ARG, "bad BAM record size");
+        const uint64_t v = voff(p);
+        const uint8_t *r = u + p + 4;
+        p += 4 + (int64_t)bs;
+        const uint64_t ve = voff(p);
+        int32_t rid, pos;
+        uint16_t bin, n_cig, flag;
+        std::memcpy(&rid, r, 4);
+        std::memcpy(&pos, r + 4, 4);
+        std::memcpy(&bin, r + 10, 2);
+        std::memcpy(&n_cig, r + 12, 2);
+        std::memcpy(&flag, r + 14, 2);
+        if (rid < 0) {
+            ++n_no_coor;
+            continue;
+        }
+        if (rid >= n_ref) return pr_set_error(PR_ERR_ARG, "record reference id out of range");
+        if (rid < last_rid || (rid == last_rid && pos < last_pos)) return pr_set_error(PR_ERR_ARG, "not coordinate-sorted");
+        last_rid = rid;
+        last_pos = pos;
+        if (32 + (int64_t)r[8] + 4 * (int64_t)n_cig > bs) return pr_set_error(PR_ERR_ARG, "bad BAM record");
+        int64_t span = 0;
+        for (int k = 0; k < n_cig; ++k) {
+            uint32_t op;
+            std::memcpy(&op, r + 32 + r[8] + 4 * k, 4);
+            const uint32_t c = op & 15;
+            if (c == 0 || c == 2 || c == 3 || c == 7 || c == 8) span += op >> 4;
+        }
+        const int64_t end = (int64_t)pos + (span ? span : 1);
+        auto &ch = bins[(size_t)rid][bin];
+        if (!ch.empty() && ch.back().second == v) ch.back().second = ve;
+        else ch.emplace_back(v, ve);
+        auto &li = lin[(size_t)rid];
+        for (int64_t w = (int64_t)pos >> 14; w <= (end - 1) >> 14; ++w) {
+            if ((int64_t)li.size() <= w) li.resize((size_t)w + 1, 0);
+            if (li[(size_t)w] == 0) li[(size_t)w] = v;
+        }
+        Meta &m = meta[(size_t)rid];
+        if (!m.any) {
+            m.any = true;
+            m.beg = v;
+        }
+        m.end = ve;
+        if (flag & 4) ++m.unmapped;
+        else ++m.mapped;
+    }
+    std::string o("BAI\1", 4);
+    put<int32_t>(o, n_ref);
+    for (int32_t rid = 0; rid < n_ref; ++rid) {
+        const auto &b = bins[(size_t)rid];
+        const Meta &m = meta[(size_t)rid];
+        put<int32_t>(o, (int32_t)b.size() + (m.any ? 1 : 0));
+        for (const auto &kv : b) {
+            put<uint32_t>(o, kv.first);
+            put<int32_t>(o, (int32_t)kv.second.size());
+            for (const auto &c : kv.second) {
+                put<uint64_t>(o, c.first);
+                put<uint64_t>(o, c.second);
+            }
+        }
+        if (m.any) {
+            put<uint32_t>(o, 37450u);
+            put<int32_t>(o, 2);
+            put<uint64_t>(o, m.beg);
+            put<uint64_t>(o, m.end);
+            put<uint64_t>(o, m.mapped);
+            put<uint64_t>(o, m.unmapped);
+        }
+        auto li = lin[(size_t)rid];
+        for (size_t i = 1; i < li.size(); ++i)
+            if (li[i] == 0) li[i] = li[i - 1];
+        put<int32_t>(o, (int32_t)li.size());
+        for (uint64_t x : li) put<uint64_t>(o, x);
+    }
+    put<uint64_t>(o, n_no_coor);
+    *out = take(o, out_len);
+    return *out ? 0 : pr_set_error(PR_ERR_ARG, "out of host memory");
 }
 
 extern "C" void pr_buffer_free(void *p) { std::free(p); }

@@ -190,3 +190,23 @@ def test_native_sort_is_byte_identical(tmp_path, n, seed):
 def test_native_inflate_rejects_corrupt_input():
     with pytest.raises(RuntimeError, match="BGZF"):
         bamio._native_inflate(b"\x1f\x8b\x08\x00not bgzf at all")
+
+
+@pytest.mark.parametrize("n,seed", [(0, 1), (1, 2), (50000, 12)])
+def test_native_index_is_byte_identical(tmp_path, n, seed):
+    """pr_bam_index writes the BAI the pure-Python index_bam writes (bins, merged chunks,
+    pseudo-bin, linear index across BGZF block boundaries, unmapped count)."""
+    recs = _records(n, seed=seed)
+    sam = _sam_file(tmp_path, recs)
+    samtools.main(["view", "-bS", str(sam), "-o", str(tmp_path / "u.bam")])
+    bamio.sort_bam(str(tmp_path / "u.bam"), str(tmp_path / "s.bam"))
+    bamio.index_bam(str(tmp_path / "s.bam"), str(tmp_path / "n.bai"), native=True, threads=4)
+    bamio.index_bam(str(tmp_path / "s.bam"), str(tmp_path / "p.bai"), native=False)
+    assert (tmp_path / "n.bai").read_bytes() == (tmp_path / "p.bai").read_bytes()
+
+
+def test_native_index_rejects_unsorted(tmp_path):
+    sam = _sam_file(tmp_path, _records(2000, seed=4))
+    samtools.main(["view", "-bS", str(sam), "-o", str(tmp_path / "u.bam")])
+    with pytest.raises(ValueError, match="coordinate-sorted"):
+        bamio.index_bam(str(tmp_path / "u.bam"))
