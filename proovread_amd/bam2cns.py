@@ -269,7 +269,10 @@ def pack_bam_chunk(reads: Sequence[cns.LongRead], names: Sequence[str], A: Dict[
     for i, r in enumerate(reads):
         want.setdefault(r.id, i)
     lut = np.array([want.get(nm, -1) for nm in names] + [-1], np.int64)
-    ridx = lut[A["rid"]] if len(A["rid"]) else np.zeros(0, np.int64)   # rid -1 -> lut[-1] = -1
+    rid = A["rid"]
+    if len(rid) and (rid.min() < -1 or rid.max() >= len(names)):
+        die(f"BAM record with reference id outside [-1, {len(names)})")
+    ridx = lut[rid] if len(rid) else np.zeros(0, np.int64)   # rid -1 -> lut[-1] = -1
     sel = np.nonzero(ridx >= 0)[0]
     if (A["flags"][sel] & _abi_flag("PR_ALN_NO_SEQ")).any():
         die("Cannot handle BAM secondary alignments without seq/qual")

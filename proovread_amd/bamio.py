@@ -558,13 +558,14 @@ def index_bam(path: str, out_path: Optional[str] = None, native: bool = True, th
         last = (rid, pos)
         l_rn = r[8]
         ops = struct.unpack(f"<{n_cig}I", r[32 + l_rn:32 + l_rn + 4 * n_cig])
-        end = pos + (ref_span(ops) or 1)
+        beg = max(pos, 0)   # hts_idx_push: a placed record without a position indexes at 0
+        end = max(pos + (ref_span(ops) or 1), beg + 1)
         ch = bins[rid].setdefault(bin_, [])
         if ch and ch[-1][1] == v:
             ch[-1][1] = ve
         else:
             ch.append([v, ve])
-        for wdw in range(pos >> 14, ((end - 1) >> 14) + 1):
+        for wdw in range(beg >> 14, ((end - 1) >> 14) + 1):
             while len(lin[rid]) <= wdw:
                 lin[rid].append(0)
             if lin[rid][wdw] == 0:

@@ -562,18 +562,18 @@ extern "C" int pr_bam_decode_alns(const uint8_t *recs, int64_t len, int n_thread
                 const char t = (char)a[2];
                 a += 3;
                 int64_t v = 0;
-                int sz = 0;
+                const int sz = (t == 'c' || t == 'C') ? 1 : (t == 's' || t == 'S') ? 2 : (t == 'i' || t == 'I') ? 4 : 0;
+                if (sz && a + sz > end) { bad[(size_t)i] = 1; break; }   // check before reading the value
                 switch (t) {
-                    case 'c': sz = 1; v = (int8_t)a[0]; break;
-                    case 'C': sz = 1; v = a[0]; break;
-                    case 's': { sz = 2; int16_t x; std::memcpy(&x, a, 2); v = x; break; }
-                    case 'S': { sz = 2; uint16_t x; std::memcpy(&x, a, 2); v = x; break; }
-                    case 'i': { sz = 4; int32_t x; std::memcpy(&x, a, 4); v = x; break; }
-                    case 'I': { sz = 4; uint32_t x; std::memcpy(&x, a, 4); v = x; break; }
+                    case 'c': v = (int8_t)a[0]; break;
+                    case 'C': v = a[0]; break;
+                    case 's': { int16_t x; std::memcpy(&x, a, 2); v = x; break; }
+                    case 'S': { uint16_t x; std::memcpy(&x, a, 2); v = x; break; }
+                    case 'i': { int32_t x; std::memcpy(&x, a, 4); v = x; break; }
+                    case 'I': { uint32_t x; std::memcpy(&x, a, 4); v = x; break; }
                     default: break;
                 }
                 if (sz) {
-                    if (a + sz > end) { bad[(size_t)i] = 1; break; }
                     if (as) { score = (double)v; fl |= PR_ALN_HAS_SCORE; }
                     a += sz;
                 } else if (t == 'A' || t == 'f') {
@@ -653,7 +653,8 @@ extern "C" int pr_bam_index(const uint8_t *data, int64_t len, int n_threads, uin
             if (x[0] == 66 && x[1] == 67 && sl == 2) bsize = x[4] | (x[5] << 8);
             e += 4 + sl;
         }
-        if (bsize < 0 || o + bsize + 1 > len) return pr_set_error(PR_ERR_ARG, "bad BGZF block");
+        // header (12 + xlen) + the CRC32 / ISIZE trailer (8) must fit in the block
+        if (bsize < 0 || bsize + 1 < 12 + xlen + 8 || o + bsize + 1 > len) return pr_set_error(PR_ERR_ARG, "bad BGZF block");
         const uint8_t *t = data + o + bsize + 1 - 4;
         coff.push_back(o);
         ustart.push_back(tot);
@@ -731,12 +732,16 @@ extern "C" int pr_bam_index(const uint8_t *data, int64_t len, int n_threads, uin
             const uint32_t c = op & 15;
             if (c == 0 || c == 2 || c == 3 || c == 7 || c == 8) span += op >> 4;
         }
-        const int64_t end = (int64_t)pos + (span ? span : 1);
+        // hts_idx_push: a placed record without a position (POS 0 in SAM, pos -1 here) indexes
+        // at 0; its end is at least one past its start
+        const int64_t beg = pos < 0 ? 0 : (int64_t)pos;
+        int64_t end = (int64_t)pos + (span ? span : 1);
+        if (end < beg + 1) end = beg + 1;
         auto &ch = bins[(size_t)rid][bin];
         if (!ch.empty() && ch.back().second == v) ch.back().second = ve;
         else ch.emplace_back(v, ve);
         auto &li = lin[(size_t)rid];
-        for (int64_t w = (int64_t)pos >> 14; w <= (end - 1) >> 14; ++w) {
+        for (int64_t w = beg >> 14; w <= (end - 1) >> 14; ++w) {
             if ((int64_t)li.size() <= w) li.resize((size_t)w + 1, 0);
             if (li[(size_t)w] == 0) li[(size_t)w] = v;
         }

@@ -210,3 +210,18 @@ def test_native_index_rejects_unsorted(tmp_path):
     samtools.main(["view", "-bS", str(sam), "-o", str(tmp_path / "u.bam")])
     with pytest.raises(ValueError, match="coordinate-sorted"):
         bamio.index_bam(str(tmp_path / "u.bam"))
+
+
+def test_native_index_placed_record_without_position(tmp_path):
+    """A placed record with POS 0 (BAM pos -1: RNAME set, unmapped mate-style placement) is
+    indexed at 0 as hts_idx_push does (beg clamped to 0, end >= beg + 1); native and Python
+    indexes agree and stay readable."""
+    recs = [f"p{i}\t4\tlr0\t0\t0\t*\t*\t0\t0\tACGTA\t*" for i in range(3)] + _records(300, seed=21)
+    sam = _sam_file(tmp_path, recs)
+    samtools.main(["view", "-bS", str(sam), "-o", str(tmp_path / "u.bam")])
+    bamio.sort_bam(str(tmp_path / "u.bam"), str(tmp_path / "s.bam"))
+    bamio.index_bam(str(tmp_path / "s.bam"), str(tmp_path / "n.bai"), native=True, threads=2)
+    bamio.index_bam(str(tmp_path / "s.bam"), str(tmp_path / "p.bai"), native=False)
+    assert (tmp_path / "n.bai").read_bytes() == (tmp_path / "p.bai").read_bytes()
+    bins, lin = bamio.read_bai(str(tmp_path / "n.bai"))[0]
+    assert lin and lin[0] > 0
