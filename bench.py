@@ -8,8 +8,11 @@ a synthetic workload of BASELINE.json configs[1] size per GPU.
 
 A step = one iteration over the rank's whole batch (every long read of the
 shard, every seed-extension task): SW extension kernel, SW global/CIGAR
-kernel, per-read coordinate sort, consensus kernel, and the per-iteration
-statistic all-reduced across GPUs (RCCL) as proovread's masked-fraction input.
+kernel, per-read coordinate sort, consensus kernel, the masking of the
+corrected reads (SeqFilter --phred-mask) with its {bpt, bpN} statistic
+all-reduced across GPUs (RCCL inside libprgpu) as proovread's
+mask_shortcut_frac input.  No torch in the process: libprgpu owns the HIP
+runtime, the device buffers and the collectives.
 Inputs are resident in HBM before the timed region.  Long reads shard across
 GPUs with no data-path collective (weak scaling: every rank holds a
 configs[1]-size shard; 8 ranks ~ configs[2]).
@@ -51,6 +54,46 @@ def parse():
                     help="task list: the product's seeding front end (host path / GPU path; bwa mem seeding "
                          "+ chaining restated), or the simulation truth; computed before the timed region")
     return ap.parse_args()
+
+
+def cpu_baseline(d, per_worker: int):
+    """The oracle chain (oracle/cpu_bench.py) on the first per_worker x workers long reads, in
+    a child process; -> (cpu_baseline JSON object, per-read oracle outputs)."""
+    import subprocess
+    import tempfile
+    workers = min(16, os.cpu_count() or 1)
+    n_s = min(d.n_lr, per_worker * workers)
+    with tempfile.TemporaryDirectory(prefix="prgpu_bench_") as td:
+        npz, out = os.path.join(td, "w.npz"), os.path.join(td, "o.json")
+        k = int(np.searchsorted(d.t_lr, n_s, side="left"))   # tasks are grouped by long read
+        np.savez(npz, lr_seq=d.lr_seq[:int(d.lr_off[n_s])], lr_off=d.lr_off[:n_s + 1], sr_seq=d.sr_seq,
+                 sr_off=d.sr_off, t_sr=d.t_sr[:k], t_lr=d.t_lr[:k], t_strand=d.t_strand[:k], t_qbeg=d.t_qbeg[:k],
+                 t_rbeg=d.t_rbeg[:k], t_slen=d.t_slen[:k])
+        subprocess.run([sys.executable, str(ROOT / "oracle" / "cpu_bench.py"), npz, str(n_s), str(workers), out],
+                       check=True)
+        r = json.loads(Path(out).read_text())
+    cpu = {"value": round(r["bases"] / r["wall_s"] / 1e6, 4), "unit": "Mbases/s", "cores": r["workers"], "kind": "port",
+           "sample": f"first {r['n']} of {d.n_lr} long reads of the same workload ({r['bases']} bases, their "
+                     f"{r['tasks']} seed-extension tasks), SW + consensus C restatement (oracle/), "
+                     f"{r['workers']} processes, {r['wall_s']:.1f} s"}
+    return cpu, r["results"]
+
+
+def check_parity(it, cpu_res):
+    """The GPU iteration's corrected reads vs the CPU chain's on the baseline sample, byte for
+    byte: FASTQ (sequence + qualities), trace and chimera lines."""
+    got = it.results()
+    bad = []
+    for i, w in enumerate(cpu_res):
+        g = got[i]
+        rc, fq, tr, ch = w
+        ok = rc == 0 and g.status == 0 and g.fastq == fq and g.trace == tr and \
+            "".join(l + "\n" for l in g.chim_lines()) == ch
+        if not ok:
+            bad.append(i)
+    return {"checked_reads": len(cpu_res), "mismatches": len(bad), "first_mismatch": bad[:5],
+            "against": "oracle chain (SW restatement -> coordinate order -> consensus restatement pinned to the "
+                       "reference Perl engine), same tasks"}
 
 
 def main():
@@ -95,52 +138,44 @@ def main():
                 "reads_per_s": round(d.n_sr / t_map, 1), "kernel_ms": ms, "tasks": int(len(tasks))}
         return synth.with_seeded_tasks(d, tasks), info
 
-    if args.seeds == "host":   # before the CPU baseline, which then runs on the same tasks
+    if args.seeds == "host":
         d, seed_info = seed_front_end()
 
-    # CPU baseline (rank 0, N=1): the oracle chain on a bounded sample of the same
-    # workload, before this process touches the GPU (the pool forks).
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, str(ROOT / "oracle"))
-        import cpu_chain
-        workers = min(16, os.cpu_count() or 1)
-        n_s = min(d.n_lr, args.cpu_lrs_per_worker * workers)
-        wall, bases, res, nw = cpu_chain.run_sample(d, range(n_s), workers=workers)
-        cpu = {"value": round(bases / wall / 1e6, 4), "unit": "Mbases/s", "cores": nw, "kind": "port",
-               "sample": f"first {n_s} of {d.n_lr} long reads of the same workload ({bases} bases, their "
-                         f"{int(d._task_off[n_s])} seed-extension tasks), SW + consensus C restatement, "
-                         f"{nw} processes, {wall:.1f} s"}
+    # CPU baseline (rank 0, N=1): the oracle chain on a bounded sample of the same workload,
+    # in a child process (its fork pool never shares a process with a HIP runtime).  Its
+    # per-read outputs are also the parity check of the GPU run below.
+    cpu, cpu_res = None, None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.seeds != "gpu":
+        cpu, cpu_res = cpu_baseline(d, args.cpu_lrs_per_worker)
 
-    import torch
-    import torch.distributed as dist
-    from proovread_amd import _abi, cns, iteration, sw
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    dev = torch.device(f"cuda:{local}")
+    # GPU: libprgpu only (its own HIP runtime and RCCL); torch is never loaded here
+    from proovread_amd import _abi, cns, comm as comm_mod, iteration, sw
     ctx = _abi.Context(local)
-    if args.seeds == "gpu":   # after the CPU baseline (its worker pool forks before any GPU use)
+    cm = comm_mod.RcclComm.from_env(ctx) if world > 1 else None
+    if args.seeds == "gpu":
         d, seed_info = seed_front_end(ctx)
-        if cpu is not None:
-            cpu["sample"] += " (simulation-truth tasks)"
     it = iteration.Iteration(d, ctx=ctx)
     opts = sw.default_opts(finish=False)
     params = cns.CnsParams(coverage=min(50.0, 15.0) * 0.75, use_ref_qual=True)   # proovread:1540-1541
-    stats = torch.zeros(2, dtype=torch.int64, device=dev)
+    from proovread_amd import mask
+    mparams = mask.params("20,41,80,130,60,0.7", 150)   # hcr-mask of bwa-sr-1 (proovread.cfg:234-242)
+    stats = _abi.DevBuffer(ctx, 16)
 
     def step():
         it.launch(opts, params)
-        it.stats_to(stats.data_ptr())
+        it.mask_to(stats.ptr, mparams)   # SeqFilter --phred-mask: next reference + {bpt, bpN}
+        if cm is not None:
+            cm.allreduce_dev(stats.ptr, 2)   # RCCL: global bpt / bpN (mask_shortcut_frac input)
         it.sync()
-        if world > 1:
-            dist.all_reduce(stats)   # RCCL: global corrected / high-quality bases
+
+    def barrier():
+        if cm is not None:
+            cm.barrier()
+        it.sync()
 
     for _ in range(args.warmup):
         step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    barrier()
     t0 = time.perf_counter()
     ms = np.zeros(4)
     dom_ms, dom_cells = 0.0, 0
@@ -150,17 +185,11 @@ def main():
         dm, dc = sw.dominant_kernel(ctx)
         dom_ms += dm
         dom_cells = dc
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    barrier()
     el = time.perf_counter() - t0
-    if world > 1:
-        te = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(te, op=dist.ReduceOp.MAX)
-        el = float(te.item())
-        tb = torch.tensor([lr_bases], dtype=torch.int64, device=dev)
-        dist.all_reduce(tb)
-        total_bases = int(tb.item())
+    if cm is not None:
+        el = cm.allreduce_floats([el], comm_mod.RED_MAX)[0]
+        total_bases = cm.allreduce_ints([lr_bases])[0]
     else:
         total_bases = lr_bases
     ms /= max(args.steps, 1)
@@ -169,10 +198,11 @@ def main():
     a = it.download()
     cns_phases = it.cns_phase_ms()
     ok = int((a["status"] == 0).sum())
-    hq = stats.cpu().tolist()
+    bpt, bpn = (int(x) for x in stats.download(np.int64))
+    parity = check_parity(it, cpu_res) if cpu_res is not None else None
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
+        if cm is not None:
+            cm.close()
         return
     value = total_bases * args.steps / el / 1e6
     cells = ce + cg
@@ -239,11 +269,14 @@ def main():
         "seeding": seed_info,
         "gen_s": round(gen_s, 1),
         "reads_ok": ok,
-        "iteration_stat": {"corrected_bases": hq[0], "phred_ge20_bases": hq[1]},
+        "iteration_stat": {"bpt": bpt, "bpN": bpn, "masked_frac": round(bpn / bpt, 4) if bpt else None},
+        "parity": parity,
     }
     print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+    if cm is not None:
+        cm.close()
+    if parity is not None and parity["mismatches"]:
+        raise SystemExit(f"bench: {parity['mismatches']} of {parity['checked_reads']} reads differ from the CPU chain")
 
 
 if __name__ == "__main__":

@@ -59,6 +59,42 @@ void pr_ctx_destroy(pr_ctx *ctx);
 int pr_device_count(int *n);
 /* wait for everything enqueued on the context's stream */
 int pr_ctx_sync(pr_ctx *ctx);
+/* device memory of the context (plumbing for drivers: e.g. the int64[2] statistic that
+ * pr_iter_stats / pr_iter_mask fill and pr_comm_allreduce_dev reduces across GPUs) */
+int pr_dev_alloc(pr_ctx *ctx, int64_t bytes, void **dev);
+int pr_dev_free(pr_ctx *ctx, void *dev);
+/* copies on the context stream; both synchronise */
+int pr_dev_download(pr_ctx *ctx, void *host, const void *dev, int64_t bytes);
+int pr_dev_upload(pr_ctx *ctx, void *dev, const void *host, int64_t bytes);
+
+/* ------------------------------------------------------------------ */
+/* multi-GPU collectives over RCCL (one process per GPU, xGMI).  The reference has no
+ * distributed backend (processes on one host exchange files); what
+ * crosses GPUs here is the per-iteration masked-fraction statistic {bpt, bpN}
+ * (bin/proovread:1702-1720, consumed by mask_shortcut_frac 2026-2047) and, in the
+ * exact-parity layout, seed-extension tasks and corrected reads.
+ * Rank 0 creates the id and hands it to the other ranks out of band (a file or
+ * socket rendezvous: proovread_amd/comm.py).  Host-buffer calls synchronise;
+ * pr_comm_allreduce_dev is asynchronous on the context stream.                  */
+#define PR_COMM_ID_BYTES 128
+enum { PR_DT_I64 = 0, PR_DT_F64 = 1, PR_DT_I32 = 2, PR_DT_U8 = 3 };
+enum { PR_RED_SUM = 0, PR_RED_MAX = 1, PR_RED_MIN = 2 };
+typedef struct pr_comm pr_comm;
+int pr_comm_unique_id(uint8_t *id);                        /* id[PR_COMM_ID_BYTES] */
+int pr_comm_init(pr_ctx *ctx, int world, int rank, const uint8_t *id, pr_comm **out);
+void pr_comm_destroy(pr_comm *c);
+int pr_comm_rank(const pr_comm *c, int *rank, int *world);
+int pr_comm_allreduce_dev(pr_comm *c, const void *dev_in, void *dev_out, int64_t n, int dtype, int op);
+int pr_comm_allreduce_host(pr_comm *c, void *buf, int64_t n, int dtype, int op);
+int pr_comm_barrier(pr_comm *c);
+/* every rank's nbytes block, back to back in rank order; counts[world] = block sizes.
+ * recv NULL: only fills counts (size query). */
+int pr_comm_allgatherv_host(pr_comm *c, const uint8_t *send, int64_t nbytes, uint8_t *recv, int64_t recv_cap,
+                            int64_t *counts);
+/* recv_counts[r] = bytes rank r sends to this rank */
+int pr_comm_alltoall_counts(pr_comm *c, const int64_t *send_counts, int64_t *recv_counts);
+int pr_comm_alltoallv_host(pr_comm *c, const uint8_t *send, const int64_t *send_counts, uint8_t *recv,
+                           const int64_t *recv_counts);
 
 /* ------------------------------------------------------------------ */
 /* consensus stage                                                     */

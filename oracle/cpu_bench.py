@@ -1,0 +1,44 @@
+"""ORACLE — BASELINE / CHECKER ONLY (bench.py's cpu_baseline leg, run as a child process).
+
+Loads the bench workload bench.py saved (reads + seed-extension tasks, .npz), runs the
+CPU chain (oracle/cpu_chain.py: SW restatement -> SAM order -> consensus restatement)
+on the first N long reads over W worker processes, and writes one JSON object: the
+timing and, per read, (rc, fastq, trace, chim lines) for bench.py's byte-for-byte
+comparison with the GPU output.  A separate process, so the fork pool never shares a
+process with a HIP runtime.
+
+    python oracle/cpu_bench.py WORKLOAD.npz N WORKERS OUT.json [finish]
+"""
+from __future__ import annotations
+
+import json
+import sys
+from pathlib import Path
+from types import SimpleNamespace
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+sys.path.insert(0, str(HERE))
+
+
+def main(argv) -> int:
+    path, n, workers, out = argv[0], int(argv[1]), int(argv[2]), argv[3]
+    finish = len(argv) > 4 and argv[4] == "1"
+    z = np.load(path)   # allow_pickle=False: arrays only
+    d = SimpleNamespace(**{k: z[k] for k in z.files})
+    d.n_lr = len(d.lr_off) - 1
+    import cpu_chain
+    n = min(n, d.n_lr)
+    wall, bases, res, nw = cpu_chain.run_sample(d, range(n), task="bwa-sr-finish" if finish else "bwa-sr",
+                                                coverage=22.5 if finish else 11.25, use_ref_qual=not finish,
+                                                detect_chimera=finish, workers=workers, full=True)
+    with open(out, "w") as f:
+        json.dump({"wall_s": wall, "bases": bases, "workers": nw, "n": n,
+                   "tasks": int(np.searchsorted(d.t_lr, n, side="left")),
+                   "results": [list(r) for r in res]}, f)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main(sys.argv[1:]))

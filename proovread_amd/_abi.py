@@ -119,6 +119,46 @@ class Context:
             pass
 
 
+class DevBuffer:
+    """Device memory of a context (pr_dev_alloc): e.g. the int64[2] statistic pr_iter_stats /
+    pr_iter_mask fill and an RCCL all-reduce sums across GPUs.  Zeroed at allocation."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        L = lib()
+        L.pr_dev_alloc.argtypes = [C.c_void_p, C.c_int64, C.POINTER(C.c_void_p)]
+        L.pr_dev_free.argtypes = [C.c_void_p, C.c_void_p]
+        L.pr_dev_download.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+        L.pr_dev_upload.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64]
+        self.ctx, self.nbytes = ctx, nbytes
+        p = C.c_void_p()
+        check(L.pr_dev_alloc(ctx.h, nbytes, C.byref(p)), "pr_dev_alloc")
+        self.ptr = p.value
+
+    def download(self, dtype=None):
+        import numpy as np
+        a = np.zeros(self.nbytes, np.uint8)
+        check(lib().pr_dev_download(self.ctx.h, a.ctypes.data, self.ptr, self.nbytes), "pr_dev_download")
+        return a.view(dtype) if dtype is not None else a
+
+    def upload(self, arr):
+        import numpy as np
+        a = np.ascontiguousarray(arr)
+        if a.nbytes > self.nbytes:
+            raise ValueError("upload larger than the device buffer")
+        check(lib().pr_dev_upload(self.ctx.h, self.ptr, a.ctypes.data, a.nbytes), "pr_dev_upload")
+
+    def close(self):
+        if self.ptr:
+            lib().pr_dev_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 _default_ctx = None
 
 

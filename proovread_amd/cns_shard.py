@@ -13,10 +13,11 @@ ranks round-robin (`chunk % world_size == rank`) with no data-path collective;
 each rank batches all of its chunks into one launch (bam2cns.execute) and writes
 the usual per-chunk files, which proovread's merge step (bin/proovread:1640-1699)
 reads unchanged.  The only collective is a final barrier so rank 0 returns after
-every chunk file exists.
+every chunk file exists (RCCL in libprgpu on GPU ranks, comm.py).
 """
 from __future__ import annotations
 
+import ctypes as C
 import os
 import shlex
 import sys
@@ -47,6 +48,20 @@ def run(cmds: Sequence[Sequence[str]], rank: int = 0, world: int = 1) -> List[in
     return mine
 
 
+def _barrier_comm(rank: int, world: int):
+    """The final barrier's communicator: RCCL inside libprgpu on GPU ranks (no torch in the
+    process), gloo where no device is visible (the CPU multi-process test: chunks without
+    --ref never reach the device)."""
+    from . import _abi, comm
+    n = C.c_int(0)
+    _abi.lib().pr_device_count(C.byref(n))
+    if n.value > 0:
+        return comm.RcclComm(_abi.default_context(), rank, world)
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    return comm.TorchComm()
+
+
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     if len(argv) != 1:
@@ -54,17 +69,16 @@ def main(argv=None) -> int:
         return 2
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        # control plane only (a barrier): gloo, so no GPU memory is touched by it
-        dist.init_process_group("gloo")
+    cm = _barrier_comm(rank, world) if world > 1 else None
     try:
         run(read_cmds(argv[0]), rank, world)
     finally:
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()
-            dist.destroy_process_group()
+        if cm is not None:
+            cm.barrier()
+            if hasattr(cm, "close"):
+                cm.close()
+            else:
+                cm.dist.destroy_process_group()
     return 0
 
 

@@ -202,66 +202,19 @@ def _rename(lines: List[str], rid: str) -> List[str]:
 
 
 # ---------------------------------------------------------------------------- multi-rank
-class Comm:
-    """The collectives of the multi-rank loop over torch.distributed (RCCL on GPUs with
-    device tensors, gloo on CPU).  Layout: SURVEY.md §8e's exact-parity option
-    (exact_shard.py): every rank keeps the whole read set and its index, seeds a
-    contiguous shard of the sampled short reads, sends each task to the owner of its
-    long read (one all-to-all), corrects and masks the long reads it owns; the corrected
-    and masked reads are then all-gathered for the next task's index and consensus
-    reference, and bpt/bpN all-reduced so every rank takes the same mask_shortcut
-    decision (the north star's per-iteration statistics gather)."""
-
-    def __init__(self, group=None, device: Optional[str] = None):
-        import torch.distributed as dist
-        self.dist = dist
-        self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
-        self.device = device
-
-    def _dev(self):
-        import torch
-        return torch.device(self.device) if self.device else torch.device("cpu")
-
-    def allreduce_ints(self, vals: Sequence[int]) -> List[int]:
-        import torch
-        t = torch.tensor(list(vals), dtype=torch.int64, device=self._dev())
-        self.dist.all_reduce(t, group=self.group)
-        return [int(x) for x in t.cpu().tolist()]
-
-    def allgather_bytes(self, blob: bytes) -> List[bytes]:
-        import torch
-        n = self.world
-        size = torch.tensor([len(blob)], dtype=torch.int64, device=self._dev())
-        sizes = [torch.zeros_like(size) for _ in range(n)]
-        self.dist.all_gather(sizes, size, group=self.group)
-        sz = [int(x.item()) for x in sizes]
-        cap = max(max(sz), 1)
-        buf = torch.zeros(cap, dtype=torch.uint8)
-        if blob:
-            buf[:len(blob)] = torch.from_numpy(np.frombuffer(blob, np.uint8).copy())
-        buf = buf.to(self._dev())
-        outs = [torch.empty(cap, dtype=torch.uint8, device=self._dev()) for _ in range(n)]
-        self.dist.all_gather(outs, buf, group=self.group)
-        return [outs[r][:sz[r]].cpu().numpy().tobytes() for r in range(n)]
-
-    def allgather_lists(self, items: List[bytes]) -> List[bytes]:
-        """Concatenation over ranks (rank order) of per-rank lists of byte strings."""
-        lens = np.array([len(x) for x in items], np.int64).tobytes()
-        parts = self.allgather_bytes(np.int64(len(items)).tobytes() + lens + b"".join(items))
-        out: List[bytes] = []
-        for p in parts:
-            k = int(np.frombuffer(p[:8], np.int64)[0])
-            ln = np.frombuffer(p[8:8 + 8 * k], np.int64)
-            o = 8 + 8 * k
-            for x in ln:
-                out.append(p[o:o + int(x)])
-                o += int(x)
-        return out
+# The collectives of the multi-rank loop (comm.py).  Layout: SURVEY.md §8e's exact-parity
+# option (exact_shard.py): every rank keeps the whole read set and its index, seeds a
+# contiguous shard of the sampled short reads, sends each task to the owner of its long
+# read (one all-to-all), corrects and masks the long reads it owns; the corrected and
+# masked reads are then all-gathered for the next task's index and consensus reference,
+# and bpt/bpN all-reduced so every rank takes the same mask_shortcut decision (the north
+# star's per-iteration statistics gather).  GPU ranks use comm.RcclComm (RCCL inside
+# libprgpu); the CPU tests use comm.TorchComm (gloo).
+from .comm import RcclComm, TorchComm  # noqa: E402
+Comm = TorchComm
 
 
-def _seed_tasks(lr_map, lr_off, sr, sr_off, finish, threads, comm: Optional[Comm]):
+def _seed_tasks(lr_map, lr_off, sr, sr_off, finish, threads, comm):
     """Tasks of the long reads this rank corrects (global ids), in the single run's order,
     and the [lo, hi) long-read range it owns."""
     from . import exact_shard as ex, seed
@@ -275,14 +228,14 @@ def _seed_tasks(lr_map, lr_off, sr, sr_off, finish, threads, comm: Optional[Comm
         ix.close()
     tk["sr"] += s
     b = ex.lr_bounds(lr_off, comm.world)
-    got = ex.group_by_lr(ex.exchange_tasks(tk, b, device=comm.device, group=comm.group))
+    got = ex.group_by_lr(ex.exchange_tasks(tk, b, comm))
     return got, int(b[comm.rank]), int(b[comm.rank + 1])
 
 
 # ---------------------------------------------------------------------------- the loop
 # ---------------------------------------------------------------------------- the loop
 def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes, cfg: Optional[LoopConfig] = None,
-        stages=None, comm: Optional[Comm] = None) -> LoopResult:
+        stages=None, comm=None) -> LoopResult:
     """The sr-noccs loop (bin/proovread:705-905) from long-read records and the short-read
     FASTQ/FASTA stream; returns the finish task's reads and chimera lines and a log per task.
     With `comm` (world > 1) every rank calls run() on the same inputs and gets the same
@@ -418,15 +371,11 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     cfg = LoopConfig(coverage=a.coverage, sampling=not a.no_sampling, seed_threads=a.threads)
     comm, rank = None, 0
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-        import torch
-        import torch.distributed as dist
-        local = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-        comm = Comm(device=f"cuda:{local}")
-        rank = comm.rank
         from . import _abi
-        stages = GpuStages(_abi.Context(local))
+        ctx = _abi.Context(int(os.environ.get("LOCAL_RANK", "0")))
+        comm = RcclComm.from_env(ctx)   # RCCL inside libprgpu: no second HIP runtime in the process
+        rank = comm.rank
+        stages = GpuStages(ctx)
     else:
         stages = GpuStages()
     res = run(lrs, sr_data, cfg, stages=stages, comm=comm)
@@ -436,7 +385,7 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
             if e.masked_frac is not None:
                 print(f"{e.task}: {e.n_sr} short reads, masked {100 * e.masked_frac:.1f}% {e.shortcut}", file=sys.stderr)
     if comm is not None:
-        comm.dist.destroy_process_group()
+        comm.close()
     return 0
 
 

@@ -1,0 +1,222 @@
+// Multi-GPU collectives of the correction loop over RCCL (include/prgpu.h pr_comm_*),
+// linked into libprgpu so a GPU process needs no second runtime (torch is not loaded
+// in the product's GPU processes).  One process per GPU; the communicator works on the
+// context's stream.
+//
+// What crosses GPUs: the per-iteration masked-fraction statistic
+// {bpt, bpN} (bin/proovread:1702-1720 -> mask_shortcut_frac 2026-2047) as an all-reduce,
+// and in the exact-parity layout the seed-extension tasks (all-to-all to the long-read
+// owners) and the corrected / masked reads (all-gather for the next iteration's index).
+// Host-buffer calls stage through one device buffer and synchronise; device-buffer calls
+// are asynchronous on the context stream.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/prgpu.h"
+
+hipStream_t ctx_stream(pr_ctx *c);
+int ctx_device(pr_ctx *c);
+int pr_set_error(int code, const char *msg);
+
+static_assert(PR_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
+
+struct pr_comm {
+    pr_ctx *ctx = nullptr;
+    ncclComm_t nc = nullptr;
+    int rank = 0, world = 1;
+    void *stage = nullptr;   // device staging buffer for host-buffer collectives
+    size_t stage_cap = 0;
+};
+
+#define HIPCHK(x)                                                                 \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            std::string m_ = std::string(#x) + " failed: " + hipGetErrorString(e_); \
+            return pr_set_error(PR_ERR_HIP, m_.c_str());                          \
+        }                                                                         \
+    } while (0)
+#define NCCLCHK(x)                                                                  \
+    do {                                                                            \
+        ncclResult_t r_ = (x);                                                      \
+        if (r_ != ncclSuccess) {                                                    \
+            std::string m_ = std::string(#x) + " failed: " + ncclGetErrorString(r_); \
+            return pr_set_error(PR_ERR_HIP, m_.c_str());                            \
+        }                                                                           \
+    } while (0)
+
+static int stage(pr_comm *c, size_t bytes) {
+    if (c->stage && c->stage_cap >= bytes) return 0;
+    if (c->stage) (void)hipFree(c->stage);
+    c->stage = nullptr;
+    c->stage_cap = 0;
+    const size_t want = bytes < 4096 ? 4096 : bytes;
+    HIPCHK(hipMalloc(&c->stage, want));
+    c->stage_cap = want;
+    return 0;
+}
+
+static ncclDataType_t dtype_of(int dt, size_t *sz) {
+    switch (dt) {
+        case PR_DT_I64: *sz = 8; return ncclInt64;
+        case PR_DT_F64: *sz = 8; return ncclFloat64;
+        case PR_DT_I32: *sz = 4; return ncclInt32;
+        default: *sz = 1; return ncclUint8;
+    }
+}
+
+extern "C" int pr_comm_unique_id(uint8_t *id) {
+    if (!id) return pr_set_error(PR_ERR_ARG, "null id");
+    ncclUniqueId u;
+    NCCLCHK(ncclGetUniqueId(&u));
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+extern "C" int pr_comm_init(pr_ctx *ctx, int world, int rank, const uint8_t *id, pr_comm **out) {
+    if (!ctx || !out || !id) return pr_set_error(PR_ERR_ARG, "null arg");
+    if (world < 1 || rank < 0 || rank >= world) return pr_set_error(PR_ERR_ARG, "bad rank / world size");
+    HIPCHK(hipSetDevice(ctx_device(ctx)));
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    pr_comm *c = new pr_comm();
+    c->ctx = ctx;
+    c->rank = rank;
+    c->world = world;
+    const ncclResult_t r = ncclCommInitRank(&c->nc, world, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return pr_set_error(PR_ERR_HIP, (std::string("ncclCommInitRank failed: ") + ncclGetErrorString(r)).c_str());
+    }
+    *out = c;
+    return 0;
+}
+
+extern "C" void pr_comm_destroy(pr_comm *c) {
+    if (!c) return;
+    (void)hipSetDevice(ctx_device(c->ctx));
+    (void)hipStreamSynchronize(ctx_stream(c->ctx));
+    if (c->nc) (void)ncclCommDestroy(c->nc);
+    if (c->stage) (void)hipFree(c->stage);
+    delete c;
+}
+
+extern "C" int pr_comm_allreduce_dev(pr_comm *c, const void *dev_in, void *dev_out, int64_t n, int dtype, int op) {
+    if (!c || (n && (!dev_in || !dev_out)) || n < 0) return pr_set_error(PR_ERR_ARG, "bad arg");
+    size_t sz;
+    const ncclDataType_t t = dtype_of(dtype, &sz);
+    const ncclRedOp_t o = op == PR_RED_MAX ? ncclMax : (op == PR_RED_MIN ? ncclMin : ncclSum);
+    HIPCHK(hipSetDevice(ctx_device(c->ctx)));
+    NCCLCHK(ncclAllReduce(dev_in, dev_out, (size_t)n, t, o, c->nc, ctx_stream(c->ctx)));
+    return 0;
+}
+
+extern "C" int pr_comm_allreduce_host(pr_comm *c, void *buf, int64_t n, int dtype, int op) {
+    if (!c || (n && !buf) || n < 0) return pr_set_error(PR_ERR_ARG, "bad arg");
+    size_t sz;
+    (void)dtype_of(dtype, &sz);
+    const size_t bytes = (size_t)n * sz;
+    int rc = stage(c, bytes);
+    if (rc) return rc;
+    hipStream_t s = ctx_stream(c->ctx);
+    HIPCHK(hipSetDevice(ctx_device(c->ctx)));
+    HIPCHK(hipMemcpyAsync(c->stage, buf, bytes, hipMemcpyHostToDevice, s));
+    if ((rc = pr_comm_allreduce_dev(c, c->stage, c->stage, n, dtype, op))) return rc;
+    HIPCHK(hipMemcpyAsync(buf, c->stage, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" int pr_comm_barrier(pr_comm *c) {
+    int64_t one = 1;
+    return pr_comm_allreduce_host(c, &one, 1, PR_DT_I64, PR_RED_SUM);
+}
+
+// variable-size all-gather: every rank's `nbytes` (all-gathered first), then one padded
+// ncclAllGather; recv gets the ranks' blocks back to back, counts[r] their sizes
+extern "C" int pr_comm_allgatherv_host(pr_comm *c, const uint8_t *send, int64_t nbytes, uint8_t *recv,
+                                       int64_t recv_cap, int64_t *counts) {
+    if (!c || nbytes < 0 || (nbytes && !send) || !counts) return pr_set_error(PR_ERR_ARG, "bad arg");
+    const int W = c->world;
+    std::vector<int64_t> sz((size_t)W, 0);
+    sz[(size_t)c->rank] = nbytes;
+    int rc = pr_comm_allreduce_host(c, sz.data(), W, PR_DT_I64, PR_RED_SUM);
+    if (rc) return rc;
+    int64_t cap = 1, tot = 0;
+    for (int r = 0; r < W; ++r) {
+        counts[r] = sz[(size_t)r];
+        cap = sz[(size_t)r] > cap ? sz[(size_t)r] : cap;
+        tot += sz[(size_t)r];
+    }
+    if (!recv) return 0;   // size query
+    if (tot > recv_cap) return pr_set_error(PR_ERR_CAPACITY, "all-gather receive buffer too small");
+    cap = (cap + 255) & ~(int64_t)255;
+    if ((rc = stage(c, (size_t)cap * (size_t)(W + 1)))) return rc;
+    hipStream_t s = ctx_stream(c->ctx);
+    uint8_t *mine = (uint8_t *)c->stage + (size_t)cap * (size_t)W;
+    uint8_t *all = (uint8_t *)c->stage;
+    HIPCHK(hipSetDevice(ctx_device(c->ctx)));
+    if (nbytes) HIPCHK(hipMemcpyAsync(mine, send, (size_t)nbytes, hipMemcpyHostToDevice, s));
+    NCCLCHK(ncclAllGather(mine, all, (size_t)cap, ncclUint8, c->nc, s));
+    int64_t o = 0;
+    for (int r = 0; r < W; ++r) {
+        if (sz[(size_t)r]) HIPCHK(hipMemcpyAsync(recv + o, all + (size_t)cap * r, (size_t)sz[(size_t)r], hipMemcpyDeviceToHost, s));
+        o += sz[(size_t)r];
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+// all-to-all of byte blocks: send_counts[r] bytes go to rank r (blocks back to back in
+// rank order); recv_counts[r] must equal what rank r sends here (exchange the counts
+// first with pr_comm_alltoall_counts).  Point-to-point send/recv pairs in one group.
+extern "C" int pr_comm_alltoallv_host(pr_comm *c, const uint8_t *send, const int64_t *send_counts, uint8_t *recv,
+                                      const int64_t *recv_counts) {
+    if (!c || !send_counts || !recv_counts) return pr_set_error(PR_ERR_ARG, "null arg");
+    const int W = c->world;
+    int64_t st = 0, rt = 0;
+    for (int r = 0; r < W; ++r) {
+        if (send_counts[r] < 0 || recv_counts[r] < 0) return pr_set_error(PR_ERR_ARG, "negative count");
+        st += send_counts[r];
+        rt += recv_counts[r];
+    }
+    if ((st && !send) || (rt && !recv)) return pr_set_error(PR_ERR_ARG, "null buffer");
+    const size_t sa = ((size_t)st + 255) & ~(size_t)255;
+    int rc = stage(c, sa + (size_t)rt + 256);
+    if (rc) return rc;
+    hipStream_t s = ctx_stream(c->ctx);
+    uint8_t *ds = (uint8_t *)c->stage, *dr = (uint8_t *)c->stage + sa;
+    HIPCHK(hipSetDevice(ctx_device(c->ctx)));
+    if (st) HIPCHK(hipMemcpyAsync(ds, send, (size_t)st, hipMemcpyHostToDevice, s));
+    NCCLCHK(ncclGroupStart());
+    int64_t so = 0, ro = 0;
+    for (int r = 0; r < W; ++r) {
+        if (send_counts[r]) NCCLCHK(ncclSend(ds + so, (size_t)send_counts[r], ncclUint8, r, c->nc, s));
+        if (recv_counts[r]) NCCLCHK(ncclRecv(dr + ro, (size_t)recv_counts[r], ncclUint8, r, c->nc, s));
+        so += send_counts[r];
+        ro += recv_counts[r];
+    }
+    NCCLCHK(ncclGroupEnd());
+    if (rt) HIPCHK(hipMemcpyAsync(recv, dr, (size_t)rt, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+// the counts exchange of an all-to-all: recv_counts[r] = what rank r sends to this rank
+extern "C" int pr_comm_alltoall_counts(pr_comm *c, const int64_t *send_counts, int64_t *recv_counts) {
+    if (!c || !send_counts || !recv_counts) return pr_set_error(PR_ERR_ARG, "null arg");
+    const int W = c->world;
+    std::vector<int64_t> ones((size_t)W, 8);
+    return pr_comm_alltoallv_host(c, (const uint8_t *)send_counts, ones.data(), (uint8_t *)recv_counts, ones.data());
+}
+
+extern "C" int pr_comm_rank(const pr_comm *c, int *rank, int *world) {
+    if (!c) return pr_set_error(PR_ERR_ARG, "null comm");
+    if (rank) *rank = c->rank;
+    if (world) *world = c->world;
+    return 0;
+}

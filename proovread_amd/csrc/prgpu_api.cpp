@@ -698,6 +698,39 @@ extern "C" int pr_ctx_sync(pr_ctx *c) {
     return 0;
 }
 
+extern "C" int pr_dev_alloc(pr_ctx *c, int64_t bytes, void **dev) {
+    if (!c || !dev || bytes < 0) return set_error(PR_ERR_ARG, "bad arg");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMalloc(dev, (size_t)(bytes ? bytes : 16)));
+    HIPCHK(hipMemsetAsync(*dev, 0, (size_t)(bytes ? bytes : 16), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int pr_dev_free(pr_ctx *c, void *dev) {
+    if (!c) return set_error(PR_ERR_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (dev) HIPCHK(hipFree(dev));
+    return 0;
+}
+
+extern "C" int pr_dev_download(pr_ctx *c, void *host, const void *dev, int64_t bytes) {
+    if (!c || bytes < 0 || (bytes && (!host || !dev))) return set_error(PR_ERR_ARG, "bad arg");
+    HIPCHK(hipSetDevice(c->device));
+    if (bytes) HIPCHK(hipMemcpyAsync(host, dev, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+extern "C" int pr_dev_upload(pr_ctx *c, void *dev, const void *host, int64_t bytes) {
+    if (!c || bytes < 0 || (bytes && (!host || !dev))) return set_error(PR_ERR_ARG, "bad arg");
+    HIPCHK(hipSetDevice(c->device));
+    if (bytes) HIPCHK(hipMemcpyAsync(dev, host, (size_t)bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 extern "C" int pr_iter_stats(pr_ctx *c, int32_t min_phred, int64_t *dev_out) {
     if (!c || !dev_out) return set_error(PR_ERR_ARG, "null arg");
     if (!c->cns_loaded) return set_error(PR_ERR_ARG, "no resident consensus batch");

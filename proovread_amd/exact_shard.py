@@ -14,11 +14,11 @@ long read.  Rank r holds reads [s_r, e_r) with s_r increasing in r, and the all-
 delivers rank 0's tasks first, then rank 1's ... each in its own read order — so the
 owner's stable grouping reproduces the single run's order exactly.
 
-The exchange uses torch.distributed (RCCL on GPUs: device tensors; gloo on CPU).
+The exchange goes through comm.py: RCCL in libprgpu on GPUs, torch gloo in the CPU tests.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import Tuple
 
 import numpy as np
 
@@ -48,27 +48,18 @@ def owners(tasks: np.ndarray, bounds: np.ndarray) -> np.ndarray:
     return np.searchsorted(bounds, tasks["lr"].astype(np.int64), side="right") - 1
 
 
-def exchange_tasks(tasks: np.ndarray, bounds: np.ndarray, device: Optional[str] = None, group=None) -> np.ndarray:
+def exchange_tasks(tasks: np.ndarray, bounds: np.ndarray, comm) -> np.ndarray:
     """All-to-all of seed-extension tasks to the owners of their long reads.
 
-    tasks: this rank's tasks (TASK_DTYPE, read order).  Returns the tasks of the long reads
-    this rank owns, source-rank-major, each source's order kept."""
-    import torch
-    import torch.distributed as dist
-    world = dist.get_world_size(group)
+    tasks: this rank's tasks (TASK_DTYPE, read order); comm: a comm.RcclComm (GPU ranks)
+    or comm.TorchComm (gloo, CPU tests).  Returns the tasks of the long reads this rank
+    owns, source-rank-major, each source's order kept."""
     own = owners(tasks, bounds)
     order = np.argsort(own, kind="stable")
     send = np.ascontiguousarray(tasks[order]).view(np.int32).reshape(-1, NFIELD)
-    send_counts = np.bincount(own, minlength=world).astype(np.int64)
-    dev = torch.device(device) if device else torch.device("cpu")
-    sc = torch.from_numpy(send_counts).to(dev)
-    rc = torch.empty_like(sc)
-    dist.all_to_all_single(rc, sc, group=group)
-    recv_counts = rc.cpu().numpy()
-    out = torch.empty((int(recv_counts.sum()), NFIELD), dtype=torch.int32, device=dev)
-    dist.all_to_all_single(out, torch.from_numpy(send).to(dev), [int(x) for x in recv_counts],
-                           [int(x) for x in send_counts], group=group)
-    return np.ascontiguousarray(out.cpu().numpy()).view(TASK_DTYPE).reshape(-1)
+    send_counts = np.bincount(own, minlength=comm.world).astype(np.int64)
+    got = comm.alltoallv_rows(send, send_counts)
+    return np.ascontiguousarray(got).view(TASK_DTYPE).reshape(-1)
 
 
 def group_by_lr(tasks: np.ndarray) -> np.ndarray:

@@ -13,7 +13,6 @@ import socket
 from pathlib import Path
 
 import pytest
-import torch.multiprocessing as mp
 
 import bamio
 from proovread_amd import bam2cns, cns_shard
@@ -58,6 +57,7 @@ def test_gloo_two_ranks_write_every_chunk(tmp_path):
              for i in range(n)]
     cmds = tmp_path / "t.cmds"
     cmds.write_text("\n".join(lines) + "\n")
+    import torch.multiprocessing as mp
     mp.start_processes(_rank_main, args=(2, _free_port(), str(cmds)), nprocs=2, join=True,
                        start_method="spawn")
     for i in range(n):

@@ -7,7 +7,6 @@ import socket
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
 
 
 def _free_port():
@@ -37,7 +36,8 @@ def _rank(rank, world, port, outdir):
     sub = ix.map(d.sr_seq[d.sr_off[s]:d.sr_off[e]], d.sr_off[s:e + 1] - d.sr_off[s], threads=2)
     assert len(sub) == len(mine) and np.array_equal(sub["sr"] + s, mine["sr"])
     b = ex.lr_bounds(d.lr_off, world)
-    got = ex.group_by_lr(ex.exchange_tasks(mine, b))
+    from proovread_amd.comm import TorchComm
+    got = ex.group_by_lr(ex.exchange_tasks(mine, b, TorchComm()))
     np.save(os.path.join(outdir, f"r{rank}.npy"), got)
     dist.barrier()
     dist.destroy_process_group()
@@ -45,6 +45,7 @@ def _rank(rank, world, port, outdir):
 
 def test_exact_layout_two_ranks(tmp_path):
     from proovread_amd import exact_shard as ex, seed
+    import torch.multiprocessing as mp
     world = 2
     mp.spawn(_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     d = _data()

@@ -90,14 +90,13 @@ def test_mask_cfg_default_and_empty():
 def test_iter_mask_matches_oracle_on_consensus():
     """pr_iter_mask on a resident iteration's consensus vs the oracle on the downloaded
     consensus seq/qual; the device statistic is exactly (bpt, bpN) over status-0 reads."""
-    import torch
-    from proovread_amd import cns, iteration, mask, sw, synth
+    from proovread_amd import _abi, cns, iteration, mask, sw, synth
     d = synth.simulate(77, 60_000, 40, 3000, 50.0, sr_frac=0.3)
     it = iteration.Iteration(d)
     it.launch(sw.default_opts(False), cns.CnsParams(coverage=11.25, use_ref_qual=True))
     p = mask.params("20,41,80,130,60,0.7", 150)
-    st = torch.zeros(2, dtype=torch.int64, device="cuda:0")
-    it.mask_to(st.data_ptr(), p)
+    st = _abi.DevBuffer(it.ctx, 16)
+    it.mask_to(st.ptr, p)
     it.sync()
     masked = it.masked()
     a = it.download()
@@ -109,7 +108,7 @@ def test_iter_mask_matches_oracle_on_consensus():
             quals.append(a["qual"][o:o + sl].tobytes())
     want, _, wst = O.mask_reads(seqs, quals, O.mask_params_from_cfg("20,41,80,130,60,0.7", 150))
     assert [m for m, s in zip(masked, a["status"]) if s == 0] == want
-    assert tuple(st.cpu().tolist()) == wst
+    assert tuple(int(x) for x in st.download(np.int64)) == wst
     assert wst[1] > 0
 
 
