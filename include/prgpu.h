@@ -225,7 +225,6 @@ typedef struct pr_sw_batch {
     const int32_t *t_qbeg, *t_rbeg, *t_slen;
 } pr_sw_batch;
 
-#define PR_SW_MAXCIG 128
 typedef struct pr_sw_out {          /* per task (any pointer may be NULL)              */
     int32_t *qb, *qe;               /* aligned query interval                          */
     int32_t *rb, *re;               /* reference interval (strand coordinates)         */
@@ -233,15 +232,26 @@ typedef struct pr_sw_out {          /* per task (any pointer may be NULL)       
     int32_t *truesc;                /* mem_alnreg_t truesc                             */
     int32_t *pos;                   /* 0-based leftmost forward position (SAM POS-1)   */
     int32_t *ncigar;
-    uint32_t *cigar;                /* [n_task * PR_SW_MAXCIG] BAM ops M0 I1 D2 S4       */
     uint8_t *pass;                  /* score >= T * (qe - qb)                          */
-    int32_t *status;                /* 0 or PR_ERR_CAPACITY (CIGAR > PR_SW_MAXCIG ops) */
+    int32_t *status;                /* 0 (PR_ERR_CAPACITY cannot occur: CIGARs have no
+                                       length limit, bwa_gen_cigar2's own bound holds) */
+    /* CIGARs, variable length, compacted in task order: task t's ops (BAM codes M0 I1 D2
+     * S4) are cigar[cigar_off[t] .. cigar_off[t+1]).  cigar_off [n_task+1] is filled when
+     * given; cigar (capacity cigar_cap ops) when given and large enough, otherwise the call
+     * returns PR_ERR_CAPACITY after filling everything else (pr_sw_cigar_total gives the
+     * size; the batch stays resident, so pr_sw_download can be repeated).              */
+    int64_t *cigar_off;
+    uint32_t *cigar;
+    int64_t cigar_cap;
 } pr_sw_out;
 
 int pr_sw_run(pr_ctx *ctx, const pr_sw_opts *o, const pr_sw_batch *b, pr_sw_out *out);
 int pr_sw_upload(pr_ctx *ctx, const pr_sw_batch *b);
 int pr_sw_launch(pr_ctx *ctx, const pr_sw_opts *o);   /* async on ctx stream */
 int pr_sw_download(pr_ctx *ctx, pr_sw_out *out);      /* syncs               */
+/* total CIGAR ops of the last launch (the pr_sw_out.cigar size) and the tasks whose CIGAR
+ * outgrew its slot and was recomputed into the spill area (syncs) */
+int pr_sw_cigar_total(pr_ctx *ctx, int64_t *total, int64_t *n_overflow);
 /* kernel milliseconds of the last launch (HIP events on the ctx stream) */
 int pr_sw_last_timing(pr_ctx *ctx, double *ms_extend, double *ms_global);
 /* canonical DP cells of the last launch (unpruned band, final width) */

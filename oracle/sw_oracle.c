@@ -337,7 +337,7 @@ int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, in
     const int lqq = qe - qb, rlen = re - rb;
     uint8_t *qq = (uint8_t *)malloc((size_t)lqq + 1);
     uint8_t *rr = (uint8_t *)malloc((size_t)rlen + 1);
-    uint32_t cig[512];
+    uint32_t cig[OSW_MAXCIG];
     int w_used = 0;
     do {
         w2 = w2 < o->w << 2 ? w2 : o->w << 2;
@@ -366,7 +366,7 @@ int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, in
             int min_w = abs(rlen - lqq) + 3;
             ww = ww > min_w ? ww : min_w;
             gsc = osw_global(lqq, qq, rlen, rr, 5, mat, o->o_del, o->e_del, o->o_ins, o->e_ins, ww,
-                             &ncig, cig, 500);
+                             &ncig, cig, OSW_MAXCIG - 4);
             w_used = ww;
         }
         if (gsc == last_sc || w2 == o->w << 2) break;
@@ -381,7 +381,7 @@ int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, in
     /* forward position; convert bwa op codes (M0 I1 D2) to BAM (M0 I1 D2 S4) */
     int pos = strand ? L - re : rb;
     int n = 0;
-    uint32_t out[512];
+    uint32_t out[OSW_MAXCIG];
     for (int i = 0; i < ncig; ++i) out[n++] = cig[i];
     if (n > 0) {
         if ((out[0] & 0xf) == 2) {

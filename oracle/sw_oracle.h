@@ -6,6 +6,10 @@
 extern "C" {
 #endif
 
+/* CIGAR capacity: >= query + reference span + clips for queries up to proovread's
+ * 1000 bp limit (bin/proovread:457) */
+#define OSW_MAXCIG 4096
+
 /* bwa mem options used by proovread (proovread.cfg:320-333, 343-365) */
 typedef struct {
     int a, b;                  /* -A, -B                      */
@@ -24,7 +28,7 @@ typedef struct {
     int global_score, w2;      /* ksw_global2 score and band used          */
     int pos;                   /* 0-based leftmost forward position        */
     int n_cigar;
-    uint32_t cigar[512];       /* len<<4|op, op M0 I1 D2 S4 (BAM codes)    */
+    uint32_t cigar[OSW_MAXCIG]; /* len<<4|op, op M0 I1 D2 S4 (BAM codes)   */
     int pass;                  /* score >= T * aligned query length        */
 } osw_result;
 

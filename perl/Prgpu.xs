@@ -367,13 +367,19 @@ sw_run(IV ctx, HV *opts, HV *batch)
     fill_sw_batch(aTHX_ batch, &b);
     nt = b.n_task;
     {
-        /* outputs, one Perl string each (PR_SW_MAXCIG ops per task for the CIGARs) */
+        /* outputs, one Perl string each; CIGARs variable length (cigar_off prefix) */
+        int64_t ctot = 0, nover = 0;
+        pr_ctx *cx = INT2PTR(pr_ctx *, ctx);
+        rc = pr_sw_upload(cx, &b);
+        if (rc == 0) rc = pr_sw_launch(cx, &o);
+        if (rc == 0) rc = pr_sw_cigar_total(cx, &ctot, &nover);
+        if (rc != 0) croak("Prgpu: pr_sw_run: %s (%d)", pr_last_error(), rc);
         SV *s_pos = newSV(4 * nt + 1), *s_sc = newSV(4 * nt + 1), *s_nc = newSV(4 * nt + 1),
-           *s_cig = newSV(4 * (size_t)PR_SW_MAXCIG * nt + 1), *s_pass = newSV(nt + 1), *s_st = newSV(4 * nt + 1),
-           *s_qb = newSV(4 * nt + 1), *s_qe = newSV(4 * nt + 1);
-        SV *all[] = {s_pos, s_sc, s_nc, s_cig, s_pass, s_st, s_qb, s_qe};
-        const STRLEN lens[] = {4 * nt, 4 * nt, 4 * nt, 4 * (size_t)PR_SW_MAXCIG * nt, nt, 4 * nt, 4 * nt, 4 * nt};
-        const char *keys[] = {"pos", "score", "ncigar", "cigar", "pass", "status", "qb", "qe"};
+           *s_cig = newSV(4 * (size_t)ctot + 1), *s_pass = newSV(nt + 1), *s_st = newSV(4 * nt + 1),
+           *s_qb = newSV(4 * nt + 1), *s_qe = newSV(4 * nt + 1), *s_coff = newSV(8 * (size_t)(nt + 1) + 1);
+        SV *all[] = {s_pos, s_sc, s_nc, s_cig, s_pass, s_st, s_qb, s_qe, s_coff};
+        const STRLEN lens[] = {4 * nt, 4 * nt, 4 * nt, 4 * (size_t)ctot, nt, 4 * nt, 4 * nt, 4 * nt, 8 * (size_t)(nt + 1)};
+        const char *keys[] = {"pos", "score", "ncigar", "cigar", "pass", "status", "qb", "qe", "cigar_off"};
         unsigned k;
         for (k = 0; k < sizeof all / sizeof all[0]; ++k) {
             SvPOK_on(all[k]);
@@ -385,11 +391,13 @@ sw_run(IV ctx, HV *opts, HV *batch)
         out.score = (int32_t *)SvPVX(s_sc);
         out.ncigar = (int32_t *)SvPVX(s_nc);
         out.cigar = (uint32_t *)SvPVX(s_cig);
+        out.cigar_cap = ctot;
+        out.cigar_off = (int64_t *)SvPVX(s_coff);
         out.pass = (uint8_t *)SvPVX(s_pass);
         out.status = (int32_t *)SvPVX(s_st);
         out.qb = (int32_t *)SvPVX(s_qb);
         out.qe = (int32_t *)SvPVX(s_qe);
-        rc = pr_sw_run(INT2PTR(pr_ctx *, ctx), &o, &b, &out);
+        rc = pr_sw_download(cx, &out);
         if (rc != 0) {
             for (k = 0; k < sizeof all / sizeof all[0]; ++k) SvREFCNT_dec(all[k]);
             croak("Prgpu: pr_sw_run: %s (%d)", pr_last_error(), rc);

@@ -232,10 +232,10 @@ use constant TASK_BYTES => 40;   # pr_seed_task: 10 x int32
 # SW results of a packed sw_run output for tasks 0..n-1
 sub sw_unpack {
     my ($o, $n) = @_;
-    my @nc = unpack('l<*', $o->{ncigar});
+    my @co = unpack('q<*', $o->{cigar_off});   # variable-length CIGARs, compacted in task order
     my @cig;
     for my $t (0 .. $n - 1) {
-        my @ops = unpack('L<*', substr($o->{cigar}, 4 * 128 * $t, 4 * $nc[$t]));
+        my @ops = unpack('L<*', substr($o->{cigar}, 4 * $co[$t], 4 * ($co[$t + 1] - $co[$t])));
         push @cig, join '', map { ($_ >> 4) . substr($CIGAR_CHARS, $_ & 15, 1) } @ops;
     }
     return {pos => [unpack('l<*', $o->{pos})], score => [unpack('l<*', $o->{score})],

@@ -7,13 +7,13 @@ namespace prgpu {
 struct PipeDev {
     int n_lr;
     int sort_cap;            // max alignments per long read the LDS sort holds
-    int maxcig;              // SW CIGAR stride (SW_MAXCIG)
     const int64_t *task_off; // [n_lr+1] tasks grouped by long read
     const int32_t *t_sr;
     const uint8_t *strand;
     const uint8_t *pass;
     const int32_t *status, *pos, *score, *ncig;
     const int64_t *sr_off;
+    const int64_t *cig_at;   // [n_task] first op of each task's CIGAR in the SW pool
     int32_t *cnt;            // [n_lr]
     int64_t *aln_off;        // [n_lr+1]
     int32_t *err;            // [n_lr]

@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(PIPE_THREADS) pipe_sort_kernel(PipeDev P) {
             P.a_flags[g] = (uint8_t)(1u | (P.strand[t] ? 8u : 0u));   // HAS_SCORE | REVCOMP
             P.a_seq_off[g] = P.sr_off[sid];
             P.a_lseq[g] = (int32_t)(P.sr_off[sid + 1] - P.sr_off[sid]);
-            P.a_cig_off[g] = t * (int64_t)P.maxcig;
+            P.a_cig_off[g] = P.cig_at[t];
             P.a_ncig[g] = P.ncig[t];
         }
         __syncthreads();

@@ -412,7 +412,7 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
     }
     if (c->pipe) {
         // consensus reads the SW batch in place: long reads and short reads as
-        // nt4, CIGARs from the SW output (stride SW_MAXCIG)
+        // nt4, CIGARs in place in the SW output pool (per-task starts: pipe hand-off)
         SwPtrs sp;
         int rc = sw_get_ptrs(c, &sp);
         if (rc) return rc;
@@ -613,7 +613,7 @@ extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_param
     PipeDev P;
     P.n_lr = c->n_lr;
     P.sort_cap = c->pipe_sort_cap;
-    P.maxcig = SW_MAXCIG;
+    P.cig_at = sp.cig_at;
     P.task_off = c->pb[0].as<int64_t>();
     P.t_sr = sp.t_sr;
     P.strand = sp.strand;

@@ -43,10 +43,16 @@ static const int SB_BUCKET = 26;
 static const int SB_X = 27;
 static const int SB_XTRY = 28;
 static const int SB_LIST = 29;
+static const int SB_CIGSLOT = 30;   // int64 [n+1] prefix of the per-task CIGAR slots
+static const int SB_CIGAT = 31;     // int64 [n] first op of each task's CIGAR
+static const int SB_EHG = 32;       // HBM DP rows of the general CIGAR kernel (long queries)
+static const int SB_CIGOFF = 33;    // pr_sw_download compaction: prefix of ncigar
+static const int SB_CIGOUT = 34;    //                            compacted ops
+static const size_t SPILL_OFF = 96;   // in the SB_CELLS buffer: 3 x u64 overflow counters
 
 namespace prgpu {
 void sw_release(SwResident &r) {
-    for (int i = 0; i < 32; ++i) {
+    for (int i = 0; i < 40; ++i) {
         if (r.buf[i]) (void)hipFree(r.buf[i]);
         r.buf[i] = nullptr;
         r.cap[i] = 0;
@@ -128,9 +134,22 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
         (rc = ensure(r, SB_X, (size_t)(nt + 1) * 4 * 12)) || (rc = ensure(r, SB_XTRY, (size_t)nt + 1)) ||
         (rc = ensure(r, SB_LIST, (size_t)(nt + 1 + (int64_t)PK_NB * PK_SEG) * 4)))
         return rc;
-    if ((rc = ensure(r, SB_PASS, (size_t)nt + 1)) || (rc = ensure(r, SB_CIG, (size_t)(nt + 1) * SW_MAXCIG * 4)) ||
+    // CIGAR slots sized from the short-read lengths, plus a spill reserve for overflows
+    // (PRGPU_SW_CIG_SLOT: a fixed slot size, a test hook that sends CIGARs to the overflow pass)
+    std::vector<int64_t> slot((size_t)nt + 1, 0);
+    const int forced = getenv("PRGPU_SW_CIG_SLOT") ? atoi(getenv("PRGPU_SW_CIG_SLOT")) : 0;
+    for (int64_t t = 0; t < nt; ++t) {
+        const int sr = b->t_sr[t];
+        const int cs = forced > 0 ? forced : cig_slot_ops((int)(b->sr_off[sr + 1] - b->sr_off[sr]));
+        slot[(size_t)t + 1] = slot[(size_t)t] + cs;
+    }
+    const int64_t slots = slot[(size_t)nt];
+    const int64_t reserve = slots / 16 > (1 << 20) ? slots / 16 : (1 << 20);
+    if ((rc = ensure(r, SB_PASS, (size_t)nt + 1)) || (rc = ensure(r, SB_CIG, (size_t)(slots + reserve) * 4)) ||
+        (rc = up(r, SB_CIGSLOT, slot.data(), slot.size(), s)) || (rc = ensure(r, SB_CIGAT, (size_t)(nt + 1) * 8)) ||
         (rc = ensure(r, SB_CELLS, CELLS_BYTES)))
         return rc;
+    r.cig_slots = slots;
     HIPCHK(hipStreamSynchronize(s));
     r.loaded = true;
     r.n_task = nt;
@@ -151,6 +170,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if (o->w > 40) return pr_set_error(PR_ERR_UNSUPPORTED, "band width w > 40 (register ring holds 2*80+2 columns)");
     if (o->a > 15 || o->b > 16) return pr_set_error(PR_ERR_UNSUPPORTED, "match score > 15 or mismatch penalty > 16");
     HIPCHK(hipSetDevice(ctx_device(c)));
+    (void)hipGetLastError();   // a failed earlier call must not poison this one
     hipStream_t s = ctx_stream(c);
     SwOptsDev O;
     O.a = o->a; O.b = o->b; O.o_del = o->o_del; O.e_del = o->e_del; O.o_ins = o->o_ins; O.e_ins = o->e_ins;
@@ -187,6 +207,10 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.o_ncig = (int32_t *)r.buf[SB_NCIG];
     D.o_status = (int32_t *)r.buf[SB_STATUS];
     D.o_cig = (uint32_t *)r.buf[SB_CIG];
+    D.cig_slot = (const int64_t *)r.buf[SB_CIGSLOT];
+    D.o_cig_at = (int64_t *)r.buf[SB_CIGAT];
+    D.spill = (unsigned long long *)((char *)r.buf[SB_CELLS] + SPILL_OFF);
+    D.spill_base = r.cig_slots;
     D.cells = (unsigned long long *)r.buf[SB_CELLS];
     D.work = (int32_t *)((char *)r.buf[SB_CELLS] + CELLS_WORK_OFF);
     D.perm = (int32_t *)r.buf[SB_PERM];
@@ -195,15 +219,26 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.x_try = (uint8_t *)r.buf[SB_XTRY];
     D.list = (int32_t *)r.buf[SB_LIST];
     D.list_n = D.bucket + SW_NBUCKET;
+    int rc0 = 0;
     D.pk_bucket = D.bucket + SW_NBUCKET + 16;
-    // LDS of the CIGAR kernel: (qmax+1) H/E words per lane + lane-major query bytes
+    // row of the general CIGAR kernel: (qmax+1) H/E words per lane + lane-major query bytes,
+    // in LDS when it fits next to the kernel's static LDS, else in HBM (queries > ~500 bp)
     const int lds_ext = (r.qmax + 1) * SW_WAVE * 4;
     const int qpad = (r.qmax + 8) & ~3;
     const int lds_glob = lds_ext + SW_WAVE * qpad;
-    if (lds_glob > 160 * 1024) return pr_set_error(PR_ERR_ARG, "short reads too long for the LDS layout");
-    const int blocks_per_cu = (160 * 1024) / (lds_glob + 64) > 0 ? (160 * 1024) / (lds_glob + 64) : 1;
-    const int grid_g = ctx_ncu(c) * (blocks_per_cu < 8 ? blocks_per_cu : 8);
+    const bool eh_hbm = lds_glob + 256 > 160 * 1024;
+    const int blocks_per_cu = eh_hbm ? 2 : ((160 * 1024) / (lds_glob + 64) > 0 ? (160 * 1024) / (lds_glob + 64) : 1);
+    int grid_g = ctx_ncu(c) * (blocks_per_cu < 8 ? blocks_per_cu : 8);
     D.z_slab = (int64_t)D.tmax * ((r.qmax + 3) / 4) * 4 * SW_WAVE;
+    {   // direction slabs of the general kernel within 4 GB
+        const int64_t gmax = ((int64_t)4 << 30) / (D.z_slab > 0 ? D.z_slab : 1);
+        if (grid_g > gmax) grid_g = (int)(gmax > 16 ? gmax : 16);
+    }
+    if (eh_hbm) {
+        D.eh_g_stride = (int64_t)((lds_glob + 255) & ~255) / 4;
+        if ((rc0 = ensure(r, SB_EHG, (size_t)D.eh_g_stride * 4 * (size_t)grid_g))) return rc0;
+        D.eh_g = (uint32_t *)r.buf[SB_EHG];
+    }
     const int grid_w = ctx_ncu(c) * 12;                       // ring kernels: 3 waves per SIMD
     D.z_ring_slab = (int64_t)D.tmax * ((2 * 80 + 2 + 7) / 8) * SW_WAVE;
     const int grid_pk = ctx_ncu(c) * 8;                       // packed kernel: ~200 VGPRs, 2 waves per SIMD
@@ -216,6 +251,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.z = (uint8_t *)r.buf[SB_Z];
     HIPCHK(hipMemsetAsync(r.buf[SB_CELLS], 0, CELLS_BYTES, s));
     if (r.n_task == 0) return 0;
+    HIPCHK(hipMemcpyAsync(r.buf[SB_CIGAT], r.buf[SB_CIGSLOT], (size_t)r.n_task * 8, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
     int e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
@@ -223,6 +259,27 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
     e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6), (void *)ctx_event(c, 7));
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    // CIGARs longer than their slots: recompute those tasks into the spill area
+    unsigned long long sp[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(sp, D.spill, sizeof sp, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (sp[0]) {
+        const size_t need = (size_t)(r.cig_slots + (int64_t)sp[1]) * 4;
+        if (need > r.cap[SB_CIG]) {   // grow the pool, keeping the slots
+            void *np = nullptr;
+            if (hipMalloc(&np, need + need / 8) != hipSuccess) return pr_set_error(PR_ERR_HIP, "hipMalloc failed (CIGAR spill)");
+            HIPCHK(hipMemcpyAsync(np, r.buf[SB_CIG], (size_t)r.cig_slots * 4, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+            (void)hipFree(r.buf[SB_CIG]);
+            r.buf[SB_CIG] = np;
+            r.cap[SB_CIG] = need + need / 8;
+            D.o_cig = (uint32_t *)np;
+        }
+        HIPCHK(hipMemsetAsync(D.work, 0, 4, s));
+        e = sw_launch_overflow(D, O, grid_g, lds_glob, (void *)s);
+        if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    }
+    r.n_overflow = (int64_t)sp[0];
     HIPCHK(hipEventRecord(ctx_event(c, 0), s));
     return 0;
 }
@@ -253,10 +310,48 @@ extern "C" int pr_sw_download(pr_ctx *c, pr_sw_out *o) {
         (rc = down(o->rb, r, SB_RB, n, s)) || (rc = down(o->re, r, SB_RE, n, s)) ||
         (rc = down(o->score, r, SB_SCORE, n, s)) || (rc = down(o->truesc, r, SB_TRUESC, n, s)) ||
         (rc = down(o->pos, r, SB_POS, n, s)) || (rc = down(o->ncigar, r, SB_NCIG, n, s)) ||
-        (rc = down(o->cigar, r, SB_CIG, n * SW_MAXCIG, s)) || (rc = down(o->pass, r, SB_PASS, n, s)) ||
-        (rc = down(o->status, r, SB_STATUS, n, s)))
+        (rc = down(o->pass, r, SB_PASS, n, s)) || (rc = down(o->status, r, SB_STATUS, n, s)))
         return rc;
     HIPCHK(hipStreamSynchronize(s));
+    if (!o->cigar_off && !o->cigar) return 0;
+    // CIGARs: prefix of the op counts (status 0 tasks), then one compaction launch
+    std::vector<int32_t> nc(n + 1, 0), st(n + 1, 0);
+    if (n) {
+        HIPCHK(hipMemcpy(nc.data(), r.buf[SB_NCIG], n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(st.data(), r.buf[SB_STATUS], n * 4, hipMemcpyDeviceToHost));
+    }
+    std::vector<int64_t> off(n + 1, 0);
+    for (size_t t = 0; t < n; ++t) off[t + 1] = off[t] + (st[t] == 0 ? nc[t] : 0);
+    if (o->cigar_off) std::memcpy(o->cigar_off, off.data(), (n + 1) * 8);
+    if (!o->cigar) return 0;
+    if (off[n] > o->cigar_cap) return pr_set_error(PR_ERR_CAPACITY, "pr_sw_out.cigar_cap below the CIGAR total");
+    if (!off[n]) return 0;
+    if ((rc = up(r, SB_CIGOFF, off.data(), n + 1, s)) || (rc = ensure(r, SB_CIGOUT, (size_t)off[n] * 4))) return rc;
+    int e = sw_launch_cig_compact((const uint32_t *)r.buf[SB_CIG], (const int64_t *)r.buf[SB_CIGAT],
+                                  (const int32_t *)r.buf[SB_NCIG], (const int64_t *)r.buf[SB_CIGOFF], (int64_t)n,
+                                  (uint32_t *)r.buf[SB_CIGOUT], (void *)s);
+    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    HIPCHK(hipMemcpyAsync(o->cigar, r.buf[SB_CIGOUT], (size_t)off[n] * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" int pr_sw_cigar_total(pr_ctx *c, int64_t *total, int64_t *n_overflow) {
+    if (!c || !total) return pr_set_error(PR_ERR_ARG, "null arg");
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    HIPCHK(hipStreamSynchronize(ctx_stream(c)));
+    const size_t n = (size_t)r.n_task;
+    std::vector<int32_t> nc(n + 1, 0), st(n + 1, 0);
+    if (n) {
+        HIPCHK(hipMemcpy(nc.data(), r.buf[SB_NCIG], n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(st.data(), r.buf[SB_STATUS], n * 4, hipMemcpyDeviceToHost));
+    }
+    int64_t tot = 0;
+    for (size_t t = 0; t < n; ++t) tot += st[t] == 0 ? nc[t] : 0;
+    *total = tot;
+    if (n_overflow) *n_overflow = r.n_overflow;
     return 0;
 }
 
@@ -321,6 +416,7 @@ int sw_get_ptrs(pr_ctx *c, SwPtrs *p) {
     p->score = (const int32_t *)r.buf[SB_SCORE];
     p->ncig = (const int32_t *)r.buf[SB_NCIG];
     p->cig = (const uint32_t *)r.buf[SB_CIG];
+    p->cig_at = (const int64_t *)r.buf[SB_CIGAT];
     p->n_task = r.n_task;
     p->n_sr = (int)r.n_sr;
     p->n_lr = (int)r.n_lr;

@@ -3,9 +3,25 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#ifdef __HIPCC__
+#define SW_HD __host__ __device__
+#else
+#define SW_HD   // the host-compiled kernel-core tests (tests/native) include this header with g++
+#endif
+
 namespace prgpu {
 
-constexpr int SW_MAXCIG = 128;   // CIGAR ops per task (PR_SW_MAXCIG)
+// CIGAR output: every task owns a slot sized from its short-read length (cig_slot_ops;
+// >= 99.7 % of 150 bp CIGARs at 15 % long-read error fit) in one pool; a CIGAR that
+// outgrows its slot marks the task SW_ST_OVERFLOW and the overflow pass recomputes it
+// into a spill area of the same pool, bounded by its aligned lengths (every op consumes
+// at least one query or reference base).  o_cig_at[t] is where the task's ops start.
+constexpr int SW_ST_OVERFLOW = 1;     // internal status, resolved before pr_sw_launch returns
+SW_HD inline int cig_slot_ops(int lq) {
+    const int c = (lq * 2 / 5 + 8 + 7) & ~7;
+    return c > 16 ? c : 16;
+}
+SW_HD inline int cig_bound_ops(int lqq, int rlen) { return lqq + rlen + 4; }
 constexpr int SW_WAVE = 64;
 constexpr int SW_NBUCKET = 1024;      // task-ordering keys (query lengths <= 1000)
 constexpr int PK_NB = 41 * 256;       // packed-kernel keys: band (<= 40) x query length (<= 255)
@@ -34,7 +50,14 @@ struct SwDev {
     uint8_t *o_pass;
     // global / CIGAR results
     int32_t *o_gscore, *o_pos, *o_ncig, *o_status;
-    uint32_t *o_cig;           // n_task * SW_MAXCIG
+    uint32_t *o_cig;           // CIGAR pool: the slots (cig_slot prefix), then the spill area
+    const int64_t *cig_slot;   // [n_task+1] prefix of the slot capacities
+    int64_t *o_cig_at;         // [n_task] first op of the task's CIGAR in o_cig
+    unsigned long long *spill; // [0] overflowed tasks, [1] their op bounds summed, [2] spill cursor
+    int64_t spill_base;        // first op of the spill area
+    int rerun;                 // sw_global_kernel: 1 = the overflow pass (ops at o_cig_at, bounded)
+    uint32_t *eh_g;            // sw_global_kernel DP row in HBM (queries too long for LDS), or null
+    int64_t eh_g_stride;       // dwords per block of eh_g
     uint8_t *z;                // direction-matrix slabs, one per resident block
     int64_t z_slab;            // bytes per slab (LDS kernel)
     int64_t z_ring_slab;       // dwords per slab (register-ring kernels: rows x words x 64 lanes)
@@ -54,8 +77,10 @@ struct SwResident {
     bool loaded = false;
     int64_t n_task = 0, n_sr = 0, n_lr = 0;
     int qmax = 0;
-    void *buf[32] = {};
-    size_t cap[32] = {};
+    void *buf[40] = {};
+    size_t cap[40] = {};
+    int64_t cig_slots = 0;      // ops in the slots (= first spill op)
+    int64_t n_overflow = 0;     // tasks of the last launch whose CIGAR went to the spill area
     float ms_ext = 0.f, ms_glob = 0.f;
     unsigned long long cells[3] = {0, 0, 0};
     float ms_glob_ring = 0.f;
@@ -67,6 +92,7 @@ struct SwPtrs {
     const int64_t *sr_off, *lr_off;
     const int32_t *t_sr, *t_lr, *status, *pos, *score, *ncig;
     const uint32_t *cig;
+    const int64_t *cig_at;
     int64_t n_task;
     int n_sr, n_lr;
 };
@@ -75,6 +101,10 @@ int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out,
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream);
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
                      void *stream, void *ev_a, void *ev_b);
+int sw_launch_lds(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
+int sw_launch_overflow(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
+int sw_launch_cig_compact(const uint32_t *pool, const int64_t *at, const int32_t *ncig, const int64_t *off,
+                          int64_t n, uint32_t *out, void *stream);
 void sw_release(SwResident &r);
 
 }  // namespace prgpu

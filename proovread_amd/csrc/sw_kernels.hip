@@ -398,19 +398,49 @@ __device__ int ksw_global_lane(uint32_t *eh, const uint8_t *qv /* lane query (8*
     return gh(eh[qlen * SW_WAVE]);
 }
 
-__device__ __forceinline__ int push_op(uint32_t *cg, int n, int op, int len) {
+__device__ __forceinline__ int push_op(uint32_t *cg, int n, int op, int len, int cap) {
+    if (n < 0) return n;
     if (n > 0 && (int)(cg[n - 1] & 0xFu) == op) {
         cg[n - 1] += (uint32_t)len << 4;
         return n;
     }
-    if (n >= SW_MAXCIG) return -1;
+    if (n >= cap) return -1;
     cg[n] = ((uint32_t)len << 4) | (uint32_t)op;
     return n + 1;
 }
 
+// the task's CIGAR destination and capacity: its slot, or (overflow pass) its spill range
+__device__ __forceinline__ uint32_t *cig_dest(const SwDev &D, int64_t t, int &cap) {
+    if (D.rerun) {
+        cap = cig_bound_ops(D.o_qe[t] - D.o_qb[t], D.o_re[t] - D.o_rb[t]);
+        return D.o_cig + D.o_cig_at[t];
+    }
+    const int64_t a = D.cig_slot[t];
+    cap = (int)(D.cig_slot[t + 1] - a);
+    return D.o_cig + a;
+}
+
+// a CIGAR longer than its slot: the overflow pass recomputes the task into the spill area
+__device__ __forceinline__ void cig_overflow(const SwDev &D, int64_t t) {
+    if (D.rerun) {   // cannot happen: the spill range bounds every op sequence of the task
+        D.o_status[t] = -9;
+        D.o_ncig[t] = 0;
+        return;
+    }
+    D.o_status[t] = SW_ST_OVERFLOW;
+    D.x_try[t] = (uint8_t)(D.x_try[t] | 0x20);
+    atomicAdd(&D.spill[0], 1ull);
+    atomicAdd(&D.spill[1], (unsigned long long)cig_bound_ops(D.o_qe[t] - D.o_qb[t], D.o_re[t] - D.o_rb[t]));
+}
+
 // mem_reg2aln after ksw_global2: position, leading/trailing D squeeze, soft clips
-__device__ __forceinline__ void glob_emit(const SwDev &D, int64_t t, uint32_t *cg, int n, int status, int gsc,
+// (n < 0: the backtrack outgrew cap)
+__device__ __forceinline__ void glob_emit(const SwDev &D, int64_t t, uint32_t *cg, int n, int cap, int gsc,
                                           bool rev, int lq, int L, int qb, int qe, int rb, int re) {
+    if (n < 0) {
+        cig_overflow(D, t);
+        return;
+    }
     int pos = rev ? L - re : rb;
     if (n > 0) {
         if ((cg[0] & 0xFu) == 2u) {
@@ -424,8 +454,9 @@ __device__ __forceinline__ void glob_emit(const SwDev &D, int64_t t, uint32_t *c
     if (qb != 0 || qe != lq) {
         const int clip5 = rev ? lq - qe : qb;
         const int clip3 = rev ? qb : lq - qe;
-        if (n + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > SW_MAXCIG) {
-            status = -9;
+        if (n + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > cap) {
+            cig_overflow(D, t);
+            return;
         } else {
             if (clip5) {
                 for (int x = n; x > 0; --x) cg[x] = cg[x - 1];
@@ -438,7 +469,7 @@ __device__ __forceinline__ void glob_emit(const SwDev &D, int64_t t, uint32_t *c
     D.o_gscore[t] = gsc;
     D.o_pos[t] = pos;
     D.o_ncig[t] = n;
-    D.o_status[t] = status;
+    D.o_status[t] = 0;
 }
 
 // band of one ksw_global2 pass (mem_reg2aln/bwa_gen_cigar2); -1: empty query or
@@ -487,13 +518,18 @@ __device__ __forceinline__ int pk_key(const SwDev &D, const SwOptsDev &O, int64_
     return ww * 256 + lqq;
 }
 
+// The general CIGAR pass (any band, N bases, the whole bwa_gen_cigar2 loop).  HBM = true:
+// the DP row and query live in a per-block HBM scratch instead of LDS (queries too long for
+// the 160 KB LDS; same [column][lane] layout, coalesced).
+template <bool HBM>
 __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_g[];
     __shared__ int s_task;
     const int lane = threadIdx.x;
     const int qpad = (D.qmax + 8) & ~3;
-    uint32_t *eh = lds_g + lane;
-    uint8_t *qv = reinterpret_cast<uint8_t *>(lds_g + (D.qmax + 1) * SW_WAVE) + lane * qpad;
+    uint32_t *base = HBM ? D.eh_g + (int64_t)blockIdx.x * D.eh_g_stride : lds_g;
+    uint32_t *eh = base + lane;
+    uint8_t *qv = reinterpret_cast<uint8_t *>(base + (D.qmax + 1) * SW_WAVE) + lane * qpad;
     const int nc4 = (D.qmax + 3) >> 2;
     uint32_t *zl = reinterpret_cast<uint32_t *>(D.z + (int64_t)blockIdx.x * D.z_slab) + lane;
     unsigned long long cells = 0;
@@ -528,8 +564,8 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
             if (w2 > O.w) w2 = w2 < wreg ? w2 : wreg;
             int last_sc = -(1 << 30), gsc = 0, iter = 0, ww = 0;
             bool nogap = false;
-            uint32_t *cg = D.o_cig + t * SW_MAXCIG;
-            int status = 0;
+            int cap = 0;
+            uint32_t *cg = cig_dest(D, t, cap);
             unsigned long long cpass = 0;
             do {
                 w2 = w2 < O.w << 2 ? w2 : O.w << 2;
@@ -576,20 +612,19 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_kernel(SwDev D, SwOptsDev O
                     const int jj = k - (i > ww ? i - ww : 0);
                     const uint32_t zw = zl[((long)i * nc4 + (jj >> 2)) * SW_WAVE];
                     which = ((zw >> ((jj & 3) << 3)) >> (which << 1)) & 3;
-                    if (which == 0) n = push_op(cg, n, 0, 1), --i, --k;
-                    else if (which == 1) n = push_op(cg, n, 2, 1), --i;
-                    else n = push_op(cg, n, 1, 1), --k;
+                    if (which == 0) n = push_op(cg, n, 0, 1, cap), --i, --k;
+                    else if (which == 1) n = push_op(cg, n, 2, 1, cap), --i;
+                    else n = push_op(cg, n, 1, 1, cap), --k;
                 }
-                if (n >= 0 && i >= 0) n = push_op(cg, n, 2, i + 1);
-                if (n >= 0 && k >= 0) n = push_op(cg, n, 1, k + 1);
-                if (n < 0) { status = -9; n = 0; }
+                if (i >= 0) n = push_op(cg, n, 2, i + 1, cap);
+                if (k >= 0) n = push_op(cg, n, 1, k + 1, cap);
                 for (int x = 0; x < n >> 1; ++x) {
                     const uint32_t tmp = cg[x];
                     cg[x] = cg[n - 1 - x];
                     cg[n - 1 - x] = tmp;
                 }
             }
-            glob_emit(D, t, cg, n, status, gsc, rev, lq, L, qb, qe, rb, re);
+            glob_emit(D, t, cg, n, cap, gsc, rev, lq, L, qb, qe, rb, re);
         }
     }
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
@@ -648,8 +683,9 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
             D.x_try[t] = (uint8_t)(D.x_try[t] | 4);
             continue;
         }
-        uint32_t *cg = D.o_cig + t * SW_MAXCIG;
-        int nc = 0, status = 0;
+        int cap = 0;
+        uint32_t *cg = cig_dest(D, t, cap);
+        int nc = 0;
         if (ww < 0) {
             nc = 0;
         } else if (!dp || (O.debug & 1)) {
@@ -657,15 +693,14 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
             nc = 1;
         } else {
             cells += band_cells(rlen, lqq, ww);
-            nc = glob_backtrack<WB>(zl, SW_WAVE, rlen, lqq, ww, cg, SW_MAXCIG);
-            if (nc < 0) { status = -9; nc = 0; }
+            nc = glob_backtrack<WB>(zl, SW_WAVE, rlen, lqq, ww, cg, cap);
             for (int x = 0; x < nc >> 1; ++x) {
                 const uint32_t tmp = cg[x];
                 cg[x] = cg[nc - 1 - x];
                 cg[nc - 1 - x] = tmp;
             }
         }
-        glob_emit(D, t, cg, nc, status, gsc, rev, lq, L, qb, qe, rb, re);
+        glob_emit(D, t, cg, nc, cap, gsc, rev, lq, L, qb, qe, rb, re);
     }
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
     if (lane == 0 && cells) {
@@ -734,7 +769,7 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
         nflag |= qn;
         // (the masks are dead from here on)
         uint32_t *cg[2] = {nullptr, nullptr};
-        int tl[2] = {0, 0};
+        int tl[2] = {0, 0}, cap[2] = {0, 0};
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int64_t t = tt[h];
@@ -745,7 +780,7 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
                 D.x_try[t] = (uint8_t)(D.x_try[t] | 4);
                 continue;
             }
-            cg[h] = D.o_cig + t * SW_MAXCIG;
+            cg[h] = cig_dest(D, t, cap[h]);
             tl[h] = rlen;
         }
         int nc[2] = {0, 0};
@@ -755,9 +790,9 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
         if (O.debug & 1) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
-                if (cg[h]) cg[h][SW_MAXCIG - 1] = fst[h] = lst[h] = ((uint32_t)lqq << 4), nc[h] = 1;
+                if (cg[h]) cg[h][cap[h] - 1] = fst[h] = lst[h] = ((uint32_t)lqq << 4), nc[h] = 1;
         } else {
-            pk_backtrack2(zl, SW_WAVE, npair, nrow, tl, lqq, ww, cg, nc, fst, lst, SW_MAXCIG);
+            pk_backtrack2(zl, SW_WAVE, npair, nrow, tl, lqq, ww, cg, nc, fst, lst, cap);
         }
         unsigned long long c3 = clock64();
         ph[2] += c3 - c2;
@@ -771,9 +806,13 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
             const int qb = D.o_qb[t], qe = D.o_qe[t], rb = D.o_rb[t], re = D.o_re[t];
             const bool rev = H[h].comp;
             // mem_reg2aln after ksw_global2 (glob_emit's rules) on the forward-ordered ops at the slots' end
-            int status = 0, m = nc[h], src = SW_MAXCIG - nc[h];
+            int m = nc[h], src = cap[h] - nc[h];
             int pos = rev ? L - re : rb;
-            if (m < 0) { status = -9; m = 0; src = SW_MAXCIG; }
+            cells += band_cells(tl[h], lqq, ww);
+            if (m < 0) {
+                cig_overflow(D, t);
+                continue;
+            }
             if (m > 0) {
                 if ((fst[h] & 0xFu) == 2u) {
                     pos += (int)(fst[h] >> 4);
@@ -786,17 +825,19 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
             if (qb != 0 || qe != lq) {
                 clip5 = rev ? lq - qe : qb;
                 clip3 = rev ? qb : lq - qe;
-                if (m + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > SW_MAXCIG) status = -9, clip5 = clip3 = 0;
+                if (m + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > cap[h]) {
+                    cig_overflow(D, t);
+                    continue;
+                }
             }
             const int d0 = clip5 ? 1 : 0;
             pk_cig_move(cg[h], d0, src, m);
             if (clip5) cg[h][0] = ((uint32_t)clip5 << 4) | 4u;
             if (clip3) cg[h][d0 + m] = ((uint32_t)clip3 << 4) | 4u;
-            cells += band_cells(tl[h], lqq, ww);
             D.o_gscore[t] = sc[h];
             D.o_pos[t] = pos;
             D.o_ncig[t] = d0 + m + (clip3 ? 1 : 0);
-            D.o_status[t] = status;
+            D.o_status[t] = 0;
         }
         ph[3] += clock64() - c3;
     }
@@ -898,6 +939,7 @@ __device__ __forceinline__ int sw_phase_key(const SwDev &D, const SwOptsDev &O, 
         case 5: return (glob_class(D, O, t) == 0 && pk_key(D, O, t) < 0) ? D.o_qe[t] - D.o_qb[t] : -1;
         case 6: return glob_class(D, O, t) == 1 ? D.o_qe[t] - D.o_qb[t] : -1;
         case 7: return (glob_class(D, O, t) == 2 || (D.x_try[t] & 4)) ? D.o_qe[t] - D.o_qb[t] : -1;
+        case 8: return (D.x_try[t] & 0x20) ? D.o_qe[t] - D.o_qb[t] : -1;   // CIGAR overflow pass
         default: return -1;
     }
 }
@@ -1016,10 +1058,62 @@ int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
     if ((rc = sw_launch_order(D, O, 6, D.list, stream))) return rc;
     hipLaunchKernelGGL(sw_global_ring_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
     if ((rc = sw_launch_order(D, O, 7, D.list, stream))) return rc;
-    hipError_t e = hipFuncSetAttribute((const void *)sw_global_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    return sw_launch_lds(D, O, grid_lds, lds, stream);
+}
+
+// the general CIGAR kernel over the current task list (LDS row, or HBM row when D.eh_g)
+int sw_launch_lds(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (D.eh_g) {
+        hipLaunchKernelGGL(sw_global_kernel<true>, dim3(grid), dim3(SW_WAVE), 0, s, D, O);
+        return (int)hipGetLastError();
+    }
+    hipError_t e = hipFuncSetAttribute((const void *)sw_global_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return (int)e;
-    hipLaunchKernelGGL(sw_global_kernel, dim3(grid_lds), dim3(SW_WAVE), lds, s, D, O);
+    hipLaunchKernelGGL(sw_global_kernel<false>, dim3(grid), dim3(SW_WAVE), lds, s, D, O);
     return (int)hipGetLastError();
+}
+
+// spill ranges of the overflowed tasks (bump allocation; placement order does not matter)
+__global__ void __launch_bounds__(256) sw_spill_assign_kernel(SwDev D) {
+    const int n = D.list_n[0];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = D.list[i];
+        const unsigned long long b = (unsigned long long)cig_bound_ops(D.o_qe[t] - D.o_qb[t], D.o_re[t] - D.o_rb[t]);
+        D.o_cig_at[t] = D.spill_base + (int64_t)atomicAdd(&D.spill[2], b);
+    }
+}
+
+// compaction of the tasks' CIGARs into one pool in task order (pr_sw_download)
+__global__ void __launch_bounds__(256) sw_cig_compact_kernel(const uint32_t *pool, const int64_t *at,
+                                                             const int32_t *ncig, const int64_t *off, int64_t n,
+                                                             uint32_t *out) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t *src = pool + at[t];
+        uint32_t *dst = out + off[t];
+        const int m = (int)(off[t + 1] - off[t]);
+        for (int k = 0; k < m; ++k) dst[k] = src[k];
+    }
+}
+int sw_launch_cig_compact(const uint32_t *pool, const int64_t *at, const int32_t *ncig, const int64_t *off,
+                          int64_t n, uint32_t *out, void *stream) {
+    int grid = (int)((n + 255) / 256);
+    grid = grid < 4096 ? (grid > 0 ? grid : 1) : 4096;
+    hipLaunchKernelGGL(sw_cig_compact_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, pool, at, ncig, off, n, out);
+    return (int)hipGetLastError();
+}
+
+// the overflow pass: list the overflowed tasks, give them spill ranges, rerun their CIGAR loop
+int sw_launch_overflow(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    int rc;
+    if ((rc = sw_launch_order(D, O, 8, D.list, stream))) return rc;
+    hipLaunchKernelGGL(sw_spill_assign_kernel, dim3(256), dim3(256), 0, s, D);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    SwDev R = D;
+    R.rerun = 1;
+    return sw_launch_lds(R, O, grid, lds, stream);
 }
 
 

@@ -565,17 +565,18 @@ SW_RING_FN int glob_pk_backtrack(const PkDir *z, int ZS, int npair, int hb, int 
 // indexing); a step whose slot left the loaded pair reads its word directly.
 // The current op run stays in registers and every finished run is stored once,
 // from the END of the task's CIGAR slots backwards: the ops land in final
-// (forward) order at cg[maxcig - n, maxcig).  n[h] = op count or -1 (more than
-// maxcig); first[h] / last[h] = the first / last op of the forward CIGAR.
+// (forward) order at cg[h][maxcig[h] - n, maxcig[h]).  n[h] = op count or -1 (more
+// than maxcig[h]); first[h] / last[h] = the first / last op of the forward CIGAR.
 SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, const int tl[2], int qlen, int w,
-                              uint32_t *const cg[2], int n[2], uint32_t first[2], uint32_t last[2], int maxcig) {
+                              uint32_t *const cg[2], int n[2], uint32_t first[2], uint32_t last[2],
+                              const int maxcig[2]) {
     int i[2], k[2], which[2] = {0, 0}, rop[2] = {-1, -1}, rln[2] = {0, 0};
     bool live[2];
     auto flush = [&](int h) {
         const uint32_t v = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
         if (n[h] == 0) last[h] = v;
         first[h] = v;
-        cg[h][maxcig - 1 - n[h]++] = v;
+        cg[h][maxcig[h] - 1 - n[h]++] = v;
     };
     // ksw's push with the last op kept in registers: false when the op count would exceed maxcig
     auto push = [&](int h, int op, int len) -> bool {
@@ -584,7 +585,7 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
             return true;
         }
         if (rop[h] >= 0) {
-            if (n[h] + 1 >= maxcig) return false;
+            if (n[h] + 1 >= maxcig[h]) return false;
             flush(h);
         }
         rop[h] = op;

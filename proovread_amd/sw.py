@@ -37,11 +37,8 @@ class SwBatch(C.Structure):
 
 class SwOut(C.Structure):
     _fields_ = [("qb", _abi.P32), ("qe", _abi.P32), ("rb", _abi.P32), ("re", _abi.P32), ("score", _abi.P32),
-                ("truesc", _abi.P32), ("pos", _abi.P32), ("ncigar", _abi.P32), ("cigar", _abi.PU32),
-                ("pass_", _abi.PU8), ("status", _abi.P32)]
-
-
-MAXCIG = 128
+                ("truesc", _abi.P32), ("pos", _abi.P32), ("ncigar", _abi.P32), ("pass_", _abi.PU8),
+                ("status", _abi.P32), ("cigar_off", _abi.P64), ("cigar", _abi.PU32), ("cigar_cap", C.c_int64)]
 
 
 def _setup(L):
@@ -56,6 +53,7 @@ def _setup(L):
     L.pr_sw_last_cells.argtypes = [C.c_void_p, _abi.P64, _abi.P64]
     L.pr_sw_dominant_kernel.argtypes = [C.c_void_p, _abi.PD, _abi.P64]
     L.pr_sw_phase_cycles.argtypes = [C.c_void_p, _abi.P64]
+    L.pr_sw_cigar_total.argtypes = [C.c_void_p, _abi.P64, _abi.P64]
     L._sw_ready = True
 
 
@@ -100,27 +98,38 @@ class SwInput:
 
 
 class SwResult:
+    """Per-task outputs; CIGARs variable length, compacted in task order (cigar_off prefix)."""
+
     def __init__(self, n: int):
         self.a = {k: np.zeros(max(n, 1), np.int32) for k in
                   ("qb", "qe", "rb", "re", "score", "truesc", "pos", "ncigar", "status")}
         self.a["pass"] = np.zeros(max(n, 1), np.uint8)
-        self.a["cigar"] = np.zeros(max(n, 1) * MAXCIG, np.uint32)
+        self.a["cigar_off"] = np.zeros(n + 1, np.int64)
+        self.a["cigar"] = np.zeros(1, np.uint32)
         o = SwOut()
         P = _abi.ptr
         for k in ("qb", "qe", "rb", "re", "score", "truesc", "pos", "ncigar", "status"):
             setattr(o, k, P(self.a[k], C.c_int32))
         o.pass_ = P(self.a["pass"], C.c_uint8)
-        o.cigar = P(self.a["cigar"], C.c_uint32)
+        o.cigar_off = P(self.a["cigar_off"], C.c_int64)
         self.c = o
         self.n = n
+        self.n_overflow = 0
+
+    def size_cigar(self, total: int):
+        self.a["cigar"] = np.zeros(max(total, 1), np.uint32)
+        self.c.cigar = _abi.ptr(self.a["cigar"], C.c_uint32)
+        self.c.cigar_cap = total
 
     def __getitem__(self, k):
-        return self.a[k][: self.n]
+        return self.a[k][: self.n] if k not in ("cigar", "cigar_off") else self.a[k]
+
+    def cigar_ops(self, t: int) -> np.ndarray:
+        o = self.a["cigar_off"]
+        return self.a["cigar"][int(o[t]):int(o[t + 1])]
 
     def cigar_str(self, t: int) -> str:
-        n = int(self.a["ncigar"][t])
-        ops = self.a["cigar"][t * MAXCIG: t * MAXCIG + n]
-        return "".join(f"{int(x) >> 4}{'MIDNSHP=X'[int(x) & 15]}" for x in ops)
+        return "".join(f"{int(x) >> 4}{'MIDNSHP=X'[int(x) & 15]}" for x in self.cigar_ops(t))
 
 
 def run(inp: SwInput, opts: Optional[SwOpts] = None, ctx: Optional[_abi.Context] = None) -> SwResult:
@@ -130,7 +139,13 @@ def run(inp: SwInput, opts: Optional[SwOpts] = None, ctx: Optional[_abi.Context]
     opts = opts or default_opts()
     b = inp.c_batch()
     res = SwResult(len(inp.t_sr))
-    _abi.check(L.pr_sw_run(ctx.h, C.byref(opts), C.byref(b), C.byref(res.c)), "pr_sw_run")
+    _abi.check(L.pr_sw_upload(ctx.h, C.byref(b)), "pr_sw_upload")
+    _abi.check(L.pr_sw_launch(ctx.h, C.byref(opts)), "pr_sw_launch")
+    tot, nov = C.c_int64(), C.c_int64()
+    _abi.check(L.pr_sw_cigar_total(ctx.h, C.byref(tot), C.byref(nov)), "pr_sw_cigar_total")
+    res.size_cigar(tot.value)
+    res.n_overflow = nov.value
+    _abi.check(L.pr_sw_download(ctx.h, C.byref(res.c)), "pr_sw_download")
     return res
 
 

@@ -80,7 +80,8 @@ extern "C" int pk_global(int a, int b, int o_del, int e_del, int o_ins, int e_in
     uint32_t *cg2[2] = {A.tlen > 0 ? cig : nullptr, B.tlen > 0 ? cig + max_cigar : nullptr};
     int n2[2] = {0, 0};
     uint32_t fst[2], lst[2];
-    pk_backtrack2(z, 1, npair, nrow, tl2, qlen, w, cg2, n2, fst, lst, max_cigar);
+    const int caps[2] = {max_cigar, max_cigar};
+    pk_backtrack2(z, 1, npair, nrow, tl2, qlen, w, cg2, n2, fst, lst, caps);
     for (int h = 0; h < 2; ++h)   // forward order at the slots' end -> reverse order at the start (plain walk's)
         if (cg2[h] && n2[h] > 0) {
             if (fst[h] != cg2[h][max_cigar - n2[h]] || lst[h] != cg2[h][max_cigar - 1]) { delete[] z; return -2000 - h; }

@@ -136,7 +136,7 @@ class OswOpts(C.Structure):
 class OswResult(C.Structure):
     _fields_ = [("qb", C.c_int), ("qe", C.c_int), ("rb", C.c_int), ("re", C.c_int),
                 ("score", C.c_int), ("truesc", C.c_int), ("w", C.c_int), ("global_score", C.c_int),
-                ("w2", C.c_int), ("pos", C.c_int), ("n_cigar", C.c_int), ("cigar", C.c_uint32 * 512),
+                ("w2", C.c_int), ("pos", C.c_int), ("n_cigar", C.c_int), ("cigar", C.c_uint32 * 4096),
                 ("pass", C.c_int)]
 
 

@@ -13,10 +13,14 @@ from pipeline_oracle import consensus_cases, sam_for_tasks
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("seeds", ["truth", "host"])
+@pytest.mark.parametrize("seeds", ["truth", "host", "truth-slot16"])
 @pytest.mark.parametrize("finish", [False, True])
-def test_iteration_matches_cpu_chain(finish, seeds):
+def test_iteration_matches_cpu_chain(finish, seeds, monkeypatch):
+    """truth-slot16: CIGAR slots forced to 16 ops, so most alignments reach the consensus
+    through the overflow pass's spill area (the hand-off reads per-task CIGAR starts)."""
     from proovread_amd import cns, iteration, seed, sw, synth
+    if seeds.endswith("slot16"):
+        monkeypatch.setenv("PRGPU_SW_CIG_SLOT", "16")
     d = synth.simulate(31 + finish, 40000, 40, 2500, 15, sr_frac=1.0)
     if seeds == "host":
         ix = seed.SeedIndex(d.lr_seq, d.lr_off)

@@ -1,9 +1,10 @@
 """Edge cases of the seed-extension stage on the GPU against the SW oracle:
-ragged short-read lengths in one batch (36 .. 509 bp: the packed kernels' per-length
-buckets, the 255 bp packed-frame limit, the 32-bit ring / LDS kernels beyond it, up to
-the LDS CIGAR kernel's 509 bp layout limit; longer reads fail loudly), N bases in short
-and long reads, and an empty task list.  Same bar as test_sw_gpu.py:
-bit-exact qb/qe/rb/re, AS, truesc, POS, CIGAR and the -T pass flag."""
+ragged short-read lengths in one batch (36 .. 1000 bp: the packed kernels' per-length
+buckets, the 255 bp packed-frame limit, the 32-bit ring / LDS kernels beyond it, the
+general CIGAR kernel's HBM row past ~500 bp, up to proovread's 1000 bp short-read limit,
+bin/proovread:457; longer reads fail loudly), N bases in short and long reads, CIGARs
+longer than their slots (the overflow pass), and an empty task list.  Same bar as
+test_sw_gpu.py: bit-exact qb/qe/rb/re, AS, truesc, POS, CIGAR and the -T pass flag."""
 import dataclasses
 
 import numpy as np
@@ -12,7 +13,7 @@ import pytest
 import oracle_bind as ob
 from sw_util import gpu_tuple, oracle_results
 
-LENGTHS = (36, 76, 100, 151, 250, 255, 256, 300, 400, 509)
+LENGTHS = (36, 76, 100, 151, 250, 255, 256, 300, 400, 509, 600, 800, 1000)
 
 
 def merge(parts):
@@ -37,7 +38,7 @@ def merge(parts):
 
 def ragged(seed=40):
     from proovread_amd import synth
-    parts = [synth.simulate(seed + i, 40000, 8, 4000, 6.0 if L < 300 else 3.0, sr_len=L)
+    parts = [synth.simulate(seed + i, 40000, 8, 4000, 6.0 if L < 300 else (3.0 if L < 600 else 2.0), sr_len=L)
              for i, L in enumerate(LENGTHS)]
     d = merge(parts)
     rng = np.random.default_rng(seed)
@@ -84,8 +85,25 @@ def test_sw_gpu_empty_task_list():
 
 
 @pytest.mark.gpu
-def test_sw_gpu_rejects_reads_beyond_lds_layout():
+def test_sw_gpu_rejects_reads_beyond_proovread_limit():
     from proovread_amd import sw, synth
-    d = synth.simulate(4, 20000, 4, 3000, 3.0, sr_len=510)
-    with pytest.raises(RuntimeError, match="too long"):
+    d = synth.simulate(4, 20000, 4, 3000, 3.0, sr_len=1001)
+    with pytest.raises(RuntimeError, match="longer than 1000"):
         sw.run(d.sw_input(), sw.default_opts(finish=False))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("task", ["bwa-sr", "bwa-sr-finish"])
+def test_sw_gpu_cigar_overflow_pass(task, monkeypatch):
+    """Every slot forced to 16 ops (PRGPU_SW_CIG_SLOT): most CIGARs outgrow their slot and go
+    through the overflow pass (spill area, general kernel); results stay bit-exact."""
+    from proovread_amd import sw, synth
+    monkeypatch.setenv("PRGPU_SW_CIG_SLOT", "16")
+    d = synth.simulate(8, 60000, 20, 3000, 10.0, sr_frac=1.0)
+    res = sw.run(d.sw_input(), sw.default_opts(finish=task.endswith("finish")))
+    assert (res["status"] == 0).all()
+    assert res.n_overflow > len(d.t_sr) // 4
+    idx = np.arange(0, len(d.t_sr), max(1, len(d.t_sr) // 400))
+    want = oracle_results(d, ob.sw_opts(task), idx)
+    bad = [(int(t), w, gpu_tuple(res, t)) for t, w in zip(idx, want) if tuple(w) != gpu_tuple(res, t)]
+    assert not bad, bad[:3]
