@@ -68,13 +68,16 @@ struct CnsDev {
     uint8_t *kept;       // per alignment
     int64_t *bin_off;    // [n_lr+1] prefix of bins
     int64_t *bin_bases;  // per bin
-    int32_t *work;       // [1] dequeue counter
-    // expanded pileup (per resident workgroup): one state code per (alignment, column)
-    uint32_t *e_pool;    // [grid * e_cap]  SEQ position of a single-base state, E_DEL, E_INS|slot
-    int64_t e_cap;
-    int4 *k_pool;        // [grid * k_cap * 2] kept alignments by start window:
-                         //   {rpos, end, E offset, lseq | rc<<31}, {seq_off lo, seq_off hi, -, -}
-    int32_t k_cap;
+    int32_t *work;       // [2] dequeue counters (small, large geometry)
+    // kept alignments bucketed by start window (per resident workgroup, k_cap ints each):
+    // window starts, then {rpos, end, alignment index, 0} per kept alignment
+    int32_t *k_pool;
+    int64_t k_cap;
+    // reads whose tables outgrew the small LDS geometry, rerun with the large one
+    int32_t *retry;      // [n_lr]
+    int32_t *retry_n;    // [1]
+    int force_large;     // diagnostics: every read through the large geometry (PRGPU_CNS_LARGE)
+    int debug;           // timing ablations only (PRGPU_CNS_DEBUG; outputs invalid when set)
     unsigned long long *prof;  // [CNS_NPHASE] summed wall-clock ticks per phase (may be null)
     // outputs
     const int64_t *out_off;  // [n_lr+1]
@@ -85,20 +88,17 @@ struct CnsDev {
     int32_t *o_chim;     // 4 ints per record
 };
 
-// host-side launcher (returns a hipError_t value); stream is a hipStream_t
-int cns_launch(const CnsDev &D, const CnsParamsDev &P, int grid, void *stream);
-int cns_lds_bytes();
+// host-side launcher (returns a hipError_t value); stream is a hipStream_t.  grid: small-
+// geometry workgroups (2 per CU); grid_retry: large-geometry workgroups (1 per CU)
+int cns_launch(const CnsDev &D, const CnsParamsDev &P, int grid, int grid_retry, void *stream);
 int cns_max_bins();
+int cns_k_header();      // ints of window starts reserved at the head of a K pool slice
 
-// LDS geometry of the per-long-read kernel
 constexpr int CNS_THREADS = 256;
-constexpr int TCAP = 2048;       // distinct insertion states per long read
-constexpr int WCOLS = 512;       // columns per pileup window
-constexpr int WCAP = 1024;       // (column, insertion state) pairs per window
 constexpr int CHIM_MAXCOLS = 128;
 constexpr int CHIM_TCAP = 256;
-constexpr int WLCAP = 256;       // window candidates staged in LDS per pass
-constexpr int WBCAP = 1024;      // start-window buckets (long reads up to WBCAP-1 windows)
-constexpr int CNS_NPHASE = 8;    // prep, binning, state table, scatter, argmax+write, cigar, chimera, idle
+// per-phase wall-clock ticks: prep, binning, state table, scatter, argmax+write, cigar, chimera,
+// idle; scatter detail: zero+ignore, group select, staging, walks; counts: groups, items, windows
+constexpr int CNS_NPHASE = 16;
 
 }  // namespace prgpu

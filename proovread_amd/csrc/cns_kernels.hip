@@ -90,6 +90,16 @@ struct SeqV {
         return c;
     }
 };
+// fixed-state index (A0 T1 G2 C3 -4 N5) of SEQ position s as SAM prints it, branchless for
+// nt4 pools (A0 C1 G2 T3 N4; reverse complement through the second nibble table)
+__device__ __forceinline__ int fixed_idx_at(const SeqV &v, int s) {
+    if (v.nt4) {
+        uint32_t c = v.rc ? v.p[v.n - 1 - s] : v.p[s];
+        c = c > 4u ? 4u : c;
+        return (int)(((v.rc ? 0x50321u : 0x51230u) >> (4u * c)) & 15u);
+    }
+    return fixed_idx(v[s]);
+}
 __device__ __forceinline__ uint64_t state_key(const SeqV &v, int off, int n) {
     if (n <= 19) {
         uint64_t k = (uint64_t)n << 57;
@@ -336,36 +346,67 @@ __device__ void prep_alignment(const CnsDev &D, const CnsParamsDev &P, int64_t g
 }
 
 // ---------------------------------------------------------------------------
-// LDS carve (bytes).  Everything lives in one dynamic array (G17 alignment).
-constexpr int OFF_CTRL = 0;                       // 256 B control block
-constexpr int OFF_SCAN = 256;                     // 256 x 8 B scan scratch
-constexpr int OFF_A = OFF_SCAN + 2048;            // region A: bin arrays, then state table
-constexpr int SZ_A = TCAP * 24;
-constexpr int OFF_B = OFF_A + SZ_A;               // region B: window / chimera buffers
-constexpr int B_CNT6 = 0;                                   // u32 [WCOLS*6] (scatter fallback)
-constexpr int B_WL = B_CNT6;                                // int4 [2*WLCAP] (expanded path, aliases CNT6)
-constexpr int B_WBEG = B_WL + WLCAP * 32;                   // i32 [WBCAP]    (expanded path)
-static_assert(WLCAP * 32 + WBCAP * 4 <= WCOLS * 6 * 4, "window staging fits the CNT6 area");
-static_assert(WCOLS == 2 * CNS_THREADS, "two pileup columns per thread");
-constexpr int B_WKEY = B_CNT6 + WCOLS * 6 * 4;              // u32 [WCAP]
-constexpr int B_WCNT = B_WKEY + WCAP * 4;                   // u32 [WCAP]
-constexpr int B_COLCNT = B_WCNT + WCAP * 4;                 // i32 [WCOLS]
-constexpr int B_COLST = B_COLCNT + WCOLS * 4;               // i32 [WCOLS]
-constexpr int B_ELIST = B_COLST + WCOLS * 4;                // u16 [WCAP]
-constexpr int B_CDESC = B_ELIST + WCAP * 2;                 // u32 [WCOLS]
-constexpr int B_COUT = B_CDESC + WCOLS * 4;                 // u16 [WCOLS] out len
-constexpr int B_CPHR = B_COUT + WCOLS * 2;                  // u8  [WCOLS] phred
-constexpr int SZ_B = B_CPHR + WCOLS;
-constexpr int CNS_LDS_BYTES = OFF_B + SZ_B;
-static_assert(CNS_LDS_BYTES <= 81920, "two workgroups per CU");
-constexpr int MAX_BINS_LDS = (SZ_A - CNS_THREADS * 4) / 8;
+// LDS geometry.  One dynamic array per workgroup (16-byte aligned regions):
+//   control block + scan scratch | region A: insertion-state table | region B: window
+// buffers (fixed-state counts, (column, insertion state) counts, per-column best
+// insertion, ignore bits, work-item prefix, argmax outputs) — chimera tables alias B;
+// the binning arrays of phase 2 use A and B together.
+// Two geometries: the small one (2 workgroups per CU) takes every read first; a read
+// whose tables overflow it is rerun with the large one (1 per CU, 4x the tables).
+constexpr int SLOT_SH = 12;                 // window / chimera keys: (column + 1) << 12 | state slot
+constexpr uint32_t SLOT_MASK = (1u << SLOT_SH) - 1u;
+constexpr int CHUNK = 32;                   // columns per scatter work item
 
-// per-column descriptor: flag bits above the 11-bit state-table slot
+template <int TCAP_, int W_, int WCAP_, int SEQB_, int CIGB_, int ICAP_, int WGCU_, bool RETRY_>
+struct CnsGeo {
+    static constexpr int TCAP = TCAP_;      // distinct insertion states per read
+    static constexpr int W = W_;            // pileup window columns
+    static constexpr int WCAP = WCAP_;      // (column, insertion state) pairs per window
+    static constexpr int SEQB = SEQB_;      // staged SEQ bytes of a candidate group
+    static constexpr int CIGB = CIGB_;      // staged CIGAR ops of a candidate group (and state runs)
+    static constexpr int ICAP = ICAP_;      // insertion-state records of a candidate group
+    static constexpr int WGCU = WGCU_;      // workgroups per CU (launch bounds)
+    static constexpr bool RETRY = RETRY_;   // capacity overflows go to the retry list
+    static constexpr int OFF_CTRL = 0;
+    static constexpr int OFF_SCAN = 256;
+    static constexpr int OFF_A = OFF_SCAN + 2048;
+    static constexpr int SZ_A = TCAP * 24;
+    static constexpr int OFF_B = OFF_A + SZ_A;
+    static constexpr int B_CNT = 0;                         // u32 [3W]: A|T<<16, G|C<<16, -|N<<16
+    static constexpr int B_WKEY = B_CNT + 12 * W;           // u32 [WCAP]
+    static constexpr int B_WCNT = B_WKEY + 4 * WCAP;        // u32 [WCAP]
+    static constexpr int B_BEST = B_WCNT + 4 * WCAP;        // u64 [W] best insertion state per column
+    static constexpr int B_IGN = B_BEST + 8 * W;            // u32 [W/32] ignored columns (MCR ranges)
+    static constexpr int B_ITEM = B_IGN + W / 8;            // i32 [CNS_THREADS+1] work-item prefix
+    static constexpr int B_CSO = B_ITEM + 4 * (CNS_THREADS + 4);  // i32 [CNS_THREADS+4] staged SEQ offsets
+    static constexpr int B_COO = B_CSO + 4 * (CNS_THREADS + 4);   // i32 [CNS_THREADS+4] staged CIGAR offsets
+    static constexpr int B_CSRC = B_COO + 4 * (CNS_THREADS + 4);  // i64 [CNS_THREADS] SEQ source dword index
+    static constexpr int B_CGSRC = B_CSRC + 8 * CNS_THREADS;      // i64 [CNS_THREADS] CIGAR source index
+    static constexpr int B_CIGS = B_CGSRC + 8 * CNS_THREADS;      // u32 [CIGB] staged CIGAR ops
+    static constexpr int B_SEQS = B_CIGS + 4 * CIGB;        // u8  [SEQB] staged SEQ bytes
+    static constexpr int B_RUN = (B_SEQS + SEQB + 15) & ~15;   // int2 [CIGB] runs of fixed states
+    static constexpr int B_INS = B_RUN + 8 * CIGB;          // int2 [ICAP] insertion-state records
+    static constexpr int B_COUT = B_RUN;                    // u16 [W] out len     } argmax outputs,
+    static constexpr int B_CDESC = B_COUT + 2 * W;          // u32 [W]             } after the scatter
+    static constexpr int B_CPHR = B_CDESC + 4 * W;          // u8  [W] phred       } (alias the runs)
+    static constexpr int SZ_WIN = B_INS + 8 * ICAP;
+    static constexpr int SZ_CHIM = (CHIM_MAXCOLS * 13 + CHIM_TCAP * 4 + 16) * 4;
+    static constexpr int SZ_B = ((SZ_WIN > SZ_CHIM ? SZ_WIN : SZ_CHIM) + 15) & ~15;
+    static constexpr int LDS = OFF_B + SZ_B;
+    static constexpr int MAX_BINS = (SZ_A + SZ_B - CNS_THREADS * 4) / 8;
+    static_assert(LDS * WGCU <= 160 * 1024, "LDS per CU");
+    static_assert(TCAP <= (1 << SLOT_SH), "slots fit the key");
+    static_assert(W % CHUNK == 0 && W % CNS_THREADS == 0, "window shape");
+    static_assert(B_BEST % 8 == 0 && B_CSRC % 16 == 0 && B_RUN % 8 == 0, "alignment");
+    static_assert(B_CPHR + W <= B_INS, "argmax outputs fit the run area");
+    static_assert(W <= 1024 && CNS_THREADS <= 256, "run record fields");
+};
+using GeoS = CnsGeo<512, 512, 1024, 8192, 2048, 1024, 2, true>;
+using GeoL = CnsGeo<2048, 512, 2048, 8192, 2560, 1024, 1, false>;
+
+// per-column descriptor: flag bits above the 12-bit state-table slot
 constexpr uint32_t DESC_FIXED = 1u << 16;
 constexpr uint32_t DESC_INS = 1u << 17;
-// expanded pileup codes (per alignment and column)
-constexpr uint32_t E_INS = 0x80000000u;   // | state-table slot
-constexpr uint32_t E_DEL = 0xFFFFFFFFu;
 
 struct Ctrl {
     int lr;
@@ -375,8 +416,7 @@ struct Ctrl {
     int cand_b0, cand_b1;
     int nchim;
     int flag;
-    unsigned long long ne;          // expanded entries: total, then running offset
-    int nk, maxspan, fast, pad;
+    int nk, maxspan, nrun, nins;
 };
 
 __device__ __forceinline__ bool in_ign(const int32_t *ig, int nig, int col) {
@@ -386,39 +426,48 @@ __device__ __forceinline__ bool in_ign(const int32_t *ig, int nig, int col) {
 }
 
 // state table (region A after binning)
+template <int TCAP>
 struct STab {
     unsigned long long *key;  // TCAP
     unsigned int *ord_cns;    // TCAP (min order of non-ignored occurrences)
     unsigned int *ord_all;    // TCAP (min order of all occurrences)
     unsigned long long *exem; // TCAP  len<<48 | SEQ offset<<32 | alignment index
-};
-__device__ __forceinline__ int stab_find(const STab &T, uint64_t k) {
-    uint32_t h = key_slot_hash(k) & (TCAP - 1);
-    for (int p = 0; p < TCAP; ++p) {
-        const uint64_t x = T.key[h];
-        if (x == k) return (int)h;
-        if (x == 0) return -1;
-        h = (h + 1) & (TCAP - 1);
-    }
-    return -1;
-}
-__device__ __forceinline__ int stab_insert(const STab &T, uint64_t k, uint64_t exem) {
-    uint32_t h = key_slot_hash(k) & (TCAP - 1);
-    for (int p = 0; p < TCAP; ++p) {
-        const unsigned long long x = T.key[h];
-        if (x == k) return (int)h;
-        if (x == 0) {
-            const unsigned long long old = atomicCAS(&T.key[h], 0ULL, (unsigned long long)k);
-            if (old == 0ULL) { T.exem[h] = exem; return (int)h; }
-            if (old == k) return (int)h;
+    __device__ __forceinline__ int find(uint64_t k) const {
+        uint32_t h = key_slot_hash(k) & (TCAP - 1);
+        for (int p = 0; p < TCAP; ++p) {
+            const uint64_t x = key[h];
+            if (x == k) return (int)h;
+            if (x == 0) return -1;
+            h = (h + 1) & (TCAP - 1);
         }
-        h = (h + 1) & (TCAP - 1);
+        return -1;
     }
-    return -1;
-}
-// (column-in-window, slot) -> count, window table in region B
+    __device__ __forceinline__ int insert(uint64_t k, uint64_t ex) const {
+        uint32_t h = key_slot_hash(k) & (TCAP - 1);
+        for (int p = 0; p < TCAP; ++p) {
+            const unsigned long long x = key[h];
+            if (x == k) return (int)h;
+            if (x == 0) {
+                const unsigned long long old = atomicCAS(&key[h], 0ULL, (unsigned long long)k);
+                if (old == 0ULL) { exem[h] = ex; return (int)h; }
+                if (old == k) return (int)h;
+            }
+            h = (h + 1) & (TCAP - 1);
+        }
+        return -1;
+    }
+    // chimera-table ordering key for a slot: consensus indices first, then states first
+    // seen only in the no-ignore recompute (Seq.pm:777, 446)
+    __device__ __forceinline__ unsigned long long chim_order(int slot) const {
+        const unsigned int oc = ord_cns[slot];
+        return oc != 0xFFFFFFFFu ? (unsigned long long)oc : (1ULL << 32) | ord_all[slot];
+    }
+};
+
+// (column-in-window + 1) << SLOT_SH | slot -> count, open addressing in LDS
+template <int WCAP>
 __device__ __forceinline__ int wtab_add(uint32_t *wkey, uint32_t *wcnt, uint32_t key) {
-    uint32_t h = (key * 2654435761u) >> 22;   // 10 bits -> WCAP 1024
+    uint32_t h = (key * 2654435761u) >> (32 - __builtin_ctz(WCAP));
     for (int p = 0; p < WCAP; ++p) {
         const uint32_t x = wkey[h];
         if (x == key) { atomicAdd(&wcnt[h], 1u); return 0; }
@@ -433,13 +482,6 @@ __device__ __forceinline__ int wtab_add(uint32_t *wkey, uint32_t *wcnt, uint32_t
 
 __device__ __forceinline__ void set_err(Ctrl *C, long idx, int code) {
     atomicMin(&C->err_first, ((unsigned long long)idx << 8) | (unsigned long long)(-code));
-}
-
-// chimera-table ordering key for a state-table slot: consensus indices first,
-// then states first seen only in the no-ignore recompute (Seq.pm:777, 446)
-__device__ __forceinline__ unsigned long long chim_order(const STab &T, int slot) {
-    const unsigned int oc = T.ord_cns[slot];
-    return oc != 0xFFFFFFFFu ? (unsigned long long)oc : (1ULL << 32) | T.ord_all[slot];
 }
 
 // count of (column c, slot) in a chimera side table (0 if absent)
@@ -458,8 +500,9 @@ __device__ __forceinline__ uint32_t chim_count(const uint32_t *tk, const uint32_
 // (side 1) or their element-wise sum (side 2, the combined column of
 // Seq.pm:857-865).  Fixed states first, then insertion states in state-index
 // order (selection over the LDS tables: no per-thread arrays).
+template <int TCAP>
 __device__ double chim_hx(int side, int c, const uint32_t *f6l, const uint32_t *f6r, const uint32_t *tkl,
-                          const uint32_t *tcl, const uint32_t *tkr, const uint32_t *tcr, const STab &T) {
+                          const uint32_t *tcl, const uint32_t *tkr, const uint32_t *tcr, const STab<TCAP> &T) {
     const double l2 = log(2.0);
     double total = 0.0;
     for (int s = 0; s < 6; ++s) {
@@ -487,14 +530,14 @@ __device__ double chim_hx(int side, int c, const uint32_t *f6l, const uint32_t *
                 const uint32_t *tk = t == 0 ? tkl : tkr;
                 for (int e = 0; e < CHIM_TCAP; ++e) {
                     const uint32_t k = tk[e];
-                    if (!k || (int)(k >> 11) - 1 != c) continue;
-                    const int slot = (int)(k & 2047u);
-                    const unsigned long long o = chim_order(T, slot);
+                    if (!k || (int)(k >> SLOT_SH) - 1 != c) continue;
+                    const int slot = (int)(k & SLOT_MASK);
+                    const unsigned long long o = T.chim_order(slot);
                     if ((first || o > prev) && o < best) { best = o; bslot = slot; }
                 }
             }
             if (bslot < 0) break;
-            const uint32_t key = ((uint32_t)(c + 1) << 11) | (uint32_t)bslot;
+            const uint32_t key = ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)bslot;
             const uint32_t v = (side != 1 ? chim_count(tkl, tcl, key) : 0u) + (side != 0 ? chim_count(tkr, tcr, key) : 0u);
             if (v) {
                 if (pass == 0) total += (double)v;
@@ -511,15 +554,106 @@ __device__ double chim_hx(int side, int c, const uint32_t *f6l, const uint32_t *
 }
 
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsParamsDev P) {
+// Append slot in an LDS list for every active lane: one atomic per wave (the lanes that
+// reach the call together), ranks by lane order.
+__device__ __forceinline__ int wave_append(int *ctr) {
+    const unsigned long long m = __ballot(1);
+    const int lane = (int)__lane_id();
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(ctr, __popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + __popcll(m & ((1ULL << lane) - 1ULL));
+}
+
+// ---------------------------------------------------------------------------
+// The states of one alignment inside a pileup window [w0, w0+wn), from its staged ops
+// (walk_states' semantics, Seq.pm:396-461): single-base and '-' states as maximal runs
+// {column, length, kind, SEQ offset} (a run's states are consecutive columns and, for
+// bases, consecutive SEQ positions), multi-character states as records {column, SEQ
+// offset, length}.  Appended to LDS lists (the counts they feed commute); capacity
+// overflow sets C->flag.
+__device__ __forceinline__ void emit_window_states(const uint32_t *cg, int nop, int rpos0, int w0, int wn, int cand, int2 *runs,
+                                   int2 *insr, Ctrl *C, int runcap, int inscap) {
+    const int cmin = w0, cmax = w0 + wn;
+    int col = rpos0, qpos = 0;
+    int p_col = 0, p_kind = -1, p_qoff = 0, p_len = 0;   // the deferred (last) state
+    int r_col = 0, r_len = 0, r_kind = 0, r_q = 0;         // pending run (r_len 0: none)
+    auto flush_run = [&]() {
+        if (r_len > 0) {
+            const int k = wave_append(&C->nrun);
+            if (k < runcap) runs[k] = make_int2((r_col - w0) | (r_len << 10) | (r_kind << 20) | (cand << 21), r_q);
+            else C->flag = 1;
+        }
+        r_len = 0;
+    };
+    // a run of states [c, c + len) of one kind (bases: SEQ offsets q ..), merged into the
+    // pending run when it continues it
+    auto add_run = [&](int c, int len, int kind, int q) {
+        if (r_len > 0 && kind == r_kind && c == r_col + r_len && (kind == 1 || q == r_q + r_len)) {
+            r_len += len;
+            return;
+        }
+        flush_run();
+        r_col = c; r_len = len; r_kind = kind; r_q = kind == 0 ? q : 0;
+    };
+    auto emit_deferred = [&]() {
+        if (p_kind < 0 || p_col < cmin || p_col >= cmax) return;
+        if (p_kind == 1) add_run(p_col, 1, 1, 0);
+        else if (p_len == 1) add_run(p_col, 1, 0, p_qoff);
+        else {
+            const int k = wave_append(&C->nins);
+            if (k < inscap) insr[k] = make_int2((p_col - w0) | (cand << 10), p_qoff | (p_len << 16));
+            else C->flag = 1;
+        }
+    };
+    for (int k = 0; k < nop; ++k) {
+        const uint32_t c = cg[k];
+        const int n = (int)(c >> 4), op = (int)(c & 15u);
+        if (op == 1) {   // I
+            if (k > 0) {
+                if (p_kind == 1) { p_kind = 0; p_qoff = qpos; p_len = n; }
+                else p_len += n;
+            } else {
+                p_col = col; p_kind = 0; p_qoff = qpos; p_len = n;
+                ++col;
+            }
+            qpos += n;
+            continue;
+        }
+        if (n == 0) continue;   // split() of an empty run pushes nothing
+        emit_deferred();
+        p_kind = -1;
+        if (col > cmax) break;
+        const int kind = (op == 0) ? 0 : 1;
+        // interior states [col, col + n - 1) clipped to the window; the last one is deferred
+        const int lo = col > cmin ? col : cmin;
+        const int hi = (col + n - 1) < cmax ? (col + n - 1) : cmax;
+        if (hi > lo) add_run(lo, hi - lo, kind, qpos + (lo - col));
+        p_col = col + n - 1; p_kind = kind; p_qoff = kind == 0 ? qpos + n - 1 : 0; p_len = 1;
+        col += n;
+        if (kind == 0) qpos += n;
+    }
+    emit_deferred();
+    flush_run();
+}
+
+// ---------------------------------------------------------------------------
+// One long read per workgroup (persistent: workgroups dequeue reads).  G: LDS geometry.
+
+template <class G>
+__global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, CnsParamsDev P) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Ctrl *C = reinterpret_cast<Ctrl *>(smem + OFF_CTRL);
-    long long *scan = reinterpret_cast<long long *>(smem + OFF_SCAN);
-    uint8_t *A = smem + OFF_A;
-    uint8_t *B = smem + OFF_B;
+    Ctrl *C = reinterpret_cast<Ctrl *>(smem + G::OFF_CTRL);
+    long long *scan = reinterpret_cast<long long *>(smem + G::OFF_SCAN);
+    uint8_t *A = smem + G::OFF_A;
+    uint8_t *B = smem + G::OFF_B;
     const int tid = threadIdx.x;
+    // the reads this launch takes: all of them, or (large geometry) the retry list
+    const int n_reads = G::RETRY ? D.n_lr : D.retry_n[0];
+    int32_t *work = G::RETRY ? D.work : D.work + 1;
     // phase clock (thread 0, 100 MHz wall clock): ticks per phase summed over workgroups
-    unsigned long long pt[CNS_NPHASE] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long pt[CNS_NPHASE] = {};
     unsigned long long tlast = wall_clock64();
 #define CNS_TICK(ph)                                                      \
     do {                                                                  \
@@ -529,10 +663,21 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             tlast = t_;                                                   \
         }                                                                 \
     } while (0)
+    // a read that overflowed the small geometry's tables goes to the retry list
+#define CNS_CAP_FAIL()                                                    \
+    do {                                                                  \
+        if (tid == 0) {                                                   \
+            D.status[lr] = PR_ERR_CODE_CAP;                               \
+            D.seq_len[lr] = 0; D.trace_len[lr] = 0; D.ncigar[lr] = 0; D.nchim[lr] = 0; \
+            if (G::RETRY) D.retry[atomicAdd(D.retry_n, 1)] = lr;          \
+        }                                                                 \
+        __syncthreads();                                                  \
+    } while (0)
 
     for (;;) {
         if (tid == 0) {
-            C->lr = atomicAdd(D.work, 1);
+            const int q = atomicAdd(work, 1);
+            C->lr = q < n_reads ? (G::RETRY ? q : D.retry[q]) : -1;
             C->err_first = ~0ULL;
             C->run_seq = 0;
             C->run_trace = 0;
@@ -542,7 +687,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         __syncthreads();
         const int lr = C->lr;
         CNS_TICK(7);
-        if (lr >= D.n_lr) break;
+        if (lr < 0) break;
         const int64_t a0 = D.aln_off[lr];
         const int na = (int)(D.aln_off[lr + 1] - a0);
         const long L = (long)(D.lr_off[lr + 1] - D.lr_off[lr]);
@@ -563,7 +708,6 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             else if ((st & ST_SCORED) && (st & ST_DIV0)) set_err(C, i, PR_ERR_CODE_DIV0);
             else if ((st & ST_SCORED) && (st & ST_BINRANGE)) set_err(C, i, PR_ERR_CODE_BIN);
         }
-        if (nbins > MAX_BINS_LDS && tid == 0) set_err(C, 0, PR_ERR_CODE_CAP);
         __syncthreads();
         CNS_TICK(0);
         if (C->err_first != ~0ULL) {
@@ -572,6 +716,10 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 D.seq_len[lr] = 0; D.trace_len[lr] = 0; D.ncigar[lr] = 0; D.nchim[lr] = 0;
             }
             __syncthreads();
+            continue;
+        }
+        if (nbins > G::MAX_BINS) {   // the binning arrays do not fit this geometry's LDS
+            CNS_CAP_FAIL();
             continue;
         }
 
@@ -661,236 +809,403 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             continue;
         }
 
-        // ---- 3. insertion-state table: first-seen order (Seq.pm:446-448), and (expanded
-        //         path) every kept alignment's states written once as one code per column
-        STab T;
+        // ---- 3. insertion-state table: first-seen order (Seq.pm:446-448) of every kept
+        //         alignment's multi-character states, and the kept alignments bucketed by
+        //         the pileup window they start in (K pool of this workgroup, HBM)
+        STab<G::TCAP> T;
         T.key = reinterpret_cast<unsigned long long *>(A);
-        T.exem = T.key + TCAP;
-        T.ord_cns = reinterpret_cast<unsigned int *>(T.exem + TCAP);
-        T.ord_all = T.ord_cns + TCAP;
-        for (int h = tid; h < TCAP; h += CNS_THREADS) {
+        T.exem = T.key + G::TCAP;
+        T.ord_cns = reinterpret_cast<unsigned int *>(T.exem + G::TCAP);
+        T.ord_all = T.ord_cns + G::TCAP;
+        for (int h = tid; h < G::TCAP; h += CNS_THREADS) {
             T.key[h] = 0ULL; T.exem[h] = 0ULL; T.ord_cns[h] = 0xFFFFFFFFu; T.ord_all[h] = 0xFFFFFFFFu;
         }
-        int4 *WL = reinterpret_cast<int4 *>(B + B_WL);
-        int32_t *wbeg = reinterpret_cast<int32_t *>(B + B_WBEG);
-        int32_t *wcur = reinterpret_cast<int32_t *>(B + B_COLCNT);   // colcnt+colst: WBCAP ints
-        const int nwin = (int)((L + WCOLS - 1) / WCOLS);
-        uint32_t *E = D.e_pool ? D.e_pool + (int64_t)blockIdx.x * D.e_cap : nullptr;
-        int4 *K = D.k_pool ? D.k_pool + (int64_t)blockIdx.x * D.k_cap * 2 : nullptr;
-        if (tid == 0) { C->ne = 0ULL; C->nk = 0; C->maxspan = 0; }
-        for (int x = tid; x < WBCAP; x += CNS_THREADS) wcur[x] = 0;
+        const int nwin = (int)((L + G::W - 1) / G::W);
+        int32_t *wcur = reinterpret_cast<int32_t *>(B + G::B_CNT);   // per-window counters (<= 3W)
+        int32_t *Kh = D.k_pool + (int64_t)blockIdx.x * D.k_cap;      // [0, nwin] window starts, then entries
+        int4 *K = reinterpret_cast<int4 *>(Kh + ((nwin + 4) & ~3));
+        if (tid == 0) { C->nk = 0; C->maxspan = 0; }
+        for (int x = tid; x <= nwin && x < 3 * G::W; x += CNS_THREADS) wcur[x] = 0;
         __syncthreads();
+        if (nwin + 1 > 3 * G::W) C->flag = 1;
         for (int i = tid; i < na; i += CNS_THREADS) {
             const int64_t g = a0 + i;
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
             const int rp = D.a_rpos[g], span = D.a_end[g] - rp;
-            atomicAdd(&C->ne, (unsigned long long)span);
             atomicAdd(&C->nk, 1);
             atomicMax(&C->maxspan, span);
-            const int win = rp / WCOLS;
-            if (win < WBCAP) atomicAdd(&wcur[win], 1);
+            const int win = rp / G::W;
+            if (win < 3 * G::W) atomicAdd(&wcur[win], 1);
+            const SeqV sv = seq_view(D, g);
+            const int sb = D.a_sb[g];
+            const uint32_t *cg = D.cig + D.cig_off[g];
+            walk_states<true>(cg, D.a_cb[g], D.a_ce[g], rp, 0, 0x7fffffff,
+                              [&](int col, int sidx, int kind, int qoff, int qlen) {
+                                  const uint64_t k = state_key(sv, sb + qoff, qlen);
+                                  if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
+                                  const int h = T.insert(k, ((uint64_t)qlen << 48) | ((uint64_t)(sb + qoff) << 32) |
+                                                                (uint64_t)g);
+                                  if (h < 0) { C->flag = 1; return; }
+                                  const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
+                                  atomicMin(&T.ord_all[h], ord);
+                                  if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
+                              });
         }
         __syncthreads();
-        const bool fast = E && K && nwin + 1 <= WBCAP && C->nk <= D.k_cap && C->ne <= (unsigned long long)D.e_cap;
-        if (fast) {
-            // start-window buckets: wbeg = exclusive scan of counts (4 windows per thread)
-            long long sc = 0;
-            for (int k = 0; k < 4; ++k) { const int w = tid * 4 + k; if (w < nwin) sc += wcur[w]; }
-            long long tot;
-            long long base = block_scan_excl(sc, scan, &tot);
-            for (int k = 0; k < 4; ++k) {
-                const int w = tid * 4 + k;
-                if (w < nwin) { wbeg[w] = (int32_t)base; base += wcur[w]; wcur[w] = 0; }
-            }
-            if (tid == 0) { wbeg[nwin] = (int32_t)tot; C->ne = 0ULL; }
-            __syncthreads();
-            for (int i = tid; i < na; i += CNS_THREADS) {
-                const int64_t g = a0 + i;
-                if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
-                const int rp = D.a_rpos[g], en = D.a_end[g];
-                const int win = rp / WCOLS;
-                const int kpos = wbeg[win] + atomicAdd(&wcur[win], 1);
-                const int eoff = (int)atomicAdd(&C->ne, (unsigned long long)(en - rp));
-                const SeqV sv = seq_view(D, g);
-                const int64_t so = D.seq_off[g];
-                K[2 * kpos] = make_int4(rp, en, eoff, sv.n | (sv.rc ? (int)0x80000000 : 0));
-                K[2 * kpos + 1] = make_int4((int)(so & 0xFFFFFFFF), (int)(so >> 32), 0, 0);
-                uint32_t *Ea = E + eoff;
-                const int sb = D.a_sb[g];
-                const uint32_t *cg = D.cig + D.cig_off[g];
-                // codes: SEQ position of a single-base state (the base is read later, in the
-                // coalesced pileup), E_DEL for '-', E_INS|slot for an insertion state
-                walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, 0, 0x7fffffff,
-                                   [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                       uint32_t code;
-                                       if (kind == 1) code = E_DEL;
-                                       else if (qlen == 1) code = (uint32_t)(sb + qoff);
-                                       else {
-                                           const uint64_t k = state_key(sv, sb + qoff, qlen);
-                                           if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
-                                           const int h = stab_insert(T, k, ((uint64_t)qlen << 48) |
-                                                                               ((uint64_t)(sb + qoff) << 32) | (uint64_t)g);
-                                           if (h < 0) { C->flag = 1; return; }
-                                           const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
-                                           atomicMin(&T.ord_all[h], ord);
-                                           if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
-                                           code = E_INS | (uint32_t)h;
-                                       }
-                                       Ea[sidx] = code;
-                                   });
-            }
-        } else {
-            for (int i = tid; i < na; i += CNS_THREADS) {
-                const int64_t g = a0 + i;
-                if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
-                const SeqV sv = seq_view(D, g);
-                const int sb = D.a_sb[g];
-                const uint32_t *cg = D.cig + D.cig_off[g];
-                walk_states<true>(cg, D.a_cb[g], D.a_ce[g], D.a_rpos[g], 0, 0x7fffffff,
-                                  [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                      const uint64_t k = state_key(sv, sb + qoff, qlen);
-                                      if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
-                                      const int h = stab_insert(T, k, ((uint64_t)qlen << 48) |
-                                                                          ((uint64_t)(sb + qoff) << 32) | (uint64_t)g);
-                                      if (h < 0) { C->flag = 1; return; }
-                                      const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
-                                      atomicMin(&T.ord_all[h], ord);
-                                      if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
-                                  });
-            }
-        }
-        __syncthreads();
-        if (C->flag) {
-            if (tid == 0) {
-                D.status[lr] = PR_ERR_CODE_CAP;
-                D.seq_len[lr] = 0; D.trace_len[lr] = 0; D.ncigar[lr] = 0; D.nchim[lr] = 0;
-            }
-            __syncthreads();
+        // 16-bit fixed-state counters: at most 65535 kept alignments per read
+        if (C->flag || (int64_t)((nwin + 4) & ~3) + 4 * (int64_t)C->nk > D.k_cap || C->nk > 65535) {
+            CNS_CAP_FAIL();
             continue;
         }
-        const int wback = (C->maxspan + WCOLS - 1) / WCOLS;   // windows an alignment can reach back
-
-        CNS_TICK(2);
-        // ---- 4. windowed pileup + argmax (Seq.pm:438-461, 1568-1654)
-        uint32_t *cnt6 = reinterpret_cast<uint32_t *>(B + B_CNT6);
-        uint32_t *wkey = reinterpret_cast<uint32_t *>(B + B_WKEY);
-        uint32_t *wcnt = reinterpret_cast<uint32_t *>(B + B_WCNT);
-        int32_t *colcnt = reinterpret_cast<int32_t *>(B + B_COLCNT);
-        int32_t *colst = reinterpret_cast<int32_t *>(B + B_COLST);
-        uint16_t *elist = reinterpret_cast<uint16_t *>(B + B_ELIST);
-        uint32_t *cdesc = reinterpret_cast<uint32_t *>(B + B_CDESC);
-        uint16_t *cout_ = reinterpret_cast<uint16_t *>(B + B_COUT);
-        uint8_t *cphr = B + B_CPHR;
-        const bool use_rq = P.use_ref_qual && D.ref_seq && D.ref_qual;
-        for (long w0 = 0; w0 < L; w0 += WCOLS) {
-            const int wn = (L - w0) < WCOLS ? (int)(L - w0) : WCOLS;
-            uint32_t cnt0[6], cnt1[6];
-#pragma unroll
-            for (int s = 0; s < 6; ++s) { cnt0[s] = 0u; cnt1[s] = 0u; }
-            if (!fast)
-                for (int x = tid; x < WCOLS * 6; x += CNS_THREADS) cnt6[x] = 0u;
-            for (int x = tid; x < WCAP; x += CNS_THREADS) { wkey[x] = 0u; wcnt[x] = 0u; }
+        {   // window starts: exclusive scan of the per-window counts
+            const int per = (nwin + 1 + CNS_THREADS - 1) / CNS_THREADS;
+            const int b0 = tid * per, b1 = (b0 + per) < nwin + 1 ? (b0 + per) : nwin + 1;
+            long long s = 0;
+            for (int w = b0; w < b1; ++w) s += w < nwin ? wcur[w] : 0;
+            long long tot;
+            long long base = block_scan_excl(s, scan, &tot);
+            for (int w = b0; w < b1; ++w) { Kh[w] = (int32_t)base; base += w < nwin ? wcur[w] : 0; }
             __syncthreads();
-            if (fast) {
-                // column-parallel: each thread owns columns tid and tid+256 and reads the
-                // codes of every candidate alignment (consecutive columns -> coalesced)
-                const int wi = (int)(w0 / WCOLS);
-                const int kb = wbeg[wi - wback > 0 ? wi - wback : 0], ke = wbeg[wi + 1];
-                for (int c0 = kb; c0 < ke; c0 += WLCAP) {
-                    const int n = (ke - c0) < WLCAP ? (ke - c0) : WLCAP;
-                    for (int x = tid; x < 2 * n; x += CNS_THREADS) WL[x] = K[2 * c0 + x];
-                    __syncthreads();
-                    auto accumulate = [&](const int c, uint32_t (&f6)[6]) {
-                        const int col = (int)w0 + c;
-                        if (c < wn && !(nig && in_ign(ig, nig, col))) {
-                            unsigned long long acc = 0ULL;   // six 10-bit counters (n <= WLCAP)
-#pragma unroll 4
-                            for (int j = 0; j < n; ++j) {
-                                const int4 e = WL[2 * j];
-                                if (col >= e.x && col < e.y) {
-                                    const uint32_t v = E[e.z + col - e.x];
-                                    if (v < E_INS) {
-                                        const int4 e2 = WL[2 * j + 1];
-                                        SeqV sv;
-                                        sv.p = D.seq + (((int64_t)e2.y << 32) | (uint32_t)e2.x);
-                                        sv.n = e.w & 0x7FFFFFFF;
-                                        sv.rc = e.w < 0;
-                                        sv.nt4 = D.seq_nt4 != 0;
-                                        acc += 1ULL << (10u * (uint32_t)fixed_idx(sv[(int)v]));
-                                    } else if (v == E_DEL) {
-                                        acc += 1ULL << 40;
-                                    } else if (wtab_add(wkey, wcnt, ((uint32_t)(c + 1) << 11) | (v & 2047u)) < 0) {
-                                        C->flag = 1;
-                                    }
-                                }
-                            }
-#pragma unroll
-                            for (int s = 0; s < 6; ++s) f6[s] += (uint32_t)(acc >> (10 * s)) & 1023u;
-                        }
-                    };
-                    accumulate(tid, cnt0);
-                    accumulate(tid + CNS_THREADS, cnt1);
-                    __syncthreads();
+            for (int w = tid; w < nwin; w += CNS_THREADS) wcur[w] = 0;
+            __syncthreads();
+        }
+        for (int i = tid; i < na; i += CNS_THREADS) {
+            const int64_t g = a0 + i;
+            if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
+            const int rp = D.a_rpos[g], win = rp / G::W;
+            const int kpos = Kh[win] + atomicAdd(&wcur[win], 1);
+            K[kpos] = make_int4(rp, D.a_end[g], i, 0);
+        }
+        __threadfence_block();
+        __syncthreads();
+        const int wback = (C->maxspan + G::W - 1) / G::W;   // windows an alignment can reach back
+        CNS_TICK(2);
+
+        // ---- 4. windowed pileup (Seq.pm:438-461) + argmax (Seq.pm:1568-1654).  Per window:
+        //   scatter: the kept alignments overlapping the window, split into work items of
+        //   CHUNK columns, walk their states (walk_states: the Perl state semantics) and add
+        //   fixed states to 16-bit LDS counters, insertion states to the window's
+        //   (column, slot) table; then the best insertion state per column (count, then
+        //   first-seen order), the argmax with the reference quality, a block scan of the
+        //   output lengths and the coalesced write of seq / qual / trace.
+        uint32_t *cnt = reinterpret_cast<uint32_t *>(B + G::B_CNT);
+        uint32_t *wkey = reinterpret_cast<uint32_t *>(B + G::B_WKEY);
+        uint32_t *wcnt = reinterpret_cast<uint32_t *>(B + G::B_WCNT);
+        unsigned long long *best = reinterpret_cast<unsigned long long *>(B + G::B_BEST);
+        uint32_t *ignb = reinterpret_cast<uint32_t *>(B + G::B_IGN);
+        int32_t *ipre = reinterpret_cast<int32_t *>(B + G::B_ITEM);
+        uint16_t *cout_ = reinterpret_cast<uint16_t *>(B + G::B_COUT);
+        uint32_t *cdesc = reinterpret_cast<uint32_t *>(B + G::B_CDESC);
+        uint8_t *cphr = B + G::B_CPHR;
+        const bool use_rq = P.use_ref_qual && D.ref_seq && D.ref_qual;
+        constexpr int CPT = G::W / CNS_THREADS;   // argmax columns per thread
+        for (int wi = 0; wi < nwin; ++wi) {
+            const long w0 = (long)wi * G::W;
+            const int wn = (L - w0) < G::W ? (int)(L - w0) : G::W;
+            for (int x = tid; x < 3 * G::W; x += CNS_THREADS) cnt[x] = 0u;
+            for (int x = tid; x < G::WCAP; x += CNS_THREADS) { wkey[x] = 0u; wcnt[x] = 0u; }
+            for (int x = tid; x < G::W; x += CNS_THREADS) best[x] = 0ULL;
+            for (int x = tid; x < G::W / 32; x += CNS_THREADS) ignb[x] = 0u;
+            __syncthreads();
+            for (int r = tid; r < nig; r += CNS_THREADS) {   // MCR ranges -> ignore bits
+                const long s0 = ig[2 * r], s1 = s0 + ig[2 * r + 1];
+                const long lo = s0 > w0 ? s0 : w0, hi = s1 < w0 + wn ? s1 : w0 + wn;
+                for (long col = lo; col < hi; ++col) atomicOr(&ignb[(col - w0) >> 5], 1u << ((col - w0) & 31));
+            }
+            const int kb = Kh[wi - wback > 0 ? wi - wback : 0], ke = Kh[wi + 1];
+            __syncthreads();
+            CNS_TICK(8);
+            if (D.prof && tid == 0) pt[14] += 1;
+            int32_t *cso = reinterpret_cast<int32_t *>(B + G::B_CSO);
+            int32_t *coo = reinterpret_cast<int32_t *>(B + G::B_COO);
+            uint32_t *cigs = reinterpret_cast<uint32_t *>(B + G::B_CIGS);
+            uint8_t *seqs = B + G::B_SEQS;
+            long long *csrc = reinterpret_cast<long long *>(B + G::B_CSRC);
+            long long *cgsrc = reinterpret_cast<long long *>(B + G::B_CGSRC);
+            int4 *cmeta = reinterpret_cast<int4 *>(B + G::B_CSRC);   // after staging: {rpos, ops, sb, lseq | rc}
+            for (int c0 = kb; c0 < ke;) {
+                // a group of candidates whose SEQ dwords and CIGAR ops fit the LDS staging
+                // buffers (prefix sums; candidates that end before the window stage nothing)
+                const int kk = c0 + tid;
+                int4 e = make_int4(0, 0, 0, 0);
+                long long need = 0;   // SEQ dwords | CIGAR ops << 32
+                int head = 0, nop = 0, sbk = 0, lsk = 0;
+                long long sdw = 0, cgi = 0;
+                if (kk < ke) {
+                    e = K[kk];
+                    const long lo = e.x > w0 ? e.x : w0, hi = e.y < w0 + wn ? e.y : w0 + wn;
+                    if (hi > lo) {
+                        const int64_t g = a0 + e.z;
+                        const int64_t so = D.seq_off[g];
+                        const int cbk = D.a_cb[g];
+                        lsk = D.lseq[g] | ((D.aflags[g] & 8) ? (int)0x80000000 : 0);
+                        sbk = D.a_sb[g];
+                        nop = D.a_ce[g] - cbk;
+                        head = (int)(so & 3);
+                        sdw = so >> 2;
+                        cgi = D.cig_off[g] + cbk;
+                        need = (long long)((head + (lsk & 0x7FFFFFFF) + 3) >> 2) | ((long long)nop << 32);
+                    }
                 }
-            } else {
-                for (int i = tid; i < na; i += CNS_THREADS) {
-                    const int64_t g = a0 + i;
-                    if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
-                    const int rp = D.a_rpos[g];
-                    if (rp >= w0 + wn || D.a_end[g] <= w0) continue;
-                    const SeqV sv = seq_view(D, g);
-                    const int sb = D.a_sb[g];
-                    const uint32_t *cg = D.cig + D.cig_off[g];
-                    walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, (int)w0, (int)(w0 + wn),
-                                       [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                           if (nig && in_ign(ig, nig, col)) return;
-                                           const int c = col - (int)w0;
-                                           if (kind == 1) { atomicAdd(&cnt6[c * 6 + 4], 1u); return; }
-                                           if (qlen == 1) { atomicAdd(&cnt6[c * 6 + fixed_idx(sv[sb + qoff])], 1u); return; }
-                                           const int h = stab_find(T, state_key(sv, sb + qoff, qlen));
-                                           if (h < 0 || wtab_add(wkey, wcnt, ((uint32_t)(c + 1) << 11) | (uint32_t)h) < 0)
-                                               C->flag = 1;
-                                       });
+                long long ntot;
+                const long long npre = block_scan_excl(need, scan, &ntot);
+                const long long incl = npre + need;
+                const bool fits = kk < ke && 4 * (incl & 0xFFFFFFFFLL) <= G::SEQB && (incl >> 32) <= G::CIGB &&
+                                  (incl >> 32) <= 2 * G::ICAP - 2;
+                const int gs = __syncthreads_count(fits);   // fits is a prefix of the candidates
+                if (gs == 0) {   // one alignment alone outgrows the staging buffers
+                    if (tid == 0) C->flag = 1;
+                    __syncthreads();
+                    break;
+                }
+                if (tid < gs) {
+                    cso[tid] = (int)(npre & 0xFFFFFFFFLL) * 4 + head;   // staged SEQ view: byte offset
+                    coo[tid] = (int)(npre >> 32);                        // staged ops: op offset
+                    csrc[tid] = sdw - (npre & 0xFFFFFFFFLL);             // source dword = dst dword + csrc
+                    cgsrc[tid] = cgi - (npre >> 32);                     // source op = dst op + cgsrc
+                    ipre[tid] = (int)(npre & 0xFFFFFFFFLL);              // (dword prefix, for the copy)
+                }
+                if (tid == gs - 1) {
+                    ipre[CNS_THREADS] = (int)(incl & 0xFFFFFFFFLL);
+                    ipre[CNS_THREADS + 1] = (int)(incl >> 32);
                 }
                 __syncthreads();
+                const int totdw = ipre[CNS_THREADS], totop = ipre[CNS_THREADS + 1];
+                CNS_TICK(9);
+                // stage: flat copies of the group's SEQ dwords and CIGAR ops, 4 independent
+                // loads in flight per thread (owner candidate by binary search over prefixes)
+                {
+                    uint32_t *seqdw = reinterpret_cast<uint32_t *>(seqs);
+                    const uint32_t *gdw = reinterpret_cast<const uint32_t *>(D.seq);
+                    for (int b0 = 0; b0 < totdw; b0 += 4 * CNS_THREADS) {
+                        uint32_t v[4];
 #pragma unroll
-                for (int s = 0; s < 6; ++s) {
-                    cnt0[s] = cnt6[tid * 6 + s];
-                    cnt1[s] = cnt6[(tid + CNS_THREADS) * 6 + s];
+                        for (int u = 0; u < 4; ++u) {
+                            const int d = b0 + u * CNS_THREADS + tid;
+                            v[u] = 0u;
+                            if (d < totdw) {
+                                int lo = 0, hi = gs - 1;
+                                while (lo < hi) {
+                                    const int mid = (lo + hi + 1) >> 1;
+                                    if (ipre[mid] <= d) lo = mid; else hi = mid - 1;
+                                }
+                                v[u] = gdw[csrc[lo] + d];
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int d = b0 + u * CNS_THREADS + tid;
+                            if (d < totdw) seqdw[d] = v[u];
+                        }
+                    }
+                    for (int b0 = 0; b0 < totop; b0 += 4 * CNS_THREADS) {
+                        uint32_t v[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int d = b0 + u * CNS_THREADS + tid;
+                            v[u] = 0u;
+                            if (d < totop) {
+                                int lo = 0, hi = gs - 1;
+                                while (lo < hi) {
+                                    const int mid = (lo + hi + 1) >> 1;
+                                    if (coo[mid] <= d) lo = mid; else hi = mid - 1;
+                                }
+                                v[u] = D.cig[cgsrc[lo] + d];
+                            }
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int d = b0 + u * CNS_THREADS + tid;
+                            if (d < totop) cigs[d] = v[u];
+                        }
+                    }
                 }
+                __syncthreads();
+                CNS_TICK(10);
+                if (tid < gs) cmeta[tid] = make_int4(e.x, nop, sbk, lsk);   // (csrc / cgsrc are dead)
+                const bool snt4 = D.seq_nt4 != 0;
+                int2 *runs = reinterpret_cast<int2 *>(B + G::B_RUN);
+                int2 *insr = reinterpret_cast<int2 *>(B + G::B_INS);
+                if (tid == 0) { C->nrun = 0; C->nins = 0; }
+                __syncthreads();
+                // pre-pass, op-parallel (Seq.pm:396-461 state semantics, as walk_states): a
+                // segmented scan gives every staged op its column and SEQ offset inside its
+                // alignment, then each op emits its states inside the window: one run of
+                // single-base / '-' states, and the multi-character state its last column
+                // becomes when insertions follow (the leading insertion's state for a first op I)
+                {
+                    const int opt = (totop + CNS_THREADS - 1) / CNS_THREADS;   // ops per thread
+                    const int k0 = tid * opt, k1 = (k0 + opt) < totop ? (k0 + opt) : totop;
+                    int j = 0;   // candidate of op k0: last j with coo[j] <= k0
+                    if (k0 < k1) {
+                        int lo = 0, hi = gs - 1;
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if (coo[mid] <= k0) lo = mid; else hi = mid - 1;
+                        }
+                        j = lo;
+                    }
+                    // chunk aggregate: advances (column | SEQ << 32) after the chunk's last
+                    // alignment start, and whether the chunk holds an alignment start
+                    long long agg = 0;
+                    int head = 0;
+                    {
+                        int jj = j;
+                        for (int k = k0; k < k1; ++k) {
+                            while (jj + 1 < gs && coo[jj + 1] <= k) ++jj;
+                            if (k == coo[jj]) { agg = 0; head = 1; }
+                            const uint32_t c = cigs[k];
+                            const long long n = (long long)(c >> 4);
+                            const int code = (int)(c & 15u);
+                            agg += code == 0 ? (n | (n << 32)) : code == 2 ? n : code == 1 ? ((k == coo[jj] ? 1LL : 0LL) | (n << 32)) : 0;
+                        }
+                    }
+                    // block segmented inclusive scan (Hillis-Steele over the 256 chunk aggregates)
+                    long long *sv64 = scan;   // 256 x 8 B scratch
+                    int *sfl = ipre;
+                    sv64[tid] = agg;
+                    sfl[tid] = head;
+                    __syncthreads();
+                    for (int o = 1; o < CNS_THREADS; o <<= 1) {
+                        long long pv = 0;
+                        int pf = 0;
+                        if (tid >= o) { pv = sv64[tid - o]; pf = sfl[tid - o]; }
+                        __syncthreads();
+                        if (tid >= o && !sfl[tid]) { sv64[tid] += pv; sfl[tid] |= pf; }
+                        __syncthreads();
+                    }
+                    long long run = tid > 0 ? sv64[tid - 1] : 0;   // carry into op k0
+                    __syncthreads();
+                    for (int k = k0; k < k1; ++k) {
+                        while (j + 1 < gs && coo[j + 1] <= k) ++j;
+                        const bool first = k == coo[j];
+                        if (first) run = 0;
+                        const int kend = j + 1 < gs ? coo[j + 1] : totop;
+                        const int4 m = cmeta[j];
+                        const int col = m.x + (int)(run & 0xFFFFFFFFLL), qpos = (int)(run >> 32);
+                        const uint32_t c = cigs[k];
+                        const int n = (int)(c >> 4), code = (int)(c & 15u);
+                        run += code == 0 ? ((long long)n | ((long long)n << 32)) : code == 2 ? (long long)n
+                             : code == 1 ? ((first ? 1LL : 0LL) | ((long long)n << 32)) : 0LL;
+                        if (code == 1 && !first) continue;   // consumed by the state before it
+                        if (code != 1 && n == 0) continue;   // split() of an empty run pushes nothing
+                        // insertions that follow (zero-length ops in between are skipped)
+                        int tot = 0;
+                        for (int kk = k + 1; kk < kend; ++kk) {
+                            const uint32_t c2 = cigs[kk];
+                            if ((c2 & 15u) == 1u) tot += (int)(c2 >> 4);
+                            else if ((c2 >> 4) != 0u) break;
+                        }
+                        int scol, sq, slen;   // the op's last (deferred) state: column, SEQ offset, length
+                        if (code == 1) {      // leading insertion: one state at col
+                            scol = col; sq = qpos; slen = n + tot;
+                        } else {
+                            const int kind = code == 0 ? 0 : 1;
+                            const int lo = col > (int)w0 ? col : (int)w0;
+                            const int endc = col + n - (tot ? 1 : 0);   // single states [col, endc)
+                            const int hi = endc < (int)w0 + wn ? endc : (int)w0 + wn;
+                            if (hi > lo) {
+                                const int k2 = wave_append(&C->nrun);
+                                if (k2 < G::CIGB)
+                                    runs[k2] = make_int2((lo - (int)w0) | ((hi - lo) << 10) | (kind << 20) | (j << 21),
+                                                         kind == 0 ? qpos + (lo - col) : 0);
+                                else C->flag = 1;
+                            }
+                            if (!tot) continue;
+                            scol = col + n - 1;
+                            if (kind == 0) { sq = qpos + n - 1; slen = 1 + tot; }
+                            else { sq = qpos; slen = tot; }   // D + I: the insertion replaces '-'
+                        }
+                        if (scol < (int)w0 || scol >= (int)w0 + wn) continue;
+                        if (slen == 1) {
+                            const int k2 = wave_append(&C->nrun);
+                            if (k2 < G::CIGB) runs[k2] = make_int2((scol - (int)w0) | (1 << 10) | (j << 21), sq);
+                            else C->flag = 1;
+                        } else {
+                            const int k2 = wave_append(&C->nins);
+                            if (k2 < G::ICAP) insr[k2] = make_int2((scol - (int)w0) | (j << 10), sq | (slen << 16));
+                            else C->flag = 1;
+                        }
+                    }
+                }
+                __syncthreads();
+                if (D.prof && tid == 0) {   // pre-pass time (slot 15), out of the walk slot
+                    const unsigned long long t_ = wall_clock64();
+                    pt[15] += t_ - tlast;
+                    tlast = t_;
+                }
+                if (C->flag) break;
+                // runs in parallel: one LDS read of the staged base and one LDS atomic per state
+                const int nrun = C->nrun, nins = C->nins;
+                for (int r = tid; r < nrun; r += CNS_THREADS) {
+                    const int2 rr = runs[r];
+                    const int c0r = rr.x & 1023, len = (rr.x >> 10) & 1023, j = (rr.x >> 21) & 255;
+                    if (rr.x & (1 << 20)) {   // '-'
+                        for (int x = 0; x < len; ++x) {
+                            const int c = c0r + x;
+                            if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
+                            atomicAdd(&cnt[3 * c + 2], 1u);
+                        }
+                        continue;
+                    }
+                    const int4 m = cmeta[j];
+                    SeqV sv;
+                    sv.p = seqs + cso[j];
+                    sv.n = m.w & 0x7FFFFFFF;
+                    sv.rc = m.w < 0;
+                    sv.nt4 = snt4;
+                    const int q0 = m.z + rr.y;   // sb + qoff
+                    for (int x = 0; x < len; ++x) {
+                        const int c = c0r + x;
+                        if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
+                        const int fi = fixed_idx_at(sv, q0 + x);
+                        atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
+                    }
+                }
+                for (int r = tid; r < nins; r += CNS_THREADS) {
+                    const int2 ir = insr[r];
+                    const int c = ir.x & 1023, j = (ir.x >> 10) & 255;
+                    if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
+                    const int4 m = cmeta[j];
+                    SeqV sv;
+                    sv.p = seqs + cso[j];
+                    sv.n = m.w & 0x7FFFFFFF;
+                    sv.rc = m.w < 0;
+                    sv.nt4 = snt4;
+                    const int h = T.find(state_key(sv, m.z + (ir.y & 0xFFFF), (int)((unsigned)ir.y >> 16)));
+                    if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
+                        C->flag = 1;
+                }
+                __syncthreads();
+                CNS_TICK(11);
+                if (D.prof && tid == 0) { pt[12] += 1; pt[13] += (unsigned long long)gs; }
+                c0 += gs;
             }
-            for (int x = tid; x < WCOLS; x += CNS_THREADS) colcnt[x] = 0;
-            __syncthreads();
             CNS_TICK(3);
-            // per-column lists of insertion entries (counting sort)
-            for (int e = tid; e < WCAP; e += CNS_THREADS)
-                if (wkey[e]) atomicAdd(&colcnt[(wkey[e] >> 11) - 1], 1);
-            __syncthreads();
-            {
-                const int per = WCOLS / CNS_THREADS;   // 2
-                long long s = 0;
-                for (int k = 0; k < per; ++k) s += colcnt[tid * per + k];
-                long long tot;
-                long long base = block_scan_excl(s, scan, &tot);
-                for (int k = 0; k < per; ++k) { colst[tid * per + k] = (int32_t)base; base += colcnt[tid * per + k]; colcnt[tid * per + k] = 0; }
+            if (C->flag) break;
+            // best insertion state per column: highest count, then lowest first-seen order
+            for (int x = tid; x < G::WCAP; x += CNS_THREADS) {
+                const uint32_t k = wkey[x];
+                if (!k) continue;
+                const int slot = (int)(k & SLOT_MASK), c = (int)(k >> SLOT_SH) - 1;
+                if (P.max_ins_length && ex_len(T.exem[slot]) > P.max_ins_length) continue;
+                const unsigned long long v = ((unsigned long long)wcnt[x] << 44) |
+                                             ((unsigned long long)(0xFFFFFFFFu - T.ord_cns[slot]) << SLOT_SH) |
+                                             (unsigned long long)slot;
+                atomicMax(&best[c], v);
             }
             __syncthreads();
-            for (int e = tid; e < WCAP; e += CNS_THREADS)
-                if (wkey[e]) {
-                    const int c = (int)(wkey[e] >> 11) - 1;
-                    elist[colst[c] + atomicAdd(&colcnt[c], 1)] = (uint16_t)e;
-                }
-            __syncthreads();
-            // argmax per column (the thread's two columns; counts stay in registers)
-            auto argmax_col = [&](const int c, const uint32_t (&f6)[6]) {
+            // argmax per column (Seq.pm:1576-1636): first index with strictly greater freq
+#pragma unroll
+            for (int k = 0; k < CPT; ++k) {
+                const int c = tid * CPT + k;
                 uint16_t olen = 0;
                 uint32_t desc = 0;
                 uint8_t ph = 0;
                 if (c < wn) {
                     const long col = w0 + c;
-                    double val[6];
-                    bool def[6];
-                    bool any = false;
+                    const uint32_t q0 = cnt[3 * c], q1 = cnt[3 * c + 1], q2 = cnt[3 * c + 2];
+                    const uint32_t f6[6] = {q0 & 0xFFFFu, q0 >> 16, q1 & 0xFFFFu, q1 >> 16, q2 & 0xFFFFu, q2 >> 16};
                     int rs = -1;
                     double vref = 0.0;
                     if (use_rq) {
@@ -904,57 +1219,41 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                             for (uint32_t kk = 0; kk < n; ++kk) vref = __dadd_rn(vref, 1.0);
                         }
                     }
-#pragma unroll
-                    for (int s = 0; s < 6; ++s) {
-                        const uint32_t n = f6[s];
-                        val[s] = s == rs ? vref : (double)n;
-                        def[s] = (n != 0u) || (s == rs);
-                        any |= def[s];
-                    }
-                    const int ne = colcnt[c];
-                    any |= ne > 0;
                     double maxf = 0.0;
                     int idx = -1;
-                    unsigned int best_ord = 0xFFFFFFFFu;
-                    int best_slot = -1;
 #pragma unroll
-                    for (int s = 0; s < 6; ++s)
-                        if (def[s] && val[s] > maxf) { maxf = val[s]; idx = s; }
-                    for (int x = 0; x < ne; ++x) {
-                        const int e = elist[colst[c] + x];
-                        const int slot = (int)(wkey[e] & 2047u);
-                        const int slen = ex_len(T.exem[slot]);
-                        if (P.max_ins_length && slen > P.max_ins_length) continue;
-                        const double v = (double)wcnt[e];
-                        const unsigned int o = T.ord_cns[slot];
-                        if (v > maxf || (v == maxf && idx >= 6 && o < best_ord)) {
-                            maxf = v; idx = 6; best_ord = o; best_slot = slot;
-                        }
+                    for (int s = 0; s < 6; ++s) {
+                        const double v = s == rs ? vref : (double)f6[s];
+                        if ((f6[s] != 0u || s == rs) && v > maxf) { maxf = v; idx = s; }
                     }
-                    if (!any || !(maxf != 0.0)) {
+                    const unsigned long long bi = best[c];
+                    int bslot = -1;
+                    if (bi && (double)(bi >> 44) > maxf) {
+                        maxf = (double)(bi >> 44);
+                        idx = 6;
+                        bslot = (int)(bi & SLOT_MASK);
+                    }
+                    if (!(maxf != 0.0)) {
                         olen = 1; desc = DESC_FIXED | (D.ref_seq ? ref_base(D, r0 + col) : (uint8_t)'n'); ph = 0;
                     } else if (idx == 4) {
                         olen = 0; desc = 0; ph = 0;
                     } else if (idx < 6) {
                         olen = 1; desc = DESC_FIXED | (uint8_t)(0x4E2D43475441ULL >> (8 * idx)); ph = (uint8_t)freq2phred(maxf);
                     } else {
-                        olen = (uint16_t)ex_len(T.exem[best_slot]); desc = DESC_INS | (uint32_t)best_slot;
+                        olen = (uint16_t)ex_len(T.exem[bslot]); desc = DESC_INS | (uint32_t)bslot;
                         ph = (uint8_t)freq2phred(maxf);
                     }
                 }
                 cout_[c] = olen;
                 cdesc[c] = desc;
                 cphr[c] = ph;
-            };
-            argmax_col(tid, cnt0);
-            argmax_col(tid + CNS_THREADS, cnt1);
+            }
             __syncthreads();
             // block scan of (seq len, trace len) over the window's columns, then write
             {
-                const int per = WCOLS / CNS_THREADS;
                 long long s = 0;
-                for (int k = 0; k < per; ++k) {
-                    const int c = tid * per + k;
+                for (int k = 0; k < CPT; ++k) {
+                    const int c = tid * CPT + k;
                     if (c < wn) {
                         const long long ol = cout_[c];
                         s += ol | ((long long)(ol ? ol : 1) << 32);
@@ -969,9 +1268,9 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                 // a guard for pipeline batches whose capacity is estimated)
                 const long long cap = D.out_off[lr + 1] - o0;
                 const bool fits = (long long)C->run_trace + (tot >> 32) <= cap;
-                if (!fits && tid == 0) C->flag = 1;
-                for (int k = 0; k < per && fits; ++k) {
-                    const int c = tid * per + k;
+                if (!fits && tid == 0) C->flag = 2;
+                for (int k = 0; k < CPT && fits; ++k) {
+                    const int c = tid * CPT + k;
                     if (c >= wn) break;
                     const int ol = cout_[c];
                     const uint32_t d = cdesc[c];
@@ -985,7 +1284,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                         D.o_trace[o0 + to] = 'M';
                         so += 1; to += 1;
                     } else {
-                        const int slot = (int)(d & 2047u);
+                        const int slot = (int)(d & SLOT_MASK);
                         const uint64_t ex = T.exem[slot];
                         const SeqV src = seq_view(D, ex_aln(ex));
                         const int eo = ex_off(ex);
@@ -1007,13 +1306,18 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
             CNS_TICK(4);
         }
         if (C->flag) {
-            if (tid == 0) {
-                D.status[lr] = PR_ERR_CODE_CAP;
-                D.seq_len[lr] = 0; D.trace_len[lr] = 0; D.ncigar[lr] = 0; D.nchim[lr] = 0;
+            if (C->flag == 2) {   // output capacity (pipeline estimate): no retry helps
+                if (tid == 0) {
+                    D.status[lr] = PR_ERR_CODE_CAP;
+                    D.seq_len[lr] = 0; D.trace_len[lr] = 0; D.ncigar[lr] = 0; D.nchim[lr] = 0;
+                }
+                __syncthreads();
+            } else {
+                CNS_CAP_FAIL();
             }
-            __syncthreads();
             continue;
         }
+
         const int tlen = C->run_trace;
 
         // ---- 5. Trace2cigar (Seq.pm:206-225): run starts -> ops
@@ -1113,7 +1417,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                                            int fi = -1, slot = -1;
                                            if (kind == 1) fi = 4;
                                            else if (qlen == 1) fi = fixed_idx(sv[sb + qoff]);
-                                           else slot = stab_find(T, state_key(sv, sb + qoff, qlen));
+                                           else slot = T.find(state_key(sv, sb + qoff, qlen));
                                            for (int side = 0; side < 2; ++side) {
                                                if (side == 0 ? !inl : !inr) continue;
                                                uint32_t *f6 = side == 0 ? f6l : f6r;
@@ -1121,7 +1425,7 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                                                uint32_t *tc = side == 0 ? tcl : tcr;
                                                if (fi >= 0) { atomicAdd(&f6[c * 6 + fi], 1u); continue; }
                                                if (slot < 0) { C->flag = 1; continue; }
-                                               const uint32_t key = ((uint32_t)(c + 1) << 11) | (uint32_t)slot;
+                                               const uint32_t key = ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)slot;
                                                uint32_t h = (key * 2654435761u) >> 24;
                                                int p = 0;
                                                for (; p < CHIM_TCAP; ++p) {
@@ -1149,8 +1453,8 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
                     bool nel = false, ner = false;
                     for (int s = 0; s < 6; ++s) { nel |= f6l[c * 6 + s] != 0u; ner |= f6r[c * 6 + s] != 0u; }
                     for (int e = 0; e < CHIM_TCAP; ++e) {
-                        nel |= tkl[e] != 0u && (int)(tkl[e] >> 11) - 1 == c;
-                        ner |= tkr[e] != 0u && (int)(tkr[e] >> 11) - 1 == c;
+                        nel |= tkl[e] != 0u && (int)(tkl[e] >> SLOT_SH) - 1 == c;
+                        ner |= tkr[e] != 0u && (int)(tkr[e] >> SLOT_SH) - 1 == c;
                     }
                     if (!nel || !ner) continue;
                     const double hr = chim_hx(1, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
@@ -1210,26 +1514,31 @@ __global__ void __launch_bounds__(CNS_THREADS, 2) cns_lr_kernel(CnsDev D, CnsPar
         }
         __syncthreads();
     }
+
     if (D.prof && tid == 0)
         for (int k = 0; k < CNS_NPHASE; ++k) atomicAdd(&D.prof[k], pt[k]);
 #undef CNS_TICK
+#undef CNS_CAP_FAIL
 }
 
-}  // namespace prgpu
-
-namespace prgpu {
-int cns_launch(const CnsDev &D, const CnsParamsDev &P, int grid, void *stream) {
+int cns_launch(const CnsDev &D, const CnsParamsDev &P, int grid, int grid_retry, void *stream) {
     static bool attr = false;
     if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)cns_lr_kernel,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, CNS_LDS_BYTES);
+        hipError_t e = hipFuncSetAttribute((const void *)cns_lr_kernel<GeoS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           GeoS::LDS);
+        if (e != hipSuccess) return (int)e;
+        e = hipFuncSetAttribute((const void *)cns_lr_kernel<GeoL>, hipFuncAttributeMaxDynamicSharedMemorySize, GeoL::LDS);
         if (e != hipSuccess) return (int)e;
         attr = true;
     }
-    hipLaunchKernelGGL(cns_lr_kernel, dim3(grid), dim3(CNS_THREADS), CNS_LDS_BYTES,
-                       (hipStream_t)stream, D, P);
+    hipStream_t s = (hipStream_t)stream;
+    if (!D.force_large)
+        hipLaunchKernelGGL(cns_lr_kernel<GeoS>, dim3(grid), dim3(CNS_THREADS), GeoS::LDS, s, D, P);
+    // reads whose tables outgrew the small geometry (device-side list; usually empty)
+    hipLaunchKernelGGL(cns_lr_kernel<GeoL>, dim3(grid_retry), dim3(CNS_THREADS), GeoL::LDS, s, D, P);
     return (int)hipGetLastError();
 }
-int cns_lds_bytes() { return CNS_LDS_BYTES; }
-int cns_max_bins() { return MAX_BINS_LDS; }
+int cns_max_bins() { return GeoL::MAX_BINS; }
+int cns_k_header() { return 1024; }
+
 }  // namespace prgpu

@@ -2,6 +2,7 @@
 // Device memory, one HIP stream per context, HIP events for kernel timing.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -49,7 +50,7 @@ struct DevBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
-        size_t want = bytes ? bytes : 16;
+        size_t want = bytes + 64;   // slack: kernels read whole dwords at the end of byte pools
         if (hipMalloc(&p, want) != hipSuccess) return set_error(PR_ERR_HIP, "hipMalloc(%zu) failed", want);
         cap = want;
         return 0;
@@ -69,7 +70,7 @@ enum CnsBufId {
     CB_A_ST, CB_A_LEN, CB_A_NC, CB_A_BIN, CB_A_CB, CB_A_CE, CB_A_SB, CB_A_RPOS, CB_A_END,
     CB_SORTED, CB_LST_SCORE, CB_LST_ALN, CB_KEPT, CB_BIN_OFF, CB_BIN_BASES, CB_WORK,
     CB_OUT_OFF, CB_CHIM_OFF, CB_STATUS, CB_SEQ_LEN, CB_TRACE_LEN, CB_NCIGAR, CB_NCHIM,
-    CB_O_SEQ, CB_O_QUAL, CB_O_TRACE, CB_O_CIG, CB_O_CHIM, CB_PROF, CB_E, CB_K,
+    CB_O_SEQ, CB_O_QUAL, CB_O_TRACE, CB_O_CIG, CB_O_CHIM, CB_PROF, CB_RETRY, CB_K,
     CB_COUNT
 };
 
@@ -92,7 +93,7 @@ struct pr_ctx {
     int32_t n_lr = 0;
     int64_t n_aln = 0, total_cols = 0, n_bins = 0, seq_cap = 0, chim_cap = 0;
     int64_t alg_bytes = 0;
-    int64_t e_need = 0, k_need = 0;   // per-read bounds of expanded pileup entries / kept alignments
+    int64_t k_need = 0;   // per-read bound of kept alignments (K pool slices)
     bool has_ref = false, has_qual = false, has_ign = false;
     std::vector<int64_t> out_off, chim_off, bin_off, lr_off_host;
     float last_ms = 0.f;
@@ -205,31 +206,27 @@ static int validate_batch(const pr_cns_batch *b) {
 // consensus bytes <= L + inserted bases of all its alignments (+1); chimera
 // records <= bins/2 + 2 (bins at the smallest bin size bam2cns uses, 20).
 static void cns_caps(const pr_cns_batch *b, std::vector<int64_t> &out_off, std::vector<int64_t> &chim_off,
-                     int64_t *in_bytes, int64_t *e_need = nullptr, int64_t *k_need = nullptr) {
+                     int64_t *in_bytes, int64_t *k_need = nullptr) {
     const int n = b->n_lr;
     out_off.assign(n + 1, 0);
     chim_off.assign(n + 1, 0);
-    int64_t ib = 0, emax = 0, kmax = 0;
+    int64_t ib = 0, kmax = 0;
     for (int i = 0; i < n; ++i) {
         const int64_t L = b->lr_off[i + 1] - b->lr_off[i];
-        int64_t ins = 0, ecount = 0;
+        int64_t ins = 0;
         for (int64_t a = b->aln_off[i]; a < b->aln_off[i + 1]; ++a) {
             ib += (b->aln_flags[a] & PR_ALN_NO_SEQ ? 0 : b->aln_lseq[a]) + 4 * (int64_t)b->aln_ncig[a] + 16;
-            ecount += 1;   // a leading insertion state
             for (int k = 0; k < b->aln_ncig[a]; ++k) {
                 const uint32_t cc = b->cig_pool[b->aln_cig_off[a] + k];
                 if ((cc & 15u) == 1u) ins += cc >> 4;
-                if ((cc & 15u) == 0u || (cc & 15u) == 2u) ecount += cc >> 4;
             }
         }
-        if (ecount > emax) emax = ecount;
         if (b->aln_off[i + 1] - b->aln_off[i] > kmax) kmax = b->aln_off[i + 1] - b->aln_off[i];
         const int64_t nb = (int64_t)((double)L / 20.0) + 1;
         out_off[i + 1] = out_off[i] + L + ins + 1;
         chim_off[i + 1] = chim_off[i] + nb / 2 + 2;
     }
     if (in_bytes) *in_bytes = ib;
-    if (e_need) *e_need = emax;
     if (k_need) *k_need = kmax;
 }
 
@@ -271,7 +268,7 @@ extern "C" int pr_cns_upload(pr_ctx *c, const pr_cns_batch *b) {
     c->has_qual = b->ref_qual != nullptr;
     c->has_ign = b->ign_off != nullptr;
     int64_t in_bytes = 0;
-    cns_caps(b, c->out_off, c->chim_off, &in_bytes, &c->e_need, &c->k_need);
+    cns_caps(b, c->out_off, c->chim_off, &in_bytes, &c->k_need);
     c->seq_cap = c->out_off[n];
     c->chim_cap = c->chim_off[n];
     // SURVEY.md §8d pileup byte model: alignments in + ref seq/qual in + consensus out + state counts
@@ -307,6 +304,7 @@ extern "C" int pr_cns_upload(pr_ctx *c, const pr_cns_batch *b) {
         return rc;
     if ((rc = B[CB_WORK].ensure(64))) return rc;
     if ((rc = B[CB_PROF].ensure(CNS_NPHASE * 8))) return rc;
+    if ((rc = B[CB_RETRY].ensure(((size_t)n + 16) * 4))) return rc;
     if ((rc = upload(B[CB_OUT_OFF], c->out_off.data(), n + 1, s))) return rc;
     if ((rc = upload(B[CB_CHIM_OFF], c->chim_off.data(), n + 1, s))) return rc;
     const size_t n1 = (size_t)n + 1;
@@ -430,23 +428,34 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
     HIPCHK(hipMemsetAsync(D.work, 0, 64, c->stream));
     HIPCHK(hipMemsetAsync(D.prof, 0, CNS_NPHASE * 8, c->stream));
     const int grid = c->n_lr < c->n_cu * 2 ? c->n_lr : c->n_cu * 2;
+    const int grid_retry = c->n_lr < c->n_cu ? c->n_lr : c->n_cu;
     {
-        // expanded-pileup scratch per resident workgroup; reads beyond it take the
-        // in-kernel scatter path
-        int64_t ec = c->e_need < 4096 ? 4096 : c->e_need;
-        if (ec > (1 << 24)) ec = 1 << 24;
-        int64_t kc = c->k_need < 64 ? 64 : c->k_need;
-        if (kc > (1 << 20)) kc = 1 << 20;
+        // K pool: per resident workgroup the window starts (longest read / 512 + 8 ints) and
+        // 4 ints per kept alignment
+        int64_t lmax = 0;
+        for (int i = 0; i < c->n_lr; ++i) lmax = std::max(lmax, c->lr_off_host[i + 1] - c->lr_off_host[i]);
+        const int64_t kc = (lmax / 512 + 12) + 4 * (c->k_need < 64 ? 64 : c->k_need);
         int rc;
-        if ((rc = B[CB_E].ensure((size_t)grid * ec * 4)) || (rc = B[CB_K].ensure((size_t)grid * kc * 32))) return rc;
-        D.e_pool = B[CB_E].as<uint32_t>();
-        D.e_cap = ec;
-        D.k_pool = B[CB_K].as<int4>();
-        D.k_cap = (int32_t)kc;
-        if (getenv("PRGPU_CNS_SCATTER")) D.e_pool = nullptr;   // force the scatter path (tests)
+        if ((rc = B[CB_K].ensure((size_t)grid * kc * 4))) return rc;
+        D.k_pool = B[CB_K].as<int32_t>();
+        D.k_cap = kc;
+        D.retry = B[CB_RETRY].as<int32_t>();
+        D.retry_n = B[CB_RETRY].as<int32_t>() + c->n_lr + 8;
+        HIPCHK(hipMemsetAsync(D.retry_n, 0, 4, c->stream));
+        D.debug = getenv("PRGPU_CNS_DEBUG") ? atoi(getenv("PRGPU_CNS_DEBUG")) : 0;
+        const char *fl = getenv("PRGPU_CNS_LARGE");   // diagnostics: all reads through the large geometry
+        if (fl && atoi(fl)) {
+            D.force_large = 1;
+            std::vector<int32_t> all((size_t)c->n_lr + 1);
+            for (int i = 0; i < c->n_lr; ++i) all[(size_t)i] = i;
+            all[(size_t)c->n_lr] = c->n_lr;
+            HIPCHK(hipMemcpyAsync(D.retry, all.data(), (size_t)c->n_lr * 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(D.retry_n, &all[(size_t)c->n_lr], 4, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
     }
     HIPCHK(hipEventRecord(c->ev[4], c->stream));
-    int e = cns_launch(D, P, grid, (void *)c->stream);
+    int e = cns_launch(D, P, grid, grid_retry, (void *)c->stream);
     if (e != 0) return set_error(PR_ERR_HIP, "cns kernel launch failed: %s", hipGetErrorString((hipError_t)e));
     HIPCHK(hipEventRecord(c->ev[5], c->stream));
     c->cns_launched = true;
@@ -503,11 +512,11 @@ extern "C" int pr_cns_last_timing(pr_ctx *c, double *ms_prep, double *ms_pileup)
 }
 
 extern "C" int pr_cns_phase_ticks(pr_ctx *c, uint64_t *ticks, int n) {
-    if (!c || !ticks || n < CNS_NPHASE) return set_error(PR_ERR_ARG, "need ctx and %d ticks", CNS_NPHASE);
+    if (!c || !ticks || n < 8) return set_error(PR_ERR_ARG, "need ctx and >= 8 ticks");
     if (!c->cns_loaded || !c->cb[CB_PROF].p) return set_error(PR_ERR_ARG, "no consensus launch yet");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
-    HIPCHK(hipMemcpy(ticks, c->cb[CB_PROF].p, CNS_NPHASE * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(ticks, c->cb[CB_PROF].p, (size_t)(n < CNS_NPHASE ? n : CNS_NPHASE) * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -561,7 +570,6 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
     c->chim_cap = c->chim_off[n];
     c->alg_bytes = 0;
     c->k_need = maxt;
-    c->e_need = (int64_t)maxt * (c->sw.qmax + 256);   // span <= query + band deletions
     int sc = 1;
     while (sc < maxt) sc <<= 1;
     c->pipe_sort_cap = sc;
@@ -584,7 +592,7 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
         (rc = B[CB_A_END].ensure(na1 * 4)) || (rc = B[CB_SORTED].ensure(na1 * 4)) ||
         (rc = B[CB_LST_SCORE].ensure(na1 * 8)) || (rc = B[CB_LST_ALN].ensure(na1 * 4)) ||
         (rc = B[CB_KEPT].ensure(na1)) || (rc = B[CB_WORK].ensure(64)) ||
-        (rc = B[CB_PROF].ensure(CNS_NPHASE * 8)))
+        (rc = B[CB_PROF].ensure(CNS_NPHASE * 8)) || (rc = B[CB_RETRY].ensure(((size_t)n + 16) * 4)))
         return rc;
     if ((rc = upload(B[CB_OUT_OFF], c->out_off.data(), n1, s))) return rc;
     if ((rc = upload(B[CB_CHIM_OFF], c->chim_off.data(), n1, s))) return rc;

@@ -66,7 +66,7 @@ static int ensure(SwResident &r, int id, size_t bytes) {
     if (r.buf[id]) (void)hipFree(r.buf[id]);
     r.buf[id] = nullptr;
     r.cap[id] = 0;
-    const size_t want = bytes ? bytes : 16;
+    const size_t want = bytes + 64;   // slack: kernels read whole dwords at the end of byte pools
     if (hipMalloc(&r.buf[id], want) != hipSuccess) return pr_set_error(PR_ERR_HIP, "hipMalloc failed (SW)");
     r.cap[id] = want;
     return 0;

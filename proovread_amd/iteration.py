@@ -139,10 +139,13 @@ class Iteration:
 
     def cns_phase_ms(self):
         """Consensus workgroup time per phase (ms summed over workgroups) of the last launch."""
-        t = (C.c_uint64 * 8)()
-        _abi.check(self.L.pr_cns_phase_ticks(self.ctx.h, t, 8), "pr_cns_phase_ticks")
-        names = ["prep", "binning", "state_table", "scatter", "argmax_write", "cigar", "chimera", "idle"]
-        return {k: t[i] / 1e5 for i, k in enumerate(names)}
+        t = (C.c_uint64 * 16)()
+        _abi.check(self.L.pr_cns_phase_ticks(self.ctx.h, t, 16), "pr_cns_phase_ticks")
+        names = ["prep", "binning", "state_table", "scatter", "argmax_write", "cigar", "chimera", "idle",
+                 "scatter_zero", "scatter_select", "scatter_stage", "scatter_walk"]
+        out = {k: t[i] / 1e5 for i, k in enumerate(names)}
+        out.update(groups=int(t[12]), items=int(t[13]), windows=int(t[14]), scatter_prepass=t[15] / 1e5)
+        return out
 
     def results(self) -> List[cns.ReadResult]:
         a = self.download()

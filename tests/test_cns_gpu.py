@@ -61,16 +61,72 @@ def test_gpu_matches_reference_batched():
     assert n > 20
 
 
-def test_gpu_scatter_fallback_path_matches_reference(monkeypatch):
-    """The in-kernel scatter path (taken when a read's expanded pileup exceeds the
-    per-workgroup scratch) forced for every read: same bytes as the reference."""
+@pytest.mark.parametrize("batched", [False, True])
+def test_gpu_large_geometry_matches_reference(monkeypatch, batched):
+    """The large LDS geometry (state table 4096, 512-column windows: the rerun of reads
+    whose tables outgrow the small one) forced for every read: same bytes as the
+    reference, one read per launch and all reads of a parameter set in one launch."""
     from proovread_amd import cns
-    monkeypatch.setenv("PRGPU_CNS_SCATTER", "1")
+    monkeypatch.setenv("PRGPU_CNS_LARGE", "1")
     n = 0
+    if not batched:
+        for c in CASES:
+            lr, alns, params = case_inputs(c)
+            if params.qual_weighted:
+                continue
+            _check(c, cns.run_chunk([lr], [alns], params)[0])
+            n += 1
+        assert n > 50
+        return
+    groups = {}
     for c in CASES:
         lr, alns, params = case_inputs(c)
-        if params.qual_weighted:
+        if params.qual_weighted or c.p("noref") == "1":
             continue
-        _check(c, cns.run_chunk([lr], [alns], params)[0])
-        n += 1
-    assert n > 50
+        groups.setdefault(params_key(params), (params, []))[1].append((c, lr, alns))
+    for params, items in groups.values():
+        for (c, _, _), r in zip(items, cns.run_chunk([x[1] for x in items], [x[2] for x in items], params)):
+            _check(c, r)
+            n += 1
+    assert n > 20
+
+
+def _insertion_heavy_case(name, seed, L, n_aln, every, ins_len, coverage):
+    """A long read whose alignments carry an insertion of ins_len random bases after every
+    `every` reference bases: many distinct insertion states (ins_len 6) or many
+    (column, state) pairs per window (ins_len 1, deep coverage)."""
+    import random
+    rng = random.Random(seed)
+    ref = "".join(rng.choice("ACGT") for _ in range(L))
+    starts = sorted(rng.randrange(0, L - 160) for _ in range(n_aln))
+    sam = []
+    for k, s in enumerate(starts):
+        seq, cig, r = [], [], s
+        while r < s + 150:
+            m = min(every, s + 150 - r)
+            seq.append(ref[r:r + m])
+            cig.append(f"{m}M")
+            r += m
+            if r < s + 150:
+                seq.append("".join(rng.choice("ACGT") for _ in range(ins_len)))
+                cig.append(f"{ins_len}I")
+        sq = "".join(seq)
+        sam.append(f"sr{k}\t0\tlr\t{s + 1}\t60\t{''.join(cig)}\t*\t0\t0\t{sq}\t{'I' * len(sq)}\tAS:i:{300 + rng.randrange(200)}")
+    return casefmt.Case(name, {"coverage": str(coverage)}, ["@lr", ref, "+", "$" * L], sam)
+
+
+@pytest.mark.parametrize("kind", ["states", "pairs"])
+def test_gpu_retry_geometry_matches_oracle(kind):
+    """Reads that overflow the small geometry's tables (> 1024 distinct insertion states, or
+    > 2048 (column, state) pairs in a 1024-column window) are rerun with the large one;
+    the result equals the C oracle's."""
+    import oracle_bind as ob
+    from proovread_amd import cns
+    c = (_insertion_heavy_case("many_states", 5, 3000, 150, 15, 6, 100.0) if kind == "states"
+         else _insertion_heavy_case("many_pairs", 6, 2000, 1000, 10, 1, 400.0))
+    lr, alns, params = case_inputs(c)
+    r = cns.run_chunk([lr], [alns], params)[0]
+    want = ob.run_case(c)
+    assert want["rc"] == 0 and r.status == 0, (want["rc"], r.status)
+    assert r.fastq == want["fastq"]
+    assert r.trace == want["trace"]
