@@ -40,6 +40,9 @@ sys.path.insert(0, str(ROOT))
 VALU_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 HBM_PEAK_GBS = 8000.0
 OPS_PER_CELL = 14   # SURVEY.md §8d canonical int ops per DP cell
+# bwa-proovread -b BIN -l LEN of a bwa-sr iteration: BIN = bin-size 20 (proovread.cfg:259-273),
+# LEN = BIN x min(--coverage 50, sr-coverage 15) (bin/proovread:1302-1313)
+BIN_FILTER = (20, 20.0 * 15.0)
 
 
 def parse():
@@ -69,8 +72,8 @@ def cpu_baseline(d, per_worker: int):
         np.savez(npz, lr_seq=d.lr_seq[:int(d.lr_off[n_s])], lr_off=d.lr_off[:n_s + 1], sr_seq=d.sr_seq,
                  sr_off=d.sr_off, t_sr=d.t_sr[:k], t_lr=d.t_lr[:k], t_strand=d.t_strand[:k], t_qbeg=d.t_qbeg[:k],
                  t_rbeg=d.t_rbeg[:k], t_slen=d.t_slen[:k])
-        subprocess.run([sys.executable, str(ROOT / "oracle" / "cpu_bench.py"), npz, str(n_s), str(workers), out],
-                       check=True)
+        subprocess.run([sys.executable, str(ROOT / "oracle" / "cpu_bench.py"), npz, str(n_s), str(workers), out, "0",
+                        str(BIN_FILTER[0]), str(BIN_FILTER[1])], check=True)
         r = json.loads(Path(out).read_text())
     cpu = {"value": round(r["bases"] / r["wall_s"] / 1e6, 4), "unit": "Mbases/s", "cores": r["workers"], "kind": "port",
            "sample": f"first {r['n']} of {d.n_lr} long reads of the same workload ({r['bases']} bases, their "
@@ -156,6 +159,7 @@ def main():
         d, seed_info = seed_front_end(ctx)
     it = iteration.Iteration(d, ctx=ctx)
     opts = sw.default_opts(finish=False)
+    opts.bin_size, opts.bin_length = BIN_FILTER     # bwa-proovread -b 20 -l 300 (proovread:1302-1313)
     params = cns.CnsParams(coverage=min(50.0, 15.0) * 0.75, use_ref_qual=True)   # proovread:1540-1541
     from proovread_amd import mask
     mparams = mask.params("20,41,80,130,60,0.7", 150)   # hcr-mask of bwa-sr-1 (proovread.cfg:234-242)

@@ -203,6 +203,12 @@ typedef struct pr_sw_opts {
     int32_t pen_clip5, pen_clip3;  /* -L 5,3 clipping penalties                     */
     int32_t zdrop;                 /* -d (bwa default 100)                          */
     double min_score_per_base;     /* -T "per-base-score" (cfg:324; semantics unpinned) */
+    /* -b BIN -l LEN: bwa-proovread's score binning of the reported alignments (its
+     * proovread.[ch], README.org:228-236; called with BIN = cfg bin-size, LEN = BIN x
+     * min(--coverage, task sr-coverage), bin/proovread:1302-1313).  Applied by pr_iter_launch
+     * between the SW stage and the consensus hand-off; 0 = off (pr_sw_opts_default).   */
+    int32_t bin_size;
+    double bin_length;
 } pr_sw_opts;
 /* finish = 0: bwa-sr iterations (-A5 -B11 -O2,1 -E4,3 -w40 -T2.5 -L30,30);
  * finish = 1: bwa-sr-finish (-A5 -B13 -O15,19 -E3,3 -w30 -T4 -L30,30)            */

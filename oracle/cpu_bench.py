@@ -7,7 +7,7 @@ timing and, per read, (rc, fastq, trace, chim lines) for bench.py's byte-for-byt
 comparison with the GPU output.  A separate process, so the fork pool never shares a
 process with a HIP runtime.
 
-    python oracle/cpu_bench.py WORKLOAD.npz N WORKERS OUT.json [finish]
+    python oracle/cpu_bench.py WORKLOAD.npz N WORKERS OUT.json [finish [BIN LEN]]
 """
 from __future__ import annotations
 
@@ -25,6 +25,7 @@ sys.path.insert(0, str(HERE))
 def main(argv) -> int:
     path, n, workers, out = argv[0], int(argv[1]), int(argv[2]), argv[3]
     finish = len(argv) > 4 and argv[4] == "1"
+    binf = (int(argv[5]), float(argv[6])) if len(argv) > 6 else None
     z = np.load(path)   # allow_pickle=False: arrays only
     d = SimpleNamespace(**{k: z[k] for k in z.files})
     d.n_lr = len(d.lr_off) - 1
@@ -32,7 +33,7 @@ def main(argv) -> int:
     n = min(n, d.n_lr)
     wall, bases, res, nw = cpu_chain.run_sample(d, range(n), task="bwa-sr-finish" if finish else "bwa-sr",
                                                 coverage=22.5 if finish else 11.25, use_ref_qual=not finish,
-                                                detect_chimera=finish, workers=workers, full=True)
+                                                detect_chimera=finish, workers=workers, full=True, bin_filter=binf)
     with open(out, "w") as f:
         json.dump({"wall_s": wall, "bases": bases, "workers": nw, "n": n,
                    "tasks": int(np.searchsorted(d.t_lr, n, side="left")),

@@ -30,6 +30,46 @@ _PARAMS = None
 _REF = None      # optional ASCII consensus reference pool (lr_off layout), else the mapped reads
 _QUAL = None     # optional reference qualities (phred+33), else '$'
 _FULL = False    # return (rc, fastq, trace, chim) instead of (rc, fastq)
+_BINF = None     # (BIN, LEN) of bwa-proovread -b/-l, or None
+
+
+def _aln_length(cig, lq):
+    """Sam::Alignment::length (Alignment.pm:417-431): M+D when SEQ is empty or the CIGAR
+    starts or ends with S, else the SEQ length."""
+    ops = [(x >> 4, x & 15) for x in cig]
+    if lq == 0 or (ops and (ops[0][1] == 4 or ops[-1][1] == 4)):
+        return sum(n for n, o in ops if o in (0, 2))
+    return lq
+
+
+def _bin_filter(recs, bin_size, bin_len):
+    """bwa-proovread -b/-l (bin/proovread:1302-1313; proovread.[ch] absent): proovread's own
+    score binning (Sam::Seq add_aln_by_score, Seq.pm:582-614) over the long read's reported
+    records in bwa output order: bin = int((POS + length/2) / BIN), ncscore =
+    AS/length * length/(40+length), a bin holding more than LEN bases admits a record only
+    if it beats the lowest ncscore, which it evicts.  recs: (pos0, score, length) in task
+    order -> keep flags."""
+    bins, keep = {}, [False] * len(recs)
+    for i, (pos0, score, length) in enumerate(recs):
+        if length <= 0:
+            continue
+        nc = (score / length) * (length / (40 + length))
+        b = int((pos0 + 1 + length / 2.0) / bin_size)
+        ent = bins.setdefault(b, [0, []])
+        lst = ent[1]
+        if ent[0] > bin_len:
+            if nc <= lst[-1][0]:
+                continue
+            _, old, olen = lst.pop()
+            keep[old] = False
+            ent[0] -= olen
+        ent[0] += length
+        k = len(lst) - 1
+        while k >= 0 and nc > lst[k][0]:
+            k -= 1
+        lst.insert(k + 1, (nc, i, length))
+        keep[i] = True
+    return keep
 
 
 def _lr_chain(lr: int):
@@ -55,7 +95,10 @@ def _lr_chain(lr: int):
         seq = (_ASCII[np.where(q < 4, 3 - q, 4)][::-1] if strand else _ASCII[q]).tobytes().decode()
         cg = "".join(f"{x >> 4}{'MIDNSHP=X'[x & 15]}" for x in r.cigar[:r.n_cigar])
         recs.append((r.pos, strand, t, f"sr{sid}\t{16 if strand else 0}\tlr{lr}\t{r.pos + 1}\t60\t{cg}\t*\t0\t0\t"
-                                       f"{seq}\t*\tAS:i:{r.score}"))
+                                       f"{seq}\t*\tAS:i:{r.score}", r.score, _aln_length(list(r.cigar[:r.n_cigar]), lq)))
+    if _BINF is not None:   # records in task order = bwa's output order for this long read
+        keep = _bin_filter([(x[0], float(x[4]), x[5]) for x in recs], *_BINF)
+        recs = [x for x, k in zip(recs, keep) if k]
     recs.sort(key=lambda x: (x[0], x[1], x[2]))
     lines = [x[3].encode() for x in recs]
     arr = (C.c_char_p * (len(lines) + 1))(*lines)
@@ -79,14 +122,16 @@ def _init_worker():
 
 
 def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers=None, ref_seq=None,
-               ref_qual=None, detect_chimera=False, full=False):
+               ref_qual=None, detect_chimera=False, full=False, bin_filter=None):
     """Run the CPU chain on long reads `lrs`; returns (wall seconds, bases, results, workers).
 
     ref_seq / ref_qual: ASCII consensus reference and its qualities in the long reads' layout
     (bam2cns --ref, the previous iteration's .fq) when it differs from the mapped reads;
-    full: per read (rc, fastq, trace, chim lines) instead of (rc, fastq)."""
-    global _D, _OPTS, _PARAMS, _REF, _QUAL, _FULL
+    full: per read (rc, fastq, trace, chim lines) instead of (rc, fastq); bin_filter: (BIN, LEN)
+    of bwa-proovread -b/-l applied to each long read's records, or None."""
+    global _D, _OPTS, _PARAMS, _REF, _QUAL, _FULL, _BINF
     _D = d
+    _BINF = tuple(bin_filter) if bin_filter else None
     _REF = None if ref_seq is None else np.ascontiguousarray(ref_seq, np.uint8)
     _QUAL = None if ref_qual is None else np.ascontiguousarray(ref_qual, np.uint8)
     _FULL = bool(full)

@@ -120,6 +120,8 @@ static void fill_sw_opts(pTHX_ HV *opts, pr_sw_opts *o) {
     o->pen_clip3 = inum(aTHX_ opts, "pen_clip3", o->pen_clip3);
     o->zdrop = inum(aTHX_ opts, "zdrop", o->zdrop);
     o->min_score_per_base = num(aTHX_ opts, "min_score_per_base", o->min_score_per_base);
+    o->bin_size = inum(aTHX_ opts, "bin_size", o->bin_size);
+    o->bin_length = num(aTHX_ opts, "bin_length", o->bin_length);
 }
 
 /* consensus output pools as Perl strings (13 of them, returned as a hash of packed data) */

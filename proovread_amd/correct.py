@@ -26,7 +26,7 @@ libprgpu.so and a gfx950 device).  Tests drive the same loop with the CPU oracle
 chain in place of the stages (tests/loop_oracle.py) to check the GPU loop
 byte-for-byte.  Deliberate scope: one GPU, the whole read set resident (at
 configs[1] size ~17 GB of device buffers, far below 288 GB); bwa-proovread's
--b/-l bin filter is not applied (the consensus' own binning follows).
+-b/-l bin filter runs on the device between the SW stage and the hand-off (A4).
 """
 from __future__ import annotations
 
@@ -70,6 +70,8 @@ class LoopConfig:
     lr_min_length: Optional[int] = None    # cfg lr-min-length (None: 2 * min_sr_length)
     tasks: Tuple[str, ...] = SR_NOCCS_TASKS
     seed_threads: int = 0
+    bin_size: int = 20                     # proovread.cfg:259-273 bin-size (sr modes)
+    bin_filter: bool = True                # bwa-proovread -b/-l in every iteration (proovread:1302-1313)
 
 
 @dataclasses.dataclass
@@ -170,11 +172,17 @@ class GpuStages:
         from . import _abi
         self.ctx = ctx or _abi.default_context()
 
-    def iteration(self, d, ref_seq: np.ndarray, ref_qual: np.ndarray, finish: bool, params) -> List[tuple]:
-        """-> per long read (status, seq, qual, chim lines with id `lr<i>`)."""
+    def iteration(self, d, ref_seq: np.ndarray, ref_qual: np.ndarray, finish: bool, params,
+                  bin_filter: Optional[Tuple[int, float]] = None) -> List[tuple]:
+        """-> per long read (status, seq, qual, chim lines with id `lr<i>`).  bin_filter: (BIN,
+        LEN) of bwa-proovread -b/-l, applied on the device between the SW stage and the
+        consensus hand-off."""
         from . import iteration, sw
         it = iteration.Iteration(d, lr_qual=ref_qual, ctx=self.ctx, ref_seq=ref_seq)
-        it.launch(sw.default_opts(finish=finish), params)
+        opts = sw.default_opts(finish=finish)
+        if bin_filter:
+            opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
+        it.launch(opts, params)
         return [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
 
     def mask(self, seqs: List[bytes], quals: List[bytes], hcr_mask: str, min_sr_length: int):
@@ -287,7 +295,9 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541
         params = cns.CnsParams(coverage=max_cov, use_ref_qual=not finish, detect_chimera=finish,
                                max_ins_length=0)
-        out = stages.iteration(d, ref_seq, ref_qual, finish, params) if hi > lo else []
+        # bwa-proovread -b BIN -l BIN*min(cov, task cov) (proovread:1302-1313, cfg bin-size)
+        binf = (cfg.bin_size, cfg.bin_size * min(cfg.coverage, task_cov)) if cfg.bin_filter else None
+        out = stages.iteration(d, ref_seq, ref_qual, finish, params, bin_filter=binf) if hi > lo else []
         seqs, quals, lines = [], [], []
         for i, (st, s, q, ch) in enumerate(out):
             if st != 0:

@@ -14,6 +14,15 @@ struct PipeDev {
     const int32_t *status, *pos, *score, *ncig;
     const int64_t *sr_off;
     const int64_t *cig_at;   // [n_task] first op of each task's CIGAR in the SW pool
+    const int64_t *lr_off;   // [n_lr+1] long-read offsets (bin count of the -b/-l filter)
+    const uint32_t *cig;     // SW CIGAR pool (cig_at)
+    uint8_t *keep;           // [n_task] survivors of the -b/-l filter, or null (filter off)
+    int32_t *fsorted;        // [n_task] scratch: tasks of a long read grouped by bin
+    int32_t *fbin;           // [n_task] scratch: bin of each task (-1: not reported)
+    double *fnc;             // [n_task] scratch: ncscore
+    int32_t *flen;           // [n_task] scratch: Sam::Alignment length
+    double *flst;            // [n_task] scratch: per-bin score lists
+    int32_t *flsti;          // [n_task] scratch: per-bin list members
     int32_t *cnt;            // [n_lr]
     int64_t *aln_off;        // [n_lr+1]
     int32_t *err;            // [n_lr]
@@ -28,6 +37,8 @@ struct PipeDev {
 };
 
 int pipe_launch(const PipeDev &P, int grid, void *stream, int lds_sort);
+// bwa-proovread -b/-l score binning (the filter runs before pipe_launch when P.keep is set)
+int pipe_binfilter_launch(const PipeDev &P, int bin_size, double bin_length, int max_bins, int grid, void *stream);
 int iter_stats_launch(const int64_t *out_off, const int32_t *status, const int32_t *seq_len, const uint8_t *qual,
                       int n_lr, int min_char, unsigned long long *out, void *stream);
 

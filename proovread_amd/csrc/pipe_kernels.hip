@@ -27,7 +27,8 @@ __global__ void __launch_bounds__(PIPE_THREADS) pipe_count_kernel(PipeDev P) {
     for (int lr = blockIdx.x; lr < P.n_lr; lr += gridDim.x) {
         const int64_t t0 = P.task_off[lr], t1 = P.task_off[lr + 1];
         int c = 0;
-        for (int64_t t = t0 + threadIdx.x; t < t1; t += PIPE_THREADS) c += (P.pass[t] && P.status[t] == 0) ? 1 : 0;
+        for (int64_t t = t0 + threadIdx.x; t < t1; t += PIPE_THREADS)
+            c += (P.pass[t] && P.status[t] == 0 && (!P.keep || P.keep[t])) ? 1 : 0;
         for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = c;
         __syncthreads();
@@ -79,7 +80,7 @@ __global__ void __launch_bounds__(PIPE_THREADS) pipe_sort_kernel(PipeDev P) {
         __syncthreads();
         for (int i = threadIdx.x; i < nt; i += PIPE_THREADS) {
             const int64_t t = t0 + i;
-            if (!(P.pass[t] && P.status[t] == 0)) continue;
+            if (!(P.pass[t] && P.status[t] == 0 && (!P.keep || P.keep[t]))) continue;
             const int slot = atomicAdd(&s_n, 1);
             keys[slot] = ((unsigned long long)(uint32_t)P.pos[t] << 33) |
                          ((unsigned long long)(P.strand[t] & 1u) << 32) | (unsigned long long)(uint32_t)i;
@@ -114,6 +115,134 @@ __global__ void __launch_bounds__(PIPE_THREADS) pipe_sort_kernel(PipeDev P) {
         }
         __syncthreads();
     }
+}
+
+// bwa-proovread's -b/-l filter (bin/proovread:1302-1313; its proovread.[ch] is absent, the
+// filter is restated as proovread's own score binning, Sam::Seq add_aln_by_score,
+// Seq.pm:582-614, as bwa_proovread.py's BinFilter does): per long read, the reported
+// alignments in bwa's output order (the read order of the tasks) are binned by centre,
+// bin = int((POS + length / 2) / BIN), length by Sam::Alignment::length
+// (Alignment.pm:417-431: M+D when clipped, else the SEQ length), ncscore =
+// AS/length * length/(40+length); a bin holding more than LEN bases admits an alignment
+// only if it beats the bin's lowest ncscore, which it evicts.  One workgroup per long
+// read: a stable counting sort by bin in LDS, then one thread per bin in task order.
+__global__ void __launch_bounds__(PIPE_THREADS) pipe_binfilter_kernel(PipeDev P, int bin_size, double bin_length,
+                                                                       int max_bins) {
+    extern __shared__ __attribute__((aligned(16))) int fsm[];
+    int *cnt = fsm, *start = fsm + max_bins, *chunk = fsm + 2 * max_bins;
+    __shared__ long long red[PIPE_THREADS / 64];
+    __shared__ int s_tot;
+    for (int lr = blockIdx.x; lr < P.n_lr; lr += gridDim.x) {
+        const int64_t t0 = P.task_off[lr], t1 = P.task_off[lr + 1];
+        const int nt = (int)(t1 - t0);
+        const long L = (long)(P.lr_off[lr + 1] - P.lr_off[lr]);
+        const int nbins = (int)((double)(L + 1024) / bin_size) + 2;   // centres <= L + query / 2
+        for (int b = threadIdx.x; b < nbins; b += PIPE_THREADS) cnt[b] = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < nt; i += PIPE_THREADS) {
+            const int64_t t = t0 + i;
+            P.keep[t] = 0;
+            int bin = -1;
+            if (P.pass[t] && P.status[t] == 0) {
+                const uint32_t *cg = P.cig + P.cig_at[t];
+                const int n = P.ncig[t];
+                const int sid = P.t_sr[t];
+                const int ls = (int)(P.sr_off[sid + 1] - P.sr_off[sid]);
+                long md = 0;
+                for (int k = 0; k < n; ++k) {
+                    const uint32_t op = cg[k] & 15u;
+                    if (op == 0u || op == 2u) md += cg[k] >> 4;
+                }
+                const bool clipped = n > 0 && ((cg[0] & 15u) == 4u || (cg[n - 1] & 15u) == 4u);
+                const long len = (ls == 0 || clipped) ? md : ls;
+                P.flen[t] = (int32_t)len;
+                if (len > 0) {
+                    const double sc = (double)P.score[t];
+                    P.fnc[t] = __dmul_rn(__ddiv_rn(sc, (double)len), __ddiv_rn((double)len, (double)(40 + len)));
+                    const double c = __ddiv_rn(__dadd_rn((double)(P.pos[t] + 1), __ddiv_rn((double)len, 2.0)),
+                                               (double)bin_size);
+                    bin = (int)(long)c;
+                    if (bin < 0 || bin >= nbins) bin = -2;   // cannot happen (nbins bound); reported as an error
+                }
+            }
+            P.fbin[t] = bin;
+            if (bin >= 0) atomicAdd(&cnt[bin], 1);
+            if (bin == -2) P.err[lr] = 2;
+        }
+        __syncthreads();
+        // exclusive scan of cnt -> start
+        {
+            const int per = (nbins + PIPE_THREADS - 1) / PIPE_THREADS;
+            const int b0 = threadIdx.x * per, b1 = (b0 + per) < nbins ? (b0 + per) : nbins;
+            long long s = 0;
+            for (int b = b0; b < b1; ++b) s += cnt[b];
+            long long x = s;
+            const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+            for (int o = 1; o < 64; o <<= 1) {
+                const long long y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (lane == 63) red[w] = x;
+            __syncthreads();
+            long long base = 0;
+            for (int k = 0; k < w; ++k) base += red[k];
+            base += x - s;
+            for (int b = b0; b < b1; ++b) { start[b] = (int)base; base += cnt[b]; cnt[b] = 0; }
+        }
+        __syncthreads();
+        // stable scatter by bin, chunks of 256 tasks in task order
+        for (int c0 = 0; c0 < nt; c0 += PIPE_THREADS) {
+            const int i = c0 + (int)threadIdx.x;
+            const int b = i < nt ? P.fbin[t0 + i] : -1;
+            chunk[threadIdx.x] = b;
+            __syncthreads();
+            int rank = 0;
+            bool last = true;
+            if (b >= 0) {
+                for (int j = 0; j < PIPE_THREADS; ++j) {
+                    const int bj = chunk[j];
+                    if (bj == b) { if (j < (int)threadIdx.x) ++rank; else if (j > (int)threadIdx.x) last = false; }
+                }
+                P.fsorted[t0 + start[b] + cnt[b] + rank] = i;
+            }
+            __syncthreads();
+            if (b >= 0 && last) cnt[b] += rank + 1;
+            __syncthreads();
+        }
+        // one thread per bin: sequential admission in task order
+        for (int b = threadIdx.x; b < nbins; b += PIPE_THREADS) {
+            const int sidx = start[b], nb = cnt[b];
+            double *ls = P.flst + t0 + sidx;
+            int32_t *la = P.flsti + t0 + sidx;
+            int ln = 0;
+            long bases = 0;
+            for (int k = 0; k < nb; ++k) {
+                const int i = P.fsorted[t0 + sidx + k];
+                const double nc = P.fnc[t0 + i];
+                if ((double)bases > bin_length) {
+                    if (nc <= ls[ln - 1]) continue;
+                    bases -= P.flen[t0 + la[ln - 1]];
+                    --ln;
+                }
+                bases += P.flen[t0 + i];
+                int j = ln - 1;
+                while (j >= 0 && nc > ls[j]) { ls[j + 1] = ls[j]; la[j + 1] = la[j]; --j; }
+                ls[j + 1] = nc; la[j + 1] = i;
+                ++ln;
+            }
+            for (int k = 0; k < ln; ++k) P.keep[t0 + la[k]] = 1;
+        }
+        __syncthreads();
+    }
+}
+
+int pipe_binfilter_launch(const PipeDev &P, int bin_size, double bin_length, int max_bins, int grid, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const int lds = (2 * max_bins + PIPE_THREADS) * 4;
+    hipError_t e = hipFuncSetAttribute((const void *)pipe_binfilter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return (int)e;
+    hipLaunchKernelGGL(pipe_binfilter_kernel, dim3(grid), dim3(PIPE_THREADS), lds, s, P, bin_size, bin_length, max_bins);
+    return (int)hipGetLastError();
 }
 
 // per-iteration statistic gathered across GPUs (proovread:1702-1720 computes

@@ -101,7 +101,7 @@ struct pr_ctx {
     bool pipe = false;
     bool pipe_ref_ascii = false;   // pr_iter_batch.ref_seq given: consensus reference in CB_REF_SEQ
     int pipe_sort_cap = 0;
-    DevBuf pb[4];           // task_off, cnt, err, (spare)
+    DevBuf pb[12];          // task_off, cnt, err, then the -b/-l filter: keep, sorted, bin, nc, len, lists
     float ms_pipe = 0.f, ms_cns = 0.f;
     // SW resident batch
     SwResident sw;
@@ -641,8 +641,34 @@ extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_param
     P.a_lseq = B[CB_LSEQ].as<int32_t>();
     P.a_cig_off = B[CB_CIG_OFF].as<int64_t>();
     P.a_ncig = B[CB_NCIG].as<int32_t>();
+    P.lr_off = B[CB_LR_OFF].as<int64_t>();
+    P.cig = sp.cig;
+    P.keep = nullptr;
     if (c->n_lr == 0) return 0;
     const int grid = c->n_lr < c->n_cu * 4 ? c->n_lr : c->n_cu * 4;
+    HIPCHK(hipMemsetAsync(c->pb[2].p, 0, (size_t)c->n_lr * 4, c->stream));
+    if (o->bin_size > 0 && o->bin_length > 0) {   // bwa-proovread -b/-l (bin/proovread:1302-1313)
+        const size_t nt1 = (size_t)sp.n_task + 1;
+        if ((rc = c->pb[3].ensure(nt1)) || (rc = c->pb[4].ensure(nt1 * 4)) || (rc = c->pb[5].ensure(nt1 * 4)) ||
+            (rc = c->pb[6].ensure(nt1 * 8)) || (rc = c->pb[7].ensure(nt1 * 4)) || (rc = c->pb[8].ensure(nt1 * 8)) ||
+            (rc = c->pb[9].ensure(nt1 * 4)))
+            return rc;
+        int64_t lmax = 0;
+        for (int i = 0; i < c->n_lr; ++i) lmax = std::max(lmax, c->lr_off_host[i + 1] - c->lr_off_host[i]);
+        const int64_t max_bins = (lmax + 1024) / o->bin_size + 2;
+        if ((2 * max_bins + 256) * 4 > 160 * 1024)
+            return set_error(PR_ERR_CAPACITY, "-b/-l filter: %lld bins per long read exceed the LDS layout",
+                             (long long)max_bins);
+        P.keep = c->pb[3].as<uint8_t>();
+        P.fsorted = c->pb[4].as<int32_t>();
+        P.fbin = c->pb[5].as<int32_t>();
+        P.fnc = c->pb[6].as<double>();
+        P.flen = c->pb[7].as<int32_t>();
+        P.flst = c->pb[8].as<double>();
+        P.flsti = c->pb[9].as<int32_t>();
+        int e = pipe_binfilter_launch(P, o->bin_size, o->bin_length, (int)max_bins, grid, (void *)c->stream);
+        if (e) return set_error(PR_ERR_HIP, "-b/-l filter kernel: %s", hipGetErrorString((hipError_t)e));
+    }
     int e = pipe_launch(P, grid, (void *)c->stream, c->pipe_sort_cap * 8);
     if (e) return set_error(PR_ERR_HIP, "pipe kernels: %s", hipGetErrorString((hipError_t)e));
     return pr_cns_launch(c, p);
@@ -650,7 +676,14 @@ extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_param
 
 extern "C" int pr_iter_download(pr_ctx *c, pr_cns_out *o) {
     if (!c) return set_error(PR_ERR_ARG, "null ctx");
-    return pr_cns_download(c, o);
+    int rc = pr_cns_download(c, o);
+    if (rc || !c->pipe || !c->n_lr) return rc;
+    // the hand-off's per-read error flags (sort capacity, filter bin range): never silent
+    std::vector<int32_t> err((size_t)c->n_lr);
+    HIPCHK(hipMemcpy(err.data(), c->pb[2].p, (size_t)c->n_lr * 4, hipMemcpyDeviceToHost));
+    for (int i = 0; i < c->n_lr; ++i)
+        if (err[(size_t)i]) return set_error(PR_ERR_CAPACITY, "hand-off of long read %d failed (code %d)", i, err[(size_t)i]);
+    return 0;
 }
 
 extern "C" int pr_iter_last_timing(pr_ctx *c, double *ms_sw_extend, double *ms_sw_global, double *ms_assemble,

@@ -80,6 +80,8 @@ static int up(SwResident &r, int id, const T *h, size_t n, hipStream_t s) {
 }
 
 extern "C" void pr_sw_opts_default(pr_sw_opts *o, int finish) {
+    o->bin_size = 0;
+    o->bin_length = 0.0;
     o->a = 5;
     o->pen_clip5 = o->pen_clip3 = 30;
     o->zdrop = 100;

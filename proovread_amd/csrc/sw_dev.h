@@ -18,7 +18,7 @@ namespace prgpu {
 // at least one query or reference base).  o_cig_at[t] is where the task's ops start.
 constexpr int SW_ST_OVERFLOW = 1;     // internal status, resolved before pr_sw_launch returns
 SW_HD inline int cig_slot_ops(int lq) {
-    const int c = (lq * 2 / 5 + 8 + 7) & ~7;
+    const int c = (lq * 5 / 8 + 16 + 7) & ~7;   // 150 bp: 112 ops (15 % error: mean 41, max seen 79)
     return c > 16 ? c : 16;
 }
 SW_HD inline int cig_bound_ops(int lqq, int rlen) { return lqq + rlen + 4; }

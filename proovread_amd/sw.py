@@ -25,7 +25,8 @@ def to_nt4(s: str) -> np.ndarray:
 class SwOpts(C.Structure):
     _fields_ = [("a", C.c_int32), ("b", C.c_int32), ("o_del", C.c_int32), ("e_del", C.c_int32),
                 ("o_ins", C.c_int32), ("e_ins", C.c_int32), ("w", C.c_int32), ("pen_clip5", C.c_int32),
-                ("pen_clip3", C.c_int32), ("zdrop", C.c_int32), ("min_score_per_base", C.c_double)]
+                ("pen_clip3", C.c_int32), ("zdrop", C.c_int32), ("min_score_per_base", C.c_double),
+                ("bin_size", C.c_int32), ("bin_length", C.c_double)]
 
 
 class SwBatch(C.Structure):

@@ -17,11 +17,11 @@ class OracleStages:
     def __init__(self, workers: int = 4):
         self.workers = workers
 
-    def iteration(self, d, ref_seq, ref_qual, finish, params):
+    def iteration(self, d, ref_seq, ref_qual, finish, params, bin_filter=None):
         _, _, res, _ = cpu_chain.run_sample(
             d, range(d.n_lr), task="bwa-sr-finish" if finish else "bwa-sr", coverage=params.coverage,
             use_ref_qual=params.use_ref_qual, workers=self.workers, ref_seq=ref_seq, ref_qual=ref_qual,
-            detect_chimera=params.detect_chimera, full=True)
+            detect_chimera=params.detect_chimera, full=True, bin_filter=bin_filter)
         out = []
         for rc, fq, _trace, chim in res:
             if rc:

@@ -13,16 +13,20 @@ from pipeline_oracle import consensus_cases, sam_for_tasks
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("seeds", ["truth", "host", "truth-slot16"])
+@pytest.mark.parametrize("seeds", ["truth", "host", "truth-slot16", "host-binfilter"])
 @pytest.mark.parametrize("finish", [False, True])
 def test_iteration_matches_cpu_chain(finish, seeds, monkeypatch):
     """truth-slot16: CIGAR slots forced to 16 ops, so most alignments reach the consensus
-    through the overflow pass's spill area (the hand-off reads per-task CIGAR starts)."""
+    through the overflow pass's spill area (the hand-off reads per-task CIGAR starts).
+    host-binfilter: bwa-proovread's -b 20 -l 20*15 filter on the device before the hand-off
+    (bin/proovread:1302-1313), against the oracle chain with the same filter; the coverage
+    is raised so the filter drops alignments."""
     from proovread_amd import cns, iteration, seed, sw, synth
     if seeds.endswith("slot16"):
         monkeypatch.setenv("PRGPU_SW_CIG_SLOT", "16")
-    d = synth.simulate(31 + finish, 40000, 40, 2500, 15, sr_frac=1.0)
-    if seeds == "host":
+    binf = (20, 20.0 * 15) if seeds.endswith("binfilter") else None
+    d = synth.simulate(31 + finish, 40000, 40, 2500, 40 if binf else 15, sr_frac=1.0)
+    if seeds.startswith("host"):
         ix = seed.SeedIndex(d.lr_seq, d.lr_off)
         d = synth.with_seeded_tasks(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(finish), threads=4))
         ix.close()
@@ -33,9 +37,14 @@ def test_iteration_matches_cpu_chain(finish, seeds, monkeypatch):
     it = iteration.Iteration(d)
     cp = cns.CnsParams(coverage=float(params["coverage"]), use_ref_qual=params["use_ref_qual"] == "1",
                        detect_chimera=params["detect_chimera"] == "1")
-    it.launch(sw.default_opts(finish=finish), cp)
+    opts = sw.default_opts(finish=finish)
+    if binf:
+        opts.bin_size, opts.bin_length = binf
+    it.launch(opts, cp)
     got = it.results()
-    sams = sam_for_tasks(d, task)
+    sams = sam_for_tasks(d, task, bin_filter=binf)
+    if binf:   # the filter must bite: fewer records than the unfiltered chain
+        assert sum(map(len, sams.values())) < sum(map(len, sam_for_tasks(d, task).values()))
     cases = consensus_cases(d, sams, params)
     n_checked = 0
     for c, g in zip(cases, got):
