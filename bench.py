@@ -157,7 +157,9 @@ def main():
     cm = comm_mod.RcclComm.from_env(ctx) if world > 1 else None
     if args.seeds == "gpu":
         d, seed_info = seed_front_end(ctx)
-    it = iteration.Iteration(d, ctx=ctx)
+    t_up = time.perf_counter()
+    it = iteration.Iteration(d, ctx=ctx)   # host -> HBM upload of reads and tasks (outside the step)
+    upload_s = time.perf_counter() - t_up
     opts = sw.default_opts(finish=False)
     opts.bin_size, opts.bin_length = BIN_FILTER     # bwa-proovread -b 20 -l 300 (proovread:1302-1313)
     params = cns.CnsParams(coverage=min(50.0, 15.0) * 0.75, use_ref_qual=True)   # proovread:1540-1541
@@ -271,6 +273,11 @@ def main():
         },
         "cpu_baseline": cpu,
         "seeding": seed_info,
+        # one whole bwa-sr iteration as proovread runs it, wall clock: index build + seeding
+        # (host C++ threads, bwa-proovread index / mem front end) + upload + the timed step
+        "iteration_end_to_end_ms": (round((seed_info["index_s"] + seed_info["map_s"] + upload_s) * 1e3 +
+                                          el / args.steps * 1e3, 1) if seed_info else None),
+        "upload_ms": round(upload_s * 1e3, 1),
         "gen_s": round(gen_s, 1),
         "reads_ok": ok,
         "iteration_stat": {"bpt": bpt, "bpN": bpn, "masked_frac": round(bpn / bpt, 4) if bpt else None},

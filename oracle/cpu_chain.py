@@ -138,7 +138,10 @@ def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers
     if not hasattr(d, "_task_off"):
         d._task_off = np.zeros(d.n_lr + 1, np.int64)
         np.cumsum(np.bincount(d.t_lr, minlength=d.n_lr), out=d._task_off[1:])
-    _OPTS = ob.sw_opts(task)
+    if isinstance(task, str):
+        _OPTS = ob.sw_opts(task)
+    else:   # (a, b, o_del, o_ins, e_del, e_ins, w, pen_clip5, pen_clip3, zdrop, min_score_per_base)
+        _OPTS = ob.OswOpts(*task)
     _PARAMS = ob.OcnsParams()
     _PARAMS.max_coverage = coverage
     _PARAMS.bin_size = 20.0

@@ -37,26 +37,25 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-from . import control, seqchunker
+from . import control, seqchunker, tasks as T
 
 NT4 = np.full(256, 4, np.uint8)
 for _i, _c in enumerate(b"ACGT"):
     NT4[_c] = _i
     NT4[_c + 32] = _i
 
-# proovread.cfg:119 (the sr-noccs task list) and the per-task values the loop reads
-SR_NOCCS_TASKS = ("read-long", "bwa-sr-1", "bwa-sr-2", "bwa-sr-3", "bwa-sr-4", "bwa-sr-5", "bwa-sr-6",
-                  "bwa-sr-finish")
-HCR_MASK_DEF = "20,41,80,130,60,0.7"                      # proovread.cfg:234-242
-HCR_MASK_LATE = "20,41,80,130,60,0.3"                     # bwa-sr-4 .. bwa-sr-6
+# proovread.cfg:119 / 125 (the sr-noccs / mr-noccs task lists) and the per-task values the
+# loop reads (tasks.py restates the cfg entries)
+SR_NOCCS_TASKS = T.MODE_TASKS["sr-noccs"]
+MR_NOCCS_TASKS = T.MODE_TASKS["mr-noccs"]
 
 
 def hcr_mask_for(task: str) -> str:
-    return HCR_MASK_LATE if task in ("bwa-sr-4", "bwa-sr-5", "bwa-sr-6") else HCR_MASK_DEF
+    return T.hcr_mask(task)                                 # proovread.cfg:234-242
 
 
 def sr_coverage_for(task: str) -> float:
-    return 30.0 if task.endswith("-finish") else 15.0       # proovread.cfg:188-192
+    return T.sr_coverage(task)                              # proovread.cfg:188-192
 
 
 @dataclasses.dataclass
@@ -68,9 +67,9 @@ class LoopConfig:
     sampling: bool = True                  # --no-sampling turns it off
     min_sr_length: Optional[int] = None    # proovread:530-532 (None: shortest short read)
     lr_min_length: Optional[int] = None    # cfg lr-min-length (None: 2 * min_sr_length)
-    tasks: Tuple[str, ...] = SR_NOCCS_TASKS
+    mode: Optional[str] = None             # sr-noccs / mr-noccs; None: by short-read length (proovread:636-642)
+    tasks: Optional[Tuple[str, ...]] = None   # None: the mode's task list (proovread.cfg:105-127)
     seed_threads: int = 0
-    bin_size: int = 20                     # proovread.cfg:259-273 bin-size (sr modes)
     bin_filter: bool = True                # bwa-proovread -b/-l in every iteration (proovread:1302-1313)
 
 
@@ -172,14 +171,14 @@ class GpuStages:
         from . import _abi
         self.ctx = ctx or _abi.default_context()
 
-    def iteration(self, d, ref_seq: np.ndarray, ref_qual: np.ndarray, finish: bool, params,
+    def iteration(self, d, ref_seq: np.ndarray, ref_qual: np.ndarray, task: str, params,
                   bin_filter: Optional[Tuple[int, float]] = None) -> List[tuple]:
-        """-> per long read (status, seq, qual, chim lines with id `lr<i>`).  bin_filter: (BIN,
-        LEN) of bwa-proovread -b/-l, applied on the device between the SW stage and the
-        consensus hand-off."""
-        from . import iteration, sw
+        """-> per long read (status, seq, qual, chim lines with id `lr<i>`).  task: the bwa task
+        whose options the SW stage takes (proovread.cfg:318-365); bin_filter: (BIN, LEN) of
+        bwa-proovread -b/-l, applied on the device between the SW stage and the hand-off."""
+        from . import iteration
         it = iteration.Iteration(d, lr_qual=ref_qual, ctx=self.ctx, ref_seq=ref_seq)
-        opts = sw.default_opts(finish=finish)
+        opts = T.options(task)[1]
         if bin_filter:
             opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
         it.launch(opts, params)
@@ -222,16 +221,16 @@ from .comm import RcclComm, TorchComm  # noqa: E402
 Comm = TorchComm
 
 
-def _seed_tasks(lr_map, lr_off, sr, sr_off, finish, threads, comm):
+def _seed_tasks(lr_map, lr_off, sr, sr_off, seed_opts, threads, comm):
     """Tasks of the long reads this rank corrects (global ids), in the single run's order,
     and the [lo, hi) long-read range it owns."""
     from . import exact_shard as ex, seed
     ix = seed.SeedIndex(lr_map, lr_off)
     try:
         if comm is None or comm.world == 1:
-            return ix.map(sr, sr_off, seed.default_opts(finish), threads=threads), 0, len(lr_off) - 1
+            return ix.map(sr, sr_off, seed_opts, threads=threads), 0, len(lr_off) - 1
         s, e = ex.sr_range(len(sr_off) - 1, comm.world, comm.rank)
-        tk = ix.map(sr[sr_off[s]:sr_off[e]], sr_off[s:e + 1] - sr_off[s], seed.default_opts(finish), threads=threads)
+        tk = ix.map(sr[sr_off[s]:sr_off[e]], sr_off[s:e + 1] - sr_off[s], seed_opts, threads=threads)
     finally:
         ix.close()
     tk["sr"] += s
@@ -255,7 +254,8 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
     min_sr = cfg.min_sr_length or (min(srs.lengths) if srs.lengths else 200)
     stubby = cfg.lr_min_length if cfg.lr_min_length is not None else 2 * min_sr
     sampler = control.Sampler(sampling=cfg.sampling)
-    tasks = list(cfg.tasks)
+    mode = cfg.mode or T.mode_for(min_sr)
+    tasks = list(cfg.tasks or T.MODE_TASKS[mode])
     fracs: List[float] = []
     log: List[TaskLog] = []
     reads, ignored = None, []
@@ -271,8 +271,8 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
             log.append(TaskLog(task))
             tc += 1
             continue
-        if not task.startswith("bwa-sr"):
-            raise ValueError(f"task {task} is outside the sr-noccs loop")
+        if not (task.startswith("bwa-sr") or task.startswith("bwa-mr")):
+            raise ValueError(f"task {task} is outside the sr / mr loops")
         finish = task.endswith("-finish")
         ent = TaskLog(task)
         task_cov = sr_coverage_for(task)
@@ -281,7 +281,7 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         ref_map = reads.seqs if finish else mapped     # finish maps to the unmasked .fq (proovread:838-850)
         lr_map, lr_off = reads.pool(ref_map)
         lr_map = NT4[lr_map]
-        tk, lo, hi = _seed_tasks(lr_map, lr_off, sr, sr_off, finish, cfg.seed_threads, comm)
+        tk, lo, hi = _seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], cfg.seed_threads, comm)
         ent.n_tasks = int(len(tk))
         if hi - lo < len(reads.ids):   # this rank's long reads only
             tk = tk.copy()
@@ -296,8 +296,9 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         params = cns.CnsParams(coverage=max_cov, use_ref_qual=not finish, detect_chimera=finish,
                                max_ins_length=0)
         # bwa-proovread -b BIN -l BIN*min(cov, task cov) (proovread:1302-1313, cfg bin-size)
-        binf = (cfg.bin_size, cfg.bin_size * min(cfg.coverage, task_cov)) if cfg.bin_filter else None
-        out = stages.iteration(d, ref_seq, ref_qual, finish, params, bin_filter=binf) if hi > lo else []
+        bsz = T.bin_size(mode)
+        binf = (bsz, bsz * min(cfg.coverage, task_cov)) if cfg.bin_filter else None
+        out = stages.iteration(d, ref_seq, ref_qual, task, params, bin_filter=binf) if hi > lo else []
         seqs, quals, lines = [], [], []
         for i, (st, s, q, ch) in enumerate(out):
             if st != 0:

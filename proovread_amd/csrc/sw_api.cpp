@@ -169,7 +169,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
         return pr_set_error(PR_ERR_ARG, "bad scoring options");
     if ((long)o->a * r.qmax >= 8192)
         return pr_set_error(PR_ERR_ARG, "a * max read length must stay below 8192 (13-bit DP words)");
-    if (o->w > 40) return pr_set_error(PR_ERR_UNSUPPORTED, "band width w > 40 (register ring holds 2*80+2 columns)");
+    if (o->w > 1000) return pr_set_error(PR_ERR_UNSUPPORTED, "band width w > 1000");
     if (o->a > 15 || o->b > 16) return pr_set_error(PR_ERR_UNSUPPORTED, "match score > 15 or mismatch penalty > 16");
     HIPCHK(hipSetDevice(ctx_device(c)));
     (void)hipGetLastError();   // a failed earlier call must not poison this one
@@ -228,7 +228,11 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     const int lds_ext = (r.qmax + 1) * SW_WAVE * 4;
     const int qpad = (r.qmax + 8) & ~3;
     const int lds_glob = lds_ext + SW_WAVE * qpad;
-    const bool eh_hbm = lds_glob + 256 > 160 * 1024;
+    const bool eh_hbm_g = lds_glob + 256 > 160 * 1024;
+    // the wide-band extension kernel (tries with w > 80) keeps (qmax+2) words per lane
+    const int lds_wide = (r.qmax + 2) * SW_WAVE * 4;
+    const bool eh_hbm_x = (o->w << 1) > 80 && lds_wide + 256 > 160 * 1024;
+    const bool eh_hbm = eh_hbm_g || eh_hbm_x;
     const int blocks_per_cu = eh_hbm ? 2 : ((160 * 1024) / (lds_glob + 64) > 0 ? (160 * 1024) / (lds_glob + 64) : 1);
     int grid_g = ctx_ncu(c) * (blocks_per_cu < 8 ? blocks_per_cu : 8);
     D.z_slab = (int64_t)D.tmax * ((r.qmax + 3) / 4) * 4 * SW_WAVE;
@@ -237,7 +241,9 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
         if (grid_g > gmax) grid_g = (int)(gmax > 16 ? gmax : 16);
     }
     if (eh_hbm) {
-        D.eh_g_stride = (int64_t)((lds_glob + 255) & ~255) / 4;
+        const int row = lds_glob > lds_wide ? lds_glob : lds_wide;
+        D.eh_g_stride = (int64_t)((row + 255) & ~255) / 4;
+        D.eh_g_blocks = grid_g;
         if ((rc0 = ensure(r, SB_EHG, (size_t)D.eh_g_stride * 4 * (size_t)grid_g))) return rc0;
         D.eh_g = (uint32_t *)r.buf[SB_EHG];
     }

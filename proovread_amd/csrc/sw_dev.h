@@ -58,6 +58,7 @@ struct SwDev {
     int rerun;                 // sw_global_kernel: 1 = the overflow pass (ops at o_cig_at, bounded)
     uint32_t *eh_g;            // sw_global_kernel DP row in HBM (queries too long for LDS), or null
     int64_t eh_g_stride;       // dwords per block of eh_g
+    int eh_g_blocks;           // blocks eh_g holds (grid of the HBM-row kernels)
     uint8_t *z;                // direction-matrix slabs, one per resident block
     int64_t z_slab;            // bytes per slab (LDS kernel)
     int64_t z_ring_slab;       // dwords per slab (register-ring kernels: rows x words x 64 lanes)

@@ -170,6 +170,151 @@ __global__ void __launch_bounds__(SW_WAVE) sw_ext_phase_kernel(SwDev D, SwOptsDe
     }
 }
 
+// ksw_extend2 (oracle/sw_oracle.c osw_extend, upstream ksw.c) for one lane with the DP row
+// in memory: eh[j * SW_WAVE] = H(i-1, j-1) | E(i, j) << 16 (both >= 0 and < 2^15 in an
+// extension: a * query length + h0 <= 10000).  The band of any width; the wide-band
+// extension kernel's core (bands beyond the register ring's 80 columns).
+__device__ int ext_row_lane(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen, const uint8_t *Lr, long tb,
+                            int ts, bool comp, int tlen, const SwOptsDev &O, int w, int end_bonus, int h0, ExtIO &io) {
+    const int a = O.a, b = O.b, o_del = O.o_del, e_del = O.e_del, o_ins = O.o_ins, e_ins = O.e_ins;
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    io.qle = io.tle = io.gtle = 0;
+    io.gscore = -1;
+    io.max_off = 0;
+    if (qlen <= 0 || tlen <= 0) {
+        io.gscore = -1;
+        return h0;
+    }
+    for (int j = 0; j <= qlen + 1; ++j) eh[j * SW_WAVE] = 0u;
+    eh[0] = (uint32_t)h0;
+    eh[SW_WAVE] = (uint32_t)(h0 > oe_ins ? h0 - oe_ins : 0);
+    for (int j = 2; j <= qlen && (int)(eh[(j - 1) * SW_WAVE] & 0xFFFFu) > e_ins; ++j)
+        eh[j * SW_WAVE] = (uint32_t)((int)(eh[(j - 1) * SW_WAVE] & 0xFFFFu) - e_ins);
+    {   // cap the band by the longest possible gap (max matrix entry = a)
+        int max_ins = (int)((double)(qlen * a + end_bonus - o_ins) / e_ins + 1.);
+        max_ins = max_ins > 1 ? max_ins : 1;
+        w = w < max_ins ? w : max_ins;
+        int max_del = (int)((double)(qlen * a + end_bonus - o_del) / e_del + 1.);
+        max_del = max_del > 1 ? max_del : 1;
+        w = w < max_del ? w : max_del;
+    }
+    int max = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+    int beg = 0, end = qlen;
+    for (int i = 0; i < tlen; ++i) {
+        int tc = (int)Lr[tb + (long)ts * i];
+        if (comp && tc < 4) tc = 3 - tc;
+        int f = 0, h1, mm = 0, mj = -1;
+        if (beg < i - w) beg = i - w;
+        if (end > i + w + 1) end = i + w + 1;
+        if (end > qlen) end = qlen;
+        if (beg == 0) {
+            h1 = h0 - (o_del + e_del * (i + 1));
+            if (h1 < 0) h1 = 0;
+        } else {
+            h1 = 0;
+        }
+        int j;
+        for (j = beg; j < end; ++j) {
+            const uint32_t p = eh[j * SW_WAVE];
+            int M = (int)(p & 0xFFFFu), e = (int)(p >> 16);
+            const int qc = (int)Q[qb + qs * j];
+            M = M ? M + sw_score(tc, qc, a, b) : 0;
+            int h = M > e ? M : e;
+            h = h > f ? h : f;
+            const int hp = h1;
+            h1 = h;
+            mj = mm > h ? mj : j;
+            mm = mm > h ? mm : h;
+            int t = M - oe_del;
+            t = t > 0 ? t : 0;
+            e -= e_del;
+            e = e > t ? e : t;
+            eh[j * SW_WAVE] = (uint32_t)hp | ((uint32_t)e << 16);
+            t = M - oe_ins;
+            t = t > 0 ? t : 0;
+            f -= e_ins;
+            f = f > t ? f : t;
+        }
+        eh[end * SW_WAVE] = (uint32_t)h1;   // h1, e = 0
+        if (j == qlen) {
+            max_ie = gscore > h1 ? max_ie : i;
+            gscore = gscore > h1 ? gscore : h1;
+        }
+        if (mm == 0) break;
+        if (mm > max) {
+            max = mm, max_i = i, max_j = mj;
+            const int d = mj - i > 0 ? mj - i : i - mj;
+            max_off = max_off > d ? max_off : d;
+        } else if (O.zdrop > 0) {
+            if (i - max_i > mj - max_j) {
+                if (max - mm - ((i - max_i) - (mj - max_j)) * e_del > O.zdrop) break;
+            } else {
+                if (max - mm - ((mj - max_j) - (i - max_i)) * e_ins > O.zdrop) break;
+            }
+        }
+        for (j = beg; j < end && eh[j * SW_WAVE] == 0u; ++j) {}
+        beg = j;
+        for (j = end; j >= beg && eh[j * SW_WAVE] == 0u; --j) {}
+        end = j + 2 < qlen ? j + 2 : qlen;
+    }
+    io.qle = max_j + 1;
+    io.tle = max_i + 1;
+    io.gtle = max_ie + 1;
+    io.gscore = gscore;
+    io.max_off = max_off;
+    return max;
+}
+
+// One extension phase for bands beyond the register ring (w > 80 at this try): the DP row
+// per lane in LDS (queries <= LDSQ) or in a per-block HBM scratch; otherwise as
+// sw_ext_phase_kernel.
+template <bool HBM>
+__global__ void __launch_bounds__(SW_WAVE) sw_ext_wide_kernel(SwDev D, SwOptsDev O, int side, int tryi) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_x[];
+    const int lane = threadIdx.x;
+    uint32_t *eh = (HBM ? D.eh_g + (int64_t)blockIdx.x * D.eh_g_stride : lds_x) + lane;
+    const int n = D.list_n[0];
+    for (int64_t c0 = (int64_t)blockIdx.x * SW_WAVE; c0 < n; c0 += (int64_t)gridDim.x * SW_WAVE) {
+        const int64_t slot = c0 + lane;
+        if (slot >= n) continue;
+        const int64_t t = D.list[slot];
+        const TaskGeo g = task_geo(D, O, t);
+        int qb, qs, qlen, tlen, ts, end_bonus, h0;
+        long tb;
+        if (side == 0) {
+            qb = g.qbeg - 1; qs = -1; qlen = g.qbeg;
+            tlen = (int)(g.rbeg - g.rmax0);
+            tb = g.rev ? (long)g.L - g.rbeg : (long)g.rbeg - 1;
+            ts = g.rev ? 1 : -1;
+            end_bonus = O.pen_clip5;
+            h0 = g.slen * O.a;
+        } else {
+            const int qe0 = g.qbeg + g.slen;
+            const int re0 = (int)(g.rbeg + g.slen - g.rmax0);
+            qb = qe0; qs = 1; qlen = g.lq - qe0;
+            tlen = (int)(g.rmax1 - g.rmax0 - re0);
+            tb = g.rev ? (long)g.L - 1 - g.rbeg - g.slen : (long)g.rbeg + g.slen;
+            ts = g.rev ? -1 : 1;
+            end_bonus = O.pen_clip3;
+            h0 = D.o_score[t];
+        }
+        ExtIO io;
+        const int aw = O.w << tryi;
+        const int score = ext_row_lane(eh, g.Q, qb, qs, qlen, g.Lr, tb, ts, g.rev, tlen, O, aw, end_bonus, h0, io);
+        xref(D, side, XF_SCORE, t) = score;
+        xref(D, side, XF_QLE, t) = io.qle;
+        xref(D, side, XF_TLE, t) = io.tle;
+        xref(D, side, XF_GTLE, t) = io.gtle;
+        xref(D, side, XF_GSCORE, t) = io.gscore;
+        xref(D, side, XF_MAXOFF, t) = io.max_off;
+        if (tryi == 0) {
+            const int prev = side == 0 ? -1 : h0;
+            const bool stop = score == prev || io.max_off < (aw >> 1) + (aw >> 2);
+            D.x_try[t] = (uint8_t)(D.x_try[t] | (stop ? 0 : (1 << side)));
+        }
+    }
+}
+
 __device__ __forceinline__ int band_w(const SwOptsDev &O, int w, int qlen, int end_bonus) {
     int max_ins = (int)((double)(qlen * O.a + end_bonus - O.o_ins) / O.e_ins + 1.);
     max_ins = max_ins > 1 ? max_ins : 1;
@@ -1033,7 +1178,13 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
             else if (wb <= 40) hipLaunchKernelGGL(sw_ext_phase_kernel<40>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
             else if (wb <= 64) hipLaunchKernelGGL(sw_ext_phase_kernel<64>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
             else if (wb <= 80) hipLaunchKernelGGL(sw_ext_phase_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
-            else return (int)hipErrorInvalidValue;   // checked on the host (w <= 40)
+            else if (D.eh_g) hipLaunchKernelGGL(sw_ext_wide_kernel<true>, dim3(D.eh_g_blocks), dim3(SW_WAVE), 0, s, D, O, side, tryi);
+            else {
+                const int lds = (D.qmax + 2) * SW_WAVE * 4;
+                e = hipFuncSetAttribute((const void *)sw_ext_wide_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+                if (e != hipSuccess) return (int)e;
+                hipLaunchKernelGGL(sw_ext_wide_kernel<false>, dim3(grid_waves), dim3(SW_WAVE), lds, s, D, O, side, tryi);
+            }
             if ((e = hipGetLastError()) != hipSuccess) return (int)e;
         }
         if (side == 0) hipLaunchKernelGGL(sw_left_finish_kernel, dim3(fgrid), dim3(256), 0, s, D, O);

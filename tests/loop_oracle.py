@@ -17,9 +17,13 @@ class OracleStages:
     def __init__(self, workers: int = 4):
         self.workers = workers
 
-    def iteration(self, d, ref_seq, ref_qual, finish, params, bin_filter=None):
+    def iteration(self, d, ref_seq, ref_qual, task, params, bin_filter=None):
+        from proovread_amd import tasks as T
+        o = T.options(task)[1]
+        sw = (o.a, o.b, o.o_del, o.o_ins, o.e_del, o.e_ins, o.w, o.pen_clip5, o.pen_clip3, o.zdrop,
+              o.min_score_per_base)
         _, _, res, _ = cpu_chain.run_sample(
-            d, range(d.n_lr), task="bwa-sr-finish" if finish else "bwa-sr", coverage=params.coverage,
+            d, range(d.n_lr), task=sw, coverage=params.coverage,
             use_ref_qual=params.use_ref_qual, workers=self.workers, ref_seq=ref_seq, ref_qual=ref_qual,
             detect_chimera=params.detect_chimera, full=True, bin_filter=bin_filter)
         out = []

@@ -19,7 +19,7 @@ def sam_for_tasks(d, task="bwa-sr", bin_filter=None):
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "oracle"))
     import cpu_chain
-    o = ob.sw_opts(task)
+    o = ob.sw_opts(task) if isinstance(task, str) else task   # a task name or an OswOpts
     per_lr = {}
     for t in range(len(d.t_sr)):
         sr, lr = int(d.t_sr[t]), int(d.t_lr[t])

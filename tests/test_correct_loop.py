@@ -17,8 +17,8 @@ from proovread_amd import correct, seqchunker, synth
 ACGT = np.frombuffer(b"ACGT", np.uint8)
 
 
-def _inputs(seed=5, gl=24000, n_lr=10, lr_len=2400, sr_cov=40.0):
-    d = synth.simulate(seed, gl, n_lr, lr_len, sr_cov, sr_frac=1.0)
+def _inputs(seed=5, gl=24000, n_lr=10, lr_len=2400, sr_cov=40.0, sr_len=150):
+    d = synth.simulate(seed, gl, n_lr, lr_len, sr_cov, sr_frac=1.0, sr_len=sr_len)
     lrs = [(f"lr_{i}", ACGT[np.minimum(d.lr_seq[d.lr_off[i]:d.lr_off[i + 1]], 3)].tobytes(), None)
            for i in range(d.n_lr)]
     sr = io.BytesIO()
@@ -85,6 +85,53 @@ def test_loop_on_oracle_stages():
     assert all(len(s) == len(q) for s, q in zip(res.reads.seqs, res.reads.quals))
     for ln in res.chim:
         assert ln.split("\t")[0] in res.reads.ids
+
+
+def test_mr_loop_on_oracle_stages():
+    """300 bp short reads: proovread picks the mr-noccs mode (bin/proovread:636-642), its
+    bwa-mr-1 / bwa-mr / bwa-mr-finish option sets (proovread.cfg:343-365) and bin size 50
+    (-b 50 -l 50*min(cov, task cov)); the reads get corrected."""
+    import loop_oracle
+    d, lrs, srd = _inputs(seed=9, sr_len=300, sr_cov=40.0)
+    res = correct.run(lrs, srd, correct.LoopConfig(coverage=40.0, seed_threads=2), stages=loop_oracle.OracleStages(4))
+    tasks = [e.task for e in res.log]
+    assert tasks[0] == "read-long" and tasks[1] == "bwa-mr-1" and tasks[-1] == "bwa-mr-finish"
+    km = _kmers(d.genome)
+    raw = np.mean([_exact(s, km) for _, s, _ in lrs])
+    cor = np.mean([_exact(s, km) for s in res.reads.seqs])
+    assert raw < 0.3 and cor > 0.85, (raw, cor)
+
+
+def test_task_options_follow_proovread_cfg():
+    from proovread_amd import seed, sw, tasks as T
+    for t, fin in [("bwa-sr-1", False), ("bwa-sr-4", False), ("bwa-sr-finish", True)]:
+        so, wo = T.options(t)
+        ds, dw = seed.default_opts(fin), sw.default_opts(fin)
+        assert all(getattr(so, n) == getattr(ds, n) for n, _ in so._fields_), t
+        assert all(getattr(wo, n) == getattr(dw, n) for n, _ in wo._fields_), t
+    so, wo = T.options("bwa-mr-3")          # cfg('bwa-mr-3') -> bwa-mr (proovread:1991-1994)
+    assert (so.min_seed_len, so.drop_ratio, wo.min_score_per_base) == (13, 0.5, 3.0)
+    so, wo = T.options("bwa-mr-finish")     # bwa defaults for -r / -D
+    assert (so.min_seed_len, so.min_chain_weight, so.split_factor, so.drop_ratio, wo.b, wo.w) == (19, 40, 1.5, 0.5, 13, 30)
+    assert T.hcr_mask("bwa-mr-5").endswith(",0.3") and T.hcr_mask("bwa-mr-2").endswith(",0.7")
+    assert (T.sr_coverage("bwa-mr-2"), T.sr_coverage("bwa-mr-finish")) == (15.0, 30.0)
+    assert (T.bin_size("sr-noccs"), T.bin_size("mr-noccs")) == (20, 50)
+    assert T.mode_for(150) == "sr-noccs" and T.mode_for(151) == "mr-noccs"
+
+
+@pytest.mark.gpu
+def test_gpu_mr_loop_matches_oracle_loop():
+    import loop_oracle
+    _, lrs, srd = _inputs(seed=10, sr_len=300, sr_cov=40.0)
+    cfg = correct.LoopConfig(coverage=40.0, seed_threads=4)
+    want = correct.run(lrs, srd, cfg, stages=loop_oracle.OracleStages(8))
+    got = correct.run(lrs, srd, cfg)
+    assert [e.task for e in got.log] == [e.task for e in want.log] and got.log[1].task == "bwa-mr-1"
+    for g, w in zip(got.log, want.log):
+        assert (g.n_sr, g.n_tasks, g.bpt, g.bpn, g.shortcut) == (w.n_sr, w.n_tasks, w.bpt, w.bpn, w.shortcut), g.task
+    assert got.reads.seqs == want.reads.seqs
+    assert got.reads.quals == want.reads.quals
+    assert got.chim == want.chim
 
 
 @pytest.mark.gpu
