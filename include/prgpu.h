@@ -184,9 +184,10 @@ int pr_cns_last_timing(pr_ctx *ctx, double *ms_prep, double *ms_pileup);
  * (SURVEY.md §8d pileup byte model) */
 /* Diagnostics: wall-clock ticks (100 MHz) the consensus workgroups spent per phase in the
  * last launch, summed over workgroups: [prep, binning, state table, pileup scatter,
- * argmax+write, Trace2cigar, chimera, dequeue/idle], then (n >= 16) the scatter's parts
- * [zero + ignore bits, group select, staging copy, state walks] and counts [candidate
- * groups, work items, windows]; n must be >= 8 (the first min(n, 16) are filled). */
+ * argmax+write, Trace2cigar, chimera, dequeue/idle], then (n >= 24) the scatter's parts
+ * [zero + ignore bits, group select, staging copy, fixed-state runs], counts [candidate
+ * groups, candidates, windows], [op pre-pass], [insertion states], 3 spare;
+ * n must be >= 8 (the first min(n, 24) are filled). */
 int pr_cns_phase_ticks(pr_ctx *ctx, uint64_t *ticks, int n);
 int pr_cns_resident_stats(pr_ctx *ctx, int64_t *columns, int64_t *alg_bytes);
 

@@ -99,6 +99,6 @@ constexpr int CHIM_MAXCOLS = 128;
 constexpr int CHIM_TCAP = 256;
 // per-phase wall-clock ticks: prep, binning, state table, scatter, argmax+write, cigar, chimera,
 // idle; scatter detail: zero+ignore, group select, staging, walks; counts: groups, items, windows
-constexpr int CNS_NPHASE = 16;
+constexpr int CNS_NPHASE = 24;
 
 }  // namespace prgpu

@@ -1135,32 +1135,111 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                     tlast = t_;
                 }
                 if (C->flag) break;
-                // runs in parallel: one LDS read of the staged base and one LDS atomic per state
+                // runs in parallel, balanced by visits: an exclusive prefix of the run lengths
+                // (kept in runs[].y above the 10-bit SEQ offset) gives every thread an equal
+                // contiguous slice of the group's (run, column) visits; per visit one LDS read
+                // of the staged base and one LDS atomic
                 const int nrun = C->nrun, nins = C->nins;
-                for (int r = tid; r < nrun; r += CNS_THREADS) {
-                    const int2 rr = runs[r];
-                    const int c0r = rr.x & 1023, len = (rr.x >> 10) & 1023, j = (rr.x >> 21) & 255;
-                    if (rr.x & (1 << 20)) {   // '-'
-                        for (int x = 0; x < len; ++x) {
-                            const int c = c0r + x;
-                            if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
-                            atomicAdd(&cnt[3 * c + 2], 1u);
+                {
+                    const int rpt = (nrun + CNS_THREADS - 1) / CNS_THREADS;
+                    const int ra = tid * rpt < nrun ? tid * rpt : nrun, rb = ra + rpt < nrun ? ra + rpt : nrun;
+                    long long ls = 0;
+                    for (int r = ra; r < rb; ++r) ls += (runs[r].x >> 10) & 1023;
+                    long long vtot;
+                    long long vp = block_scan_excl(ls, scan, &vtot);
+                    for (int r = ra; r < rb; ++r) {
+                        const int2 rr = runs[r];
+                        runs[r].y = (rr.y & 1023) | (int)(vp << 10);
+                        vp += (rr.x >> 10) & 1023;
+                    }
+                    __syncthreads();
+                    if (D.prof && tid == 0) {
+                        pt[17] += (unsigned long long)vtot; pt[18] += (unsigned long long)nrun; pt[19] += (unsigned long long)nins;
+                        const unsigned long long t_ = wall_clock64();
+                        pt[20] += t_ - tlast;
+                        tlast = t_;
+                    }
+                    const long long v0 = vtot * tid / CNS_THREADS, v1 = vtot * (tid + 1) / CNS_THREADS;
+                    if (v0 < v1) {
+                        int lo = 0, hi = nrun - 1;   // last run starting at or before v0
+                        while (lo < hi) {
+                            const int mid = (lo + hi + 1) >> 1;
+                            if ((long long)((uint32_t)runs[mid].y >> 10) <= v0) lo = mid; else hi = mid - 1;
                         }
-                        continue;
+                        int r = lo;
+                        int x = (int)(v0 - (long long)((uint32_t)runs[r].y >> 10));
+                        if (snt4) {
+                            // one loop over the thread's visits (no per-run inner loops, so the
+                            // lanes of a wave stay in step); a run is decoded into a column base,
+                            // a staged-SEQ address + step (reverse strand: backwards) and the
+                            // nucleotide -> state-index nibble table ('-' runs: every code -> 4)
+                            int len = 0, cb = 0, sa = 0, st = 0;
+                            uint32_t lut = 0;
+                            auto decode = [&](int rk) {
+                                const int2 rr = runs[rk];
+                                cb = rr.x & 1023;
+                                len = (rr.x >> 10) & 1023;
+                                if (rr.x & (1 << 20)) {
+                                    sa = 0; st = 0; lut = 0x44444u;
+                                } else {
+                                    const int j = (rr.x >> 21) & 255;
+                                    const int4 m = cmeta[j];
+                                    const int q0 = m.z + (rr.y & 1023);
+                                    const bool rc = m.w < 0;
+                                    sa = cso[j] + (rc ? (m.w & 0x7FFFFFFF) - 1 - q0 : q0);
+                                    st = rc ? -1 : 1;
+                                    lut = rc ? 0x50321u : 0x51230u;
+                                }
+                            };
+                            decode(r);
+                            for (long long v = v0; v < v1; ++v) {
+                                if (x >= len) { decode(++r); x = 0; }
+                                const int c = cb + x;
+                                uint32_t b8 = seqs[sa + st * x];
+                                b8 = b8 > 4u ? 4u : b8;
+                                const int fi = (int)((lut >> (4u * b8)) & 15u);
+                                ++x;
+                                if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
+                                atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
+                            }
+                        } else {
+                            long long v = v0;
+                            while (v < v1) {
+                                const int2 rr = runs[r];
+                                const int c0r = rr.x & 1023, len = (rr.x >> 10) & 1023, j = (rr.x >> 21) & 255;
+                                const int xe = (long long)(len - x) < v1 - v ? len : x + (int)(v1 - v);
+                                v += xe - x;
+                                if (rr.x & (1 << 20)) {   // '-'
+                                    for (; x < xe; ++x) {
+                                        const int c = c0r + x;
+                                        if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
+                                        atomicAdd(&cnt[3 * c + 2], 1u);
+                                    }
+                                } else {
+                                    const int4 m = cmeta[j];
+                                    SeqV sv;
+                                    sv.p = seqs + cso[j];
+                                    sv.n = m.w & 0x7FFFFFFF;
+                                    sv.rc = m.w < 0;
+                                    sv.nt4 = false;
+                                    const int q0 = m.z + (rr.y & 1023);   // sb + qoff
+                                    for (; x < xe; ++x) {
+                                        const int c = c0r + x;
+                                        if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
+                                        const int fi = fixed_idx_at(sv, q0 + x);
+                                        atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
+                                    }
+                                }
+                                ++r;
+                                x = 0;
+                            }
+                        }
                     }
-                    const int4 m = cmeta[j];
-                    SeqV sv;
-                    sv.p = seqs + cso[j];
-                    sv.n = m.w & 0x7FFFFFFF;
-                    sv.rc = m.w < 0;
-                    sv.nt4 = snt4;
-                    const int q0 = m.z + rr.y;   // sb + qoff
-                    for (int x = 0; x < len; ++x) {
-                        const int c = c0r + x;
-                        if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
-                        const int fi = fixed_idx_at(sv, q0 + x);
-                        atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
-                    }
+                }
+                if (D.prof && tid == 0) {   // runs: slot 11; insertion states: slot 16
+                    const unsigned long long t_ = wall_clock64();
+                    pt[11] += t_ - tlast;
+                    tlast = t_;
                 }
                 for (int r = tid; r < nins; r += CNS_THREADS) {
                     const int2 ir = insr[r];
@@ -1177,7 +1256,7 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                         C->flag = 1;
                 }
                 __syncthreads();
-                CNS_TICK(11);
+                CNS_TICK(16);
                 if (D.prof && tid == 0) { pt[12] += 1; pt[13] += (unsigned long long)gs; }
                 c0 += gs;
             }

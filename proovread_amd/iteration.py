@@ -139,12 +139,14 @@ class Iteration:
 
     def cns_phase_ms(self):
         """Consensus workgroup time per phase (ms summed over workgroups) of the last launch."""
-        t = (C.c_uint64 * 16)()
-        _abi.check(self.L.pr_cns_phase_ticks(self.ctx.h, t, 16), "pr_cns_phase_ticks")
+        t = (C.c_uint64 * 24)()
+        _abi.check(self.L.pr_cns_phase_ticks(self.ctx.h, t, 24), "pr_cns_phase_ticks")
         names = ["prep", "binning", "state_table", "scatter", "argmax_write", "cigar", "chimera", "idle",
                  "scatter_zero", "scatter_select", "scatter_stage", "scatter_walk"]
         out = {k: t[i] / 1e5 for i, k in enumerate(names)}
-        out.update(groups=int(t[12]), items=int(t[13]), windows=int(t[14]), scatter_prepass=t[15] / 1e5)
+        out.update(groups=int(t[12]), items=int(t[13]), windows=int(t[14]), scatter_prepass=t[15] / 1e5,
+                   scatter_ins=t[16] / 1e5, visits=int(t[17]), runs=int(t[18]), ins_states=int(t[19]),
+                   scatter_runscan=t[20] / 1e5)
         return out
 
     def results(self) -> List[cns.ReadResult]:
