@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the configs[1] workload per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-lrs-per-worker", type=int, default=256)
-    ap.add_argument("--seeds", choices=("truth", "host", "gpu"), default="host",
+    ap.add_argument("--seeds", choices=("truth", "host", "gpu"), default="gpu",
                     help="task list: the product's seeding front end (host path / GPU path; bwa mem seeding "
                          "+ chaining restated), or the simulation truth; computed before the timed region")
     return ap.parse_args()
@@ -121,24 +121,45 @@ def main():
     seed_info = None
 
     def seed_front_end(ctx=None):
-        """The front end (bwa-proovread mem seeding + chaining) on this rank's reads, outside
-        the timed region: the step measures the iteration from resident tasks."""
+        """The front end (bwa-proovread index + mem seeding and chaining) on this rank's reads,
+        outside the timed region: the step measures the iteration from resident tasks.
+        ctx: index built in HBM and seeding on the GPU (checked against the host path on a
+        sample of reads); None: host C++ threads."""
         from proovread_amd import seed as seeding
+        o = seeding.default_opts(False)
         t = time.perf_counter()
-        ix = seeding.SeedIndex(d.lr_seq, d.lr_off)
+        if ctx is None:
+            ix = seeding.SeedIndex(d.lr_seq, d.lr_off)
+        else:
+            ix = seeding.DeviceSeedIndex(ctx, d.lr_seq, d.lr_off)
         t_ix = time.perf_counter() - t
         t = time.perf_counter()
         if ctx is None:
-            tasks = ix.map(d.sr_seq, d.sr_off, seeding.default_opts(False), threads=min(16, os.cpu_count() or 1))
-            ms = None
+            tasks = ix.map(d.sr_seq, d.sr_off, o, threads=min(16, os.cpu_count() or 1))
+            ms = ix_ms = None
+            check = seed_phases = None
         else:
-            ix.to_gpu(ctx)
-            tasks, _ = ix.map_gpu(d.sr_seq, d.sr_off, seeding.default_opts(False))
-            ms = ix.gpu_ms()
+            tasks, _ = ix.map(d.sr_seq, d.sr_off, o)
+            ms, ix_ms = ix.gpu_ms(), ix.build_ms()
+            seed_phases = ix.phase_ms()
         t_map = time.perf_counter() - t
-        ix.close()
-        info = {"path": "gpu" if ctx is not None else "host", "index_s": round(t_ix, 2), "map_s": round(t_map, 2),
-                "reads_per_s": round(d.n_sr / t_map, 1), "kernel_ms": ms, "tasks": int(len(tasks))}
+        if ctx is None:
+            ix.close()
+        else:
+            # parity of the GPU front end: the host path (host index + host seeding) on the
+            # first reads of the shard, task for task
+            ns = min(d.n_sr, 20_000)
+            hx = seeding.SeedIndex(d.lr_seq, d.lr_off)
+            want = hx.map(d.sr_seq[:d.sr_off[ns]], d.sr_off[:ns + 1], o, threads=min(16, os.cpu_count() or 1))
+            hx.close()
+            got = tasks[tasks["sr"] < ns]
+            check = {"reads": int(ns), "tasks": int(len(want)), "equal": bool(np.array_equal(got, want))}
+            if not check["equal"]:
+                raise SystemExit(f"bench: GPU seeding differs from the host path on the first {ns} reads")
+        info = {"path": "gpu" if ctx is not None else "host", "index_s": round(t_ix, 3), "map_s": round(t_map, 3),
+                "reads_per_s": round(d.n_sr / t_map, 1), "index_kernel_ms": ix_ms, "kernel_ms": ms,
+                "tasks": int(len(tasks)), "parity_vs_host": check,
+                "kernel_phase_ms_summed_over_waves": seed_phases}
         return synth.with_seeded_tasks(d, tasks), info
 
     if args.seeds == "host":
@@ -148,7 +169,8 @@ def main():
     # in a child process (its fork pool never shares a process with a HIP runtime).  Its
     # per-read outputs are also the parity check of the GPU run below.
     cpu, cpu_res = None, None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.seeds != "gpu":
+    want_cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+    if want_cpu and args.seeds != "gpu":
         cpu, cpu_res = cpu_baseline(d, args.cpu_lrs_per_worker)
 
     # GPU: libprgpu only (its own HIP runtime and RCCL); torch is never loaded here
@@ -157,6 +179,8 @@ def main():
     cm = comm_mod.RcclComm.from_env(ctx) if world > 1 else None
     if args.seeds == "gpu":
         d, seed_info = seed_front_end(ctx)
+        if want_cpu:   # the same GPU-seeded tasks, CPU chain in a child process
+            cpu, cpu_res = cpu_baseline(d, args.cpu_lrs_per_worker)
     t_up = time.perf_counter()
     it = iteration.Iteration(d, ctx=ctx)   # host -> HBM upload of reads and tasks (outside the step)
     upload_s = time.perf_counter() - t_up

@@ -328,8 +328,20 @@ int pr_seed_smem(const pr_seed_index *h, const uint8_t *q, int len, int x, int64
 int pr_seed_gpu_upload(pr_ctx *ctx, const pr_seed_index *h);
 int pr_seed_gpu_map(pr_ctx *ctx, const pr_seed_opts *o, const uint8_t *sr_seq, const int64_t *sr_off, int n_sr,
                     pr_seed_tasks *out, int32_t *status);
+/* The seed index built in the context's HBM from the long reads (bwa-proovread index,
+ * proovread:1270): the tables of pr_seed_index_build byte for byte (text, 12-mer lists
+ * sorted by a stable device radix sort, the bases after every hit, j-mer counts); replaces
+ * pr_seed_index_build + pr_seed_gpu_upload.  lr_seq: host codes (0-3 bases, else N). */
+int pr_seed_gpu_index_build(pr_ctx *ctx, const uint8_t *lr_seq, const int64_t *lr_off, int n_lr);
+/* pr_seed_index_digest's six values over the device-built index (test hook) */
+int pr_seed_gpu_index_digest(pr_ctx *ctx, uint64_t *out6);
+/* milliseconds of the last pr_seed_gpu_index_build (HIP events on the ctx stream) */
+int pr_seed_gpu_index_last_ms(pr_ctx *ctx, double *ms);
 /* milliseconds of the last pr_seed_gpu_map kernel (HIP events on the ctx stream) */
 int pr_seed_gpu_last_ms(pr_ctx *ctx, double *ms);
+/* Diagnostics: wall-clock ticks (100 MHz) of the last pr_seed_gpu_map summed over waves:
+ * [occurrence table, SMEMs + re-seeding, chaining, chain filter + output] */
+int pr_seed_gpu_phase_ticks(pr_ctx *ctx, uint64_t *ticks4);
 /* diagnostics (tests): the device path's core and capacities run on the host */
 int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opts *o, const uint8_t *sr_seq,
                             const int64_t *sr_off, int n_sr, int n_threads, pr_seed_tasks *out, int32_t *status);

@@ -652,8 +652,12 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
     // the reads this launch takes: all of them, or (large geometry) the retry list
     const int n_reads = G::RETRY ? D.n_lr : D.retry_n[0];
     int32_t *work = G::RETRY ? D.work : D.work + 1;
-    // phase clock (thread 0, 100 MHz wall clock): ticks per phase summed over workgroups
-    unsigned long long pt[CNS_NPHASE] = {};
+    // phase clock (thread 0, 100 MHz wall clock): ticks per phase summed over workgroups,
+    // kept in LDS after the control block (not in every lane's registers)
+    static_assert(sizeof(Ctrl) <= 64 && 64 + 8 * CNS_NPHASE <= G::OFF_SCAN, "phase clock slots");
+    unsigned long long *pt = reinterpret_cast<unsigned long long *>(smem + 64);
+    if (tid < CNS_NPHASE) pt[tid] = 0ULL;
+    __syncthreads();
     unsigned long long tlast = wall_clock64();
 #define CNS_TICK(ph)                                                      \
     do {                                                                  \

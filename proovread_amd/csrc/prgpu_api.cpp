@@ -17,6 +17,7 @@
 #include "pipe_dev.h"
 #include "mask_dev.h"
 #include "seed_dev.h"
+#include "seed_index_dev.h"
 
 using namespace prgpu;
 int sw_get_ptrs(pr_ctx *c, SwPtrs *p);
@@ -79,7 +80,8 @@ enum MaskBufId { MB_OFF, MB_SEQ, MB_QUAL, MB_OUT, MB_RUN_OFF, MB_RUNS, MB_TMP, M
 // device seeding: the index copy (SI_*) and per-call buffers (SB_*)
 enum SeedBufId {
     SI_TEXT, SI_CSTART, SI_CBLK, SI_LROFF, SI_KOFF, SI_KPOS, SI_KEXT, SI_CNT0,
-    SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SD_COUNT
+    SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SB_NEXT, SB_PRE, SB_DENSE,
+    SX_LRSEQ, SX_KEY0, SX_KEY1, SX_VAL0, SX_KC, SX_CNTPTR, SX_TEMP, SD_COUNT
 };
 
 struct pr_ctx {
@@ -112,6 +114,8 @@ struct pr_ctx {
     bool seed_loaded = false;
     seedc::IndexView seed_view{};
     float ms_seed = 0.f;
+    float ms_index = 0.f;
+    int64_t seed_n_text = 0, seed_n_hits = 0;
     bool iter_masked = false;
     bool cns_launched = false;   // a consensus launch filled the CB_O_* outputs
 };
@@ -991,6 +995,135 @@ extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
     return 0;
 }
 
+// the seed index built in HBM (seed_index.hip): the tables of pr_seed_index_build
+extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, int n_lr) {
+    if (!c || n_lr < 0 || (n_lr && (!lr_seq || !lr_off))) return set_error(PR_ERR_ARG, "null arg");
+    for (int i = 0; i < n_lr; ++i)
+        if (lr_off[i + 1] < lr_off[i]) return set_error(PR_ERR_ARG, "lr_off not monotone");
+    const int64_t l_pac = n_lr ? lr_off[n_lr] - lr_off[0] : 0;
+    if (2 * l_pac + 2 * (int64_t)n_lr >= (int64_t)UINT32_MAX)
+        return set_error(PR_ERR_CAPACITY, "long-read shard too large for the 32-bit seed index");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    DevBuf *D = c->sd;
+    const int64_t n_text = 2 * l_pac + 2 * (int64_t)n_lr;
+    // small host tables: rebased read offsets, contig starts, 4 KB block -> contig
+    std::vector<int64_t> off((size_t)n_lr + 1, 0), cstart(2 * (size_t)n_lr, 0);
+    for (int i = 0; i <= n_lr; ++i) off[(size_t)i] = lr_off[i] - (n_lr ? lr_off[0] : 0);
+    for (int i = 0; i < n_lr; ++i) {
+        cstart[(size_t)i] = off[(size_t)i] + i;
+        cstart[2 * (size_t)n_lr - 1 - i] = l_pac + n_lr + (l_pac - off[(size_t)i + 1]) + (n_lr - 1 - i);
+    }
+    const int64_t nb = (n_text >> seedc::CB_SHIFT) + 1;
+    std::vector<int32_t> cblk((size_t)nb, 0);
+    {
+        int ci = 0;
+        const int nc = 2 * n_lr;
+        for (int64_t b = 0; b < nb; ++b) {
+            while (ci + 1 < nc && cstart[(size_t)ci + 1] <= (b << seedc::CB_SHIFT)) ++ci;
+            cblk[(size_t)b] = ci;
+        }
+    }
+    const size_t nt = (size_t)(n_text > 0 ? n_text : 1);
+    const size_t temp = seed_index_temp_bytes(n_text);
+    int rc;
+    if ((rc = upload(D[SX_LRSEQ], n_lr ? lr_seq + lr_off[0] : lr_seq, (size_t)l_pac, s)) ||
+        (rc = upload(D[SI_LROFF], off.data(), off.size(), s)) || (rc = upload(D[SI_CSTART], cstart.data(), cstart.size(), s)) ||
+        (rc = upload(D[SI_CBLK], cblk.data(), cblk.size(), s)) || (rc = D[SI_TEXT].ensure(nt)) ||
+        (rc = D[SX_KEY0].ensure(nt * 4)) || (rc = D[SX_KEY1].ensure(nt * 4)) || (rc = D[SX_VAL0].ensure(nt * 4)) ||
+        (rc = D[SX_KC].ensure(((size_t)seedc::NK + 1) * 4)) || (rc = D[SI_KOFF].ensure(((size_t)seedc::NK + 1) * 4)) ||
+        (rc = D[SI_KPOS].ensure(nt * 4)) || (rc = D[SI_KEXT].ensure(nt * 8)) || (rc = D[SX_TEMP].ensure(temp)) ||
+        (rc = D[SX_CNTPTR].ensure(sizeof(uint32_t *) * (seedc::KI - 1))))
+        return rc;
+    SeedIndexBuild B{};
+    uint32_t *cptr[seedc::KI - 1];
+    for (int j = 1; j < seedc::KI; ++j) {
+        if ((rc = D[SI_CNT0 + j - 1].ensure(((size_t)1 << (2 * j)) * 4))) return rc;
+        cptr[j - 1] = B.cnt[j - 1] = D[SI_CNT0 + j - 1].as<uint32_t>();
+    }
+    HIPCHK(hipMemcpyAsync(D[SX_CNTPTR].p, cptr, sizeof cptr, hipMemcpyHostToDevice, s));
+    B.lr_seq = D[SX_LRSEQ].as<uint8_t>();
+    B.lr_off = D[SI_LROFF].as<int64_t>();
+    B.n_lr = n_lr;
+    B.l_pac = l_pac;
+    B.cstart = D[SI_CSTART].as<int64_t>();
+    B.n_text = n_text;
+    B.text = D[SI_TEXT].as<uint8_t>();
+    B.key0 = D[SX_KEY0].as<uint32_t>();
+    B.key1 = D[SX_KEY1].as<uint32_t>();
+    B.val0 = D[SX_VAL0].as<uint32_t>();
+    B.kc = D[SX_KC].as<uint32_t>();
+    B.koff = D[SI_KOFF].as<uint32_t>();
+    B.kpos = D[SI_KPOS].as<uint32_t>();
+    B.kext = D[SI_KEXT].as<uint64_t>();
+    B.cnt_dev = reinterpret_cast<uint32_t *const *>(D[SX_CNTPTR].p);
+    B.temp = D[SX_TEMP].p;
+    B.temp_bytes = temp;
+    HIPCHK(hipEventRecord(c->ev[8], s));
+    const int e = seed_index_device_build(B, s);
+    if (e) return set_error(PR_ERR_HIP, "seed index build: %s", hipGetErrorString((hipError_t)e));
+    HIPCHK(hipEventRecord(c->ev[9], s));
+    uint32_t nh = 0;
+    HIPCHK(hipMemcpyAsync(&nh, B.koff + seedc::NK, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_index = ms;
+    seedc::IndexView v{};
+    v.text = B.text;
+    v.n_text = n_text;
+    v.cstart = B.cstart;
+    v.n_contig = 2 * n_lr;
+    v.cblk = D[SI_CBLK].as<int32_t>();
+    v.lr_off = B.lr_off;
+    v.n_lr = n_lr;
+    v.l_pac = l_pac;
+    v.koff = B.koff;
+    v.kpos = B.kpos;
+    v.kext = B.kext;
+    for (int j = 0; j < seedc::KI - 1; ++j) v.cnt[j] = B.cnt[j];
+    c->seed_view = v;
+    c->seed_loaded = true;
+    c->seed_n_text = n_text;
+    c->seed_n_hits = nh;
+    return 0;
+}
+
+// the six digests of pr_seed_index_digest over the device index (test hook)
+extern "C" int pr_seed_gpu_index_digest(pr_ctx *c, uint64_t *out6) {
+    if (!c || !out6) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->seed_loaded || !c->seed_n_text) return set_error(PR_ERR_ARG, "no device-built seed index");
+    HIPCHK(hipSetDevice(c->device));
+    const seedc::IndexView &v = c->seed_view;
+    const size_t nt = (size_t)c->seed_n_text, nh = (size_t)c->seed_n_hits, nk = (size_t)seedc::NK;
+    std::vector<uint8_t> text(nt);
+    std::vector<uint32_t> koff(nk + 1), kpos(nh), kc(nk);
+    std::vector<uint64_t> kext(nh);
+    std::vector<int64_t> cstart((size_t)v.n_contig), lro((size_t)v.n_lr + 1);
+    std::vector<int32_t> cblk((size_t)((c->seed_n_text >> seedc::CB_SHIFT) + 1));
+    std::vector<std::vector<uint32_t>> cnt(seedc::KI);
+    HIPCHK(hipMemcpy(text.data(), v.text, nt, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(koff.data(), v.koff, (nk + 1) * 4, hipMemcpyDeviceToHost));
+    if (nh) HIPCHK(hipMemcpy(kpos.data(), v.kpos, nh * 4, hipMemcpyDeviceToHost));
+    if (nh) HIPCHK(hipMemcpy(kext.data(), v.kext, nh * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(kc.data(), c->sd[SX_KC].p, nk * 4, hipMemcpyDeviceToHost));
+    if (!cstart.empty()) HIPCHK(hipMemcpy(cstart.data(), v.cstart, cstart.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(lro.data(), v.lr_off, lro.size() * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(cblk.data(), v.cblk, cblk.size() * 4, hipMemcpyDeviceToHost));
+    for (int j = 0; j < seedc::KI - 1; ++j) {
+        cnt[(size_t)j].resize((size_t)1 << (2 * (j + 1)));
+        HIPCHK(hipMemcpy(cnt[(size_t)j].data(), v.cnt[j], cnt[(size_t)j].size() * 4, hipMemcpyDeviceToHost));
+    }
+    cnt[seedc::KI - 1] = std::move(kc);
+    seed_digest_tables(text, koff, kpos, kext, cnt, cstart, cblk, lro, out6);
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_index_last_ms(pr_ctx *c, double *ms) {
+    if (!c || !ms) return set_error(PR_ERR_ARG, "null arg");
+    *ms = c->ms_index;
+    return 0;
+}
+
 extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *sr_seq, const int64_t *sr_off, int n_sr,
                                pr_seed_tasks *out, int32_t *status) {
     if (!c || !o || !out || n_sr < 0 || (n_sr && (!sr_seq || !sr_off))) return set_error(PR_ERR_ARG, "null arg");
@@ -1012,18 +1145,19 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     K.n_sr = n_sr;
     K.caps = caps;
     K.stride = seedc::scratch_bytes(caps);
-    // lanes: two resident 64-lane waves per CU, bounded by the scratch (~0.45 MB per lane,
-    // ~15 GB at 256 CUs)
-    int64_t lanes = (int64_t)c->n_cu * 64 * 2;
-    if (lanes > n_sr) lanes = ((int64_t)n_sr + 63) / 64 * 64;
-    if (lanes < 64) lanes = 64;
+    // scratch slots: one per resident wave (a wave maps one read at a time; 12 per CU at
+    // the kernel's register use), ~0.45 MB each (~1.4 GB at 256 CUs)
+    int64_t lanes = (int64_t)c->n_cu * seed_slots_per_cu();
+    if (lanes > n_sr) lanes = n_sr;
+    if (lanes < 1) lanes = 1;
     K.n_lanes = lanes;
     const int64_t nb = n_sr ? sr_off[n_sr] : 0;
     int rc;
     if ((rc = upload(D[SB_SEQ], sr_seq, (size_t)nb, s)) || (rc = upload(D[SB_OFF], sr_off, (size_t)n_sr + 1, s)) ||
         (rc = D[SB_SCRATCH].ensure((size_t)(lanes * K.stride))) ||
         (rc = D[SB_OUT].ensure((size_t)n_sr * caps.out * sizeof(pr_seed_task) + 16)) ||
-        (rc = D[SB_NOUT].ensure((size_t)n_sr * 4 + 16)) || (rc = D[SB_STATUS].ensure((size_t)n_sr * 4 + 16)))
+        (rc = D[SB_NOUT].ensure((size_t)n_sr * 4 + 16)) || (rc = D[SB_STATUS].ensure((size_t)n_sr * 4 + 16)) ||
+        (rc = D[SB_NEXT].ensure(128)))
         return rc;
     K.sr_seq = D[SB_SEQ].as<uint8_t>();
     K.sr_off = D[SB_OFF].as<int64_t>();
@@ -1031,6 +1165,9 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     K.out = D[SB_OUT].as<pr_seed_task>();
     K.n_out = D[SB_NOUT].as<int32_t>();
     K.status = D[SB_STATUS].as<int32_t>();
+    K.next = D[SB_NEXT].as<int32_t>();
+    K.prof = reinterpret_cast<unsigned long long *>(D[SB_NEXT].as<uint8_t>() + 64);
+    HIPCHK(hipMemsetAsync(K.next, 0, 128, s));
     HIPCHK(hipEventRecord(c->ev[8], s));
     const int e = seed_launch(K, (void *)s);
     if (e) return set_error(PR_ERR_HIP, "seed kernel: %s", hipGetErrorString((hipError_t)e));
@@ -1047,14 +1184,19 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         total += nout[i];
         bad += st[i] != 0;
     }
-    std::vector<pr_seed_task> slots((size_t)n_sr * caps.out);
-    if ((rc = download(slots.data(), D[SB_OUT], slots.size(), s))) return rc;
-    HIPCHK(hipStreamSynchronize(s));
+    // compact on the device (read order), download the dense list
+    std::vector<int64_t> pre((size_t)n_sr + 1, 0);
+    for (int i = 0; i < n_sr; ++i) pre[(size_t)i + 1] = pre[(size_t)i] + nout[i];
+    if ((rc = upload(D[SB_PRE], pre.data(), (size_t)n_sr + 1, s)) ||
+        (rc = D[SB_DENSE].ensure(sizeof(pr_seed_task) * (size_t)(total > 0 ? total : 1))))
+        return rc;
+    const int e2 = seed_compact_launch(D[SB_OUT].as<pr_seed_task>(), D[SB_NOUT].as<int32_t>(), D[SB_PRE].as<int64_t>(),
+                                       n_sr, caps.out, D[SB_DENSE].as<pr_seed_task>(), (void *)s);
+    if (e2) return set_error(PR_ERR_HIP, "seed compaction: %s", hipGetErrorString((hipError_t)e2));
     out->t = (pr_seed_task *)std::malloc(sizeof(pr_seed_task) * (size_t)(total > 0 ? total : 1));
     if (!out->t) return set_error(PR_ERR_ARG, "out of host memory");
-    int64_t k = 0;
-    for (int i = 0; i < n_sr; ++i)
-        for (int j = 0; j < nout[i]; ++j) out->t[k++] = slots[(size_t)i * caps.out + j];
+    if (total && (rc = download(out->t, D[SB_DENSE], (size_t)total, s))) return rc;
+    HIPCHK(hipStreamSynchronize(s));
     out->n = total;
     if (status) std::memcpy(status, st.data(), (size_t)n_sr * 4);
     if (bad) return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags)", (long long)bad);
@@ -1064,6 +1206,14 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
 extern "C" int pr_seed_gpu_last_ms(pr_ctx *c, double *ms) {
     if (!c || !ms) return set_error(PR_ERR_ARG, "null arg");
     *ms = c->ms_seed;
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_phase_ticks(pr_ctx *c, uint64_t *ticks4) {
+    if (!c || !ticks4) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->sd[SB_NEXT].p) return set_error(PR_ERR_ARG, "no pr_seed_gpu_map launch yet");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(ticks4, c->sd[SB_NEXT].as<uint8_t>() + 64, 32, hipMemcpyDeviceToHost));
     return 0;
 }
 

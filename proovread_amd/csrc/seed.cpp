@@ -582,20 +582,35 @@ static uint64_t digest_of(const T *p, size_t n) {
     return h;
 }
 
+template <class A, class B, class Cc, class Dd, class E, class F, class G, class H>
+static void digest6(const A &text, const B &koff, const Cc &kpos, const Dd &kext, const E &cnt, const F &cstart,
+                    const G &cblk, const H &lr_off, uint64_t *out6) {
+    out6[0] = digest_of(text.data(), text.size());
+    out6[1] = digest_of(koff.data(), koff.size());
+    out6[2] = digest_of(kpos.data(), kpos.size());
+    out6[3] = digest_of(kext.data(), kext.size());
+    uint64_t c = 0;
+    for (int j = 0; j < KI; ++j) c = c * 31 + digest_of(cnt[j].data(), cnt[j].size());
+    out6[4] = c;
+    out6[5] = digest_of(cstart.data(), cstart.size()) * 31 + digest_of(cblk.data(), cblk.size()) * 7 +
+              digest_of(lr_off.data(), lr_off.size());
+}
+
 extern "C" int pr_seed_index_digest(const pr_seed_index *h, uint64_t *out6) {
     if (!h || !out6) return pr_set_error(PR_ERR_ARG, "null arg");
     const Index &I = h->I;
-    out6[0] = digest_of(I.text.data(), I.text.size());
-    out6[1] = digest_of(I.koff.data(), I.koff.size());
-    out6[2] = digest_of(I.kpos.data(), I.kpos.size());
-    out6[3] = digest_of(I.kext.data(), I.kext.size());
-    uint64_t c = 0;
-    for (int j = 0; j < KI; ++j) c = c * 31 + digest_of(I.cnt[j].data(), I.cnt[j].size());
-    out6[4] = c;
-    out6[5] = digest_of(I.cstart.data(), I.cstart.size()) * 31 + digest_of(I.cblk.data(), I.cblk.size()) * 7 +
-              digest_of(I.lr_off.data(), I.lr_off.size());
+    digest6(I.text, I.koff, I.kpos, I.kext, I.cnt, I.cstart, I.cblk, I.lr_off, out6);
     return 0;
 }
+
+namespace prgpu {
+void seed_digest_tables(const std::vector<uint8_t> &text, const std::vector<uint32_t> &koff,
+                        const std::vector<uint32_t> &kpos, const std::vector<uint64_t> &kext,
+                        const std::vector<std::vector<uint32_t>> &cnt, const std::vector<int64_t> &cstart,
+                        const std::vector<int32_t> &cblk, const std::vector<int64_t> &lr_off, uint64_t *out6) {
+    digest6(text, koff, kpos, kext, cnt, cstart, cblk, lr_off, out6);
+}
+}  // namespace prgpu
 
 extern "C" int pr_seed_index_occ(const pr_seed_index *h, const uint8_t *s, int n, int64_t *count) {
     if (!h || !s || !count || n <= 0) return pr_set_error(PR_ERR_ARG, "bad arg");

@@ -423,16 +423,34 @@ SC_HD int cal_max_gap(const pr_seed_opts &O, int qlen) {
     return l < O.w << 1 ? l : O.w << 1;
 }
 
-// The whole read: tasks into out[0, *n_out) (chain order after mem_chain_flt).
+// Everything after the occurrence table (S.hoff / hpos / hml / ge of the read, built by
+// build_occ or by the device's wave-parallel equivalent): SMEMs, chaining, the chain
+// filter and the tasks into out[0, *n_out) (chain order after mem_chain_flt).
 // Returns 0 or an SC_OVER_* mask (then the read's output is not valid).
-SC_HD int map_read(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
-                   pr_seed_task *out, int cap_out, int *n_out) {
+// ticks (device, optional): wall-clock ticks added per part [SMEMs, chaining, filter + output]
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SC_TICK(k)                                          \
+    do {                                                    \
+        if (ticks) {                                        \
+            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   \
+            ticks[k] += t_ - t_last;                        \
+            t_last = t_;                                    \
+        }                                                   \
+    } while (0)
+#else
+#define SC_TICK(k) do { (void)ticks; } while (0)
+#endif
+SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
+                        pr_seed_task *out, int cap_out, int *n_out, unsigned long long *ticks = nullptr) {
     *n_out = 0;
-    int err = build_occ(I, S, q, len);
-    if (err) return err;
+    int err = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
+#endif
     const Occ occ{&I, &S, q, len};
     const int nm = collect_intv(occ, S, O, q, len, err);
     if (err) return err;
+    SC_TICK(0);
     // mem_chain
     int32_t ns = 0, ncv = 0;
     for (int mi = 0; mi < nm; ++mi) {
@@ -482,6 +500,7 @@ SC_HD int map_read(const IndexView &I, const pr_seed_opts &O, Scratch &S, const 
             S.ord[lo] = ncv++;
         }
     }
+    SC_TICK(1);
     // mem_chain_flt
     int nch = 0;
     for (int j = 0; j < ncv; ++j) {
@@ -566,7 +585,18 @@ SC_HD int map_read(const IndexView &I, const pr_seed_opts &O, Scratch &S, const 
         t.nseed = c.n;
     }
     *n_out = no;
+    SC_TICK(2);
     return 0;
+}
+#undef SC_TICK
+
+// The whole read: occurrence table, then map_after_occ.
+SC_HD int map_read(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
+                   pr_seed_task *out, int cap_out, int *n_out) {
+    *n_out = 0;
+    const int err = build_occ(I, S, q, len);
+    if (err) return err;
+    return map_after_occ(I, O, S, q, len, sid, out, cap_out, n_out);
 }
 
 }  // namespace seedc

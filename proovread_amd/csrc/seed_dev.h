@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <vector>
+
 #include "seed_core.h"
 
 namespace prgpu {
@@ -14,7 +16,10 @@ struct SeedDev {
     int64_t n_sr;
     uint8_t *scratch;          // n_lanes * stride bytes
     int64_t stride;            // seedc::scratch_bytes(caps), 8-byte multiple
-    int64_t n_lanes;
+    int64_t n_lanes;           // scratch slots = resident waves (one read per wave at a time)
+    int32_t *next;             // read counter the waves dequeue from (zeroed before the launch)
+    unsigned long long *prof;  // [8] wall-clock ticks summed over waves: occurrence table, SMEMs,
+                               // chaining, filter + output (may be null)
     seedc::Caps caps;
     pr_seed_task *out;         // [n_sr * caps.out]
     int32_t *n_out;            // [n_sr]
@@ -22,6 +27,11 @@ struct SeedDev {
 };
 
 int seed_launch(const SeedDev &D, void *stream);
+// resident waves per CU of the seeding kernel (= scratch slots per CU)
+int seed_slots_per_cu();
+// dense task list: out[pre[i] + j] = slots[i * cap + j] for j < n_out[i]
+int seed_compact_launch(const pr_seed_task *slots, const int32_t *n_out, const int64_t *pre, int64_t n_sr, int cap,
+                        pr_seed_task *out, void *stream);
 
 // host-side view of a built index (seed.cpp)
 seedc::IndexView seed_index_view(const pr_seed_index *h);
@@ -30,5 +40,10 @@ struct SeedIndexSizes {
     int64_t text, cstart, cblk, lr_off, koff, kpos, cnt[seedc::KI - 1];
 };
 SeedIndexSizes seed_index_sizes(const pr_seed_index *h);
+// pr_seed_index_digest's six values over tables copied to the host (device index test hook)
+void seed_digest_tables(const std::vector<uint8_t> &text, const std::vector<uint32_t> &koff,
+                        const std::vector<uint32_t> &kpos, const std::vector<uint64_t> &kext,
+                        const std::vector<std::vector<uint32_t>> &cnt, const std::vector<int64_t> &cstart,
+                        const std::vector<int32_t> &cblk, const std::vector<int64_t> &lr_off, uint64_t *out6);
 
 }  // namespace prgpu

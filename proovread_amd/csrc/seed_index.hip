@@ -1,0 +1,177 @@
+// The seed index built on the device (`bwa-proovread index`): the
+// same tables as seed.cpp's pr_seed_index_build, byte for byte, from the long reads
+// straight into the context's HBM (no host build, no index upload).
+//
+//   text   forward long reads, then the reverse complement of their concatenation,
+//          each contig followed by SEP (5); one thread per forward base writes both
+//          strands (read found by binary search over the read offsets)
+//   keys   one thread per text position: the 12-mer code starting there (or NK when
+//          the 12 bases are not all A/C/G/T) -> (key, position) pairs, and the k-mer
+//          histogram (device atomics)
+//   kpos   stable LSD radix sort of the pairs by key (rocPRIM, 25 key bits): every
+//          k-mer's positions in ascending text order, as the host build leaves them
+//   koff   exclusive scan of the histogram
+//   kext   one thread per hit: the <= 28 bases after the 12-mer (2 bits each, stopping
+//          at N / SEP) and their count << 56
+//   cnt    j-mer counts, j = 11 .. 1: C_j(x) = sum_c C_{j+1}(4x + c) + #(runs of bases
+//          ending in x), the run ends counted by one thread per N / SEP position
+// HBM-bound integer work: ~n_text x (1 + 8 + 8 + 16) B for text, pairs and the sort's
+// passes, ~12 B per hit for kpos / kext.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "seed_core.h"
+#include "seed_index_dev.h"
+
+namespace prgpu {
+
+namespace {
+constexpr uint8_t SEP = 5;
+constexpr uint32_t NK = seedc::NK;
+constexpr int KI = seedc::KI;
+constexpr int KX = seedc::KX;
+
+__global__ void ix_text_kernel(const uint8_t *lr_seq, const int64_t *lr_off, int n_lr, const int64_t *cstart,
+                               int64_t l_pac, uint8_t *text) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < l_pac) {
+        int lo = 0, hi = n_lr - 1;   // read i: lr_off[i] <= g < lr_off[i + 1]
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (lr_off[mid] <= g) lo = mid; else hi = mid - 1;
+        }
+        const int i = lo;
+        const int64_t p = g - lr_off[i], len = lr_off[i + 1] - lr_off[i];
+        const uint8_t c = lr_seq[g];
+        text[cstart[i] + p] = c < 4 ? c : 4;
+        text[cstart[2 * (int64_t)n_lr - 1 - i] + (len - 1 - p)] = c < 4 ? (uint8_t)(3 - c) : 4;
+    }
+    if (g < n_lr) {   // separators
+        const int64_t len = lr_off[g + 1] - lr_off[g];
+        text[cstart[g] + len] = SEP;
+        text[cstart[2 * (int64_t)n_lr - 1 - g] + len] = SEP;
+    }
+}
+
+__global__ void ix_keys_kernel(const uint8_t *text, int64_t n, uint32_t *key, uint32_t *val, uint32_t *kc) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    uint32_t code = 0;
+    bool ok = p + KI <= n;
+    if (ok) {
+        for (int x = 0; x < KI; ++x) {
+            const uint8_t c = text[p + x];
+            ok &= c < 4;
+            code = (code << 2) | (c & 3u);
+        }
+    }
+    key[p] = ok ? code : NK;
+    val[p] = (uint32_t)p;
+    if (ok) atomicAdd(&kc[code], 1u);
+}
+
+__global__ void ix_kext_kernel(const uint8_t *text, int64_t n, const uint32_t *kpos, const uint32_t *koff,
+                               uint64_t *kext) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= (int64_t)koff[NK]) return;   // the hits: the sorted pairs with a valid key
+    const int64_t p = (int64_t)kpos[r] + KI;
+    uint64_t v = 0;
+    int m = 0;
+    for (; m < KX && p + m < n; ++m) {
+        const uint8_t c = text[p + m];
+        if (c > 3) break;
+        v |= (uint64_t)c << (2 * m);
+    }
+    kext[r] = v | ((uint64_t)m << 56);
+}
+
+// run ends: one thread per text position holding N / SEP; the j-mers (j < 12) that end
+// just before it inside the run of bases are counted into cnt[j - 1]
+__global__ void ix_tail_kernel(const uint8_t *text, int64_t n, uint32_t *const *cnt) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n || text[p] <= 3) return;
+    uint32_t code = 0;
+    for (int j = 1; j < KI; ++j) {
+        if (p - j < 0) break;
+        const uint8_t c = text[p - j];
+        if (c > 3) break;
+        code |= (uint32_t)c << (2 * (j - 1));   // T[p-j] is the first base of the j-mer
+        atomicAdd(&cnt[j - 1][code], 1u);
+    }
+}
+
+// C_j(x) += sum_c C_{j+1}(4x + c)
+__global__ void ix_jmer_kernel(uint32_t *cj, const uint32_t *cn, int64_t nj) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= nj) return;
+    const uint4 v = reinterpret_cast<const uint4 *>(cn)[x];
+    cj[x] += v.x + v.y + v.z + v.w;
+}
+
+inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+}  // namespace
+
+#define IXCHK(x)                                   \
+    do {                                           \
+        const hipError_t e_ = (x);                 \
+        if (e_ != hipSuccess) return (int)e_;      \
+    } while (0)
+
+int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
+    const int64_t n = B.n_text;
+    // text
+    if (B.l_pac > 0 || B.n_lr > 0) {
+        const int64_t nt = B.l_pac > B.n_lr ? B.l_pac : B.n_lr;
+        hipLaunchKernelGGL(ix_text_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, s, B.lr_seq, B.lr_off, B.n_lr,
+                           B.cstart, B.l_pac, B.text);
+        IXCHK(hipGetLastError());
+    }
+    // 12-mer keys + histogram
+    IXCHK(hipMemsetAsync(B.kc, 0, ((size_t)NK + 1) * 4, s));
+    if (n > 0) {
+        hipLaunchKernelGGL(ix_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.key0, B.val0, B.kc);
+        IXCHK(hipGetLastError());
+    }
+    // koff = exclusive scan of the histogram (NK + 1 entries: the last is the total)
+    {
+        size_t tb = B.temp_bytes;
+        IXCHK(rocprim::exclusive_scan(B.temp, tb, B.kc, B.koff, 0u, (size_t)NK + 1, rocprim::plus<uint32_t>(), s));
+    }
+    if (n > 0) {
+        // stable sort of (key, position) by key: positions ascend within a k-mer
+        size_t tb = B.temp_bytes;
+        IXCHK(rocprim::radix_sort_pairs(B.temp, tb, B.key0, B.key1, B.val0, B.kpos, (size_t)n, 0u, 25u, s));
+        // kext for the hits
+        hipLaunchKernelGGL(ix_kext_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kpos, B.koff, B.kext);
+        IXCHK(hipGetLastError());
+    }
+    // j-mer count tables: run ends first, then the children's sums from j = 11 down
+    for (int j = 1; j < KI; ++j) IXCHK(hipMemsetAsync(B.cnt[j - 1], 0, ((size_t)1 << (2 * j)) * 4, s));
+    if (n > 0) {
+        hipLaunchKernelGGL(ix_tail_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.cnt_dev);
+        IXCHK(hipGetLastError());
+    }
+    for (int j = KI - 1; j >= 1; --j) {
+        const uint32_t *cn = j == KI - 1 ? B.kc : B.cnt[j];
+        const int64_t nj = (int64_t)1 << (2 * j);
+        hipLaunchKernelGGL(ix_jmer_kernel, dim3(blocks_for(nj, 256)), dim3(256), 0, s, B.cnt[j - 1], cn, nj);
+        IXCHK(hipGetLastError());
+    }
+    return 0;
+}
+
+// bytes of rocPRIM temporary storage for n text positions
+size_t seed_index_temp_bytes(int64_t n) {
+    size_t a = 0, b = 0;
+    (void)rocprim::exclusive_scan(nullptr, a, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)NK + 1,
+                                  rocprim::plus<uint32_t>());
+    (void)rocprim::radix_sort_pairs(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                    (uint32_t *)nullptr, (size_t)(n > 0 ? n : 1), 0u, 25u);
+    return (a > b ? a : b) + 256;
+}
+
+}  // namespace prgpu

@@ -1,15 +1,19 @@
-// Seeding and chaining on the GPU: seed_core.h's map_read, one
-// lane per short read, each lane working in its own slice of a global scratch
-// buffer (seedc::carve, seedc::device_caps).  The index (text, 12-mer hit lists
-// with the 28 bases after every hit, count tables) is resident in HBM.  A read
-// whose work outgrows the lane's scratch is reported with its SC_OVER_* flags
-// and no tasks; the host decides what to do with it.
+// Seeding and chaining on the GPU: seed_core.h's map_read with one
+// 64-lane wave per short read.  The index (text, 12-mer hit lists with the 28 bases
+// after every hit, count tables) is resident in HBM.
 //
-// Per lane: the read's occurrence table (the 12-mer lists of its ~140 starts:
-// contiguous kpos/kext segments), the SMEM / re-seeding / -y passes over that
-// table, chaining into a sorted chain array with a seed pool, the chain filter
-// and the task output.  Latency-bound, irregular integer work: the lanes of a
-// wave follow different reads, so the kernel relies on many resident waves.
+// Per read (a wave, persistent: waves dequeue reads from a counter):
+//   1. occurrence table, wave-parallel: lanes over the read's starts compute the 12-mer
+//      code, the packed bases after it and the start's hit count; a wave scan gives the
+//      start offsets (kept in LDS for the lookup below); lanes over the read's ~3k hits
+//      (consecutive hits -> coalesced kpos / kext loads) compute each hit's exact match
+//      length (LCP with the packed bases, then the text past them) and count it into the
+//      start's match-length histogram; a per-start suffix sum makes the count table.
+//      This is build_occ's table without its diagonal shortcut (same match lengths).
+//   2. SMEMs, re-seeding, -y seeds, chaining, chain filter, task output: seed_core.h's
+//      map_after_occ on lane 0 (sequential decisions; the wave's scratch slice is small
+//      and L2-resident).  A read whose work outgrows the slice is reported with its
+//      SC_OVER_* flags and no tasks.
 #include <hip/hip_runtime.h>
 
 #include "seed_core.h"
@@ -17,26 +21,173 @@
 
 namespace prgpu {
 
-__global__ void __launch_bounds__(64) seed_map_kernel(SeedDev D) {
-    const int64_t lane = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t nl = (int64_t)gridDim.x * blockDim.x;
-    if (lane >= D.n_lanes) return;
-    seedc::Scratch S = seedc::carve(D.scratch + lane * D.stride, D.caps);
-    for (int64_t i = lane; i < D.n_sr; i += nl) {
+constexpr int SEED_WAVES = 4;          // waves (reads in flight) per workgroup
+constexpr int SEED_LMAX = 1024;        // LDS start offsets per wave: reads <= 1024 bases
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ void __launch_bounds__(64 * SEED_WAVES) seed_wave_kernel(SeedDev D) {
+    __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t slot = (int64_t)blockIdx.x * SEED_WAVES + wv;
+    if (slot >= D.n_lanes) return;
+    seedc::Scratch S = seedc::carve(D.scratch + slot * D.stride, D.caps);
+    int32_t *ho = hoff_lds[wv];
+    const seedc::IndexView &V = D.V;
+    unsigned long long pt[4] = {0ULL, 0ULL, 0ULL, 0ULL};   // lane 0: phase ticks of this wave
+    using seedc::HB;
+    using seedc::KI;
+    using seedc::KX;
+    for (;;) {
+        int i = 0;
+        if (lane == 0) i = atomicAdd(D.next, 1);
+        i = __shfl(i, 0, 64);
+        if (i >= D.n_sr) {   // every wave reaches this: the grid drains
+            if (D.prof && lane == 0)
+                for (int k = 0; k < 4; ++k) atomicAdd(&D.prof[k], pt[k]);
+            break;
+        }
         const int64_t o = D.sr_off[i];
         const int len = (int)(D.sr_off[i + 1] - o);
-        int n = 0, err = 0;
-        if (len > 0)
-            err = seedc::map_read(D.V, D.O, S, D.sr_seq + o, len, (int)i, D.out + i * D.caps.out, D.caps.out, &n);
-        D.n_out[i] = err ? 0 : n;
-        D.status[i] = err;
+        const uint8_t *q = D.sr_seq + o;
+        int err = 0;
+        const unsigned long long t0 = D.prof && lane == 0 ? wall_clock64() : 0ULL;
+        if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
+        if (len > 0 && !err) {
+            // ---- 1. occurrence table
+            for (int64_t k = lane; k < (int64_t)len * HB; k += 64) S.ge[k] = 0u;
+            int run = 0;
+            for (int a0 = 0; a0 <= len; a0 += 64) {
+                const int a = a0 + lane;
+                int ca = 0;
+                if (a <= len) {
+                    int32_t code_a = -1;
+                    uint64_t qe = 0;
+                    if (a + KI <= len) {
+                        uint32_t code = 0;
+                        bool ok = true;
+                        for (int x = 0; x < KI; ++x) {
+                            const uint8_t c = q[a + x];
+                            ok &= c < 4;
+                            code = (code << 2) | (c & 3u);
+                        }
+                        const int n = len - a - KI;
+                        qe = seedc::pack_ext(q + a + KI, n < KX ? n : KX);
+                        if (ok) {
+                            code_a = (int32_t)code;
+                            ca = (int)(V.koff[code + 1] - V.koff[code]);
+                        }
+                    }
+                    S.codes[a] = code_a;
+                    S.qext[a] = qe;
+                }
+                int x = ca;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const int y = __shfl_up(x, d, 64);
+                    if (lane >= d) x += y;
+                }
+                const int ex = run + x - ca;
+                if (a <= len) {
+                    ho[a] = ex;
+                    S.hoff[a] = ex;
+                }
+                run += __shfl(x, 63, 64);
+            }
+            const int nh = run;
+            if (nh > S.cap_hits) err = seedc::SC_OVER_HITS;
+            wave_sync_lds();
+            __threadfence_block();
+            if (!err) {
+                const int amax = len - KI;   // last start with a 12-mer
+                for (int k = lane; k < nh; k += 64) {
+                    int lo = 0, hi = amax;   // last start whose hits begin at or before k
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (ho[mid] <= k) lo = mid; else hi = mid - 1;
+                    }
+                    const int a = lo;
+                    const uint32_t code = (uint32_t)S.codes[a];
+                    const uint32_t r = V.koff[code] + (uint32_t)(k - ho[a]);
+                    const uint32_t p = V.kpos[r];
+                    const uint64_t exb = V.kext[r];
+                    const uint64_t qe = S.qext[a];
+                    const int le = (int)(exb >> 56), lq = (int)(qe >> 56);
+                    const uint64_t xd = (exb ^ qe) & seedc::KX_MASK;
+                    int m = xd ? seedc::ctz64(xd) >> 1 : KX;
+                    m = m < le ? m : le;
+                    m = m < lq ? m : lq;
+                    int ml = KI + m;
+                    if (m == KX)
+                        while (a + ml < len && q[a + ml] < 4 && V.text[p + ml] == q[a + ml]) ++ml;
+                    S.hpos[k] = p;
+                    S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
+                    atomicAdd(&S.ge[(int64_t)a * HB + (ml - KI < HB - 1 ? ml - KI : HB - 1)], 1u);
+                }
+                __threadfence_block();
+                for (int a = lane; a + KI <= len; a += 64) {
+                    if (S.codes[a] < 0) continue;
+                    uint32_t *g = S.ge + (int64_t)a * HB;
+                    uint32_t acc = 0;
+                    for (int t = HB - 1; t >= 0; --t) {
+                        acc += g[t];
+                        g[t] = acc;
+                    }
+                }
+                __threadfence_block();
+            }
+        }
+        // ---- 2. the sequential rest of the read on lane 0
+        if (lane == 0) {
+            int n = 0;
+            if (D.prof) pt[0] += wall_clock64() - t0;
+            if (len > 0 && !err)
+                err = seedc::map_after_occ(V, D.O, S, q, len, i, D.out + (int64_t)i * D.caps.out, D.caps.out, &n,
+                                           D.prof ? pt + 1 : nullptr);
+            D.n_out[i] = err ? 0 : n;
+            D.status[i] = err;
+        }
+        __threadfence_block();
     }
+}
+
+int seed_slots_per_cu() {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, seed_wave_kernel, 64 * SEED_WAVES, 0) != hipSuccess || nb < 1)
+        nb = 2;
+    return nb * SEED_WAVES;
 }
 
 int seed_launch(const SeedDev &D, void *stream) {
     if (D.n_sr <= 0) return 0;
-    const int64_t blocks = (D.n_lanes + 63) / 64;
-    hipLaunchKernelGGL(seed_map_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, D);
+    const int64_t blocks = (D.n_lanes + SEED_WAVES - 1) / SEED_WAVES;
+    hipLaunchKernelGGL(seed_wave_kernel, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
+    return (int)hipGetLastError();
+}
+
+__global__ void seed_compact_kernel(const pr_seed_task *slots, const int32_t *n_out, const int64_t *pre, int64_t n_sr,
+                                    int cap, pr_seed_task *out) {
+    // one wave per read: lanes copy the read's tasks (10 dwords each) as dwords
+    const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (i >= n_sr) return;
+    const int n = n_out[i];
+    constexpr int TW = (int)(sizeof(pr_seed_task) / 4);
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(slots + i * cap);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(out + pre[i]);
+    for (int k = lane; k < n * TW; k += 64) dst[k] = src[k];
+}
+
+int seed_compact_launch(const pr_seed_task *slots, const int32_t *n_out, const int64_t *pre, int64_t n_sr, int cap,
+                        pr_seed_task *out, void *stream) {
+    if (n_sr <= 0) return 0;
+    const int64_t blocks = (n_sr + 3) / 4;
+    hipLaunchKernelGGL(seed_compact_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, slots, n_out, pre,
+                       n_sr, cap, out);
     return (int)hipGetLastError();
 }
 

@@ -55,6 +55,10 @@ def _setup(L):
     L.pr_seed_gpu_map.argtypes = [C.c_void_p, C.POINTER(SeedOpts), C.c_void_p, C.c_void_p, C.c_int,
                                   C.POINTER(SeedTasks), C.c_void_p]
     L.pr_seed_gpu_last_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+    L.pr_seed_gpu_index_build.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    L.pr_seed_gpu_index_digest.argtypes = [C.c_void_p, C.c_void_p]
+    L.pr_seed_gpu_index_last_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+    L.pr_seed_gpu_phase_ticks.argtypes = [C.c_void_p, C.c_void_p]
     _done = True
 
 
@@ -145,29 +149,82 @@ class SeedIndex:
                 allow_flagged: bool = False):
         """Seeding on the GPU -> (tasks, status per read).  Reads flagged with a scratch overflow
         have no tasks; unless allow_flagged, that raises."""
-        opts = opts or default_opts()
-        sr_seq = np.ascontiguousarray(sr_seq, np.uint8)
-        sr_off = np.ascontiguousarray(sr_off, np.int64)
-        st = np.zeros(max(1, len(sr_off) - 1), np.int32)
-        out = SeedTasks()
-        rc = self.L.pr_seed_gpu_map(self._ctx.h, C.byref(opts), sr_seq.ctypes.data, sr_off.ctypes.data,
-                                    len(sr_off) - 1, C.byref(out), st.ctypes.data)
-        if rc != 0 and not (allow_flagged and rc == -9):
-            self.L.pr_seed_tasks_free(C.byref(out))
-            _abi.check(rc, "pr_seed_gpu_map")
-        return self._take(out), st[:len(sr_off) - 1]
+        return _map_gpu(self.L, self._ctx, sr_seq, sr_off, opts, allow_flagged)
 
     def gpu_ms(self) -> float:
-        v = C.c_double()
-        _abi.check(self.L.pr_seed_gpu_last_ms(self._ctx.h, C.byref(v)), "pr_seed_gpu_last_ms")
-        return v.value
+        return _last_ms(self.L.pr_seed_gpu_last_ms, self._ctx)
+
+    def phase_ms(self) -> dict:
+        return _phase_ms(self.L, self._ctx)
 
     def _take(self, out: SeedTasks):
-        try:
-            n = int(out.n)
-            if n == 0:
-                return np.zeros(0, TASK_DTYPE)
-            buf = C.cast(out.t, C.POINTER(C.c_int32 * (10 * n))).contents
-            return np.frombuffer(bytes(buf), dtype=TASK_DTYPE).copy()
-        finally:
-            self.L.pr_seed_tasks_free(C.byref(out))
+        return _take(self.L, out)
+
+
+def _take(L, out: SeedTasks):
+    try:
+        n = int(out.n)
+        if n == 0:
+            return np.zeros(0, TASK_DTYPE)
+        buf = C.cast(out.t, C.POINTER(C.c_int32 * (10 * n))).contents
+        return np.frombuffer(bytes(buf), dtype=TASK_DTYPE).copy()
+    finally:
+        L.pr_seed_tasks_free(C.byref(out))
+
+
+def _last_ms(fn, ctx) -> float:
+    v = C.c_double()
+    _abi.check(fn(ctx.h, C.byref(v)), fn.__name__)
+    return v.value
+
+
+def _phase_ms(L, ctx) -> dict:
+    """Wave time per part of the last GPU seeding launch (ms summed over waves)."""
+    t = np.zeros(4, np.uint64)
+    _abi.check(L.pr_seed_gpu_phase_ticks(ctx.h, t.ctypes.data), "pr_seed_gpu_phase_ticks")
+    return {k: round(float(v) / 1e5, 1) for k, v in zip(("occ_table", "smems", "chaining", "filter_out"), t)}
+
+
+def _map_gpu(L, ctx, sr_seq, sr_off, opts, allow_flagged):
+    opts = opts or default_opts()
+    sr_seq = np.ascontiguousarray(sr_seq, np.uint8)
+    sr_off = np.ascontiguousarray(sr_off, np.int64)
+    st = np.zeros(max(1, len(sr_off) - 1), np.int32)
+    out = SeedTasks()
+    rc = L.pr_seed_gpu_map(ctx.h, C.byref(opts), sr_seq.ctypes.data, sr_off.ctypes.data, len(sr_off) - 1,
+                           C.byref(out), st.ctypes.data)
+    if rc != 0 and not (allow_flagged and rc == -9):
+        L.pr_seed_tasks_free(C.byref(out))
+        _abi.check(rc, "pr_seed_gpu_map")
+    return _take(L, out), st[:len(sr_off) - 1]
+
+
+class DeviceSeedIndex:
+    """The index of a long-read shard built in the context's HBM (pr_seed_gpu_index_build:
+    the host build's tables, byte for byte) and seeding against it (pr_seed_gpu_map)."""
+
+    def __init__(self, ctx: "_abi.Context", lr_seq: np.ndarray, lr_off: np.ndarray):
+        self.L = _abi.lib()
+        _setup(self.L)
+        self._ctx = ctx
+        seq = np.ascontiguousarray(lr_seq, np.uint8)
+        off = np.ascontiguousarray(lr_off, np.int64)
+        _abi.check(self.L.pr_seed_gpu_index_build(ctx.h, seq.ctypes.data, off.ctypes.data, len(off) - 1),
+                   "pr_seed_gpu_index_build")
+
+    def digest(self) -> tuple:
+        out = np.zeros(6, np.uint64)
+        _abi.check(self.L.pr_seed_gpu_index_digest(self._ctx.h, out.ctypes.data), "pr_seed_gpu_index_digest")
+        return tuple(int(x) for x in out)
+
+    def build_ms(self) -> float:
+        return _last_ms(self.L.pr_seed_gpu_index_last_ms, self._ctx)
+
+    def map(self, sr_seq: np.ndarray, sr_off: np.ndarray, opts: SeedOpts | None = None, allow_flagged: bool = False):
+        return _map_gpu(self.L, self._ctx, sr_seq, sr_off, opts, allow_flagged)
+
+    def gpu_ms(self) -> float:
+        return _last_ms(self.L.pr_seed_gpu_last_ms, self._ctx)
+
+    def phase_ms(self) -> dict:
+        return _phase_ms(self.L, self._ctx)

@@ -1,14 +1,23 @@
-"""GPU seeding path (seed_kernels.hip: seed_core.h, one lane per read, fixed scratch).
+"""GPU seeding path (seed_kernels.hip: one wave per read, wave-parallel occurrence table,
+seed_core.h's SMEM / chaining / filter on lane 0, fixed scratch per wave).
 
 CPU: the same core with the device's fixed capacities, run on the host
 (pr_seed_map_device_caps), gives exactly the host path's tasks for every read it
 does not flag, and flags only reads whose work outgrows a capacity.
-GPU: pr_seed_gpu_map returns exactly the host run of the device path: tasks and
-per-read flags (run last: not yet exercised on hardware)."""
+GPU: pr_seed_gpu_map against the pure-Python oracle (oracle/seed_oracle.py: string
+search occurrence counts, bwt_smem1a, mem_chain, mem_chain_flt) directly, for both
+option sets, -c sampling and -D dropping; and against the host run of the device path
+on a larger simulated sample (tasks and per-read flags)."""
+import sys
+from pathlib import Path
+
 import numpy as np
 import pytest
 
 from proovread_amd import seed, synth
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "oracle"))
+import seed_oracle as so  # noqa: E402
 
 
 def _data(scale_seed=11, gl=300_000, n_lr=300):
@@ -67,3 +76,106 @@ def test_gpu_seeding_matches_device_caps_on_host():
         assert np.array_equal(st, wst)
         assert np.array_equal(got, want)
     assert ix.gpu_ms() > 0
+
+
+def _oracle_data():
+    """Six 1.5 kb long reads with indels, a repeat shared by three of them and N bases;
+    41 short reads (substitutions, reverse strands, one from the repeat)."""
+    rng = np.random.default_rng(7)
+    G = rng.integers(0, 4, 5000)
+    rep = G[1000:1200].copy()
+
+    def mutate(g):
+        out = []
+        for c in g:
+            u = rng.random()
+            if u < 0.045:
+                continue
+            if u < 0.06:
+                c = (c + rng.integers(1, 4)) % 4
+            out.append(int(c))
+            while rng.random() < 0.09:
+                out.append(int(rng.integers(0, 4)))
+        return out
+    lrs = []
+    for i in range(6):
+        s0 = int(rng.integers(0, 3500))
+        lr = mutate(G[s0:s0 + 1500])
+        if i % 2:
+            lr[100:100] = list(rep)
+        if i == 3:
+            for j in rng.integers(0, len(lr), 5):
+                lr[j] = 4
+        lrs.append(lr)
+    srs = []
+    for i in range(40):
+        s0 = int(rng.integers(0, 4850))
+        r = [int(x) for x in G[s0:s0 + 150]]
+        if rng.random() < 0.3:
+            r[int(rng.integers(0, 150))] = (r[0] + 1) % 4
+        if rng.random() < 0.5:
+            r = [3 - x for x in reversed(r)]
+        srs.append(r)
+    srs.append([int(x) for x in rep[:150]])
+    lr_off = np.concatenate([[0], np.cumsum([len(x) for x in lrs])]).astype(np.int64)
+    sr_off = np.concatenate([[0], np.cumsum([len(x) for x in srs])]).astype(np.int64)
+    return (lrs, srs, np.concatenate([np.array(x, np.uint8) for x in lrs]), lr_off,
+            np.concatenate([np.array(x, np.uint8) for x in srs]), sr_off)
+
+
+@pytest.mark.gpu
+def test_gpu_seeding_matches_python_oracle():
+    from proovread_amd import _abi
+    lrs, srs, lr_seq, lr_off, sr_seq, sr_off = _oracle_data()
+    oidx = so.Index(lrs)
+    ix = seed.SeedIndex(lr_seq, lr_off)
+    ix.to_gpu(_abi.default_context())
+    o_samp = seed.default_opts(False)
+    o_samp.max_occ, o_samp.drop_ratio, o_samp.min_chain_weight = 2, 0.5, 12
+    cases = [(seed.default_opts(False), so.Opts()), (seed.default_opts(True), so.Opts.finish()),
+             (o_samp, so.Opts(max_occ=2, drop_ratio=0.5, min_chain_weight=12))]
+    for o, oo in cases:
+        got, st = ix.map_gpu(sr_seq, sr_off, o)
+        assert (st == 0).all()
+        got = [tuple(int(t[k]) for k in seed.TASK_DTYPE.names) for t in got]
+        want = []
+        for i, r in enumerate(srs):
+            want += [tuple(t[k] for k in seed.TASK_DTYPE.names) for t in so.map_read(oidx, oo, r, i)]
+        assert got == want
+        assert len(got) > 20
+
+
+def _index_cases():
+    d, ss, so_ = _data(13, gl=200_000, n_lr=200)
+    yield "sim", d.lr_seq, d.lr_off, ss, so_
+    lrs, srs, lr_seq, lr_off, sr_seq, sr_off = _oracle_data()
+    yield "repeat+N", lr_seq, lr_off, sr_seq, sr_off
+    # an empty long read, IUPAC-like codes > 4, a long read shorter than a 12-mer
+    rng = np.random.default_rng(5)
+    parts = [rng.integers(0, 4, 3000), np.zeros(0, np.int64), rng.integers(0, 6, 800), rng.integers(0, 4, 7),
+             rng.integers(0, 4, 2500)]
+    seq = np.concatenate(parts).astype(np.uint8)
+    off = np.concatenate([[0], np.cumsum([len(x) for x in parts])]).astype(np.int64)
+    reads = [seq[100:250], seq[3100:3250], seq[3900:4050][::-1].copy()]
+    sro = np.concatenate([[0], np.cumsum([len(x) for x in reads])]).astype(np.int64)
+    yield "edge", seq, off, np.concatenate(reads).astype(np.uint8), sro
+
+
+@pytest.mark.gpu
+def test_device_index_build_equals_host_index():
+    """pr_seed_gpu_index_build: the host build's tables byte for byte (digests of text, koff,
+    kpos, kext, j-mer counts, contig tables), and seeding against it = the host path."""
+    from proovread_amd import _abi
+    ctx = _abi.default_context()
+    for name, lr_seq, lr_off, sr_seq, sr_off in _index_cases():
+        hx = seed.SeedIndex(lr_seq, lr_off)
+        dx = seed.DeviceSeedIndex(ctx, lr_seq, lr_off)
+        assert dx.digest() == hx.digest(), name
+        assert dx.build_ms() > 0
+        for finish in (False, True):
+            o = seed.default_opts(finish)
+            want = hx.map(sr_seq, sr_off, o, threads=4)
+            got, st = dx.map(sr_seq, sr_off, o)
+            assert (st == 0).all(), name
+            assert np.array_equal(got, want), name
+        hx.close()
