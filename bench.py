@@ -54,8 +54,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-lrs-per-worker", type=int, default=256)
     ap.add_argument("--seeds", choices=("truth", "host", "gpu"), default="gpu",
-                    help="task list: the product's seeding front end (host path / GPU path; bwa mem seeding "
-                         "+ chaining restated), or the simulation truth; computed before the timed region")
+                    help="seeds: the product's seeding front end (host path / GPU path; bwa mem seeding "
+                         "+ chaining restated; every seed of the kept chains in bwa mode), or the simulation "
+                         "truth (one single-seed task per pair); computed before the timed region")
     return ap.parse_args()
 
 
@@ -68,17 +69,26 @@ def cpu_baseline(d, per_worker: int):
     n_s = min(d.n_lr, per_worker * workers)
     with tempfile.TemporaryDirectory(prefix="prgpu_bench_") as td:
         npz, out = os.path.join(td, "w.npz"), os.path.join(td, "o.json")
-        k = int(np.searchsorted(d.t_lr, n_s, side="left"))   # tasks are grouped by long read
-        np.savez(npz, lr_seq=d.lr_seq[:int(d.lr_off[n_s])], lr_off=d.lr_off[:n_s + 1], sr_seq=d.sr_seq,
-                 sr_off=d.sr_off, t_sr=d.t_sr[:k], t_lr=d.t_lr[:k], t_strand=d.t_strand[:k], t_qbeg=d.t_qbeg[:k],
-                 t_rbeg=d.t_rbeg[:k], t_slen=d.t_slen[:k])
+        if d.t_chain is not None:   # bwa mode: every seed of each short read with a seed on the sample
+            want = np.zeros(d.n_sr, bool)
+            want[d.t_sr[d.t_lr < n_s]] = True
+            sel = want[d.t_sr]
+            np.savez(npz, lr_seq=d.lr_seq, lr_off=d.lr_off, sr_seq=d.sr_seq, sr_off=d.sr_off,
+                     **{k: getattr(d, k)[sel] for k in ("t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen",
+                                                        "t_chain")})
+        else:
+            k = int(np.searchsorted(d.t_lr, n_s, side="left"))   # tasks are grouped by long read
+            np.savez(npz, lr_seq=d.lr_seq[:int(d.lr_off[n_s])], lr_off=d.lr_off[:n_s + 1], sr_seq=d.sr_seq,
+                     sr_off=d.sr_off, t_sr=d.t_sr[:k], t_lr=d.t_lr[:k], t_strand=d.t_strand[:k],
+                     t_qbeg=d.t_qbeg[:k], t_rbeg=d.t_rbeg[:k], t_slen=d.t_slen[:k])
         subprocess.run([sys.executable, str(ROOT / "oracle" / "cpu_bench.py"), npz, str(n_s), str(workers), out, "0",
                         str(BIN_FILTER[0]), str(BIN_FILTER[1])], check=True)
         r = json.loads(Path(out).read_text())
     cpu = {"value": round(r["bases"] / r["wall_s"] / 1e6, 4), "unit": "Mbases/s", "cores": r["workers"], "kind": "port",
-           "sample": f"first {r['n']} of {d.n_lr} long reads of the same workload ({r['bases']} bases, their "
-                     f"{r['tasks']} seed-extension tasks), SW + consensus C restatement (oracle/), "
-                     f"{r['workers']} processes, {r['wall_s']:.1f} s"}
+           "sample": f"first {r['n']} of {d.n_lr} long reads of the same workload ({r['bases']} bases; "
+                     + (f"bwa mem per-read alignment of every short read seeded on them, {r['tasks']} seeds"
+                        if d.t_chain is not None else f"their {r['tasks']} seed-extension tasks")
+                     + f"), SW + consensus C restatement (oracle/), {r['workers']} processes, {r['wall_s']:.1f} s"}
     return cpu, r["results"]
 
 
@@ -95,8 +105,8 @@ def check_parity(it, cpu_res):
         if not ok:
             bad.append(i)
     return {"checked_reads": len(cpu_res), "mismatches": len(bad), "first_mismatch": bad[:5],
-            "against": "oracle chain (SW restatement -> coordinate order -> consensus restatement pinned to the "
-                       "reference Perl engine), same tasks"}
+            "against": "oracle chain (bwa mem per-read alignment + SW restatement -> coordinate order -> consensus "
+                       "restatement pinned to the reference Perl engine), same seeds"}
 
 
 def main():
@@ -160,7 +170,9 @@ def main():
                 "reads_per_s": round(d.n_sr / t_map, 1), "index_kernel_ms": ix_ms, "kernel_ms": ms,
                 "tasks": int(len(tasks)), "parity_vs_host": check,
                 "kernel_phase_ms_summed_over_waves": seed_phases}
-        return synth.with_seeded_tasks(d, tasks), info
+        if args.seeds != "truth":
+            info["chains"] = int((tasks["rank"] == 0).sum())
+        return synth.with_seeds(d, tasks), info
 
     if args.seeds == "host":
         d, seed_info = seed_front_end()
@@ -182,7 +194,7 @@ def main():
         if want_cpu:   # the same GPU-seeded tasks, CPU chain in a child process
             cpu, cpu_res = cpu_baseline(d, args.cpu_lrs_per_worker)
     t_up = time.perf_counter()
-    it = iteration.Iteration(d, ctx=ctx)   # host -> HBM upload of reads and tasks (outside the step)
+    it = iteration.Iteration(d, ctx=ctx)   # host -> HBM upload of reads and seeds (outside the step)
     upload_s = time.perf_counter() - t_up
     opts = sw.default_opts(finish=False)
     opts.bin_size, opts.bin_length = BIN_FILTER     # bwa-proovread -b 20 -l 300 (proovread:1302-1313)
@@ -224,6 +236,7 @@ def main():
         total_bases = lr_bases
     ms /= max(args.steps, 1)
     me, mg, ce, cg = sw.last_timing(ctx)
+    bwa_rounds, bwa_ext, bwa_patch = sw.bwa_stats(ctx) if d.t_chain is not None else (0, 0, 0)
     pc = sw.phase_cycles(ctx)
     a = it.download()
     cns_phases = it.cns_phase_ms()
@@ -266,10 +279,13 @@ def main():
             "workload": "configs[1] per GPU: 4.6 Mb genome, 13,800 x 10 kb long reads (30x, 15% error), "
                         "50x 2x150 short reads sampled to 15x for one bwa-sr iteration",
             "genome_bp": gl, "long_reads_per_gpu": d.n_lr, "long_read_bases_per_gpu": lr_bases,
-            "short_reads_per_gpu": d.n_sr, "sw_tasks_per_gpu": int(len(d.t_sr)), "task": "bwa-sr-1",
+            "short_reads_per_gpu": d.n_sr, "seeds_per_gpu": int(len(d.t_sr)), "task": "bwa-sr-1",
             "coverage_cap": params.coverage, "parallelism": f"long-read shards x{world}",
         },
         "sw_gcups": round(cells / ((ms[0] + ms[1]) * 1e-3) / 1e9, 2),
+        # bwa mode: mem_chain2aln rounds, seeds extended (first seeds of every chain + the ones the
+        # containment test sends), mem_patch_reg global scores; alignments reported
+        "bwa": {"rounds": bwa_rounds, "seeds_extended": bwa_ext, "patches": bwa_patch},
         "stage_ms": {"sw_extend": round(ms[0], 3), "sw_global_cigar": round(ms[1], 3),
                      "handoff_sort": round(ms[2], 3), "consensus": round(ms[3], 3)},
         "cigar_kernel_phase_share": {k: round(v / max(sum(pc), 1), 3) for k, v in

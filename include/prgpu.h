@@ -210,6 +210,13 @@ typedef struct pr_sw_opts {
      * between the SW stage and the consensus hand-off; 0 = off (pr_sw_opts_default).   */
     int32_t bin_size;
     double bin_length;
+    /* bwa mode only (pr_sw_batch.t_chain): -D of mem_reg2sam (a secondary scoring below
+     * drop_ratio x its primary is not reported), mem_mark_primary_se's mask_level (0.5),
+     * mem_sort_dedup_patch's mask_level_redun (0.95) and max_chain_gap (10000)           */
+    double drop_ratio;
+    double mask_level;
+    double mask_level_redun;
+    int32_t max_chain_gap;
 } pr_sw_opts;
 /* finish = 0: bwa-sr iterations (-A5 -B11 -O2,1 -E4,3 -w40 -T2.5 -L30,30);
  * finish = 1: bwa-sr-finish (-A5 -B13 -O15,19 -E3,3 -w30 -T4 -L30,30)            */
@@ -232,6 +239,15 @@ typedef struct pr_sw_batch {
     const int32_t *t_sr, *t_lr;
     const uint8_t *t_strand;
     const int32_t *t_qbeg, *t_rbeg, *t_slen;
+    /* bwa mode (NULL: single-seed tasks as above).  The tasks are every seed of the kept
+     * chains, as pr_seed_map returns them: grouped by short read (ascending), then chain
+     * (t_chain, mem_chain_flt order), in mem_chain2aln's order inside a chain.  The stage
+     * then runs bwa mem's per-read alignment (bwamem.c): mem_chain2aln's containment test
+     * over every seed (a seed inside an earlier region is not extended), mem_sort_dedup_patch,
+     * mem_mark_primary_se and mem_reg2sam's -T / -D filters, and its outputs are the reported
+     * alignments in SAM order (pr_sw_aln_count of them), not one per task.                */
+    const int32_t *t_chain;
+    int64_t read_id0;               /* bwa's input index of short read 0 (hash_64 ties)       */
 } pr_sw_batch;
 
 typedef struct pr_sw_out {          /* per task (any pointer may be NULL)              */
@@ -252,6 +268,11 @@ typedef struct pr_sw_out {          /* per task (any pointer may be NULL)       
     int64_t *cigar_off;
     uint32_t *cigar;
     int64_t cigar_cap;
+    /* bwa mode: per reported alignment (SAM order, read by read) the seed task that made it
+     * (its sr / lr / strand) and the SAM FLAG bits 0x10 / 0x100 (secondary) / 0x800; all the
+     * arrays above are then per alignment (pr_sw_aln_count entries)                       */
+    int32_t *task;
+    int32_t *flag;
 } pr_sw_out;
 
 int pr_sw_run(pr_ctx *ctx, const pr_sw_opts *o, const pr_sw_batch *b, pr_sw_out *out);
@@ -261,6 +282,11 @@ int pr_sw_download(pr_ctx *ctx, pr_sw_out *out);      /* syncs               */
 /* total CIGAR ops of the last launch (the pr_sw_out.cigar size) and the tasks whose CIGAR
  * outgrew its slot and was recomputed into the spill area (syncs) */
 int pr_sw_cigar_total(pr_ctx *ctx, int64_t *total, int64_t *n_overflow);
+/* bwa mode: reported alignments of the last launch (syncs) */
+int pr_sw_aln_count(pr_ctx *ctx, int64_t *n_aln);
+/* bwa mode diagnostics of the last launch: extension rounds, seeds extended, mem_patch_reg
+ * global scores computed */
+int pr_sw_bwa_stats(pr_ctx *ctx, int32_t *rounds, int64_t *n_extended, int64_t *n_patch);
 /* kernel milliseconds of the last launch (HIP events on the ctx stream) */
 int pr_sw_last_timing(pr_ctx *ctx, double *ms_extend, double *ms_global);
 /* canonical DP cells of the last launch (unpruned band, final width) */
@@ -298,7 +324,8 @@ typedef struct pr_seed_task {
     int32_t strand;          /* 1: the read aligns to the long read's reverse complement */
     int32_t qbeg, rbeg, slen;/* seed: read offset, long-read offset in strand coordinates, length */
     int32_t rmax0, rmax1;    /* the chain's reference window (strand coordinates) */
-    int32_t weight, nseed;   /* chain weight and seed count                   */
+    int32_t chain;           /* the chain among the read's kept chains (mem_chain_flt order) */
+    int32_t rank;            /* the seed's place in mem_chain2aln's extension order (0 first) */
 } pr_seed_task;
 typedef struct pr_seed_tasks {
     int64_t n;

@@ -1,8 +1,9 @@
 """ORACLE — BASELINE / CHECKER ONLY (bench.py's cpu_baseline leg, run as a child process).
 
-Loads the bench workload bench.py saved (reads + seed-extension tasks, .npz), runs the
-CPU chain (oracle/cpu_chain.py: SW restatement -> SAM order -> consensus restatement)
-on the first N long reads over W worker processes, and writes one JSON object: the
+Loads the bench workload bench.py saved (reads + seeds, .npz; bwa mode when t_chain is
+there: the seeds of every short read with a seed on the first N long reads), runs the
+CPU chain (oracle/cpu_chain.py: bwa mem per-read alignment restatement -> SAM order ->
+consensus restatement) on the first N long reads over W worker processes, and writes one JSON object: the
 timing and, per read, (rc, fastq, trace, chim lines) for bench.py's byte-for-byte
 comparison with the GPU output.  A separate process, so the fork pool never shares a
 process with a HIP runtime.
@@ -29,6 +30,9 @@ def main(argv) -> int:
     z = np.load(path)   # allow_pickle=False: arrays only
     d = SimpleNamespace(**{k: z[k] for k in z.files})
     d.n_lr = len(d.lr_off) - 1
+    d.n_sr = len(d.sr_off) - 1
+    if "t_chain" not in z.files:
+        d.t_chain = None
     import cpu_chain
     n = min(n, d.n_lr)
     wall, bases, res, nw = cpu_chain.run_sample(d, range(n), task="bwa-sr-finish" if finish else "bwa-sr",
@@ -36,7 +40,7 @@ def main(argv) -> int:
                                                 detect_chimera=finish, workers=workers, full=True, bin_filter=binf)
     with open(out, "w") as f:
         json.dump({"wall_s": wall, "bases": bases, "workers": nw, "n": n,
-                   "tasks": int(np.searchsorted(d.t_lr, n, side="left")),
+                   "tasks": int(len(d.t_sr)) if d.t_chain is not None else int(np.searchsorted(d.t_lr, n, side="left")),
                    "results": [list(r) for r in res]}, f)
     return 0
 

@@ -1,12 +1,14 @@
 """ORACLE — TEST / BASELINE INFRASTRUCTURE ONLY.
 
 CPU restatement of one proovread correction iteration, used as the checker of
-the GPU pipeline and as bench.py's cpu_baseline leg (kind "port"): for every
-seed-extension task the SW oracle (oracle/sw_oracle.c, restatement of
-bwa-proovread's ksw stage), SAM records with AS:i, the per-long-read
-coordinate order samtools would produce, and the consensus oracle
-(oracle/cns_oracle.c, restatement of bam2cns / Sam::Seq, pinned to the
-reference's Perl engine).
+the GPU pipeline and as bench.py's cpu_baseline leg (kind "port"): bwa mem's
+per-read alignment over the seeds of every short read (oracle/aln_oracle.c:
+mem_chain2aln over every seed with the SW oracle oracle/sw_oracle.c,
+mem_sort_dedup_patch, mem_mark_primary_se, mem_reg2sam's filters and order; or,
+for a single-seed task list, the SW oracle per task), SAM records with AS:i in
+bwa's output order, bwa-proovread's -b/-l filter, the per-long-read coordinate
+order samtools would produce, and the consensus oracle (oracle/cns_oracle.c,
+restatement of bam2cns / Sam::Seq, pinned to the reference's Perl engine).
 """
 from __future__ import annotations
 
@@ -31,6 +33,10 @@ _REF = None      # optional ASCII consensus reference pool (lr_off layout), else
 _QUAL = None     # optional reference qualities (phred+33), else '$'
 _FULL = False    # return (rc, fastq, trace, chim) instead of (rc, fastq)
 _BINF = None     # (BIN, LEN) of bwa-proovread -b/-l, or None
+_AOPTS = None    # bwa mode: oracle_bind.OalnOpts
+_SEEDS = None    # bwa mode: int32 [n_seed, 10] in OalnSeed layout, and per-read offsets
+_SEED_FIRST = None
+_RECS = None     # bwa mode: per long read, its records in bwa output order
 
 
 def _aln_length(cig, lq):
@@ -72,8 +78,75 @@ def _bin_filter(recs, bin_size, bin_len):
     return keep
 
 
-def _lr_chain(lr: int):
-    """SW oracle for all tasks of long read `lr`, then its consensus."""
+def _record(lr, strand, sid, pos, cigar, score, flag, lq):
+    d = _D
+    so = int(d.sr_off[sid])
+    q = d.sr_seq[so:so + lq]
+    seq = (_ASCII[np.where(q < 4, 3 - q, 4)][::-1] if strand else _ASCII[q]).tobytes().decode()
+    cg = "".join(f"{x >> 4}{'MIDNSHP=X'[x & 15]}" for x in cigar)
+    line = f"sr{sid}\t{flag}\tlr{lr}\t{pos + 1}\t60\t{cg}\t*\t0\t0\t{seq}\t*\tAS:i:{score}"
+    return (pos, strand, line, score, _aln_length(list(cigar), lq))
+
+
+def _sr_alignments(r: int):
+    """bwa mode: the reported alignments of short read r in SAM order (aln_oracle.c):
+    (lr, strand, pos, cigar ops, score, flag, qb, qe, rb, re, truesc, seed task)."""
+    d = _D
+    L = ob.aln_lib()
+    a, b = int(_SEED_FIRST[r]), int(_SEED_FIRST[r + 1])
+    if a == b:
+        return []
+    so = int(d.sr_off[r])
+    lq = int(d.sr_off[r + 1]) - so
+    qp = d.sr_seq.ctypes.data + so
+    outs = (ob.OalnReg * (b - a))()
+    no, ne = C.c_int(), C.c_int()
+    rc = L.oaln_read(C.byref(_OPTS), C.byref(_AOPTS), qp, lq, d.lr_seq.ctypes.data, d.lr_off.ctypes.data, d.n_lr,
+                     _SEEDS.ctypes.data + a * 40, b - a, r, outs, C.byref(no), C.byref(ne))
+    if rc:
+        raise RuntimeError(f"oaln_read failed on read {r}")
+    res = ob.OswResult()
+    out = []
+    for k in range(no.value):
+        g = outs[k]
+        lr = int(g.lr)
+        lo = int(d.lr_off[lr])
+        Llen = int(d.lr_off[lr + 1]) - lo
+        L.osw_reg2aln(C.byref(_OPTS), qp, lq, d.lr_seq.ctypes.data + lo, Llen, int(g.strand), C.byref(g.g),
+                      C.byref(res))
+        out.append((lr, int(g.strand), int(res.pos), list(res.cigar[:res.n_cigar]), int(res.score), int(g.flag),
+                    int(g.g.qb), int(g.g.qe), int(g.g.rb), int(g.g.re), int(g.g.truesc), a + int(g.seed)))
+    return out
+
+
+def _sr_records(r: int):
+    """bwa mode: (lr, record) pairs of short read r in SAM order."""
+    lq = int(_D.sr_off[r + 1] - _D.sr_off[r])
+    return [(a[0], _record(a[0], a[1], r, a[2], a[3], a[4], a[5], lq)) for a in _sr_alignments(r)]
+
+
+def bwa_alignments(d, task="bwa-sr", drop_ratio=None, reads=None):
+    """bwa mode (d.t_chain set): per short read its reported alignments in SAM order
+    (_sr_alignments tuples), single process."""
+    global _D, _OPTS, _AOPTS, _SEEDS, _SEED_FIRST
+    _D = d
+    _OPTS = ob.sw_opts(task) if isinstance(task, str) else ob.OswOpts(*task)
+    _AOPTS = ob.aln_opts(task if isinstance(task, str) else "bwa-sr")
+    if drop_ratio is not None:
+        _AOPTS.drop_ratio = float(drop_ratio)
+    ob.build() if not ob.LIB.exists() else None
+    ob.aln_lib()
+    n = len(d.t_sr)
+    _SEEDS = np.zeros((n, 10), np.int32)
+    for k, col in enumerate(("t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen")):
+        _SEEDS[:, k] = getattr(d, col)
+    _SEEDS[:, 8] = d.t_chain
+    _SEED_FIRST = np.searchsorted(d.t_sr, np.arange(d.n_sr + 1)).astype(np.int64)
+    return [_sr_alignments(r) for r in (range(d.n_sr) if reads is None else reads)]
+
+
+def _lr_task_records(lr: int):
+    """Single-seed tasks: the SW oracle for all tasks of long read `lr`, in task order."""
     d = _D
     L = ob.sw_lib()
     t0, t1 = int(d._task_off[lr]), int(d._task_off[lr + 1])
@@ -91,12 +164,17 @@ def _lr_chain(lr: int):
         if rc or not getattr(r, "pass"):
             continue
         strand = int(d.t_strand[t])
-        q = d.sr_seq[so:so + lq]
-        seq = (_ASCII[np.where(q < 4, 3 - q, 4)][::-1] if strand else _ASCII[q]).tobytes().decode()
-        cg = "".join(f"{x >> 4}{'MIDNSHP=X'[x & 15]}" for x in r.cigar[:r.n_cigar])
-        recs.append((r.pos, strand, t, f"sr{sid}\t{16 if strand else 0}\tlr{lr}\t{r.pos + 1}\t60\t{cg}\t*\t0\t0\t"
-                                       f"{seq}\t*\tAS:i:{r.score}", r.score, _aln_length(list(r.cigar[:r.n_cigar]), lq)))
-    if _BINF is not None:   # records in task order = bwa's output order for this long read
+        recs.append(_record(lr, strand, sid, r.pos, r.cigar[:r.n_cigar], r.score, 16 if strand else 0, lq))
+    return recs
+
+
+def _lr_chain(lr: int):
+    """The records of long read `lr` (bwa output order) -> -b/-l filter -> coordinate order ->
+    consensus."""
+    d = _D
+    recs = _RECS[lr] if _RECS is not None else _lr_task_records(lr)
+    recs = [(x[0], x[1], i, x[2], x[3], x[4]) for i, x in enumerate(recs)]
+    if _BINF is not None:   # records in bwa's output order for this long read
         keep = _bin_filter([(x[0], float(x[4]), x[5]) for x in recs], *_BINF)
         recs = [x for x, k in zip(recs, keep) if k]
     recs.sort(key=lambda x: (x[0], x[1], x[2]))
@@ -118,30 +196,36 @@ def _lr_chain(lr: int):
 
 
 def _init_worker():
-    ob.sw_lib()
+    ob.aln_lib()
 
 
 def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers=None, ref_seq=None,
-               ref_qual=None, detect_chimera=False, full=False, bin_filter=None):
+               ref_qual=None, detect_chimera=False, full=False, bin_filter=None, drop_ratio=None):
     """Run the CPU chain on long reads `lrs`; returns (wall seconds, bases, results, workers).
 
+    d.t_chain set (bwa mode): d's tasks are every seed of the kept chains grouped by short
+    read; every short read with a seed on `lrs` goes through bwa mem's per-read alignment
+    (all of its seeds, so the result is exact for those long reads).  Otherwise d's tasks are
+    single-seed alignments grouped by long read.
     ref_seq / ref_qual: ASCII consensus reference and its qualities in the long reads' layout
     (bam2cns --ref, the previous iteration's .fq) when it differs from the mapped reads;
     full: per read (rc, fastq, trace, chim lines) instead of (rc, fastq); bin_filter: (BIN, LEN)
-    of bwa-proovread -b/-l applied to each long read's records, or None."""
-    global _D, _OPTS, _PARAMS, _REF, _QUAL, _FULL, _BINF
+    of bwa-proovread -b/-l applied to each long read's records, or None; drop_ratio: bwa -D
+    (default: 0.75 for bwa-sr-finish, else 0)."""
+    global _D, _OPTS, _PARAMS, _REF, _QUAL, _FULL, _BINF, _AOPTS, _SEEDS, _SEED_FIRST, _RECS
     _D = d
     _BINF = tuple(bin_filter) if bin_filter else None
     _REF = None if ref_seq is None else np.ascontiguousarray(ref_seq, np.uint8)
     _QUAL = None if ref_qual is None else np.ascontiguousarray(ref_qual, np.uint8)
     _FULL = bool(full)
-    if not hasattr(d, "_task_off"):
-        d._task_off = np.zeros(d.n_lr + 1, np.int64)
-        np.cumsum(np.bincount(d.t_lr, minlength=d.n_lr), out=d._task_off[1:])
     if isinstance(task, str):
         _OPTS = ob.sw_opts(task)
+        _AOPTS = ob.aln_opts(task)
     else:   # (a, b, o_del, o_ins, e_del, e_ins, w, pen_clip5, pen_clip3, zdrop, min_score_per_base)
         _OPTS = ob.OswOpts(*task)
+        _AOPTS = ob.aln_opts("bwa-sr")
+    if drop_ratio is not None:
+        _AOPTS.drop_ratio = float(drop_ratio)
     _PARAMS = ob.OcnsParams()
     _PARAMS.max_coverage = coverage
     _PARAMS.bin_size = 20.0
@@ -158,13 +242,41 @@ def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers
     _PARAMS.detect_chimera = int(detect_chimera)
     _PARAMS.invert_scores = 0
     ob.build() if not ob.LIB.exists() else None
-    ob.sw_lib()
+    ob.aln_lib()
     workers = workers or min(16, os.cpu_count() or 1)
+    lrs = list(lrs)
     bases = int(sum(int(d.lr_off[i + 1] - d.lr_off[i]) for i in lrs))
+    bwa = getattr(d, "t_chain", None) is not None
+    _RECS = None
+    if bwa:
+        n = len(d.t_sr)
+        _SEEDS = np.zeros((n, 10), np.int32)
+        for k, col in enumerate(("t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen")):
+            _SEEDS[:, k] = getattr(d, col)
+        _SEEDS[:, 8] = d.t_chain
+        _SEEDS = np.ascontiguousarray(_SEEDS)
+        _SEED_FIRST = np.searchsorted(d.t_sr, np.arange(d.n_sr + 1)).astype(np.int64)
+        want = np.zeros(d.n_lr, bool)
+        want[lrs] = True
+        reads = np.unique(d.t_sr[want[d.t_lr]]).tolist()
+    elif not hasattr(d, "_task_off"):
+        d._task_off = np.zeros(d.n_lr + 1, np.int64)
+        np.cumsum(np.bincount(d.t_lr, minlength=d.n_lr), out=d._task_off[1:])
     t = time.perf_counter()
+    if bwa:
+        if workers == 1:
+            per_read = [_sr_records(r) for r in reads]
+        else:
+            with mp.get_context("fork").Pool(workers, initializer=_init_worker) as pool:
+                per_read = pool.map(_sr_records, reads, chunksize=64)
+        _RECS = {i: [] for i in lrs}
+        for recs in per_read:   # read order, then SAM order inside a read
+            for lr, rec in recs:
+                if lr in _RECS:
+                    _RECS[lr].append(rec)
     if workers == 1:
         res = [_lr_chain(i) for i in lrs]
     else:
         with mp.get_context("fork").Pool(workers, initializer=_init_worker) as pool:
-            res = pool.map(_lr_chain, list(lrs), chunksize=1)
+            res = pool.map(_lr_chain, lrs, chunksize=1)
     return time.perf_counter() - t, bases, res, workers

@@ -10,7 +10,8 @@ complements (no k-mer index, no count tables).
 Restated from upstream bwa (absent here; bwa-proovread's pinned commit is
 unknown, .gitmodules:4-6 — parity unpinned):
   bwamem.c  mem_collect_intv (three seeding rounds), mem_chain, test_and_merge,
-            mem_chain_weight, mem_chain_flt, mem_chain2aln's seed order / window
+            mem_chain_weight, mem_chain_flt, mem_chain2aln's seed order (every seed of a
+            kept chain, srt order) and window
   bwt.c     bwt_smem1a (max_intv = 0), bwt_seed_strategy1
 over the same index definition as the library: forward long reads then the
 reverse complement of their concatenation (bwa's forward-reverse coordinates),
@@ -275,21 +276,22 @@ def map_read(I: Index, O: Opts, q, sid=0):
             if chains[j]["first"] >= 0:
                 chains[chains[j]["first"]]["kept"] = 1
     out = []
+    nk = 0
     for c in chains:
         if c["kept"] == 0:
             continue
-        best = 0
-        for i in range(1, len(c["seeds"])):
-            if c["seeds"][i]["len"] >= c["seeds"][best]["len"]:
-                best = i
-        s = c["seeds"][best]
-        rev = s["rbeg"] >= I.l_pac
+        rev = c["seeds"][0]["rbeg"] >= I.l_pac
         rid = c["rid"]
         L = I.lr_off[rid + 1] - I.lr_off[rid]
         cs = I.l_pac + (I.l_pac - I.lr_off[rid + 1]) if rev else I.lr_off[rid]
         r0 = min(t["rbeg"] - (t["qbeg"] + _max_gap(O, t["qbeg"])) for t in c["seeds"]) - cs
         r1 = max(t["rbeg"] + t["len"] + ((n - t["qbeg"] - t["len"]) + _max_gap(O, n - t["qbeg"] - t["len"]))
                  for t in c["seeds"]) - cs
-        out.append(dict(sr=sid, lr=rid, strand=int(rev), qbeg=s["qbeg"], rbeg=s["rbeg"] - cs, slen=s["len"],
-                        rmax0=max(r0, 0), rmax1=min(r1, L), weight=c["w"], nseed=len(c["seeds"])))
+        # mem_chain2aln's srt order: (score = length, index) descending
+        order = sorted(range(len(c["seeds"])), key=lambda i: (c["seeds"][i]["len"], i), reverse=True)
+        for rank, i in enumerate(order):
+            s = c["seeds"][i]
+            out.append(dict(sr=sid, lr=rid, strand=int(rev), qbeg=s["qbeg"], rbeg=s["rbeg"] - cs, slen=s["len"],
+                            rmax0=max(r0, 0), rmax1=min(r1, L), chain=nk, rank=rank))
+        nk += 1
     return out

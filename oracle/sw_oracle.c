@@ -259,11 +259,18 @@ static inline uint8_t strand_base(const uint8_t *ref, int L, int strand, int x) 
     return c < 4 ? (uint8_t)(3 - c) : c;
 }
 
-int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, int L, int strand,
-             int qbeg, int rbeg, int slen, osw_result *r) {
+/* one strand-coordinate base of long read `ref` (forward, length L) */
+static void fetch_strand(const uint8_t *ref, int L, int strand, long b, long e, uint8_t *out) {
+    for (long x = b; x < e; ++x) out[x - b] = strand_base(ref, L, strand, (int)x);
+}
+
+/* bwamem.c mem_chain2aln, the extension of one seed (the window of a single seed: a chain's
+ * wider window adds only rows the band cannot reach with a gain, cal_max_gap's bound) */
+int osw_extend_seed(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, int L, int strand,
+                    int qbeg, int rbeg, int slen, osw_region *g) {
     int8_t mat[25];
     osw_fill_scmat(o->a, o->b, mat);
-    memset(r, 0, sizeof(*r));
+    memset(g, 0, sizeof(*g));
     if (lq <= 0 || slen <= 0 || qbeg < 0 || qbeg + slen > lq || rbeg < 0 || rbeg + slen > L) return -1;
     /* mem_chain2aln: max possible span */
     long rmax0 = (long)rbeg - (qbeg + cal_max_gap(o, qbeg));
@@ -272,7 +279,7 @@ int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, in
     if (rmax1 > L) rmax1 = L;
     const int rl = (int)(rmax1 - rmax0);
     uint8_t *rseq = (uint8_t *)malloc((size_t)rl + 1);
-    for (int x = 0; x < rl; ++x) rseq[x] = strand_base(ref, L, strand, (int)rmax0 + x);
+    fetch_strand(ref, L, strand, rmax0, rmax1, rseq);
     int aw0 = o->w, aw1 = o->w;
     int score = -1, truesc = -1, qb, qe, rb, re;
     if (qbeg) {
@@ -323,61 +330,91 @@ int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, in
     } else {
         qe = lq, re = rbeg + slen;
     }
-    r->qb = qb; r->qe = qe; r->rb = rb; r->re = re;
-    r->score = score; r->truesc = truesc;
-    r->w = aw0 > aw1 ? aw0 : aw1;
-    r->pass = (double)score >= o->min_score_per_base * (double)(qe - qb);
+    free(rseq);
+    g->qb = qb; g->qe = qe; g->rb = rb; g->re = re;
+    g->score = score; g->truesc = truesc;
+    g->w = aw0 > aw1 ? aw0 : aw1;
+    g->seedlen0 = slen;
+    return 0;
+}
 
-    /* mem_reg2aln: global alignment of [qb,qe) x [rb,re) */
+/* bwa.c bwa_gen_cigar2 over query q[0,lqq) and strand reference [rb, re): the global score,
+ * and the CIGAR (bwa op codes, reversed-both placement on the reverse strand) when cig != 0 */
+static int gen_cigar2(const osw_opts *o, const int8_t *mat, int w_, const uint8_t *qseg, int lqq, const uint8_t *ref,
+                      int L, int strand, int rb, int re, uint32_t *cig, int *ncig, int *w_used) {
+    const int rlen = re - rb;
+    int gsc = 0;
+    *ncig = 0;
+    *w_used = 0;
+    if (lqq <= 0 || rlen <= 0) return 0;
+    uint8_t *qq = (uint8_t *)malloc((size_t)lqq + 1);
+    uint8_t *rr = (uint8_t *)malloc((size_t)rlen + 1);
+    memcpy(qq, qseg, (size_t)lqq);
+    fetch_strand(ref, L, strand, rb, re, rr);
+    if (strand) { /* reverse both so indels are placed leftmost on the forward strand */
+        for (int i = 0; i < lqq >> 1; ++i) { uint8_t t = qq[i]; qq[i] = qq[lqq - 1 - i]; qq[lqq - 1 - i] = t; }
+        for (int i = 0; i < rlen >> 1; ++i) { uint8_t t = rr[i]; rr[i] = rr[rlen - 1 - i]; rr[rlen - 1 - i] = t; }
+    }
+    if (lqq == rlen && w_ == 0) {
+        if (cig) { cig[0] = (uint32_t)lqq << 4; *ncig = 1; }
+        for (int i = 0; i < lqq; ++i) gsc += mat[rr[i] * 5 + qq[i]];
+    } else {
+        int mn = lqq < rlen ? lqq : rlen;
+        int max_ins = (int)((double)(mn * mat[0] - o->o_ins) / o->e_ins + 1.);
+        int max_del = (int)((double)(mn * mat[0] - o->o_del) / o->e_del + 1.);
+        int max_gap = max_ins > max_del ? max_ins : max_del;
+        max_gap = max_gap > 1 ? max_gap : 1;
+        int ww = (max_gap + abs(rlen - lqq) + 1) >> 1;
+        ww = ww < w_ ? ww : w_;
+        int min_w = abs(rlen - lqq) + 3;
+        ww = ww > min_w ? ww : min_w;
+        int nc = 0;
+        uint32_t *tmp = cig ? cig : (uint32_t *)malloc(sizeof(uint32_t) * OSW_MAXCIG);
+        gsc = osw_global(lqq, qq, rlen, rr, 5, mat, o->o_del, o->e_del, o->o_ins, o->e_ins, ww, &nc, tmp,
+                         OSW_MAXCIG - 4);
+        if (cig) *ncig = nc; else free(tmp);
+        *w_used = ww;
+    }
+    free(qq);
+    free(rr);
+    return gsc;
+}
+
+int osw_gen_score(const osw_opts *o, int w_, const uint8_t *qseg, int lqq, const uint8_t *ref, int L, int strand,
+                  int rb, int re) {
+    int8_t mat[25];
+    osw_fill_scmat(o->a, o->b, mat);
+    int nc, wu;
+    return gen_cigar2(o, mat, w_, qseg, lqq, ref, L, strand, rb, re, 0, &nc, &wu);
+}
+
+/* bwamem.c mem_reg2aln: the CIGAR of region g (infer_bw, up to 3 global passes) */
+int osw_reg2aln(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, int L, int strand,
+                const osw_region *g, osw_result *r) {
+    int8_t mat[25];
+    osw_fill_scmat(o->a, o->b, mat);
+    memset(r, 0, sizeof(*r));
+    const int qb = g->qb, qe = g->qe, rb = g->rb, re = g->re, truesc = g->truesc;
+    r->qb = qb; r->qe = qe; r->rb = rb; r->re = re;
+    r->score = g->score; r->truesc = truesc; r->w = g->w;
+    r->pass = (double)g->score >= o->min_score_per_base * (double)(qe - qb);
     int tmpw = infer_bw(qe - qb, re - rb, truesc, o->a, o->o_del, o->e_del);
     int w2 = infer_bw(qe - qb, re - rb, truesc, o->a, o->o_ins, o->e_ins);
     w2 = w2 > tmpw ? w2 : tmpw;
-    if (w2 > o->w) w2 = w2 < r->w ? w2 : r->w;
+    if (w2 > o->w) w2 = w2 < g->w ? w2 : g->w;
     int last_sc = -(1 << 30), gsc = 0, ncig = 0, iter = 0;
-    const int lqq = qe - qb, rlen = re - rb;
-    uint8_t *qq = (uint8_t *)malloc((size_t)lqq + 1);
-    uint8_t *rr = (uint8_t *)malloc((size_t)rlen + 1);
     uint32_t cig[OSW_MAXCIG];
     int w_used = 0;
     do {
         w2 = w2 < o->w << 2 ? w2 : o->w << 2;
-        /* bwa_gen_cigar2 */
-        for (int i = 0; i < lqq; ++i) qq[i] = q[qb + i];
-        for (int i = 0; i < rlen; ++i) rr[i] = rseq[rb - rmax0 + i];
-        if (strand) { /* reverse both so indels are placed leftmost on the forward strand */
-            for (int i = 0; i < lqq >> 1; ++i) { uint8_t t = qq[i]; qq[i] = qq[lqq - 1 - i]; qq[lqq - 1 - i] = t; }
-            for (int i = 0; i < rlen >> 1; ++i) { uint8_t t = rr[i]; rr[i] = rr[rlen - 1 - i]; rr[rlen - 1 - i] = t; }
-        }
-        if (lqq <= 0 || rlen <= 0) { ncig = 0; gsc = 0; break; }
-        if (lqq == rlen && w2 == 0) {
-            cig[0] = (uint32_t)lqq << 4;
-            ncig = 1;
-            gsc = 0;
-            for (int i = 0; i < lqq; ++i) gsc += mat[rr[i] * 5 + qq[i]];
-            w_used = 0;
-        } else {
-            int mn = lqq < rlen ? lqq : rlen;
-            int max_ins = (int)((double)(mn * mat[0] - o->o_ins) / o->e_ins + 1.);
-            int max_del = (int)((double)(mn * mat[0] - o->o_del) / o->e_del + 1.);
-            int max_gap = max_ins > max_del ? max_ins : max_del;
-            max_gap = max_gap > 1 ? max_gap : 1;
-            int ww = (max_gap + abs(rlen - lqq) + 1) >> 1;
-            ww = ww < w2 ? ww : w2;
-            int min_w = abs(rlen - lqq) + 3;
-            ww = ww > min_w ? ww : min_w;
-            gsc = osw_global(lqq, qq, rlen, rr, 5, mat, o->o_del, o->e_del, o->o_ins, o->e_ins, ww,
-                             &ncig, cig, OSW_MAXCIG - 4);
-            w_used = ww;
-        }
+        gsc = gen_cigar2(o, mat, w2, q + qb, qe - qb, ref, L, strand, rb, re, cig, &ncig, &w_used);
+        if (qe - qb <= 0 || re - rb <= 0) break;
         if (gsc == last_sc || w2 == o->w << 2) break;
         last_sc = gsc;
         w2 <<= 1;
     } while (++iter < 3 && gsc < truesc - o->a);
     r->global_score = gsc;
     r->w2 = w_used;
-    free(qq);
-    free(rr);
-    free(rseq);
     /* forward position; convert bwa op codes (M0 I1 D2) to BAM (M0 I1 D2 S4) */
     int pos = strand ? L - re : rb;
     int n = 0;
@@ -403,4 +440,13 @@ int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, in
     r->n_cigar = m;
     r->pos = pos;
     return 0;
+}
+
+/* one single-seed task: extension + CIGAR */
+int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, int L, int strand,
+             int qbeg, int rbeg, int slen, osw_result *r) {
+    osw_region g;
+    memset(r, 0, sizeof(*r));
+    if (osw_extend_seed(o, q, lq, ref, L, strand, qbeg, rbeg, slen, &g)) return -1;
+    return osw_reg2aln(o, q, lq, ref, L, strand, &g, r);
 }

@@ -44,6 +44,18 @@ int osw_global(int qlen, const uint8_t *query, int tlen, const uint8_t *target, 
  * `ref` (forward strand, nt4, length L); strand 1 = the read aligns to the
  * reverse complement; (qbeg, rbeg, slen) is the exact-match seed with rbeg in
  * strand coordinates.  Returns 0 or <0 on error. */
+/* mem_alnreg_t of one extended seed (strand coordinates) */
+typedef struct {
+    int qb, qe, rb, re, score, truesc, w, seedlen0;
+} osw_region;
+int osw_extend_seed(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, int L, int strand,
+                    int qbeg, int rbeg, int slen, osw_region *g);
+/* mem_reg2aln: CIGAR, POS and the -T flag of a region */
+int osw_reg2aln(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, int L, int strand,
+                const osw_region *g, osw_result *r);
+/* bwa_gen_cigar2's global score of qseg[0,lqq) against strand reference [rb,re) at band w_ */
+int osw_gen_score(const osw_opts *o, int w_, const uint8_t *qseg, int lqq, const uint8_t *ref, int L, int strand,
+                  int rb, int re);
 int osw_task(const osw_opts *o, const uint8_t *q, int lq, const uint8_t *ref, int L, int strand,
              int qbeg, int rbeg, int slen, osw_result *r);
 

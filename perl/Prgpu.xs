@@ -122,6 +122,10 @@ static void fill_sw_opts(pTHX_ HV *opts, pr_sw_opts *o) {
     o->min_score_per_base = num(aTHX_ opts, "min_score_per_base", o->min_score_per_base);
     o->bin_size = inum(aTHX_ opts, "bin_size", o->bin_size);
     o->bin_length = num(aTHX_ opts, "bin_length", o->bin_length);
+    o->drop_ratio = num(aTHX_ opts, "drop_ratio", o->drop_ratio);
+    o->mask_level = num(aTHX_ opts, "mask_level", o->mask_level);
+    o->mask_level_redun = num(aTHX_ opts, "mask_level_redun", o->mask_level_redun);
+    o->max_chain_gap = inum(aTHX_ opts, "max_chain_gap", o->max_chain_gap);
 }
 
 /* consensus output pools as Perl strings (13 of them, returned as a hash of packed data) */
@@ -186,6 +190,9 @@ static void fill_sw_batch(pTHX_ HV *batch, pr_sw_batch *b) {
     b->t_qbeg = (const int32_t *)field(aTHX_ batch, "t_qbeg", 4 * (size_t)nt, 0, NULL);
     b->t_rbeg = (const int32_t *)field(aTHX_ batch, "t_rbeg", 4 * (size_t)nt, 0, NULL);
     b->t_slen = (const int32_t *)field(aTHX_ batch, "t_slen", 4 * (size_t)nt, 0, NULL);
+    /* bwa mode: the seeds of every kept chain with their chain index (pr_seed_map order) */
+    b->t_chain = (const int32_t *)field(aTHX_ batch, "t_chain", 4 * (size_t)nt, 1, NULL);
+    b->read_id0 = (int64_t)num(aTHX_ batch, "read_id0", 0);
 }
 
 MODULE = Prgpu  PACKAGE = Prgpu
@@ -367,21 +374,24 @@ sw_run(IV ctx, HV *opts, HV *batch)
     HV *res;
     fill_sw_opts(aTHX_ opts, &o);
     fill_sw_batch(aTHX_ batch, &b);
-    nt = b.n_task;
     {
-        /* outputs, one Perl string each; CIGARs variable length (cigar_off prefix) */
+        /* outputs, one Perl string each, per task (bwa mode: per reported alignment, SAM order,
+           with the seed task and FLAG); CIGARs variable length (cigar_off prefix) */
         int64_t ctot = 0, nover = 0;
         pr_ctx *cx = INT2PTR(pr_ctx *, ctx);
         rc = pr_sw_upload(cx, &b);
         if (rc == 0) rc = pr_sw_launch(cx, &o);
+        if (rc == 0) rc = pr_sw_aln_count(cx, &nt);
         if (rc == 0) rc = pr_sw_cigar_total(cx, &ctot, &nover);
         if (rc != 0) croak("Prgpu: pr_sw_run: %s (%d)", pr_last_error(), rc);
         SV *s_pos = newSV(4 * nt + 1), *s_sc = newSV(4 * nt + 1), *s_nc = newSV(4 * nt + 1),
            *s_cig = newSV(4 * (size_t)ctot + 1), *s_pass = newSV(nt + 1), *s_st = newSV(4 * nt + 1),
-           *s_qb = newSV(4 * nt + 1), *s_qe = newSV(4 * nt + 1), *s_coff = newSV(8 * (size_t)(nt + 1) + 1);
-        SV *all[] = {s_pos, s_sc, s_nc, s_cig, s_pass, s_st, s_qb, s_qe, s_coff};
-        const STRLEN lens[] = {4 * nt, 4 * nt, 4 * nt, 4 * (size_t)ctot, nt, 4 * nt, 4 * nt, 4 * nt, 8 * (size_t)(nt + 1)};
-        const char *keys[] = {"pos", "score", "ncigar", "cigar", "pass", "status", "qb", "qe", "cigar_off"};
+           *s_qb = newSV(4 * nt + 1), *s_qe = newSV(4 * nt + 1), *s_coff = newSV(8 * (size_t)(nt + 1) + 1),
+           *s_task = newSV(4 * nt + 1), *s_flag = newSV(4 * nt + 1);
+        SV *all[] = {s_pos, s_sc, s_nc, s_cig, s_pass, s_st, s_qb, s_qe, s_coff, s_task, s_flag};
+        const STRLEN lens[] = {4 * nt, 4 * nt, 4 * nt, 4 * (size_t)ctot, nt, 4 * nt, 4 * nt, 4 * nt, 8 * (size_t)(nt + 1),
+                               4 * nt, 4 * nt};
+        const char *keys[] = {"pos", "score", "ncigar", "cigar", "pass", "status", "qb", "qe", "cigar_off", "task", "flag"};
         unsigned k;
         for (k = 0; k < sizeof all / sizeof all[0]; ++k) {
             SvPOK_on(all[k]);
@@ -399,6 +409,8 @@ sw_run(IV ctx, HV *opts, HV *batch)
         out.status = (int32_t *)SvPVX(s_st);
         out.qb = (int32_t *)SvPVX(s_qb);
         out.qe = (int32_t *)SvPVX(s_qe);
+        out.task = (int32_t *)SvPVX(s_task);
+        out.flag = (int32_t *)SvPVX(s_flag);
         rc = pr_sw_download(cx, &out);
         if (rc != 0) {
             for (k = 0; k < sizeof all / sizeof all[0]; ++k) SvREFCNT_dec(all[k]);
@@ -406,6 +418,7 @@ sw_run(IV ctx, HV *opts, HV *batch)
         }
         res = newHV();
         for (k = 0; k < sizeof all / sizeof all[0]; ++k) hv_store(res, keys[k], (I32)strlen(keys[k]), all[k], 0);
+        hv_store(res, "n", 1, newSViv((IV)nt), 0);
     }
     RETVAL = newRV_noinc((SV *)res);
   OUTPUT:
@@ -490,7 +503,8 @@ iter_run(IV ctx, HV *sw_opts, HV *params, HV *batch)
     /* One correction iteration on the device (bin/proovread:835-869 for one task: run_bwa,
        create_sorted_bam and correct_sr_mt without the SAM/BAM files): seed extension + CIGAR
        of every task, the hand-off into samtools coordinate order, the consensus of every long
-       read.  Tasks grouped by long read (task_lr_off); lr_qual / ref_seq optional. */
+       read.  Tasks grouped by long read (task_lr_off), or bwa mode (t_chain: the seeds of every
+       kept chain, grouped by short read); lr_qual / ref_seq optional. */
     pr_sw_opts o;
     pr_cns_params p;
     pr_iter_batch b;
@@ -505,12 +519,14 @@ iter_run(IV ctx, HV *sw_opts, HV *params, HV *batch)
     memset(&b, 0, sizeof b);
     fill_sw_batch(aTHX_ batch, &b.sw);
     nbases = i64_at((const char *)b.sw.lr_off, b.sw.n_lr);
-    tlo = field(aTHX_ batch, "task_lr_off", 8 * (size_t)(b.sw.n_lr + 1), 0, NULL);
-    if (i64_at(tlo, 0) != 0 || i64_at(tlo, b.sw.n_lr) != b.sw.n_task)
-        croak("Prgpu::iter_run: task_lr_off must run from 0 to n_task");
-    for (i = 0; i < b.sw.n_lr; ++i)
-        if (i64_at(tlo, i + 1) < i64_at(tlo, i)) croak("Prgpu::iter_run: task_lr_off not monotone");
-    b.task_lr_off = (const int64_t *)tlo;
+    if (!b.sw.t_chain) {   /* single-seed tasks grouped by long read; bwa mode groups on the device */
+        tlo = field(aTHX_ batch, "task_lr_off", 8 * (size_t)(b.sw.n_lr + 1), 0, NULL);
+        if (i64_at(tlo, 0) != 0 || i64_at(tlo, b.sw.n_lr) != b.sw.n_task)
+            croak("Prgpu::iter_run: task_lr_off must run from 0 to n_task");
+        for (i = 0; i < b.sw.n_lr; ++i)
+            if (i64_at(tlo, i + 1) < i64_at(tlo, i)) croak("Prgpu::iter_run: task_lr_off not monotone");
+        b.task_lr_off = (const int64_t *)tlo;
+    }
     b.lr_qual = (const uint8_t *)field(aTHX_ batch, "lr_qual", (size_t)nbases, 1, NULL);
     b.ref_seq = (const uint8_t *)field(aTHX_ batch, "ref_seq", (size_t)nbases, 1, NULL);
     if ((rc = pr_iter_upload(INT2PTR(pr_ctx *, ctx), &b)) != 0)

@@ -239,7 +239,8 @@ sub sw_unpack {
         push @cig, join '', map { ($_ >> 4) . substr($CIGAR_CHARS, $_ & 15, 1) } @ops;
     }
     return {pos => [unpack('l<*', $o->{pos})], score => [unpack('l<*', $o->{score})],
-            pass => [unpack('C*', $o->{pass})], status => [unpack('l<*', $o->{status})], cigar => \@cig};
+            pass => [unpack('C*', $o->{pass})], status => [unpack('l<*', $o->{status})], cigar => \@cig,
+            task => [unpack('l<*', $o->{task})], flag => [unpack('l<*', $o->{flag})]};
 }
 
 # Sam::Alignment::length (Alignment.pm:417-431): M+D if SEQ is empty or the CIGAR starts or
@@ -267,7 +268,7 @@ sub seed_batch {
     seed_index_free($ix);
     die $err if $err;
     my $nt = length($packed) / TASK_BYTES;
-    my (@t_sr, @t_lr, @t_strand, @t_qbeg, @t_rbeg, @t_slen);
+    my (@t_sr, @t_lr, @t_strand, @t_qbeg, @t_rbeg, @t_slen, @t_chain);
     for my $t (0 .. $nt - 1) {
         my @f = unpack('l<10', substr($packed, TASK_BYTES * $t, TASK_BYTES));
         push @t_sr, $f[0];
@@ -276,17 +277,21 @@ sub seed_batch {
         push @t_qbeg, $f[3];
         push @t_rbeg, $f[4];
         push @t_slen, $f[5];
+        push @t_chain, $f[8];
     }
+    # bwa mode: every seed of the kept chains, grouped by short read, then chain (t_chain)
     my %batch = (sr_seq => $sr_pool, sr_off => $sr_off, lr_seq => $lr_pool, lr_off => $lr_off, n_task => $nt,
                  t_sr => pack('l<*', @t_sr), t_lr => pack('l<*', @t_lr), t_strand => pack('C*', @t_strand),
-                 t_qbeg => pack('l<*', @t_qbeg), t_rbeg => pack('l<*', @t_rbeg), t_slen => pack('l<*', @t_slen));
+                 t_qbeg => pack('l<*', @t_qbeg), t_rbeg => pack('l<*', @t_rbeg), t_slen => pack('l<*', @t_slen),
+                 t_chain => pack('l<*', @t_chain));
     return (\%batch, {sr => \@t_sr, lr => \@t_lr, strand => \@t_strand, qbeg => \@t_qbeg, rbeg => \@t_rbeg,
-                      slen => \@t_slen});
+                      slen => \@t_slen, chain => \@t_chain});
 }
 
 # mem(%a) -> (header lines, record lines): the output of `bwa-proovread mem`.
-#   ctx        Prgpu::Context (or a sw_runner coderef taking the task batch hash and
-#              returning {pos, score, pass, status, cigar} arrays — the tests inject the oracle)
+#   ctx        Prgpu::Context (or a sw_runner coderef taking the seed batch hash and returning
+#              {pos, score, pass, status, cigar, task, flag} arrays per reported alignment in SAM
+#              order — the tests inject the oracle)
 #   seed_opts, sw_opts  option hashes for seed_map / sw_run ({finish => 0|1, ...})
 #   b, l       the -b/-l bin filter (0: off)
 #   threads    host seeding threads
@@ -301,8 +306,14 @@ sub mem {
     my @t_sr = @$t_sr;
     my @t_lr = @$t_lr;
     my @t_strand = @$t_strand;
-    my $res = ref $a{ctx} eq 'CODE' ? $a{ctx}->(\%batch)
-            : sw_unpack(sw_run(ref $a{ctx} ? $a{ctx}->handle : $a{ctx}, $a{sw_opts} || {}, \%batch), $nt);
+    my $res;
+    if (ref $a{ctx} eq 'CODE') {
+        $res = $a{ctx}->(\%batch);
+    } else {
+        my $o = sw_run(ref $a{ctx} ? $a{ctx}->handle : $a{ctx}, $a{sw_opts} || {}, \%batch);
+        $res = sw_unpack($o, $o->{n});
+    }
+
 
     my @head = ("\@HD\tVN:1.5\tSO:unsorted\n");
     push @head, "\@SQ\tSN:$a{lr_names}[$_]\tLN:" . length($a{lr_seqs}[$_]) . "\n" for 0 .. $#{$a{lr_names}};
@@ -332,39 +343,32 @@ sub mem {
         $alive[$rid] = 1;
     };
 
+    # the reported alignments in SAM order, read by read (bwa mode: the device ran mem_chain2aln,
+    # mem_sort_dedup_patch, mem_mark_primary_se and mem_reg2sam's filters)
     my @rec;
-    my ($pos, $sc, $ps, $st, $cg) = @$res{qw(pos score pass status cigar)};
-    my $t = 0;
-    while ($t < $nt) {
-        my $r = $t_sr[$t];
-        my $e = $t;
-        ++$e while $e < $nt && $t_sr[$e] == $r;
-        my @hits = grep { $st->[$_] == 0 && $ps->[$_] } $t .. $e - 1;
-        if (@hits) {
-            my $best = $hits[0];
-            for my $x (@hits) { $best = $x if $sc->[$x] > $sc->[$best] }   # highest score, first on ties
-            my $q = $a{sr_seqs}[$r];
-            my $qual = $a{sr_quals}[$r];
-            for my $x (@hits) {
-                my $strand = $t_strand[$x];
-                my ($s, $qq);
-                if ($strand) {
-                    ($s = $q) =~ tr/ACGTacgt/N/c;
-                    $s =~ tr/ACGTacgt/TGCATGCA/;
-                    $s = reverse $s;
-                    $qq = defined $qual ? scalar reverse($qual) : '*';
-                } else {
-                    $s = uc $q;
-                    $qq = defined $qual ? $qual : '*';
-                }
-                my $flag = ($strand ? 16 : 0) | ($x == $best ? 0 : 256);
-                my $mapq = $x == $best ? 60 : 0;
-                push @rec, join("\t", $a{sr_names}[$r], $flag, $a{lr_names}[$t_lr[$x]], $pos->[$x] + 1, $mapq,
-                                $cg->[$x], '*', 0, 0, $s, $qq, "AS:i:$sc->[$x]") . "\n";
-                $bin_add->($t_lr[$x], $pos->[$x] + 1, aln_length($cg->[$x], length $q), $sc->[$x]) if $filter;
-            }
+    my ($pos, $sc, $ps, $st, $cg, $tk, $fl) = @$res{qw(pos score pass status cigar task flag)};
+    for my $i (0 .. $#$pos) {
+        next unless $st->[$i] == 0 && $ps->[$i];
+        my $x = $tk->[$i];
+        my $r = $t_sr[$x];
+        my $strand = $t_strand[$x];
+        my $q = $a{sr_seqs}[$r];
+        my $qual = $a{sr_quals}[$r];
+        my ($s, $qq);
+        if ($strand) {
+            ($s = $q) =~ tr/ACGTacgt/N/c;
+            $s =~ tr/ACGTacgt/TGCATGCA/;
+            $s = reverse $s;
+            $qq = defined $qual ? scalar reverse($qual) : '*';
+        } else {
+            $s = uc $q;
+            $qq = defined $qual ? $qual : '*';
         }
-        $t = $e;
+        my $flag = $fl->[$i];
+        my $mapq = $flag & 0x100 ? 0 : 60;   # mem_approx_mapq_se is not restated
+        push @rec, join("\t", $a{sr_names}[$r], $flag, $a{lr_names}[$t_lr[$x]], $pos->[$i] + 1, $mapq,
+                        $cg->[$i], '*', 0, 0, $s, $qq, "AS:i:$sc->[$i]") . "\n";
+        $bin_add->($t_lr[$x], $pos->[$i] + 1, aln_length($cg->[$i], length $q), $sc->[$i]) if $filter;
     }
     @rec = @rec[grep { $alive[$_] } 0 .. $#rec] if $filter;
     return (\@head, \@rec);
@@ -384,16 +388,7 @@ sub mem {
 sub iteration {
     my (%a) = @_;
     my ($bt, $tc) = seed_batch(%a);
-    my %batch = %$bt;
-    my $nt = $batch{n_task};
-    my @ord = sort { $tc->{lr}[$a] <=> $tc->{lr}[$b] || $a <=> $b } 0 .. $nt - 1;   # grouped by long read, stable
-    for my $k (qw(sr lr qbeg rbeg slen)) { $batch{"t_$k"} = pack('l<*', @{$tc->{$k}}[@ord]) }
-    $batch{t_strand} = pack('C*', @{$tc->{strand}}[@ord]);
-    my @cnt = (0) x @{$a{lr_seqs}};
-    ++$cnt[$_] for @{$tc->{lr}};
-    my @tlo = (0);
-    push @tlo, $tlo[-1] + $_ for @cnt;
-    $batch{task_lr_off} = pack('q<*', @tlo);
+    my %batch = %$bt;   # bwa mode: the seeds as pr_seed_map returns them, grouped on the device
     $batch{lr_qual} = join '', map {
         my $q = $a{lr_quals} ? $a{lr_quals}[$_] : undef;
         defined $q ? $q : '$' x length $a{lr_seqs}[$_]

@@ -149,6 +149,7 @@ def options(a) -> Tuple[seed.SeedOpts, sw.SwOpts]:
     wo.w, wo.zdrop = a.w, a.d
     wo.pen_clip5, wo.pen_clip3 = _pair(a.L)
     wo.min_score_per_base = a.T
+    wo.drop_ratio = a.D   # mem_reg2sam drops secondaries below -D x their primary
     return so, wo
 
 
@@ -208,48 +209,45 @@ def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=Non
     ix = seed.SeedIndex(lr_pool, lr_off)
     tasks = ix.map(sr_pool, sr_off, so, threads=a.t)
     ix.close()
-    print(f"[bwa-proovread] {len(sr_seqs)} reads, {len(lr_seqs)} long reads, {len(tasks)} chains", file=log)
+    print(f"[bwa-proovread] {len(sr_seqs)} reads, {len(lr_seqs)} long reads, {len(tasks)} seeds", file=log)
+    # bwa mode: every seed of the kept chains goes to the device, which runs mem_chain2aln,
+    # mem_sort_dedup_patch, mem_mark_primary_se and mem_reg2sam's filters; the alignments come
+    # back in SAM order, read by read
     inp = sw.SwInput(sr_off, sr_pool, lr_off, lr_pool, tasks["sr"].astype(np.int32), tasks["lr"].astype(np.int32),
                      tasks["strand"].astype(np.uint8), tasks["qbeg"].astype(np.int32),
-                     tasks["rbeg"].astype(np.int32), tasks["slen"].astype(np.int32))
+                     tasks["rbeg"].astype(np.int32), tasks["slen"].astype(np.int32),
+                     tasks["chain"].astype(np.int32))
     res = (sw_runner or sw.run)(inp, wo)
     out.write("@HD\tVN:1.5\tSO:unsorted\n")
     for n, s in zip(lr_names, lr_seqs):
         out.write(f"@SQ\tSN:{n}\tLN:{len(s)}\n")
     out.write("@PG\tID:bwa-proovread\tPN:bwa-proovread\tVN:prgpu\tCL:bwa-proovread mem " + " ".join(argv) + "\n")
-    st, ps, sc, pos = res["status"], res["pass"], res["score"], res["pos"]
     filt = BinFilter(a.b, a.l) if a.b > 0 and a.l > 0 else None
     records = []
-    t = 0
-    nt = len(tasks)
-    while t < nt:
-        r = int(tasks["sr"][t])
-        e = t
-        while e < nt and int(tasks["sr"][e]) == r:
-            e += 1
-        hits = [x for x in range(t, e) if st[x] == 0 and ps[x]]
-        if hits:
-            best = max(hits, key=lambda x: (int(sc[x]), -x))
-            q = sr_seqs[r]
-            qual = sr_quals[r]
-            for x in hits:
-                strand = int(tasks["strand"][x])
-                if strand:
-                    codes = sw.NT4[np.frombuffer(q, np.uint8)]
-                    seqs = _ASCII[np.where(codes < 4, 3 - codes, 4)][::-1].tobytes().decode()
-                    quals = qual[::-1].decode() if qual is not None else "*"
-                else:
-                    seqs = q.decode().upper()
-                    quals = qual.decode() if qual is not None else "*"
-                flag = (16 if strand else 0) | (0 if x == best else 256)
-                mapq = 60 if x == best else 0
-                cig = res.cigar_str(x)
-                rec = (f"{sr_names[r]}\t{flag}\t{lr_names[int(tasks['lr'][x])]}\t{int(pos[x]) + 1}\t{mapq}\t"
-                       f"{cig}\t*\t0\t0\t{seqs}\t{quals}\tAS:i:{int(sc[x])}\n")
-                if filt is not None:
-                    filt.add(int(tasks["lr"][x]), int(pos[x]) + 1, aln_length(cig, len(q)), float(sc[x]))
-                records.append(rec)
-        t = e
+    for i in range(res.n):
+        if res["status"][i] != 0 or not res["pass"][i]:
+            continue
+        x = int(res["task"][i])
+        r, lr, strand = int(tasks["sr"][x]), int(tasks["lr"][x]), int(tasks["strand"][x])
+        q = sr_seqs[r]
+        qual = sr_quals[r]
+        if strand:
+            codes = sw.NT4[np.frombuffer(q, np.uint8)]
+            seqs = _ASCII[np.where(codes < 4, 3 - codes, 4)][::-1].tobytes().decode()
+            quals = qual[::-1].decode() if qual is not None else "*"
+        else:
+            seqs = q.decode().upper()
+            quals = qual.decode() if qual is not None else "*"
+        flag = int(res["flag"][i])
+        mapq = 0 if flag & 0x100 else 60   # mem_approx_mapq_se is not restated
+        cig = res.cigar_str(i)
+        sc = int(res["score"][i])
+        pos = int(res["pos"][i])
+        rec = (f"{sr_names[r]}\t{flag}\t{lr_names[lr]}\t{pos + 1}\t{mapq}\t"
+               f"{cig}\t*\t0\t0\t{seqs}\t{quals}\tAS:i:{sc}\n")
+        if filt is not None:
+            filt.add(lr, pos + 1, aln_length(cig, len(q)), float(sc))
+        records.append(rec)
     if filt is not None:
         records = [rec for rec, keep in zip(records, filt.alive) if keep]
         print(f"[bwa-proovread] -b {a.b} -l {a.l}: {len(records)} of {len(filt.alive)} records kept", file=log)

@@ -165,7 +165,8 @@ class ShortReads:
 
 # ---------------------------------------------------------------------------- device stages
 class GpuStages:
-    """The product's device stages: pr_iter_* (SW + hand-off + consensus) and pr_mask_run."""
+    """The product's device stages: pr_iter_* (bwa-mode SW + hand-off + consensus), and for the
+    multi-rank layout pr_sw_run (bwa mode) and pr_cns_run separately; pr_mask_run."""
 
     def __init__(self, ctx=None):
         from . import _abi
@@ -173,9 +174,10 @@ class GpuStages:
 
     def iteration(self, d, ref_seq: np.ndarray, ref_qual: np.ndarray, task: str, params,
                   bin_filter: Optional[Tuple[int, float]] = None) -> List[tuple]:
-        """-> per long read (status, seq, qual, chim lines with id `lr<i>`).  task: the bwa task
-        whose options the SW stage takes (proovread.cfg:318-365); bin_filter: (BIN, LEN) of
-        bwa-proovread -b/-l, applied on the device between the SW stage and the hand-off."""
+        """-> per long read (status, seq, qual, chim lines with id `lr<i>`).  d: bwa-mode seeds of
+        every sampled short read; task: the bwa task whose options the SW stage takes
+        (proovread.cfg:318-365); bin_filter: (BIN, LEN) of bwa-proovread -b/-l, applied on the
+        device between the SW stage and the hand-off."""
         from . import iteration
         it = iteration.Iteration(d, lr_qual=ref_qual, ctx=self.ctx, ref_seq=ref_seq)
         opts = T.options(task)[1]
@@ -184,6 +186,31 @@ class GpuStages:
         it.launch(opts, params)
         return [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
 
+    def align(self, d, task: str) -> List[tuple]:
+        """bwa-mode SW of d's seeds (pr_sw_run): the reported alignments in SAM order, read by
+        read, as (sr, lr, strand, pos, score, flag, cigar ops)."""
+        from . import sw
+        res = sw.run(d.sw_input(), T.options(task)[1], ctx=self.ctx)
+        out = []
+        for i in range(res.n):
+            if res["status"][i] != 0 or not res["pass"][i]:
+                continue
+            t = int(res["task"][i])
+            out.append((int(d.t_sr[t]), int(d.t_lr[t]), int(d.t_strand[t]), int(res["pos"][i]), int(res["score"][i]),
+                        int(res["flag"][i]), [int(x) for x in res.cigar_ops(i)]))
+        return out
+
+    def consensus(self, ids: List[str], ref_seq: List[bytes], ref_qual: List[bytes], sams: List[List[str]],
+                  params) -> List[tuple]:
+        """bam2cns on records already in samtools order (pr_cns_run) -> per long read (status,
+        seq, qual, chim lines)."""
+        from . import cns
+        reads = [cns.LongRead(ids[i], ref_seq[i].decode("latin-1"), ref_qual[i].decode("latin-1"))
+                 for i in range(len(ids))]
+        alns = [[cns.SamRecord.from_line(x) for x in v] for v in sams]
+        res = cns.run_chunk(reads, alns, params, ctx=self.ctx)
+        return [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in res]
+
     def mask(self, seqs: List[bytes], quals: List[bytes], hcr_mask: str, min_sr_length: int):
         """-> (masked reads, bpt, bpN)."""
         from . import mask
@@ -191,16 +218,17 @@ class GpuStages:
         return masked, bpt, bpn
 
 
-def _tasks_dataset(lr_map: np.ndarray, lr_off: np.ndarray, sr: np.ndarray, sr_off: np.ndarray, tasks: np.ndarray):
+def _seeds_dataset(lr_map: np.ndarray, lr_off: np.ndarray, sr: np.ndarray, sr_off: np.ndarray, tasks: np.ndarray):
+    """bwa mode: the seeds of every kept chain (pr_seed_map order: grouped by short read)."""
     from .sw import SwInput
-    order = np.argsort(tasks["lr"], kind="stable")
-    t = tasks[order]
+    t = tasks
     d = SimpleNamespace(lr_seq=lr_map, lr_off=lr_off, sr_seq=sr, sr_off=sr_off, n_lr=len(lr_off) - 1,
                         n_sr=len(sr_off) - 1, t_sr=t["sr"].astype(np.int32), t_lr=t["lr"].astype(np.int32),
                         t_strand=t["strand"].astype(np.uint8), t_qbeg=t["qbeg"].astype(np.int32),
-                        t_rbeg=t["rbeg"].astype(np.int32), t_slen=t["slen"].astype(np.int32))
+                        t_rbeg=t["rbeg"].astype(np.int32), t_slen=t["slen"].astype(np.int32),
+                        t_chain=t["chain"].astype(np.int32))
     d.sw_input = lambda: SwInput(d.sr_off, d.sr_seq, d.lr_off, d.lr_seq, d.t_sr, d.t_lr, d.t_strand, d.t_qbeg,
-                                 d.t_rbeg, d.t_slen)
+                                 d.t_rbeg, d.t_slen, d.t_chain)
     return d
 
 
@@ -210,33 +238,76 @@ def _rename(lines: List[str], rid: str) -> List[str]:
 
 # ---------------------------------------------------------------------------- multi-rank
 # The collectives of the multi-rank loop (comm.py).  Layout: SURVEY.md §8e's exact-parity
-# option (exact_shard.py): every rank keeps the whole read set and its index, seeds a
-# contiguous shard of the sampled short reads, sends each task to the owner of its long
-# read (one all-to-all), corrects and masks the long reads it owns; the corrected and
-# masked reads are then all-gathered for the next task's index and consensus reference,
-# and bpt/bpN all-reduced so every rank takes the same mask_shortcut decision (the north
-# star's per-iteration statistics gather).  GPU ranks use comm.RcclComm (RCCL inside
+# option (exact_shard.py): every rank keeps the whole read set and its index, seeds and
+# aligns a contiguous shard of the sampled short reads (bwa mode: every read's alignment is
+# decided on one rank, as bwa decides it over all long reads), sends each reported
+# alignment to the owner of its long read (all-to-all), corrects and masks the long reads
+# it owns; the corrected and masked reads are then all-gathered for the next task's index
+# and consensus reference, and bpt/bpN all-reduced so every rank takes the same
+# mask_shortcut decision (the north star's per-iteration statistics gather).  GPU ranks use comm.RcclComm (RCCL inside
 # libprgpu); the CPU tests use comm.TorchComm (gloo).
 from .comm import RcclComm, TorchComm  # noqa: E402
 Comm = TorchComm
 
 
 def _seed_tasks(lr_map, lr_off, sr, sr_off, seed_opts, threads, comm):
-    """Tasks of the long reads this rank corrects (global ids), in the single run's order,
-    and the [lo, hi) long-read range it owns."""
+    """bwa-mode seeds of this rank's short reads (global ids; every short read on one rank)."""
     from . import exact_shard as ex, seed
     ix = seed.SeedIndex(lr_map, lr_off)
     try:
         if comm is None or comm.world == 1:
-            return ix.map(sr, sr_off, seed_opts, threads=threads), 0, len(lr_off) - 1
+            return ix.map(sr, sr_off, seed_opts, threads=threads)
         s, e = ex.sr_range(len(sr_off) - 1, comm.world, comm.rank)
         tk = ix.map(sr[sr_off[s]:sr_off[e]], sr_off[s:e + 1] - sr_off[s], seed_opts, threads=threads)
     finally:
         ix.close()
     tk["sr"] += s
+    return tk
+
+
+_ASC = np.frombuffer(b"ACGTN", np.uint8)
+
+
+def _records_by_owner(recs, sr, sr_off, lr_off, comm, bin_filter):
+    """Multi-rank layout: this rank's reported alignments (SAM order, read by read) go to the
+    owners of their long reads (one all-to-all of fixed fields + one of CIGAR ops); the owner
+    gets them source-rank-major, i.e. in the single run's read order, applies bwa-proovread's
+    -b/-l filter in that order and returns, per owned long read, its SAM lines in samtools
+    coordinate order (POS, strand, arrival)."""
+    from . import exact_shard as ex
+    from .bwa_proovread import BinFilter, aln_length
     b = ex.lr_bounds(lr_off, comm.world)
-    got = ex.group_by_lr(ex.exchange_tasks(tk, b, comm))
-    return got, int(b[comm.rank]), int(b[comm.rank + 1])
+    lo, hi = int(b[comm.rank]), int(b[comm.rank + 1])
+    fix = np.array([r[:6] + (len(r[6]),) for r in recs], np.int32).reshape(-1, 7)
+    own = np.searchsorted(b, fix[:, 1].astype(np.int64), side="right") - 1 if len(fix) else np.zeros(0, np.int64)
+    order = np.argsort(own, kind="stable")
+    counts = np.bincount(own, minlength=comm.world).astype(np.int64)
+    got = comm.alltoallv_rows(np.ascontiguousarray(fix[order]), counts)
+    cig = [np.asarray(recs[i][6], np.int32) for i in order]
+    cig_rows = np.concatenate(cig).reshape(-1, 1) if cig else np.zeros((0, 1), np.int32)
+    per_dst = np.zeros(comm.world, np.int64)
+    for k, i in enumerate(order):
+        per_dst[own[i]] += len(recs[i][6])
+    got_cig = comm.alltoallv_rows(np.ascontiguousarray(cig_rows, np.int32), per_dst).reshape(-1)
+    filt = BinFilter(*bin_filter) if bin_filter else None
+    per_lr = [[] for _ in range(hi - lo)]
+    c = 0
+    for k in range(len(got)):
+        srid, lr, strand, pos, score, flag, nc = (int(x) for x in got[k])
+        ops = got_cig[c:c + nc]
+        c += nc
+        q = sr[sr_off[srid]:sr_off[srid + 1]]
+        seq = (_ASC[np.where(q < 4, 3 - q, 4)][::-1] if strand else _ASC[q]).tobytes().decode()
+        cg = "".join(f"{int(x) >> 4}{'MIDNSHP=X'[int(x) & 15]}" for x in ops)
+        keep = filt.add(lr, pos + 1, aln_length(cg, len(q)), float(score)) if filt else None
+        per_lr[lr - lo].append((pos, strand, k, keep, f"sr{srid}\t{flag}\tlr{lr}\t{pos + 1}\t60\t{cg}\t*\t0\t0\t"
+                                                      f"{seq}\t*\tAS:i:{score}"))
+    out = []
+    for v in per_lr:
+        if filt is not None:
+            v = [x for x in v if filt.alive[x[3]]]
+        out.append([x[4] for x in sorted(v, key=lambda x: (x[0], x[1], x[2]))])
+    return out, lo, hi
 
 
 # ---------------------------------------------------------------------------- the loop
@@ -281,24 +352,25 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         ref_map = reads.seqs if finish else mapped     # finish maps to the unmasked .fq (proovread:838-850)
         lr_map, lr_off = reads.pool(ref_map)
         lr_map = NT4[lr_map]
-        tk, lo, hi = _seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], cfg.seed_threads, comm)
+        tk = _seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], cfg.seed_threads, comm)
         ent.n_tasks = int(len(tk))
-        if hi - lo < len(reads.ids):   # this rank's long reads only
-            tk = tk.copy()
-            tk["lr"] -= lo
-            lr_map = lr_map[lr_off[lo]:lr_off[hi]]
-            lr_off = lr_off[lo:hi + 1] - lr_off[lo]
-        d = _tasks_dataset(lr_map, lr_off, sr, sr_off, tk)
-        ids = reads.ids[lo:hi]
-        ref_seq, _ = reads.pool(reads.seqs[lo:hi])
-        ref_qual, _ = reads.pool(reads.quals[lo:hi])
+        d = _seeds_dataset(lr_map, lr_off, sr, sr_off, tk)
         max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541
         params = cns.CnsParams(coverage=max_cov, use_ref_qual=not finish, detect_chimera=finish,
                                max_ins_length=0)
         # bwa-proovread -b BIN -l BIN*min(cov, task cov) (proovread:1302-1313, cfg bin-size)
         bsz = T.bin_size(mode)
         binf = (bsz, bsz * min(cfg.coverage, task_cov)) if cfg.bin_filter else None
-        out = stages.iteration(d, ref_seq, ref_qual, task, params, bin_filter=binf) if hi > lo else []
+        if comm is None or comm.world == 1:
+            lo, hi = 0, len(reads.ids)
+            ref_seq, _ = reads.pool(reads.seqs)
+            ref_qual, _ = reads.pool(reads.quals)
+            out = stages.iteration(d, ref_seq, ref_qual, task, params, bin_filter=binf)
+        else:   # short-read shards -> alignments -> owners of the long reads -> consensus
+            sams, lo, hi = _records_by_owner(stages.align(d, task), sr, sr_off, lr_off, comm, binf)
+            out = stages.consensus([f"lr{i}" for i in range(lo, hi)], reads.seqs[lo:hi], reads.quals[lo:hi], sams,
+                                   params) if hi > lo else []
+        ids = reads.ids[lo:hi]
         seqs, quals, lines = [], [], []
         for i, (st, s, q, ch) in enumerate(out):
             if st != 0:

@@ -1,0 +1,467 @@
+// bwa mode's per-read logic (mem_chain2aln's walk, mem_sort_dedup_patch .. mem_reg2sam,
+// mem_patch_reg's global score): one implementation for the device kernels
+// (aln_kernels.hip, one lane per read) and the host build of the CPU tests
+// (tests/native/aln_host.cpp).  Restated from upstream bwa (>= 0.7.13) bwamem.c, klib
+// ksort.h's ks_introsort and bwa.c bwa_gen_cigar2 / ksw.c ksw_global2; bwa-proovread is an
+// absent submodule (.gitmodules:4-6), parity unpinned.
+#pragma once
+#include <stdint.h>
+
+#include "aln_dev.h"
+
+#if defined(__HIPCC__)
+#define AL_HD __host__ __device__ inline
+#else
+#define AL_HD inline
+#endif
+
+namespace prgpu {
+namespace alnc {
+
+AL_HD int cal_max_gap_a(const AlnDev &A, int qlen) {
+    int l_del = (int)((double)(qlen * A.a - A.o_del) / A.e_del + 1.);
+    int l_ins = (int)((double)(qlen * A.a - A.o_ins) / A.e_ins + 1.);
+    int l = l_del > l_ins ? l_del : l_ins;
+    l = l > 1 ? l : 1;
+    return l < A.w << 1 ? l : A.w << 1;
+}
+
+AL_HD int64_t fr_of(const AlnDev &A, int lr, int strand, int64_t x) {
+    const int64_t l_pac = A.lr_off[A.n_lr];
+    return strand ? l_pac + (l_pac - A.lr_off[lr + 1]) + x : A.lr_off[lr] + x;
+}
+
+AL_HD uint64_t hash_64(uint64_t key) {
+    key += ~(key << 32);
+    key ^= (key >> 22);
+    key += ~(key << 13);
+    key ^= (key >> 8);
+    key += (key << 3);
+    key ^= (key >> 15);
+    key += ~(key << 27);
+    key ^= (key >> 31);
+    return key;
+}
+
+// ---------------------------------------------------------------- klib ks_introsort
+// over an index array into the read's regions (the permutation klib's element moves make)
+struct LtEnd {   // alnreg_slt2 (mem_ars2)
+    AL_HD bool operator()(const AlnReg &a, const AlnReg &b) const { return a.re < b.re; }
+};
+struct LtScore {   // alnreg_slt (mem_ars)
+    AL_HD bool operator()(const AlnReg &a, const AlnReg &b) const {
+        return a.score > b.score || (a.score == b.score && (a.rb < b.rb || (a.rb == b.rb && a.qb < b.qb)));
+    }
+};
+struct LtHash {   // alnreg_hlt (mem_ars_hash)
+    AL_HD bool operator()(const AlnReg &a, const AlnReg &b) const {
+        return a.score > b.score || (a.score == b.score && a.hash < b.hash);
+    }
+};
+
+// klib ks_introsort (ksort.h as vendored by bwa) over an index array into the read's
+// regions, written with integer positions (the permutation klib's element moves make)
+template <class Lt>
+AL_HD void insertsort(int32_t *a, int s, int t, const AlnReg *R, Lt lt) {   // [s, t)
+    for (int i = s + 1; i < t; ++i)
+        for (int j = i; j > s && lt(R[a[j]], R[a[j - 1]]); --j) {
+            const int32_t x = a[j];
+            a[j] = a[j - 1];
+            a[j - 1] = x;
+        }
+}
+template <class Lt>
+AL_HD void combsort(int32_t *a, int s, int n, const AlnReg *R, Lt lt) {   // [s, s + n)
+    const double shrink_factor = 1.2473309501039786540366528676643;
+    int do_swap;
+    int gap = n;
+    do {
+        if (gap > 2) {
+            gap = (int)((double)gap / shrink_factor);
+            if (gap == 9 || gap == 10) gap = 11;
+        }
+        do_swap = 0;
+        for (int i = s; i < s + n - gap; ++i) {
+            const int j = i + gap;
+            if (lt(R[a[j]], R[a[i]])) {
+                const int32_t x = a[i];
+                a[i] = a[j];
+                a[j] = x;
+                do_swap = 1;
+            }
+        }
+    } while (do_swap || gap > 2);
+    if (gap != 1) insertsort(a, s, s + n, R, lt);
+}
+template <class Lt>
+AL_HD void introsort(int n, int32_t *a, const AlnReg *R, Lt lt) {
+    int st_l[64], st_r[64], st_d[64];
+    int top = 0, d;
+    if (n < 1) return;
+    if (n == 2) {
+        if (lt(R[a[1]], R[a[0]])) {
+            const int32_t x = a[0];
+            a[0] = a[1];
+            a[1] = x;
+        }
+        return;
+    }
+    for (d = 2; (1ll << d) < n; ++d) {}
+    int s = 0, t = n - 1;
+    d <<= 1;
+    for (;;) {
+        if (s < t) {
+            if (--d == 0) {
+                combsort(a, s, t - s + 1, R, lt);
+                t = s;
+                continue;
+            }
+            int i = s, j = t, k = i + ((j - i) >> 1) + 1;
+            if (lt(R[a[k]], R[a[i]])) {
+                if (lt(R[a[k]], R[a[j]])) k = j;
+            } else {
+                k = lt(R[a[j]], R[a[i]]) ? i : j;
+            }
+            const int32_t rp = a[k];
+            if (k != t) {
+                a[k] = a[t];
+                a[t] = rp;
+            }
+            for (;;) {
+                do ++i; while (lt(R[a[i]], R[rp]));
+                do --j; while (i <= j && lt(R[rp], R[a[j]]));
+                if (j <= i) break;
+                const int32_t x = a[i];
+                a[i] = a[j];
+                a[j] = x;
+            }
+            {
+                const int32_t x = a[i];
+                a[i] = a[t];
+                a[t] = x;
+            }
+            if (i - s > t - i) {
+                if (i - s > 16) {
+                    st_l[top] = s;
+                    st_r[top] = i - 1;
+                    st_d[top] = d;
+                    ++top;
+                }
+                s = t - i > 16 ? i + 1 : t;
+            } else {
+                if (t - i > 16) {
+                    st_l[top] = i + 1;
+                    st_r[top] = t;
+                    st_d[top] = d;
+                    ++top;
+                }
+                t = i - s > 16 ? s : i - 1;
+            }
+        } else {
+            if (top == 0) {
+                insertsort(a, 0, n, R, lt);
+                return;
+            }
+            --top;
+            s = st_l[top];
+            t = st_r[top];
+            d = st_d[top];
+        }
+    }
+}
+
+// mem_chain2aln for read r, resumed at its first open seed -> 1: an extension was requested
+AL_HD int aln_walk_read(const AlnDev &A, int64_t r) {
+    const int64_t s0 = A.seed_off[r], s1 = A.seed_off[r + 1];
+    int64_t k = A.resume[r];
+    if (k >= s1) return 0;
+    for (int64_t j = s0; j < s1; ++j)   // results of the last extension round
+        if (A.sel[j] & SEL_EXT) {
+            A.ext[j] = 1;
+            A.sel[j] = 0;
+        }
+    const int lq = (int)(A.sr_off[r + 1] - A.sr_off[r]);
+    int64_t c0 = k;   // first seed of k's chain
+    while (c0 > s0 && A.t_chain[c0 - 1] == A.t_chain[k]) --c0;
+    for (; k < s1; ++k) {
+        if (k > s0 && A.t_chain[k] != A.t_chain[k - 1]) c0 = k;
+        if (A.dec[k]) continue;
+        const int slr = A.t_lr[k], sst = A.t_strand[k];
+        const int64_t srb = A.t_rbeg[k];   // strand coordinates: regions compared on one strand only
+        const int sqb = A.t_qbeg[k], slen = A.t_slen[k];
+        bool around = false;
+        for (int64_t i = s0; i < k; ++i) {   // av: the regions made before this seed
+            if (A.dec[i] != 1) continue;
+            if (A.t_lr[i] != slr || A.t_strand[i] != sst) continue;   // other contig or strand: disjoint
+            const int pqb = A.o_qb[i], pqe = A.o_qe[i];
+            const int64_t prb = A.o_rb[i], pre = A.o_re[i];
+            if (srb < prb || srb + slen > pre || sqb < pqb || sqb + slen > pqe) continue;   // not contained
+            if ((double)(slen - A.t_slen[i]) > .1 * lq) continue;   // may give a better alignment
+            const int pw = A.o_w[i];
+            int64_t qd = sqb - pqb, rd = srb - prb;
+            int mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
+            int w = mg < pw ? mg : pw;
+            if (qd - rd < w && rd - qd < w) { around = true; break; }
+            qd = pqe - (sqb + slen);
+            rd = pre - (srb + slen);
+            mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
+            w = mg < pw ? mg : pw;
+            if (qd - rd < w && rd - qd < w) { around = true; break; }
+        }
+        if (around) {
+            bool other = false;   // a longer extended seed of the chain overlapping on another diagonal
+            for (int64_t j = c0; j < k; ++j) {
+                if (A.dec[j] != 1) continue;
+                const int tl = A.t_slen[j], tq = A.t_qbeg[j];
+                const int64_t tr = A.t_rbeg[j];
+                if (tl < slen * .95) continue;
+                if (sqb <= tq && sqb + slen - tq >= slen >> 2 && (int64_t)(tq - sqb) != tr - srb) { other = true; break; }
+                if (tq <= sqb && tq + tl - sqb >= slen >> 2 && (int64_t)(sqb - tq) != srb - tr) { other = true; break; }
+            }
+            if (!other) {
+                A.dec[k] = 2;
+                continue;
+            }
+        }
+        if (!A.ext[k]) {   // extension needed: request it, resume here next round
+            A.sel[k] = SEL_EXT;
+            A.resume[r] = (int32_t)k;
+            return 1;
+        }
+        A.dec[k] = 1;
+    }
+    A.resume[r] = (int32_t)s1;
+    return 0;
+}
+
+// the final pass of read r -> 0 done, 1: the global score of patch *req is needed first
+AL_HD int aln_final_read(const AlnDev &A, int64_t r, AlnPatch *req) {
+    if (A.fdone[r]) return 0;
+    const int64_t s0 = A.seed_off[r], s1 = A.seed_off[r + 1];
+    AlnReg *R = A.R + s0;
+    int32_t *ix = A.ix + s0;
+    int n = 0;
+    for (int64_t t = s0; t < s1; ++t) {
+        if (A.dec[t] != 1) continue;
+        AlnReg &g = R[n];
+        const int lr = A.t_lr[t], st = A.t_strand[t];
+        const int64_t base = fr_of(A, lr, st, 0);
+        g.rb = base + A.o_rb[t];
+        g.re = base + A.o_re[t];
+        g.qb = A.o_qb[t];
+        g.qe = A.o_qe[t];
+        g.score = A.o_score[t];
+        g.truesc = A.o_truesc[t];
+        g.w = A.o_w[t];
+        g.seedlen0 = A.t_slen[t];
+        g.lr = lr;
+        g.strand = st;
+        g.task = (int32_t)t;
+        g.secondary = -1;
+        g.patched = 0;
+        ix[n] = n;
+        ++n;
+    }
+    const int64_t l_pac = A.lr_off[A.n_lr];
+    int m_patch = 0;
+    if (n > 1) {
+        introsort(n, ix, R, LtEnd());
+        for (int i = 1; i < n; ++i) {
+            AlnReg &p = R[ix[i]];
+            const AlnReg &pv = R[ix[i - 1]];
+            if (p.lr != pv.lr || p.rb >= pv.re + A.max_chain_gap) continue;
+            for (int j = i - 1; j >= 0 && p.lr == R[ix[j]].lr && p.rb < R[ix[j]].re + A.max_chain_gap; --j) {
+                AlnReg &q = R[ix[j]];
+                if (q.qe == q.qb) continue;   // excluded
+                const int64_t orr = q.re - p.rb;
+                const int64_t oq = q.qb < p.qb ? q.qe - p.qb : p.qe - q.qb;
+                const int64_t mr = q.re - q.rb < p.re - p.rb ? q.re - q.rb : p.re - p.rb;
+                const int64_t mq = q.qe - q.qb < p.qe - p.qb ? q.qe - q.qb : p.qe - p.qb;
+                if (orr > A.mask_level_redun * mr && oq > A.mask_level_redun * mq) {   // one is redundant
+                    if (p.score < q.score) {
+                        p.qe = p.qb;
+                        break;
+                    }
+                    q.qe = q.qb;
+                    continue;
+                }
+                if (!(q.rb < p.rb)) continue;
+                // mem_patch_reg(q, p)
+                if (q.rb < l_pac && p.rb >= l_pac) continue;   // different strands
+                if (q.qb >= p.qb || q.qe >= p.qe || q.re >= p.re) continue;   // not colinear
+                int w = (int)((q.re - p.rb) - (q.qe - p.qb));
+                w = w > 0 ? w : -w;
+                double rr = (double)(q.re - p.rb) / (double)(p.re - q.rb) - (double)(q.qe - p.qb) / (double)(p.qe - q.qb);
+                rr = rr > 0. ? rr : -rr;
+                if (q.re < p.rb || q.qe < p.qb) {
+                    if (w > A.w << 1 || rr >= 0.05) continue;
+                } else if (w > A.w << 2 || rr >= 0.05 * 2) {
+                    continue;
+                }
+                w += q.w + p.w;
+                w = w < A.w << 2 ? w : A.w << 2;
+                int score;
+                if (m_patch < A.npk[r]) {
+                    score = A.pscore[s0 + m_patch];
+                } else {   // the global score is not known yet: request it, replay the read later
+                    const int64_t base = fr_of(A, q.lr, q.strand, 0);
+                    req->read = (int32_t)r;
+                    req->m = m_patch;
+                    req->lr = q.lr;
+                    req->strand = q.strand;
+                    req->qb = q.qb;
+                    req->qe = p.qe;
+                    req->rb = (int32_t)(q.rb - base);
+                    req->re = (int32_t)(p.re - base);
+                    req->w = w;
+                    req->pad = 0;
+                    return 1;
+                }
+                ++m_patch;
+                const int q_s = (int)((double)(p.qe - q.qb) / ((p.qe - p.qb) + (q.qe - q.qb)) * (p.score + q.score) + .5);
+                const int r_s = (int)((double)(p.re - q.rb) / (double)((p.re - p.rb) + (q.re - q.rb)) * (p.score + q.score) + .5);
+                if (score <= 0 || (double)score / (q_s > r_s ? q_s : r_s) < 0.90) continue;
+                p.qb = q.qb, p.rb = q.rb;
+                p.truesc = p.score = score;
+                p.w = w;
+                p.patched = 1;
+                q.qb = q.qe;
+            }
+        }
+        int m = 0;
+        for (int i = 0; i < n; ++i)
+            if (R[ix[i]].qe > R[ix[i]].qb) ix[m++] = ix[i];
+        n = m;
+        introsort(n, ix, R, LtScore());
+        for (int i = 1; i < n; ++i) {
+            AlnReg &a = R[ix[i]];
+            const AlnReg &b = R[ix[i - 1]];
+            if (a.score == b.score && a.rb == b.rb && a.qb == b.qb) a.qe = a.qb;
+        }
+        m = n > 0 ? 1 : 0;
+        for (int i = 1; i < n; ++i)
+            if (R[ix[i]].qe > R[ix[i]].qb) ix[m++] = ix[i];
+        n = m;
+    }
+    // mem_mark_primary_se
+    for (int i = 0; i < n; ++i) R[ix[i]].hash = hash_64((uint64_t)(A.read_id0 + r + i));
+    introsort(n, ix, R, LtHash());
+    // secondaries: a region overlapping an earlier primary (z of mem_mark_primary_se_core)
+    for (int i = 0; i < n; ++i) R[ix[i]].secondary = -1;
+    for (int i = 1; i < n; ++i) {
+        AlnReg &ai = R[ix[i]];
+        for (int j = 0; j < i; ++j) {   // the primaries before i, in order (z of mem_mark_primary_se_core)
+            const AlnReg &aj = R[ix[j]];
+            if (aj.secondary >= 0) continue;
+            const int b_max = aj.qb > ai.qb ? aj.qb : ai.qb;
+            const int e_min = aj.qe < ai.qe ? aj.qe : ai.qe;
+            if (e_min > b_max) {
+                const int min_l = ai.qe - ai.qb < aj.qe - aj.qb ? ai.qe - ai.qb : aj.qe - aj.qb;
+                if (e_min - b_max >= min_l * A.mask_level) {
+                    ai.secondary = j;
+                    break;
+                }
+            }
+        }
+    }
+    // mem_reg2sam: -T per aligned base, -D for secondaries; SAM order; mark for the CIGAR pass
+    for (int64_t t = s0; t < s1; ++t) {
+        A.sel[t] = 0;
+        A.o_pass[t] = 0;
+    }
+    int no = 0;
+    for (int k = 0; k < n; ++k) {
+        const AlnReg &p = R[ix[k]];
+        if (!((double)p.score >= A.min_score_per_base * (double)(p.qe - p.qb))) continue;
+        if (p.secondary >= 0 && p.score < R[ix[p.secondary]].score * A.drop_ratio) continue;
+        const int t = p.task;
+        const int64_t base = fr_of(A, p.lr, p.strand, 0);
+        A.o_qb[t] = p.qb;
+        A.o_rb[t] = (int32_t)(p.rb - base);
+        A.o_score[t] = p.score;
+        A.o_truesc[t] = p.truesc;
+        A.o_w[t] = p.w;
+        A.o_pass[t] = 1;
+        A.sel[t] = SEL_CIG;
+        A.olist[s0 + no] = t;
+        A.oflag[s0 + no] = (p.strand ? 0x10 : 0) | (p.secondary >= 0 ? 0x100 : (no > 0 ? 0x800 : 0));
+        ++no;
+    }
+    A.nout[r] = no;
+    A.fdone[r] = 1;
+    return 0;
+}
+
+// bwa_gen_cigar2 (score only) of patch P with the H/E row in pool[0, 2 * stride)
+AL_HD int aln_patch_score(const AlnDev &A, const AlnPatch &P, int32_t *pool, int64_t stride) {
+    const int r = P.read;
+    const uint8_t *Q = A.sr + A.sr_off[r] + P.qb;
+    const int lq = P.qe - P.qb;
+    const uint8_t *Lr = A.lr + A.lr_off[P.lr];
+    const int L = (int)(A.lr_off[P.lr + 1] - A.lr_off[P.lr]);
+    const int rlen = P.re - P.rb;
+    int score = 0;
+    auto qb_at = [&](int j) -> int {   // query, reversed on the reverse strand (indels leftmost)
+        return P.strand ? Q[lq - 1 - j] : Q[j];
+    };
+    auto rf_at = [&](int i) -> int {   // strand reference [rb, re), reversed on the reverse strand
+        const int x = P.strand ? P.re - 1 - i : P.rb + i;   // strand coordinate
+        if (!P.strand) return Lr[x];
+        const int c = Lr[L - 1 - x];
+        return c < 4 ? 3 - c : c;
+    };
+    auto sc = [&](int tb, int qb) -> int { return (tb > 3 || qb > 3) ? -1 : (tb == qb ? A.a : -A.b); };
+    if (lq > 0 && rlen > 0) {
+        if (lq == rlen && P.w == 0) {
+            for (int i = 0; i < lq; ++i) score += sc(rf_at(i), qb_at(i));
+        } else {
+            const int mn = lq < rlen ? lq : rlen;
+            const int max_ins = (int)((double)(mn * A.a - A.o_ins) / A.e_ins + 1.);
+            const int max_del = (int)((double)(mn * A.a - A.o_del) / A.e_del + 1.);
+            int max_gap = max_ins > max_del ? max_ins : max_del;
+            max_gap = max_gap > 1 ? max_gap : 1;
+            const int dl = rlen > lq ? rlen - lq : lq - rlen;
+            int w = (max_gap + dl + 1) >> 1;
+            w = w < P.w ? w : P.w;
+            w = w > dl + 3 ? w : dl + 3;
+            // ksw_global2, score path
+            constexpr int NEG = -0x40000000;
+            int32_t *H = pool, *E = pool + (stride >> 1);
+            const int oe_del = A.o_del + A.e_del, oe_ins = A.o_ins + A.e_ins;
+            H[0] = 0;
+            E[0] = NEG;
+            int j;
+            for (j = 1; j <= lq && j <= w; ++j) H[j] = -(A.o_ins + A.e_ins * j), E[j] = NEG;
+            for (; j <= lq; ++j) H[j] = E[j] = NEG;
+            for (int i = 0; i < rlen; ++i) {
+                int f = NEG, h1;
+                const int beg = i > w ? i - w : 0;
+                const int end = i + w + 1 < lq ? i + w + 1 : lq;
+                h1 = beg == 0 ? -(A.o_del + A.e_del * (i + 1)) : NEG;
+                const int tb = rf_at(i);
+                for (j = beg; j < end; ++j) {
+                    int mm = H[j], e = E[j];
+                    H[j] = h1;
+                    mm += sc(tb, qb_at(j));
+                    int h = mm >= e ? mm : e;
+                    h = h >= f ? h : f;
+                    h1 = h;
+                    int tt = mm - oe_del;
+                    e -= A.e_del;
+                    e = e > tt ? e : tt;
+                    E[j] = e;
+                    tt = mm - oe_ins;
+                    f -= A.e_ins;
+                    f = f > tt ? f : tt;
+                }
+                H[end] = h1;
+                E[end] = NEG;
+            }
+            score = H[lq];
+        }
+    }
+    return score;
+}
+
+}  // namespace alnc
+}  // namespace prgpu

@@ -1,0 +1,228 @@
+// bwa mode on the device: what `bwa-proovread mem` (bin/proovread:1313; absent submodule,
+// restated from upstream bwa >= 0.7.13 bwamem.c, parity unpinned) does with a short read
+// between seeding and SAM output, around the batched SW kernels (sw_kernels.hip):
+//
+//   aln_init_kernel   every chain's first seed (rank 0) is extended speculatively in the
+//                     first round (a contained rank-0 seed is later skipped and its result
+//                     dropped, so the speculation never changes an output)
+//   aln_walk_kernel   mem_chain2aln's loop, one lane per read, resumed every round: seeds in
+//                     chain order and srt order; a seed inside an earlier region ("around" it
+//                     within min(cal_max_gap, band)) is skipped unless a longer (>= 95 %)
+//                     extended seed of its chain overlaps it on another diagonal; a seed to
+//                     extend whose result is not there yet is requested for the next round and
+//                     the lane stops there (decisions before it are final: they only depend on
+//                     earlier seeds)
+//   aln_final_kernel  mem_sort_dedup_patch (klib introsort by end, redundant hits, colinear
+//                     merges through mem_patch_reg whose global scores come from
+//                     aln_patch_kernel in extra rounds), the (score, rb, qb) sort with identical
+//                     hits removed, mem_mark_primary_se (score, hash_64(read_id + i)) and
+//                     mem_reg2sam's -T (per aligned base, proovread cfg:324) and -D filters;
+//                     writes the reported alignments in SAM order and marks them for the CIGAR
+//                     pass (SEL_CIG)
+// One lane per read: the per-read work is a few dozen sequential decisions over
+// HBM-resident scratch (latency-bound bookkeeping, no roofline claim).
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "aln_core.h"
+
+namespace prgpu {
+
+using namespace alnc;
+
+// ---------------------------------------------------------------- round 0
+__global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < A.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+        // rank-0 seeds: the first seed of a chain (seeds grouped by read, then chain)
+        const bool first = t == 0 || A.t_sr[t] != A.t_sr[t - 1] || A.t_chain[t] != A.t_chain[t - 1];
+        A.sel[t] = first ? SEL_EXT : 0;
+        A.ext[t] = 0;
+        A.dec[t] = 0;
+    }
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < A.n_sr; r += (int64_t)gridDim.x * blockDim.x) {
+        A.resume[r] = (int32_t)A.seed_off[r];
+        A.npk[r] = 0;
+        A.fdone[r] = 0;
+        A.nout[r] = 0;
+    }
+}
+
+// ---------------------------------------------------------------- mem_chain2aln
+__global__ void __launch_bounds__(256) aln_walk_kernel(AlnDev A) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < A.n_sr && aln_walk_read(A, r)) atomicAdd(&A.counter[0], 1);
+}
+
+__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n_sr) return;
+    AlnPatch req;
+    if (aln_final_read(A, r, &req)) {   // a patch score is needed: the read is replayed later
+        const int slot = atomicAdd(&A.counter[1], 1);
+        if (slot < A.preq_cap) A.preq[slot] = req;
+    }
+}
+
+__global__ void __launch_bounds__(64) aln_patch_kernel(AlnDev A, int n_req, int32_t *pool, int64_t stride) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_req) return;
+    const AlnPatch P = A.preq[k];
+    A.pscore[A.seed_off[P.read] + P.m] = aln_patch_score(A, P, pool + (int64_t)k * stride, stride);
+    A.npk[P.read] = P.m + 1;
+}
+
+// ---------------------------------------------------------------- outputs
+__global__ void __launch_bounds__(256) aln_slot_kernel(AlnDev A, int64_t *slot) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < A.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+        int64_t v = 0;
+        if (A.sel[t] & SEL_CIG) {
+            const int64_t r = A.t_sr[t];
+            v = cig_slot_ops((int)(A.sr_off[r + 1] - A.sr_off[r]));
+        }
+        slot[t] = v;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) slot[A.n_task] = 0;
+}
+__global__ void __launch_bounds__(256) aln_nout64_kernel(const int32_t *nout, int64_t n, int64_t *o) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= n; r += (int64_t)gridDim.x * blockDim.x)
+        o[r] = r < n ? nout[r] : 0;
+}
+__global__ void __launch_bounds__(256) aln_compact_kernel(AlnDev A, const int64_t *aoff, int32_t *alist, int32_t *aflag) {
+    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < A.n_sr; r += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s0 = A.seed_off[r], o = aoff[r];
+        const int n = A.nout[r];
+        for (int i = 0; i < n; ++i) {
+            alist[o + i] = A.olist[s0 + i];
+            aflag[o + i] = A.oflag[s0 + i];
+        }
+    }
+}
+__global__ void __launch_bounds__(256) aln_key_kernel(const int32_t *alist, const int32_t *t_lr, int64_t n, int32_t *key,
+                                                      int32_t *cnt) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t lr = t_lr[alist[i]];
+        key[i] = lr;
+        atomicAdd(&cnt[lr], 1);
+    }
+}
+__global__ void __launch_bounds__(256) aln_cnt64_kernel(const int32_t *cnt, int32_t n, int64_t *o) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x)
+        o[i] = i < n ? cnt[i] : 0;
+}
+
+__global__ void __launch_bounds__(256) sw_gather_kernel(SwGather G) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < G.n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t t = G.list[i];
+        if (G.o_sr) G.o_sr[i] = G.t_sr[t];
+        if (G.o_lr) G.o_lr[i] = G.t_lr[t];
+        if (G.o_task) G.o_task[i] = t;
+        if (G.o_status) G.o_status[i] = G.status[t];
+        if (G.o_pos) G.o_pos[i] = G.pos[t];
+        if (G.o_score) G.o_score[i] = G.score[t];
+        if (G.o_ncig) G.o_ncig[i] = G.ncig[t];
+        if (G.o_qb) G.o_qb[i] = G.qb[t];
+        if (G.o_qe) G.o_qe[i] = G.qe[t];
+        if (G.o_rb) G.o_rb[i] = G.rb[t];
+        if (G.o_re) G.o_re[i] = G.re[t];
+        if (G.o_truesc) G.o_truesc[i] = G.truesc[t];
+        if (G.o_strand) G.o_strand[i] = G.strand[t];
+        if (G.o_pass) G.o_pass[i] = G.pass[t];
+        if (G.o_cig_at) G.o_cig_at[i] = G.cig_at[t];
+    }
+}
+
+static int grid_of(int64_t n, int cap = 8192) {
+    int64_t g = (n + 255) / 256;
+    return (int)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+int aln_launch_init(const AlnDev &A, void *stream) {
+    const int64_t n = A.n_task > A.n_sr ? A.n_task : A.n_sr;
+    hipLaunchKernelGGL(aln_init_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, A);
+    return (int)hipGetLastError();
+}
+int aln_launch_walk(const AlnDev &A, void *stream) {
+    if (A.n_sr <= 0) return 0;
+    hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+    return (int)hipGetLastError();
+}
+int aln_launch_final(const AlnDev &A, void *stream) {
+    if (A.n_sr <= 0) return 0;
+    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+    return (int)hipGetLastError();
+}
+int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, void *stream) {
+    if (n_req <= 0) return 0;
+    hipLaunchKernelGGL(aln_patch_kernel, dim3((unsigned)((n_req + 63) / 64)), dim3(64), 0, (hipStream_t)stream, A, n_req,
+                       pool, stride);
+    return (int)hipGetLastError();
+}
+
+int sw_launch_gather(const SwGather &G, void *stream) {
+    if (G.n <= 0) return 0;
+    hipLaunchKernelGGL(sw_gather_kernel, dim3(grid_of(G.n)), dim3(256), 0, (hipStream_t)stream, G);
+    return (int)hipGetLastError();
+}
+
+size_t aln_scan_temp_bytes(int64_t n) {
+    size_t a = 0;
+    (void)rocprim::exclusive_scan(nullptr, a, (int64_t *)nullptr, (int64_t *)nullptr, (int64_t)0, (size_t)n + 1,
+                                  rocprim::plus<int64_t>(), (hipStream_t)0);
+    return a;
+}
+int aln_launch_cig_slots(const AlnDev &A, int64_t *slot, int64_t *tmp_in, void *temp, size_t temp_bytes,
+                         void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(aln_slot_kernel, dim3(grid_of(A.n_task + 1)), dim3(256), 0, s, A, tmp_in);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    size_t tb = temp_bytes;
+    e = rocprim::exclusive_scan(temp, tb, tmp_in, slot, (int64_t)0, (size_t)A.n_task + 1, rocprim::plus<int64_t>(), s);
+    return (int)e;
+}
+int aln_launch_compact(const AlnDev &A, int64_t *aoff, int64_t *tmp_in, int32_t *alist, int32_t *aflag, void *temp,
+                       size_t temp_bytes, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(aln_nout64_kernel, dim3(grid_of(A.n_sr + 1)), dim3(256), 0, s, A.nout, (int64_t)A.n_sr, tmp_in);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    size_t tb = temp_bytes;
+    if ((e = rocprim::exclusive_scan(temp, tb, tmp_in, aoff, (int64_t)0, (size_t)A.n_sr + 1, rocprim::plus<int64_t>(),
+                                     s)) != hipSuccess)
+        return (int)e;
+    if (A.n_sr > 0) hipLaunchKernelGGL(aln_compact_kernel, dim3(grid_of(A.n_sr)), dim3(256), 0, s, A, aoff, alist, aflag);
+    return (int)hipGetLastError();
+}
+
+size_t aln_group_temp_bytes(int64_t n, int32_t n_lr) {
+    size_t a = 0, b = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, a, (int32_t *)nullptr, (int32_t *)nullptr, (int32_t *)nullptr,
+                                    (int32_t *)nullptr, (size_t)(n > 0 ? n : 1), 0, 32, (hipStream_t)0);
+    (void)rocprim::exclusive_scan(nullptr, b, (int64_t *)nullptr, (int64_t *)nullptr, (int64_t)0, (size_t)n_lr + 1,
+                                  rocprim::plus<int64_t>(), (hipStream_t)0);
+    return a > b ? a : b;
+}
+int aln_launch_group_lr(const int32_t *alist, const int32_t *t_lr, int64_t n, int32_t n_lr, int32_t *key0, int32_t *key1,
+                        int32_t *out_list, int32_t *cnt, int64_t *lr_off, int64_t *tmp_in, void *temp,
+                        size_t temp_bytes, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = hipMemsetAsync(cnt, 0, (size_t)(n_lr + 1) * 4, s);
+    if (e != hipSuccess) return (int)e;
+    if (n > 0) {
+        hipLaunchKernelGGL(aln_key_kernel, dim3(grid_of(n)), dim3(256), 0, s, alist, t_lr, n, key0, cnt);
+        if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+        int bits = 1;
+        while (bits < 31 && (1 << bits) < n_lr) ++bits;
+        size_t tb = temp_bytes;   // LSD radix sort: stable, so a long read's alignments stay in read order
+        if ((e = rocprim::radix_sort_pairs(temp, tb, key0, key1, alist, out_list, (size_t)n, 0, bits, s)) != hipSuccess)
+            return (int)e;
+    }
+    hipLaunchKernelGGL(aln_cnt64_kernel, dim3(grid_of((int64_t)n_lr + 1)), dim3(256), 0, s, cnt, n_lr, tmp_in);
+    if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    size_t tb = temp_bytes;
+    return (int)rocprim::exclusive_scan(temp, tb, tmp_in, lr_off, (int64_t)0, (size_t)n_lr + 1, rocprim::plus<int64_t>(), s);
+}
+
+}  // namespace prgpu

@@ -21,6 +21,7 @@
 
 using namespace prgpu;
 int sw_get_ptrs(pr_ctx *c, SwPtrs *p);
+int sw_get_pipe_ptrs(pr_ctx *c, SwPtrs *p, bool regroup);
 
 static thread_local std::string g_err;
 static int set_error(int code, const char *fmt, ...) {
@@ -537,10 +538,11 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
     if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
     const pr_sw_batch &sb = b->sw;
     const int n = sb.n_lr;
-    if (!b->task_lr_off || b->task_lr_off[0] != 0 || b->task_lr_off[n] != sb.n_task)
+    const bool bwa = sb.t_chain != nullptr;   // seeds in, alignments grouped by long read on the device
+    if (!bwa && (!b->task_lr_off || b->task_lr_off[0] != 0 || b->task_lr_off[n] != sb.n_task))
         return set_error(PR_ERR_ARG, "task_lr_off must partition the tasks");
     int maxt = 1;
-    for (int i = 0; i < n; ++i) {
+    for (int i = 0; i < n && !bwa; ++i) {
         if (b->task_lr_off[i + 1] < b->task_lr_off[i]) return set_error(PR_ERR_ARG, "task_lr_off not monotone");
         for (int64_t t = b->task_lr_off[i]; t < b->task_lr_off[i + 1]; ++t)
             if (sb.t_lr[t] != i) return set_error(PR_ERR_ARG, "tasks must be grouped by long read");
@@ -582,7 +584,7 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
     if ((rc = upload(B[CB_LR_OFF], sb.lr_off, n1, s))) return rc;
     if (b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)sb.lr_off[n], s))) return rc;
     if (b->ref_seq && (rc = upload(B[CB_REF_SEQ], b->ref_seq, (size_t)sb.lr_off[n], s))) return rc;
-    if ((rc = upload(c->pb[0], b->task_lr_off, n1, s))) return rc;
+    if (!bwa && (rc = upload(c->pb[0], b->task_lr_off, n1, s))) return rc;
     if ((rc = c->pb[1].ensure(n1 * 4)) || (rc = c->pb[2].ensure(n1 * 4))) return rc;
     if ((rc = B[CB_ALN_OFF].ensure(n1 * 8)) || (rc = B[CB_POS].ensure(na1 * 4)) ||
         (rc = B[CB_SCORE].ensure(na1 * 8)) || (rc = B[CB_AFLAGS].ensure(na1)) ||
@@ -620,13 +622,21 @@ extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_param
     int rc = pr_sw_launch(c, o);   // records ev[2], ev[3], ev[0]
     if (rc) return rc;
     SwPtrs sp;
-    if ((rc = sw_get_ptrs(c, &sp))) return rc;
+    if ((rc = sw_get_pipe_ptrs(c, &sp, true))) return rc;
+    if (sp.task_off) {   // bwa mode: the reported alignments grouped by long read on the device
+        if (sp.max_per_lr > 16384)
+            return set_error(PR_ERR_CAPACITY, "more than 16384 alignments on one long read (%d)", sp.max_per_lr);
+        c->k_need = sp.max_per_lr > 1 ? sp.max_per_lr : 1;
+        int sc = 1;
+        while (sc < c->k_need) sc <<= 1;
+        c->pipe_sort_cap = sc;
+    }
     DevBuf *B = c->cb;
     PipeDev P;
     P.n_lr = c->n_lr;
     P.sort_cap = c->pipe_sort_cap;
     P.cig_at = sp.cig_at;
-    P.task_off = c->pb[0].as<int64_t>();
+    P.task_off = sp.task_off ? sp.task_off : c->pb[0].as<int64_t>();
     P.t_sr = sp.t_sr;
     P.strand = sp.strand;
     P.pass = sp.pass;

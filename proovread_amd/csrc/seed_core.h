@@ -13,8 +13,10 @@
 //                     test_and_merge or opening a new chain after the chains of
 //                     equal pos (the btree order)
 //   mem_chain_flt     chain weight, -W minimum, stable sort, -D / mask_level
-//   mem_chain2aln     the chain's best seed (longest, last on ties) and the
-//                     chain's reference window (cal_max_gap over its seeds)
+//   mem_chain2aln     its input: every seed of every kept chain in the order it
+//                     tries them (longest first, last on ties) with the chain's
+//                     reference window (cal_max_gap over its seeds); the
+//                     extension and the containment test run on the device
 // Occurrence counts come from a per-read table: for every start a, the hits of
 // the 12-mer q[a, a+12) with their exact match length ml = LCP(q[a..], T[p..]);
 // occ(q[a, b)) = #{hits of a with ml >= b - a} (a per-start count table for
@@ -549,16 +551,13 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         for (int k = 0; k < nk; ++k)
             if (S.ch[S.kept[k]].first >= 0) S.ch[S.ch[S.kept[k]].first].kept = 1;
     }
-    // mem_chain2aln: the best seed of every kept chain and the chain's reference window
-    int no = 0;
+    // mem_chain2aln's input: every seed of every kept chain with the chain's reference window,
+    // seeds in the order mem_chain2aln tries them (srt: score = length, larger index first on ties)
+    int no = 0, nkept = 0;
     for (int ci = 0; ci < nch; ++ci) {
         const Chain &c = S.ch[ci];
         if (c.kept == 0) continue;
-        int32_t best = c.head;
-        for (int32_t k = S.next[c.head]; k >= 0; k = S.next[k])
-            if (S.seeds[k].len >= S.seeds[best].len) best = k;   // srt order: (score, index), last wins
-        const Seed &s = S.seeds[best];
-        const bool rev = s.rbeg >= I.l_pac;
+        const bool rev = S.seeds[c.head].rbeg >= I.l_pac;
         const int64_t L = I.lr_off[c.rid + 1] - I.lr_off[c.rid];
         const int64_t cs = rev ? I.l_pac + (I.l_pac - I.lr_off[c.rid + 1]) : I.lr_off[c.rid];
         int64_t r0 = INT64_MAX, r1 = INT64_MIN;
@@ -571,18 +570,32 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         }
         r0 -= cs;
         r1 -= cs;
-        if (no >= cap_out) return SC_OVER_OUT;
-        pr_seed_task &t = out[no++];
-        t.sr = sid;
-        t.lr = c.rid;
-        t.strand = rev ? 1 : 0;
-        t.qbeg = s.qbeg;
-        t.rbeg = (int32_t)(s.rbeg - cs);
-        t.slen = s.len;
-        t.rmax0 = (int32_t)(r0 > 0 ? r0 : 0);
-        t.rmax1 = (int32_t)(r1 < L ? r1 : L);
-        t.weight = c.w;
-        t.nseed = c.n;
+        if (no + c.n > cap_out) return SC_OVER_OUT;
+        const int first = no;
+        int idx = 0;
+        for (int32_t k = c.head; k >= 0; k = S.next[k], ++idx) {
+            const Seed &s = S.seeds[k];
+            pr_seed_task &t = out[no];
+            t.sr = sid;
+            t.lr = c.rid;
+            t.strand = rev ? 1 : 0;
+            t.qbeg = s.qbeg;
+            t.rbeg = (int32_t)(s.rbeg - cs);
+            t.slen = s.len;
+            t.rmax0 = (int32_t)(r0 > 0 ? r0 : 0);
+            t.rmax1 = (int32_t)(r1 < L ? r1 : L);
+            t.chain = nkept;
+            t.rank = idx;   // insertion index until the sort below
+            // insertion sort by (length, index) descending
+            int j = no - 1;
+            while (j >= first && (out[j].slen < t.slen || (out[j].slen == t.slen && out[j].rank < t.rank))) --j;
+            const pr_seed_task v = t;
+            for (int m = no; m > j + 1; --m) out[m] = out[m - 1];
+            out[j + 1] = v;
+            ++no;
+        }
+        for (int m = first; m < no; ++m) out[m].rank = m - first;
+        ++nkept;
     }
     *n_out = no;
     SC_TICK(2);
@@ -610,7 +623,7 @@ namespace seedc {
 struct Caps {
     int32_t lmax, hits, iv, mems, seeds, chains, out;
 };
-SC_HD Caps device_caps() { return Caps{1024, 8192, 256, 1024, 4096, 2048, 128}; }
+SC_HD Caps device_caps() { return Caps{1024, 8192, 256, 1024, 4096, 2048, 384}; }
 
 SC_HD int64_t align8(int64_t x) { return (x + 7) & ~(int64_t)7; }
 

@@ -1,11 +1,13 @@
 // Host side of the SW stage C-ABI (include/prgpu.h pr_sw_*).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "../../include/prgpu.h"
+#include "aln_dev.h"
 #include "sw_dev.h"
 #include "sw_pk.h"
 
@@ -49,10 +51,17 @@ static const int SB_EHG = 32;       // HBM DP rows of the general CIGAR kernel (
 static const int SB_CIGOFF = 33;    // pr_sw_download compaction: prefix of ncigar
 static const int SB_CIGOUT = 34;    //                            compacted ops
 static const size_t SPILL_OFF = 96;   // in the SB_CELLS buffer: 3 x u64 overflow counters
+// bwa mode (aln_kernels.hip)
+enum AlnBuf {
+    SB_CHAIN = 35, SB_SEEDOFF, SB_SEL, SB_EXTF, SB_DEC, SB_RESUME, SB_ACNT, SB_AREG, SB_AIX, SB_PSCORE, SB_NPK,
+    SB_FDONE, SB_PREQ, SB_NOUT, SB_OLIST, SB_OFLAG, SB_ATEMP, SB_AOFF, SB_ALIST, SB_AFLAG, SB_PPOOL, SB_GLIST,
+    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_NBUF
+};
+static_assert(SB_NBUF <= 64, "SwResident buffer table");
 
 namespace prgpu {
 void sw_release(SwResident &r) {
-    for (int i = 0; i < 40; ++i) {
+    for (int i = 0; i < 64; ++i) {
         if (r.buf[i]) (void)hipFree(r.buf[i]);
         r.buf[i] = nullptr;
         r.cap[i] = 0;
@@ -82,6 +91,10 @@ static int up(SwResident &r, int id, const T *h, size_t n, hipStream_t s) {
 extern "C" void pr_sw_opts_default(pr_sw_opts *o, int finish) {
     o->bin_size = 0;
     o->bin_length = 0.0;
+    o->drop_ratio = finish ? 0.75 : 0.0;   // -D (proovread.cfg:325 / 332)
+    o->mask_level = 0.5;
+    o->mask_level_redun = 0.95;
+    o->max_chain_gap = 10000;
     o->a = 5;
     o->pen_clip5 = o->pen_clip3 = 30;
     o->zdrop = 100;
@@ -120,6 +133,21 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
             return pr_set_error(PR_ERR_ARG, "seed outside its reads");
     }
     const int64_t nt = b->n_task;
+    const bool bwa = b->t_chain != nullptr;
+    std::vector<int64_t> seed_off;
+    if (bwa) {   // seeds grouped by short read, then chain
+        if (nt >= (int64_t)1 << 31) return pr_set_error(PR_ERR_CAPACITY, "more than 2^31 seeds in one batch");
+        seed_off.assign((size_t)b->n_sr + 1, 0);
+        for (int64_t t = 0; t < nt; ++t) {
+            if (t && (b->t_sr[t] < b->t_sr[t - 1] || (b->t_sr[t] == b->t_sr[t - 1] && b->t_chain[t] < b->t_chain[t - 1])))
+                return pr_set_error(PR_ERR_ARG, "bwa mode: seeds must be grouped by short read, then chain");
+            ++seed_off[(size_t)b->t_sr[t] + 1];
+        }
+        for (int i = 0; i < b->n_sr; ++i) seed_off[(size_t)i + 1] += seed_off[(size_t)i];
+        r.n_rank0 = 0;
+        for (int64_t t = 0; t < nt; ++t)
+            r.n_rank0 += (t == 0 || b->t_sr[t] != b->t_sr[t - 1] || b->t_chain[t] != b->t_chain[t - 1]) ? 1 : 0;
+    }
     int rc;
     if ((rc = up(r, SB_SR, b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
         (rc = up(r, SB_SR_OFF, b->sr_off, (size_t)b->n_sr + 1, s)) ||
@@ -136,6 +164,34 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
         (rc = ensure(r, SB_X, (size_t)(nt + 1) * 4 * 12)) || (rc = ensure(r, SB_XTRY, (size_t)nt + 1)) ||
         (rc = ensure(r, SB_LIST, (size_t)(nt + 1 + (int64_t)PK_NB * PK_SEG) * 4)))
         return rc;
+    r.bwa = bwa;
+    r.read_id0 = b->read_id0;
+    r.n_aln = 0;
+    if (bwa) {
+        const size_t n1 = (size_t)nt + 1, r1 = (size_t)b->n_sr + 1;
+        if ((rc = up(r, SB_CHAIN, b->t_chain, (size_t)nt, s)) || (rc = up(r, SB_SEEDOFF, seed_off.data(), r1, s)) ||
+            (rc = ensure(r, SB_SEL, n1)) || (rc = ensure(r, SB_EXTF, n1)) || (rc = ensure(r, SB_DEC, n1)) ||
+            (rc = ensure(r, SB_RESUME, r1 * 4)) || (rc = ensure(r, SB_ACNT, 64)) ||
+            (rc = ensure(r, SB_AREG, n1 * sizeof(AlnReg))) || (rc = ensure(r, SB_AIX, n1 * 4)) ||
+            (rc = ensure(r, SB_PSCORE, n1 * 4)) || (rc = ensure(r, SB_NPK, r1 * 4)) || (rc = ensure(r, SB_FDONE, r1)) ||
+            (rc = ensure(r, SB_NOUT, r1 * 4)) || (rc = ensure(r, SB_OLIST, n1 * 4)) || (rc = ensure(r, SB_OFLAG, n1 * 4)) ||
+            (rc = ensure(r, SB_AOFF, r1 * 8)) || (rc = ensure(r, SB_ALIST, n1 * 4)) || (rc = ensure(r, SB_AFLAG, n1 * 4)) ||
+            (rc = ensure(r, SB_PREQ, 1024 * sizeof(AlnPatch))) || (rc = ensure(r, SB_CIGSLOT, n1 * 8)) ||
+            (rc = ensure(r, SB_CIGAT, n1 * 8)) || (rc = ensure(r, SB_PASS, n1)) || (rc = ensure(r, SB_CELLS, CELLS_BYTES)))
+            return rc;
+        size_t tb = aln_scan_temp_bytes(nt);
+        tb = std::max(tb, aln_scan_temp_bytes(b->n_sr));
+        tb = std::max(tb, aln_group_temp_bytes(nt, b->n_lr));
+        if ((rc = ensure(r, SB_ATEMP, tb))) return rc;
+        r.cig_slots = 0;
+        HIPCHK(hipStreamSynchronize(s));
+        r.loaded = true;
+        r.n_task = nt;
+        r.n_sr = b->n_sr;
+        r.n_lr = b->n_lr;
+        r.qmax = qmax;
+        return 0;
+    }
     // CIGAR slots sized from the short-read lengths, plus a spill reserve for overflows
     // (PRGPU_SW_CIG_SLOT: a fixed slot size, a test hook that sends CIGARs to the overflow pass)
     std::vector<int64_t> slot((size_t)nt + 1, 0);
@@ -158,6 +214,159 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
     r.n_sr = b->n_sr;
     r.n_lr = b->n_lr;
     r.qmax = qmax;
+    return 0;
+}
+
+static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {
+    AlnDev A;
+    std::memset(&A, 0, sizeof A);
+    A.n_task = r.n_task;
+    A.n_sr = (int32_t)r.n_sr;
+    A.n_lr = (int32_t)r.n_lr;
+    A.read_id0 = r.read_id0;
+    A.seed_off = (const int64_t *)r.buf[SB_SEEDOFF];
+    A.t_sr = D.t_sr;
+    A.t_lr = D.t_lr;
+    A.t_qbeg = D.t_qbeg;
+    A.t_rbeg = D.t_rbeg;
+    A.t_slen = D.t_slen;
+    A.t_chain = (const int32_t *)r.buf[SB_CHAIN];
+    A.t_strand = D.t_strand;
+    A.sr_off = D.sr_off;
+    A.lr_off = D.lr_off;
+    A.sr = D.sr;
+    A.lr = D.lr;
+    A.o_qb = D.o_qb; A.o_qe = D.o_qe; A.o_rb = D.o_rb; A.o_re = D.o_re;
+    A.o_score = D.o_score; A.o_truesc = D.o_truesc; A.o_w = D.o_w;
+    A.o_pass = D.o_pass;
+    A.sel = (uint8_t *)r.buf[SB_SEL];
+    A.ext = (uint8_t *)r.buf[SB_EXTF];
+    A.dec = (uint8_t *)r.buf[SB_DEC];
+    A.resume = (int32_t *)r.buf[SB_RESUME];
+    A.counter = (int32_t *)r.buf[SB_ACNT];
+    A.R = (AlnReg *)r.buf[SB_AREG];
+    A.ix = (int32_t *)r.buf[SB_AIX];
+    A.pscore = (int32_t *)r.buf[SB_PSCORE];
+    A.npk = (int32_t *)r.buf[SB_NPK];
+    A.fdone = (uint8_t *)r.buf[SB_FDONE];
+    A.preq = (AlnPatch *)r.buf[SB_PREQ];
+    A.preq_cap = (int32_t)(r.cap[SB_PREQ] / sizeof(AlnPatch));
+    A.nout = (int32_t *)r.buf[SB_NOUT];
+    A.olist = (int32_t *)r.buf[SB_OLIST];
+    A.oflag = (int32_t *)r.buf[SB_OFLAG];
+    A.a = o->a; A.b = o->b; A.o_del = o->o_del; A.e_del = o->e_del; A.o_ins = o->o_ins; A.e_ins = o->e_ins;
+    A.w = o->w;
+    A.max_chain_gap = o->max_chain_gap;
+    A.min_score_per_base = o->min_score_per_base;
+    A.drop_ratio = o->drop_ratio;
+    A.mask_level = o->mask_level;
+    A.mask_level_redun = o->mask_level_redun;
+    return A;
+}
+
+// bwa mode: extension rounds (mem_chain2aln), the final pass (mem_sort_dedup_patch ..
+// mem_reg2sam) with mem_patch_reg rounds, then the CIGAR pass over the reported alignments
+static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, const pr_sw_opts *o, int grid_w,
+                      int grid_pk, int grid_g, int lds_glob) {
+    hipStream_t s = ctx_stream(c);
+    int rc, e;
+    D.sel = (const uint8_t *)r.buf[SB_SEL];
+    AlnDev A = aln_dev(r, D, o);
+    r.ext_rounds = 0;
+    r.n_ext = r.n_rank0;   // rank-0 seeds, extended in the first round
+    r.n_patch = 0;
+    r.n_aln = 0;
+    HIPCHK(hipEventRecord(ctx_event(c, 2), s));
+    if ((e = aln_launch_init(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    int32_t cnt[4] = {0, 0, 0, 0};
+    for (;;) {   // mem_chain2aln: every round extends the requested seeds, the walk resumes
+        HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
+        if (r.n_task) {
+            e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s);
+            if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        }
+        if ((e = aln_launch_walk(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipMemcpyAsync(cnt, A.counter, 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        ++r.ext_rounds;
+        r.n_ext += cnt[0];
+        if (getenv("PRGPU_BWA_DEBUG")) fprintf(stderr, "[bwa] round %d: %d requests\n", r.ext_rounds, cnt[0]);
+        if (cnt[0] == 0) break;
+        if (r.ext_rounds > r.n_task + 2) return pr_set_error(PR_ERR_HIP, "bwa mode: extension rounds do not converge");
+    }
+    for (int round = 0;; ++round) {   // final pass; mem_patch_reg global scores in extra rounds
+        HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
+        if ((e = aln_launch_final(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipMemcpyAsync(cnt, A.counter, 16, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (getenv("PRGPU_BWA_DEBUG")) fprintf(stderr, "[bwa] final round %d: %d patch requests\n", round, cnt[1]);
+        if (cnt[1] == 0) break;
+        if (round > r.n_task + 2) return pr_set_error(PR_ERR_HIP, "bwa mode: patch rounds do not converge");
+        const int n_req = cnt[1] < A.preq_cap ? cnt[1] : A.preq_cap;
+        const int64_t stride = 2 * ((int64_t)r.qmax + 2);
+        if ((rc = ensure(r, SB_PPOOL, (size_t)n_req * (size_t)stride * 4))) return rc;
+        if ((e = aln_launch_patch(A, n_req, (int32_t *)r.buf[SB_PPOOL], stride, (void *)s)))
+            return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        r.n_patch += n_req;
+        if (cnt[1] > A.preq_cap) {   // requests beyond the list are made again next round
+            HIPCHK(hipStreamSynchronize(s));
+            if ((rc = ensure(r, SB_PREQ, (size_t)cnt[1] * sizeof(AlnPatch)))) return rc;
+            A.preq = (AlnPatch *)r.buf[SB_PREQ];
+            A.preq_cap = (int32_t)(r.cap[SB_PREQ] / sizeof(AlnPatch));
+        }
+    }
+    // CIGAR slots of the reported alignments, the pool, then the CIGAR pass over them
+    {
+        const int64_t nmax = (r.n_task > r.n_sr ? r.n_task : r.n_sr) + 1;
+        if ((rc = ensure(r, SB_SCANIN, (size_t)nmax * 8))) return rc;
+    }
+    if (getenv("PRGPU_BWA_DEBUG"))
+        fprintf(stderr, "[bwa] rounds %d, extended %lld, patches %lld\n", r.ext_rounds, (long long)r.n_ext,
+                (long long)r.n_patch);
+    if ((e = aln_launch_cig_slots(A, (int64_t *)r.buf[SB_CIGSLOT], (int64_t *)r.buf[SB_SCANIN], r.buf[SB_ATEMP],
+                                  r.cap[SB_ATEMP], (void *)s)))
+        return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    int64_t slots = 0;
+    HIPCHK(hipMemcpyAsync(&slots, (int64_t *)r.buf[SB_CIGSLOT] + r.n_task, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t reserve = slots / 16 > (1 << 20) ? slots / 16 : (1 << 20);
+    if ((rc = ensure(r, SB_CIG, (size_t)(slots + reserve) * 4))) return rc;
+    r.cig_slots = slots;
+    D.o_cig = (uint32_t *)r.buf[SB_CIG];
+    D.cig_slot = (const int64_t *)r.buf[SB_CIGSLOT];
+    D.spill_base = slots;
+    if (r.n_task) HIPCHK(hipMemcpyAsync(r.buf[SB_CIGAT], r.buf[SB_CIGSLOT], (size_t)r.n_task * 8, hipMemcpyDeviceToDevice, s));
+    if ((e = aln_launch_compact(A, (int64_t *)r.buf[SB_AOFF], (int64_t *)r.buf[SB_SCANIN], (int32_t *)r.buf[SB_ALIST],
+                                (int32_t *)r.buf[SB_AFLAG], r.buf[SB_ATEMP], r.cap[SB_ATEMP], (void *)s)))
+        return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    HIPCHK(hipMemcpyAsync(&r.n_aln, (int64_t *)r.buf[SB_AOFF] + r.n_sr, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipEventRecord(ctx_event(c, 3), s));
+    if (r.n_task) {
+        e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6),
+                             (void *)ctx_event(c, 7));
+        if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    }
+    unsigned long long sp[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(sp, D.spill, sizeof sp, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (sp[0]) {
+        const size_t need = (size_t)(r.cig_slots + (int64_t)sp[1]) * 4;
+        if (need > r.cap[SB_CIG]) {   // grow the pool, keeping the slots
+            void *np = nullptr;
+            if (hipMalloc(&np, need + need / 8) != hipSuccess) return pr_set_error(PR_ERR_HIP, "hipMalloc failed (CIGAR spill)");
+            HIPCHK(hipMemcpyAsync(np, r.buf[SB_CIG], (size_t)r.cig_slots * 4, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipStreamSynchronize(s));
+            (void)hipFree(r.buf[SB_CIG]);
+            r.buf[SB_CIG] = np;
+            r.cap[SB_CIG] = need + need / 8;
+            D.o_cig = (uint32_t *)np;
+        }
+        HIPCHK(hipMemsetAsync(D.work, 0, 4, s));
+        e = sw_launch_overflow(D, O, grid_g, lds_glob, (void *)s);
+        if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    }
+    r.n_overflow = (int64_t)sp[0];
+    HIPCHK(hipEventRecord(ctx_event(c, 0), s));
     return 0;
 }
 
@@ -185,7 +394,9 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     std::memset(&D, 0, sizeof D);
     D.n_task = r.n_task;
     D.qmax = r.qmax;
-    D.tmax = r.qmax + 4 * o->w + 4;
+    // reference rows of a region: query + 2 x 2w of extension; a patched (merged) region of bwa
+    // mode adds up to 4w more (mem_patch_reg's band bound)
+    D.tmax = r.qmax + (r.bwa ? 8 : 4) * o->w + 8;
     D.sr = (const uint8_t *)r.buf[SB_SR];
     D.sr_off = (const int64_t *)r.buf[SB_SR_OFF];
     D.lr = (const uint8_t *)r.buf[SB_LR];
@@ -258,6 +469,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if ((rc = ensure(r, SB_Z, zb))) return rc;
     D.z = (uint8_t *)r.buf[SB_Z];
     HIPCHK(hipMemsetAsync(r.buf[SB_CELLS], 0, CELLS_BYTES, s));
+    if (r.bwa) return bwa_launch(c, r, D, O, o, grid_w, grid_pk, grid_g, lds_glob);
     if (r.n_task == 0) return 0;
     HIPCHK(hipMemcpyAsync(r.buf[SB_CIGAT], r.buf[SB_CIGSLOT], (size_t)r.n_task * 8, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
@@ -298,6 +510,86 @@ static int down(T *h, const SwResident &r, int id, size_t n, hipStream_t s) {
     return 0;
 }
 
+// bwa mode: the per-task arrays gathered per reported alignment (SAM order) into SB_GDOWN
+struct BwaRows {
+    int32_t *qb, *qe, *rb, *re, *score, *truesc, *pos, *ncig, *status, *task;
+    int64_t *cig_at;
+    uint8_t *pass;
+};
+static int bwa_gather(pr_ctx *c, SwResident &r, BwaRows &g) {
+    hipStream_t s = ctx_stream(c);
+    const int64_t n = r.n_aln;
+    const size_t n1 = (size_t)n + 1;
+    int rc;
+    if ((rc = ensure(r, SB_GDOWN, n1 * (10 * 4 + 8 + 1) + 64))) return rc;
+    char *b = (char *)r.buf[SB_GDOWN];
+    int32_t **f[10] = {&g.qb, &g.qe, &g.rb, &g.re, &g.score, &g.truesc, &g.pos, &g.ncig, &g.status, &g.task};
+    for (int k = 0; k < 10; ++k) *f[k] = (int32_t *)(b + (size_t)k * n1 * 4);
+    g.cig_at = (int64_t *)(b + ((10 * n1 * 4 + 7) & ~(size_t)7));
+    g.pass = (uint8_t *)(g.cig_at + n1);
+    SwGather G;
+    std::memset(&G, 0, sizeof G);
+    G.list = (const int32_t *)r.buf[SB_ALIST];
+    G.n = n;
+    G.t_sr = (const int32_t *)r.buf[SB_T_SR];
+    G.t_lr = (const int32_t *)r.buf[SB_T_LR];
+    G.status = (const int32_t *)r.buf[SB_STATUS];
+    G.pos = (const int32_t *)r.buf[SB_POS];
+    G.score = (const int32_t *)r.buf[SB_SCORE];
+    G.ncig = (const int32_t *)r.buf[SB_NCIG];
+    G.qb = (const int32_t *)r.buf[SB_QB];
+    G.qe = (const int32_t *)r.buf[SB_QE];
+    G.rb = (const int32_t *)r.buf[SB_RB];
+    G.re = (const int32_t *)r.buf[SB_RE];
+    G.truesc = (const int32_t *)r.buf[SB_TRUESC];
+    G.pass = (const uint8_t *)r.buf[SB_PASS];
+    G.cig_at = (const int64_t *)r.buf[SB_CIGAT];
+    G.o_qb = g.qb; G.o_qe = g.qe; G.o_rb = g.rb; G.o_re = g.re; G.o_score = g.score; G.o_truesc = g.truesc;
+    G.o_pos = g.pos; G.o_ncig = g.ncig; G.o_status = g.status; G.o_task = g.task; G.o_cig_at = g.cig_at;
+    G.o_pass = g.pass;
+    const int e = sw_launch_gather(G, (void *)s);
+    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    return 0;
+}
+
+static int bwa_download(pr_ctx *c, SwResident &r, pr_sw_out *o) {
+    hipStream_t s = ctx_stream(c);
+    BwaRows g;
+    int rc;
+    if ((rc = bwa_gather(c, r, g))) return rc;
+    const size_t n = (size_t)r.n_aln;
+    auto d32 = [&](int32_t *h, const int32_t *dv) -> int {
+        if (h && n) HIPCHK(hipMemcpyAsync(h, dv, n * 4, hipMemcpyDeviceToHost, s));
+        return 0;
+    };
+    if ((rc = d32(o->qb, g.qb)) || (rc = d32(o->qe, g.qe)) || (rc = d32(o->rb, g.rb)) || (rc = d32(o->re, g.re)) ||
+        (rc = d32(o->score, g.score)) || (rc = d32(o->truesc, g.truesc)) || (rc = d32(o->pos, g.pos)) ||
+        (rc = d32(o->ncigar, g.ncig)) || (rc = d32(o->status, g.status)) || (rc = d32(o->task, g.task)) ||
+        (rc = d32(o->flag, (const int32_t *)r.buf[SB_AFLAG])))
+        return rc;
+    if (o->pass && n) HIPCHK(hipMemcpyAsync(o->pass, g.pass, n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (!o->cigar_off && !o->cigar) return 0;
+    std::vector<int32_t> nc(n + 1, 0), st(n + 1, 0);
+    if (n) {
+        HIPCHK(hipMemcpy(nc.data(), g.ncig, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(st.data(), g.status, n * 4, hipMemcpyDeviceToHost));
+    }
+    std::vector<int64_t> off(n + 1, 0);
+    for (size_t t = 0; t < n; ++t) off[t + 1] = off[t] + (st[t] == 0 ? nc[t] : 0);
+    if (o->cigar_off) std::memcpy(o->cigar_off, off.data(), (n + 1) * 8);
+    if (!o->cigar) return 0;
+    if (off[n] > o->cigar_cap) return pr_set_error(PR_ERR_CAPACITY, "pr_sw_out.cigar_cap below the CIGAR total");
+    if (!off[n]) return 0;
+    if ((rc = up(r, SB_CIGOFF, off.data(), n + 1, s)) || (rc = ensure(r, SB_CIGOUT, (size_t)off[n] * 4))) return rc;
+    int e = sw_launch_cig_compact((const uint32_t *)r.buf[SB_CIG], g.cig_at, g.ncig, (const int64_t *)r.buf[SB_CIGOFF],
+                                  (int64_t)n, (uint32_t *)r.buf[SB_CIGOUT], (void *)s);
+    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    HIPCHK(hipMemcpyAsync(o->cigar, r.buf[SB_CIGOUT], (size_t)off[n] * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
 extern "C" int pr_sw_download(pr_ctx *c, pr_sw_out *o) {
     if (!c || !o) return pr_set_error(PR_ERR_ARG, "null arg");
     SwResident &r = ctx_sw(c);
@@ -312,6 +604,7 @@ extern "C" int pr_sw_download(pr_ctx *c, pr_sw_out *o) {
         if (hipEventElapsedTime(&b, ctx_event(c, 6), ctx_event(c, 7)) == hipSuccess) r.ms_glob_ring = b;
     }
     HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 24, hipMemcpyDeviceToHost));
+    if (r.bwa) return bwa_download(c, r, o);
     const size_t n = (size_t)r.n_task;
     int rc;
     if ((rc = down(o->qb, r, SB_QB, n, s)) || (rc = down(o->qe, r, SB_QE, n, s)) ||
@@ -350,9 +643,16 @@ extern "C" int pr_sw_cigar_total(pr_ctx *c, int64_t *total, int64_t *n_overflow)
     if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
     HIPCHK(hipSetDevice(ctx_device(c)));
     HIPCHK(hipStreamSynchronize(ctx_stream(c)));
-    const size_t n = (size_t)r.n_task;
+    const size_t n = (size_t)(r.bwa ? r.n_aln : r.n_task);
     std::vector<int32_t> nc(n + 1, 0), st(n + 1, 0);
-    if (n) {
+    if (n && r.bwa) {
+        BwaRows g;
+        int rc = bwa_gather(c, r, g);
+        if (rc) return rc;
+        HIPCHK(hipStreamSynchronize(ctx_stream(c)));
+        HIPCHK(hipMemcpy(nc.data(), g.ncig, n * 4, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(st.data(), g.status, n * 4, hipMemcpyDeviceToHost));
+    } else if (n) {
         HIPCHK(hipMemcpy(nc.data(), r.buf[SB_NCIG], n * 4, hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(st.data(), r.buf[SB_STATUS], n * 4, hipMemcpyDeviceToHost));
     }
@@ -360,6 +660,25 @@ extern "C" int pr_sw_cigar_total(pr_ctx *c, int64_t *total, int64_t *n_overflow)
     for (size_t t = 0; t < n; ++t) tot += st[t] == 0 ? nc[t] : 0;
     *total = tot;
     if (n_overflow) *n_overflow = r.n_overflow;
+    return 0;
+}
+
+extern "C" int pr_sw_aln_count(pr_ctx *c, int64_t *n_aln) {
+    if (!c || !n_aln) return pr_set_error(PR_ERR_ARG, "null arg");
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    HIPCHK(hipStreamSynchronize(ctx_stream(c)));
+    *n_aln = r.bwa ? r.n_aln : r.n_task;
+    return 0;
+}
+
+extern "C" int pr_sw_bwa_stats(pr_ctx *c, int32_t *rounds, int64_t *n_extended, int64_t *n_patch) {
+    if (!c) return pr_set_error(PR_ERR_ARG, "null ctx");
+    SwResident &r = ctx_sw(c);
+    if (rounds) *rounds = r.ext_rounds;
+    if (n_extended) *n_extended = r.n_ext;
+    if (n_patch) *n_patch = r.n_patch;
     return 0;
 }
 
@@ -408,9 +727,72 @@ extern "C" int pr_sw_dominant_kernel(pr_ctx *c, double *ms, int64_t *cells) {
 }
 
 // for the SW -> consensus pipeline (prgpu_api.cpp)
+// bwa mode: the reported alignments regrouped by long read (stable) and gathered into the
+// per-task arrays the hand-off reads (SB_GPIPE), with task_off on the device
+static int bwa_group(pr_ctx *c, SwResident &r, SwPtrs *p) {
+    hipStream_t s = ctx_stream(c);
+    const int64_t n = r.n_aln;
+    const size_t n1 = (size_t)n + 1, l1 = (size_t)r.n_lr + 1;
+    int rc;
+    if ((rc = ensure(r, SB_GLIST, n1 * 4)) || (rc = ensure(r, SB_GKEY0, n1 * 4)) || (rc = ensure(r, SB_GKEY1, n1 * 4)) ||
+        (rc = ensure(r, SB_GCNT, l1 * 4)) || (rc = ensure(r, SB_GLROFF, l1 * 8)) ||
+        (rc = ensure(r, SB_GPIPE, n1 * (6 * 4 + 8 + 2) + 64)) || (rc = ensure(r, SB_SCANIN, (l1 + n1) * 8)))
+        return rc;
+    size_t tb = aln_group_temp_bytes(n, (int32_t)r.n_lr);
+    if (tb > r.cap[SB_ATEMP] && (rc = ensure(r, SB_ATEMP, tb))) return rc;
+    int e = aln_launch_group_lr((const int32_t *)r.buf[SB_ALIST], (const int32_t *)r.buf[SB_T_LR], n, (int32_t)r.n_lr,
+                                (int32_t *)r.buf[SB_GKEY0], (int32_t *)r.buf[SB_GKEY1], (int32_t *)r.buf[SB_GLIST],
+                                (int32_t *)r.buf[SB_GCNT], (int64_t *)r.buf[SB_GLROFF], (int64_t *)r.buf[SB_SCANIN],
+                                r.buf[SB_ATEMP], r.cap[SB_ATEMP], (void *)s);
+    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    char *b = (char *)r.buf[SB_GPIPE];
+    int32_t *o32[6];
+    for (int k = 0; k < 6; ++k) o32[k] = (int32_t *)(b + (size_t)k * n1 * 4);
+    int64_t *cig_at = (int64_t *)(b + ((6 * n1 * 4 + 7) & ~(size_t)7));
+    uint8_t *strand = (uint8_t *)(cig_at + n1), *pass = strand + n1;
+    SwGather G;
+    std::memset(&G, 0, sizeof G);
+    G.list = (const int32_t *)r.buf[SB_GLIST];
+    G.n = n;
+    G.t_sr = (const int32_t *)r.buf[SB_T_SR];
+    G.t_lr = (const int32_t *)r.buf[SB_T_LR];
+    G.status = (const int32_t *)r.buf[SB_STATUS];
+    G.pos = (const int32_t *)r.buf[SB_POS];
+    G.score = (const int32_t *)r.buf[SB_SCORE];
+    G.ncig = (const int32_t *)r.buf[SB_NCIG];
+    G.strand = (const uint8_t *)r.buf[SB_T_STRAND];
+    G.pass = (const uint8_t *)r.buf[SB_PASS];
+    G.cig_at = (const int64_t *)r.buf[SB_CIGAT];
+    G.o_sr = o32[0]; G.o_lr = o32[1]; G.o_status = o32[2]; G.o_pos = o32[3]; G.o_score = o32[4]; G.o_ncig = o32[5];
+    G.o_cig_at = cig_at;
+    G.o_strand = strand;
+    G.o_pass = pass;
+    if ((e = sw_launch_gather(G, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    std::vector<int32_t> cnt(l1, 0);
+    HIPCHK(hipMemcpyAsync(cnt.data(), r.buf[SB_GCNT], l1 * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    int mx = 0;
+    for (int64_t i = 0; i < r.n_lr; ++i) mx = cnt[(size_t)i] > mx ? cnt[(size_t)i] : mx;
+    p->t_sr = o32[0];
+    p->t_lr = o32[1];
+    p->status = o32[2];
+    p->pos = o32[3];
+    p->score = o32[4];
+    p->ncig = o32[5];
+    p->cig_at = cig_at;
+    p->strand = strand;
+    p->pass = pass;
+    p->n_task = n;
+    p->task_off = (const int64_t *)r.buf[SB_GLROFF];
+    p->max_per_lr = mx;
+    return 0;
+}
+
 int sw_get_ptrs(pr_ctx *c, SwPtrs *p) {
     SwResident &r = ctx_sw(c);
     if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
+    p->task_off = nullptr;
+    p->max_per_lr = 0;
     p->sr = (const uint8_t *)r.buf[SB_SR];
     p->lr = (const uint8_t *)r.buf[SB_LR];
     p->strand = (const uint8_t *)r.buf[SB_T_STRAND];
@@ -428,6 +810,31 @@ int sw_get_ptrs(pr_ctx *c, SwPtrs *p) {
     p->n_task = r.n_task;
     p->n_sr = (int)r.n_sr;
     p->n_lr = (int)r.n_lr;
+    return 0;
+}
+
+// the hand-off's view of the SW output: per task, or (bwa mode) the reported alignments grouped
+// by long read (regrouped on the first call after a launch)
+int sw_get_pipe_ptrs(pr_ctx *c, SwPtrs *p, bool regroup) {
+    int rc = sw_get_ptrs(c, p);
+    if (rc) return rc;
+    SwResident &r = ctx_sw(c);
+    if (!r.bwa) return 0;
+    if (regroup) return bwa_group(c, r, p);
+    const int64_t n = r.n_aln;
+    const size_t n1 = (size_t)n + 1;
+    char *b = (char *)r.buf[SB_GPIPE];
+    p->t_sr = (const int32_t *)b;
+    p->t_lr = (const int32_t *)(b + n1 * 4);
+    p->status = (const int32_t *)(b + 2 * n1 * 4);
+    p->pos = (const int32_t *)(b + 3 * n1 * 4);
+    p->score = (const int32_t *)(b + 4 * n1 * 4);
+    p->ncig = (const int32_t *)(b + 5 * n1 * 4);
+    p->cig_at = (const int64_t *)(b + ((6 * n1 * 4 + 7) & ~(size_t)7));
+    p->strand = (const uint8_t *)(p->cig_at + n1);
+    p->pass = p->strand + n1;
+    p->n_task = n;
+    p->task_off = (const int64_t *)r.buf[SB_GLROFF];
     return 0;
 }
 

@@ -72,14 +72,28 @@ struct SwDev {
     int32_t *list;             // task list of the current extension phase
     const int32_t *list_n;     // its length (device)
     int32_t *pk_bucket;        // [PK_SCAN + 1] packed-kernel key counts -> padded offsets; [PK_SCAN] = list length
+    // bwa mode (tasks = every seed of the kept chains): which tasks the extension phases
+    // (bit SEL_EXT) and the CIGAR phases (bit SEL_CIG) take; null = all tasks in both
+    const uint8_t *sel;
 };
+constexpr uint8_t SEL_EXT = 1, SEL_CIG = 2;
+SW_HD inline bool sel_ext(const SwDev &D, int64_t t) { return !D.sel || (D.sel[t] & SEL_EXT); }
+SW_HD inline bool sel_cig(const SwDev &D, int64_t t) { return !D.sel || (D.sel[t] & SEL_CIG); }
 
 struct SwResident {
     bool loaded = false;
     int64_t n_task = 0, n_sr = 0, n_lr = 0;
     int qmax = 0;
-    void *buf[40] = {};
-    size_t cap[40] = {};
+    void *buf[64] = {};
+    size_t cap[64] = {};
+    // bwa mode (pr_sw_batch.t_chain): the tasks are seeds, the outputs reported alignments
+    bool bwa = false;
+    int64_t read_id0 = 0;
+    int64_t n_aln = 0;          // reported alignments of the last launch
+    int ext_rounds = 0;         // extension rounds of the last launch (mem_chain2aln resumes)
+    int64_t n_ext = 0;          // seeds extended
+    int64_t n_rank0 = 0;        // first seeds of the chains (the first round)
+    int64_t n_patch = 0;        // mem_patch_reg global scores computed
     int64_t cig_slots = 0;      // ops in the slots (= first spill op)
     int64_t n_overflow = 0;     // tasks of the last launch whose CIGAR went to the spill area
     float ms_ext = 0.f, ms_glob = 0.f;
@@ -87,7 +101,8 @@ struct SwResident {
     float ms_glob_ring = 0.f;
 };
 
-// device pointers of a resident SW batch (for the SW -> consensus pipeline)
+// device pointers of a resident SW batch (for the SW -> consensus pipeline); in bwa mode
+// the per-task arrays are the reported alignments grouped by long read (task_off)
 struct SwPtrs {
     const uint8_t *sr, *lr, *strand, *pass;
     const int64_t *sr_off, *lr_off;
@@ -96,6 +111,8 @@ struct SwPtrs {
     const int64_t *cig_at;
     int64_t n_task;
     int n_sr, n_lr;
+    const int64_t *task_off;    // bwa mode: [n_lr+1] alignments of long read i; else null
+    int max_per_lr;             // bwa mode: most alignments on one long read
 };
 
 int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out, void *stream);
@@ -107,5 +124,18 @@ int sw_launch_overflow(const SwDev &D, const SwOptsDev &O, int grid, int lds, vo
 int sw_launch_cig_compact(const uint32_t *pool, const int64_t *at, const int32_t *ncig, const int64_t *off,
                           int64_t n, uint32_t *out, void *stream);
 void sw_release(SwResident &r);
+// bwa mode: gather the reported alignments by long read (stable: read order inside a long read)
+struct SwGather {
+    const int32_t *list;        // alignment -> task
+    int64_t n;
+    const int32_t *t_sr, *status, *pos, *score, *ncig, *qb, *qe, *rb, *re, *truesc, *flag_in;
+    const uint8_t *strand, *pass;
+    const int64_t *cig_at;
+    int32_t *o_sr, *o_status, *o_pos, *o_score, *o_ncig, *o_qb, *o_qe, *o_rb, *o_re, *o_truesc, *o_task, *o_lr;
+    const int32_t *t_lr;
+    uint8_t *o_strand, *o_pass;
+    int64_t *o_cig_at;
+};
+int sw_launch_gather(const SwGather &G, void *stream);
 
 }  // namespace prgpu

@@ -98,7 +98,7 @@ __device__ __forceinline__ TaskGeo task_geo(const SwDev &D, const SwOptsDev &O, 
 // packed extension key (mode 1 = left, 2 = right side, first band try): the side's
 // query length, for tasks whose scores fit the kernel's int16 frame; -1 otherwise
 __device__ __forceinline__ int pk_ext_key(const SwDev &D, const SwOptsDev &O, int64_t t, int side) {
-    if (!O.pk || O.w > 40) return -1;
+    if (!O.pk || O.w > 40 || !sel_ext(D, t)) return -1;
     const int sid = D.t_sr[t];
     const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
     const int ql = side == 0 ? D.t_qbeg[t] : lq - D.t_qbeg[t] - D.t_slen[t];
@@ -400,6 +400,7 @@ __global__ void sw_left_finish_kernel(SwDev D, SwOptsDev O) {
     unsigned long long cells = 0;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task;
          t += (int64_t)gridDim.x * blockDim.x) {
+        if (!sel_ext(D, t)) continue;
         const TaskGeo g = task_geo(D, O, t);
         int score, truesc, qb, rb, aw0 = O.w;
         if (g.qbeg) {
@@ -433,6 +434,7 @@ __global__ void sw_right_finish_kernel(SwDev D, SwOptsDev O) {
     unsigned long long cells = 0;
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task;
          t += (int64_t)gridDim.x * blockDim.x) {
+        if (!sel_ext(D, t)) continue;
         const TaskGeo g = task_geo(D, O, t);
         int score = D.o_score[t], truesc = D.o_truesc[t], qe, re, aw1 = O.w;
         const int qb = D.o_qb[t];
@@ -654,7 +656,7 @@ __device__ __forceinline__ int glob_class(const SwDev &D, const SwOptsDev &O, in
 // packed-kernel key (band * 256 + query length) of a task whose first pass runs a
 // DP with band <= 40 inside the kernel's int16 frame; -1 otherwise
 __device__ __forceinline__ int pk_key(const SwDev &D, const SwOptsDev &O, int64_t t) {
-    if (!O.pk) return -1;
+    if (!O.pk || !sel_cig(D, t)) return -1;
     const int lqq = D.o_qe[t] - D.o_qb[t], rlen = D.o_re[t] - D.o_rb[t];
     if (lqq > PK_QMAX || rlen > PK_TMAX) return -1;
     bool nogap;
@@ -1076,6 +1078,7 @@ __device__ __forceinline__ int sw_phase_key(const SwDev &D, const SwOptsDev &O, 
     const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
     const int qbeg = D.t_qbeg[t];
     const int right = lq - qbeg - D.t_slen[t];
+    if (!(phase < 4 ? sel_ext(D, t) : sel_cig(D, t))) return -1;
     switch (phase) {
         case 0: return (qbeg > 0 && (pk_ext_key(D, O, t, 0) < 0 || (D.x_try[t] & 8))) ? qbeg : -1;
         case 1: return (D.x_try[t] & 1) ? qbeg : -1;

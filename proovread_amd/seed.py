@@ -21,7 +21,7 @@ class SeedOpts(C.Structure):
 
 class SeedTask(C.Structure):
     _fields_ = [(k, C.c_int32) for k in ("sr", "lr", "strand", "qbeg", "rbeg", "slen", "rmax0", "rmax1",
-                                          "weight", "nseed")]
+                                          "chain", "rank")]
 
 
 class SeedTasks(C.Structure):

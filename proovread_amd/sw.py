@@ -26,20 +26,22 @@ class SwOpts(C.Structure):
     _fields_ = [("a", C.c_int32), ("b", C.c_int32), ("o_del", C.c_int32), ("e_del", C.c_int32),
                 ("o_ins", C.c_int32), ("e_ins", C.c_int32), ("w", C.c_int32), ("pen_clip5", C.c_int32),
                 ("pen_clip3", C.c_int32), ("zdrop", C.c_int32), ("min_score_per_base", C.c_double),
-                ("bin_size", C.c_int32), ("bin_length", C.c_double)]
+                ("bin_size", C.c_int32), ("bin_length", C.c_double), ("drop_ratio", C.c_double),
+                ("mask_level", C.c_double), ("mask_level_redun", C.c_double), ("max_chain_gap", C.c_int32)]
 
 
 class SwBatch(C.Structure):
     _fields_ = [("n_sr", C.c_int32), ("sr_off", _abi.P64), ("sr_seq", _abi.PU8), ("n_lr", C.c_int32),
                 ("lr_off", _abi.P64), ("lr_seq", _abi.PU8), ("n_task", C.c_int64), ("t_sr", _abi.P32),
                 ("t_lr", _abi.P32), ("t_strand", _abi.PU8), ("t_qbeg", _abi.P32), ("t_rbeg", _abi.P32),
-                ("t_slen", _abi.P32)]
+                ("t_slen", _abi.P32), ("t_chain", _abi.P32), ("read_id0", C.c_int64)]
 
 
 class SwOut(C.Structure):
     _fields_ = [("qb", _abi.P32), ("qe", _abi.P32), ("rb", _abi.P32), ("re", _abi.P32), ("score", _abi.P32),
                 ("truesc", _abi.P32), ("pos", _abi.P32), ("ncigar", _abi.P32), ("pass_", _abi.PU8),
-                ("status", _abi.P32), ("cigar_off", _abi.P64), ("cigar", _abi.PU32), ("cigar_cap", C.c_int64)]
+                ("status", _abi.P32), ("cigar_off", _abi.P64), ("cigar", _abi.PU32), ("cigar_cap", C.c_int64),
+                ("task", _abi.P32), ("flag", _abi.P32)]
 
 
 def _setup(L):
@@ -55,6 +57,8 @@ def _setup(L):
     L.pr_sw_dominant_kernel.argtypes = [C.c_void_p, _abi.PD, _abi.P64]
     L.pr_sw_phase_cycles.argtypes = [C.c_void_p, _abi.P64]
     L.pr_sw_cigar_total.argtypes = [C.c_void_p, _abi.P64, _abi.P64]
+    L.pr_sw_aln_count.argtypes = [C.c_void_p, _abi.P64]
+    L.pr_sw_bwa_stats.argtypes = [C.c_void_p, _abi.P32, _abi.P64, _abi.P64]
     L._sw_ready = True
 
 
@@ -78,6 +82,10 @@ class SwInput:
     t_qbeg: np.ndarray   # int32
     t_rbeg: np.ndarray   # int32
     t_slen: np.ndarray   # int32
+    # bwa mode: the tasks are pr_seed_map's seeds (grouped by short read, then chain, in
+    # rank order) and t_chain their chain index; outputs are the reported alignments
+    t_chain: Optional[np.ndarray] = None
+    read_id0: int = 0
 
     def c_batch(self) -> SwBatch:
         P = _abi.ptr
@@ -95,21 +103,26 @@ class SwInput:
         b.t_qbeg = P(self.t_qbeg, C.c_int32)
         b.t_rbeg = P(self.t_rbeg, C.c_int32)
         b.t_slen = P(self.t_slen, C.c_int32)
+        if self.t_chain is not None:
+            b.t_chain = P(self.t_chain, C.c_int32)
+            b.read_id0 = int(self.read_id0)
         return b
 
 
 class SwResult:
-    """Per-task outputs; CIGARs variable length, compacted in task order (cigar_off prefix)."""
+    """Per-task outputs (bwa mode: per reported alignment, SAM order, with the seed `task`
+    that made it and the SAM `flag` bits); CIGARs variable length, compacted in order
+    (cigar_off prefix)."""
 
     def __init__(self, n: int):
         self.a = {k: np.zeros(max(n, 1), np.int32) for k in
-                  ("qb", "qe", "rb", "re", "score", "truesc", "pos", "ncigar", "status")}
+                  ("qb", "qe", "rb", "re", "score", "truesc", "pos", "ncigar", "status", "task", "flag")}
         self.a["pass"] = np.zeros(max(n, 1), np.uint8)
         self.a["cigar_off"] = np.zeros(n + 1, np.int64)
         self.a["cigar"] = np.zeros(1, np.uint32)
         o = SwOut()
         P = _abi.ptr
-        for k in ("qb", "qe", "rb", "re", "score", "truesc", "pos", "ncigar", "status"):
+        for k in ("qb", "qe", "rb", "re", "score", "truesc", "pos", "ncigar", "status", "task", "flag"):
             setattr(o, k, P(self.a[k], C.c_int32))
         o.pass_ = P(self.a["pass"], C.c_uint8)
         o.cigar_off = P(self.a["cigar_off"], C.c_int64)
@@ -139,15 +152,26 @@ def run(inp: SwInput, opts: Optional[SwOpts] = None, ctx: Optional[_abi.Context]
     ctx = ctx or _abi.default_context()
     opts = opts or default_opts()
     b = inp.c_batch()
-    res = SwResult(len(inp.t_sr))
     _abi.check(L.pr_sw_upload(ctx.h, C.byref(b)), "pr_sw_upload")
     _abi.check(L.pr_sw_launch(ctx.h, C.byref(opts)), "pr_sw_launch")
+    na = C.c_int64()
+    _abi.check(L.pr_sw_aln_count(ctx.h, C.byref(na)), "pr_sw_aln_count")
+    res = SwResult(na.value)
     tot, nov = C.c_int64(), C.c_int64()
     _abi.check(L.pr_sw_cigar_total(ctx.h, C.byref(tot), C.byref(nov)), "pr_sw_cigar_total")
     res.size_cigar(tot.value)
     res.n_overflow = nov.value
     _abi.check(L.pr_sw_download(ctx.h, C.byref(res.c)), "pr_sw_download")
     return res
+
+
+def bwa_stats(ctx: _abi.Context):
+    """bwa mode: (extension rounds, seeds extended, mem_patch_reg scores) of the last launch."""
+    L = _abi.lib()
+    _setup(L)
+    r, n, p = C.c_int32(), C.c_int64(), C.c_int64()
+    _abi.check(L.pr_sw_bwa_stats(ctx.h, C.byref(r), C.byref(n), C.byref(p)), "pr_sw_bwa_stats")
+    return r.value, n.value, p.value
 
 
 def last_timing(ctx: _abi.Context):

@@ -16,6 +16,8 @@ from __future__ import annotations
 
 import dataclasses
 
+from typing import Optional
+
 import numpy as np
 
 
@@ -35,6 +37,9 @@ class Dataset:
     t_qbeg: np.ndarray
     t_rbeg: np.ndarray
     t_slen: np.ndarray
+    # bwa mode: tasks are every seed of the kept chains grouped by short read (pr_seed_map
+    # order) and t_chain their chain; None: single-seed tasks grouped by long read
+    t_chain: Optional[np.ndarray] = None
 
     @property
     def n_lr(self):
@@ -53,7 +58,7 @@ class Dataset:
     def sw_input(self):
         from .sw import SwInput
         return SwInput(self.sr_off, self.sr_seq, self.lr_off, self.lr_seq, self.t_sr, self.t_lr, self.t_strand,
-                       self.t_qbeg, self.t_rbeg, self.t_slen)
+                       self.t_qbeg, self.t_rbeg, self.t_slen, self.t_chain)
 
 
 def simulate(seed: int, genome_len: int, n_lr: int, lr_len: int, sr_cov: float,
@@ -175,6 +180,17 @@ def simulate(seed: int, genome_len: int, n_lr: int, lr_len: int, sr_cov: float,
     return Dataset(genome, lr_seq, lr_off, lr_start, sr_seq, sr_off, sr_start, sr_strand,
                    p_sr[order].astype(np.int32), p_lr[order].astype(np.int32), strand[order].astype(np.uint8),
                    qbeg[order].astype(np.int32), rbeg[order].astype(np.int32), best_len[order].astype(np.int32))
+
+
+def with_seeds(d: Dataset, tasks: np.ndarray) -> Dataset:
+    """The same reads with the seeding front end's output (seed.TASK_DTYPE records of
+    pr_seed_map / pr_seed_gpu_map: every seed of the kept chains, grouped by short read, then
+    chain, in mem_chain2aln's order) as a bwa-mode task list."""
+    t = tasks
+    return dataclasses.replace(d, t_sr=t["sr"].astype(np.int32), t_lr=t["lr"].astype(np.int32),
+                               t_strand=t["strand"].astype(np.uint8), t_qbeg=t["qbeg"].astype(np.int32),
+                               t_rbeg=t["rbeg"].astype(np.int32), t_slen=t["slen"].astype(np.int32),
+                               t_chain=t["chain"].astype(np.int32))
 
 
 def with_seeded_tasks(d: Dataset, tasks: np.ndarray) -> Dataset:

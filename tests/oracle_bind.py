@@ -198,3 +198,49 @@ def sw_extend(q, t, h0, w=40, a=5, b=11, o_del=2, e_del=4, o_ins=1, e_ins=3, end
     sc = L.osw_extend(len(q), nt4(q), len(t), nt4(t), 5, mat, o_del, e_del, o_ins, e_ins, w, end_bonus,
                       zdrop, h0, *[C.byref(x) for x in outs])
     return sc, [x.value for x in outs]   # qle, tle, gtle, gscore, max_off
+
+
+# ---------------------------------------------------------------------------
+# bwa mem per-read alignment oracle (oracle/aln_oracle.c)
+class OswRegion(C.Structure):
+    _fields_ = [(k, C.c_int) for k in ("qb", "qe", "rb", "re", "score", "truesc", "w", "seedlen0")]
+
+
+class OalnSeed(C.Structure):
+    _fields_ = [(k, C.c_int) for k in ("sr", "lr", "strand", "qbeg", "rbeg", "slen", "rmax0", "rmax1", "chain",
+                                       "rank")]
+
+
+class OalnOpts(C.Structure):
+    _fields_ = [("drop_ratio", C.c_double), ("mask_level", C.c_double), ("mask_level_redun", C.c_double),
+                ("max_chain_gap", C.c_int)]
+
+
+class OalnReg(C.Structure):
+    _fields_ = [("lr", C.c_int), ("strand", C.c_int), ("g", OswRegion), ("secondary", C.c_int), ("flag", C.c_int),
+                ("seed", C.c_int), ("patched", C.c_int)]
+
+
+def aln_opts(task="bwa-sr"):
+    o = OalnOpts()
+    o.drop_ratio = 0.75 if task == "bwa-sr-finish" else 0.0
+    o.mask_level, o.mask_level_redun, o.max_chain_gap = 0.5, 0.95, 10000
+    return o
+
+
+_aln_set = False
+
+
+def aln_lib():
+    global _aln_set
+    L = sw_lib()
+    if not _aln_set:
+        L.oaln_read.argtypes = [C.POINTER(OswOpts), C.POINTER(OalnOpts), C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                C.c_int, C.c_void_p, C.c_int, C.c_int64, C.c_void_p, C.POINTER(C.c_int),
+                                C.POINTER(C.c_int)]
+        L.osw_reg2aln.argtypes = [C.POINTER(OswOpts), C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                  C.POINTER(OswRegion), C.POINTER(OswResult)]
+        L.osw_extend_seed.argtypes = [C.POINTER(OswOpts), C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int,
+                                      C.c_int, C.c_int, C.c_int, C.POINTER(OswRegion)]
+        _aln_set = True
+    return L

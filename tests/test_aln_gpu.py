@@ -1,0 +1,78 @@
+"""bwa mode on the device: pr_sw_run with pr_sw_batch.t_chain (the seeds of every kept chain,
+aln_kernels.hip: mem_chain2aln over every seed with speculative first seeds and resumed walks,
+mem_sort_dedup_patch, mem_mark_primary_se, mem_reg2sam's -T / -D filters and SAM order)
+against the CPU restatement (oracle/aln_oracle.c over oracle/sw_oracle.c) read by read: the
+same reported alignments in the same order with the same long read, strand, POS, CIGAR, AS,
+FLAG and aligned intervals.  bwa-proovread itself is absent: parity with it is unpinned."""
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "oracle"))
+pytestmark = pytest.mark.gpu
+
+
+def _data(seed_, err, finish, n_lr=40, lr_len=2500, cov=15):
+    from proovread_amd import seed, synth
+    f = err / 0.15
+    d = synth.simulate(seed_, 40000, n_lr, lr_len, cov, p_ins=0.09 * f, p_del=0.045 * f, p_sub=0.015 * f)
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    d = synth.with_seeds(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(finish), threads=4))
+    ix.close()
+    return d
+
+
+def _by_read(res, d):
+    out = {}
+    for i in range(res.n):
+        t = int(res["task"][i])
+        r = int(d.t_sr[t])
+        assert res["status"][i] == 0
+        out.setdefault(r, []).append((int(d.t_lr[t]), int(d.t_strand[t]), int(res["pos"][i]),
+                                      [int(x) for x in res.cigar_ops(i)], int(res["score"][i]),
+                                      int(res["flag"][i]), int(res["qb"][i]), int(res["qe"][i]),
+                                      int(res["rb"][i]), int(res["re"][i]), int(res["truesc"][i]), t))
+    return out
+
+
+@pytest.mark.parametrize("finish,err", [(False, 0.15), (False, 0.05), (True, 0.05), (True, 0.02)])
+def test_bwa_mode_matches_oracle(finish, err):
+    import cpu_chain
+    from proovread_amd import _abi, sw
+    d = _data(41 + int(finish) + int(err * 100), err, finish)
+    task = "bwa-sr-finish" if finish else "bwa-sr"
+    ctx = _abi.default_context()
+    res = sw.run(d.sw_input(), sw.default_opts(finish), ctx=ctx)
+    rounds, n_ext, n_patch = sw.bwa_stats(ctx)
+    want = cpu_chain.bwa_alignments(d, task)
+    got = _by_read(res, d)
+    n = 0
+    for r in range(d.n_sr):
+        assert got.get(r, []) == want[r], r
+        n += len(want[r])
+    assert n == res.n and n > 5 * d.n_lr
+    n_chain = len(np.unique(d.t_sr.astype(np.int64) * 65536 + d.t_chain))
+    assert rounds >= 1 and n_ext >= n_chain > 0
+    if finish:   # -D .75 drops low secondaries, -T 4 per base drops most 5 %-error alignments
+        assert any(f & 0x100 for v in got.values() for (_, _, _, _, _, f, *_r) in v)
+
+
+def test_bwa_mode_seed_order_and_empty_reads():
+    """reads without seeds, and a batch whose seeds are not grouped by read, fail loudly"""
+    from proovread_amd import _abi, sw
+    d = _data(77, 0.15, False, n_lr=12, lr_len=2000)
+    inp = d.sw_input()
+    bad = sw.SwInput(**{**inp.__dict__})
+    perm = np.arange(len(inp.t_sr))[::-1].copy()
+    for k in ("t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen", "t_chain"):
+        setattr(bad, k, np.ascontiguousarray(getattr(inp, k)[perm]))
+    with pytest.raises(RuntimeError):
+        sw.run(bad, sw.default_opts(False))
+    keep = inp.t_sr >= d.n_sr // 2   # the first half of the reads have no seeds
+    half = sw.SwInput(**{**inp.__dict__})
+    for k in ("t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen", "t_chain"):
+        setattr(half, k, np.ascontiguousarray(getattr(inp, k)[keep]))
+    res = sw.run(half, sw.default_opts(False), ctx=_abi.default_context())
+    assert res.n > 0 and (half.t_sr[res["task"][:res.n]] >= d.n_sr // 2).all()

@@ -1,9 +1,9 @@
 """`bwa-proovread` drop-in CLI (proovread_amd/bwa_proovread.py): option parsing as
 proovread passes it (bin/proovread:1313 with proovread.cfg bwa-sr), FASTA/FASTQ
-input, host seeding, SAM output.  The SW stage is injected here as the CPU
-oracle (oracle/sw_oracle.c through tests/oracle_bind.py) so the CLI logic is
-checked without a GPU; on the GPU the same CLI calls pr_sw_run, whose parity
-with the oracle is covered by test_sw_gpu.py."""
+input, host seeding, SAM output.  The bwa-mode SW stage is injected here as the
+CPU oracle (oracle/aln_oracle.c through oracle/cpu_chain.py) so the CLI logic is
+checked without a GPU; on the GPU the same CLI calls pr_sw_run in bwa mode, whose
+parity with the oracle is covered by test_aln_gpu.py."""
 import io
 
 import numpy as np
@@ -14,10 +14,16 @@ from proovread_amd import sw
 
 
 class _OracleResult:
-    def __init__(self, n):
-        self.a = {k: np.zeros(max(n, 1), np.int32) for k in ("pos", "score", "status", "ncigar")}
-        self.a["pass"] = np.zeros(max(n, 1), np.uint8)
-        self.cig = [""] * n
+    """pr_sw_out of bwa mode from the CPU restatement (oracle/aln_oracle.c)."""
+
+    def __init__(self, rows):
+        n = len(rows)
+        self.a = {k: np.zeros(max(n, 1), np.int32) for k in ("pos", "score", "status", "task", "flag")}
+        self.a["pass"] = np.ones(max(n, 1), np.uint8)
+        self.cig = []
+        for i, x in enumerate(rows):
+            self.a["pos"][i], self.a["score"][i], self.a["flag"][i], self.a["task"][i] = x[2], x[4], x[5], x[11]
+            self.cig.append("".join(f"{c >> 4}{'MIDNSHP=X'[c & 15]}" for c in x[3]))
         self.n = n
 
     def __getitem__(self, k):
@@ -28,19 +34,19 @@ class _OracleResult:
 
 
 def oracle_runner(task):
+    import sys
+    import types
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "oracle"))
+    import cpu_chain
+
     def run(inp, opts):
-        o = ob.sw_opts(task)
-        n = len(inp.t_sr)
-        res = _OracleResult(n)
-        for t in range(n):
-            s, l = int(inp.t_sr[t]), int(inp.t_lr[t])
-            q = "".join("ACGTN"[c] for c in inp.sr_seq[inp.sr_off[s]:inp.sr_off[s + 1]])
-            ref = "".join("ACGTN"[c] for c in inp.lr_seq[inp.lr_off[l]:inp.lr_off[l + 1]])
-            r, cg = ob.sw_task(o, q, ref, int(inp.t_strand[t]), int(inp.t_qbeg[t]), int(inp.t_rbeg[t]),
-                               int(inp.t_slen[t]))
-            res.a["pos"][t], res.a["score"][t], res.a["pass"][t] = r.pos, r.score, getattr(r, "pass")
-            res.cig[t] = cg
-        return res
+        d = types.SimpleNamespace(sr_seq=inp.sr_seq, sr_off=inp.sr_off, lr_seq=inp.lr_seq, lr_off=inp.lr_off,
+                                  t_sr=inp.t_sr, t_lr=inp.t_lr, t_strand=inp.t_strand, t_qbeg=inp.t_qbeg,
+                                  t_rbeg=inp.t_rbeg, t_slen=inp.t_slen, t_chain=inp.t_chain,
+                                  n_sr=len(inp.sr_off) - 1, n_lr=len(inp.lr_off) - 1)
+        rows = [x for per in cpu_chain.bwa_alignments(d, task, drop_ratio=opts.drop_ratio) for x in per]
+        return _OracleResult(rows)
     return run
 
 
@@ -111,9 +117,10 @@ def test_cli_sam_output(tmp_path):
         ref_len = sum(int(n) for n, o in ops if o in "MD")
         assert 1 <= pos and pos - 1 + ref_len <= len(lrs[int(rname[2:])])
         assert f[11].startswith("AS:i:") and int(f[11][5:]) >= 2.5 * sum(int(n) for n, o in ops if o in "MI")
-        if not flag & 256:
+        if not flag & 0x900:   # the read's first record is its best (mem_mark_primary_se order)
             assert mapq == 60 and name not in prim
             prim[name] = int(f[11][5:])
+        assert name in prim   # secondaries / supplementaries follow their read's first record
     for f in recs:
         assert int(f[11][5:]) <= prim[f[0]]
 

@@ -13,7 +13,7 @@ from pipeline_oracle import consensus_cases, sam_for_tasks
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("seeds", ["truth", "host", "truth-slot16", "host-binfilter"])
+@pytest.mark.parametrize("seeds", ["truth", "host", "truth-slot16", "host-binfilter", "bwa", "bwa-binfilter"])
 @pytest.mark.parametrize("finish", [False, True])
 def test_iteration_matches_cpu_chain(finish, seeds, monkeypatch):
     """truth-slot16: CIGAR slots forced to 16 ops, so most alignments reach the consensus
@@ -26,9 +26,12 @@ def test_iteration_matches_cpu_chain(finish, seeds, monkeypatch):
         monkeypatch.setenv("PRGPU_SW_CIG_SLOT", "16")
     binf = (20, 20.0 * 15) if seeds.endswith("binfilter") else None
     d = synth.simulate(31 + finish, 40000, 40, 2500, 40 if binf else 15, sr_frac=1.0)
-    if seeds.startswith("host"):
+    if seeds.startswith("host") or seeds.startswith("bwa"):
         ix = seed.SeedIndex(d.lr_seq, d.lr_off)
-        d = synth.with_seeded_tasks(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(finish), threads=4))
+        tk = ix.map(d.sr_seq, d.sr_off, seed.default_opts(finish), threads=4)
+        if seeds.startswith("host"):   # single-seed tasks: each chain's first seed
+            tk = tk[tk["rank"] == 0]
+        d = (synth.with_seeds if seeds.startswith("bwa") else synth.with_seeded_tasks)(d, tk)
         ix.close()
         assert len(d.t_sr) > 10 * d.n_lr
     task = "bwa-sr-finish" if finish else "bwa-sr"
@@ -42,6 +45,21 @@ def test_iteration_matches_cpu_chain(finish, seeds, monkeypatch):
         opts.bin_size, opts.bin_length = binf
     it.launch(opts, cp)
     got = it.results()
+    if seeds.startswith("bwa"):   # bwa mode: the oracle chain over every seed (aln_oracle.c)
+        import sys
+        from pathlib import Path
+        sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "oracle"))
+        import cpu_chain
+        _, _, want, _ = cpu_chain.run_sample(d, range(d.n_lr), task=task, coverage=float(params["coverage"]),
+                                             use_ref_qual=params["use_ref_qual"] == "1", workers=4,
+                                             detect_chimera=params["detect_chimera"] == "1", full=True,
+                                             bin_filter=binf)
+        for i, (g, (rc, fq, trace, chim)) in enumerate(zip(got, want)):
+            assert rc == 0 and g.status == 0, (i, rc, g.status)
+            assert g.fastq == fq.replace(f"@lr{i}", f"@lr{i}"), i
+            assert g.trace == trace, i
+            assert "".join(l + "\n" for l in g.chim_lines()) == chim, i
+        return
     sams = sam_for_tasks(d, task, bin_filter=binf)
     if binf:   # the filter must bite: fewer records than the unfiltered chain
         assert sum(map(len, sams.values())) < sum(map(len, sam_for_tasks(d, task).values()))

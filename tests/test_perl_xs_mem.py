@@ -92,20 +92,21 @@ def test_perl_mem_equals_python_mem_with_oracle_sw(tmp_path, binning, odd):
     inp, res = seen["inp"], seen["res"]
     n = len(inp.t_sr)
     js["sw"] = {"pos": res["pos"].tolist(), "score": res["score"].tolist(), "pass": res["pass"].tolist(),
-                "status": res["status"].tolist(), "cigar": [res.cigar_str(t) for t in range(n)]}
+                "status": res["status"].tolist(), "cigar": [res.cigar_str(t) for t in range(res.n)],
+                "task": res["task"].tolist(), "flag": res["flag"].tolist()}
     got = _perl_mem(js, tmp_path)
     # the task list Perl handed to the SW stage is the Python host's, byte for byte
     b = got["batch"]
     assert int(b["n_task"]) == n > 40
     for k, dt in (("t_sr", np.int32), ("t_lr", np.int32), ("t_strand", np.uint8), ("t_qbeg", np.int32),
-                  ("t_rbeg", np.int32), ("t_slen", np.int32)):
+                  ("t_rbeg", np.int32), ("t_slen", np.int32), ("t_chain", np.int32)):
         assert bytes.fromhex(b[k]) == np.asarray(getattr(inp, k[0:]), dt).tobytes(), k
     assert bytes.fromhex(b["sr_seq"]) == np.asarray(inp.sr_seq, np.uint8).tobytes()
     assert bytes.fromhex(b["lr_off"]) == np.asarray(inp.lr_off, np.int64).tobytes()
     assert got["head"] == head
     assert got["rec"] == rec
     if binning:
-        assert len(rec) < sum(1 for t in range(n) if res["pass"][t])
+        assert len(rec) < sum(1 for t in range(res.n) if res["pass"][t])
     if odd:
         names = {x.split("\t")[0] for x in rec}
         assert {"sr3/1", "sr5/1", "sr11/1"} & names
@@ -193,21 +194,20 @@ def _perl_iter(js, tmp_path):
 
 
 def test_perl_iteration_batch_equals_python_iteration_batch(tmp_path):
-    """The batch Prgpu::iteration hands to iter_run: host-seeded tasks grouped by long read
-    (stable) exactly as synth.with_seeded_tasks groups them for iteration.Iteration."""
+    """The batch Prgpu::iteration hands to iter_run: the host seeds in bwa mode (every seed of
+    the kept chains, grouped by short read, with their chains) exactly as synth.with_seeds
+    hands them to iteration.Iteration."""
     from proovread_amd import seed, synth
     d, js = _iter_inputs()
     js["inject"] = 1
     got = _perl_iter(js, tmp_path)
     ix = seed.SeedIndex(d.lr_seq, d.lr_off)
-    dd = synth.with_seeded_tasks(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=2))
+    dd = synth.with_seeds(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=2))
     b = got["batch"]
     assert int(b["n_task"]) == len(dd.t_sr) > 1000
-    for k in ("t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen"):
+    for k in ("t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen", "t_chain"):
         assert bytes.fromhex(b[k]) == np.asarray(getattr(dd, k)).tobytes(), k
-    tlo = np.zeros(d.n_lr + 1, np.int64)
-    np.cumsum(np.bincount(dd.t_lr, minlength=d.n_lr), out=tlo[1:])
-    assert bytes.fromhex(b["task_lr_off"]) == tlo.tobytes()
+    assert "task_lr_off" not in b
     assert bytes.fromhex(b["lr_qual"]) == b"$" * int(d.lr_off[-1])
     assert bytes.fromhex(b["lr_seq"]) == np.asarray(d.lr_seq, np.uint8).tobytes()
     assert [r["status"] for r in got["res"]] == [-1] * d.n_lr
@@ -219,7 +219,7 @@ def test_perl_iteration_equals_python_iteration_on_gpu(tmp_path):
     d, js = _iter_inputs()
     got = _perl_iter(js, tmp_path)["res"]
     ix = seed.SeedIndex(d.lr_seq, d.lr_off)
-    dd = synth.with_seeded_tasks(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=2))
+    dd = synth.with_seeds(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=2))
     it = iteration.Iteration(dd)
     it.launch(sw.default_opts(False), cns.CnsParams(coverage=11.25, use_ref_qual=True))
     want = it.results()
