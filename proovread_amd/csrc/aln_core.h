@@ -170,8 +170,64 @@ AL_HD void introsort(int n, int32_t *a, const AlnReg *R, Lt lt) {
     }
 }
 
-// mem_chain2aln for read r, resumed at its first open seed -> 1: an extension was requested
-AL_HD int aln_walk_read(const AlnDev &A, int64_t r) {
+// round-0 state of task t: every chain's first seed is extended speculatively; cnext[t] of
+// a chain's first seed = the next chain's first seed (chains are consecutive)
+AL_HD bool aln_init_task(const AlnDev &A, int64_t t) {
+    const bool first = t == 0 || A.t_sr[t] != A.t_sr[t - 1] || A.t_chain[t] != A.t_chain[t - 1];
+    A.sel[t] = first ? SEL_EXT : 0;
+    A.ext[t] = 0;
+    A.dec[t] = 0;
+    if (first) {
+        int64_t e = t + 1;
+        while (e < A.n_task && A.t_sr[e] == A.t_sr[t] && A.t_chain[e] == A.t_chain[t]) ++e;
+        A.cnext[t] = (int32_t)e;
+    }
+    return first;
+}
+
+// is seed (slr, sst, srb, sqb, slen) "around" region i (mem_chain2aln's containment test)?
+AL_HD bool aln_around(const AlnDev &A, int64_t i, int64_t srb, int sqb, int slen, int lq) {
+    const int pqb = A.o_qb[i], pqe = A.o_qe[i];
+    const int64_t prb = A.o_rb[i], pre = A.o_re[i];
+    if (srb < prb || srb + slen > pre || sqb < pqb || sqb + slen > pqe) return false;   // not contained
+    if ((double)(slen - A.t_slen[i]) > .1 * lq) return false;   // may give a better alignment
+    const int pw = A.o_w[i];
+    int64_t qd = sqb - pqb, rd = srb - prb;
+    int mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
+    int w = mg < pw ? mg : pw;
+    if (qd - rd < w && rd - qd < w) return true;
+    qd = pqe - (sqb + slen);
+    rd = pre - (srb + slen);
+    mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
+    w = mg < pw ? mg : pw;
+    return qd - rd < w && rd - qd < w;
+}
+
+// any region made before seed k (dec == 1) that seed k is around?  Regions on another long
+// read or strand never contain it (disjoint in bwa's coordinates), so after k's own chain
+// [c0, k) only the earlier chains on k's long read and strand are looked at (their first
+// seeds carry the chain's long read, strand and end).  "Exists" is order-free.
+AL_HD bool aln_around_any(const AlnDev &A, int64_t s0, int64_t c0, int64_t k, int lq) {
+    const int slr = A.t_lr[k], sst = A.t_strand[k];
+    const int64_t srb = A.t_rbeg[k];
+    const int sqb = A.t_qbeg[k], slen = A.t_slen[k];
+    for (int64_t i = c0; i < k; ++i)
+        if (A.dec[i] == 1 && aln_around(A, i, srb, sqb, slen, lq)) return true;
+    for (int64_t h = s0; h < c0; h = A.cnext[h]) {
+        if (A.t_lr[h] != slr || A.t_strand[h] != sst) continue;
+        for (int64_t i = h; i < A.cnext[h]; ++i)
+            if (A.dec[i] == 1 && aln_around(A, i, srb, sqb, slen, lq)) return true;
+    }
+    return false;
+}
+
+// mem_chain2aln for read r, resumed at its first open seed.  A seed to extend whose result
+// is not there stops the walk (decisions before it are final: they only depend on earlier
+// seeds); the later open seeds that are around no region yet are requested with it
+// (speculation: an extension result only ever replaces a kernel launch, the walk still
+// decides).  push(t) lists a requested seed; -> the number requested.
+template <class Push>
+AL_HD int aln_walk_read(const AlnDev &A, int64_t r, Push push) {
     const int64_t s0 = A.seed_off[r], s1 = A.seed_off[r + 1];
     int64_t k = A.resume[r];
     if (k >= s1) return 0;
@@ -186,29 +242,9 @@ AL_HD int aln_walk_read(const AlnDev &A, int64_t r) {
     for (; k < s1; ++k) {
         if (k > s0 && A.t_chain[k] != A.t_chain[k - 1]) c0 = k;
         if (A.dec[k]) continue;
-        const int slr = A.t_lr[k], sst = A.t_strand[k];
-        const int64_t srb = A.t_rbeg[k];   // strand coordinates: regions compared on one strand only
+        const int64_t srb = A.t_rbeg[k];
         const int sqb = A.t_qbeg[k], slen = A.t_slen[k];
-        bool around = false;
-        for (int64_t i = s0; i < k; ++i) {   // av: the regions made before this seed
-            if (A.dec[i] != 1) continue;
-            if (A.t_lr[i] != slr || A.t_strand[i] != sst) continue;   // other contig or strand: disjoint
-            const int pqb = A.o_qb[i], pqe = A.o_qe[i];
-            const int64_t prb = A.o_rb[i], pre = A.o_re[i];
-            if (srb < prb || srb + slen > pre || sqb < pqb || sqb + slen > pqe) continue;   // not contained
-            if ((double)(slen - A.t_slen[i]) > .1 * lq) continue;   // may give a better alignment
-            const int pw = A.o_w[i];
-            int64_t qd = sqb - pqb, rd = srb - prb;
-            int mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
-            int w = mg < pw ? mg : pw;
-            if (qd - rd < w && rd - qd < w) { around = true; break; }
-            qd = pqe - (sqb + slen);
-            rd = pre - (srb + slen);
-            mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
-            w = mg < pw ? mg : pw;
-            if (qd - rd < w && rd - qd < w) { around = true; break; }
-        }
-        if (around) {
+        if (aln_around_any(A, s0, c0, k, lq)) {
             bool other = false;   // a longer extended seed of the chain overlapping on another diagonal
             for (int64_t j = c0; j < k; ++j) {
                 if (A.dec[j] != 1) continue;
@@ -223,10 +259,21 @@ AL_HD int aln_walk_read(const AlnDev &A, int64_t r) {
                 continue;
             }
         }
-        if (!A.ext[k]) {   // extension needed: request it, resume here next round
+        if (!A.ext[k]) {   // extension needed: request it (and the likely ones after it), resume here
             A.sel[k] = SEL_EXT;
+            push(k);
+            int n = 1;
+            int64_t cc = c0;
+            for (int64_t kk = k + 1; kk < s1; ++kk) {
+                if (A.t_chain[kk] != A.t_chain[kk - 1]) cc = kk;
+                if (A.dec[kk] || A.ext[kk] || (A.sel[kk] & SEL_EXT)) continue;
+                if (aln_around_any(A, s0, cc, kk, lq)) continue;
+                A.sel[kk] = SEL_EXT;
+                push(kk);
+                ++n;
+            }
             A.resume[r] = (int32_t)k;
-            return 1;
+            return n;
         }
         A.dec[k] = 1;
     }

@@ -37,7 +37,9 @@ struct AlnDev {
     uint8_t *ext;              // 1: the task's extension result is available
     uint8_t *dec;              // mem_chain2aln's decision: 0 open, 1 extended (a region), 2 skipped
     int32_t *resume;           // [n_sr] first undecided seed of the read
-    int32_t *counter;          // [0] extension requests, [1] patch requests, [2] reads left
+    int32_t *counter;          // [0] extension requests, [1] patch requests, [3] first-round seeds
+    int32_t *tlist;            // [n_task] the seeds to extend in the next round (their count in counter)
+    int32_t *cnext;            // [n_task] of a chain's first seed: the next chain's first seed
     AlnReg *R;                 // [n_task] region scratch (read r: from seed_off[r])
     int32_t *ix;               // [n_task] sort scratch
     int32_t *pscore;           // [n_task] known patch scores of read r (from seed_off[r])

@@ -34,12 +34,16 @@ using namespace alnc;
 
 // ---------------------------------------------------------------- round 0
 __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < A.n_task; t += (int64_t)gridDim.x * blockDim.x) {
-        // rank-0 seeds: the first seed of a chain (seeds grouped by read, then chain)
-        const bool first = t == 0 || A.t_sr[t] != A.t_sr[t - 1] || A.t_chain[t] != A.t_chain[t - 1];
-        A.sel[t] = first ? SEL_EXT : 0;
-        A.ext[t] = 0;
-        A.dec[t] = 0;
+    const int lane = threadIdx.x & 63;
+    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < A.n_task; t0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = t0 + threadIdx.x;
+        const bool first = t < A.n_task && aln_init_task(A, t);
+        // one atomic per wave for the round-0 list (10 M first seeds on one counter otherwise)
+        const unsigned long long m = __ballot(first);
+        int base = 0;
+        if (lane == 0 && m) base = atomicAdd(&A.counter[3], __popcll(m));
+        base = __shfl(base, 0, 64);
+        if (first) A.tlist[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)t;
     }
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < A.n_sr; r += (int64_t)gridDim.x * blockDim.x) {
         A.resume[r] = (int32_t)A.seed_off[r];
@@ -52,7 +56,7 @@ __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
 // ---------------------------------------------------------------- mem_chain2aln
 __global__ void __launch_bounds__(256) aln_walk_kernel(AlnDev A) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < A.n_sr && aln_walk_read(A, r)) atomicAdd(&A.counter[0], 1);
+    if (r < A.n_sr) aln_walk_read(A, r, [&](int64_t t) { A.tlist[atomicAdd(&A.counter[0], 1)] = (int32_t)t; });
 }
 
 __global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A) {

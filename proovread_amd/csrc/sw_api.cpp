@@ -55,13 +55,13 @@ static const size_t SPILL_OFF = 96;   // in the SB_CELLS buffer: 3 x u64 overflo
 enum AlnBuf {
     SB_CHAIN = 35, SB_SEEDOFF, SB_SEL, SB_EXTF, SB_DEC, SB_RESUME, SB_ACNT, SB_AREG, SB_AIX, SB_PSCORE, SB_NPK,
     SB_FDONE, SB_PREQ, SB_NOUT, SB_OLIST, SB_OFLAG, SB_ATEMP, SB_AOFF, SB_ALIST, SB_AFLAG, SB_PPOOL, SB_GLIST,
-    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_NBUF
+    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_TLIST, SB_CNEXT, SB_NBUF
 };
-static_assert(SB_NBUF <= 64, "SwResident buffer table");
+static_assert(SB_NBUF <= 80, "SwResident buffer table");
 
 namespace prgpu {
 void sw_release(SwResident &r) {
-    for (int i = 0; i < 64; ++i) {
+    for (int i = 0; i < 80; ++i) {
         if (r.buf[i]) (void)hipFree(r.buf[i]);
         r.buf[i] = nullptr;
         r.cap[i] = 0;
@@ -177,6 +177,7 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
             (rc = ensure(r, SB_NOUT, r1 * 4)) || (rc = ensure(r, SB_OLIST, n1 * 4)) || (rc = ensure(r, SB_OFLAG, n1 * 4)) ||
             (rc = ensure(r, SB_AOFF, r1 * 8)) || (rc = ensure(r, SB_ALIST, n1 * 4)) || (rc = ensure(r, SB_AFLAG, n1 * 4)) ||
             (rc = ensure(r, SB_PREQ, 1024 * sizeof(AlnPatch))) || (rc = ensure(r, SB_CIGSLOT, n1 * 8)) ||
+            (rc = ensure(r, SB_TLIST, n1 * 4)) || (rc = ensure(r, SB_CNEXT, n1 * 4)) ||
             (rc = ensure(r, SB_CIGAT, n1 * 8)) || (rc = ensure(r, SB_PASS, n1)) || (rc = ensure(r, SB_CELLS, CELLS_BYTES)))
             return rc;
         size_t tb = aln_scan_temp_bytes(nt);
@@ -244,6 +245,8 @@ static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {
     A.dec = (uint8_t *)r.buf[SB_DEC];
     A.resume = (int32_t *)r.buf[SB_RESUME];
     A.counter = (int32_t *)r.buf[SB_ACNT];
+    A.tlist = (int32_t *)r.buf[SB_TLIST];
+    A.cnext = (int32_t *)r.buf[SB_CNEXT];
     A.R = (AlnReg *)r.buf[SB_AREG];
     A.ix = (int32_t *)r.buf[SB_AIX];
     A.pscore = (int32_t *)r.buf[SB_PSCORE];
@@ -277,11 +280,15 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     r.n_patch = 0;
     r.n_aln = 0;
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
+    HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
     if ((e = aln_launch_init(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     int32_t cnt[4] = {0, 0, 0, 0};
-    for (;;) {   // mem_chain2aln: every round extends the requested seeds, the walk resumes
-        HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
-        if (r.n_task) {
+    int64_t n_list = r.n_rank0;   // round 0: every chain's first seed (listed by the init kernel)
+    D.tsel = A.tlist;
+    for (;;) {   // mem_chain2aln: every round extends the listed seeds, the walk resumes
+        D.tsel_n = n_list;
+        HIPCHK(hipMemsetAsync(A.counter, 0, 8, s));
+        if (n_list) {
             e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s);
             if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         }
@@ -293,7 +300,9 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         if (getenv("PRGPU_BWA_DEBUG")) fprintf(stderr, "[bwa] round %d: %d requests\n", r.ext_rounds, cnt[0]);
         if (cnt[0] == 0) break;
         if (r.ext_rounds > r.n_task + 2) return pr_set_error(PR_ERR_HIP, "bwa mode: extension rounds do not converge");
+        n_list = cnt[0];
     }
+    D.tsel = nullptr;
     for (int round = 0;; ++round) {   // final pass; mem_patch_reg global scores in extra rounds
         HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
         if ((e = aln_launch_final(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
@@ -340,8 +349,11 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
                                 (int32_t *)r.buf[SB_AFLAG], r.buf[SB_ATEMP], r.cap[SB_ATEMP], (void *)s)))
         return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     HIPCHK(hipMemcpyAsync(&r.n_aln, (int64_t *)r.buf[SB_AOFF] + r.n_sr, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    D.tsel = (const int32_t *)r.buf[SB_ALIST];   // the CIGAR pass over the reported alignments
+    D.tsel_n = r.n_aln;
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
-    if (r.n_task) {
+    if (r.n_aln) {
         e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6),
                              (void *)ctx_event(c, 7));
         if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));

@@ -75,17 +75,22 @@ struct SwDev {
     // bwa mode (tasks = every seed of the kept chains): which tasks the extension phases
     // (bit SEL_EXT) and the CIGAR phases (bit SEL_CIG) take; null = all tasks in both
     const uint8_t *sel;
+    // bwa mode: the phases iterate this task list (tsel_n entries) instead of 0 .. n_task
+    const int32_t *tsel;
+    int64_t tsel_n;
 };
 constexpr uint8_t SEL_EXT = 1, SEL_CIG = 2;
 SW_HD inline bool sel_ext(const SwDev &D, int64_t t) { return !D.sel || (D.sel[t] & SEL_EXT); }
 SW_HD inline bool sel_cig(const SwDev &D, int64_t t) { return !D.sel || (D.sel[t] & SEL_CIG); }
+SW_HD inline int64_t sel_count(const SwDev &D) { return D.tsel ? D.tsel_n : D.n_task; }
+SW_HD inline int64_t sel_task(const SwDev &D, int64_t k) { return D.tsel ? (int64_t)D.tsel[k] : k; }
 
 struct SwResident {
     bool loaded = false;
     int64_t n_task = 0, n_sr = 0, n_lr = 0;
     int qmax = 0;
-    void *buf[64] = {};
-    size_t cap[64] = {};
+    void *buf[80] = {};
+    size_t cap[80] = {};
     // bwa mode (pr_sw_batch.t_chain): the tasks are seeds, the outputs reported alignments
     bool bwa = false;
     int64_t read_id0 = 0;

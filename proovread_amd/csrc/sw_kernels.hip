@@ -398,8 +398,9 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_ext_pk_kernel(SwDev D, SwOptsDe
 // after the left phases: qb, rb, score, truesc (mem_chain2aln); o_w holds aw[0]
 __global__ void sw_left_finish_kernel(SwDev D, SwOptsDev O) {
     unsigned long long cells = 0;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task;
-         t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sel_count(D);
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = sel_task(D, k);
         if (!sel_ext(D, t)) continue;
         const TaskGeo g = task_geo(D, O, t);
         int score, truesc, qb, rb, aw0 = O.w;
@@ -432,8 +433,9 @@ __global__ void sw_left_finish_kernel(SwDev D, SwOptsDev O) {
 // after the right phases: qe, re, score, truesc, w, pass
 __global__ void sw_right_finish_kernel(SwDev D, SwOptsDev O) {
     unsigned long long cells = 0;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task;
-         t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < sel_count(D);
+         k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = sel_task(D, k);
         if (!sel_ext(D, t)) continue;
         const TaskGeo g = task_geo(D, O, t);
         int score = D.o_score[t], truesc = D.o_truesc[t], qe, re, aw1 = O.w;
@@ -1006,7 +1008,8 @@ __global__ void __launch_bounds__(256) pk_order_count(SwDev D, SwOptsDev O, int 
     __shared__ int hist[PK_NB];
     for (int k = threadIdx.x; k < PK_NB; k += blockDim.x) hist[k] = 0;
     __syncthreads();
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = sel_task(D, q);
         const int k = pk_mode_key(D, O, t, mode);
         if (k >= 0) atomicAdd(&hist[k], 1);
     }
@@ -1040,7 +1043,8 @@ __global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O, in
     __shared__ int hist[PK_NB];
     for (int k = threadIdx.x; k < PK_NB; k += blockDim.x) hist[k] = 0;
     __syncthreads();
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = sel_task(D, q);
         const int k = pk_mode_key(D, O, t, mode);
         if (k >= 0) atomicAdd(&hist[k], 1);
     }
@@ -1048,7 +1052,8 @@ __global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O, in
     for (int k = threadIdx.x; k < PK_NB; k += blockDim.x)
         if (hist[k]) hist[k] = atomicAdd(&D.pk_bucket[k], hist[k]);
     __syncthreads();
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = sel_task(D, q);
         const int k = pk_mode_key(D, O, t, mode);
         if (k >= 0) D.list[atomicAdd(&hist[k], 1)] = (int32_t)t;
     }
@@ -1057,9 +1062,9 @@ int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *strea
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(D.pk_bucket, 0, (PK_SCAN + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
-    e = hipMemsetAsync(D.list, 0xFF, (size_t)(D.n_task + (int64_t)PK_NB * PK_SEG + 1) * sizeof(int32_t), s);
+    e = hipMemsetAsync(D.list, 0xFF, (size_t)(sel_count(D) + (int64_t)PK_NB * PK_SEG + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
-    int grid = (int)((D.n_task + 255) / 256);
+    int grid = (int)((sel_count(D) + 255) / 256);
     grid = grid < 2048 ? (grid > 0 ? grid : 1) : 2048;
     hipLaunchKernelGGL(pk_order_count, dim3(grid), dim3(256), 0, s, D, O, mode);
     hipLaunchKernelGGL(pk_order_scan, dim3(1), dim3(1024), 0, s, D.pk_bucket);
@@ -1096,7 +1101,8 @@ __global__ void __launch_bounds__(256) sw_order_count(SwDev D, SwOptsDev O, int 
     __shared__ int hist[SW_NBUCKET];
     for (int k = threadIdx.x; k < SW_NBUCKET; k += blockDim.x) hist[k] = 0;
     __syncthreads();
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = sel_task(D, q);
         const int k = sw_phase_key(D, O, t, phase);
         if (k >= 0) atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1);
     }
@@ -1131,7 +1137,8 @@ __global__ void __launch_bounds__(256) sw_order_scatter(SwDev D, SwOptsDev O, in
     __shared__ int hist[SW_NBUCKET];
     for (int k = threadIdx.x; k < SW_NBUCKET; k += blockDim.x) hist[k] = 0;
     __syncthreads();
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = sel_task(D, q);
         const int k = sw_phase_key(D, O, t, phase);
         if (k >= 0) atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1);
     }
@@ -1139,7 +1146,8 @@ __global__ void __launch_bounds__(256) sw_order_scatter(SwDev D, SwOptsDev O, in
     for (int k = threadIdx.x; k < SW_NBUCKET; k += blockDim.x)
         if (hist[k]) hist[k] = atomicAdd(&D.bucket[k], hist[k]);
     __syncthreads();
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < D.n_task; t += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = sel_task(D, q);
         const int k = sw_phase_key(D, O, t, phase);
         if (k >= 0) out[atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1)] = (int32_t)t;
     }
@@ -1149,7 +1157,7 @@ int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out,
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(D.bucket, 0, (SW_NBUCKET + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
-    int grid = (int)((D.n_task + 255) / 256);
+    int grid = (int)((sel_count(D) + 255) / 256);
     grid = grid < 2048 ? (grid > 0 ? grid : 1) : 2048;
     hipLaunchKernelGGL(sw_order_count, dim3(grid), dim3(256), 0, s, D, O, phase);
     hipLaunchKernelGGL(sw_order_scan, dim3(1), dim3(1024), 0, s, D.bucket);
@@ -1162,7 +1170,7 @@ int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *strea
 // the four extension phases + the two finish passes (mem_chain2aln)
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream) {
     hipStream_t s = (hipStream_t)stream;
-    int fgrid = (int)((D.n_task + 255) / 256);
+    int fgrid = (int)((sel_count(D) + 255) / 256);
     fgrid = fgrid < 8192 ? (fgrid > 0 ? fgrid : 1) : 8192;
     hipError_t e = hipMemsetAsync(D.x_try, 0, (size_t)D.n_task + 1, s);
     if (e != hipSuccess) return (int)e;

@@ -23,7 +23,7 @@ extern "C" int aln_host_run(const osw_opts *o, double drop_ratio, double mask_le
     std::vector<int64_t> seed_off(r1, 0);
     for (int64_t t = 0; t < n_task; ++t) ++seed_off[(size_t)t_sr[t] + 1];
     for (int i = 0; i < n_sr; ++i) seed_off[(size_t)i + 1] += seed_off[(size_t)i];
-    std::vector<int32_t> w(n1), resume(r1), pscore(n1), npk(r1);
+    std::vector<int32_t> w(n1), resume(r1), pscore(n1), npk(r1), tlist(n1), cnext(n1);
     std::vector<uint8_t> pass(n1), sel(n1), ext(n1), dec(n1), fdone(r1);
     std::vector<AlnReg> R(n1);
     std::vector<int32_t> ix(n1);
@@ -44,15 +44,13 @@ extern "C" int aln_host_run(const osw_opts *o, double drop_ratio, double mask_le
     A.resume = resume.data();
     A.R = R.data(); A.ix = ix.data(); A.pscore = pscore.data(); A.npk = npk.data(); A.fdone = fdone.data();
     A.nout = nout; A.olist = olist; A.oflag = oflag;
+    A.tlist = tlist.data(); A.cnext = cnext.data();
     A.a = o->a; A.b = o->b; A.o_del = o->o_del; A.e_del = o->e_del; A.o_ins = o->o_ins; A.e_ins = o->e_ins; A.w = o->w;
     A.max_chain_gap = max_chain_gap;
     A.min_score_per_base = o->min_score_per_base;
     A.drop_ratio = drop_ratio; A.mask_level = mask_level; A.mask_level_redun = mask_level_redun;
     // aln_init_kernel
-    for (int64_t t = 0; t < n_task; ++t) {
-        sel[(size_t)t] = (t == 0 || t_sr[t] != t_sr[t - 1] || t_chain[t] != t_chain[t - 1]) ? SEL_EXT : 0;
-        ext[(size_t)t] = dec[(size_t)t] = 0;
-    }
+    for (int64_t t = 0; t < n_task; ++t) alnc::aln_init_task(A, t);
     for (int r = 0; r < n_sr; ++r) resume[(size_t)r] = (int32_t)seed_off[(size_t)r];
     int64_t rounds = 0, n_ext = 0, n_patch = 0;
     for (;;) {   // the extension rounds (sw_launch_extend on SEL_EXT tasks, then the walk)
@@ -68,7 +66,7 @@ extern "C" int aln_host_run(const osw_opts *o, double drop_ratio, double mask_le
             ++n_ext;
         }
         int req = 0;
-        for (int r = 0; r < n_sr; ++r) req += alnc::aln_walk_read(A, r);
+        for (int r = 0; r < n_sr; ++r) req += alnc::aln_walk_read(A, r, [](int64_t) {});
         ++rounds;
         if (!req) break;
     }

@@ -65,12 +65,13 @@ def test_fantasticus_iteration(sample):
     tk = ix.map(sample["sr_seq"], sample["sr_off"], seed.default_opts(False), threads=4)
     tk2 = ix.map(sample["sr_seq"], sample["sr_off"], seed.default_opts(False), threads=1)
     assert np.array_equal(tk, tk2)
-    tk = tk[np.lexsort((tk["sr"], tk["lr"]))]
+    # bwa mode: every seed of the kept chains, bwa mem's per-read alignment on the oracle
     d = SimpleNamespace(lr_seq=sample["lr_seq"], lr_off=sample["lr_off"], sr_seq=sample["sr_seq"],
                         sr_off=sample["sr_off"], t_sr=tk["sr"].astype(np.int32), t_lr=tk["lr"].astype(np.int32),
                         t_strand=tk["strand"].astype(np.uint8), t_qbeg=tk["qbeg"].astype(np.int32),
                         t_rbeg=tk["rbeg"].astype(np.int32), t_slen=tk["slen"].astype(np.int32),
-                        n_lr=len(sample["seqs"]))
+                        t_chain=tk["chain"].astype(np.int32), n_lr=len(sample["seqs"]),
+                        n_sr=len(sample["sr_off"]) - 1)
     _, _, res, _ = cpu_chain.run_sample(d, range(d.n_lr), workers=4)
     km = _kmers(sample["G"])
     for name, raw, (rc, fq) in zip(sample["names"], sample["seqs"], res):
