@@ -22,6 +22,7 @@ Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import json
 import os
 import sys
@@ -130,11 +131,13 @@ def main():
     lr_bases = int(d.lr_off[-1])
     seed_info = None
 
-    def seed_front_end(ctx=None):
+    def seed_front_end(ctx=None, want_host_copy=True):
         """The front end (bwa-proovread index + mem seeding and chaining) on this rank's reads,
-        outside the timed region: the step measures the iteration from resident tasks.
-        ctx: index built in HBM and seeding on the GPU (checked against the host path on a
-        sample of reads); None: host C++ threads."""
+        outside the timed region: the step measures the iteration from resident seeds.
+        ctx: index built in HBM and seeding on the GPU, the seeds left in HBM for the
+        iteration (no host round trip); with want_host_copy they are also downloaded (CPU
+        baseline, and the check against the host path on a sample of reads).  None: host C++
+        threads."""
         from proovread_amd import seed as seeding
         o = seeding.default_opts(False)
         t = time.perf_counter()
@@ -144,20 +147,23 @@ def main():
             ix = seeding.DeviceSeedIndex(ctx, d.lr_seq, d.lr_off)
         t_ix = time.perf_counter() - t
         t = time.perf_counter()
+        tasks = None
         if ctx is None:
             tasks = ix.map(d.sr_seq, d.sr_off, o, threads=min(16, os.cpu_count() or 1))
             ms = ix_ms = None
             check = seed_phases = None
         else:
-            tasks, _ = ix.map(d.sr_seq, d.sr_off, o)
+            ix.map(d.sr_seq, d.sr_off, o, keep_on_device=True)
             ms, ix_ms = ix.gpu_ms(), ix.build_ms()
             seed_phases = ix.phase_ms()
         t_map = time.perf_counter() - t
         if ctx is None:
             ix.close()
-        else:
-            # parity of the GPU front end: the host path (host index + host seeding) on the
-            # first reads of the shard, task for task
+        elif want_host_copy:
+            # the same seeds downloaded (the kernel is deterministic; the device copy stays the
+            # iteration's input), and checked against the host path (host index + host seeding)
+            # on the first reads of the shard, seed for seed
+            tasks, _ = ix.map(d.sr_seq, d.sr_off, o)
             ns = min(d.n_sr, 20_000)
             hx = seeding.SeedIndex(d.lr_seq, d.lr_off)
             want = hx.map(d.sr_seq[:d.sr_off[ns]], d.sr_off[:ns + 1], o, threads=min(16, os.cpu_count() or 1))
@@ -166,13 +172,16 @@ def main():
             check = {"reads": int(ns), "tasks": int(len(want)), "equal": bool(np.array_equal(got, want))}
             if not check["equal"]:
                 raise SystemExit(f"bench: GPU seeding differs from the host path on the first {ns} reads")
+        else:
+            check = None
         info = {"path": "gpu" if ctx is not None else "host", "index_s": round(t_ix, 3), "map_s": round(t_map, 3),
                 "reads_per_s": round(d.n_sr / t_map, 1), "index_kernel_ms": ix_ms, "kernel_ms": ms,
-                "tasks": int(len(tasks)), "parity_vs_host": check,
-                "kernel_phase_ms_summed_over_waves": seed_phases}
-        if args.seeds != "truth":
+                "parity_vs_host": check, "kernel_phase_ms_summed_over_waves": seed_phases}
+        if tasks is not None:
+            info["tasks"] = int(len(tasks))
             info["chains"] = int((tasks["rank"] == 0).sum())
-        return synth.with_seeds(d, tasks), info
+            return synth.with_seeds(d, tasks), info
+        return dataclasses.replace(d, t_chain=np.zeros(0, np.int32)), info
 
     if args.seeds == "host":
         d, seed_info = seed_front_end()
@@ -190,11 +199,12 @@ def main():
     ctx = _abi.Context(local)
     cm = comm_mod.RcclComm.from_env(ctx) if world > 1 else None
     if args.seeds == "gpu":
-        d, seed_info = seed_front_end(ctx)
-        if want_cpu:   # the same GPU-seeded tasks, CPU chain in a child process
+        d, seed_info = seed_front_end(ctx, want_host_copy=rank == 0)
+        if want_cpu:   # the same GPU-made seeds, CPU chain in a child process
             cpu, cpu_res = cpu_baseline(d, args.cpu_lrs_per_worker)
     t_up = time.perf_counter()
-    it = iteration.Iteration(d, ctx=ctx)   # host -> HBM upload of reads and seeds (outside the step)
+    # host -> HBM upload of the reads; GPU seeds stay in HBM (outside the step)
+    it = iteration.Iteration(d, ctx=ctx, gpu_seeds=args.seeds == "gpu")
     upload_s = time.perf_counter() - t_up
     opts = sw.default_opts(finish=False)
     opts.bin_size, opts.bin_length = BIN_FILTER     # bwa-proovread -b 20 -l 300 (proovread:1302-1313)
@@ -279,7 +289,7 @@ def main():
             "workload": "configs[1] per GPU: 4.6 Mb genome, 13,800 x 10 kb long reads (30x, 15% error), "
                         "50x 2x150 short reads sampled to 15x for one bwa-sr iteration",
             "genome_bp": gl, "long_reads_per_gpu": d.n_lr, "long_read_bases_per_gpu": lr_bases,
-            "short_reads_per_gpu": d.n_sr, "seeds_per_gpu": int(len(d.t_sr)), "task": "bwa-sr-1",
+            "short_reads_per_gpu": d.n_sr, "seeds_per_gpu": it.n_task, "task": "bwa-sr-1",
             "coverage_cap": params.coverage, "parallelism": f"long-read shards x{world}",
         },
         "sw_gcups": round(cells / ((ms[0] + ms[1]) * 1e-3) / 1e9, 2),
@@ -314,7 +324,7 @@ def main():
         "cpu_baseline": cpu,
         "seeding": seed_info,
         # one whole bwa-sr iteration as proovread runs it, wall clock: index build + seeding
-        # (host C++ threads, bwa-proovread index / mem front end) + upload + the timed step
+        # (bwa-proovread index / mem front end; seeds left in HBM) + upload + the timed step
         "iteration_end_to_end_ms": (round((seed_info["index_s"] + seed_info["map_s"] + upload_s) * 1e3 +
                                           el / args.steps * 1e3, 1) if seed_info else None),
         "upload_ms": round(upload_s * 1e3, 1),

@@ -346,12 +346,13 @@ int pr_seed_index_occ(const pr_seed_index *h, const uint8_t *s, int n, int64_t *
 int pr_seed_index_digest(const pr_seed_index *h, uint64_t *out6);
 int pr_seed_smem(const pr_seed_index *h, const uint8_t *q, int len, int x, int64_t min_intv, int32_t *start,
                  int32_t *end, int64_t *occ, int cap, int *n_out);
-/* The GPU seeding path (seed_kernels.hip: the same per-read core, one lane per read,
- * fixed scratch per lane).  pr_seed_gpu_upload copies a built index into the context's
- * HBM; pr_seed_gpu_map seeds n_sr reads (nt4 codes) into library-owned tasks in read
- * order; status[i] (may be NULL) is 0 or the overflow flags of a read whose work
- * outgrew the lane scratch (it then has no tasks, and the call returns PR_ERR_CAPACITY
- * after filling everything else). */
+/* The GPU seeding path (seed_kernels.hip: the same per-read core; pass 1 64 reads per wave,
+ * pass 2 one wave per read for the reads that outgrew pass 1's scratch).  pr_seed_gpu_upload
+ * copies a built index into the context's HBM; pr_seed_gpu_map seeds n_sr reads (nt4 codes)
+ * into library-owned tasks in read order (out = NULL: the tasks stay in HBM for
+ * pr_iter_upload_gpu_seeds); status[i] (may be NULL) is 0 or the overflow flags of a read
+ * whose work outgrew the scratch (it then has no tasks, and the call returns
+ * PR_ERR_CAPACITY after filling everything else). */
 int pr_seed_gpu_upload(pr_ctx *ctx, const pr_seed_index *h);
 int pr_seed_gpu_map(pr_ctx *ctx, const pr_seed_opts *o, const uint8_t *sr_seq, const int64_t *sr_off, int n_sr,
                     pr_seed_tasks *out, int32_t *status);
@@ -364,6 +365,9 @@ int pr_seed_gpu_index_build(pr_ctx *ctx, const uint8_t *lr_seq, const int64_t *l
 int pr_seed_gpu_index_digest(pr_ctx *ctx, uint64_t *out6);
 /* milliseconds of the last pr_seed_gpu_index_build (HIP events on the ctx stream) */
 int pr_seed_gpu_index_last_ms(pr_ctx *ctx, double *ms);
+/* reads of the last pr_seed_gpu_map that outgrew pass 1's small scratch slices (64 reads per
+ * wave, lane per read) and ran in pass 2 (one wave per read, the large slices) */
+int pr_seed_gpu_pass2_reads(pr_ctx *ctx, int64_t *n);
 /* milliseconds of the last pr_seed_gpu_map kernel (HIP events on the ctx stream) */
 int pr_seed_gpu_last_ms(pr_ctx *ctx, double *ms);
 /* Diagnostics: wall-clock ticks (100 MHz) of the last pr_seed_gpu_map summed over waves:
@@ -389,6 +393,10 @@ typedef struct pr_iter_batch {
                                    * to .masked.fa, bam2cns reads the unmasked .fq)             */
 } pr_iter_batch;
 int pr_iter_upload(pr_ctx *ctx, const pr_iter_batch *b);
+/* bwa mode straight from the device seeding: the seeds of the last pr_seed_gpu_map called with
+ * out = NULL (they stay in HBM, no host round trip) are the tasks; b->sw gives the reads (the
+ * same short reads, sr pool + offsets) and the long reads, its task fields are ignored. */
+int pr_iter_upload_gpu_seeds(pr_ctx *ctx, const pr_iter_batch *b);
 int pr_iter_launch(pr_ctx *ctx, const pr_sw_opts *o, const pr_cns_params *p);   /* async */
 int pr_iter_download(pr_ctx *ctx, pr_cns_out *out);   /* consensus outputs, syncs */
 int pr_iter_bounds(pr_ctx *ctx, int32_t *n_lr, int64_t *n_task, pr_cns_bounds *bd);

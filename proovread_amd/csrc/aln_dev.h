@@ -5,6 +5,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "../../include/prgpu.h"
 #include "sw_dev.h"
 
 namespace prgpu {
@@ -71,5 +72,10 @@ int aln_launch_group_lr(const int32_t *alist, const int32_t *t_lr, int64_t n, in
                         int32_t *out_list, int32_t *cnt, int64_t *lr_off, int64_t *tmp_in, void *temp,
                         size_t temp_bytes, void *stream);
 size_t aln_group_temp_bytes(int64_t n, int32_t n_lr);
+// the dense seed list of pr_seed_gpu_map (pr_seed_task AoS) -> the SW task columns; n_first[0]
+// += the seeds of rank 0 (every chain's first seed)
+int aln_launch_unpack_seeds(const pr_seed_task *src, int64_t n, int32_t *sr, int32_t *lr, uint8_t *strand,
+                            int32_t *qbeg, int32_t *rbeg, int32_t *slen, int32_t *chain, int32_t *n_first,
+                            void *stream);
 
 }  // namespace prgpu

@@ -137,6 +137,29 @@ __global__ void __launch_bounds__(256) sw_gather_kernel(SwGather G) {
     }
 }
 
+__global__ void __launch_bounds__(256) aln_unpack_kernel(const pr_seed_task *src, int64_t n, int32_t *sr, int32_t *lr,
+                                                         uint8_t *strand, int32_t *qbeg, int32_t *rbeg, int32_t *slen,
+                                                         int32_t *chain, int32_t *n_first) {
+    const int lane = threadIdx.x & 63;
+    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < n; t0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t t = t0 + threadIdx.x;
+        bool first = false;
+        if (t < n) {
+            const pr_seed_task x = src[t];
+            sr[t] = x.sr;
+            lr[t] = x.lr;
+            strand[t] = (uint8_t)x.strand;
+            qbeg[t] = x.qbeg;
+            rbeg[t] = x.rbeg;
+            slen[t] = x.slen;
+            chain[t] = x.chain;
+            first = x.rank == 0;
+        }
+        const unsigned long long m = __ballot(first);
+        if (lane == 0 && m) atomicAdd(n_first, __popcll(m));
+    }
+}
+
 static int grid_of(int64_t n, int cap = 8192) {
     int64_t g = (n + 255) / 256;
     return (int)(g < 1 ? 1 : (g > cap ? cap : g));
@@ -167,6 +190,15 @@ int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, 
 int sw_launch_gather(const SwGather &G, void *stream) {
     if (G.n <= 0) return 0;
     hipLaunchKernelGGL(sw_gather_kernel, dim3(grid_of(G.n)), dim3(256), 0, (hipStream_t)stream, G);
+    return (int)hipGetLastError();
+}
+
+int aln_launch_unpack_seeds(const pr_seed_task *src, int64_t n, int32_t *sr, int32_t *lr, uint8_t *strand,
+                            int32_t *qbeg, int32_t *rbeg, int32_t *slen, int32_t *chain, int32_t *n_first,
+                            void *stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(aln_unpack_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, src, n, sr, lr, strand,
+                       qbeg, rbeg, slen, chain, n_first);
     return (int)hipGetLastError();
 }
 

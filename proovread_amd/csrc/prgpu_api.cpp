@@ -22,6 +22,7 @@
 using namespace prgpu;
 int sw_get_ptrs(pr_ctx *c, SwPtrs *p);
 int sw_get_pipe_ptrs(pr_ctx *c, SwPtrs *p, bool regroup);
+int sw_upload_device_seeds(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h);
 
 static thread_local std::string g_err;
 static int set_error(int code, const char *fmt, ...) {
@@ -95,6 +96,8 @@ struct pr_ctx {
     bool cns_loaded = false;
     int32_t n_lr = 0;
     int64_t n_aln = 0, total_cols = 0, n_bins = 0, seq_cap = 0, chim_cap = 0;
+    int64_t seed_pass2 = 0;   // reads of the last pr_seed_gpu_map that needed the large slices
+    std::vector<int64_t> seed_pre;   // per-read prefix of the last pr_seed_gpu_map's seeds (SB_DENSE)
     int64_t alg_bytes = 0;
     int64_t k_need = 0;   // per-read bound of kept alignments (K pool slices)
     bool has_ref = false, has_qual = false, has_ign = false;
@@ -534,11 +537,19 @@ extern "C" int pr_cns_resident_stats(pr_ctx *c, int64_t *columns, int64_t *alg_b
 
 // ---------------------------------------------------------------------------
 // one iteration on the device: SW -> assemble -> consensus (pr_iter_*)
-extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
+static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds) {
     if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
-    const pr_sw_batch &sb = b->sw;
+    pr_sw_batch sbv = b->sw;
+    if (gpu_seeds) {   // the seeds of the last pr_seed_gpu_map, still in HBM
+        if (c->seed_pre.size() != (size_t)sbv.n_sr + 1)
+            return set_error(PR_ERR_ARG, "no device seeds for these short reads (pr_seed_gpu_map with out = NULL first)");
+        sbv.n_task = c->seed_pre.back();
+        sbv.t_sr = sbv.t_lr = sbv.t_qbeg = sbv.t_rbeg = sbv.t_slen = sbv.t_chain = nullptr;
+        sbv.t_strand = nullptr;
+    }
+    const pr_sw_batch &sb = sbv;
     const int n = sb.n_lr;
-    const bool bwa = sb.t_chain != nullptr;   // seeds in, alignments grouped by long read on the device
+    const bool bwa = sb.t_chain != nullptr || gpu_seeds;   // seeds in, alignments grouped by long read on the device
     if (!bwa && (!b->task_lr_off || b->task_lr_off[0] != 0 || b->task_lr_off[n] != sb.n_task))
         return set_error(PR_ERR_ARG, "task_lr_off must partition the tasks");
     int maxt = 1;
@@ -550,7 +561,8 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
         if (k > maxt) maxt = (int)k;
     }
     if (maxt > 16384) return set_error(PR_ERR_CAPACITY, "more than 16384 tasks on one long read");
-    int rc = pr_sw_upload(c, &sb);
+    int rc = gpu_seeds ? sw_upload_device_seeds(c, &sb, c->sd[SB_DENSE].as<pr_seed_task>(), c->seed_pre.data())
+                       : pr_sw_upload(c, &sb);
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
     c->cns_launched = false;
@@ -615,6 +627,9 @@ extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) {
     c->pipe = true;
     return 0;
 }
+
+extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) { return iter_upload(c, b, false); }
+extern "C" int pr_iter_upload_gpu_seeds(pr_ctx *c, const pr_iter_batch *b) { return iter_upload(c, b, true); }
 
 extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_params *p) {
     if (!c || !o || !p) return set_error(PR_ERR_ARG, "null arg");
@@ -1136,7 +1151,11 @@ extern "C" int pr_seed_gpu_index_last_ms(pr_ctx *c, double *ms) {
 
 extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *sr_seq, const int64_t *sr_off, int n_sr,
                                pr_seed_tasks *out, int32_t *status) {
-    if (!c || !o || !out || n_sr < 0 || (n_sr && (!sr_seq || !sr_off))) return set_error(PR_ERR_ARG, "null arg");
+    if (!c || !o || n_sr < 0 || (n_sr && (!sr_seq || !sr_off))) return set_error(PR_ERR_ARG, "null arg");
+    pr_seed_tasks dummy;
+    const bool keep_on_device = out == nullptr;
+    if (!out) out = &dummy;
+    c->seed_pre.clear();
     if (!c->seed_loaded) return set_error(PR_ERR_ARG, "no seed index on the device (pr_seed_gpu_upload)");
     if (o->min_seed_len < seedc::KI) return set_error(PR_ERR_UNSUPPORTED, "min seed length below the 12-mer index");
     if (o->max_occ <= 0 || o->w < 0) return set_error(PR_ERR_ARG, "bad seeding options");
@@ -1149,25 +1168,33 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     hipStream_t s = c->stream;
     DevBuf *D = c->sd;
     const seedc::Caps caps = seedc::device_caps();
+    int qmax = 1;
+    for (int i = 0; i < n_sr; ++i) qmax = std::max<int>(qmax, (int)(sr_off[i + 1] - sr_off[i]));
+    // pass 1: 64 reads per wave, small slices sized for the batch; pass 2 (flagged reads): the
+    // large slices, one wave per read
+    seedc::Caps small = seedc::device_caps_small(std::min(qmax, caps.lmax));
+    if (const char *sc = getenv("PRGPU_SEED_SMALL"))   // tuning hook: hits,iv,mems,seeds,chains
+        sscanf(sc, "%d,%d,%d,%d,%d", &small.hits, &small.iv, &small.mems, &small.seeds, &small.chains);
     SeedDev K{};
     K.V = c->seed_view;
     K.O = *o;
     K.n_sr = n_sr;
-    K.caps = caps;
-    K.stride = seedc::scratch_bytes(caps);
-    // scratch slots: one per resident wave (a wave maps one read at a time; 12 per CU at
-    // the kernel's register use), ~0.45 MB each (~1.4 GB at 256 CUs)
-    int64_t lanes = (int64_t)c->n_cu * seed_slots_per_cu();
-    if (lanes > n_sr) lanes = n_sr;
-    if (lanes < 1) lanes = 1;
-    K.n_lanes = lanes;
+    K.caps = small;
+    K.stride = seedc::scratch_bytes(small);
+    const char *wpc = getenv("PRGPU_SEED_WAVES_PER_CU");   // tuning hook
+    int64_t waves = (int64_t)c->n_cu * (wpc ? atoi(wpc) : 16);   // ~78 KB x 64 slices per wave at 150 bp
+    if (waves > (n_sr + 63) / 64) waves = (n_sr + 63) / 64;
+    if (waves < 1) waves = 1;
+    K.n_lanes = waves;
+    int64_t lanes2 = (int64_t)c->n_cu * seed_slots_per_cu();
+    const int64_t scratch = std::max<int64_t>(waves * 64 * K.stride, lanes2 * seedc::scratch_bytes(caps));
     const int64_t nb = n_sr ? sr_off[n_sr] : 0;
     int rc;
     if ((rc = upload(D[SB_SEQ], sr_seq, (size_t)nb, s)) || (rc = upload(D[SB_OFF], sr_off, (size_t)n_sr + 1, s)) ||
-        (rc = D[SB_SCRATCH].ensure((size_t)(lanes * K.stride))) ||
+        (rc = D[SB_SCRATCH].ensure((size_t)scratch)) ||
         (rc = D[SB_OUT].ensure((size_t)n_sr * caps.out * sizeof(pr_seed_task) + 16)) ||
         (rc = D[SB_NOUT].ensure((size_t)n_sr * 4 + 16)) || (rc = D[SB_STATUS].ensure((size_t)n_sr * 4 + 16)) ||
-        (rc = D[SB_NEXT].ensure(128)))
+        (rc = D[SB_NEXT].ensure(128)) || (rc = D[SB_PRE].ensure(((size_t)n_sr + 1) * 8)))
         return rc;
     K.sr_seq = D[SB_SEQ].as<uint8_t>();
     K.sr_off = D[SB_OFF].as<int64_t>();
@@ -1179,8 +1206,29 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     K.prof = reinterpret_cast<unsigned long long *>(D[SB_NEXT].as<uint8_t>() + 64);
     HIPCHK(hipMemsetAsync(K.next, 0, 128, s));
     HIPCHK(hipEventRecord(c->ev[8], s));
-    const int e = seed_launch(K, (void *)s);
+    int e = seed_batch_launch(K, (void *)s);
     if (e) return set_error(PR_ERR_HIP, "seed kernel: %s", hipGetErrorString((hipError_t)e));
+    {
+        std::vector<int32_t> st1((size_t)n_sr);
+        if ((rc = download(st1.data(), D[SB_STATUS], (size_t)n_sr, s))) return rc;
+        HIPCHK(hipStreamSynchronize(s));
+        std::vector<int32_t> redo;
+        for (int i = 0; i < n_sr; ++i)
+            if (st1[(size_t)i]) redo.push_back(i);
+        c->seed_pass2 = (int64_t)redo.size();
+        if (!redo.empty()) {   // pass 2 over the flagged reads (rlist in SB_PRE, rewritten later)
+            HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
+            K.caps = caps;
+            K.stride = seedc::scratch_bytes(caps);
+            K.n_lanes = std::min<int64_t>(lanes2, (int64_t)redo.size());
+            K.rlist = D[SB_PRE].as<int32_t>();
+            K.n_list = (int64_t)redo.size();
+            e = seed_launch(K, (void *)s);
+            if (e) return set_error(PR_ERR_HIP, "seed kernel (pass 2): %s", hipGetErrorString((hipError_t)e));
+            HIPCHK(hipStreamSynchronize(s));
+        }
+    }
     HIPCHK(hipEventRecord(c->ev[9], s));
     std::vector<int32_t> nout((size_t)n_sr), st((size_t)n_sr);
     if ((rc = download(nout.data(), D[SB_NOUT], (size_t)n_sr, s)) || (rc = download(st.data(), D[SB_STATUS], (size_t)n_sr, s)))
@@ -1203,6 +1251,13 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     const int e2 = seed_compact_launch(D[SB_OUT].as<pr_seed_task>(), D[SB_NOUT].as<int32_t>(), D[SB_PRE].as<int64_t>(),
                                        n_sr, caps.out, D[SB_DENSE].as<pr_seed_task>(), (void *)s);
     if (e2) return set_error(PR_ERR_HIP, "seed compaction: %s", hipGetErrorString((hipError_t)e2));
+    c->seed_pre = pre;
+    if (keep_on_device) {   // the seeds stay in HBM for pr_iter_upload_gpu_seeds
+        HIPCHK(hipStreamSynchronize(s));
+        if (status) std::memcpy(status, st.data(), (size_t)n_sr * 4);
+        if (bad) return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags)", (long long)bad);
+        return 0;
+    }
     out->t = (pr_seed_task *)std::malloc(sizeof(pr_seed_task) * (size_t)(total > 0 ? total : 1));
     if (!out->t) return set_error(PR_ERR_ARG, "out of host memory");
     if (total && (rc = download(out->t, D[SB_DENSE], (size_t)total, s))) return rc;
@@ -1210,6 +1265,12 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     out->n = total;
     if (status) std::memcpy(status, st.data(), (size_t)n_sr * 4);
     if (bad) return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags)", (long long)bad);
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_pass2_reads(pr_ctx *c, int64_t *n) {
+    if (!c || !n) return set_error(PR_ERR_ARG, "null arg");
+    *n = c->seed_pass2;
     return 0;
 }
 

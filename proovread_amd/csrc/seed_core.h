@@ -624,6 +624,11 @@ struct Caps {
     int32_t lmax, hits, iv, mems, seeds, chains, out;
 };
 SC_HD Caps device_caps() { return Caps{1024, 8192, 256, 1024, 4096, 2048, 384}; }
+// pass 1 of the device path: 64 slices per wave, sized for reads of <= lmax bases
+SC_HD Caps device_caps_small(int lmax) {
+    const int l = lmax < 16 ? 16 : (lmax + 15) & ~15;
+    return Caps{l, 4096, 64, 256, 512, 256, 384};
+}
 
 SC_HD int64_t align8(int64_t x) { return (x + 7) & ~(int64_t)7; }
 

@@ -18,15 +18,19 @@ struct SeedDev {
     int64_t stride;            // seedc::scratch_bytes(caps), 8-byte multiple
     int64_t n_lanes;           // scratch slots = resident waves (one read per wave at a time)
     int32_t *next;             // read counter the waves dequeue from (zeroed before the launch)
-    unsigned long long *prof;  // [8] wall-clock ticks summed over waves: occurrence table, SMEMs,
-                               // chaining, filter + output (may be null)
+    unsigned long long *prof;  // [8] wall-clock ticks summed over waves: occurrence tables, SMEMs
+                               // (pass 1: the whole lane-per-read phase), chaining and filter +
+                               // output of pass 2 (may be null)
     seedc::Caps caps;
     pr_seed_task *out;         // [n_sr * caps.out]
     int32_t *n_out;            // [n_sr]
     int32_t *status;           // [n_sr] 0 or SC_OVER_* bits
+    const int32_t *rlist;      // pass 2: the reads to map (n_list of them); null: 0 .. n_list
+    int64_t n_list;
 };
 
-int seed_launch(const SeedDev &D, void *stream);
+int seed_launch(const SeedDev &D, void *stream);         // pass 2: one wave per read of rlist
+int seed_batch_launch(const SeedDev &D, void *stream);   // pass 1: 64 reads per wave, lane per read
 // resident waves per CU of the seeding kernel (= scratch slots per CU)
 int seed_slots_per_cu();
 // dense task list: out[pre[i] + j] = slots[i * cap + j] for j < n_out[i]

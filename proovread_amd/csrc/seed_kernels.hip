@@ -2,18 +2,15 @@
 // 64-lane wave per short read.  The index (text, 12-mer hit lists with the 28 bases
 // after every hit, count tables) is resident in HBM.
 //
-// Per read (a wave, persistent: waves dequeue reads from a counter):
-//   1. occurrence table, wave-parallel: lanes over the read's starts compute the 12-mer
-//      code, the packed bases after it and the start's hit count; a wave scan gives the
-//      start offsets (kept in LDS for the lookup below); lanes over the read's ~3k hits
-//      (consecutive hits -> coalesced kpos / kext loads) compute each hit's exact match
-//      length (LCP with the packed bases, then the text past them) and count it into the
-//      start's match-length histogram; a per-start suffix sum makes the count table.
-//      This is build_occ's table without its diagonal shortcut (same match lengths).
+// Pass 1 (seed_batch_kernel, persistent waves dequeue 64 reads at a time):
+//   1. the 64 occurrence tables, one after the other, each wave-parallel (build_occ_wave)
 //   2. SMEMs, re-seeding, -y seeds, chaining, chain filter, task output: seed_core.h's
-//      map_after_occ on lane 0 (sequential decisions; the wave's scratch slice is small
-//      and L2-resident).  A read whose work outgrows the slice is reported with its
-//      SC_OVER_* flags and no tasks.
+//      map_after_occ, one lane per read (sequential, latency-bound decisions; 64 reads'
+//      loads in flight per wave).  Scratch slices are sized for the batch's reads; a read
+//      that outgrows its slice is flagged.
+// Pass 2 (seed_wave_kernel, the flagged reads): one wave per read with the large slice,
+// map_after_occ on lane 0.  A read that still outgrows it is reported with its SC_OVER_*
+// flags and no tasks.
 #include <hip/hip_runtime.h>
 
 #include "seed_core.h"
@@ -30,6 +27,106 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// The occurrence table of read q (len bases) in S, wave-parallel (all 64 lanes): lanes over the
+// read's starts compute the 12-mer code, the packed bases after it and the start's hit count; a
+// wave scan gives the start offsets (also kept in LDS `ho` for the lookup below); lanes over the
+// read's hits (consecutive hits -> coalesced kpos / kext loads) compute each hit's exact match
+// length (LCP with the packed bases, then the text past them) and count it into the start's
+// match-length histogram; a per-start suffix sum makes the count table.  This is
+// build_occ's table without its diagonal shortcut (same match lengths).  -> 0 or SC_OVER_HITS.
+__device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, const uint8_t *q, int len, int32_t *ho,
+                              int lane) {
+    using seedc::HB;
+    using seedc::KI;
+    using seedc::KX;
+    int err = 0;
+    for (int64_t k = lane; k < (int64_t)len * HB; k += 64) S.ge[k] = 0u;
+    int run = 0;
+    for (int a0 = 0; a0 <= len; a0 += 64) {
+        const int a = a0 + lane;
+        int ca = 0;
+        if (a <= len) {
+            int32_t code_a = -1;
+            uint64_t qe = 0;
+            if (a + KI <= len) {
+                uint32_t code = 0;
+                bool ok = true;
+                for (int x = 0; x < KI; ++x) {
+                    const uint8_t c = q[a + x];
+                    ok &= c < 4;
+                    code = (code << 2) | (c & 3u);
+                }
+                const int n = len - a - KI;
+                qe = seedc::pack_ext(q + a + KI, n < KX ? n : KX);
+                if (ok) {
+                    code_a = (int32_t)code;
+                    ca = (int)(V.koff[code + 1] - V.koff[code]);
+                }
+            }
+            S.codes[a] = code_a;
+            S.qext[a] = qe;
+        }
+        int x = ca;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        const int ex = run + x - ca;
+        if (a <= len) {
+            ho[a] = ex;
+            S.hoff[a] = ex;
+        }
+        run += __shfl(x, 63, 64);
+    }
+    const int nh = run;
+    if (nh > S.cap_hits) err = seedc::SC_OVER_HITS;
+    wave_sync_lds();
+    __threadfence_block();
+    if (!err) {
+        const int amax = len - KI;   // last start with a 12-mer
+        for (int k = lane; k < nh; k += 64) {
+            int lo = 0, hi = amax;   // last start whose hits begin at or before k
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (ho[mid] <= k) lo = mid; else hi = mid - 1;
+            }
+            const int a = lo;
+            const uint32_t code = (uint32_t)S.codes[a];
+            const uint32_t r = V.koff[code] + (uint32_t)(k - ho[a]);
+            const uint32_t p = V.kpos[r];
+            const uint64_t exb = V.kext[r];
+            const uint64_t qe = S.qext[a];
+            const int le = (int)(exb >> 56), lq = (int)(qe >> 56);
+            const uint64_t xd = (exb ^ qe) & seedc::KX_MASK;
+            int m = xd ? seedc::ctz64(xd) >> 1 : KX;
+            m = m < le ? m : le;
+            m = m < lq ? m : lq;
+            int ml = KI + m;
+            if (m == KX)
+                while (a + ml < len && q[a + ml] < 4 && V.text[p + ml] == q[a + ml]) ++ml;
+            S.hpos[k] = p;
+            S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
+            atomicAdd(&S.ge[(int64_t)a * HB + (ml - KI < HB - 1 ? ml - KI : HB - 1)], 1u);
+        }
+        __threadfence_block();
+        for (int a = lane; a + KI <= len; a += 64) {
+            if (S.codes[a] < 0) continue;
+            uint32_t *g = S.ge + (int64_t)a * HB;
+            uint32_t acc = 0;
+            for (int t = HB - 1; t >= 0; --t) {
+                acc += g[t];
+                g[t] = acc;
+            }
+        }
+        __threadfence_block();
+    }
+    wave_sync_lds();
+    return err;
+}
+
+// Pass 2: one wave per read with the large scratch slice (the reads of D.rlist: those that
+// outgrew pass 1's slices), the sequential part on lane 0.
 __global__ void __launch_bounds__(64 * SEED_WAVES) seed_wave_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -37,119 +134,91 @@ __global__ void __launch_bounds__(64 * SEED_WAVES) seed_wave_kernel(SeedDev D) {
     if (slot >= D.n_lanes) return;
     seedc::Scratch S = seedc::carve(D.scratch + slot * D.stride, D.caps);
     int32_t *ho = hoff_lds[wv];
-    const seedc::IndexView &V = D.V;
     unsigned long long pt[4] = {0ULL, 0ULL, 0ULL, 0ULL};   // lane 0: phase ticks of this wave
-    using seedc::HB;
-    using seedc::KI;
-    using seedc::KX;
     for (;;) {
-        int i = 0;
-        if (lane == 0) i = atomicAdd(D.next, 1);
-        i = __shfl(i, 0, 64);
-        if (i >= D.n_sr) {   // every wave reaches this: the grid drains
+        int j = 0;
+        if (lane == 0) j = atomicAdd(D.next, 1);
+        j = __shfl(j, 0, 64);
+        if (j >= D.n_list) {   // every wave reaches this: the grid drains
             if (D.prof && lane == 0)
                 for (int k = 0; k < 4; ++k) atomicAdd(&D.prof[k], pt[k]);
             break;
         }
+        const int i = D.rlist ? D.rlist[j] : j;
         const int64_t o = D.sr_off[i];
         const int len = (int)(D.sr_off[i + 1] - o);
         const uint8_t *q = D.sr_seq + o;
         int err = 0;
         const unsigned long long t0 = D.prof && lane == 0 ? wall_clock64() : 0ULL;
         if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
-        if (len > 0 && !err) {
-            // ---- 1. occurrence table
-            for (int64_t k = lane; k < (int64_t)len * HB; k += 64) S.ge[k] = 0u;
-            int run = 0;
-            for (int a0 = 0; a0 <= len; a0 += 64) {
-                const int a = a0 + lane;
-                int ca = 0;
-                if (a <= len) {
-                    int32_t code_a = -1;
-                    uint64_t qe = 0;
-                    if (a + KI <= len) {
-                        uint32_t code = 0;
-                        bool ok = true;
-                        for (int x = 0; x < KI; ++x) {
-                            const uint8_t c = q[a + x];
-                            ok &= c < 4;
-                            code = (code << 2) | (c & 3u);
-                        }
-                        const int n = len - a - KI;
-                        qe = seedc::pack_ext(q + a + KI, n < KX ? n : KX);
-                        if (ok) {
-                            code_a = (int32_t)code;
-                            ca = (int)(V.koff[code + 1] - V.koff[code]);
-                        }
-                    }
-                    S.codes[a] = code_a;
-                    S.qext[a] = qe;
-                }
-                int x = ca;
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const int y = __shfl_up(x, d, 64);
-                    if (lane >= d) x += y;
-                }
-                const int ex = run + x - ca;
-                if (a <= len) {
-                    ho[a] = ex;
-                    S.hoff[a] = ex;
-                }
-                run += __shfl(x, 63, 64);
-            }
-            const int nh = run;
-            if (nh > S.cap_hits) err = seedc::SC_OVER_HITS;
-            wave_sync_lds();
-            __threadfence_block();
-            if (!err) {
-                const int amax = len - KI;   // last start with a 12-mer
-                for (int k = lane; k < nh; k += 64) {
-                    int lo = 0, hi = amax;   // last start whose hits begin at or before k
-                    while (lo < hi) {
-                        const int mid = (lo + hi + 1) >> 1;
-                        if (ho[mid] <= k) lo = mid; else hi = mid - 1;
-                    }
-                    const int a = lo;
-                    const uint32_t code = (uint32_t)S.codes[a];
-                    const uint32_t r = V.koff[code] + (uint32_t)(k - ho[a]);
-                    const uint32_t p = V.kpos[r];
-                    const uint64_t exb = V.kext[r];
-                    const uint64_t qe = S.qext[a];
-                    const int le = (int)(exb >> 56), lq = (int)(qe >> 56);
-                    const uint64_t xd = (exb ^ qe) & seedc::KX_MASK;
-                    int m = xd ? seedc::ctz64(xd) >> 1 : KX;
-                    m = m < le ? m : le;
-                    m = m < lq ? m : lq;
-                    int ml = KI + m;
-                    if (m == KX)
-                        while (a + ml < len && q[a + ml] < 4 && V.text[p + ml] == q[a + ml]) ++ml;
-                    S.hpos[k] = p;
-                    S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
-                    atomicAdd(&S.ge[(int64_t)a * HB + (ml - KI < HB - 1 ? ml - KI : HB - 1)], 1u);
-                }
-                __threadfence_block();
-                for (int a = lane; a + KI <= len; a += 64) {
-                    if (S.codes[a] < 0) continue;
-                    uint32_t *g = S.ge + (int64_t)a * HB;
-                    uint32_t acc = 0;
-                    for (int t = HB - 1; t >= 0; --t) {
-                        acc += g[t];
-                        g[t] = acc;
-                    }
-                }
-                __threadfence_block();
-            }
-        }
-        // ---- 2. the sequential rest of the read on lane 0
+        if (len > 0 && !err) err = build_occ_wave(D.V, S, q, len, ho, lane);
         if (lane == 0) {
             int n = 0;
             if (D.prof) pt[0] += wall_clock64() - t0;
             if (len > 0 && !err)
-                err = seedc::map_after_occ(V, D.O, S, q, len, i, D.out + (int64_t)i * D.caps.out, D.caps.out, &n,
+                err = seedc::map_after_occ(D.V, D.O, S, q, len, i, D.out + (int64_t)i * D.caps.out, D.caps.out, &n,
                                            D.prof ? pt + 1 : nullptr);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
+        }
+        __threadfence_block();
+    }
+}
+
+// Pass 1: a wave takes 64 reads at a time; their occurrence tables are built one after the
+// other by the whole wave (build_occ_wave), then every lane runs its own read's SMEMs,
+// chaining and chain filter (seed_core.h map_after_occ) -- the sequential, latency-bound part
+// with 64 reads' loads in flight per wave instead of one.  Scratch: 64 small slices per wave
+// (D.caps sized for the batch's read lengths); a read that outgrows its slice is flagged and
+// goes to pass 2.
+__global__ void __launch_bounds__(64 * SEED_WAVES) seed_batch_kernel(SeedDev D) {
+    __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t slot = (int64_t)blockIdx.x * SEED_WAVES + wv;
+    if (slot >= D.n_lanes) return;
+    uint8_t *base = D.scratch + slot * 64 * D.stride;
+    int32_t *ho = hoff_lds[wv];
+    unsigned long long pt[2] = {0ULL, 0ULL};   // wave wall-clock: occurrence tables, lane work
+    for (;;) {
+        int b0 = 0;
+        if (lane == 0) b0 = atomicAdd(D.next, 64);
+        b0 = __shfl(b0, 0, 64);
+        if (b0 >= D.n_sr) {   // every wave reaches this: the grid drains
+            if (D.prof && lane == 0) {
+                atomicAdd(&D.prof[0], pt[0]);
+                atomicAdd(&D.prof[1], pt[1]);
+            }
+            break;
+        }
+        const unsigned long long t0 = D.prof ? wall_clock64() : 0ULL;
+        int my_err = 0;
+        const int nb = (int)(D.n_sr - b0 < 64 ? D.n_sr - b0 : 64);
+        for (int rd = 0; rd < nb; ++rd) {
+            const int i = b0 + rd;
+            const int64_t o = D.sr_off[i];
+            const int len = (int)(D.sr_off[i + 1] - o);
+            seedc::Scratch S = seedc::carve(base + (int64_t)rd * D.stride, D.caps);
+            int err = 0;
+            if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
+            if (len > 0 && !err) err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane);
+            if (lane == rd) my_err = err;
+        }
+        const unsigned long long t1 = D.prof ? wall_clock64() : 0ULL;
+        if (lane < nb) {
+            const int i = b0 + lane;
+            const int64_t o = D.sr_off[i];
+            const int len = (int)(D.sr_off[i + 1] - o);
+            seedc::Scratch S = seedc::carve(base + (int64_t)lane * D.stride, D.caps);
+            int n = 0, err = my_err;
+            if (len > 0 && !err)
+                err = seedc::map_after_occ(D.V, D.O, S, D.sr_seq + o, len, i, D.out + (int64_t)i * D.caps.out,
+                                           D.caps.out, &n, nullptr);
+            D.n_out[i] = err ? 0 : n;
+            D.status[i] = err;
+        }
+        if (D.prof && lane == 0) {
+            pt[0] += t1 - t0;
+            pt[1] += wall_clock64() - t1;
         }
         __threadfence_block();
     }
@@ -163,9 +232,16 @@ int seed_slots_per_cu() {
 }
 
 int seed_launch(const SeedDev &D, void *stream) {
-    if (D.n_sr <= 0) return 0;
+    if (D.n_list <= 0) return 0;
     const int64_t blocks = (D.n_lanes + SEED_WAVES - 1) / SEED_WAVES;
     hipLaunchKernelGGL(seed_wave_kernel, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
+    return (int)hipGetLastError();
+}
+
+int seed_batch_launch(const SeedDev &D, void *stream) {
+    if (D.n_sr <= 0) return 0;
+    const int64_t blocks = (D.n_lanes + SEED_WAVES - 1) / SEED_WAVES;
+    hipLaunchKernelGGL(seed_batch_kernel, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
     return (int)hipGetLastError();
 }
 

@@ -107,7 +107,9 @@ extern "C" void pr_sw_opts_default(pr_sw_opts *o, int finish) {
     }
 }
 
-extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
+// dev_tasks: bwa mode with the seeds already in HBM (the dense list of pr_seed_gpu_map, n_task
+// of them, grouped by read; seed_off_h its per-read prefix on the host); b's task fields unused
+static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h) {
     if (!c || !b) return pr_set_error(PR_ERR_ARG, "null arg");
     if (b->n_sr < 0 || b->n_lr < 0 || b->n_task < 0) return pr_set_error(PR_ERR_ARG, "negative sizes");
     HIPCHK(hipSetDevice(ctx_device(c)));
@@ -123,7 +125,7 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
     for (int i = 0; i < b->n_lr; ++i)
         if (b->lr_off[i + 1] < b->lr_off[i] || b->lr_off[i + 1] - b->lr_off[i] > (1 << 30))
             return pr_set_error(PR_ERR_ARG, "lr_off not monotone");
-    for (int64_t t = 0; t < b->n_task; ++t) {
+    for (int64_t t = 0; t < b->n_task && !dev_tasks; ++t) {
         const int sr = b->t_sr[t], lr = b->t_lr[t];
         if (sr < 0 || sr >= b->n_sr || lr < 0 || lr >= b->n_lr)
             return pr_set_error(PR_ERR_ARG, "task references a missing read");
@@ -133,9 +135,11 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
             return pr_set_error(PR_ERR_ARG, "seed outside its reads");
     }
     const int64_t nt = b->n_task;
-    const bool bwa = b->t_chain != nullptr;
+    const bool bwa = b->t_chain != nullptr || dev_tasks;
     std::vector<int64_t> seed_off;
-    if (bwa) {   // seeds grouped by short read, then chain
+    if (dev_tasks) {
+        seed_off.assign(seed_off_h, seed_off_h + b->n_sr + 1);
+    } else if (bwa) {   // seeds grouped by short read, then chain
         if (nt >= (int64_t)1 << 31) return pr_set_error(PR_ERR_CAPACITY, "more than 2^31 seeds in one batch");
         seed_off.assign((size_t)b->n_sr + 1, 0);
         for (int64_t t = 0; t < nt; ++t) {
@@ -152,11 +156,29 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
     if ((rc = up(r, SB_SR, b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
         (rc = up(r, SB_SR_OFF, b->sr_off, (size_t)b->n_sr + 1, s)) ||
         (rc = up(r, SB_LR, b->lr_seq, (size_t)b->lr_off[b->n_lr], s)) ||
-        (rc = up(r, SB_LR_OFF, b->lr_off, (size_t)b->n_lr + 1, s)) || (rc = up(r, SB_T_SR, b->t_sr, nt, s)) ||
-        (rc = up(r, SB_T_LR, b->t_lr, nt, s)) || (rc = up(r, SB_T_STRAND, b->t_strand, nt, s)) ||
-        (rc = up(r, SB_T_QBEG, b->t_qbeg, nt, s)) || (rc = up(r, SB_T_RBEG, b->t_rbeg, nt, s)) ||
-        (rc = up(r, SB_T_SLEN, b->t_slen, nt, s)))
+        (rc = up(r, SB_LR_OFF, b->lr_off, (size_t)b->n_lr + 1, s)))
         return rc;
+    if (dev_tasks) {   // unpack the device seed list into the task columns, count the first seeds
+        if ((rc = ensure(r, SB_T_SR, (size_t)nt * 4)) || (rc = ensure(r, SB_T_LR, (size_t)nt * 4)) ||
+            (rc = ensure(r, SB_T_STRAND, (size_t)nt)) || (rc = ensure(r, SB_T_QBEG, (size_t)nt * 4)) ||
+            (rc = ensure(r, SB_T_RBEG, (size_t)nt * 4)) || (rc = ensure(r, SB_T_SLEN, (size_t)nt * 4)) ||
+            (rc = ensure(r, SB_CHAIN, (size_t)nt * 4)) || (rc = ensure(r, SB_ACNT, 64)))
+            return rc;
+        HIPCHK(hipMemsetAsync(r.buf[SB_ACNT], 0, 64, s));
+        int e = aln_launch_unpack_seeds(dev_tasks, nt, (int32_t *)r.buf[SB_T_SR], (int32_t *)r.buf[SB_T_LR],
+                                        (uint8_t *)r.buf[SB_T_STRAND], (int32_t *)r.buf[SB_T_QBEG],
+                                        (int32_t *)r.buf[SB_T_RBEG], (int32_t *)r.buf[SB_T_SLEN],
+                                        (int32_t *)r.buf[SB_CHAIN], (int32_t *)r.buf[SB_ACNT], (void *)s);
+        if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        int32_t n0 = 0;
+        HIPCHK(hipMemcpyAsync(&n0, r.buf[SB_ACNT], 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        r.n_rank0 = n0;
+    } else if ((rc = up(r, SB_T_SR, b->t_sr, nt, s)) || (rc = up(r, SB_T_LR, b->t_lr, nt, s)) ||
+               (rc = up(r, SB_T_STRAND, b->t_strand, nt, s)) || (rc = up(r, SB_T_QBEG, b->t_qbeg, nt, s)) ||
+               (rc = up(r, SB_T_RBEG, b->t_rbeg, nt, s)) || (rc = up(r, SB_T_SLEN, b->t_slen, nt, s))) {
+        return rc;
+    }
     const size_t n4 = (size_t)(nt + 1) * 4;
     for (int id : {SB_QB, SB_QE, SB_RB, SB_RE, SB_SCORE, SB_TRUESC, SB_W, SB_GSCORE, SB_POS, SB_NCIG, SB_STATUS})
         if ((rc = ensure(r, id, n4))) return rc;
@@ -169,7 +191,8 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
     r.n_aln = 0;
     if (bwa) {
         const size_t n1 = (size_t)nt + 1, r1 = (size_t)b->n_sr + 1;
-        if ((rc = up(r, SB_CHAIN, b->t_chain, (size_t)nt, s)) || (rc = up(r, SB_SEEDOFF, seed_off.data(), r1, s)) ||
+        if ((!dev_tasks && (rc = up(r, SB_CHAIN, b->t_chain, (size_t)nt, s))) ||
+            (rc = up(r, SB_SEEDOFF, seed_off.data(), r1, s)) ||
             (rc = ensure(r, SB_SEL, n1)) || (rc = ensure(r, SB_EXTF, n1)) || (rc = ensure(r, SB_DEC, n1)) ||
             (rc = ensure(r, SB_RESUME, r1 * 4)) || (rc = ensure(r, SB_ACNT, 64)) ||
             (rc = ensure(r, SB_AREG, n1 * sizeof(AlnReg))) || (rc = ensure(r, SB_AIX, n1 * 4)) ||
@@ -216,6 +239,13 @@ extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) {
     r.n_lr = b->n_lr;
     r.qmax = qmax;
     return 0;
+}
+
+extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) { return sw_upload_impl(c, b, nullptr, nullptr); }
+
+// the iteration's SW upload with the device-resident seeds of pr_seed_gpu_map (prgpu_api.cpp)
+int sw_upload_device_seeds(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h) {
+    return sw_upload_impl(c, b, dev_tasks, seed_off_h);
 }
 
 static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {

@@ -22,6 +22,7 @@ def _setup(L):
         return
     sw._setup(L)
     L.pr_iter_upload.argtypes = [C.c_void_p, C.POINTER(IterBatch)]
+    L.pr_iter_upload_gpu_seeds.argtypes = [C.c_void_p, C.POINTER(IterBatch)]
     L.pr_iter_launch.argtypes = [C.c_void_p, C.POINTER(sw.SwOpts), C.POINTER(_abi.CnsParams)]
     L.pr_iter_download.argtypes = [C.c_void_p, C.POINTER(_abi.CnsOut)]
     L.pr_iter_bounds.argtypes = [C.c_void_p, _abi.P32, _abi.P64, C.POINTER(_abi.CnsBounds)]
@@ -36,18 +37,24 @@ class Iteration:
     """A resident iteration batch on one GPU (upload once, launch many)."""
 
     def __init__(self, d, lr_qual: Optional[np.ndarray] = None, ctx: Optional[_abi.Context] = None,
-                 ref_seq: Optional[np.ndarray] = None):
+                 ref_seq: Optional[np.ndarray] = None, gpu_seeds: bool = False):
         """d: reads + tasks (synth.Dataset fields); lr_qual: the reference qualities (phred+33,
         default '$'); ref_seq: ASCII consensus reference when it differs from the mapped long
-        reads d.lr_seq (iterations after the first map to the masked consensus)."""
+        reads d.lr_seq (iterations after the first map to the masked consensus); gpu_seeds: the
+        tasks are the seeds the last DeviceSeedIndex.map(keep_on_device=True) left in HBM (d's
+        task fields are not used)."""
         self.L = _abi.lib()
         _setup(self.L)
         self.ctx = ctx or _abi.default_context()
         self.d = d
-        self.inp = d.sw_input()
         n_lr = len(d.lr_off) - 1
         self.task_lr_off = np.zeros(n_lr + 1, np.int64)
-        np.cumsum(np.bincount(d.t_lr, minlength=n_lr), out=self.task_lr_off[1:])
+        if gpu_seeds:
+            z = np.zeros(0, np.int32)
+            self.inp = sw.SwInput(d.sr_off, d.sr_seq, d.lr_off, d.lr_seq, z, z, np.zeros(0, np.uint8), z, z, z)
+        else:
+            self.inp = d.sw_input()
+            np.cumsum(np.bincount(d.t_lr, minlength=n_lr), out=self.task_lr_off[1:])
         if lr_qual is None:
             lr_qual = np.full(int(d.lr_off[-1]), ord("$"), np.uint8)   # raw CLR reads: phred 3
         self.lr_qual = lr_qual
@@ -63,7 +70,10 @@ class Iteration:
         if ref_seq is not None:
             b.ref_seq = _abi.ptr(self.ref_seq, C.c_uint8)
         self._b = b
-        _abi.check(self.L.pr_iter_upload(self.ctx.h, C.byref(b)), "pr_iter_upload")
+        if gpu_seeds:
+            _abi.check(self.L.pr_iter_upload_gpu_seeds(self.ctx.h, C.byref(b)), "pr_iter_upload_gpu_seeds")
+        else:
+            _abi.check(self.L.pr_iter_upload(self.ctx.h, C.byref(b)), "pr_iter_upload")
         nl, nt, bd = C.c_int32(), C.c_int64(), _abi.CnsBounds()
         _abi.check(self.L.pr_iter_bounds(self.ctx.h, C.byref(nl), C.byref(nt), C.byref(bd)), "pr_iter_bounds")
         self.n_lr, self.n_task, self.bounds = nl.value, nt.value, bd

@@ -59,6 +59,7 @@ def _setup(L):
     L.pr_seed_gpu_index_digest.argtypes = [C.c_void_p, C.c_void_p]
     L.pr_seed_gpu_index_last_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     L.pr_seed_gpu_phase_ticks.argtypes = [C.c_void_p, C.c_void_p]
+    L.pr_seed_gpu_pass2_reads.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     _done = True
 
 
@@ -182,14 +183,25 @@ def _phase_ms(L, ctx) -> dict:
     """Wave time per part of the last GPU seeding launch (ms summed over waves)."""
     t = np.zeros(4, np.uint64)
     _abi.check(L.pr_seed_gpu_phase_ticks(ctx.h, t.ctypes.data), "pr_seed_gpu_phase_ticks")
-    return {k: round(float(v) / 1e5, 1) for k, v in zip(("occ_table", "smems", "chaining", "filter_out"), t)}
+    n2 = C.c_int64()
+    _abi.check(L.pr_seed_gpu_pass2_reads(ctx.h, C.byref(n2)), "pr_seed_gpu_pass2_reads")
+    out = {k: round(float(v) / 1e5, 1) for k, v in
+           zip(("occ_table", "lane_phase_and_pass2_smems", "pass2_chaining", "pass2_filter_out"), t)}
+    out["pass2_reads"] = n2.value
+    return out
 
 
-def _map_gpu(L, ctx, sr_seq, sr_off, opts, allow_flagged):
+def _map_gpu(L, ctx, sr_seq, sr_off, opts, allow_flagged, keep_on_device=False):
     opts = opts or default_opts()
     sr_seq = np.ascontiguousarray(sr_seq, np.uint8)
     sr_off = np.ascontiguousarray(sr_off, np.int64)
     st = np.zeros(max(1, len(sr_off) - 1), np.int32)
+    if keep_on_device:   # the seeds stay in HBM for iteration.Iteration(gpu_seeds=True)
+        rc = L.pr_seed_gpu_map(ctx.h, C.byref(opts), sr_seq.ctypes.data, sr_off.ctypes.data, len(sr_off) - 1,
+                               None, st.ctypes.data)
+        if rc != 0 and not (allow_flagged and rc == -9):
+            _abi.check(rc, "pr_seed_gpu_map")
+        return None, st[:len(sr_off) - 1]
     out = SeedTasks()
     rc = L.pr_seed_gpu_map(ctx.h, C.byref(opts), sr_seq.ctypes.data, sr_off.ctypes.data, len(sr_off) - 1,
                            C.byref(out), st.ctypes.data)
@@ -220,8 +232,10 @@ class DeviceSeedIndex:
     def build_ms(self) -> float:
         return _last_ms(self.L.pr_seed_gpu_index_last_ms, self._ctx)
 
-    def map(self, sr_seq: np.ndarray, sr_off: np.ndarray, opts: SeedOpts | None = None, allow_flagged: bool = False):
-        return _map_gpu(self.L, self._ctx, sr_seq, sr_off, opts, allow_flagged)
+    def map(self, sr_seq: np.ndarray, sr_off: np.ndarray, opts: SeedOpts | None = None, allow_flagged: bool = False,
+            keep_on_device: bool = False):
+        """-> (seeds or None when keep_on_device, status per read)."""
+        return _map_gpu(self.L, self._ctx, sr_seq, sr_off, opts, allow_flagged, keep_on_device)
 
     def gpu_ms(self) -> float:
         return _last_ms(self.L.pr_seed_gpu_last_ms, self._ctx)

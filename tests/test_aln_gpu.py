@@ -76,3 +76,26 @@ def test_bwa_mode_seed_order_and_empty_reads():
         setattr(half, k, np.ascontiguousarray(getattr(inp, k)[keep]))
     res = sw.run(half, sw.default_opts(False), ctx=_abi.default_context())
     assert res.n > 0 and (half.t_sr[res["task"][:res.n]] >= d.n_sr // 2).all()
+
+
+def test_iteration_from_device_seeds_equals_host_handed_seeds():
+    """pr_iter_upload_gpu_seeds: the seeds pr_seed_gpu_map leaves in HBM feed the iteration
+    without a host round trip; the corrected reads equal those of the same seeds handed over
+    from the host (pr_iter_upload in bwa mode)."""
+    from proovread_amd import _abi, cns, iteration, seed, sw, synth
+    d = synth.simulate(53, 40000, 40, 2500, 15)
+    ctx = _abi.default_context()
+    ix = seed.DeviceSeedIndex(ctx, d.lr_seq, d.lr_off)
+    tasks, st = ix.map(d.sr_seq, d.sr_off, seed.default_opts(False))
+    assert (st == 0).all() and len(tasks) > 10 * d.n_lr
+    db = synth.with_seeds(d, tasks)
+    cp = cns.CnsParams(coverage=11.25, use_ref_qual=True)
+    it = iteration.Iteration(db, ctx=ctx)
+    it.launch(sw.default_opts(False), cp)
+    want = [(r.status, r.fastq, r.trace) for r in it.results()]
+    ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), keep_on_device=True)
+    it2 = iteration.Iteration(d, ctx=ctx, gpu_seeds=True)
+    assert it2.n_task == len(tasks)
+    it2.launch(sw.default_opts(False), cp)
+    got = [(r.status, r.fastq, r.trace) for r in it2.results()]
+    assert got == want and all(g[0] == 0 for g in got)
