@@ -92,6 +92,7 @@ struct CnsDev {
 // geometry workgroups (2 per CU); grid_retry: large-geometry workgroups (1 per CU)
 int cns_launch(const CnsDev &D, const CnsParamsDev &P, int grid, int grid_retry, void *stream);
 int cns_max_bins();
+int cns_wg_per_cu();   // workgroups per CU of the first-pass geometry
 int cns_k_header();      // ints of window starts reserved at the head of a K pool slice
 
 constexpr int CNS_THREADS = 256;

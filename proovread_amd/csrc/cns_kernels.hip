@@ -20,6 +20,8 @@
 // Build flags include -ffp-contract=off: every double op of the Perl code is
 // evaluated separately (bit-exact ncscore / Phreds2freqs / Freqs2phreds).
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <stdint.h>
 
 #include "cns_dev.h"
@@ -351,8 +353,8 @@ __device__ void prep_alignment(const CnsDev &D, const CnsParamsDev &P, int64_t g
 // buffers (fixed-state counts, (column, insertion state) counts, per-column best
 // insertion, ignore bits, work-item prefix, argmax outputs) — chimera tables alias B;
 // the binning arrays of phase 2 use A and B together.
-// Two geometries: the small one (2 workgroups per CU) takes every read first; a read
-// whose tables overflow it is rerun with the large one (1 per CU, 4x the tables).
+// Three geometries: a small one (GeoM, 4 workgroups per CU; or GeoS, 2 per CU) takes every
+// read first; a read whose tables overflow it is rerun with the large one (1 per CU).
 constexpr int SLOT_SH = 12;                 // window / chimera keys: (column + 1) << 12 | state slot
 constexpr uint32_t SLOT_MASK = (1u << SLOT_SH) - 1u;
 constexpr int CHUNK = 32;                   // columns per scatter work item
@@ -402,6 +404,10 @@ struct CnsGeo {
     static_assert(W <= 1024 && CNS_THREADS <= 256, "run record fields");
 };
 using GeoS = CnsGeo<512, 512, 1024, 8192, 2048, 1024, 2, true>;
+// the default first pass: 256-column windows, smaller staging, 4 workgroups per CU (16 waves:
+// the pileup is latency-bound, occupancy hides it; 29.4 -> 23.8 ms at configs[1]); GeoS (2 per
+// CU, 512-column windows) stays selectable with PRGPU_CNS_GEO=S
+using GeoM = CnsGeo<256, 256, 384, 3072, 768, 384, 4, true>;
 using GeoL = CnsGeo<2048, 512, 2048, 8192, 2560, 1024, 1, false>;
 
 // per-column descriptor: flag bits above the 12-bit state-table slot
@@ -1604,19 +1610,29 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
 #undef CNS_CAP_FAIL
 }
 
+static bool cns_geo_m() {
+    const char *g = getenv("PRGPU_CNS_GEO");
+    return !(g && g[0] == 'S');
+}
+int cns_wg_per_cu() { return cns_geo_m() ? GeoM::WGCU : GeoS::WGCU; }
+
 int cns_launch(const CnsDev &D, const CnsParamsDev &P, int grid, int grid_retry, void *stream) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void *)cns_lr_kernel<GeoS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            GeoS::LDS);
         if (e != hipSuccess) return (int)e;
+        e = hipFuncSetAttribute((const void *)cns_lr_kernel<GeoM>, hipFuncAttributeMaxDynamicSharedMemorySize, GeoM::LDS);
+        if (e != hipSuccess) return (int)e;
         e = hipFuncSetAttribute((const void *)cns_lr_kernel<GeoL>, hipFuncAttributeMaxDynamicSharedMemorySize, GeoL::LDS);
         if (e != hipSuccess) return (int)e;
         attr = true;
     }
     hipStream_t s = (hipStream_t)stream;
-    if (!D.force_large)
-        hipLaunchKernelGGL(cns_lr_kernel<GeoS>, dim3(grid), dim3(CNS_THREADS), GeoS::LDS, s, D, P);
+    if (!D.force_large) {
+        if (cns_geo_m()) hipLaunchKernelGGL(cns_lr_kernel<GeoM>, dim3(grid), dim3(CNS_THREADS), GeoM::LDS, s, D, P);
+        else hipLaunchKernelGGL(cns_lr_kernel<GeoS>, dim3(grid), dim3(CNS_THREADS), GeoS::LDS, s, D, P);
+    }
     // reads whose tables outgrew the small geometry (device-side list; usually empty)
     hipLaunchKernelGGL(cns_lr_kernel<GeoL>, dim3(grid_retry), dim3(CNS_THREADS), GeoL::LDS, s, D, P);
     return (int)hipGetLastError();

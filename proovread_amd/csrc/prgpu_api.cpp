@@ -435,7 +435,8 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
     }
     HIPCHK(hipMemsetAsync(D.work, 0, 64, c->stream));
     HIPCHK(hipMemsetAsync(D.prof, 0, CNS_NPHASE * 8, c->stream));
-    const int grid = c->n_lr < c->n_cu * 2 ? c->n_lr : c->n_cu * 2;
+    const int wgcu = cns_wg_per_cu();
+    const int grid = c->n_lr < c->n_cu * wgcu ? c->n_lr : c->n_cu * wgcu;
     const int grid_retry = c->n_lr < c->n_cu ? c->n_lr : c->n_cu;
     {
         // K pool: per resident workgroup the window starts (longest read / 512 + 8 ints) and
