@@ -248,8 +248,12 @@ def main():
     me, mg, ce, cg = sw.last_timing(ctx)
     bwa_rounds, bwa_ext, bwa_patch = sw.bwa_stats(ctx) if d.t_chain is not None else (0, 0, 0)
     pc = sw.phase_cycles(ctx)
-    a = it.download()
+    # one more, untimed step with the consensus kernel's per-phase clock counters on
+    os.environ["PRGPU_CNS_PROF"] = "1"
+    step()
+    os.environ.pop("PRGPU_CNS_PROF")
     cns_phases = it.cns_phase_ms()
+    a = it.download()
     ok = int((a["status"] == 0).sum())
     bpt, bpn = (int(x) for x in stats.download(np.int64))
     parity = check_parity(it, cpu_res) if cpu_res is not None else None
@@ -264,13 +268,17 @@ def main():
     # pileup kernel: algorithmic bytes (SURVEY.md §8d model) / kernel time
     n_aln, sum_ncig, sum_lseq = it.alignment_stats()
     cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + lr_bases * (2 + 2 + 6 * 4 * 2)
-    prof = ROOT / "profiles" / "pmc_r01.json"
-    traffic = None
+    # HBM bytes per launch from the PMC FETCH_SIZE / WRITE_SIZE passes of this bwa-mode step
+    # (tools/r02_gpu5.sh -> tools/pmc_summary.py -> profiles/pmc_r02_bwa.json)
+    prof = ROOT / "profiles" / "pmc_r02_bwa.json"
+    traffic = traffic_cns = None
     if prof.exists():
         try:
-            traffic = json.loads(prof.read_text()).get("sw_global_pk_kernel<40>", {}).get("hbm_bytes_per_launch")
+            pm = json.loads(prof.read_text())
+            traffic = pm.get("sw_global_pk_kernel<40>", {}).get("hbm_bytes_per_launch")
+            traffic_cns = next((v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith("cns_lr_kernel")), None)
         except Exception:
-            traffic = None
+            traffic = traffic_cns = None
     out = {
         "metric": "corrected long-read Mbases/sec per node",
         "value": round(value, 3),
@@ -319,7 +327,7 @@ def main():
             "kernel": "cns_lr_kernel (bin cap + pileup + argmax, one long read per workgroup)", "bound": "hbm",
             "achieved": round(cns_bytes / (ms[3] * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(cns_bytes / (ms[3] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": int(cns_bytes),
-            "alignments": int(n_aln),
+            "alignments": int(n_aln), "traffic": traffic_cns,
         },
         "cpu_baseline": cpu,
         "seeding": seed_info,

@@ -23,6 +23,8 @@
 // HBM-resident scratch (latency-bound bookkeeping, no roofline claim).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -172,12 +174,18 @@ int aln_launch_init(const AlnDev &A, void *stream) {
 }
 int aln_launch_walk(const AlnDev &A, void *stream) {
     if (A.n_sr <= 0) return 0;
-    hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+    static const int wgcu = getenv("PRGPU_ALN_WALK_WG") ? atoi(getenv("PRGPU_ALN_WALK_WG")) : 0;
+    const unsigned lds = wgcu > 0 ? (unsigned)(160 * 1024 / wgcu) & ~255u : 0u;
+    hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
 int aln_launch_final(const AlnDev &A, void *stream) {
     if (A.n_sr <= 0) return 0;
-    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+    // tuning hook: PRGPU_ALN_FINAL_WG=k caps the resident workgroups per CU at k (dynamic LDS),
+    // i.e. the reads whose region scratch is live at once
+    static const int wgcu = getenv("PRGPU_ALN_FINAL_WG") ? atoi(getenv("PRGPU_ALN_FINAL_WG")) : 0;
+    const unsigned lds = wgcu > 0 ? (unsigned)(160 * 1024 / wgcu) & ~255u : 0u;
+    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, void *stream) {

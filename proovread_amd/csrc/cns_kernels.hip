@@ -1070,21 +1070,25 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                             agg += code == 0 ? (n | (n << 32)) : code == 2 ? n : code == 1 ? ((k == coo[jj] ? 1LL : 0LL) | (n << 32)) : 0;
                         }
                     }
-                    // block segmented inclusive scan (Hillis-Steele over the 256 chunk aggregates)
-                    long long *sv64 = scan;   // 256 x 8 B scratch
-                    int *sfl = ipre;
-                    sv64[tid] = agg;
-                    sfl[tid] = head;
-                    __syncthreads();
-                    for (int o = 1; o < CNS_THREADS; o <<= 1) {
-                        long long pv = 0;
-                        int pf = 0;
-                        if (tid >= o) { pv = sv64[tid - o]; pf = sfl[tid - o]; }
-                        __syncthreads();
-                        if (tid >= o && !sfl[tid]) { sv64[tid] += pv; sfl[tid] |= pf; }
-                        __syncthreads();
+                    // block segmented scan of the 256 chunk aggregates: (value, head) pairs under
+                    // (a, b) -> (b.head ? b : a + b), inside each wave by shuffles, then the
+                    // wave totals carried across the 4 waves through LDS (one barrier)
+                    const int lane = tid & 63, wv = tid >> 6;
+                    long long sv = agg;
+                    int sf = head;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) {
+                        const long long pv = __shfl_up(sv, o, 64);
+                        const int pf = __shfl_up(sf, o, 64);
+                        if (lane >= o && !sf) { sv += pv; sf = pf; }
                     }
-                    long long run = tid > 0 ? sv64[tid - 1] : 0;   // carry into op k0
+                    if (lane == 63) { scan[wv] = sv; ipre[wv] = sf; }
+                    __syncthreads();
+                    long long carry = 0;   // inclusive value at the end of the previous waves
+                    for (int x = 0; x < wv; ++x) carry = ipre[x] ? scan[x] : carry + scan[x];
+                    if (!sf) sv += carry;
+                    const long long prev = __shfl_up(sv, 1, 64);
+                    long long run = lane > 0 ? prev : carry;   // carry into op k0 (thread tid - 1's inclusive value)
                     __syncthreads();
                     for (int k = k0; k < k1; ++k) {
                         while (j + 1 < gs && coo[j + 1] <= k) ++j;
