@@ -211,6 +211,19 @@ class GpuStages:
         res = cns.run_chunk(reads, alns, params, ctx=self.ctx)
         return [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in res]
 
+    def seed(self, lr_map, lr_off, sr, sr_off, seed_opts, comm):
+        """bwa-mode seeds of this rank's short reads on the device: the index of the whole
+        mapping reference built in HBM (pr_seed_gpu_index_build, the host build's tables byte for
+        byte) and pr_seed_gpu_map over the rank's contiguous short-read shard (the host path's
+        task lists exactly, tests/test_seed_gpu.py)."""
+        from . import exact_shard as ex, seed
+        s, e = (0, len(sr_off) - 1) if comm is None or comm.world == 1 else ex.sr_range(len(sr_off) - 1, comm.world,
+                                                                                         comm.rank)
+        ix = seed.DeviceSeedIndex(self.ctx, lr_map, lr_off)
+        tk, _ = ix.map(sr[sr_off[s]:sr_off[e]], sr_off[s:e + 1] - sr_off[s], seed_opts)
+        tk["sr"] += s
+        return tk
+
     def mask(self, seqs: List[bytes], quals: List[bytes], hcr_mask: str, min_sr_length: int):
         """-> (masked reads, bpt, bpN)."""
         from . import mask
@@ -352,7 +365,10 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         ref_map = reads.seqs if finish else mapped     # finish maps to the unmasked .fq (proovread:838-850)
         lr_map, lr_off = reads.pool(ref_map)
         lr_map = NT4[lr_map]
-        tk = _seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], cfg.seed_threads, comm)
+        if hasattr(stages, "seed"):   # device stages: index and seeding in HBM
+            tk = stages.seed(lr_map, lr_off, sr, sr_off, T.options(task)[0], comm)
+        else:
+            tk = _seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], cfg.seed_threads, comm)
         ent.n_tasks = int(len(tk))
         d = _seeds_dataset(lr_map, lr_off, sr, sr_off, tk)
         max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541

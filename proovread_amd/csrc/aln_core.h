@@ -177,7 +177,7 @@ AL_HD bool aln_init_task(const AlnDev &A, int64_t t) {
     A.sel[t] = first ? SEL_EXT : 0;
     A.ext[t] = 0;
     A.dec[t] = 0;
-    if (first) {
+    if (first && !A.cnext_ready) {
         int64_t e = t + 1;
         while (e < A.n_task && A.t_sr[e] == A.t_sr[t] && A.t_chain[e] == A.t_chain[t]) ++e;
         A.cnext[t] = (int32_t)e;

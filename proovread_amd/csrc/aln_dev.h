@@ -38,9 +38,10 @@ struct AlnDev {
     uint8_t *ext;              // 1: the task's extension result is available
     uint8_t *dec;              // mem_chain2aln's decision: 0 open, 1 extended (a region), 2 skipped
     int32_t *resume;           // [n_sr] first undecided seed of the read
-    int32_t *counter;          // [0] extension requests, [1] patch requests, [3] first-round seeds
+    int32_t *counter;          // [0] extension requests (aln_list_kernel), [1] patch requests
     int32_t *tlist;            // [n_task] the seeds to extend in the next round (their count in counter)
     int32_t *cnext;            // [n_task] of a chain's first seed: the next chain's first seed
+    int32_t cnext_ready;       // cnext already written (aln_unpack_kernel, from the seeds' ranks)
     AlnReg *R;                 // [n_task] region scratch (read r: from seed_off[r])
     int32_t *ix;               // [n_task] sort scratch
     int32_t *pscore;           // [n_task] known patch scores of read r (from seed_off[r])
@@ -58,6 +59,8 @@ struct AlnDev {
 
 int aln_launch_init(const AlnDev &A, void *stream);
 int aln_launch_walk(const AlnDev &A, void *stream);
+// the seeds flagged SEL_EXT -> tlist, their count -> counter[0] (add to it)
+int aln_launch_list(const AlnDev &A, void *stream);
 int aln_launch_final(const AlnDev &A, void *stream);
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t pool_stride, void *stream);
 // CIGAR slots of the reported tasks: slot[t] = cig_slot_ops(lq) or 0 -> exclusive prefix (n+1)
@@ -73,9 +76,10 @@ int aln_launch_group_lr(const int32_t *alist, const int32_t *t_lr, int64_t n, in
                         size_t temp_bytes, void *stream);
 size_t aln_group_temp_bytes(int64_t n, int32_t n_lr);
 // the dense seed list of pr_seed_gpu_map (pr_seed_task AoS) -> the SW task columns; n_first[0]
-// += the seeds of rank 0 (every chain's first seed)
+// += the seeds of rank 0 (every chain's first seed); cnext of every chain's first seed
+// (a chain's seeds are consecutive with ranks 0, 1, ..: its first is t - rank)
 int aln_launch_unpack_seeds(const pr_seed_task *src, int64_t n, int32_t *sr, int32_t *lr, uint8_t *strand,
                             int32_t *qbeg, int32_t *rbeg, int32_t *slen, int32_t *chain, int32_t *n_first,
-                            void *stream);
+                            int32_t *cnext, void *stream);
 
 }  // namespace prgpu

@@ -36,17 +36,9 @@ using namespace alnc;
 
 // ---------------------------------------------------------------- round 0
 __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
-    const int lane = threadIdx.x & 63;
-    for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < A.n_task; t0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = t0 + threadIdx.x;
-        const bool first = t < A.n_task && aln_init_task(A, t);
-        // one atomic per wave for the round-0 list (10 M first seeds on one counter otherwise)
-        const unsigned long long m = __ballot(first);
-        int base = 0;
-        if (lane == 0 && m) base = atomicAdd(&A.counter[3], __popcll(m));
-        base = __shfl(base, 0, 64);
-        if (first) A.tlist[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)t;
-    }
+    // (the round-0 list -- every chain's first seed, sel = SEL_EXT -- is made by aln_list_kernel)
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < A.n_task; t += (int64_t)gridDim.x * blockDim.x)
+        (void)aln_init_task(A, t);
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < A.n_sr; r += (int64_t)gridDim.x * blockDim.x) {
         A.resume[r] = (int32_t)A.seed_off[r];
         A.npk[r] = 0;
@@ -58,7 +50,45 @@ __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
 // ---------------------------------------------------------------- mem_chain2aln
 __global__ void __launch_bounds__(256) aln_walk_kernel(AlnDev A) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < A.n_sr) aln_walk_read(A, r, [&](int64_t t) { A.tlist[atomicAdd(&A.counter[0], 1)] = (int32_t)t; });
+    // requested seeds carry SEL_EXT; aln_list_kernel lists them
+    if (r < A.n_sr) aln_walk_read(A, r, [](int64_t) {});
+}
+
+// The seeds flagged SEL_EXT -> tlist (any order: the extension kernels order their tasks
+// themselves), their count -> counter[0].  A workgroup takes a contiguous range, counts it,
+// reserves its part of the list with ONE device-scope atomic and writes it (a single counter
+// word serialises ~88 atomics per us: per-wave or per-lane atomics on it cost 6-8 ms for the
+// 10 M first seeds / 0.7 M requests of a configs[1] iteration).
+__global__ void __launch_bounds__(256) aln_list_kernel(AlnDev A) {
+    __shared__ int32_t ws[4];
+    __shared__ int32_t base_s;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t per = ((A.n_task + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+    const int64_t b0 = (int64_t)blockIdx.x * per;
+    const int64_t b1 = b0 + per < A.n_task ? b0 + per : A.n_task;
+    int c = 0;
+    for (int64_t t = b0 + threadIdx.x; t < b1; t += 256) c += (A.sel[t] & SEL_EXT) ? 1 : 0;
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if (lane == 0) ws[wv] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = ws[0] + ws[1] + ws[2] + ws[3];
+        base_s = tot ? atomicAdd(&A.counter[0], tot) : 0;
+    }
+    __syncthreads();
+    int base = base_s;
+    for (int64_t t0 = b0; t0 < b1; t0 += 256) {
+        const int64_t t = t0 + threadIdx.x;
+        const bool f = t < b1 && (A.sel[t] & SEL_EXT);
+        const unsigned long long m = __ballot(f);
+        __syncthreads();   // the previous tile is done with ws
+        if (lane == 0) ws[wv] = __popcll(m);
+        __syncthreads();
+        int off = base;
+        for (int x = 0; x < wv; ++x) off += ws[x];
+        if (f) A.tlist[off + __popcll(m & ((1ull << lane) - 1))] = (int32_t)t;
+        base += ws[0] + ws[1] + ws[2] + ws[3];
+    }
 }
 
 __global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A) {
@@ -141,7 +171,10 @@ __global__ void __launch_bounds__(256) sw_gather_kernel(SwGather G) {
 
 __global__ void __launch_bounds__(256) aln_unpack_kernel(const pr_seed_task *src, int64_t n, int32_t *sr, int32_t *lr,
                                                          uint8_t *strand, int32_t *qbeg, int32_t *rbeg, int32_t *slen,
-                                                         int32_t *chain, int32_t *n_first) {
+                                                         int32_t *chain, int32_t *n_first, int32_t *cnext) {
+    __shared__ int32_t nf;   // first seeds of this workgroup: one device-scope atomic per workgroup
+    if (threadIdx.x == 0) nf = 0;
+    __syncthreads();
     const int lane = threadIdx.x & 63;
     for (int64_t t0 = (int64_t)blockIdx.x * blockDim.x; t0 < n; t0 += (int64_t)gridDim.x * blockDim.x) {
         const int64_t t = t0 + threadIdx.x;
@@ -156,10 +189,13 @@ __global__ void __launch_bounds__(256) aln_unpack_kernel(const pr_seed_task *src
             slen[t] = x.slen;
             chain[t] = x.chain;
             first = x.rank == 0;
+            if (t + 1 == n || src[t + 1].rank == 0) cnext[t - x.rank] = (int32_t)(t + 1);   // the chain's last seed
         }
         const unsigned long long m = __ballot(first);
-        if (lane == 0 && m) atomicAdd(n_first, __popcll(m));
+        if (lane == 0 && m) atomicAdd(&nf, __popcll(m));
     }
+    __syncthreads();
+    if (threadIdx.x == 0 && nf) atomicAdd(n_first, nf);
 }
 
 static int grid_of(int64_t n, int cap = 8192) {
@@ -170,6 +206,11 @@ static int grid_of(int64_t n, int cap = 8192) {
 int aln_launch_init(const AlnDev &A, void *stream) {
     const int64_t n = A.n_task > A.n_sr ? A.n_task : A.n_sr;
     hipLaunchKernelGGL(aln_init_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, A);
+    return (int)hipGetLastError();
+}
+int aln_launch_list(const AlnDev &A, void *stream) {
+    if (A.n_task <= 0) return 0;
+    hipLaunchKernelGGL(aln_list_kernel, dim3((unsigned)grid_of(A.n_task, 2048)), dim3(256), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
 int aln_launch_walk(const AlnDev &A, void *stream) {
@@ -183,7 +224,9 @@ int aln_launch_final(const AlnDev &A, void *stream) {
     if (A.n_sr <= 0) return 0;
     // tuning hook: PRGPU_ALN_FINAL_WG=k caps the resident workgroups per CU at k (dynamic LDS),
     // i.e. the reads whose region scratch is live at once
-    static const int wgcu = getenv("PRGPU_ALN_FINAL_WG") ? atoi(getenv("PRGPU_ALN_FINAL_WG")) : 0;
+    // (default 3: 17.5 -> 13.6 ms at configs[1]; the per-lane region scratch of all resident reads
+    // then stays on chip instead of thrashing L2; profiles/r02_alnwg_sweep.txt)
+    static const int wgcu = getenv("PRGPU_ALN_FINAL_WG") ? atoi(getenv("PRGPU_ALN_FINAL_WG")) : 3;
     const unsigned lds = wgcu > 0 ? (unsigned)(160 * 1024 / wgcu) & ~255u : 0u;
     hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
@@ -203,10 +246,10 @@ int sw_launch_gather(const SwGather &G, void *stream) {
 
 int aln_launch_unpack_seeds(const pr_seed_task *src, int64_t n, int32_t *sr, int32_t *lr, uint8_t *strand,
                             int32_t *qbeg, int32_t *rbeg, int32_t *slen, int32_t *chain, int32_t *n_first,
-                            void *stream) {
+                            int32_t *cnext, void *stream) {
     if (n <= 0) return 0;
     hipLaunchKernelGGL(aln_unpack_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, src, n, sr, lr, strand,
-                       qbeg, rbeg, slen, chain, n_first);
+                       qbeg, rbeg, slen, chain, n_first, cnext);
     return (int)hipGetLastError();
 }
 

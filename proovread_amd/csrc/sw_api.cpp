@@ -162,18 +162,21 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
         if ((rc = ensure(r, SB_T_SR, (size_t)nt * 4)) || (rc = ensure(r, SB_T_LR, (size_t)nt * 4)) ||
             (rc = ensure(r, SB_T_STRAND, (size_t)nt)) || (rc = ensure(r, SB_T_QBEG, (size_t)nt * 4)) ||
             (rc = ensure(r, SB_T_RBEG, (size_t)nt * 4)) || (rc = ensure(r, SB_T_SLEN, (size_t)nt * 4)) ||
-            (rc = ensure(r, SB_CHAIN, (size_t)nt * 4)) || (rc = ensure(r, SB_ACNT, 64)))
+            (rc = ensure(r, SB_CHAIN, (size_t)nt * 4)) || (rc = ensure(r, SB_ACNT, 64)) ||
+            (rc = ensure(r, SB_CNEXT, ((size_t)nt + 1) * 4)))
             return rc;
         HIPCHK(hipMemsetAsync(r.buf[SB_ACNT], 0, 64, s));
         int e = aln_launch_unpack_seeds(dev_tasks, nt, (int32_t *)r.buf[SB_T_SR], (int32_t *)r.buf[SB_T_LR],
                                         (uint8_t *)r.buf[SB_T_STRAND], (int32_t *)r.buf[SB_T_QBEG],
                                         (int32_t *)r.buf[SB_T_RBEG], (int32_t *)r.buf[SB_T_SLEN],
-                                        (int32_t *)r.buf[SB_CHAIN], (int32_t *)r.buf[SB_ACNT], (void *)s);
+                                        (int32_t *)r.buf[SB_CHAIN], (int32_t *)r.buf[SB_ACNT],
+                                        (int32_t *)r.buf[SB_CNEXT], (void *)s);
         if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         int32_t n0 = 0;
         HIPCHK(hipMemcpyAsync(&n0, r.buf[SB_ACNT], 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         r.n_rank0 = n0;
+        r.cnext_ready = true;
     } else if ((rc = up(r, SB_T_SR, b->t_sr, nt, s)) || (rc = up(r, SB_T_LR, b->t_lr, nt, s)) ||
                (rc = up(r, SB_T_STRAND, b->t_strand, nt, s)) || (rc = up(r, SB_T_QBEG, b->t_qbeg, nt, s)) ||
                (rc = up(r, SB_T_RBEG, b->t_rbeg, nt, s)) || (rc = up(r, SB_T_SLEN, b->t_slen, nt, s))) {
@@ -187,6 +190,7 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
         (rc = ensure(r, SB_LIST, (size_t)(nt + 1 + (int64_t)PK_NB * PK_SEG) * 4)))
         return rc;
     r.bwa = bwa;
+    if (!dev_tasks) r.cnext_ready = false;
     r.read_id0 = b->read_id0;
     r.n_aln = 0;
     if (bwa) {
@@ -277,6 +281,7 @@ static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {
     A.counter = (int32_t *)r.buf[SB_ACNT];
     A.tlist = (int32_t *)r.buf[SB_TLIST];
     A.cnext = (int32_t *)r.buf[SB_CNEXT];
+    A.cnext_ready = r.cnext_ready ? 1 : 0;
     A.R = (AlnReg *)r.buf[SB_AREG];
     A.ix = (int32_t *)r.buf[SB_AIX];
     A.pscore = (int32_t *)r.buf[SB_PSCORE];
@@ -312,8 +317,9 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
     HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
     if ((e = aln_launch_init(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    if ((e = aln_launch_list(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     int32_t cnt[4] = {0, 0, 0, 0};
-    int64_t n_list = r.n_rank0;   // round 0: every chain's first seed (listed by the init kernel)
+    int64_t n_list = r.n_rank0;   // round 0: every chain's first seed (listed after the init kernel)
     D.tsel = A.tlist;
     for (;;) {   // mem_chain2aln: every round extends the listed seeds, the walk resumes
         D.tsel_n = n_list;
@@ -323,6 +329,7 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
             if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         }
         if ((e = aln_launch_walk(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        if ((e = aln_launch_list(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         HIPCHK(hipMemcpyAsync(cnt, A.counter, 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         ++r.ext_rounds;
