@@ -185,6 +185,31 @@ AL_HD bool aln_init_task(const AlnDev &A, int64_t t) {
     return first;
 }
 
+// hprev of every chain head of read r: the closest earlier head of the read on the same long
+// read and strand (-1: none).  A short read's chains lie on ~one long read each, so the walk's
+// containment test then visits the few chains that can contain a seed instead of every earlier
+// chain head (a dependent cnext chase per head).  The heads met so far and their keys sit in
+// the read's own ix / R scratch (contiguous per lane; the final pass rewrites both).
+AL_HD void aln_heads_read(const AlnDev &A, int64_t r) {
+    const int64_t s0 = A.seed_off[r], s1 = A.seed_off[r + 1];
+    int32_t *hl = A.ix + s0;
+    int32_t *hk = reinterpret_cast<int32_t *>(A.R + s0);   // 16 ints per task of room
+    int nh = 0;
+    for (int64_t h = s0; h < s1; h = A.cnext[h]) {
+        const int32_t key = A.t_lr[h] * 2 + (A.t_strand[h] ? 1 : 0);
+        int32_t p = -1;
+        for (int j = nh - 1; j >= 0; --j)
+            if (hk[j] == key) {
+                p = hl[j];
+                break;
+            }
+        A.hprev[h] = p;
+        hl[nh] = (int32_t)h;
+        hk[nh] = key;
+        ++nh;
+    }
+}
+
 // is seed (slr, sst, srb, sqb, slen) "around" region i (mem_chain2aln's containment test)?
 AL_HD bool aln_around(const AlnDev &A, int64_t i, int64_t srb, int sqb, int slen, int lq) {
     const int pqb = A.o_qb[i], pqe = A.o_qe[i];
@@ -213,6 +238,12 @@ AL_HD bool aln_around_any(const AlnDev &A, int64_t s0, int64_t c0, int64_t k, in
     const int sqb = A.t_qbeg[k], slen = A.t_slen[k];
     for (int64_t i = c0; i < k; ++i)
         if (A.dec[i] == 1 && aln_around(A, i, srb, sqb, slen, lq)) return true;
+    if (A.hprev) {   // only the earlier chains on k's long read and strand (aln_heads_read's links)
+        for (int64_t h = A.hprev[c0]; h >= 0; h = A.hprev[h])
+            for (int64_t i = h; i < A.cnext[h]; ++i)
+                if (A.dec[i] == 1 && aln_around(A, i, srb, sqb, slen, lq)) return true;
+        return false;
+    }
     for (int64_t h = s0; h < c0; h = A.cnext[h]) {
         if (A.t_lr[h] != slr || A.t_strand[h] != sst) continue;
         for (int64_t i = h; i < A.cnext[h]; ++i)

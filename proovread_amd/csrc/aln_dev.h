@@ -42,6 +42,7 @@ struct AlnDev {
     int32_t *tlist;            // [n_task] the seeds to extend in the next round (their count in counter)
     int32_t *cnext;            // [n_task] of a chain's first seed: the next chain's first seed
     int32_t cnext_ready;       // cnext already written (aln_unpack_kernel, from the seeds' ranks)
+    int32_t *hprev;            // [n_task] of a chain head: the read's previous head on the same long read and strand (or -1); null: scan every head
     AlnReg *R;                 // [n_task] region scratch (read r: from seed_off[r])
     int32_t *ix;               // [n_task] sort scratch
     int32_t *pscore;           // [n_task] known patch scores of read r (from seed_off[r])
@@ -59,6 +60,8 @@ struct AlnDev {
 
 int aln_launch_init(const AlnDev &A, void *stream);
 int aln_launch_walk(const AlnDev &A, void *stream);
+// hprev of every chain head (after the init kernel)
+int aln_launch_heads(const AlnDev &A, void *stream);
 // the seeds flagged SEL_EXT -> tlist, their count -> counter[0] (add to it)
 int aln_launch_list(const AlnDev &A, void *stream);
 int aln_launch_final(const AlnDev &A, void *stream);

@@ -47,6 +47,11 @@ __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
     }
 }
 
+__global__ void __launch_bounds__(256) aln_heads_kernel(AlnDev A) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < A.n_sr) aln_heads_read(A, r);
+}
+
 // ---------------------------------------------------------------- mem_chain2aln
 __global__ void __launch_bounds__(256) aln_walk_kernel(AlnDev A) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -206,6 +211,11 @@ static int grid_of(int64_t n, int cap = 8192) {
 int aln_launch_init(const AlnDev &A, void *stream) {
     const int64_t n = A.n_task > A.n_sr ? A.n_task : A.n_sr;
     hipLaunchKernelGGL(aln_init_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, A);
+    return (int)hipGetLastError();
+}
+int aln_launch_heads(const AlnDev &A, void *stream) {
+    if (A.n_sr <= 0) return 0;
+    hipLaunchKernelGGL(aln_heads_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
 int aln_launch_list(const AlnDev &A, void *stream) {
