@@ -212,11 +212,14 @@ AL_HD void aln_heads_read(const AlnDev &A, int64_t r) {
 
 // is seed (slr, sst, srb, sqb, slen) "around" region i (mem_chain2aln's containment test)?
 AL_HD bool aln_around(const AlnDev &A, int64_t i, int64_t srb, int sqb, int slen, int lq) {
-    const int pqb = A.o_qb[i], pqe = A.o_qe[i];
-    const int64_t prb = A.o_rb[i], pre = A.o_re[i];
+    AlnBox bx;
+    if (A.box) bx = A.box[i];
+    else bx = AlnBox{A.o_qb[i], A.o_qe[i], A.o_rb[i], A.o_re[i], A.t_slen[i], A.o_w[i], 0, 0};
+    const int pqb = bx.qb, pqe = bx.qe;
+    const int64_t prb = bx.rb, pre = bx.re;
     if (srb < prb || srb + slen > pre || sqb < pqb || sqb + slen > pqe) return false;   // not contained
-    if ((double)(slen - A.t_slen[i]) > .1 * lq) return false;   // may give a better alignment
-    const int pw = A.o_w[i];
+    if ((double)(slen - bx.slen) > .1 * lq) return false;   // may give a better alignment
+    const int pw = bx.w;
     int64_t qd = sqb - pqb, rd = srb - prb;
     int mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
     int w = mg < pw ? mg : pw;
@@ -266,6 +269,9 @@ AL_HD int aln_walk_read(const AlnDev &A, int64_t r, Push push) {
         if (A.sel[j] & SEL_EXT) {
             A.ext[j] = 1;
             A.sel[j] = 0;
+            if (A.box)
+                A.box[j] = AlnBox{A.o_qb[j], A.o_qe[j], A.o_rb[j], A.o_re[j], A.t_slen[j], A.o_w[j], A.t_qbeg[j],
+                                  A.t_rbeg[j]};
         }
     const int lq = (int)(A.sr_off[r + 1] - A.sr_off[r]);
     int64_t c0 = k;   // first seed of k's chain
@@ -279,8 +285,14 @@ AL_HD int aln_walk_read(const AlnDev &A, int64_t r, Push push) {
             bool other = false;   // a longer extended seed of the chain overlapping on another diagonal
             for (int64_t j = c0; j < k; ++j) {
                 if (A.dec[j] != 1) continue;
-                const int tl = A.t_slen[j], tq = A.t_qbeg[j];
-                const int64_t tr = A.t_rbeg[j];
+                int tl, tq;
+                int64_t tr;
+                if (A.box) {
+                    const AlnBox bj = A.box[j];
+                    tl = bj.slen, tq = bj.tq, tr = bj.tr;
+                } else {
+                    tl = A.t_slen[j], tq = A.t_qbeg[j], tr = A.t_rbeg[j];
+                }
                 if (tl < slen * .95) continue;
                 if (sqb <= tq && sqb + slen - tq >= slen >> 2 && (int64_t)(tq - sqb) != tr - srb) { other = true; break; }
                 if (tq <= sqb && tq + tl - sqb >= slen >> 2 && (int64_t)(sqb - tq) != srb - tr) { other = true; break; }

@@ -17,6 +17,12 @@ struct AlnReg {
     int32_t qb, qe, score, truesc, w, seedlen0, lr, strand, task, secondary, patched, pad;
 };
 
+// an extended seed's region as the walk's containment tests read it, packed in one 32-byte
+// record (one cache line per test instead of one per field array)
+struct alignas(32) AlnBox {
+    int32_t qb, qe, rb, re, slen, w, tq, tr;   // region (strand coordinates), seed length, seed qbeg / rbeg
+};
+
 // a patch (mem_patch_reg) whose global score the final pass needs
 struct AlnPatch {
     int32_t read, m, lr, strand, qb, qe, rb, re, w, pad;   // query [qb,qe) x strand reference [rb,re)
@@ -42,6 +48,7 @@ struct AlnDev {
     int32_t *tlist;            // [n_task] the seeds to extend in the next round (their count in counter)
     int32_t *cnext;            // [n_task] of a chain's first seed: the next chain's first seed
     int32_t cnext_ready;       // cnext already written (aln_unpack_kernel, from the seeds' ranks)
+    AlnBox *box;               // [n_task] the extended seeds' regions, packed by the walk (null: the field arrays)
     int32_t *hprev;            // [n_task] of a chain head: the read's previous head on the same long read and strand (or -1); null: scan every head
     AlnReg *R;                 // [n_task] region scratch (read r: from seed_off[r])
     int32_t *ix;               // [n_task] sort scratch

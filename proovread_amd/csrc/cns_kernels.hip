@@ -863,7 +863,7 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         }
         __syncthreads();
         // 16-bit fixed-state counters: at most 65535 kept alignments per read
-        if (C->flag || (int64_t)((nwin + 4) & ~3) + 4 * (int64_t)C->nk > D.k_cap || C->nk > 65535) {
+        if (C->flag || (int64_t)((nwin + 4) & ~3) + 12 * (int64_t)C->nk > D.k_cap || C->nk > 65535) {
             CNS_CAP_FAIL();
             continue;
         }
@@ -884,7 +884,14 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
             const int rp = D.a_rpos[g], win = rp / G::W;
             const int kpos = Kh[win] + atomicAdd(&wcur[win], 1);
-            K[kpos] = make_int4(rp, D.a_end[g], i, 0);
+            // the entry carries what the windows' candidate selection needs (one 48-byte record
+            // instead of seven scattered per-alignment loads per window)
+            const int cbk = D.a_cb[g];
+            const int64_t so = D.seq_off[g], cgi = D.cig_off[g] + cbk;
+            int4 *Ke = K + 3 * (int64_t)kpos;
+            Ke[0] = make_int4(rp, D.a_end[g], D.lseq[g] | ((D.aflags[g] & 8) ? (int)0x80000000 : 0), D.a_sb[g]);
+            Ke[1] = make_int4(D.a_ce[g] - cbk, i, (int)(uint32_t)(so & 0xFFFFFFFFLL), (int)(so >> 32));
+            Ke[2] = make_int4((int)(uint32_t)(cgi & 0xFFFFFFFFLL), (int)(cgi >> 32), 0, 0);
         }
         __threadfence_block();
         __syncthreads();
@@ -942,18 +949,17 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                 int head = 0, nop = 0, sbk = 0, lsk = 0;
                 long long sdw = 0, cgi = 0;
                 if (kk < ke) {
-                    e = K[kk];
+                    e = K[3 * (int64_t)kk];
                     const long lo = e.x > w0 ? e.x : w0, hi = e.y < w0 + wn ? e.y : w0 + wn;
                     if (hi > lo) {
-                        const int64_t g = a0 + e.z;
-                        const int64_t so = D.seq_off[g];
-                        const int cbk = D.a_cb[g];
-                        lsk = D.lseq[g] | ((D.aflags[g] & 8) ? (int)0x80000000 : 0);
-                        sbk = D.a_sb[g];
-                        nop = D.a_ce[g] - cbk;
+                        const int4 e1 = K[3 * (int64_t)kk + 1], e2 = K[3 * (int64_t)kk + 2];
+                        const int64_t so = (int64_t)(uint32_t)e1.z | ((int64_t)e1.w << 32);
+                        lsk = e.z;
+                        sbk = e.w;
+                        nop = e1.x;
                         head = (int)(so & 3);
                         sdw = so >> 2;
-                        cgi = D.cig_off[g] + cbk;
+                        cgi = (int64_t)(uint32_t)e2.x | ((int64_t)e2.y << 32);
                         need = (long long)((head + (lsk & 0x7FFFFFFF) + 3) >> 2) | ((long long)nop << 32);
                     }
                 }

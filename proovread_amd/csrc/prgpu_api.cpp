@@ -444,11 +444,11 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
     const int grid = c->n_lr < c->n_cu * wgcu ? c->n_lr : c->n_cu * wgcu;
     const int grid_retry = c->n_lr < c->n_cu ? c->n_lr : c->n_cu;
     {
-        // K pool: per resident workgroup the window starts (longest read / 512 + 8 ints) and
-        // 4 ints per kept alignment
+        // K pool: per resident workgroup the window starts (longest read / 256 + 8 ints) and
+        // 12 ints per kept alignment
         int64_t lmax = 0;
         for (int i = 0; i < c->n_lr; ++i) lmax = std::max(lmax, c->lr_off_host[i + 1] - c->lr_off_host[i]);
-        const int64_t kc = (lmax / 512 + 12) + 4 * (c->k_need < 64 ? 64 : c->k_need);
+        const int64_t kc = ((lmax / 256 + 12) + 12 * (c->k_need < 64 ? 64 : c->k_need) + 3) & ~(int64_t)3;   // 16-byte entries
         int rc;
         if ((rc = B[CB_K].ensure((size_t)grid * kc * 4))) return rc;
         D.k_pool = B[CB_K].as<int32_t>();

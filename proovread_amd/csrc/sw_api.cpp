@@ -55,7 +55,7 @@ static const size_t SPILL_OFF = 96;   // in the SB_CELLS buffer: 3 x u64 overflo
 enum AlnBuf {
     SB_CHAIN = 35, SB_SEEDOFF, SB_SEL, SB_EXTF, SB_DEC, SB_RESUME, SB_ACNT, SB_AREG, SB_AIX, SB_PSCORE, SB_NPK,
     SB_FDONE, SB_PREQ, SB_NOUT, SB_OLIST, SB_OFLAG, SB_ATEMP, SB_AOFF, SB_ALIST, SB_AFLAG, SB_PPOOL, SB_GLIST,
-    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_TLIST, SB_CNEXT, SB_HPREV, SB_NBUF
+    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_TLIST, SB_CNEXT, SB_HPREV, SB_ABOX, SB_NBUF
 };
 static_assert(SB_NBUF <= 80, "SwResident buffer table");
 
@@ -205,6 +205,7 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
             (rc = ensure(r, SB_AOFF, r1 * 8)) || (rc = ensure(r, SB_ALIST, n1 * 4)) || (rc = ensure(r, SB_AFLAG, n1 * 4)) ||
             (rc = ensure(r, SB_PREQ, 1024 * sizeof(AlnPatch))) || (rc = ensure(r, SB_CIGSLOT, n1 * 8)) ||
             (rc = ensure(r, SB_TLIST, n1 * 4)) || (rc = ensure(r, SB_CNEXT, n1 * 4)) || (rc = ensure(r, SB_HPREV, n1 * 4)) ||
+            (rc = ensure(r, SB_ABOX, n1 * sizeof(AlnBox))) ||
             (rc = ensure(r, SB_CIGAT, n1 * 8)) || (rc = ensure(r, SB_PASS, n1)) || (rc = ensure(r, SB_CELLS, CELLS_BYTES)))
             return rc;
         size_t tb = aln_scan_temp_bytes(nt);
@@ -283,6 +284,7 @@ static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {
     A.cnext = (int32_t *)r.buf[SB_CNEXT];
     A.cnext_ready = r.cnext_ready ? 1 : 0;
     A.hprev = getenv("PRGPU_ALN_NO_HPREV") ? nullptr : (int32_t *)r.buf[SB_HPREV];
+    A.box = (AlnBox *)r.buf[SB_ABOX];
     A.R = (AlnReg *)r.buf[SB_AREG];
     A.ix = (int32_t *)r.buf[SB_AIX];
     A.pscore = (int32_t *)r.buf[SB_PSCORE];

@@ -53,6 +53,8 @@ extern "C" int aln_host_run(const osw_opts *o, double drop_ratio, double mask_le
     for (int64_t t = 0; t < n_task; ++t) alnc::aln_init_task(A, t);
     std::vector<int32_t> hprev((size_t)n1, -1);   // aln_heads_kernel (the device's walk path)
     A.hprev = hprev.data();
+    std::vector<AlnBox> box((size_t)n1);   // the walk's packed regions (the device path)
+    A.box = box.data();
     for (int r = 0; r < n_sr; ++r) alnc::aln_heads_read(A, r);
     for (int r = 0; r < n_sr; ++r) resume[(size_t)r] = (int32_t)seed_off[(size_t)r];
     int64_t rounds = 0, n_ext = 0, n_patch = 0;
