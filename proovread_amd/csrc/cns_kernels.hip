@@ -181,8 +181,14 @@ __device__ __forceinline__ void walk_states(const uint32_t *cg, int cb, int ce, 
                                             int cmin, int cmax, F &&f) {
     int col = rpos0, sidx = 0, qpos = 0;
     int p_col = 0, p_sidx = 0, p_kind = -1, p_qoff = 0, p_len = 0;
+    // a rolling window of the next 4 ops: each op is loaded 4 iterations before it is used
+    // (4 loads in flight instead of one HBM latency per op)
+    uint32_t w0 = cb < ce ? cg[cb] : 0u, w1 = cb + 1 < ce ? cg[cb + 1] : 0u;
+    uint32_t w2 = cb + 2 < ce ? cg[cb + 2] : 0u, w3 = cb + 3 < ce ? cg[cb + 3] : 0u;
     for (int k = cb; k < ce; ++k) {
-        const uint32_t c = cg[k];
+        const uint32_t c = w0;
+        w0 = w1; w1 = w2; w2 = w3;
+        w3 = k + 4 < ce ? cg[k + 4] : 0u;
         const int n = (int)(c >> 4), op = (int)(c & 15u);
         if (op == 1) {  // I
             if (k > cb) {
@@ -228,12 +234,19 @@ __device__ void prep_alignment(const CnsDev &D, const CnsParamsDev &P, int64_t g
     uint32_t st = 0;
     if (fl & 4) st |= ST_NOSEQ;
     long qlen = 0, md = 0;
-    for (int k = 0; k < n; ++k) {
-        const int op = cg[k] & 15, m = (int)(cg[k] >> 4);
-        if (op > 8) st |= ST_SAM;
-        if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) qlen += m;
-        if (op == 0 || op == 2) md += m;
-        if (op == 1 && m == 0) st |= ST_SAM;
+    for (int k0 = 0; k0 < n; k0 += 8) {   // 8 independent loads in flight (the later passes hit cache)
+        uint32_t v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = k0 + u < n ? cg[k0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (k0 + u >= n) break;
+            const int op = v[u] & 15, m = (int)(v[u] >> 4);
+            if (op > 8) st |= ST_SAM;
+            if (op == 0 || op == 1 || op == 4 || op == 7 || op == 8) qlen += m;
+            if (op == 0 || op == 2) md += m;
+            if (op == 1 && m == 0) st |= ST_SAM;
+        }
     }
     if (!(fl & 4) && n > 0 && qlen != ls) st |= ST_SAM;
     const bool clipped = n > 0 && (((cg[0] & 15) == 4) || ((cg[n - 1] & 15) == 4));
