@@ -11,7 +11,7 @@ sys.path.insert(0, str(HERE.parent))
 # cannot hide the results of the validated kernels.  test_bam2cns_cli.py: its BAM input
 # now goes through the native decoder (pr_bam_decode_alns; CPU-checked field for field).
 RUN_LAST = ("test_bam2cns_cli.py", "test_fantasticus_cns.py", "test_mask_gpu.py", "test_seed_gpu.py", "test_correct_loop.py",
-            "test_sw_edge_gpu.py", "test_perl_xs.py", "test_perl_xs_mem.py")
+            "test_sw_edge_gpu.py", "test_perl_xs.py", "test_perl_xs_mem.py", "test_file_chain_gpu.py")
 
 
 def pytest_configure(config):
