@@ -96,11 +96,12 @@ __global__ void __launch_bounds__(256) aln_list_kernel(AlnDev A) {
     }
 }
 
-__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A) {
+__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, int early) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= A.n_sr) return;
+    if (early && A.resume[r] < A.seed_off[r + 1]) return;   // its walk is still going
     AlnPatch req;
-    if (aln_final_read(A, r, &req)) {   // a patch score is needed: the read is replayed later
+    if (aln_final_read(A, r, &req) && !early) {   // a patch score is needed: the read is replayed later
         const int slot = atomicAdd(&A.counter[1], 1);
         if (slot < A.preq_cap) A.preq[slot] = req;
     }
@@ -230,7 +231,7 @@ int aln_launch_walk(const AlnDev &A, void *stream) {
     hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
-int aln_launch_final(const AlnDev &A, void *stream) {
+int aln_launch_final(const AlnDev &A, void *stream, int early) {
     if (A.n_sr <= 0) return 0;
     // tuning hook: PRGPU_ALN_FINAL_WG=k caps the resident workgroups per CU at k (dynamic LDS),
     // i.e. the reads whose region scratch is live at once
@@ -238,7 +239,8 @@ int aln_launch_final(const AlnDev &A, void *stream) {
     // then stays on chip instead of thrashing L2; profiles/r02_alnwg_sweep.txt)
     static const int wgcu = getenv("PRGPU_ALN_FINAL_WG") ? atoi(getenv("PRGPU_ALN_FINAL_WG")) : 3;
     const unsigned lds = wgcu > 0 ? (unsigned)(160 * 1024 / wgcu) & ~255u : 0u;
-    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A);
+    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A,
+                       early);
     return (int)hipGetLastError();
 }
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, void *stream) {

@@ -61,6 +61,10 @@ static_assert(SB_NBUF <= 80, "SwResident buffer table");
 
 namespace prgpu {
 void sw_release(SwResident &r) {
+    if (r.side) (void)hipStreamDestroy((hipStream_t)r.side);
+    for (void *&e : r.side_ev)
+        if (e) (void)hipEventDestroy((hipEvent_t)e), e = nullptr;
+    r.side = nullptr;
     for (int i = 0; i < 80; ++i) {
         if (r.buf[i]) (void)hipFree(r.buf[i]);
         r.buf[i] = nullptr;
@@ -325,6 +329,7 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     int32_t cnt[4] = {0, 0, 0, 0};
     int64_t n_list = r.n_rank0;   // round 0: every chain's first seed (listed after the init kernel)
     D.tsel = A.tlist;
+    bool early = false;
     for (;;) {   // mem_chain2aln: every round extends the listed seeds, the walk resumes
         D.tsel_n = n_list;
         HIPCHK(hipMemsetAsync(A.counter, 0, 8, s));
@@ -338,15 +343,37 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         HIPCHK(hipStreamSynchronize(s));
         ++r.ext_rounds;
         r.n_ext += cnt[0];
+        // after the first resumed walk most reads are decided: their final pass runs on a side
+        // stream while the later (small, latency-bound) rounds finish the rest; the late pass
+        // below skips them (fdone) and also replays any read whose patch score the early pass
+        // would have had to request
+        if (r.ext_rounds == 1 && cnt[0] > 0 && !getenv("PRGPU_BWA_NO_EARLY_FINAL")) {
+            if (!r.side) {
+                hipStream_t st;
+                HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+                r.side = (void *)st;
+                for (void *&ev : r.side_ev) {
+                    hipEvent_t x;
+                    HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+                    ev = (void *)x;
+                }
+            }
+            HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[0], s));
+            HIPCHK(hipStreamWaitEvent((hipStream_t)r.side, (hipEvent_t)r.side_ev[0], 0));
+            if ((e = aln_launch_final(A, r.side, 1))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+            HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[1], (hipStream_t)r.side));
+            early = true;
+        }
         if (getenv("PRGPU_BWA_DEBUG")) fprintf(stderr, "[bwa] round %d: %d requests\n", r.ext_rounds, cnt[0]);
         if (cnt[0] == 0) break;
         if (r.ext_rounds > r.n_task + 2) return pr_set_error(PR_ERR_HIP, "bwa mode: extension rounds do not converge");
         n_list = cnt[0];
     }
     D.tsel = nullptr;
+    if (early) HIPCHK(hipStreamWaitEvent(s, (hipEvent_t)r.side_ev[1], 0));
     for (int round = 0;; ++round) {   // final pass; mem_patch_reg global scores in extra rounds
         HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
-        if ((e = aln_launch_final(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        if ((e = aln_launch_final(A, (void *)s, 0))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         HIPCHK(hipMemcpyAsync(cnt, A.counter, 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (getenv("PRGPU_BWA_DEBUG")) fprintf(stderr, "[bwa] final round %d: %d patch requests\n", round, cnt[1]);
