@@ -1242,6 +1242,12 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0.f;
     if (n_sr && hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_seed = ms;
+    if (getenv("PRGPU_SEED_DEBUG") && K.prof) {   // pass 1's lane phase split (lane-summed ticks)
+        unsigned long long t8[8] = {};
+        if (hipMemcpy(t8, K.prof, sizeof t8, hipMemcpyDeviceToHost) == hipSuccess)
+            fprintf(stderr, "[seed] pass-1 lane ms (summed over lanes): smems %.1f chaining %.1f filter+out %.1f\n",
+                    t8[4] / 1e5, t8[5] / 1e5, t8[6] / 1e5);
+    }
     int64_t total = 0, bad = 0;
     for (int i = 0; i < n_sr; ++i) {
         if (nout[i] < 0 || nout[i] > caps.out) return set_error(PR_ERR_HIP, "seed kernel: bad task count");

@@ -112,17 +112,28 @@ SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
 SC_HD int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 
 // ---------------------------------------------------------------- occurrence table
+// the j-mer count tables j = 1..LC_MAX held on chip by the device kernels (5,460 entries):
+// table j at LC_OFF(j) = (4^j - 4) / 3
+constexpr int LC_MAX = 6;
+SC_HD constexpr int lc_off(int j) { return ((1 << (2 * j)) - 4) / 3; }
+constexpr int LC_N = lc_off(LC_MAX + 1);   // 4 + 16 + ... + 4^LC_MAX
+
 struct Occ {
     const IndexView *I;
     const Scratch *S;
     const uint8_t *q;
     int len;
+    const uint32_t *lc = nullptr;   // LDS copy of cnt[0 .. LC_MAX-1] (device) or null
 
     SC_HD int64_t operator()(int a, int b) const {
         const int n = b - a;
         if (n < KI) {
             uint32_t code = 0;
-            for (int x = a; x < b; ++x) code = (code << 2) | q[x];
+            const int32_t c12 = a + KI <= len ? S->codes[a] : -1;
+            if (c12 >= 0) code = (uint32_t)c12 >> (2 * (KI - n));   // the start's 12-mer code, truncated
+            else
+                for (int x = a; x < b; ++x) code = (code << 2) | q[x];
+            if (lc && n <= LC_MAX) return lc[lc_off(n) + code];
             return I->cnt[n - 1][code];
         }
         if (n - KI < HB) return S->ge[(int64_t)a * HB + (n - KI)];
@@ -443,13 +454,14 @@ SC_HD int cal_max_gap(const pr_seed_opts &O, int qlen) {
 #define SC_TICK(k) do { (void)ticks; } while (0)
 #endif
 SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
-                        pr_seed_task *out, int cap_out, int *n_out, unsigned long long *ticks = nullptr) {
+                        pr_seed_task *out, int cap_out, int *n_out, unsigned long long *ticks = nullptr,
+                        const uint32_t *lcnt = nullptr) {
     *n_out = 0;
     int err = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
     unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
 #endif
-    const Occ occ{&I, &S, q, len};
+    const Occ occ{&I, &S, q, len, lcnt};
     const int nm = collect_intv(occ, S, O, q, len, err);
     if (err) return err;
     SC_TICK(0);

@@ -21,6 +21,16 @@ namespace prgpu {
 constexpr int SEED_WAVES = 4;          // waves (reads in flight) per workgroup
 constexpr int SEED_LMAX = 1024;        // LDS start offsets per wave: reads <= 1024 bases
 
+// the short j-mer count tables (j <= LC_MAX) into the workgroup's LDS: the SMEM search's
+// occurrence counts of short extensions are dependent lookups, on chip instead of L2/MALL
+__device__ void load_lcnt(const seedc::IndexView &V, uint32_t *lc) {
+    for (int j = 1; j <= seedc::LC_MAX; ++j) {
+        const int o = seedc::lc_off(j), n = 1 << (2 * j);
+        for (int k = threadIdx.x; k < n; k += blockDim.x) lc[o + k] = V.cnt[j - 1][k];
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -129,6 +139,8 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
 // outgrew pass 1's slices), the sequential part on lane 0.
 __global__ void __launch_bounds__(64 * SEED_WAVES) seed_wave_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
+    __shared__ uint32_t lcnt[seedc::LC_N];
+    load_lcnt(D.V, lcnt);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t slot = (int64_t)blockIdx.x * SEED_WAVES + wv;
     if (slot >= D.n_lanes) return;
@@ -157,7 +169,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES) seed_wave_kernel(SeedDev D) {
             if (D.prof) pt[0] += wall_clock64() - t0;
             if (len > 0 && !err)
                 err = seedc::map_after_occ(D.V, D.O, S, q, len, i, D.out + (int64_t)i * D.caps.out, D.caps.out, &n,
-                                           D.prof ? pt + 1 : nullptr);
+                                           D.prof ? pt + 1 : nullptr, lcnt);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
         }
@@ -173,20 +185,29 @@ __global__ void __launch_bounds__(64 * SEED_WAVES) seed_wave_kernel(SeedDev D) {
 // goes to pass 2.
 __global__ void __launch_bounds__(64 * SEED_WAVES) seed_batch_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
+    __shared__ uint32_t lcnt[seedc::LC_N];
+    load_lcnt(D.V, lcnt);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t slot = (int64_t)blockIdx.x * SEED_WAVES + wv;
     if (slot >= D.n_lanes) return;
     uint8_t *base = D.scratch + slot * 64 * D.stride;
     int32_t *ho = hoff_lds[wv];
     unsigned long long pt[2] = {0ULL, 0ULL};   // wave wall-clock: occurrence tables, lane work
+    unsigned long long lt[3] = {0ULL, 0ULL, 0ULL};   // per lane: SMEMs, chaining, filter + output
     for (;;) {
         int b0 = 0;
         if (lane == 0) b0 = atomicAdd(D.next, 64);
         b0 = __shfl(b0, 0, 64);
         if (b0 >= D.n_sr) {   // every wave reaches this: the grid drains
+            if (D.prof) {
+#pragma unroll
+                for (int k = 0; k < 3; ++k)
+                    for (int o = 32; o > 0; o >>= 1) lt[k] += __shfl_xor(lt[k], o, 64);
+            }
             if (D.prof && lane == 0) {
                 atomicAdd(&D.prof[0], pt[0]);
                 atomicAdd(&D.prof[1], pt[1]);
+                for (int k = 0; k < 3; ++k) atomicAdd(&D.prof[4 + k], lt[k]);   // lane-summed
             }
             break;
         }
@@ -212,7 +233,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES) seed_batch_kernel(SeedDev D) 
             int n = 0, err = my_err;
             if (len > 0 && !err)
                 err = seedc::map_after_occ(D.V, D.O, S, D.sr_seq + o, len, i, D.out + (int64_t)i * D.caps.out,
-                                           D.caps.out, &n, nullptr);
+                                           D.caps.out, &n, D.prof ? lt : nullptr, lcnt);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
         }
