@@ -510,7 +510,17 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             c.w = c.kept = 0;
             c.first = -1;
             S.cv[ncv] = c;
-            for (int j = ncv; j > lo; --j) S.ord[j] = S.ord[j - 1];
+            // shift ord[lo, ncv) up by one, 8 independent loads before their stores (the
+            // element-wise loop waited out one scratch-load latency per element)
+            int j = ncv;
+            for (; j - 8 >= lo; j -= 8) {
+                int32_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[u] = S.ord[j - 8 + u];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) S.ord[j - 7 + u] = v[u];
+            }
+            for (; j > lo; --j) S.ord[j] = S.ord[j - 1];
             S.ord[lo] = ncv++;
         }
     }
