@@ -243,6 +243,7 @@ struct HostScratch {
     std::vector<seedc::Iv> mems, m1, curr, prev;
     std::vector<seedc::Seed> seeds;
     std::vector<int32_t> next, ord, kept;
+    std::vector<int64_t> spos;
     std::vector<seedc::Chain> cv, ch;
     std::vector<pr_seed_task> out;
     seedc::Scratch S{};
@@ -266,11 +267,12 @@ struct HostScratch {
         ch.resize((size_t)chains);
         ord.resize((size_t)chains);
         kept.resize((size_t)chains);
+        spos.resize((size_t)chains);
         out.resize((size_t)out_cap);
         S = seedc::Scratch{lmax,        hoff.data(),  qext.data(), codes.data(), ge.data(),   hpos.data(),
                            hml.data(),  hits,         mems.data(), mems_cap,     m1.data(),   curr.data(),
                            prev.data(), iv,           seeds.data(), next.data(), seeds_cap,   cv.data(),
-                           ch.data(),   ord.data(),   kept.data(), chains};
+                           ch.data(),   ord.data(),   kept.data(), spos.data(), chains};
     }
     void grow(int err) {
         if (err & seedc::SC_OVER_HITS) hits *= 2;

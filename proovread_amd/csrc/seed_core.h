@@ -99,6 +99,7 @@ struct Scratch {
     int32_t cap_seeds;
     Chain *cv, *ch;                            // [cap_chains] each
     int32_t *ord, *kept;                       // [cap_chains] each
+    int64_t *spos;                             // [cap_chains] cv[ord[i]].pos, kept beside ord
     int32_t cap_chains;
 };
 
@@ -487,10 +488,10 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             text_to_fr(I, S.hpos[k], s.rbeg, rid);
             s.qbeg = p.start;
             s.len = slen;
-            int lo = 0, hi = ncv;   // first chain with pos > rbeg
+            int lo = 0, hi = ncv;   // first chain with pos > rbeg (positions beside ord: one load a step)
             while (lo < hi) {
                 const int mid = (lo + hi) >> 1;
-                if (S.cv[S.ord[mid]].pos <= s.rbeg) lo = mid + 1;
+                if (S.spos[mid] <= s.rbeg) lo = mid + 1;
                 else hi = mid;
             }
             if (lo > 0) {
@@ -515,13 +516,15 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             int j = ncv;
             for (; j - 8 >= lo; j -= 8) {
                 int32_t v[8];
+                int64_t p[8];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = S.ord[j - 8 + u];
+                for (int u = 0; u < 8; ++u) v[u] = S.ord[j - 8 + u], p[u] = S.spos[j - 8 + u];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) S.ord[j - 7 + u] = v[u];
+                for (int u = 0; u < 8; ++u) S.ord[j - 7 + u] = v[u], S.spos[j - 7 + u] = p[u];
             }
-            for (; j > lo; --j) S.ord[j] = S.ord[j - 1];
+            for (; j > lo; --j) S.ord[j] = S.ord[j - 1], S.spos[j] = S.spos[j - 1];
             S.ord[lo] = ncv++;
+            S.spos[lo] = c.pos;
         }
     }
     SC_TICK(1);
@@ -669,6 +672,7 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += align8(4 * (int64_t)c.seeds);                   // next
     b += 2 * align8((int64_t)sizeof(Chain) * c.chains);  // cv, ch
     b += 2 * align8(4 * (int64_t)c.chains);              // ord, kept
+    b += align8(8 * (int64_t)c.chains);                  // spos
     return b;
 }
 
@@ -701,6 +705,7 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.ch = (Chain *)take((int64_t)sizeof(Chain) * c.chains);
     S.ord = (int32_t *)take(4 * (int64_t)c.chains);
     S.kept = (int32_t *)take(4 * (int64_t)c.chains);
+    S.spos = (int64_t *)take(8 * (int64_t)c.chains);
     S.cap_chains = c.chains;
     return S;
 }
