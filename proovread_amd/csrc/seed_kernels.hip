@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, 3) seed_wave_kernel(SeedDev D
 // with 64 reads' loads in flight per wave instead of one.  Scratch: 64 small slices per wave
 // (D.caps sized for the batch's read lengths); a read that outgrows its slice is flagged and
 // goes to pass 2.
-__global__ void __launch_bounds__(64 * SEED_WAVES, 3) seed_batch_kernel(SeedDev D) {
+__global__ void __launch_bounds__(64 * SEED_WAVES, 4) seed_batch_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
     load_lcnt(D.V, lcnt);
