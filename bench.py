@@ -153,6 +153,10 @@ def main():
             ms = ix_ms = None
             check = seed_phases = None
         else:
+            # steady state: a first, untimed call makes the scratch / output allocations, the
+            # timed one is what every later iteration pays
+            ix.map(d.sr_seq, d.sr_off, o, keep_on_device=True)
+            t = time.perf_counter()
             ix.map(d.sr_seq, d.sr_off, o, keep_on_device=True)
             ms, ix_ms = ix.gpu_ms(), ix.build_ms()
             seed_phases = ix.phase_ms()

@@ -265,14 +265,22 @@ AL_HD int aln_walk_read(const AlnDev &A, int64_t r, Push push) {
     const int64_t s0 = A.seed_off[r], s1 = A.seed_off[r + 1];
     int64_t k = A.resume[r];
     if (k >= s1) return 0;
-    for (int64_t j = s0; j < s1; ++j)   // results of the last extension round
-        if (A.sel[j] & SEL_EXT) {
+    // results of the last extension round (the flags read 8 at a time: independent loads)
+    for (int64_t j0 = s0; j0 < s1; j0 += 8) {
+        uint8_t f[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) f[u] = j0 + u < s1 ? A.sel[j0 + u] : (uint8_t)0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int64_t j = j0 + u;
+            if (!(f[u] & SEL_EXT)) continue;
             A.ext[j] = 1;
             A.sel[j] = 0;
             if (A.box)
                 A.box[j] = AlnBox{A.o_qb[j], A.o_qe[j], A.o_rb[j], A.o_re[j], A.t_slen[j], A.o_w[j], A.t_qbeg[j],
                                   A.t_rbeg[j]};
         }
+    }
     const int lq = (int)(A.sr_off[r + 1] - A.sr_off[r]);
     int64_t c0 = k;   // first seed of k's chain
     while (c0 > s0 && A.t_chain[c0 - 1] == A.t_chain[k]) --c0;
@@ -331,8 +339,14 @@ AL_HD int aln_final_read(const AlnDev &A, int64_t r, AlnPatch *req) {
     AlnReg *R = A.R + s0;
     int32_t *ix = A.ix + s0;
     int n = 0;
-    for (int64_t t = s0; t < s1; ++t) {
-        if (A.dec[t] != 1) continue;
+    for (int64_t t0 = s0; t0 < s1; t0 += 8) {   // the decisions read 8 at a time (independent loads)
+      uint8_t dv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) dv[u] = t0 + u < s1 ? A.dec[t0 + u] : (uint8_t)0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t t = t0 + u;
+        if (dv[u] != 1) continue;
         AlnReg &g = R[n];
         const int lr = A.t_lr[t], st = A.t_strand[t];
         const int64_t base = fr_of(A, lr, st, 0);
@@ -351,6 +365,7 @@ AL_HD int aln_final_read(const AlnDev &A, int64_t r, AlnPatch *req) {
         g.patched = 0;
         ix[n] = n;
         ++n;
+      }
     }
     const int64_t l_pac = A.lr_off[A.n_lr];
     int m_patch = 0;
