@@ -244,9 +244,30 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
     int nc = 0, np = 0;
     Iv ik{x, x + 1, occ(x, x + 1)};
     int i;
+    // the forward extension's counts for lengths 7..15 do not depend on each other: when the
+    // 12-mer at x is N-free they are loaded up front (9 independent loads instead of a
+    // dependent chain of table and count-row lookups); the same values as occ()
+    uint32_t pre[9];
+    const bool have = S.codes != nullptr && x + KI <= len && S.codes[x] >= 0;
+    if (have) {
+        const uint32_t c12 = (uint32_t)S.codes[x];
+#pragma unroll
+        for (int n = 7; n < KI; ++n) pre[n - 7] = occ.I->cnt[n - 1][c12 >> (2 * (KI - n))];
+#pragma unroll
+        for (int n = KI; n < 16; ++n) pre[n - 7] = S.ge[(int64_t)x * HB + (n - KI)];
+    }
     for (i = x + 1; i < len; ++i) {
         if (q[i] < 4) {
-            const int64_t o = occ(x, i + 1);
+            const int n = i + 1 - x;
+            int64_t o;
+            if (have && n >= 7 && n < 16) {
+                uint32_t v = pre[0];
+#pragma unroll
+                for (int t = 1; t < 9; ++t) v = n - 7 == t ? pre[t] : v;
+                o = v;
+            } else {
+                o = occ(x, i + 1);
+            }
             if (o != ik.occ) {
                 if (nc >= cap) { err |= SC_OVER_IV; return len; }
                 curr[nc++] = ik;
