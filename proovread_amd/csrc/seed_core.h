@@ -295,16 +295,25 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
     for (i = x - 1; i >= -1; --i) {
         const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
         nc = 0;
-        for (int k = 0; k < np; ++k) {
-            const Iv p = prev[k];
-            const int64_t o = c >= 0 ? occ(i, p.end) : 0;
-            if (c < 0 || o < min_intv) {
-                if (nc == 0 && (nmem == 0 || i + 1 < mem[nmem - 1].start)) {
-                    if (nmem >= cap) { err |= SC_OVER_IV; return len; }
-                    mem[nmem++] = Iv{i + 1, p.end, p.occ};
+        // the counts of this column's extensions do not depend on each other: 8 at a time
+        // (their loads in flight together), then the intervals in order as before
+        for (int k0 = 0; k0 < np; k0 += 8) {
+            int64_t ov[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) ov[u] = (c >= 0 && k0 + u < np) ? occ(i, prev[k0 + u].end) : 0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (k0 + u >= np) break;
+                const Iv p = prev[k0 + u];
+                const int64_t o = ov[u];
+                if (c < 0 || o < min_intv) {
+                    if (nc == 0 && (nmem == 0 || i + 1 < mem[nmem - 1].start)) {
+                        if (nmem >= cap) { err |= SC_OVER_IV; return len; }
+                        mem[nmem++] = Iv{i + 1, p.end, p.occ};
+                    }
+                } else if (nc == 0 || o != curr[nc - 1].occ) {
+                    curr[nc++] = Iv{i, p.end, o};   // nc <= np <= cap
                 }
-            } else if (nc == 0 || o != curr[nc - 1].occ) {
-                curr[nc++] = Iv{i, p.end, o};   // nc <= np <= cap
             }
         }
         if (nc == 0) break;
