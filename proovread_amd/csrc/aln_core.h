@@ -255,6 +255,23 @@ AL_HD bool aln_around_any(const AlnDev &A, int64_t s0, int64_t c0, int64_t k, in
     return false;
 }
 
+// could mem_chain2aln's "longer seed on another diagonal" exception apply to seed k later: a
+// chain mate j in [c0, k) not skipped (dec != 2), >= 95 % of k's length, overlapping k on the
+// query on another diagonal (the walk's own test, for mates whose region is not known yet)
+AL_HD bool aln_maybe_other(const AlnDev &A, int64_t c0, int64_t k) {
+    const int64_t srb = A.t_rbeg[k];
+    const int sqb = A.t_qbeg[k], slen = A.t_slen[k];
+    for (int64_t j = c0; j < k; ++j) {
+        if (A.dec[j] == 2) continue;
+        const int tl = A.t_slen[j], tq = A.t_qbeg[j];
+        const int64_t tr = A.t_rbeg[j];
+        if (tl < slen * .95) continue;
+        if (sqb <= tq && sqb + slen - tq >= slen >> 2 && (int64_t)(tq - sqb) != tr - srb) return true;
+        if (tq <= sqb && tq + tl - sqb >= slen >> 2 && (int64_t)(sqb - tq) != srb - tr) return true;
+    }
+    return false;
+}
+
 // mem_chain2aln for read r, resumed at its first open seed.  A seed to extend whose result
 // is not there stops the walk (decisions before it are final: they only depend on earlier
 // seeds); the later open seeds that are around no region yet are requested with it
@@ -318,7 +335,11 @@ AL_HD int aln_walk_read(const AlnDev &A, int64_t r, Push push) {
             for (int64_t kk = k + 1; kk < s1; ++kk) {
                 if (A.t_chain[kk] != A.t_chain[kk - 1]) cc = kk;
                 if (A.dec[kk] || A.ext[kk] || (A.sel[kk] & SEL_EXT)) continue;
-                if (aln_around_any(A, s0, cc, kk, lq)) continue;
+                // a seed inside a region is still extended when a longer (>= 95 %) seed of its
+                // chain overlaps it on another diagonal; that seed's region may not exist yet,
+                // so any such chain mate that is not skipped makes the seed speculated too
+                // (saves the late rounds those seeds would each cost)
+                if (aln_around_any(A, s0, cc, kk, lq) && !aln_maybe_other(A, cc, kk)) continue;
                 A.sel[kk] = SEL_EXT;
                 push(kk);
                 ++n;
