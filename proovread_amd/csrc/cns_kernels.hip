@@ -422,8 +422,6 @@ using GeoS = CnsGeo<512, 512, 1024, 8192, 2048, 1024, 2, true>;
 // CU, 512-column windows) stays selectable with PRGPU_CNS_GEO=S
 using GeoM = CnsGeo<256, 256, 384, 3072, 768, 384, 4, true>;
 using GeoL = CnsGeo<2048, 512, 2048, 8192, 2560, 1024, 1, false>;
-// experimental: 5 workgroups per CU (<= 32 KB LDS: smaller staging and tables), PRGPU_CNS_GEO=5
-using GeoM5 = CnsGeo<240, 256, 256, 2048, 512, 256, 5, true>;
 
 // per-column descriptor: flag bits above the 12-bit state-table slot
 constexpr uint32_t DESC_FIXED = 1u << 16;
@@ -1639,11 +1637,7 @@ static bool cns_geo_m() {
     const char *g = getenv("PRGPU_CNS_GEO");
     return !(g && g[0] == 'S');
 }
-static bool cns_geo_5() {
-    const char *g = getenv("PRGPU_CNS_GEO");
-    return g && g[0] == '5';
-}
-int cns_wg_per_cu() { return cns_geo_5() ? GeoM5::WGCU : cns_geo_m() ? GeoM::WGCU : GeoS::WGCU; }
+int cns_wg_per_cu() { return cns_geo_m() ? GeoM::WGCU : GeoS::WGCU; }
 
 int cns_launch(const CnsDev &D, const CnsParamsDev &P, int grid, int grid_retry, void *stream) {
     static bool attr = false;
@@ -1655,14 +1649,11 @@ int cns_launch(const CnsDev &D, const CnsParamsDev &P, int grid, int grid_retry,
         if (e != hipSuccess) return (int)e;
         e = hipFuncSetAttribute((const void *)cns_lr_kernel<GeoL>, hipFuncAttributeMaxDynamicSharedMemorySize, GeoL::LDS);
         if (e != hipSuccess) return (int)e;
-        e = hipFuncSetAttribute((const void *)cns_lr_kernel<GeoM5>, hipFuncAttributeMaxDynamicSharedMemorySize, GeoM5::LDS);
-        if (e != hipSuccess) return (int)e;
         attr = true;
     }
     hipStream_t s = (hipStream_t)stream;
     if (!D.force_large) {
-        if (cns_geo_5()) hipLaunchKernelGGL(cns_lr_kernel<GeoM5>, dim3(grid), dim3(CNS_THREADS), GeoM5::LDS, s, D, P);
-        else if (cns_geo_m()) hipLaunchKernelGGL(cns_lr_kernel<GeoM>, dim3(grid), dim3(CNS_THREADS), GeoM::LDS, s, D, P);
+        if (cns_geo_m()) hipLaunchKernelGGL(cns_lr_kernel<GeoM>, dim3(grid), dim3(CNS_THREADS), GeoM::LDS, s, D, P);
         else hipLaunchKernelGGL(cns_lr_kernel<GeoS>, dim3(grid), dim3(CNS_THREADS), GeoS::LDS, s, D, P);
     }
     // reads whose tables outgrew the small geometry (device-side list; usually empty)

@@ -309,6 +309,20 @@ static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {
     return A;
 }
 
+// the side stream (and its events) of the bwa-mode rounds
+static int side_stream(SwResident &r) {
+    if (r.side) return 0;
+    hipStream_t st;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    r.side = (void *)st;
+    for (void *&ev : r.side_ev) {
+        hipEvent_t x;
+        HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
+        ev = (void *)x;
+    }
+    return 0;
+}
+
 // bwa mode: extension rounds (mem_chain2aln), the final pass (mem_sort_dedup_patch ..
 // mem_reg2sam) with mem_patch_reg rounds, then the CIGAR pass over the reported alignments
 static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, const pr_sw_opts *o, int grid_w,
@@ -325,7 +339,16 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
     if ((e = aln_launch_init(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     if ((e = aln_launch_list(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
-    if (A.hprev && (e = aln_launch_heads(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    // the chain-head links only feed the walk: built on the side stream beside round 0's extension
+    bool heads_side = false;
+    if (A.hprev) {
+        if ((rc = side_stream(r))) return rc;
+        HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[0], s));
+        HIPCHK(hipStreamWaitEvent((hipStream_t)r.side, (hipEvent_t)r.side_ev[0], 0));
+        if ((e = aln_launch_heads(A, r.side))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[2], (hipStream_t)r.side));
+        heads_side = true;
+    }
     int32_t cnt[4] = {0, 0, 0, 0};
     int64_t n_list = r.n_rank0;   // round 0: every chain's first seed (listed after the init kernel)
     D.tsel = A.tlist;
@@ -336,6 +359,10 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         if (n_list) {
             e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s);
             if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        }
+        if (heads_side) {
+            HIPCHK(hipStreamWaitEvent(s, (hipEvent_t)r.side_ev[2], 0));
+            heads_side = false;
         }
         if ((e = aln_launch_walk(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         if ((e = aln_launch_list(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
@@ -348,16 +375,7 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         // below skips them (fdone) and also replays any read whose patch score the early pass
         // would have had to request
         if (r.ext_rounds == 1 && cnt[0] > 0 && !getenv("PRGPU_BWA_NO_EARLY_FINAL")) {
-            if (!r.side) {
-                hipStream_t st;
-                HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-                r.side = (void *)st;
-                for (void *&ev : r.side_ev) {
-                    hipEvent_t x;
-                    HIPCHK(hipEventCreateWithFlags(&x, hipEventDisableTiming));
-                    ev = (void *)x;
-                }
-            }
+            if ((rc = side_stream(r))) return rc;
             HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[0], s));
             HIPCHK(hipStreamWaitEvent((hipStream_t)r.side, (hipEvent_t)r.side_ev[0], 0));
             if ((e = aln_launch_final(A, r.side, 1))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));

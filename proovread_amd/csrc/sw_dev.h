@@ -100,7 +100,7 @@ struct SwResident {
     int64_t n_rank0 = 0;        // first seeds of the chains (the first round)
     bool cnext_ready = false;   // cnext written by the device-seed unpack (seed ranks)
     void *side = nullptr;       // hipStream_t: the early final pass beside the later extension rounds
-    void *side_ev[2] = {nullptr, nullptr};   // hipEvent_t
+    void *side_ev[3] = {nullptr, nullptr, nullptr};   // hipEvent_t
     int64_t n_patch = 0;        // mem_patch_reg global scores computed
     int64_t cig_slots = 0;      // ops in the slots (= first spill op)
     int64_t n_overflow = 0;     // tasks of the last launch whose CIGAR went to the spill area
