@@ -137,7 +137,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
 
 // Pass 2: one wave per read with the large scratch slice (the reads of D.rlist: those that
 // outgrew pass 1's slices), the sequential part on lane 0.
-__global__ void __launch_bounds__(64 * SEED_WAVES, 3) seed_wave_kernel(SeedDev D) {
+__global__ void __launch_bounds__(64 * SEED_WAVES, 4) seed_wave_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
     load_lcnt(D.V, lcnt);
