@@ -44,6 +44,9 @@ OPS_PER_CELL = 14   # SURVEY.md §8d canonical int ops per DP cell
 # bwa-proovread -b BIN -l LEN of a bwa-sr iteration: BIN = bin-size 20 (proovread.cfg:259-273),
 # LEN = BIN x min(--coverage 50, sr-coverage 15) (bin/proovread:1302-1313)
 BIN_FILTER = (20, 20.0 * 15.0)
+# HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over this bench
+# (tools/pmc_summary.py; MI355X_MICROARCH.md's corrections)
+PMC_FILE = "pmc_r02_bwa.json"
 
 
 def parse():
@@ -54,6 +57,9 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the configs[1] workload per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-lrs-per-worker", type=int, default=256)
+    ap.add_argument("--comm", choices=("rccl", "none"), default="rccl",
+                    help="rccl: the step all-reduces the device {bpt, bpN} statistic over an RCCL communicator at "
+                         "every world size (N=1 included, exactly as N>1 runs it); none: no communicator at N=1")
     ap.add_argument("--seeds", choices=("truth", "host", "gpu"), default="gpu",
                     help="seeds: the product's seeding front end (host path / GPU path; bwa mem seeding "
                          "+ chaining restated; every seed of the kept chains in bwa mode), or the simulation "
@@ -201,7 +207,7 @@ def main():
     # GPU: libprgpu only (its own HIP runtime and RCCL); torch is never loaded here
     from proovread_amd import _abi, cns, comm as comm_mod, iteration, sw
     ctx = _abi.Context(local)
-    cm = comm_mod.RcclComm.from_env(ctx) if world > 1 else None
+    cm = comm_mod.RcclComm.from_env(ctx) if world > 1 or args.comm == "rccl" else None
     if args.seeds == "gpu":
         d, seed_info = seed_front_end(ctx, want_host_copy=rank == 0)
         if want_cpu:   # the same GPU-made seeds, CPU chain in a child process
@@ -235,12 +241,16 @@ def main():
     t0 = time.perf_counter()
     ms = np.zeros(4)
     dom_ms, dom_cells = 0.0, 0
+    ext_ms, ext_cells, ext_launches = 0.0, 0, 0
     for _ in range(args.steps):
         step()
         ms += np.array(it.timing())
         dm, dc = sw.dominant_kernel(ctx)
         dom_ms += dm
         dom_cells = dc
+        xm, xc, xn = sw.extension_kernels(ctx)
+        ext_ms += xm
+        ext_cells, ext_launches = xc, xn
     barrier()
     el = time.perf_counter() - t0
     if cm is not None:
@@ -269,20 +279,35 @@ def main():
     cells = ce + cg
     dom_ms /= max(args.steps, 1)
     dom_tops = dom_cells * OPS_PER_CELL / (dom_ms * 1e-3) / 1e12
+    ext_ms /= max(args.steps, 1)
+    ext_tops = ext_cells * OPS_PER_CELL / (ext_ms * 1e-3) / 1e12 if ext_ms > 0 else 0.0
     # pileup kernel: algorithmic bytes (SURVEY.md §8d model) / kernel time
     n_aln, sum_ncig, sum_lseq = it.alignment_stats()
     cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + lr_bases * (2 + 2 + 6 * 4 * 2)
     # HBM bytes per launch from the PMC FETCH_SIZE / WRITE_SIZE passes of this bwa-mode step
     # (tools/r02_gpu5.sh -> tools/pmc_summary.py -> profiles/pmc_r02_bwa.json)
-    prof = ROOT / "profiles" / "pmc_r02_bwa.json"
-    traffic = traffic_cns = None
+    prof = ROOT / "profiles" / PMC_FILE
+    traffic = traffic_cns = traffic_ext = None
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())
             traffic = pm.get("sw_global_pk_kernel<40>", {}).get("hbm_bytes_per_launch")
             traffic_cns = next((v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith("cns_lr_kernel")), None)
+            traffic_ext = {k: v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith("sw_ext_")}
         except Exception:
-            traffic = traffic_cns = None
+            traffic = traffic_cns = traffic_ext = None
+    ref_cpu = None   # the reference's own Perl consensus, timed in the build container
+    rp = ROOT / "profiles" / "r03_reference_cpu_consensus.json"
+    if rp.exists():
+        try:
+            r3 = json.loads(rp.read_text())
+            rpl = r3["reference_perl"]
+            ref_cpu = {"value": rpl["Mbases_per_s"], "unit": "Mbases/s", "cores": rpl["processes"], "kind": "reference",
+                       "scope": "consensus only, build container", "cpu": r3["host"]["cpu"],
+                       "sample": r3["workload"] + f"; {rpl['engine']}; {rpl['wall_s']} s wall",
+                       "source": "profiles/r03_reference_cpu_consensus.json (tools/time_reference_r03.py)"}
+        except Exception:
+            ref_cpu = None
     out = {
         "metric": "corrected long-read Mbases/sec per node",
         "value": round(value, 3),
@@ -333,7 +358,18 @@ def main():
             "frac": round(cns_bytes / (ms[3] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": int(cns_bytes),
             "alignments": int(n_aln), "traffic": traffic_cns,
         },
+        "roofline_extension": {
+            "kernels": "every ksw_extend2 DP launch of the step (sw_ext_pk_kernel<40>, sw_ext_phase_kernel<*>, wide), "
+                       "all bwa-mode rounds, both sides and band tries",
+            "bound": "valu", "achieved": round(ext_tops, 3), "peak": round(VALU_PEAK_TOPS, 2), "unit": "TOP/s (int32)",
+            "frac": round(ext_tops / VALU_PEAK_TOPS, 4), "summed_launch_ms": round(ext_ms, 3),
+            "launches": ext_launches, "cells": int(ext_cells), "ops_per_cell": OPS_PER_CELL,
+            "frac_of_packed_int16_peak": round(ext_tops / (2 * VALU_PEAK_TOPS), 4),
+            "traffic_per_launch": traffic_ext,
+        },
         "cpu_baseline": cpu,
+        "cpu_baseline_reference": ref_cpu,
+        "comm": "rccl" if cm is not None else "none",
         "seeding": seed_info,
         # one whole bwa-sr iteration as proovread runs it, wall clock: index build + seeding
         # (bwa-proovread index / mem front end; seeds left in HBM) + upload + the timed step

@@ -295,6 +295,12 @@ int pr_sw_last_cells(pr_ctx *ctx, int64_t *cells_extend, int64_t *cells_global);
  * launch's dominant kernel, the CIGAR pass's packed launch (the band <= 40 ring launch
  * when the packed kernel is off), and the DP cells it computed. */
 int pr_sw_dominant_kernel(pr_ctx *ctx, double *ms, int64_t *cells);
+/* Diagnostics for the extension stage's roofline: the summed durations (HIP events around
+ * each launch on the SW stream) of every extension DP launch of the last pr_sw_launch
+ * (ksw_extend2: packed, ring and wide kernels, both sides, both band tries, every bwa-mode
+ * round), the DP cells they computed and the number of launches.  PR_ERR_CAPACITY when
+ * there were more launches than the 64 timed ones. */
+int pr_sw_extension_kernels(pr_ctx *ctx, double *ms, int64_t *cells, int32_t *launches);
 /* Diagnostics: shader-clock cycles summed over waves of the packed CIGAR kernel's
  * phases in the last launch: [0] query masks, [1] DP, [2] backtrack, [3] CIGAR emit. */
 int pr_sw_phase_cycles(pr_ctx *ctx, int64_t *out4);
@@ -317,7 +323,10 @@ typedef struct pr_seed_opts {
     double drop_ratio;       /* -D                                            */
     int max_chain_gap;       /* bwa default 10000                             */
     double mask_level;       /* bwa default 0.5                               */
-    int a, o_del, e_del, o_ins, e_ins;   /* scoring, for the chain window (cal_max_gap) */
+    int a, o_del, e_del, o_ins, e_ins;   /* scoring, for the chain window (cal_max_gap) and
+                                            mem_flt_chained_seeds' seed SW            */
+    int b;                   /* -B mismatch penalty (mem_flt_chained_seeds' seed SW; that
+                                filter runs for reads with 1.1 W <= 0.05 length only) */
 } pr_seed_opts;
 typedef struct pr_seed_task {
     int32_t sr, lr;          /* short read, long read                         */

@@ -168,17 +168,22 @@ def _lr_task_records(lr: int):
     return recs
 
 
-def _lr_chain(lr: int):
-    """The records of long read `lr` (bwa output order) -> -b/-l filter -> coordinate order ->
-    consensus."""
-    d = _D
+def _lr_sam_lines(lr: int):
+    """The records of long read `lr` (bwa output order) -> -b/-l filter -> coordinate order:
+    the SAM lines bam2cns reads for it (bin/bam2cns:336)."""
     recs = _RECS[lr] if _RECS is not None else _lr_task_records(lr)
     recs = [(x[0], x[1], i, x[2], x[3], x[4]) for i, x in enumerate(recs)]
     if _BINF is not None:   # records in bwa's output order for this long read
         keep = _bin_filter([(x[0], float(x[4]), x[5]) for x in recs], *_BINF)
         recs = [x for x, k in zip(recs, keep) if k]
     recs.sort(key=lambda x: (x[0], x[1], x[2]))
-    lines = [x[3].encode() for x in recs]
+    return [x[3] for x in recs]
+
+
+def _lr_chain(lr: int):
+    """The records of long read `lr` (_lr_sam_lines) -> consensus."""
+    d = _D
+    lines = [x.encode() for x in _lr_sam_lines(lr)]
     arr = (C.c_char_p * (len(lines) + 1))(*lines)
     a, b = int(d.lr_off[lr]), int(d.lr_off[lr + 1])
     ref = _REF[a:b].tobytes() if _REF is not None else _ASCII[d.lr_seq[a:b]].tobytes()
@@ -200,7 +205,7 @@ def _init_worker():
 
 
 def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers=None, ref_seq=None,
-               ref_qual=None, detect_chimera=False, full=False, bin_filter=None, drop_ratio=None):
+               ref_qual=None, detect_chimera=False, full=False, bin_filter=None, drop_ratio=None, sam_only=False):
     """Run the CPU chain on long reads `lrs`; returns (wall seconds, bases, results, workers).
 
     d.t_chain set (bwa mode): d's tasks are every seed of the kept chains grouped by short
@@ -211,7 +216,8 @@ def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers
     (bam2cns --ref, the previous iteration's .fq) when it differs from the mapped reads;
     full: per read (rc, fastq, trace, chim lines) instead of (rc, fastq); bin_filter: (BIN, LEN)
     of bwa-proovread -b/-l applied to each long read's records, or None; drop_ratio: bwa -D
-    (default: 0.75 for bwa-sr-finish, else 0)."""
+    (default: 0.75 for bwa-sr-finish, else 0); sam_only: per read its SAM lines in coordinate
+    order (what the consensus would read) instead of the consensus."""
     global _D, _OPTS, _PARAMS, _REF, _QUAL, _FULL, _BINF, _AOPTS, _SEEDS, _SEED_FIRST, _RECS
     _D = d
     _BINF = tuple(bin_filter) if bin_filter else None
@@ -274,9 +280,10 @@ def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers
             for lr, rec in recs:
                 if lr in _RECS:
                     _RECS[lr].append(rec)
+    fn = _lr_sam_lines if sam_only else _lr_chain
     if workers == 1:
-        res = [_lr_chain(i) for i in lrs]
+        res = [fn(i) for i in lrs]
     else:
         with mp.get_context("fork").Pool(workers, initializer=_init_worker) as pool:
-            res = pool.map(_lr_chain, lrs, chunksize=1)
+            res = pool.map(fn, lrs, chunksize=1)
     return time.perf_counter() - t, bases, res, workers

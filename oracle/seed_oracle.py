@@ -10,8 +10,10 @@ complements (no k-mer index, no count tables).
 Restated from upstream bwa (absent here; bwa-proovread's pinned commit is
 unknown, .gitmodules:4-6 — parity unpinned):
   bwamem.c  mem_collect_intv (three seeding rounds), mem_chain, test_and_merge,
-            mem_chain_weight, mem_chain_flt, mem_chain2aln's seed order (every seed of a
-            kept chain, srt order) and window
+            mem_chain_weight, mem_chain_flt, mem_flt_chained_seeds + mem_seed_sw (bwa >=
+            0.7.13: reads with 1.1 W <= 0.05 length), mem_chain2aln's seed order (every
+            seed of a kept chain, srt order) and window
+  ksw.c     ksw_align2's best local score (mem_seed_sw), as a plain affine-gap local DP
   bwt.c     bwt_smem1a (max_intv = 0), bwt_seed_strategy1
 over the same index definition as the library: forward long reads then the
 reverse complement of their concatenation (bwa's forward-reverse coordinates),
@@ -21,6 +23,8 @@ from __future__ import annotations
 
 import bisect
 import dataclasses
+import math
+import struct
 
 COMP = {0: 3, 1: 2, 2: 1, 3: 0}
 
@@ -42,11 +46,12 @@ class Opts:
     e_del: int = 4
     o_ins: int = 1
     e_ins: int = 3
+    b: int = 11
 
     @classmethod
     def finish(cls):
         return cls(min_seed_len=17, min_chain_weight=18, w=30, split_factor=1.5, drop_ratio=0.75,
-                   o_del=15, e_del=3, o_ins=19, e_ins=3)
+                   o_del=15, e_del=3, o_ins=19, e_ins=3, b=13)
 
 
 class Index:
@@ -220,6 +225,79 @@ def _max_gap(O, qlen):
     return min(max(l_del, l_ins, 1), O.w << 1)
 
 
+def _f32(x: float) -> float:
+    return struct.unpack("f", struct.pack("f", x))[0]
+
+
+def flt_min_score(O: Opts, n: int):
+    """mem_flt_chained_seeds' min_HSP_score for a read of n bases, or None when bwa skips the
+    filter: min_l = MEM_HSP_COEF * W (1.1f, float arithmetic), skipped when min_l >
+    MEM_SEEDSW_COEF * l_query (0.05f * n, float)."""
+    if O.min_chain_weight:
+        min_l = _f32(_f32(1.1) * O.min_chain_weight)
+    else:
+        min_l = _f32(5.5) * math.log(n)   # MEM_MINSC_COEF * log(l_query)
+    if min_l > _f32(_f32(0.05) * n):
+        return None
+    return int(O.a * min_l + .499)
+
+
+def _ref_base(I: Index, rid: int, p: int) -> int:
+    """The base at forward-reverse coordinate p of long read rid (code 0-4)."""
+    if p < I.l_pac:
+        return "ACGTN".index(I.contigs[rid][p - I.lr_off[rid]])
+    return "ACGTN".index(I.contigs[2 * I.n_lr - 1 - rid][p - (2 * I.l_pac - I.lr_off[rid + 1])])
+
+
+def local_sw(O: Opts, q, t) -> int:
+    """ksw_align2's score: best local alignment of query q against target t, a gap of k
+    bases costing o + k e (deletions = target bases: o_del/e_del; insertions: o_ins/e_ins),
+    match a, mismatch -b, N -1."""
+    qn = len(q)
+    H = [0] * qn
+    E = [0] * qn
+    best = 0
+    for tb in t:
+        hdiag = f = 0
+        for j in range(qn):
+            qb = q[j]
+            sc = -1 if (tb > 3 or qb > 3) else (O.a if tb == qb else -O.b)
+            e = E[j]
+            h = max(hdiag + sc, e, f, 0)
+            hdiag = H[j]
+            H[j] = h
+            best = max(best, h)
+            E[j] = max(e - O.e_del, h - O.o_del - O.e_del, 0)
+            f = max(f - O.e_ins, h - O.o_ins - O.e_ins, 0)
+    return best
+
+
+def seed_sw(I: Index, O: Opts, q, s, rid) -> int:
+    """mem_seed_sw: the local score around seed s (+- MEM_SHORT_EXT = 50), or -1 when the seed
+    or a window reaches MEM_SHORT_LEN = 200; the reference window is clamped to [0, 2 l_pac),
+    the seed's strand half and (bns_fetch_seq) its long read."""
+    n = len(q)
+    if s["len"] >= 200:
+        return -1
+    qb, qe = max(s["qbeg"] - 50, 0), min(s["qbeg"] + s["len"] + 50, n)
+    rb, re = s["rbeg"], s["rbeg"] + s["len"]
+    mid = (rb + re) >> 1
+    rb, re = max(rb - 50, 0), min(re + 50, 2 * I.l_pac)
+    if rb < I.l_pac < re:
+        if mid < I.l_pac:
+            re = I.l_pac
+        else:
+            rb = I.l_pac
+    if qe - qb >= 200 or re - rb >= 200:
+        return -1
+    if mid >= I.l_pac:
+        fb, fe = 2 * I.l_pac - I.lr_off[rid + 1], 2 * I.l_pac - I.lr_off[rid]
+    else:
+        fb, fe = I.lr_off[rid], I.lr_off[rid + 1]
+    rb, re = max(rb, fb), min(re, fe)
+    return local_sw(O, q[qb:qe], [_ref_base(I, rid, p) for p in range(rb, re)])
+
+
 def map_read(I: Index, O: Opts, q, sid=0):
     """Tasks of one read: dicts with the pr_seed_task fields."""
     n = len(q)
@@ -277,20 +355,33 @@ def map_read(I: Index, O: Opts, q, sid=0):
                 chains[chains[j]["first"]]["kept"] = 1
     out = []
     nk = 0
+    flt = flt_min_score(O, n)
     for c in chains:
         if c["kept"] == 0:
             continue
-        rev = c["seeds"][0]["rbeg"] >= I.l_pac
+        seeds = c["seeds"]
+        scores = [t["len"] for t in seeds]
+        if flt is not None:   # mem_flt_chained_seeds
+            kept_s = []
+            for t in seeds:
+                x = seed_sw(I, O, q, t, c["rid"])
+                if x < 0 or x >= flt:
+                    kept_s.append((t, t["len"] * O.a if x < 0 else x))
+            seeds = [x[0] for x in kept_s]
+            scores = [x[1] for x in kept_s]
+            if not seeds:   # mem_chain2aln returns on an empty chain
+                continue
+        rev = seeds[0]["rbeg"] >= I.l_pac
         rid = c["rid"]
         L = I.lr_off[rid + 1] - I.lr_off[rid]
         cs = I.l_pac + (I.l_pac - I.lr_off[rid + 1]) if rev else I.lr_off[rid]
-        r0 = min(t["rbeg"] - (t["qbeg"] + _max_gap(O, t["qbeg"])) for t in c["seeds"]) - cs
+        r0 = min(t["rbeg"] - (t["qbeg"] + _max_gap(O, t["qbeg"])) for t in seeds) - cs
         r1 = max(t["rbeg"] + t["len"] + ((n - t["qbeg"] - t["len"]) + _max_gap(O, n - t["qbeg"] - t["len"]))
-                 for t in c["seeds"]) - cs
-        # mem_chain2aln's srt order: (score = length, index) descending
-        order = sorted(range(len(c["seeds"])), key=lambda i: (c["seeds"][i]["len"], i), reverse=True)
+                 for t in seeds) - cs
+        # mem_chain2aln's srt order: (score, index) descending; score = length unless filtered
+        order = sorted(range(len(seeds)), key=lambda i: (scores[i], i), reverse=True)
         for rank, i in enumerate(order):
-            s = c["seeds"][i]
+            s = seeds[i]
             out.append(dict(sr=sid, lr=rid, strand=int(rev), qbeg=s["qbeg"], rbeg=s["rbeg"] - cs, slen=s["len"],
                             rmax0=max(r0, 0), rmax1=min(r1, L), chain=nk, rank=rank))
         nk += 1

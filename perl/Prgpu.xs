@@ -354,6 +354,7 @@ seed_map(IV ix, HV *opts, SV *sr_seq, SV *sr_off, int threads)
     o.e_del = inum(aTHX_ opts, "e_del", o.e_del);
     o.o_ins = inum(aTHX_ opts, "o_ins", o.o_ins);
     o.e_ins = inum(aTHX_ opts, "e_ins", o.e_ins);
+    o.b = inum(aTHX_ opts, "b", o.b);
     rc = pr_seed_map(INT2PTR(const pr_seed_index *, ix), &o, (const uint8_t *)seq, (const int64_t *)off, (int)n,
                      threads, &t);
     if (rc != 0) croak("Prgpu: pr_seed_map: %s (%d)", pr_last_error(), rc);

@@ -143,7 +143,7 @@ def options(a) -> Tuple[seed.SeedOpts, sw.SwOpts]:
     so.min_chain_weight = a.W if a.W > 0 else a.k
     o_del, o_ins = _pair(a.O)
     e_del, e_ins = _pair(a.E)
-    so.a, so.o_del, so.e_del, so.o_ins, so.e_ins = a.A, o_del, e_del, o_ins, e_ins
+    so.a, so.o_del, so.e_del, so.o_ins, so.e_ins, so.b = a.A, o_del, e_del, o_ins, e_ins, a.B
     wo = sw.default_opts(False)
     wo.a, wo.b, wo.o_del, wo.e_del, wo.o_ins, wo.e_ins = a.A, a.B, o_del, e_del, o_ins, e_ins
     wo.w, wo.zdrop = a.w, a.d

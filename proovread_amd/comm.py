@@ -37,10 +37,12 @@ RED_SUM, RED_MAX, RED_MIN = 0, 1, 2
 def rendezvous_path(key: Optional[str] = None) -> Path:
     """The file through which rank 0 publishes the RCCL id.  All ranks of a job are
     children of one launcher (torch.distributed.run's agent, or a test's spawner), so
-    the parent pid + MASTER_PORT + run id name the job."""
+    the parent pid + MASTER_PORT + run id name the job, and the elastic restart count names
+    the attempt (a file an earlier attempt left behind is never read by a later one)."""
     if key is None:
         key = os.environ.get("PRGPU_RDZV_KEY") or "_".join(
-            [str(os.getppid()), os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "none")])
+            [str(os.getppid()), os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", "none"),
+             os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")])
     base = Path(os.environ.get("PRGPU_RDZV_DIR", "/tmp"))
     return base / f"prgpu_rdzv_{key}.id"
 

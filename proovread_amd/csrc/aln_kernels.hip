@@ -96,10 +96,15 @@ __global__ void __launch_bounds__(256) aln_list_kernel(AlnDev A) {
     }
 }
 
-__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, int early) {
+// early pass (snap != nullptr, on a side stream beside the later extension rounds): only the
+// reads whose walk had finished when it was launched, read from a snapshot of `resume` taken on
+// the main stream before the launch -- the live array (and the read's decisions / extension
+// outputs) of a read still walking is written concurrently by the main stream's rounds
+__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t *snap) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= A.n_sr) return;
-    if (early && A.resume[r] < A.seed_off[r + 1]) return;   // its walk is still going
+    const bool early = snap != nullptr;
+    if (early && snap[r] < A.seed_off[r + 1]) return;   // its walk was still going at the snapshot
     AlnPatch req;
     if (aln_final_read(A, r, &req) && !early) {   // a patch score is needed: the read is replayed later
         const int slot = atomicAdd(&A.counter[1], 1);
@@ -231,7 +236,7 @@ int aln_launch_walk(const AlnDev &A, void *stream) {
     hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
-int aln_launch_final(const AlnDev &A, void *stream, int early) {
+int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap) {
     if (A.n_sr <= 0) return 0;
     // tuning hook: PRGPU_ALN_FINAL_WG=k caps the resident workgroups per CU at k (dynamic LDS),
     // i.e. the reads whose region scratch is live at once
@@ -240,7 +245,7 @@ int aln_launch_final(const AlnDev &A, void *stream, int early) {
     static const int wgcu = getenv("PRGPU_ALN_FINAL_WG") ? atoi(getenv("PRGPU_ALN_FINAL_WG")) : 3;
     const unsigned lds = wgcu > 0 ? (unsigned)(160 * 1024 / wgcu) & ~255u : 0u;
     hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A,
-                       early);
+                       early_snap);
     return (int)hipGetLastError();
 }
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, void *stream) {

@@ -49,7 +49,9 @@ struct pr_comm {
         }                                                                           \
     } while (0)
 
+// (the staging buffer lives on the context's device, whatever the calling thread's current one)
 static int stage(pr_comm *c, size_t bytes) {
+    HIPCHK(hipSetDevice(ctx_device(c->ctx)));
     if (c->stage && c->stage_cap >= bytes) return 0;
     if (c->stage) (void)hipFree(c->stage);
     c->stage = nullptr;

@@ -1263,7 +1263,10 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     const int e2 = seed_compact_launch(D[SB_OUT].as<pr_seed_task>(), D[SB_NOUT].as<int32_t>(), D[SB_PRE].as<int64_t>(),
                                        n_sr, caps.out, D[SB_DENSE].as<pr_seed_task>(), (void *)s);
     if (e2) return set_error(PR_ERR_HIP, "seed compaction: %s", hipGetErrorString((hipError_t)e2));
-    c->seed_pre = pre;
+    // an incomplete seed set (flagged reads have no seeds) is never handed to
+    // pr_iter_upload_gpu_seeds: it refuses when seed_pre does not match the reads
+    if (bad) c->seed_pre.clear();
+    else c->seed_pre = pre;
     if (keep_on_device) {   // the seeds stay in HBM for pr_iter_upload_gpu_seeds
         HIPCHK(hipStreamSynchronize(s));
         if (status) std::memcpy(status, st.data(), (size_t)n_sr * 4);

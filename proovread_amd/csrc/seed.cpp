@@ -344,6 +344,7 @@ extern "C" void pr_seed_opts_default(pr_seed_opts *o, int finish) {
     o->e_del = finish ? 3 : 4;
     o->o_ins = finish ? 19 : 1;
     o->e_ins = 3;
+    o->b = finish ? 13 : 11;
 }
 
 extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off, int n_lr, pr_seed_index **out) {

@@ -13,6 +13,10 @@
 //                     test_and_merge or opening a new chain after the chains of
 //                     equal pos (the btree order)
 //   mem_chain_flt     chain weight, -W minimum, stable sort, -D / mask_level
+//   mem_flt_chained_seeds (bwa >= 0.7.13; runs for reads with 1.1 W <= 0.05 len, i.e.
+//                     >= 440 bp at proovread's mr -W 20): each seed's local SW score
+//                     (ksw_align2 over the seed +- 50 bp when both windows stay < 200)
+//                     drops seeds scoring below a*1.1*W and becomes the seed's score
 //   mem_chain2aln     its input: every seed of every kept chain in the order it
 //                     tries them (longest first, last on ties) with the chain's
 //                     reference window (cal_max_gap over its seeds); the
@@ -25,6 +29,7 @@
 // compares the KX bases the index stores after the hit (kext) and reads the
 // text only after a full KX-base match.
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #include "../../include/prgpu.h"
@@ -467,6 +472,75 @@ SC_HD int cal_max_gap(const pr_seed_opts &O, int qlen) {
     return l < O.w << 1 ? l : O.w << 1;
 }
 
+// ---------------------------------------------------------------- mem_flt_chained_seeds
+// min_HSP_score of mem_flt_chained_seeds for a read of len bases, or -1 when bwa skips the
+// filter ("don't run the following for short reads"): min_l = MEM_HSP_COEF (1.1f) * W in
+// float arithmetic, compared with MEM_SEEDSW_COEF (0.05f) * len, as bwamem.c computes them
+SC_HD int seed_flt_min_score(const pr_seed_opts &O, int len) {
+    double min_l;
+    if (O.min_chain_weight) min_l = (double)(1.1f * (float)O.min_chain_weight);
+    else min_l = (double)5.5f * log((double)len);   // MEM_MINSC_COEF * log(l_query)
+    if (min_l > (double)(0.05f * (float)len)) return -1;
+    return (int)(O.a * min_l + .499);
+}
+
+// mem_seed_sw: the best local score (ksw_align2: affine gaps, a gap of k bases costs o + k e,
+// deletions o_del/e_del, insertions o_ins/e_ins; match a, mismatch -b, N -1) of the read
+// around seed s against the reference around it, or -1 when the seed or a window reaches
+// MEM_SHORT_LEN (200) bases.  Windows: +- MEM_SHORT_EXT (50), clamped to [0, 2 l_pac) and to
+// the seed's strand half, then (bns_fetch_seq) to its long read.  H / E: 2 x 201 ints.
+SC_HD int seed_sw_score(const IndexView &I, const pr_seed_opts &O, const uint8_t *q, int len, const Seed &s, int rid,
+                        int32_t *H, int32_t *E) {
+    if (s.len >= 200) return -1;
+    int qb = s.qbeg - 50, qe = s.qbeg + s.len + 50;
+    qb = qb > 0 ? qb : 0;
+    qe = qe < len ? qe : len;
+    int64_t rb = s.rbeg - 50, re = s.rbeg + s.len + 50;
+    const int64_t mid = (s.rbeg + s.rbeg + s.len) >> 1;
+    rb = rb > 0 ? rb : 0;
+    re = re < (I.l_pac << 1) ? re : (I.l_pac << 1);
+    if (rb < I.l_pac && I.l_pac < re) {
+        if (mid < I.l_pac) re = I.l_pac;
+        else rb = I.l_pac;
+    }
+    if (qe - qb >= 200 || re - rb >= 200) return -1;
+    const bool rev = mid >= I.l_pac;
+    const int64_t fb = rev ? (I.l_pac << 1) - I.lr_off[rid + 1] : I.lr_off[rid];
+    const int64_t fe = rev ? (I.l_pac << 1) - I.lr_off[rid] : I.lr_off[rid + 1];
+    rb = rb > fb ? rb : fb;
+    re = re < fe ? re : fe;
+    // the text: forward long reads, then the reverse complement of their concatenation
+    const int64_t tc = rev ? I.cstart[2 * I.n_lr - 1 - rid] : I.cstart[rid];
+    const uint8_t *t = I.text + tc + (rb - fb);
+    const int qn = qe - qb, tn = (int)(re - rb);
+    const int oe_del = O.o_del + O.e_del, oe_ins = O.o_ins + O.e_ins;
+    for (int j = 0; j < qn; ++j) H[j] = 0, E[j] = 0;
+    int best = 0;
+    for (int i = 0; i < tn; ++i) {
+        const int ti = t[i];
+        int hdiag = 0, f = 0;
+        for (int j = 0; j < qn; ++j) {
+            const int qj = q[qb + j];
+            const int sc = (ti > 3 || qj > 3) ? -1 : (ti == qj ? O.a : -O.b);
+            int h = hdiag + sc;
+            const int e = E[j];
+            h = h > e ? h : e;
+            h = h > f ? h : f;
+            h = h > 0 ? h : 0;
+            hdiag = H[j];
+            H[j] = h;
+            best = best > h ? best : h;
+            int en = e - O.e_del, eo = h - oe_del;
+            en = en > eo ? en : eo;
+            E[j] = en > 0 ? en : 0;
+            int fn = f - O.e_ins, fo = h - oe_ins;
+            fn = fn > fo ? fn : fo;
+            f = fn > 0 ? fn : 0;
+        }
+    }
+    return best;
+}
+
 // Everything after the occurrence table (S.hoff / hpos / hml / ge of the read, built by
 // build_occ or by the device's wave-parallel equivalent): SMEMs, chaining, the chain
 // filter and the tasks into out[0, *n_out) (chain order after mem_chain_flt).
@@ -606,8 +680,14 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         for (int k = 0; k < nk; ++k)
             if (S.ch[S.kept[k]].first >= 0) S.ch[S.ch[S.kept[k]].first].kept = 1;
     }
+    // mem_flt_chained_seeds over the kept chains (long reads only; the occurrence table's
+    // per-start array `ge` is dead by now and holds the SW rows)
+    const int flt = seed_flt_min_score(O, len);
+    int32_t *swH = (int32_t *)S.ge, *swE = swH + 201;
     // mem_chain2aln's input: every seed of every kept chain with the chain's reference window,
-    // seeds in the order mem_chain2aln tries them (srt: score = length, larger index first on ties)
+    // seeds in the order mem_chain2aln tries them (srt: score -- the length, or the seed SW
+    // score after mem_flt_chained_seeds -- then the larger index first on ties); a chain the
+    // filter empties is never extended (mem_chain2aln returns on c->n == 0)
     int no = 0, nkept = 0;
     for (int ci = 0; ci < nch; ++ci) {
         const Chain &c = S.ch[ci];
@@ -615,21 +695,23 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         const bool rev = S.seeds[c.head].rbeg >= I.l_pac;
         const int64_t L = I.lr_off[c.rid + 1] - I.lr_off[c.rid];
         const int64_t cs = rev ? I.l_pac + (I.l_pac - I.lr_off[c.rid + 1]) : I.lr_off[c.rid];
-        int64_t r0 = INT64_MAX, r1 = INT64_MIN;
-        for (int32_t k = c.head; k >= 0; k = S.next[k]) {
-            const Seed &t = S.seeds[k];
-            const int64_t b = t.rbeg - (t.qbeg + cal_max_gap(O, t.qbeg));
-            const int64_t e = t.rbeg + t.len + ((len - t.qbeg - t.len) + cal_max_gap(O, len - t.qbeg - t.len));
-            r0 = r0 < b ? r0 : b;
-            r1 = r1 > e ? r1 : e;
-        }
-        r0 -= cs;
-        r1 -= cs;
         if (no + c.n > cap_out) return SC_OVER_OUT;
         const int first = no;
         int idx = 0;
-        for (int32_t k = c.head; k >= 0; k = S.next[k], ++idx) {
+        int64_t r0 = INT64_MAX, r1 = INT64_MIN;
+        for (int32_t k = c.head; k >= 0; k = S.next[k]) {
             const Seed &s = S.seeds[k];
+            int score = s.len;
+            if (flt >= 0) {
+                const int x = seed_sw_score(I, O, q, len, s, c.rid, swH, swE);
+                if (x >= 0 && x < flt) continue;   // dropped
+                score = x < 0 ? s.len * O.a : x;
+            }
+            // the chain's window over its (remaining) seeds
+            const int64_t b = s.rbeg - (s.qbeg + cal_max_gap(O, s.qbeg));
+            const int64_t e = s.rbeg + s.len + ((len - s.qbeg - s.len) + cal_max_gap(O, len - s.qbeg - s.len));
+            r0 = r0 < b ? r0 : b;
+            r1 = r1 > e ? r1 : e;
             pr_seed_task &t = out[no];
             t.sr = sid;
             t.lr = c.rid;
@@ -637,19 +719,24 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             t.qbeg = s.qbeg;
             t.rbeg = (int32_t)(s.rbeg - cs);
             t.slen = s.len;
-            t.rmax0 = (int32_t)(r0 > 0 ? r0 : 0);
-            t.rmax1 = (int32_t)(r1 < L ? r1 : L);
             t.chain = nkept;
-            t.rank = idx;   // insertion index until the sort below
-            // insertion sort by (length, index) descending
+            t.rank = score * 65536 + idx++;   // the srt key until the sort below (score < 2^15)
+            // insertion sort by (score, index) descending
             int j = no - 1;
-            while (j >= first && (out[j].slen < t.slen || (out[j].slen == t.slen && out[j].rank < t.rank))) --j;
+            while (j >= first && out[j].rank < t.rank) --j;
             const pr_seed_task v = t;
             for (int m = no; m > j + 1; --m) out[m] = out[m - 1];
             out[j + 1] = v;
             ++no;
         }
-        for (int m = first; m < no; ++m) out[m].rank = m - first;
+        if (no == first) continue;
+        r0 -= cs;
+        r1 -= cs;
+        for (int m = first; m < no; ++m) {
+            out[m].rank = m - first;
+            out[m].rmax0 = (int32_t)(r0 > 0 ? r0 : 0);
+            out[m].rmax1 = (int32_t)(r1 < L ? r1 : L);
+        }
         ++nkept;
     }
     *n_out = no;

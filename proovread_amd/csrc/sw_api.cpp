@@ -55,12 +55,15 @@ static const size_t SPILL_OFF = 96;   // in the SB_CELLS buffer: 3 x u64 overflo
 enum AlnBuf {
     SB_CHAIN = 35, SB_SEEDOFF, SB_SEL, SB_EXTF, SB_DEC, SB_RESUME, SB_ACNT, SB_AREG, SB_AIX, SB_PSCORE, SB_NPK,
     SB_FDONE, SB_PREQ, SB_NOUT, SB_OLIST, SB_OFLAG, SB_ATEMP, SB_AOFF, SB_ALIST, SB_AFLAG, SB_PPOOL, SB_GLIST,
-    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_TLIST, SB_CNEXT, SB_HPREV, SB_ABOX, SB_NBUF
+    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_TLIST, SB_CNEXT, SB_HPREV, SB_ABOX, SB_RSNAP, SB_NBUF
 };
 static_assert(SB_NBUF <= 80, "SwResident buffer table");
 
 namespace prgpu {
 void sw_release(SwResident &r) {
+    for (void *&e : r.ext_ev.ev)
+        if (e) (void)hipEventDestroy((hipEvent_t)e), e = nullptr;
+    r.ext_ev.n = 0;
     if (r.side) (void)hipStreamDestroy((hipStream_t)r.side);
     for (void *&e : r.side_ev)
         if (e) (void)hipEventDestroy((hipEvent_t)e), e = nullptr;
@@ -209,7 +212,7 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
             (rc = ensure(r, SB_AOFF, r1 * 8)) || (rc = ensure(r, SB_ALIST, n1 * 4)) || (rc = ensure(r, SB_AFLAG, n1 * 4)) ||
             (rc = ensure(r, SB_PREQ, 1024 * sizeof(AlnPatch))) || (rc = ensure(r, SB_CIGSLOT, n1 * 8)) ||
             (rc = ensure(r, SB_TLIST, n1 * 4)) || (rc = ensure(r, SB_CNEXT, n1 * 4)) || (rc = ensure(r, SB_HPREV, n1 * 4)) ||
-            (rc = ensure(r, SB_ABOX, n1 * sizeof(AlnBox))) ||
+            (rc = ensure(r, SB_ABOX, n1 * sizeof(AlnBox))) || (rc = ensure(r, SB_RSNAP, r1 * 4)) ||
             (rc = ensure(r, SB_CIGAT, n1 * 8)) || (rc = ensure(r, SB_PASS, n1)) || (rc = ensure(r, SB_CELLS, CELLS_BYTES)))
             return rc;
         size_t tb = aln_scan_temp_bytes(nt);
@@ -357,7 +360,7 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         D.tsel_n = n_list;
         HIPCHK(hipMemsetAsync(A.counter, 0, 8, s));
         if (n_list) {
-            e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s);
+            e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s, &r.ext_ev);
             if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         }
         if (heads_side) {
@@ -376,9 +379,13 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         // would have had to request
         if (r.ext_rounds == 1 && cnt[0] > 0 && !getenv("PRGPU_BWA_NO_EARLY_FINAL")) {
             if ((rc = side_stream(r))) return rc;
+            // the reads finished now, snapshotted on the main stream: the early pass never reads
+            // the live resume array the later rounds' walks write
+            int32_t *snap = (int32_t *)r.buf[SB_RSNAP];
+            HIPCHK(hipMemcpyAsync(snap, A.resume, (size_t)r.n_sr * 4, hipMemcpyDeviceToDevice, s));
             HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[0], s));
             HIPCHK(hipStreamWaitEvent((hipStream_t)r.side, (hipEvent_t)r.side_ev[0], 0));
-            if ((e = aln_launch_final(A, r.side, 1))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+            if ((e = aln_launch_final(A, r.side, snap))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
             HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[1], (hipStream_t)r.side));
             early = true;
         }
@@ -391,7 +398,7 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     if (early) HIPCHK(hipStreamWaitEvent(s, (hipEvent_t)r.side_ev[1], 0));
     for (int round = 0;; ++round) {   // final pass; mem_patch_reg global scores in extra rounds
         HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
-        if ((e = aln_launch_final(A, (void *)s, 0))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        if ((e = aln_launch_final(A, (void *)s, nullptr))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         HIPCHK(hipMemcpyAsync(cnt, A.counter, 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (getenv("PRGPU_BWA_DEBUG")) fprintf(stderr, "[bwa] final round %d: %d patch requests\n", round, cnt[1]);
@@ -567,11 +574,18 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if ((rc = ensure(r, SB_Z, zb))) return rc;
     D.z = (uint8_t *)r.buf[SB_Z];
     HIPCHK(hipMemsetAsync(r.buf[SB_CELLS], 0, CELLS_BYTES, s));
+    for (void *&ev : r.ext_ev.ev)
+        if (!ev) {
+            hipEvent_t x;
+            HIPCHK(hipEventCreate(&x));
+            ev = (void *)x;
+        }
+    r.ext_ev.n = 0;
     if (r.bwa) return bwa_launch(c, r, D, O, o, grid_w, grid_pk, grid_g, lds_glob);
     if (r.n_task == 0) return 0;
     HIPCHK(hipMemcpyAsync(r.buf[SB_CIGAT], r.buf[SB_CIGSLOT], (size_t)r.n_task * 8, hipMemcpyDeviceToDevice, s));
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
-    int e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s);
+    int e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s, &r.ext_ev);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
 
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
@@ -821,6 +835,29 @@ extern "C" int pr_sw_dominant_kernel(pr_ctx *c, double *ms, int64_t *cells) {
     HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 24, hipMemcpyDeviceToHost));
     if (ms) *ms = r.ms_glob_ring;
     if (cells) *cells = (int64_t)r.cells[2];
+    return 0;
+}
+
+extern "C" int pr_sw_extension_kernels(pr_ctx *c, double *ms, int64_t *cells, int32_t *launches) {
+    // every extension DP launch of the last pr_sw_launch (packed, ring, wide; all bwa-mode
+    // rounds and both band tries): HIP events around each on the SW stream, summed, and the
+    // DP cells they computed
+    if (!c) return pr_set_error(PR_ERR_ARG, "null ctx");
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    HIPCHK(hipStreamSynchronize(ctx_stream(c)));
+    double tot = 0.0;
+    for (int i = 0; i + 1 < r.ext_ev.n; i += 2) {
+        float a = 0.f;
+        HIPCHK(hipEventElapsedTime(&a, (hipEvent_t)r.ext_ev.ev[i], (hipEvent_t)r.ext_ev.ev[i + 1]));
+        tot += a;
+    }
+    HIPCHK(hipMemcpy(r.cells, r.buf[SB_CELLS], 24, hipMemcpyDeviceToHost));
+    if (ms) *ms = tot;
+    if (cells) *cells = (int64_t)r.cells[0];
+    if (launches) *launches = r.ext_ev.n / 2;
+    if (r.ext_ev.n >= SwEvPool::CAP) return pr_set_error(PR_ERR_CAPACITY, "more extension launches than timed events");
     return 0;
 }
 

@@ -85,6 +85,14 @@ SW_HD inline bool sel_cig(const SwDev &D, int64_t t) { return !D.sel || (D.sel[t
 SW_HD inline int64_t sel_count(const SwDev &D) { return D.tsel ? D.tsel_n : D.n_task; }
 SW_HD inline int64_t sel_task(const SwDev &D, int64_t k) { return D.tsel ? (int64_t)D.tsel[k] : k; }
 
+// HIP events around every extension DP launch of one pr_sw_launch (the extension stage's
+// roofline: its DP cells over the summed launch durations); pairs (start, end)
+struct SwEvPool {
+    static const int CAP = 128;
+    void *ev[CAP] = {};
+    int n = 0;
+};
+
 struct SwResident {
     bool loaded = false;
     int64_t n_task = 0, n_sr = 0, n_lr = 0;
@@ -107,6 +115,7 @@ struct SwResident {
     float ms_ext = 0.f, ms_glob = 0.f;
     unsigned long long cells[3] = {0, 0, 0};
     float ms_glob_ring = 0.f;
+    SwEvPool ext_ev;
 };
 
 // device pointers of a resident SW batch (for the SW -> consensus pipeline); in bwa mode
@@ -124,7 +133,8 @@ struct SwPtrs {
 };
 
 int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out, void *stream);
-int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream);
+int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream,
+                     SwEvPool *evp = nullptr);
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
                      void *stream, void *ev_a, void *ev_b);
 int sw_launch_lds(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);

@@ -1168,8 +1168,11 @@ int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out,
 int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *stream);
 
 // the four extension phases + the two finish passes (mem_chain2aln)
-int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream) {
+int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream, SwEvPool *evp) {
     hipStream_t s = (hipStream_t)stream;
+    auto mark = [&]() {   // an event before / after each DP launch (when the pool has room)
+        if (evp && evp->n < SwEvPool::CAP && evp->ev[evp->n]) (void)hipEventRecord((hipEvent_t)evp->ev[evp->n++], s);
+    };
     int fgrid = (int)((sel_count(D) + 255) / 256);
     fgrid = fgrid < 8192 ? (fgrid > 0 ? fgrid : 1) : 8192;
     hipError_t e = hipMemsetAsync(D.x_try, 0, (size_t)D.n_task + 1, s);
@@ -1179,12 +1182,15 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
             if (tryi == 0 && O.pk && O.w <= 40) {
                 int rc = sw_launch_pk_order(D, O, 1 + side, stream);
                 if (rc) return rc;
+                mark();
                 hipLaunchKernelGGL(sw_ext_pk_kernel<40>, dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, side);
+                mark();
                 if ((e = hipGetLastError()) != hipSuccess) return (int)e;
             }
             int rc = sw_launch_order(D, O, side * 2 + tryi, D.list, stream);
             if (rc) return rc;
             const int wb = O.w << tryi;
+            mark();
             if (wb <= 32) hipLaunchKernelGGL(sw_ext_phase_kernel<32>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
             else if (wb <= 40) hipLaunchKernelGGL(sw_ext_phase_kernel<40>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
             else if (wb <= 64) hipLaunchKernelGGL(sw_ext_phase_kernel<64>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
@@ -1196,6 +1202,7 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
                 if (e != hipSuccess) return (int)e;
                 hipLaunchKernelGGL(sw_ext_wide_kernel<false>, dim3(grid_waves), dim3(SW_WAVE), lds, s, D, O, side, tryi);
             }
+            mark();
             if ((e = hipGetLastError()) != hipSuccess) return (int)e;
         }
         if (side == 0) hipLaunchKernelGGL(sw_left_finish_kernel, dim3(fgrid), dim3(256), 0, s, D, O);

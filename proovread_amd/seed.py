@@ -16,7 +16,7 @@ class SeedOpts(C.Structure):
                 ("split_factor", C.c_double), ("split_width", C.c_int), ("max_mem_intv", C.c_int),
                 ("max_occ", C.c_int), ("drop_ratio", C.c_double), ("max_chain_gap", C.c_int),
                 ("mask_level", C.c_double), ("a", C.c_int), ("o_del", C.c_int), ("e_del", C.c_int),
-                ("o_ins", C.c_int), ("e_ins", C.c_int)]
+                ("o_ins", C.c_int), ("e_ins", C.c_int), ("b", C.c_int)]
 
 
 class SeedTask(C.Structure):

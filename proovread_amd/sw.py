@@ -55,6 +55,7 @@ def _setup(L):
     L.pr_sw_last_timing.argtypes = [C.c_void_p, _abi.PD, _abi.PD]
     L.pr_sw_last_cells.argtypes = [C.c_void_p, _abi.P64, _abi.P64]
     L.pr_sw_dominant_kernel.argtypes = [C.c_void_p, _abi.PD, _abi.P64]
+    L.pr_sw_extension_kernels.argtypes = [C.c_void_p, _abi.PD, _abi.P64, _abi.P32]
     L.pr_sw_phase_cycles.argtypes = [C.c_void_p, _abi.P64]
     L.pr_sw_cigar_total.argtypes = [C.c_void_p, _abi.P64, _abi.P64]
     L.pr_sw_aln_count.argtypes = [C.c_void_p, _abi.P64]
@@ -191,6 +192,15 @@ def dominant_kernel(ctx: _abi.Context):
     ms, cells = C.c_double(), C.c_int64()
     _abi.check(L.pr_sw_dominant_kernel(ctx.h, C.byref(ms), C.byref(cells)), "pr_sw_dominant_kernel")
     return ms.value, cells.value
+
+
+def extension_kernels(ctx: _abi.Context):
+    """(summed ms, DP cells, launches) of every extension DP launch of the last launch."""
+    L = _abi.lib()
+    _setup(L)
+    ms, cells, n = C.c_double(), C.c_int64(), C.c_int32()
+    _abi.check(L.pr_sw_extension_kernels(ctx.h, C.byref(ms), C.byref(cells), C.byref(n)), "pr_sw_extension_kernels")
+    return ms.value, cells.value, n.value
 
 
 def phase_cycles(ctx: _abi.Context):

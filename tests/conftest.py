@@ -6,12 +6,15 @@ sys.path.insert(0, str(HERE))
 sys.path.insert(0, str(HERE / "golden"))
 sys.path.insert(0, str(HERE.parent))
 
-# GPU test modules whose kernels (or host paths feeding them) have not yet run on an
-# MI355X run after the rest of the suite, so that under `pytest -x` a failure there
-# cannot hide the results of the validated kernels.  test_bam2cns_cli.py: its BAM input
-# now goes through the native decoder (pr_bam_decode_alns; CPU-checked field for field).
-RUN_LAST = ("test_bam2cns_cli.py", "test_fantasticus_cns.py", "test_mask_gpu.py", "test_seed_gpu.py", "test_correct_loop.py",
-            "test_sw_edge_gpu.py", "test_perl_xs.py", "test_perl_xs_mem.py", "test_file_chain_gpu.py")
+# GPU test modules run in this order after every other one, so that under `pytest -x` a
+# failure in newer code cannot hide the results of the validated kernels: first what was
+# green on a driver box before, then the Perl XS boundary (never yet driver-observed), then
+# round-2 additions, then round-3 additions.
+RUN_LAST = ("test_bam2cns_cli.py", "test_fantasticus_cns.py", "test_mask_gpu.py", "test_correct_loop.py",
+            "test_perl_xs.py", "test_perl_xs_mem.py",
+            "test_seed_gpu.py", "test_sw_edge_gpu.py", "test_aln_gpu.py", "test_configs4_gpu.py",
+            "test_file_chain_gpu.py",
+            "test_comm.py", "test_product_configs_gpu.py")
 
 
 def pytest_configure(config):

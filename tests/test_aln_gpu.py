@@ -99,3 +99,35 @@ def test_iteration_from_device_seeds_equals_host_handed_seeds():
     it2.launch(sw.default_opts(False), cp)
     got = [(r.status, r.fastq, r.trace) for r in it2.results()]
     assert got == want and all(g[0] == 0 for g in got)
+
+
+@pytest.mark.parametrize("task,sr_len", [("bwa-mr-1", 600), ("bwa-mr-finish", 950)])
+def test_bwa_mode_mr_reads_match_oracle(task, sr_len):
+    """mr mode (short reads > 150 bp, bin/proovread:637-641; up to 1000 bp, :457) with
+    proovread.cfg:343-365's options: the seeds come through mem_flt_chained_seeds (reads
+    >= 440 bp at -W 20, >= 880 bp at -W 40), GPU seeding = host seeding, and the device's
+    bwa mode = the oracle read by read."""
+    import cpu_chain
+    from proovread_amd import _abi, seed, sw, synth, tasks
+    so_, wo = tasks.options(task)
+    d = synth.simulate(61 + sr_len, 60000, 30, 4000, 8, sr_len=sr_len)
+    ctx = _abi.default_context()
+    hx = seed.SeedIndex(d.lr_seq, d.lr_off)
+    tk = hx.map(d.sr_seq, d.sr_off, so_, threads=4)
+    hx.close()
+    gx = seed.DeviceSeedIndex(ctx, d.lr_seq, d.lr_off)
+    gtk, st = gx.map(d.sr_seq, d.sr_off, so_)
+    assert (st == 0).all() and np.array_equal(gtk, tk)
+    d = synth.with_seeds(d, tk)
+    res = sw.run(d.sw_input(), wo, ctx=ctx)
+    finish = task.endswith("finish")
+    swt = (wo.a, wo.b, wo.o_del, wo.o_ins, wo.e_del, wo.e_ins, wo.w, wo.pen_clip5, wo.pen_clip3, wo.zdrop,
+           wo.min_score_per_base)
+    want = cpu_chain.bwa_alignments(d, swt, drop_ratio=wo.drop_ratio)
+    got = _by_read(res, d)
+    n = 0
+    for r in range(d.n_sr):
+        assert got.get(r, []) == want[r], r
+        n += len(want[r])
+    assert n == res.n and n > 2 * d.n_lr
+    assert finish or len(tk) > 0

@@ -183,3 +183,96 @@ def test_index_tables_unchanged(name):
     ix = seed.SeedIndex(s, o)
     assert ix.digest() == tuple(INDEX_DIGESTS[name])
     ix.close()
+
+
+def _oracle_opts(o: "seed.SeedOpts") -> "so.Opts":
+    return so.Opts(min_seed_len=o.min_seed_len, min_chain_weight=o.min_chain_weight, w=o.w,
+                   split_factor=o.split_factor, split_width=o.split_width, max_mem_intv=o.max_mem_intv,
+                   max_occ=o.max_occ, drop_ratio=o.drop_ratio, max_chain_gap=o.max_chain_gap,
+                   mask_level=o.mask_level, a=o.a, o_del=o.o_del, e_del=o.e_del, o_ins=o.o_ins, e_ins=o.e_ins,
+                   b=o.b)
+
+
+def test_flt_threshold_follows_bwa_float_arithmetic():
+    """mem_flt_chained_seeds runs from 1.1f * W <= 0.05f * len: 440 bp at -W 20, 880 at -W 40
+    (proovread.cfg:343-365: bwa-mr-1 / bwa-mr -W 20, bwa-mr-finish -W 40), never for sr reads."""
+    o = so.Opts(min_chain_weight=20)
+    assert so.flt_min_score(o, 439) is None and so.flt_min_score(o, 440) == 110
+    assert so.flt_min_score(o, 150) is None
+    o40 = so.Opts(min_chain_weight=40)
+    assert so.flt_min_score(o40, 879) is None and so.flt_min_score(o40, 880) == 220
+    assert so.flt_min_score(so.Opts(min_chain_weight=18), 396) == 99
+
+
+def test_local_sw_known_answers():
+    o = so.Opts()
+    assert so.local_sw(o, [0, 1, 2, 3], [0, 1, 2, 3]) == 20
+    assert so.local_sw(o, [0, 1, 2, 3] * 5, [3, 3]) == 5
+    # one deletion inside 20 matches: 20*5 - (o_del + e_del) = 94 > the 10-base side alone (50)
+    q = [0, 1, 2, 3, 1] * 4
+    t = q[:10] + [2] + q[10:]
+    assert so.local_sw(o, q, t) == 100 - 6
+    # one insertion: o_ins + e_ins = 4
+    assert so.local_sw(o, t, q) == 100 - 4
+    assert so.local_sw(o, [4] * 10, [4] * 10) == 0
+
+
+@pytest.fixture(scope="module")
+def mr_data():
+    """mr mode (short reads > 150 bp, bin/proovread:637-641): 450-1000 bp reads from a genome
+    whose long reads carry CLR errors, a repeat, and pairs of 13-mers of the genome pasted at
+    random places (a chain of weight 26 >= -W whose seeds' +-50 bp windows are otherwise
+    random: their seed SW scores fall below mem_flt_chained_seeds' minimum of 110)."""
+    rng = np.random.default_rng(11)
+    G = rng.integers(0, 4, 8000)
+    rep = G[2000:2300].copy()
+    lrs = []
+    for i in range(8):
+        s = int(rng.integers(0, 5500))
+        lr = _mutate(rng, G[s:s + 2500], 0.12, 0.06, 0.03)
+        if i % 3 == 1:
+            lr[300:300] = list(rep)
+        for _ in range(6):   # two 13-mers 40 bp apart on the genome, random bases between
+            a = int(rng.integers(0, 7900))
+            at = int(rng.integers(0, len(lr)))
+            lr[at:at] = [int(x) for x in G[a:a + 13]] + [int(x) for x in rng.integers(0, 4, 27)] + \
+                [int(x) for x in G[a + 40:a + 53]]
+        lrs.append(lr)
+    srs = []
+    for L in (450, 520, 600, 700, 800, 879, 880, 950, 1000, 640):
+        s = int(rng.integers(0, 8000 - L))
+        r = [int(x) for x in G[s:s + L]]
+        for j in rng.integers(0, L, 3):
+            r[int(j)] = (r[int(j)] + 1) % 4
+        if rng.random() < 0.5:
+            r = [3 - x for x in reversed(r)]
+        srs.append(r)
+    lr_off = np.concatenate([[0], np.cumsum([len(x) for x in lrs])]).astype(np.int64)
+    sr_off = np.concatenate([[0], np.cumsum([len(x) for x in srs])]).astype(np.int64)
+    return dict(lrs=lrs, srs=srs, lr_seq=np.concatenate([np.array(x, np.uint8) for x in lrs]), lr_off=lr_off,
+                sr_seq=np.concatenate([np.array(x, np.uint8) for x in srs]), sr_off=sr_off, oidx=so.Index(lrs))
+
+
+@pytest.mark.parametrize("task", ["bwa-mr-1", "bwa-mr-finish"])
+def test_map_mr_reads_matches_oracle_with_seed_filter(mr_data, task, monkeypatch):
+    """mem_flt_chained_seeds on 450-1000 bp reads (bwa-mr-1 / bwa-mr: -W 20, so every read;
+    bwa-mr-finish: -W 40, reads >= 880 bp): the host path equals the oracle task for task
+    (dropped seeds, srt order by seed SW score, chain windows over the kept seeds), and the
+    filter changes the task lists."""
+    from proovread_amd import tasks
+    o, _ = tasks.options(task)
+    ix = seed.SeedIndex(mr_data["lr_seq"], mr_data["lr_off"])
+    got = [tuple(int(t[k]) for k in seed.TASK_DTYPE.names)
+           for t in ix.map(mr_data["sr_seq"], mr_data["sr_off"], o, threads=4)]
+    ix.close()
+    oo = _oracle_opts(o)
+    want = []
+    for i, r in enumerate(mr_data["srs"]):
+        want += [tuple(t[k] for k in seed.TASK_DTYPE.names) for t in so.map_read(mr_data["oidx"], oo, r, i)]
+    assert got == want and len(got) > 20
+    if task == "bwa-mr-1":   # the filter bites: without it, more seeds in another order
+        monkeypatch.setattr(so, "flt_min_score", lambda O, n: None)
+        plain = []
+        for i, r in enumerate(mr_data["srs"]):
+            plain += [tuple(t[k] for k in seed.TASK_DTYPE.names) for t in so.map_read(mr_data["oidx"], oo, r, i)]
+        assert len(plain) > len(want)

@@ -1,0 +1,114 @@
+"""Time the reference's own CPU consensus (the Perl Sam::Seq engine bam2cns runs) the way
+proovread runs it -- `xargs -P N -L 1` over one worker process per 100-long-read chunk
+(bin/proovread:1596-1619, bin/bam2cns:332-365) -- on the bench's workload: the first
+N_LR long reads of bench.py's configs[1] generator, their bwa-mode alignments from the
+oracle chain (host seeding, oracle/aln_oracle.c + sw_oracle.c, -b 20 -l 300), coverage cap
+11.25 with the reads' own qualities (bwa-sr-1).
+
+The worker is tests/golden/gen_cns_golden.pl (bam2cns's per-read loop over lib/Sam/Seq.pm
+without its samtools forks; Sam::Seq::alns returns arrival order for determinism).  The C
+oracle runs the same chunks and its outputs are compared with Perl's read by read.
+Needs /root/reference: build container only.  Writes profiles/r03_reference_cpu_consensus.json,
+which bench.py reports as `cpu_baseline_reference`.
+
+    python tools/time_reference_r03.py [n_long_reads] [workers]
+"""
+import json
+import os
+import platform
+import subprocess
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "tests"), str(ROOT / "tests" / "golden"), str(ROOT / "oracle")]
+import cpu_chain  # noqa: E402
+import oracle_bind as ob  # noqa: E402
+from casefmt import Case, read_expect, write_cases  # noqa: E402
+
+from proovread_amd import seed, synth  # noqa: E402
+
+ASCII = np.frombuffer(b"ACGTN", np.uint8)
+
+
+def cpu_model():
+    for line in Path("/proc/cpuinfo").read_text().splitlines():
+        if line.startswith("model name"):
+            return line.split(":", 1)[1].strip()
+    return platform.processor()
+
+
+def main():
+    n_lr = int(sys.argv[1]) if len(sys.argv) > 1 else 1600
+    workers = int(sys.argv[2]) if len(sys.argv) > 2 else (os.cpu_count() or 1)
+    out = ROOT / "profiles" / "r03_reference_cpu_consensus.json"
+    import bench
+    t = time.perf_counter()
+    d = synth.simulate(20261015 + 2, 4_600_000, 13_800, 10_000, 50.0, sr_frac=0.3)   # bench.py, rank 0
+    hx = seed.SeedIndex(d.lr_seq, d.lr_off)
+    tasks = hx.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=workers)
+    hx.close()
+    db = synth.with_seeds(d, tasks)
+    _, _, sams, _ = cpu_chain.run_sample(db, range(n_lr), task="bwa-sr", workers=workers, bin_filter=bench.BIN_FILTER,
+                                         sam_only=True)
+    prep_s = time.perf_counter() - t
+    cases = []
+    for lr in range(n_lr):
+        ref = ASCII[d.lr_seq[int(d.lr_off[lr]):int(d.lr_off[lr + 1])]].tobytes().decode()
+        cases.append(Case(f"lr{lr}", {"coverage": "11.25", "use_ref_qual": "1"}, [f"@lr{lr}", ref, "+", "$" * len(ref)],
+                          sams[lr]))
+    cols = sum(len(c.ref[1]) for c in cases)
+    alns = sum(len(c.sam) for c in cases)
+    env = {"PERL_HASH_SEED": "0", "PERL_PERTURB_KEYS": "0", "PATH": "/usr/bin:/bin"}
+    with tempfile.TemporaryDirectory() as td:
+        td = Path(td)
+        chunks = []
+        for k in range(0, n_lr, 100):   # proovread's chunks of 100 long reads (proovread.cfg:253)
+            cf = td / f"chunk{k // 100:04d}.txt"
+            write_cases(cf, cases[k:k + 100])
+            chunks.append(cf)
+        cmds = td / "cmds"
+        cmds.write_text("".join(f"{ROOT / 'tests' / 'golden' / 'gen_cns_golden.pl'} {c} {c}.out\n" for c in chunks))
+        # each line: perl harness chunk > chunk.out (xargs -L 1 runs one worker per chunk)
+        sh = td / "w.sh"
+        sh.write_text('#!/bin/sh\nexec perl "$1" "$2" > "$3"\n')
+        sh.chmod(0o755)
+        t = time.perf_counter()
+        subprocess.run(f"xargs -P {workers} -L 1 {sh} < {cmds}", shell=True, check=True, env=env)
+        t_perl = time.perf_counter() - t
+        expect = {}
+        for c in chunks:
+            expect.update(read_expect(Path(f"{c}.out")))
+    t = time.perf_counter()
+    res = [ob.run_case(c) for c in cases]
+    t_c = time.perf_counter() - t
+    same = sum(1 for c, x in zip(cases, res)
+               if x["rc"] == 0 and not expect[c.name].error and x["fastq"].rstrip("\n").split("\n") == expect[c.name].fastq
+               and x["trace"] == expect[c.name].trace and x["kept"] == expect[c.name].kept)
+    summary = {
+        "what": "consensus only (bam2cns per-read loop over lib/Sam/Seq.pm), bench.py's configs[1] workload",
+        "workload": f"first {n_lr} of 13,800 long reads of bench.py's generator (seed 20261015+2), their bwa-mode "
+                    f"alignments (oracle chain, -b 20 -l 300), coverage 11.25, use_ref_qual",
+        "long_reads": n_lr, "columns": cols, "alignments": alns,
+        "reference_perl": {"engine": "lib/Sam/Seq.pm via tests/golden/gen_cns_golden.pl, xargs -P over 100-read chunks "
+                                     "(bin/proovread:1596-1619)",
+                           "processes": workers, "chunks": len(chunks), "wall_s": round(t_perl, 3),
+                           "Mbases_per_s": round(cols / t_perl / 1e6, 5),
+                           "Mbases_per_s_per_core": round(cols / t_perl / 1e6 / workers, 5)},
+        "oracle_c_single_core": {"seconds": round(t_c, 3), "Mbases_per_s": round(cols / t_c / 1e6, 4),
+                                 "reads_identical_to_perl": same},
+        "host": {"cpu": cpu_model(), "nproc": os.cpu_count(), "where": "build container (the reference cannot travel "
+                                                                         "to the GPU box)"},
+        "prep_s": round(prep_s, 1),
+    }
+    out.write_text(json.dumps(summary, indent=1) + "\n")
+    print(json.dumps(summary))
+    assert same == n_lr, f"{n_lr - same} reads differ between Perl and the C oracle"
+
+
+if __name__ == "__main__":
+    main()
