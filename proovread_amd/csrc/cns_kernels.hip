@@ -370,16 +370,12 @@ __device__ void prep_alignment(const CnsDev &D, const CnsParamsDev &P, int64_t g
 // read first; a read whose tables overflow it is rerun with the large one (1 per CU).
 constexpr int SLOT_SH = 12;                 // window / chimera keys: (column + 1) << 12 | state slot
 constexpr uint32_t SLOT_MASK = (1u << SLOT_SH) - 1u;
-constexpr int CHUNK = 32;                   // columns per scatter work item
 
-template <int TCAP_, int W_, int WCAP_, int SEQB_, int CIGB_, int ICAP_, int WGCU_, bool RETRY_>
+template <int TCAP_, int W_, int WCAP_, int WGCU_, bool RETRY_>
 struct CnsGeo {
     static constexpr int TCAP = TCAP_;      // distinct insertion states per read
     static constexpr int W = W_;            // pileup window columns
     static constexpr int WCAP = WCAP_;      // (column, insertion state) pairs per window
-    static constexpr int SEQB = SEQB_;      // staged SEQ bytes of a candidate group
-    static constexpr int CIGB = CIGB_;      // staged CIGAR ops of a candidate group (and state runs)
-    static constexpr int ICAP = ICAP_;      // insertion-state records of a candidate group
     static constexpr int WGCU = WGCU_;      // workgroups per CU (launch bounds)
     static constexpr bool RETRY = RETRY_;   // capacity overflows go to the retry list
     static constexpr int OFF_CTRL = 0;
@@ -388,40 +384,28 @@ struct CnsGeo {
     static constexpr int SZ_A = TCAP * 24;
     static constexpr int OFF_B = OFF_A + SZ_A;
     static constexpr int B_CNT = 0;                         // u32 [3W]: A|T<<16, G|C<<16, -|N<<16
-    static constexpr int B_WKEY = B_CNT + 12 * W;           // u32 [WCAP]
+    static constexpr int B_BEST = B_CNT + 12 * W;           // u64 [W] best insertion state per column
+    static constexpr int B_WKEY = B_BEST + 8 * W;           // u32 [WCAP]
     static constexpr int B_WCNT = B_WKEY + 4 * WCAP;        // u32 [WCAP]
-    static constexpr int B_BEST = B_WCNT + 4 * WCAP;        // u64 [W] best insertion state per column
-    static constexpr int B_IGN = B_BEST + 8 * W;            // u32 [W/32] ignored columns (MCR ranges)
-    static constexpr int B_ITEM = B_IGN + W / 8;            // i32 [CNS_THREADS+1] work-item prefix
-    static constexpr int B_CSO = B_ITEM + 4 * (CNS_THREADS + 4);  // i32 [CNS_THREADS+4] staged SEQ offsets
-    static constexpr int B_COO = B_CSO + 4 * (CNS_THREADS + 4);   // i32 [CNS_THREADS+4] staged CIGAR offsets
-    static constexpr int B_CSRC = B_COO + 4 * (CNS_THREADS + 4);  // i64 [CNS_THREADS] SEQ source dword index
-    static constexpr int B_CGSRC = B_CSRC + 8 * CNS_THREADS;      // i64 [CNS_THREADS] CIGAR source index
-    static constexpr int B_CIGS = B_CGSRC + 8 * CNS_THREADS;      // u32 [CIGB] staged CIGAR ops
-    static constexpr int B_SEQS = B_CIGS + 4 * CIGB;        // u8  [SEQB] staged SEQ bytes
-    static constexpr int B_RUN = (B_SEQS + SEQB + 15) & ~15;   // int2 [CIGB] runs of fixed states
-    static constexpr int B_INS = B_RUN + 8 * CIGB;          // int2 [ICAP] insertion-state records
-    static constexpr int B_COUT = B_RUN;                    // u16 [W] out len     } argmax outputs,
-    static constexpr int B_CDESC = B_COUT + 2 * W;          // u32 [W]             } after the scatter
-    static constexpr int B_CPHR = B_CDESC + 4 * W;          // u8  [W] phred       } (alias the runs)
-    static constexpr int SZ_WIN = B_INS + 8 * ICAP;
+    static constexpr int B_IGN = B_WCNT + 4 * WCAP;         // u32 [W/32] ignored columns (MCR ranges)
+    static constexpr int WAVE_BYTES = 64 * 16 + 64 * 4;     // per wave: op table int4[64], SEQ dwords u32[64]
+    static constexpr int B_WAVE = (B_IGN + W / 8 + 15) & ~15;
+    static constexpr int SZ_WIN = B_WAVE + (CNS_THREADS / 64) * WAVE_BYTES;
     static constexpr int SZ_CHIM = (CHIM_MAXCOLS * 13 + CHIM_TCAP * 4 + 16) * 4;
     static constexpr int SZ_B = ((SZ_WIN > SZ_CHIM ? SZ_WIN : SZ_CHIM) + 15) & ~15;
     static constexpr int LDS = OFF_B + SZ_B;
     static constexpr int MAX_BINS = (SZ_A + SZ_B - CNS_THREADS * 4) / 8;
     static_assert(LDS * WGCU <= 160 * 1024, "LDS per CU");
     static_assert(TCAP <= (1 << SLOT_SH), "slots fit the key");
-    static_assert(W % CHUNK == 0 && W % CNS_THREADS == 0, "window shape");
-    static_assert(B_BEST % 8 == 0 && B_CSRC % 16 == 0 && B_RUN % 8 == 0, "alignment");
-    static_assert(B_CPHR + W <= B_INS, "argmax outputs fit the run area");
-    static_assert(W <= 1024 && CNS_THREADS <= 256, "run record fields");
+    static_assert(W % CNS_THREADS == 0 && W % 32 == 0, "window shape");
+    static_assert(B_BEST % 8 == 0 && B_WAVE % 16 == 0, "alignment");
 };
-using GeoS = CnsGeo<512, 512, 1024, 8192, 2048, 1024, 2, true>;
-// the default first pass: 256-column windows, smaller staging, 4 workgroups per CU (16 waves:
-// the pileup is latency-bound, occupancy hides it; 29.4 -> 23.8 ms at configs[1]); GeoS (2 per
-// CU, 512-column windows) stays selectable with PRGPU_CNS_GEO=S
-using GeoM = CnsGeo<256, 256, 384, 3072, 768, 384, 4, true>;
-using GeoL = CnsGeo<2048, 512, 2048, 8192, 2560, 1024, 1, false>;
+// the first pass: 1024-column windows, 4 workgroups per CU (16 waves per CU: the per-alignment
+// wave work is latency-bound, occupancy hides it); GeoS (more insertion states, 2 per CU)
+// stays selectable with PRGPU_CNS_GEO=S; GeoL (1 per CU) reruns the reads that overflow
+using GeoS = CnsGeo<512, 1024, 1024, 2, true>;
+using GeoM = CnsGeo<256, 1024, 512, 4, true>;
+using GeoL = CnsGeo<2048, 1024, 8192, 1, false>;
 
 // per-column descriptor: flag bits above the 12-bit state-table slot
 constexpr uint32_t DESC_FIXED = 1u << 16;
@@ -586,75 +570,94 @@ __device__ __forceinline__ int wave_append(int *ctr) {
 }
 
 // ---------------------------------------------------------------------------
-// The states of one alignment inside a pileup window [w0, w0+wn), from its staged ops
-// (walk_states' semantics, Seq.pm:396-461): single-base and '-' states as maximal runs
-// {column, length, kind, SEQ offset} (a run's states are consecutive columns and, for
-// bases, consecutive SEQ positions), multi-character states as records {column, SEQ
-// offset, length}.  Appended to LDS lists (the counts they feed commute); capacity
-// overflow sets C->flag.
-__device__ __forceinline__ void emit_window_states(const uint32_t *cg, int nop, int rpos0, int w0, int wn, int cand, int2 *runs,
-                                   int2 *insr, Ctrl *C, int runcap, int inscap) {
-    const int cmin = w0, cmax = w0 + wn;
-    int col = rpos0, qpos = 0;
-    int p_col = 0, p_kind = -1, p_qoff = 0, p_len = 0;   // the deferred (last) state
-    int r_col = 0, r_len = 0, r_kind = 0, r_q = 0;         // pending run (r_len 0: none)
-    auto flush_run = [&]() {
-        if (r_len > 0) {
-            const int k = wave_append(&C->nrun);
-            if (k < runcap) runs[k] = make_int2((r_col - w0) | (r_len << 10) | (r_kind << 20) | (cand << 21), r_q);
-            else C->flag = 1;
+// a wave's LDS writes visible to its own later LDS reads (lanes exchange through LDS)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// One kept alignment's states (walk_states' semantics, Seq.pm:396-461) by one wave,
+// op-parallel: lane k takes CIGAR op k (chunks of 64 ops) and wave scans give every op its
+// first column and SEQ position (q0 = the SEQ position of the first kept base).  An op that
+// owns columns (M / D with n > 0, a leading I: one column) ends in a deferred state: when
+// insertions follow it (zero-length ops skipped), or for a leading I, that last column holds
+// a multi-character state -- base + inserted bases; after a D the inserted bases replace '-'
+// (a single inserted base is then a one-character state) -- emitted by the op's own lane as
+// special(column, SEQ position, length) when the column lies in [cmin, cmax).  Every other
+// column in [cmin, cmax) is a single-base or '-' state, visited lane-parallel as
+// column(column, SEQ position or -1 for '-'), its op found by a binary search over the
+// chunk's op starts (ops: the wave's LDS table, 64 int4).
+template <bool COLUMNS, class FS, class FC>
+__device__ __forceinline__ void wave_states(const uint32_t *cg, int nop, int rp, int q0, int cmin, int cmax, int4 *ops,
+                                            FS &&special, FC &&column) {
+    const int lane = (int)__lane_id();
+    int col0 = rp, qb = q0;
+    for (int k0 = 0; k0 < nop && col0 < cmax; k0 += 64) {
+        const int k = k0 + lane;
+        const bool valid = k < nop;
+        const uint32_t c = valid ? cg[k] : 0u;
+        const int n = (int)(c >> 4), code = (int)(c & 15u);
+        const bool lead = k == 0 && code == 1;
+        const int ncol = !valid ? 0 : (code == 0 || code == 2) ? n : (lead ? 1 : 0);
+        const int qadv = valid && (code == 0 || code == 1) ? n : 0;
+        // inserted bases after each op up to the next op with a length that is not an I: a
+        // segmented suffix scan towards lower lanes (past the CIGAR end: a break)
+        int tv = valid && code == 1 ? n : 0;
+        int tf = !valid || (code != 1 && n != 0) ? 1 : 0;
+        if (tf) tv = 0;
+        int sc = ncol, sq = qadv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int ov = __shfl_down(tv, o, 64), of = __shfl_down(tf, o, 64);
+            const int y = __shfl_up(sc, o, 64), z = __shfl_up(sq, o, 64);
+            if (lane + o < 64 && !tf) { tv += ov; tf = of; }
+            if (lane >= o) { sc += y; sq += z; }
         }
-        r_len = 0;
-    };
-    // a run of states [c, c + len) of one kind (bases: SEQ offsets q ..), merged into the
-    // pending run when it continues it
-    auto add_run = [&](int c, int len, int kind, int q) {
-        if (r_len > 0 && kind == r_kind && c == r_col + r_len && (kind == 1 || q == r_q + r_len)) {
-            r_len += len;
-            return;
-        }
-        flush_run();
-        r_col = c; r_len = len; r_kind = kind; r_q = kind == 0 ? q : 0;
-    };
-    auto emit_deferred = [&]() {
-        if (p_kind < 0 || p_col < cmin || p_col >= cmax) return;
-        if (p_kind == 1) add_run(p_col, 1, 1, 0);
-        else if (p_len == 1) add_run(p_col, 1, 0, p_qoff);
-        else {
-            const int k = wave_append(&C->nins);
-            if (k < inscap) insr[k] = make_int2((p_col - w0) | (cand << 10), p_qoff | (p_len << 16));
-            else C->flag = 1;
-        }
-    };
-    for (int k = 0; k < nop; ++k) {
-        const uint32_t c = cg[k];
-        const int n = (int)(c >> 4), op = (int)(c & 15u);
-        if (op == 1) {   // I
-            if (k > 0) {
-                if (p_kind == 1) { p_kind = 0; p_qoff = qpos; p_len = n; }
-                else p_len += n;
-            } else {
-                p_col = col; p_kind = 0; p_qoff = qpos; p_len = n;
-                ++col;
+        int tot = __shfl_down(tv, 1, 64);
+        const int tf1 = __shfl_down(tf, 1, 64);
+        if (k0 + 64 < nop) {   // the chunk ends inside the CIGAR: insertions may run on past it
+            int cont = 0;
+            for (int j = k0 + 64; j < nop; ++j) {
+                const uint32_t c2 = cg[j];
+                if ((c2 & 15u) == 1u) cont += (int)(c2 >> 4);
+                else if ((c2 >> 4) != 0u) break;
             }
-            qpos += n;
-            continue;
+            if (lane == 63) tot = cont;
+            else if (!tf1) tot += cont;
+        } else if (lane == 63) {
+            tot = 0;
         }
-        if (n == 0) continue;   // split() of an empty run pushes nothing
-        emit_deferred();
-        p_kind = -1;
-        if (col > cmax) break;
-        const int kind = (op == 0) ? 0 : 1;
-        // interior states [col, col + n - 1) clipped to the window; the last one is deferred
-        const int lo = col > cmin ? col : cmin;
-        const int hi = (col + n - 1) < cmax ? (col + n - 1) : cmax;
-        if (hi > lo) add_run(lo, hi - lo, kind, qpos + (lo - col));
-        p_col = col + n - 1; p_kind = kind; p_qoff = kind == 0 ? qpos + n - 1 : 0; p_len = 1;
-        col += n;
-        if (kind == 0) qpos += n;
+        const int cs = col0 + sc - ncol, qs = qb + sq - qadv;
+        const int ctot = __shfl(sc, 63, 64), qtot = __shfl(sq, 63, 64);
+        int scol = -1;
+        if (ncol > 0 && (tot > 0 || lead)) {
+            int sqp, slen;
+            if (lead) { scol = cs; sqp = qs; slen = n + tot; }
+            else if (code == 0) { scol = cs + n - 1; sqp = qs + n - 1; slen = 1 + tot; }
+            else { scol = cs + n - 1; sqp = qs; slen = tot; }   // D + I: the insertion replaces '-'
+            if (scol >= cmin && scol < cmax) special(scol, sqp, slen);
+        }
+        if (COLUMNS) {
+            ops[lane] = make_int4(valid ? cs : 0x7fffffff, qs, code == 2 ? 1 : 0, scol);
+            wave_sync();
+            const int cA = col0 > cmin ? col0 : cmin, cB = col0 + ctot < cmax ? col0 + ctot : cmax;
+            const int nv = nop - k0 < 64 ? nop - k0 : 64;
+            for (int cc = cA + lane; cc < cB; cc += 64) {
+                int lo = 0, hi = nv - 1;   // the last op starting at or before cc owns it
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (ops[mid].x <= cc) lo = mid; else hi = mid - 1;
+                }
+                const int4 o = ops[lo];
+                if (cc == o.w) continue;   // the deferred special state, emitted above
+                column(cc, o.z ? -1 : o.y + (cc - o.x));
+            }
+            wave_sync();
+        }
+        col0 += ctot;
+        qb += qtot;
     }
-    emit_deferred();
-    flush_run();
 }
 
 // ---------------------------------------------------------------------------
@@ -833,8 +836,9 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         }
 
         // ---- 3. insertion-state table: first-seen order (Seq.pm:446-448) of every kept
-        //         alignment's multi-character states, and the kept alignments bucketed by
-        //         the pileup window they start in (K pool of this workgroup, HBM)
+        //         alignment's multi-character states (one wave per alignment, op-parallel:
+        //         wave_states), and the kept alignments bucketed by the pileup window they
+        //         start in (K pool of this workgroup, HBM)
         STab<G::TCAP> T;
         T.key = reinterpret_cast<unsigned long long *>(A);
         T.exem = T.key + G::TCAP;
@@ -847,6 +851,11 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         int32_t *wcur = reinterpret_cast<int32_t *>(B + G::B_CNT);   // per-window counters (<= 3W)
         int32_t *Kh = D.k_pool + (int64_t)blockIdx.x * D.k_cap;      // [0, nwin] window starts, then entries
         int4 *K = reinterpret_cast<int4 *>(Kh + ((nwin + 4) & ~3));
+        const int lane = tid & 63, wv = tid >> 6;
+        constexpr int NWAVE = CNS_THREADS / 64;
+        int4 *wops = reinterpret_cast<int4 *>(B + G::B_WAVE + wv * G::WAVE_BYTES);   // this wave's op table
+        uint32_t *wseq = reinterpret_cast<uint32_t *>(B + G::B_WAVE + wv * G::WAVE_BYTES + 64 * 16);   // its SEQ dwords
+        const bool snt4 = D.seq_nt4 != 0;
         if (tid == 0) { C->nk = 0; C->maxspan = 0; }
         for (int x = tid; x <= nwin && x < 3 * G::W; x += CNS_THREADS) wcur[x] = 0;
         __syncthreads();
@@ -859,20 +868,24 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             atomicMax(&C->maxspan, span);
             const int win = rp / G::W;
             if (win < 3 * G::W) atomicAdd(&wcur[win], 1);
+        }
+        for (int i = wv; i < na; i += NWAVE) {   // a wave per kept alignment
+            const int64_t g = a0 + i;
+            if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
+            const int rp = D.a_rpos[g], cb = D.a_cb[g], sb = D.a_sb[g];
             const SeqV sv = seq_view(D, g);
-            const int sb = D.a_sb[g];
-            const uint32_t *cg = D.cig + D.cig_off[g];
-            walk_states<true>(cg, D.a_cb[g], D.a_ce[g], rp, 0, 0x7fffffff,
-                              [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                  const uint64_t k = state_key(sv, sb + qoff, qlen);
-                                  if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
-                                  const int h = T.insert(k, ((uint64_t)qlen << 48) | ((uint64_t)(sb + qoff) << 32) |
-                                                                (uint64_t)g);
-                                  if (h < 0) { C->flag = 1; return; }
-                                  const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
-                                  atomicMin(&T.ord_all[h], ord);
-                                  if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
-                              });
+            wave_states<false>(D.cig + D.cig_off[g] + cb, D.a_ce[g] - cb, rp, sb, 0, 0x7fffffff, wops,
+                               [&](int scol, int sqp, int slen) {
+                                   if (slen <= 1) return;   // a single character: a fixed state
+                                   if (slen > 0xFFFF || sqp > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
+                                   const uint64_t k = state_key(sv, sqp, slen);
+                                   const int h = T.insert(k, ((uint64_t)slen << 48) | ((uint64_t)sqp << 32) | (uint64_t)g);
+                                   if (h < 0) { C->flag = 1; return; }
+                                   const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)(scol - rp);
+                                   atomicMin(&T.ord_all[h], ord);
+                                   if (!(nig && in_ign(ig, nig, scol))) atomicMin(&T.ord_cns[h], ord);
+                               },
+                               [](int, int) {});
         }
         __syncthreads();
         // 16-bit fixed-state counters: at most 65535 kept alignments per read
@@ -897,8 +910,8 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
             const int rp = D.a_rpos[g], win = rp / G::W;
             const int kpos = Kh[win] + atomicAdd(&wcur[win], 1);
-            // the entry carries what the windows' candidate selection needs (one 48-byte record
-            // instead of seven scattered per-alignment loads per window)
+            // the entry carries what a window's wave needs (one 48-byte record instead of seven
+            // scattered per-alignment loads per window)
             const int cbk = D.a_cb[g];
             const int64_t so = D.seq_off[g], cgi = D.cig_off[g] + cbk;
             int4 *Ke = K + 3 * (int64_t)kpos;
@@ -911,24 +924,21 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         const int wback = (C->maxspan + G::W - 1) / G::W;   // windows an alignment can reach back
         CNS_TICK(2);
 
-        // ---- 4. windowed pileup (Seq.pm:438-461) + argmax (Seq.pm:1568-1654).  Per window:
-        //   scatter: the kept alignments overlapping the window, split into work items of
-        //   CHUNK columns, walk their states (walk_states: the Perl state semantics) and add
-        //   fixed states to 16-bit LDS counters, insertion states to the window's
-        //   (column, slot) table; then the best insertion state per column (count, then
-        //   first-seen order), the argmax with the reference quality, a block scan of the
+        // ---- 4. windowed pileup (Seq.pm:438-461) + argmax (Seq.pm:1568-1654).  Per window of
+        //   W columns: every kept alignment overlapping it is taken by one wave (wave_states:
+        //   the Perl state semantics, op-parallel, columns lane-parallel, its SEQ bytes in the
+        //   wave's LDS area); fixed states go to 16-bit LDS counters, insertion states to the
+        //   window's (column, slot) table; then the best insertion state per column (count,
+        //   then first-seen order), the argmax with the reference quality, a block scan of the
         //   output lengths and the coalesced write of seq / qual / trace.
         uint32_t *cnt = reinterpret_cast<uint32_t *>(B + G::B_CNT);
         uint32_t *wkey = reinterpret_cast<uint32_t *>(B + G::B_WKEY);
         uint32_t *wcnt = reinterpret_cast<uint32_t *>(B + G::B_WCNT);
         unsigned long long *best = reinterpret_cast<unsigned long long *>(B + G::B_BEST);
         uint32_t *ignb = reinterpret_cast<uint32_t *>(B + G::B_IGN);
-        int32_t *ipre = reinterpret_cast<int32_t *>(B + G::B_ITEM);
-        uint16_t *cout_ = reinterpret_cast<uint16_t *>(B + G::B_COUT);
-        uint32_t *cdesc = reinterpret_cast<uint32_t *>(B + G::B_CDESC);
-        uint8_t *cphr = B + G::B_CPHR;
         const bool use_rq = P.use_ref_qual && D.ref_seq && D.ref_qual;
         constexpr int CPT = G::W / CNS_THREADS;   // argmax columns per thread
+        const uint32_t *gdw = reinterpret_cast<const uint32_t *>(D.seq);
         for (int wi = 0; wi < nwin; ++wi) {
             const long w0 = (long)wi * G::W;
             const int wn = (L - w0) < G::W ? (int)(L - w0) : G::W;
@@ -946,353 +956,53 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             __syncthreads();
             CNS_TICK(8);
             if (D.prof && tid == 0) pt[14] += 1;
-            int32_t *cso = reinterpret_cast<int32_t *>(B + G::B_CSO);
-            int32_t *coo = reinterpret_cast<int32_t *>(B + G::B_COO);
-            uint32_t *cigs = reinterpret_cast<uint32_t *>(B + G::B_CIGS);
-            uint8_t *seqs = B + G::B_SEQS;
-            long long *csrc = reinterpret_cast<long long *>(B + G::B_CSRC);
-            long long *cgsrc = reinterpret_cast<long long *>(B + G::B_CGSRC);
-            int4 *cmeta = reinterpret_cast<int4 *>(B + G::B_CSRC);   // after staging: {rpos, ops, sb, lseq | rc}
-            for (int c0 = kb; c0 < ke;) {
-                // a group of candidates whose SEQ dwords and CIGAR ops fit the LDS staging
-                // buffers (prefix sums; candidates that end before the window stage nothing)
-                const int kk = c0 + tid;
-                int4 e = make_int4(0, 0, 0, 0);
-                long long need = 0;   // SEQ dwords | CIGAR ops << 32
-                int head = 0, nop = 0, sbk = 0, lsk = 0;
-                long long sdw = 0, cgi = 0;
-                if (kk < ke) {
-                    e = K[3 * (int64_t)kk];
-                    const long lo = e.x > w0 ? e.x : w0, hi = e.y < w0 + wn ? e.y : w0 + wn;
-                    if (hi > lo) {
-                        const int4 e1 = K[3 * (int64_t)kk + 1], e2 = K[3 * (int64_t)kk + 2];
-                        const int64_t so = (int64_t)(uint32_t)e1.z | ((int64_t)e1.w << 32);
-                        lsk = e.z;
-                        sbk = e.w;
-                        nop = e1.x;
-                        head = (int)(so & 3);
-                        sdw = so >> 2;
-                        cgi = (int64_t)(uint32_t)e2.x | ((int64_t)e2.y << 32);
-                        need = (long long)((head + (lsk & 0x7FFFFFFF) + 3) >> 2) | ((long long)nop << 32);
+            const int cw0 = (int)w0, cw1 = (int)w0 + wn;
+            for (int kk = kb + wv; kk < ke; kk += NWAVE) {
+                const int4 e0 = K[3 * (int64_t)kk];
+                if (e0.x >= cw1 || e0.y <= cw0) continue;   // ends before / starts after the window
+                const int4 e1 = K[3 * (int64_t)kk + 1], e2 = K[3 * (int64_t)kk + 2];
+                const int rp = e0.x, ls = e0.z & 0x7FFFFFFF, sb = e0.w, nop = e1.x;
+                const bool rc = e0.z < 0;
+                const int64_t so = (int64_t)(uint32_t)e1.z | ((int64_t)e1.w << 32);
+                const int64_t cgi = (int64_t)(uint32_t)e2.x | ((int64_t)e2.y << 32);
+                const int head = (int)(so & 3);
+                const int ndw = (head + ls + 3) >> 2;
+                // the alignment's SEQ in the wave's LDS area (one coalesced load), when it fits
+                const bool fast = ndw <= 64;
+                if (fast) wseq[lane] = lane < ndw ? gdw[(so >> 2) + lane] : 0u;
+                const uint8_t *sl = reinterpret_cast<const uint8_t *>(wseq) + head;
+                SeqV sv;   // (the insertion states' keys; the slow path's bases)
+                sv.p = fast ? sl : D.seq + so;
+                sv.n = ls;
+                sv.rc = rc;
+                sv.nt4 = snt4;
+                const uint32_t lut = rc ? 0x50321u : 0x51230u;   // nt4 code -> fixed-state index
+                auto fixed_at = [&](int s) -> int {
+                    if (fast && snt4) {
+                        uint32_t c8 = sl[rc ? ls - 1 - s : s];
+                        c8 = c8 > 4u ? 4u : c8;
+                        return (int)((lut >> (4u * c8)) & 15u);
                     }
-                }
-                long long ntot;
-                const long long npre = block_scan_excl(need, scan, &ntot);
-                const long long incl = npre + need;
-                const bool fits = kk < ke && 4 * (incl & 0xFFFFFFFFLL) <= G::SEQB && (incl >> 32) <= G::CIGB &&
-                                  (incl >> 32) <= 2 * G::ICAP - 2;
-                const int gs = __syncthreads_count(fits);   // fits is a prefix of the candidates
-                if (gs == 0) {   // one alignment alone outgrows the staging buffers
-                    if (tid == 0) C->flag = 1;
-                    __syncthreads();
-                    break;
-                }
-                if (tid < gs) {
-                    cso[tid] = (int)(npre & 0xFFFFFFFFLL) * 4 + head;   // staged SEQ view: byte offset
-                    coo[tid] = (int)(npre >> 32);                        // staged ops: op offset
-                    csrc[tid] = sdw - (npre & 0xFFFFFFFFLL);             // source dword = dst dword + csrc
-                    cgsrc[tid] = cgi - (npre >> 32);                     // source op = dst op + cgsrc
-                    ipre[tid] = (int)(npre & 0xFFFFFFFFLL);              // (dword prefix, for the copy)
-                }
-                if (tid == gs - 1) {
-                    ipre[CNS_THREADS] = (int)(incl & 0xFFFFFFFFLL);
-                    ipre[CNS_THREADS + 1] = (int)(incl >> 32);
-                }
-                __syncthreads();
-                const int totdw = ipre[CNS_THREADS], totop = ipre[CNS_THREADS + 1];
-                CNS_TICK(9);
-                // stage: flat copies of the group's SEQ dwords and CIGAR ops, 4 independent
-                // loads in flight per thread (owner candidate by binary search over prefixes)
-                {
-                    uint32_t *seqdw = reinterpret_cast<uint32_t *>(seqs);
-                    const uint32_t *gdw = reinterpret_cast<const uint32_t *>(D.seq);
-                    for (int b0 = 0; b0 < totdw; b0 += 4 * CNS_THREADS) {
-                        uint32_t v[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int d = b0 + u * CNS_THREADS + tid;
-                            v[u] = 0u;
-                            if (d < totdw) {
-                                int lo = 0, hi = gs - 1;
-                                while (lo < hi) {
-                                    const int mid = (lo + hi + 1) >> 1;
-                                    if (ipre[mid] <= d) lo = mid; else hi = mid - 1;
-                                }
-                                v[u] = gdw[csrc[lo] + d];
-                            }
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int d = b0 + u * CNS_THREADS + tid;
-                            if (d < totdw) seqdw[d] = v[u];
-                        }
-                    }
-                    for (int b0 = 0; b0 < totop; b0 += 4 * CNS_THREADS) {
-                        uint32_t v[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int d = b0 + u * CNS_THREADS + tid;
-                            v[u] = 0u;
-                            if (d < totop) {
-                                int lo = 0, hi = gs - 1;
-                                while (lo < hi) {
-                                    const int mid = (lo + hi + 1) >> 1;
-                                    if (coo[mid] <= d) lo = mid; else hi = mid - 1;
-                                }
-                                v[u] = D.cig[cgsrc[lo] + d];
-                            }
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const int d = b0 + u * CNS_THREADS + tid;
-                            if (d < totop) cigs[d] = v[u];
-                        }
-                    }
-                }
-                __syncthreads();
-                CNS_TICK(10);
-                if (tid < gs) cmeta[tid] = make_int4(e.x, nop, sbk, lsk);   // (csrc / cgsrc are dead)
-                const bool snt4 = D.seq_nt4 != 0;
-                int2 *runs = reinterpret_cast<int2 *>(B + G::B_RUN);
-                int2 *insr = reinterpret_cast<int2 *>(B + G::B_INS);
-                if (tid == 0) { C->nrun = 0; C->nins = 0; }
-                __syncthreads();
-                // pre-pass, op-parallel (Seq.pm:396-461 state semantics, as walk_states): a
-                // segmented scan gives every staged op its column and SEQ offset inside its
-                // alignment, then each op emits its states inside the window: one run of
-                // single-base / '-' states, and the multi-character state its last column
-                // becomes when insertions follow (the leading insertion's state for a first op I)
-                {
-                    const int opt = (totop + CNS_THREADS - 1) / CNS_THREADS;   // ops per thread
-                    const int k0 = tid * opt, k1 = (k0 + opt) < totop ? (k0 + opt) : totop;
-                    int j = 0;   // candidate of op k0: last j with coo[j] <= k0
-                    if (k0 < k1) {
-                        int lo = 0, hi = gs - 1;
-                        while (lo < hi) {
-                            const int mid = (lo + hi + 1) >> 1;
-                            if (coo[mid] <= k0) lo = mid; else hi = mid - 1;
-                        }
-                        j = lo;
-                    }
-                    // chunk aggregate: advances (column | SEQ << 32) after the chunk's last
-                    // alignment start, and whether the chunk holds an alignment start
-                    long long agg = 0;
-                    int head = 0;
-                    {
-                        int jj = j;
-                        for (int k = k0; k < k1; ++k) {
-                            while (jj + 1 < gs && coo[jj + 1] <= k) ++jj;
-                            if (k == coo[jj]) { agg = 0; head = 1; }
-                            const uint32_t c = cigs[k];
-                            const long long n = (long long)(c >> 4);
-                            const int code = (int)(c & 15u);
-                            agg += code == 0 ? (n | (n << 32)) : code == 2 ? n : code == 1 ? ((k == coo[jj] ? 1LL : 0LL) | (n << 32)) : 0;
-                        }
-                    }
-                    // block segmented scan of the 256 chunk aggregates: (value, head) pairs under
-                    // (a, b) -> (b.head ? b : a + b), inside each wave by shuffles, then the
-                    // wave totals carried across the 4 waves through LDS (one barrier)
-                    const int lane = tid & 63, wv = tid >> 6;
-                    long long sv = agg;
-                    int sf = head;
-#pragma unroll
-                    for (int o = 1; o < 64; o <<= 1) {
-                        const long long pv = __shfl_up(sv, o, 64);
-                        const int pf = __shfl_up(sf, o, 64);
-                        if (lane >= o && !sf) { sv += pv; sf = pf; }
-                    }
-                    if (lane == 63) { scan[wv] = sv; ipre[wv] = sf; }
-                    __syncthreads();
-                    long long carry = 0;   // inclusive value at the end of the previous waves
-                    for (int x = 0; x < wv; ++x) carry = ipre[x] ? scan[x] : carry + scan[x];
-                    if (!sf) sv += carry;
-                    const long long prev = __shfl_up(sv, 1, 64);
-                    long long run = lane > 0 ? prev : carry;   // carry into op k0 (thread tid - 1's inclusive value)
-                    __syncthreads();
-                    for (int k = k0; k < k1; ++k) {
-                        while (j + 1 < gs && coo[j + 1] <= k) ++j;
-                        const bool first = k == coo[j];
-                        if (first) run = 0;
-                        const int kend = j + 1 < gs ? coo[j + 1] : totop;
-                        const int4 m = cmeta[j];
-                        const int col = m.x + (int)(run & 0xFFFFFFFFLL), qpos = (int)(run >> 32);
-                        const uint32_t c = cigs[k];
-                        const int n = (int)(c >> 4), code = (int)(c & 15u);
-                        run += code == 0 ? ((long long)n | ((long long)n << 32)) : code == 2 ? (long long)n
-                             : code == 1 ? ((first ? 1LL : 0LL) | ((long long)n << 32)) : 0LL;
-                        if (code == 1 && !first) continue;   // consumed by the state before it
-                        if (code != 1 && n == 0) continue;   // split() of an empty run pushes nothing
-                        // insertions that follow (zero-length ops in between are skipped)
-                        int tot = 0;
-                        for (int kk = k + 1; kk < kend; ++kk) {
-                            const uint32_t c2 = cigs[kk];
-                            if ((c2 & 15u) == 1u) tot += (int)(c2 >> 4);
-                            else if ((c2 >> 4) != 0u) break;
-                        }
-                        int scol, sq, slen;   // the op's last (deferred) state: column, SEQ offset, length
-                        if (code == 1) {      // leading insertion: one state at col
-                            scol = col; sq = qpos; slen = n + tot;
-                        } else {
-                            const int kind = code == 0 ? 0 : 1;
-                            const int lo = col > (int)w0 ? col : (int)w0;
-                            const int endc = col + n - (tot ? 1 : 0);   // single states [col, endc)
-                            const int hi = endc < (int)w0 + wn ? endc : (int)w0 + wn;
-                            if (hi > lo) {
-                                const int k2 = wave_append(&C->nrun);
-                                if (k2 < G::CIGB)
-                                    runs[k2] = make_int2((lo - (int)w0) | ((hi - lo) << 10) | (kind << 20) | (j << 21),
-                                                         kind == 0 ? qpos + (lo - col) : 0);
-                                else C->flag = 1;
-                            }
-                            if (!tot) continue;
-                            scol = col + n - 1;
-                            if (kind == 0) { sq = qpos + n - 1; slen = 1 + tot; }
-                            else { sq = qpos; slen = tot; }   // D + I: the insertion replaces '-'
-                        }
-                        if (scol < (int)w0 || scol >= (int)w0 + wn) continue;
-                        if (slen == 1) {
-                            const int k2 = wave_append(&C->nrun);
-                            if (k2 < G::CIGB) runs[k2] = make_int2((scol - (int)w0) | (1 << 10) | (j << 21), sq);
-                            else C->flag = 1;
-                        } else {
-                            const int k2 = wave_append(&C->nins);
-                            if (k2 < G::ICAP) insr[k2] = make_int2((scol - (int)w0) | (j << 10), sq | (slen << 16));
-                            else C->flag = 1;
-                        }
-                    }
-                }
-                __syncthreads();
-                if (D.prof && tid == 0) {   // pre-pass time (slot 15), out of the walk slot
-                    const unsigned long long t_ = wall_clock64();
-                    pt[15] += t_ - tlast;
-                    tlast = t_;
-                }
-                if (C->flag) break;
-                // runs in parallel, balanced by visits: an exclusive prefix of the run lengths
-                // (kept in runs[].y above the 10-bit SEQ offset) gives every thread an equal
-                // contiguous slice of the group's (run, column) visits; per visit one LDS read
-                // of the staged base and one LDS atomic
-                const int nrun = C->nrun, nins = C->nins;
-                {
-                    const int rpt = (nrun + CNS_THREADS - 1) / CNS_THREADS;
-                    const int ra = tid * rpt < nrun ? tid * rpt : nrun, rb = ra + rpt < nrun ? ra + rpt : nrun;
-                    long long ls = 0;
-                    for (int r = ra; r < rb; ++r) ls += (runs[r].x >> 10) & 1023;
-                    long long vtot;
-                    long long vp = block_scan_excl(ls, scan, &vtot);
-                    for (int r = ra; r < rb; ++r) {
-                        const int2 rr = runs[r];
-                        runs[r].y = (rr.y & 1023) | (int)(vp << 10);
-                        vp += (rr.x >> 10) & 1023;
-                    }
-                    __syncthreads();
-                    if (D.prof && tid == 0) {
-                        pt[17] += (unsigned long long)vtot; pt[18] += (unsigned long long)nrun; pt[19] += (unsigned long long)nins;
-                        const unsigned long long t_ = wall_clock64();
-                        pt[20] += t_ - tlast;
-                        tlast = t_;
-                    }
-                    const long long v0 = vtot * tid / CNS_THREADS, v1 = vtot * (tid + 1) / CNS_THREADS;
-                    if (v0 < v1) {
-                        int lo = 0, hi = nrun - 1;   // last run starting at or before v0
-                        while (lo < hi) {
-                            const int mid = (lo + hi + 1) >> 1;
-                            if ((long long)((uint32_t)runs[mid].y >> 10) <= v0) lo = mid; else hi = mid - 1;
-                        }
-                        int r = lo;
-                        int x = (int)(v0 - (long long)((uint32_t)runs[r].y >> 10));
-                        if (snt4) {
-                            // one loop over the thread's visits (no per-run inner loops, so the
-                            // lanes of a wave stay in step); a run is decoded into a column base,
-                            // a staged-SEQ address + step (reverse strand: backwards) and the
-                            // nucleotide -> state-index nibble table ('-' runs: every code -> 4)
-                            int len = 0, cb = 0, sa = 0, st = 0;
-                            uint32_t lut = 0;
-                            auto decode = [&](int rk) {
-                                const int2 rr = runs[rk];
-                                cb = rr.x & 1023;
-                                len = (rr.x >> 10) & 1023;
-                                if (rr.x & (1 << 20)) {
-                                    sa = 0; st = 0; lut = 0x44444u;
-                                } else {
-                                    const int j = (rr.x >> 21) & 255;
-                                    const int4 m = cmeta[j];
-                                    const int q0 = m.z + (rr.y & 1023);
-                                    const bool rc = m.w < 0;
-                                    sa = cso[j] + (rc ? (m.w & 0x7FFFFFFF) - 1 - q0 : q0);
-                                    st = rc ? -1 : 1;
-                                    lut = rc ? 0x50321u : 0x51230u;
-                                }
-                            };
-                            decode(r);
-                            for (long long v = v0; v < v1; ++v) {
-                                if (x >= len) { decode(++r); x = 0; }
-                                const int c = cb + x;
-                                uint32_t b8 = seqs[sa + st * x];
-                                b8 = b8 > 4u ? 4u : b8;
-                                const int fi = (int)((lut >> (4u * b8)) & 15u);
-                                ++x;
-                                if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
-                                atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
-                            }
-                        } else {
-                            long long v = v0;
-                            while (v < v1) {
-                                const int2 rr = runs[r];
-                                const int c0r = rr.x & 1023, len = (rr.x >> 10) & 1023, j = (rr.x >> 21) & 255;
-                                const int xe = (long long)(len - x) < v1 - v ? len : x + (int)(v1 - v);
-                                v += xe - x;
-                                if (rr.x & (1 << 20)) {   // '-'
-                                    for (; x < xe; ++x) {
-                                        const int c = c0r + x;
-                                        if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
-                                        atomicAdd(&cnt[3 * c + 2], 1u);
-                                    }
-                                } else {
-                                    const int4 m = cmeta[j];
-                                    SeqV sv;
-                                    sv.p = seqs + cso[j];
-                                    sv.n = m.w & 0x7FFFFFFF;
-                                    sv.rc = m.w < 0;
-                                    sv.nt4 = false;
-                                    const int q0 = m.z + (rr.y & 1023);   // sb + qoff
-                                    for (; x < xe; ++x) {
-                                        const int c = c0r + x;
-                                        if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
-                                        const int fi = fixed_idx_at(sv, q0 + x);
-                                        atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
-                                    }
-                                }
-                                ++r;
-                                x = 0;
-                            }
-                        }
-                    }
-                }
-                if (D.prof && tid == 0) {   // runs: slot 11; insertion states: slot 16
-                    const unsigned long long t_ = wall_clock64();
-                    pt[11] += t_ - tlast;
-                    tlast = t_;
-                }
-                for (int r = tid; r < nins; r += CNS_THREADS) {
-                    const int2 ir = insr[r];
-                    const int c = ir.x & 1023, j = (ir.x >> 10) & 255;
-                    if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) continue;
-                    const int4 m = cmeta[j];
-                    SeqV sv;
-                    sv.p = seqs + cso[j];
-                    sv.n = m.w & 0x7FFFFFFF;
-                    sv.rc = m.w < 0;
-                    sv.nt4 = snt4;
-                    const int h = T.find(state_key(sv, m.z + (ir.y & 0xFFFF), (int)((unsigned)ir.y >> 16)));
-                    if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
-                        C->flag = 1;
-                }
-                __syncthreads();
-                CNS_TICK(16);
-                if (D.prof && tid == 0) { pt[12] += 1; pt[13] += (unsigned long long)gs; }
-                c0 += gs;
+                    return fixed_idx_at(sv, s);
+                };
+                auto add_fixed = [&](int cc, int fi) {
+                    const int c = cc - cw0;
+                    if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
+                    atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
+                };
+                wave_sync();
+                wave_states<true>(D.cig + cgi, nop, rp, sb, cw0, cw1, wops,
+                                  [&](int scol, int sqp, int slen) {
+                                      if (slen == 1) { add_fixed(scol, fixed_at(sqp)); return; }
+                                      const int c = scol - cw0;
+                                      if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
+                                      const int h = T.find(state_key(sv, sqp, slen));
+                                      if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
+                                          C->flag = 1;
+                                  },
+                                  [&](int cc, int qp) { add_fixed(cc, qp < 0 ? 4 : fixed_at(qp)); });
             }
+            __syncthreads();
             CNS_TICK(3);
             if (C->flag) break;
             // best insertion state per column: highest count, then lowest first-seen order
@@ -1308,6 +1018,9 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             }
             __syncthreads();
             // argmax per column (Seq.pm:1576-1636): first index with strictly greater freq
+            uint16_t olen_r[CPT];
+            uint32_t desc_r[CPT];
+            uint8_t ph_r[CPT];
 #pragma unroll
             for (int k = 0; k < CPT; ++k) {
                 const int c = tid * CPT + k;
@@ -1356,18 +1069,19 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                         ph = (uint8_t)freq2phred(maxf);
                     }
                 }
-                cout_[c] = olen;
-                cdesc[c] = desc;
-                cphr[c] = ph;
+                olen_r[k] = olen;
+                desc_r[k] = desc;
+                ph_r[k] = ph;
             }
-            __syncthreads();
-            // block scan of (seq len, trace len) over the window's columns, then write
+            // block scan of (seq len, trace len) over the window's columns (each thread's own
+            // columns, from registers), then the write
             {
                 long long s = 0;
+#pragma unroll
                 for (int k = 0; k < CPT; ++k) {
                     const int c = tid * CPT + k;
                     if (c < wn) {
-                        const long long ol = cout_[c];
+                        const long long ol = olen_r[k];
                         s += ol | ((long long)(ol ? ol : 1) << 32);
                     }
                 }
@@ -1381,12 +1095,13 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                 const long long cap = D.out_off[lr + 1] - o0;
                 const bool fits = (long long)C->run_trace + (tot >> 32) <= cap;
                 if (!fits && tid == 0) C->flag = 2;
-                for (int k = 0; k < CPT && fits; ++k) {
+#pragma unroll
+                for (int k = 0; k < CPT; ++k) {
                     const int c = tid * CPT + k;
-                    if (c >= wn) break;
-                    const int ol = cout_[c];
-                    const uint32_t d = cdesc[c];
-                    const uint8_t qc = (uint8_t)(cphr[c] + qch_off);
+                    if (!fits || c >= wn) break;
+                    const int ol = olen_r[k];
+                    const uint32_t d = desc_r[k];
+                    const uint8_t qc = (uint8_t)(ph_r[k] + qch_off);
                     if (ol == 0) {
                         D.o_trace[o0 + to] = 'I';
                         to += 1;

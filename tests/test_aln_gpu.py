@@ -110,7 +110,10 @@ def test_bwa_mode_mr_reads_match_oracle(task, sr_len):
     import cpu_chain
     from proovread_amd import _abi, seed, sw, synth, tasks
     so_, wo = tasks.options(task)
-    d = synth.simulate(61 + sr_len, 60000, 30, 4000, 8, sr_len=sr_len)
+    finish = task.endswith("finish")
+    f = 0.02 / 0.15 if finish else 1.0   # finish's -T 4 per base needs long reads corrected to ~2 % error
+    d = synth.simulate(61 + sr_len, 60000, 30, 4000, 8, p_ins=0.09 * f, p_del=0.045 * f, p_sub=0.015 * f,
+                       sr_len=sr_len)
     ctx = _abi.default_context()
     hx = seed.SeedIndex(d.lr_seq, d.lr_off)
     tk = hx.map(d.sr_seq, d.sr_off, so_, threads=4)
@@ -120,7 +123,6 @@ def test_bwa_mode_mr_reads_match_oracle(task, sr_len):
     assert (st == 0).all() and np.array_equal(gtk, tk)
     d = synth.with_seeds(d, tk)
     res = sw.run(d.sw_input(), wo, ctx=ctx)
-    finish = task.endswith("finish")
     swt = (wo.a, wo.b, wo.o_del, wo.o_ins, wo.e_del, wo.e_ins, wo.w, wo.pen_clip5, wo.pen_clip3, wo.zdrop,
            wo.min_score_per_base)
     want = cpu_chain.bwa_alignments(d, swt, drop_ratio=wo.drop_ratio)
@@ -130,4 +132,3 @@ def test_bwa_mode_mr_reads_match_oracle(task, sr_len):
         assert got.get(r, []) == want[r], r
         n += len(want[r])
     assert n == res.n and n > 2 * d.n_lr
-    assert finish or len(tk) > 0
