@@ -642,41 +642,15 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     const int nib = (int)(((X >> bt) & 1u) | (((X >> (bt + 8)) & 1u) << 1) |
                                           (((Y >> bt) & 1u) << 2) | (((Y >> (bt + 8)) & 1u) << 3));
                     which[h] = pk_which(which[h], nib);
-                    if (which[h] == 2) {
-                        // I steps in bulk: this one, then one per F-continuation bit (D4) below
-                        // it in the loaded pair; the first D4 = 0 ends the run with an M step
-                        // (ksw's F -> M transition), unless the query column runs out first
-                        const int j = sl & 15;
-                        const uint32_t d4 = ((Y >> 8) & 0xFFu) | (((Y >> 24) & 0xFFu) << 8);
-                        const uint32_t zeros = ~d4 & ((1u << j) - 1u);
-                        const int m = zeros ? j - 1 - (31 - __builtin_clz(zeros)) : j;   // ones below sl
-                        const int mi = m < k[h] ? m : k[h];                                // k stays >= 0
-                        if (!push(h, 1, 1 + mi)) {
-                            n[h] = -1;
-                            live[h] = false;
-                            break;
-                        }
-                        k[h] -= 1 + mi;
-                        if (zeros && mi == m && k[h] >= 0) {   // the slot below the run: D4 = 0
-                            which[h] = 0;
-                            if (!push(h, 0, 1)) {
-                                n[h] = -1;
-                                live[h] = false;
-                                break;
-                            }
-                            --i[h], --k[h];
-                        }
-                        live[h] = i[h] >= 0 && k[h] >= 0;
-                        continue;
-                    }
-                    const int op = which[h] == 0 ? 0 : 2;
+                    const int op = which[h] == 0 ? 0 : (which[h] == 1 ? 2 : 1);
                     if (!push(h, op, 1)) {
                         n[h] = -1;
                         live[h] = false;
                         break;
                     }
                     if (which[h] == 0) --i[h], --k[h];
-                    else --i[h];
+                    else if (which[h] == 1) --i[h];
+                    else --k[h];
                     live[h] = i[h] >= 0 && k[h] >= 0;
                 }
             }
