@@ -47,6 +47,7 @@ BIN_FILTER = (20, 20.0 * 15.0)
 # HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over this bench
 # (tools/pmc_summary.py; MI355X_MICROARCH.md's corrections)
 PMC_FILE = "pmc_r02_bwa.json"
+_JSON_OUT = sys.stdout
 
 
 def parse():
@@ -118,6 +119,13 @@ def check_parity(it, cpu_res):
 
 def main():
     args = parse()
+    # the contract is ONE JSON line on stdout: libraries that print there (RCCL's version
+    # banner at communicator init) are sent to stderr, the line goes to the saved stdout
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    global _JSON_OUT
+    _JSON_OUT = os.fdopen(out_fd, "w")
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -381,7 +389,7 @@ def main():
         "iteration_stat": {"bpt": bpt, "bpN": bpn, "masked_frac": round(bpn / bpt, 4) if bpt else None},
         "parity": parity,
     }
-    print(json.dumps(out), flush=True)
+    print(json.dumps(out), file=_JSON_OUT, flush=True)
     if cm is not None:
         cm.close()
     if parity is not None and parity["mismatches"]:

@@ -65,6 +65,15 @@ __device__ __forceinline__ int code5(uint8_t c) {
 __device__ __forceinline__ uint8_t nt4_ascii(uint32_t c) { return (uint8_t)(0x4E54474341ULL >> (8 * c)); }
 // injective key for insertion-state strings of <=19 chars over ACGTN, else a
 // 63-bit FNV-1a hash with the top bit set (collision note)
+__device__ __forceinline__ uint8_t ascii_comp(uint8_t c) {
+    switch (c) {
+        case 'A': return 'T';
+        case 'C': return 'G';
+        case 'G': return 'C';
+        case 'T': return 'A';
+        default: return c;
+    }
+}
 // Read-only view of an alignment's SEQ as SAM prints it: the stored bytes are
 // ASCII or nt4 codes (0-4, bwa's nst_nt4_table); `rc` means SEQ is the reverse
 // complement of the stored read (GPU pipeline: bwa prints reverse-strand hits
@@ -183,12 +192,15 @@ __device__ __forceinline__ void walk_states(const uint32_t *cg, int cb, int ce, 
     int p_col = 0, p_sidx = 0, p_kind = -1, p_qoff = 0, p_len = 0;
     // a rolling window of the next 4 ops: each op is loaded 4 iterations before it is used
     // (4 loads in flight instead of one HBM latency per op)
-    uint32_t w0 = cb < ce ? cg[cb] : 0u, w1 = cb + 1 < ce ? cg[cb + 1] : 0u;
-    uint32_t w2 = cb + 2 < ce ? cg[cb + 2] : 0u, w3 = cb + 3 < ce ? cg[cb + 3] : 0u;
+    constexpr int PF = 4;
+    uint32_t w[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) w[u] = cb + u < ce ? cg[cb + u] : 0u;
     for (int k = cb; k < ce; ++k) {
-        const uint32_t c = w0;
-        w0 = w1; w1 = w2; w2 = w3;
-        w3 = k + 4 < ce ? cg[k + 4] : 0u;
+        const uint32_t c = w[0];
+#pragma unroll
+        for (int u = 0; u + 1 < PF; ++u) w[u] = w[u + 1];
+        w[PF - 1] = k + PF < ce ? cg[k + PF] : 0u;
         const int n = (int)(c >> 4), op = (int)(c & 15u);
         if (op == 1) {  // I
             if (k > cb) {
@@ -577,56 +589,50 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// One kept alignment's states (walk_states' semantics, Seq.pm:396-461) by one wave,
-// op-parallel: lane k takes CIGAR op k (chunks of 64 ops) and wave scans give every op its
-// first column and SEQ position (q0 = the SEQ position of the first kept base).  An op that
-// owns columns (M / D with n > 0, a leading I: one column) ends in a deferred state: when
+// One kept alignment's states inside the window [cmin, cmax) (walk_states' semantics,
+// Seq.pm:396-461) by one wave, op-parallel: lane k takes CIGAR op k (chunks of 64 ops; c_first:
+// this lane's op of the first chunk, loaded ahead by the caller) and wave scans give every op
+// its first column and SEQ position (q0 = the SEQ position of the first kept base).  An op
+// that owns columns (M / D with n > 0, a leading I: one column) ends in a deferred state: when
 // insertions follow it (zero-length ops skipped), or for a leading I, that last column holds
 // a multi-character state -- base + inserted bases; after a D the inserted bases replace '-'
 // (a single inserted base is then a one-character state) -- emitted by the op's own lane as
-// special(column, SEQ position, length) when the column lies in [cmin, cmax).  Every other
-// column in [cmin, cmax) is a single-base or '-' state, visited lane-parallel as
-// column(column, SEQ position or -1 for '-'), its op found by a binary search over the
-// chunk's op starts (ops: the wave's LDS table, 64 int4).
-template <bool COLUMNS, class FS, class FC>
+// special(column, SEQ position, length).  Every other column is a single-base or '-' state,
+// visited as column(column, SEQ position or -1 for '-'): each lane takes a contiguous block
+// of the chunk's columns, finds the first one's op by a binary search over the chunk's op
+// starts (ops: the wave's LDS table, 64 int4) and walks on from there.
+template <class FS, class FC>
 __device__ __forceinline__ void wave_states(const uint32_t *cg, int nop, int rp, int q0, int cmin, int cmax, int4 *ops,
-                                            FS &&special, FC &&column) {
+                                            uint32_t c_first, FS &&special, FC &&column) {
     const int lane = (int)__lane_id();
     int col0 = rp, qb = q0;
     for (int k0 = 0; k0 < nop && col0 < cmax; k0 += 64) {
         const int k = k0 + lane;
         const bool valid = k < nop;
-        const uint32_t c = valid ? cg[k] : 0u;
+        const uint32_t c = k0 == 0 ? c_first : (valid ? cg[k] : 0u);
         const int n = (int)(c >> 4), code = (int)(c & 15u);
         const bool lead = k == 0 && code == 1;
         const int ncol = !valid ? 0 : (code == 0 || code == 2) ? n : (lead ? 1 : 0);
         const int qadv = valid && (code == 0 || code == 1) ? n : 0;
-        // inserted bases after each op up to the next op with a length that is not an I: a
-        // segmented suffix scan towards lower lanes (past the CIGAR end: a break)
-        int tv = valid && code == 1 ? n : 0;
-        int tf = !valid || (code != 1 && n != 0) ? 1 : 0;
-        if (tf) tv = 0;
+        const uint32_t nx1 = __shfl_down(c, 1, 64), nx2 = __shfl_down(c, 2, 64);
         int sc = ncol, sq = qadv;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
-            const int ov = __shfl_down(tv, o, 64), of = __shfl_down(tf, o, 64);
             const int y = __shfl_up(sc, o, 64), z = __shfl_up(sq, o, 64);
-            if (lane + o < 64 && !tf) { tv += ov; tf = of; }
             if (lane >= o) { sc += y; sq += z; }
         }
-        int tot = __shfl_down(tv, 1, 64);
-        const int tf1 = __shfl_down(tf, 1, 64);
-        if (k0 + 64 < nop) {   // the chunk ends inside the CIGAR: insertions may run on past it
-            int cont = 0;
-            for (int j = k0 + 64; j < nop; ++j) {
-                const uint32_t c2 = cg[j];
-                if ((c2 & 15u) == 1u) cont += (int)(c2 >> 4);
-                else if ((c2 >> 4) != 0u) break;
+        // inserted bases right after an op that owns columns (zero-length ops skipped)
+        int tot = 0;
+        if (ncol > 0 && k + 1 < nop) {
+            const uint32_t x1 = lane <= 62 ? nx1 : cg[k + 1];
+            if ((x1 & 15u) == 1u || (x1 >> 4) == 0u) {
+                tot = (x1 & 15u) == 1u ? (int)(x1 >> 4) : 0;
+                for (int j = k + 2; j < nop; ++j) {
+                    const uint32_t x2 = (j == k + 2 && lane <= 61) ? nx2 : cg[j];
+                    if ((x2 & 15u) == 1u) tot += (int)(x2 >> 4);
+                    else if ((x2 >> 4) != 0u) break;
+                }
             }
-            if (lane == 63) tot = cont;
-            else if (!tf1) tot += cont;
-        } else if (lane == 63) {
-            tot = 0;
         }
         const int cs = col0 + sc - ncol, qs = qb + sq - qadv;
         const int ctot = __shfl(sc, 63, 64), qtot = __shfl(sq, 63, 64);
@@ -638,23 +644,34 @@ __device__ __forceinline__ void wave_states(const uint32_t *cg, int nop, int rp,
             else { scol = cs + n - 1; sqp = qs; slen = tot; }   // D + I: the insertion replaces '-'
             if (scol >= cmin && scol < cmax) special(scol, sqp, slen);
         }
-        if (COLUMNS) {
-            ops[lane] = make_int4(valid ? cs : 0x7fffffff, qs, code == 2 ? 1 : 0, scol);
-            wave_sync();
-            const int cA = col0 > cmin ? col0 : cmin, cB = col0 + ctot < cmax ? col0 + ctot : cmax;
-            const int nv = nop - k0 < 64 ? nop - k0 : 64;
-            for (int cc = cA + lane; cc < cB; cc += 64) {
+        ops[lane] = make_int4(valid ? cs : 0x7fffffff, qs, code == 2 ? 1 : 0, scol);
+        wave_sync();
+        const int cA = col0 > cmin ? col0 : cmin, cB = col0 + ctot < cmax ? col0 + ctot : cmax;
+        const int nv = nop - k0 < 64 ? nop - k0 : 64;
+        if (cB > cA) {
+            const int per = (cB - cA + 63) >> 6;
+            int cc = cA + lane * per;
+            const int ce_ = cc + per < cB ? cc + per : cB;
+            if (cc < ce_) {
                 int lo = 0, hi = nv - 1;   // the last op starting at or before cc owns it
                 while (lo < hi) {
                     const int mid = (lo + hi + 1) >> 1;
                     if (ops[mid].x <= cc) lo = mid; else hi = mid - 1;
                 }
-                const int4 o = ops[lo];
-                if (cc == o.w) continue;   // the deferred special state, emitted above
-                column(cc, o.z ? -1 : o.y + (cc - o.x));
+                int4 o = ops[lo];
+                int nxs = lo + 1 < nv ? ops[lo + 1].x : 0x7fffffff;
+                for (; cc < ce_; ++cc) {
+                    while (nxs <= cc) {
+                        ++lo;
+                        o = ops[lo];
+                        nxs = lo + 1 < nv ? ops[lo + 1].x : 0x7fffffff;
+                    }
+                    if (cc == o.w) continue;   // the deferred special state, emitted above
+                    column(cc, o.z ? -1 : o.y + (cc - o.x));
+                }
             }
-            wave_sync();
         }
+        wave_sync();
         col0 += ctot;
         qb += qtot;
     }
@@ -836,9 +853,9 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         }
 
         // ---- 3. insertion-state table: first-seen order (Seq.pm:446-448) of every kept
-        //         alignment's multi-character states (one wave per alignment, op-parallel:
-        //         wave_states), and the kept alignments bucketed by the pileup window they
-        //         start in (K pool of this workgroup, HBM)
+        //         alignment's multi-character states (a thread per alignment: walk_states),
+        //         and the kept alignments bucketed by the pileup window they start in (K pool
+        //         of this workgroup, HBM)
         STab<G::TCAP> T;
         T.key = reinterpret_cast<unsigned long long *>(A);
         T.exem = T.key + G::TCAP;
@@ -860,7 +877,7 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         for (int x = tid; x <= nwin && x < 3 * G::W; x += CNS_THREADS) wcur[x] = 0;
         __syncthreads();
         if (nwin + 1 > 3 * G::W) C->flag = 1;
-        for (int i = tid; i < na; i += CNS_THREADS) {
+        for (int i = tid; i < na; i += CNS_THREADS) {   // a thread per kept alignment
             const int64_t g = a0 + i;
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
             const int rp = D.a_rpos[g], span = D.a_end[g] - rp;
@@ -868,24 +885,20 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             atomicMax(&C->maxspan, span);
             const int win = rp / G::W;
             if (win < 3 * G::W) atomicAdd(&wcur[win], 1);
-        }
-        for (int i = wv; i < na; i += NWAVE) {   // a wave per kept alignment
-            const int64_t g = a0 + i;
-            if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
-            const int rp = D.a_rpos[g], cb = D.a_cb[g], sb = D.a_sb[g];
             const SeqV sv = seq_view(D, g);
-            wave_states<false>(D.cig + D.cig_off[g] + cb, D.a_ce[g] - cb, rp, sb, 0, 0x7fffffff, wops,
-                               [&](int scol, int sqp, int slen) {
-                                   if (slen <= 1) return;   // a single character: a fixed state
-                                   if (slen > 0xFFFF || sqp > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
-                                   const uint64_t k = state_key(sv, sqp, slen);
-                                   const int h = T.insert(k, ((uint64_t)slen << 48) | ((uint64_t)sqp << 32) | (uint64_t)g);
-                                   if (h < 0) { C->flag = 1; return; }
-                                   const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)(scol - rp);
-                                   atomicMin(&T.ord_all[h], ord);
-                                   if (!(nig && in_ign(ig, nig, scol))) atomicMin(&T.ord_cns[h], ord);
-                               },
-                               [](int, int) {});
+            const int sb = D.a_sb[g];
+            const uint32_t *cg = D.cig + D.cig_off[g];
+            walk_states<true>(cg, D.a_cb[g], D.a_ce[g], rp, 0, 0x7fffffff,
+                              [&](int col, int sidx, int kind, int qoff, int qlen) {
+                                  const uint64_t k = state_key(sv, sb + qoff, qlen);
+                                  if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
+                                  const int h = T.insert(k, ((uint64_t)qlen << 48) | ((uint64_t)(sb + qoff) << 32) |
+                                                                (uint64_t)g);
+                                  if (h < 0) { C->flag = 1; return; }
+                                  const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
+                                  atomicMin(&T.ord_all[h], ord);
+                                  if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
+                              });
         }
         __syncthreads();
         // 16-bit fixed-state counters: at most 65535 kept alignments per read
@@ -957,50 +970,86 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             CNS_TICK(8);
             if (D.prof && tid == 0) pt[14] += 1;
             const int cw0 = (int)w0, cw1 = (int)w0 + wn;
+            // the wave's candidates kb + wv + NWAVE j, software-pipelined: the next one's first 64
+            // CIGAR ops and SEQ dwords, and the K entry of the one after it, are in flight while
+            // the current one is processed
+            auto ldK = [&](int kk, int4 &x0, int4 &x1, int4 &x2) {
+                if (kk < ke) {
+                    x0 = K[3 * (int64_t)kk];
+                    x1 = K[3 * (int64_t)kk + 1];
+                    x2 = K[3 * (int64_t)kk + 2];
+                } else {
+                    x0 = make_int4(0x7fffffff, 0, 0, 0);
+                    x1 = x2 = make_int4(0, 0, 0, 0);
+                }
+            };
+            auto overl = [&](const int4 &x0) { return x0.x < cw1 && x0.y > cw0; };   // overlaps the window
+            auto ldD = [&](const int4 &x0, const int4 &x1, const int4 &x2, uint32_t &opv, uint32_t &dwv) {
+                opv = 0u;
+                dwv = 0u;
+                if (!overl(x0)) return;
+                const int64_t so = (int64_t)(uint32_t)x1.z | ((int64_t)x1.w << 32);
+                const int64_t cgi = (int64_t)(uint32_t)x2.x | ((int64_t)x2.y << 32);
+                if (lane < x1.x) opv = D.cig[cgi + lane];
+                const int ndw = ((int)(so & 3) + (x0.z & 0x7FFFFFFF) + 3) >> 2;
+                if (ndw <= 64 && lane < ndw) dwv = gdw[(so >> 2) + lane];
+            };
+            int4 c0e, c1e, c2e, n0e, n1e, n2e;
+            uint32_t cop, cdw;
+            ldK(kb + wv, c0e, c1e, c2e);
+            ldD(c0e, c1e, c2e, cop, cdw);
+            ldK(kb + wv + NWAVE, n0e, n1e, n2e);
             for (int kk = kb + wv; kk < ke; kk += NWAVE) {
-                const int4 e0 = K[3 * (int64_t)kk];
-                if (e0.x >= cw1 || e0.y <= cw0) continue;   // ends before / starts after the window
-                const int4 e1 = K[3 * (int64_t)kk + 1], e2 = K[3 * (int64_t)kk + 2];
-                const int rp = e0.x, ls = e0.z & 0x7FFFFFFF, sb = e0.w, nop = e1.x;
-                const bool rc = e0.z < 0;
-                const int64_t so = (int64_t)(uint32_t)e1.z | ((int64_t)e1.w << 32);
-                const int64_t cgi = (int64_t)(uint32_t)e2.x | ((int64_t)e2.y << 32);
-                const int head = (int)(so & 3);
-                const int ndw = (head + ls + 3) >> 2;
-                // the alignment's SEQ in the wave's LDS area (one coalesced load), when it fits
-                const bool fast = ndw <= 64;
-                if (fast) wseq[lane] = lane < ndw ? gdw[(so >> 2) + lane] : 0u;
-                const uint8_t *sl = reinterpret_cast<const uint8_t *>(wseq) + head;
-                SeqV sv;   // (the insertion states' keys; the slow path's bases)
-                sv.p = fast ? sl : D.seq + so;
-                sv.n = ls;
-                sv.rc = rc;
-                sv.nt4 = snt4;
-                const uint32_t lut = rc ? 0x50321u : 0x51230u;   // nt4 code -> fixed-state index
-                auto fixed_at = [&](int s) -> int {
-                    if (fast && snt4) {
-                        uint32_t c8 = sl[rc ? ls - 1 - s : s];
-                        c8 = c8 > 4u ? 4u : c8;
-                        return (int)((lut >> (4u * c8)) & 15u);
-                    }
-                    return fixed_idx_at(sv, s);
-                };
-                auto add_fixed = [&](int cc, int fi) {
-                    const int c = cc - cw0;
-                    if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
-                    atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
-                };
-                wave_sync();
-                wave_states<true>(D.cig + cgi, nop, rp, sb, cw0, cw1, wops,
-                                  [&](int scol, int sqp, int slen) {
-                                      if (slen == 1) { add_fixed(scol, fixed_at(sqp)); return; }
-                                      const int c = scol - cw0;
-                                      if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
-                                      const int h = T.find(state_key(sv, sqp, slen));
-                                      if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
-                                          C->flag = 1;
-                                  },
-                                  [&](int cc, int qp) { add_fixed(cc, qp < 0 ? 4 : fixed_at(qp)); });
+                uint32_t nop_, ndw_;
+                ldD(n0e, n1e, n2e, nop_, ndw_);
+                int4 m0e, m1e, m2e;
+                ldK(kk + 2 * NWAVE, m0e, m1e, m2e);
+                if (overl(c0e)) {
+                    const int rp = c0e.x, ls = c0e.z & 0x7FFFFFFF, sb = c0e.w, nop = c1e.x;
+                    const bool rc = c0e.z < 0;
+                    const int64_t so = (int64_t)(uint32_t)c1e.z | ((int64_t)c1e.w << 32);
+                    const int64_t cgi = (int64_t)(uint32_t)c2e.x | ((int64_t)c2e.y << 32);
+                    const int head = (int)(so & 3);
+                    const int ndw = (head + ls + 3) >> 2;
+                    // the alignment's SEQ in the wave's LDS area (loaded ahead), when it fits
+                    const bool fast = ndw <= 64;
+                    if (fast) wseq[lane] = cdw;
+                    const uint8_t *sl = reinterpret_cast<const uint8_t *>(wseq) + head;
+                    SeqV sv;   // (the insertion states' keys; the slow path's bases)
+                    sv.p = fast ? sl : D.seq + so;
+                    sv.n = ls;
+                    sv.rc = rc;
+                    sv.nt4 = snt4;
+                    const uint32_t lut = rc ? 0x50321u : 0x51230u;   // nt4 code -> fixed-state index
+                    auto fixed_at = [&](int s) -> int {
+                        if (fast && snt4) {
+                            uint32_t c8 = sl[rc ? ls - 1 - s : s];
+                            c8 = c8 > 4u ? 4u : c8;
+                            return (int)((lut >> (4u * c8)) & 15u);
+                        }
+                        return fixed_idx_at(sv, s);
+                    };
+                    auto add_fixed = [&](int cc, int fi) {
+                        const int c = cc - cw0;
+                        if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
+                        atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
+                    };
+                    wave_sync();
+                    wave_states(D.cig + cgi, nop, rp, sb, cw0, cw1, wops, cop,
+                                [&](int scol, int sqp, int slen) {
+                                    if (slen == 1) { add_fixed(scol, fixed_at(sqp)); return; }
+                                    const int c = scol - cw0;
+                                    if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
+                                    const int h = T.find(state_key(sv, sqp, slen));
+                                    if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
+                                        C->flag = 1;
+                                },
+                                [&](int cc, int qp) { add_fixed(cc, qp < 0 ? 4 : fixed_at(qp)); });
+                }
+                c0e = n0e; c1e = n1e; c2e = n2e;
+                n0e = m0e; n1e = m1e; n2e = m2e;
+                cop = nop_;
+                cdw = ndw_;
             }
             __syncthreads();
             CNS_TICK(3);
