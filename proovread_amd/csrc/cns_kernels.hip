@@ -112,6 +112,18 @@ __device__ __forceinline__ int fixed_idx_at(const SeqV &v, int s) {
     return fixed_idx(v[s]);
 }
 __device__ __forceinline__ uint64_t state_key(const SeqV &v, int off, int n) {
+    if (v.nt4 && n <= 19) {   // every nt4 code is one of ACGTN: the injective key, no ASCII round trip
+        uint64_t k = (uint64_t)n << 57;
+        for (int i = 0; i < n; ++i) {
+            const int s = off + i;
+            uint32_t c = v.rc ? v.p[v.n - 1 - s] : v.p[s];
+            c = c > 4u ? 4u : c;
+            if (v.rc && c < 4u) c = 3u - c;
+            // code5 of 'A','C','G','T','N' = 1..5 = nt4 code + 1
+            k |= (uint64_t)(c + 1u) << (3 * i);
+        }
+        return k;
+    }
     if (n <= 19) {
         uint64_t k = (uint64_t)n << 57;
         bool ok = true;
@@ -582,6 +594,18 @@ __device__ __forceinline__ int wave_append(int *ctr) {
 }
 
 // ---------------------------------------------------------------------------
+// inclusive prefix sum over the 64 lanes of a wave with DPP moves (no LDS crossbar): row
+// shifts 1, 2, 4, 8 scan each row of 16 lanes, row_bcast:15 / :31 carry the row totals on
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // a wave's LDS writes visible to its own later LDS reads (lanes exchange through LDS)
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -615,12 +639,7 @@ __device__ __forceinline__ void wave_states(const uint32_t *cg, int nop, int rp,
         const int ncol = !valid ? 0 : (code == 0 || code == 2) ? n : (lead ? 1 : 0);
         const int qadv = valid && (code == 0 || code == 1) ? n : 0;
         const uint32_t nx1 = __shfl_down(c, 1, 64), nx2 = __shfl_down(c, 2, 64);
-        int sc = ncol, sq = qadv;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(sc, o, 64), z = __shfl_up(sq, o, 64);
-            if (lane >= o) { sc += y; sq += z; }
-        }
+        const int sc = wave_incl_scan(ncol), sq = wave_incl_scan(qadv);
         // inserted bases right after an op that owns columns (zero-length ops skipped)
         int tot = 0;
         if (ncol > 0 && k + 1 < nop) {
@@ -635,7 +654,7 @@ __device__ __forceinline__ void wave_states(const uint32_t *cg, int nop, int rp,
             }
         }
         const int cs = col0 + sc - ncol, qs = qb + sq - qadv;
-        const int ctot = __shfl(sc, 63, 64), qtot = __shfl(sq, 63, 64);
+        const int ctot = __builtin_amdgcn_readlane(sc, 63), qtot = __builtin_amdgcn_readlane(sq, 63);
         int scol = -1;
         if (ncol > 0 && (tot > 0 || lead)) {
             int sqp, slen;

@@ -642,15 +642,35 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     const int nib = (int)(((X >> bt) & 1u) | (((X >> (bt + 8)) & 1u) << 1) |
                                           (((Y >> bt) & 1u) << 2) | (((Y >> (bt + 8)) & 1u) << 3));
                     which[h] = pk_which(which[h], nib);
+                    // an I step takes the F-continuations below it in the loaded pair along (one
+                    // per D4 bit set, ksw's F state); the first D4 = 0 ends the run with the M
+                    // step of ksw's F -> M transition, unless the query column runs out first
+                    int len = 1;
+                    bool mstep = false;
+                    if (which[h] == 2) {
+                        const int j = sl & 15;
+                        const uint32_t d4 = ((Y >> 8) & 0xFFu) | (((Y >> 24) & 0xFFu) << 8);
+                        const uint32_t zeros = ~d4 & ((1u << j) - 1u);
+                        const int m = zeros ? j - 1 - (31 - __builtin_clz(zeros)) : j;   // ones below sl
+                        const int mi = m < k[h] ? m : k[h];
+                        len = 1 + mi;
+                        mstep = zeros != 0u && mi == m && k[h] - len >= 0;
+                    }
                     const int op = which[h] == 0 ? 0 : (which[h] == 1 ? 2 : 1);
-                    if (!push(h, op, 1)) {
+                    bool ok = push(h, op, len);
+                    if (which[h] == 0) --i[h], --k[h];
+                    else if (which[h] == 1) --i[h];
+                    else k[h] -= len;
+                    if (ok && mstep) {
+                        which[h] = 0;
+                        ok = push(h, 0, 1);
+                        --i[h], --k[h];
+                    }
+                    if (!ok) {
                         n[h] = -1;
                         live[h] = false;
                         break;
                     }
-                    if (which[h] == 0) --i[h], --k[h];
-                    else if (which[h] == 1) --i[h];
-                    else --k[h];
                     live[h] = i[h] >= 0 && k[h] >= 0;
                 }
             }
