@@ -992,42 +992,38 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             // the wave's candidates kb + wv + NWAVE j, software-pipelined: the next one's first 64
             // CIGAR ops and SEQ dwords, and the K entry of the one after it, are in flight while
             // the current one is processed
-            auto ldK = [&](int kk, int4 &x0, int4 &x1, int4 &x2) {
-                if (kk < ke) {
-                    x0 = K[3 * (int64_t)kk];
-                    x1 = K[3 * (int64_t)kk + 1];
-                    x2 = K[3 * (int64_t)kk + 2];
-                } else {
-                    x0 = make_int4(0x7fffffff, 0, 0, 0);
-                    x1 = x2 = make_int4(0, 0, 0, 0);
-                }
+            // a K entry (12 ints) is held spread over lanes 0..11 of one register and read back
+            // into scalar registers when used (v_readlane): the pipeline costs 2 VGPRs, not 24
+            const int32_t *Ki = reinterpret_cast<const int32_t *>(K);
+            auto ldK = [&](int kk) -> int32_t {
+                return kk < ke ? (lane < 12 ? Ki[12 * (int64_t)kk + lane] : 0) : (lane == 0 ? 0x7fffffff : 0);
             };
-            auto overl = [&](const int4 &x0) { return x0.x < cw1 && x0.y > cw0; };   // overlaps the window
-            auto ldD = [&](const int4 &x0, const int4 &x1, const int4 &x2, uint32_t &opv, uint32_t &dwv) {
+            auto fld = [](int32_t kv, int f) -> int32_t { return __builtin_amdgcn_readlane(kv, f); };
+            auto overl = [&](int32_t kv) { return fld(kv, 0) < cw1 && fld(kv, 1) > cw0; };   // overlaps the window
+            auto ldD = [&](int32_t kv, uint32_t &opv, uint32_t &dwv) {
                 opv = 0u;
                 dwv = 0u;
-                if (!overl(x0)) return;
-                const int64_t so = (int64_t)(uint32_t)x1.z | ((int64_t)x1.w << 32);
-                const int64_t cgi = (int64_t)(uint32_t)x2.x | ((int64_t)x2.y << 32);
-                if (lane < x1.x) opv = D.cig[cgi + lane];
-                const int ndw = ((int)(so & 3) + (x0.z & 0x7FFFFFFF) + 3) >> 2;
+                if (!overl(kv)) return;
+                const int64_t so = (int64_t)(uint32_t)fld(kv, 6) | ((int64_t)fld(kv, 7) << 32);
+                const int64_t cgi = (int64_t)(uint32_t)fld(kv, 8) | ((int64_t)fld(kv, 9) << 32);
+                if (lane < fld(kv, 4)) opv = D.cig[cgi + lane];
+                const int ndw = ((int)(so & 3) + (fld(kv, 2) & 0x7FFFFFFF) + 3) >> 2;
                 if (ndw <= 64 && lane < ndw) dwv = gdw[(so >> 2) + lane];
             };
-            int4 c0e, c1e, c2e, n0e, n1e, n2e;
+            int32_t ckv = ldK(kb + wv), nkv;
             uint32_t cop, cdw;
-            ldK(kb + wv, c0e, c1e, c2e);
-            ldD(c0e, c1e, c2e, cop, cdw);
-            ldK(kb + wv + NWAVE, n0e, n1e, n2e);
+            ldD(ckv, cop, cdw);
+            nkv = ldK(kb + wv + NWAVE);
             for (int kk = kb + wv; kk < ke; kk += NWAVE) {
                 uint32_t nop_, ndw_;
-                ldD(n0e, n1e, n2e, nop_, ndw_);
-                int4 m0e, m1e, m2e;
-                ldK(kk + 2 * NWAVE, m0e, m1e, m2e);
-                if (overl(c0e)) {
-                    const int rp = c0e.x, ls = c0e.z & 0x7FFFFFFF, sb = c0e.w, nop = c1e.x;
-                    const bool rc = c0e.z < 0;
-                    const int64_t so = (int64_t)(uint32_t)c1e.z | ((int64_t)c1e.w << 32);
-                    const int64_t cgi = (int64_t)(uint32_t)c2e.x | ((int64_t)c2e.y << 32);
+                ldD(nkv, nop_, ndw_);
+                const int32_t mkv = ldK(kk + 2 * NWAVE);
+                if (overl(ckv)) {
+                    const int rp = fld(ckv, 0), e0z = fld(ckv, 2), sb = fld(ckv, 3), nop = fld(ckv, 4);
+                    const int ls = e0z & 0x7FFFFFFF;
+                    const bool rc = e0z < 0;
+                    const int64_t so = (int64_t)(uint32_t)fld(ckv, 6) | ((int64_t)fld(ckv, 7) << 32);
+                    const int64_t cgi = (int64_t)(uint32_t)fld(ckv, 8) | ((int64_t)fld(ckv, 9) << 32);
                     const int head = (int)(so & 3);
                     const int ndw = (head + ls + 3) >> 2;
                     // the alignment's SEQ in the wave's LDS area (loaded ahead), when it fits
@@ -1065,8 +1061,8 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                                 },
                                 [&](int cc, int qp) { add_fixed(cc, qp < 0 ? 4 : fixed_at(qp)); });
                 }
-                c0e = n0e; c1e = n1e; c2e = n2e;
-                n0e = m0e; n1e = m1e; n2e = m2e;
+                ckv = nkv;
+                nkv = mkv;
                 cop = nop_;
                 cdw = ndw_;
             }
