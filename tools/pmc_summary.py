@@ -1,10 +1,10 @@
 """Summarise the PMC passes of tools/pmc.sh into profiles/<name>.json.
 
-FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB per dispatch.  Per
-MI355X_MICROARCH.md (HBM [CDNA4]) FETCH_SIZE counts half the bytes of wide
-coalesced reads on gfx950, so the read figure is doubled; WRITE_SIZE is taken
-as is.  Our loads are narrower than 16 B/lane (the guide calls those widths
-uncalibrated), so the doubled read figure is an upper estimate.
+FETCH_SIZE / WRITE_SIZE are reported by rocprofv3 in KiB per dispatch.  On gfx950
+FETCH_SIZE counts 64 B per 128-B line fetched, for every access width and pattern
+calibrated on MI355X (16 / 4 / 1 B per lane, one dword per line, hashed lines:
+tools/fetch_calib.hip -> profiles/r03_fetch_calibration.json), so the read figure is
+doubled to the bytes of the lines moved; WRITE_SIZE reads the written bytes exactly.
 """
 import csv
 import json
