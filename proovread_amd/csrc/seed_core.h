@@ -40,6 +40,14 @@
 #define SC_HD inline
 #endif
 
+// work counters of a host-only statistics build (tools/seed_stats.sh); compiled out otherwise
+#if defined(PR_SEED_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+extern unsigned long long pr_seed_stat_g[24];
+#define SC_STAT(k, v) __atomic_fetch_add(&pr_seed_stat_g[k], (unsigned long long)(v), __ATOMIC_RELAXED)
+#else
+#define SC_STAT(k, v) ((void)0)
+#endif
+
 namespace prgpu {
 namespace seedc {
 
@@ -133,6 +141,7 @@ struct Occ {
 
     SC_HD int64_t operator()(int a, int b) const {
         const int n = b - a;
+        SC_STAT(8, 1);
         if (n < KI) {
             uint32_t code = 0;
             const int32_t c12 = a + KI <= len ? S->codes[a] : -1;
@@ -144,6 +153,8 @@ struct Occ {
         }
         if (n - KI < HB) return S->ge[(int64_t)a * HB + (n - KI)];
         int64_t c = 0;
+        SC_STAT(9, 1);
+        SC_STAT(10, S->hoff[a + 1] - S->hoff[a]);
         for (int32_t k = S->hoff[a]; k < S->hoff[a + 1]; ++k) c += S->hml[k] >= n;
         return c;
     }
@@ -243,6 +254,7 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
                 int &nmem, int &err) {
     nmem = 0;
     if (q[x] > 3) return x + 1;
+    SC_STAT(16, 1);
     if (min_intv < 1) min_intv = 1;
     Iv *curr = S.curr, *prev = S.prev;
     const int cap = S.cap_iv;
@@ -300,6 +312,7 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
     for (i = x - 1; i >= -1; --i) {
         const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
         nc = 0;
+        SC_STAT(17, np);
         // the counts of this column's extensions do not depend on each other: 8 at a time
         // (their loads in flight together), then the intervals in order as before
         for (int k0 = 0; k0 < np; k0 += 8) {
@@ -569,6 +582,8 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
     const Occ occ{&I, &S, q, len, lcnt};
     const int nm = collect_intv(occ, S, O, q, len, err);
     if (err) return err;
+    SC_STAT(0, 1);
+    SC_STAT(1, nm);
     SC_TICK(0);
     // mem_chain
     int32_t ns = 0, ncv = 0;
@@ -578,6 +593,7 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         const int32_t h0 = S.hoff[p.start], h1 = S.hoff[p.start + 1];
         int64_t np = 0;
         for (int32_t k = h0; k < h1; ++k) np += S.hml[k] >= slen;
+        SC_STAT(2, h1 - h0);
         const int64_t step = np > O.max_occ ? np / O.max_occ : 1;
         int64_t fidx = 0, take = 0, count = 0;
         for (int32_t k = h0; k < h1 && count < O.max_occ; ++k) {
@@ -587,6 +603,7 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             if (!use) continue;
             take += step;
             ++count;
+            SC_STAT(3, 1);
             Seed s;
             int rid;
             text_to_fr(I, S.hpos[k], s.rbeg, rid);
@@ -597,12 +614,15 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
                 const int mid = (lo + hi) >> 1;
                 if (S.spos[mid] <= s.rbeg) lo = mid + 1;
                 else hi = mid;
+                SC_STAT(4, 1);
             }
             if (lo > 0) {
                 const int r = test_and_merge(O, I.l_pac, S, ns, S.cv[S.ord[lo - 1]], s, rid);
                 if (r < 0) return SC_OVER_SEEDS;
-                if (r) continue;
+                if (r) { SC_STAT(5, 1); continue; }
             }
+            SC_STAT(6, 1);
+            SC_STAT(7, ncv - lo);
             if (ncv >= S.cap_chains) return SC_OVER_CHAINS;
             if (ns >= S.cap_seeds) return SC_OVER_SEEDS;
             S.seeds[ns] = s;
@@ -632,6 +652,8 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         }
     }
     SC_TICK(1);
+    SC_STAT(11, ncv);
+    SC_STAT(12, (unsigned long long)ncv * ncv);
     // mem_chain_flt
     int nch = 0;
     for (int j = 0; j < ncv; ++j) {
@@ -645,6 +667,7 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         while (j >= 0 && S.ch[j].w < v.w) {
             S.ch[j + 1] = S.ch[j];
             --j;
+            SC_STAT(13, 1);
         }
         S.ch[j + 1] = v;
     }
@@ -740,6 +763,8 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         ++nkept;
     }
     *n_out = no;
+    SC_STAT(14, nch);
+    SC_STAT(15, no);
     SC_TICK(2);
     return 0;
 }
