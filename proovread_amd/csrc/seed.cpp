@@ -242,8 +242,7 @@ struct HostScratch {
     std::vector<uint16_t> hml;
     std::vector<seedc::Iv> mems, m1, curr, prev;
     std::vector<seedc::Seed> seeds;
-    std::vector<int32_t> next, ord, kept;
-    std::vector<int64_t> spos;
+    std::vector<int32_t> next, cnx, kept, hkey, hhead, htail;
     std::vector<seedc::Chain> cv, ch;
     std::vector<pr_seed_task> out;
     seedc::Scratch S{};
@@ -265,14 +264,18 @@ struct HostScratch {
         next.resize((size_t)seeds_cap);
         cv.resize((size_t)chains);
         ch.resize((size_t)chains);
-        ord.resize((size_t)chains);
+        cnx.resize((size_t)chains);
         kept.resize((size_t)chains);
-        spos.resize((size_t)chains);
+        const int32_t hs = seedc::range_table_size(chains);
+        hkey.resize((size_t)hs);
+        hhead.resize((size_t)hs);
+        htail.resize((size_t)hs);
         out.resize((size_t)out_cap);
         S = seedc::Scratch{lmax,        hoff.data(),  qext.data(), codes.data(), ge.data(),   hpos.data(),
                            hml.data(),  hits,         mems.data(), mems_cap,     m1.data(),   curr.data(),
                            prev.data(), iv,           seeds.data(), next.data(), seeds_cap,   cv.data(),
-                           ch.data(),   ord.data(),   kept.data(), spos.data(), chains};
+                           ch.data(),   cnx.data(),   kept.data(), hkey.data(), hhead.data(),
+                           htail.data(), chains,      hs};
     }
     void grow(int err) {
         if (err & seedc::SC_OVER_HITS) hits *= 2;

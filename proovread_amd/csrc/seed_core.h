@@ -11,7 +11,7 @@
 //   mem_chain         occurrences (<= -c per SMEM, sampled in text order), each
 //                     merged into the chain with the largest pos <= its rbeg by
 //                     test_and_merge or opening a new chain after the chains of
-//                     equal pos (the btree order)
+//                     equal pos (the btree order; per-range lists here, see range_slot)
 //   mem_chain_flt     chain weight, -W minimum, stable sort, -D / mask_level
 //   mem_flt_chained_seeds (bwa >= 0.7.13; runs for reads with 1.1 W <= 0.05 len, i.e.
 //                     >= 440 bp at proovread's mr -W 20): each seed's local SW score
@@ -111,9 +111,9 @@ struct Scratch {
     int32_t *next;                             // [cap_seeds]
     int32_t cap_seeds;
     Chain *cv, *ch;                            // [cap_chains] each
-    int32_t *ord, *kept;                       // [cap_chains] each
-    int64_t *spos;                             // [cap_chains] cv[ord[i]].pos, kept beside ord
-    int32_t cap_chains;
+    int32_t *cnx, *kept;                       // [cap_chains] each; cnx: next chain of its range's list
+    int32_t *hkey, *hhead, *htail;             // [hsize] range table: key (-1 free), list head / tail
+    int32_t cap_chains, hsize;                 // hsize: power of two >= 2 * cap_chains
 };
 
 SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
@@ -432,6 +432,23 @@ SC_HD void text_to_fr(const IndexView &I, uint32_t p, int64_t &fr, int &rid) {
     }
 }
 
+// ---------------------------------------------------------------- chain order
+// mem_chain keeps its chains in a btree by pos (ties: creation order) and tests every
+// occurrence against the chain with the largest pos <= its rbeg (the predecessor).
+// test_and_merge never merges across long reads or strands, and every (long read, strand)
+// is one contiguous range of the forward-reverse coordinate, so the predecessor can merge
+// only when it lies in the occurrence's own range -- and then it is the last chain of that
+// range with pos <= rbeg.  So the chains sit in one list per range (sorted by pos, ties in
+// creation order), found through a small open-addressing table keyed by rid * 2 + strand;
+// an occurrence with no such chain opens a new one.  mem_chain_flt's stable weight sort of
+// the pos-ordered chains becomes one sort by (weight desc, pos, creation).  Round 2 kept
+// one sorted array (every insert shifted ~40 entries, the seeding kernel's largest cost).
+SC_HD int range_slot(const Scratch &S, int32_t key) {
+    uint32_t h = ((uint32_t)key * 0x9E3779B1u) & (uint32_t)(S.hsize - 1);
+    while (S.hkey[h] != -1 && S.hkey[h] != key) h = (h + 1) & (uint32_t)(S.hsize - 1);
+    return (int)h;
+}
+
 // -> 1 merged, 0 not, -1 pool full
 SC_HD int test_and_merge(const pr_seed_opts &O, int64_t l_pac, Scratch &S, int32_t &ns, Chain &c, const Seed &p,
                          int rid) {
@@ -587,6 +604,7 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
     SC_TICK(0);
     // mem_chain
     int32_t ns = 0, ncv = 0;
+    for (int k = 0; k < S.hsize; ++k) S.hkey[k] = -1;
     for (int mi = 0; mi < nm; ++mi) {
         const Iv p = S.mems[mi];
         const int slen = p.end - p.start;
@@ -609,20 +627,29 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             text_to_fr(I, S.hpos[k], s.rbeg, rid);
             s.qbeg = p.start;
             s.len = slen;
-            int lo = 0, hi = ncv;   // first chain with pos > rbeg (positions beside ord: one load a step)
-            while (lo < hi) {
-                const int mid = (lo + hi) >> 1;
-                if (S.spos[mid] <= s.rbeg) lo = mid + 1;
-                else hi = mid;
+            // the predecessor that can merge: the last chain of the occurrence's range with
+            // pos <= rbeg (`at`, also the insertion point); occurrences at one locus mostly come
+            // in increasing rbeg, so the list's tail first
+            const int32_t key = rid * 2 + (s.rbeg >= I.l_pac ? 1 : 0);
+            const int hs = range_slot(S, key);
+            const bool found = S.hkey[hs] == key;
+            int at = -1;
+            if (found) {
+                const int tl = S.htail[hs];
                 SC_STAT(4, 1);
+                if (S.cv[tl].pos <= s.rbeg) at = tl;
+                else
+                    for (int x = S.hhead[hs]; x >= 0 && S.cv[x].pos <= s.rbeg; x = S.cnx[x]) {
+                        at = x;
+                        SC_STAT(4, 1);
+                    }
             }
-            if (lo > 0) {
-                const int r = test_and_merge(O, I.l_pac, S, ns, S.cv[S.ord[lo - 1]], s, rid);
+            if (at >= 0) {
+                const int r = test_and_merge(O, I.l_pac, S, ns, S.cv[at], s, rid);
                 if (r < 0) return SC_OVER_SEEDS;
                 if (r) { SC_STAT(5, 1); continue; }
             }
             SC_STAT(6, 1);
-            SC_STAT(7, ncv - lo);
             if (ncv >= S.cap_chains) return SC_OVER_CHAINS;
             if (ns >= S.cap_seeds) return SC_OVER_SEEDS;
             S.seeds[ns] = s;
@@ -635,36 +662,38 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             c.w = c.kept = 0;
             c.first = -1;
             S.cv[ncv] = c;
-            // shift ord[lo, ncv) up by one, 8 independent loads before their stores (the
-            // element-wise loop waited out one scratch-load latency per element)
-            int j = ncv;
-            for (; j - 8 >= lo; j -= 8) {
-                int32_t v[8];
-                int64_t p[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[u] = S.ord[j - 8 + u], p[u] = S.spos[j - 8 + u];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) S.ord[j - 7 + u] = v[u], S.spos[j - 7 + u] = p[u];
+            if (!found) {   // the range's first chain
+                S.hkey[hs] = key;
+                S.hhead[hs] = S.htail[hs] = ncv;
+                S.cnx[ncv] = -1;
+            } else if (at < 0) {   // before every chain of the range
+                S.cnx[ncv] = S.hhead[hs];
+                S.hhead[hs] = ncv;
+            } else {   // after `at` (and after every chain of equal pos)
+                const int nx = S.cnx[at];
+                S.cnx[ncv] = nx;
+                S.cnx[at] = ncv;
+                if (nx < 0) S.htail[hs] = ncv;
             }
-            for (; j > lo; --j) S.ord[j] = S.ord[j - 1], S.spos[j] = S.spos[j - 1];
-            S.ord[lo] = ncv++;
-            S.spos[lo] = c.pos;
+            ++ncv;
         }
     }
     SC_TICK(1);
     SC_STAT(11, ncv);
     SC_STAT(12, (unsigned long long)ncv * ncv);
-    // mem_chain_flt
+    // mem_chain_flt: the weight filter, then bwa's stable sort by weight (descending) of the
+    // pos-ordered chains = a sort by (weight desc, pos, creation order = first seed's index)
     int nch = 0;
     for (int j = 0; j < ncv; ++j) {
-        Chain c = S.cv[S.ord[j]];
+        Chain c = S.cv[j];
         c.w = chain_weight(S, c);
         if (c.w >= O.min_chain_weight) S.ch[nch++] = c;
     }
-    for (int i = 1; i < nch; ++i) {   // stable sort by weight, descending
+    for (int i = 1; i < nch; ++i) {
         const Chain v = S.ch[i];
         int j = i - 1;
-        while (j >= 0 && S.ch[j].w < v.w) {
+        while (j >= 0 && (S.ch[j].w < v.w || (S.ch[j].w == v.w && (S.ch[j].pos > v.pos ||
+                                                                   (S.ch[j].pos == v.pos && S.ch[j].head > v.head))))) {
             S.ch[j + 1] = S.ch[j];
             --j;
             SC_STAT(13, 1);
@@ -798,6 +827,11 @@ SC_HD Caps device_caps_small(int lmax) {
 }
 
 SC_HD int64_t align8(int64_t x) { return (x + 7) & ~(int64_t)7; }
+SC_HD int32_t range_table_size(int32_t chains) {
+    int32_t h = 64;
+    while (h < 2 * chains) h <<= 1;
+    return h;
+}
 
 // bytes of one lane's scratch slice
 SC_HD int64_t scratch_bytes(const Caps &c) {
@@ -813,8 +847,8 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += align8((int64_t)sizeof(Seed) * c.seeds);        // seeds
     b += align8(4 * (int64_t)c.seeds);                   // next
     b += 2 * align8((int64_t)sizeof(Chain) * c.chains);  // cv, ch
-    b += 2 * align8(4 * (int64_t)c.chains);              // ord, kept
-    b += align8(8 * (int64_t)c.chains);                  // spos
+    b += 2 * align8(4 * (int64_t)c.chains);              // cnx, kept
+    b += 3 * align8(4 * (int64_t)range_table_size(c.chains));   // hkey, hhead, htail
     return b;
 }
 
@@ -845,9 +879,12 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.cap_seeds = c.seeds;
     S.cv = (Chain *)take((int64_t)sizeof(Chain) * c.chains);
     S.ch = (Chain *)take((int64_t)sizeof(Chain) * c.chains);
-    S.ord = (int32_t *)take(4 * (int64_t)c.chains);
+    S.cnx = (int32_t *)take(4 * (int64_t)c.chains);
     S.kept = (int32_t *)take(4 * (int64_t)c.chains);
-    S.spos = (int64_t *)take(8 * (int64_t)c.chains);
+    S.hsize = range_table_size(c.chains);
+    S.hkey = (int32_t *)take(4 * (int64_t)S.hsize);
+    S.hhead = (int32_t *)take(4 * (int64_t)S.hsize);
+    S.htail = (int32_t *)take(4 * (int64_t)S.hsize);
     S.cap_chains = c.chains;
     return S;
 }

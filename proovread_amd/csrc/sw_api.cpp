@@ -326,6 +326,42 @@ static int side_stream(SwResident &r) {
     return 0;
 }
 
+// The packed CIGAR pass's task order (sorted by key, padded to 128-task segments), then its
+// launch geometry: the segment count read back, split into chunks whose slabs (one per
+// segment, PK_TMAX rows) fit the slab budget (PRGPU_PK_SLAB_GB, default 32 GB), each chunk
+// a DP launch and a backtrack launch; PRGPU_PK_FUSED=1 keeps the fused kernel.
+static int pk_prepare(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O) {
+    D.pk_chunk = 0;
+    if (!O.pk) return 0;
+    hipStream_t s = ctx_stream(c);
+    int e = sw_launch_pk_order(D, O, 0, (void *)s);
+    if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+    const char *fz = getenv("PRGPU_PK_FUSED");
+    if (fz && atoi(fz)) return 0;
+    int32_t len = 0;
+    HIPCHK(hipMemcpyAsync(&len, D.pk_bucket + PK_SCAN, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const int64_t nseg = len / PK_SEG;
+    const size_t slab = (size_t)D.z_pk_slab * sizeof(PkDir);
+    const char *gb = getenv("PRGPU_PK_SLAB_GB");
+    const double budget = (gb ? atof(gb) : 32.0) * (double)(1ull << 30);
+    int64_t per = (int64_t)(budget / (double)slab);
+    per = per < 64 ? 64 : per;
+    const int64_t nch = nseg > 0 ? (nseg + per - 1) / per : 1;
+    const int64_t chunk = nseg > 0 ? (nseg + nch - 1) / nch : 1;
+    if ((size_t)chunk * slab > r.cap[SB_Z]) {
+        int rc = ensure(r, SB_Z, (size_t)chunk * slab);
+        if (rc) return rc;
+    }
+    D.z = (uint8_t *)r.buf[SB_Z];
+    D.pk_chunk = (int)chunk;
+    D.pk_nseg_bound = nseg;
+    const char *bw = getenv("PRGPU_PK_BT_WIN");
+    D.pk_bt_win = bw && atoi(bw) == 16 ? 16 : 8;
+    D.pk_bt_grid = ctx_ncu(c) * sw_pk_bt_occupancy(D.pk_bt_win);
+    return 0;
+}
+
 // bwa mode: extension rounds (mem_chain2aln), the final pass (mem_sort_dedup_patch ..
 // mem_reg2sam) with mem_patch_reg rounds, then the CIGAR pass over the reported alignments
 static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, const pr_sw_opts *o, int grid_w,
@@ -447,8 +483,9 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     D.tsel_n = r.n_aln;
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
     if (r.n_aln) {
+        if ((rc = pk_prepare(c, r, D, O))) return rc;
         e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6),
-                             (void *)ctx_event(c, 7));
+                             (void *)ctx_event(c, 7), true);
         if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     }
     unsigned long long sp[2] = {0, 0};
@@ -589,7 +626,9 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
 
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
-    e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6), (void *)ctx_event(c, 7));
+    if ((rc = pk_prepare(c, r, D, O))) return rc;
+    e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6), (void *)ctx_event(c, 7),
+                         true);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     // CIGARs longer than their slots: recompute those tasks into the spill area
     unsigned long long sp[2] = {0, 0};

@@ -63,6 +63,9 @@ struct SwDev {
     int64_t z_slab;            // bytes per slab (LDS kernel)
     int64_t z_ring_slab;       // dwords per slab (register-ring kernels: rows x words x 64 lanes)
     int64_t z_pk_slab;         // PkDir entries per slab (packed kernel: rows x chunks x 64 lanes)
+    int pk_chunk;              // packed CIGAR pass: segments per DP + backtrack launch pair (0: fused kernel)
+    int64_t pk_nseg_bound;     // upper bound on its segments (the launch loop's extent)
+    int pk_bt_grid, pk_bt_win; // backtrack kernel: grid (waves), window rows (8 or 16)
     unsigned long long *cells; // [3] canonical DP cells (extension, global, dominant launch), [3..6] pk phase cycles
     int32_t *perm;             // lane -> task order (tasks bucketed by extension lengths)
     int32_t *bucket;           // [SW_NBUCKET + 1] counting-sort scratch
@@ -136,7 +139,9 @@ int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out,
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream,
                      SwEvPool *evp = nullptr);
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
-                     void *stream, void *ev_a, void *ev_b);
+                     void *stream, void *ev_a, void *ev_b, bool pk_ordered = false);
+int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *stream);
+int sw_pk_bt_occupancy(int win);
 int sw_launch_lds(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
 int sw_launch_overflow(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);
 int sw_launch_cig_compact(const uint32_t *pool, const int64_t *at, const int32_t *ncig, const int64_t *off,

@@ -864,18 +864,68 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
 // tasks list[128k + l] (low halves) and list[128k + 64 + l] (high halves).
 // Tasks that meet an N, or whose loop would run a second pass, are left to the
 // LDS kernel (x_try bit 2).
+//
+// Two kernels per chunk of segments [seg0, seg1): the DP (sw_global_pk_kernel, 256 VGPRs,
+// 2 waves per SIMD, VALU-bound) writes every segment's direction words into its own slab
+// of the chunk's slab array and the scores; the backtrack + emit (sw_global_pk_bt_kernel:
+// divergent, load-latency-bound walks with few registers, many waves per SIMD) reads them
+// back.  split = 0 keeps round 2's fused kernel (one slab per resident wave, the walk right
+// after the DP) for comparison (PRGPU_PK_FUSED).
+
+// mem_reg2aln after ksw_global2 (glob_emit's rules) on the forward-ordered ops at the end of
+// the task's slots: position, leading/trailing D squeeze, soft clips
+__device__ __forceinline__ void pk_emit(const SwDev &D, int64_t t, uint32_t *cg, int cap, int nc, uint32_t fst,
+                                        uint32_t lst, int gsc, bool rev) {
+    const int sid = D.t_sr[t], lid = D.t_lr[t];
+    const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
+    const int L = (int)(D.lr_off[lid + 1] - D.lr_off[lid]);
+    const int qb = D.o_qb[t], qe = D.o_qe[t], rb = D.o_rb[t], re = D.o_re[t];
+    int m = nc, src = cap - nc;
+    int pos = rev ? L - re : rb;
+    if (m < 0) {
+        cig_overflow(D, t);
+        return;
+    }
+    if (m > 0) {
+        if ((fst & 0xFu) == 2u) {
+            pos += (int)(fst >> 4);
+            ++src, --m;
+        } else if ((lst & 0xFu) == 2u) {
+            --m;
+        }
+    }
+    int clip5 = 0, clip3 = 0;
+    if (qb != 0 || qe != lq) {
+        clip5 = rev ? lq - qe : qb;
+        clip3 = rev ? qb : lq - qe;
+        if (m + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > cap) {
+            cig_overflow(D, t);
+            return;
+        }
+    }
+    const int d0 = clip5 ? 1 : 0;
+    pk_cig_move(cg, d0, src, m);
+    if (clip5) cg[0] = ((uint32_t)clip5 << 4) | 4u;
+    if (clip3) cg[d0 + m] = ((uint32_t)clip3 << 4) | 4u;
+    D.o_gscore[t] = gsc;
+    D.o_pos[t] = pos;
+    D.o_ncig[t] = d0 + m + (clip3 ? 1 : 0);
+    D.o_status[t] = 0;
+}
 
 template <int WB>
-__global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOptsDev O) {
+__global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOptsDev O, int seg0, int seg1, int split) {
     // query masks ([half][bit][word][lane])
     __shared__ __attribute__((aligned(16))) uint32_t lsh[2 * 2 * PK_NQW * SW_WAVE];
     const int lane = threadIdx.x;
     uint32_t *lm = lsh;
-    PkDir *zl = reinterpret_cast<PkDir *>(D.z) + (int64_t)blockIdx.x * D.z_pk_slab + lane;
     unsigned long long cells = 0;
-    const int nseg = D.pk_bucket[PK_SCAN] / PK_SEG;
+    const int nseg_all = D.pk_bucket[PK_SCAN] / PK_SEG;
+    const int nseg = seg1 < nseg_all ? seg1 : nseg_all;
     unsigned long long ph[4] = {0, 0, 0, 0};   // wave cycles: masks, DP, backtrack, emit
-    for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    for (int seg = seg0 + blockIdx.x; seg < nseg; seg += gridDim.x) {
+        // split: the segment's slab in the chunk's array; fused: this wave's own slab
+        PkDir *zl = reinterpret_cast<PkDir *>(D.z) + (int64_t)(split ? seg - seg0 : blockIdx.x) * D.z_pk_slab + lane;
         unsigned long long c0 = clock64();
         const int64_t tt[2] = {D.list[(int64_t)seg * PK_SEG + lane], D.list[(int64_t)seg * PK_SEG + 64 + lane]};
         // the segment's key (its first task is never padding)
@@ -929,13 +979,19 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
                 D.x_try[t] = (uint8_t)(D.x_try[t] | 4);
                 continue;
             }
+            cells += band_cells(rlen, lqq, ww);
+            if (split) {   // the score for the backtrack kernel's emit
+                D.o_gscore[t] = sc[h];
+                continue;
+            }
             cg[h] = cig_dest(D, t, cap[h]);
             tl[h] = rlen;
         }
-        int nc[2] = {0, 0};
-        uint32_t fst[2] = {0u, 0u}, lst[2] = {0u, 0u};
         unsigned long long c2 = clock64();
         ph[1] += c2 - c1;
+        if (split) continue;
+        int nc[2] = {0, 0};
+        uint32_t fst[2] = {0u, 0u}, lst[2] = {0u, 0u};
         if (O.debug & 1) {
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -946,56 +1002,69 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
         unsigned long long c3 = clock64();
         ph[2] += c3 - c2;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!cg[h]) continue;
-            const int64_t t = tt[h];
-            const int sid = D.t_sr[t], lid = D.t_lr[t];
-            const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
-            const int L = (int)(D.lr_off[lid + 1] - D.lr_off[lid]);
-            const int qb = D.o_qb[t], qe = D.o_qe[t], rb = D.o_rb[t], re = D.o_re[t];
-            const bool rev = H[h].comp;
-            // mem_reg2aln after ksw_global2 (glob_emit's rules) on the forward-ordered ops at the slots' end
-            int m = nc[h], src = cap[h] - nc[h];
-            int pos = rev ? L - re : rb;
-            cells += band_cells(tl[h], lqq, ww);
-            if (m < 0) {
-                cig_overflow(D, t);
-                continue;
-            }
-            if (m > 0) {
-                if ((fst[h] & 0xFu) == 2u) {
-                    pos += (int)(fst[h] >> 4);
-                    ++src, --m;
-                } else if ((lst[h] & 0xFu) == 2u) {
-                    --m;
-                }
-            }
-            int clip5 = 0, clip3 = 0;
-            if (qb != 0 || qe != lq) {
-                clip5 = rev ? lq - qe : qb;
-                clip3 = rev ? qb : lq - qe;
-                if (m + (clip5 ? 1 : 0) + (clip3 ? 1 : 0) > cap[h]) {
-                    cig_overflow(D, t);
-                    continue;
-                }
-            }
-            const int d0 = clip5 ? 1 : 0;
-            pk_cig_move(cg[h], d0, src, m);
-            if (clip5) cg[h][0] = ((uint32_t)clip5 << 4) | 4u;
-            if (clip3) cg[h][d0 + m] = ((uint32_t)clip3 << 4) | 4u;
-            D.o_gscore[t] = sc[h];
-            D.o_pos[t] = pos;
-            D.o_ncig[t] = d0 + m + (clip3 ? 1 : 0);
-            D.o_status[t] = 0;
-        }
+        for (int h = 0; h < 2; ++h)
+            if (cg[h]) pk_emit(D, tt[h], cg[h], cap[h], nc[h], fst[h], lst[h], sc[h], H[h].comp);
         ph[3] += clock64() - c3;
     }
     if (lane == 0)
-        for (int q = 0; q < 4; ++q) atomicAdd(&D.cells[3 + q], ph[q]);
+        for (int q = 0; q < 4; ++q)
+            if (ph[q]) atomicAdd(&D.cells[3 + q], ph[q]);
     for (int o = 32; o > 0; o >>= 1) cells += __shfl_down(cells, o, 64);
     if (lane == 0 && cells) {
         atomicAdd(&D.cells[1], cells);
         atomicAdd(&D.cells[2], cells);   // the dominant launch's own cells (bench roofline)
+    }
+}
+
+// The backtrack + emit of the packed CIGAR pass over the slabs sw_global_pk_kernel(split = 1)
+// wrote for the chunk [seg0, seg1): one wave per segment, the same lanes and halves as the DP;
+// tasks the DP handed to the LDS kernel (x_try bit 2) are skipped.
+template <int WIN>
+__global__ void __launch_bounds__(SW_WAVE, WIN == 8 ? 4 : 3) sw_global_pk_bt_kernel(SwDev D, SwOptsDev O, int seg0, int seg1) {
+    const int lane = threadIdx.x;
+    const int nseg_all = D.pk_bucket[PK_SCAN] / PK_SEG;
+    const int nseg = seg1 < nseg_all ? seg1 : nseg_all;
+    unsigned long long ph[2] = {0, 0};   // wave cycles: backtrack, emit
+    for (int seg = seg0 + blockIdx.x; seg < nseg; seg += gridDim.x) {
+        const unsigned long long c0 = clock64();
+        const PkDir *zl = reinterpret_cast<const PkDir *>(D.z) + (int64_t)(seg - seg0) * D.z_pk_slab + lane;
+        const int64_t tt[2] = {D.list[(int64_t)seg * PK_SEG + lane], D.list[(int64_t)seg * PK_SEG + 64 + lane]};
+        const int key = __builtin_amdgcn_readfirstlane(pk_key(D, O, D.list[(int64_t)seg * PK_SEG]));
+        const int ww = key >> 8, lqq = key & 255;
+        uint32_t *cg[2] = {nullptr, nullptr};
+        int tl[2] = {0, 0}, cap[2] = {0, 0}, nrow = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int64_t t = tt[h];
+            if (t < 0 || (D.x_try[t] & 4)) continue;
+            tl[h] = D.o_re[t] - D.o_rb[t];
+            cg[h] = cig_dest(D, t, cap[h]);
+            nrow = nrow > tl[h] ? nrow : tl[h];
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            const int v = __shfl_xor(nrow, o, 64);
+            nrow = nrow > v ? nrow : v;
+        }
+        nrow = __builtin_amdgcn_readfirstlane(nrow);
+        int nc[2] = {0, 0};
+        uint32_t fst[2] = {0u, 0u}, lst[2] = {0u, 0u};
+        if (O.debug & 1) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (cg[h]) cg[h][cap[h] - 1] = fst[h] = lst[h] = ((uint32_t)lqq << 4), nc[h] = 1;
+        } else if (nrow > 0) {
+            pk_backtrack2<WIN>(zl, SW_WAVE, pk_npair(ww), nrow, tl, lqq, ww, cg, nc, fst, lst, cap);
+        }
+        const unsigned long long c1 = clock64();
+        ph[0] += c1 - c0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            if (cg[h]) pk_emit(D, tt[h], cg[h], cap[h], nc[h], fst[h], lst[h], D.o_gscore[tt[h]], D.t_strand[tt[h]] != 0);
+        ph[1] += clock64() - c1;
+    }
+    if (lane == 0) {
+        if (ph[0]) atomicAdd(&D.cells[5], ph[0]);
+        if (ph[1]) atomicAdd(&D.cells[6], ph[1]);
     }
 }
 
@@ -1165,7 +1234,14 @@ int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out,
     return (int)hipGetLastError();
 }
 
-int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *stream);
+// resident waves per CU of the packed CIGAR backtrack kernel (window of win rows)
+int sw_pk_bt_occupancy(int win) {
+    int nb = 0;
+    const hipError_t e = win == 8
+        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_global_pk_bt_kernel<8>, SW_WAVE, 0)
+        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_global_pk_bt_kernel<16>, SW_WAVE, 0);
+    return e == hipSuccess && nb > 0 ? nb : 8;
+}
 
 // the four extension phases + the two finish passes (mem_chain2aln)
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream, SwEvPool *evp) {
@@ -1211,13 +1287,28 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
     return (int)hipGetLastError();
 }
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
-                     void *stream, void *ev_a, void *ev_b) {
+                     void *stream, void *ev_a, void *ev_b, bool pk_ordered) {
     hipStream_t s = (hipStream_t)stream;
     int rc;
     if (O.pk) {
-        if ((rc = sw_launch_pk_order(D, O, 0, stream))) return rc;
+        if (!pk_ordered && (rc = sw_launch_pk_order(D, O, 0, stream))) return rc;
         if (ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
-        hipLaunchKernelGGL(sw_global_pk_kernel<40>, dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O);
+        if (D.pk_chunk <= 0) {   // fused: DP and backtrack in one kernel, a slab per resident wave
+            hipLaunchKernelGGL(sw_global_pk_kernel<40>, dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, 0, INT32_MAX, 0);
+        } else {   // chunks of segments: the DP kernel, then the backtrack kernel over the chunk's slabs
+            for (int64_t c0 = 0; c0 < D.pk_nseg_bound; c0 += D.pk_chunk) {
+                const int c1 = (int)(c0 + D.pk_chunk < D.pk_nseg_bound ? c0 + D.pk_chunk : D.pk_nseg_bound);
+                const int n = c1 - (int)c0;
+                hipLaunchKernelGGL(sw_global_pk_kernel<40>, dim3(n < grid_pk ? n : grid_pk), dim3(SW_WAVE), 0, s, D, O,
+                                   (int)c0, c1, 1);
+                if (D.pk_bt_win == 8)
+                    hipLaunchKernelGGL(sw_global_pk_bt_kernel<8>, dim3(n < D.pk_bt_grid ? n : D.pk_bt_grid), dim3(SW_WAVE),
+                                       0, s, D, O, (int)c0, c1);
+                else
+                    hipLaunchKernelGGL(sw_global_pk_bt_kernel<16>, dim3(n < D.pk_bt_grid ? n : D.pk_bt_grid), dim3(SW_WAVE),
+                                       0, s, D, O, (int)c0, c1);
+            }
+        }
         if (ev_b) (void)hipEventRecord((hipEvent_t)ev_b, s);
     }
     if ((rc = sw_launch_order(D, O, 5, D.list, stream))) return rc;

@@ -61,6 +61,11 @@ SW_RING_FN uint32_t pk_min(uint32_t a, uint32_t b) { return PU(__builtin_element
 SW_RING_FN uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) { return PU(PV(a) * PV(b) + PV(c)); }
 SW_RING_FN uint32_t pk_shl(uint32_t a, int k) { return PU(PV(a) << pk_v{(short)k, (short)k}); }
 SW_RING_FN uint32_t pk_asr15(uint32_t a) { return PU(PV(a) >> pk_v{15, 15}); }
+typedef unsigned short pku_v __attribute__((ext_vector_type(2)));
+// unsigned saturating subtract: max(a - b, 0) per half for a, b in [0, 32767] (v_pk_sub_u16 clamp)
+SW_RING_FN uint32_t pk_subs(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(pku_v, a), __builtin_bit_cast(pku_v, b)));
+}
 SW_RING_FN uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) { return __builtin_amdgcn_perm(s0, s1, sel); }
 SW_RING_FN uint32_t align_b32(uint32_t hi, uint32_t lo, uint32_t sh) { return __builtin_amdgcn_alignbit(hi, lo, sh); }
 #else
@@ -80,6 +85,10 @@ SW_RING_FN uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
 }
 SW_RING_FN uint32_t pk_shl(uint32_t a, int k) { return pk_mk((uint16_t)(a << k), (uint16_t)((a >> 16) << k)); }
 SW_RING_FN uint32_t pk_asr15(uint32_t a) { return pk_mk(pk_lo(a) >> 15, pk_hi(a) >> 15); }
+SW_RING_FN uint32_t pk_subs(uint32_t a, uint32_t b) {
+    const uint32_t al = a & 0xFFFFu, bl = b & 0xFFFFu, ah = a >> 16, bh = b >> 16;
+    return (al > bl ? al - bl : 0u) | ((ah > bh ? ah - bh : 0u) << 16);
+}
 SW_RING_FN uint32_t perm_b32(uint32_t s0, uint32_t s1, uint32_t sel) {
     const uint64_t d = ((uint64_t)s0 << 32) | s1;
     uint32_t r = 0;
@@ -437,11 +446,13 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
                 const uint32_t Hd = s + 1 < NS ? RH[s + 1] : qin;
                 const uint32_t e0 = s + 1 < NS ? RE[s + 1] : 0u;
                 const uint32_t mm = pk_asr15(pk_shl(G[s >> 4], 15 - (s & 15)));
-                // M = H(i-1,j-1) ? H(i-1,j-1) + S : 0 (a negative M acts as 0 below)
-                const uint32_t M = pk_min(pk_shl(Hd, 4), pk_mad(mm, NAB, pk_sub(Hd, BD)));
+                // M = H(i-1,j-1) ? H(i-1,j-1) + S : 0, clamped at 0 (a negative M acts as 0 in
+                // every use: h = max(M, e, f) with e, f >= 0, and the gap openings max(M - oe, 0)),
+                // so the unsigned saturating subtracts replace the max-with-0 steps
+                const uint32_t M = pk_min(pk_shl(Hd, 4), pk_subs(pk_mad(mm, NAB, Hd), BD));
                 const uint32_t h = pk_max(pk_max(M, e0), f);
-                const uint32_t en = pk_max(pk_sub(e0, cED), pk_max(pk_sub(M, cOD), 0u));
-                const uint32_t fn = pk_max(pk_sub(f, cEI), pk_max(pk_sub(M, cOI), 0u));
+                const uint32_t en = pk_max(pk_subs(e0, cED), pk_subs(M, cOD));
+                const uint32_t fn = pk_max(pk_subs(f, cEI), pk_subs(M, cOI));
                 const uint32_t ge = perm_b32(0u, pk_sub(sev, pk_dup(s)), 0x09090808u);   // s >= se
                 RH[s] = bfi_b32v(gt, Hd, h1);
                 RE[s] = bfi_b32v(gt, e0, bfi_b32v(ge, 0u, en));
@@ -567,6 +578,7 @@ SW_RING_FN int glob_pk_backtrack(const PkDir *z, int ZS, int npair, int hb, int 
 // from the END of the task's CIGAR slots backwards: the ops land in final
 // (forward) order at cg[h][maxcig[h] - n, maxcig[h]).  n[h] = op count or -1 (more
 // than maxcig[h]); first[h] / last[h] = the first / last op of the forward CIGAR.
+template <int WIN = 16>
 SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, const int tl[2], int qlen, int w,
                               uint32_t *const cg[2], int n[2], uint32_t first[2], uint32_t last[2],
                               const int maxcig[2]) {
@@ -606,15 +618,15 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
         first[h] = last[h] = 0u;
         live[h] = cg[h] != nullptr && i[h] >= 0 && k[h] >= 0;
     }
-    for (int R = nrows - 1; R >= 0 && SW_RING_ANY(live[0] || live[1]); R -= 16) {
-        uint32_t bx[2][16], by[2][16];
+    for (int R = nrows - 1; R >= 0 && SW_RING_ANY(live[0] || live[1]); R -= WIN) {
+        uint32_t bx[2][WIN], by[2][WIN];
         int p[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             p[h] = (k[h] - i[h] + w) >> 4;
-            PkDir v[16];
+            PkDir v[WIN];
 #pragma unroll
-            for (int d = 0; d < 16; ++d) {
+            for (int d = 0; d < WIN; ++d) {
                 v[d] = PkDir{0u, 0u, 0u, 0u};
                 if (live[h] && R - d >= 0 && R - d <= i[h]) {
                     const long ix = ((long)(R - d) * npair + p[h]) * ZS;
@@ -623,10 +635,10 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                 }
             }
 #pragma unroll
-            for (int d = 0; d < 16; ++d) pick(v[d], h, bx[h][d], by[h][d]);
+            for (int d = 0; d < WIN; ++d) pick(v[d], h, bx[h][d], by[h][d]);
         }
 #pragma unroll
-        for (int d = 0; d < 16; ++d) {
+        for (int d = 0; d < WIN; ++d) {
             const int r = R - d;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
