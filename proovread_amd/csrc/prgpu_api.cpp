@@ -1188,9 +1188,16 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     K.caps = small;
     K.stride = seedc::scratch_bytes(small);
     const char *wpc = getenv("PRGPU_SEED_WAVES_PER_CU");   // tuning hook
-    int64_t waves = (int64_t)c->n_cu * (wpc ? atoi(wpc) : 16);   // ~78 KB x 64 slices per wave at 150 bp
-    if (waves > (n_sr + 63) / 64) waves = (n_sr + 63) / 64;
+    int64_t waves = (int64_t)c->n_cu * (wpc ? atoi(wpc) : 16);   // ~98 KB x 64 slices per wave at 150 bp
+    const int64_t nbatch = (n_sr + 63) / 64;
+    if (waves > nbatch) waves = nbatch;
     if (waves < 1) waves = 1;
+    // PRGPU_SEED_BALANCE: every wave the same number of 64-read batches (fewer waves; measured
+    // slower at configs[1], 357 vs 345 ms: the lane phase wants every wave it can get)
+    if (getenv("PRGPU_SEED_BALANCE")) {
+        const int64_t rounds = (nbatch + waves - 1) / waves;
+        waves = (nbatch + rounds - 1) / rounds;
+    }
     K.n_lanes = waves;
     int64_t lanes2 = (int64_t)c->n_cu * seed_slots_per_cu();
     const int64_t scratch = std::max<int64_t>(waves * 64 * K.stride, lanes2 * seedc::scratch_bytes(caps));

@@ -609,9 +609,9 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         const Iv p = S.mems[mi];
         const int slen = p.end - p.start;
         const int32_t h0 = S.hoff[p.start], h1 = S.hoff[p.start + 1];
-        int64_t np = 0;
-        for (int32_t k = h0; k < h1; ++k) np += S.hml[k] >= slen;
-        SC_STAT(2, h1 - h0);
+        // the SMEM's occurrence count is the number of the start's hits with ml >= slen
+        // (every interval's occ comes from the same per-start table, slen >= 12)
+        const int64_t np = p.occ;
         const int64_t step = np > O.max_occ ? np / O.max_occ : 1;
         int64_t fidx = 0, take = 0, count = 0;
         for (int32_t k = h0; k < h1 && count < O.max_occ; ++k) {
@@ -823,7 +823,7 @@ SC_HD Caps device_caps() { return Caps{1024, 8192, 256, 1024, 4096, 2048, 384}; 
 // pass 1 of the device path: 64 slices per wave, sized for reads of <= lmax bases
 SC_HD Caps device_caps_small(int lmax) {
     const int l = lmax < 16 ? 16 : (lmax + 15) & ~15;
-    return Caps{l, 4096, 64, 256, 512, 256, 384};
+    return Caps{l, 4096, 64, 512, 512, 384, 384};   // ~0.1 % of configs[1]'s reads outgrow it (mems)
 }
 
 SC_HD int64_t align8(int64_t x) { return (x + 7) & ~(int64_t)7; }

@@ -327,17 +327,19 @@ static int side_stream(SwResident &r) {
 }
 
 // The packed CIGAR pass's task order (sorted by key, padded to 128-task segments), then its
-// launch geometry: the segment count read back, split into chunks whose slabs (one per
-// segment, PK_TMAX rows) fit the slab budget (PRGPU_PK_SLAB_GB, default 32 GB), each chunk
-// a DP launch and a backtrack launch; PRGPU_PK_FUSED=1 keeps the fused kernel.
+// launch geometry.  Default: the fused kernel (DP and backtrack per segment in one wave, a
+// slab per resident wave).  PRGPU_PK_SPLIT=1: the segment count read back, split into chunks
+// whose slabs (one per segment, PK_TMAX rows) fit PRGPU_PK_SLAB_GB (default 32 GB), each chunk
+// a DP launch and a backtrack launch (measured at configs[1]: DP 43.4 + backtrack 15.4 ms
+// against 58.8 ms fused -- the walk is latency- and issue-bound).
 static int pk_prepare(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O) {
     D.pk_chunk = 0;
     if (!O.pk) return 0;
     hipStream_t s = ctx_stream(c);
     int e = sw_launch_pk_order(D, O, 0, (void *)s);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
-    const char *fz = getenv("PRGPU_PK_FUSED");
-    if (fz && atoi(fz)) return 0;
+    const char *sp = getenv("PRGPU_PK_SPLIT");
+    if (!sp || !atoi(sp)) return 0;
     int32_t len = 0;
     HIPCHK(hipMemcpyAsync(&len, D.pk_bucket + PK_SCAN, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -357,7 +359,7 @@ static int pk_prepare(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O) {
     D.pk_chunk = (int)chunk;
     D.pk_nseg_bound = nseg;
     const char *bw = getenv("PRGPU_PK_BT_WIN");
-    D.pk_bt_win = bw && atoi(bw) == 16 ? 16 : 8;
+    D.pk_bt_win = bw && (atoi(bw) == 16 || atoi(bw) == 4) ? atoi(bw) : 8;
     D.pk_bt_grid = ctx_ncu(c) * sw_pk_bt_occupancy(D.pk_bt_win);
     return 0;
 }
@@ -1019,8 +1021,10 @@ extern "C" int pr_sw_phase_cycles(pr_ctx *c, int64_t *out4) {
     if (!r.loaded) return pr_set_error(PR_ERR_ARG, "no resident SW batch");
     HIPCHK(hipSetDevice(ctx_device(c)));
     HIPCHK(hipStreamSynchronize(ctx_stream(c)));
-    unsigned long long v[7];
+    unsigned long long v[10];
     HIPCHK(hipMemcpy(v, r.buf[SB_CELLS], sizeof v, hipMemcpyDeviceToHost));
     for (int q = 0; q < 4; ++q) out4[q] = (int64_t)v[3 + q];
+    if (getenv("PRGPU_SW_DEBUG") && (atoi(getenv("PRGPU_SW_DEBUG")) & 4))   // backtrack walk statistics
+        fprintf(stderr, "[sw] backtrack: %llu walk steps, %llu off-pair loads\n", v[9], v[7]);
     return 0;
 }

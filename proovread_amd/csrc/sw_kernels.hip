@@ -865,12 +865,11 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
 // Tasks that meet an N, or whose loop would run a second pass, are left to the
 // LDS kernel (x_try bit 2).
 //
-// Two kernels per chunk of segments [seg0, seg1): the DP (sw_global_pk_kernel, 256 VGPRs,
-// 2 waves per SIMD, VALU-bound) writes every segment's direction words into its own slab
-// of the chunk's slab array and the scores; the backtrack + emit (sw_global_pk_bt_kernel:
-// divergent, load-latency-bound walks with few registers, many waves per SIMD) reads them
-// back.  split = 0 keeps round 2's fused kernel (one slab per resident wave, the walk right
-// after the DP) for comparison (PRGPU_PK_FUSED).
+// split = 0 (the default): the fused kernel, one slab per resident wave, the walk right after
+// the DP.  split = 1 (PRGPU_PK_SPLIT, sw_api.cpp pk_prepare): two kernels per chunk of
+// segments [seg0, seg1): the DP writes every segment's direction words into its own slab of
+// the chunk's slab array and the scores; the backtrack + emit (sw_global_pk_bt_kernel, fewer
+// registers, more waves per SIMD) reads them back.  Measured equal in total.
 
 // mem_reg2aln after ksw_global2 (glob_emit's rules) on the forward-ordered ops at the end of
 // the task's slots: position, leading/trailing D squeeze, soft clips
@@ -1020,11 +1019,12 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
 // wrote for the chunk [seg0, seg1): one wave per segment, the same lanes and halves as the DP;
 // tasks the DP handed to the LDS kernel (x_try bit 2) are skipped.
 template <int WIN>
-__global__ void __launch_bounds__(SW_WAVE, WIN == 8 ? 4 : 3) sw_global_pk_bt_kernel(SwDev D, SwOptsDev O, int seg0, int seg1) {
+__global__ void __launch_bounds__(SW_WAVE, WIN == 4 ? 6 : (WIN == 8 ? 4 : 3)) sw_global_pk_bt_kernel(SwDev D, SwOptsDev O, int seg0, int seg1) {
     const int lane = threadIdx.x;
     const int nseg_all = D.pk_bucket[PK_SCAN] / PK_SEG;
     const int nseg = seg1 < nseg_all ? seg1 : nseg_all;
     unsigned long long ph[2] = {0, 0};   // wave cycles: backtrack, emit
+    unsigned st[2] = {0u, 0u};           // O.debug & 4: off-pair loads, walk steps
     for (int seg = seg0 + blockIdx.x; seg < nseg; seg += gridDim.x) {
         const unsigned long long c0 = clock64();
         const PkDir *zl = reinterpret_cast<const PkDir *>(D.z) + (int64_t)(seg - seg0) * D.z_pk_slab + lane;
@@ -1053,7 +1053,8 @@ __global__ void __launch_bounds__(SW_WAVE, WIN == 8 ? 4 : 3) sw_global_pk_bt_ker
             for (int h = 0; h < 2; ++h)
                 if (cg[h]) cg[h][cap[h] - 1] = fst[h] = lst[h] = ((uint32_t)lqq << 4), nc[h] = 1;
         } else if (nrow > 0) {
-            pk_backtrack2<WIN>(zl, SW_WAVE, pk_npair(ww), nrow, tl, lqq, ww, cg, nc, fst, lst, cap);
+            pk_backtrack2<WIN>(zl, SW_WAVE, pk_npair(ww), nrow, tl, lqq, ww, cg, nc, fst, lst, cap,
+                               (O.debug & 4) ? st : nullptr);
         }
         const unsigned long long c1 = clock64();
         ph[0] += c1 - c0;
@@ -1065,6 +1066,11 @@ __global__ void __launch_bounds__(SW_WAVE, WIN == 8 ? 4 : 3) sw_global_pk_bt_ker
     if (lane == 0) {
         if (ph[0]) atomicAdd(&D.cells[5], ph[0]);
         if (ph[1]) atomicAdd(&D.cells[6], ph[1]);
+    }
+    if (O.debug & 4) {
+        unsigned long long a = st[0], b = st[1];
+        for (int o = 32; o > 0; o >>= 1) a += __shfl_down(a, o, 64), b += __shfl_down(b, o, 64);
+        if (lane == 0) atomicAdd(&D.cells[7], a), atomicAdd(&D.cells[9], b);
     }
 }
 
@@ -1237,8 +1243,8 @@ int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out,
 // resident waves per CU of the packed CIGAR backtrack kernel (window of win rows)
 int sw_pk_bt_occupancy(int win) {
     int nb = 0;
-    const hipError_t e = win == 8
-        ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_global_pk_bt_kernel<8>, SW_WAVE, 0)
+    const hipError_t e = win == 4 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_global_pk_bt_kernel<4>, SW_WAVE, 0)
+        : win == 8 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_global_pk_bt_kernel<8>, SW_WAVE, 0)
         : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, sw_global_pk_bt_kernel<16>, SW_WAVE, 0);
     return e == hipSuccess && nb > 0 ? nb : 8;
 }
@@ -1301,7 +1307,10 @@ int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
                 const int n = c1 - (int)c0;
                 hipLaunchKernelGGL(sw_global_pk_kernel<40>, dim3(n < grid_pk ? n : grid_pk), dim3(SW_WAVE), 0, s, D, O,
                                    (int)c0, c1, 1);
-                if (D.pk_bt_win == 8)
+                if (D.pk_bt_win == 4)
+                    hipLaunchKernelGGL(sw_global_pk_bt_kernel<4>, dim3(n < D.pk_bt_grid ? n : D.pk_bt_grid), dim3(SW_WAVE),
+                                       0, s, D, O, (int)c0, c1);
+                else if (D.pk_bt_win == 8)
                     hipLaunchKernelGGL(sw_global_pk_bt_kernel<8>, dim3(n < D.pk_bt_grid ? n : D.pk_bt_grid), dim3(SW_WAVE),
                                        0, s, D, O, (int)c0, c1);
                 else

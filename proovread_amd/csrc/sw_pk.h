@@ -581,7 +581,7 @@ SW_RING_FN int glob_pk_backtrack(const PkDir *z, int ZS, int npair, int hb, int 
 template <int WIN = 16>
 SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, const int tl[2], int qlen, int w,
                               uint32_t *const cg[2], int n[2], uint32_t first[2], uint32_t last[2],
-                              const int maxcig[2]) {
+                              const int maxcig[2], unsigned *stat = nullptr) {
     int i[2], k[2], which[2] = {0, 0}, rop[2] = {-1, -1}, rln[2] = {0, 0};
     bool live[2];
     auto flush = [&](int h) {
@@ -649,7 +649,9 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                         const long ix = ((long)r * npair + (sl >> 4)) * ZS;
                         PK_ZCHECK(ix);
                         pick(zl[ix], h, X, Y);
+                        if (stat) ++stat[0];
                     }
+                    if (stat) ++stat[1];
                     const int bt = ((sl >> 3) & 1) * 16 + (sl & 7);
                     const int nib = (int)(((X >> bt) & 1u) | (((X >> (bt + 8)) & 1u) << 1) |
                                           (((Y >> bt) & 1u) << 2) | (((Y >> (bt + 8)) & 1u) << 3));

@@ -10,7 +10,7 @@ for c in 4096,64,256,512,256 4096,64,512,512,384; do
   PRGPU_SEED_SMALL=$c timeout -k 10 300 python -u tools/seed_time.py >> gpurun_out/cs_seed.log 2>&1 || exit 1
 done
 cat gpurun_out/cs_seed.log
-for v in "win8:" "win16:PRGPU_PK_BT_WIN=16" "fused:PRGPU_PK_FUSED=1"; do
+for v in "win8:PRGPU_PK_SPLIT=1" "win16:PRGPU_PK_SPLIT=1 PRGPU_PK_BT_WIN=16" "fused:"; do
   n=${v%%:*}; e=${v#*:}
   env $e timeout -k 10 400 python -u bench.py --no-cpu-baseline --steps 3 > gpurun_out/cs_bench_$n.json 2> gpurun_out/cs_bench_$n.err || exit 1
   python -c "import json;d=json.load(open('gpurun_out/cs_bench_$n.json'));print('$n',d['value'],d['stage_ms'],d['roofline']['launch_ms'],d['cigar_kernel_phase_share'],d['seeding']['kernel_ms'],d['iteration_end_to_end_ms'])"
