@@ -614,68 +614,95 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         const int64_t np = p.occ;
         const int64_t step = np > O.max_occ ? np / O.max_occ : 1;
         int64_t fidx = 0, take = 0, count = 0;
-        for (int32_t k = h0; k < h1 && count < O.max_occ; ++k) {
-            if (S.hml[k] < slen) continue;   // text-position order: the 12-mer lists are sorted
-            const bool use = fidx == take;
-            ++fidx;
-            if (!use) continue;
-            take += step;
-            ++count;
-            SC_STAT(3, 1);
-            Seed s;
-            int rid;
-            text_to_fr(I, S.hpos[k], s.rbeg, rid);
-            s.qbeg = p.start;
-            s.len = slen;
-            // the predecessor that can merge: the last chain of the occurrence's range with
-            // pos <= rbeg (`at`, also the insertion point); occurrences at one locus mostly come
-            // in increasing rbeg, so the list's tail first
-            const int32_t key = rid * 2 + (s.rbeg >= I.l_pac ? 1 : 0);
-            const int hs = range_slot(S, key);
-            const bool found = S.hkey[hs] == key;
-            int at = -1;
-            if (found) {
-                const int tl = S.htail[hs];
-                SC_STAT(4, 1);
-                if (S.cv[tl].pos <= s.rbeg) at = tl;
-                else
-                    for (int x = S.hhead[hs]; x >= 0 && S.cv[x].pos <= s.rbeg; x = S.cnx[x]) {
-                        at = x;
-                        SC_STAT(4, 1);
-                    }
+        // the selected occurrences in batches of CB: their text positions, forward-reverse
+        // coordinates and range-table probes are independent loads, issued together (one
+        // latency per batch instead of ~5 dependent ones per occurrence); then each in order
+        constexpr int CB = 8;
+        int32_t k = h0;
+        while (k < h1 && count < O.max_occ) {
+            int32_t sel[CB];
+            int nsel = 0;
+            for (; k < h1 && count < O.max_occ && nsel < CB; ++k) {
+                if (S.hml[k] < slen) continue;   // text-position order: the 12-mer lists are sorted
+                const bool use = fidx == take;
+                ++fidx;
+                if (!use) continue;
+                take += step;
+                ++count;
+                sel[nsel++] = k;
             }
-            if (at >= 0) {
-                const int r = test_and_merge(O, I.l_pac, S, ns, S.cv[at], s, rid);
-                if (r < 0) return SC_OVER_SEEDS;
-                if (r) { SC_STAT(5, 1); continue; }
+            uint32_t hp[CB];
+            int64_t rb[CB];
+            int rd[CB], hsl[CB];
+            int32_t key[CB];
+#pragma unroll
+            for (int u = 0; u < CB; ++u) hp[u] = u < nsel ? S.hpos[sel[u]] : 0u;
+#pragma unroll
+            for (int u = 0; u < CB; ++u) {
+                rb[u] = 0, rd[u] = 0;
+                if (u < nsel) text_to_fr(I, hp[u], rb[u], rd[u]);
+                key[u] = rd[u] * 2 + (rb[u] >= I.l_pac ? 1 : 0);
             }
-            SC_STAT(6, 1);
-            if (ncv >= S.cap_chains) return SC_OVER_CHAINS;
-            if (ns >= S.cap_seeds) return SC_OVER_SEEDS;
-            S.seeds[ns] = s;
-            S.next[ns] = -1;
-            Chain c;
-            c.pos = s.rbeg;
-            c.rid = rid;
-            c.head = c.tail = ns++;
-            c.n = 1;
-            c.w = c.kept = 0;
-            c.first = -1;
-            S.cv[ncv] = c;
-            if (!found) {   // the range's first chain
-                S.hkey[hs] = key;
-                S.hhead[hs] = S.htail[hs] = ncv;
-                S.cnx[ncv] = -1;
-            } else if (at < 0) {   // before every chain of the range
-                S.cnx[ncv] = S.hhead[hs];
-                S.hhead[hs] = ncv;
-            } else {   // after `at` (and after every chain of equal pos)
-                const int nx = S.cnx[at];
-                S.cnx[ncv] = nx;
-                S.cnx[at] = ncv;
-                if (nx < 0) S.htail[hs] = ncv;
+#pragma unroll
+            for (int u = 0; u < CB; ++u) hsl[u] = u < nsel ? range_slot(S, key[u]) : 0;
+            bool opened = false;   // a range opened in this batch moves later probes: redo them
+            for (int u = 0; u < nsel; ++u) {
+                SC_STAT(3, 1);
+                Seed s;
+                s.rbeg = rb[u];
+                s.qbeg = p.start;
+                s.len = slen;
+                const int rid = rd[u];
+                // the predecessor that can merge: the last chain of the occurrence's range with
+                // pos <= rbeg (`at`, also the insertion point); occurrences at one locus mostly
+                // come in increasing rbeg, so the list's tail first
+                const int hs = opened ? range_slot(S, key[u]) : hsl[u];
+                const bool found = S.hkey[hs] == key[u];
+                int at = -1;
+                if (found) {
+                    const int tl = S.htail[hs];
+                    SC_STAT(4, 1);
+                    if (S.cv[tl].pos <= s.rbeg) at = tl;
+                    else
+                        for (int x = S.hhead[hs]; x >= 0 && S.cv[x].pos <= s.rbeg; x = S.cnx[x]) {
+                            at = x;
+                            SC_STAT(4, 1);
+                        }
+                }
+                if (at >= 0) {
+                    const int r = test_and_merge(O, I.l_pac, S, ns, S.cv[at], s, rid);
+                    if (r < 0) return SC_OVER_SEEDS;
+                    if (r) { SC_STAT(5, 1); continue; }
+                }
+                SC_STAT(6, 1);
+                if (ncv >= S.cap_chains) return SC_OVER_CHAINS;
+                if (ns >= S.cap_seeds) return SC_OVER_SEEDS;
+                S.seeds[ns] = s;
+                S.next[ns] = -1;
+                Chain c;
+                c.pos = s.rbeg;
+                c.rid = rid;
+                c.head = c.tail = ns++;
+                c.n = 1;
+                c.w = c.kept = 0;
+                c.first = -1;
+                S.cv[ncv] = c;
+                if (!found) {   // the range's first chain
+                    S.hkey[hs] = key[u];
+                    S.hhead[hs] = S.htail[hs] = ncv;
+                    S.cnx[ncv] = -1;
+                    opened = true;
+                } else if (at < 0) {   // before every chain of the range
+                    S.cnx[ncv] = S.hhead[hs];
+                    S.hhead[hs] = ncv;
+                } else {   // after `at` (and after every chain of equal pos)
+                    const int nx = S.cnx[at];
+                    S.cnx[ncv] = nx;
+                    S.cnx[at] = ncv;
+                    if (nx < 0) S.htail[hs] = ncv;
+                }
+                ++ncv;
             }
-            ++ncv;
         }
     }
     SC_TICK(1);
