@@ -202,9 +202,9 @@ __device__ __forceinline__ void walk_states(const uint32_t *cg, int cb, int ce, 
                                             int cmin, int cmax, F &&f) {
     int col = rpos0, sidx = 0, qpos = 0;
     int p_col = 0, p_sidx = 0, p_kind = -1, p_qoff = 0, p_len = 0;
-    // a rolling window of the next 8 ops: each op is loaded 8 iterations before it is used
-    // (8 loads in flight instead of one HBM latency per op; 4 measured slower)
-    constexpr int PF = 8;
+    // a rolling window of the next 4 ops: each op is loaded 4 iterations before it is used
+    // (4 loads in flight instead of one HBM latency per op; 8 measured no faster)
+    constexpr int PF = 4;
     uint32_t w[PF];
 #pragma unroll
     for (int u = 0; u < PF; ++u) w[u] = cb + u < ce ? cg[cb + u] : 0u;

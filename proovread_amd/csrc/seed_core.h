@@ -273,6 +273,8 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
 #pragma unroll
         for (int n = KI; n < 16; ++n) pre[n - 7] = S.ge[(int64_t)x * HB + (n - KI)];
     }
+    uint32_t blk[8];   // lengths 16..31: the start's count row 8 entries at a time
+    int blk0 = -1;
     for (i = x + 1; i < len; ++i) {
         if (q[i] < 4) {
             const int n = i + 1 - x;
@@ -281,6 +283,17 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
                 uint32_t v = pre[0];
 #pragma unroll
                 for (int t = 1; t < 9; ++t) v = n - 7 == t ? pre[t] : v;
+                o = v;
+            } else if (have && n >= 16 && n < KI + HB) {
+                const int b0 = n & ~7;
+                if (b0 != blk0) {
+#pragma unroll
+                    for (int t = 0; t < 8; ++t) blk[t] = S.ge[(int64_t)x * HB + (b0 - KI) + t];
+                    blk0 = b0;
+                }
+                uint32_t v = blk[0];
+#pragma unroll
+                for (int t = 1; t < 8; ++t) v = (n & 7) == t ? blk[t] : v;
                 o = v;
             } else {
                 o = occ(x, i + 1);
@@ -622,14 +635,21 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         while (k < h1 && count < O.max_occ) {
             int32_t sel[CB];
             int nsel = 0;
-            for (; k < h1 && count < O.max_occ && nsel < CB; ++k) {
-                if (S.hml[k] < slen) continue;   // text-position order: the 12-mer lists are sorted
-                const bool use = fidx == take;
-                ++fidx;
-                if (!use) continue;
-                take += step;
-                ++count;
-                sel[nsel++] = k;
+            while (k < h1 && count < O.max_occ && nsel < CB) {
+                // the start's match lengths 8 at a time (independent loads), then in order
+                uint16_t ml[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) ml[u] = k + u < h1 ? S.hml[k + u] : (uint16_t)0;
+                int u = 0;
+                for (; u < 8 && k < h1 && count < O.max_occ && nsel < CB; ++u, ++k) {
+                    if (ml[u] < slen) continue;   // text-position order: the 12-mer lists are sorted
+                    const bool use = fidx == take;
+                    ++fidx;
+                    if (!use) continue;
+                    take += step;
+                    ++count;
+                    sel[nsel++] = k;
+                }
             }
             uint32_t hp[CB];
             int64_t rb[CB];

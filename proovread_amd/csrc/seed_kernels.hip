@@ -50,7 +50,6 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
     using seedc::KI;
     using seedc::KX;
     int err = 0;
-    for (int64_t k = lane; k < (int64_t)len * HB; k += 64) S.ge[k] = 0u;
     int run = 0;
     for (int a0 = 0; a0 <= len; a0 += 64) {
         const int a = a0 + lane;
@@ -117,17 +116,25 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                 while (a + ml < len && q[a + ml] < 4 && V.text[p + ml] == q[a + ml]) ++ml;
             S.hpos[k] = p;
             S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
-            atomicAdd(&S.ge[(int64_t)a * HB + (ml - KI < HB - 1 ? ml - KI : HB - 1)], 1u);
         }
         __threadfence_block();
-        for (int a = lane; a + KI <= len; a += 64) {
-            if (S.codes[a] < 0) continue;
-            uint32_t *g = S.ge + (int64_t)a * HB;
-            uint32_t acc = 0;
-            for (int t = HB - 1; t >= 0; --t) {
-                acc += g[t];
-                g[t] = acc;
+        wave_sync_lds();
+        // the count table, a lane per start: ge[a][t] = #{hits of a with ml - KI >= t} summed
+        // directly in registers (no zeroing, no atomics, no suffix pass over HBM)
+        for (int a = lane; a < len; a += 64) {
+            uint32_t g[HB];
+#pragma unroll
+            for (int t = 0; t < HB; ++t) g[t] = 0u;
+            if (a + KI <= len && S.codes[a] >= 0) {
+                for (int h = ho[a]; h < ho[a + 1]; ++h) {
+                    const int d = (int)S.hml[h] - KI;
+#pragma unroll
+                    for (int t = 0; t < HB; ++t) g[t] += d >= t ? 1u : 0u;
+                }
             }
+            uint32_t *dst = S.ge + (int64_t)a * HB;
+#pragma unroll
+            for (int t = 0; t < HB; ++t) dst[t] = g[t];
         }
         __threadfence_block();
     }
