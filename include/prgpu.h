@@ -382,6 +382,8 @@ int pr_seed_gpu_last_ms(pr_ctx *ctx, double *ms);
 /* Diagnostics: wall-clock ticks (100 MHz) of the last pr_seed_gpu_map summed over waves:
  * [occurrence table, SMEMs + re-seeding, chaining, chain filter + output] */
 int pr_seed_gpu_phase_ticks(pr_ctx *ctx, uint64_t *ticks4);
+/* wall time of the last pr_seed_gpu_map's second pass (the reads that outgrew pass 1's slices), ms */
+int pr_seed_gpu_pass2_ms(pr_ctx *ctx, double *ms);
 /* diagnostics (tests): the device path's core and capacities run on the host */
 int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opts *o, const uint8_t *sr_seq,
                             const int64_t *sr_off, int n_sr, int n_threads, pr_seed_tasks *out, int32_t *status);

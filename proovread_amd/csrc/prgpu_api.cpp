@@ -90,7 +90,7 @@ struct pr_ctx {
     int device = 0;
     int n_cu = 256;
     hipStream_t stream = nullptr;
-    hipEvent_t ev[10] = {};   // 0-7: SW, consensus, pipeline; 8-9: seeding
+    hipEvent_t ev[11] = {};   // 0-7: SW, consensus, pipeline; 8-10: seeding
     // consensus resident batch
     DevBuf cb[CB_COUNT];
     bool cns_loaded = false;
@@ -117,7 +117,7 @@ struct pr_ctx {
     DevBuf sd[SD_COUNT];
     bool seed_loaded = false;
     seedc::IndexView seed_view{};
-    float ms_seed = 0.f;
+    float ms_seed = 0.f, ms_seed_pass2 = 0.f;
     float ms_index = 0.f;
     int64_t seed_n_text = 0, seed_n_hits = 0;
     bool iter_masked = false;
@@ -1221,6 +1221,7 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     HIPCHK(hipEventRecord(c->ev[8], s));
     int e = seed_batch_launch(K, (void *)s);
     if (e) return set_error(PR_ERR_HIP, "seed kernel: %s", hipGetErrorString((hipError_t)e));
+    HIPCHK(hipEventRecord(c->ev[10], s));
     {
         std::vector<int32_t> st1((size_t)n_sr);
         if ((rc = download(st1.data(), D[SB_STATUS], (size_t)n_sr, s))) return rc;
@@ -1249,6 +1250,8 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0.f;
     if (n_sr && hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_seed = ms;
+    c->ms_seed_pass2 = 0.f;
+    if (n_sr && hipEventElapsedTime(&ms, c->ev[10], c->ev[9]) == hipSuccess) c->ms_seed_pass2 = ms;
     if (getenv("PRGPU_SEED_DEBUG") && K.prof) {   // pass 1's lane phase split (lane-summed ticks)
         unsigned long long t8[8] = {};
         if (hipMemcpy(t8, K.prof, sizeof t8, hipMemcpyDeviceToHost) == hipSuccess)
@@ -1299,6 +1302,12 @@ extern "C" int pr_seed_gpu_pass2_reads(pr_ctx *c, int64_t *n) {
 extern "C" int pr_seed_gpu_last_ms(pr_ctx *c, double *ms) {
     if (!c || !ms) return set_error(PR_ERR_ARG, "null arg");
     *ms = c->ms_seed;
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_pass2_ms(pr_ctx *c, double *ms) {
+    if (!c || !ms) return set_error(PR_ERR_ARG, "null arg");
+    *ms = c->ms_seed_pass2;   // from pass 1's end to pass 2's (its status download included)
     return 0;
 }
 

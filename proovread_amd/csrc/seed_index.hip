@@ -74,17 +74,31 @@ __global__ void ix_keys_kernel(const uint8_t *text, int64_t n, uint32_t *key, ui
     if (ok) atomicAdd(&kc[code], 1u);
 }
 
+// the KX bases after every hit: the 9 dwords around them loaded at once (independent loads
+// from a random text position; the buffer's 64-byte slack covers the end), aligned with
+// v_alignbyte, then the run up to the first N / separator / text end packed in registers
+// (round 2: one dependent byte load per base, 41 ms at configs[1])
 __global__ void ix_kext_kernel(const uint8_t *text, int64_t n, const uint32_t *kpos, const uint32_t *koff,
                                uint64_t *kext) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= (int64_t)koff[NK]) return;   // the hits: the sorted pairs with a valid key
     const int64_t p = (int64_t)kpos[r] + KI;
+    const uint32_t *tw = reinterpret_cast<const uint32_t *>(text) + (p >> 2);
+    const uint32_t sh = (uint32_t)(p & 3);
+    uint32_t w[9];
+#pragma unroll
+    for (int u = 0; u < 9; ++u) w[u] = tw[u];
+    uint32_t x[7];
+#pragma unroll
+    for (int u = 0; u < 7; ++u) x[u] = __builtin_amdgcn_alignbyte(w[u + 1], w[u], sh);
+    const int lim = n - p < KX ? (int)(n - p) : KX;
     uint64_t v = 0;
-    int m = 0;
-    for (; m < KX && p + m < n; ++m) {
-        const uint8_t c = text[p + m];
-        if (c > 3) break;
-        v |= (uint64_t)c << (2 * m);
+    int m = KX;
+#pragma unroll
+    for (int j = 0; j < KX; ++j) {
+        const uint32_t c = (x[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+        if (m == KX && (j >= lim || c > 3u)) m = j;
+        if (m == KX) v |= (uint64_t)c << (2 * j);
     }
     kext[r] = v | ((uint64_t)m << 56);
 }

@@ -59,6 +59,7 @@ def _setup(L):
     L.pr_seed_gpu_index_digest.argtypes = [C.c_void_p, C.c_void_p]
     L.pr_seed_gpu_index_last_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     L.pr_seed_gpu_phase_ticks.argtypes = [C.c_void_p, C.c_void_p]
+    L.pr_seed_gpu_pass2_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     L.pr_seed_gpu_pass2_reads.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     _done = True
 
@@ -188,6 +189,9 @@ def _phase_ms(L, ctx) -> dict:
     out = {k: round(float(v) / 1e5, 1) for k, v in
            zip(("occ_table", "lane_phase_and_pass2_smems", "pass2_chaining", "pass2_filter_out"), t)}
     out["pass2_reads"] = n2.value
+    p2 = C.c_double()
+    _abi.check(L.pr_seed_gpu_pass2_ms(ctx.h, C.byref(p2)), "pr_seed_gpu_pass2_ms")
+    out["pass2_wall_ms"] = round(p2.value, 1)
     return out
 
 

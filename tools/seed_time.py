@@ -21,7 +21,7 @@ def main():
         t = time.perf_counter()
         tasks, _ = ix.map(d.sr_seq, d.sr_off, o)
         wall = time.perf_counter() - t
-    print(json.dumps({"waves_per_cu": os.environ.get("PRGPU_SEED_WAVES_PER_CU"), "reads": d.n_sr,
+    print(json.dumps({"waves_per_cu": os.environ.get("PRGPU_SEED_WAVES_PER_CU"), "reads": d.n_sr, "index_ms": round(ix.build_ms(), 1),
                       "seeds": int(len(tasks)), "kernel_ms": round(ix.gpu_ms(), 1), "map_wall_s": round(wall, 3),
                       "phases": ix.phase_ms()}), flush=True)
 
