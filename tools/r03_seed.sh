@@ -1,4 +1,5 @@
-# seeding changes: GPU = oracle tests, then the seeding time at configs[1]
+# seeding changes: GPU = oracle tests, the seeding time at configs[1] (heavy queue / separate pass 2),
+# then the bench (its seeding parity check against the host path)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -6,5 +7,9 @@ T=${TAG:-seed}
 timeout -k 10 600 python -u -m pytest tests/test_seed_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/${T}_test.log 2>&1
 rc=$?; tail -2 gpurun_out/${T}_test.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/seed_time.py > gpurun_out/${T}_seed.log 2>&1 || exit 1
+PRGPU_SEED_DEBUG=1 timeout -k 10 300 python -u tools/seed_time.py > gpurun_out/${T}_seed.log 2>&1 || exit 1
+PRGPU_SEED_PASS2=1 timeout -k 10 300 python -u tools/seed_time.py >> gpurun_out/${T}_seed.log 2>&1 || exit 1
 cat gpurun_out/${T}_seed.log
+[ -n "$NOBENCH" ] && exit 0
+timeout -k 10 400 python -u bench.py --no-cpu-baseline --steps 3 > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || exit 1
+python -c "import json;d=json.load(open('gpurun_out/${T}_bench.json'));print(d['value'],d['stage_ms'],d['seeding']['kernel_ms'],d['seeding']['parity_vs_host'],d['seeding']['index_kernel_ms'],d['iteration_end_to_end_ms'])"
