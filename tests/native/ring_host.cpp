@@ -109,9 +109,10 @@ extern "C" int pk_global(int a, int b, int o_del, int e_del, int o_ins, int e_in
 // ksw_extend2 for a lane pair in the packed kernel's arithmetic (sw_pk.h ext_pk):
 // two tasks with the same query length and band; out[12] = (score, qle, tle, gtle,
 // gscore, max_off) per half; returns the N flags.
-extern "C" int pk_extend(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int zdrop, int qlen, int w,
-                         const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb,
-                         const uint8_t *tb, int h0a, int h0b, int nrow_min, int *out) {
+template <bool SMALLH>
+static int pk_extend_t(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int zdrop, int qlen, int w,
+                       const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb,
+                       const uint8_t *tb, int h0a, int h0b, int nrow_min, int *out) {
     SwOptsDev O{};
     O.a = a; O.b = b; O.o_del = o_del; O.e_del = e_del; O.o_ins = o_ins; O.e_ins = e_ins; O.zdrop = zdrop;
     uint32_t m[2][2 * PK_NQW];
@@ -122,10 +123,23 @@ extern "C" int pk_extend(int a, int b, int o_del, int e_del, int o_ins, int e_in
     int nrow = tla > tlb ? tla : tlb;
     if (nrow < nrow_min) nrow = nrow_min;
     PkExtOut o[2];
-    ext_pk<40>(A, B, qlen, w, nrow, O, m[0], m[1], 1, o, nflag);
+    ext_pk<40, SMALLH>(A, B, qlen, w, nrow, O, m[0], m[1], 1, o, nflag);
     for (int h = 0; h < 2; ++h) {
         out[6 * h + 0] = o[h].score; out[6 * h + 1] = o[h].qle; out[6 * h + 2] = o[h].tle;
         out[6 * h + 3] = o[h].gtle; out[6 * h + 4] = o[h].gscore; out[6 * h + 5] = o[h].max_off;
     }
     return nflag;
+}
+extern "C" int pk_extend(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int zdrop, int qlen, int w,
+                         const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb,
+                         const uint8_t *tb, int h0a, int h0b, int nrow_min, int *out) {
+    return pk_extend_t<false>(a, b, o_del, e_del, o_ins, e_ins, zdrop, qlen, w, qa, qb, tla, ta, tlb, tb, h0a, h0b,
+                              nrow_min, out);
+}
+// the one-accumulator row maximum (every H <= 511)
+extern "C" int pk_extend_small(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int zdrop, int qlen, int w,
+                               const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb,
+                               const uint8_t *tb, int h0a, int h0b, int nrow_min, int *out) {
+    return pk_extend_t<true>(a, b, o_del, e_del, o_ins, e_ins, zdrop, qlen, w, qa, qb, tla, ta, tlb, tb, h0a, h0b,
+                             nrow_min, out);
 }

@@ -154,6 +154,42 @@ def _band_w(lq, a, od, ed, oi, ei, eb, w):
     return min(w, mi, md)
 
 
+@pytest.mark.parametrize("seed", [51, 52])
+def test_extend_pk_small_h_matches_oracle(ring, seed):
+    """The packed extension's one-accumulator row maximum (SMALLH: h * 128 + slot in one
+    unsigned 16-bit max, used when a x read length <= 511) vs oracle osw_extend, on tasks whose
+    start score + a x query length stays <= 511 (bwa-sr: 150 bp reads, a = 1)."""
+    rng = random.Random(seed)
+    n = 0
+    for _ in range(200):
+        L = rng.choice([1, 2, 5, 10, 20, 40, 60, 75, 100, 150])
+        qs = ["".join(rng.choice("ACGT") for _ in range(L)) for _ in range(2)]
+        ts = []
+        for q in qs:
+            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])).replace("N", "C") + \
+                "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 60)))
+            if rng.random() < 0.2:
+                t = "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 200)))
+            ts.append(t[:300])
+        eb = rng.choice([30, 0, 5])
+        for a, b, od, ed, oi, ei, zd in SCORING:
+            if a * L > 511:
+                continue
+            h0s = [rng.randint(0, 511 - a * L) for _ in range(2)]
+            w = _band_w(L, a, od, ed, oi, ei, eb, 40)
+            out = (C.c_int * 12)()
+            fl = ring.pk_extend_small(a, b, od, ed, oi, ei, zd, L, w, _nt4(qs[0]), _nt4(qs[1]), len(ts[0]),
+                                      _nt4(ts[0] or "A"), len(ts[1]), _nt4(ts[1] or "A"), h0s[0], h0s[1],
+                                      rng.choice([0, 300]), out)
+            assert fl == 0
+            for h in range(2):
+                sc, outs = ob.sw_extend(qs[h], ts[h], h0s[h], w=w, a=a, b=b, o_del=od, e_del=ed, o_ins=oi,
+                                        e_ins=ei, end_bonus=eb, zdrop=zd)
+                assert list(out[6 * h:6 * h + 6]) == [sc] + list(outs), (h, qs[h], ts[h], w, h0s[h], eb)
+                n += 1
+    assert n > 500
+
+
 @pytest.mark.parametrize("seed", [41, 42, 43])
 def test_extend_pk_matches_oracle(ring, seed):
     """ksw_extend2 of the packed two-tasks-per-lane kernel (sw_pk.h ext_pk), host
