@@ -328,7 +328,7 @@ __device__ __forceinline__ int band_w(const SwOptsDev &O, int w, int qlen, int e
 // wave k takes the 128-task segment of one side query length (so qlen and the
 // capped band are wave-uniform); lane l runs list[128k + l] and list[128k + 64 + l].
 // Tasks that meet an N are flagged (x_try bit 3 + side) for sw_ext_phase_kernel.
-template <int WB>
+template <int WB, bool SMALLH>
 __global__ void __launch_bounds__(SW_WAVE, 2) sw_ext_pk_kernel(SwDev D, SwOptsDev O, int side) {
     __shared__ __attribute__((aligned(16))) uint32_t lm[2 * 2 * PK_NQW * SW_WAVE];
     const int lane = threadIdx.x;
@@ -372,7 +372,7 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_ext_pk_kernel(SwDev D, SwOptsDe
         }
         nrow = __builtin_amdgcn_readfirstlane(nrow);
         PkExtOut out[2];
-        ext_pk<WB>(H[0], H[1], qlen, w, nrow, O, lm + lane, lm + 2 * PK_NQW * SW_WAVE + lane, SW_WAVE, out, nflag);
+        ext_pk<WB, SMALLH>(H[0], H[1], qlen, w, nrow, O, lm + lane, lm + 2 * PK_NQW * SW_WAVE + lane, SW_WAVE, out, nflag);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int64_t t = tt[h];
@@ -1265,7 +1265,11 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
                 int rc = sw_launch_pk_order(D, O, 1 + side, stream);
                 if (rc) return rc;
                 mark();
-                hipLaunchKernelGGL(sw_ext_pk_kernel<40>, dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, side);
+                // every DP value <= a x read length: the one-accumulator row maximum when that fits 9 bits
+                if ((long)O.a * D.qmax <= 511)
+                    hipLaunchKernelGGL((sw_ext_pk_kernel<40, true>), dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, side);
+                else
+                    hipLaunchKernelGGL((sw_ext_pk_kernel<40, false>), dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, side);
                 mark();
                 if ((e = hipGetLastError()) != hipSuccess) return (int)e;
             }

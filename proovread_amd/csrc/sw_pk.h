@@ -58,6 +58,10 @@ SW_RING_FN uint32_t pk_add(uint32_t a, uint32_t b) { return PU(PV(a) + PV(b)); }
 SW_RING_FN uint32_t pk_sub(uint32_t a, uint32_t b) { return PU(PV(a) - PV(b)); }
 SW_RING_FN uint32_t pk_max(uint32_t a, uint32_t b) { return PU(__builtin_elementwise_max(PV(a), PV(b))); }
 SW_RING_FN uint32_t pk_min(uint32_t a, uint32_t b) { return PU(__builtin_elementwise_min(PV(a), PV(b))); }
+SW_RING_FN uint32_t pk_maxu(uint32_t a, uint32_t b) {
+    typedef unsigned short pu_v __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(pu_v, a), __builtin_bit_cast(pu_v, b)));
+}
 SW_RING_FN uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) { return PU(PV(a) * PV(b) + PV(c)); }
 SW_RING_FN uint32_t pk_shl(uint32_t a, int k) { return PU(PV(a) << pk_v{(short)k, (short)k}); }
 SW_RING_FN uint32_t pk_asr15(uint32_t a) { return PU(PV(a) >> pk_v{15, 15}); }
@@ -82,6 +86,10 @@ SW_RING_FN uint32_t pk_min(uint32_t a, uint32_t b) {
 }
 SW_RING_FN uint32_t pk_mad(uint32_t a, uint32_t b, uint32_t c) {
     return pk_mk(pk_lo(a) * pk_lo(b) + pk_lo(c), pk_hi(a) * pk_hi(b) + pk_hi(c));
+}
+SW_RING_FN uint32_t pk_maxu(uint32_t a, uint32_t b) {
+    const uint32_t al = a & 0xFFFFu, bl = b & 0xFFFFu, ah = a >> 16, bh = b >> 16;
+    return (al > bl ? al : bl) | ((ah > bh ? ah : bh) << 16);
 }
 SW_RING_FN uint32_t pk_shl(uint32_t a, int k) { return pk_mk((uint16_t)(a << k), (uint16_t)((a >> 16) << k)); }
 SW_RING_FN uint32_t pk_asr15(uint32_t a) { return pk_mk(pk_lo(a) >> 15, pk_hi(a) >> 15); }
@@ -340,13 +348,17 @@ struct PkExtOut {
     int score, qle, tle, gtle, gscore, max_off;
 };
 
-template <int WB>
+// SMALLH (every H <= 511: a x read length <= 511): the row maximum and its last slot as one
+// packed unsigned max of h * 128 + s instead of one h * 16 + (s & 15) per 16-slot group (one
+// accumulator, no per-row reduction over the groups)
+template <int WB, bool SMALLH = false>
 SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, int nrows, const SwOptsDev &O,
                        const uint32_t *mA, const uint32_t *mB, int MS, PkExtOut out[2], int &nflag) {
     constexpr int NS = 2 * WB + 2;
     constexpr int CH = 8;
     constexpr int NCH = (NS + CH - 1) / CH;
-    constexpr int NG = (NS + 15) / 16;
+    constexpr int NG = SMALLH ? 1 : (NS + 15) / 16;
+    static_assert(!SMALLH || NS <= 128, "slot index in 7 bits");
     const int b = O.b, oe_del = O.o_del + O.e_del, oe_ins = O.o_ins + O.e_ins;
     const uint32_t NAB = pk_dup(-(O.a + b)), BD = pk_dup(b);
     const uint32_t cOD = pk_dup(oe_del), cED = pk_dup(O.e_del), cOI = pk_dup(oe_ins), cEI = pk_dup(O.e_ins);
@@ -457,7 +469,8 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
                 RH[s] = bfi_b32v(gt, Hd, h1);
                 RE[s] = bfi_b32v(gt, e0, bfi_b32v(ge, 0u, en));
                 const uint32_t hm = bfi_b32v(ge, 0u, h);
-                gm[s >> 4] = pk_max(gm[s >> 4], pk_mad(hm, pk_dup(16), pk_dup(s & 15)));
+                if (SMALLH) gm[0] = pk_maxu(gm[0], pk_mad(hm, pk_dup(128), pk_dup(s)));
+                else gm[s >> 4] = pk_max(gm[s >> 4], pk_mad(hm, pk_dup(16), pk_dup(s & 15)));
                 lp = pk_max(lp, pk_mad(pk_min(hm, pk_dup(1)), pk_dup(s + 1), 0u));
                 h1 = h;
                 f = fn;
@@ -485,11 +498,16 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
                 gscore[h] = gscore[h] > v ? gscore[h] : v;
             }
             int best = -1;
+            if (SMALLH) {
+                const int kv = (int)((gm[0] >> (16 * h)) & 0xFFFFu);
+                best = ((kv >> 7) << 8) | (kv & 127);
+            } else {
 #pragma unroll
-            for (int g = 0; g < NG; ++g) {
-                const int kv = (int)((gm[g] >> (16 * h)) & 0xFFFFu);
-                const int cand = ((kv >> 4) << 8) | (g * 16 + (kv & 15));
-                best = best > cand ? best : cand;
+                for (int g = 0; g < NG; ++g) {
+                    const int kv = (int)((gm[g] >> (16 * h)) & 0xFFFFu);
+                    const int cand = ((kv >> 4) << 8) | (g * 16 + (kv & 15));
+                    best = best > cand ? best : cand;
+                }
             }
             const int m = best >> 8;
             if (m == 0) {

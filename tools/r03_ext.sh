@@ -1,0 +1,10 @@
+# extension kernel change: SW parity tests, then the bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+T=${TAG:-ext}
+timeout -k 10 600 python -u -m pytest tests/test_sw_gpu.py tests/test_sw_edge_gpu.py tests/test_iter_gpu.py tests/test_aln_gpu.py \
+  -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/${T}_test.log 2>&1
+rc=$?; tail -2 gpurun_out/${T}_test.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 400 python -u bench.py --no-cpu-baseline --steps 3 > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || exit 1
+python -c "import json;d=json.load(open('gpurun_out/${T}_bench.json'));print(d['value'],d['stage_ms'],d['roofline_extension']['summed_launch_ms'],d['roofline_extension']['frac'])"
