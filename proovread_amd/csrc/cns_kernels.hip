@@ -412,7 +412,7 @@ struct CnsGeo {
     static constexpr int B_WKEY = B_BEST + 8 * W;           // u32 [WCAP]
     static constexpr int B_WCNT = B_WKEY + 4 * WCAP;        // u32 [WCAP]
     static constexpr int B_IGN = B_WCNT + 4 * WCAP;         // u32 [W/32] ignored columns (MCR ranges)
-    static constexpr int WAVE_BYTES = 64 * 16 + 64 * 4;     // per wave: op table int4[64], SEQ dwords u32[64]
+    static constexpr int WAVE_BYTES = 64 * 16 + 128 * 4;    // per wave (two 32-lane halves): op tables int4[2][32], SEQ dwords u32[2][64]
     static constexpr int B_WAVE = (B_IGN + W / 8 + 15) & ~15;
     static constexpr int SZ_WIN = B_WAVE + (CNS_THREADS / 64) * WAVE_BYTES;
     static constexpr int SZ_CHIM = (CHIM_MAXCOLS * 13 + CHIM_TCAP * 4 + 16) * 4;
@@ -594,15 +594,14 @@ __device__ __forceinline__ int wave_append(int *ctr) {
 }
 
 // ---------------------------------------------------------------------------
-// inclusive prefix sum over the 64 lanes of a wave with DPP moves (no LDS crossbar): row
-// shifts 1, 2, 4, 8 scan each row of 16 lanes, row_bcast:15 / :31 carry the row totals on
-__device__ __forceinline__ int wave_incl_scan(int v) {
+// inclusive prefix sum over each 32-lane half of the wave (row shifts 1, 2, 4, 8 scan the rows
+// of 16, row_bcast:15 carries row 0's total into row 1 and row 2's into row 3)
+__device__ __forceinline__ int half_incl_scan(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
     v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
     v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
     v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
-    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
     return v;
 }
 
@@ -613,48 +612,54 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+constexpr int CNS_GW = 32;   // lanes per kept alignment in the pileup: two alignments per wave
+
 // One kept alignment's states inside the window [cmin, cmax) (walk_states' semantics,
-// Seq.pm:396-461) by one wave, op-parallel: lane k takes CIGAR op k (chunks of 64 ops; c_first:
-// this lane's op of the first chunk, loaded ahead by the caller) and wave scans give every op
-// its first column and SEQ position (q0 = the SEQ position of the first kept base).  An op
-// that owns columns (M / D with n > 0, a leading I: one column) ends in a deferred state: when
-// insertions follow it (zero-length ops skipped), or for a leading I, that last column holds
-// a multi-character state -- base + inserted bases; after a D the inserted bases replace '-'
-// (a single inserted base is then a one-character state) -- emitted by the op's own lane as
-// special(column, SEQ position, length).  Every other column is a single-base or '-' state,
-// visited as column(column, SEQ position or -1 for '-'): each lane takes a contiguous block
-// of the chunk's columns, finds the first one's op by a binary search over the chunk's op
-// starts (ops: the wave's LDS table, 64 int4) and walks on from there.
+// Seq.pm:396-461) by one 32-lane half of a wave, op-parallel: lane k of the half takes CIGAR op
+// k (chunks of 32 ops; c_first0 / c_first1: this lane's ops of the first two chunks, loaded
+// ahead by the caller) and half-wave scans give every op its first column and SEQ position
+// (q0 = the SEQ position of the first kept base).  An op that owns columns (M / D with n > 0,
+// a leading I: one column) ends in a deferred state: when insertions follow it (zero-length
+// ops skipped), or for a leading I, that last column holds a multi-character state -- base +
+// inserted bases; after a D the inserted bases replace '-' (a single inserted base is then a
+// one-character state) -- emitted by the op's own lane as special(column, SEQ position,
+// length).  Every other column is a single-base or '-' state, visited as column(column, SEQ
+// position or -1 for '-'): each lane takes a contiguous block of the chunk's columns, finds
+// the first one's op by a binary search over the chunk's op starts (ops: the half's LDS
+// table, 32 int4) and walks on from there.  The two halves of a wave run their own
+// alignments (their loops may differ in length: every cross-lane step stays in the half).
 template <class FS, class FC>
-__device__ __forceinline__ void wave_states(const uint32_t *cg, int nop, int rp, int q0, int cmin, int cmax, int4 *ops,
-                                            uint32_t c_first, FS &&special, FC &&column) {
+__device__ __forceinline__ void group_states(const uint32_t *cg, int nop, int rp, int q0, int cmin, int cmax, int4 *ops,
+                                             uint32_t c_first0, uint32_t c_first1, FS &&special, FC &&column) {
+    constexpr int GW = CNS_GW;
     const int lane = (int)__lane_id();
+    const int gl = lane & (GW - 1), glast = (lane & ~(GW - 1)) + GW - 1;
     int col0 = rp, qb = q0;
-    for (int k0 = 0; k0 < nop && col0 < cmax; k0 += 64) {
-        const int k = k0 + lane;
+    for (int k0 = 0; k0 < nop && col0 < cmax; k0 += GW) {
+        const int k = k0 + gl;
         const bool valid = k < nop;
-        const uint32_t c = k0 == 0 ? c_first : (valid ? cg[k] : 0u);
+        const uint32_t c = k0 == 0 ? c_first0 : (k0 == GW ? c_first1 : (valid ? cg[k] : 0u));
         const int n = (int)(c >> 4), code = (int)(c & 15u);
         const bool lead = k == 0 && code == 1;
         const int ncol = !valid ? 0 : (code == 0 || code == 2) ? n : (lead ? 1 : 0);
         const int qadv = valid && (code == 0 || code == 1) ? n : 0;
-        const uint32_t nx1 = __shfl_down(c, 1, 64), nx2 = __shfl_down(c, 2, 64);
-        const int sc = wave_incl_scan(ncol), sq = wave_incl_scan(qadv);
+        const uint32_t nx1 = __shfl_down(c, 1, GW), nx2 = __shfl_down(c, 2, GW);
+        const int sc = half_incl_scan(ncol), sq = half_incl_scan(qadv);
         // inserted bases right after an op that owns columns (zero-length ops skipped)
         int tot = 0;
         if (ncol > 0 && k + 1 < nop) {
-            const uint32_t x1 = lane <= 62 ? nx1 : cg[k + 1];
+            const uint32_t x1 = gl <= GW - 2 ? nx1 : cg[k + 1];
             if ((x1 & 15u) == 1u || (x1 >> 4) == 0u) {
                 tot = (x1 & 15u) == 1u ? (int)(x1 >> 4) : 0;
                 for (int j = k + 2; j < nop; ++j) {
-                    const uint32_t x2 = (j == k + 2 && lane <= 61) ? nx2 : cg[j];
+                    const uint32_t x2 = (j == k + 2 && gl <= GW - 3) ? nx2 : cg[j];
                     if ((x2 & 15u) == 1u) tot += (int)(x2 >> 4);
                     else if ((x2 >> 4) != 0u) break;
                 }
             }
         }
         const int cs = col0 + sc - ncol, qs = qb + sq - qadv;
-        const int ctot = __builtin_amdgcn_readlane(sc, 63), qtot = __builtin_amdgcn_readlane(sq, 63);
+        const int ctot = __shfl(sc, glast, 64), qtot = __shfl(sq, glast, 64);
         int scol = -1;
         if (ncol > 0 && (tot > 0 || lead)) {
             int sqp, slen;
@@ -663,13 +668,13 @@ __device__ __forceinline__ void wave_states(const uint32_t *cg, int nop, int rp,
             else { scol = cs + n - 1; sqp = qs; slen = tot; }   // D + I: the insertion replaces '-'
             if (scol >= cmin && scol < cmax) special(scol, sqp, slen);
         }
-        ops[lane] = make_int4(valid ? cs : 0x7fffffff, qs, code == 2 ? 1 : 0, scol);
+        ops[gl] = make_int4(valid ? cs : 0x7fffffff, qs, code == 2 ? 1 : 0, scol);
         wave_sync();
         const int cA = col0 > cmin ? col0 : cmin, cB = col0 + ctot < cmax ? col0 + ctot : cmax;
-        const int nv = nop - k0 < 64 ? nop - k0 : 64;
+        const int nv = nop - k0 < GW ? nop - k0 : GW;
         if (cB > cA) {
-            const int per = (cB - cA + 63) >> 6;
-            int cc = cA + lane * per;
+            const int per = (cB - cA + GW - 1) / GW;
+            int cc = cA + gl * per;
             const int ce_ = cc + per < cB ? cc + per : cB;
             if (cc < ce_) {
                 int lo = 0, hi = nv - 1;   // the last op starting at or before cc owns it
@@ -989,35 +994,47 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             CNS_TICK(8);
             if (D.prof && tid == 0) pt[14] += 1;
             const int cw0 = (int)w0, cw1 = (int)w0 + wn;
-            // the wave's candidates kb + wv + NWAVE j, software-pipelined: the next one's first 64
-            // CIGAR ops and SEQ dwords, and the K entry of the one after it, are in flight while
-            // the current one is processed
-            // a K entry (12 ints) is held spread over lanes 0..11 of one register and read back
-            // into scalar registers when used (v_readlane): the pipeline costs 2 VGPRs, not 24
+            // two candidate streams per wave, one per 32-lane half (stream wv * 2 + g takes the
+            // candidates kb + stream + 2 NWAVE j), software-pipelined: the next candidate's first 64
+            // CIGAR ops and SEQ dwords (two per lane), and the K entry of the one after it, are in
+            // flight while the current one is processed.  A K entry (12 ints) is held spread over
+            // lanes 0..11 of its half in one register and read back with v_readlane.
+            const int g = lane >> 5, gl = lane & 31;
+            const int stream = wv * 2 + g;
+            constexpr int NSTREAM = 2 * NWAVE;
+            int4 *gops = wops + g * CNS_GW;
+            uint32_t *gseq = wseq + g * 64;
             const int32_t *Ki = reinterpret_cast<const int32_t *>(K);
             auto ldK = [&](int kk) -> int32_t {
-                return kk < ke ? (lane < 12 ? Ki[12 * (int64_t)kk + lane] : 0) : (lane == 0 ? 0x7fffffff : 0);
+                return kk < ke ? (gl < 12 ? Ki[12 * (int64_t)kk + gl] : 0) : (gl == 0 ? 0x7fffffff : 0);
             };
-            auto fld = [](int32_t kv, int f) -> int32_t { return __builtin_amdgcn_readlane(kv, f); };
+            auto fld = [g](int32_t kv, int f) -> int32_t {
+                const int32_t a0 = __builtin_amdgcn_readlane(kv, f), a1 = __builtin_amdgcn_readlane(kv, 32 + f);
+                return g ? a1 : a0;
+            };
             auto overl = [&](int32_t kv) { return fld(kv, 0) < cw1 && fld(kv, 1) > cw0; };   // overlaps the window
-            auto ldD = [&](int32_t kv, uint32_t &opv, uint32_t &dwv) {
-                opv = 0u;
-                dwv = 0u;
+            auto ldD = [&](int32_t kv, uint32_t &op0, uint32_t &op1, uint32_t &dw0, uint32_t &dw1) {
+                op0 = op1 = dw0 = dw1 = 0u;
                 if (!overl(kv)) return;
                 const int64_t so = (int64_t)(uint32_t)fld(kv, 6) | ((int64_t)fld(kv, 7) << 32);
                 const int64_t cgi = (int64_t)(uint32_t)fld(kv, 8) | ((int64_t)fld(kv, 9) << 32);
-                if (lane < fld(kv, 4)) opv = D.cig[cgi + lane];
+                const int nop = fld(kv, 4);
+                if (gl < nop) op0 = D.cig[cgi + gl];
+                if (gl + CNS_GW < nop) op1 = D.cig[cgi + CNS_GW + gl];
                 const int ndw = ((int)(so & 3) + (fld(kv, 2) & 0x7FFFFFFF) + 3) >> 2;
-                if (ndw <= 64 && lane < ndw) dwv = gdw[(so >> 2) + lane];
+                if (ndw <= 64) {
+                    if (gl < ndw) dw0 = gdw[(so >> 2) + gl];
+                    if (gl + 32 < ndw) dw1 = gdw[(so >> 2) + 32 + gl];
+                }
             };
-            int32_t ckv = ldK(kb + wv), nkv;
-            uint32_t cop, cdw;
-            ldD(ckv, cop, cdw);
-            nkv = ldK(kb + wv + NWAVE);
-            for (int kk = kb + wv; kk < ke; kk += NWAVE) {
-                uint32_t nop_, ndw_;
-                ldD(nkv, nop_, ndw_);
-                const int32_t mkv = ldK(kk + 2 * NWAVE);
+            int32_t ckv = ldK(kb + stream), nkv;
+            uint32_t cop0, cop1, cdw0, cdw1;
+            ldD(ckv, cop0, cop1, cdw0, cdw1);
+            nkv = ldK(kb + stream + NSTREAM);
+            for (int kk = kb + stream; kk < ke; kk += NSTREAM) {
+                uint32_t nop0, nop1, ndw0, ndw1;
+                ldD(nkv, nop0, nop1, ndw0, ndw1);
+                const int32_t mkv = ldK(kk + 2 * NSTREAM);
                 if (overl(ckv)) {
                     const int rp = fld(ckv, 0), e0z = fld(ckv, 2), sb = fld(ckv, 3), nop = fld(ckv, 4);
                     const int ls = e0z & 0x7FFFFFFF;
@@ -1026,10 +1043,13 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                     const int64_t cgi = (int64_t)(uint32_t)fld(ckv, 8) | ((int64_t)fld(ckv, 9) << 32);
                     const int head = (int)(so & 3);
                     const int ndw = (head + ls + 3) >> 2;
-                    // the alignment's SEQ in the wave's LDS area (loaded ahead), when it fits
+                    // the alignment's SEQ in the half's LDS area (loaded ahead), when it fits
                     const bool fast = ndw <= 64;
-                    if (fast) wseq[lane] = cdw;
-                    const uint8_t *sl = reinterpret_cast<const uint8_t *>(wseq) + head;
+                    if (fast) {
+                        gseq[gl] = cdw0;
+                        gseq[gl + 32] = cdw1;
+                    }
+                    const uint8_t *sl = reinterpret_cast<const uint8_t *>(gseq) + head;
                     SeqV sv;   // (the insertion states' keys; the slow path's bases)
                     sv.p = fast ? sl : D.seq + so;
                     sv.n = ls;
@@ -1050,21 +1070,23 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                         atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
                     };
                     wave_sync();
-                    wave_states(D.cig + cgi, nop, rp, sb, cw0, cw1, wops, cop,
-                                [&](int scol, int sqp, int slen) {
-                                    if (slen == 1) { add_fixed(scol, fixed_at(sqp)); return; }
-                                    const int c = scol - cw0;
-                                    if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
-                                    const int h = T.find(state_key(sv, sqp, slen));
-                                    if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
-                                        C->flag = 1;
-                                },
-                                [&](int cc, int qp) { add_fixed(cc, qp < 0 ? 4 : fixed_at(qp)); });
+                    group_states(D.cig + cgi, nop, rp, sb, cw0, cw1, gops, cop0, cop1,
+                                 [&](int scol, int sqp, int slen) {
+                                     if (slen == 1) { add_fixed(scol, fixed_at(sqp)); return; }
+                                     const int c = scol - cw0;
+                                     if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
+                                     const int h = T.find(state_key(sv, sqp, slen));
+                                     if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
+                                         C->flag = 1;
+                                 },
+                                 [&](int cc, int qp) { add_fixed(cc, qp < 0 ? 4 : fixed_at(qp)); });
                 }
                 ckv = nkv;
                 nkv = mkv;
-                cop = nop_;
-                cdw = ndw_;
+                cop0 = nop0;
+                cop1 = nop1;
+                cdw0 = ndw0;
+                cdw1 = ndw1;
             }
             __syncthreads();
             CNS_TICK(3);
