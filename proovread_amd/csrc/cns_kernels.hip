@@ -395,6 +395,16 @@ __device__ void prep_alignment(const CnsDev &D, const CnsParamsDev &P, int64_t g
 constexpr int SLOT_SH = 12;                 // window / chimera keys: (column + 1) << 12 | state slot
 constexpr uint32_t SLOT_MASK = (1u << SLOT_SH) - 1u;
 
+// the pileup: kept alignments processed by groups of CNS_GW lanes, CNS_NG per wave
+#ifndef CNS_GW_DEF
+#define CNS_GW_DEF 16
+#endif
+constexpr int CNS_GW = CNS_GW_DEF;   // lanes per kept alignment in the pileup (16: four per wave)
+constexpr int CNS_NG = 64 / CNS_GW;  // alignments per wave
+constexpr int CNS_OPF = CNS_GW == 16 ? 3 : 2;                 // CIGAR ops per lane loaded ahead (48 / 64 ops)
+constexpr int CNS_SEQ_DW = CNS_GW == 16 ? 40 : 64;            // SEQ dwords a group keeps in LDS (160 / 256 bytes)
+constexpr int CNS_SEQ_PL = (CNS_SEQ_DW + CNS_GW - 1) / CNS_GW; // of them per lane
+
 template <int TCAP_, int W_, int WCAP_, int WGCU_, bool RETRY_>
 struct CnsGeo {
     static constexpr int TCAP = TCAP_;      // distinct insertion states per read
@@ -412,7 +422,7 @@ struct CnsGeo {
     static constexpr int B_WKEY = B_BEST + 8 * W;           // u32 [WCAP]
     static constexpr int B_WCNT = B_WKEY + 4 * WCAP;        // u32 [WCAP]
     static constexpr int B_IGN = B_WCNT + 4 * WCAP;         // u32 [W/32] ignored columns (MCR ranges)
-    static constexpr int WAVE_BYTES = 64 * 16 + 128 * 4;    // per wave (two 32-lane halves): op tables int4[2][32], SEQ dwords u32[2][64]
+    static constexpr int WAVE_BYTES = 64 * 16 + (64 / CNS_GW) * CNS_SEQ_DW * 4;   // per wave: op tables int4[NG][GW], SEQ dwords u32[NG][SEQ_DW]
     static constexpr int B_WAVE = (B_IGN + W / 8 + 15) & ~15;
     static constexpr int SZ_WIN = B_WAVE + (CNS_THREADS / 64) * WAVE_BYTES;
     static constexpr int SZ_CHIM = (CHIM_MAXCOLS * 13 + CHIM_TCAP * 4 + 16) * 4;
@@ -594,14 +604,15 @@ __device__ __forceinline__ int wave_append(int *ctr) {
 }
 
 // ---------------------------------------------------------------------------
-// inclusive prefix sum over each 32-lane half of the wave (row shifts 1, 2, 4, 8 scan the rows
-// of 16, row_bcast:15 carries row 0's total into row 1 and row 2's into row 3)
-__device__ __forceinline__ int half_incl_scan(int v) {
+// inclusive prefix sum over each GW-lane group of the wave (row shifts 1, 2, 4, 8 scan the
+// rows of 16; for 32-lane groups row_bcast:15 carries row 0's total into row 1, row 2's into 3)
+template <int GW>
+__device__ __forceinline__ int group_incl_scan(int v) {
     v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
     v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
     v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
     v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
-    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    if (GW == 32) v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
     return v;
 }
 
@@ -612,7 +623,16 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr int CNS_GW = 32;   // lanes per kept alignment in the pileup: two alignments per wave
+// field F of the K entry held in lanes 0..11 of each group, for every lane of the group
+template <int F>
+__device__ __forceinline__ int32_t kfld(int32_t kv, int g) {
+    if constexpr (CNS_GW == 16) {
+        return __builtin_amdgcn_update_dpp(0, kv, 0x150 + F, 0xf, 0xf, false);   // row_newbcast:F
+    } else {
+        const int32_t a0 = __builtin_amdgcn_readlane(kv, F), a1 = __builtin_amdgcn_readlane(kv, 32 + F);
+        return g ? a1 : a0;
+    }
+}
 
 // One kept alignment's states inside the window [cmin, cmax) (walk_states' semantics,
 // Seq.pm:396-461) by one 32-lane half of a wave, op-parallel: lane k of the half takes CIGAR op
@@ -630,7 +650,7 @@ constexpr int CNS_GW = 32;   // lanes per kept alignment in the pileup: two alig
 // alignments (their loops may differ in length: every cross-lane step stays in the half).
 template <class FS, class FC>
 __device__ __forceinline__ void group_states(const uint32_t *cg, int nop, int rp, int q0, int cmin, int cmax, int4 *ops,
-                                             uint32_t c_first0, uint32_t c_first1, FS &&special, FC &&column) {
+                                             const uint32_t (&c_first)[CNS_OPF], FS &&special, FC &&column) {
     constexpr int GW = CNS_GW;
     const int lane = (int)__lane_id();
     const int gl = lane & (GW - 1), glast = (lane & ~(GW - 1)) + GW - 1;
@@ -638,13 +658,15 @@ __device__ __forceinline__ void group_states(const uint32_t *cg, int nop, int rp
     for (int k0 = 0; k0 < nop && col0 < cmax; k0 += GW) {
         const int k = k0 + gl;
         const bool valid = k < nop;
-        const uint32_t c = k0 == 0 ? c_first0 : (k0 == GW ? c_first1 : (valid ? cg[k] : 0u));
+        uint32_t c = valid && k0 >= CNS_OPF * GW ? cg[k] : 0u;
+#pragma unroll
+        for (int u = 0; u < CNS_OPF; ++u) c = k0 == u * GW ? c_first[u] : c;
         const int n = (int)(c >> 4), code = (int)(c & 15u);
         const bool lead = k == 0 && code == 1;
         const int ncol = !valid ? 0 : (code == 0 || code == 2) ? n : (lead ? 1 : 0);
         const int qadv = valid && (code == 0 || code == 1) ? n : 0;
         const uint32_t nx1 = __shfl_down(c, 1, GW), nx2 = __shfl_down(c, 2, GW);
-        const int sc = half_incl_scan(ncol), sq = half_incl_scan(qadv);
+        const int sc = group_incl_scan<GW>(ncol), sq = group_incl_scan<GW>(qadv);
         // inserted bases right after an op that owns columns (zero-length ops skipped)
         int tot = 0;
         if (ncol > 0 && k + 1 < nop) {
@@ -994,60 +1016,62 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             CNS_TICK(8);
             if (D.prof && tid == 0) pt[14] += 1;
             const int cw0 = (int)w0, cw1 = (int)w0 + wn;
-            // two candidate streams per wave, one per 32-lane half (stream wv * 2 + g takes the
-            // candidates kb + stream + 2 NWAVE j), software-pipelined: the next candidate's first 64
-            // CIGAR ops and SEQ dwords (two per lane), and the K entry of the one after it, are in
-            // flight while the current one is processed.  A K entry (12 ints) is held spread over
-            // lanes 0..11 of its half in one register and read back with v_readlane.
-            const int g = lane >> 5, gl = lane & 31;
-            const int stream = wv * 2 + g;
-            constexpr int NSTREAM = 2 * NWAVE;
+            // CNS_NG candidate streams per wave, one per CNS_GW-lane group (stream wv * CNS_NG + g
+            // takes the candidates kb + stream + NSTREAM j), software-pipelined: the next
+            // candidate's first CIGAR ops and SEQ dwords, and the K entry of the one after it, are
+            // in flight while the current one is processed.  A K entry (12 ints) is held spread
+            // over lanes 0..11 of its group in one register.
+            const int g = lane / CNS_GW, gl = lane % CNS_GW;
+            const int stream = wv * CNS_NG + g;
+            constexpr int NSTREAM = CNS_NG * NWAVE;
             int4 *gops = wops + g * CNS_GW;
-            uint32_t *gseq = wseq + g * 64;
+            uint32_t *gseq = wseq + g * CNS_SEQ_DW;
             const int32_t *Ki = reinterpret_cast<const int32_t *>(K);
             auto ldK = [&](int kk) -> int32_t {
                 return kk < ke ? (gl < 12 ? Ki[12 * (int64_t)kk + gl] : 0) : (gl == 0 ? 0x7fffffff : 0);
             };
-            auto fld = [g](int32_t kv, int f) -> int32_t {
-                const int32_t a0 = __builtin_amdgcn_readlane(kv, f), a1 = __builtin_amdgcn_readlane(kv, 32 + f);
-                return g ? a1 : a0;
-            };
-            auto overl = [&](int32_t kv) { return fld(kv, 0) < cw1 && fld(kv, 1) > cw0; };   // overlaps the window
-            auto ldD = [&](int32_t kv, uint32_t &op0, uint32_t &op1, uint32_t &dw0, uint32_t &dw1) {
-                op0 = op1 = dw0 = dw1 = 0u;
+            auto overl = [&](int32_t kv) { return kfld<0>(kv, g) < cw1 && kfld<1>(kv, g) > cw0; };   // overlaps the window
+            auto ldD = [&](int32_t kv, uint32_t (&op)[CNS_OPF], uint32_t (&dw)[CNS_SEQ_PL]) {
+#pragma unroll
+                for (int u = 0; u < CNS_OPF; ++u) op[u] = 0u;
+#pragma unroll
+                for (int u = 0; u < CNS_SEQ_PL; ++u) dw[u] = 0u;
                 if (!overl(kv)) return;
-                const int64_t so = (int64_t)(uint32_t)fld(kv, 6) | ((int64_t)fld(kv, 7) << 32);
-                const int64_t cgi = (int64_t)(uint32_t)fld(kv, 8) | ((int64_t)fld(kv, 9) << 32);
-                const int nop = fld(kv, 4);
-                if (gl < nop) op0 = D.cig[cgi + gl];
-                if (gl + CNS_GW < nop) op1 = D.cig[cgi + CNS_GW + gl];
-                const int ndw = ((int)(so & 3) + (fld(kv, 2) & 0x7FFFFFFF) + 3) >> 2;
-                if (ndw <= 64) {
-                    if (gl < ndw) dw0 = gdw[(so >> 2) + gl];
-                    if (gl + 32 < ndw) dw1 = gdw[(so >> 2) + 32 + gl];
+                const int64_t so = (int64_t)(uint32_t)kfld<6>(kv, g) | ((int64_t)kfld<7>(kv, g) << 32);
+                const int64_t cgi = (int64_t)(uint32_t)kfld<8>(kv, g) | ((int64_t)kfld<9>(kv, g) << 32);
+                const int nop = kfld<4>(kv, g);
+#pragma unroll
+                for (int u = 0; u < CNS_OPF; ++u)
+                    if (u * CNS_GW + gl < nop) op[u] = D.cig[cgi + u * CNS_GW + gl];
+                const int ndw = ((int)(so & 3) + (kfld<2>(kv, g) & 0x7FFFFFFF) + 3) >> 2;
+                if (ndw <= CNS_SEQ_DW) {
+#pragma unroll
+                    for (int u = 0; u < CNS_SEQ_PL; ++u)
+                        if (u * CNS_GW + gl < ndw) dw[u] = gdw[(so >> 2) + u * CNS_GW + gl];
                 }
             };
             int32_t ckv = ldK(kb + stream), nkv;
-            uint32_t cop0, cop1, cdw0, cdw1;
-            ldD(ckv, cop0, cop1, cdw0, cdw1);
+            uint32_t cop[CNS_OPF], cdw[CNS_SEQ_PL];
+            ldD(ckv, cop, cdw);
             nkv = ldK(kb + stream + NSTREAM);
             for (int kk = kb + stream; kk < ke; kk += NSTREAM) {
-                uint32_t nop0, nop1, ndw0, ndw1;
-                ldD(nkv, nop0, nop1, ndw0, ndw1);
+                uint32_t nop_[CNS_OPF], ndw_[CNS_SEQ_PL];
+                ldD(nkv, nop_, ndw_);
                 const int32_t mkv = ldK(kk + 2 * NSTREAM);
                 if (overl(ckv)) {
-                    const int rp = fld(ckv, 0), e0z = fld(ckv, 2), sb = fld(ckv, 3), nop = fld(ckv, 4);
+                    const int rp = kfld<0>(ckv, g), e0z = kfld<2>(ckv, g), sb = kfld<3>(ckv, g), nop = kfld<4>(ckv, g);
                     const int ls = e0z & 0x7FFFFFFF;
                     const bool rc = e0z < 0;
-                    const int64_t so = (int64_t)(uint32_t)fld(ckv, 6) | ((int64_t)fld(ckv, 7) << 32);
-                    const int64_t cgi = (int64_t)(uint32_t)fld(ckv, 8) | ((int64_t)fld(ckv, 9) << 32);
+                    const int64_t so = (int64_t)(uint32_t)kfld<6>(ckv, g) | ((int64_t)kfld<7>(ckv, g) << 32);
+                    const int64_t cgi = (int64_t)(uint32_t)kfld<8>(ckv, g) | ((int64_t)kfld<9>(ckv, g) << 32);
                     const int head = (int)(so & 3);
                     const int ndw = (head + ls + 3) >> 2;
-                    // the alignment's SEQ in the half's LDS area (loaded ahead), when it fits
-                    const bool fast = ndw <= 64;
+                    // the alignment's SEQ in the group's LDS area (loaded ahead), when it fits
+                    const bool fast = ndw <= CNS_SEQ_DW;
                     if (fast) {
-                        gseq[gl] = cdw0;
-                        gseq[gl + 32] = cdw1;
+#pragma unroll
+                        for (int u = 0; u < CNS_SEQ_PL; ++u)
+                            if (u * CNS_GW + gl < CNS_SEQ_DW) gseq[u * CNS_GW + gl] = cdw[u];
                     }
                     const uint8_t *sl = reinterpret_cast<const uint8_t *>(gseq) + head;
                     SeqV sv;   // (the insertion states' keys; the slow path's bases)
@@ -1070,7 +1094,7 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                         atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
                     };
                     wave_sync();
-                    group_states(D.cig + cgi, nop, rp, sb, cw0, cw1, gops, cop0, cop1,
+                    group_states(D.cig + cgi, nop, rp, sb, cw0, cw1, gops, cop,
                                  [&](int scol, int sqp, int slen) {
                                      if (slen == 1) { add_fixed(scol, fixed_at(sqp)); return; }
                                      const int c = scol - cw0;
@@ -1083,10 +1107,10 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                 }
                 ckv = nkv;
                 nkv = mkv;
-                cop0 = nop0;
-                cop1 = nop1;
-                cdw0 = ndw0;
-                cdw1 = ndw1;
+#pragma unroll
+                for (int u = 0; u < CNS_OPF; ++u) cop[u] = nop_[u];
+#pragma unroll
+                for (int u = 0; u < CNS_SEQ_PL; ++u) cdw[u] = ndw_[u];
             }
             __syncthreads();
             CNS_TICK(3);
