@@ -334,6 +334,8 @@ static int side_stream(SwResident &r) {
 // against 58.8 ms fused -- the walk is latency- and issue-bound).
 static int pk_prepare(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O) {
     D.pk_chunk = 0;
+    const char *fw = getenv("PRGPU_PK_WIN");
+    D.pk_bt_win = fw && atoi(fw) == 8 ? 8 : 16;   // the fused kernel's backtrack window
     if (!O.pk) return 0;
     hipStream_t s = ctx_stream(c);
     int e = sw_launch_pk_order(D, O, 0, (void *)s);

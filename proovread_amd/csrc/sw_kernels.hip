@@ -912,7 +912,7 @@ __device__ __forceinline__ void pk_emit(const SwDev &D, int64_t t, uint32_t *cg,
     D.o_status[t] = 0;
 }
 
-template <int WB>
+template <int WB, int BTW>
 __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOptsDev O, int seg0, int seg1, int split) {
     // query masks ([half][bit][word][lane])
     __shared__ __attribute__((aligned(16))) uint32_t lsh[2 * 2 * PK_NQW * SW_WAVE];
@@ -996,7 +996,7 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
             for (int h = 0; h < 2; ++h)
                 if (cg[h]) cg[h][cap[h] - 1] = fst[h] = lst[h] = ((uint32_t)lqq << 4), nc[h] = 1;
         } else {
-            pk_backtrack2(zl, SW_WAVE, npair, nrow, tl, lqq, ww, cg, nc, fst, lst, cap);
+            pk_backtrack2<BTW>(zl, SW_WAVE, npair, nrow, tl, lqq, ww, cg, nc, fst, lst, cap);
         }
         unsigned long long c3 = clock64();
         ph[2] += c3 - c2;
@@ -1257,7 +1257,9 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
     };
     int fgrid = (int)((sel_count(D) + 255) / 256);
     fgrid = fgrid < 8192 ? (fgrid > 0 ? fgrid : 1) : 8192;
-    hipError_t e = hipMemsetAsync(D.x_try, 0, (size_t)D.n_task + 1, s);
+    // (a whole number of dwords: a byte-sized fill takes the runtime's byte kernel, 2 ms for the
+    // 35 MB of configs[1]; the buffer has 64 bytes of slack)
+    hipError_t e = hipMemsetAsync(D.x_try, 0, ((size_t)D.n_task + 1 + 15) & ~(size_t)15, s);
     if (e != hipSuccess) return (int)e;
     for (int side = 0; side < 2; ++side) {
         for (int tryi = 0; tryi < 2; ++tryi) {
@@ -1304,12 +1306,16 @@ int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
         if (!pk_ordered && (rc = sw_launch_pk_order(D, O, 0, stream))) return rc;
         if (ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
         if (D.pk_chunk <= 0) {   // fused: DP and backtrack in one kernel, a slab per resident wave
-            hipLaunchKernelGGL(sw_global_pk_kernel<40>, dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, 0, INT32_MAX, 0);
+            // (backtrack window: 16 rows, or 8 with PRGPU_PK_WIN=8 -- half the walk's unrolled code)
+            if (D.pk_bt_win == 8)
+                hipLaunchKernelGGL((sw_global_pk_kernel<40, 8>), dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, 0, INT32_MAX, 0);
+            else
+                hipLaunchKernelGGL((sw_global_pk_kernel<40, 16>), dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, 0, INT32_MAX, 0);
         } else {   // chunks of segments: the DP kernel, then the backtrack kernel over the chunk's slabs
             for (int64_t c0 = 0; c0 < D.pk_nseg_bound; c0 += D.pk_chunk) {
                 const int c1 = (int)(c0 + D.pk_chunk < D.pk_nseg_bound ? c0 + D.pk_chunk : D.pk_nseg_bound);
                 const int n = c1 - (int)c0;
-                hipLaunchKernelGGL(sw_global_pk_kernel<40>, dim3(n < grid_pk ? n : grid_pk), dim3(SW_WAVE), 0, s, D, O,
+                hipLaunchKernelGGL((sw_global_pk_kernel<40, 16>), dim3(n < grid_pk ? n : grid_pk), dim3(SW_WAVE), 0, s, D, O,
                                    (int)c0, c1, 1);
                 if (D.pk_bt_win == 4)
                     hipLaunchKernelGGL(sw_global_pk_bt_kernel<4>, dim3(n < D.pk_bt_grid ? n : D.pk_bt_grid), dim3(SW_WAVE),
