@@ -46,7 +46,7 @@ OPS_PER_CELL = 14   # SURVEY.md §8d canonical int ops per DP cell
 BIN_FILTER = (20, 20.0 * 15.0)
 # HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over this bench
 # (tools/pmc_summary.py; MI355X_MICROARCH.md's corrections)
-PMC_FILE = "pmc_r03k.json"
+PMC_FILE = "pmc_r03m.json"
 _JSON_OUT = sys.stdout
 
 
