@@ -293,13 +293,14 @@ def main():
     n_aln, sum_ncig, sum_lseq = it.alignment_stats()
     cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + lr_bases * (2 + 2 + 6 * 4 * 2)
     # HBM bytes per launch from the PMC FETCH_SIZE / WRITE_SIZE passes of this bwa-mode step
-    # (tools/r02_gpu5.sh -> tools/pmc_summary.py -> profiles/pmc_r02_bwa.json)
+    # (tools/r03_final.sh -> tools/pmc_summary.py -> profiles/pmc_r03m.json)
     prof = ROOT / "profiles" / PMC_FILE
     traffic = traffic_cns = traffic_ext = None
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())
-            traffic = pm.get("sw_global_pk_kernel<40>", {}).get("hbm_bytes_per_launch")
+            traffic = next((v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith("sw_global_pk_kernel<40")),
+                           None)
             traffic_cns = next((v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith("cns_lr_kernel")), None)
             traffic_ext = {k: v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith("sw_ext_")}
         except Exception:
