@@ -74,11 +74,10 @@ struct IndexView {
     const uint32_t *cnt[KI - 1];   // cnt[j-1][code]: occurrences of the j-mer `code`, j = 1..11
 };
 
-struct Iv {   // 12 bytes (occurrence counts < 2^32: text positions are 32-bit)
+struct Iv {
     int32_t start, end;
-    uint32_t occ;
+    int64_t occ;
 };
-SC_HD Iv iv_make(int start, int end, int64_t occ) { return Iv{start, end, (uint32_t)occ}; }
 struct Seed {
     int64_t rbeg;   // forward-reverse coordinate (bwa): reverse strand >= l_pac
     int32_t qbeg, len;
@@ -260,7 +259,7 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
     Iv *curr = S.curr, *prev = S.prev;
     const int cap = S.cap_iv;
     int nc = 0, np = 0;
-    Iv ik = iv_make(x, x + 1, occ(x, x + 1));
+    Iv ik{x, x + 1, occ(x, x + 1)};
     int i;
     // the forward extension's counts for lengths 7..15 do not depend on each other: when the
     // 12-mer at x is N-free they are loaded up front (9 independent loads instead of a
@@ -299,12 +298,12 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
             } else {
                 o = occ(x, i + 1);
             }
-            if (o != (int64_t)ik.occ) {
+            if (o != ik.occ) {
                 if (nc >= cap) { err |= SC_OVER_IV; return len; }
                 curr[nc++] = ik;
                 if (o < min_intv) break;
             }
-            ik = iv_make(x, i + 1, o);
+            ik = Iv{x, i + 1, o};
         } else {
             if (nc >= cap) { err |= SC_OVER_IV; return len; }
             curr[nc++] = ik;
@@ -343,8 +342,8 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
                         if (nmem >= cap) { err |= SC_OVER_IV; return len; }
                         mem[nmem++] = Iv{i + 1, p.end, p.occ};
                     }
-                } else if (nc == 0 || o != (int64_t)curr[nc - 1].occ) {
-                    curr[nc++] = iv_make(i, p.end, o);   // nc <= np <= cap
+                } else if (nc == 0 || o != curr[nc - 1].occ) {
+                    curr[nc++] = Iv{i, p.end, o};   // nc <= np <= cap
                 }
             }
         }
@@ -367,7 +366,7 @@ SC_HD int seed_strategy1(const Occ &occ, const uint8_t *q, int len, int x, int m
         if (i - x >= min_len) {
             const int64_t o = occ(x, i + 1);
             if (o < max_intv) {
-                m = iv_make(x, i + 1, o);
+                m = Iv{x, i + 1, o};
                 return i + 1;
             }
         }
@@ -398,8 +397,8 @@ SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const 
     const int nfirst = nm;
     for (int k = 0; k < nfirst && !err; ++k) {
         const Iv p = S.mems[k];
-        if (p.end - p.start < split_len || (int64_t)p.occ > O.split_width) continue;
-        smem1(occ, S, q, len, (p.start + p.end) >> 1, (int64_t)p.occ + 1, S.m1, n1, err);
+        if (p.end - p.start < split_len || p.occ > O.split_width) continue;
+        smem1(occ, S, q, len, (p.start + p.end) >> 1, p.occ + 1, S.m1, n1, err);
         for (int j = 0; j < n1; ++j)
             if (S.m1[j].end - S.m1[j].start >= O.min_seed_len) push(S.m1[j]);
     }

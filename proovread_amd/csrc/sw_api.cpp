@@ -382,12 +382,16 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
     if ((e = aln_launch_init(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     if ((e = aln_launch_list(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
-    // the chain-head links only feed the walk: built on the side stream beside round 0's extension,
-    // once its left-side DP launch is done (ahead of it, the latency-bound links kernel filled the
-    // GPU and held back the DP launch by ~2.5 ms; after it, it fills the retry and finish
-    // kernels' idle CUs)
+    // the chain-head links only feed the walk: built on the side stream beside round 0's extension
     bool heads_side = false;
-    if (A.hprev && (rc = side_stream(r))) return rc;
+    if (A.hprev) {
+        if ((rc = side_stream(r))) return rc;
+        HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[0], s));
+        HIPCHK(hipStreamWaitEvent((hipStream_t)r.side, (hipEvent_t)r.side_ev[0], 0));
+        if ((e = aln_launch_heads(A, r.side))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[2], (hipStream_t)r.side));
+        heads_side = true;
+    }
     int32_t cnt[4] = {0, 0, 0, 0};
     int64_t n_list = r.n_rank0;   // round 0: every chain's first seed (listed after the init kernel)
     D.tsel = A.tlist;
@@ -395,21 +399,9 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     for (;;) {   // mem_chain2aln: every round extends the listed seeds, the walk resumes
         D.tsel_n = n_list;
         HIPCHK(hipMemsetAsync(A.counter, 0, 8, s));
-        const int ev0 = r.ext_ev.n;
         if (n_list) {
             e = sw_launch_extend(D, O, ctx_ncu(c) * 16, grid_pk, (void *)s, &r.ext_ev);
             if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
-        }
-        if (A.hprev && r.ext_rounds == 0) {
-            // after the first DP launch of this round (its closing event), else after everything
-            // enqueued so far
-            hipEvent_t after = (hipEvent_t)r.side_ev[0];
-            if (r.ext_ev.n >= ev0 + 2 && r.ext_ev.ev[ev0 + 1]) after = (hipEvent_t)r.ext_ev.ev[ev0 + 1];
-            else HIPCHK(hipEventRecord(after, s));
-            HIPCHK(hipStreamWaitEvent((hipStream_t)r.side, after, 0));
-            if ((e = aln_launch_heads(A, r.side))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
-            HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[2], (hipStream_t)r.side));
-            heads_side = true;
         }
         if (heads_side) {
             HIPCHK(hipStreamWaitEvent(s, (hipEvent_t)r.side_ev[2], 0));
