@@ -673,37 +673,44 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     const int bt = ((sl >> 3) & 1) * 16 + (sl & 7);
                     const int nib = (int)(((X >> bt) & 1u) | (((X >> (bt + 8)) & 1u) << 1) |
                                           (((Y >> bt) & 1u) << 2) | (((Y >> (bt + 8)) & 1u) << 3));
-                    which[h] = pk_which(which[h], nib);
-                    // an I step takes the F-continuations below it in the loaded pair along (one
-                    // per D4 bit set, ksw's F state); the first D4 = 0 ends the run with the M
-                    // step of ksw's F -> M transition, unless the query column runs out first
-                    int len = 1;
-                    bool mstep = false;
-                    if (which[h] == 2) {
-                        const int j = sl & 15;
-                        const uint32_t d4 = ((Y >> 8) & 0xFFu) | (((Y >> 24) & 0xFFu) << 8);
-                        const uint32_t zeros = ~d4 & ((1u << j) - 1u);
-                        const int m = zeros ? j - 1 - (31 - __builtin_clz(zeros)) : j;   // ones below sl
-                        const int mi = m < k[h] ? m : k[h];
-                        len = 1 + mi;
-                        mstep = zeros != 0u && mi == m && k[h] - len >= 0;
-                    }
-                    const int op = which[h] == 0 ? 0 : (which[h] == 1 ? 2 : 1);
-                    bool ok = push(h, op, len);
-                    if (which[h] == 0) --i[h], --k[h];
-                    else if (which[h] == 1) --i[h];
-                    else k[h] -= len;
-                    if (ok && mstep) {
-                        which[h] = 0;
-                        ok = push(h, 0, 1);
-                        --i[h], --k[h];
-                    }
-                    if (!ok) {
-                        n[h] = -1;
-                        live[h] = false;
-                        break;
-                    }
-                    live[h] = i[h] >= 0 && k[h] >= 0;
+                    // the step, branch-free apart from the stores (round 3: the nested push /
+                    // move branches cost ~280 instructions per step, most of them exec-mask
+                    // bookkeeping): pk_which, then an I step takes the F-continuations below
+                    // it in the loaded pair along (one per D4 bit set, ksw's F state); the
+                    // first D4 = 0 ends the run with the M step of ksw's F -> M transition,
+                    // unless the query column runs out first
+                    // pk_which as a table: 2-bit next states for which = 0 / 1 / 2 packed in T
+                    const uint32_t un = (uint32_t)nib;
+                    const uint32_t T = (un & 2u) | (un & 1u & ~(un >> 1)) | (un & 4u) | ((un & 8u) << 2);
+                    const int wn = (int)((T >> (2 * which[h])) & 3u);
+                    const int j = sl & 15;
+                    const uint32_t d4 = ((Y >> 8) & 0xFFu) | (((Y >> 24) & 0xFFu) << 8);
+                    const uint32_t zeros = ~d4 & ((1u << j) - 1u);
+                    const int m = zeros ? j - 1 - (31 - __builtin_clz(zeros | 1u)) : j;   // ones below sl
+                    const int mi = m < k[h] ? m : k[h];
+                    const bool isI = wn == 2;
+                    const int len = isI ? 1 + mi : 1;
+                    const bool mstep = isI & (zeros != 0u) & (mi == m) & (k[h] - len >= 0);
+                    const int op = (int)((0x18u >> (2 * wn)) & 3u);   // M, D, I for which = 0, 1, 2
+                    // push(op, len), then (mstep) push(M, 1), which always closes the I run
+                    const bool same = op == rop[h];
+                    const bool fl1 = !same & (rop[h] >= 0);
+                    const uint32_t v1 = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
+                    const int ra = same ? rln[h] + len : len;
+                    const uint32_t v2 = ((uint32_t)ra << 4) | 1u;
+                    const int n0 = n[h], n1 = n0 + (int)fl1;
+                    const bool fail = (fl1 & (n0 + 1 >= maxcig[h])) | (mstep & (n1 + 1 >= maxcig[h]));
+                    if (fl1 & !fail) cg[h][maxcig[h] - 1 - n0] = v1;
+                    if (mstep & !fail) cg[h][maxcig[h] - 1 - n1] = v2;
+                    last[h] = (fl1 & (n0 == 0)) ? v1 : ((mstep & (n1 == 0)) ? v2 : last[h]);
+                    first[h] = mstep ? v2 : (fl1 ? v1 : first[h]);
+                    n[h] = fail ? -1 : n1 + (int)mstep;
+                    rop[h] = mstep ? 0 : op;
+                    rln[h] = mstep ? 1 : ra;
+                    which[h] = mstep ? 0 : wn;
+                    i[h] -= (int)!isI + (int)mstep;
+                    k[h] -= (isI ? len : (int)(wn == 0)) + (int)mstep;
+                    live[h] = !fail & (i[h] >= 0) & (k[h] >= 0);
                 }
             }
         }

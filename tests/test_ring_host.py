@@ -222,3 +222,42 @@ def test_extend_pk_matches_oracle(ring, seed):
                 assert list(out[6 * h:6 * h + 6]) == [sc] + list(outs), (h, qs[h], ts[h], w, h0s[h], eb, (a, b, od, ed, oi, ei, zd))
                 n += 1
     assert n == 1000
+
+
+def test_global_pk_cigar_cap(ring):
+    """The packed backtrack's op cap: a CIGAR of N ops fits max_cigar = N and reports -1
+    (the task goes to the overflow pass) at N - 1, for both halves."""
+    L = ob.sw_lib()
+    rng = random.Random(77)
+    a, b, od, ed, oi, ei, _ = SCORING[0]
+    mat = (C.c_int8 * 25)()
+    L.osw_fill_scmat(a, b, mat)
+    n = 0
+    for _ in range(60):
+        lq = rng.choice([30, 60, 100, 150])
+        qs = ["".join(rng.choice("ACGT") for _ in range(lq)) for _ in range(2)]
+        ts = [(_mutate(q, rng, 0.15).replace("N", "A") or "A") for q in qs]
+        dls = [abs(len(t) - lq) for t in ts]
+        if max(dls) + 3 > 40:
+            continue
+        w = rng.randint(max(dls) + 3, 40)
+        want = []
+        for h in range(2):
+            nco, cigo = C.c_int(), (C.c_uint32 * 4096)()
+            L.osw_global(lq, _nt4(qs[h]), len(ts[h]), _nt4(ts[h]), 5, mat, od, ed, oi, ei, w, C.byref(nco), cigo, 4096)
+            want.append(list(cigo[:nco.value]))
+        for cap_delta in (0, -1):
+            caps = min(len(want[0]), len(want[1])) + cap_delta
+            if caps < 1:
+                continue
+            sc, nc, cig = (C.c_int * 2)(), (C.c_int * 2)(), (C.c_uint32 * 8192)()
+            fl = ring.pk_global(a, b, od, ed, oi, ei, lq, w, _nt4(qs[0]), _nt4(qs[1]), len(ts[0]), _nt4(ts[0]),
+                                len(ts[1]), _nt4(ts[1]), sc, nc, cig, caps, 0)
+            assert fl == 0
+            for h in range(2):
+                if len(want[h]) <= caps:
+                    assert list(cig[h * caps:h * caps + nc[h]]) == want[h]
+                else:
+                    assert nc[h] == -1
+                n += 1
+    assert n > 100
