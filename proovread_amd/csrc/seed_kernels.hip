@@ -20,6 +20,9 @@ namespace prgpu {
 
 constexpr int SEED_WAVES = 4;          // waves (reads in flight) per workgroup
 constexpr int SEED_LMAX = 1024;        // LDS start offsets per wave: reads <= 1024 bases
+#ifndef SEED_MINB
+#define SEED_MINB 4
+#endif
 
 // the short j-mer count tables (j <= LC_MAX) into the workgroup's LDS: the SMEM search's
 // occurrence counts of short extensions are dependent lookups, on chip instead of L2/MALL
@@ -144,7 +147,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
 
 // Pass 2: one wave per read with the large scratch slice (the reads of D.rlist: those that
 // outgrew pass 1's slices), the sequential part on lane 0.
-__global__ void __launch_bounds__(64 * SEED_WAVES, 4) seed_wave_kernel(SeedDev D) {
+__global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
     load_lcnt(D.V, lcnt);
@@ -190,7 +193,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, 4) seed_wave_kernel(SeedDev D
 // with 64 reads' loads in flight per wave instead of one.  Scratch: 64 small slices per wave
 // (D.caps sized for the batch's read lengths); a read that outgrows its slice is flagged and
 // goes to pass 2.
-__global__ void __launch_bounds__(64 * SEED_WAVES, 4) seed_batch_kernel(SeedDev D) {
+__global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
     load_lcnt(D.V, lcnt);

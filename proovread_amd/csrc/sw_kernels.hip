@@ -1306,7 +1306,7 @@ int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
         if (!pk_ordered && (rc = sw_launch_pk_order(D, O, 0, stream))) return rc;
         if (ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
         if (D.pk_chunk <= 0) {   // fused: DP and backtrack in one kernel, a slab per resident wave
-            // (backtrack window: 16 rows, or 8 with PRGPU_PK_WIN=8 -- half the walk's unrolled code)
+            // (backtrack window: 8 rows, or 16 with PRGPU_PK_WIN=16)
             if (D.pk_bt_win == 8)
                 hipLaunchKernelGGL((sw_global_pk_kernel<40, 8>), dim3(grid_pk), dim3(SW_WAVE), 0, s, D, O, 0, INT32_MAX, 0);
             else

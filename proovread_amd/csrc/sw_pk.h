@@ -671,18 +671,17 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     }
                     if (stat) ++stat[1];
                     const int bt = ((sl >> 3) & 1) * 16 + (sl & 7);
-                    const int nib = (int)(((X >> bt) & 1u) | (((X >> (bt + 8)) & 1u) << 1) |
-                                          (((Y >> bt) & 1u) << 2) | (((Y >> (bt + 8)) & 1u) << 3));
                     // the step, branch-free apart from the stores (round 3: the nested push /
                     // move branches cost ~280 instructions per step, most of them exec-mask
-                    // bookkeeping): pk_which, then an I step takes the F-continuations below
-                    // it in the loaded pair along (one per D4 bit set, ksw's F state); the
-                    // first D4 = 0 ends the run with the M step of ksw's F -> M transition,
-                    // unless the query column runs out first
-                    // pk_which as a table: 2-bit next states for which = 0 / 1 / 2 packed in T
-                    const uint32_t un = (uint32_t)nib;
-                    const uint32_t T = (un & 2u) | (un & 1u & ~(un >> 1)) | (un & 4u) | ((un & 8u) << 2);
-                    const int wn = (int)((T >> (2 * which[h])) & 3u);
+                    // bookkeeping): pk_which on the slot's bits (a: D1 at bit 0, D2 at bit 8;
+                    // b: D3, D4), then an I step takes the F-continuations below it in the
+                    // loaded pair along (one per D4 bit set, ksw's F state); the first D4 = 0
+                    // ends the run with the M step of ksw's F -> M transition, unless the query
+                    // column runs out first
+                    const uint32_t a = X >> bt, b = Y >> bt;
+                    const int w0 = (a & 0x100u) ? 2 : (int)(a & 1u);
+                    const int w1 = (int)(b & 1u), w2 = (int)((b >> 7) & 2u);
+                    const int wn = which[h] == 0 ? w0 : (which[h] == 1 ? w1 : w2);
                     const int j = sl & 15;
                     const uint32_t d4 = ((Y >> 8) & 0xFFu) | (((Y >> 24) & 0xFFu) << 8);
                     const uint32_t zeros = ~d4 & ((1u << j) - 1u);
