@@ -586,7 +586,7 @@ SW_RING_FN int glob_pk_backtrack(const PkDir *z, int ZS, int npair, int hb, int 
 // Backtrack of both halves of a lane (glob_pk_backtrack's walk; the plain
 // version above is its reference), in row lockstep across the wave: every
 // walk leaves a row only by an M or D step, so all lanes can sweep the rows
-// together from the wave's last row down.  Windows of 16 rows are loaded at
+// together from the wave's last row down.  Windows of WIN rows (8 in the fused kernel) are loaded at
 // each half's current 16-slot pair (the walks hug the band centre, so the 64
 // lanes mostly read the same pair: the loads are coalesced rows of the
 // [row][pair][lane] slab), the half's direction bytes are picked out with
