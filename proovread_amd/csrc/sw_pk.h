@@ -658,9 +658,13 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
 #pragma unroll
         for (int d = 0; d < WIN; ++d) {
             const int r = R - d;
+            // one loop for both halves: an iteration steps every half still on row r
+            for (;;) {
+                const bool go[2] = {live[0] && i[0] == r, live[1] && i[1] == r};
+                if (!SW_RING_ANY(go[0] || go[1])) break;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                while (live[h] && i[h] == r) {
+                for (int h = 0; h < 2; ++h) {
+                    if (!go[h]) continue;
                     const int sl = k[h] - r + w;
                     uint32_t X = bx[h][d], Y = by[h][d];
                     if ((sl >> 4) != p[h]) {
