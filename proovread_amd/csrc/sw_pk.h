@@ -683,9 +683,10 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     // ends the run with the M step of ksw's F -> M transition, unless the query
                     // column runs out first
                     const uint32_t a = X >> bt, b = Y >> bt;
-                    const int w0 = (a & 0x100u) ? 2 : (int)(a & 1u);
-                    const int w1 = (int)(b & 1u), w2 = (int)((b >> 7) & 2u);
-                    const int wn = which[h] == 0 ? w0 : (which[h] == 1 ? w1 : w2);
+                    const uint32_t d2 = (a >> 8) & 1u;
+                    // next states for which = 0 / 1 / 2 as 2-bit fields (a table, not a branch)
+                    const uint32_t T = (d2 << 1) | (a & 1u & ~d2) | ((b & 1u) << 2) | (((b >> 8) & 1u) << 5);
+                    const int wn = (int)((T >> (2 * which[h])) & 3u);
                     const int j = sl & 15;
                     const uint32_t d4 = ((Y >> 8) & 0xFFu) | (((Y >> 24) & 0xFFu) << 8);
                     const uint32_t zeros = ~d4 & ((1u << j) - 1u);
@@ -693,19 +694,19 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     const int mi = m < k[h] ? m : k[h];
                     const bool isI = wn == 2;
                     const int len = isI ? 1 + mi : 1;
-                    const bool mstep = isI & (zeros != 0u) & (mi == m) & (k[h] - len >= 0);
+                    const bool mstep = isI && zeros != 0u && mi == m && k[h] - len >= 0;
                     const int op = (int)((0x18u >> (2 * wn)) & 3u);   // M, D, I for which = 0, 1, 2
                     // push(op, len), then (mstep) push(M, 1), which always closes the I run
                     const bool same = op == rop[h];
-                    const bool fl1 = !same & (rop[h] >= 0);
+                    const bool fl1 = !same && rop[h] >= 0;
                     const uint32_t v1 = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
                     const int ra = same ? rln[h] + len : len;
                     const uint32_t v2 = ((uint32_t)ra << 4) | 1u;
                     const int n0 = n[h], n1 = n0 + (int)fl1;
-                    const bool fail = (fl1 & (n0 + 1 >= maxcig[h])) | (mstep & (n1 + 1 >= maxcig[h]));
-                    if (fl1 & !fail) cg[h][maxcig[h] - 1 - n0] = v1;
-                    if (mstep & !fail) cg[h][maxcig[h] - 1 - n1] = v2;
-                    last[h] = (fl1 & (n0 == 0)) ? v1 : ((mstep & (n1 == 0)) ? v2 : last[h]);
+                    const bool fail = (fl1 && n0 + 1 >= maxcig[h]) || (mstep && n1 + 1 >= maxcig[h]);
+                    if (fl1 && !fail) cg[h][maxcig[h] - 1 - n0] = v1;
+                    if (mstep && !fail) cg[h][maxcig[h] - 1 - n1] = v2;
+                    last[h] = (fl1 && n0 == 0) ? v1 : ((mstep && n1 == 0) ? v2 : last[h]);
                     first[h] = mstep ? v2 : (fl1 ? v1 : first[h]);
                     n[h] = fail ? -1 : n1 + (int)mstep;
                     rop[h] = mstep ? 0 : op;
@@ -713,7 +714,7 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     which[h] = mstep ? 0 : wn;
                     i[h] -= (int)!isI + (int)mstep;
                     k[h] -= (isI ? len : (int)(wn == 0)) + (int)mstep;
-                    live[h] = !fail & (i[h] >= 0) & (k[h] >= 0);
+                    live[h] = !fail && i[h] >= 0 && k[h] >= 0;
                 }
             }
         }
