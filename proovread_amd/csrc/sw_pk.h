@@ -682,13 +682,15 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     // loaded pair along (one per D4 bit set, ksw's F state); the first D4 = 0
                     // ends the run with the M step of ksw's F -> M transition, unless the query
                     // column runs out first
-                    const uint32_t a = X >> bt, b = Y >> bt;
-                    const uint32_t d2 = (a >> 8) & 1u;
-                    // next states for which = 0 / 1 / 2 as 2-bit fields (a table, not a branch)
-                    const uint32_t T = (d2 << 1) | (a & 1u & ~d2) | ((b & 1u) << 2) | (((b >> 8) & 1u) << 5);
-                    const int wn = (int)((T >> (2 * which[h])) & 3u);
+                    // which = 0 reads D1 (bit 0) / D2 (bit 8) of X, which = 1 D3 (bit 0) and
+                    // which = 2 D4 (bit 8) of Y: D2 or D4 -> 2 (unless which = 1), else D1 or D3
+                    // (unless which = 2)
+                    const uint32_t u = (which[h] == 0 ? X : Y) >> bt;
+                    const bool s2 = (u & 0x100u) != 0u && which[h] != 1;
+                    const bool s1 = (u & 1u) != 0u && which[h] != 2;
+                    const int wn = s2 ? 2 : (s1 ? 1 : 0);
                     const int j = sl & 15;
-                    const uint32_t d4 = ((Y >> 8) & 0xFFu) | (((Y >> 24) & 0xFFu) << 8);
+                    const uint32_t d4 = perm_b32(0u, Y, 0x0C0C0301u);   // D4 bytes of both chunks
                     const uint32_t zeros = ~d4 & ((1u << j) - 1u);
                     const int m = zeros ? j - 1 - (31 - __builtin_clz(zeros | 1u)) : j;   // ones below sl
                     const int mi = m < k[h] ? m : k[h];
@@ -702,13 +704,15 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
                     const uint32_t v1 = ((uint32_t)rln[h] << 4) | (uint32_t)rop[h];
                     const int ra = same ? rln[h] + len : len;
                     const uint32_t v2 = ((uint32_t)ra << 4) | 1u;
-                    const int n0 = n[h], n1 = n0 + (int)fl1;
-                    const bool fail = (fl1 && n0 + 1 >= maxcig[h]) || (mstep && n1 + 1 >= maxcig[h]);
-                    if (fl1 && !fail) cg[h][maxcig[h] - 1 - n0] = v1;
-                    if (mstep && !fail) cg[h][maxcig[h] - 1 - n1] = v2;
+                    const int n0 = n[h], n1 = n0 + (int)fl1, n2 = n1 + (int)mstep;
+                    // a flush needs n + 1 < maxcig; n0 < maxcig always holds, so the pushes fail
+                    // exactly when the count after them reaches maxcig
+                    const bool fail = n2 >= maxcig[h];
+                    if (fl1 && !fail) cg[h][(uint32_t)(maxcig[h] - 1 - n0)] = v1;   // (unsigned: no sign extension)
+                    if (mstep && !fail) cg[h][(uint32_t)(maxcig[h] - 1 - n1)] = v2;
                     last[h] = (fl1 && n0 == 0) ? v1 : ((mstep && n1 == 0) ? v2 : last[h]);
                     first[h] = mstep ? v2 : (fl1 ? v1 : first[h]);
-                    n[h] = fail ? -1 : n1 + (int)mstep;
+                    n[h] = fail ? -1 : n2;
                     rop[h] = mstep ? 0 : op;
                     rln[h] = mstep ? 1 : ra;
                     which[h] = mstep ? 0 : wn;
