@@ -33,7 +33,12 @@ An expected-output file holds, per case::
 from __future__ import annotations
 
 import dataclasses
+import gzip
 from typing import Dict, List
+
+
+def _open(path):
+    return gzip.open(path, "rt") if str(path).endswith(".gz") else open(path)
 
 DEFAULT_PARAMS = {
     "coverage": "11.25",
@@ -94,7 +99,7 @@ def read_cases(path) -> List[Case]:
     out = []
     cur = None
     sect = None
-    with open(path) as fh:
+    with _open(path) as fh:
         for line in fh:
             line = line.rstrip("\n")
             if line.startswith(">>CASE "):
@@ -122,7 +127,7 @@ def read_expect(path) -> Dict[str, Expect]:
     out = {}
     cur = None
     sect = None
-    with open(path) as fh:
+    with _open(path) as fh:
         for line in fh:
             line = line.rstrip("\n")
             if line.startswith(">>CASE "):
