@@ -95,6 +95,9 @@ int pr_comm_allgatherv_host(pr_comm *c, const uint8_t *send, int64_t nbytes, uin
 int pr_comm_alltoall_counts(pr_comm *c, const int64_t *send_counts, int64_t *recv_counts);
 int pr_comm_alltoallv_host(pr_comm *c, const uint8_t *send, const int64_t *send_counts, uint8_t *recv,
                            const int64_t *recv_counts);
+/* the same on DEVICE buffers, asynchronous on the context stream (no host copy) */
+int pr_comm_alltoallv_dev(pr_comm *c, const void *send, const int64_t *send_counts, void *recv,
+                          const int64_t *recv_counts);
 
 /* ------------------------------------------------------------------ */
 /* consensus stage                                                     */
@@ -374,6 +377,8 @@ int pr_seed_gpu_index_build(pr_ctx *ctx, const uint8_t *lr_seq, const int64_t *l
 int pr_seed_gpu_index_digest(pr_ctx *ctx, uint64_t *out6);
 /* milliseconds of the last pr_seed_gpu_index_build (HIP events on the ctx stream) */
 int pr_seed_gpu_index_last_ms(pr_ctx *ctx, double *ms);
+/* seeds of the last pr_seed_gpu_map (those kept in HBM when out = NULL) */
+int pr_seed_gpu_seed_count(pr_ctx *ctx, int64_t *n);
 /* reads of the last pr_seed_gpu_map that outgrew pass 1's small scratch slices (64 reads per
  * wave, lane per read) and ran in pass 2 (one wave per read, the large slices) */
 int pr_seed_gpu_pass2_reads(pr_ctx *ctx, int64_t *n);
@@ -415,6 +420,44 @@ int pr_iter_bounds(pr_ctx *ctx, int32_t *n_lr, int64_t *n_task, pr_cns_bounds *b
 int pr_iter_alignment_stats(pr_ctx *ctx, int64_t *n_aln, int64_t *sum_ncig, int64_t *sum_lseq);
 int pr_iter_last_timing(pr_ctx *ctx, double *ms_sw_extend, double *ms_sw_global, double *ms_assemble,
                         double *ms_consensus);
+/* The exact-parity multi-GPU layout, device-resident.  proovread maps every
+ * short read against ALL long reads (bin/proovread:1270, 1313) and then corrects the long
+ * reads in chunks (xargs -P, 1596-1619); across GPUs every rank holds the index of all long
+ * reads, seeds and aligns a contiguous shard of the short reads (bwa mode), and sends each
+ * reported alignment to the owner of its long read (contiguous long-read ranges), which then
+ * runs bwa-proovread's -b/-l filter, the hand-off and the consensus for the reads it owns.
+ * Because the shards are contiguous and the blocks arrive source-rank-major, the owner sees
+ * every long read's alignments in the single run's order: the outputs equal one GPU's.
+ *
+ * 1. pr_sw_upload_gpu_seeds: the SW batch of the rank's shard from the device seeds of the last
+ *    pr_seed_gpu_map(out = NULL) (b: the shard's short reads -- sr 0 is global id read_id0 --
+ *    and all long reads; task fields ignored), then pr_sw_launch (bwa mode).
+ * 2. pr_aln_exchange: the reported alignments -> 24-byte records + CIGAR ops packed by owner on
+ *    the device, the counts exchanged, one RCCL all-to-all of device buffers (comm NULL: world
+ *    1, no RCCL); lr_bounds[world+1] are the owners' long-read ranges, sr0 the global id of the
+ *    shard's first short read.  n_recv: records this rank received.
+ * 3. pr_iter_upload_owned (after 2): the owned long reads (consensus reference, qualities) and
+ *    every short read of the task (the consensus reads SEQ from it by global id).
+ * 4. pr_iter_launch (its SW options give -b/-l) runs filter + hand-off + consensus over the
+ *    received alignments (no SW); pr_iter_download / pr_iter_mask / pr_iter_stats as usual. */
+int pr_sw_upload_gpu_seeds(pr_ctx *ctx, const pr_sw_batch *b);
+int pr_aln_exchange(pr_ctx *ctx, pr_comm *comm, int64_t sr0, const int64_t *lr_bounds, int64_t *n_recv);
+/* the same exchange among `world` contexts of ONE process (several shards on one GPU, or one
+ * process driving several GPUs): every context's pack, then device copies in source order in
+ * place of RCCL; sr0[k] is context k's first short read, n_recv[world] (may be NULL) */
+int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64_t *sr0, const int64_t *lr_bounds,
+                          int64_t *n_recv);
+typedef struct pr_own_batch {
+    int32_t lr0, n_lr;            /* owned long reads: global ids [lr0, lr0 + n_lr)          */
+    const int64_t *lr_off;        /* [n_lr+1] their offsets (from 0)                          */
+    const uint8_t *ref_seq;       /* ASCII consensus reference (bam2cns --ref), required      */
+    const uint8_t *lr_qual;       /* phred+33 qualities (lr_off), or NULL                     */
+    int32_t n_sr;                 /* every short read of the task, global ids                 */
+    const int64_t *sr_off;        /* [n_sr+1]                                                 */
+    const uint8_t *sr_seq;        /* nt4                                                      */
+} pr_own_batch;
+int pr_iter_upload_owned(pr_ctx *ctx, const pr_own_batch *b);
+
 /* enqueue (ctx stream) the per-iteration statistic of the resident consensus:
  * dev_out[0] = corrected bases, dev_out[1] = bases with phred >= min_phred.
  * dev_out is DEVICE memory (e.g. a tensor gathered with RCCL all_reduce across

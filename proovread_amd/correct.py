@@ -71,6 +71,7 @@ class LoopConfig:
     tasks: Optional[Tuple[str, ...]] = None   # None: the mode's task list (proovread.cfg:105-127)
     seed_threads: int = 0
     bin_filter: bool = True                # bwa-proovread -b/-l in every iteration (proovread:1302-1313)
+    exact_layout: bool = False             # world 1: run the multi-GPU exact-parity layout anyway (tests)
 
 
 @dataclasses.dataclass
@@ -186,42 +187,50 @@ class GpuStages:
         it.launch(opts, params)
         return [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
 
-    def align(self, d, task: str) -> List[tuple]:
-        """bwa-mode SW of d's seeds (pr_sw_run): the reported alignments in SAM order, read by
-        read, as (sr, lr, strand, pos, score, flag, cigar ops)."""
-        from . import sw
-        res = sw.run(d.sw_input(), T.options(task)[1], ctx=self.ctx)
-        out = []
-        for i in range(res.n):
-            if res["status"][i] != 0 or not res["pass"][i]:
-                continue
-            t = int(res["task"][i])
-            out.append((int(d.t_sr[t]), int(d.t_lr[t]), int(d.t_strand[t]), int(res["pos"][i]), int(res["score"][i]),
-                        int(res["flag"][i]), [int(x) for x in res.cigar_ops(i)]))
-        return out
-
-    def consensus(self, ids: List[str], ref_seq: List[bytes], ref_qual: List[bytes], sams: List[List[str]],
-                  params) -> List[tuple]:
-        """bam2cns on records already in samtools order (pr_cns_run) -> per long read (status,
-        seq, qual, chim lines)."""
-        from . import cns
-        reads = [cns.LongRead(ids[i], ref_seq[i].decode("latin-1"), ref_qual[i].decode("latin-1"))
-                 for i in range(len(ids))]
-        alns = [[cns.SamRecord.from_line(x) for x in v] for v in sams]
-        res = cns.run_chunk(reads, alns, params, ctx=self.ctx)
-        return [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in res]
-
-    def seed(self, lr_map, lr_off, sr, sr_off, seed_opts, comm):
-        """bwa-mode seeds of this rank's short reads on the device: the index of the whole
-        mapping reference built in HBM (pr_seed_gpu_index_build, the host build's tables byte for
-        byte) and pr_seed_gpu_map over the rank's contiguous short-read shard (the host path's
-        task lists exactly, tests/test_seed_gpu.py)."""
-        from . import exact_shard as ex, seed
-        s, e = (0, len(sr_off) - 1) if comm is None or comm.world == 1 else ex.sr_range(len(sr_off) - 1, comm.world,
-                                                                                         comm.rank)
+    def owned_iteration(self, lr_map, lr_off, sr, sr_off, task: str, params, ref_seq: np.ndarray,
+                        ref_qual: np.ndarray, bin_filter, comm, mask_cfg=None):
+        """The exact-parity multi-GPU layout for one task, on the device end to
+        end: the index of ALL long reads in HBM, this rank's contiguous short-read shard seeded
+        and aligned (bwa mode), every reported alignment sent to the owner of its long read
+        (pr_aln_exchange: device pack + one RCCL all-to-all of device buffers), the -b/-l
+        filter, hand-off and consensus of the owned reads, and (mask_cfg = (hcr-mask,
+        min_sr_length)) their masking on the resident consensus.  -> (lo, hi, per owned read
+        (status, seq, qual, chim lines), seeds of this rank, (masked, bpt, bpN) or None)."""
+        from . import _abi, exact_shard as ex, iteration, mask, seed
+        world, rank = (comm.world, comm.rank) if comm is not None else (1, 0)
+        n_sr = len(sr_off) - 1
+        s, e = ex.sr_range(n_sr, world, rank)
+        bounds = ex.lr_bounds(lr_off, world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         ix = seed.DeviceSeedIndex(self.ctx, lr_map, lr_off)
-        tk, _ = ix.map(sr[sr_off[s]:sr_off[e]], sr_off[s:e + 1] - sr_off[s], seed_opts)
-        tk["sr"] += s
+        a0, a1 = int(sr_off[s]), int(sr_off[e])
+        ix.map(sr[a0:a1], np.asarray(sr_off[s:e + 1]) - a0, T.options(task)[0], keep_on_device=True)
+        n_seeds = ix.seed_count()
+        opts = T.options(task)[1]
+        if bin_filter:
+            opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
+        iteration.shard_sw(self.ctx, opts, sr, sr_off, s, e, lr_map, lr_off)
+        iteration.exchange(self.ctx, comm if isinstance(comm, RcclComm) else None, s, bounds)
+        it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, ref_seq, ref_qual, sr, sr_off)
+        it.launch(opts, params)
+        out = [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
+        mres = None
+        if mask_cfg is not None:
+            buf = _abi.DevBuffer(self.ctx, 16)
+            it.mask_to(buf.ptr, mask.params(mask_cfg[0], mask_cfg[1]))
+            masked = it.masked()
+            st = buf.download(np.int64)
+            buf.close()
+            mres = (masked, int(st[0]), int(st[1]))
+        return lo, hi, out, n_seeds, mres
+
+    def seed(self, lr_map, lr_off, sr, sr_off, seed_opts):
+        """bwa-mode seeds of the short reads on the device: the index of the whole mapping
+        reference built in HBM (pr_seed_gpu_index_build, the host build's tables byte for byte)
+        and pr_seed_gpu_map (the host path's task lists exactly, tests/test_seed_gpu.py)."""
+        from . import seed
+        ix = seed.DeviceSeedIndex(self.ctx, lr_map, lr_off)
+        tk, _ = ix.map(sr, sr_off, seed_opts)
         return tk
 
     def mask(self, seqs: List[bytes], quals: List[bytes], hcr_mask: str, min_sr_length: int):
@@ -229,6 +238,16 @@ class GpuStages:
         from . import mask
         masked, _, (bpt, bpn) = mask.run(seqs, quals, mask.params(hcr_mask, min_sr_length), ctx=self.ctx)
         return masked, bpt, bpn
+
+
+def _seed_tasks(lr_map, lr_off, sr, sr_off, seed_opts, threads):
+    """bwa-mode seeds of every short read on the host (pr_seed_map)."""
+    from . import seed
+    ix = seed.SeedIndex(lr_map, lr_off)
+    try:
+        return ix.map(sr, sr_off, seed_opts, threads=threads)
+    finally:
+        ix.close()
 
 
 def _seeds_dataset(lr_map: np.ndarray, lr_off: np.ndarray, sr: np.ndarray, sr_off: np.ndarray, tasks: np.ndarray):
@@ -251,79 +270,20 @@ def _rename(lines: List[str], rid: str) -> List[str]:
 
 # ---------------------------------------------------------------------------- multi-rank
 # The collectives of the multi-rank loop (comm.py).  Layout: SURVEY.md §8e's exact-parity
-# option (exact_shard.py): every rank keeps the whole read set and its index, seeds and
-# aligns a contiguous shard of the sampled short reads (bwa mode: every read's alignment is
-# decided on one rank, as bwa decides it over all long reads), sends each reported
-# alignment to the owner of its long read (all-to-all), corrects and masks the long reads
-# it owns; the corrected and masked reads are then all-gathered for the next task's index
-# and consensus reference, and bpt/bpN all-reduced so every rank takes the same
-# mask_shortcut decision (the north star's per-iteration statistics gather).  GPU ranks use comm.RcclComm (RCCL inside
-# libprgpu); the CPU tests use comm.TorchComm (gloo).
+# option (exact_shard.py): every rank keeps the whole read set and the index of all long
+# reads, seeds and aligns a contiguous shard of the sampled short reads (bwa mode: every
+# read's alignment is decided on one rank, as bwa decides it over all long reads), sends
+# each reported alignment to the owner of its long read and corrects and masks the long
+# reads it owns (stages.owned_iteration; GpuStages does all of it on the device, the
+# alignments crossing GPUs as one RCCL all-to-all of device buffers); the corrected and
+# masked reads are then all-gathered for the next task's index and consensus reference,
+# and bpt/bpN all-reduced so every rank takes the same mask_shortcut decision (the north
+# star's per-iteration statistics gather).  GPU ranks use comm.RcclComm (RCCL inside
+# libprgpu); the CPU tests use comm.TorchComm (gloo) with the oracle stages.
 from .comm import RcclComm, TorchComm  # noqa: E402
 Comm = TorchComm
 
 
-def _seed_tasks(lr_map, lr_off, sr, sr_off, seed_opts, threads, comm):
-    """bwa-mode seeds of this rank's short reads (global ids; every short read on one rank)."""
-    from . import exact_shard as ex, seed
-    ix = seed.SeedIndex(lr_map, lr_off)
-    try:
-        if comm is None or comm.world == 1:
-            return ix.map(sr, sr_off, seed_opts, threads=threads)
-        s, e = ex.sr_range(len(sr_off) - 1, comm.world, comm.rank)
-        tk = ix.map(sr[sr_off[s]:sr_off[e]], sr_off[s:e + 1] - sr_off[s], seed_opts, threads=threads)
-    finally:
-        ix.close()
-    tk["sr"] += s
-    return tk
-
-
-_ASC = np.frombuffer(b"ACGTN", np.uint8)
-
-
-def _records_by_owner(recs, sr, sr_off, lr_off, comm, bin_filter):
-    """Multi-rank layout: this rank's reported alignments (SAM order, read by read) go to the
-    owners of their long reads (one all-to-all of fixed fields + one of CIGAR ops); the owner
-    gets them source-rank-major, i.e. in the single run's read order, applies bwa-proovread's
-    -b/-l filter in that order and returns, per owned long read, its SAM lines in samtools
-    coordinate order (POS, strand, arrival)."""
-    from . import exact_shard as ex
-    from .bwa_proovread import BinFilter, aln_length
-    b = ex.lr_bounds(lr_off, comm.world)
-    lo, hi = int(b[comm.rank]), int(b[comm.rank + 1])
-    fix = np.array([r[:6] + (len(r[6]),) for r in recs], np.int32).reshape(-1, 7)
-    own = np.searchsorted(b, fix[:, 1].astype(np.int64), side="right") - 1 if len(fix) else np.zeros(0, np.int64)
-    order = np.argsort(own, kind="stable")
-    counts = np.bincount(own, minlength=comm.world).astype(np.int64)
-    got = comm.alltoallv_rows(np.ascontiguousarray(fix[order]), counts)
-    cig = [np.asarray(recs[i][6], np.int32) for i in order]
-    cig_rows = np.concatenate(cig).reshape(-1, 1) if cig else np.zeros((0, 1), np.int32)
-    per_dst = np.zeros(comm.world, np.int64)
-    for k, i in enumerate(order):
-        per_dst[own[i]] += len(recs[i][6])
-    got_cig = comm.alltoallv_rows(np.ascontiguousarray(cig_rows, np.int32), per_dst).reshape(-1)
-    filt = BinFilter(*bin_filter) if bin_filter else None
-    per_lr = [[] for _ in range(hi - lo)]
-    c = 0
-    for k in range(len(got)):
-        srid, lr, strand, pos, score, flag, nc = (int(x) for x in got[k])
-        ops = got_cig[c:c + nc]
-        c += nc
-        q = sr[sr_off[srid]:sr_off[srid + 1]]
-        seq = (_ASC[np.where(q < 4, 3 - q, 4)][::-1] if strand else _ASC[q]).tobytes().decode()
-        cg = "".join(f"{int(x) >> 4}{'MIDNSHP=X'[int(x) & 15]}" for x in ops)
-        keep = filt.add(lr, pos + 1, aln_length(cg, len(q)), float(score)) if filt else None
-        per_lr[lr - lo].append((pos, strand, k, keep, f"sr{srid}\t{flag}\tlr{lr}\t{pos + 1}\t60\t{cg}\t*\t0\t0\t"
-                                                      f"{seq}\t*\tAS:i:{score}"))
-    out = []
-    for v in per_lr:
-        if filt is not None:
-            v = [x for x in v if filt.alive[x[3]]]
-        out.append([x[4] for x in sorted(v, key=lambda x: (x[0], x[1], x[2]))])
-    return out, lo, hi
-
-
-# ---------------------------------------------------------------------------- the loop
 # ---------------------------------------------------------------------------- the loop
 def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes, cfg: Optional[LoopConfig] = None,
         stages=None, comm=None) -> LoopResult:
@@ -365,27 +325,28 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         ref_map = reads.seqs if finish else mapped     # finish maps to the unmasked .fq (proovread:838-850)
         lr_map, lr_off = reads.pool(ref_map)
         lr_map = NT4[lr_map]
-        if hasattr(stages, "seed"):   # device stages: index and seeding in HBM
-            tk = stages.seed(lr_map, lr_off, sr, sr_off, T.options(task)[0], comm)
-        else:
-            tk = _seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], cfg.seed_threads, comm)
-        ent.n_tasks = int(len(tk))
-        d = _seeds_dataset(lr_map, lr_off, sr, sr_off, tk)
         max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541
         params = cns.CnsParams(coverage=max_cov, use_ref_qual=not finish, detect_chimera=finish,
                                max_ins_length=0)
         # bwa-proovread -b BIN -l BIN*min(cov, task cov) (proovread:1302-1313, cfg bin-size)
         bsz = T.bin_size(mode)
         binf = (bsz, bsz * min(cfg.coverage, task_cov)) if cfg.bin_filter else None
-        if comm is None or comm.world == 1:
+        ref_seq, _ = reads.pool(reads.seqs)
+        ref_qual, _ = reads.pool(reads.quals)
+        mres = None
+        if (comm is None or comm.world == 1) and not cfg.exact_layout:
+            if hasattr(stages, "seed"):   # device stages: index and seeding in HBM
+                tk = stages.seed(lr_map, lr_off, sr, sr_off, T.options(task)[0])
+            else:
+                tk = _seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], cfg.seed_threads)
+            ent.n_tasks = int(len(tk))
+            d = _seeds_dataset(lr_map, lr_off, sr, sr_off, tk)
             lo, hi = 0, len(reads.ids)
-            ref_seq, _ = reads.pool(reads.seqs)
-            ref_qual, _ = reads.pool(reads.quals)
             out = stages.iteration(d, ref_seq, ref_qual, task, params, bin_filter=binf)
-        else:   # short-read shards -> alignments -> owners of the long reads -> consensus
-            sams, lo, hi = _records_by_owner(stages.align(d, task), sr, sr_off, lr_off, comm, binf)
-            out = stages.consensus([f"lr{i}" for i in range(lo, hi)], reads.seqs[lo:hi], reads.quals[lo:hi], sams,
-                                   params) if hi > lo else []
+        else:   # exact-parity layout: short-read shards -> alignments to the long reads' owners
+            lo, hi, out, ent.n_tasks, mres = stages.owned_iteration(
+                lr_map, lr_off, sr, sr_off, task, params, ref_seq, ref_qual, binf, comm,
+                None if finish else (hcr_mask_for(task), min_sr))
         ids = reads.ids[lo:hi]
         seqs, quals, lines = [], [], []
         for i, (st, s, q, ch) in enumerate(out):
@@ -396,7 +357,9 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
             if finish:
                 lines += _rename(ch, ids[i])
         masked, bpt, bpn = [], 0, 0
-        if not finish and seqs:
+        if mres is not None:
+            masked, bpt, bpn = mres
+        elif not finish and seqs:
             masked, bpt, bpn = stages.mask(seqs, quals, hcr_mask_for(task), min_sr)
         if comm is not None and comm.world > 1:
             seqs, quals = comm.allgather_lists(seqs), comm.allgather_lists(quals)

@@ -208,6 +208,38 @@ extern "C" int pr_comm_alltoallv_host(pr_comm *c, const uint8_t *send, const int
     return 0;
 }
 
+// all-to-all of device byte blocks (the exact-parity layout's alignment exchange,
+// pr_aln_exchange): asynchronous on the context stream, point-to-point pairs in one group
+// (xGMI is point to point: every pair of GPUs has its own link)
+extern "C" int pr_comm_alltoallv_dev(pr_comm *c, const void *send, const int64_t *send_counts, void *recv,
+                                     const int64_t *recv_counts) {
+    if (!c || !send_counts || !recv_counts) return pr_set_error(PR_ERR_ARG, "null arg");
+    const int W = c->world;
+    int64_t st = 0, rt = 0;
+    for (int r = 0; r < W; ++r) {
+        if (send_counts[r] < 0 || recv_counts[r] < 0) return pr_set_error(PR_ERR_ARG, "negative count");
+        st += send_counts[r];
+        rt += recv_counts[r];
+    }
+    if ((st && !send) || (rt && !recv)) return pr_set_error(PR_ERR_ARG, "null buffer");
+    hipStream_t s = ctx_stream(c->ctx);
+    HIPCHK(hipSetDevice(ctx_device(c->ctx)));
+    const uint8_t *ds = (const uint8_t *)send;
+    uint8_t *dr = (uint8_t *)recv;
+    NCCLCHK(ncclGroupStart());
+    int64_t so = 0, ro = 0;
+    for (int r = 0; r < W; ++r) {
+        if (send_counts[r]) NCCLCHK(ncclSend(ds + so, (size_t)send_counts[r], ncclUint8, r, c->nc, s));
+        if (recv_counts[r]) NCCLCHK(ncclRecv(dr + ro, (size_t)recv_counts[r], ncclUint8, r, c->nc, s));
+        so += send_counts[r];
+        ro += recv_counts[r];
+    }
+    NCCLCHK(ncclGroupEnd());
+    return 0;
+}
+
+pr_ctx *comm_ctx(pr_comm *c) { return c ? c->ctx : nullptr; }
+
 // the counts exchange of an all-to-all: recv_counts[r] = what rank r sends to this rank
 extern "C" int pr_comm_alltoall_counts(pr_comm *c, const int64_t *send_counts, int64_t *recv_counts) {
     if (!c || !send_counts || !recv_counts) return pr_set_error(PR_ERR_ARG, "null arg");

@@ -18,9 +18,12 @@
 #include "mask_dev.h"
 #include "seed_dev.h"
 #include "seed_index_dev.h"
+#include "xchg_dev.h"
 
 using namespace prgpu;
 int sw_get_ptrs(pr_ctx *c, SwPtrs *p);
+int sw_xchg_send(pr_ctx *c, XchgSend *X);
+pr_ctx *comm_ctx(pr_comm *c);
 int sw_get_pipe_ptrs(pr_ctx *c, SwPtrs *p, bool regroup);
 int sw_upload_device_seeds(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h);
 
@@ -85,6 +88,14 @@ enum SeedBufId {
     SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SB_NEXT, SB_PRE, SB_DENSE,
     SX_LRSEQ, SX_KEY0, SX_KEY1, SX_VAL0, SX_KC, SX_CNTPTR, SX_TEMP, SD_COUNT
 };
+// the exact-parity layout's exchange (pr_aln_exchange, owned batches): bounds, sort keys and
+// indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
+// the task's short reads
+enum XchgBufId {
+    XB_BOUNDS, XB_KEY0, XB_KEY1, XB_IDX0, XB_IDX1, XB_CNT, XB_OPIN, XB_OPAT, XB_SREC, XB_SCIG, XB_TEMP,
+    XB_RREC, XB_RCIG, XB_RCIGAT, XB_GCNT, XB_GCNT64, XB_TASKOFF, XB_ERR, XB_GSR, XB_GSTATUS, XB_GPOS, XB_GSCORE,
+    XB_GNCIG, XB_GCIGAT, XB_GSTRAND, XB_GPASS, XB_SR, XB_SROFF, XB_COUNT
+};
 
 struct pr_ctx {
     int device = 0;
@@ -122,6 +133,12 @@ struct pr_ctx {
     int64_t seed_n_text = 0, seed_n_hits = 0;
     bool iter_masked = false;
     bool cns_launched = false;   // a consensus launch filled the CB_O_* outputs
+    // exact-parity layout: received alignments (pr_aln_exchange) and an owned batch
+    DevBuf xb[XB_COUNT];
+    bool x_ready = false;        // XB_RREC / XB_RCIG hold the last exchange's records
+    int64_t x_nrecv = 0, x_nrcig = 0;
+    bool own = false;            // the resident iteration batch is an owned batch (pr_iter_upload_owned)
+    int32_t own_lr0 = 0;
 };
 
 extern "C" int pr_device_count(int *n) {
@@ -161,6 +178,7 @@ extern "C" void pr_ctx_destroy(pr_ctx *c) {
     for (auto &b : c->cb) b.release();
     for (auto &b : c->mb) b.release();
     for (auto &b : c->sd) b.release();
+    for (auto &b : c->xb) b.release();
     sw_release(c->sw);
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -262,6 +280,7 @@ extern "C" int pr_cns_upload(pr_ctx *c, const pr_cns_batch *b) {
     if (rc) return rc;
     c->cns_launched = false;
     c->iter_masked = false;
+    c->own = false;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     const int n = b->n_lr;
@@ -421,7 +440,15 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         D.bin_off = B[CB_BIN_OFF].as<int64_t>();
         D.bin_bases = B[CB_BIN_BASES].as<int64_t>();
     }
-    if (c->pipe) {
+    if (c->pipe && c->own) {
+        // owned batch: short reads (nt4, global ids) from the task's pool, CIGARs in place in
+        // the received wire pool, the ASCII consensus reference of the owned reads
+        D.ref_seq = B[CB_REF_SEQ].as<uint8_t>();
+        D.ref_nt4 = 0;
+        D.seq = c->xb[XB_SR].as<uint8_t>();
+        D.seq_nt4 = 1;
+        D.cig = c->xb[XB_RCIG].as<uint32_t>();
+    } else if (c->pipe) {
         // consensus reads the SW batch in place: long reads and short reads as
         // nt4, CIGARs in place in the SW output pool (per-task starts: pipe hand-off)
         SwPtrs sp;
@@ -573,6 +600,7 @@ static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds) {
     HIPCHK(hipSetDevice(c->device));
     c->cns_launched = false;
     c->iter_masked = false;
+    c->own = false;
     hipStream_t s = c->stream;
     c->n_lr = n;
     c->n_aln = sb.n_task;
@@ -637,13 +665,333 @@ static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds) {
 extern "C" int pr_iter_upload(pr_ctx *c, const pr_iter_batch *b) { return iter_upload(c, b, false); }
 extern "C" int pr_iter_upload_gpu_seeds(pr_ctx *c, const pr_iter_batch *b) { return iter_upload(c, b, true); }
 
+// ---------------------------------------------------------------------------
+// exact-parity multi-GPU layout (include/prgpu.h: pr_sw_upload_gpu_seeds, pr_aln_exchange,
+// pr_iter_upload_owned, then pr_iter_launch on the owned batch)
+extern "C" int pr_sw_upload_gpu_seeds(pr_ctx *c, const pr_sw_batch *b) {
+    if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
+    if (c->seed_pre.size() != (size_t)b->n_sr + 1)
+        return set_error(PR_ERR_ARG, "no device seeds for these short reads (pr_seed_gpu_map with out = NULL first)");
+    pr_sw_batch sb = *b;
+    sb.n_task = c->seed_pre.back();
+    sb.t_sr = sb.t_lr = sb.t_qbeg = sb.t_rbeg = sb.t_slen = sb.t_chain = nullptr;
+    sb.t_strand = nullptr;
+    return sw_upload_device_seeds(c, &sb, c->sd[SB_DENSE].as<pr_seed_task>(), c->seed_pre.data());
+}
+
+// the sender half of the exchange: the reported alignments of the last bwa-mode pr_sw_launch
+// packed by owner into XB_SREC / XB_SCIG; counts (records, ops) per owner into cnt (syncs)
+static int xchg_pack(pr_ctx *c, int world, int64_t sr0, const int64_t *lr_bounds, std::vector<int64_t> &n_rec,
+                     std::vector<int64_t> &n_ops) {
+    if (world < 1 || world > 64) return set_error(PR_ERR_CAPACITY, "1 to 64 ranks");
+    if (lr_bounds[0] != 0) return set_error(PR_ERR_ARG, "lr_bounds must start at 0");
+    for (int r = 0; r < world; ++r)
+        if (lr_bounds[r + 1] < lr_bounds[r]) return set_error(PR_ERR_ARG, "lr_bounds must be ascending");
+    XchgSend X;
+    std::memset(&X, 0, sizeof X);
+    int rc;
+    if ((rc = sw_xchg_send(c, &X))) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    DevBuf *B = c->xb;
+    const size_t n1 = (size_t)X.n + 1;
+    if ((rc = upload(B[XB_BOUNDS], lr_bounds, (size_t)world + 1, s)) || (rc = B[XB_KEY0].ensure(n1 * 4)) ||
+        (rc = B[XB_KEY1].ensure(n1 * 4)) || (rc = B[XB_IDX0].ensure(n1 * 4)) || (rc = B[XB_IDX1].ensure(n1 * 4)) ||
+        (rc = B[XB_CNT].ensure(2 * 65 * 8)) || (rc = B[XB_OPIN].ensure(n1 * 8)) || (rc = B[XB_OPAT].ensure(n1 * 8)) ||
+        (rc = B[XB_SREC].ensure(n1 * sizeof(XRec))))
+        return rc;
+    const size_t tb = xchg_temp_bytes(X.n, 1);
+    if ((rc = B[XB_TEMP].ensure(tb))) return rc;
+    X.bounds = B[XB_BOUNDS].as<int64_t>();
+    X.world = world;
+    X.sr0 = sr0;
+    X.key0 = B[XB_KEY0].as<int32_t>();
+    X.key1 = B[XB_KEY1].as<int32_t>();
+    X.idx0 = B[XB_IDX0].as<int32_t>();
+    X.idx1 = B[XB_IDX1].as<int32_t>();
+    X.cnt = B[XB_CNT].as<unsigned long long>();
+    X.op_in = B[XB_OPIN].as<int64_t>();
+    X.op_at = B[XB_OPAT].as<int64_t>();
+    X.rec = B[XB_SREC].as<XRec>();
+    int e = xchg_pack_launch(X, B[XB_TEMP].p, B[XB_TEMP].cap, (void *)s);
+    if (e) return set_error(PR_ERR_HIP, "exchange pack: %s", hipGetErrorString((hipError_t)e));
+    std::vector<unsigned long long> cnt((size_t)2 * (world + 1), 0ull);
+    HIPCHK(hipMemcpyAsync(cnt.data(), X.cnt, cnt.size() * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    n_rec.assign((size_t)world, 0);
+    n_ops.assign((size_t)world, 0);
+    int64_t ops = 0;
+    for (int r = 0; r < world; ++r) {
+        n_rec[(size_t)r] = (int64_t)cnt[(size_t)r];
+        n_ops[(size_t)r] = (int64_t)cnt[(size_t)world + 1 + r];
+        ops += n_ops[(size_t)r];
+    }
+    if ((rc = B[XB_SCIG].ensure(((size_t)ops + 1) * 4))) return rc;
+    X.wcig = B[XB_SCIG].as<uint32_t>();
+    if ((e = xchg_write_launch(X, (void *)s))) return set_error(PR_ERR_HIP, "exchange pack: %s", hipGetErrorString((hipError_t)e));
+    return 0;
+}
+
+static int xchg_recv_buffers(pr_ctx *c, int64_t rec_bytes, int64_t cig_bytes) {
+    if (rec_bytes % (int64_t)sizeof(XRec)) return set_error(PR_ERR_ARG, "exchange: ragged record counts");
+    c->x_nrecv = rec_bytes / (int64_t)sizeof(XRec);
+    c->x_nrcig = cig_bytes / 4;
+    int rc;
+    if ((rc = c->xb[XB_RREC].ensure((size_t)rec_bytes + sizeof(XRec))) || (rc = c->xb[XB_RCIG].ensure((size_t)cig_bytes + 64)))
+        return rc;
+    return 0;
+}
+
+extern "C" int pr_aln_exchange(pr_ctx *c, pr_comm *comm, int64_t sr0, const int64_t *lr_bounds, int64_t *n_recv) {
+    if (!c || !lr_bounds) return set_error(PR_ERR_ARG, "null arg");
+    int rank = 0, world = 1, rc;
+    if (comm) {
+        if (comm_ctx(comm) != c) return set_error(PR_ERR_ARG, "the communicator belongs to another context");
+        if ((rc = pr_comm_rank(comm, &rank, &world))) return rc;
+    }
+    c->x_ready = false;
+    std::vector<int64_t> nrec, nops;
+    if ((rc = xchg_pack(c, world, sr0, lr_bounds, nrec, nops))) return rc;
+    std::vector<int64_t> sc_rec((size_t)world), sc_cig((size_t)world), rc_rec((size_t)world), rc_cig((size_t)world);
+    for (int r = 0; r < world; ++r) {
+        sc_rec[(size_t)r] = nrec[(size_t)r] * (int64_t)sizeof(XRec);
+        sc_cig[(size_t)r] = nops[(size_t)r] * 4;
+    }
+    if (comm) {
+        if ((rc = pr_comm_alltoall_counts(comm, sc_rec.data(), rc_rec.data())) ||
+            (rc = pr_comm_alltoall_counts(comm, sc_cig.data(), rc_cig.data())))
+            return rc;
+    } else {
+        rc_rec = sc_rec;
+        rc_cig = sc_cig;
+    }
+    int64_t nr = 0, nc = 0;
+    for (int r = 0; r < world; ++r) {
+        nr += rc_rec[(size_t)r];
+        nc += rc_cig[(size_t)r];
+    }
+    if ((rc = xchg_recv_buffers(c, nr, nc))) return rc;
+    DevBuf *B = c->xb;
+    if (comm) {
+        if ((rc = pr_comm_alltoallv_dev(comm, B[XB_SREC].p, sc_rec.data(), B[XB_RREC].p, rc_rec.data())) ||
+            (rc = pr_comm_alltoallv_dev(comm, B[XB_SCIG].p, sc_cig.data(), B[XB_RCIG].p, rc_cig.data())))
+            return rc;
+    } else {
+        HIPCHK(hipSetDevice(c->device));
+        if (nr) HIPCHK(hipMemcpyAsync(B[XB_RREC].p, B[XB_SREC].p, (size_t)nr, hipMemcpyDeviceToDevice, c->stream));
+        if (nc) HIPCHK(hipMemcpyAsync(B[XB_RCIG].p, B[XB_SCIG].p, (size_t)nc, hipMemcpyDeviceToDevice, c->stream));
+    }
+    c->x_ready = true;
+    if (n_recv) *n_recv = c->x_nrecv;
+    return 0;
+}
+
+extern "C" int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64_t *sr0, const int64_t *lr_bounds,
+                                     int64_t *n_recv) {
+    // the same exchange among `world` contexts of one process (e.g. several shards on one GPU):
+    // the packs, then device-to-device block copies in source order instead of RCCL
+    if (!ctxs || !sr0 || !lr_bounds || world < 1) return set_error(PR_ERR_ARG, "bad arg");
+    std::vector<std::vector<int64_t>> nrec((size_t)world), nops((size_t)world);
+    int rc;
+    for (int k = 0; k < world; ++k) {
+        if (!ctxs[k]) return set_error(PR_ERR_ARG, "null context");
+        ctxs[k]->x_ready = false;
+        if ((rc = xchg_pack(ctxs[k], world, sr0[k], lr_bounds, nrec[(size_t)k], nops[(size_t)k]))) return rc;
+    }
+    for (int k = 0; k < world; ++k) {
+        HIPCHK(hipSetDevice(ctxs[k]->device));
+        HIPCHK(hipStreamSynchronize(ctxs[k]->stream));
+    }
+    for (int r = 0; r < world; ++r) {
+        pr_ctx *d = ctxs[r];
+        int64_t nr = 0, nc = 0;
+        for (int k = 0; k < world; ++k) {
+            nr += nrec[(size_t)k][(size_t)r] * (int64_t)sizeof(XRec);
+            nc += nops[(size_t)k][(size_t)r] * 4;
+        }
+        if ((rc = xchg_recv_buffers(d, nr, nc))) return rc;
+        int64_t ro = 0, co = 0;
+        for (int k = 0; k < world; ++k) {
+            int64_t so = 0, sco = 0;   // this destination's block in the source's send buffers
+            for (int q = 0; q < r; ++q) {
+                so += nrec[(size_t)k][(size_t)q] * (int64_t)sizeof(XRec);
+                sco += nops[(size_t)k][(size_t)q] * 4;
+            }
+            const int64_t bn = nrec[(size_t)k][(size_t)r] * (int64_t)sizeof(XRec), bc = nops[(size_t)k][(size_t)r] * 4;
+            HIPCHK(hipSetDevice(d->device));
+            if (bn) HIPCHK(hipMemcpyAsync((uint8_t *)d->xb[XB_RREC].p + ro, (uint8_t *)ctxs[k]->xb[XB_SREC].p + so,
+                                          (size_t)bn, hipMemcpyDeviceToDevice, d->stream));
+            if (bc) HIPCHK(hipMemcpyAsync((uint8_t *)d->xb[XB_RCIG].p + co, (uint8_t *)ctxs[k]->xb[XB_SCIG].p + sco,
+                                          (size_t)bc, hipMemcpyDeviceToDevice, d->stream));
+            ro += bn;
+            co += bc;
+        }
+        HIPCHK(hipStreamSynchronize(d->stream));
+        d->x_ready = true;
+        if (n_recv) n_recv[r] = d->x_nrecv;
+    }
+    return 0;
+}
+
+extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
+    if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->x_ready) return set_error(PR_ERR_ARG, "no received alignments (pr_aln_exchange first)");
+    const int n = b->n_lr;
+    if (n < 0 || b->n_sr < 0 || (n && (!b->lr_off || !b->ref_seq)) || !b->sr_off || (b->n_sr && !b->sr_seq))
+        return set_error(PR_ERR_ARG, "owned batch: lr_off, ref_seq and the short reads are required");
+    if (n && b->lr_off[0] != 0) return set_error(PR_ERR_ARG, "lr_off must start at 0");
+    for (int i = 0; i < n; ++i)
+        if (b->lr_off[i + 1] < b->lr_off[i]) return set_error(PR_ERR_ARG, "lr_off not monotone");
+    for (int i = 0; i < b->n_sr; ++i)
+        if (b->sr_off[i + 1] < b->sr_off[i]) return set_error(PR_ERR_ARG, "sr_off not monotone");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc;
+    c->cns_launched = false;
+    c->iter_masked = false;
+    c->n_lr = n;
+    c->n_aln = c->x_nrecv;
+    const int64_t tl = n ? b->lr_off[n] : 0;
+    c->total_cols = tl;
+    c->has_ref = true;
+    c->pipe_ref_ascii = true;
+    c->has_qual = b->lr_qual != nullptr;
+    c->has_ign = false;
+    c->lr_off_host.assign(b->lr_off, b->lr_off + n + 1);
+    if (!n) c->lr_off_host.assign(1, 0);
+    c->out_off.assign(n + 1, 0);
+    c->chim_off.assign(n + 1, 0);
+    for (int i = 0; i < n; ++i) {
+        const int64_t L = b->lr_off[i + 1] - b->lr_off[i];
+        const int64_t nb = (int64_t)((double)L / 20.0) + 1;
+        c->out_off[i + 1] = c->out_off[i] + 2 * L + 1024;   // guarded in the kernel
+        c->chim_off[i + 1] = c->chim_off[i] + nb / 2 + 2;
+    }
+    c->seq_cap = c->out_off[n];
+    c->chim_cap = c->chim_off[n];
+    c->alg_bytes = 0;
+    c->k_need = 1;
+    c->pipe_sort_cap = 1;
+    DevBuf *B = c->cb;
+    const size_t na1 = (size_t)c->x_nrecv + 1, n1 = (size_t)n + 1;
+    if ((rc = upload(B[CB_LR_OFF], c->lr_off_host.data(), n1, s))) return rc;
+    if (b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)tl, s))) return rc;
+    if ((rc = upload(B[CB_REF_SEQ], b->ref_seq, (size_t)tl, s))) return rc;
+    if ((rc = upload(c->xb[XB_SR], b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
+        (rc = upload(c->xb[XB_SROFF], b->sr_off, (size_t)b->n_sr + 1, s)))
+        return rc;
+    if ((rc = c->pb[1].ensure(n1 * 4)) || (rc = c->pb[2].ensure(n1 * 4))) return rc;
+    if ((rc = B[CB_ALN_OFF].ensure(n1 * 8)) || (rc = B[CB_POS].ensure(na1 * 4)) ||
+        (rc = B[CB_SCORE].ensure(na1 * 8)) || (rc = B[CB_AFLAGS].ensure(na1)) ||
+        (rc = B[CB_SEQ_OFF].ensure(na1 * 8)) || (rc = B[CB_LSEQ].ensure(na1 * 4)) ||
+        (rc = B[CB_CIG_OFF].ensure(na1 * 8)) || (rc = B[CB_NCIG].ensure(na1 * 4)))
+        return rc;
+    if ((rc = B[CB_A_ST].ensure(na1 * 4)) || (rc = B[CB_A_LEN].ensure(na1 * 4)) ||
+        (rc = B[CB_A_NC].ensure(na1 * 8)) || (rc = B[CB_A_BIN].ensure(na1 * 4)) ||
+        (rc = B[CB_A_CB].ensure(na1 * 4)) || (rc = B[CB_A_CE].ensure(na1 * 4)) ||
+        (rc = B[CB_A_SB].ensure(na1 * 4)) || (rc = B[CB_A_RPOS].ensure(na1 * 4)) ||
+        (rc = B[CB_A_END].ensure(na1 * 4)) || (rc = B[CB_SORTED].ensure(na1 * 4)) ||
+        (rc = B[CB_LST_SCORE].ensure(na1 * 8)) || (rc = B[CB_LST_ALN].ensure(na1 * 4)) ||
+        (rc = B[CB_KEPT].ensure(na1)) || (rc = B[CB_WORK].ensure(64)) ||
+        (rc = B[CB_PROF].ensure(CNS_NPHASE * 8)) || (rc = B[CB_RETRY].ensure(((size_t)n + 16) * 4)))
+        return rc;
+    if ((rc = upload(B[CB_OUT_OFF], c->out_off.data(), n1, s))) return rc;
+    if ((rc = upload(B[CB_CHIM_OFF], c->chim_off.data(), n1, s))) return rc;
+    if ((rc = B[CB_STATUS].ensure(n1 * 4)) || (rc = B[CB_SEQ_LEN].ensure(n1 * 4)) ||
+        (rc = B[CB_TRACE_LEN].ensure(n1 * 4)) || (rc = B[CB_NCIGAR].ensure(n1 * 4)) ||
+        (rc = B[CB_NCHIM].ensure(n1 * 4)))
+        return rc;
+    const size_t scap = (size_t)c->seq_cap + 1;
+    if ((rc = B[CB_O_SEQ].ensure(scap)) || (rc = B[CB_O_QUAL].ensure(scap)) || (rc = B[CB_O_TRACE].ensure(scap)) ||
+        (rc = B[CB_O_CIG].ensure(scap * 4)) || (rc = B[CB_O_CHIM].ensure(((size_t)c->chim_cap + 1) * 16)))
+        return rc;
+    // the hand-off's grouped inputs
+    DevBuf *X = c->xb;
+    if ((rc = X[XB_RCIGAT].ensure(na1 * 8)) || (rc = X[XB_GCNT].ensure(n1 * 4)) || (rc = X[XB_GCNT64].ensure(n1 * 8)) ||
+        (rc = X[XB_TASKOFF].ensure(n1 * 8)) || (rc = X[XB_ERR].ensure(16)) || (rc = X[XB_GSR].ensure(na1 * 4)) ||
+        (rc = X[XB_GSTATUS].ensure(na1 * 4)) || (rc = X[XB_GPOS].ensure(na1 * 4)) || (rc = X[XB_GSCORE].ensure(na1 * 4)) ||
+        (rc = X[XB_GNCIG].ensure(na1 * 4)) || (rc = X[XB_GCIGAT].ensure(na1 * 8)) || (rc = X[XB_GSTRAND].ensure(na1)) ||
+        (rc = X[XB_GPASS].ensure(na1)) || (rc = X[XB_KEY0].ensure(na1 * 4)) || (rc = X[XB_KEY1].ensure(na1 * 4)) ||
+        (rc = X[XB_IDX0].ensure(na1 * 4)) || (rc = X[XB_IDX1].ensure(na1 * 4)) || (rc = X[XB_OPIN].ensure(na1 * 8)))
+        return rc;
+    const size_t tb = xchg_temp_bytes(c->x_nrecv, n);
+    if ((rc = X[XB_TEMP].ensure(tb))) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    c->own_lr0 = b->lr0;
+    c->own = true;
+    c->cns_loaded = true;
+    c->pipe = true;
+    return 0;
+}
+
+// owned batch: the received records regrouped by long read into the hand-off's inputs
+static int own_group(pr_ctx *c, SwPtrs *sp) {
+    hipStream_t s = c->stream;
+    DevBuf *B = c->xb;
+    XchgRecv R;
+    std::memset(&R, 0, sizeof R);
+    R.n = c->x_nrecv;
+    R.rec = B[XB_RREC].as<XRec>();
+    R.lr0 = c->own_lr0;
+    R.n_lr = c->n_lr;
+    R.key0 = B[XB_KEY0].as<int32_t>();
+    R.key1 = B[XB_KEY1].as<int32_t>();
+    R.idx0 = B[XB_IDX0].as<int32_t>();
+    R.idx1 = B[XB_IDX1].as<int32_t>();
+    R.cnt = B[XB_GCNT].as<int32_t>();
+    R.cnt64 = B[XB_GCNT64].as<int64_t>();
+    R.task_off = B[XB_TASKOFF].as<int64_t>();
+    R.op_in = B[XB_OPIN].as<int64_t>();
+    R.rcig_at = B[XB_RCIGAT].as<int64_t>();
+    R.err = B[XB_ERR].as<int32_t>();
+    R.o_sr = B[XB_GSR].as<int32_t>();
+    R.o_status = B[XB_GSTATUS].as<int32_t>();
+    R.o_pos = B[XB_GPOS].as<int32_t>();
+    R.o_score = B[XB_GSCORE].as<int32_t>();
+    R.o_ncig = B[XB_GNCIG].as<int32_t>();
+    R.o_cig_at = B[XB_GCIGAT].as<int64_t>();
+    R.o_strand = B[XB_GSTRAND].as<uint8_t>();
+    R.o_pass = B[XB_GPASS].as<uint8_t>();
+    int e = xchg_group_launch(R, B[XB_TEMP].p, B[XB_TEMP].cap, (void *)s);
+    if (e) return set_error(PR_ERR_HIP, "exchange regroup: %s", hipGetErrorString((hipError_t)e));
+    std::vector<int32_t> cnt((size_t)c->n_lr + 1, 0);
+    int32_t err = 0;
+    if (c->n_lr) HIPCHK(hipMemcpyAsync(cnt.data(), R.cnt, (size_t)c->n_lr * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&err, R.err, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (err) return set_error(PR_ERR_ARG, "exchange: a received alignment lies outside the owned long reads");
+    int mx = 0;
+    for (int i = 0; i < c->n_lr; ++i) mx = std::max(mx, cnt[(size_t)i]);
+    std::memset(sp, 0, sizeof *sp);
+    sp->t_sr = R.o_sr;
+    sp->status = R.o_status;
+    sp->pos = R.o_pos;
+    sp->score = R.o_score;
+    sp->ncig = R.o_ncig;
+    sp->cig_at = R.o_cig_at;
+    sp->strand = R.o_strand;
+    sp->pass = R.o_pass;
+    sp->sr_off = B[XB_SROFF].as<int64_t>();
+    sp->cig = B[XB_RCIG].as<uint32_t>();
+    sp->n_task = R.n;
+    sp->task_off = R.task_off;
+    sp->max_per_lr = mx;
+    return 0;
+}
+
 extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_params *p) {
     if (!c || !o || !p) return set_error(PR_ERR_ARG, "null arg");
     if (!c->pipe) return set_error(PR_ERR_ARG, "no resident iteration batch (pr_iter_upload first)");
-    int rc = pr_sw_launch(c, o);   // records ev[2], ev[3], ev[0]
-    if (rc) return rc;
+    int rc;
     SwPtrs sp;
-    if ((rc = sw_get_pipe_ptrs(c, &sp, true))) return rc;
+    if (c->own) {   // owned batch: the SW ran before the exchange
+        HIPCHK(hipSetDevice(c->device));
+        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        if ((rc = own_group(c, &sp))) return rc;
+    } else {
+        if ((rc = pr_sw_launch(c, o))) return rc;   // records ev[2], ev[3], ev[0]
+        if ((rc = sw_get_pipe_ptrs(c, &sp, true))) return rc;
+    }
     if (sp.task_off) {   // bwa mode: the reported alignments grouped by long read on the device
         if (sp.max_per_lr > 16384)
             return set_error(PR_ERR_CAPACITY, "more than 16384 alignments on one long read (%d)", sp.max_per_lr);
@@ -1290,6 +1638,12 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     out->n = total;
     if (status) std::memcpy(status, st.data(), (size_t)n_sr * 4);
     if (bad) return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags)", (long long)bad);
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_seed_count(pr_ctx *c, int64_t *n) {
+    if (!c || !n) return set_error(PR_ERR_ARG, "null arg");
+    *n = c->seed_pre.empty() ? 0 : c->seed_pre.back();
     return 0;
 }
 

@@ -10,6 +10,7 @@
 #include "aln_dev.h"
 #include "sw_dev.h"
 #include "sw_pk.h"
+#include "xchg_dev.h"
 
 using namespace prgpu;
 
@@ -965,6 +966,26 @@ static int bwa_group(pr_ctx *c, SwResident &r, SwPtrs *p) {
     p->n_task = n;
     p->task_off = (const int64_t *)r.buf[SB_GLROFF];
     p->max_per_lr = mx;
+    return 0;
+}
+
+// the exchange's view of the last bwa-mode launch: the reported alignments (SAM order) and the
+// per-task arrays they index (xchg_kernels.hip)
+int sw_xchg_send(pr_ctx *c, XchgSend *X) {
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded || !r.bwa) return pr_set_error(PR_ERR_ARG, "no resident bwa-mode SW launch (pr_sw_launch first)");
+    X->n = r.n_aln;
+    X->alist = (const int32_t *)r.buf[SB_ALIST];
+    X->t_sr = (const int32_t *)r.buf[SB_T_SR];
+    X->t_lr = (const int32_t *)r.buf[SB_T_LR];
+    X->status = (const int32_t *)r.buf[SB_STATUS];
+    X->pos = (const int32_t *)r.buf[SB_POS];
+    X->score = (const int32_t *)r.buf[SB_SCORE];
+    X->ncig = (const int32_t *)r.buf[SB_NCIG];
+    X->strand = (const uint8_t *)r.buf[SB_T_STRAND];
+    X->pass = (const uint8_t *)r.buf[SB_PASS];
+    X->cig_at = (const int64_t *)r.buf[SB_CIGAT];
+    X->cig = (const uint32_t *)r.buf[SB_CIG];
     return 0;
 }
 

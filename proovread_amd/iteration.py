@@ -6,6 +6,7 @@ hand-off into samtools coordinate order, and the consensus of every long read
 from __future__ import annotations
 
 import ctypes as C
+from types import SimpleNamespace
 from typing import List, Optional
 
 import numpy as np
@@ -15,6 +16,11 @@ from . import _abi, cns, sw
 
 class IterBatch(C.Structure):
     _fields_ = [("sw", sw.SwBatch), ("task_lr_off", _abi.P64), ("lr_qual", _abi.PU8), ("ref_seq", _abi.PU8)]
+
+
+class OwnBatch(C.Structure):
+    _fields_ = [("lr0", C.c_int32), ("n_lr", C.c_int32), ("lr_off", _abi.P64), ("ref_seq", _abi.PU8),
+                ("lr_qual", _abi.PU8), ("n_sr", C.c_int32), ("sr_off", _abi.P64), ("sr_seq", _abi.PU8)]
 
 
 def _setup(L):
@@ -30,6 +36,10 @@ def _setup(L):
     L.pr_iter_stats.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     L.pr_ctx_sync.argtypes = [C.c_void_p]
     L.pr_iter_alignment_stats.argtypes = [C.c_void_p, _abi.P64, _abi.P64, _abi.P64]
+    L.pr_sw_upload_gpu_seeds.argtypes = [C.c_void_p, C.POINTER(sw.SwBatch)]
+    L.pr_aln_exchange.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, _abi.P64, _abi.P64]
+    L.pr_aln_exchange_local.argtypes = [C.c_void_p, C.c_int, _abi.P64, _abi.P64, _abi.P64]
+    L.pr_iter_upload_owned.argtypes = [C.c_void_p, C.POINTER(OwnBatch)]
     L._iter_ready = True
 
 
@@ -176,3 +186,94 @@ class Iteration:
                 r.chim = [tuple(int(v) for v in row) for row in a["chim"][4 * c0:4 * (c0 + nch)].reshape(-1, 4)]
             out.append(r)
         return out
+
+
+def shard_sw(ctx, sw_opts: sw.SwOpts, sr: np.ndarray, sr_off: np.ndarray, s: int, e: int, lr_map: np.ndarray,
+             lr_off: np.ndarray) -> None:
+    """Exact-parity layout, step 1 on a rank: bwa-mode SW of the short-read shard [s, e) whose
+    seeds the last DeviceSeedIndex.map(keep_on_device=True) left in HBM (the index of ALL long
+    reads, lr_map / lr_off as mapped); sr 0 of the shard is global id s (bwa's hash ties)."""
+    L = _abi.lib()
+    _setup(L)
+    sr_off = np.asarray(sr_off, np.int64)
+    sh_off = np.ascontiguousarray(sr_off[s:e + 1] - sr_off[s], np.int64)
+    sh_seq = np.ascontiguousarray(sr[sr_off[s]:sr_off[e]], np.uint8)
+    z = np.zeros(0, np.int32)
+    inp = sw.SwInput(sh_off, sh_seq, np.ascontiguousarray(lr_off, np.int64), np.ascontiguousarray(lr_map, np.uint8),
+                     z, z, np.zeros(0, np.uint8), z, z, z)
+    b = inp.c_batch()
+    b.read_id0 = int(s)
+    _abi.check(L.pr_sw_upload_gpu_seeds(ctx.h, C.byref(b)), "pr_sw_upload_gpu_seeds")
+    _abi.check(L.pr_sw_launch(ctx.h, C.byref(sw_opts)), "pr_sw_launch")
+
+
+def exchange(ctx, comm, s: int, bounds: np.ndarray) -> int:
+    """Step 2: every reported alignment of the last shard_sw to the owner of its long read
+    (pr_aln_exchange: device pack, RCCL all-to-all of device buffers; comm None = world 1).
+    Returns the alignments this rank received."""
+    L = _abi.lib()
+    _setup(L)
+    bd = np.ascontiguousarray(bounds, np.int64)
+    nr = C.c_int64()
+    _abi.check(L.pr_aln_exchange(ctx.h, comm.h if comm is not None else None, int(s), _abi.ptr(bd, C.c_int64),
+                                 C.byref(nr)), "pr_aln_exchange")
+    return nr.value
+
+
+def exchange_local(ctxs, starts, bounds: np.ndarray) -> List[int]:
+    """Step 2 among several contexts of this process (pr_aln_exchange_local: the same packs,
+    device copies in place of RCCL): context k holds the shard starting at starts[k]."""
+    L = _abi.lib()
+    _setup(L)
+    w = len(ctxs)
+    hs = (C.c_void_p * w)(*[c.h for c in ctxs])
+    s0 = np.ascontiguousarray(starts, np.int64)
+    bd = np.ascontiguousarray(bounds, np.int64)
+    nr = np.zeros(w, np.int64)
+    _abi.check(L.pr_aln_exchange_local(hs, w, _abi.ptr(s0, C.c_int64), _abi.ptr(bd, C.c_int64),
+                                       _abi.ptr(nr, C.c_int64)), "pr_aln_exchange_local")
+    return [int(x) for x in nr]
+
+
+class OwnedIteration(Iteration):
+    """Step 3 of the exact-parity multi-GPU layout (include/prgpu.h
+    pr_aln_exchange): after shard_sw + exchange, this rank's owned long reads [lo, hi) get the
+    -b/-l filter, hand-off and consensus over the alignments it received (launch(); no SW).
+    The results (download, results, mask_to, stats_to, masked) are those of the owned reads
+    and equal a single-GPU Iteration's on them."""
+
+    def __init__(self, ctx, lo: int, hi: int, lr_off: np.ndarray, ref_seq: np.ndarray,
+                 ref_qual: Optional[np.ndarray], sr: np.ndarray, sr_off: np.ndarray):
+        """lr_off: every long read's offsets; ref_seq / ref_qual: the consensus reference
+        (ASCII, bam2cns --ref) and qualities of all long reads in lr_off's layout (the owned
+        slice is uploaded); sr / sr_off: every short read of the task (nt4), which the
+        consensus reads by global id."""
+        self.L = _abi.lib()
+        _setup(self.L)
+        self.ctx = ctx
+        self.lo, self.hi = lo, hi
+        lr_off = np.asarray(lr_off, np.int64)
+        a0, a1 = int(lr_off[lo]), int(lr_off[hi])
+        if len(ref_seq) != int(lr_off[-1]) or (ref_qual is not None and len(ref_qual) != int(lr_off[-1])):
+            raise ValueError("ref_seq / ref_qual must have every long read's layout (lr_off)")
+        self._own_off = np.ascontiguousarray(lr_off[lo:hi + 1] - a0, np.int64)
+        self._ref = np.ascontiguousarray(ref_seq[a0:a1], np.uint8)
+        self._qual = None if ref_qual is None else np.ascontiguousarray(ref_qual[a0:a1], np.uint8)
+        self._sr = np.ascontiguousarray(sr, np.uint8)
+        self._sr_off = np.ascontiguousarray(sr_off, np.int64)
+        ob = OwnBatch()
+        ob.lr0, ob.n_lr = lo, hi - lo
+        ob.lr_off = _abi.ptr(self._own_off, C.c_int64)
+        ob.ref_seq = _abi.ptr(self._ref, C.c_uint8)
+        if self._qual is not None:
+            ob.lr_qual = _abi.ptr(self._qual, C.c_uint8)
+        ob.n_sr = len(self._sr_off) - 1
+        ob.sr_off = _abi.ptr(self._sr_off, C.c_int64)
+        ob.sr_seq = _abi.ptr(self._sr, C.c_uint8)
+        self._ob = ob
+        _abi.check(self.L.pr_iter_upload_owned(ctx.h, C.byref(ob)), "pr_iter_upload_owned")
+        self.d = SimpleNamespace(lr_off=self._own_off)
+        nl, nt, bd = C.c_int32(), C.c_int64(), _abi.CnsBounds()
+        _abi.check(self.L.pr_iter_bounds(ctx.h, C.byref(nl), C.byref(nt), C.byref(bd)), "pr_iter_bounds")
+        self.n_lr, self.n_task, self.bounds = nl.value, nt.value, bd
+        self.out = None

@@ -61,6 +61,7 @@ def _setup(L):
     L.pr_seed_gpu_phase_ticks.argtypes = [C.c_void_p, C.c_void_p]
     L.pr_seed_gpu_pass2_ms.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     L.pr_seed_gpu_pass2_reads.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
+    L.pr_seed_gpu_seed_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     _done = True
 
 
@@ -159,6 +160,12 @@ class SeedIndex:
     def phase_ms(self) -> dict:
         return _phase_ms(self.L, self._ctx)
 
+    def seed_count(self) -> int:
+        """Seeds of the last map (kept in HBM with keep_on_device)."""
+        n = C.c_int64()
+        _abi.check(self.L.pr_seed_gpu_seed_count(self._ctx.h, C.byref(n)), "pr_seed_gpu_seed_count")
+        return n.value
+
     def _take(self, out: SeedTasks):
         return _take(self.L, out)
 
@@ -246,3 +253,9 @@ class DeviceSeedIndex:
 
     def phase_ms(self) -> dict:
         return _phase_ms(self.L, self._ctx)
+
+    def seed_count(self) -> int:
+        """Seeds of the last map (kept in HBM with keep_on_device)."""
+        n = C.c_int64()
+        _abi.check(self.L.pr_seed_gpu_seed_count(self._ctx.h, C.byref(n)), "pr_seed_gpu_seed_count")
+        return n.value

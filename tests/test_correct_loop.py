@@ -149,6 +149,34 @@ def test_gpu_loop_matches_oracle_loop():
     assert got.chim == want.chim
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["none", "rccl"])
+def test_gpu_exact_layout_loop_matches_oracle_loop(transport, monkeypatch, tmp_path):
+    """The multi-GPU exact-parity layout of the loop at world 1 (GpuStages.owned_iteration:
+    device seeding of the shard, SW, pr_aln_exchange -- through RCCL's self send/recv with a
+    communicator --, owned consensus and masking on the device) = the oracle loop."""
+    import dataclasses
+    import loop_oracle
+    from proovread_amd import _abi, comm
+    _, lrs, srd = _inputs(seed=6)
+    cfg = correct.LoopConfig(coverage=40.0, seed_threads=4)
+    want = correct.run(lrs, srd, cfg, stages=loop_oracle.OracleStages(8))
+    cm = None
+    if transport == "rccl":
+        monkeypatch.setenv("PRGPU_RDZV_DIR", str(tmp_path))
+        cm = comm.RcclComm(_abi.default_context(), 0, 1, key="loopx")
+    try:
+        got = correct.run(lrs, srd, dataclasses.replace(cfg, exact_layout=True), comm=cm)
+    finally:
+        if cm is not None:
+            cm.close()
+    for g, w in zip(got.log, want.log):
+        assert (g.n_sr, g.n_tasks, g.bpt, g.bpn, g.shortcut) == (w.n_sr, w.n_tasks, w.bpt, w.bpn, w.shortcut), g.task
+    assert got.reads.seqs == want.reads.seqs
+    assert got.reads.quals == want.reads.quals
+    assert got.chim == want.chim
+
+
 # ---------------------------------------------------------------- configs[0]: the bundled sample
 def _sample_inputs():
     from test_fantasticus_chain import FX, simulate_sr
