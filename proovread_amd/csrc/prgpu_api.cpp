@@ -86,7 +86,8 @@ enum MaskBufId { MB_OFF, MB_SEQ, MB_QUAL, MB_OUT, MB_RUN_OFF, MB_RUNS, MB_TMP, M
 enum SeedBufId {
     SI_TEXT, SI_CSTART, SI_CBLK, SI_LROFF, SI_KOFF, SI_KPOS, SI_KEXT, SI_CNT0,
     SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SB_NEXT, SB_PRE, SB_DENSE,
-    SX_LRSEQ, SX_KEY0, SX_KEY1, SX_VAL0, SX_KC, SX_CNTPTR, SX_TEMP, SD_COUNT
+    SX_LRSEQ, SX_KEY0, SX_KEY1, SX_VAL0, SX_KC, SX_CNTPTR, SX_TEMP, SI_KSPLIT, SX_VAL1, SX_KCC, SX_KOFFC, SX_KCUR,
+    SD_COUNT
 };
 // the exact-parity layout's exchange (pr_aln_exchange, owned batches): bounds, sort keys and
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
@@ -1354,7 +1355,8 @@ extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
     if ((rc = upload(D[SI_TEXT], hv.text, (size_t)z.text, s)) || (rc = upload(D[SI_CSTART], hv.cstart, (size_t)z.cstart, s)) ||
         (rc = upload(D[SI_CBLK], hv.cblk, (size_t)z.cblk, s)) || (rc = upload(D[SI_LROFF], hv.lr_off, (size_t)z.lr_off, s)) ||
         (rc = upload(D[SI_KOFF], hv.koff, (size_t)z.koff, s)) || (rc = upload(D[SI_KPOS], hv.kpos, (size_t)z.kpos, s)) ||
-        (rc = upload(D[SI_KEXT], hv.kext, (size_t)z.kpos, s)))
+        (rc = upload(D[SI_KEXT], hv.kext, (size_t)z.kpos, s)) ||
+        (z.ksplit && (rc = upload(D[SI_KSPLIT], hv.ksplit, (size_t)z.ksplit, s))))
         return rc;
     seedc::IndexView v = hv;
     for (int j = 0; j < seedc::KI - 1; ++j) {
@@ -1365,9 +1367,10 @@ extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
     v.cstart = D[SI_CSTART].as<int64_t>();
     v.cblk = D[SI_CBLK].as<int32_t>();
     v.lr_off = D[SI_LROFF].as<int64_t>();
-    v.koff = D[SI_KOFF].as<uint32_t>();
+    v.koff = D[SI_KOFF].as<uint64_t>();
     v.kpos = D[SI_KPOS].as<uint32_t>();
     v.kext = D[SI_KEXT].as<uint64_t>();
+    v.ksplit = z.ksplit ? D[SI_KSPLIT].as<uint64_t>() : nullptr;
     HIPCHK(hipStreamSynchronize(s));
     c->seed_view = v;
     c->seed_loaded = true;
@@ -1380,8 +1383,8 @@ extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const i
     for (int i = 0; i < n_lr; ++i)
         if (lr_off[i + 1] < lr_off[i]) return set_error(PR_ERR_ARG, "lr_off not monotone");
     const int64_t l_pac = n_lr ? lr_off[n_lr] - lr_off[0] : 0;
-    if (2 * l_pac + 2 * (int64_t)n_lr >= (int64_t)UINT32_MAX)
-        return set_error(PR_ERR_CAPACITY, "long-read shard too large for the 32-bit seed index");
+    if (2 * l_pac + 2 * (int64_t)n_lr > seedc::MAX_TEXT)
+        return set_error(PR_ERR_CAPACITY, "long reads beyond the index's 2^33 text positions (l_pac < 4.29 Gb)");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     DevBuf *D = c->sd;
@@ -1404,16 +1407,32 @@ extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const i
         }
     }
     const size_t nt = (size_t)(n_text > 0 ? n_text : 1);
-    const size_t temp = seed_index_temp_bytes(n_text);
+    // sorts of up to 2^30 text positions (a divisor of 2^32; PRGPU_INDEX_CHUNK=k: 2^k, a test
+    // hook that sends small texts through the chunked build)
+    int64_t chunk = (int64_t)1 << 30;
+    if (const char *ch = getenv("PRGPU_INDEX_CHUNK")) {
+        const int k = atoi(ch);
+        if (k >= 16 && k <= 32) chunk = (int64_t)1 << k;
+    }
+    const bool chunked = n_text > chunk;
+    const size_t ns = (size_t)(chunked ? chunk : (int64_t)nt);   // sort scratch entries
+    const size_t temp = seed_index_temp_bytes((int64_t)ns);
+    const size_t nk1 = (size_t)seedc::NK + 1;
+    // hits <= 12-mer starts; kpos / kext sized by the text (the count is known after the build)
     int rc;
     if ((rc = upload(D[SX_LRSEQ], n_lr ? lr_seq + lr_off[0] : lr_seq, (size_t)l_pac, s)) ||
         (rc = upload(D[SI_LROFF], off.data(), off.size(), s)) || (rc = upload(D[SI_CSTART], cstart.data(), cstart.size(), s)) ||
         (rc = upload(D[SI_CBLK], cblk.data(), cblk.size(), s)) || (rc = D[SI_TEXT].ensure(nt)) ||
-        (rc = D[SX_KEY0].ensure(nt * 4)) || (rc = D[SX_KEY1].ensure(nt * 4)) || (rc = D[SX_VAL0].ensure(nt * 4)) ||
-        (rc = D[SX_KC].ensure(((size_t)seedc::NK + 1) * 4)) || (rc = D[SI_KOFF].ensure(((size_t)seedc::NK + 1) * 4)) ||
+        (rc = D[SX_KEY0].ensure(ns * 4)) || (rc = D[SX_KEY1].ensure(ns * 4)) || (rc = D[SX_VAL0].ensure(ns * 4)) ||
+        (rc = D[SX_KC].ensure(nk1 * 4)) || (rc = D[SI_KOFF].ensure(nk1 * 8)) ||
         (rc = D[SI_KPOS].ensure(nt * 4)) || (rc = D[SI_KEXT].ensure(nt * 8)) || (rc = D[SX_TEMP].ensure(temp)) ||
         (rc = D[SX_CNTPTR].ensure(sizeof(uint32_t *) * (seedc::KI - 1))))
         return rc;
+    if (chunked && ((rc = D[SX_VAL1].ensure(ns * 4)) || (rc = D[SX_KCC].ensure(nk1 * 4)) ||
+                    (rc = D[SX_KOFFC].ensure(nk1 * 4)) || (rc = D[SX_KCUR].ensure(nk1 * 8))))
+        return rc;
+    const bool paged = n_text > (int64_t)seedc::POS_PAGE;
+    if (paged && (rc = D[SI_KSPLIT].ensure(nk1 * 8))) return rc;
     SeedIndexBuild B{};
     uint32_t *cptr[seedc::KI - 1];
     for (int j = 1; j < seedc::KI; ++j) {
@@ -1428,13 +1447,19 @@ extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const i
     B.cstart = D[SI_CSTART].as<int64_t>();
     B.n_text = n_text;
     B.text = D[SI_TEXT].as<uint8_t>();
+    B.chunk = chunk;
     B.key0 = D[SX_KEY0].as<uint32_t>();
     B.key1 = D[SX_KEY1].as<uint32_t>();
     B.val0 = D[SX_VAL0].as<uint32_t>();
+    B.val1 = chunked ? D[SX_VAL1].as<uint32_t>() : nullptr;
     B.kc = D[SX_KC].as<uint32_t>();
-    B.koff = D[SI_KOFF].as<uint32_t>();
+    B.koff = D[SI_KOFF].as<uint64_t>();
+    B.kcc = chunked ? D[SX_KCC].as<uint32_t>() : nullptr;
+    B.koffc = chunked ? D[SX_KOFFC].as<uint32_t>() : nullptr;
+    B.kcur = chunked ? D[SX_KCUR].as<uint64_t>() : nullptr;
     B.kpos = D[SI_KPOS].as<uint32_t>();
     B.kext = D[SI_KEXT].as<uint64_t>();
+    B.ksplit = paged ? D[SI_KSPLIT].as<uint64_t>() : nullptr;
     B.cnt_dev = reinterpret_cast<uint32_t *const *>(D[SX_CNTPTR].p);
     B.temp = D[SX_TEMP].p;
     B.temp_bytes = temp;
@@ -1442,8 +1467,8 @@ extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const i
     const int e = seed_index_device_build(B, s);
     if (e) return set_error(PR_ERR_HIP, "seed index build: %s", hipGetErrorString((hipError_t)e));
     HIPCHK(hipEventRecord(c->ev[9], s));
-    uint32_t nh = 0;
-    HIPCHK(hipMemcpyAsync(&nh, B.koff + seedc::NK, 4, hipMemcpyDeviceToHost, s));
+    uint64_t nh = 0;
+    HIPCHK(hipMemcpyAsync(&nh, B.koff + seedc::NK, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_index = ms;
@@ -1459,6 +1484,7 @@ extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const i
     v.koff = B.koff;
     v.kpos = B.kpos;
     v.kext = B.kext;
+    v.ksplit = B.ksplit;
     for (int j = 0; j < seedc::KI - 1; ++j) v.cnt[j] = B.cnt[j];
     c->seed_view = v;
     c->seed_loaded = true;
@@ -1475,13 +1501,14 @@ extern "C" int pr_seed_gpu_index_digest(pr_ctx *c, uint64_t *out6) {
     const seedc::IndexView &v = c->seed_view;
     const size_t nt = (size_t)c->seed_n_text, nh = (size_t)c->seed_n_hits, nk = (size_t)seedc::NK;
     std::vector<uint8_t> text(nt);
-    std::vector<uint32_t> koff(nk + 1), kpos(nh), kc(nk);
+    std::vector<uint64_t> koff(nk + 1);
+    std::vector<uint32_t> kpos(nh), kc(nk);
     std::vector<uint64_t> kext(nh);
     std::vector<int64_t> cstart((size_t)v.n_contig), lro((size_t)v.n_lr + 1);
     std::vector<int32_t> cblk((size_t)((c->seed_n_text >> seedc::CB_SHIFT) + 1));
     std::vector<std::vector<uint32_t>> cnt(seedc::KI);
     HIPCHK(hipMemcpy(text.data(), v.text, nt, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(koff.data(), v.koff, (nk + 1) * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(koff.data(), v.koff, (nk + 1) * 8, hipMemcpyDeviceToHost));
     if (nh) HIPCHK(hipMemcpy(kpos.data(), v.kpos, nh * 4, hipMemcpyDeviceToHost));
     if (nh) HIPCHK(hipMemcpy(kext.data(), v.kext, nh * 8, hipMemcpyDeviceToHost));
     HIPCHK(hipMemcpy(kc.data(), c->sd[SX_KC].p, nk * 4, hipMemcpyDeviceToHost));
@@ -1521,12 +1548,14 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     DevBuf *D = c->sd;
-    const seedc::Caps caps = seedc::device_caps();
+    seedc::Caps caps = seedc::device_caps();
+    caps.hi = c->seed_view.ksplit != nullptr;   // text beyond 2^32: positions carry bit 32
     int qmax = 1;
     for (int i = 0; i < n_sr; ++i) qmax = std::max<int>(qmax, (int)(sr_off[i + 1] - sr_off[i]));
     // pass 1: 64 reads per wave, small slices sized for the batch; pass 2 (flagged reads): the
     // large slices, one wave per read
     seedc::Caps small = seedc::device_caps_small(std::min(qmax, caps.lmax));
+    small.hi = caps.hi;
     if (const char *sc = getenv("PRGPU_SEED_SMALL"))   // tuning hook: hits,iv,mems,seeds,chains
         sscanf(sc, "%d,%d,%d,%d,%d", &small.hits, &small.iv, &small.mems, &small.seeds, &small.chains);
     SeedDev K{};

@@ -97,8 +97,10 @@ struct Index {
     std::vector<int64_t> lr_off;   // forward long-read offsets (n_lr + 1), l_pac = lr_off[n_lr]
     int n_lr = 0;
     int64_t l_pac = 0;
-    std::vector<uint32_t> koff;    // [NK + 1] offsets into kpos
+    std::vector<uint64_t> koff;    // [NK + 1] offsets into kpos
     BigVec<uint32_t> kpos;         // text positions of every valid 12-mer, grouped by k-mer, ascending
+                                   // (low 32 bits; seedc::hit_pos adds bit 32 from ksplit)
+    std::vector<uint64_t> ksplit;  // [NK] the first hit of each k-mer at or beyond 2^32 (empty: text < 2^32)
     BigVec<uint64_t> kext;         // per kpos entry: the next KX bases after the 12-mer (2 bits each,
                                    // base i at bits 2i) and their count before N / SEP (bits 56..61)
     std::vector<uint32_t> cnt[KI]; // cnt[j][code] = occurrences of the (j+1)-mer `code` (j < KI-1)
@@ -116,7 +118,9 @@ inline int contig_of(const Index &I, int64_t p) {
 }
 
 // occurrence count of q[a, b) (codes 0-3 only), optionally collecting text positions
-int64_t occ(const Index &I, const uint8_t *q, int a, int b, std::vector<uint32_t> *pos = nullptr) {
+seedc::IndexView view_of(const Index &I);
+
+int64_t occ(const Index &I, const uint8_t *q, int a, int b, std::vector<uint64_t> *pos = nullptr) {
     const int n = b - a;
     uint32_t code = 0;
     for (int x = a; x < a + (n < KI ? n : KI); ++x) code = (code << 2) | q[x];
@@ -125,8 +129,9 @@ int64_t occ(const Index &I, const uint8_t *q, int a, int b, std::vector<uint32_t
     if (pos) pos->clear();
     int64_t m = 0;
     const uint8_t *T = I.text.data();
-    for (uint32_t r = I.koff[code]; r < I.koff[code + 1]; ++r) {
-        const uint32_t p = I.kpos[r];
+    const seedc::IndexView V = view_of(I);
+    for (uint64_t r = I.koff[code]; r < I.koff[code + 1]; ++r) {
+        const uint64_t p = seedc::hit_pos(V, code, r);
         bool ok = true;
         for (int x = KI; x < n && ok; ++x) ok = T[p + x] == q[a + x];   // SEP / N never match
         if (ok) {
@@ -148,7 +153,7 @@ struct IndexOcc {
     const Index &I;
     const uint8_t *q;
     int64_t operator()(int a, int b) const { return occ(I, q, a, b); }
-    void positions(int a, int b, std::vector<uint32_t> &pos) const { occ(I, q, a, b, &pos); }
+    void positions(int a, int b, std::vector<uint64_t> &pos) const { occ(I, q, a, b, &pos); }
 };
 
 // bwt_smem1a (max_intv = 0): SMEMs covering x with >= min_intv occurrences, sorted by start;
@@ -230,6 +235,7 @@ seedc::IndexView view_of(const Index &I) {
     v.l_pac = I.l_pac;
     v.koff = I.koff.data();
     v.kpos = I.kpos.data();
+    v.ksplit = I.ksplit.empty() ? nullptr : I.ksplit.data();
     v.kext = I.kext.data();
     for (int j = 0; j < KI - 1; ++j) v.cnt[j] = I.cnt[j].data();
     return v;
@@ -239,6 +245,7 @@ struct HostScratch {
     std::vector<int32_t> hoff, codes;
     std::vector<uint64_t> qext;
     std::vector<uint32_t> ge, hpos;
+    std::vector<uint8_t> hhi;
     std::vector<uint16_t> hml;
     std::vector<seedc::Iv> mems, m1, curr, prev;
     std::vector<seedc::Seed> seeds;
@@ -247,9 +254,11 @@ struct HostScratch {
     std::vector<pr_seed_task> out;
     seedc::Scratch S{};
     int lmax = 0, hits = 1 << 14, iv = 256, mems_cap = 1024, seeds_cap = 4096, chains = 2048, out_cap = 512;
+    bool hi = false;   // the index's text reaches beyond 2^32 (hhi carries bit 32 of the positions)
 
     void size(int len) {
         lmax = len > lmax ? len : lmax;
+        hhi.resize(hi ? (size_t)hits : 0);
         hoff.resize((size_t)lmax + 1);
         codes.resize((size_t)lmax + 1);
         qext.resize((size_t)lmax + 1);
@@ -272,7 +281,7 @@ struct HostScratch {
         htail.resize((size_t)hs);
         out.resize((size_t)out_cap);
         S = seedc::Scratch{lmax,        hoff.data(),  qext.data(), codes.data(), ge.data(),   hpos.data(),
-                           hml.data(),  hits,         mems.data(), mems_cap,     m1.data(),   curr.data(),
+                           hi ? hhi.data() : nullptr, hml.data(),  hits, mems.data(), mems_cap, m1.data(), curr.data(),
                            prev.data(), iv,           seeds.data(), next.data(), seeds_cap,   cv.data(),
                            ch.data(),   cnx.data(),   kept.data(), hkey.data(), hhead.data(),
                            htail.data(), chains,      hs};
@@ -293,7 +302,11 @@ struct ReadOut {
 
 void map_read(const seedc::IndexView &V, const pr_seed_opts &O, const uint8_t *q, int len, int sid, ReadOut &res) {
     static thread_local HostScratch H;
-    if (len > H.lmax || H.S.hoff == nullptr) H.size(len);
+    const bool hi = V.ksplit != nullptr;
+    if (len > H.lmax || H.S.hoff == nullptr || hi != H.hi) {
+        H.hi = hi;
+        H.size(len);
+    }
     for (;;) {
         int n = 0;
         const int err = seedc::map_read(V, O, H.S, q, len, sid, H.out.data(), H.out_cap, &n);
@@ -323,6 +336,7 @@ SeedIndexSizes seed_index_sizes(const pr_seed_index *h) {
     z.lr_off = (int64_t)I.lr_off.size();
     z.koff = (int64_t)I.koff.size();
     z.kpos = (int64_t)I.kpos.size();
+    z.ksplit = (int64_t)I.ksplit.size();
     for (int j = 0; j < KI - 1; ++j) z.cnt[j] = (int64_t)I.cnt[j].size();
     return z;
 }
@@ -356,8 +370,8 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     for (int i = 0; i < n_lr; ++i)
         if (lr_off[i + 1] < lr_off[i]) return pr_set_error(PR_ERR_ARG, "lr_off not monotone");
     const int64_t l_pac = n_lr ? lr_off[n_lr] - lr_off[0] : 0;
-    if (2 * l_pac + 2 * (int64_t)n_lr >= (int64_t)UINT32_MAX)
-        return pr_set_error(PR_ERR_CAPACITY, "long-read shard too large for the 32-bit seed index");
+    if (2 * l_pac + 2 * (int64_t)n_lr > seedc::MAX_TEXT)
+        return pr_set_error(PR_ERR_CAPACITY, "long reads beyond the index's 2^33 text positions (l_pac < 4.29 Gb)");
     pr_seed_index *h = new pr_seed_index;
     Index &I = h->I;
     I.n_lr = n_lr;
@@ -419,7 +433,7 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
         for (; p < p1 + KI - 1 && p < n; ++p) {
             if (T[p] > 3) { run = 0; code = 0; continue; }
             code = ((code << 2) | T[p]) & (NK - 1);
-            if (++run >= KI && p - KI + 1 >= p0) f(code, (uint32_t)(p - KI + 1));
+            if (++run >= KI && p - KI + 1 >= p0) f(code, (int64_t)(p - KI + 1));
         }
     };
     // counting split over text chunks (per-chunk counts, each thread zeroing and filling
@@ -428,7 +442,7 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     run_threads([&](int t) {
         std::vector<uint32_t> &c = tc[(size_t)t];
         c.assign(NK, 0);
-        for_kmers(n * t / nt, n * (t + 1) / nt, [&](uint32_t k, uint32_t) { ++c[k]; });
+        for_kmers(n * t / nt, n * (t + 1) / nt, [&](uint32_t k, int64_t) { ++c[k]; });
     });
     std::vector<uint32_t> kc(NK);
     I.koff.assign(NK + 1, 0);
@@ -441,14 +455,14 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
             for (int u = 0; u < nt; ++u) sum += tc[(size_t)u][k];
             kc[k] = sum;
             run += sum;
-            I.koff[k + 1] = (uint32_t)run;   // range-local prefix, shifted below
+            I.koff[k + 1] = run;   // range-local prefix, shifted below
         }
         part[(size_t)t + 1] = run;
     });
     for (int t = 0; t < nt; ++t) part[(size_t)t + 1] += part[(size_t)t];
     run_threads([&](int t) {
         const uint32_t k0 = (uint32_t)((uint64_t)NK * t / nt), k1 = (uint32_t)((uint64_t)NK * (t + 1) / nt);
-        const uint32_t base = (uint32_t)part[(size_t)t];
+        const uint64_t base = part[(size_t)t];
         for (uint32_t k = k0; k < k1; ++k) I.koff[k + 1] += base;
     });
     I.kpos.resize(I.koff[NK]);
@@ -464,9 +478,11 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     constexpr int LB = 12;                    // low k-mer bits sorted in pass 2
     constexpr uint32_t NB = NK >> LB;         // buckets
     struct Rec {
-        uint32_t pos, low;
+        uint32_t pos, low;   // low 32 bits of the position; the k-mer's low bits | bit 32 of the position << 31
         uint64_t ext;
     };
+    const bool paged = n > (int64_t)seedc::POS_PAGE;
+    if (paged) I.ksplit.assign(NK, 0);
     BigVec<Rec> tmp(I.koff[NK]);
     {
         // per-thread bucket cursors: bucket b starts at koff[b << LB]; thread t after threads < t
@@ -514,7 +530,7 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
                     const uint64_t ext = (m ? (w & ((1ull << (2 * m)) - 1)) : 0) | ((uint64_t)m << 56);
                     Rec &r = R[c[code >> LB]++];
                     r.pos = (uint32_t)(p - KI + 1);
-                    r.low = code & ((1u << LB) - 1);
+                    r.low = (code & ((1u << LB) - 1)) | ((uint32_t)((uint64_t)(p - KI + 1) >> 32) << 31);
                     r.ext = ext;
                 }
             }
@@ -523,13 +539,17 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     {
         std::atomic<uint32_t> next{0};
         run_threads([&](int) {
-            std::vector<uint32_t> fill((size_t)1 << LB);
+            std::vector<uint64_t> fill((size_t)1 << LB);
             for (uint32_t b; (b = next.fetch_add(1)) < NB;) {
                 const uint32_t k0 = b << LB;
                 for (uint32_t j = 0; j < (1u << LB); ++j) fill[j] = I.koff[k0 + j];
+                if (paged)   // no hit beyond 2^32 yet: the split is the list's end
+                    for (uint32_t j = 0; j < (1u << LB); ++j) I.ksplit[k0 + j] = I.koff[k0 + j + 1];
                 for (uint64_t i = I.koff[k0]; i < I.koff[k0 + (1u << LB)]; ++i) {
                     const Rec &r = tmp[i];
-                    const uint32_t slot = fill[r.low]++;
+                    const uint32_t lo = r.low & ((1u << LB) - 1);
+                    const uint64_t slot = fill[lo]++;
+                    if ((r.low >> 31) && I.ksplit[k0 + lo] > slot) I.ksplit[k0 + lo] = slot;   // text order
                     I.kpos[slot] = r.pos;
                     I.kext[slot] = r.ext;
                 }
@@ -543,23 +563,21 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     // base of its run, then it prefixes a (j+1)-mer occurrence, or it ends the run)
     std::vector<std::vector<uint32_t>> tail(KI);
     {
-        std::vector<std::vector<int64_t>> stops((size_t)nt);   // non-base positions, per text chunk
+        // the positions that end a run of bases (a non-base after a base; the text ends with
+        // SEP), one list per text chunk; the j-mers (j < 12) ending just before each
+        std::vector<std::vector<int64_t>> stops((size_t)nt);
         run_threads([&](int t) {
             for (int64_t p = n * t / nt; p < n * (t + 1) / nt; ++p)
-                if (T[p] > 3) stops[(size_t)t].push_back(p);
+                if (T[p] > 3 && p > 0 && T[p - 1] <= 3) stops[(size_t)t].push_back(p);
         });
-        std::vector<int64_t> ends;
-        for (auto &v : stops) ends.insert(ends.end(), v.begin(), v.end());
-        ends.push_back(n);
-        int64_t s0 = 0;
-        for (const int64_t p : ends) {
-            for (int j = 1; j < KI && p - j >= s0; ++j) {   // run [s0, p)
+        for (auto &v : stops)
+            for (const int64_t p : v) {
                 uint32_t code = 0;
-                for (int64_t e = p - j; e < p; ++e) code = (code << 2) | T[e];
-                tail[j].push_back(code);
+                for (int j = 1; j < KI && p - j >= 0 && T[p - j] <= 3; ++j) {
+                    code |= (uint32_t)T[p - j] << (2 * (j - 1));   // T[p-j] starts the j-mer
+                    tail[j].push_back(code);
+                }
             }
-            s0 = p + 1;
-        }
     }
     I.cnt[KI - 1] = std::move(kc);
     for (int j = KI - 1; j >= 1; --j) {
@@ -610,7 +628,7 @@ extern "C" int pr_seed_index_digest(const pr_seed_index *h, uint64_t *out6) {
 }
 
 namespace prgpu {
-void seed_digest_tables(const std::vector<uint8_t> &text, const std::vector<uint32_t> &koff,
+void seed_digest_tables(const std::vector<uint8_t> &text, const std::vector<uint64_t> &koff,
                         const std::vector<uint32_t> &kpos, const std::vector<uint64_t> &kext,
                         const std::vector<std::vector<uint32_t>> &cnt, const std::vector<int64_t> &cstart,
                         const std::vector<int32_t> &cblk, const std::vector<int64_t> &lr_off, uint64_t *out6) {
@@ -697,7 +715,8 @@ extern "C" int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opt
     out->n = 0;
     out->t = nullptr;
     const seedc::IndexView V = view_of(h->I);
-    const seedc::Caps caps = seedc::device_caps();
+    seedc::Caps caps = seedc::device_caps();
+    caps.hi = V.ksplit != nullptr;
     const int64_t bytes = seedc::scratch_bytes(caps);
     int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
     nt = nt < 1 ? 1 : (nt > 64 ? 64 : nt);

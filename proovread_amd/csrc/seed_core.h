@@ -58,6 +58,13 @@ constexpr uint64_t KX_MASK = (1ull << (2 * KX)) - 1;
 constexpr int HB = 20;                        // per-start count table width
 constexpr int CB_SHIFT = 12;                  // contig block table granularity
 
+// Text positions: the text holds both strands of every long read, 2 l_pac + 2 n_lr bases, up to
+// 2^33 (l_pac < 4.29 Gb: configs[3]'s 2.7 Gb read set).  Hit positions are
+// stored as their low 32 bits; a k-mer's hits are in text order, so those at or beyond 2^32
+// form the tail of its list, from ksplit[code] on (ksplit null: the text is below 2^32).
+constexpr uint64_t POS_PAGE = 1ull << 32;
+constexpr int64_t MAX_TEXT = (int64_t)1 << 33;
+
 // Device- or host-resident index, plain pointers (built by seed.cpp).
 struct IndexView {
     const uint8_t *text;       // forward long reads, then rc of their concatenation, SEP (5) after each
@@ -68,8 +75,9 @@ struct IndexView {
     const int64_t *lr_off;     // [n_lr + 1] forward long-read offsets
     int32_t n_lr;
     int64_t l_pac;
-    const uint32_t *koff;      // [NK + 1]
-    const uint32_t *kpos;      // 12-mer hits, text order within a k-mer
+    const uint64_t *koff;      // [NK + 1]
+    const uint32_t *kpos;      // 12-mer hits (low 32 bits of the text position), text order within a k-mer
+    const uint64_t *ksplit;    // [NK] first hit of k-mer `code` at or beyond POS_PAGE, or null
     const uint64_t *kext;      // per hit: KX bases after it (2 bits each) | count << 56
     const uint32_t *cnt[KI - 1];   // cnt[j-1][code]: occurrences of the j-mer `code`, j = 1..11
 };
@@ -100,7 +108,8 @@ struct Scratch {
     uint64_t *qext;                            // [lmax + 1]
     int32_t *codes;                            // [lmax + 1]
     uint32_t *ge;                              // [lmax * HB]
-    uint32_t *hpos;                            // [cap_hits]
+    uint32_t *hpos;                            // [cap_hits] low 32 bits of the hit's text position
+    uint8_t *hhi;                              // [cap_hits] bit 32 of it (null: the text is below 2^32)
     uint16_t *hml;                             // [cap_hits]
     int32_t cap_hits;
     Iv *mems;                                  // [cap_mems]
@@ -124,6 +133,21 @@ SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
 }
 
 SC_HD int ctz64(uint64_t x) { return __builtin_ctzll(x); }
+
+// text position of hit r of k-mer `code`
+SC_HD uint64_t hit_pos(const IndexView &I, uint32_t code, uint64_t r) {
+    uint64_t p = I.kpos[r];
+    if (I.ksplit && r >= I.ksplit[code]) p += POS_PAGE;
+    return p;
+}
+// the per-read hit table's positions
+SC_HD uint64_t get_hpos(const Scratch &S, int64_t k) {
+    return (uint64_t)S.hpos[k] | (S.hhi ? (uint64_t)S.hhi[k] << 32 : 0ull);
+}
+SC_HD void set_hpos(const Scratch &S, int64_t k, uint64_t p) {
+    S.hpos[k] = (uint32_t)p;
+    if (S.hhi) S.hhi[k] = (uint8_t)(p >> 32);
+}
 
 // ---------------------------------------------------------------- occurrence table
 // the j-mer count tables j = 1..LC_MAX held on chip by the device kernels (5,460 entries):
@@ -194,7 +218,7 @@ SC_HD int build_occ(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
         constexpr int PF_OFF = 24, PF_POS = 12;   // latency-bound on the host: prefetch ahead
         if (a + PF_OFF < len && S.codes[a + PF_OFF] >= 0) __builtin_prefetch(&I.koff[S.codes[a + PF_OFF]]);
         if (a + PF_POS < len && S.codes[a + PF_POS] >= 0) {
-            const uint32_t r0 = I.koff[S.codes[a + PF_POS]];
+            const uint64_t r0 = I.koff[S.codes[a + PF_POS]];
             __builtin_prefetch(&I.kpos[r0]);
             __builtin_prefetch(&I.kext[r0]);
             __builtin_prefetch(&I.kext[r0] + 8);
@@ -203,15 +227,15 @@ SC_HD int build_occ(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
         S.hoff[a] = nh;
         if (S.codes[a] >= 0) {
             const uint32_t code = (uint32_t)S.codes[a];
-            const uint32_t r0 = I.koff[code], r1 = I.koff[code + 1];
-            if ((int64_t)nh + (r1 - r0) > S.cap_hits) return SC_OVER_HITS;
+            const uint64_t r0 = I.koff[code], r1 = I.koff[code + 1];
+            if ((int64_t)nh + (int64_t)(r1 - r0) > S.cap_hits) return SC_OVER_HITS;
             uint32_t *g = S.ge + (int64_t)a * HB;
             int32_t k = prev0;
-            for (uint32_t r = r0; r < r1; ++r) {
-                const uint32_t p = I.kpos[r];
-                while (k < prev1 && S.hpos[k] + 1 < p) ++k;
+            for (uint64_t r = r0; r < r1; ++r) {
+                const uint64_t p = hit_pos(I, code, r);
+                while (k < prev1 && get_hpos(S, k) + 1 < p) ++k;
                 int ml;
-                if (k < prev1 && S.hpos[k] + 1 == p && S.hml[k] > KI) {
+                if (k < prev1 && get_hpos(S, k) + 1 == p && S.hml[k] > KI) {
                     ml = S.hml[k] - 1;
                 } else {
                     const uint64_t ex = I.kext[r];
@@ -225,7 +249,7 @@ SC_HD int build_occ(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
                     if (m == KX)
                         while (a + ml < len && q[a + ml] < 4 && T[p + ml] == q[a + ml]) ++ml;
                 }
-                S.hpos[nh] = p;
+                set_hpos(S, nh, p);
                 S.hml[nh] = (uint16_t)(ml < 65535 ? ml : 65535);
                 ++nh;
                 ++g[ml - KI < HB - 1 ? ml - KI : HB - 1];
@@ -433,7 +457,7 @@ SC_HD int contig_of(const IndexView &I, int64_t p) {
     return c;
 }
 
-SC_HD void text_to_fr(const IndexView &I, uint32_t p, int64_t &fr, int &rid) {
+SC_HD void text_to_fr(const IndexView &I, uint64_t p, int64_t &fr, int &rid) {
     const int c = contig_of(I, p);
     const int64_t o = (int64_t)p - I.cstart[c];
     if (c < I.n_lr) {
@@ -651,12 +675,12 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
                     sel[nsel++] = k;
                 }
             }
-            uint32_t hp[CB];
+            uint64_t hp[CB];
             int64_t rb[CB];
             int rd[CB], hsl[CB];
             int32_t key[CB];
 #pragma unroll
-            for (int u = 0; u < CB; ++u) hp[u] = u < nsel ? S.hpos[sel[u]] : 0u;
+            for (int u = 0; u < CB; ++u) hp[u] = u < nsel ? get_hpos(S, sel[u]) : 0ull;
 #pragma unroll
             for (int u = 0; u < CB; ++u) {
                 rb[u] = 0, rd[u] = 0;
@@ -865,12 +889,13 @@ namespace seedc {
 // need more are flagged with the SC_OVER_* bit of the array that overflowed.
 struct Caps {
     int32_t lmax, hits, iv, mems, seeds, chains, out;
+    int32_t hi;   // the text reaches beyond 2^32: the hit table carries bit 32 of the positions (hhi)
 };
-SC_HD Caps device_caps() { return Caps{1024, 8192, 256, 1024, 4096, 2048, 384}; }
+SC_HD Caps device_caps() { return Caps{1024, 8192, 256, 1024, 4096, 2048, 384, 0}; }
 // pass 1 of the device path: 64 slices per wave, sized for reads of <= lmax bases
 SC_HD Caps device_caps_small(int lmax) {
     const int l = lmax < 16 ? 16 : (lmax + 15) & ~15;
-    return Caps{l, 4096, 64, 512, 512, 384, 384};   // ~0.1 % of configs[1]'s reads outgrow it (mems)
+    return Caps{l, 4096, 64, 512, 512, 384, 384, 0};   // ~0.1 % of configs[1]'s reads outgrow it (mems)
 }
 
 SC_HD int64_t align8(int64_t x) { return (x + 7) & ~(int64_t)7; }
@@ -896,6 +921,7 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += 2 * align8((int64_t)sizeof(Chain) * c.chains);  // cv, ch
     b += 2 * align8(4 * (int64_t)c.chains);              // cnx, kept
     b += 3 * align8(4 * (int64_t)range_table_size(c.chains));   // hkey, hhead, htail
+    if (c.hi) b += align8((int64_t)c.hits);              // hhi (last: the small-text layout is unchanged)
     return b;
 }
 
@@ -933,6 +959,7 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.hhead = (int32_t *)take(4 * (int64_t)S.hsize);
     S.htail = (int32_t *)take(4 * (int64_t)S.hsize);
     S.cap_chains = c.chains;
+    S.hhi = c.hi ? (uint8_t *)take((int64_t)c.hits) : nullptr;
     return S;
 }
 

@@ -41,11 +41,11 @@ int seed_compact_launch(const pr_seed_task *slots, const int32_t *n_out, const i
 seedc::IndexView seed_index_view(const pr_seed_index *h);
 // sizes of the index arrays for the device copy
 struct SeedIndexSizes {
-    int64_t text, cstart, cblk, lr_off, koff, kpos, cnt[seedc::KI - 1];
+    int64_t text, cstart, cblk, lr_off, koff, kpos, ksplit, cnt[seedc::KI - 1];
 };
 SeedIndexSizes seed_index_sizes(const pr_seed_index *h);
 // pr_seed_index_digest's six values over tables copied to the host (device index test hook)
-void seed_digest_tables(const std::vector<uint8_t> &text, const std::vector<uint32_t> &koff,
+void seed_digest_tables(const std::vector<uint8_t> &text, const std::vector<uint64_t> &koff,
                         const std::vector<uint32_t> &kpos, const std::vector<uint64_t> &kext,
                         const std::vector<std::vector<uint32_t>> &cnt, const std::vector<int64_t> &cstart,
                         const std::vector<int32_t> &cblk, const std::vector<int64_t> &lr_off, uint64_t *out6);

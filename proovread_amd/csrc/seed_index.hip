@@ -19,6 +19,7 @@
 // passes, ~12 B per hit for kpos / kext.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -74,15 +75,12 @@ __global__ void ix_keys_kernel(const uint8_t *text, int64_t n, uint32_t *key, ui
     if (ok) atomicAdd(&kc[code], 1u);
 }
 
-// the KX bases after every hit: the 9 dwords around them loaded at once (independent loads
-// from a random text position; the buffer's 64-byte slack covers the end), aligned with
-// v_alignbyte, then the run up to the first N / separator / text end packed in registers
-// (round 2: one dependent byte load per base, 41 ms at configs[1])
-__global__ void ix_kext_kernel(const uint8_t *text, int64_t n, const uint32_t *kpos, const uint32_t *koff,
-                               uint64_t *kext) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= (int64_t)koff[NK]) return;   // the hits: the sorted pairs with a valid key
-    const int64_t p = (int64_t)kpos[r] + KI;
+// the KX bases after the 12-mer at text position p: the 9 dwords around them loaded at once
+// (independent loads from a random text position; the buffer's 64-byte slack covers the end),
+// aligned with v_alignbyte, then the run up to the first N / separator / text end packed in
+// registers (round 2: one dependent byte load per base, 41 ms at configs[1])
+__device__ __forceinline__ uint64_t kext_at(const uint8_t *text, int64_t n, int64_t p12) {
+    const int64_t p = p12 + KI;
     const uint32_t *tw = reinterpret_cast<const uint32_t *>(text) + (p >> 2);
     const uint32_t sh = (uint32_t)(p & 3);
     uint32_t w[9];
@@ -100,7 +98,66 @@ __global__ void ix_kext_kernel(const uint8_t *text, int64_t n, const uint32_t *k
         if (m == KX && (j >= lim || c > 3u)) m = j;
         if (m == KX) v |= (uint64_t)c << (2 * j);
     }
-    kext[r] = v | ((uint64_t)m << 56);
+    return v | ((uint64_t)m << 56);
+}
+
+__global__ void ix_kext_kernel(const uint8_t *text, int64_t n, const uint32_t *kpos, const uint64_t *koff,
+                               uint64_t *kext) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= (int64_t)koff[NK]) return;   // the hits: the sorted pairs with a valid key
+    kext[r] = kext_at(text, n, (int64_t)kpos[r]);
+}
+
+// chunked build (texts beyond one sort): the 12-mer histogram of the whole text
+__global__ void ix_count_kernel(const uint8_t *text, int64_t n, uint32_t *kc) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p + KI > n) return;
+    uint32_t code = 0;
+    bool ok = true;
+    for (int x = 0; x < KI; ++x) {
+        const uint8_t c = text[p + x];
+        ok &= c < 4;
+        code = (code << 2) | (c & 3u);
+    }
+    if (ok) atomicAdd(&kc[code], 1u);
+}
+
+// one chunk [c0, c0 + m): (key, position - c0) pairs and the chunk's histogram
+__global__ void ix_chunk_keys_kernel(const uint8_t *text, int64_t n, int64_t c0, int64_t m, uint32_t *key,
+                                     uint32_t *val, uint32_t *kcc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int64_t p = c0 + i;
+    uint32_t code = 0;
+    bool ok = p + KI <= n;
+    if (ok) {
+        for (int x = 0; x < KI; ++x) {
+            const uint8_t c = text[p + x];
+            ok &= c < 4;
+            code = (code << 2) | (c & 3u);
+        }
+    }
+    key[i] = ok ? code : NK;
+    val[i] = (uint32_t)i;
+    if (ok) atomicAdd(&kcc[code], 1u);
+}
+
+// the chunk's sorted hits to their slots after the earlier chunks' hits of the same k-mer
+__global__ void ix_chunk_scatter_kernel(const uint8_t *text, int64_t n, int64_t c0, const uint32_t *key,
+                                        const uint32_t *val, const uint32_t *koffc, const uint64_t *kcur,
+                                        uint32_t *kpos, uint64_t *kext) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)koffc[NK]) return;   // the valid keys sort first
+    const uint32_t code = key[i];
+    const uint64_t dst = kcur[code] + (uint64_t)(i - (int64_t)koffc[code]);
+    const int64_t p = c0 + (int64_t)val[i];
+    kpos[dst] = (uint32_t)p;
+    kext[dst] = kext_at(text, n, p);
+}
+
+__global__ void ix_chunk_advance_kernel(uint64_t *kcur, const uint32_t *kcc) {
+    const int64_t x = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (x < (int64_t)NK) kcur[x] += kcc[x];
 }
 
 // run ends: one thread per text position holding N / SEP; the j-mers (j < 12) that end
@@ -144,24 +201,52 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
                            B.cstart, B.l_pac, B.text);
         IXCHK(hipGetLastError());
     }
-    // 12-mer keys + histogram
     IXCHK(hipMemsetAsync(B.kc, 0, ((size_t)NK + 1) * 4, s));
-    if (n > 0) {
-        hipLaunchKernelGGL(ix_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.key0, B.val0, B.kc);
-        IXCHK(hipGetLastError());
-    }
-    // koff = exclusive scan of the histogram (NK + 1 entries: the last is the total)
-    {
+    if (n <= B.chunk) {
+        // one sort: 12-mer keys + histogram, koff = exclusive scan, stable sort of (key,
+        // position) by key (positions ascend within a k-mer) straight into kpos, then kext
+        if (n > 0) {
+            hipLaunchKernelGGL(ix_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.key0, B.val0,
+                               B.kc);
+            IXCHK(hipGetLastError());
+        }
         size_t tb = B.temp_bytes;
-        IXCHK(rocprim::exclusive_scan(B.temp, tb, B.kc, B.koff, 0u, (size_t)NK + 1, rocprim::plus<uint32_t>(), s));
-    }
-    if (n > 0) {
-        // stable sort of (key, position) by key: positions ascend within a k-mer
-        size_t tb = B.temp_bytes;
-        IXCHK(rocprim::radix_sort_pairs(B.temp, tb, B.key0, B.key1, B.val0, B.kpos, (size_t)n, 0u, 25u, s));
-        // kext for the hits
-        hipLaunchKernelGGL(ix_kext_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kpos, B.koff, B.kext);
+        IXCHK(rocprim::exclusive_scan(B.temp, tb, B.kc, B.koff, (uint64_t)0, (size_t)NK + 1, rocprim::plus<uint64_t>(), s));
+        if (n > 0) {
+            tb = B.temp_bytes;
+            IXCHK(rocprim::radix_sort_pairs(B.temp, tb, B.key0, B.key1, B.val0, B.kpos, (size_t)n, 0u, 25u, s));
+            hipLaunchKernelGGL(ix_kext_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kpos, B.koff,
+                               B.kext);
+            IXCHK(hipGetLastError());
+        }
+    } else {
+        // chunks of B.chunk positions (a divisor of 2^32, so one starts at 2^32): the global
+        // histogram and koff first, then per chunk a sort and a scatter of its hits behind the
+        // earlier chunks' (kcur); ksplit = kcur when the chunk at 2^32 begins
+        hipLaunchKernelGGL(ix_count_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kc);
         IXCHK(hipGetLastError());
+        size_t tb = B.temp_bytes;
+        IXCHK(rocprim::exclusive_scan(B.temp, tb, B.kc, B.koff, (uint64_t)0, (size_t)NK + 1, rocprim::plus<uint64_t>(), s));
+        IXCHK(hipMemcpyAsync(B.kcur, B.koff, (size_t)NK * 8, hipMemcpyDeviceToDevice, s));
+        for (int64_t c0 = 0; c0 < n; c0 += B.chunk) {
+            const int64_t m = n - c0 < B.chunk ? n - c0 : B.chunk;
+            if (c0 == (int64_t)seedc::POS_PAGE && B.ksplit)
+                IXCHK(hipMemcpyAsync(B.ksplit, B.kcur, (size_t)NK * 8, hipMemcpyDeviceToDevice, s));
+            IXCHK(hipMemsetAsync(B.kcc, 0, ((size_t)NK + 1) * 4, s));
+            hipLaunchKernelGGL(ix_chunk_keys_kernel, dim3(blocks_for(m, 256)), dim3(256), 0, s, B.text, n, c0, m,
+                               B.key0, B.val0, B.kcc);
+            IXCHK(hipGetLastError());
+            tb = B.temp_bytes;
+            IXCHK(rocprim::exclusive_scan(B.temp, tb, B.kcc, B.koffc, 0u, (size_t)NK + 1, rocprim::plus<uint32_t>(), s));
+            tb = B.temp_bytes;
+            IXCHK(rocprim::radix_sort_pairs(B.temp, tb, B.key0, B.key1, B.val0, B.val1, (size_t)m, 0u, 25u, s));
+            hipLaunchKernelGGL(ix_chunk_scatter_kernel, dim3(blocks_for(m, 256)), dim3(256), 0, s, B.text, n, c0, B.key1,
+                               B.val1, B.koffc, B.kcur, B.kpos, B.kext);
+            IXCHK(hipGetLastError());
+            hipLaunchKernelGGL(ix_chunk_advance_kernel, dim3(blocks_for((int64_t)NK, 256)), dim3(256), 0, s, B.kcur,
+                               B.kcc);
+            IXCHK(hipGetLastError());
+        }
     }
     // j-mer count tables: run ends first, then the children's sums from j = 11 down
     for (int j = 1; j < KI; ++j) IXCHK(hipMemsetAsync(B.cnt[j - 1], 0, ((size_t)1 << (2 * j)) * 4, s));
@@ -178,14 +263,16 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
     return 0;
 }
 
-// bytes of rocPRIM temporary storage for n text positions
-size_t seed_index_temp_bytes(int64_t n) {
-    size_t a = 0, b = 0;
-    (void)rocprim::exclusive_scan(nullptr, a, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)NK + 1,
+// bytes of rocPRIM temporary storage for sorts of `chunk` text positions
+size_t seed_index_temp_bytes(int64_t chunk) {
+    size_t a = 0, b = 0, c = 0;
+    (void)rocprim::exclusive_scan(nullptr, a, (uint32_t *)nullptr, (uint64_t *)nullptr, (uint64_t)0, (size_t)NK + 1,
+                                  rocprim::plus<uint64_t>());
+    (void)rocprim::exclusive_scan(nullptr, c, (uint32_t *)nullptr, (uint32_t *)nullptr, 0u, (size_t)NK + 1,
                                   rocprim::plus<uint32_t>());
     (void)rocprim::radix_sort_pairs(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                    (uint32_t *)nullptr, (size_t)(n > 0 ? n : 1), 0u, 25u);
-    return (a > b ? a : b) + 256;
+                                    (uint32_t *)nullptr, (size_t)(chunk > 0 ? chunk : 1), 0u, 25u);
+    return std::max(a, std::max(b, c)) + 256;
 }
 
 }  // namespace prgpu

@@ -105,8 +105,8 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
             }
             const int a = lo;
             const uint32_t code = (uint32_t)S.codes[a];
-            const uint32_t r = V.koff[code] + (uint32_t)(k - ho[a]);
-            const uint32_t p = V.kpos[r];
+            const uint64_t r = V.koff[code] + (uint64_t)(k - ho[a]);
+            const uint64_t p = seedc::hit_pos(V, code, r);
             const uint64_t exb = V.kext[r];
             const uint64_t qe = S.qext[a];
             const int le = (int)(exb >> 56), lq = (int)(qe >> 56);
@@ -117,7 +117,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
             int ml = KI + m;
             if (m == KX)
                 while (a + ml < len && q[a + ml] < 4 && V.text[p + ml] == q[a + ml]) ++ml;
-            S.hpos[k] = p;
+            seedc::set_hpos(S, k, p);
             S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
         }
         __threadfence_block();
