@@ -356,6 +356,10 @@ int pr_seed_index_occ(const pr_seed_index *h, const uint8_t *s, int n, int64_t *
 /* order-sensitive digests of the index tables (text, koff, kpos, kext, j-mer counts,
    contig tables): a test hook proving that build changes leave the tables identical */
 int pr_seed_index_digest(const pr_seed_index *h, uint64_t *out6);
+/* test hooks: the k-mer offsets koff[4^12 + 1] and, for texts beyond 2^32, the first hit of
+ * every k-mer at or beyond 2^32 (ksplit[4^12], left untouched otherwise); host / device index */
+int pr_seed_index_koff(const pr_seed_index *h, uint64_t *koff, uint64_t *ksplit);
+int pr_seed_gpu_index_koff(pr_ctx *ctx, uint64_t *koff, uint64_t *ksplit);
 int pr_seed_smem(const pr_seed_index *h, const uint8_t *q, int len, int x, int64_t min_intv, int32_t *start,
                  int32_t *end, int64_t *occ, int cap, int *n_out);
 /* The GPU seeding path (seed_kernels.hip: the same per-read core; pass 1 64 reads per wave,

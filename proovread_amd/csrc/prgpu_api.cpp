@@ -1412,7 +1412,7 @@ extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const i
     int64_t chunk = (int64_t)1 << 30;
     if (const char *ch = getenv("PRGPU_INDEX_CHUNK")) {
         const int k = atoi(ch);
-        if (k >= 16 && k <= 32) chunk = (int64_t)1 << k;
+        if (k >= 16 && k <= 31) chunk = (int64_t)1 << k;
     }
     const bool chunked = n_text > chunk;
     const size_t ns = (size_t)(chunked ? chunk : (int64_t)nt);   // sort scratch entries
@@ -1520,7 +1520,20 @@ extern "C" int pr_seed_gpu_index_digest(pr_ctx *c, uint64_t *out6) {
         HIPCHK(hipMemcpy(cnt[(size_t)j].data(), v.cnt[j], cnt[(size_t)j].size() * 4, hipMemcpyDeviceToHost));
     }
     cnt[seedc::KI - 1] = std::move(kc);
-    seed_digest_tables(text, koff, kpos, kext, cnt, cstart, cblk, lro, out6);
+    std::vector<uint64_t> ksplit(v.ksplit ? nk : 0);
+    if (v.ksplit) HIPCHK(hipMemcpy(ksplit.data(), v.ksplit, nk * 8, hipMemcpyDeviceToHost));
+    seed_digest_tables(text, koff, kpos, kext, cnt, cstart, cblk, lro, ksplit, out6);
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_index_koff(pr_ctx *c, uint64_t *koff, uint64_t *ksplit) {
+    if (!c || !koff) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->seed_loaded) return set_error(PR_ERR_ARG, "no device seed index");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(koff, c->seed_view.koff, ((size_t)seedc::NK + 1) * 8, hipMemcpyDeviceToHost));
+    if (ksplit && c->seed_view.ksplit)
+        HIPCHK(hipMemcpy(ksplit, c->seed_view.ksplit, (size_t)seedc::NK * 8, hipMemcpyDeviceToHost));
     return 0;
 }
 

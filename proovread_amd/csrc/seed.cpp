@@ -624,6 +624,15 @@ extern "C" int pr_seed_index_digest(const pr_seed_index *h, uint64_t *out6) {
     if (!h || !out6) return pr_set_error(PR_ERR_ARG, "null arg");
     const Index &I = h->I;
     digest6(I.text, I.koff, I.kpos, I.kext, I.cnt, I.cstart, I.cblk, I.lr_off, out6);
+    if (!I.ksplit.empty()) out6[1] ^= digest_of(I.ksplit.data(), I.ksplit.size()) * 31;   // texts beyond 2^32
+    return 0;
+}
+
+// test hook: the k-mer offsets [NK + 1] and (texts beyond 2^32) the page splits [NK]
+extern "C" int pr_seed_index_koff(const pr_seed_index *h, uint64_t *koff, uint64_t *ksplit) {
+    if (!h || !koff) return pr_set_error(PR_ERR_ARG, "null arg");
+    std::memcpy(koff, h->I.koff.data(), h->I.koff.size() * 8);
+    if (ksplit && !h->I.ksplit.empty()) std::memcpy(ksplit, h->I.ksplit.data(), h->I.ksplit.size() * 8);
     return 0;
 }
 
@@ -631,8 +640,10 @@ namespace prgpu {
 void seed_digest_tables(const std::vector<uint8_t> &text, const std::vector<uint64_t> &koff,
                         const std::vector<uint32_t> &kpos, const std::vector<uint64_t> &kext,
                         const std::vector<std::vector<uint32_t>> &cnt, const std::vector<int64_t> &cstart,
-                        const std::vector<int32_t> &cblk, const std::vector<int64_t> &lr_off, uint64_t *out6) {
+                        const std::vector<int32_t> &cblk, const std::vector<int64_t> &lr_off,
+                        const std::vector<uint64_t> &ksplit, uint64_t *out6) {
     digest6(text, koff, kpos, kext, cnt, cstart, cblk, lr_off, out6);
+    if (!ksplit.empty()) out6[1] ^= digest_of(ksplit.data(), ksplit.size()) * 31;
 }
 }  // namespace prgpu
 

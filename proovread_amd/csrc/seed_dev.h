@@ -48,6 +48,7 @@ SeedIndexSizes seed_index_sizes(const pr_seed_index *h);
 void seed_digest_tables(const std::vector<uint8_t> &text, const std::vector<uint64_t> &koff,
                         const std::vector<uint32_t> &kpos, const std::vector<uint64_t> &kext,
                         const std::vector<std::vector<uint32_t>> &cnt, const std::vector<int64_t> &cstart,
-                        const std::vector<int32_t> &cblk, const std::vector<int64_t> &lr_off, uint64_t *out6);
+                        const std::vector<int32_t> &cblk, const std::vector<int64_t> &lr_off,
+                        const std::vector<uint64_t> &ksplit, uint64_t *out6);
 
 }  // namespace prgpu

@@ -36,9 +36,12 @@ constexpr uint32_t NK = seedc::NK;
 constexpr int KI = seedc::KI;
 constexpr int KX = seedc::KX;
 
+// Kernels over the whole text are grid-stride loops over a capped grid: a dispatch's grid is
+// counted in work-items in 32 bits, and the text may exceed 2^32 positions.
 __global__ void ix_text_kernel(const uint8_t *lr_seq, const int64_t *lr_off, int n_lr, const int64_t *cstart,
                                int64_t l_pac, uint8_t *text) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nt = l_pac > n_lr ? l_pac : n_lr;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nt; g += (int64_t)gridDim.x * blockDim.x) {
     if (g < l_pac) {
         int lo = 0, hi = n_lr - 1;   // read i: lr_off[i] <= g < lr_off[i + 1]
         while (lo < hi) {
@@ -56,6 +59,7 @@ __global__ void ix_text_kernel(const uint8_t *lr_seq, const int64_t *lr_off, int
         text[cstart[g] + len] = SEP;
         text[cstart[2 * (int64_t)n_lr - 1 - g] + len] = SEP;
     }
+  }
 }
 
 __global__ void ix_keys_kernel(const uint8_t *text, int64_t n, uint32_t *key, uint32_t *val, uint32_t *kc) {
@@ -110,16 +114,16 @@ __global__ void ix_kext_kernel(const uint8_t *text, int64_t n, const uint32_t *k
 
 // chunked build (texts beyond one sort): the 12-mer histogram of the whole text
 __global__ void ix_count_kernel(const uint8_t *text, int64_t n, uint32_t *kc) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p + KI > n) return;
-    uint32_t code = 0;
-    bool ok = true;
-    for (int x = 0; x < KI; ++x) {
-        const uint8_t c = text[p + x];
-        ok &= c < 4;
-        code = (code << 2) | (c & 3u);
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p + KI <= n; p += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t code = 0;
+        bool ok = true;
+        for (int x = 0; x < KI; ++x) {
+            const uint8_t c = text[p + x];
+            ok &= c < 4;
+            code = (code << 2) | (c & 3u);
+        }
+        if (ok) atomicAdd(&kc[code], 1u);
     }
-    if (ok) atomicAdd(&kc[code], 1u);
 }
 
 // one chunk [c0, c0 + m): (key, position - c0) pairs and the chunk's histogram
@@ -163,15 +167,16 @@ __global__ void ix_chunk_advance_kernel(uint64_t *kcur, const uint32_t *kcc) {
 // run ends: one thread per text position holding N / SEP; the j-mers (j < 12) that end
 // just before it inside the run of bases are counted into cnt[j - 1]
 __global__ void ix_tail_kernel(const uint8_t *text, int64_t n, uint32_t *const *cnt) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n || text[p] <= 3) return;
-    uint32_t code = 0;
-    for (int j = 1; j < KI; ++j) {
-        if (p - j < 0) break;
-        const uint8_t c = text[p - j];
-        if (c > 3) break;
-        code |= (uint32_t)c << (2 * (j - 1));   // T[p-j] is the first base of the j-mer
-        atomicAdd(&cnt[j - 1][code], 1u);
+    for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
+        if (text[p] <= 3) continue;
+        uint32_t code = 0;
+        for (int j = 1; j < KI; ++j) {
+            if (p - j < 0) break;
+            const uint8_t c = text[p - j];
+            if (c > 3) break;
+            code |= (uint32_t)c << (2 * (j - 1));   // T[p-j] is the first base of the j-mer
+            atomicAdd(&cnt[j - 1][code], 1u);
+        }
     }
 }
 
@@ -184,6 +189,11 @@ __global__ void ix_jmer_kernel(uint32_t *cj, const uint32_t *cn, int64_t nj) {
 }
 
 inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+// grid-stride kernels: at most 2^22 workgroups (2^30 work-items per dispatch)
+inline unsigned blocks_capped(int64_t n, int t) {
+    const int64_t b = (n + t - 1) / t;
+    return (unsigned)(b < 1 ? 1 : (b > ((int64_t)1 << 22) ? ((int64_t)1 << 22) : b));
+}
 }  // namespace
 
 #define IXCHK(x)                                   \
@@ -197,7 +207,7 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
     // text
     if (B.l_pac > 0 || B.n_lr > 0) {
         const int64_t nt = B.l_pac > B.n_lr ? B.l_pac : B.n_lr;
-        hipLaunchKernelGGL(ix_text_kernel, dim3(blocks_for(nt, 256)), dim3(256), 0, s, B.lr_seq, B.lr_off, B.n_lr,
+        hipLaunchKernelGGL(ix_text_kernel, dim3(blocks_capped(nt, 256)), dim3(256), 0, s, B.lr_seq, B.lr_off, B.n_lr,
                            B.cstart, B.l_pac, B.text);
         IXCHK(hipGetLastError());
     }
@@ -223,7 +233,7 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
         // chunks of B.chunk positions (a divisor of 2^32, so one starts at 2^32): the global
         // histogram and koff first, then per chunk a sort and a scatter of its hits behind the
         // earlier chunks' (kcur); ksplit = kcur when the chunk at 2^32 begins
-        hipLaunchKernelGGL(ix_count_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kc);
+        hipLaunchKernelGGL(ix_count_kernel, dim3(blocks_capped(n, 256)), dim3(256), 0, s, B.text, n, B.kc);
         IXCHK(hipGetLastError());
         size_t tb = B.temp_bytes;
         IXCHK(rocprim::exclusive_scan(B.temp, tb, B.kc, B.koff, (uint64_t)0, (size_t)NK + 1, rocprim::plus<uint64_t>(), s));
@@ -251,7 +261,7 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
     // j-mer count tables: run ends first, then the children's sums from j = 11 down
     for (int j = 1; j < KI; ++j) IXCHK(hipMemsetAsync(B.cnt[j - 1], 0, ((size_t)1 << (2 * j)) * 4, s));
     if (n > 0) {
-        hipLaunchKernelGGL(ix_tail_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.cnt_dev);
+        hipLaunchKernelGGL(ix_tail_kernel, dim3(blocks_capped(n, 256)), dim3(256), 0, s, B.text, n, B.cnt_dev);
         IXCHK(hipGetLastError());
     }
     for (int j = KI - 1; j >= 1; --j) {

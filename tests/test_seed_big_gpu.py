@@ -78,8 +78,12 @@ def test_device_index_beyond_2_32_matches_host(finish):
     assert n_text > 2 ** 32
     sr, sr_off = d.sr_seq, d.sr_off
     want = host_tasks(seq, off, sr, sr_off, finish)
+    hx = seed.SeedIndex(seq, off)
+    want_digest = hx.digest()
+    hx.close()
     ctx = _abi.default_context()
     ix = seed.DeviceSeedIndex(ctx, seq, off)
+    assert ix.digest() == want_digest   # every table, ksplit included
     got, st = ix.map(sr, sr_off, seed.default_opts(finish))
     assert (st == 0).all()
     assert len(want) > d.n_sr

@@ -26,7 +26,9 @@ ASCII = np.frombuffer(b"ACGTN", np.uint8)
 
 def _data(finish):
     from proovread_amd import synth
-    d = synth.simulate(71 + finish, 60000, 48, 3000, 30, sr_frac=1.0)
+    # finish: reads as after the iterations (the finish scoring rejects raw 15 % CLR alignments)
+    err = dict(p_ins=0.02, p_del=0.01, p_sub=0.005) if finish else {}
+    d = synth.simulate(71 + finish, 60000, 48, 3000, 30, sr_frac=1.0, **err)
     ref = ASCII[d.lr_seq]
     rng = np.random.default_rng(5)
     qual = (rng.integers(0, 30, len(ref)) + 33).astype(np.uint8)
