@@ -6,16 +6,23 @@ a synthetic workload of BASELINE.json configs[1] size per GPU.
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-A step = one iteration over the rank's whole batch (every long read of the
-shard, every seed-extension task): SW extension kernel, SW global/CIGAR
-kernel, per-read coordinate sort, consensus kernel, the masking of the
-corrected reads (SeqFilter --phred-mask) with its {bpt, bpN} statistic
+A step = one iteration over the rank's whole batch: SW extension kernels, SW
+global/CIGAR kernel, per-read coordinate sort, consensus kernel, the masking of
+the corrected reads (SeqFilter --phred-mask) with its {bpt, bpN} statistic
 all-reduced across GPUs (RCCL inside libprgpu) as proovread's
 mask_shortcut_frac input.  No torch in the process: libprgpu owns the HIP
-runtime, the device buffers and the collectives.
-Inputs are resident in HBM before the timed region.  Long reads shard across
-GPUs with no data-path collective (weak scaling: every rank holds a
-configs[1]-size shard; 8 ranks ~ configs[2]).
+runtime, the device buffers and the collectives.  Inputs are resident in HBM
+before the timed region.  Weak scaling: every rank generates a configs[1]-size
+share of the reads (8 ranks ~ configs[2]).
+
+--layout exact (default): the correction loop's own multi-GPU layout
+(correct.py; SURVEY.md §8e exact-parity option): every rank
+indexes ALL long reads (the ranks' shares all-gathered), seeds and aligns its
+short reads against them, and the step sends every reported alignment to the
+owner of its long read (device pack + one RCCL all-to-all of device buffers,
+pr_aln_exchange) before the owners' -b/-l filter, hand-off and consensus.
+--layout shards: every rank indexes only its own long reads (no alignment
+exchange; not bit-exact against one index at -D / occurrence caps).
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §Measurement for every field).
 """
@@ -61,6 +68,9 @@ def parse():
     ap.add_argument("--comm", choices=("rccl", "none"), default="rccl",
                     help="rccl: the step all-reduces the device {bpt, bpN} statistic over an RCCL communicator at "
                          "every world size (N=1 included, exactly as N>1 runs it); none: no communicator at N=1")
+    ap.add_argument("--layout", choices=("exact", "shards"), default="exact",
+                    help="exact: the correction loop's multi-GPU layout (all long reads indexed on every rank, "
+                         "alignments all-to-all to the long reads' owners); shards: independent long-read shards")
     ap.add_argument("--seeds", choices=("truth", "host", "gpu"), default="gpu",
                     help="seeds: the product's seeding front end (host path / GPU path; bwa mem seeding "
                          "+ chaining restated; every seed of the kept chains in bwa mode), or the simulation "
@@ -98,6 +108,18 @@ def cpu_baseline(d, per_worker: int):
                         if d.t_chain is not None else f"their {r['tasks']} seed-extension tasks")
                      + f"), SW + consensus C restatement (oracle/), {r['workers']} processes, {r['wall_s']:.1f} s"}
     return cpu, r["results"]
+
+
+def gather_pool(cm, seq, off):
+    """The ranks' read pools back to back in rank order (RCCL all-gather, outside the timed
+    region) -> (pool, offsets, global id of this rank's first read)."""
+    parts = cm.allgather_bytes(np.ascontiguousarray(seq, np.uint8).tobytes())
+    lens = cm.allgather_bytes(np.diff(np.asarray(off, np.int64)).astype(np.int64).tobytes())
+    n = [len(x) // 8 for x in lens]
+    L = np.concatenate([np.frombuffer(x, np.int64) for x in lens])
+    o = np.zeros(len(L) + 1, np.int64)
+    np.cumsum(L, out=o[1:])
+    return np.frombuffer(b"".join(parts), np.uint8), o, int(sum(n[:cm.rank]))
 
 
 def check_parity(it, cpu_res):
@@ -145,20 +167,22 @@ def main():
     lr_bases = int(d.lr_off[-1])
     seed_info = None
 
-    def seed_front_end(ctx=None, want_host_copy=True):
+    def seed_front_end(ctx=None, want_host_copy=True, lr_seq=None, lr_off=None):
         """The front end (bwa-proovread index + mem seeding and chaining) on this rank's reads,
         outside the timed region: the step measures the iteration from resident seeds.
         ctx: index built in HBM and seeding on the GPU, the seeds left in HBM for the
         iteration (no host round trip); with want_host_copy they are also downloaded (CPU
         baseline, and the check against the host path on a sample of reads).  None: host C++
-        threads."""
+        threads.  lr_seq / lr_off: the long reads indexed (default: this rank's)."""
         from proovread_amd import seed as seeding
         o = seeding.default_opts(False)
+        if lr_seq is None:
+            lr_seq, lr_off = d.lr_seq, d.lr_off
         t = time.perf_counter()
         if ctx is None:
-            ix = seeding.SeedIndex(d.lr_seq, d.lr_off)
+            ix = seeding.SeedIndex(lr_seq, lr_off)
         else:
-            ix = seeding.DeviceSeedIndex(ctx, d.lr_seq, d.lr_off)
+            ix = seeding.DeviceSeedIndex(ctx, lr_seq, lr_off)
         t_ix = time.perf_counter() - t
         t = time.perf_counter()
         tasks = None
@@ -193,6 +217,7 @@ def main():
         else:
             check = None
         info = {"path": "gpu" if ctx is not None else "host", "index_s": round(t_ix, 3), "map_s": round(t_map, 3),
+                "indexed_long_read_bases": int(lr_off[-1]),
                 "reads_per_s": round(d.n_sr / t_map, 1), "index_kernel_ms": ix_ms, "kernel_ms": ms,
                 "parity_vs_host": check, "kernel_phase_ms_summed_over_waves": seed_phases}
         if tasks is not None:
@@ -201,6 +226,9 @@ def main():
             return synth.with_seeds(d, tasks), info
         return dataclasses.replace(d, t_chain=np.zeros(0, np.int32)), info
 
+    exact = args.layout == "exact"
+    if exact and args.seeds != "gpu":
+        raise SystemExit("bench: --layout exact seeds on the GPU (--seeds gpu)")
     if args.seeds == "host":
         d, seed_info = seed_front_end()
 
@@ -216,13 +244,32 @@ def main():
     from proovread_amd import _abi, cns, comm as comm_mod, iteration, sw
     ctx = _abi.Context(local)
     cm = comm_mod.RcclComm.from_env(ctx) if world > 1 or args.comm == "rccl" else None
+    # exact layout: the global read set = the ranks' shares in rank order (all-gathered)
+    lr_all, lr_off_all, sr_all, sr_off_all, s0 = d.lr_seq, d.lr_off, d.sr_seq, d.sr_off, 0
+    gather_s = 0.0
+    if exact and world > 1:
+        t = time.perf_counter()
+        lr_all, lr_off_all, _ = gather_pool(cm, d.lr_seq, d.lr_off)
+        sr_all, sr_off_all, s0 = gather_pool(cm, d.sr_seq, d.sr_off)
+        gather_s = time.perf_counter() - t
     if args.seeds == "gpu":
-        d, seed_info = seed_front_end(ctx, want_host_copy=rank == 0)
+        d, seed_info = seed_front_end(ctx, want_host_copy=rank == 0 and world == 1, lr_seq=lr_all, lr_off=lr_off_all)
         if want_cpu:   # the same GPU-made seeds, CPU chain in a child process
             cpu, cpu_res = cpu_baseline(d, args.cpu_lrs_per_worker)
     t_up = time.perf_counter()
     # host -> HBM upload of the reads; GPU seeds stay in HBM (outside the step)
-    it = iteration.Iteration(d, ctx=ctx, gpu_seeds=args.seeds == "gpu")
+    if exact:
+        from proovread_amd import exact_shard as ex
+        bounds = ex.lr_bounds(lr_off_all, world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        shard = iteration.ShardSW(ctx, sr_all, sr_off_all, s0, s0 + d.n_sr, lr_all, lr_off_all)
+        ref_all = np.frombuffer(b"ACGTN", np.uint8)[lr_all]
+        qual_all = np.full(len(lr_all), ord("$"), np.uint8)   # raw CLR reads: phred 3
+        it = iteration.OwnedIteration(ctx, lo, hi, lr_off_all, ref_all, qual_all, sr_all, sr_off_all)
+        own_bases = int(lr_off_all[hi] - lr_off_all[lo])
+    else:
+        it = iteration.Iteration(d, ctx=ctx, gpu_seeds=args.seeds == "gpu")
+        own_bases = lr_bases
     upload_s = time.perf_counter() - t_up
     opts = sw.default_opts(finish=False)
     opts.bin_size, opts.bin_length = BIN_FILTER     # bwa-proovread -b 20 -l 300 (proovread:1302-1313)
@@ -231,8 +278,14 @@ def main():
     mparams = mask.params("20,41,80,130,60,0.7", 150)   # hcr-mask of bwa-sr-1 (proovread.cfg:234-242)
     stats = _abi.DevBuffer(ctx, 16)
 
-    def step():
+    def launch():
+        if exact:   # SW of the short-read shard, alignments to their owners, owners' consensus
+            shard.launch(opts)
+            iteration.exchange(ctx, cm, s0, bounds)
         it.launch(opts, params)
+
+    def step():
+        launch()
         it.mask_to(stats.ptr, mparams)   # SeqFilter --phred-mask: next reference + {bpt, bpN}
         if cm is not None:
             cm.allreduce_dev(stats.ptr, 2)   # RCCL: global bpt / bpN (mask_shortcut_frac input)
@@ -261,11 +314,15 @@ def main():
         ext_cells, ext_launches = xc, xn
     barrier()
     el = time.perf_counter() - t0
+    e2e_ms = ((seed_info["index_s"] + seed_info["map_s"] + upload_s) * 1e3 + el / args.steps * 1e3
+              if seed_info else None)
     if cm is not None:
         el = cm.allreduce_floats([el], comm_mod.RED_MAX)[0]
-        total_bases = cm.allreduce_ints([lr_bases])[0]
+        total_bases = cm.allreduce_ints([own_bases])[0]
+        if e2e_ms is not None:
+            e2e_ms = cm.allreduce_floats([e2e_ms], comm_mod.RED_MAX)[0]
     else:
-        total_bases = lr_bases
+        total_bases = own_bases
     ms /= max(args.steps, 1)
     me, mg, ce, cg = sw.last_timing(ctx)
     bwa_rounds, bwa_ext, bwa_patch = sw.bwa_stats(ctx) if d.t_chain is not None else (0, 0, 0)
@@ -291,7 +348,7 @@ def main():
     ext_tops = ext_cells * OPS_PER_CELL / (ext_ms * 1e-3) / 1e12 if ext_ms > 0 else 0.0
     # pileup kernel: algorithmic bytes (SURVEY.md §8d model) / kernel time
     n_aln, sum_ncig, sum_lseq = it.alignment_stats()
-    cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + lr_bases * (2 + 2 + 6 * 4 * 2)
+    cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + own_bases * (2 + 2 + 6 * 4 * 2)
     # HBM bytes per launch from the PMC FETCH_SIZE / WRITE_SIZE passes of this bwa-mode step
     # (tools/r03_final.sh -> tools/pmc_summary.py -> profiles/pmc_r03o.json)
     prof = ROOT / "profiles" / PMC_FILE
@@ -336,7 +393,11 @@ def main():
                         "50x 2x150 short reads sampled to 15x for one bwa-sr iteration",
             "genome_bp": gl, "long_reads_per_gpu": d.n_lr, "long_read_bases_per_gpu": lr_bases,
             "short_reads_per_gpu": d.n_sr, "seeds_per_gpu": it.n_task, "task": "bwa-sr-1",
-            "coverage_cap": params.coverage, "parallelism": f"long-read shards x{world}",
+            "coverage_cap": params.coverage,
+            "parallelism": (f"exact-parity layout x{world}: every rank indexes all {len(lr_off_all) - 1} long reads "
+                            f"({int(lr_off_all[-1])} bases), aligns its short reads, alignments all-to-all to the "
+                            f"long reads' owners over RCCL (pr_aln_exchange)" if exact else f"long-read shards x{world}"),
+            "layout": args.layout,
         },
         "sw_gcups": round(cells / ((ms[0] + ms[1]) * 1e-3) / 1e9, 2),
         # bwa mode: mem_chain2aln rounds, seeds extended (first seeds of every chain + the ones the
@@ -382,8 +443,11 @@ def main():
         "seeding": seed_info,
         # one whole bwa-sr iteration as proovread runs it, wall clock: index build + seeding
         # (bwa-proovread index / mem front end; seeds left in HBM) + upload + the timed step
-        "iteration_end_to_end_ms": (round((seed_info["index_s"] + seed_info["map_s"] + upload_s) * 1e3 +
-                                          el / args.steps * 1e3, 1) if seed_info else None),
+        "iteration_end_to_end_ms": round(e2e_ms, 1) if e2e_ms is not None else None,
+        # whole-iteration throughput (index + seeding + upload + step, max over ranks): the rate of a
+        # bwa-sr task as the loop runs it; `value` is the step alone (inputs and seeds resident)
+        "value_iteration": round(total_bases / (e2e_ms * 1e-3) / 1e6, 3) if e2e_ms else None,
+        "read_gather_ms": round(gather_s * 1e3, 1),
         "upload_ms": round(upload_s * 1e3, 1),
         "gen_s": round(gen_s, 1),
         "reads_ok": ok,

@@ -440,10 +440,12 @@ int pr_iter_last_timing(pr_ctx *ctx, double *ms_sw_extend, double *ms_sw_global,
  *    the device, the counts exchanged, one RCCL all-to-all of device buffers (comm NULL: world
  *    1, no RCCL); lr_bounds[world+1] are the owners' long-read ranges, sr0 the global id of the
  *    shard's first short read.  n_recv: records this rank received.
- * 3. pr_iter_upload_owned (after 2): the owned long reads (consensus reference, qualities) and
- *    every short read of the task (the consensus reads SEQ from it by global id).
+ * 3. pr_iter_upload_owned: the owned long reads (consensus reference, qualities) and every
+ *    short read of the task (the consensus reads SEQ from it by global id); once per task --
+ *    steps 1's launch, 2 and 4 may be repeated on the resident batches.
  * 4. pr_iter_launch (its SW options give -b/-l) runs filter + hand-off + consensus over the
- *    received alignments (no SW); pr_iter_download / pr_iter_mask / pr_iter_stats as usual. */
+ *    alignments the last exchange received (no SW); pr_iter_download / pr_iter_mask /
+ *    pr_iter_stats as usual; pr_iter_last_timing's hand-off includes the exchange. */
 int pr_sw_upload_gpu_seeds(pr_ctx *ctx, const pr_sw_batch *b);
 int pr_aln_exchange(pr_ctx *ctx, pr_comm *comm, int64_t sr0, const int64_t *lr_bounds, int64_t *n_recv);
 /* the same exchange among `world` contexts of ONE process (several shards on one GPU, or one

@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -23,6 +24,7 @@ int ctx_device(pr_ctx *c);
 int pr_set_error(int code, const char *msg);
 
 static_assert(PR_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
+constexpr int64_t P2P_PIECE = (int64_t)1 << 28;   // bytes per ncclSend / ncclRecv
 
 struct pr_comm {
     pr_ctx *ctx = nullptr;
@@ -156,20 +158,26 @@ extern "C" int pr_comm_allgatherv_host(pr_comm *c, const uint8_t *send, int64_t 
     }
     if (!recv) return 0;   // size query
     if (tot > recv_cap) return pr_set_error(PR_ERR_CAPACITY, "all-gather receive buffer too small");
-    cap = (cap + 255) & ~(int64_t)255;
-    if ((rc = stage(c, (size_t)cap * (size_t)(W + 1)))) return rc;
+    // in pieces of at most P2P_PIECE bytes per rank (one staging area of world + 1 pieces)
+    const int64_t piece = std::min<int64_t>((cap + 255) & ~(int64_t)255, P2P_PIECE);
+    if ((rc = stage(c, (size_t)piece * (size_t)(W + 1)))) return rc;
     hipStream_t s = ctx_stream(c->ctx);
-    uint8_t *mine = (uint8_t *)c->stage + (size_t)cap * (size_t)W;
+    uint8_t *mine = (uint8_t *)c->stage + (size_t)piece * (size_t)W;
     uint8_t *all = (uint8_t *)c->stage;
     HIPCHK(hipSetDevice(ctx_device(c->ctx)));
-    if (nbytes) HIPCHK(hipMemcpyAsync(mine, send, (size_t)nbytes, hipMemcpyHostToDevice, s));
-    NCCLCHK(ncclAllGather(mine, all, (size_t)cap, ncclUint8, c->nc, s));
-    int64_t o = 0;
-    for (int r = 0; r < W; ++r) {
-        if (sz[(size_t)r]) HIPCHK(hipMemcpyAsync(recv + o, all + (size_t)cap * r, (size_t)sz[(size_t)r], hipMemcpyDeviceToHost, s));
-        o += sz[(size_t)r];
+    std::vector<int64_t> o((size_t)W + 1, 0);
+    for (int r = 0; r < W; ++r) o[(size_t)r + 1] = o[(size_t)r] + sz[(size_t)r];
+    for (int64_t k = 0; k < cap; k += piece) {
+        const int64_t mk = std::min<int64_t>(piece, nbytes - k);
+        if (mk > 0) HIPCHK(hipMemcpyAsync(mine, send + k, (size_t)mk, hipMemcpyHostToDevice, s));
+        NCCLCHK(ncclAllGather(mine, all, (size_t)piece, ncclUint8, c->nc, s));
+        for (int r = 0; r < W; ++r) {
+            const int64_t n = std::min<int64_t>(piece, sz[(size_t)r] - k);
+            if (n > 0) HIPCHK(hipMemcpyAsync(recv + o[(size_t)r] + k, all + (size_t)piece * r, (size_t)n,
+                                             hipMemcpyDeviceToHost, s));
+        }
+        HIPCHK(hipStreamSynchronize(s));   // `mine` / `all` are reused by the next piece
     }
-    HIPCHK(hipStreamSynchronize(s));
     return 0;
 }
 
@@ -194,15 +202,7 @@ extern "C" int pr_comm_alltoallv_host(pr_comm *c, const uint8_t *send, const int
     uint8_t *ds = (uint8_t *)c->stage, *dr = (uint8_t *)c->stage + sa;
     HIPCHK(hipSetDevice(ctx_device(c->ctx)));
     if (st) HIPCHK(hipMemcpyAsync(ds, send, (size_t)st, hipMemcpyHostToDevice, s));
-    NCCLCHK(ncclGroupStart());
-    int64_t so = 0, ro = 0;
-    for (int r = 0; r < W; ++r) {
-        if (send_counts[r]) NCCLCHK(ncclSend(ds + so, (size_t)send_counts[r], ncclUint8, r, c->nc, s));
-        if (recv_counts[r]) NCCLCHK(ncclRecv(dr + ro, (size_t)recv_counts[r], ncclUint8, r, c->nc, s));
-        so += send_counts[r];
-        ro += recv_counts[r];
-    }
-    NCCLCHK(ncclGroupEnd());
+    if ((rc = pr_comm_alltoallv_dev(c, ds, send_counts, dr, recv_counts))) return rc;
     if (rt) HIPCHK(hipMemcpyAsync(recv, dr, (size_t)rt, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return 0;
@@ -226,13 +226,27 @@ extern "C" int pr_comm_alltoallv_dev(pr_comm *c, const void *send, const int64_t
     HIPCHK(hipSetDevice(ctx_device(c->ctx)));
     const uint8_t *ds = (const uint8_t *)send;
     uint8_t *dr = (uint8_t *)recv;
-    NCCLCHK(ncclGroupStart());
-    int64_t so = 0, ro = 0;
+    std::vector<int64_t> so((size_t)W + 1, 0), ro((size_t)W + 1, 0);
     for (int r = 0; r < W; ++r) {
-        if (send_counts[r]) NCCLCHK(ncclSend(ds + so, (size_t)send_counts[r], ncclUint8, r, c->nc, s));
-        if (recv_counts[r]) NCCLCHK(ncclRecv(dr + ro, (size_t)recv_counts[r], ncclUint8, r, c->nc, s));
-        so += send_counts[r];
-        ro += recv_counts[r];
+        so[(size_t)r + 1] = so[(size_t)r] + send_counts[r];
+        ro[(size_t)r + 1] = ro[(size_t)r] + recv_counts[r];
+    }
+    // this rank's own block: a device copy (no link involved)
+    if (send_counts[c->rank] != recv_counts[c->rank]) return pr_set_error(PR_ERR_ARG, "self block sizes differ");
+    if (send_counts[c->rank])
+        HIPCHK(hipMemcpyAsync(dr + ro[(size_t)c->rank], ds + so[(size_t)c->rank], (size_t)send_counts[c->rank],
+                              hipMemcpyDeviceToDevice, s));
+    // the other ranks: send/recv pairs in pieces of at most P2P_PIECE bytes (multi-GB blocks in one
+    // ncclSend/ncclRecv came back corrupted at configs[1] size; both sides cut a block the same way)
+    NCCLCHK(ncclGroupStart());
+    for (int r = 0; r < W; ++r) {
+        if (r == c->rank) continue;
+        for (int64_t k = 0; k < send_counts[r]; k += P2P_PIECE)
+            NCCLCHK(ncclSend(ds + so[(size_t)r] + k, (size_t)std::min<int64_t>(P2P_PIECE, send_counts[r] - k), ncclUint8,
+                             r, c->nc, s));
+        for (int64_t k = 0; k < recv_counts[r]; k += P2P_PIECE)
+            NCCLCHK(ncclRecv(dr + ro[(size_t)r] + k, (size_t)std::min<int64_t>(P2P_PIECE, recv_counts[r] - k), ncclUint8,
+                             r, c->nc, s));
     }
     NCCLCHK(ncclGroupEnd());
     return 0;

@@ -751,6 +751,8 @@ extern "C" int pr_aln_exchange(pr_ctx *c, pr_comm *comm, int64_t sr0, const int6
         if ((rc = pr_comm_rank(comm, &rank, &world))) return rc;
     }
     c->x_ready = false;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));   // pr_iter_last_timing: the hand-off includes the exchange
     std::vector<int64_t> nrec, nops;
     if ((rc = xchg_pack(c, world, sr0, lr_bounds, nrec, nops))) return rc;
     std::vector<int64_t> sc_rec((size_t)world), sc_cig((size_t)world), rc_rec((size_t)world), rc_cig((size_t)world);
@@ -836,7 +838,6 @@ extern "C" int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64
 
 extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
-    if (!c->x_ready) return set_error(PR_ERR_ARG, "no received alignments (pr_aln_exchange first)");
     const int n = b->n_lr;
     if (n < 0 || b->n_sr < 0 || (n && (!b->lr_off || !b->ref_seq)) || !b->sr_off || (b->n_sr && !b->sr_seq))
         return set_error(PR_ERR_ARG, "owned batch: lr_off, ref_seq and the short reads are required");
@@ -851,7 +852,7 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     c->cns_launched = false;
     c->iter_masked = false;
     c->n_lr = n;
-    c->n_aln = c->x_nrecv;
+    c->n_aln = 0;   // the received alignments (sized at launch: own_group)
     const int64_t tl = n ? b->lr_off[n] : 0;
     c->total_cols = tl;
     c->has_ref = true;
@@ -874,7 +875,7 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     c->k_need = 1;
     c->pipe_sort_cap = 1;
     DevBuf *B = c->cb;
-    const size_t na1 = (size_t)c->x_nrecv + 1, n1 = (size_t)n + 1;
+    const size_t n1 = (size_t)n + 1;
     if ((rc = upload(B[CB_LR_OFF], c->lr_off_host.data(), n1, s))) return rc;
     if (b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)tl, s))) return rc;
     if ((rc = upload(B[CB_REF_SEQ], b->ref_seq, (size_t)tl, s))) return rc;
@@ -882,19 +883,8 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
         (rc = upload(c->xb[XB_SROFF], b->sr_off, (size_t)b->n_sr + 1, s)))
         return rc;
     if ((rc = c->pb[1].ensure(n1 * 4)) || (rc = c->pb[2].ensure(n1 * 4))) return rc;
-    if ((rc = B[CB_ALN_OFF].ensure(n1 * 8)) || (rc = B[CB_POS].ensure(na1 * 4)) ||
-        (rc = B[CB_SCORE].ensure(na1 * 8)) || (rc = B[CB_AFLAGS].ensure(na1)) ||
-        (rc = B[CB_SEQ_OFF].ensure(na1 * 8)) || (rc = B[CB_LSEQ].ensure(na1 * 4)) ||
-        (rc = B[CB_CIG_OFF].ensure(na1 * 8)) || (rc = B[CB_NCIG].ensure(na1 * 4)))
-        return rc;
-    if ((rc = B[CB_A_ST].ensure(na1 * 4)) || (rc = B[CB_A_LEN].ensure(na1 * 4)) ||
-        (rc = B[CB_A_NC].ensure(na1 * 8)) || (rc = B[CB_A_BIN].ensure(na1 * 4)) ||
-        (rc = B[CB_A_CB].ensure(na1 * 4)) || (rc = B[CB_A_CE].ensure(na1 * 4)) ||
-        (rc = B[CB_A_SB].ensure(na1 * 4)) || (rc = B[CB_A_RPOS].ensure(na1 * 4)) ||
-        (rc = B[CB_A_END].ensure(na1 * 4)) || (rc = B[CB_SORTED].ensure(na1 * 4)) ||
-        (rc = B[CB_LST_SCORE].ensure(na1 * 8)) || (rc = B[CB_LST_ALN].ensure(na1 * 4)) ||
-        (rc = B[CB_KEPT].ensure(na1)) || (rc = B[CB_WORK].ensure(64)) ||
-        (rc = B[CB_PROF].ensure(CNS_NPHASE * 8)) || (rc = B[CB_RETRY].ensure(((size_t)n + 16) * 4)))
+    if ((rc = B[CB_ALN_OFF].ensure(n1 * 8)) || (rc = B[CB_WORK].ensure(64)) || (rc = B[CB_PROF].ensure(CNS_NPHASE * 8)) ||
+        (rc = B[CB_RETRY].ensure(((size_t)n + 16) * 4)))
         return rc;
     if ((rc = upload(B[CB_OUT_OFF], c->out_off.data(), n1, s))) return rc;
     if ((rc = upload(B[CB_CHIM_OFF], c->chim_off.data(), n1, s))) return rc;
@@ -906,17 +896,10 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     if ((rc = B[CB_O_SEQ].ensure(scap)) || (rc = B[CB_O_QUAL].ensure(scap)) || (rc = B[CB_O_TRACE].ensure(scap)) ||
         (rc = B[CB_O_CIG].ensure(scap * 4)) || (rc = B[CB_O_CHIM].ensure(((size_t)c->chim_cap + 1) * 16)))
         return rc;
-    // the hand-off's grouped inputs
     DevBuf *X = c->xb;
-    if ((rc = X[XB_RCIGAT].ensure(na1 * 8)) || (rc = X[XB_GCNT].ensure(n1 * 4)) || (rc = X[XB_GCNT64].ensure(n1 * 8)) ||
-        (rc = X[XB_TASKOFF].ensure(n1 * 8)) || (rc = X[XB_ERR].ensure(16)) || (rc = X[XB_GSR].ensure(na1 * 4)) ||
-        (rc = X[XB_GSTATUS].ensure(na1 * 4)) || (rc = X[XB_GPOS].ensure(na1 * 4)) || (rc = X[XB_GSCORE].ensure(na1 * 4)) ||
-        (rc = X[XB_GNCIG].ensure(na1 * 4)) || (rc = X[XB_GCIGAT].ensure(na1 * 8)) || (rc = X[XB_GSTRAND].ensure(na1)) ||
-        (rc = X[XB_GPASS].ensure(na1)) || (rc = X[XB_KEY0].ensure(na1 * 4)) || (rc = X[XB_KEY1].ensure(na1 * 4)) ||
-        (rc = X[XB_IDX0].ensure(na1 * 4)) || (rc = X[XB_IDX1].ensure(na1 * 4)) || (rc = X[XB_OPIN].ensure(na1 * 8)))
+    if ((rc = X[XB_GCNT].ensure(n1 * 4)) || (rc = X[XB_GCNT64].ensure(n1 * 8)) || (rc = X[XB_TASKOFF].ensure(n1 * 8)) ||
+        (rc = X[XB_ERR].ensure(16)))
         return rc;
-    const size_t tb = xchg_temp_bytes(c->x_nrecv, n);
-    if ((rc = X[XB_TEMP].ensure(tb))) return rc;
     HIPCHK(hipStreamSynchronize(s));
     c->own_lr0 = b->lr0;
     c->own = true;
@@ -927,8 +910,33 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
 
 // owned batch: the received records regrouped by long read into the hand-off's inputs
 static int own_group(pr_ctx *c, SwPtrs *sp) {
+    if (!c->x_ready) return set_error(PR_ERR_ARG, "no received alignments (pr_aln_exchange first)");
     hipStream_t s = c->stream;
     DevBuf *B = c->xb;
+    {   // per-alignment arrays of the hand-off and the consensus, sized by what arrived
+        c->n_aln = c->x_nrecv;
+        const size_t na1 = (size_t)c->x_nrecv + 1;
+        DevBuf *C = c->cb;
+        int rc;
+        if ((rc = C[CB_POS].ensure(na1 * 4)) || (rc = C[CB_SCORE].ensure(na1 * 8)) || (rc = C[CB_AFLAGS].ensure(na1)) ||
+            (rc = C[CB_SEQ_OFF].ensure(na1 * 8)) || (rc = C[CB_LSEQ].ensure(na1 * 4)) ||
+            (rc = C[CB_CIG_OFF].ensure(na1 * 8)) || (rc = C[CB_NCIG].ensure(na1 * 4)) ||
+            (rc = C[CB_A_ST].ensure(na1 * 4)) || (rc = C[CB_A_LEN].ensure(na1 * 4)) ||
+            (rc = C[CB_A_NC].ensure(na1 * 8)) || (rc = C[CB_A_BIN].ensure(na1 * 4)) ||
+            (rc = C[CB_A_CB].ensure(na1 * 4)) || (rc = C[CB_A_CE].ensure(na1 * 4)) ||
+            (rc = C[CB_A_SB].ensure(na1 * 4)) || (rc = C[CB_A_RPOS].ensure(na1 * 4)) ||
+            (rc = C[CB_A_END].ensure(na1 * 4)) || (rc = C[CB_SORTED].ensure(na1 * 4)) ||
+            (rc = C[CB_LST_SCORE].ensure(na1 * 8)) || (rc = C[CB_LST_ALN].ensure(na1 * 4)) ||
+            (rc = C[CB_KEPT].ensure(na1)) || (rc = B[XB_RCIGAT].ensure(na1 * 8)) || (rc = B[XB_GSR].ensure(na1 * 4)) ||
+            (rc = B[XB_GSTATUS].ensure(na1 * 4)) || (rc = B[XB_GPOS].ensure(na1 * 4)) ||
+            (rc = B[XB_GSCORE].ensure(na1 * 4)) || (rc = B[XB_GNCIG].ensure(na1 * 4)) ||
+            (rc = B[XB_GCIGAT].ensure(na1 * 8)) || (rc = B[XB_GSTRAND].ensure(na1)) || (rc = B[XB_GPASS].ensure(na1)) ||
+            (rc = B[XB_KEY0].ensure(na1 * 4)) || (rc = B[XB_KEY1].ensure(na1 * 4)) || (rc = B[XB_IDX0].ensure(na1 * 4)) ||
+            (rc = B[XB_IDX1].ensure(na1 * 4)) || (rc = B[XB_OPIN].ensure(na1 * 8)))
+            return rc;
+        const size_t tb = xchg_temp_bytes(c->x_nrecv, c->n_lr);
+        if ((rc = B[XB_TEMP].ensure(tb))) return rc;
+    }
     XchgRecv R;
     std::memset(&R, 0, sizeof R);
     R.n = c->x_nrecv;
@@ -985,9 +993,8 @@ extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_param
     if (!c->pipe) return set_error(PR_ERR_ARG, "no resident iteration batch (pr_iter_upload first)");
     int rc;
     SwPtrs sp;
-    if (c->own) {   // owned batch: the SW ran before the exchange
+    if (c->own) {   // owned batch: the SW and the exchange ran before (ev[0]: the exchange's start)
         HIPCHK(hipSetDevice(c->device));
-        HIPCHK(hipEventRecord(c->ev[0], c->stream));
         if ((rc = own_group(c, &sp))) return rc;
     } else {
         if ((rc = pr_sw_launch(c, o))) return rc;   // records ev[2], ev[3], ev[0]

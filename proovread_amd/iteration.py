@@ -188,23 +188,37 @@ class Iteration:
         return out
 
 
+class ShardSW:
+    """Exact-parity layout, step 1 on a rank: the bwa-mode SW batch of the short-read shard
+    [s, e) whose seeds the last DeviceSeedIndex.map(keep_on_device=True) left in HBM (the index of
+    ALL long reads, lr_map / lr_off as mapped), uploaded once; launch() runs the SW on it (sr 0
+    of the shard is global id s: bwa's hash ties)."""
+
+    def __init__(self, ctx, sr: np.ndarray, sr_off: np.ndarray, s: int, e: int, lr_map: np.ndarray,
+                 lr_off: np.ndarray):
+        self.L = _abi.lib()
+        _setup(self.L)
+        self.ctx = ctx
+        sr_off = np.asarray(sr_off, np.int64)
+        self._sh_off = np.ascontiguousarray(sr_off[s:e + 1] - sr_off[s], np.int64)
+        self._sh_seq = np.ascontiguousarray(sr[sr_off[s]:sr_off[e]], np.uint8)
+        self._lr_off = np.ascontiguousarray(lr_off, np.int64)
+        self._lr_map = np.ascontiguousarray(lr_map, np.uint8)
+        z = np.zeros(0, np.int32)
+        inp = sw.SwInput(self._sh_off, self._sh_seq, self._lr_off, self._lr_map, z, z, np.zeros(0, np.uint8), z, z, z)
+        b = inp.c_batch()
+        b.read_id0 = int(s)
+        _abi.check(self.L.pr_sw_upload_gpu_seeds(ctx.h, C.byref(b)), "pr_sw_upload_gpu_seeds")
+
+    def launch(self, sw_opts: sw.SwOpts):
+        self._so = sw_opts
+        _abi.check(self.L.pr_sw_launch(self.ctx.h, C.byref(sw_opts)), "pr_sw_launch")
+
+
 def shard_sw(ctx, sw_opts: sw.SwOpts, sr: np.ndarray, sr_off: np.ndarray, s: int, e: int, lr_map: np.ndarray,
              lr_off: np.ndarray) -> None:
-    """Exact-parity layout, step 1 on a rank: bwa-mode SW of the short-read shard [s, e) whose
-    seeds the last DeviceSeedIndex.map(keep_on_device=True) left in HBM (the index of ALL long
-    reads, lr_map / lr_off as mapped); sr 0 of the shard is global id s (bwa's hash ties)."""
-    L = _abi.lib()
-    _setup(L)
-    sr_off = np.asarray(sr_off, np.int64)
-    sh_off = np.ascontiguousarray(sr_off[s:e + 1] - sr_off[s], np.int64)
-    sh_seq = np.ascontiguousarray(sr[sr_off[s]:sr_off[e]], np.uint8)
-    z = np.zeros(0, np.int32)
-    inp = sw.SwInput(sh_off, sh_seq, np.ascontiguousarray(lr_off, np.int64), np.ascontiguousarray(lr_map, np.uint8),
-                     z, z, np.zeros(0, np.uint8), z, z, z)
-    b = inp.c_batch()
-    b.read_id0 = int(s)
-    _abi.check(L.pr_sw_upload_gpu_seeds(ctx.h, C.byref(b)), "pr_sw_upload_gpu_seeds")
-    _abi.check(L.pr_sw_launch(ctx.h, C.byref(sw_opts)), "pr_sw_launch")
+    """ShardSW upload + one launch."""
+    ShardSW(ctx, sr, sr_off, s, e, lr_map, lr_off).launch(sw_opts)
 
 
 def exchange(ctx, comm, s: int, bounds: np.ndarray) -> int:
@@ -273,7 +287,15 @@ class OwnedIteration(Iteration):
         self._ob = ob
         _abi.check(self.L.pr_iter_upload_owned(ctx.h, C.byref(ob)), "pr_iter_upload_owned")
         self.d = SimpleNamespace(lr_off=self._own_off)
+        self._bounds()
+
+    def _bounds(self):
         nl, nt, bd = C.c_int32(), C.c_int64(), _abi.CnsBounds()
-        _abi.check(self.L.pr_iter_bounds(ctx.h, C.byref(nl), C.byref(nt), C.byref(bd)), "pr_iter_bounds")
+        _abi.check(self.L.pr_iter_bounds(self.ctx.h, C.byref(nl), C.byref(nt), C.byref(bd)), "pr_iter_bounds")
         self.n_lr, self.n_task, self.bounds = nl.value, nt.value, bd
         self.out = None
+
+    def launch(self, sw_opts: sw.SwOpts, params: cns.CnsParams):
+        """-b/-l filter, hand-off and consensus over the alignments of the last exchange."""
+        super().launch(sw_opts, params)
+        self._bounds()   # the alignments are counted at launch (the output buffers follow)

@@ -76,7 +76,7 @@ def test_file_level_chain_equals_device_iteration(tmp_path):
     names, seqs, _ = bp.read_fastx(str(sr_fq))
     sr, sr_off = bp._pool(seqs)
     st = correct.GpuStages()
-    tk = st.seed(lr_map, lr_off, sr, sr_off, T.options(task)[0], None)
+    tk = st.seed(lr_map, lr_off, sr, sr_off, T.options(task)[0])
     d = correct._seeds_dataset(lr_map, lr_off, sr, sr_off, tk)
     ref_seq, _ = reads.pool(reads.seqs)
     ref_qual, _ = reads.pool(reads.quals)
