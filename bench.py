@@ -262,10 +262,12 @@ def main():
         from proovread_amd import exact_shard as ex
         bounds = ex.lr_bounds(lr_off_all, world)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
-        shard = iteration.ShardSW(ctx, sr_all, sr_off_all, s0, s0 + d.n_sr, lr_all, lr_off_all)
-        ref_all = np.frombuffer(b"ACGTN", np.uint8)[lr_all]
+        # the SW batch from the seeding's device pools (no second upload); the consensus reference
+        # is the mapped long reads (bwa-sr-1), read from the SW batch on the device
+        shard = iteration.ShardSW(ctx, sr_all, sr_off_all, s0, s0 + d.n_sr, lr_all, lr_off_all, device_pools=True)
         qual_all = np.full(len(lr_all), ord("$"), np.uint8)   # raw CLR reads: phred 3
-        it = iteration.OwnedIteration(ctx, lo, hi, lr_off_all, ref_all, qual_all, sr_all, sr_off_all)
+        it = iteration.OwnedIteration(ctx, lo, hi, lr_off_all, None, qual_all, None if world == 1 else sr_all,
+                                      sr_off_all)
         own_bases = int(lr_off_all[hi] - lr_off_all[lo])
     else:
         it = iteration.Iteration(d, ctx=ctx, gpu_seeds=args.seeds == "gpu")

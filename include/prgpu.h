@@ -435,7 +435,8 @@ int pr_iter_last_timing(pr_ctx *ctx, double *ms_sw_extend, double *ms_sw_global,
  *
  * 1. pr_sw_upload_gpu_seeds: the SW batch of the rank's shard from the device seeds of the last
  *    pr_seed_gpu_map(out = NULL) (b: the shard's short reads -- sr 0 is global id read_id0 --
- *    and all long reads; task fields ignored), then pr_sw_launch (bwa mode).
+ *    and all long reads; task fields ignored; sr_seq / lr_seq NULL: the device copies of the
+ *    last pr_seed_gpu_map / pr_seed_gpu_index_build, no second upload), then pr_sw_launch.
  * 2. pr_aln_exchange: the reported alignments -> 24-byte records + CIGAR ops packed by owner on
  *    the device, the counts exchanged, one RCCL all-to-all of device buffers (comm NULL: world
  *    1, no RCCL); lr_bounds[world+1] are the owners' long-read ranges, sr0 the global id of the
@@ -456,11 +457,12 @@ int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64_t *sr0, co
 typedef struct pr_own_batch {
     int32_t lr0, n_lr;            /* owned long reads: global ids [lr0, lr0 + n_lr)          */
     const int64_t *lr_off;        /* [n_lr+1] their offsets (from 0)                          */
-    const uint8_t *ref_seq;       /* ASCII consensus reference (bam2cns --ref), required      */
+    const uint8_t *ref_seq;       /* ASCII consensus reference (bam2cns --ref), or NULL: the
+                                   * SW batch's long reads (mapping reference = reference)    */
     const uint8_t *lr_qual;       /* phred+33 qualities (lr_off), or NULL                     */
     int32_t n_sr;                 /* every short read of the task, global ids                 */
     const int64_t *sr_off;        /* [n_sr+1]                                                 */
-    const uint8_t *sr_seq;        /* nt4                                                      */
+    const uint8_t *sr_seq;        /* nt4, or NULL when the SW batch holds every short read    */
 } pr_own_batch;
 int pr_iter_upload_owned(pr_ctx *ctx, const pr_own_batch *b);
 

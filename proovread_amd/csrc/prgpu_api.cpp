@@ -25,7 +25,8 @@ int sw_get_ptrs(pr_ctx *c, SwPtrs *p);
 int sw_xchg_send(pr_ctx *c, XchgSend *X);
 pr_ctx *comm_ctx(pr_comm *c);
 int sw_get_pipe_ptrs(pr_ctx *c, SwPtrs *p, bool regroup);
-int sw_upload_device_seeds(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h);
+int sw_upload_device_seeds(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h,
+                           const uint8_t *dev_sr = nullptr, const uint8_t *dev_lr = nullptr);
 
 static thread_local std::string g_err;
 static int set_error(int code, const char *fmt, ...) {
@@ -132,13 +133,16 @@ struct pr_ctx {
     float ms_seed = 0.f, ms_seed_pass2 = 0.f;
     float ms_index = 0.f;
     int64_t seed_n_text = 0, seed_n_hits = 0;
+    int64_t seed_sr_bases = -1;   // bases of the short reads of the last pr_seed_gpu_map (SB_SEQ)
     bool iter_masked = false;
     bool cns_launched = false;   // a consensus launch filled the CB_O_* outputs
     // exact-parity layout: received alignments (pr_aln_exchange) and an owned batch
     DevBuf xb[XB_COUNT];
     bool x_ready = false;        // XB_RREC / XB_RCIG hold the last exchange's records
+    bool x_pass = false;         // world 1: the exchange is the identity, the owned launch reads the SW output
     int64_t x_nrecv = 0, x_nrcig = 0;
     bool own = false;            // the resident iteration batch is an owned batch (pr_iter_upload_owned)
+    bool own_ref_nt4 = false;    // its consensus reference is the SW long-read pool's slice (nt4)
     int32_t own_lr0 = 0;
 };
 
@@ -445,10 +449,16 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         // owned batch: short reads (nt4, global ids) from the task's pool, CIGARs in place in
         // the received wire pool, the ASCII consensus reference of the owned reads
         D.ref_seq = B[CB_REF_SEQ].as<uint8_t>();
-        D.ref_nt4 = 0;
+        D.ref_nt4 = c->own_ref_nt4 ? 1 : 0;
         D.seq = c->xb[XB_SR].as<uint8_t>();
         D.seq_nt4 = 1;
         D.cig = c->xb[XB_RCIG].as<uint32_t>();
+        if (c->x_pass) {   // world 1: CIGARs in place in the SW output pool
+            SwPtrs sp;
+            int rc = sw_get_ptrs(c, &sp);
+            if (rc) return rc;
+            D.cig = sp.cig;
+        }
     } else if (c->pipe) {
         // consensus reads the SW batch in place: long reads and short reads as
         // nt4, CIGARs in place in the SW output pool (per-task starts: pipe hand-off)
@@ -677,7 +687,19 @@ extern "C" int pr_sw_upload_gpu_seeds(pr_ctx *c, const pr_sw_batch *b) {
     sb.n_task = c->seed_pre.back();
     sb.t_sr = sb.t_lr = sb.t_qbeg = sb.t_rbeg = sb.t_slen = sb.t_chain = nullptr;
     sb.t_strand = nullptr;
-    return sw_upload_device_seeds(c, &sb, c->sd[SB_DENSE].as<pr_seed_task>(), c->seed_pre.data());
+    // pools left NULL: the device copies the seeding made (no second host upload)
+    const uint8_t *dsr = nullptr, *dlr = nullptr;
+    if (!b->sr_seq) {
+        if (b->n_sr && c->seed_sr_bases != b->sr_off[b->n_sr])
+            return set_error(PR_ERR_ARG, "sr_seq NULL: the short reads must be those of the last pr_seed_gpu_map");
+        dsr = c->sd[SB_SEQ].as<uint8_t>();
+    }
+    if (!b->lr_seq) {
+        if (!c->seed_n_text || c->seed_view.l_pac != b->lr_off[b->n_lr] || c->seed_view.n_lr != b->n_lr)
+            return set_error(PR_ERR_ARG, "lr_seq NULL: the long reads must be those of the last pr_seed_gpu_index_build");
+        dlr = c->sd[SX_LRSEQ].as<uint8_t>();
+    }
+    return sw_upload_device_seeds(c, &sb, c->sd[SB_DENSE].as<pr_seed_task>(), c->seed_pre.data(), dsr, dlr);
 }
 
 // the sender half of the exchange: the reported alignments of the last bwa-mode pr_sw_launch
@@ -751,8 +773,20 @@ extern "C" int pr_aln_exchange(pr_ctx *c, pr_comm *comm, int64_t sr0, const int6
         if ((rc = pr_comm_rank(comm, &rank, &world))) return rc;
     }
     c->x_ready = false;
+    c->x_pass = false;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipEventRecord(c->ev[0], c->stream));   // pr_iter_last_timing: the hand-off includes the exchange
+    if (world == 1 && sr0 == 0 && !getenv("PRGPU_XCHG_FORCE")) {
+        // one rank holding every short read: it owns every long read, nothing moves -- the owned
+        // launch takes the SW output directly (PRGPU_XCHG_FORCE=1: pack and copy anyway, a test hook)
+        XchgSend X;
+        if ((rc = sw_xchg_send(c, &X))) return rc;
+        c->x_pass = true;
+        c->x_ready = true;
+        c->x_nrecv = X.n;
+        if (n_recv) *n_recv = X.n;
+        return 0;
+    }
     std::vector<int64_t> nrec, nops;
     if ((rc = xchg_pack(c, world, sr0, lr_bounds, nrec, nops))) return rc;
     std::vector<int64_t> sc_rec((size_t)world), sc_cig((size_t)world), rc_rec((size_t)world), rc_cig((size_t)world);
@@ -839,8 +873,8 @@ extern "C" int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64
 extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
     const int n = b->n_lr;
-    if (n < 0 || b->n_sr < 0 || (n && (!b->lr_off || !b->ref_seq)) || !b->sr_off || (b->n_sr && !b->sr_seq))
-        return set_error(PR_ERR_ARG, "owned batch: lr_off, ref_seq and the short reads are required");
+    if (n < 0 || b->n_sr < 0 || (n && !b->lr_off) || !b->sr_off)
+        return set_error(PR_ERR_ARG, "owned batch: lr_off and the short-read offsets are required");
     if (n && b->lr_off[0] != 0) return set_error(PR_ERR_ARG, "lr_off must start at 0");
     for (int i = 0; i < n; ++i)
         if (b->lr_off[i + 1] < b->lr_off[i]) return set_error(PR_ERR_ARG, "lr_off not monotone");
@@ -878,10 +912,32 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     const size_t n1 = (size_t)n + 1;
     if ((rc = upload(B[CB_LR_OFF], c->lr_off_host.data(), n1, s))) return rc;
     if (b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)tl, s))) return rc;
-    if ((rc = upload(B[CB_REF_SEQ], b->ref_seq, (size_t)tl, s))) return rc;
-    if ((rc = upload(c->xb[XB_SR], b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
-        (rc = upload(c->xb[XB_SROFF], b->sr_off, (size_t)b->n_sr + 1, s)))
-        return rc;
+    // ref_seq / sr_seq NULL: the resident SW batch's long reads (the owned slice, nt4: the mapping
+    // reference is the consensus reference) / short reads (every short read of the task) on the device
+    SwPtrs sp{};
+    if ((!b->ref_seq || !b->sr_seq) && (rc = sw_get_ptrs(c, &sp))) return rc;
+    c->own_ref_nt4 = !b->ref_seq;
+    if (b->ref_seq) {
+        if ((rc = upload(B[CB_REF_SEQ], b->ref_seq, (size_t)tl, s))) return rc;
+    } else {
+        if (b->lr0 < 0 || b->lr0 + n > sp.n_lr) return set_error(PR_ERR_ARG, "owned long reads outside the SW batch");
+        int64_t base = 0, end = 0;
+        HIPCHK(hipMemcpyAsync(&base, sp.lr_off + b->lr0, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(&end, sp.lr_off + b->lr0 + n, 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (end - base != tl) return set_error(PR_ERR_ARG, "owned long reads differ from the SW batch's");
+        if ((rc = B[CB_REF_SEQ].ensure((size_t)tl + 1))) return rc;
+        if (tl) HIPCHK(hipMemcpyAsync(B[CB_REF_SEQ].p, sp.lr + base, (size_t)tl, hipMemcpyDeviceToDevice, s));
+    }
+    if ((rc = upload(c->xb[XB_SROFF], b->sr_off, (size_t)b->n_sr + 1, s))) return rc;
+    if (b->sr_seq) {
+        if ((rc = upload(c->xb[XB_SR], b->sr_seq, (size_t)b->sr_off[b->n_sr], s))) return rc;
+    } else {
+        if (sp.n_sr != b->n_sr) return set_error(PR_ERR_ARG, "sr_seq NULL: the SW batch must hold every short read");
+        if ((rc = c->xb[XB_SR].ensure((size_t)b->sr_off[b->n_sr] + 1))) return rc;
+        if (b->sr_off[b->n_sr])
+            HIPCHK(hipMemcpyAsync(c->xb[XB_SR].p, sp.sr, (size_t)b->sr_off[b->n_sr], hipMemcpyDeviceToDevice, s));
+    }
     if ((rc = c->pb[1].ensure(n1 * 4)) || (rc = c->pb[2].ensure(n1 * 4))) return rc;
     if ((rc = B[CB_ALN_OFF].ensure(n1 * 8)) || (rc = B[CB_WORK].ensure(64)) || (rc = B[CB_PROF].ensure(CNS_NPHASE * 8)) ||
         (rc = B[CB_RETRY].ensure(((size_t)n + 16) * 4)))
@@ -913,6 +969,24 @@ static int own_group(pr_ctx *c, SwPtrs *sp) {
     if (!c->x_ready) return set_error(PR_ERR_ARG, "no received alignments (pr_aln_exchange first)");
     hipStream_t s = c->stream;
     DevBuf *B = c->xb;
+    if (c->x_pass) {   // world 1: the SW output regrouped by long read, as pr_iter_launch does
+        int rc = sw_get_pipe_ptrs(c, sp, true);
+        if (rc) return rc;
+        c->n_aln = sp->n_task;
+        const size_t na1 = (size_t)sp->n_task + 1;
+        DevBuf *C = c->cb;
+        if ((rc = C[CB_POS].ensure(na1 * 4)) || (rc = C[CB_SCORE].ensure(na1 * 8)) || (rc = C[CB_AFLAGS].ensure(na1)) ||
+            (rc = C[CB_SEQ_OFF].ensure(na1 * 8)) || (rc = C[CB_LSEQ].ensure(na1 * 4)) ||
+            (rc = C[CB_CIG_OFF].ensure(na1 * 8)) || (rc = C[CB_NCIG].ensure(na1 * 4)) ||
+            (rc = C[CB_A_ST].ensure(na1 * 4)) || (rc = C[CB_A_LEN].ensure(na1 * 4)) ||
+            (rc = C[CB_A_NC].ensure(na1 * 8)) || (rc = C[CB_A_BIN].ensure(na1 * 4)) ||
+            (rc = C[CB_A_CB].ensure(na1 * 4)) || (rc = C[CB_A_CE].ensure(na1 * 4)) ||
+            (rc = C[CB_A_SB].ensure(na1 * 4)) || (rc = C[CB_A_RPOS].ensure(na1 * 4)) ||
+            (rc = C[CB_A_END].ensure(na1 * 4)) || (rc = C[CB_SORTED].ensure(na1 * 4)) ||
+            (rc = C[CB_LST_SCORE].ensure(na1 * 8)) || (rc = C[CB_LST_ALN].ensure(na1 * 4)) || (rc = C[CB_KEPT].ensure(na1)))
+            return rc;
+        return 0;
+    }
     {   // per-alignment arrays of the hand-off and the consensus, sized by what arrived
         c->n_aln = c->x_nrecv;
         const size_t na1 = (size_t)c->x_nrecv + 1;
@@ -1600,6 +1674,7 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     const int64_t scratch = std::max<int64_t>(waves * 64 * K.stride, lanes2 * seedc::scratch_bytes(caps));
     const int64_t nb = n_sr ? sr_off[n_sr] : 0;
     int rc;
+    c->seed_sr_bases = nb;
     if ((rc = upload(D[SB_SEQ], sr_seq, (size_t)nb, s)) || (rc = upload(D[SB_OFF], sr_off, (size_t)n_sr + 1, s)) ||
         (rc = D[SB_SCRATCH].ensure((size_t)scratch)) ||
         (rc = D[SB_OUT].ensure((size_t)n_sr * caps.out * sizeof(pr_seed_task) + 16)) ||

@@ -117,7 +117,10 @@ extern "C" void pr_sw_opts_default(pr_sw_opts *o, int finish) {
 
 // dev_tasks: bwa mode with the seeds already in HBM (the dense list of pr_seed_gpu_map, n_task
 // of them, grouped by read; seed_off_h its per-read prefix on the host); b's task fields unused
-static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h) {
+// dev_sr / dev_lr (may be null): device copies of b's read pools (e.g. the seeding's), copied on
+// the device instead of uploading b->sr_seq / b->lr_seq
+static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h,
+                          const uint8_t *dev_sr = nullptr, const uint8_t *dev_lr = nullptr) {
     if (!c || !b) return pr_set_error(PR_ERR_ARG, "null arg");
     if (b->n_sr < 0 || b->n_lr < 0 || b->n_task < 0) return pr_set_error(PR_ERR_ARG, "negative sizes");
     HIPCHK(hipSetDevice(ctx_device(c)));
@@ -161,11 +164,15 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
             r.n_rank0 += (t == 0 || b->t_sr[t] != b->t_sr[t - 1] || b->t_chain[t] != b->t_chain[t - 1]) ? 1 : 0;
     }
     int rc;
-    if ((rc = up(r, SB_SR, b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
+    if ((rc = up(r, SB_SR, dev_sr ? nullptr : b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
         (rc = up(r, SB_SR_OFF, b->sr_off, (size_t)b->n_sr + 1, s)) ||
-        (rc = up(r, SB_LR, b->lr_seq, (size_t)b->lr_off[b->n_lr], s)) ||
+        (rc = up(r, SB_LR, dev_lr ? nullptr : b->lr_seq, (size_t)b->lr_off[b->n_lr], s)) ||
         (rc = up(r, SB_LR_OFF, b->lr_off, (size_t)b->n_lr + 1, s)))
         return rc;
+    if (dev_sr && b->sr_off[b->n_sr])
+        HIPCHK(hipMemcpyAsync(r.buf[SB_SR], dev_sr, (size_t)b->sr_off[b->n_sr], hipMemcpyDeviceToDevice, s));
+    if (dev_lr && b->lr_off[b->n_lr])
+        HIPCHK(hipMemcpyAsync(r.buf[SB_LR], dev_lr, (size_t)b->lr_off[b->n_lr], hipMemcpyDeviceToDevice, s));
     if (dev_tasks) {   // unpack the device seed list into the task columns, count the first seeds
         if ((rc = ensure(r, SB_T_SR, (size_t)nt * 4)) || (rc = ensure(r, SB_T_LR, (size_t)nt * 4)) ||
             (rc = ensure(r, SB_T_STRAND, (size_t)nt)) || (rc = ensure(r, SB_T_QBEG, (size_t)nt * 4)) ||
@@ -257,8 +264,9 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
 extern "C" int pr_sw_upload(pr_ctx *c, const pr_sw_batch *b) { return sw_upload_impl(c, b, nullptr, nullptr); }
 
 // the iteration's SW upload with the device-resident seeds of pr_seed_gpu_map (prgpu_api.cpp)
-int sw_upload_device_seeds(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h) {
-    return sw_upload_impl(c, b, dev_tasks, seed_off_h);
+int sw_upload_device_seeds(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *dev_tasks, const int64_t *seed_off_h,
+                           const uint8_t *dev_sr, const uint8_t *dev_lr) {
+    return sw_upload_impl(c, b, dev_tasks, seed_off_h, dev_sr, dev_lr);
 }
 
 static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {

@@ -195,15 +195,17 @@ class ShardSW:
     of the shard is global id s: bwa's hash ties)."""
 
     def __init__(self, ctx, sr: np.ndarray, sr_off: np.ndarray, s: int, e: int, lr_map: np.ndarray,
-                 lr_off: np.ndarray):
+                 lr_off: np.ndarray, device_pools: bool = False):
+        """device_pools: the read pools are the device copies the seeding made (the index's long
+        reads, the seeded shard) -- no second host upload."""
         self.L = _abi.lib()
         _setup(self.L)
         self.ctx = ctx
         sr_off = np.asarray(sr_off, np.int64)
         self._sh_off = np.ascontiguousarray(sr_off[s:e + 1] - sr_off[s], np.int64)
-        self._sh_seq = np.ascontiguousarray(sr[sr_off[s]:sr_off[e]], np.uint8)
+        self._sh_seq = None if device_pools else np.ascontiguousarray(sr[sr_off[s]:sr_off[e]], np.uint8)
         self._lr_off = np.ascontiguousarray(lr_off, np.int64)
-        self._lr_map = np.ascontiguousarray(lr_map, np.uint8)
+        self._lr_map = None if device_pools else np.ascontiguousarray(lr_map, np.uint8)
         z = np.zeros(0, np.int32)
         inp = sw.SwInput(self._sh_off, self._sh_seq, self._lr_off, self._lr_map, z, z, np.zeros(0, np.uint8), z, z, z)
         b = inp.c_batch()
@@ -260,20 +262,22 @@ class OwnedIteration(Iteration):
                  ref_qual: Optional[np.ndarray], sr: np.ndarray, sr_off: np.ndarray):
         """lr_off: every long read's offsets; ref_seq / ref_qual: the consensus reference
         (ASCII, bam2cns --ref) and qualities of all long reads in lr_off's layout (the owned
-        slice is uploaded); sr / sr_off: every short read of the task (nt4), which the
-        consensus reads by global id."""
+        slice is uploaded; ref_seq None: the SW batch's long reads, when the mapping reference
+        is the consensus reference); sr / sr_off: every short read of the task (nt4), which
+        the consensus reads by global id (sr None: the SW batch holds every short read)."""
         self.L = _abi.lib()
         _setup(self.L)
         self.ctx = ctx
         self.lo, self.hi = lo, hi
         lr_off = np.asarray(lr_off, np.int64)
         a0, a1 = int(lr_off[lo]), int(lr_off[hi])
-        if len(ref_seq) != int(lr_off[-1]) or (ref_qual is not None and len(ref_qual) != int(lr_off[-1])):
+        if (ref_seq is not None and len(ref_seq) != int(lr_off[-1])) or \
+                (ref_qual is not None and len(ref_qual) != int(lr_off[-1])):
             raise ValueError("ref_seq / ref_qual must have every long read's layout (lr_off)")
         self._own_off = np.ascontiguousarray(lr_off[lo:hi + 1] - a0, np.int64)
-        self._ref = np.ascontiguousarray(ref_seq[a0:a1], np.uint8)
+        self._ref = None if ref_seq is None else np.ascontiguousarray(ref_seq[a0:a1], np.uint8)
         self._qual = None if ref_qual is None else np.ascontiguousarray(ref_qual[a0:a1], np.uint8)
-        self._sr = np.ascontiguousarray(sr, np.uint8)
+        self._sr = None if sr is None else np.ascontiguousarray(sr, np.uint8)
         self._sr_off = np.ascontiguousarray(sr_off, np.int64)
         ob = OwnBatch()
         ob.lr0, ob.n_lr = lo, hi - lo

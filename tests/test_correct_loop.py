@@ -162,7 +162,8 @@ def test_gpu_exact_layout_loop_matches_oracle_loop(transport, monkeypatch, tmp_p
     cfg = correct.LoopConfig(coverage=40.0, seed_threads=4)
     want = correct.run(lrs, srd, cfg, stages=loop_oracle.OracleStages(8))
     cm = None
-    if transport == "rccl":
+    if transport == "rccl":   # the full exchange through RCCL (world 1 would pass the SW output through)
+        monkeypatch.setenv("PRGPU_XCHG_FORCE", "1")
         monkeypatch.setenv("PRGPU_RDZV_DIR", str(tmp_path))
         cm = comm.RcclComm(_abi.default_context(), 0, 1, key="loopx")
     try:

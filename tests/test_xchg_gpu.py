@@ -64,19 +64,19 @@ def _single(ctx, d, ref, qual, finish, mask_params):
     return _outputs(it, mask_params)
 
 
-def _shard(ctx, d, finish, s, e):
+def _shard(ctx, d, finish, s, e, device_pools=False):
     from proovread_amd import iteration, seed
     seed_opts, so, _ = _opts(finish)
     ix = seed.DeviceSeedIndex(ctx, d.lr_seq, d.lr_off)
     a, b = int(d.sr_off[s]), int(d.sr_off[e])
     ix.map(d.sr_seq[a:b], d.sr_off[s:e + 1] - a, seed_opts, keep_on_device=True)
-    iteration.shard_sw(ctx, so, d.sr_seq, d.sr_off, s, e, d.lr_seq, d.lr_off)
+    iteration.ShardSW(ctx, d.sr_seq, d.sr_off, s, e, d.lr_seq, d.lr_off, device_pools=device_pools).launch(so)
 
 
-def _owned(ctx, d, ref, qual, finish, lo, hi, mask_params):
+def _owned(ctx, d, ref, qual, finish, lo, hi, mask_params, sr=True):
     from proovread_amd import iteration
     _, so, cp = _opts(finish)
-    it = iteration.OwnedIteration(ctx, lo, hi, d.lr_off, ref, qual, d.sr_seq, d.sr_off)
+    it = iteration.OwnedIteration(ctx, lo, hi, d.lr_off, ref, qual, d.sr_seq if sr else None, d.sr_off)
     it.launch(so, cp)
     return _outputs(it, mask_params)
 
@@ -89,12 +89,15 @@ def _mask_params():
 @pytest.mark.parametrize("finish", [False, True])
 @pytest.mark.parametrize("transport", ["none", "rccl"])
 def test_world1_exchange_equals_single_iteration(finish, transport, monkeypatch, tmp_path):
+    """The whole exchange (pack, counts, RCCL self send/recv -- or a device copy --, regroup) at
+    world 1, forced (without PRGPU_XCHG_FORCE world 1 passes the SW output straight through)."""
     from proovread_amd import _abi, comm, iteration
     ctx = _abi.default_context()
     d, ref, qual = _data(finish)
     mp = _mask_params()
     want = _single(ctx, d, ref, qual, finish, mp)
     assert sum(1 for x in want[0] if x[0] == 0) == d.n_lr
+    monkeypatch.setenv("PRGPU_XCHG_FORCE", "1")   # world 1 would skip the identity exchange
     cm = None
     if transport == "rccl":
         monkeypatch.setenv("PRGPU_RDZV_DIR", str(tmp_path))
@@ -117,7 +120,9 @@ def test_world1_exchange_equals_single_iteration(finish, transport, monkeypatch,
 @pytest.mark.parametrize("finish", [False, True])
 def test_local_exchange_equals_single_iteration(world, finish):
     """`world` shards as contexts of this process on one GPU: the owners' results concatenated
-    in rank order equal the single iteration's; the {bpt, bpN} sums too."""
+    in rank order equal the single iteration's; the {bpt, bpN} sums too.  Even worlds take the
+    SW pools and the consensus reference from the device (the seeding's copies, the SW's long
+    reads); the single run uses the ASCII reference of the same bases."""
     from proovread_amd import _abi, exact_shard as ex, iteration
     d, ref, qual = _data(finish)
     mp = _mask_params()
@@ -129,13 +134,14 @@ def test_local_exchange_equals_single_iteration(world, finish):
         starts = []
         for r in range(world):
             s, e = ex.sr_range(d.n_sr, world, r)
-            _shard(ctxs[r], d, finish, s, e)
+            _shard(ctxs[r], d, finish, s, e, device_pools=world % 2 == 0)
             starts.append(s)
         nrecv = iteration.exchange_local(ctxs, starts, bounds)
         assert sum(nrecv) > 10 * d.n_lr
         res, masked, st = [], [], [0, 0]
         for r in range(world):
-            g = _owned(ctxs[r], d, ref, qual, finish, int(bounds[r]), int(bounds[r + 1]), mp)
+            g = _owned(ctxs[r], d, None if world % 2 == 0 else ref, qual, finish, int(bounds[r]), int(bounds[r + 1]),
+                       mp)
             res += g[0]
             masked += g[1]
             st = [st[0] + g[2][0], st[1] + g[2][1]]
@@ -146,3 +152,17 @@ def test_local_exchange_equals_single_iteration(world, finish):
     assert res == want[0]
     assert masked == want[1]
     assert st == want[2]
+
+
+@pytest.mark.parametrize("finish", [False, True])
+def test_world1_passthrough_equals_single_iteration(finish):
+    """World 1 without the test hook: the owned launch takes the SW output directly."""
+    from proovread_amd import _abi, iteration
+    ctx = _abi.default_context()
+    d, ref, qual = _data(finish)
+    mp = _mask_params()
+    want = _single(ctx, d, ref, qual, finish, mp)
+    _shard(ctx, d, finish, 0, d.n_sr, device_pools=True)
+    iteration.exchange(ctx, None, 0, np.array([0, d.n_lr], np.int64))
+    got = _owned(ctx, d, None, qual, finish, 0, d.n_lr, mp, sr=False)   # every pool from the device
+    assert got == want
