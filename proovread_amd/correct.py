@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import dataclasses
 import functools
+import time
 from types import SimpleNamespace
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -100,6 +101,8 @@ class TaskLog:
     bpn: int = 0
     masked_frac: Optional[float] = None
     shortcut: str = ""
+    wall_ms: Optional[float] = None        # the task's wall time in run()
+    device_ms: Optional[float] = None      # kernel time the device stages report (HIP events), if any
 
 
 @dataclasses.dataclass
@@ -172,6 +175,7 @@ class GpuStages:
     def __init__(self, ctx=None):
         from . import _abi
         self.ctx = ctx or _abi.default_context()
+        self.device_ms = 0.0   # kernel time of the calls so far (index, seeding, SW .. consensus)
 
     def iteration(self, d, ref_seq: np.ndarray, ref_qual: np.ndarray, task: str, params,
                   bin_filter: Optional[Tuple[int, float]] = None) -> List[tuple]:
@@ -185,7 +189,9 @@ class GpuStages:
         if bin_filter:
             opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
         it.launch(opts, params)
-        return [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
+        out = [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
+        self.device_ms += sum(it.timing())
+        return out
 
     def owned_iteration(self, lr_map, lr_off, sr, sr_off, task: str, params, ref_seq: np.ndarray,
                         ref_qual: np.ndarray, bin_filter, comm, mask_cfg=None):
@@ -206,6 +212,7 @@ class GpuStages:
         a0, a1 = int(sr_off[s]), int(sr_off[e])
         ix.map(sr[a0:a1], np.asarray(sr_off[s:e + 1]) - a0, T.options(task)[0], keep_on_device=True)
         n_seeds = ix.seed_count()
+        self.device_ms += ix.build_ms() + ix.gpu_ms()
         opts = T.options(task)[1]
         if bin_filter:
             opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
@@ -214,6 +221,7 @@ class GpuStages:
         it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, ref_seq, ref_qual, sr, sr_off)
         it.launch(opts, params)
         out = [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
+        self.device_ms += sum(it.timing())
         mres = None
         if mask_cfg is not None:
             buf = _abi.DevBuffer(self.ctx, 16)
@@ -230,7 +238,13 @@ class GpuStages:
         and pr_seed_gpu_map (the host path's task lists exactly, tests/test_seed_gpu.py)."""
         from . import seed
         ix = seed.DeviceSeedIndex(self.ctx, lr_map, lr_off)
+        if getattr(self, "debug_dir", None):   # diagnostics: the task's inputs, then the map
+            import os
+            np.savez(os.path.join(self.debug_dir, f"seed{getattr(self, '_dbg_n', 0)}.npz"), lr=lr_map, lr_off=lr_off,
+                     sr=sr, sr_off=sr_off)
+            self._dbg_n = getattr(self, "_dbg_n", 0) + 1
         tk, _ = ix.map(sr, sr_off, seed_opts)
+        self.device_ms += ix.build_ms() + ix.gpu_ms()
         return tk
 
     def mask(self, seqs: List[bytes], quals: List[bytes], hcr_mask: str, min_sr_length: int):
@@ -319,6 +333,8 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
             raise ValueError(f"task {task} is outside the sr / mr loops")
         finish = task.endswith("-finish")
         ent = TaskLog(task)
+        t_task = time.perf_counter()
+        dev0 = getattr(stages, "device_ms", None)
         task_cov = sr_coverage_for(task)
         sr, sr_off = srs.sample(sampler.cov2seqchunker(cfg.coverage, task_cov))
         ent.n_sr = len(sr_off) - 1
@@ -377,6 +393,9 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
             ent.masked_frac = control.masked_fraction(bpt, bpn) if bpt else 0.0
             ent.shortcut = control.mask_shortcut(tasks, tc, ent.masked_frac, fracs, cfg.mask_shortcut_frac,
                                                  cfg.mask_min_gain_frac)
+        ent.wall_ms = round((time.perf_counter() - t_task) * 1e3, 1)
+        if dev0 is not None:
+            ent.device_ms = round(stages.device_ms - dev0, 1)
         log.append(ent)
         tc += 1
     return LoopResult(reads, chim, ignored, log, last_masked)

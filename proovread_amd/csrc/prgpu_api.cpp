@@ -1731,10 +1731,12 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
                     t8[4] / 1e5, t8[5] / 1e5, t8[6] / 1e5);
     }
     int64_t total = 0, bad = 0;
+    int32_t bad_flags = 0;
     for (int i = 0; i < n_sr; ++i) {
         if (nout[i] < 0 || nout[i] > caps.out) return set_error(PR_ERR_HIP, "seed kernel: bad task count");
         total += nout[i];
         bad += st[i] != 0;
+        bad_flags |= st[i];
     }
     // compact on the device (read order), download the dense list
     std::vector<int64_t> pre((size_t)n_sr + 1, 0);
@@ -1752,7 +1754,9 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     if (keep_on_device) {   // the seeds stay in HBM for pr_iter_upload_gpu_seeds
         HIPCHK(hipStreamSynchronize(s));
         if (status) std::memcpy(status, st.data(), (size_t)n_sr * 4);
-        if (bad) return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags)", (long long)bad);
+        if (bad)
+            return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags, or: 0x%x)",
+                             (long long)bad, bad_flags);
         return 0;
     }
     out->t = (pr_seed_task *)std::malloc(sizeof(pr_seed_task) * (size_t)(total > 0 ? total : 1));
@@ -1761,7 +1765,9 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     HIPCHK(hipStreamSynchronize(s));
     out->n = total;
     if (status) std::memcpy(status, st.data(), (size_t)n_sr * 4);
-    if (bad) return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags)", (long long)bad);
+    if (bad)
+        return set_error(PR_ERR_CAPACITY, "%lld reads outgrew the seeding scratch (status flags, or: 0x%x)", (long long)bad,
+                         bad_flags);
     return 0;
 }
 

@@ -843,10 +843,11 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             t.rbeg = (int32_t)(s.rbeg - cs);
             t.slen = s.len;
             t.chain = nkept;
-            t.rank = score * 65536 + idx++;   // the srt key until the sort below (score < 2^15)
+            t.rmax0 = score;   // the srt key (score, index) until the sort below: rmax0 / rank
+            t.rank = idx++;
             // insertion sort by (score, index) descending
             int j = no - 1;
-            while (j >= first && out[j].rank < t.rank) --j;
+            while (j >= first && (out[j].rmax0 < t.rmax0 || (out[j].rmax0 == t.rmax0 && out[j].rank < t.rank))) --j;
             const pr_seed_task v = t;
             for (int m = no; m > j + 1; --m) out[m] = out[m - 1];
             out[j + 1] = v;

@@ -338,7 +338,8 @@ static int side_stream(SwResident &r) {
 // The packed CIGAR pass's task order (sorted by key, padded to 128-task segments), then its
 // launch geometry.  Default: the fused kernel (DP and backtrack per segment in one wave, a
 // slab per resident wave).  PRGPU_PK_SPLIT=1: the segment count read back, split into chunks
-// whose slabs (one per segment, PK_TMAX rows) fit PRGPU_PK_SLAB_GB (default 32 GB), each chunk
+// whose slabs (one per segment, PK_TMAX rows) fit PRGPU_PK_SLAB_GB (default 4 GB, at most half
+// of the free device memory), each chunk
 // a DP launch and a backtrack launch (measured at configs[1]: DP 43.4 + backtrack 15.4 ms
 // against 58.8 ms fused -- the walk is latency- and issue-bound).
 static int pk_prepare(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O) {
@@ -359,7 +360,9 @@ static int pk_prepare(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O) {
     const int64_t nseg = len / PK_SEG;
     const size_t slab = (size_t)D.z_pk_slab * sizeof(PkDir);
     const char *gb = getenv("PRGPU_PK_SLAB_GB");
-    const double budget = (gb ? atof(gb) : 32.0) * (double)(1ull << 30);
+    double budget = (gb ? atof(gb) : 4.0) * (double)(1ull << 30);
+    size_t free_b = 0, total_b = 0;   // never more than half of what is free
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && budget > 0.5 * (double)free_b) budget = 0.5 * (double)free_b;
     int64_t per = (int64_t)(budget / (double)slab);
     per = per < 64 ? 64 : per;
     const int64_t nch = nseg > 0 ? (nseg + per - 1) / per : 1;
@@ -633,6 +636,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
             ev = (void *)x;
         }
     r.ext_ev.n = 0;
+    r.ext_ev.dropped = 0;
     if (r.bwa) return bwa_launch(c, r, D, O, o, grid_w, grid_pk, grid_g, lds_glob);
     if (r.n_task == 0) return 0;
     HIPCHK(hipMemcpyAsync(r.buf[SB_CIGAT], r.buf[SB_CIGSLOT], (size_t)r.n_task * 8, hipMemcpyDeviceToDevice, s));
@@ -911,7 +915,7 @@ extern "C" int pr_sw_extension_kernels(pr_ctx *c, double *ms, int64_t *cells, in
     if (ms) *ms = tot;
     if (cells) *cells = (int64_t)r.cells[0];
     if (launches) *launches = r.ext_ev.n / 2;
-    if (r.ext_ev.n >= SwEvPool::CAP) return pr_set_error(PR_ERR_CAPACITY, "more extension launches than timed events");
+    if (r.ext_ev.dropped) return pr_set_error(PR_ERR_CAPACITY, "more extension launches than timed events");
     return 0;
 }
 

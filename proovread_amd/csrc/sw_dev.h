@@ -94,6 +94,7 @@ struct SwEvPool {
     static const int CAP = 128;
     void *ev[CAP] = {};
     int n = 0;
+    int dropped = 0;   // marks the full pool could not take (launches left untimed)
 };
 
 struct SwResident {

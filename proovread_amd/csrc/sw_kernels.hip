@@ -1254,6 +1254,7 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
     hipStream_t s = (hipStream_t)stream;
     auto mark = [&]() {   // an event before / after each DP launch (when the pool has room)
         if (evp && evp->n < SwEvPool::CAP && evp->ev[evp->n]) (void)hipEventRecord((hipEvent_t)evp->ev[evp->n++], s);
+        else if (evp) ++evp->dropped;   // pool full: this launch goes untimed (reported by the caller)
     };
     int fgrid = (int)((sel_count(D) + 255) / 256);
     fgrid = fgrid < 8192 ? (fgrid > 0 ? fgrid : 1) : 8192;
