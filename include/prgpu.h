@@ -98,6 +98,9 @@ int pr_comm_alltoallv_host(pr_comm *c, const uint8_t *send, const int64_t *send_
 /* the same on DEVICE buffers, asynchronous on the context stream (no host copy) */
 int pr_comm_alltoallv_dev(pr_comm *c, const void *send, const int64_t *send_counts, void *recv,
                           const int64_t *recv_counts);
+/* all-gather of DEVICE byte blocks: counts[world] (the same on every rank) = each rank's bytes;
+ * rank r's block lands at recv + sum(counts[0..r)); asynchronous on the context stream */
+int pr_comm_allgatherv_dev(pr_comm *c, const void *send, const int64_t *counts, void *recv);
 
 /* ------------------------------------------------------------------ */
 /* consensus stage                                                     */
@@ -363,7 +366,8 @@ int pr_seed_gpu_index_koff(pr_ctx *ctx, uint64_t *koff, uint64_t *ksplit);
 int pr_seed_smem(const pr_seed_index *h, const uint8_t *q, int len, int x, int64_t min_intv, int32_t *start,
                  int32_t *end, int64_t *occ, int cap, int *n_out);
 /* The GPU seeding path (seed_kernels.hip: the same per-read core; pass 1 64 reads per wave,
- * pass 2 one wave per read for the reads that outgrew pass 1's scratch).  pr_seed_gpu_upload
+ * pass 2 one wave per read for the reads that outgrew pass 1's scratch, up to 4 more passes with
+ * the overflowed arrays grown -- hits x4, the others x2 -- for the reads that outgrew pass 2's).  pr_seed_gpu_upload
  * copies a built index into the context's HBM; pr_seed_gpu_map seeds n_sr reads (nt4 codes)
  * into library-owned tasks in read order (out = NULL: the tasks stay in HBM for
  * pr_iter_upload_gpu_seeds); status[i] (may be NULL) is 0 or the overflow flags of a read
@@ -393,7 +397,7 @@ int pr_seed_gpu_last_ms(pr_ctx *ctx, double *ms);
 int pr_seed_gpu_phase_ticks(pr_ctx *ctx, uint64_t *ticks4);
 /* wall time of the last pr_seed_gpu_map's second pass (the reads that outgrew pass 1's slices), ms */
 int pr_seed_gpu_pass2_ms(pr_ctx *ctx, double *ms);
-/* diagnostics (tests): the device path's core and capacities run on the host */
+/* diagnostics (tests): the device path's core and capacities (its passes included) run on the host */
 int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opts *o, const uint8_t *sr_seq,
                             const int64_t *sr_off, int n_sr, int n_threads, pr_seed_tasks *out, int32_t *status);
 
@@ -463,8 +467,33 @@ typedef struct pr_own_batch {
     int32_t n_sr;                 /* every short read of the task, global ids                 */
     const int64_t *sr_off;        /* [n_sr+1]                                                 */
     const uint8_t *sr_seq;        /* nt4, or NULL when the SW batch holds every short read    */
+    int32_t from_set;             /* 1: reference and qualities from the resident long-read set
+                                   * (pr_lrset_*; ref_seq / lr_qual ignored)                   */
 } pr_own_batch;
 int pr_iter_upload_owned(pr_ctx *ctx, const pr_own_batch *b);
+
+/* The resident long-read set: the correction loop's state between tasks -- the current reads
+ * (proovread's LR.fq: sequence and qualities) and their mapping reference (LR.masked.fa,
+ * bin/proovread:835-869, 1700-1720) -- kept in HBM, so a task moves only its short reads
+ * across PCIe.  pr_lrset_load: the read-long output (ASCII bases, phred+33 qualities); the
+ * mapping reference starts as the reads.  pr_lrset_index: the seed index over the mapping
+ * reference (PR_LRSET_MAP) or the reads (PR_LRSET_READS: the finish task, proovread:838-850),
+ * replacing pr_seed_gpu_index_build; its long-read pool then feeds the SW batch on the device.
+ * pr_iter_upload_lrset: a world-1 iteration from the seeds of the last pr_seed_gpu_map (b: the
+ * short reads -- sr_seq NULL: the seeding's copy -- and read_id0; its long-read fields are
+ * ignored) with the set's reads and qualities as the consensus reference (bam2cns --ref).
+ * pr_lrset_commit: after pr_iter_launch (+ pr_iter_mask with with_mask): every read's
+ * consensus (and quality; with_mask its masked copy as the next mapping reference) replaces
+ * the set's -- a read whose consensus failed makes the call fail with its status; an owned
+ * batch (pr_iter_upload_owned) needs comm: the ranks' reads are all-gathered on the device.
+ * pr_lrset_download: offsets [n+1] and pools (any may be NULL; map = the mapping reference). */
+enum { PR_LRSET_MAP = 0, PR_LRSET_READS = 1 };
+int pr_lrset_load(pr_ctx *ctx, int32_t n_lr, const int64_t *off, const uint8_t *seq, const uint8_t *qual);
+int pr_lrset_info(pr_ctx *ctx, int32_t *n_lr, int64_t *bases);
+int pr_lrset_index(pr_ctx *ctx, int which);
+int pr_iter_upload_lrset(pr_ctx *ctx, const pr_sw_batch *b);
+int pr_lrset_commit(pr_ctx *ctx, pr_comm *comm, int with_mask);
+int pr_lrset_download(pr_ctx *ctx, int64_t *off, uint8_t *seq, uint8_t *qual, uint8_t *map);
 
 /* enqueue (ctx stream) the per-iteration statistic of the resident consensus:
  * dev_out[0] = corrected bases, dev_out[1] = bases with phred >= min_phred.

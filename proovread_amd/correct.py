@@ -32,6 +32,7 @@ from __future__ import annotations
 
 import dataclasses
 import functools
+import math
 import time
 from types import SimpleNamespace
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -73,23 +74,51 @@ class LoopConfig:
     seed_threads: int = 0
     bin_filter: bool = True                # bwa-proovread -b/-l in every iteration (proovread:1302-1313)
     exact_layout: bool = False             # world 1: run the multi-GPU exact-parity layout anyway (tests)
+    keep_masked: bool = False              # LoopResult.masked: the last regular task's masked reads
 
 
-@dataclasses.dataclass
 class LongReads:
-    """The current long-read set: the .fq of the last task (ids, sequences, qualities)."""
-    ids: List[str]
-    seqs: List[bytes]
-    quals: List[bytes]
+    """The current long-read set: the .fq of the last task (ids, sequences, qualities), held as
+    byte pools with offsets (ASCII bases, phred+33 qualities); `seqs` / `quals` are per-read
+    views built on first use."""
+
+    def __init__(self, ids: List[str], seqs: Optional[List[bytes]] = None, quals: Optional[List[bytes]] = None,
+                 pools: Optional[Tuple[np.ndarray, np.ndarray, np.ndarray]] = None):
+        self.ids = ids
+        if pools is None:
+            pools = (*_pool(seqs), _pool(quals)[0])
+        self.seq_pool, self.off, self.qual_pool = pools
+        self._seqs, self._quals = seqs, quals
+
+    @property
+    def seqs(self) -> List[bytes]:
+        if self._seqs is None:
+            self._seqs = _split(self.seq_pool, self.off)
+        return self._seqs
+
+    @property
+    def quals(self) -> List[bytes]:
+        if self._quals is None:
+            self._quals = _split(self.qual_pool, self.off)
+        return self._quals
 
     def pool(self, which: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
-        off = np.zeros(len(which) + 1, np.int64)
-        np.cumsum([len(s) for s in which], out=off[1:])
-        buf = np.frombuffer(b"".join(which), np.uint8).copy() if which else np.zeros(0, np.uint8)
-        return buf, off
+        return _pool(which)
 
     def fastq(self) -> str:
         return "".join(f"@{i}\n{s.decode()}\n+\n{q.decode()}\n" for i, s, q in zip(self.ids, self.seqs, self.quals))
+
+
+def _pool(items: Sequence[bytes]) -> Tuple[np.ndarray, np.ndarray]:
+    off = np.zeros(len(items) + 1, np.int64)
+    np.cumsum([len(s) for s in items], out=off[1:])
+    buf = np.frombuffer(b"".join(items), np.uint8).copy() if items else np.zeros(0, np.uint8)
+    return buf, off
+
+
+def _split(pool: np.ndarray, off: np.ndarray) -> List[bytes]:
+    b = pool.tobytes()
+    return [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
 
 
 @dataclasses.dataclass
@@ -111,10 +140,13 @@ class LoopResult:
     chim: List[str]                        # .chim.tsv lines of the finish task (id from to score)
     ignored: List[str]                     # .ignored.tsv lines (stubby reads)
     log: List[TaskLog]
-    masked: Optional[List[bytes]] = None   # the last regular iteration's masked reads
+    masked: Optional[List[bytes]] = None   # the last regular iteration's masked reads (keep_masked)
 
 
 # ---------------------------------------------------------------------------- read-long
+_LR_TABLE = bytes(c if chr(c) in "ACGTN" else (c - 32 if chr(c) in "acgtn" else ord("N")) for c in range(256))
+
+
 def read_long(records: Sequence[Tuple[str, bytes, Optional[bytes]]], stubby_length: int) -> Tuple[LongReads, List[str]]:
     """proovread:1368-1524 on (id, seq, qual or None) records: FASTA reads get '$'
     qualities, reads shorter than stubby_length go to .ignored.tsv, sequences are
@@ -128,8 +160,7 @@ def read_long(records: Sequence[Tuple[str, bytes, Optional[bytes]]], stubby_leng
             continue
         if rid in keep:
             raise ValueError(f"Non-unique long read id ({rid})")
-        s = seq.upper()
-        s = bytes(c if c in b"ACGTN" else ord("N") for c in s)
+        s = seq.translate(_LR_TABLE)   # upper case, every non-ACGTN -> N
         keep[rid] = (s, qual if qual is not None else b"$" * len(s))
     ids = sorted(keep, key=functools.cmp_to_key(byfile_cmp))
     return LongReads(ids, [keep[i][0] for i in ids], [keep[i][1] for i in ids]), ignored
@@ -138,16 +169,39 @@ def read_long(records: Sequence[Tuple[str, bytes, Optional[bytes]]], stubby_leng
 # ---------------------------------------------------------------------------- short reads
 class ShortReads:
     """The short-read input as one byte stream (`cat $or_files`, proovread:1293) with its
-    FASTQ/FASTA records, sampled per task like SeqChunker."""
+    FASTQ/FASTA records, sampled per task like SeqChunker.  The records' sequences are kept
+    as one nt4 pool in stream order; SeqChunker's chunks are contiguous record ranges, so a
+    task's sample is a concatenation of pool slices."""
 
     def __init__(self, data: bytes, chunk_number: int = 1000):
         self.data = data
-        self.n_chunks, self.chunks = seqchunker.chunk(data, n_chunks=chunk_number)
-        self.spans = [r for c in self.chunks for r in c]
-        self.lengths = [len(self._seq(s, e)) for s, e in self.spans]
+        total = len(data)
+        arr = np.frombuffer(data, np.uint8)
+        rec = _fastq4_records(arr)
+        if rec is not None:   # plain 4-line FASTQ: record starts and sequence lines by numpy
+            starts, s0, s1 = rec
+        else:                 # FASTA (multi-line) or irregular FASTQ: the record parser
+            spans = list(seqchunker.records(data))
+            starts = np.array([x for x, _ in spans], np.int64)
+            seqs = [self._seq_of(data[x:e]) for x, e in spans]
+        self.n_chunks = max(1, chunk_number)
+        csize = max(1, math.ceil(total / self.n_chunks)) if total else 1
+        chunk_of = np.minimum(starts // csize, self.n_chunks - 1) if len(starts) else np.zeros(0, np.int64)
+        # records of chunk k (1-based): [cfirst[k-1], cfirst[k])
+        self.cfirst = np.searchsorted(chunk_of, np.arange(self.n_chunks + 1), side="left").astype(np.int64)
+        if rec is not None:
+            lens = s1 - s0
+            self.off = np.zeros(len(lens) + 1, np.int64)
+            np.cumsum(lens, out=self.off[1:])
+            idx = np.repeat(s0 - self.off[:-1], lens) + np.arange(int(self.off[-1]), dtype=np.int64)
+            self.pool = NT4[arr[idx]]
+        else:
+            self.pool, self.off = _pool(seqs)
+            self.pool = NT4[self.pool]
+        self.lengths = np.diff(self.off)
 
-    def _seq(self, s: int, e: int) -> bytes:
-        rec = self.data[s:e]
+    @staticmethod
+    def _seq_of(rec: bytes) -> bytes:
         if rec[:1] == b">":
             return b"".join(rec.split(b"\n")[1:]).strip()
         return rec.split(b"\n")[1].strip()
@@ -156,102 +210,131 @@ class ShortReads:
         """nt4 pool of the records SeqChunker writes for cov2seqchunker's parameters
         (None: every record), in stream order."""
         if sc is None:
-            spans = self.spans
-        else:
-            ks = seqchunker.select(self.n_chunks, sc["--first-chunk"], sc["--chunk-step"], sc["--chunks-per-step"])
-            spans = [r for k in ks for r in self.chunks[k - 1]]
-        seqs = [self._seq(s, e) for s, e in spans]
-        off = np.zeros(len(seqs) + 1, np.int64)
-        np.cumsum([len(x) for x in seqs], out=off[1:])
-        pool = NT4[np.frombuffer(b"".join(seqs), np.uint8)] if seqs else np.zeros(0, np.uint8)
-        return np.ascontiguousarray(pool), off
+            return self.pool, self.off
+        ks = seqchunker.select(self.n_chunks, sc["--first-chunk"], sc["--chunk-step"], sc["--chunks-per-step"])
+        r0 = self.cfirst[np.asarray(ks, np.int64) - 1]
+        r1 = self.cfirst[np.asarray(ks, np.int64)]
+        parts = [self.pool[self.off[a]:self.off[b]] for a, b in zip(r0, r1) if b > a]
+        lens = np.concatenate([self.lengths[a:b] for a, b in zip(r0, r1) if b > a]) if parts else np.zeros(0, np.int64)
+        off = np.zeros(len(lens) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        pool = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+        return pool, off
+
+
+def _fastq4_records(arr: np.ndarray):
+    """(record starts, sequence-line starts, sequence-line ends) of a FASTQ stream of plain
+    4-line records (no blank lines, no CR), or None."""
+    if len(arr) == 0 or arr[0] != ord("@") or arr[-1] != 10:
+        return None
+    nl = np.flatnonzero(arr == 10)
+    if len(nl) % 4 or (arr == 13).any():
+        return None
+    starts = np.concatenate([[0], nl[3::4][:-1] + 1]).astype(np.int64)
+    if not (arr[starts] == ord("@")).all() or not (arr[nl[1::4] + 1] == ord("+")).all():
+        return None
+    s0 = (nl[0::4] + 1).astype(np.int64)
+    s1 = nl[1::4].astype(np.int64)
+    if not ((nl[3::4] - nl[2::4]) == (s1 - s0) + 1).all():   # quality lines as long as the sequences
+        return None
+    return starts, s0, s1
 
 
 # ---------------------------------------------------------------------------- device stages
+@dataclasses.dataclass
+class TaskOut:
+    """What a task leaves on the host (the reads stay with the stages)."""
+    n_tasks: int                           # seeds of this rank's short reads
+    chim: List[str]                        # finish: bam2cns chimera lines of this rank's reads
+    bpt: int = 0                           # regular: SeqFilter --phred-mask statistics of this
+    bpn: int = 0                           # rank's reads (the loop all-reduces them)
+
+
 class GpuStages:
-    """The product's device stages: pr_iter_* (bwa-mode SW + hand-off + consensus), and for the
-    multi-rank layout pr_sw_run (bwa mode) and pr_cns_run separately; pr_mask_run."""
+    """The product's device stages.  The loop's state -- the current long reads, their
+    qualities and the mapping reference -- stays in HBM between tasks (iteration.LongReadSet,
+    pr_lrset_*); a task uploads its sampled short reads and downloads the finish task's
+    chimera lines and two counters:
+
+      index     pr_lrset_index: the seed index of the mapping reference (finish: the reads)
+      seeding   pr_seed_gpu_map, seeds kept in HBM
+      world 1   pr_iter_upload_lrset + pr_iter_launch: SW + -b/-l filter + hand-off + consensus
+      ranks     pr_sw_upload_gpu_seeds + pr_sw_launch on the rank's short-read shard,
+                pr_aln_exchange (RCCL all-to-all to the long reads' owners),
+                pr_iter_upload_owned(from_set) + pr_iter_launch
+      mask      pr_iter_mask (SeqFilter --phred-mask of the resident consensus) -> bpt, bpN
+      commit    pr_lrset_commit: the consensus (and masked copy) replace the set's reads;
+                with ranks the owned slices are all-gathered on the device."""
 
     def __init__(self, ctx=None):
         from . import _abi
         self.ctx = ctx or _abi.default_context()
         self.device_ms = 0.0   # kernel time of the calls so far (index, seeding, SW .. consensus)
+        self.lrs = None
+        self.ids: List[str] = []
 
-    def iteration(self, d, ref_seq: np.ndarray, ref_qual: np.ndarray, task: str, params,
-                  bin_filter: Optional[Tuple[int, float]] = None) -> List[tuple]:
-        """-> per long read (status, seq, qual, chim lines with id `lr<i>`).  d: bwa-mode seeds of
-        every sampled short read; task: the bwa task whose options the SW stage takes
-        (proovread.cfg:318-365); bin_filter: (BIN, LEN) of bwa-proovread -b/-l, applied on the
-        device between the SW stage and the hand-off."""
+    def load(self, reads: LongReads) -> None:
         from . import iteration
-        it = iteration.Iteration(d, lr_qual=ref_qual, ctx=self.ctx, ref_seq=ref_seq)
-        opts = T.options(task)[1]
-        if bin_filter:
-            opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
-        it.launch(opts, params)
-        out = [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
-        self.device_ms += sum(it.timing())
-        return out
+        self.lrs = iteration.LongReadSet(self.ctx, reads.seq_pool, reads.off, reads.qual_pool)
+        self.ids = list(reads.ids)
 
-    def owned_iteration(self, lr_map, lr_off, sr, sr_off, task: str, params, ref_seq: np.ndarray,
-                        ref_qual: np.ndarray, bin_filter, comm, mask_cfg=None):
-        """The exact-parity multi-GPU layout for one task, on the device end to
-        end: the index of ALL long reads in HBM, this rank's contiguous short-read shard seeded
-        and aligned (bwa mode), every reported alignment sent to the owner of its long read
-        (pr_aln_exchange: device pack + one RCCL all-to-all of device buffers), the -b/-l
-        filter, hand-off and consensus of the owned reads, and (mask_cfg = (hcr-mask,
-        min_sr_length)) their masking on the resident consensus.  -> (lo, hi, per owned read
-        (status, seq, qual, chim lines), seeds of this rank, (masked, bpt, bpN) or None)."""
+    def task(self, task: str, sr: np.ndarray, sr_off: np.ndarray, params, bin_filter, comm=None,
+             exact: bool = False, mask_cfg=None) -> TaskOut:
+        """One bwa-sr task on the resident set.  mask_cfg = (hcr-mask, min_sr_length) for the
+        regular tasks, None for the finish task (which maps to the unmasked reads,
+        proovread:838-850); exact: the multi-GPU exact-parity layout."""
         from . import _abi, exact_shard as ex, iteration, mask, seed
-        world, rank = (comm.world, comm.rank) if comm is not None else (1, 0)
-        n_sr = len(sr_off) - 1
-        s, e = ex.sr_range(n_sr, world, rank)
-        bounds = ex.lr_bounds(lr_off, world)
-        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
-        ix = seed.DeviceSeedIndex(self.ctx, lr_map, lr_off)
-        a0, a1 = int(sr_off[s]), int(sr_off[e])
-        ix.map(sr[a0:a1], np.asarray(sr_off[s:e + 1]) - a0, T.options(task)[0], keep_on_device=True)
-        n_seeds = ix.seed_count()
-        self.device_ms += ix.build_ms() + ix.gpu_ms()
-        opts = T.options(task)[1]
+        L = _abi.lib()
+        seed._setup(L)
+        finish = mask_cfg is None
+        self.device_ms += self.lrs.index(self.lrs.READS if finish else self.lrs.MAP)
+        seed_opts, opts = T.options(task)
         if bin_filter:
             opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
-        iteration.shard_sw(self.ctx, opts, sr, sr_off, s, e, lr_map, lr_off)
-        iteration.exchange(self.ctx, comm if isinstance(comm, RcclComm) else None, s, bounds)
-        it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, ref_seq, ref_qual, sr, sr_off)
+        lr_off = self.lrs.offsets()
+        world, rank = (comm.world, comm.rank) if comm is not None else (1, 0)
+        if world > 1 and not isinstance(comm, RcclComm):
+            raise TypeError("the device stages exchange over RCCL (comm.RcclComm)")
+        n_sr = len(sr_off) - 1
+        if not exact:
+            seed._map_gpu(L, self.ctx, sr, sr_off, seed_opts, False, keep_on_device=True)
+            it = iteration.SetIteration(self.ctx, None, sr_off, lr_off)
+            lo, hi = 0, len(lr_off) - 1
+        else:
+            s, e = ex.sr_range(n_sr, world, rank)
+            bounds = ex.lr_bounds(lr_off, world)
+            lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+            a0, a1 = int(sr_off[s]), int(sr_off[e])
+            seed._map_gpu(L, self.ctx, sr[a0:a1], np.asarray(sr_off[s:e + 1]) - a0, seed_opts, False,
+                          keep_on_device=True)
+            iteration.ShardSW(self.ctx, sr, sr_off, s, e, None, lr_off, device_pools=True).launch(opts)
+            iteration.exchange(self.ctx, comm if world > 1 else None, s, bounds)
+            it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, None, None, sr if world > 1 else None, sr_off,
+                                          from_set=True)
+        n_tasks = seed._count(L, self.ctx)
+        self.device_ms += seed._last_ms(L.pr_seed_gpu_last_ms, self.ctx)
         it.launch(opts, params)
-        out = [(r.status, r.seq.encode("latin-1"), r.qual.encode("latin-1"), r.chim_lines()) for r in it.results()]
-        self.device_ms += sum(it.timing())
-        mres = None
-        if mask_cfg is not None:
+        out = TaskOut(n_tasks, [])
+        if finish:
+            out.chim = it.chim_lines(self.ids[lo:hi])
+        else:
             buf = _abi.DevBuffer(self.ctx, 16)
             it.mask_to(buf.ptr, mask.params(mask_cfg[0], mask_cfg[1]))
-            masked = it.masked()
             st = buf.download(np.int64)
             buf.close()
-            mres = (masked, int(st[0]), int(st[1]))
-        return lo, hi, out, n_seeds, mres
+            out.bpt, out.bpn = int(st[0]), int(st[1])
+        self.device_ms += sum(it.timing())
+        self.lrs.commit(comm if world > 1 else None, with_mask=not finish)
+        return out
 
-    def seed(self, lr_map, lr_off, sr, sr_off, seed_opts):
-        """bwa-mode seeds of the short reads on the device: the index of the whole mapping
-        reference built in HBM (pr_seed_gpu_index_build, the host build's tables byte for byte)
-        and pr_seed_gpu_map (the host path's task lists exactly, tests/test_seed_gpu.py)."""
-        from . import seed
-        ix = seed.DeviceSeedIndex(self.ctx, lr_map, lr_off)
-        if getattr(self, "debug_dir", None):   # diagnostics: the task's inputs, then the map
-            import os
-            np.savez(os.path.join(self.debug_dir, f"seed{getattr(self, '_dbg_n', 0)}.npz"), lr=lr_map, lr_off=lr_off,
-                     sr=sr, sr_off=sr_off)
-            self._dbg_n = getattr(self, "_dbg_n", 0) + 1
-        tk, _ = ix.map(sr, sr_off, seed_opts)
-        self.device_ms += ix.build_ms() + ix.gpu_ms()
-        return tk
+    def reads(self) -> LongReads:
+        off, seq, qual, _ = self.lrs.download(seq=True, qual=True)
+        return LongReads(self.ids, pools=(seq, off, qual))
 
-    def mask(self, seqs: List[bytes], quals: List[bytes], hcr_mask: str, min_sr_length: int):
-        """-> (masked reads, bpt, bpN)."""
-        from . import mask
-        masked, _, (bpt, bpn) = mask.run(seqs, quals, mask.params(hcr_mask, min_sr_length), ctx=self.ctx)
-        return masked, bpt, bpn
+    def masked(self) -> List[bytes]:
+        """The mapping reference of the next task (LR.masked.fa)."""
+        off, _, _, m = self.lrs.download(seq=False, qual=False, mapping=True)
+        return _split(m, off)
 
 
 def _seed_tasks(lr_map, lr_off, sr, sr_off, seed_opts, threads):
@@ -309,15 +392,15 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
     cfg = cfg or LoopConfig()
     stages = stages or GpuStages()
     srs = ShortReads(sr_data)
-    min_sr = cfg.min_sr_length or (min(srs.lengths) if srs.lengths else 200)
+    min_sr = cfg.min_sr_length or (int(srs.lengths.min()) if len(srs.lengths) else 200)
     stubby = cfg.lr_min_length if cfg.lr_min_length is not None else 2 * min_sr
     sampler = control.Sampler(sampling=cfg.sampling)
     mode = cfg.mode or T.mode_for(min_sr)
     tasks = list(cfg.tasks or T.MODE_TASKS[mode])
     fracs: List[float] = []
     log: List[TaskLog] = []
-    reads, ignored = None, []
-    mapped: List[bytes] = []          # the mapping reference of the next task (.masked.fa)
+    ids: List[str] = []
+    ignored: List[str] = []
     chim: List[str] = []
     last_masked = None
     tc = 0
@@ -325,7 +408,8 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         task = tasks[tc]
         if task == "read-long":
             reads, ignored = read_long(lr_records, stubby)
-            mapped = list(reads.seqs)
+            ids = reads.ids
+            stages.load(reads)    # the mapping reference starts as the reads (.masked.fa)
             log.append(TaskLog(task))
             tc += 1
             continue
@@ -338,57 +422,26 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         task_cov = sr_coverage_for(task)
         sr, sr_off = srs.sample(sampler.cov2seqchunker(cfg.coverage, task_cov))
         ent.n_sr = len(sr_off) - 1
-        ref_map = reads.seqs if finish else mapped     # finish maps to the unmasked .fq (proovread:838-850)
-        lr_map, lr_off = reads.pool(ref_map)
-        lr_map = NT4[lr_map]
         max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541
         params = cns.CnsParams(coverage=max_cov, use_ref_qual=not finish, detect_chimera=finish,
                                max_ins_length=0)
         # bwa-proovread -b BIN -l BIN*min(cov, task cov) (proovread:1302-1313, cfg bin-size)
         bsz = T.bin_size(mode)
         binf = (bsz, bsz * min(cfg.coverage, task_cov)) if cfg.bin_filter else None
-        ref_seq, _ = reads.pool(reads.seqs)
-        ref_qual, _ = reads.pool(reads.quals)
-        mres = None
-        if (comm is None or comm.world == 1) and not cfg.exact_layout:
-            if hasattr(stages, "seed"):   # device stages: index and seeding in HBM
-                tk = stages.seed(lr_map, lr_off, sr, sr_off, T.options(task)[0])
-            else:
-                tk = _seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], cfg.seed_threads)
-            ent.n_tasks = int(len(tk))
-            d = _seeds_dataset(lr_map, lr_off, sr, sr_off, tk)
-            lo, hi = 0, len(reads.ids)
-            out = stages.iteration(d, ref_seq, ref_qual, task, params, bin_filter=binf)
-        else:   # exact-parity layout: short-read shards -> alignments to the long reads' owners
-            lo, hi, out, ent.n_tasks, mres = stages.owned_iteration(
-                lr_map, lr_off, sr, sr_off, task, params, ref_seq, ref_qual, binf, comm,
-                None if finish else (hcr_mask_for(task), min_sr))
-        ids = reads.ids[lo:hi]
-        seqs, quals, lines = [], [], []
-        for i, (st, s, q, ch) in enumerate(out):
-            if st != 0:
-                raise RuntimeError(f"{task}: consensus of {ids[i]} failed with status {st}")
-            seqs.append(s)
-            quals.append(q)
-            if finish:
-                lines += _rename(ch, ids[i])
-        masked, bpt, bpn = [], 0, 0
-        if mres is not None:
-            masked, bpt, bpn = mres
-        elif not finish and seqs:
-            masked, bpt, bpn = stages.mask(seqs, quals, hcr_mask_for(task), min_sr)
-        if comm is not None and comm.world > 1:
-            seqs, quals = comm.allgather_lists(seqs), comm.allgather_lists(quals)
+        multi = comm is not None and comm.world > 1
+        if finish and cfg.keep_masked:
+            last_masked = stages.masked()
+        r = stages.task(task, sr, sr_off, params, binf, comm if multi else None, multi or cfg.exact_layout,
+                        None if finish else (hcr_mask_for(task), min_sr)) if ids else TaskOut(0, [])
+        ent.n_tasks = r.n_tasks
+        lines, bpt, bpn = r.chim, r.bpt, r.bpn
+        if multi:
             if finish:
                 lines = [x.decode() for x in comm.allgather_lists([x.encode() for x in lines])]
             else:
-                masked = comm.allgather_lists(masked)
                 bpt, bpn = comm.allreduce_ints([bpt, bpn])
         chim += lines
-        reads = LongReads(reads.ids, seqs, quals)
         if not finish:
-            mapped = masked
-            last_masked = masked
             ent.bpt, ent.bpn = bpt, bpn
             ent.masked_frac = control.masked_fraction(bpt, bpn) if bpt else 0.0
             ent.shortcut = control.mask_shortcut(tasks, tc, ent.masked_frac, fracs, cfg.mask_shortcut_frac,
@@ -398,6 +451,9 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
             ent.device_ms = round(stages.device_ms - dev0, 1)
         log.append(ent)
         tc += 1
+    reads = stages.reads() if ids else LongReads([], [], [])
+    if cfg.keep_masked and last_masked is None and ids:
+        last_masked = stages.masked()
     return LoopResult(reads, chim, ignored, log, last_masked)
 
 

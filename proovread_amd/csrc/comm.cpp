@@ -252,6 +252,36 @@ extern "C" int pr_comm_alltoallv_dev(pr_comm *c, const void *send, const int64_t
     return 0;
 }
 
+// all-gather of device byte blocks of different sizes (counts[r] = rank r's bytes, known to every
+// rank): rank r's block lands at the sum of the earlier counts; point-to-point pairs in pieces
+extern "C" int pr_comm_allgatherv_dev(pr_comm *c, const void *send, const int64_t *counts, void *recv) {
+    if (!c || !counts) return pr_set_error(PR_ERR_ARG, "null arg");
+    const int W = c->world, me = c->rank;
+    std::vector<int64_t> o((size_t)W + 1, 0);
+    for (int r = 0; r < W; ++r) {
+        if (counts[r] < 0) return pr_set_error(PR_ERR_ARG, "negative count");
+        o[(size_t)r + 1] = o[(size_t)r] + counts[r];
+    }
+    if ((counts[me] && !send) || (o[(size_t)W] && !recv)) return pr_set_error(PR_ERR_ARG, "null buffer");
+    hipStream_t s = ctx_stream(c->ctx);
+    HIPCHK(hipSetDevice(ctx_device(c->ctx)));
+    uint8_t *dr = (uint8_t *)recv;
+    const uint8_t *ds = (const uint8_t *)send;
+    if (counts[me] && ds != dr + o[(size_t)me])
+        HIPCHK(hipMemcpyAsync(dr + o[(size_t)me], ds, (size_t)counts[me], hipMemcpyDeviceToDevice, s));
+    NCCLCHK(ncclGroupStart());
+    for (int r = 0; r < W; ++r) {
+        if (r == me) continue;
+        for (int64_t k = 0; k < counts[me]; k += P2P_PIECE)
+            NCCLCHK(ncclSend(ds + k, (size_t)std::min<int64_t>(P2P_PIECE, counts[me] - k), ncclUint8, r, c->nc, s));
+        for (int64_t k = 0; k < counts[r]; k += P2P_PIECE)
+            NCCLCHK(ncclRecv(dr + o[(size_t)r] + k, (size_t)std::min<int64_t>(P2P_PIECE, counts[r] - k), ncclUint8, r,
+                             c->nc, s));
+    }
+    NCCLCHK(ncclGroupEnd());
+    return 0;
+}
+
 pr_ctx *comm_ctx(pr_comm *c) { return c ? c->ctx : nullptr; }
 
 // the counts exchange of an all-to-all: recv_counts[r] = what rank r sends to this rank

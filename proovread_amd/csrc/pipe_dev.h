@@ -39,6 +39,9 @@ struct PipeDev {
 int pipe_launch(const PipeDev &P, int grid, void *stream, int lds_sort);
 // bwa-proovread -b/-l score binning (the filter runs before pipe_launch when P.keep is set)
 int pipe_binfilter_launch(const PipeDev &P, int bin_size, double bin_length, int max_bins, int grid, void *stream);
+// dense pools of the consensus (d0), its quality (d1) and masked copy (d2) from the capacity layout
+int lr_compact_launch(const int64_t *src_off, const int32_t *len, const int64_t *dst_off, int n, const uint8_t *s0,
+                      uint8_t *d0, const uint8_t *s1, uint8_t *d1, const uint8_t *s2, uint8_t *d2, void *stream);
 int iter_stats_launch(const int64_t *out_off, const int32_t *status, const int32_t *seq_len, const uint8_t *qual,
                       int n_lr, int min_char, unsigned long long *out, void *stream);
 

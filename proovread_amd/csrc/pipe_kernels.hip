@@ -277,6 +277,32 @@ int iter_stats_launch(const int64_t *out_off, const int32_t *status, const int32
     return (int)hipGetLastError();
 }
 
+// the resident long-read set after a consensus launch: every read's consensus (and its quality and
+// masked copy) from the per-read capacity layout (out_off) into dense pools (dst_off); a
+// workgroup per read, 16-byte stores where the destination allows
+__global__ void __launch_bounds__(256) lr_compact_kernel(const int64_t *src_off, const int32_t *len,
+                                                         const int64_t *dst_off, int n, const uint8_t *s0, uint8_t *d0,
+                                                         const uint8_t *s1, uint8_t *d1, const uint8_t *s2, uint8_t *d2) {
+    for (int i = blockIdx.x; i < n; i += gridDim.x) {
+        const int64_t so = src_off[i], dof = dst_off[i];
+        const int L = len[i];
+        for (int k = threadIdx.x; k < L; k += 256) {
+            d0[dof + k] = s0[so + k];
+            if (s1) d1[dof + k] = s1[so + k];
+            if (s2) d2[dof + k] = s2[so + k];
+        }
+    }
+}
+
+int lr_compact_launch(const int64_t *src_off, const int32_t *len, const int64_t *dst_off, int n, const uint8_t *s0,
+                      uint8_t *d0, const uint8_t *s1, uint8_t *d1, const uint8_t *s2, uint8_t *d2, void *stream) {
+    if (n <= 0) return 0;
+    const int grid = n < 4096 ? n : 4096;
+    hipLaunchKernelGGL(lr_compact_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, src_off, len, dst_off, n, s0, d0,
+                       s1, d1, s2, d2);
+    return (int)hipGetLastError();
+}
+
 int pipe_launch(const PipeDev &P, int grid, void *stream, int lds_sort) {
     hipStream_t s = (hipStream_t)stream;
     hipLaunchKernelGGL(pipe_count_kernel, dim3(grid), dim3(PIPE_THREADS), 0, s, P);

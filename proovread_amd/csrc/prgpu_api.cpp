@@ -93,6 +93,8 @@ enum SeedBufId {
 // the exact-parity layout's exchange (pr_aln_exchange, owned batches): bounds, sort keys and
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
 // the task's short reads
+// the resident long-read set: pools, the dense offsets of a commit, the commit's staging pools
+enum LrSetBufId { LS_SEQ, LS_QUAL, LS_MAP, LS_OFF, LS_TSEQ, LS_TQUAL, LS_TMAP, LS_COUNT };
 enum XchgBufId {
     XB_BOUNDS, XB_KEY0, XB_KEY1, XB_IDX0, XB_IDX1, XB_CNT, XB_OPIN, XB_OPAT, XB_SREC, XB_SCIG, XB_TEMP,
     XB_RREC, XB_RCIG, XB_RCIGAT, XB_GCNT, XB_GCNT64, XB_TASKOFF, XB_ERR, XB_GSR, XB_GSTATUS, XB_GPOS, XB_GSCORE,
@@ -110,6 +112,7 @@ struct pr_ctx {
     int32_t n_lr = 0;
     int64_t n_aln = 0, total_cols = 0, n_bins = 0, seq_cap = 0, chim_cap = 0;
     int64_t seed_pass2 = 0;   // reads of the last pr_seed_gpu_map that needed the large slices
+    int64_t seed_pass3 = 0;   // ... and the grown slices of the later passes (counted per pass)
     std::vector<int64_t> seed_pre;   // per-read prefix of the last pr_seed_gpu_map's seeds (SB_DENSE)
     int64_t alg_bytes = 0;
     int64_t k_need = 0;   // per-read bound of kept alignments (K pool slices)
@@ -141,6 +144,11 @@ struct pr_ctx {
     bool x_ready = false;        // XB_RREC / XB_RCIG hold the last exchange's records
     bool x_pass = false;         // world 1: the exchange is the identity, the owned launch reads the SW output
     int64_t x_nrecv = 0, x_nrcig = 0;
+    // the resident long-read set (pr_lrset_*): reads, qualities, mapping reference (masked reads)
+    DevBuf ls[LS_COUNT];
+    std::vector<int64_t> ls_off;
+    int32_t ls_n = -1;
+    bool ls_map_is_reads = true;
     bool own = false;            // the resident iteration batch is an owned batch (pr_iter_upload_owned)
     bool own_ref_nt4 = false;    // its consensus reference is the SW long-read pool's slice (nt4)
     int32_t own_lr0 = 0;
@@ -184,6 +192,7 @@ extern "C" void pr_ctx_destroy(pr_ctx *c) {
     for (auto &b : c->mb) b.release();
     for (auto &b : c->sd) b.release();
     for (auto &b : c->xb) b.release();
+    for (auto &b : c->ls) b.release();
     sw_release(c->sw);
     for (auto &e : c->ev) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -581,7 +590,11 @@ extern "C" int pr_cns_resident_stats(pr_ctx *c, int64_t *columns, int64_t *alg_b
 
 // ---------------------------------------------------------------------------
 // one iteration on the device: SW -> assemble -> consensus (pr_iter_*)
-static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds) {
+// dev_*: device sources in place of the batch's host pools (the resident long-read set and the
+// seeding's copies: pr_iter_upload_lrset)
+static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds, const uint8_t *dev_sr = nullptr,
+                       const uint8_t *dev_lr = nullptr, const uint8_t *dev_ref = nullptr,
+                       const uint8_t *dev_qual = nullptr) {
     if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
     pr_sw_batch sbv = b->sw;
     if (gpu_seeds) {   // the seeds of the last pr_seed_gpu_map, still in HBM
@@ -605,7 +618,8 @@ static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds) {
         if (k > maxt) maxt = (int)k;
     }
     if (maxt > 16384) return set_error(PR_ERR_CAPACITY, "more than 16384 tasks on one long read");
-    int rc = gpu_seeds ? sw_upload_device_seeds(c, &sb, c->sd[SB_DENSE].as<pr_seed_task>(), c->seed_pre.data())
+    int rc = gpu_seeds ? sw_upload_device_seeds(c, &sb, c->sd[SB_DENSE].as<pr_seed_task>(), c->seed_pre.data(),
+                                                dev_sr, dev_lr)
                        : pr_sw_upload(c, &sb);
     if (rc) return rc;
     HIPCHK(hipSetDevice(c->device));
@@ -617,8 +631,8 @@ static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds) {
     c->n_aln = sb.n_task;
     c->total_cols = sb.lr_off[n];
     c->has_ref = true;
-    c->pipe_ref_ascii = b->ref_seq != nullptr;
-    c->has_qual = b->lr_qual != nullptr;
+    c->pipe_ref_ascii = b->ref_seq != nullptr || dev_ref != nullptr;
+    c->has_qual = b->lr_qual != nullptr || dev_qual != nullptr;
     c->has_ign = false;
     c->lr_off_host.assign(sb.lr_off, sb.lr_off + n + 1);
     c->out_off.assign(n + 1, 0);
@@ -641,6 +655,13 @@ static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds) {
     if ((rc = upload(B[CB_LR_OFF], sb.lr_off, n1, s))) return rc;
     if (b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)sb.lr_off[n], s))) return rc;
     if (b->ref_seq && (rc = upload(B[CB_REF_SEQ], b->ref_seq, (size_t)sb.lr_off[n], s))) return rc;
+    for (int k = 0; k < 2; ++k) {   // device sources of the reference and its qualities
+        const uint8_t *src = k ? dev_qual : dev_ref;
+        if (!src) continue;
+        DevBuf &dst = B[k ? CB_REF_QUAL : CB_REF_SEQ];
+        if ((rc = dst.ensure((size_t)sb.lr_off[n] + 1))) return rc;
+        if (sb.lr_off[n]) HIPCHK(hipMemcpyAsync(dst.p, src, (size_t)sb.lr_off[n], hipMemcpyDeviceToDevice, s));
+    }
     if (!bwa && (rc = upload(c->pb[0], b->task_lr_off, n1, s))) return rc;
     if ((rc = c->pb[1].ensure(n1 * 4)) || (rc = c->pb[2].ensure(n1 * 4))) return rc;
     if ((rc = B[CB_ALN_OFF].ensure(n1 * 8)) || (rc = B[CB_POS].ensure(na1 * 4)) ||
@@ -891,7 +912,7 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     c->total_cols = tl;
     c->has_ref = true;
     c->pipe_ref_ascii = true;
-    c->has_qual = b->lr_qual != nullptr;
+    c->has_qual = b->lr_qual != nullptr || b->from_set;
     c->has_ign = false;
     c->lr_off_host.assign(b->lr_off, b->lr_off + n + 1);
     if (!n) c->lr_off_host.assign(1, 0);
@@ -903,6 +924,15 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
         c->out_off[i + 1] = c->out_off[i] + 2 * L + 1024;   // guarded in the kernel
         c->chim_off[i + 1] = c->chim_off[i] + nb / 2 + 2;
     }
+    int64_t set0 = 0;   // from_set: the owned reads' first base in the set
+    if (b->from_set) {
+        if (c->ls_n < 0) return set_error(PR_ERR_ARG, "from_set: no resident long-read set");
+        if (b->lr0 < 0 || b->lr0 + n > c->ls_n) return set_error(PR_ERR_ARG, "owned long reads outside the set");
+        set0 = c->ls_off[(size_t)b->lr0];
+        for (int i = 0; i <= n; ++i)
+            if (c->ls_off[(size_t)(b->lr0 + i)] - set0 != b->lr_off[i])
+                return set_error(PR_ERR_ARG, "owned long reads differ from the set's");
+    }
     c->seq_cap = c->out_off[n];
     c->chim_cap = c->chim_off[n];
     c->alg_bytes = 0;
@@ -911,13 +941,19 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     DevBuf *B = c->cb;
     const size_t n1 = (size_t)n + 1;
     if ((rc = upload(B[CB_LR_OFF], c->lr_off_host.data(), n1, s))) return rc;
-    if (b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)tl, s))) return rc;
+    if (!b->from_set && b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)tl, s))) return rc;
     // ref_seq / sr_seq NULL: the resident SW batch's long reads (the owned slice, nt4: the mapping
     // reference is the consensus reference) / short reads (every short read of the task) on the device
     SwPtrs sp{};
-    if ((!b->ref_seq || !b->sr_seq) && (rc = sw_get_ptrs(c, &sp))) return rc;
-    c->own_ref_nt4 = !b->ref_seq;
-    if (b->ref_seq) {
+    if (((!b->ref_seq && !b->from_set) || !b->sr_seq) && (rc = sw_get_ptrs(c, &sp))) return rc;
+    c->own_ref_nt4 = !b->ref_seq && !b->from_set;
+    if (b->from_set) {   // the set's reads and qualities (the previous task's consensus)
+        if ((rc = B[CB_REF_SEQ].ensure((size_t)tl + 1)) || (rc = B[CB_REF_QUAL].ensure((size_t)tl + 1))) return rc;
+        if (tl) {
+            HIPCHK(hipMemcpyAsync(B[CB_REF_SEQ].p, c->ls[LS_SEQ].as<uint8_t>() + set0, (size_t)tl, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(B[CB_REF_QUAL].p, c->ls[LS_QUAL].as<uint8_t>() + set0, (size_t)tl, hipMemcpyDeviceToDevice, s));
+        }
+    } else if (b->ref_seq) {
         if ((rc = upload(B[CB_REF_SEQ], b->ref_seq, (size_t)tl, s))) return rc;
     } else {
         if (b->lr0 < 0 || b->lr0 + n > sp.n_lr) return set_error(PR_ERR_ARG, "owned long reads outside the SW batch");
@@ -1423,6 +1459,150 @@ extern "C" int pr_iter_mask_download(pr_ctx *c, uint8_t *masked) {
     return 0;
 }
 
+static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, int n_lr, bool lr_dev);
+
+// ---------------------------------------------------------------------------
+// the resident long-read set (include/prgpu.h pr_lrset_*): the loop's LR.fq and LR.masked.fa
+// between tasks, in HBM
+extern "C" int pr_lrset_load(pr_ctx *c, int32_t n_lr, const int64_t *off, const uint8_t *seq, const uint8_t *qual) {
+    if (!c || n_lr < 0 || !off || (n_lr && (!seq || !qual))) return set_error(PR_ERR_ARG, "null arg");
+    if (off[0] != 0) return set_error(PR_ERR_ARG, "offsets must start at 0");
+    for (int i = 0; i < n_lr; ++i)
+        if (off[i + 1] < off[i]) return set_error(PR_ERR_ARG, "offsets not monotone");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t nb = (size_t)off[n_lr];
+    int rc;
+    if ((rc = upload(c->ls[LS_SEQ], seq, nb, s)) || (rc = upload(c->ls[LS_QUAL], qual, nb, s))) return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    c->ls_off.assign(off, off + n_lr + 1);
+    c->ls_n = n_lr;
+    c->ls_map_is_reads = true;   // read-long: the mapping reference is the reads themselves
+    return 0;
+}
+
+extern "C" int pr_lrset_info(pr_ctx *c, int32_t *n_lr, int64_t *bases) {
+    if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+    if (n_lr) *n_lr = c->ls_n;
+    if (bases) *bases = c->ls_off.back();
+    return 0;
+}
+
+extern "C" int pr_lrset_download(pr_ctx *c, int64_t *off, uint8_t *seq, uint8_t *qual, uint8_t *map) {
+    if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t nb = (size_t)c->ls_off.back();
+    if (off) std::memcpy(off, c->ls_off.data(), c->ls_off.size() * 8);
+    int rc;
+    if ((rc = download(seq, c->ls[LS_SEQ], nb, s)) || (rc = download(qual, c->ls[LS_QUAL], nb, s)) ||
+        (rc = download(map, c->ls[c->ls_map_is_reads ? LS_SEQ : LS_MAP], nb, s)))
+        return rc;
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+}
+
+extern "C" int pr_lrset_index(pr_ctx *c, int which) {
+    if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+    if (which != PR_LRSET_MAP && which != PR_LRSET_READS) return set_error(PR_ERR_ARG, "which: PR_LRSET_MAP / _READS");
+    const int id = which == PR_LRSET_READS || c->ls_map_is_reads ? LS_SEQ : LS_MAP;
+    return index_build(c, c->ls[id].as<uint8_t>(), c->ls_off.data(), c->ls_n, true);
+}
+
+extern "C" int pr_iter_upload_lrset(pr_ctx *c, const pr_sw_batch *b) {
+    if (!c || !b) return set_error(PR_ERR_ARG, "null arg");
+    if (c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+    if (!c->seed_n_text || c->seed_view.n_lr != c->ls_n || c->seed_view.l_pac != c->ls_off.back())
+        return set_error(PR_ERR_ARG, "the seed index is not over the long-read set (pr_lrset_index first)");
+    if (c->seed_pre.size() != (size_t)b->n_sr + 1)
+        return set_error(PR_ERR_ARG, "no device seeds for these short reads (pr_seed_gpu_map with out = NULL first)");
+    if (!b->sr_seq && b->n_sr && c->seed_sr_bases != b->sr_off[b->n_sr])
+        return set_error(PR_ERR_ARG, "sr_seq NULL: the short reads must be those of the last pr_seed_gpu_map");
+    pr_iter_batch ib;
+    std::memset(&ib, 0, sizeof ib);
+    ib.sw = *b;
+    ib.sw.n_lr = c->ls_n;
+    ib.sw.lr_off = c->ls_off.data();
+    ib.sw.lr_seq = nullptr;
+    return iter_upload(c, &ib, true, b->sr_seq ? nullptr : c->sd[SB_SEQ].as<uint8_t>(), c->sd[SX_LRSEQ].as<uint8_t>(),
+                       c->ls[LS_SEQ].as<uint8_t>(), c->ls[LS_QUAL].as<uint8_t>());
+}
+
+extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int with_mask) {
+    if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+    if (!c->cns_launched || !c->pipe) return set_error(PR_ERR_ARG, "no iteration launch to commit");
+    if (with_mask && !c->iter_masked) return set_error(PR_ERR_ARG, "with_mask: no pr_iter_mask launch");
+    int rank = 0, world = 1, rc;
+    if (comm && (rc = pr_comm_rank(comm, &rank, &world))) return rc;
+    const int lr0 = c->own ? c->own_lr0 : 0, n = c->n_lr;
+    if (world == 1 && (lr0 != 0 || n != c->ls_n)) return set_error(PR_ERR_ARG, "the batch must hold every long read");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    if (with_mask && (rc = mask_check_err(c))) return rc;
+    std::vector<int32_t> st((size_t)n + 1, 0), len((size_t)n + 1, 0), herr((size_t)n + 1, 0);
+    if (n) {
+        HIPCHK(hipMemcpyAsync(st.data(), c->cb[CB_STATUS].p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(len.data(), c->cb[CB_SEQ_LEN].p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(herr.data(), c->pb[2].p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < n; ++i) {   // as pr_iter_download: never silent
+        if (herr[(size_t)i])
+            return set_error(PR_ERR_CAPACITY, "hand-off of long read %d failed (code %d)", lr0 + i, herr[(size_t)i]);
+        if (st[(size_t)i]) return set_error(st[(size_t)i], "consensus of long read %d failed (status %d)", lr0 + i, st[(size_t)i]);
+    }
+    std::vector<int64_t> doff((size_t)n + 1, 0);
+    for (int i = 0; i < n; ++i) doff[(size_t)i + 1] = doff[(size_t)i] + len[(size_t)i];
+    const int64_t own = doff[(size_t)n];
+    DevBuf *L = c->ls;
+    if ((rc = upload(L[LS_OFF], doff.data(), (size_t)n + 1, s)) || (rc = L[LS_TSEQ].ensure((size_t)own + 1)) ||
+        (rc = L[LS_TQUAL].ensure((size_t)own + 1)) || (with_mask && (rc = L[LS_TMAP].ensure((size_t)own + 1))))
+        return rc;
+    int e = lr_compact_launch(c->cb[CB_OUT_OFF].as<int64_t>(), c->cb[CB_SEQ_LEN].as<int32_t>(), L[LS_OFF].as<int64_t>(),
+                              n, c->cb[CB_O_SEQ].as<uint8_t>(), L[LS_TSEQ].as<uint8_t>(), c->cb[CB_O_QUAL].as<uint8_t>(),
+                              L[LS_TQUAL].as<uint8_t>(), with_mask ? c->mb[MB_OUT].as<uint8_t>() : nullptr,
+                              with_mask ? L[LS_TMAP].as<uint8_t>() : nullptr, (void *)s);
+    if (e) return set_error(PR_ERR_HIP, "long-read set compaction: %s", hipGetErrorString((hipError_t)e));
+    std::vector<int64_t> off((size_t)c->ls_n + 1, 0);
+    if (world == 1) {
+        std::swap(L[LS_SEQ], L[LS_TSEQ]);
+        std::swap(L[LS_QUAL], L[LS_TQUAL]);
+        if (with_mask) std::swap(L[LS_MAP], L[LS_TMAP]);
+        off = doff;
+    } else {
+        // every rank's owned reads in rank order (= global order: the owners' ranges ascend):
+        // the lengths all-gathered on the host (small), the pools on the device
+        std::vector<int64_t> cnt((size_t)world, 0);
+        cnt[(size_t)rank] = n;
+        if ((rc = pr_comm_allreduce_host(comm, cnt.data(), world, PR_DT_I64, PR_RED_SUM))) return rc;
+        int64_t tot_n = 0;
+        for (int r = 0; r < world; ++r) tot_n += cnt[(size_t)r];
+        if (tot_n != c->ls_n) return set_error(PR_ERR_ARG, "the ranks' owned reads do not make up the set");
+        std::vector<int64_t> lens((size_t)c->ls_n, 0), bytes((size_t)world, 0);
+        int64_t first = 0;
+        for (int r = 0; r < rank; ++r) first += cnt[(size_t)r];
+        for (int i = 0; i < n; ++i) lens[(size_t)(first + i)] = len[(size_t)i];
+        if ((rc = pr_comm_allreduce_host(comm, lens.data(), c->ls_n, PR_DT_I64, PR_RED_SUM))) return rc;
+        for (int i = 0; i < c->ls_n; ++i) off[(size_t)i + 1] = off[(size_t)i] + lens[(size_t)i];
+        int64_t k = 0;
+        for (int r = 0; r < world; ++r) {
+            bytes[(size_t)r] = off[(size_t)(k + cnt[(size_t)r])] - off[(size_t)k];
+            k += cnt[(size_t)r];
+        }
+        const size_t tot = (size_t)off.back();
+        const int ids[3][2] = {{LS_TSEQ, LS_SEQ}, {LS_TQUAL, LS_QUAL}, {LS_TMAP, LS_MAP}};
+        for (int q = 0; q < (with_mask ? 3 : 2); ++q) {
+            if ((rc = L[ids[q][1]].ensure(tot + 1))) return rc;
+            if ((rc = pr_comm_allgatherv_dev(comm, L[ids[q][0]].p, bytes.data(), L[ids[q][1]].p))) return rc;
+        }
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    c->ls_off = off;
+    if (with_mask) c->ls_map_is_reads = false;
+    else c->ls_map_is_reads = true;   // the finish task: the reads are their own mapping reference
+    return 0;
+}
+
 // ---------------------------------------------------------------------------
 // seeding on the device (seed_kernels.hip over seed_core.h)
 extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
@@ -1459,7 +1639,12 @@ extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
 }
 
 // the seed index built in HBM (seed_index.hip): the tables of pr_seed_index_build
+// lr_dev: lr_seq is a device pointer (the resident long-read set), copied on the device
 extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, int n_lr) {
+    return index_build(c, lr_seq, lr_off, n_lr, false);
+}
+
+static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, int n_lr, bool lr_dev) {
     if (!c || n_lr < 0 || (n_lr && (!lr_seq || !lr_off))) return set_error(PR_ERR_ARG, "null arg");
     for (int i = 0; i < n_lr; ++i)
         if (lr_off[i + 1] < lr_off[i]) return set_error(PR_ERR_ARG, "lr_off not monotone");
@@ -1501,7 +1686,7 @@ extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const i
     const size_t nk1 = (size_t)seedc::NK + 1;
     // hits <= 12-mer starts; kpos / kext sized by the text (the count is known after the build)
     int rc;
-    if ((rc = upload(D[SX_LRSEQ], n_lr ? lr_seq + lr_off[0] : lr_seq, (size_t)l_pac, s)) ||
+    if ((rc = upload(D[SX_LRSEQ], lr_dev ? nullptr : (n_lr ? lr_seq + lr_off[0] : lr_seq), (size_t)l_pac, s)) ||
         (rc = upload(D[SI_LROFF], off.data(), off.size(), s)) || (rc = upload(D[SI_CSTART], cstart.data(), cstart.size(), s)) ||
         (rc = upload(D[SI_CBLK], cblk.data(), cblk.size(), s)) || (rc = D[SI_TEXT].ensure(nt)) ||
         (rc = D[SX_KEY0].ensure(ns * 4)) || (rc = D[SX_KEY1].ensure(ns * 4)) || (rc = D[SX_VAL0].ensure(ns * 4)) ||
@@ -1514,6 +1699,7 @@ extern "C" int pr_seed_gpu_index_build(pr_ctx *c, const uint8_t *lr_seq, const i
         return rc;
     const bool paged = n_text > (int64_t)seedc::POS_PAGE;
     if (paged && (rc = D[SI_KSPLIT].ensure(nk1 * 8))) return rc;
+    if (lr_dev && l_pac) HIPCHK(hipMemcpyAsync(D[SX_LRSEQ].p, lr_seq + lr_off[0], (size_t)l_pac, hipMemcpyDeviceToDevice, s));
     SeedIndexBuild B{};
     uint32_t *cptr[seedc::KI - 1];
     for (int j = 1; j < seedc::KI; ++j) {
@@ -1702,6 +1888,7 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         for (int i = 0; i < n_sr; ++i)
             if (st1[(size_t)i]) redo.push_back(i);
         c->seed_pass2 = (int64_t)redo.size();
+        c->seed_pass3 = 0;
         if (!redo.empty()) {   // pass 2 over the flagged reads (rlist in SB_PRE, rewritten later)
             HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
             HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
@@ -1713,6 +1900,38 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
             e = seed_launch(K, (void *)s);
             if (e) return set_error(PR_ERR_HIP, "seed kernel (pass 2): %s", hipGetErrorString((hipError_t)e));
             HIPCHK(hipStreamSynchronize(s));
+            // later passes: the reads that outgrew the large slices too (e.g. the finish task's
+            // near-exact reads at 30-60x long-read coverage: every 12-mer hits every copy, > 8192
+            // hits per read) again, with the arrays that overflowed grown, up to 4 times
+            seedc::Caps cg = caps;
+            for (int pass = 3; pass <= 6; ++pass) {
+                std::vector<int32_t> st2((size_t)n_sr);
+                if ((rc = download(st2.data(), D[SB_STATUS], (size_t)n_sr, s))) return rc;
+                HIPCHK(hipStreamSynchronize(s));
+                std::vector<int32_t> again;
+                int32_t fl = 0;
+                for (int32_t i : redo)
+                    if (st2[(size_t)i]) again.push_back(i), fl |= st2[(size_t)i];
+                if (again.empty() || (fl & (seedc::SC_OVER_LEN | seedc::SC_OVER_OUT))) break;
+                if (fl & seedc::SC_OVER_HITS) cg.hits *= 4;
+                if (fl & seedc::SC_OVER_IV) cg.iv *= 2;
+                if (fl & seedc::SC_OVER_MEMS) cg.mems *= 2;
+                if (fl & seedc::SC_OVER_SEEDS) cg.seeds *= 2;
+                if (fl & seedc::SC_OVER_CHAINS) cg.chains *= 2;
+                redo.swap(again);
+                K.caps = cg;
+                K.stride = seedc::scratch_bytes(cg);
+                K.n_lanes = std::min<int64_t>(lanes2, (int64_t)redo.size());
+                if ((rc = D[SB_SCRATCH].ensure((size_t)(K.n_lanes * K.stride)))) return rc;
+                K.scratch = D[SB_SCRATCH].as<uint8_t>();
+                K.n_list = (int64_t)redo.size();
+                HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
+                HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
+                e = seed_launch(K, (void *)s);
+                if (e) return set_error(PR_ERR_HIP, "seed kernel (pass %d): %s", pass, hipGetErrorString((hipError_t)e));
+                HIPCHK(hipStreamSynchronize(s));
+                c->seed_pass3 += (int64_t)redo.size();
+            }
         }
     }
     HIPCHK(hipEventRecord(c->ev[9], s));

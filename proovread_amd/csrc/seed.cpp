@@ -404,8 +404,8 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
             uint8_t *f = X + I.cstart[i];
             uint8_t *b = X + I.cstart[2 * (size_t)n_lr - 1 - i];
             for (int64_t p = 0; p < len; ++p) {
-                const uint8_t c = r[p];
-                f[p] = c < 4 ? c : 4;
+                const uint8_t c = seedc::base_code(r[p]);
+                f[p] = c;
                 b[len - 1 - p] = c < 4 ? (uint8_t)(3 - c) : 4;
             }
             f[len] = SEP;
@@ -737,12 +737,25 @@ extern "C" int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opt
         std::vector<uint64_t> slab((size_t)(bytes / 8 + 1));
         seedc::Scratch S = seedc::carve(reinterpret_cast<uint8_t *>(slab.data()), caps);
         std::vector<pr_seed_task> buf((size_t)caps.out);
+        std::vector<uint64_t> big;
         for (;;) {
             const int i = next.fetch_add(1);
             if (i >= n_sr) break;
             const int len = (int)(sr_off[i + 1] - sr_off[i]);
             int n = 0, err = 0;
             if (len > 0) err = seedc::map_read(V, *o, S, sr_seq + sr_off[i], len, i, buf.data(), caps.out, &n);
+            // the device's later passes: the arrays that overflowed grown, up to 4 times
+            seedc::Caps cg = caps;
+            for (int pass = 3; pass <= 6 && err && !(err & (seedc::SC_OVER_LEN | seedc::SC_OVER_OUT)); ++pass) {
+                if (err & seedc::SC_OVER_HITS) cg.hits *= 4;
+                if (err & seedc::SC_OVER_IV) cg.iv *= 2;
+                if (err & seedc::SC_OVER_MEMS) cg.mems *= 2;
+                if (err & seedc::SC_OVER_SEEDS) cg.seeds *= 2;
+                if (err & seedc::SC_OVER_CHAINS) cg.chains *= 2;
+                big.assign((size_t)(seedc::scratch_bytes(cg) / 8 + 1), 0);
+                seedc::Scratch G = seedc::carve(reinterpret_cast<uint8_t *>(big.data()), cg);
+                err = seedc::map_read(V, *o, G, sr_seq + sr_off[i], len, i, buf.data(), caps.out, &n);
+            }
             status[i] = err;
             if (!err) res[i].tasks.assign(buf.begin(), buf.begin() + n);
         }

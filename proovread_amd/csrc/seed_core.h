@@ -134,6 +134,18 @@ SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
 
 SC_HD int ctz64(uint64_t x) { return __builtin_ctzll(x); }
 
+// a long-read byte as a base code: nt4 codes (0-3, else N) or ASCII (ACGT in either case, else N)
+SC_HD uint8_t base_code(uint8_t c) {
+    if (c < 4) return c;
+    switch (c | 0x20) {
+        case 'a': return 0;
+        case 'c': return 1;
+        case 'g': return 2;
+        case 't': return 3;
+        default: return 4;
+    }
+}
+
 // text position of hit r of k-mer `code`
 SC_HD uint64_t hit_pos(const IndexView &I, uint32_t code, uint64_t r) {
     uint64_t p = I.kpos[r];

@@ -38,7 +38,9 @@ constexpr int KX = seedc::KX;
 
 // Kernels over the whole text are grid-stride loops over a capped grid: a dispatch's grid is
 // counted in work-items in 32 bits, and the text may exceed 2^32 positions.
-__global__ void ix_text_kernel(const uint8_t *lr_seq, const int64_t *lr_off, int n_lr, const int64_t *cstart,
+// the long reads arrive as nt4 codes or ASCII (seedc::base_code); their nt4 codes are written
+// back in place (the SW batch can take them from here: pr_sw_upload_gpu_seeds with lr_seq NULL)
+__global__ void ix_text_kernel(uint8_t *lr_seq, const int64_t *lr_off, int n_lr, const int64_t *cstart,
                                int64_t l_pac, uint8_t *text) {
   const int64_t nt = l_pac > n_lr ? l_pac : n_lr;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nt; g += (int64_t)gridDim.x * blockDim.x) {
@@ -50,8 +52,9 @@ __global__ void ix_text_kernel(const uint8_t *lr_seq, const int64_t *lr_off, int
         }
         const int i = lo;
         const int64_t p = g - lr_off[i], len = lr_off[i + 1] - lr_off[i];
-        const uint8_t c = lr_seq[g];
-        text[cstart[i] + p] = c < 4 ? c : 4;
+        const uint8_t c = seedc::base_code(lr_seq[g]);
+        lr_seq[g] = c;
+        text[cstart[i] + p] = c;
         text[cstart[2 * (int64_t)n_lr - 1 - i] + (len - 1 - p)] = c < 4 ? (uint8_t)(3 - c) : 4;
     }
     if (g < n_lr) {   // separators

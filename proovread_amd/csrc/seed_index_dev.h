@@ -9,7 +9,7 @@
 namespace prgpu {
 
 struct SeedIndexBuild {
-    const uint8_t *lr_seq;        // [l_pac] long-read codes (0-3 bases, anything else N)
+    uint8_t *lr_seq;              // [l_pac] long-read codes (nt4 or ASCII), rewritten as nt4
     const int64_t *lr_off;        // [n_lr + 1] rebased to 0
     int n_lr;
     int64_t l_pac;

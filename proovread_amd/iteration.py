@@ -20,7 +20,8 @@ class IterBatch(C.Structure):
 
 class OwnBatch(C.Structure):
     _fields_ = [("lr0", C.c_int32), ("n_lr", C.c_int32), ("lr_off", _abi.P64), ("ref_seq", _abi.PU8),
-                ("lr_qual", _abi.PU8), ("n_sr", C.c_int32), ("sr_off", _abi.P64), ("sr_seq", _abi.PU8)]
+                ("lr_qual", _abi.PU8), ("n_sr", C.c_int32), ("sr_off", _abi.P64), ("sr_seq", _abi.PU8),
+                ("from_set", C.c_int32)]
 
 
 def _setup(L):
@@ -40,6 +41,12 @@ def _setup(L):
     L.pr_aln_exchange.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, _abi.P64, _abi.P64]
     L.pr_aln_exchange_local.argtypes = [C.c_void_p, C.c_int, _abi.P64, _abi.P64, _abi.P64]
     L.pr_iter_upload_owned.argtypes = [C.c_void_p, C.POINTER(OwnBatch)]
+    L.pr_lrset_load.argtypes = [C.c_void_p, C.c_int32, _abi.P64, _abi.PU8, _abi.PU8]
+    L.pr_lrset_info.argtypes = [C.c_void_p, _abi.P32, _abi.P64]
+    L.pr_lrset_index.argtypes = [C.c_void_p, C.c_int]
+    L.pr_lrset_commit.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
+    L.pr_lrset_download.argtypes = [C.c_void_p, _abi.P64, _abi.PU8, _abi.PU8, _abi.PU8]
+    L.pr_iter_upload_lrset.argtypes = [C.c_void_p, C.POINTER(sw.SwBatch)]
     L._iter_ready = True
 
 
@@ -169,6 +176,27 @@ class Iteration:
                    scatter_runscan=t[20] / 1e5)
         return out
 
+    def chimeras(self):
+        """-> (status, nchim, chim_off, chim rows [from, to, npos, ntot]) per long read: the part
+        of the output the finish task keeps on the host (detect_chimera)."""
+        n = self.n_lr
+        a = dict(status=np.zeros(n, np.int32), nchim=np.zeros(n, np.int32), chim_off=np.zeros(n + 1, np.int64),
+                 chim=np.zeros(4 * (self.bounds.chim_cap + 1), np.int32))
+        o = _abi.CnsOut()
+        for k, ct in (("status", C.c_int32), ("nchim", C.c_int32), ("chim_off", C.c_int64), ("chim", C.c_int32)):
+            setattr(o, k, _abi.ptr(a[k], ct))
+        _abi.check(self.L.pr_iter_download(self.ctx.h, C.byref(o)), "pr_iter_download")
+        return a["status"], a["nchim"], a["chim_off"], a["chim"].reshape(-1, 4)
+
+    def chim_lines(self, ids: List[str]) -> List[str]:
+        """bam2cns:488's chimera lines of every long read (ids: theirs, in batch order)."""
+        st, nch, c0, rows = self.chimeras()
+        out = []
+        for i in np.flatnonzero(nch):
+            for fr, to, npos, ntot in rows[int(c0[i]):int(c0[i]) + int(nch[i])]:
+                out.append(f"{ids[i]}\t{int(fr)}\t{int(to)}\t{cns.perl_num(int(npos) / int(ntot))}")
+        return out
+
     def results(self) -> List[cns.ReadResult]:
         a = self.download()
         out = []
@@ -258,13 +286,16 @@ class OwnedIteration(Iteration):
     The results (download, results, mask_to, stats_to, masked) are those of the owned reads
     and equal a single-GPU Iteration's on them."""
 
-    def __init__(self, ctx, lo: int, hi: int, lr_off: np.ndarray, ref_seq: np.ndarray,
-                 ref_qual: Optional[np.ndarray], sr: np.ndarray, sr_off: np.ndarray):
+    def __init__(self, ctx, lo: int, hi: int, lr_off: np.ndarray, ref_seq: Optional[np.ndarray],
+                 ref_qual: Optional[np.ndarray], sr: Optional[np.ndarray], sr_off: np.ndarray,
+                 from_set: bool = False):
         """lr_off: every long read's offsets; ref_seq / ref_qual: the consensus reference
         (ASCII, bam2cns --ref) and qualities of all long reads in lr_off's layout (the owned
         slice is uploaded; ref_seq None: the SW batch's long reads, when the mapping reference
         is the consensus reference); sr / sr_off: every short read of the task (nt4), which
-        the consensus reads by global id (sr None: the SW batch holds every short read)."""
+        the consensus reads by global id (sr None: the SW batch holds every short read);
+        from_set: the reference and qualities are the resident long-read set's (LongReadSet;
+        ref_seq / ref_qual not used)."""
         self.L = _abi.lib()
         _setup(self.L)
         self.ctx = ctx
@@ -288,6 +319,7 @@ class OwnedIteration(Iteration):
         ob.n_sr = len(self._sr_off) - 1
         ob.sr_off = _abi.ptr(self._sr_off, C.c_int64)
         ob.sr_seq = _abi.ptr(self._sr, C.c_uint8)
+        ob.from_set = int(from_set)
         self._ob = ob
         _abi.check(self.L.pr_iter_upload_owned(ctx.h, C.byref(ob)), "pr_iter_upload_owned")
         self.d = SimpleNamespace(lr_off=self._own_off)
@@ -303,3 +335,78 @@ class OwnedIteration(Iteration):
         """-b/-l filter, hand-off and consensus over the alignments of the last exchange."""
         super().launch(sw_opts, params)
         self._bounds()   # the alignments are counted at launch (the output buffers follow)
+
+
+class LongReadSet:
+    """The resident long-read set (include/prgpu.h pr_lrset_*): the loop's current reads and
+    qualities (LR.fq) and their mapping reference (LR.masked.fa) in HBM between tasks."""
+
+    MAP, READS = 0, 1
+
+    def __init__(self, ctx, seq_pool: np.ndarray, off: np.ndarray, qual_pool: np.ndarray):
+        """ASCII bases and phred+33 qualities of every long read in one pool each (off[n+1])."""
+        self.L = _abi.lib()
+        _setup(self.L)
+        self.ctx = ctx
+        off = np.ascontiguousarray(off, np.int64)
+        seq = np.ascontiguousarray(seq_pool, np.uint8)
+        qual = np.ascontiguousarray(qual_pool, np.uint8)
+        if len(seq) != int(off[-1]) or len(qual) != int(off[-1]):
+            raise ValueError("pools must have the offsets' layout")
+        _abi.check(self.L.pr_lrset_load(ctx.h, len(off) - 1, _abi.ptr(off, C.c_int64), _abi.ptr(seq, C.c_uint8),
+                                        _abi.ptr(qual, C.c_uint8)), "pr_lrset_load")
+        self.n = len(off) - 1
+
+    def offsets(self) -> np.ndarray:
+        off = np.zeros(self.n + 1, np.int64)
+        _abi.check(self.L.pr_lrset_download(self.ctx.h, _abi.ptr(off, C.c_int64), None, None, None),
+                   "pr_lrset_download")
+        return off
+
+    def download(self, seq: bool = True, qual: bool = True, mapping: bool = False):
+        """-> (offsets, ASCII bases, qualities, mapping reference); pools not asked for are None."""
+        off = self.offsets()
+        nb = int(off[-1])
+        bufs = [np.zeros(nb + 1, np.uint8) if w else None for w in (seq, qual, mapping)]
+        _abi.check(self.L.pr_lrset_download(self.ctx.h, None, *[_abi.ptr(b, C.c_uint8) for b in bufs]),
+                   "pr_lrset_download")
+        return (off, *[None if b is None else b[:nb] for b in bufs])
+
+    def index(self, which: int):
+        """Seed index over the mapping reference (MAP) or the reads (READS), replacing the
+        context's (pr_lrset_index); -> its build time (ms)."""
+        from . import seed
+        seed._setup(self.L)
+        _abi.check(self.L.pr_lrset_index(self.ctx.h, int(which)), "pr_lrset_index")
+        return seed._last_ms(self.L.pr_seed_gpu_index_last_ms, self.ctx)
+
+    def commit(self, comm=None, with_mask: bool = False):
+        """Every read's consensus (with_mask: and its masked copy as the next mapping reference)
+        replaces the set's; comm: the owned batches of all ranks, all-gathered on the device."""
+        _abi.check(self.L.pr_lrset_commit(self.ctx.h, comm.h if comm is not None else None, int(with_mask)),
+                   "pr_lrset_commit")
+
+
+class SetIteration(Iteration):
+    """A world-1 iteration over the resident long-read set (pr_iter_upload_lrset): the seeds
+    the last pr_seed_gpu_map left in HBM against the set's index (LongReadSet.index), the
+    set's reads and qualities as the consensus reference (bam2cns --ref)."""
+
+    def __init__(self, ctx, sr: Optional[np.ndarray], sr_off: np.ndarray, lr_off: np.ndarray):
+        """sr None: the seeding's device copy of the short reads; lr_off: the set's offsets."""
+        self.L = _abi.lib()
+        _setup(self.L)
+        self.ctx = ctx
+        self._sr_off = np.ascontiguousarray(sr_off, np.int64)
+        self._sr = None if sr is None else np.ascontiguousarray(sr, np.uint8)
+        b = sw.SwBatch()
+        b.n_sr = len(self._sr_off) - 1
+        b.sr_off = _abi.ptr(self._sr_off, C.c_int64)
+        b.sr_seq = _abi.ptr(self._sr, C.c_uint8)
+        self._b = b
+        _abi.check(self.L.pr_iter_upload_lrset(ctx.h, C.byref(b)), "pr_iter_upload_lrset")
+        self.d = SimpleNamespace(lr_off=np.ascontiguousarray(lr_off, np.int64))
+        nl, nt, bd = C.c_int32(), C.c_int64(), _abi.CnsBounds()
+        _abi.check(self.L.pr_iter_bounds(self.ctx.h, C.byref(nl), C.byref(nt), C.byref(bd)), "pr_iter_bounds")
+        self.n_lr, self.n_task, self.bounds = nl.value, nt.value, bd
+        self.out = None

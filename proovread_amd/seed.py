@@ -187,6 +187,13 @@ def _last_ms(fn, ctx) -> float:
     return v.value
 
 
+def _count(L, ctx) -> int:
+    """Seeds of the context's last pr_seed_gpu_map."""
+    n = C.c_int64()
+    _abi.check(L.pr_seed_gpu_seed_count(ctx.h, C.byref(n)), "pr_seed_gpu_seed_count")
+    return n.value
+
+
 def _phase_ms(L, ctx) -> dict:
     """Wave time per part of the last GPU seeding launch (ms summed over waves)."""
     t = np.zeros(4, np.uint64)

@@ -23,6 +23,56 @@ class OracleStages:
     def __init__(self, workers: int = 4):
         self.workers = workers
 
+    # -- the loop's stage interface (correct.GpuStages), the state held on the host
+    def load(self, reads):
+        self.ids, self.seqs, self.quals = list(reads.ids), list(reads.seqs), list(reads.quals)
+        self.map = list(self.seqs)
+
+    def task(self, task, sr, sr_off, params, bin_filter, comm=None, exact=False, mask_cfg=None):
+        from proovread_amd import correct, tasks as T
+        finish = mask_cfg is None
+        lr_map, lr_off = correct._pool(self.seqs if finish else self.map)   # finish: the unmasked reads
+        lr_map = correct.NT4[lr_map]
+        ref_seq, _ = correct._pool(self.seqs)
+        ref_qual, _ = correct._pool(self.quals)
+        mres = None
+        if not exact:
+            tk = correct._seed_tasks(lr_map, lr_off, sr, sr_off, T.options(task)[0], self.workers)
+            n_tasks = int(len(tk))
+            d = correct._seeds_dataset(lr_map, lr_off, sr, sr_off, tk)
+            out = self.iteration(d, ref_seq, ref_qual, task, params, bin_filter=bin_filter)
+            lo, hi = 0, len(self.ids)
+        else:
+            lo, hi, out, n_tasks, mres = self.owned_iteration(lr_map, lr_off, sr, sr_off, task, params, ref_seq,
+                                                              ref_qual, bin_filter, comm, mask_cfg)
+        seqs, quals, lines = [], [], []
+        for rid, (st, s, q, ch) in zip(self.ids[lo:hi], out):
+            if st != 0:
+                raise RuntimeError(f"{task}: consensus of {rid} failed with status {st}")
+            seqs.append(s)
+            quals.append(q)
+            lines += correct._rename(ch, rid)
+        masked, bpt, bpn = [], 0, 0
+        if mres is not None:
+            masked, bpt, bpn = mres
+        elif not finish and seqs:
+            masked, bpt, bpn = self.mask(seqs, quals, mask_cfg[0], mask_cfg[1])
+        if comm is not None and comm.world > 1:
+            seqs, quals = comm.allgather_lists(seqs), comm.allgather_lists(quals)
+            if not finish:
+                masked = comm.allgather_lists(masked)
+        self.seqs, self.quals = seqs, quals
+        if not finish:
+            self.map = masked
+        return correct.TaskOut(n_tasks, lines if finish else [], bpt, bpn)
+
+    def reads(self):
+        from proovread_amd import correct
+        return correct.LongReads(self.ids, self.seqs, self.quals)
+
+    def masked(self):
+        return list(self.map)
+
     def iteration(self, d, ref_seq, ref_qual, task, params, bin_filter=None):
         from proovread_amd import tasks as T
         o = T.options(task)[1]

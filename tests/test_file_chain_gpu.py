@@ -5,8 +5,8 @@
   (host seeding, pr_sw_run, SAM text, the -b/-l bin filter on the host), `samtools view
   -bS` and `samtools sort` (the BAM drop-ins), then `bam2cns --bam --ref` (BAM decode,
   pr_cns_run) writing the corrected .fq;
-* in process: the loop's device stages (correct.GpuStages: index and seeding in HBM,
-  pr_iter_* = bwa-mode SW, the -b/-l filter on the device, hand-off in coordinate order,
+* in process: the loop's device stages (correct.GpuStages: the read set resident in HBM,
+  index and seeding there, pr_iter_* = bwa-mode SW, the -b/-l filter on the device, hand-off in coordinate order,
   consensus) with no SAM/BAM in between.
 
 Inputs: the bundled sample's long reads (read-long's output: the stubby filter, upper case)
@@ -18,13 +18,12 @@ import io
 import sys
 from pathlib import Path
 
-import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "tests"))
 
-from proovread_amd import bam2cns, cns, correct, samtools, sw  # noqa: E402
+from proovread_amd import bam2cns, cns, correct, samtools  # noqa: E402
 from proovread_amd import bwa_proovread as bp  # noqa: E402
 from proovread_amd import tasks as T  # noqa: E402
 
@@ -70,18 +69,15 @@ def test_file_level_chain_equals_device_iteration(tmp_path):
                          "--max-ins-length", "0", "--qv-offset", "33", "--append"]) == 0
     got_file = _read_fq(pre + ".fq")
 
-    # ---- in process: the loop's device stages
-    lr_map, lr_off = reads.pool(reads.seqs)
-    lr_map = sw.NT4[lr_map]
+    # ---- in process: the loop's device stages (the read set resident in HBM)
     names, seqs, _ = bp.read_fastx(str(sr_fq))
     sr, sr_off = bp._pool(seqs)
     st = correct.GpuStages()
-    tk = st.seed(lr_map, lr_off, sr, sr_off, T.options(task)[0])
-    d = correct._seeds_dataset(lr_map, lr_off, sr, sr_off, tk)
-    ref_seq, _ = reads.pool(reads.seqs)
-    ref_qual, _ = reads.pool(reads.quals)
+    st.load(reads)
     params = cns.CnsParams(coverage=max_cov, use_ref_qual=True, detect_chimera=False, max_ins_length=0)
-    out = st.iteration(d, ref_seq, ref_qual, task, params, bin_filter=(bsz, blen))
+    st.task(task, sr, sr_off, params, (bsz, blen), mask_cfg=(correct.hcr_mask_for(task), 150))
+    got = st.reads()
+    out = [(0, s, q, []) for s, q in zip(got.seqs, got.quals)]   # pr_lrset_commit: every status 0
 
     assert len(got_file) > 0.9 * len(reads.ids)
     n_cmp = 0

@@ -63,8 +63,6 @@ def main():
           flush=True)
     cfg = correct.LoopConfig(coverage=50.0)
     stages = correct.GpuStages()
-    if len(sys.argv) > 3:
-        stages.debug_dir = sys.argv[3]
     prof = cProfile.Profile()
     t = time.perf_counter()
     prof.enable()
