@@ -101,6 +101,14 @@ int pr_comm_alltoallv_dev(pr_comm *c, const void *send, const int64_t *send_coun
 /* all-gather of DEVICE byte blocks: counts[world] (the same on every rank) = each rank's bytes;
  * rank r's block lands at recv + sum(counts[0..r)); asynchronous on the context stream */
 int pr_comm_allgatherv_dev(pr_comm *c, const void *send, const int64_t *counts, void *recv);
+/* An in-process group: `world` ranks as threads of one process, each with its own context
+ * (on one GPU or several), collectives through device copies in place of RCCL; every call
+ * above works on such a communicator (synchronously).  A single-GPU box runs the multi-rank
+ * paths with it (tests/test_local_group_gpu.py).  The group outlives its communicators. */
+typedef struct pr_comm_group pr_comm_group;
+int pr_comm_group_create(int world, pr_comm_group **out);
+void pr_comm_group_destroy(pr_comm_group *g);
+int pr_comm_init_local(pr_ctx *ctx, pr_comm_group *g, int rank, pr_comm **out);
 
 /* ------------------------------------------------------------------ */
 /* consensus stage                                                     */

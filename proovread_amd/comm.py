@@ -122,17 +122,7 @@ class RcclComm(_Base):
         from . import _abi
         self.L = _abi.lib()
         L = self.L
-        L.pr_comm_unique_id.argtypes = [C.c_char_p]
-        L.pr_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]
-        L.pr_comm_destroy.argtypes = [C.c_void_p]
-        L.pr_comm_allreduce_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
-        L.pr_comm_allreduce_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
-        L.pr_comm_barrier.argtypes = [C.c_void_p]
-        L.pr_comm_allgatherv_host.argtypes = [C.c_void_p, C.c_char_p, C.c_int64, C.c_void_p, C.c_int64,
-                                              C.POINTER(C.c_int64)]
-        L.pr_comm_alltoall_counts.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
-        L.pr_comm_alltoallv_host.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.c_void_p,
-                                             C.POINTER(C.c_int64)]
+        _setup(L)
         self.ctx, self.rank, self.world = ctx, rank, world
 
         def make_id() -> bytes:
@@ -206,6 +196,58 @@ class RcclComm(_Base):
         self._chk(self.L.pr_comm_alltoallv_host(self.h, send, sc.ctypes.data_as(P), out, rc.ctypes.data_as(P)),
                   "pr_comm_alltoallv_host")
         return out.raw[:int(rc.sum())]
+
+
+def _setup(L):
+    if getattr(L, "_comm_ready", False):
+        return
+    L.pr_comm_unique_id.argtypes = [C.c_char_p]
+    L.pr_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.POINTER(C.c_void_p)]
+    L.pr_comm_destroy.argtypes = [C.c_void_p]
+    L.pr_comm_allreduce_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
+    L.pr_comm_allreduce_host.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int]
+    L.pr_comm_barrier.argtypes = [C.c_void_p]
+    L.pr_comm_allgatherv_host.argtypes = [C.c_void_p, C.c_char_p, C.c_int64, C.c_void_p, C.c_int64,
+                                          C.POINTER(C.c_int64)]
+    L.pr_comm_alltoall_counts.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.pr_comm_alltoallv_host.argtypes = [C.c_void_p, C.c_char_p, C.POINTER(C.c_int64), C.c_void_p,
+                                         C.POINTER(C.c_int64)]
+    L.pr_comm_group_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    L.pr_comm_group_destroy.argtypes = [C.c_void_p]
+    L.pr_comm_init_local.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
+    L._comm_ready = True
+
+
+class LocalGroup:
+    """pr_comm_group: `world` ranks as threads of this process, one context each (include/prgpu.h
+    pr_comm_init_local) -- the multi-rank device paths on a single GPU."""
+
+    def __init__(self, world: int):
+        from . import _abi
+        self.L = _abi.lib()
+        _setup(self.L)
+        self.world = world
+        h = C.c_void_p()
+        _abi.check(self.L.pr_comm_group_create(world, C.byref(h)), "pr_comm_group_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.pr_comm_group_destroy(self.h)
+            self.h = None
+
+
+class LocalComm(RcclComm):
+    """A rank of a LocalGroup: the RcclComm interface over the in-process group's collectives."""
+
+    def __init__(self, ctx, group: LocalGroup, rank: int):
+        from . import _abi
+        self.L = _abi.lib()
+        _setup(self.L)
+        self.ctx, self.rank, self.world = ctx, rank, group.world
+        h = C.c_void_p()
+        _abi.check(self.L.pr_comm_init_local(ctx.h, group.h, rank, C.byref(h)), "pr_comm_init_local")
+        self.h = h
 
 
 # ---------------------------------------------------------------------------- torch (CPU tests)

@@ -293,8 +293,8 @@ class GpuStages:
             opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
         lr_off = self.lrs.offsets()
         world, rank = (comm.world, comm.rank) if comm is not None else (1, 0)
-        if world > 1 and not isinstance(comm, RcclComm):
-            raise TypeError("the device stages exchange over RCCL (comm.RcclComm)")
+        if comm is not None and not isinstance(comm, RcclComm):
+            raise TypeError("the device stages exchange over libprgpu's communicator (comm.RcclComm / LocalComm)")
         n_sr = len(sr_off) - 1
         if not exact:
             seed._map_gpu(L, self.ctx, sr, sr_off, seed_opts, False, keep_on_device=True)
@@ -308,7 +308,7 @@ class GpuStages:
             seed._map_gpu(L, self.ctx, sr[a0:a1], np.asarray(sr_off[s:e + 1]) - a0, seed_opts, False,
                           keep_on_device=True)
             iteration.ShardSW(self.ctx, sr, sr_off, s, e, None, lr_off, device_pools=True).launch(opts)
-            iteration.exchange(self.ctx, comm if world > 1 else None, s, bounds)
+            iteration.exchange(self.ctx, comm, s, bounds)
             it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, None, None, sr if world > 1 else None, sr_off,
                                           from_set=True)
         n_tasks = seed._count(L, self.ctx)
@@ -324,7 +324,7 @@ class GpuStages:
             buf.close()
             out.bpt, out.bpn = int(st[0]), int(st[1])
         self.device_ms += sum(it.timing())
-        self.lrs.commit(comm if world > 1 else None, with_mask=not finish)
+        self.lrs.commit(comm if exact else None, with_mask=not finish)
         return out
 
     def reads(self) -> LongReads:
@@ -377,7 +377,7 @@ def _rename(lines: List[str], rid: str) -> List[str]:
 # and bpt/bpN all-reduced so every rank takes the same mask_shortcut decision (the north
 # star's per-iteration statistics gather).  GPU ranks use comm.RcclComm (RCCL inside
 # libprgpu); the CPU tests use comm.TorchComm (gloo) with the oracle stages.
-from .comm import RcclComm, TorchComm  # noqa: E402
+from .comm import LocalComm, LocalGroup, RcclComm, TorchComm  # noqa: E402,F401
 Comm = TorchComm
 
 
@@ -431,7 +431,7 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         multi = comm is not None and comm.world > 1
         if finish and cfg.keep_masked:
             last_masked = stages.masked()
-        r = stages.task(task, sr, sr_off, params, binf, comm if multi else None, multi or cfg.exact_layout,
+        r = stages.task(task, sr, sr_off, params, binf, comm, multi or cfg.exact_layout,
                         None if finish else (hcr_mask_for(task), min_sr)) if ids else TaskOut(0, [])
         ent.n_tasks = r.n_tasks
         lines, bpt, bpn = r.chim, r.bpt, r.bpn

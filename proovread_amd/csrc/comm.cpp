@@ -13,7 +13,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -26,9 +28,41 @@ int pr_set_error(int code, const char *msg);
 static_assert(PR_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 constexpr int64_t P2P_PIECE = (int64_t)1 << 28;   // bytes per ncclSend / ncclRecv
 
+// An in-process group: the ranks are threads of one process, each with its own context (on
+// one GPU or several).  The collectives meet at a barrier, publish their buffers and copy
+// from each other's (device to device); they are synchronous.  The multi-rank code above the
+// communicator (pr_aln_exchange, pr_lrset_commit, the loop) runs unchanged on it, so a
+// single-GPU box exercises the world > 1 paths that RCCL runs across GPUs.
+struct pr_comm_group {
+    int world = 1;
+    std::mutex m;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    struct Slot {
+        const void *send = nullptr;
+        const int64_t *counts = nullptr;
+        int64_t n = 0;
+        std::vector<uint8_t> host;
+    };
+    std::vector<Slot> slot;
+    void barrier() {
+        std::unique_lock<std::mutex> l(m);
+        const uint64_t g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(l, [&] { return gen != g; });
+        }
+    }
+};
+
 struct pr_comm {
     pr_ctx *ctx = nullptr;
     ncclComm_t nc = nullptr;
+    pr_comm_group *grp = nullptr;   // in-process group (pr_comm_init_local) instead of RCCL
     int rank = 0, world = 1;
     void *stage = nullptr;   // device staging buffer for host-buffer collectives
     size_t stage_cap = 0;
@@ -100,11 +134,112 @@ extern "C" int pr_comm_init(pr_ctx *ctx, int world, int rank, const uint8_t *id,
     return 0;
 }
 
+extern "C" int pr_comm_group_create(int world, pr_comm_group **out) {
+    if (!out || world < 1) return pr_set_error(PR_ERR_ARG, "bad arg");
+    pr_comm_group *g = new pr_comm_group();
+    g->world = world;
+    g->slot.resize((size_t)world);
+    *out = g;
+    return 0;
+}
+
+extern "C" void pr_comm_group_destroy(pr_comm_group *g) { delete g; }
+
+extern "C" int pr_comm_init_local(pr_ctx *ctx, pr_comm_group *g, int rank, pr_comm **out) {
+    if (!ctx || !g || !out) return pr_set_error(PR_ERR_ARG, "null arg");
+    if (rank < 0 || rank >= g->world) return pr_set_error(PR_ERR_ARG, "bad rank");
+    pr_comm *c = new pr_comm();
+    c->ctx = ctx;
+    c->grp = g;
+    c->rank = rank;
+    c->world = g->world;
+    *out = c;
+    return 0;
+}
+
+// the in-process group's collectives (synchronous: each rank's stream is drained first)
+static int local_sync(pr_comm *c) {
+    HIPCHK(hipSetDevice(ctx_device(c->ctx)));
+    HIPCHK(hipStreamSynchronize(ctx_stream(c->ctx)));
+    return 0;
+}
+
+template <class T> static void reduce_into(T *acc, const T *v, int64_t n, int op) {
+    for (int64_t i = 0; i < n; ++i)
+        acc[i] = op == PR_RED_MAX ? std::max(acc[i], v[i]) : (op == PR_RED_MIN ? std::min(acc[i], v[i]) : acc[i] + v[i]);
+}
+
+static int local_allreduce_host(pr_comm *c, void *buf, int64_t n, int dtype, int op) {
+    size_t sz;
+    (void)dtype_of(dtype, &sz);
+    pr_comm_group *g = c->grp;
+    g->slot[(size_t)c->rank].send = buf;
+    g->barrier();
+    std::vector<uint8_t> acc((size_t)n * sz);
+    if (n) std::memcpy(acc.data(), g->slot[0].send, acc.size());
+    for (int r = 1; r < c->world; ++r) {
+        const void *v = g->slot[(size_t)r].send;
+        if (dtype == PR_DT_I64) reduce_into((int64_t *)acc.data(), (const int64_t *)v, n, op);
+        else if (dtype == PR_DT_F64) reduce_into((double *)acc.data(), (const double *)v, n, op);
+        else if (dtype == PR_DT_I32) reduce_into((int32_t *)acc.data(), (const int32_t *)v, n, op);
+        else reduce_into(acc.data(), (const uint8_t *)v, n, op);
+    }
+    g->barrier();   // every rank has read every buffer
+    if (n) std::memcpy(buf, acc.data(), acc.size());
+    return 0;
+}
+
+static int local_allreduce_dev(pr_comm *c, const void *dev_in, void *dev_out, int64_t n, int dtype, int op) {
+    size_t sz;
+    (void)dtype_of(dtype, &sz);
+    int rc = local_sync(c);
+    if (rc) return rc;
+    std::vector<uint8_t> h((size_t)n * sz + 1);
+    if (n) HIPCHK(hipMemcpy(h.data(), dev_in, (size_t)n * sz, hipMemcpyDeviceToHost));
+    if ((rc = local_allreduce_host(c, h.data(), n, dtype, op))) return rc;
+    if (n) HIPCHK(hipMemcpy(dev_out, h.data(), (size_t)n * sz, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// rank me pulls block `me` of every rank's send buffer (alltoallv: the rank's counts say where
+// it sits) or the whole send buffer (allgatherv: counts = nullptr)
+static int local_pull(pr_comm *c, const void *send, const int64_t *send_counts, int64_t my_bytes, void *recv,
+                      const int64_t *recv_counts) {
+    int rc = local_sync(c);
+    if (rc) return rc;
+    pr_comm_group *g = c->grp;
+    auto &me = g->slot[(size_t)c->rank];
+    me.send = send;
+    me.counts = send_counts;
+    me.n = my_bytes;
+    g->barrier();
+    int64_t o = 0;
+    for (int r = 0; r < c->world && !rc; ++r) {
+        const auto &p = g->slot[(size_t)r];
+        int64_t off = 0, n = p.n;
+        if (p.counts) {
+            for (int k = 0; k < c->rank; ++k) off += p.counts[k];
+            n = p.counts[c->rank];
+        }
+        if (n != recv_counts[r]) {
+            rc = pr_set_error(PR_ERR_ARG, "all-to-all: block size differs from the receive count");
+            break;
+        }
+        if (n && hipMemcpyAsync((uint8_t *)recv + o, (const uint8_t *)p.send + off, (size_t)n, hipMemcpyDefault,
+                                ctx_stream(c->ctx)) != hipSuccess)
+            rc = pr_set_error(PR_ERR_HIP, "in-process all-to-all copy failed");
+        o += n;
+    }
+    if (!rc && hipStreamSynchronize(ctx_stream(c->ctx)) != hipSuccess) rc = pr_set_error(PR_ERR_HIP, "stream sync");
+    g->barrier();   // every rank has finished reading the send buffers (always reached)
+    return rc;
+}
+
 extern "C" void pr_comm_destroy(pr_comm *c) {
     if (!c) return;
     (void)hipSetDevice(ctx_device(c->ctx));
     (void)hipStreamSynchronize(ctx_stream(c->ctx));
-    if (c->nc) (void)ncclCommDestroy(c->nc);
+    if (c->nc) (void)ncclCommDestroy(c->nc);   // (an in-process group is the caller's: pr_comm_group_destroy)
     if (c->stage) (void)hipFree(c->stage);
     delete c;
 }
@@ -114,6 +249,7 @@ extern "C" int pr_comm_allreduce_dev(pr_comm *c, const void *dev_in, void *dev_o
     size_t sz;
     const ncclDataType_t t = dtype_of(dtype, &sz);
     const ncclRedOp_t o = op == PR_RED_MAX ? ncclMax : (op == PR_RED_MIN ? ncclMin : ncclSum);
+    if (c->grp) return local_allreduce_dev(c, dev_in, dev_out, n, dtype, op);
     HIPCHK(hipSetDevice(ctx_device(c->ctx)));
     NCCLCHK(ncclAllReduce(dev_in, dev_out, (size_t)n, t, o, c->nc, ctx_stream(c->ctx)));
     return 0;
@@ -124,6 +260,7 @@ extern "C" int pr_comm_allreduce_host(pr_comm *c, void *buf, int64_t n, int dtyp
     size_t sz;
     (void)dtype_of(dtype, &sz);
     const size_t bytes = (size_t)n * sz;
+    if (c->grp) return local_allreduce_host(c, buf, n, dtype, op);
     int rc = stage(c, bytes);
     if (rc) return rc;
     hipStream_t s = ctx_stream(c->ctx);
@@ -158,6 +295,16 @@ extern "C" int pr_comm_allgatherv_host(pr_comm *c, const uint8_t *send, int64_t 
     }
     if (!recv) return 0;   // size query
     if (tot > recv_cap) return pr_set_error(PR_ERR_CAPACITY, "all-gather receive buffer too small");
+    if (c->grp) {   // in-process: host blocks read directly
+        pr_comm_group *g = c->grp;
+        g->slot[(size_t)c->rank].send = send;
+        g->barrier();
+        int64_t o = 0;
+        for (int r = 0; r < W; o += sz[(size_t)r], ++r)
+            if (sz[(size_t)r]) std::memcpy(recv + o, g->slot[(size_t)r].send, (size_t)sz[(size_t)r]);
+        g->barrier();
+        return 0;
+    }
     // in pieces of at most P2P_PIECE bytes per rank (one staging area of world + 1 pieces)
     const int64_t piece = std::min<int64_t>((cap + 255) & ~(int64_t)255, P2P_PIECE);
     if ((rc = stage(c, (size_t)piece * (size_t)(W + 1)))) return rc;
@@ -222,6 +369,7 @@ extern "C" int pr_comm_alltoallv_dev(pr_comm *c, const void *send, const int64_t
         rt += recv_counts[r];
     }
     if ((st && !send) || (rt && !recv)) return pr_set_error(PR_ERR_ARG, "null buffer");
+    if (c->grp) return local_pull(c, send, send_counts, 0, recv, recv_counts);
     hipStream_t s = ctx_stream(c->ctx);
     HIPCHK(hipSetDevice(ctx_device(c->ctx)));
     const uint8_t *ds = (const uint8_t *)send;
@@ -263,6 +411,7 @@ extern "C" int pr_comm_allgatherv_dev(pr_comm *c, const void *send, const int64_
         o[(size_t)r + 1] = o[(size_t)r] + counts[r];
     }
     if ((counts[me] && !send) || (o[(size_t)W] && !recv)) return pr_set_error(PR_ERR_ARG, "null buffer");
+    if (c->grp) return local_pull(c, send, nullptr, counts[me], recv, counts);
     hipStream_t s = ctx_stream(c->ctx);
     HIPCHK(hipSetDevice(ctx_device(c->ctx)));
     uint8_t *dr = (uint8_t *)recv;
