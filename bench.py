@@ -253,7 +253,7 @@ def main():
         sr_all, sr_off_all, s0 = gather_pool(cm, d.sr_seq, d.sr_off)
         gather_s = time.perf_counter() - t
     if args.seeds == "gpu":
-        d, seed_info = seed_front_end(ctx, want_host_copy=rank == 0 and world == 1, lr_seq=lr_all, lr_off=lr_off_all)
+        d, seed_info = seed_front_end(ctx, want_host_copy=want_cpu, lr_seq=lr_all, lr_off=lr_off_all)
         if want_cpu:   # the same GPU-made seeds, CPU chain in a child process
             cpu, cpu_res = cpu_baseline(d, args.cpu_lrs_per_worker)
     t_up = time.perf_counter()

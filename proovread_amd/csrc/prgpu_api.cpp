@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdarg>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -49,23 +50,68 @@ extern "C" const char *pr_last_error(void) { return g_err.c_str(); }
 extern "C" const char *pr_version(void) { return "prgpu 0.1.0 (gfx950)"; }
 
 // ---------------------------------------------------------------------------
+// device memory of the library's buffers (all contexts of the process), and PRGPU_MEM_TRACE=1:
+// every growth to stderr with the buffer's group and index (sizing at scale)
+std::atomic<int64_t> g_dev_bytes{0};
+static bool mem_trace() {
+    static const bool on = [] { const char *e = std::getenv("PRGPU_MEM_TRACE"); return e && *e && *e != '0'; }();
+    return on;
+}
+void prgpu_mem_note(const char *grp, int id, int64_t delta) {
+    const int64_t tot = g_dev_bytes.fetch_add(delta) + delta;
+    if (mem_trace() && delta > 0)
+        std::fprintf(stderr, "[prgpu mem] %s[%d] +%.1f MB -> %.2f GB\n", grp, id, delta / 1e6, tot / 1e9);
+}
+int prgpu_oom(const char *grp, int id, size_t want) {
+    size_t fr = 0, total = 0;
+    (void)hipMemGetInfo(&fr, &total);
+    (void)hipGetLastError();
+    return set_error(PR_ERR_HIP, "hipMalloc(%zu) failed (%s[%d]; the library holds %.2f GB, device free %.2f of %.2f GB)",
+                     want, grp, id, g_dev_bytes.load() / 1e9, fr / 1e9, total / 1e9);
+}
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
+    const char *grp = "buf";
+    int id = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return 0;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
+        release();
         size_t want = bytes + 64;   // slack: kernels read whole dwords at the end of byte pools
-        if (hipMalloc(&p, want) != hipSuccess) return set_error(PR_ERR_HIP, "hipMalloc(%zu) failed", want);
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            return prgpu_oom(grp, id, want);
+        }
         cap = want;
+        prgpu_mem_note(grp, id, (int64_t)want);
         return 0;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)hipFree(p);
+            prgpu_mem_note(grp, id, -(int64_t)cap);
+        }
         p = nullptr;
         cap = 0;
+    }
+    // grow to `bytes` keeping the first `used` bytes (stream-ordered copy, then synchronised)
+    int grow_keep(size_t bytes, size_t used, hipStream_t s) {
+        if (bytes <= cap && p) return 0;
+        void *np = nullptr;
+        const size_t want = bytes + bytes / 4 + 64;
+        if (hipMalloc(&np, want) != hipSuccess) return prgpu_oom(grp, id, want);
+        if (p && used) {
+            if (hipMemcpyAsync(np, p, used, hipMemcpyDeviceToDevice, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+                (void)hipFree(np);
+                return set_error(PR_ERR_HIP, "device copy failed (%s[%d] growth)", grp, id);
+            }
+        }
+        release();
+        p = np;
+        cap = want;
+        prgpu_mem_note(grp, id, (int64_t)want);
+        return 0;
     }
     template <class T>
     T *as() const { return reinterpret_cast<T *>(p); }
@@ -175,6 +221,15 @@ extern "C" int pr_ctx_create(int device, pr_ctx **out) {
         return set_error(PR_ERR_HIP, "device %d is %s, libprgpu is built for gfx950", device, prop.gcnArchName);
     pr_ctx *c = new pr_ctx();
     c->device = device;
+    auto tag = [](DevBuf *b, int n, const char *g) {
+        for (int i = 0; i < n; ++i) b[i].grp = g, b[i].id = i;
+    };
+    tag(c->cb, CB_COUNT, "cns");
+    tag(c->pb, 12, "pipe");
+    tag(c->mb, MB_COUNT, "mask");
+    tag(c->sd, SD_COUNT, "seed");
+    tag(c->xb, XB_COUNT, "xchg");
+    tag(c->ls, LS_COUNT, "lrset");
     c->n_cu = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
@@ -524,8 +579,8 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
 }
 
 template <class T>
-static int download(T *h, const DevBuf &d, size_t n, hipStream_t s) {
-    if (h && n) HIPCHK(hipMemcpyAsync(h, d.p, n * sizeof(T), hipMemcpyDeviceToHost, s));
+static int download(T *h, const DevBuf &d, size_t n, hipStream_t s, size_t first = 0) {   // elements [first, first + n)
+    if (h && n) HIPCHK(hipMemcpyAsync(h, d.as<T>() + first, n * sizeof(T), hipMemcpyDeviceToHost, s));
     return 0;
 }
 
@@ -1859,17 +1914,24 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     int64_t lanes2 = (int64_t)c->n_cu * seed_slots_per_cu();
     const int64_t scratch = std::max<int64_t>(waves * 64 * K.stride, lanes2 * seedc::scratch_bytes(caps));
     const int64_t nb = n_sr ? sr_off[n_sr] : 0;
+    // reads are mapped in chunks whose output slabs (caps.out seeds per read) fit a budget
+    // (PRGPU_SEED_OUT_MB, default 8 GB; configs[1]'s 460k reads are one chunk); every chunk's
+    // seeds are compacted into the dense list before the next chunk reuses the slab
+    const int64_t slot_bytes = (int64_t)caps.out * (int64_t)sizeof(pr_seed_task);
+    const char *ob = getenv("PRGPU_SEED_OUT_MB");
+    const int64_t out_budget = (ob ? std::max<int64_t>(1, atoll(ob)) : 8192) << 20;
+    const int64_t chunk = std::max<int64_t>(64, out_budget / slot_bytes / 64 * 64);
     int rc;
     c->seed_sr_bases = nb;
     if ((rc = upload(D[SB_SEQ], sr_seq, (size_t)nb, s)) || (rc = upload(D[SB_OFF], sr_off, (size_t)n_sr + 1, s)) ||
         (rc = D[SB_SCRATCH].ensure((size_t)scratch)) ||
-        (rc = D[SB_OUT].ensure((size_t)n_sr * caps.out * sizeof(pr_seed_task) + 16)) ||
+        (rc = D[SB_OUT].ensure((size_t)(std::min<int64_t>(chunk, n_sr) * slot_bytes + 16))) ||
         (rc = D[SB_NOUT].ensure((size_t)n_sr * 4 + 16)) || (rc = D[SB_STATUS].ensure((size_t)n_sr * 4 + 16)) ||
-        (rc = D[SB_NEXT].ensure(128)) || (rc = D[SB_PRE].ensure(((size_t)n_sr + 1) * 8)))
+        (rc = D[SB_NEXT].ensure(128)) || (rc = D[SB_PRE].ensure(((size_t)n_sr + 1) * 8)) ||
+        (rc = D[SB_DENSE].ensure(sizeof(pr_seed_task))))
         return rc;
     K.sr_seq = D[SB_SEQ].as<uint8_t>();
     K.sr_off = D[SB_OFF].as<int64_t>();
-    K.scratch = D[SB_SCRATCH].as<uint8_t>();
     K.out = D[SB_OUT].as<pr_seed_task>();
     K.n_out = D[SB_NOUT].as<int32_t>();
     K.status = D[SB_STATUS].as<int32_t>();
@@ -1877,19 +1939,35 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     K.prof = reinterpret_cast<unsigned long long *>(D[SB_NEXT].as<uint8_t>() + 64);
     HIPCHK(hipMemsetAsync(K.next, 0, 128, s));
     HIPCHK(hipEventRecord(c->ev[8], s));
-    int e = seed_batch_launch(K, (void *)s);
-    if (e) return set_error(PR_ERR_HIP, "seed kernel: %s", hipGetErrorString((hipError_t)e));
-    HIPCHK(hipEventRecord(c->ev[10], s));
-    {
-        std::vector<int32_t> st1((size_t)n_sr);
-        if ((rc = download(st1.data(), D[SB_STATUS], (size_t)n_sr, s))) return rc;
+    c->seed_pass2 = 0;
+    c->seed_pass3 = 0;
+    std::vector<int32_t> nout((size_t)n_sr), st((size_t)n_sr);
+    std::vector<int64_t> pre((size_t)n_sr + 1, 0);
+    int64_t total = 0, bad = 0;
+    int32_t bad_flags = 0;
+    for (int64_t r0 = 0; r0 < n_sr; r0 += chunk) {
+        const int64_t r1 = std::min<int64_t>(n_sr, r0 + chunk);
+        K.caps = small;
+        K.stride = seedc::scratch_bytes(small);
+        K.n_lanes = waves;
+        K.scratch = D[SB_SCRATCH].as<uint8_t>();
+        K.rlist = nullptr;
+        K.n_list = 0;
+        K.out0 = r0;
+        K.n_sr = r1;
+        const int32_t start = (int32_t)r0;
+        HIPCHK(hipMemcpyAsync(K.next, &start, 4, hipMemcpyHostToDevice, s));
+        int e = seed_batch_launch(K, (void *)s);
+        if (e) return set_error(PR_ERR_HIP, "seed kernel: %s", hipGetErrorString((hipError_t)e));
+        if (r0 == 0) HIPCHK(hipEventRecord(c->ev[10], s));
+        std::vector<int32_t> st1((size_t)(r1 - r0));
+        if ((rc = download(st1.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0))) return rc;
         HIPCHK(hipStreamSynchronize(s));
         std::vector<int32_t> redo;
-        for (int i = 0; i < n_sr; ++i)
-            if (st1[(size_t)i]) redo.push_back(i);
-        c->seed_pass2 = (int64_t)redo.size();
-        c->seed_pass3 = 0;
-        if (!redo.empty()) {   // pass 2 over the flagged reads (rlist in SB_PRE, rewritten later)
+        for (int64_t i = r0; i < r1; ++i)
+            if (st1[(size_t)(i - r0)]) redo.push_back((int32_t)i);
+        c->seed_pass2 += (int64_t)redo.size();
+        if (!redo.empty()) {   // pass 2 over the flagged reads (rlist in SB_PRE)
             HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
             HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
             K.caps = caps;
@@ -1905,13 +1983,13 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
             // hits per read) again, with the arrays that overflowed grown, up to 4 times
             seedc::Caps cg = caps;
             for (int pass = 3; pass <= 6; ++pass) {
-                std::vector<int32_t> st2((size_t)n_sr);
-                if ((rc = download(st2.data(), D[SB_STATUS], (size_t)n_sr, s))) return rc;
+                std::vector<int32_t> st2((size_t)(r1 - r0));
+                if ((rc = download(st2.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0))) return rc;
                 HIPCHK(hipStreamSynchronize(s));
                 std::vector<int32_t> again;
                 int32_t fl = 0;
                 for (int32_t i : redo)
-                    if (st2[(size_t)i]) again.push_back(i), fl |= st2[(size_t)i];
+                    if (st2[(size_t)(i - r0)]) again.push_back(i), fl |= st2[(size_t)(i - r0)];
                 if (again.empty() || (fl & (seedc::SC_OVER_LEN | seedc::SC_OVER_OUT))) break;
                 if (fl & seedc::SC_OVER_HITS) cg.hits *= 4;
                 if (fl & seedc::SC_OVER_IV) cg.iv *= 2;
@@ -1933,15 +2011,33 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
                 c->seed_pass3 += (int64_t)redo.size();
             }
         }
+        // the chunk's seeds: compacted on the device (read order) behind the earlier chunks'
+        if ((rc = download(nout.data() + r0, D[SB_NOUT], (size_t)(r1 - r0), s, (size_t)r0)) ||
+            (rc = download(st.data() + r0, D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0)))
+            return rc;
+        HIPCHK(hipStreamSynchronize(s));
+        const int64_t t0 = total;
+        for (int64_t i = r0; i < r1; ++i) {
+            if (nout[(size_t)i] < 0 || nout[(size_t)i] > caps.out) return set_error(PR_ERR_HIP, "seed kernel: bad task count");
+            total += nout[(size_t)i];
+            pre[(size_t)i + 1] = total;
+            bad += st[(size_t)i] != 0;
+            bad_flags |= st[(size_t)i];
+        }
+        if ((rc = upload(D[SB_PRE], pre.data() + r0, (size_t)(r1 - r0 + 1), s)) ||
+            (rc = D[SB_DENSE].grow_keep(sizeof(pr_seed_task) * (size_t)(total > 0 ? total : 1),
+                                        sizeof(pr_seed_task) * (size_t)t0, s)))
+            return rc;
+        const int e2 = seed_compact_launch(D[SB_OUT].as<pr_seed_task>(), D[SB_NOUT].as<int32_t>() + r0,
+                                           D[SB_PRE].as<int64_t>(), r1 - r0, caps.out, D[SB_DENSE].as<pr_seed_task>(),
+                                           (void *)s);
+        if (e2) return set_error(PR_ERR_HIP, "seed compaction: %s", hipGetErrorString((hipError_t)e2));
     }
     HIPCHK(hipEventRecord(c->ev[9], s));
-    std::vector<int32_t> nout((size_t)n_sr), st((size_t)n_sr);
-    if ((rc = download(nout.data(), D[SB_NOUT], (size_t)n_sr, s)) || (rc = download(st.data(), D[SB_STATUS], (size_t)n_sr, s)))
-        return rc;
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0.f;
     if (n_sr && hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_seed = ms;
-    c->ms_seed_pass2 = 0.f;
+    c->ms_seed_pass2 = 0.f;   // (the passes after the first chunk's pass 1; one chunk at configs[1])
     if (n_sr && hipEventElapsedTime(&ms, c->ev[10], c->ev[9]) == hipSuccess) c->ms_seed_pass2 = ms;
     if (getenv("PRGPU_SEED_DEBUG") && K.prof) {   // pass 1's lane phase split (lane-summed ticks)
         unsigned long long t8[8] = {};
@@ -1949,23 +2045,6 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
             fprintf(stderr, "[seed] pass-1 lane ms (summed over lanes): smems %.1f chaining %.1f filter+out %.1f\n",
                     t8[4] / 1e5, t8[5] / 1e5, t8[6] / 1e5);
     }
-    int64_t total = 0, bad = 0;
-    int32_t bad_flags = 0;
-    for (int i = 0; i < n_sr; ++i) {
-        if (nout[i] < 0 || nout[i] > caps.out) return set_error(PR_ERR_HIP, "seed kernel: bad task count");
-        total += nout[i];
-        bad += st[i] != 0;
-        bad_flags |= st[i];
-    }
-    // compact on the device (read order), download the dense list
-    std::vector<int64_t> pre((size_t)n_sr + 1, 0);
-    for (int i = 0; i < n_sr; ++i) pre[(size_t)i + 1] = pre[(size_t)i] + nout[i];
-    if ((rc = upload(D[SB_PRE], pre.data(), (size_t)n_sr + 1, s)) ||
-        (rc = D[SB_DENSE].ensure(sizeof(pr_seed_task) * (size_t)(total > 0 ? total : 1))))
-        return rc;
-    const int e2 = seed_compact_launch(D[SB_OUT].as<pr_seed_task>(), D[SB_NOUT].as<int32_t>(), D[SB_PRE].as<int64_t>(),
-                                       n_sr, caps.out, D[SB_DENSE].as<pr_seed_task>(), (void *)s);
-    if (e2) return set_error(PR_ERR_HIP, "seed compaction: %s", hipGetErrorString((hipError_t)e2));
     // an incomplete seed set (flagged reads have no seeds) is never handed to
     // pr_iter_upload_gpu_seeds: it refuses when seed_pre does not match the reads
     if (bad) c->seed_pre.clear();

@@ -733,8 +733,12 @@ extern "C" int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opt
     nt = nt < 1 ? 1 : (nt > 64 ? 64 : nt);
     std::vector<ReadOut> res(n_sr);
     std::atomic<int> next{0};
+    // PRGPU_SCRATCH_FILL=<byte>: the slabs start filled with that byte instead of zeros -- device
+    // scratch is never cleared, so a result that depends on the fill is a read of stale scratch
+    const char *fe = getenv("PRGPU_SCRATCH_FILL");
+    const uint64_t fill = fe ? 0x0101010101010101ull * (uint64_t)(strtoul(fe, nullptr, 0) & 0xFF) : 0;
     auto work = [&]() {
-        std::vector<uint64_t> slab((size_t)(bytes / 8 + 1));
+        std::vector<uint64_t> slab((size_t)(bytes / 8 + 1), fill);
         seedc::Scratch S = seedc::carve(reinterpret_cast<uint8_t *>(slab.data()), caps);
         std::vector<pr_seed_task> buf((size_t)caps.out);
         std::vector<uint64_t> big;
@@ -752,7 +756,7 @@ extern "C" int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opt
                 if (err & seedc::SC_OVER_MEMS) cg.mems *= 2;
                 if (err & seedc::SC_OVER_SEEDS) cg.seeds *= 2;
                 if (err & seedc::SC_OVER_CHAINS) cg.chains *= 2;
-                big.assign((size_t)(seedc::scratch_bytes(cg) / 8 + 1), 0);
+                big.assign((size_t)(seedc::scratch_bytes(cg) / 8 + 1), fill);
                 seedc::Scratch G = seedc::carve(reinterpret_cast<uint8_t *>(big.data()), cg);
                 err = seedc::map_read(V, *o, G, sr_seq + sr_off[i], len, i, buf.data(), caps.out, &n);
             }

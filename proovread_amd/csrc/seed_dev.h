@@ -22,7 +22,8 @@ struct SeedDev {
                                // (pass 1: the whole lane-per-read phase), chaining and filter +
                                // output of pass 2 (may be null)
     seedc::Caps caps;
-    pr_seed_task *out;         // [n_sr * caps.out]
+    pr_seed_task *out;         // [(reads of the chunk) * caps.out]: read i's slots at (i - out0) * caps.out
+    int64_t out0;              // first read of the chunk (pass 1 maps reads [*next, n_sr) at entry)
     int32_t *n_out;            // [n_sr]
     int32_t *status;           // [n_sr] 0 or SC_OVER_* bits
     const int32_t *rlist;      // pass 2: the reads to map (n_list of them); null: 0 .. n_list

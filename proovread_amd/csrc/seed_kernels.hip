@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
             int n = 0;
             if (D.prof) pt[0] += wall_clock64() - t0;
             if (len > 0 && !err)
-                err = seedc::map_after_occ(D.V, D.O, S, q, len, i, D.out + (int64_t)i * D.caps.out, D.caps.out, &n,
+                err = seedc::map_after_occ(D.V, D.O, S, q, len, i, D.out + (int64_t)(i - D.out0) * D.caps.out, D.caps.out, &n,
                                            D.prof ? pt + 1 : nullptr, lcnt);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
@@ -242,7 +242,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             seedc::Scratch S = seedc::carve(base + (int64_t)lane * D.stride, D.caps);
             int n = 0, err = my_err;
             if (len > 0 && !err)
-                err = seedc::map_after_occ(D.V, D.O, S, D.sr_seq + o, len, i, D.out + (int64_t)i * D.caps.out,
+                err = seedc::map_after_occ(D.V, D.O, S, D.sr_seq + o, len, i, D.out + (int64_t)(i - D.out0) * D.caps.out,
                                            D.caps.out, &n, D.prof ? lt : nullptr, lcnt);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;

@@ -60,6 +60,9 @@ enum AlnBuf {
 };
 static_assert(SB_NBUF <= 80, "SwResident buffer table");
 
+void prgpu_mem_note(const char *grp, int id, int64_t delta);
+int prgpu_oom(const char *grp, int id, size_t want);
+
 namespace prgpu {
 void sw_release(SwResident &r) {
     for (void *&e : r.ext_ev.ev)
@@ -70,7 +73,7 @@ void sw_release(SwResident &r) {
         if (e) (void)hipEventDestroy((hipEvent_t)e), e = nullptr;
     r.side = nullptr;
     for (int i = 0; i < 80; ++i) {
-        if (r.buf[i]) (void)hipFree(r.buf[i]);
+        if (r.buf[i]) (void)hipFree(r.buf[i]), prgpu_mem_note("sw", i, -(int64_t)r.cap[i]);
         r.buf[i] = nullptr;
         r.cap[i] = 0;
     }
@@ -78,14 +81,19 @@ void sw_release(SwResident &r) {
 }
 }  // namespace prgpu
 
+
 static int ensure(SwResident &r, int id, size_t bytes) {
     if (r.buf[id] && r.cap[id] >= bytes) return 0;
-    if (r.buf[id]) (void)hipFree(r.buf[id]);
+    if (r.buf[id]) (void)hipFree(r.buf[id]), prgpu_mem_note("sw", id, -(int64_t)r.cap[id]);
     r.buf[id] = nullptr;
     r.cap[id] = 0;
     const size_t want = bytes + 64;   // slack: kernels read whole dwords at the end of byte pools
-    if (hipMalloc(&r.buf[id], want) != hipSuccess) return pr_set_error(PR_ERR_HIP, "hipMalloc failed (SW)");
+    if (hipMalloc(&r.buf[id], want) != hipSuccess) {
+        r.buf[id] = nullptr;
+        return prgpu_oom("sw", id, want);
+    }
     r.cap[id] = want;
+    prgpu_mem_note("sw", id, (int64_t)want);
     return 0;
 }
 template <class T>
@@ -513,10 +521,11 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         const size_t need = (size_t)(r.cig_slots + (int64_t)sp[1]) * 4;
         if (need > r.cap[SB_CIG]) {   // grow the pool, keeping the slots
             void *np = nullptr;
-            if (hipMalloc(&np, need + need / 8) != hipSuccess) return pr_set_error(PR_ERR_HIP, "hipMalloc failed (CIGAR spill)");
+            if (hipMalloc(&np, need + need / 8) != hipSuccess) return prgpu_oom("sw CIGAR spill", SB_CIG, need + need / 8);
             HIPCHK(hipMemcpyAsync(np, r.buf[SB_CIG], (size_t)r.cig_slots * 4, hipMemcpyDeviceToDevice, s));
             HIPCHK(hipStreamSynchronize(s));
             (void)hipFree(r.buf[SB_CIG]);
+            prgpu_mem_note("sw", SB_CIG, (int64_t)(need + need / 8) - (int64_t)r.cap[SB_CIG]);
             r.buf[SB_CIG] = np;
             r.cap[SB_CIG] = need + need / 8;
             D.o_cig = (uint32_t *)np;
@@ -657,10 +666,11 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
         const size_t need = (size_t)(r.cig_slots + (int64_t)sp[1]) * 4;
         if (need > r.cap[SB_CIG]) {   // grow the pool, keeping the slots
             void *np = nullptr;
-            if (hipMalloc(&np, need + need / 8) != hipSuccess) return pr_set_error(PR_ERR_HIP, "hipMalloc failed (CIGAR spill)");
+            if (hipMalloc(&np, need + need / 8) != hipSuccess) return prgpu_oom("sw CIGAR spill", SB_CIG, need + need / 8);
             HIPCHK(hipMemcpyAsync(np, r.buf[SB_CIG], (size_t)r.cig_slots * 4, hipMemcpyDeviceToDevice, s));
             HIPCHK(hipStreamSynchronize(s));
             (void)hipFree(r.buf[SB_CIG]);
+            prgpu_mem_note("sw", SB_CIG, (int64_t)(need + need / 8) - (int64_t)r.cap[SB_CIG]);
             r.buf[SB_CIG] = np;
             r.cap[SB_CIG] = need + need / 8;
             D.o_cig = (uint32_t *)np;

@@ -49,6 +49,22 @@ def test_device_caps_core_matches_host_path(finish):
     assert len(host) > 2 * n
 
 
+def test_device_caps_core_reads_no_stale_scratch(monkeypatch):
+    """Device scratch is never cleared between reads: the core's result must not depend on what
+    the slab held before (PRGPU_SCRATCH_FILL poisons the host emulation's slabs)."""
+    d, ss, so = _data(12)
+    ss, so = ss[:so[2000]], so[:2001]
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    for finish in (False, True):
+        o = seed.default_opts(finish)
+        want, wst = ix.map_device_caps(ss, so, o, threads=4)
+        for fill in ("0xFF", "0xA5"):
+            monkeypatch.setenv("PRGPU_SCRATCH_FILL", fill)
+            got, st = ix.map_device_caps(ss, so, o, threads=4)
+            monkeypatch.delenv("PRGPU_SCRATCH_FILL")
+            assert np.array_equal(st, wst) and np.array_equal(got, want), fill
+
+
 def test_device_caps_flags_long_reads():
     d, _, _ = _data()
     ix = seed.SeedIndex(d.lr_seq, d.lr_off)
@@ -76,6 +92,27 @@ def test_gpu_seeding_matches_device_caps_on_host():
         assert np.array_equal(st, wst)
         assert np.array_equal(got, want)
     assert ix.gpu_ms() > 0
+
+
+@pytest.mark.gpu
+def test_gpu_seeding_in_output_chunks(monkeypatch):
+    """Reads mapped in chunks of bounded output slabs (PRGPU_SEED_OUT_MB; 1 MB = 64 reads per
+    chunk here, 94 chunks) give the one-chunk run's seeds and flags exactly, kept on the device
+    (seed count) and downloaded."""
+    from proovread_amd import _abi
+    d, ss, so = _data(12)
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    ctx = _abi.default_context()
+    ix.to_gpu(ctx)
+    o = seed.default_opts(False)
+    want, wst = ix.map_gpu(ss, so, o, allow_flagged=True)
+    monkeypatch.setenv("PRGPU_SEED_OUT_MB", "1")
+    got, st = ix.map_gpu(ss, so, o, allow_flagged=True)
+    assert np.array_equal(st, wst)
+    assert np.array_equal(got, want)
+    if not wst.any():
+        seed._map_gpu(ix.L, ctx, ss, so, o, False, keep_on_device=True)
+        assert seed._count(ix.L, ctx) == len(want)
 
 
 def _oracle_data():
