@@ -20,6 +20,7 @@ override -w 100, `--coverage 100` with sr-coverage 50: cap 0.75 * 50 = 37.5
 bwa-sr-finish (-D .75, chimera detection, no reference qualities).
 configs[1] (C2) scaled to a tenth: the bench's own workload generator, options and path.
 """
+import dataclasses
 import sys
 from pathlib import Path
 
@@ -128,3 +129,62 @@ def test_configs1_scaled_shard_bench_path_matches_oracle_chain():
     n_aln, _, frac = _check(d, False, 40, 15.0 * 0.75, bench.BIN_FILTER, "20,41,80,130,60,0.7", 150)
     assert n_aln > 100_000
     assert 0.0 < frac < 1.0
+
+
+def test_configs4_finish_on_iterated_full_error_reads():
+    """configs[4] at full error through two tasks: a 1 Mb genome, 1,200 x 25 kb long reads at
+    20 % error (30x long-read coverage), 50x short reads, w = 100.  bwa-sr-1 (cap 37.5, -l
+    1000, the reads' own qualities) corrects every read on the device; bwa-sr-finish then maps
+    to those corrected reads (-D .75, chimera detection, no reference qualities, cap
+    0.75 * 30 = 22.5, -l 600): at 30x every 12-mer of a near-exact read hits ~30 copies, so
+    seeding runs its later passes.  GPU seeding = host seeding over every read of both tasks;
+    the consensus (sequence, quality, trace, chimera lines) = the oracle chain on a spread
+    sample of long reads (the oracle chain is exact for the long reads it is asked about)."""
+    import cpu_chain
+    from proovread_amd import _abi, seed, synth
+    NT4 = np.full(256, 4, np.uint8)
+    for i, c in enumerate(b"ACGT"):
+        NT4[c] = NT4[c + 32] = i
+    d = synth.simulate(20261015 + 44, 1_000_000, 1_200, 25_000, 50.0, p_ins=0.05, p_del=0.08, p_sub=0.07,
+                       sr_frac=1.0)
+    ctx = _abi.default_context()
+    sample = list(range(0, d.n_lr, d.n_lr // 6))[:6]
+
+    def oracle(dd, finish, cap, binf):
+        hx = seed.SeedIndex(dd.lr_seq, dd.lr_off)
+        sop = seed.default_opts(finish)
+        sop.w = 100
+        want_tasks = hx.map(dd.sr_seq, dd.sr_off, sop, threads=16)
+        hx.close()
+        so = ob.sw_opts("bwa-sr-finish" if finish else "bwa-sr")
+        so.w = 100
+        swt = (so.a, so.b, so.o_del, so.o_ins, so.e_del, so.e_ins, so.w, so.pen_clip5, so.pen_clip3, so.zdrop,
+               so.min_score_per_base)
+        _, _, want, _ = cpu_chain.run_sample(synth.with_seeds(dd, want_tasks), sample, task=swt, coverage=cap,
+                                             use_ref_qual=not finish, detect_chimera=finish, workers=16, full=True,
+                                             bin_filter=binf, drop_ratio=0.75 if finish else 0.0)
+        return want_tasks, want
+
+    def check(dd, finish, cap, binf):
+        it, tasks, _, _ = _product_iteration(ctx, dd, finish, 100, cap, binf, not finish, finish,
+                                             "20,41,80,130,60,0.7", 150)
+        want_tasks, want = oracle(dd, finish, cap, binf)
+        assert np.array_equal(tasks, want_tasks), "GPU seeding != host seeding path"
+        got = it.results()
+        assert all(g.status == 0 for g in got)
+        for k, i in enumerate(sample):
+            rc, fq, trace, ch = want[k]
+            assert rc == 0, i
+            assert got[i].fastq == fq, i
+            assert got[i].trace == trace, i
+            assert "".join(l + "\n" for l in got[i].chim_lines()) == ch, i
+        return got, len(tasks)
+
+    got1, n1 = check(d, False, 37.5, (20, 1000.0))
+    seqs = [np.frombuffer(g.seq.encode("latin-1"), np.uint8) for g in got1]
+    off = np.zeros(d.n_lr + 1, np.int64)
+    np.cumsum([len(s) for s in seqs], out=off[1:])
+    d2 = dataclasses.replace(d, lr_seq=NT4[np.concatenate(seqs)], lr_off=off)
+    got2, n2 = check(d2, True, 22.5, (20, 600.0))
+    # the finish task sees corrected reads: the per-read seed load grows with the near-exact matches
+    assert n2 > 0 and n1 > 0
