@@ -170,6 +170,224 @@ __global__ void __launch_bounds__(SW_WAVE) sw_ext_phase_kernel(SwDev D, SwOptsDe
     }
 }
 
+// ksw_extend2 (oracle/sw_oracle.c osw_extend) for ONE task per wave: the row's band
+// [beg, end) -- at most XW_COLS * 64 columns, 2w+1 <= 192 -- spread over the lanes (column
+// beg + lane + 64 r), the DP row eh in the wave's LDS area (h | e << 16 per column, as
+// ext_row_lane).  ksw's horizontal recurrence f(j+1) = max(f(j) - e_ins, max(M(j) - oe_ins, 0))
+// with f(beg) = 0 is F(j) = max_{beg <= k < j} (t(k) + k e_ins) - (j - 1) e_ins (t >= 0 makes the
+// f(beg) term lose), an exclusive prefix max over the band; H(i, j-1) for eh[j].h is the left
+// neighbour's h; the row maximum (last column on ties), the band pruning (first / last
+// non-zero eh) and the z-drop are wave reductions / ballots.  The w = 80 band retries ran one
+// task per LANE (sw_ext_phase_kernel<80>): ~300 rows x 161 cells in one dependent chain per
+// lane, ~1.5 ms per launch whatever the number of retried tasks.
+constexpr int XW_COLS = 3;
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int t = __shfl_xor(v, o, 64);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+// inclusive prefix max over the wave's lanes
+__device__ __forceinline__ int wave_scan_max_i32(int v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int t = __shfl_up(v, d, 64);
+        if (lane >= d) v = t > v ? t : v;
+    }
+    return v;
+}
+
+__device__ int ext_wave(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen, const uint8_t *Lr, long tb, int ts,
+                        bool comp, int tlen, const SwOptsDev &O, int w, int end_bonus, int h0, int lane, ExtIO &io) {
+    const int a = O.a, b = O.b, o_del = O.o_del, e_del = O.e_del, o_ins = O.o_ins, e_ins = O.e_ins;
+    const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
+    {   // row -1 (ksw's first row) and the band cap by the longest possible gap (max entry = a)
+        const int hj1 = h0 > oe_ins ? h0 - oe_ins : 0;
+        for (int j = lane; j <= qlen + 1; j += 64) {
+            int h = j == 0 ? h0 : (j <= qlen ? hj1 - e_ins * (j - 1) : 0);
+            eh[j] = (uint32_t)(h > 0 ? h : 0);
+        }
+        int max_ins = (int)((double)(qlen * a + end_bonus - o_ins) / e_ins + 1.);
+        max_ins = max_ins > 1 ? max_ins : 1;
+        w = w < max_ins ? w : max_ins;
+        int max_del = (int)((double)(qlen * a + end_bonus - o_del) / e_del + 1.);
+        max_del = max_del > 1 ? max_del : 1;
+        w = w < max_del ? w : max_del;
+    }
+    __builtin_amdgcn_wave_barrier();
+    int max = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
+    int beg = 0, end = qlen;
+    for (int i = 0; i < tlen; ++i) {
+        int tc = (int)Lr[tb + (long)ts * i];
+        if (comp && tc < 4) tc = 3 - tc;
+        if (beg < i - w) beg = i - w;
+        if (end > i + w + 1) end = i + w + 1;
+        if (end > qlen) end = qlen;
+        int h1 = 0;
+        if (beg == 0) {
+            h1 = h0 - (o_del + e_del * (i + 1));
+            if (h1 < 0) h1 = 0;
+        }
+        const int nr = end > beg ? (end - beg + 63) >> 6 : 0;   // lane blocks of the band (uniform)
+        int M[XW_COLS], E[XW_COLS], H[XW_COLS];
+        int carry = INT32_MIN;   // prefix max of A over the earlier blocks
+        int key = 0;             // row maximum: h << 10 | (j - beg + 1), last column on ties
+        int hprev_blk = h1;      // h of the column left of the block's lane 0 (h1 before the band)
+        uint32_t nzb[XW_COLS];
+#pragma unroll
+        for (int r = 0; r < XW_COLS; ++r) {
+            M[r] = E[r] = H[r] = 0;
+            nzb[r] = 0u;
+            if (r >= nr) continue;
+            const int j = beg + lane + 64 * r;
+            const bool in = j < end;
+            int Mv = 0, e = 0, A = INT32_MIN;
+            if (in) {
+                const uint32_t p = eh[j];
+                const int hp = (int)(p & 0xFFFFu);
+                e = (int)(p >> 16);
+                Mv = hp ? hp + sw_score(tc, (int)Q[qb + qs * j], a, b) : 0;
+                const int t = Mv - oe_ins > 0 ? Mv - oe_ins : 0;
+                A = t + j * e_ins;
+            }
+            // F(j) = exclusive prefix max of A - (j - 1) e_ins, F(beg) = 0
+            const int inc = wave_scan_max_i32(A, lane);
+            int exl = __shfl_up(inc, 1, 64);
+            if (lane == 0) exl = INT32_MIN;
+            exl = exl > carry ? exl : carry;
+            carry = __shfl(inc, 63, 64) > carry ? __shfl(inc, 63, 64) : carry;
+            const int F = exl == INT32_MIN ? 0 : exl - (j - 1) * e_ins;
+            int h = Mv > e ? Mv : e;
+            h = h > F ? h : F;
+            int tn = Mv - oe_del > 0 ? Mv - oe_del : 0;
+            const int en = e - e_del > tn ? e - e_del : tn;
+            M[r] = Mv;
+            E[r] = in ? en : 0;
+            H[r] = in ? h : 0;
+            if (in) {
+                const int kk = (h << 10) | (j - beg + 1);
+                key = kk > key ? kk : key;
+            }
+        }
+        // the new row: eh[j] = H(i, j-1) | E(i+1, j) << 16 for j in [beg, end), eh[end] = h1'
+        int hlast = h1;   // H(i, end-1), or h1 when the band is empty
+#pragma unroll
+        for (int r = 0; r < XW_COLS; ++r) {
+            if (r >= nr) continue;
+            const int j = beg + lane + 64 * r;
+            int left = __shfl_up(H[r], 1, 64);
+            const int prev63 = __shfl(hprev_blk, 63, 64);   // (lane 63's value of the previous block)
+            if (lane == 0) left = r == 0 ? h1 : prev63;
+            hprev_blk = H[r];
+            if (j < end) {
+                const uint32_t nw = (uint32_t)left | ((uint32_t)E[r] << 16);
+                eh[j] = nw;
+                nzb[r] = nw != 0u ? 1u : 0u;
+            }
+            const int jl = end - 1;   // the band's last column
+            if (jl >= beg + 64 * r && jl < beg + 64 * (r + 1)) hlast = __shfl(H[r], jl - beg - 64 * r, 64);
+        }
+        if (lane == 0) eh[end] = (uint32_t)hlast;   // e = 0
+        __builtin_amdgcn_wave_barrier();
+        const int jend = beg < end ? end : beg;
+        if (jend == qlen) {
+            max_ie = gscore > hlast ? max_ie : i;
+            gscore = gscore > hlast ? gscore : hlast;
+        }
+        key = wave_max_i32(key);
+        const int mm = key >> 10;
+        if (mm == 0) break;
+        const int mj = beg + (key & 1023) - 1;
+        if (mm > max) {
+            max = mm, max_i = i, max_j = mj;
+            const int d = mj - i > 0 ? mj - i : i - mj;
+            max_off = max_off > d ? max_off : d;
+        } else if (O.zdrop > 0) {
+            if (i - max_i > mj - max_j) {
+                if (max - mm - ((i - max_i) - (mj - max_j)) * e_del > O.zdrop) break;
+            } else {
+                if (max - mm - ((mj - max_j) - (i - max_i)) * e_ins > O.zdrop) break;
+            }
+        }
+        // band pruning: beg = first non-zero eh in [beg, end) (else end); end = last non-zero in
+        // [beg', end] + 2 (capped), eh[end] = {hlast, 0} included
+        int nb = end, ne = -1;
+#pragma unroll
+        for (int r = 0; r < XW_COLS; ++r) {
+            if (r >= nr) continue;
+            const uint64_t m = __ballot(nzb[r] != 0u);
+            if (m) {
+                const int f0 = beg + 64 * r + __builtin_ctzll(m);
+                const int l0 = beg + 64 * r + 63 - __builtin_clzll(m);
+                nb = nb < f0 ? nb : f0;
+                ne = ne > l0 ? ne : l0;
+            }
+        }
+        if (hlast != 0) ne = end;
+        beg = nb;
+        const int jj = ne >= beg ? ne : beg - 1;
+        end = jj + 2 < qlen ? jj + 2 : qlen;
+    }
+    io.qle = max_j + 1;
+    io.tle = max_i + 1;
+    io.gtle = max_ie + 1;
+    io.gscore = gscore;
+    io.max_off = max_off;
+    return max;
+}
+
+// One extension phase with one task per wave (ext_wave): the w = 80 band retries.  LDS: one
+// DP row of qmax + 2 words per wave.
+__global__ void __launch_bounds__(256) sw_ext_wave_kernel(SwDev D, SwOptsDev O, int side, int tryi) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    uint32_t *eh = lds_w + wv * (D.qmax + 2);
+    const int n = D.list_n[0];
+    for (int64_t k = (int64_t)blockIdx.x * nwv + wv; k < n; k += (int64_t)gridDim.x * nwv) {
+        const int64_t t = D.list[k];
+        const TaskGeo g = task_geo(D, O, t);
+        int qb, qs, qlen, tlen, ts, end_bonus, h0;
+        long tb;
+        if (side == 0) {
+            qb = g.qbeg - 1; qs = -1; qlen = g.qbeg;
+            tlen = (int)(g.rbeg - g.rmax0);
+            tb = g.rev ? (long)g.L - g.rbeg : (long)g.rbeg - 1;
+            ts = g.rev ? 1 : -1;
+            end_bonus = O.pen_clip5;
+            h0 = g.slen * O.a;
+        } else {
+            const int qe0 = g.qbeg + g.slen;
+            const int re0 = (int)(g.rbeg + g.slen - g.rmax0);
+            qb = qe0; qs = 1; qlen = g.lq - qe0;
+            tlen = (int)(g.rmax1 - g.rmax0 - re0);
+            tb = g.rev ? (long)g.L - 1 - g.rbeg - g.slen : (long)g.rbeg + g.slen;
+            ts = g.rev ? -1 : 1;
+            end_bonus = O.pen_clip3;
+            h0 = D.o_score[t];   // left result (sc0)
+        }
+        ExtIO io;
+        const int aw = O.w << tryi;
+        const int score = ext_wave(eh, g.Q, qb, qs, qlen, g.Lr, tb, ts, g.rev, tlen, O, aw, end_bonus, h0, lane, io);
+        if (lane == 0) {
+            xref(D, side, XF_SCORE, t) = score;
+            xref(D, side, XF_QLE, t) = io.qle;
+            xref(D, side, XF_TLE, t) = io.tle;
+            xref(D, side, XF_GTLE, t) = io.gtle;
+            xref(D, side, XF_GSCORE, t) = io.gscore;
+            xref(D, side, XF_MAXOFF, t) = io.max_off;
+            if (tryi == 0) {
+                const int prev = side == 0 ? -1 : h0;
+                const bool stop = score == prev || io.max_off < (aw >> 1) + (aw >> 2);
+                D.x_try[t] = (uint8_t)(D.x_try[t] | (stop ? 0 : (1 << side)));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // ksw_extend2 (oracle/sw_oracle.c osw_extend, upstream ksw.c) for one lane with the DP row
 // in memory: eh[j * SW_WAVE] = H(i-1, j-1) | E(i, j) << 16 (both >= 0 and < 2^15 in an
 // extension: a * query length + h0 <= 10000).  The band of any width; the wide-band
@@ -1283,7 +1501,12 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
             if (wb <= 32) hipLaunchKernelGGL(sw_ext_phase_kernel<32>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
             else if (wb <= 40) hipLaunchKernelGGL(sw_ext_phase_kernel<40>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
             else if (wb <= 64) hipLaunchKernelGGL(sw_ext_phase_kernel<64>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
-            else if (wb <= 80) hipLaunchKernelGGL(sw_ext_phase_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
+            else if (wb <= 80 && (2 * wb + 1 > XW_COLS * 64 || getenv("PRGPU_EXT80_LANE")))   // one task per lane
+                hipLaunchKernelGGL(sw_ext_phase_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
+            else if (wb <= 80) {   // one task per wave (ext_wave)
+                const int lds = 4 * (D.qmax + 2) * 4;
+                hipLaunchKernelGGL(sw_ext_wave_kernel, dim3(grid_waves), dim3(256), lds, s, D, O, side, tryi);
+            }
             else if (D.eh_g) hipLaunchKernelGGL(sw_ext_wide_kernel<true>, dim3(D.eh_g_blocks), dim3(SW_WAVE), 0, s, D, O, side, tryi);
             else {
                 const int lds = (D.qmax + 2) * SW_WAVE * 4;
