@@ -1883,10 +1883,10 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     DevBuf *D = c->sd;
-    seedc::Caps caps = seedc::device_caps();
-    caps.hi = c->seed_view.ksplit != nullptr;   // text beyond 2^32: positions carry bit 32
     int qmax = 1;
     for (int i = 0; i < n_sr; ++i) qmax = std::max<int>(qmax, (int)(sr_off[i + 1] - sr_off[i]));
+    seedc::Caps caps = seedc::device_caps(qmax);
+    caps.hi = c->seed_view.ksplit != nullptr;   // text beyond 2^32: positions carry bit 32
     // pass 1: 64 reads per wave, small slices sized for the batch; pass 2 (flagged reads): the
     // large slices, one wave per read
     seedc::Caps small = seedc::device_caps_small(std::min(qmax, caps.lmax));
@@ -1909,6 +1909,10 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     if (getenv("PRGPU_SEED_BALANCE")) {
         const int64_t rounds = (nbatch + waves - 1) / waves;
         waves = (nbatch + rounds - 1) / rounds;
+    }
+    {   // pass 1's slices within a scratch budget (long mr reads: fewer waves, ~24 GB)
+        const int64_t wmax = std::max<int64_t>(c->n_cu, ((int64_t)24 << 30) / (64 * K.stride));
+        if (waves > wmax) waves = wmax;
     }
     K.n_lanes = waves;
     int64_t lanes2 = (int64_t)c->n_cu * seed_slots_per_cu();

@@ -726,7 +726,9 @@ extern "C" int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opt
     out->n = 0;
     out->t = nullptr;
     const seedc::IndexView V = view_of(h->I);
-    seedc::Caps caps = seedc::device_caps();
+    int qmax = 1;
+    for (int i = 0; i < n_sr; ++i) qmax = std::max<int>(qmax, (int)(sr_off[i + 1] - sr_off[i]));
+    seedc::Caps caps = seedc::device_caps(qmax);   // (the output slots follow the longest read, as on the device)
     caps.hi = V.ksplit != nullptr;
     const int64_t bytes = seedc::scratch_bytes(caps);
     int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();

@@ -568,8 +568,11 @@ SC_HD int seed_flt_min_score(const pr_seed_opts &O, int len) {
 // around seed s against the reference around it, or -1 when the seed or a window reaches
 // MEM_SHORT_LEN (200) bases.  Windows: +- MEM_SHORT_EXT (50), clamped to [0, 2 l_pac) and to
 // the seed's strand half, then (bns_fetch_seq) to its long read.  H / E: 2 x 201 ints.
+// (H / E: rows of 201 values at a stride -- int32 on one thread, or int16 interleaved over
+// the lanes of a wave; every value is <= 5 x 200)
+template <class T>
 SC_HD int seed_sw_score(const IndexView &I, const pr_seed_opts &O, const uint8_t *q, int len, const Seed &s, int rid,
-                        int32_t *H, int32_t *E) {
+                        T *H, T *E, int stride = 1) {
     if (s.len >= 200) return -1;
     int qb = s.qbeg - 50, qe = s.qbeg + s.len + 50;
     qb = qb > 0 ? qb : 0;
@@ -593,7 +596,7 @@ SC_HD int seed_sw_score(const IndexView &I, const pr_seed_opts &O, const uint8_t
     const uint8_t *t = I.text + tc + (rb - fb);
     const int qn = qe - qb, tn = (int)(re - rb);
     const int oe_del = O.o_del + O.e_del, oe_ins = O.o_ins + O.e_ins;
-    for (int j = 0; j < qn; ++j) H[j] = 0, E[j] = 0;
+    for (int j = 0; j < qn; ++j) H[j * stride] = 0, E[j * stride] = 0;
     int best = 0;
     for (int i = 0; i < tn; ++i) {
         const int ti = t[i];
@@ -602,16 +605,16 @@ SC_HD int seed_sw_score(const IndexView &I, const pr_seed_opts &O, const uint8_t
             const int qj = q[qb + j];
             const int sc = (ti > 3 || qj > 3) ? -1 : (ti == qj ? O.a : -O.b);
             int h = hdiag + sc;
-            const int e = E[j];
+            const int e = E[j * stride];
             h = h > e ? h : e;
             h = h > f ? h : f;
             h = h > 0 ? h : 0;
-            hdiag = H[j];
-            H[j] = h;
+            hdiag = H[j * stride];
+            H[j * stride] = (T)h;
             best = best > h ? best : h;
             int en = e - O.e_del, eo = h - oe_del;
             en = en > eo ? en : eo;
-            E[j] = en > 0 ? en : 0;
+            E[j * stride] = (T)(en > 0 ? en : 0);
             int fn = f - O.e_ins, fo = h - oe_ins;
             fn = fn > fo ? fn : fo;
             f = fn > 0 ? fn : 0;
@@ -637,10 +640,10 @@ SC_HD int seed_sw_score(const IndexView &I, const pr_seed_opts &O, const uint8_t
 #else
 #define SC_TICK(k) do { (void)ticks; } while (0)
 #endif
-SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
-                        pr_seed_task *out, int cap_out, int *n_out, unsigned long long *ticks = nullptr,
-                        const uint32_t *lcnt = nullptr) {
-    *n_out = 0;
+// Part 1: SMEMs, chaining and mem_chain_flt; *n_chains = the chains in S.ch (kept flags set).
+SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int *n_chains,
+                     unsigned long long *ticks = nullptr, const uint32_t *lcnt = nullptr) {
+    *n_chains = 0;
     int err = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
     unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
@@ -815,8 +818,37 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
         for (int k = 0; k < nk; ++k)
             if (S.ch[S.kept[k]].first >= 0) S.ch[S.ch[S.kept[k]].first].kept = 1;
     }
-    // mem_flt_chained_seeds over the kept chains (long reads only; the occurrence table's
-    // per-start array `ge` is dead by now and holds the SW rows)
+    *n_chains = nch;
+    SC_TICK(2);   // (mem_chain_flt: with the filter + output part, as before the split)
+    return 0;
+}
+
+// The seeds whose mem_flt_chained_seeds score part 2 needs (every seed of every kept chain,
+// chain order) into list[0, return); -1 when they do not fit cap
+SC_HD int flt_seed_list(const Scratch &S, int nch, int32_t *list, int cap) {
+    int n = 0;
+    for (int ci = 0; ci < nch; ++ci) {
+        const Chain &c = S.ch[ci];
+        if (c.kept == 0) continue;
+        for (int32_t k = c.head; k >= 0; k = S.next[k]) {
+            if (n >= cap) return -1;
+            list[n++] = k;
+        }
+    }
+    return n;
+}
+
+// Part 2: mem_flt_chained_seeds over the kept chains (long reads only) and the tasks into
+// out[0, *n_out).  scores: the seeds' seed_sw_score by seed index when computed beforehand
+// (the device's one-wave-per-read pass scores them over all lanes), else null.
+SC_HD int map_output(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
+                     int nch, pr_seed_task *out, int cap_out, int *n_out, const int32_t *scores = nullptr,
+                     unsigned long long *ticks = nullptr) {
+    *n_out = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
+#endif
+    // (the occurrence table's per-start array `ge` is dead by now and holds the SW rows)
     const int flt = seed_flt_min_score(O, len);
     int32_t *swH = (int32_t *)S.ge, *swE = swH + 201;
     // mem_chain2aln's input: every seed of every kept chain with the chain's reference window,
@@ -838,7 +870,7 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
             const Seed &s = S.seeds[k];
             int score = s.len;
             if (flt >= 0) {
-                const int x = seed_sw_score(I, O, q, len, s, c.rid, swH, swE);
+                const int x = scores ? scores[k] : seed_sw_score(I, O, q, len, s, c.rid, swH, swE);
                 if (x >= 0 && x < flt) continue;   // dropped
                 score = x < 0 ? s.len * O.a : x;
             }
@@ -881,6 +913,17 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
     SC_TICK(2);
     return 0;
 }
+
+// Everything after the occurrence table: parts 1 and 2 on one thread.
+SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
+                        pr_seed_task *out, int cap_out, int *n_out, unsigned long long *ticks = nullptr,
+                        const uint32_t *lcnt = nullptr) {
+    *n_out = 0;
+    int nch = 0;
+    const int err = map_chains(I, O, S, q, len, &nch, ticks, lcnt);
+    if (err) return err;
+    return map_output(I, O, S, q, len, sid, nch, out, cap_out, n_out, nullptr, ticks);
+}
 #undef SC_TICK
 
 // The whole read: occurrence table, then map_after_occ.
@@ -904,11 +947,37 @@ struct Caps {
     int32_t lmax, hits, iv, mems, seeds, chains, out;
     int32_t hi;   // the text reaches beyond 2^32: the hit table carries bit 32 of the positions (hhi)
 };
-SC_HD Caps device_caps() { return Caps{1024, 8192, 256, 1024, 4096, 2048, 384, 0}; }
-// pass 1 of the device path: 64 slices per wave, sized for reads of <= lmax bases
+// output slots per read (the seeds of its kept chains): 384 for short reads, 2 per base for
+// the mr modes' 300-1000 bp reads (~300 seeds per 600 bp read at 15x long-read coverage)
+SC_HD int device_out_cap(int qmax) { return qmax > 192 ? 2 * ((qmax + 15) & ~15) : 384; }
+SC_HD Caps device_caps(int qmax = 0) {
+    Caps c{1024, 8192, 256, 1024, 4096, 2048, 384, 0};
+    c.out = device_out_cap(qmax);
+    if (qmax > 192) {   // pass 2 for mr reads: at least twice pass 1's room (device_caps_small)
+        const int l = (qmax + 15) & ~15;
+        c.hits = c.hits > 48 * l ? c.hits : 48 * l;
+        c.iv = c.iv > l / 2 ? c.iv : l / 2;
+        c.mems = c.mems > 2 * l ? c.mems : 2 * l;
+        c.seeds = c.seeds > 4 * l ? c.seeds : 4 * l;
+        c.chains = c.chains > 2 * l ? c.chains : 2 * l;
+    }
+    return c;
+}
+// pass 1 of the device path: 64 slices per wave, sized for reads of <= lmax bases.  Reads
+// beyond 160 bases (mr modes) get hit / interval / seed / chain room in proportion to their
+// length (a 600 bp read at 15x long-read coverage has ~9k hits), so they stay in the lane-per-read
+// pass instead of the one-wave-per-read pass 2; configs[1]'s 150 bp slices are unchanged.
 SC_HD Caps device_caps_small(int lmax) {
     const int l = lmax < 16 ? 16 : (lmax + 15) & ~15;
-    return Caps{l, 4096, 64, 512, 512, 384, 384, 0};   // ~0.1 % of configs[1]'s reads outgrow it (mems)
+    Caps c{l, 4096, 64, 512, 512, 384, device_out_cap(lmax), 0};   // ~0.1 % of configs[1]'s reads outgrow it (mems)
+    if (l > 160) {
+        c.hits = c.hits > 24 * l ? c.hits : 24 * l;
+        c.iv = c.iv > l / 4 ? c.iv : l / 4;
+        c.mems = c.mems > 2 * l ? c.mems : 2 * l;
+        c.seeds = c.seeds > 2 * l ? c.seeds : 2 * l;
+        c.chains = c.chains > l ? c.chains : l;
+    }
+    return c;
 }
 
 SC_HD int64_t align8(int64_t x) { return (x + 7) & ~(int64_t)7; }

@@ -174,12 +174,48 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
         const unsigned long long t0 = D.prof && lane == 0 ? wall_clock64() : 0ULL;
         if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
         if (len > 0 && !err) err = build_occ_wave(D.V, S, q, len, ho, lane);
+        // SMEMs and chaining on lane 0; then, for reads where bwa runs mem_flt_chained_seeds
+        // (>= 440 bp), the seeds' local SW scores over all 64 lanes (a seed per lane, the rows
+        // int16 and lane-interleaved in the dead count table); the output on lane 0
+        int nch = 0, nlist = -1;
+        if (lane == 0) {
+            if (D.prof) pt[0] += wall_clock64() - t0;
+            if (len > 0 && !err) {
+                err = seedc::map_chains(D.V, D.O, S, q, len, &nch, D.prof ? pt + 1 : nullptr, lcnt);
+                if (!err && seedc::seed_flt_min_score(D.O, len) >= 0 && 3 * S.cap_seeds <= S.cap_hits &&
+                    2 * 201 * 64 * 2 <= 4 * S.lmax * seedc::HB)
+                    nlist = seedc::flt_seed_list(S, nch, (int32_t *)S.hpos + S.cap_seeds, S.cap_seeds);
+            }
+        }
+        err = __shfl(err, 0, 64);
+        nlist = __shfl(nlist, 0, 64);
+        if (nlist > 0) {
+            __threadfence_block();
+            const int32_t *list = (const int32_t *)S.hpos + S.cap_seeds;
+            int32_t *rid = (int32_t *)S.hpos + 2 * S.cap_seeds;
+            if (lane == 0) {   // each listed seed's long read (its chain's)
+                int x = 0;
+                for (int ci = 0; ci < nch; ++ci) {
+                    const seedc::Chain &c = S.ch[ci];
+                    if (c.kept == 0) continue;
+                    for (int32_t k = c.head; k >= 0; k = S.next[k]) rid[x++] = c.rid;
+                }
+            }
+            __threadfence_block();
+            int32_t *scores = (int32_t *)S.hpos;
+            int16_t *H = (int16_t *)S.ge + lane, *E = H + 201 * 64;
+            for (int x = lane; x < nlist; x += 64) {
+                const int32_t k = list[x];
+                scores[k] = seedc::seed_sw_score(D.V, D.O, q, len, S.seeds[k], rid[x], H, E, 64);
+            }
+            __threadfence_block();
+        }
         if (lane == 0) {
             int n = 0;
-            if (D.prof) pt[0] += wall_clock64() - t0;
             if (len > 0 && !err)
-                err = seedc::map_after_occ(D.V, D.O, S, q, len, i, D.out + (int64_t)(i - D.out0) * D.caps.out, D.caps.out, &n,
-                                           D.prof ? pt + 1 : nullptr, lcnt);
+                err = seedc::map_output(D.V, D.O, S, q, len, i, nch, D.out + (int64_t)(i - D.out0) * D.caps.out,
+                                        D.caps.out, &n, nlist >= 0 ? (const int32_t *)S.hpos : nullptr,
+                                        D.prof ? pt + 1 : nullptr);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
         }

@@ -95,6 +95,27 @@ def test_gpu_seeding_matches_device_caps_on_host():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sr_len", [600, 950])
+def test_gpu_seeding_mr_reads_match_host_path(sr_len):
+    """The mr modes' long short reads (bwa-mr-1 options): mem_flt_chained_seeds' local SW runs
+    for every seed of every kept chain (>= 440 bp); the capacities follow the read length and
+    the one-wave-per-read pass scores the seeds over all lanes.  Every read is seeded (none
+    flagged) and the seeds equal the host path's."""
+    from proovread_amd import _abi, tasks as T
+    d = synth.simulate(20261017 + sr_len, 300_000, 900, 10_000, 15.0, sr_len=sr_len, sr_frac=1.0)
+    n = min(2500, d.n_sr)
+    ss, so = d.sr_seq[:d.sr_off[n]], d.sr_off[:n + 1]
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    ix.to_gpu(_abi.default_context())
+    o = T.options("bwa-mr-1")[0]
+    want = ix.map(ss, so, o, threads=8)
+    got, st = ix.map_gpu(ss, so, o, allow_flagged=True)
+    assert not st.any()
+    assert np.array_equal(got, want)
+    assert len(want) > 100 * n
+
+
+@pytest.mark.gpu
 def test_gpu_seeding_in_output_chunks(monkeypatch):
     """Reads mapped in chunks of bounded output slabs (PRGPU_SEED_OUT_MB; 1 MB = 64 reads per
     chunk here, 94 chunks) give the one-chunk run's seeds and flags exactly, kept on the device
