@@ -134,7 +134,7 @@ enum SeedBufId {
     SI_TEXT, SI_CSTART, SI_CBLK, SI_LROFF, SI_KOFF, SI_KPOS, SI_KEXT, SI_CNT0,
     SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SB_NEXT, SB_PRE, SB_DENSE,
     SX_LRSEQ, SX_KEY0, SX_KEY1, SX_VAL0, SX_KC, SX_CNTPTR, SX_TEMP, SI_KSPLIT, SX_VAL1, SX_KCC, SX_KOFFC, SX_KCUR,
-    SD_COUNT
+    SB_DP, SD_COUNT
 };
 // the exact-parity layout's exchange (pr_aln_exchange, owned batches): bounds, sort keys and
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
@@ -1915,6 +1915,13 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         if (waves > wmax) waves = wmax;
     }
     K.n_lanes = waves;
+    // mem_flt_chained_seeds' SW rows of pass 1 (reads >= 440 bp), lane-interleaved per wave
+    K.dp = nullptr;
+    if (seedc::seed_flt_min_score(*o, qmax) >= 0) {
+        int rc0 = D[SB_DP].ensure((size_t)waves * 2 * 201 * 64 * sizeof(int16_t));
+        if (rc0) return rc0;
+        K.dp = D[SB_DP].as<int16_t>();
+    }
     int64_t lanes2 = (int64_t)c->n_cu * seed_slots_per_cu();
     const int64_t scratch = std::max<int64_t>(waves * 64 * K.stride, lanes2 * seedc::scratch_bytes(caps));
     const int64_t nb = n_sr ? sr_off[n_sr] : 0;

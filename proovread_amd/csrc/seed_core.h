@@ -841,9 +841,12 @@ SC_HD int flt_seed_list(const Scratch &S, int nch, int32_t *list, int cap) {
 // Part 2: mem_flt_chained_seeds over the kept chains (long reads only) and the tasks into
 // out[0, *n_out).  scores: the seeds' seed_sw_score by seed index when computed beforehand
 // (the device's one-wave-per-read pass scores them over all lanes), else null.
+// dp16 (device, lane per read): the SW rows as int16 interleaved over the wave's lanes (dp16 =
+// the wave's area + lane, stride 64: the lanes' row accesses share cache lines), else the
+// int32 rows in `ge`.
 SC_HD int map_output(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
                      int nch, pr_seed_task *out, int cap_out, int *n_out, const int32_t *scores = nullptr,
-                     unsigned long long *ticks = nullptr) {
+                     unsigned long long *ticks = nullptr, int16_t *dp16 = nullptr) {
     *n_out = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
     unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
@@ -870,7 +873,9 @@ SC_HD int map_output(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
             const Seed &s = S.seeds[k];
             int score = s.len;
             if (flt >= 0) {
-                const int x = scores ? scores[k] : seed_sw_score(I, O, q, len, s, c.rid, swH, swE);
+                const int x = scores ? scores[k]
+                                     : (dp16 ? seed_sw_score(I, O, q, len, s, c.rid, dp16, dp16 + 201 * 64, 64)
+                                             : seed_sw_score(I, O, q, len, s, c.rid, swH, swE));
                 if (x >= 0 && x < flt) continue;   // dropped
                 score = x < 0 ? s.len * O.a : x;
             }
@@ -917,12 +922,12 @@ SC_HD int map_output(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
 // Everything after the occurrence table: parts 1 and 2 on one thread.
 SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
                         pr_seed_task *out, int cap_out, int *n_out, unsigned long long *ticks = nullptr,
-                        const uint32_t *lcnt = nullptr) {
+                        const uint32_t *lcnt = nullptr, int16_t *dp16 = nullptr) {
     *n_out = 0;
     int nch = 0;
     const int err = map_chains(I, O, S, q, len, &nch, ticks, lcnt);
     if (err) return err;
-    return map_output(I, O, S, q, len, sid, nch, out, cap_out, n_out, nullptr, ticks);
+    return map_output(I, O, S, q, len, sid, nch, out, cap_out, n_out, nullptr, ticks, dp16);
 }
 #undef SC_TICK
 

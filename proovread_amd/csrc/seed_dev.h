@@ -26,6 +26,7 @@ struct SeedDev {
     int64_t out0;              // first read of the chunk (pass 1 maps reads [*next, n_sr) at entry)
     int32_t *n_out;            // [n_sr]
     int32_t *status;           // [n_sr] 0 or SC_OVER_* bits
+    int16_t *dp;               // pass 1: per wave 2 x 201 x 64 int16 (mem_flt_chained_seeds rows, lane-interleaved)
     const int32_t *rlist;      // pass 2: the reads to map (n_list of them); null: 0 .. n_list
     int64_t n_list;
 };

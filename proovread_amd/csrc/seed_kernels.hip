@@ -279,7 +279,8 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             int n = 0, err = my_err;
             if (len > 0 && !err)
                 err = seedc::map_after_occ(D.V, D.O, S, D.sr_seq + o, len, i, D.out + (int64_t)(i - D.out0) * D.caps.out,
-                                           D.caps.out, &n, D.prof ? lt : nullptr, lcnt);
+                                           D.caps.out, &n, D.prof ? lt : nullptr, lcnt,
+                                           D.dp ? D.dp + slot * (2 * 201 * 64) + lane : nullptr);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
         }
