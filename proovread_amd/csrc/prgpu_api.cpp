@@ -134,7 +134,7 @@ enum SeedBufId {
     SI_TEXT, SI_CSTART, SI_CBLK, SI_LROFF, SI_KOFF, SI_KPOS, SI_KEXT, SI_CNT0,
     SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SB_NEXT, SB_PRE, SB_DENSE,
     SX_LRSEQ, SX_KEY0, SX_KEY1, SX_VAL0, SX_KC, SX_CNTPTR, SX_TEMP, SI_KSPLIT, SX_VAL1, SX_KCC, SX_KOFFC, SX_KCUR,
-    SB_DP, SD_COUNT
+    SB_DP, SI_TEXT4, SD_COUNT
 };
 // the exact-parity layout's exchange (pr_aln_exchange, owned batches): bounds, sort keys and
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
@@ -1660,6 +1660,16 @@ extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int with_mask) {
 
 // ---------------------------------------------------------------------------
 // seeding on the device (seed_kernels.hip over seed_core.h)
+// the index text 16 bases per word (IndexView.text4) for the occurrence table's match lengths
+static int seed_text4(pr_ctx *c, seedc::IndexView &v, hipStream_t s) {
+    int rc = c->sd[SI_TEXT4].ensure((size_t)ix_pack4_words(v.n_text) * 8);
+    if (rc) return rc;
+    const int e = ix_pack4_launch(v.text, v.n_text, c->sd[SI_TEXT4].as<uint64_t>(), s);
+    if (e) return set_error(PR_ERR_HIP, "text packing: %s", hipGetErrorString((hipError_t)e));
+    v.text4 = c->sd[SI_TEXT4].as<uint64_t>();
+    return 0;
+}
+
 extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
     if (!c || !h) return set_error(PR_ERR_ARG, "null arg");
     HIPCHK(hipSetDevice(c->device));
@@ -1687,6 +1697,7 @@ extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
     v.kpos = D[SI_KPOS].as<uint32_t>();
     v.kext = D[SI_KEXT].as<uint64_t>();
     v.ksplit = z.ksplit ? D[SI_KSPLIT].as<uint64_t>() : nullptr;
+    if ((rc = seed_text4(c, v, s))) return rc;
     HIPCHK(hipStreamSynchronize(s));
     c->seed_view = v;
     c->seed_loaded = true;
@@ -1808,6 +1819,7 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
     v.kext = B.kext;
     v.ksplit = B.ksplit;
     for (int j = 0; j < seedc::KI - 1; ++j) v.cnt[j] = B.cnt[j];
+    if ((rc = seed_text4(c, v, s))) return rc;
     c->seed_view = v;
     c->seed_loaded = true;
     c->seed_n_text = n_text;
@@ -1975,8 +1987,44 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         if ((rc = download(st1.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0))) return rc;
         HIPCHK(hipStreamSynchronize(s));
         std::vector<int32_t> redo;
+        int32_t fl1 = 0;
         for (int64_t i = r0; i < r1; ++i)
-            if (st1[(size_t)(i - r0)]) redo.push_back((int32_t)i);
+            if (st1[(size_t)(i - r0)]) redo.push_back((int32_t)i), fl1 |= st1[(size_t)(i - r0)];
+        // many flagged reads (the finish task maps to corrected reads at 30x long-read coverage:
+        // ~140 starts x 30 hits > 4096 for nearly every read): pass 1 again, lane per read, over
+        // them with the arrays that overflowed grown (within the scratch already allocated),
+        // instead of pass 2's one wave per read
+        if (redo.size() > 4096 && !(fl1 & (seedc::SC_OVER_LEN | seedc::SC_OVER_OUT))) {
+            seedc::Caps cb = small;
+            if (fl1 & seedc::SC_OVER_HITS) cb.hits *= 4;
+            if (fl1 & seedc::SC_OVER_IV) cb.iv *= 2;
+            if (fl1 & seedc::SC_OVER_MEMS) cb.mems *= 2;
+            if (fl1 & seedc::SC_OVER_SEEDS) cb.seeds *= 2;
+            if (fl1 & seedc::SC_OVER_CHAINS) cb.chains *= 2;
+            const int64_t sb = seedc::scratch_bytes(cb);
+            int64_t wb = std::min<int64_t>((int64_t)D[SB_SCRATCH].cap / (64 * sb), ((int64_t)redo.size() + 63) / 64);
+            wb = std::min<int64_t>(wb, waves);   // (the filter rows' area holds `waves` waves)
+            if (wb >= c->n_cu) {
+                K.caps = cb;
+                K.stride = sb;
+                K.n_lanes = wb;
+                K.rlist = D[SB_PRE].as<int32_t>();
+                K.n_list = (int64_t)redo.size();
+                HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
+                HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
+                e = seed_batch_launch(K, (void *)s);
+                if (e) return set_error(PR_ERR_HIP, "seed kernel (pass 1b): %s", hipGetErrorString((hipError_t)e));
+                std::vector<int32_t> st1b((size_t)(r1 - r0));
+                if ((rc = download(st1b.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0))) return rc;
+                HIPCHK(hipStreamSynchronize(s));
+                std::vector<int32_t> left;
+                for (int32_t i : redo)
+                    if (st1b[(size_t)(i - r0)]) left.push_back(i);
+                redo.swap(left);
+                K.rlist = nullptr;
+                K.n_list = 0;
+            }
+        }
         c->seed_pass2 += (int64_t)redo.size();
         if (!redo.empty()) {   // pass 2 over the flagged reads (rlist in SB_PRE)
             HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));

@@ -80,6 +80,7 @@ struct IndexView {
     const uint64_t *ksplit;    // [NK] first hit of k-mer `code` at or beyond POS_PAGE, or null
     const uint64_t *kext;      // per hit: KX bases after it (2 bits each) | count << 56
     const uint32_t *cnt[KI - 1];   // cnt[j-1][code]: occurrences of the j-mer `code`, j = 1..11
+    const uint64_t *text4;     // device: the text 16 bases per word (4 bits each) + a padding word, or null
 };
 
 struct Iv {

@@ -276,6 +276,28 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
     return 0;
 }
 
+// the text 16 bases per word, 4 bits each (base k of word w at bits 4k..4k+3; past the text: SEP),
+// for the device occurrence table's 16-base match-length comparisons
+__global__ void ix_pack4_kernel(const uint8_t *text, int64_t n_text, uint64_t *text4, int64_t n_words) {
+    for (int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t v = 0;
+        for (int k = 0; k < 16; ++k) {
+            const int64_t x = w * 16 + k;
+            const uint64_t c = x < n_text ? (uint64_t)text[x] : (uint64_t)SEP;
+            v |= c << (4 * k);
+        }
+        text4[w] = v;
+    }
+}
+int64_t ix_pack4_words(int64_t n_text) { return n_text / 16 + 2; }
+int ix_pack4_launch(const uint8_t *text, int64_t n_text, uint64_t *text4, hipStream_t s) {
+    const int64_t nw = ix_pack4_words(n_text);
+    int64_t blocks = (nw + 255) / 256;
+    blocks = blocks < (1 << 20) ? (blocks > 0 ? blocks : 1) : (1 << 20);
+    hipLaunchKernelGGL(ix_pack4_kernel, dim3((unsigned)blocks), dim3(256), 0, s, text, n_text, text4, nw);
+    return (int)hipGetLastError();
+}
+
 // bytes of rocPRIM temporary storage for sorts of `chunk` text positions
 size_t seed_index_temp_bytes(int64_t chunk) {
     size_t a = 0, b = 0, c = 0;

@@ -36,6 +36,9 @@ struct SeedIndexBuild {
 
 // enqueue the whole build on stream s; 0 or a hipError_t
 int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s);
+// the 4-bit packed copy of a device text (IndexView.text4): words needed, launch
+int64_t ix_pack4_words(int64_t n_text);
+int ix_pack4_launch(const uint8_t *text, int64_t n_text, uint64_t *text4, hipStream_t s);
 size_t seed_index_temp_bytes(int64_t chunk);
 
 }  // namespace prgpu

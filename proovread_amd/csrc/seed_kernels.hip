@@ -47,13 +47,32 @@ __device__ __forceinline__ void wave_sync_lds() {
 // length (LCP with the packed bases, then the text past them) and count it into the start's
 // match-length histogram; a per-start suffix sum makes the count table.  This is
 // build_occ's table without its diagonal shortcut (same match lengths).  -> 0 or SC_OVER_HITS.
+// 16 bases from base x of a 4-bit packed sequence (a padding word after the last)
+__device__ __forceinline__ uint64_t nib16(const uint64_t *w4, uint64_t x) {
+    const uint64_t w = x >> 4;
+    const int sh = (int)(x & 15) * 4;
+    const uint64_t lo = w4[w];
+    return sh ? (lo >> sh) | (w4[w + 1] << (64 - sh)) : lo;
+}
+
 __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, const uint8_t *q, int len, int32_t *ho,
-                              int lane) {
+                              int lane, uint64_t *q4) {
     using seedc::HB;
     using seedc::KI;
     using seedc::KX;
     int err = 0;
     int run = 0;
+    // the read 16 bases per word in LDS (past the read: 6, never a text code) for the match
+    // lengths below; visible after the wave_sync_lds that follows the start pass
+    if (V.text4)
+        for (int w = lane; w <= (len >> 4) + 1; w += 64) {
+            uint64_t v = 0;
+            for (int k = 0; k < 16; ++k) {
+                const int x = w * 16 + k;
+                v |= (uint64_t)(x < len ? (q[x] < 4 ? q[x] : 4) : 6) << (4 * k);
+            }
+            q4[w] = v;
+        }
     for (int a0 = 0; a0 <= len; a0 += 64) {
         const int a = a0 + lane;
         int ca = 0;
@@ -115,8 +134,30 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
             m = m < le ? m : le;
             m = m < lq ? m : lq;
             int ml = KI + m;
-            if (m == KX)
-                while (a + ml < len && q[a + ml] < 4 && V.text[p + ml] == q[a + ml]) ++ml;
+            if (m == KX) {
+                if (V.text4) {   // 16 bases at a time: the first differing nibble, or a read N, or the read's end
+                    for (;;) {
+                        const int x = a + ml;
+                        if (x >= len) break;
+                        const uint64_t qw = nib16(q4, (uint64_t)x), tw = nib16(V.text4, p + ml);
+                        const uint64_t nq = (qw >> 2) & 0x1111111111111111ull;   // read N (code 4) or past the end (6)
+                        const uint64_t bad = (qw ^ tw) | (nq * 0xFull);
+                        const int lim = len - x;
+                        if (bad) {
+                            const int f = __builtin_ctzll(bad) >> 2;
+                            ml += f < lim ? f : lim;
+                            break;
+                        }
+                        if (lim <= 16) {
+                            ml += lim;
+                            break;
+                        }
+                        ml += 16;
+                    }
+                } else {
+                    while (a + ml < len && q[a + ml] < 4 && V.text[p + ml] == q[a + ml]) ++ml;
+                }
+            }
             seedc::set_hpos(S, k, p);
             S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
         }
@@ -149,6 +190,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
 // outgrew pass 1's slices), the sequential part on lane 0.
 __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
+    __shared__ uint64_t q4_lds[SEED_WAVES][SEED_LMAX / 16 + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
     load_lcnt(D.V, lcnt);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -173,7 +215,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
         int err = 0;
         const unsigned long long t0 = D.prof && lane == 0 ? wall_clock64() : 0ULL;
         if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
-        if (len > 0 && !err) err = build_occ_wave(D.V, S, q, len, ho, lane);
+        if (len > 0 && !err) err = build_occ_wave(D.V, S, q, len, ho, lane, q4_lds[wv]);
         // SMEMs and chaining on lane 0; then, for reads where bwa runs mem_flt_chained_seeds
         // (>= 440 bp), the seeds' local SW scores over all 64 lanes (a seed per lane, the rows
         // int16 and lane-interleaved in the dead count table); the output on lane 0
@@ -231,6 +273,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
 // goes to pass 2.
 __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(SeedDev D) {
     __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
+    __shared__ uint64_t q4_lds[SEED_WAVES][SEED_LMAX / 16 + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
     load_lcnt(D.V, lcnt);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -244,7 +287,8 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
         int b0 = 0;
         if (lane == 0) b0 = atomicAdd(D.next, 64);
         b0 = __shfl(b0, 0, 64);
-        if (b0 >= D.n_sr) {   // every wave reaches this: the grid drains
+        const int64_t nlim = D.rlist ? D.n_list : D.n_sr;   // rlist: the reads of a retry pass
+        if (b0 >= nlim) {   // every wave reaches this: the grid drains
             if (D.prof) {
 #pragma unroll
                 for (int k = 0; k < 3; ++k)
@@ -259,20 +303,20 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
         }
         const unsigned long long t0 = D.prof ? wall_clock64() : 0ULL;
         int my_err = 0;
-        const int nb = (int)(D.n_sr - b0 < 64 ? D.n_sr - b0 : 64);
+        const int nb = (int)(nlim - b0 < 64 ? nlim - b0 : 64);
         for (int rd = 0; rd < nb; ++rd) {
-            const int i = b0 + rd;
+            const int i = D.rlist ? D.rlist[b0 + rd] : b0 + rd;
             const int64_t o = D.sr_off[i];
             const int len = (int)(D.sr_off[i + 1] - o);
             seedc::Scratch S = seedc::carve(base + (int64_t)rd * D.stride, D.caps);
             int err = 0;
             if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
-            if (len > 0 && !err) err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane);
+            if (len > 0 && !err) err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv]);
             if (lane == rd) my_err = err;
         }
         const unsigned long long t1 = D.prof ? wall_clock64() : 0ULL;
         if (lane < nb) {
-            const int i = b0 + lane;
+            const int i = D.rlist ? D.rlist[b0 + lane] : b0 + lane;
             const int64_t o = D.sr_off[i];
             const int len = (int)(D.sr_off[i + 1] - o);
             seedc::Scratch S = seedc::carve(base + (int64_t)lane * D.stride, D.caps);
