@@ -502,6 +502,13 @@ int pr_lrset_index(pr_ctx *ctx, int which);
 int pr_iter_upload_lrset(pr_ctx *ctx, const pr_sw_batch *b);
 int pr_lrset_commit(pr_ctx *ctx, pr_comm *comm, int with_mask);
 int pr_lrset_download(pr_ctx *ctx, int64_t *off, uint8_t *seq, uint8_t *qual, uint8_t *map);
+/* The resident short reads: the whole short-read input (nt4, in stream order) once; a task's
+ * sample -- SeqChunker's chunks are contiguous record ranges (bin/proovread:2085-2102) -- is then
+ * gathered on the device from ranges[2k], ranges[2k+1] (records [r0, r1)) and seeded as
+ * pr_seed_gpu_map with out = NULL (the seeds and the gathered reads stay in HBM;
+ * pr_iter_upload_lrset with sr_seq NULL takes them). */
+int pr_srset_load(pr_ctx *ctx, int64_t n_sr, const int64_t *off, const uint8_t *seq);
+int pr_seed_gpu_map_sampled(pr_ctx *ctx, const pr_seed_opts *o, const int64_t *ranges, int n_ranges, int32_t *status);
 
 /* enqueue (ctx stream) the per-iteration statistic of the resident consensus:
  * dev_out[0] = corrected bases, dev_out[1] = bases with phred >= min_phred.

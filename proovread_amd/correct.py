@@ -30,6 +30,7 @@ configs[1] size ~17 GB of device buffers, far below 288 GB); bwa-proovread's
 """
 from __future__ import annotations
 
+import ctypes as C
 import dataclasses
 import functools
 import math
@@ -206,20 +207,32 @@ class ShortReads:
             return b"".join(rec.split(b"\n")[1:]).strip()
         return rec.split(b"\n")[1].strip()
 
+    def sample_ranges(self, sc: Optional[Dict[str, int]]) -> Tuple[np.ndarray, np.ndarray]:
+        """-> (record ranges [k, 2] of the chunks SeqChunker writes for cov2seqchunker's
+        parameters (None: every record), the offsets of the sampled reads)."""
+        if sc is None:
+            return np.array([[0, len(self.lengths)]], np.int64), self.off
+        ks = np.asarray(seqchunker.select(self.n_chunks, sc["--first-chunk"], sc["--chunk-step"],
+                                          sc["--chunks-per-step"]), np.int64)
+        rg = np.stack([self.cfirst[ks - 1], self.cfirst[ks]], axis=1)
+        rg = rg[rg[:, 1] > rg[:, 0]]
+        lens = np.concatenate([self.lengths[a:b] for a, b in rg]) if len(rg) else np.zeros(0, np.int64)
+        off = np.zeros(len(lens) + 1, np.int64)
+        np.cumsum(lens, out=off[1:])
+        return rg, off
+
+    def gather(self, ranges: np.ndarray) -> np.ndarray:
+        """The nt4 pool of the records in `ranges` (stream order)."""
+        if len(ranges) == 1 and ranges[0, 0] == 0 and ranges[0, 1] == len(self.lengths):
+            return self.pool
+        parts = [self.pool[self.off[a]:self.off[b]] for a, b in ranges]
+        return np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+
     def sample(self, sc: Optional[Dict[str, int]]) -> Tuple[np.ndarray, np.ndarray]:
         """nt4 pool of the records SeqChunker writes for cov2seqchunker's parameters
         (None: every record), in stream order."""
-        if sc is None:
-            return self.pool, self.off
-        ks = seqchunker.select(self.n_chunks, sc["--first-chunk"], sc["--chunk-step"], sc["--chunks-per-step"])
-        r0 = self.cfirst[np.asarray(ks, np.int64) - 1]
-        r1 = self.cfirst[np.asarray(ks, np.int64)]
-        parts = [self.pool[self.off[a]:self.off[b]] for a, b in zip(r0, r1) if b > a]
-        lens = np.concatenate([self.lengths[a:b] for a, b in zip(r0, r1) if b > a]) if parts else np.zeros(0, np.int64)
-        off = np.zeros(len(lens) + 1, np.int64)
-        np.cumsum(lens, out=off[1:])
-        pool = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
-        return pool, off
+        rg, off = self.sample_ranges(sc)
+        return self.gather(rg), off
 
 
 def _fastq4_records(arr: np.ndarray):
@@ -273,13 +286,25 @@ class GpuStages:
         self.lrs = None
         self.ids: List[str] = []
 
+    device_short_reads = True   # world 1: a task's sample is gathered on the device (pr_srset_*)
+
     def load(self, reads: LongReads) -> None:
         from . import iteration
         self.lrs = iteration.LongReadSet(self.ctx, reads.seq_pool, reads.off, reads.qual_pool)
         self.ids = list(reads.ids)
 
-    def task(self, task: str, sr: np.ndarray, sr_off: np.ndarray, params, bin_filter, comm=None,
-             exact: bool = False, mask_cfg=None) -> TaskOut:
+    def load_short_reads(self, srs: "ShortReads") -> None:
+        """The whole short-read input into HBM once (pr_srset_load)."""
+        from . import _abi, iteration
+        L = _abi.lib()
+        iteration._setup(L)
+        pool = np.ascontiguousarray(srs.pool, np.uint8)
+        off = np.ascontiguousarray(srs.off, np.int64)
+        _abi.check(L.pr_srset_load(self.ctx.h, len(off) - 1, _abi.ptr(off, C.c_int64), _abi.ptr(pool, C.c_uint8)),
+                   "pr_srset_load")
+
+    def task(self, task: str, sr: Optional[np.ndarray], sr_off: np.ndarray, params, bin_filter, comm=None,
+             exact: bool = False, mask_cfg=None, sr_ranges: Optional[np.ndarray] = None) -> TaskOut:
         """One bwa-sr task on the resident set.  mask_cfg = (hcr-mask, min_sr_length) for the
         regular tasks, None for the finish task (which maps to the unmasked reads,
         proovread:838-850); exact: the multi-GPU exact-parity layout."""
@@ -297,7 +322,13 @@ class GpuStages:
             raise TypeError("the device stages exchange over libprgpu's communicator (comm.RcclComm / LocalComm)")
         n_sr = len(sr_off) - 1
         if not exact:
-            seed._map_gpu(L, self.ctx, sr, sr_off, seed_opts, False, keep_on_device=True)
+            if sr is None:   # gathered from the resident short reads (load_short_reads)
+                rg = np.ascontiguousarray(sr_ranges, np.int64)
+                st = np.zeros(max(1, n_sr), np.int32)
+                _abi.check(L.pr_seed_gpu_map_sampled(self.ctx.h, C.byref(seed_opts), _abi.ptr(rg, C.c_int64), len(rg),
+                                                     _abi.ptr(st, C.c_int32)), "pr_seed_gpu_map_sampled")
+            else:
+                seed._map_gpu(L, self.ctx, sr, sr_off, seed_opts, False, keep_on_device=True)
             it = iteration.SetIteration(self.ctx, None, sr_off, lr_off)
             lo, hi = 0, len(lr_off) - 1
         else:
@@ -318,10 +349,10 @@ class GpuStages:
         if finish:
             out.chim = it.chim_lines(self.ids[lo:hi])
         else:
-            buf = _abi.DevBuffer(self.ctx, 16)
-            it.mask_to(buf.ptr, mask.params(mask_cfg[0], mask_cfg[1]))
-            st = buf.download(np.int64)
-            buf.close()
+            if getattr(self, "_stats", None) is None:   # the {bpt, bpN} device words, kept across tasks
+                self._stats = _abi.DevBuffer(self.ctx, 16)
+            it.mask_to(self._stats.ptr, mask.params(mask_cfg[0], mask_cfg[1]))
+            st = self._stats.download(np.int64)
             out.bpt, out.bpn = int(st[0]), int(st[1])
         self.device_ms += sum(it.timing())
         self.lrs.commit(comm if exact else None, with_mask=not finish)
@@ -410,6 +441,8 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
             reads, ignored = read_long(lr_records, stubby)
             ids = reads.ids
             stages.load(reads)    # the mapping reference starts as the reads (.masked.fa)
+            if hasattr(stages, "load_short_reads"):
+                stages.load_short_reads(srs)
             log.append(TaskLog(task))
             tc += 1
             continue
@@ -420,7 +453,11 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         t_task = time.perf_counter()
         dev0 = getattr(stages, "device_ms", None)
         task_cov = sr_coverage_for(task)
-        sr, sr_off = srs.sample(sampler.cov2seqchunker(cfg.coverage, task_cov))
+        multi = comm is not None and comm.world > 1
+        ranges, sr_off = srs.sample_ranges(sampler.cov2seqchunker(cfg.coverage, task_cov))
+        # device stages at world 1: the sample is gathered from the resident short reads on the device
+        on_dev = bool(getattr(stages, "device_short_reads", False)) and not (multi or cfg.exact_layout)
+        sr = None if on_dev else srs.gather(ranges)
         ent.n_sr = len(sr_off) - 1
         max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541
         params = cns.CnsParams(coverage=max_cov, use_ref_qual=not finish, detect_chimera=finish,
@@ -428,11 +465,10 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         # bwa-proovread -b BIN -l BIN*min(cov, task cov) (proovread:1302-1313, cfg bin-size)
         bsz = T.bin_size(mode)
         binf = (bsz, bsz * min(cfg.coverage, task_cov)) if cfg.bin_filter else None
-        multi = comm is not None and comm.world > 1
         if finish and cfg.keep_masked:
             last_masked = stages.masked()
         r = stages.task(task, sr, sr_off, params, binf, comm, multi or cfg.exact_layout,
-                        None if finish else (hcr_mask_for(task), min_sr)) if ids else TaskOut(0, [])
+                        None if finish else (hcr_mask_for(task), min_sr), sr_ranges=ranges) if ids else TaskOut(0, [])
         ent.n_tasks = r.n_tasks
         lines, bpt, bpn = r.chim, r.bpt, r.bpn
         if multi:

@@ -140,7 +140,7 @@ enum SeedBufId {
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
 // the task's short reads
 // the resident long-read set: pools, the dense offsets of a commit, the commit's staging pools
-enum LrSetBufId { LS_SEQ, LS_QUAL, LS_MAP, LS_OFF, LS_TSEQ, LS_TQUAL, LS_TMAP, LS_COUNT };
+enum LrSetBufId { LS_SEQ, LS_QUAL, LS_MAP, LS_OFF, LS_TSEQ, LS_TQUAL, LS_TMAP, LS_SRSEQ, LS_COUNT };
 enum XchgBufId {
     XB_BOUNDS, XB_KEY0, XB_KEY1, XB_IDX0, XB_IDX1, XB_CNT, XB_OPIN, XB_OPAT, XB_SREC, XB_SCIG, XB_TEMP,
     XB_RREC, XB_RCIG, XB_RCIGAT, XB_GCNT, XB_GCNT64, XB_TASKOFF, XB_ERR, XB_GSR, XB_GSTATUS, XB_GPOS, XB_GSCORE,
@@ -195,6 +195,8 @@ struct pr_ctx {
     std::vector<int64_t> ls_off;
     int32_t ls_n = -1;
     bool ls_map_is_reads = true;
+    std::vector<int64_t> ss_off;   // the resident short reads (pr_srset_load): offsets on the host
+    bool seed_sr_staged = false;   // SB_SEQ already holds the reads of the next pr_seed_gpu_map
     bool own = false;            // the resident iteration batch is an owned batch (pr_iter_upload_owned)
     bool own_ref_nt4 = false;    // its consensus reference is the SW long-read pool's slice (nt4)
     int32_t own_lr0 = 0;
@@ -1877,9 +1879,53 @@ extern "C" int pr_seed_gpu_index_last_ms(pr_ctx *c, double *ms) {
     return 0;
 }
 
+// the resident short reads (include/prgpu.h pr_srset_load): the whole short-read input once;
+// a task's sample is gathered on the device from its record ranges
+extern "C" int pr_srset_load(pr_ctx *c, int64_t n_sr, const int64_t *off, const uint8_t *seq) {
+    if (!c || n_sr < 0 || !off || (off[n_sr] && !seq) || off[0] != 0) return set_error(PR_ERR_ARG, "bad arg");
+    HIPCHK(hipSetDevice(c->device));
+    int rc = upload(c->ls[LS_SRSEQ], seq, (size_t)off[n_sr], c->stream);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->ss_off.assign(off, off + n_sr + 1);
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_map_sampled(pr_ctx *c, const pr_seed_opts *o, const int64_t *ranges, int n_ranges,
+                                       int32_t *status) {
+    if (!c || !o || n_ranges < 0 || (n_ranges && !ranges)) return set_error(PR_ERR_ARG, "null arg");
+    if (c->ss_off.empty()) return set_error(PR_ERR_ARG, "no resident short reads (pr_srset_load)");
+    const int64_t N = (int64_t)c->ss_off.size() - 1;
+    std::vector<int64_t> off(1, 0);
+    for (int k = 0; k < n_ranges; ++k) {
+        const int64_t r0 = ranges[2 * k], r1 = ranges[2 * k + 1];
+        if (r0 < 0 || r1 < r0 || r1 > N) return set_error(PR_ERR_ARG, "record range outside the short reads");
+        for (int64_t i = r0; i < r1; ++i) off.push_back(off.back() + c->ss_off[(size_t)i + 1] - c->ss_off[(size_t)i]);
+    }
+    const int64_t n = (int64_t)off.size() - 1;
+    if (n > INT32_MAX) return set_error(PR_ERR_CAPACITY, "too many short reads in one sample");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc = c->sd[SB_SEQ].ensure((size_t)off.back() + 1);
+    if (rc) return rc;
+    int64_t at = 0;
+    for (int k = 0; k < n_ranges; ++k) {
+        const int64_t b0 = c->ss_off[(size_t)ranges[2 * k]], b1 = c->ss_off[(size_t)ranges[2 * k + 1]];
+        if (b1 > b0)
+            HIPCHK(hipMemcpyAsync(c->sd[SB_SEQ].as<uint8_t>() + at, c->ls[LS_SRSEQ].as<uint8_t>() + b0, (size_t)(b1 - b0),
+                                  hipMemcpyDeviceToDevice, s));
+        at += b1 - b0;
+    }
+    c->seed_sr_staged = true;
+    return pr_seed_gpu_map(c, o, nullptr, off.data(), (int)n, nullptr, status);
+}
+
 extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *sr_seq, const int64_t *sr_off, int n_sr,
                                pr_seed_tasks *out, int32_t *status) {
-    if (!c || !o || n_sr < 0 || (n_sr && (!sr_seq || !sr_off))) return set_error(PR_ERR_ARG, "null arg");
+    if (!c) return set_error(PR_ERR_ARG, "null arg");
+    const bool staged = c->seed_sr_staged;   // pr_seed_gpu_map_sampled gathered the reads on the device
+    c->seed_sr_staged = false;
+    if (!o || n_sr < 0 || (n_sr && ((!sr_seq && !staged) || !sr_off))) return set_error(PR_ERR_ARG, "null arg");
     pr_seed_tasks dummy;
     const bool keep_on_device = out == nullptr;
     if (!out) out = &dummy;
@@ -1946,7 +1992,7 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     const int64_t chunk = std::max<int64_t>(64, out_budget / slot_bytes / 64 * 64);
     int rc;
     c->seed_sr_bases = nb;
-    if ((rc = upload(D[SB_SEQ], sr_seq, (size_t)nb, s)) || (rc = upload(D[SB_OFF], sr_off, (size_t)n_sr + 1, s)) ||
+    if ((!staged && (rc = upload(D[SB_SEQ], sr_seq, (size_t)nb, s))) || (rc = upload(D[SB_OFF], sr_off, (size_t)n_sr + 1, s)) ||
         (rc = D[SB_SCRATCH].ensure((size_t)scratch)) ||
         (rc = D[SB_OUT].ensure((size_t)(std::min<int64_t>(chunk, n_sr) * slot_bytes + 16))) ||
         (rc = D[SB_NOUT].ensure((size_t)n_sr * 4 + 16)) || (rc = D[SB_STATUS].ensure((size_t)n_sr * 4 + 16)) ||

@@ -47,6 +47,9 @@ def _setup(L):
     L.pr_lrset_commit.argtypes = [C.c_void_p, C.c_void_p, C.c_int]
     L.pr_lrset_download.argtypes = [C.c_void_p, _abi.P64, _abi.PU8, _abi.PU8, _abi.PU8]
     L.pr_iter_upload_lrset.argtypes = [C.c_void_p, C.POINTER(sw.SwBatch)]
+    from . import seed
+    L.pr_srset_load.argtypes = [C.c_void_p, C.c_int64, _abi.P64, _abi.PU8]
+    L.pr_seed_gpu_map_sampled.argtypes = [C.c_void_p, C.POINTER(seed.SeedOpts), _abi.P64, C.c_int, _abi.P32]
     L._iter_ready = True
 
 
@@ -191,11 +194,15 @@ class Iteration:
     def chim_lines(self, ids: List[str]) -> List[str]:
         """bam2cns:488's chimera lines of every long read (ids: theirs, in batch order)."""
         st, nch, c0, rows = self.chimeras()
-        out = []
-        for i in np.flatnonzero(nch):
-            for fr, to, npos, ntot in rows[int(c0[i]):int(c0[i]) + int(nch[i])]:
-                out.append(f"{ids[i]}\t{int(fr)}\t{int(to)}\t{cns.perl_num(int(npos) / int(ntot))}")
-        return out
+        idx = np.flatnonzero(nch)
+        if not len(idx):
+            return []
+        cnt = nch[idx].astype(np.int64)
+        first = np.repeat(c0[idx] - (np.cumsum(cnt) - cnt), cnt)
+        r = rows[first + np.arange(int(cnt.sum()))]
+        ratio = (r[:, 2].astype(np.float64) / r[:, 3]).tolist()   # perl_num: %.15g of npos / ntot
+        rid = [ids[i] for i in np.repeat(idx, cnt).tolist()]
+        return [f"{i}\t{fr}\t{to}\t{x:.15g}" for i, fr, to, x in zip(rid, r[:, 0].tolist(), r[:, 1].tolist(), ratio)]
 
     def results(self) -> List[cns.ReadResult]:
         a = self.download()

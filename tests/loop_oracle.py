@@ -28,7 +28,7 @@ class OracleStages:
         self.ids, self.seqs, self.quals = list(reads.ids), list(reads.seqs), list(reads.quals)
         self.map = list(self.seqs)
 
-    def task(self, task, sr, sr_off, params, bin_filter, comm=None, exact=False, mask_cfg=None):
+    def task(self, task, sr, sr_off, params, bin_filter, comm=None, exact=False, mask_cfg=None, sr_ranges=None):
         from proovread_amd import correct, tasks as T
         finish = mask_cfg is None
         lr_map, lr_off = correct._pool(self.seqs if finish else self.map)   # finish: the unmasked reads
