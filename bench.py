@@ -53,7 +53,7 @@ OPS_PER_CELL = 14   # SURVEY.md §8d canonical int ops per DP cell
 BIN_FILTER = (20, 20.0 * 15.0)
 # HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over this bench
 # (tools/pmc_summary.py; MI355X_MICROARCH.md's corrections)
-PMC_FILE = "pmc_r03o.json"
+PMC_FILE = "pmc_r04.json"
 _JSON_OUT = sys.stdout
 
 
@@ -352,7 +352,7 @@ def main():
     n_aln, sum_ncig, sum_lseq = it.alignment_stats()
     cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + own_bases * (2 + 2 + 6 * 4 * 2)
     # HBM bytes per launch from the PMC FETCH_SIZE / WRITE_SIZE passes of this bwa-mode step
-    # (tools/r03_final.sh -> tools/pmc_summary.py -> profiles/pmc_r03o.json)
+    # (tools/r04_final.sh -> tools/pmc_summary.py -> profiles/pmc_r04.json)
     prof = ROOT / "profiles" / PMC_FILE
     traffic = traffic_cns = traffic_ext = None
     if prof.exists():
