@@ -182,33 +182,40 @@ __global__ void __launch_bounds__(SW_WAVE) sw_ext_phase_kernel(SwDev D, SwOptsDe
 // lane, ~1.5 ms per launch whatever the number of retried tasks.
 constexpr int XW_COLS = 3;
 
-__device__ __forceinline__ int wave_max_i32(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const int t = __shfl_xor(v, o, 64);
-        v = t > v ? t : v;
-    }
+// one DPP step of a max scan: lanes without a source (outside the row / masked rows) keep INT_MIN
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_max_step(int v) {
+    const int t = __builtin_amdgcn_update_dpp((int)INT32_MIN, v, CTRL, ROWS, 0xf, false);
+    return t > v ? t : v;
+}
+// inclusive prefix max over the wave's lanes: row_shr 1, 2, 4, 8 scan the rows of 16, then
+// row_bcast:15 carries rows 0 / 2 into 1 / 3 and row_bcast:31 the first half into the second
+// (register-to-register DPP moves: no LDS round trip per step, unlike __shfl_up)
+__device__ __forceinline__ int wave_scan_max_i32(int v) {
+    v = dpp_max_step<0x111, 0xf>(v);
+    v = dpp_max_step<0x112, 0xf>(v);
+    v = dpp_max_step<0x114, 0xf>(v);
+    v = dpp_max_step<0x118, 0xf>(v);
+    v = dpp_max_step<0x142, 0xa>(v);
+    v = dpp_max_step<0x143, 0xc>(v);
     return v;
 }
-// inclusive prefix max over the wave's lanes
-__device__ __forceinline__ int wave_scan_max_i32(int v, int lane) {
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int t = __shfl_up(v, d, 64);
-        if (lane >= d) v = t > v ? t : v;
-    }
-    return v;
-}
+__device__ __forceinline__ int wave_max_i32(int v) { return __builtin_amdgcn_readlane(wave_scan_max_i32(v), 63); }
+// lane l gets lane l - 1's value, lane 0 gets `first` (wave_shr:1)
+__device__ __forceinline__ int wave_shr1(int v, int first) { return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false); }
 
-__device__ int ext_wave(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen, const uint8_t *Lr, long tb, int ts,
-                        bool comp, int tlen, const SwOptsDev &O, int w, int end_bonus, int h0, int lane, ExtIO &io) {
+__device__ int ext_wave(uint32_t *eh, uint8_t *qrow, const uint8_t *Q, int qb, int qs, int qlen, const uint8_t *Lr,
+                        long tb, int ts, bool comp, int tlen, const SwOptsDev &O, int w, int end_bonus, int h0, int lane,
+                        ExtIO &io) {
     const int a = O.a, b = O.b, o_del = O.o_del, e_del = O.e_del, o_ins = O.o_ins, e_ins = O.e_ins;
     const int oe_del = o_del + e_del, oe_ins = o_ins + e_ins;
-    {   // row -1 (ksw's first row) and the band cap by the longest possible gap (max entry = a)
+    {   // row -1 (ksw's first row) and the band cap by the longest possible gap (max entry = a);
+        // the query in extension order in the wave's LDS (one load per column per task, not per row)
         const int hj1 = h0 > oe_ins ? h0 - oe_ins : 0;
         for (int j = lane; j <= qlen + 1; j += 64) {
             int h = j == 0 ? h0 : (j <= qlen ? hj1 - e_ins * (j - 1) : 0);
             eh[j] = (uint32_t)(h > 0 ? h : 0);
+            if (j < qlen) qrow[j] = Q[qb + qs * j];
         }
         int max_ins = (int)((double)(qlen * a + end_bonus - o_ins) / e_ins + 1.);
         max_ins = max_ins > 1 ? max_ins : 1;
@@ -220,9 +227,14 @@ __device__ int ext_wave(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen
     __builtin_amdgcn_wave_barrier();
     int max = h0, max_i = -1, max_j = -1, max_ie = -1, gscore = -1, max_off = 0;
     int beg = 0, end = qlen;
+    int tv = 0;   // target bases of rows i0 .. i0 + 63, one per lane (loaded every 64 rows)
     for (int i = 0; i < tlen; ++i) {
-        int tc = (int)Lr[tb + (long)ts * i];
-        if (comp && tc < 4) tc = 3 - tc;
+        if ((i & 63) == 0) {
+            const int ii = i + lane;
+            tv = ii < tlen ? (int)Lr[tb + (long)ts * ii] : 0;
+            if (comp && tv < 4) tv = 3 - tv;
+        }
+        const int tc = __builtin_amdgcn_readlane(tv, i & 63);
         if (beg < i - w) beg = i - w;
         if (end > i + w + 1) end = i + w + 1;
         if (end > qlen) end = qlen;
@@ -249,16 +261,16 @@ __device__ int ext_wave(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen
                 const uint32_t p = eh[j];
                 const int hp = (int)(p & 0xFFFFu);
                 e = (int)(p >> 16);
-                Mv = hp ? hp + sw_score(tc, (int)Q[qb + qs * j], a, b) : 0;
+                Mv = hp ? hp + sw_score(tc, (int)qrow[j], a, b) : 0;
                 const int t = Mv - oe_ins > 0 ? Mv - oe_ins : 0;
                 A = t + j * e_ins;
             }
             // F(j) = exclusive prefix max of A - (j - 1) e_ins, F(beg) = 0
-            const int inc = wave_scan_max_i32(A, lane);
-            int exl = __shfl_up(inc, 1, 64);
-            if (lane == 0) exl = INT32_MIN;
+            const int inc = wave_scan_max_i32(A);
+            int exl = wave_shr1(inc, (int)INT32_MIN);
             exl = exl > carry ? exl : carry;
-            carry = __shfl(inc, 63, 64) > carry ? __shfl(inc, 63, 64) : carry;
+            const int top = __builtin_amdgcn_readlane(inc, 63);
+            carry = top > carry ? top : carry;
             const int F = exl == INT32_MIN ? 0 : exl - (j - 1) * e_ins;
             int h = Mv > e ? Mv : e;
             h = h > F ? h : F;
@@ -278,9 +290,8 @@ __device__ int ext_wave(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen
         for (int r = 0; r < XW_COLS; ++r) {
             if (r >= nr) continue;
             const int j = beg + lane + 64 * r;
-            int left = __shfl_up(H[r], 1, 64);
-            const int prev63 = __shfl(hprev_blk, 63, 64);   // (lane 63's value of the previous block)
-            if (lane == 0) left = r == 0 ? h1 : prev63;
+            // lane 0: h1 before the band, else lane 63's h of the previous block
+            const int left = wave_shr1(H[r], r == 0 ? h1 : __builtin_amdgcn_readlane(hprev_blk, 63));
             hprev_blk = H[r];
             if (j < end) {
                 const uint32_t nw = (uint32_t)left | ((uint32_t)E[r] << 16);
@@ -288,7 +299,7 @@ __device__ int ext_wave(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen
                 nzb[r] = nw != 0u ? 1u : 0u;
             }
             const int jl = end - 1;   // the band's last column
-            if (jl >= beg + 64 * r && jl < beg + 64 * (r + 1)) hlast = __shfl(H[r], jl - beg - 64 * r, 64);
+            if (jl >= beg + 64 * r && jl < beg + 64 * (r + 1)) hlast = __builtin_amdgcn_readlane(H[r], jl - beg - 64 * r);
         }
         if (lane == 0) eh[end] = (uint32_t)hlast;   // e = 0
         __builtin_amdgcn_wave_barrier();
@@ -344,7 +355,9 @@ __device__ int ext_wave(uint32_t *eh, const uint8_t *Q, int qb, int qs, int qlen
 __global__ void __launch_bounds__(256) sw_ext_wave_kernel(SwDev D, SwOptsDev O, int side, int tryi) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds_w[];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-    uint32_t *eh = lds_w + wv * (D.qmax + 2);
+    const int per_wave = (D.qmax + 2) + (D.qmax + 3) / 4;   // DP row words + the query's bytes
+    uint32_t *eh = lds_w + wv * per_wave;
+    uint8_t *qrow = reinterpret_cast<uint8_t *>(eh + D.qmax + 2);
     const int n = D.list_n[0];
     for (int64_t k = (int64_t)blockIdx.x * nwv + wv; k < n; k += (int64_t)gridDim.x * nwv) {
         const int64_t t = D.list[k];
@@ -370,7 +383,7 @@ __global__ void __launch_bounds__(256) sw_ext_wave_kernel(SwDev D, SwOptsDev O, 
         }
         ExtIO io;
         const int aw = O.w << tryi;
-        const int score = ext_wave(eh, g.Q, qb, qs, qlen, g.Lr, tb, ts, g.rev, tlen, O, aw, end_bonus, h0, lane, io);
+        const int score = ext_wave(eh, qrow, g.Q, qb, qs, qlen, g.Lr, tb, ts, g.rev, tlen, O, aw, end_bonus, h0, lane, io);
         if (lane == 0) {
             xref(D, side, XF_SCORE, t) = score;
             xref(D, side, XF_QLE, t) = io.qle;
@@ -1351,11 +1364,32 @@ __global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O, in
         if (k >= 0) D.list[atomicAdd(&hist[k], 1)] = (int32_t)t;
     }
 }
+// Fill of a large buffer with a byte-pattern word (0 / 0xFF..): 16-byte stores over a grid that
+// spreads over the chip.  The runtime's fill kernel for tens of MB takes a few workgroups and,
+// beside a kernel that holds most CUs (the chain-head links on the side stream), ran 2 ms for
+// the 35 MB x_try of configs[1].
+__global__ void __launch_bounds__(256) sw_fill_kernel(uint32_t *p, uint32_t v, int64_t n) {
+    const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+    uint4 *q = reinterpret_cast<uint4 *>(p);
+    const uint4 vv = make_uint4(v, v, v, v);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) q[i] = vv;
+    for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = v;
+}
+static hipError_t sw_fill(void *p, uint32_t byte, size_t bytes, hipStream_t s) {
+    if (((uintptr_t)p & 15u) || (bytes & 3u) || bytes < ((size_t)1 << 20))
+        return hipMemsetAsync(p, (int)byte, bytes, s);
+    const int64_t n = (int64_t)(bytes >> 2);
+    int64_t grid = (n / 4 + 255) / 256;
+    grid = grid < 2048 ? grid : 2048;
+    hipLaunchKernelGGL(sw_fill_kernel, dim3((unsigned)grid), dim3(256), 0, s, (uint32_t *)p, byte * 0x01010101u, n);
+    return hipGetLastError();
+}
+
 int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *stream) {
     hipStream_t s = (hipStream_t)stream;
     hipError_t e = hipMemsetAsync(D.pk_bucket, 0, (PK_SCAN + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
-    e = hipMemsetAsync(D.list, 0xFF, (size_t)(sel_count(D) + (int64_t)PK_NB * PK_SEG + 1) * sizeof(int32_t), s);
+    e = sw_fill(D.list, 0xFFu, (size_t)(sel_count(D) + (int64_t)PK_NB * PK_SEG + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
     int grid = (int)((sel_count(D) + 255) / 256);
     grid = grid < 2048 ? (grid > 0 ? grid : 1) : 2048;
@@ -1478,7 +1512,7 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
     fgrid = fgrid < 8192 ? (fgrid > 0 ? fgrid : 1) : 8192;
     // (a whole number of dwords: a byte-sized fill takes the runtime's byte kernel, 2 ms for the
     // 35 MB of configs[1]; the buffer has 64 bytes of slack)
-    hipError_t e = hipMemsetAsync(D.x_try, 0, ((size_t)D.n_task + 1 + 15) & ~(size_t)15, s);
+    hipError_t e = sw_fill(D.x_try, 0u, ((size_t)D.n_task + 1 + 15) & ~(size_t)15, s);
     if (e != hipSuccess) return (int)e;
     for (int side = 0; side < 2; ++side) {
         for (int tryi = 0; tryi < 2; ++tryi) {
@@ -1504,7 +1538,7 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
             else if (wb <= 80 && (2 * wb + 1 > XW_COLS * 64 || getenv("PRGPU_EXT80_LANE")))   // one task per lane
                 hipLaunchKernelGGL(sw_ext_phase_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O, side, tryi);
             else if (wb <= 80) {   // one task per wave (ext_wave)
-                const int lds = 4 * (D.qmax + 2) * 4;
+                const int lds = 4 * ((D.qmax + 2) + (D.qmax + 3) / 4) * 4;
                 hipLaunchKernelGGL(sw_ext_wave_kernel, dim3(grid_waves), dim3(256), lds, s, D, O, side, tryi);
             }
             else if (D.eh_g) hipLaunchKernelGGL(sw_ext_wide_kernel<true>, dim3(D.eh_g_blocks), dim3(SW_WAVE), 0, s, D, O, side, tryi);
