@@ -555,6 +555,18 @@ __device__ __forceinline__ int band_w(const SwOptsDev &O, int w, int qlen, int e
     return w < max_del ? w : max_del;
 }
 
+// The next segment of a packed launch, longest first: segments sit in ascending key order (query
+// length; band, then query length for the CIGAR pass), so the dequeue walks the list from its
+// end, and the waves that finish early take the short segments (a static round robin left the
+// longest segments for the last, partial round).  Counter `which` is zeroed by
+// sw_launch_pk_order; -1 when the list is done.
+__device__ __forceinline__ int pk_next_seg(const SwDev &D, int which, int nseg) {
+    int s = 0;
+    if (threadIdx.x == 0) s = atomicAdd(D.bucket + SW_NBUCKET + 8 + which, 1);
+    s = __builtin_amdgcn_readfirstlane(s);
+    return s < nseg ? nseg - 1 - s : -1;
+}
+
 // First band try of one extension side for two tasks per lane (sw_pk.h ext_pk):
 // wave k takes the 128-task segment of one side query length (so qlen and the
 // capped band are wave-uniform); lane l runs list[128k + l] and list[128k + 64 + l].
@@ -565,7 +577,9 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_ext_pk_kernel(SwDev D, SwOptsDe
     const int lane = threadIdx.x;
     const int nseg = D.pk_bucket[PK_SCAN] / PK_SEG;
     const int end_bonus = side == 0 ? O.pen_clip5 : O.pen_clip3;
-    for (int seg = blockIdx.x; seg < nseg; seg += gridDim.x) {
+    for (;;) {
+        const int seg = pk_next_seg(D, 0, nseg);
+        if (seg < 0) break;
         const int64_t tt[2] = {D.list[(int64_t)seg * PK_SEG + lane], D.list[(int64_t)seg * PK_SEG + 64 + lane]};
         const int qlen = __builtin_amdgcn_readfirstlane(pk_ext_key(D, O, D.list[(int64_t)seg * PK_SEG], side));
         const int w = __builtin_amdgcn_readfirstlane(band_w(O, O.w, qlen, end_bonus));
@@ -1153,7 +1167,15 @@ __global__ void __launch_bounds__(SW_WAVE, 2) sw_global_pk_kernel(SwDev D, SwOpt
     const int nseg_all = D.pk_bucket[PK_SCAN] / PK_SEG;
     const int nseg = seg1 < nseg_all ? seg1 : nseg_all;
     unsigned long long ph[4] = {0, 0, 0, 0};   // wave cycles: masks, DP, backtrack, emit
-    for (int seg = seg0 + blockIdx.x; seg < nseg; seg += gridDim.x) {
+    for (int it = 0;; ++it) {   // fused: longest segments first from the dequeue; split: the chunk's round robin
+        int seg;
+        if (split) {
+            seg = seg0 + blockIdx.x + it * gridDim.x;
+            if (seg >= nseg) break;
+        } else {
+            seg = pk_next_seg(D, 1, nseg);
+            if (seg < 0) break;
+        }
         // split: the segment's slab in the chunk's array; fused: this wave's own slab
         PkDir *zl = reinterpret_cast<PkDir *>(D.z) + (int64_t)(split ? seg - seg0 : blockIdx.x) * D.z_pk_slab + lane;
         unsigned long long c0 = clock64();
@@ -1387,7 +1409,8 @@ static hipError_t sw_fill(void *p, uint32_t byte, size_t bytes, hipStream_t s) {
 
 int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *stream) {
     hipStream_t s = (hipStream_t)stream;
-    hipError_t e = hipMemsetAsync(D.pk_bucket, 0, (PK_SCAN + 1) * sizeof(int32_t), s);
+    // the key counts and (8 words before them) the packed kernels' segment dequeue counters
+    hipError_t e = hipMemsetAsync(D.pk_bucket - 8, 0, (8 + PK_SCAN + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
     e = sw_fill(D.list, 0xFFu, (size_t)(sel_count(D) + (int64_t)PK_NB * PK_SEG + 1) * sizeof(int32_t), s);
     if (e != hipSuccess) return (int)e;
