@@ -100,15 +100,26 @@ __global__ void __launch_bounds__(256) aln_list_kernel(AlnDev A) {
 // reads whose walk had finished when it was launched, read from a snapshot of `resume` taken on
 // the main stream before the launch -- the live array (and the read's decisions / extension
 // outputs) of a read still walking is written concurrently by the main stream's rounds
-__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t *snap) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= A.n_sr) return;
+// Persistent: the grid holds the resident workgroups the residency cap allows, and each wave
+// takes 64 consecutive reads at a time from a dequeue counter (`next`, zeroed before the launch).
+// With one lane per read over the whole read set the cap left 2.34 rounds of workgroups at
+// configs[1], the last one a third full.
+__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t *snap, int32_t *next) {
+    const int lane = threadIdx.x & 63;
     const bool early = snap != nullptr;
-    if (early && snap[r] < A.seed_off[r + 1]) return;   // its walk was still going at the snapshot
-    AlnPatch req;
-    if (aln_final_read(A, r, &req) && !early) {   // a patch score is needed: the read is replayed later
-        const int slot = atomicAdd(&A.counter[1], 1);
-        if (slot < A.preq_cap) A.preq[slot] = req;
+    for (;;) {
+        int c = 0;
+        if (lane == 0) c = atomicAdd(next, 1);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if ((int64_t)c * 64 >= A.n_sr) break;
+        const int64_t r = (int64_t)c * 64 + lane;
+        if (r >= A.n_sr) continue;
+        if (early && snap[r] < A.seed_off[r + 1]) continue;   // its walk was still going at the snapshot
+        AlnPatch req;
+        if (aln_final_read(A, r, &req) && !early) {   // a patch score is needed: the read is replayed later
+            const int slot = atomicAdd(&A.counter[1], 1);
+            if (slot < A.preq_cap) A.preq[slot] = req;
+        }
     }
 }
 
@@ -243,9 +254,23 @@ int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap) {
     // (default 3: 17.5 -> 13.6 ms at configs[1]; the per-lane region scratch of all resident reads
     // then stays on chip instead of thrashing L2; profiles/r02_alnwg_sweep.txt)
     static const int wgcu = getenv("PRGPU_ALN_FINAL_WG") ? atoi(getenv("PRGPU_ALN_FINAL_WG")) : 3;
+    static int n_cu = 0;
+    if (!n_cu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            n_cu <= 0)
+            n_cu = 256;
+    }
     const unsigned lds = wgcu > 0 ? (unsigned)(160 * 1024 / wgcu) & ~255u : 0u;
-    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A,
-                       early_snap);
+    // the dequeue counter: its own word for the early (side stream) and the late passes
+    int32_t *next = A.counter + (early_snap ? 8 : 9);
+    hipError_t e = hipMemsetAsync(next, 0, 4, (hipStream_t)stream);
+    if (e != hipSuccess) return (int)e;
+    const int64_t chunks = (A.n_sr + 63) / 64;
+    int64_t grid = (int64_t)n_cu * (wgcu > 0 ? wgcu : 8);
+    if (grid > (chunks + 3) / 4) grid = (chunks + 3) / 4;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)grid), dim3(256), lds, (hipStream_t)stream, A, early_snap, next);
     return (int)hipGetLastError();
 }
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, void *stream) {

@@ -8,3 +8,8 @@ timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/${T:-r04_d}_
 rc=$?; echo "bench rc=$rc"; cut -c1-300 gpurun_out/${T:-r04_d}_bench.json; [ $rc -eq 0 ] || exit $rc
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/${T:-r04_d}_prof" -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --no-cpu-baseline > "$GRAFT_REPO_ROOT/gpurun_out/${T:-r04_d}_bench_prof.json" 2>&1)
 echo "prof rc=$?"
+# optional extra bench runs, one per "VAR=value" word in $SWEEP (tuning hooks)
+for kv in $SWEEP; do
+  env "$kv" timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 3 > gpurun_out/${T}_sweep_${kv}.json 2>&1
+  rc=$?; echo "sweep $kv rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
