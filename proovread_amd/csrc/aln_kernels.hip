@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(256) aln_heads_kernel(AlnDev A) {
 }
 
 // ---------------------------------------------------------------- mem_chain2aln
-__global__ void __launch_bounds__(256) aln_walk_kernel(AlnDev A) {
+__global__ void __launch_bounds__(256, 8) aln_walk_kernel(AlnDev A) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     // requested seeds carry SEL_EXT; aln_list_kernel lists them
     if (r < A.n_sr) aln_walk_read(A, r, [](int64_t) {});
