@@ -47,9 +47,61 @@ __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
     }
 }
 
+// hprev (aln_heads_read's links) with one wave per read: the read's chain heads (a seed whose
+// chain differs from its predecessor's) and their (long read, strand) keys are gathered into the
+// wave's LDS with a ballot per 64 seeds, then every head's closest earlier head with its key is
+// found lane-parallel against the LDS list.  The lane-per-read version followed the heads one
+// dependent cnext load at a time and searched its list in HBM scratch: 2.8 ms at configs[1],
+// on the critical path in front of round 0's extension.  Reads with more heads than the LDS list
+// holds take that path on lane 0.
+constexpr int HEADS_CAP = 512;
 __global__ void __launch_bounds__(256) aln_heads_kernel(AlnDev A) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r < A.n_sr) aln_heads_read(A, r);
+    __shared__ int32_t sh_key[4][HEADS_CAP];
+    __shared__ int32_t sh_head[4][HEADS_CAP];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t *hk = sh_key[wv], *hh = sh_head[wv];
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int64_t r = (int64_t)blockIdx.x * 4 + wv; r < A.n_sr; r += (int64_t)gridDim.x * 4) {
+        const int64_t s0 = A.seed_off[r], s1 = A.seed_off[r + 1];
+        int nh = 0;
+        for (int64_t b = s0; b < s1; b += 64) {
+            const int64_t t = b + lane;
+            bool head = false;
+            int key = 0;
+            if (t < s1) {
+                head = t == s0 || A.t_chain[t] != A.t_chain[t - 1];
+                if (head) key = A.t_lr[t] * 2 + (A.t_strand[t] ? 1 : 0);
+            }
+            const unsigned long long m = __ballot(head);
+            const int pos = nh + __popcll(m & below);
+            if (head && pos < HEADS_CAP) {
+                hk[pos] = key;
+                hh[pos] = (int32_t)t;
+            }
+            nh += __popcll(m);
+        }
+        if (nh > HEADS_CAP) {
+            if (lane == 0) aln_heads_read(A, r);
+            continue;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (int c = 0; c < nh; c += 64) {
+            const int i = c + lane;
+            const int key = i < nh ? hk[i] : -1;
+            const int jend = (c + 64 < nh ? c + 64 : nh) - 1;   // heads below the chunk's last one
+            int p = -1;
+            for (int j = 0; j < jend; ++j) {
+                const int kj = hk[j];
+                if (j < i && kj == key) p = hh[j];
+            }
+            if (i < nh) A.hprev[hh[i]] = p;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();   // the list is read before the next read rewrites it
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
 }
 
 // ---------------------------------------------------------------- mem_chain2aln
@@ -232,7 +284,9 @@ int aln_launch_init(const AlnDev &A, void *stream) {
 }
 int aln_launch_heads(const AlnDev &A, void *stream) {
     if (A.n_sr <= 0) return 0;
-    hipLaunchKernelGGL(aln_heads_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), 0, (hipStream_t)stream, A);
+    const int64_t blocks = (A.n_sr + 3) / 4;   // a wave per read (grid-stride beyond 16 k workgroups)
+    hipLaunchKernelGGL(aln_heads_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,
+                       (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
 int aln_launch_list(const AlnDev &A, void *stream) {
