@@ -1340,6 +1340,12 @@ __global__ void __launch_bounds__(256) pk_order_count(SwDev D, SwOptsDev O, int 
         const int64_t t = sel_task(D, q);
         const int k = pk_mode_key(D, O, t, mode);
         if (k >= 0) atomicAdd(&hist[k], 1);
+        else if (mode == 0 && sel_cig(D, t)) {
+            // the CIGAR pass's other kernels: their class as an x_try bit, so the three listing
+            // passes after the packed kernel test one byte (0x40 ring<40>, 0x80 ring<80>, 4 LDS)
+            const int c = glob_class(D, O, t);
+            D.x_try[t] = (uint8_t)(D.x_try[t] | (c == 0 ? 0x40 : (c == 1 ? 0x80 : 4)));
+        }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < PK_NB; k += blockDim.x)
@@ -1429,20 +1435,27 @@ int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *strea
 // right extension try 0/1 (right length), 5/6 CIGAR pass 1 in the register
 // ring (band <= 40 / <= 80), 7 CIGAR passes in the LDS kernel (query length).
 __device__ __forceinline__ int sw_phase_key(const SwDev &D, const SwOptsDev &O, int64_t t, int phase) {
-    const int sid = D.t_sr[t];
-    const int lq = (int)(D.sr_off[sid + 1] - D.sr_off[sid]);
-    const int qbeg = D.t_qbeg[t];
-    const int right = lq - qbeg - D.t_slen[t];
+    // (the task's flags first: most tasks of a listing pass are decided by that one byte, and
+    // their geometry loads are skipped)
     if (!(phase < 4 ? sel_ext(D, t) : sel_cig(D, t))) return -1;
+    const uint8_t x = D.x_try[t];
+    // every extension inside the packed kernel's frame went through it: only N-flagged tasks are left
+    const bool pk_all = O.pk && O.w <= 40 && D.qmax <= PK_QMAX && O.a * D.qmax <= 2047;
     switch (phase) {
-        case 0: return (qbeg > 0 && (pk_ext_key(D, O, t, 0) < 0 || (D.x_try[t] & 8))) ? qbeg : -1;
-        case 1: return (D.x_try[t] & 1) ? qbeg : -1;
-        case 2: return (right > 0 && (pk_ext_key(D, O, t, 1) < 0 || (D.x_try[t] & 16))) ? right : -1;
-        case 3: return (D.x_try[t] & 2) ? right : -1;
-        case 5: return (glob_class(D, O, t) == 0 && pk_key(D, O, t) < 0) ? D.o_qe[t] - D.o_qb[t] : -1;
-        case 6: return glob_class(D, O, t) == 1 ? D.o_qe[t] - D.o_qb[t] : -1;
-        case 7: return (glob_class(D, O, t) == 2 || (D.x_try[t] & 4)) ? D.o_qe[t] - D.o_qb[t] : -1;
-        case 8: return (D.x_try[t] & 0x20) ? D.o_qe[t] - D.o_qb[t] : -1;   // CIGAR overflow pass
+        case 0: case 1: case 2: case 3: {
+            const int side = phase >> 1;
+            if (phase & 1 ? !(x & (1 << side)) : (pk_all && !(x & (8 << side)))) return -1;
+            const int qbeg = D.t_qbeg[t];
+            if (side == 0) return phase == 1 ? qbeg : ((qbeg > 0 && (pk_ext_key(D, O, t, 0) < 0 || (x & 8))) ? qbeg : -1);
+            const int sid = D.t_sr[t];
+            const int right = (int)(D.sr_off[sid + 1] - D.sr_off[sid]) - qbeg - D.t_slen[t];
+            return phase == 3 ? right : ((right > 0 && (pk_ext_key(D, O, t, 1) < 0 || (x & 16))) ? right : -1);
+        }
+        // with the packed kernel, its ordering pass left the class of every other task in x_try
+        case 5: return (O.pk ? (x & 0x40) != 0 : glob_class(D, O, t) == 0) ? D.o_qe[t] - D.o_qb[t] : -1;
+        case 6: return (O.pk ? (x & 0x80) != 0 : glob_class(D, O, t) == 1) ? D.o_qe[t] - D.o_qb[t] : -1;
+        case 7: return ((x & 4) || (!O.pk && glob_class(D, O, t) == 2)) ? D.o_qe[t] - D.o_qb[t] : -1;
+        case 8: return (x & 0x20) ? D.o_qe[t] - D.o_qb[t] : -1;   // CIGAR overflow pass
         default: return -1;
     }
 }
