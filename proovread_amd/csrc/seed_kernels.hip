@@ -18,8 +18,14 @@
 
 namespace prgpu {
 
-constexpr int SEED_WAVES = 4;          // waves (reads in flight) per workgroup
-constexpr int SEED_LMAX = 1024;        // LDS start offsets per wave: reads <= 1024 bases
+#ifndef SEED_WAVES_DEF   // (tuning builds: tools/probe/build_variant.sh)
+#define SEED_WAVES_DEF 4
+#endif
+#ifndef SEED_LMAX_DEF
+#define SEED_LMAX_DEF 1024
+#endif
+constexpr int SEED_WAVES = SEED_WAVES_DEF;   // waves (reads in flight) per workgroup
+constexpr int SEED_LMAX = SEED_LMAX_DEF;     // LDS start offsets per wave: reads <= 1024 bases
 #ifndef SEED_MINB
 #define SEED_MINB 4
 #endif
