@@ -149,11 +149,20 @@ __global__ void __launch_bounds__(PIPE_THREADS) pipe_binfilter_kernel(PipeDev P,
                 const int sid = P.t_sr[t];
                 const int ls = (int)(P.sr_off[sid + 1] - P.sr_off[sid]);
                 long md = 0;
-                for (int k = 0; k < n; ++k) {
-                    const uint32_t op = cg[k] & 15u;
-                    if (op == 0u || op == 2u) md += cg[k] >> 4;
+                uint32_t c_first = 0u, c_last = 0u;
+                for (int k0 = 0; k0 < n; k0 += 8) {   // 8 independent loads in flight per step
+                    uint32_t v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v[u] = k0 + u < n ? cg[k0 + u] : 0u;
+                    if (k0 == 0) c_first = v[0];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const uint32_t op = v[u] & 15u;
+                        if (k0 + u < n && (op == 0u || op == 2u)) md += v[u] >> 4;
+                        if (k0 + u == n - 1) c_last = v[u];
+                    }
                 }
-                const bool clipped = n > 0 && ((cg[0] & 15u) == 4u || (cg[n - 1] & 15u) == 4u);
+                const bool clipped = n > 0 && ((c_first & 15u) == 4u || (c_last & 15u) == 4u);
                 const long len = (ls == 0 || clipped) ? md : ls;
                 P.flen[t] = (int32_t)len;
                 if (len > 0) {

@@ -1224,7 +1224,9 @@ extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_param
         P.flen = c->pb[7].as<int32_t>();
         P.flst = c->pb[8].as<double>();
         P.flsti = c->pb[9].as<int32_t>();
-        int e = pipe_binfilter_launch(P, o->bin_size, o->bin_length, (int)max_bins, grid, (void *)c->stream);
+        // (latency-bound, a few KB of LDS per workgroup: 8 workgroups per CU)
+        const int grid_f = c->n_lr < c->n_cu * 8 ? c->n_lr : c->n_cu * 8;
+        int e = pipe_binfilter_launch(P, o->bin_size, o->bin_length, (int)max_bins, grid_f, (void *)c->stream);
         if (e) return set_error(PR_ERR_HIP, "-b/-l filter kernel: %s", hipGetErrorString((hipError_t)e));
     }
     int e = pipe_launch(P, grid, (void *)c->stream, c->pipe_sort_cap * 8);
