@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
 // on the critical path in front of round 0's extension.  Reads with more heads than the LDS list
 // holds take that path on lane 0.
 constexpr int HEADS_CAP = 512;
-__global__ void __launch_bounds__(256) aln_heads_kernel(AlnDev A) {
+__global__ void __launch_bounds__(256) aln_heads_kernel(AlnDev A, int cap) {
     __shared__ int32_t sh_key[4][HEADS_CAP];
     __shared__ int32_t sh_head[4][HEADS_CAP];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -74,13 +74,13 @@ __global__ void __launch_bounds__(256) aln_heads_kernel(AlnDev A) {
             }
             const unsigned long long m = __ballot(head);
             const int pos = nh + __popcll(m & below);
-            if (head && pos < HEADS_CAP) {
+            if (head && pos < cap) {
                 hk[pos] = key;
                 hh[pos] = (int32_t)t;
             }
             nh += __popcll(m);
         }
-        if (nh > HEADS_CAP) {
+        if (nh > cap) {
             if (lane == 0) aln_heads_read(A, r);
             continue;
         }
@@ -285,8 +285,11 @@ int aln_launch_init(const AlnDev &A, void *stream) {
 int aln_launch_heads(const AlnDev &A, void *stream) {
     if (A.n_sr <= 0) return 0;
     const int64_t blocks = (A.n_sr + 3) / 4;   // a wave per read (grid-stride beyond 16 k workgroups)
+    // PRGPU_HEADS_CAP (tests): a smaller LDS list, so that reads take the lane-0 path sooner
+    const int cap_env = getenv("PRGPU_HEADS_CAP") ? atoi(getenv("PRGPU_HEADS_CAP")) : HEADS_CAP;
+    const int cap = cap_env > 0 && cap_env < HEADS_CAP ? cap_env : HEADS_CAP;
     hipLaunchKernelGGL(aln_heads_kernel, dim3((unsigned)(blocks < 16384 ? blocks : 16384)), dim3(256), 0,
-                       (hipStream_t)stream, A);
+                       (hipStream_t)stream, A, cap);
     return (int)hipGetLastError();
 }
 int aln_launch_list(const AlnDev &A, void *stream) {

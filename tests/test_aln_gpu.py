@@ -59,6 +59,22 @@ def test_bwa_mode_matches_oracle(finish, err):
         assert any(f & 0x100 for v in got.values() for (_, _, _, _, _, f, *_r) in v)
 
 
+def test_bwa_mode_heads_lane_path(monkeypatch):
+    """aln_heads_kernel's lane-0 path (reads with more chain heads than the wave's LDS list,
+    forced here with a list of 3): the same alignments as the oracle"""
+    import cpu_chain
+    from proovread_amd import _abi, sw
+    d = _data(43, 0.15, False)
+    heads = np.unique(d.t_sr.astype(np.int64) * 65536 + d.t_chain) >> 16
+    assert (np.bincount(heads) > 3).sum() > 100   # many reads take the lane path
+    monkeypatch.setenv("PRGPU_HEADS_CAP", "3")
+    res = sw.run(d.sw_input(), sw.default_opts(False), ctx=_abi.default_context())
+    want = cpu_chain.bwa_alignments(d, "bwa-sr")
+    got = _by_read(res, d)
+    assert all(got.get(r, []) == want[r] for r in range(d.n_sr))
+    assert res.n == sum(len(v) for v in want) > 0
+
+
 def test_bwa_mode_seed_order_and_empty_reads():
     """reads without seeds, and a batch whose seeds are not grouped by read, fail loudly"""
     from proovread_amd import _abi, sw
