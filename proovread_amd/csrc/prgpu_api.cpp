@@ -134,7 +134,7 @@ enum SeedBufId {
     SI_TEXT, SI_CSTART, SI_CBLK, SI_LROFF, SI_KOFF, SI_KPOS, SI_KEXT, SI_CNT0,
     SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SB_NEXT, SB_PRE, SB_DENSE,
     SX_LRSEQ, SX_KEY0, SX_KEY1, SX_VAL0, SX_KC, SX_CNTPTR, SX_TEMP, SI_KSPLIT, SX_VAL1, SX_KCC, SX_KOFFC, SX_KCUR,
-    SB_DP, SI_TEXT4, SD_COUNT
+    SB_DP, SI_TEXT4, SB_ORDER, SD_COUNT
 };
 // the exact-parity layout's exchange (pr_aln_exchange, owned batches): bounds, sort keys and
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
@@ -2026,7 +2026,20 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         K.n_list = 0;
         K.out0 = r0;
         K.n_sr = r1;
-        const int32_t start = (int32_t)r0;
+        int32_t start = (int32_t)r0;
+        // PRGPU_SEED_LPT=1: the chunk's reads costliest first (seed_order_launch).  Measured at
+        // configs[1]: 312.5 against 306.2 ms in read order (the batches' lane phase grew more than
+        // the tail shrank), so read order stays the default
+        const char *lpt = getenv("PRGPU_SEED_LPT");
+        if (lpt && lpt[0] == '1') {
+            int32_t *order = nullptr;
+            if ((rc = D[SB_ORDER].ensure(seed_order_bytes(r1 - r0)))) return rc;
+            int eo = seed_order_launch(K, r0, r1 - r0, D[SB_ORDER].p, &order, (void *)s);
+            if (eo) return set_error(PR_ERR_HIP, "seed order: %s", hipGetErrorString((hipError_t)eo));
+            K.rlist = order;
+            K.n_list = r1 - r0;
+            start = 0;
+        }
         HIPCHK(hipMemcpyAsync(K.next, &start, 4, hipMemcpyHostToDevice, s));
         int e = seed_batch_launch(K, (void *)s);
         if (e) return set_error(PR_ERR_HIP, "seed kernel: %s", hipGetErrorString((hipError_t)e));

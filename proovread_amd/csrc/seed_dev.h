@@ -33,6 +33,11 @@ struct SeedDev {
 
 int seed_launch(const SeedDev &D, void *stream);         // pass 2: one wave per read of rlist
 int seed_batch_launch(const SeedDev &D, void *stream);   // pass 1: 64 reads per wave, lane per read
+// pass 1's read order, costliest first: a per-read cost estimate (the summed occurrence counts of
+// its 12-mers, every second start) sorted descending -> order[0 .. n) (reads r0 .. r0 + n).
+// buf: seed_order_bytes(n) bytes of device scratch
+size_t seed_order_bytes(int64_t n);
+int seed_order_launch(const SeedDev &D, int64_t r0, int64_t n, void *buf, int32_t **order, void *stream);
 // resident waves per CU of the seeding kernel (= scratch slots per CU)
 int seed_slots_per_cu();
 // dense task list: out[pre[i] + j] = slots[i * cap + j] for j < n_out[i]

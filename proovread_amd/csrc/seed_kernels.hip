@@ -13,6 +13,8 @@
 // flags and no tasks.
 #include <hip/hip_runtime.h>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 #include "seed_core.h"
 #include "seed_dev.h"
 
@@ -340,6 +342,62 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
         }
         __threadfence_block();
     }
+}
+
+// Pass 1's tail: a wave maps 64 reads in lock-step (its time is its slowest lane's read) and the
+// ~7.2 k batches of configs[1] fill the 4,096 resident waves 1.75 times, so the last batches ran
+// with a quarter of the waves idle and the waves' busy time averaged 73 % of the launch.  Mapping
+// the reads costliest first (longest-processing-time order) puts similar reads in a batch and
+// the cheap batches at the end.  The estimate: every second 12-mer start's occurrence count in
+// the index (capped at 1024), summed; reads with N bases only lose those starts.  Measured slower
+// at configs[1] (312.5 vs 306.2 ms): opt-in only (PRGPU_SEED_LPT=1, pr_seed_gpu_map).
+__global__ void __launch_bounds__(256) seed_cost_kernel(seedc::IndexView V, const uint8_t *sr_seq, const int64_t *sr_off,
+                                                        int64_t r0, int64_t n, uint32_t *key, int32_t *val) {
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = r0 + k;
+        const int64_t o = sr_off[i];
+        const int len = (int)(sr_off[i + 1] - o);
+        uint32_t code = 0u, cost = 0u;
+        int valid = 0;
+        for (int p = 0; p < len; ++p) {
+            const uint32_t c = sr_seq[o + p];
+            if (c > 3u) {
+                valid = 0;
+                continue;
+            }
+            code = ((code << 2) | c) & (seedc::NK - 1u);
+            if (++valid >= seedc::KI && (p & 1) == 0) {
+                const uint64_t m = V.koff[code + 1] - V.koff[code];
+                cost += m < 1024u ? (uint32_t)m : 1024u;
+            }
+        }
+        key[k] = 0xFFFFFFFFu - cost;   // ascending sort = costliest first
+        val[k] = (int32_t)i;
+    }
+}
+size_t seed_order_bytes(int64_t n) {
+    size_t tb = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int32_t *)nullptr,
+                                    (int32_t *)nullptr, (size_t)(n > 0 ? n : 1), 0u, 32u, (hipStream_t)0);
+    return (size_t)(n > 0 ? n : 1) * 16 + ((tb + 255) & ~(size_t)255) + 256;
+}
+int seed_order_launch(const SeedDev &D, int64_t r0, int64_t n, void *buf, int32_t **order, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const size_t n1 = (size_t)(n > 0 ? n : 1);
+    uint32_t *k0 = (uint32_t *)buf, *k1 = k0 + n1;
+    int32_t *v0 = (int32_t *)(k1 + n1), *v1 = v0 + n1;
+    void *temp = (void *)(((uintptr_t)(v1 + n1) + 255) & ~(uintptr_t)255);
+    size_t tb = 0;
+    (void)rocprim::radix_sort_pairs(nullptr, tb, k0, k1, v0, v1, n1, 0u, 32u, s);
+    int64_t grid = (n + 255) / 256;
+    grid = grid < 4096 ? (grid > 0 ? grid : 1) : 4096;
+    hipLaunchKernelGGL(seed_cost_kernel, dim3((unsigned)grid), dim3(256), 0, s, D.V, D.sr_seq, D.sr_off, r0, n, k0, v0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    // (stable LSD sort: equal estimates keep read order)
+    if ((e = rocprim::radix_sort_pairs(temp, tb, k0, k1, v0, v1, (size_t)n, 0u, 32u, s)) != hipSuccess) return (int)e;
+    *order = v1;
+    return 0;
 }
 
 int seed_slots_per_cu() {

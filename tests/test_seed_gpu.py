@@ -136,6 +136,24 @@ def test_gpu_seeding_in_output_chunks(monkeypatch):
         assert seed._count(ix.L, ctx) == len(want)
 
 
+@pytest.mark.gpu
+def test_gpu_seeding_costliest_first_order(monkeypatch):
+    """Pass 1 over the reads sorted costliest first (the opt-in PRGPU_SEED_LPT=1 order): the
+    same seeds and flags as read order."""
+    from proovread_amd import _abi
+    d, ss, so_ = _data(12)
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    ix.to_gpu(_abi.default_context())
+    for finish in (False, True):
+        o = seed.default_opts(finish)
+        monkeypatch.setenv("PRGPU_SEED_LPT", "0")
+        want, wst = ix.map_gpu(ss, so_, o, allow_flagged=True)
+        monkeypatch.setenv("PRGPU_SEED_LPT", "1")
+        got, st = ix.map_gpu(ss, so_, o, allow_flagged=True)
+        assert np.array_equal(st, wst) and np.array_equal(got, want)
+        assert len(want) > 2 * (len(so_) - 1)
+
+
 def _oracle_data():
     """Six 1.5 kb long reads with indels, a repeat shared by three of them and N bases;
     41 short reads (substitutions, reverse strands, one from the repeat)."""
