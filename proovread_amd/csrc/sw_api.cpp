@@ -329,6 +329,18 @@ static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {
     return A;
 }
 
+// direction slabs of the band-80 ring kernel when it runs beside the fused packed CIGAR kernel
+// (sw_launch_global's side path): after the packed kernel's slabs in SB_Z; null when SB_Z has no
+// room for both (split packed kernel, or PRGPU_RING80_SIDE=0)
+static void *ring_side_z(const SwResident &r, const SwDev &D, int grid_pk, int grid_w) {
+    const char *e = getenv("PRGPU_RING80_SIDE");
+    if ((e && e[0] == '0') || D.pk_chunk > 0) return nullptr;
+    const size_t pk = ((size_t)D.z_pk_slab * sizeof(PkDir) * grid_pk + 255) & ~(size_t)255;
+    const size_t ring = (size_t)D.z_ring_slab * 4 * grid_w;
+    if (!r.buf[SB_Z] || r.cap[SB_Z] < pk + ring) return nullptr;
+    return (uint8_t *)r.buf[SB_Z] + pk;
+}
+
 // the side stream (and its events) of the bwa-mode rounds
 static int side_stream(SwResident &r) {
     if (r.side) return 0;
@@ -510,8 +522,10 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
     if (r.n_aln) {
         if ((rc = pk_prepare(c, r, D, O))) return rc;
+        if ((rc = side_stream(r))) return rc;
         e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6),
-                             (void *)ctx_event(c, 7), true);
+                             (void *)ctx_event(c, 7), true, r.side, r.side_ev[0], r.side_ev[2],
+                             ring_side_z(r, D, grid_pk, grid_w), r.side_ev[1]);
         if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     }
     unsigned long long sp[2] = {0, 0};
@@ -634,6 +648,11 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     size_t zb = (size_t)D.z_slab * grid_g > (size_t)D.z_ring_slab * 4 * grid_w
                     ? (size_t)D.z_slab * grid_g : (size_t)D.z_ring_slab * 4 * grid_w;
     if ((size_t)D.z_pk_slab * sizeof(PkDir) * grid_pk > zb) zb = (size_t)D.z_pk_slab * sizeof(PkDir) * grid_pk;
+    if (O.pk) {   // the band-80 ring kernel's slabs after the packed kernel's (run beside it, ring_side_z)
+        const size_t both = (((size_t)D.z_pk_slab * sizeof(PkDir) * grid_pk + 255) & ~(size_t)255) +
+                            (size_t)D.z_ring_slab * 4 * grid_w;
+        if (both > zb) zb = both;
+    }
     int rc;
     if ((rc = ensure(r, SB_Z, zb))) return rc;
     D.z = (uint8_t *)r.buf[SB_Z];
@@ -655,8 +674,9 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
 
     HIPCHK(hipEventRecord(ctx_event(c, 3), s));
     if ((rc = pk_prepare(c, r, D, O))) return rc;
+    if ((rc = side_stream(r))) return rc;
     e = sw_launch_global(D, O, grid_w, grid_pk, grid_g, lds_glob, (void *)s, (void *)ctx_event(c, 6), (void *)ctx_event(c, 7),
-                         true);
+                         true, r.side, r.side_ev[0], r.side_ev[2], ring_side_z(r, D, grid_pk, grid_w), r.side_ev[1]);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     // CIGARs longer than their slots: recompute those tasks into the spill area
     unsigned long long sp[2] = {0, 0};

@@ -139,8 +139,11 @@ struct SwPtrs {
 int sw_launch_order(const SwDev &D, const SwOptsDev &O, int phase, int32_t *out, void *stream);
 int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, void *stream,
                      SwEvPool *evp = nullptr);
+// side / ev_fork / ev_join / z_side (optional): the band-80 ring kernel's tasks listed and run on
+// the side stream beside the packed kernel, with its own direction slabs at z_side
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
-                     void *stream, void *ev_a, void *ev_b, bool pk_ordered = false);
+                     void *stream, void *ev_a, void *ev_b, bool pk_ordered = false, void *side = nullptr,
+                     void *ev_fork = nullptr, void *ev_join = nullptr, void *z_side = nullptr, void *ev_mid = nullptr);
 int sw_launch_pk_order(const SwDev &D, const SwOptsDev &O, int mode, void *stream);
 int sw_pk_bt_occupancy(int win);
 int sw_launch_lds(const SwDev &D, const SwOptsDev &O, int grid, int lds, void *stream);

@@ -1593,11 +1593,31 @@ int sw_launch_extend(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
     return (int)hipGetLastError();
 }
 int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int grid_pk, int grid_lds, int lds,
-                     void *stream, void *ev_a, void *ev_b, bool pk_ordered) {
+                     void *stream, void *ev_a, void *ev_b, bool pk_ordered, void *side, void *ev_fork, void *ev_join,
+                     void *z_side, void *ev_mid) {
     hipStream_t s = (hipStream_t)stream;
     int rc;
+    // band-80 tasks beside the packed kernel: their class is known from the packed ordering pass
+    // (x_try 0x80), their list goes to D.perm and their direction slabs to z_side; the main stream
+    // waits for them before its next listing pass (which reuses the bucket counts)
+    // (the packed kernel is launched once the band-80 list is made, so that the dispatcher takes
+    // the ring kernel's workgroups beside the packed kernel's instead of after them)
+    const bool ring80_side = O.pk && D.pk_chunk <= 0 && side && ev_fork && ev_join && ev_mid && z_side && D.perm;
     if (O.pk) {
         if (!pk_ordered && (rc = sw_launch_pk_order(D, O, 0, stream))) return rc;
+        if (ring80_side) {
+            hipError_t e = hipEventRecord((hipEvent_t)ev_fork, s);
+            if (e == hipSuccess) e = hipStreamWaitEvent((hipStream_t)side, (hipEvent_t)ev_fork, 0);
+            if (e != hipSuccess) return (int)e;
+            SwDev D6 = D;
+            D6.list = D.perm;
+            D6.z = (uint8_t *)z_side;
+            if ((rc = sw_launch_order(D6, O, 6, D6.list, side))) return rc;
+            if ((e = hipEventRecord((hipEvent_t)ev_mid, (hipStream_t)side)) != hipSuccess) return (int)e;
+            hipLaunchKernelGGL(sw_global_ring_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, (hipStream_t)side, D6, O);
+            if ((e = hipEventRecord((hipEvent_t)ev_join, (hipStream_t)side)) != hipSuccess) return (int)e;
+            if ((e = hipStreamWaitEvent(s, (hipEvent_t)ev_mid, 0)) != hipSuccess) return (int)e;
+        }
         if (ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
         if (D.pk_chunk <= 0) {   // fused: DP and backtrack in one kernel, a slab per resident wave
             // (backtrack window: 8 rows, or 16 with PRGPU_PK_WIN=16)
@@ -1623,13 +1643,19 @@ int sw_launch_global(const SwDev &D, const SwOptsDev &O, int grid_waves, int gri
             }
         }
         if (ev_b) (void)hipEventRecord((hipEvent_t)ev_b, s);
+        if (ring80_side) {
+            hipError_t e = hipStreamWaitEvent(s, (hipEvent_t)ev_join, 0);
+            if (e != hipSuccess) return (int)e;
+        }
     }
     if ((rc = sw_launch_order(D, O, 5, D.list, stream))) return rc;
     if (!O.pk && ev_a) (void)hipEventRecord((hipEvent_t)ev_a, s);
     hipLaunchKernelGGL(sw_global_ring_kernel<40>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
     if (!O.pk && ev_b) (void)hipEventRecord((hipEvent_t)ev_b, s);
-    if ((rc = sw_launch_order(D, O, 6, D.list, stream))) return rc;
-    hipLaunchKernelGGL(sw_global_ring_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
+    if (!ring80_side) {
+        if ((rc = sw_launch_order(D, O, 6, D.list, stream))) return rc;
+        hipLaunchKernelGGL(sw_global_ring_kernel<80>, dim3(grid_waves), dim3(SW_WAVE), 0, s, D, O);
+    }
     if ((rc = sw_launch_order(D, O, 7, D.list, stream))) return rc;
     return sw_launch_lds(D, O, grid_lds, lds, stream);
 }
