@@ -72,7 +72,8 @@ int aln_launch_heads(const AlnDev &A, void *stream);
 // the seeds flagged SEL_EXT -> tlist, their count -> counter[0] (add to it)
 int aln_launch_list(const AlnDev &A, void *stream);
 // early: only reads whose walk has finished, patch requests not recorded (the late pass replays)
-int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap);
+// complement (with early_snap): the reads the early pass skips, beside it
+int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap, bool complement = false);
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t pool_stride, void *stream);
 // CIGAR slots of the reported tasks: slot[t] = cig_slot_ops(lq) or 0 -> exclusive prefix (n+1)
 int aln_launch_cig_slots(const AlnDev &A, int64_t *slot_prefix, int64_t *tmp_in, void *temp, size_t temp_bytes,

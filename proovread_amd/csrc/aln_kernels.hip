@@ -156,7 +156,10 @@ __global__ void __launch_bounds__(256) aln_list_kernel(AlnDev A) {
 // takes 64 consecutive reads at a time from a dequeue counter (`next`, zeroed before the launch).
 // With one lane per read over the whole read set the cap left 2.34 rounds of workgroups at
 // configs[1], the last one a third full.
-__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t *snap, int32_t *next) {
+// complement: the reads the early pass does NOT take (still walking at the snapshot), run on the
+// main stream beside the early pass once every walk is done (disjoint reads); no patch requests
+// are recorded there either (the late pass replays what is left)
+__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t *snap, int32_t *next, int complement) {
     const int lane = threadIdx.x & 63;
     const bool early = snap != nullptr;
     for (;;) {
@@ -166,7 +169,7 @@ __global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t 
         if ((int64_t)c * 64 >= A.n_sr) break;
         const int64_t r = (int64_t)c * 64 + lane;
         if (r >= A.n_sr) continue;
-        if (early && snap[r] < A.seed_off[r + 1]) continue;   // its walk was still going at the snapshot
+        if (early && (snap[r] < A.seed_off[r + 1]) != (complement != 0)) continue;   // (not) walking at the snapshot
         AlnPatch req;
         if (aln_final_read(A, r, &req) && !early) {   // a patch score is needed: the read is replayed later
             const int slot = atomicAdd(&A.counter[1], 1);
@@ -304,7 +307,7 @@ int aln_launch_walk(const AlnDev &A, void *stream) {
     hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
-int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap) {
+int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap, bool complement) {
     if (A.n_sr <= 0) return 0;
     // tuning hook: PRGPU_ALN_FINAL_WG=k caps the resident workgroups per CU at k (dynamic LDS),
     // i.e. the reads whose region scratch is live at once
@@ -320,14 +323,15 @@ int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap) {
     }
     const unsigned lds = wgcu > 0 ? (unsigned)(160 * 1024 / wgcu) & ~255u : 0u;
     // the dequeue counter: its own word for the early (side stream) and the late passes
-    int32_t *next = A.counter + (early_snap ? 8 : 9);
+    int32_t *next = A.counter + (early_snap ? (complement ? 10 : 8) : 9);
     hipError_t e = hipMemsetAsync(next, 0, 4, (hipStream_t)stream);
     if (e != hipSuccess) return (int)e;
     const int64_t chunks = (A.n_sr + 63) / 64;
     int64_t grid = (int64_t)n_cu * (wgcu > 0 ? wgcu : 8);
     if (grid > (chunks + 3) / 4) grid = (chunks + 3) / 4;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)grid), dim3(256), lds, (hipStream_t)stream, A, early_snap, next);
+    hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)grid), dim3(256), lds, (hipStream_t)stream, A, early_snap, next,
+                       complement ? 1 : 0);
     return (int)hipGetLastError();
 }
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, void *stream) {

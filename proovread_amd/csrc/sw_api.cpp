@@ -469,7 +469,12 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         n_list = cnt[0];
     }
     D.tsel = nullptr;
-    if (early) HIPCHK(hipStreamWaitEvent(s, (hipEvent_t)r.side_ev[1], 0));
+    if (early) {   // the reads the early pass skips, beside it (disjoint reads), then join it
+        if (!getenv("PRGPU_BWA_NO_COMPLEMENT") &&
+            (e = aln_launch_final(A, (void *)s, (const int32_t *)r.buf[SB_RSNAP], true)))
+            return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipStreamWaitEvent(s, (hipEvent_t)r.side_ev[1], 0));
+    }
     for (int round = 0;; ++round) {   // final pass; mem_patch_reg global scores in extra rounds
         HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
         if ((e = aln_launch_final(A, (void *)s, nullptr))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
