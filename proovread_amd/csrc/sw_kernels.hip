@@ -1339,6 +1339,7 @@ __global__ void __launch_bounds__(256) pk_order_count(SwDev D, SwOptsDev O, int 
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
         const int64_t t = sel_task(D, q);
         const int k = pk_mode_key(D, O, t, mode);
+        D.perm[q] = k;   // the scatter pass reads the key back instead of recomputing it twice
         if (k >= 0) atomicAdd(&hist[k], 1);
         else if (mode == 0 && sel_cig(D, t)) {
             // the CIGAR pass's other kernels: their class as an x_try bit, so the three listing
@@ -1378,8 +1379,7 @@ __global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O, in
     for (int k = threadIdx.x; k < PK_NB; k += blockDim.x) hist[k] = 0;
     __syncthreads();
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = sel_task(D, q);
-        const int k = pk_mode_key(D, O, t, mode);
+        const int k = D.perm[q];   // (pk_order_count's key of selection entry q)
         if (k >= 0) atomicAdd(&hist[k], 1);
     }
     __syncthreads();
@@ -1387,9 +1387,8 @@ __global__ void __launch_bounds__(256) pk_order_scatter(SwDev D, SwOptsDev O, in
         if (hist[k]) hist[k] = atomicAdd(&D.pk_bucket[k], hist[k]);
     __syncthreads();
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = sel_task(D, q);
-        const int k = pk_mode_key(D, O, t, mode);
-        if (k >= 0) D.list[atomicAdd(&hist[k], 1)] = (int32_t)t;
+        const int k = D.perm[q];
+        if (k >= 0) D.list[atomicAdd(&hist[k], 1)] = (int32_t)sel_task(D, q);
     }
 }
 // Fill of a large buffer with a byte-pattern word (0 / 0xFF..): 16-byte stores over a grid that
