@@ -56,7 +56,7 @@ static const size_t SPILL_OFF = 96;   // in the SB_CELLS buffer: 3 x u64 overflo
 enum AlnBuf {
     SB_CHAIN = 35, SB_SEEDOFF, SB_SEL, SB_EXTF, SB_DEC, SB_RESUME, SB_ACNT, SB_AREG, SB_AIX, SB_PSCORE, SB_NPK,
     SB_FDONE, SB_PREQ, SB_NOUT, SB_OLIST, SB_OFLAG, SB_ATEMP, SB_AOFF, SB_ALIST, SB_AFLAG, SB_PPOOL, SB_GLIST,
-    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_TLIST, SB_CNEXT, SB_HPREV, SB_ABOX, SB_RSNAP, SB_NBUF
+    SB_GKEY0, SB_GKEY1, SB_GCNT, SB_GLROFF, SB_GPIPE, SB_GDOWN, SB_SCANIN, SB_TLIST, SB_CNEXT, SB_HPREV, SB_ABOX, SB_RSNAP, SB_KEYC, SB_NBUF
 };
 static_assert(SB_NBUF <= 80, "SwResident buffer table");
 
@@ -208,7 +208,7 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
     const size_t n4 = (size_t)(nt + 1) * 4;
     for (int id : {SB_QB, SB_QE, SB_RB, SB_RE, SB_SCORE, SB_TRUESC, SB_W, SB_GSCORE, SB_POS, SB_NCIG, SB_STATUS})
         if ((rc = ensure(r, id, n4))) return rc;
-    if ((rc = ensure(r, SB_PERM, (size_t)(nt + 1) * 4)) || (rc = ensure(r, SB_BUCKET, (SW_NBUCKET + 16 + PK_SCAN + 1) * 4)) ||
+    if ((rc = ensure(r, SB_PERM, (size_t)(nt + 1) * 4)) || (rc = ensure(r, SB_KEYC, (size_t)(nt + 1) * 4)) || (rc = ensure(r, SB_BUCKET, (SW_NBUCKET + 16 + PK_SCAN + 1) * 4)) ||
         (rc = ensure(r, SB_X, (size_t)(nt + 1) * 4 * 12)) || (rc = ensure(r, SB_XTRY, (size_t)nt + 1)) ||
         (rc = ensure(r, SB_LIST, (size_t)(nt + 1 + (int64_t)PK_NB * PK_SEG) * 4)))
         return rc;
@@ -615,6 +615,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.cells = (unsigned long long *)r.buf[SB_CELLS];
     D.work = (int32_t *)((char *)r.buf[SB_CELLS] + CELLS_WORK_OFF);
     D.perm = (int32_t *)r.buf[SB_PERM];
+    D.keyc = (int32_t *)r.buf[SB_KEYC];
     D.bucket = (int32_t *)r.buf[SB_BUCKET];
     D.x = (int32_t *)r.buf[SB_X];
     D.x_try = (uint8_t *)r.buf[SB_XTRY];

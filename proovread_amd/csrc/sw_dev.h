@@ -68,6 +68,7 @@ struct SwDev {
     int pk_bt_grid, pk_bt_win; // backtrack kernel: grid (waves), window rows (8 or 16)
     unsigned long long *cells; // [3] canonical DP cells (extension, global, dominant launch), [3..6] pk phase cycles
     int32_t *perm;             // lane -> task order (tasks bucketed by extension lengths)
+    int32_t *keyc;             // [selection] phase keys of the last listing pass (count -> scatter)
     int32_t *bucket;           // [SW_NBUCKET + 1] counting-sort scratch
     int32_t *work;             // dequeue counter for the global kernel
     int32_t *x;                // extension scratch: 2 sides x XF fields x n_task

@@ -1466,6 +1466,7 @@ __global__ void __launch_bounds__(256) sw_order_count(SwDev D, SwOptsDev O, int 
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
         const int64_t t = sel_task(D, q);
         const int k = sw_phase_key(D, O, t, phase);
+        D.keyc[q] = k;   // read back by sw_order_scatter
         if (k >= 0) atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1);
     }
     __syncthreads();
@@ -1500,8 +1501,7 @@ __global__ void __launch_bounds__(256) sw_order_scatter(SwDev D, SwOptsDev O, in
     for (int k = threadIdx.x; k < SW_NBUCKET; k += blockDim.x) hist[k] = 0;
     __syncthreads();
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = sel_task(D, q);
-        const int k = sw_phase_key(D, O, t, phase);
+        const int k = D.keyc[q];   // (sw_order_count's key of selection entry q)
         if (k >= 0) atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1);
     }
     __syncthreads();
@@ -1509,9 +1509,8 @@ __global__ void __launch_bounds__(256) sw_order_scatter(SwDev D, SwOptsDev O, in
         if (hist[k]) hist[k] = atomicAdd(&D.bucket[k], hist[k]);
     __syncthreads();
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < sel_count(D); q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t t = sel_task(D, q);
-        const int k = sw_phase_key(D, O, t, phase);
-        if (k >= 0) out[atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1)] = (int32_t)t;
+        const int k = D.keyc[q];
+        if (k >= 0) out[atomicAdd(&hist[k < SW_NBUCKET ? k : SW_NBUCKET - 1], 1)] = (int32_t)sel_task(D, q);
     }
 }
 
