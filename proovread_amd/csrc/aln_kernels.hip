@@ -202,11 +202,16 @@ __global__ void __launch_bounds__(256) aln_nout64_kernel(const int32_t *nout, in
     for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= n; r += (int64_t)gridDim.x * blockDim.x)
         o[r] = r < n ? nout[r] : 0;
 }
+// 16 lanes per read (a read reports ~20 alignments at configs[1]: one lane per read copied them
+// one dependent pair of loads at a time)
 __global__ void __launch_bounds__(256) aln_compact_kernel(AlnDev A, const int64_t *aoff, int32_t *alist, int32_t *aflag) {
-    for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < A.n_sr; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int sub = (int)(gid & 15);
+    const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> 4;
+    for (int64_t r = gid >> 4; r < A.n_sr; r += stride) {
         const int64_t s0 = A.seed_off[r], o = aoff[r];
         const int n = A.nout[r];
-        for (int i = 0; i < n; ++i) {
+        for (int i = sub; i < n; i += 16) {
             alist[o + i] = A.olist[s0 + i];
             aflag[o + i] = A.oflag[s0 + i];
         }
@@ -382,7 +387,8 @@ int aln_launch_compact(const AlnDev &A, int64_t *aoff, int64_t *tmp_in, int32_t 
     if ((e = rocprim::exclusive_scan(temp, tb, tmp_in, aoff, (int64_t)0, (size_t)A.n_sr + 1, rocprim::plus<int64_t>(),
                                      s)) != hipSuccess)
         return (int)e;
-    if (A.n_sr > 0) hipLaunchKernelGGL(aln_compact_kernel, dim3(grid_of(A.n_sr)), dim3(256), 0, s, A, aoff, alist, aflag);
+    if (A.n_sr > 0)
+        hipLaunchKernelGGL(aln_compact_kernel, dim3(grid_of(16 * (int64_t)A.n_sr)), dim3(256), 0, s, A, aoff, alist, aflag);
     return (int)hipGetLastError();
 }
 
