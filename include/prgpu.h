@@ -66,6 +66,17 @@ int pr_dev_free(pr_ctx *ctx, void *dev);
 /* copies on the context stream; both synchronise */
 int pr_dev_download(pr_ctx *ctx, void *host, const void *dev, int64_t bytes);
 int pr_dev_upload(pr_ctx *ctx, void *dev, const void *host, int64_t bytes);
+/* Device memory the library's buffers hold (every context of the process; not the HIP
+ * runtime's own): bytes now, the peak since the last pr_mem_reset_peak, and per buffer group
+ * ("cns", "pipe", "mask", "seed", "xchg", "lrset", "sw") its bytes now, its own peak and its
+ * bytes at the moment of the total peak.  No reference counterpart (sizing at configs[2] /
+ * configs[3]). */
+typedef struct {
+    char name[16];
+    int64_t cur, peak, at_total_peak;
+} pr_mem_group;
+int pr_mem_stats(int64_t *cur, int64_t *peak, pr_mem_group *groups, int cap, int *n_groups);
+void pr_mem_reset_peak(void);
 
 /* ------------------------------------------------------------------ */
 /* multi-GPU collectives over RCCL (one process per GPU, xGMI).  The reference has no
@@ -84,6 +95,11 @@ int pr_comm_unique_id(uint8_t *id);                        /* id[PR_COMM_ID_BYTE
 int pr_comm_init(pr_ctx *ctx, int world, int rank, const uint8_t *id, pr_comm **out);
 void pr_comm_destroy(pr_comm *c);
 int pr_comm_rank(const pr_comm *c, int *rank, int *world);
+/* every rank passes its local status (0 or a PR_ERR_*): 0 on all ranks only if all were 0;
+ * a rank that failed gets its own code back, the others PR_ERR_ARG.  The multi-rank calls
+ * (pr_aln_exchange, pr_lrset_commit) agree this way before their first data collective, so
+ * an error on one GPU returns on every rank instead of leaving the others in a collective. */
+int pr_comm_agree(pr_comm *c, int local_rc);
 int pr_comm_allreduce_dev(pr_comm *c, const void *dev_in, void *dev_out, int64_t n, int dtype, int op);
 int pr_comm_allreduce_host(pr_comm *c, void *buf, int64_t n, int dtype, int op);
 int pr_comm_barrier(pr_comm *c);
@@ -108,6 +124,9 @@ int pr_comm_allgatherv_dev(pr_comm *c, const void *send, const int64_t *counts, 
 typedef struct pr_comm_group pr_comm_group;
 int pr_comm_group_create(int world, pr_comm_group **out);
 void pr_comm_group_destroy(pr_comm_group *g);
+/* a rank of the in-process group left its collective sequence (an exception in its thread):
+ * the ranks waiting in a collective return PR_ERR_ARG, and so does every later collective */
+void pr_comm_group_abort(pr_comm_group *g);
 int pr_comm_init_local(pr_ctx *ctx, pr_comm_group *g, int rank, pr_comm **out);
 
 /* ------------------------------------------------------------------ */
@@ -431,6 +450,10 @@ int pr_iter_upload(pr_ctx *ctx, const pr_iter_batch *b);
 int pr_iter_upload_gpu_seeds(pr_ctx *ctx, const pr_iter_batch *b);
 int pr_iter_launch(pr_ctx *ctx, const pr_sw_opts *o, const pr_cns_params *p);   /* async */
 int pr_iter_download(pr_ctx *ctx, pr_cns_out *out);   /* consensus outputs, syncs */
+/* the outputs of reads [first, first + n) only (one bam2cns chunk's FASTQ, bam2cns:332-365;
+ * a sample of a configs[3]-size batch): per-read arrays of n entries, out_off / chim_off of
+ * n + 1 counted from the range's first read, pools sized by them; kept / bin_bases NULL */
+int pr_iter_download_range(pr_ctx *ctx, int32_t first, int32_t n, pr_cns_out *out);
 int pr_iter_bounds(pr_ctx *ctx, int32_t *n_lr, int64_t *n_task, pr_cns_bounds *bd);
 /* reported alignments of the last iteration: count, total CIGAR ops, total SEQ bytes (syncs) */
 int pr_iter_alignment_stats(pr_ctx *ctx, int64_t *n_aln, int64_t *sum_ncig, int64_t *sum_lseq);
@@ -475,9 +498,12 @@ typedef struct pr_own_batch {
     int32_t n_sr;                 /* every short read of the task, global ids                 */
     const int64_t *sr_off;        /* [n_sr+1]                                                 */
     const uint8_t *sr_seq;        /* nt4, or NULL when the SW batch holds every short read    */
-    int32_t from_set;             /* 1: reference and qualities from the resident long-read set
-                                   * (pr_lrset_*; ref_seq / lr_qual ignored)                   */
+    int32_t from_set;             /* PR_OWN_FROM_SET: reference and qualities from the resident
+                                   * long-read set (pr_lrset_*; ref_seq / lr_qual ignored);
+                                   * | PR_OWN_RESIDENT_SR: the short reads are the resident ones
+                                   * (pr_srset_load, sr_seq NULL; no upload per task)          */
 } pr_own_batch;
+enum { PR_OWN_FROM_SET = 1, PR_OWN_RESIDENT_SR = 2 };
 int pr_iter_upload_owned(pr_ctx *ctx, const pr_own_batch *b);
 
 /* The resident long-read set: the correction loop's state between tasks -- the current reads
@@ -496,11 +522,15 @@ int pr_iter_upload_owned(pr_ctx *ctx, const pr_own_batch *b);
  * batch (pr_iter_upload_owned) needs comm: the ranks' reads are all-gathered on the device.
  * pr_lrset_download: offsets [n+1] and pools (any may be NULL; map = the mapping reference). */
 enum { PR_LRSET_MAP = 0, PR_LRSET_READS = 1 };
+/* pr_lrset_commit flags: MASK = the masked copy becomes the next mapping reference (a regular
+ * iteration); DRY = every step of the commit (checks, compaction, the ranks' all-gathers into
+ * scratch pools) without replacing the set (bench.py repeats one task on the same input) */
+enum { PR_LRSET_COMMIT_MASK = 1, PR_LRSET_COMMIT_DRY = 2 };
 int pr_lrset_load(pr_ctx *ctx, int32_t n_lr, const int64_t *off, const uint8_t *seq, const uint8_t *qual);
 int pr_lrset_info(pr_ctx *ctx, int32_t *n_lr, int64_t *bases);
 int pr_lrset_index(pr_ctx *ctx, int which);
 int pr_iter_upload_lrset(pr_ctx *ctx, const pr_sw_batch *b);
-int pr_lrset_commit(pr_ctx *ctx, pr_comm *comm, int with_mask);
+int pr_lrset_commit(pr_ctx *ctx, pr_comm *comm, int flags);
 int pr_lrset_download(pr_ctx *ctx, int64_t *off, uint8_t *seq, uint8_t *qual, uint8_t *map);
 /* The resident short reads: the whole short-read input (nt4, in stream order) once; a task's
  * sample -- SeqChunker's chunks are contiguous record ranges (bin/proovread:2085-2102) -- is then

@@ -159,6 +159,29 @@ class DevBuffer:
             pass
 
 
+class MemGroup(C.Structure):
+    _fields_ = [("name", C.c_char * 16), ("cur", C.c_int64), ("peak", C.c_int64), ("at_total_peak", C.c_int64)]
+
+
+def mem_stats() -> dict:
+    """Device memory of the library's buffers (pr_mem_stats): bytes now, the peak since the
+    last mem_reset_peak(), and per buffer group {cur, peak, at_total_peak} in bytes."""
+    L = lib()
+    L.pr_mem_stats.argtypes = [P64, P64, C.POINTER(MemGroup), C.c_int, P32]
+    g = (MemGroup * 16)()
+    cur, peak, n = C.c_int64(), C.c_int64(), C.c_int32()
+    check(L.pr_mem_stats(C.byref(cur), C.byref(peak), g, 16, C.byref(n)), "pr_mem_stats")
+    return {"cur": cur.value, "peak": peak.value,
+            "groups": {g[k].name.decode(): {"cur": g[k].cur, "peak": g[k].peak, "at_total_peak": g[k].at_total_peak}
+                       for k in range(min(n.value, 16))}}
+
+
+def mem_reset_peak() -> None:
+    L = lib()
+    L.pr_mem_reset_peak.restype = None
+    L.pr_mem_reset_peak()
+
+
 _default_ctx = None
 
 

@@ -57,6 +57,13 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
+    # the synthetic-workload generator of the bench and the scale tests (host C, not product)
+    syn_src, syn_out = SRC / "synth.c", PKG / "libprsynth.so"
+    if force or not syn_out.exists() or syn_out.stat().st_mtime < syn_src.stat().st_mtime:
+        cmd = ["gcc", "-O3", "-fPIC", "-shared", "-pthread", "-std=c11", "-Wall", "-o", str(syn_out), str(syn_src)]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
     return OUT
 
 

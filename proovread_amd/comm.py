@@ -214,6 +214,8 @@ def _setup(L):
                                          C.POINTER(C.c_int64)]
     L.pr_comm_group_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     L.pr_comm_group_destroy.argtypes = [C.c_void_p]
+    L.pr_comm_group_abort.argtypes = [C.c_void_p]
+    L.pr_comm_group_abort.restype = None
     L.pr_comm_init_local.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]
     L._comm_ready = True
 
@@ -230,6 +232,12 @@ class LocalGroup:
         h = C.c_void_p()
         _abi.check(self.L.pr_comm_group_create(world, C.byref(h)), "pr_comm_group_create")
         self.h = h
+
+    def abort(self):
+        """A rank left its collective sequence: the ranks waiting in (or later entering) a
+        collective return an error instead of waiting forever (pr_comm_group_abort)."""
+        if getattr(self, "h", None):
+            self.L.pr_comm_group_abort(self.h)
 
     def close(self):
         if getattr(self, "h", None):

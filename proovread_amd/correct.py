@@ -356,6 +356,7 @@ class GpuStages:
             out.bpt, out.bpn = int(st[0]), int(st[1])
         self.device_ms += sum(it.timing())
         self.lrs.commit(comm if exact else None, with_mask=not finish)
+        self.last_iteration = it   # the task's consensus outputs stay readable (tests, drivers)
         return out
 
     def reads(self) -> LongReads:

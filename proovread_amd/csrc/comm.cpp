@@ -46,18 +46,29 @@ struct pr_comm_group {
         std::vector<uint8_t> host;
     };
     std::vector<Slot> slot;
-    void barrier() {
+    bool aborted = false;   // pr_comm_group_abort: a rank left the collective sequence
+    // false once the group is aborted (the waiters are woken; later barriers fail at once)
+    bool barrier() {
         std::unique_lock<std::mutex> l(m);
+        if (aborted) return false;
         const uint64_t g = gen;
         if (++arrived == world) {
             arrived = 0;
             ++gen;
             cv.notify_all();
-        } else {
-            cv.wait(l, [&] { return gen != g; });
+            return true;
         }
+        cv.wait(l, [&] { return gen != g || aborted; });
+        return gen != g;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> l(m);
+        aborted = true;
+        cv.notify_all();
     }
 };
+
+static int group_aborted() { return pr_set_error(PR_ERR_ARG, "in-process group aborted (another rank failed)"); }
 
 struct pr_comm {
     pr_ctx *ctx = nullptr;
@@ -145,6 +156,10 @@ extern "C" int pr_comm_group_create(int world, pr_comm_group **out) {
 
 extern "C" void pr_comm_group_destroy(pr_comm_group *g) { delete g; }
 
+extern "C" void pr_comm_group_abort(pr_comm_group *g) {
+    if (g) g->abort();
+}
+
 extern "C" int pr_comm_init_local(pr_ctx *ctx, pr_comm_group *g, int rank, pr_comm **out) {
     if (!ctx || !g || !out) return pr_set_error(PR_ERR_ARG, "null arg");
     if (rank < 0 || rank >= g->world) return pr_set_error(PR_ERR_ARG, "bad rank");
@@ -174,7 +189,7 @@ static int local_allreduce_host(pr_comm *c, void *buf, int64_t n, int dtype, int
     (void)dtype_of(dtype, &sz);
     pr_comm_group *g = c->grp;
     g->slot[(size_t)c->rank].send = buf;
-    g->barrier();
+    if (!g->barrier()) return group_aborted();
     std::vector<uint8_t> acc((size_t)n * sz);
     if (n) std::memcpy(acc.data(), g->slot[0].send, acc.size());
     for (int r = 1; r < c->world; ++r) {
@@ -184,7 +199,7 @@ static int local_allreduce_host(pr_comm *c, void *buf, int64_t n, int dtype, int
         else if (dtype == PR_DT_I32) reduce_into((int32_t *)acc.data(), (const int32_t *)v, n, op);
         else reduce_into(acc.data(), (const uint8_t *)v, n, op);
     }
-    g->barrier();   // every rank has read every buffer
+    if (!g->barrier()) return group_aborted();   // every rank has read every buffer
     if (n) std::memcpy(buf, acc.data(), acc.size());
     return 0;
 }
@@ -205,17 +220,21 @@ static int local_allreduce_dev(pr_comm *c, const void *dev_in, void *dev_out, in
 // it sits) or the whole send buffer (allgatherv: counts = nullptr)
 static int local_pull(pr_comm *c, const void *send, const int64_t *send_counts, int64_t my_bytes, void *recv,
                       const int64_t *recv_counts) {
+    // every rank reaches both barriers, a local failure included (it is reported after them)
     int rc = local_sync(c);
-    if (rc) return rc;
     pr_comm_group *g = c->grp;
     auto &me = g->slot[(size_t)c->rank];
-    me.send = send;
+    me.send = rc ? nullptr : send;
     me.counts = send_counts;
-    me.n = my_bytes;
-    g->barrier();
+    me.n = rc ? -1 : my_bytes;   // -1: this rank failed, its block is not there
+    if (!g->barrier()) return group_aborted();
     int64_t o = 0;
     for (int r = 0; r < c->world && !rc; ++r) {
         const auto &p = g->slot[(size_t)r];
+        if (p.n < 0) {
+            rc = pr_set_error(PR_ERR_ARG, "in-process collective: another rank failed before it");
+            break;
+        }
         int64_t off = 0, n = p.n;
         if (p.counts) {
             for (int k = 0; k < c->rank; ++k) off += p.counts[k];
@@ -231,7 +250,7 @@ static int local_pull(pr_comm *c, const void *send, const int64_t *send_counts, 
         o += n;
     }
     if (!rc && hipStreamSynchronize(ctx_stream(c->ctx)) != hipSuccess) rc = pr_set_error(PR_ERR_HIP, "stream sync");
-    g->barrier();   // every rank has finished reading the send buffers (always reached)
+    if (!g->barrier()) return rc ? rc : group_aborted();   // every rank has finished reading the send buffers
     return rc;
 }
 
@@ -298,11 +317,11 @@ extern "C" int pr_comm_allgatherv_host(pr_comm *c, const uint8_t *send, int64_t 
     if (c->grp) {   // in-process: host blocks read directly
         pr_comm_group *g = c->grp;
         g->slot[(size_t)c->rank].send = send;
-        g->barrier();
+        if (!g->barrier()) return group_aborted();
         int64_t o = 0;
         for (int r = 0; r < W; o += sz[(size_t)r], ++r)
             if (sz[(size_t)r]) std::memcpy(recv + o, g->slot[(size_t)r].send, (size_t)sz[(size_t)r]);
-        g->barrier();
+        if (!g->barrier()) return group_aborted();
         return 0;
     }
     // in pieces of at most P2P_PIECE bytes per rank (one staging area of world + 1 pieces)
@@ -439,6 +458,20 @@ extern "C" int pr_comm_alltoall_counts(pr_comm *c, const int64_t *send_counts, i
     const int W = c->world;
     std::vector<int64_t> ones((size_t)W, 8);
     return pr_comm_alltoallv_host(c, (const uint8_t *)send_counts, ones.data(), (uint8_t *)recv_counts, ones.data());
+}
+
+// every rank passes its local status; all get 0 only if every rank had 0 (the call every
+// multi-rank entry point makes before its first data collective, so that an error on one rank
+// returns on all of them instead of leaving the others inside a collective)
+extern "C" int pr_comm_agree(pr_comm *c, int local_rc) {
+    if (!c) return local_rc;
+    const std::string msg = local_rc ? pr_last_error() : "";
+    int64_t bad = local_rc != 0;
+    const int rc = pr_comm_allreduce_host(c, &bad, 1, PR_DT_I64, PR_RED_MAX);
+    if (local_rc) return pr_set_error(local_rc, msg.c_str());
+    if (rc) return rc;
+    if (bad) return pr_set_error(PR_ERR_ARG, "another rank failed in this multi-rank call");
+    return 0;
 }
 
 extern "C" int pr_comm_rank(const pr_comm *c, int *rank, int *world) {

@@ -9,6 +9,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -57,10 +58,63 @@ static bool mem_trace() {
     static const bool on = [] { const char *e = std::getenv("PRGPU_MEM_TRACE"); return e && *e && *e != '0'; }();
     return on;
 }
+// per-group accounting behind pr_mem_stats (groups are the DevBuf tags and "sw")
+namespace {
+struct MemGroup {
+    char name[16];
+    int64_t cur, peak, at_peak;
+};
+std::mutex g_mem_mu;
+MemGroup g_mem[16];
+int g_mem_n = 0;
+int64_t g_mem_peak = 0;
+}   // namespace
 void prgpu_mem_note(const char *grp, int id, int64_t delta) {
     const int64_t tot = g_dev_bytes.fetch_add(delta) + delta;
+    {
+        std::lock_guard<std::mutex> lk(g_mem_mu);
+        // "sw CIGAR spill" and the like count under their group's first word
+        char key[16] = {};
+        for (int i = 0; i < 15 && grp[i] && grp[i] != ' '; ++i) key[i] = grp[i];
+        int k = 0;
+        while (k < g_mem_n && std::strcmp(g_mem[k].name, key) != 0) ++k;
+        if (k == g_mem_n && g_mem_n < 16) {
+            std::memcpy(g_mem[k].name, key, 16);
+            g_mem[k].cur = g_mem[k].peak = g_mem[k].at_peak = 0;
+            ++g_mem_n;
+        }
+        if (k < g_mem_n) {
+            g_mem[k].cur += delta;
+            g_mem[k].peak = std::max(g_mem[k].peak, g_mem[k].cur);
+        }
+        if (tot > g_mem_peak) {
+            g_mem_peak = tot;
+            for (int j = 0; j < g_mem_n; ++j) g_mem[j].at_peak = g_mem[j].cur;
+        }
+    }
     if (mem_trace() && delta > 0)
         std::fprintf(stderr, "[prgpu mem] %s[%d] +%.1f MB -> %.2f GB\n", grp, id, delta / 1e6, tot / 1e9);
+}
+
+extern "C" int pr_mem_stats(int64_t *cur, int64_t *peak, pr_mem_group *groups, int cap, int *n_groups) {
+    std::lock_guard<std::mutex> lk(g_mem_mu);
+    if (cur) *cur = g_dev_bytes.load();
+    if (peak) *peak = g_mem_peak;
+    const int n = std::min(g_mem_n, std::max(cap, 0));
+    for (int k = 0; groups && k < n; ++k) {
+        std::memcpy(groups[k].name, g_mem[k].name, 16);
+        groups[k].cur = g_mem[k].cur;
+        groups[k].peak = g_mem[k].peak;
+        groups[k].at_total_peak = g_mem[k].at_peak;
+    }
+    if (n_groups) *n_groups = g_mem_n;
+    return 0;
+}
+
+extern "C" void pr_mem_reset_peak(void) {
+    std::lock_guard<std::mutex> lk(g_mem_mu);
+    g_mem_peak = g_dev_bytes.load();
+    for (int k = 0; k < g_mem_n; ++k) g_mem[k].peak = g_mem[k].at_peak = g_mem[k].cur;
 }
 int prgpu_oom(const char *grp, int id, size_t want) {
     size_t fr = 0, total = 0;
@@ -140,7 +194,7 @@ enum SeedBufId {
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
 // the task's short reads
 // the resident long-read set: pools, the dense offsets of a commit, the commit's staging pools
-enum LrSetBufId { LS_SEQ, LS_QUAL, LS_MAP, LS_OFF, LS_TSEQ, LS_TQUAL, LS_TMAP, LS_SRSEQ, LS_COUNT };
+enum LrSetBufId { LS_SEQ, LS_QUAL, LS_MAP, LS_OFF, LS_TSEQ, LS_TQUAL, LS_TMAP, LS_SRSEQ, LS_GSEQ, LS_GQUAL, LS_GMAP, LS_COUNT };
 enum XchgBufId {
     XB_BOUNDS, XB_KEY0, XB_KEY1, XB_IDX0, XB_IDX1, XB_CNT, XB_OPIN, XB_OPAT, XB_SREC, XB_SCIG, XB_TEMP,
     XB_RREC, XB_RCIG, XB_RCIGAT, XB_GCNT, XB_GCNT64, XB_TASKOFF, XB_ERR, XB_GSR, XB_GSTATUS, XB_GPOS, XB_GSCORE,
@@ -199,6 +253,7 @@ struct pr_ctx {
     bool seed_sr_staged = false;   // SB_SEQ already holds the reads of the next pr_seed_gpu_map
     bool own = false;            // the resident iteration batch is an owned batch (pr_iter_upload_owned)
     bool own_ref_nt4 = false;    // its consensus reference is the SW long-read pool's slice (nt4)
+    bool own_sr_resident = false;   // its short reads are the resident ones (LS_SRSEQ)
     int32_t own_lr0 = 0;
 };
 
@@ -516,7 +571,7 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         // the received wire pool, the ASCII consensus reference of the owned reads
         D.ref_seq = B[CB_REF_SEQ].as<uint8_t>();
         D.ref_nt4 = c->own_ref_nt4 ? 1 : 0;
-        D.seq = c->xb[XB_SR].as<uint8_t>();
+        D.seq = c->own_sr_resident ? c->ls[LS_SRSEQ].as<uint8_t>() : c->xb[XB_SR].as<uint8_t>();
         D.seq_nt4 = 1;
         D.cig = c->xb[XB_RCIG].as<uint32_t>();
         if (c->x_pass) {   // world 1: CIGARs in place in the SW output pool
@@ -679,6 +734,7 @@ static int iter_upload(pr_ctx *c, const pr_iter_batch *b, bool gpu_seeds, const 
                                                 dev_sr, dev_lr)
                        : pr_sw_upload(c, &sb);
     if (rc) return rc;
+    c->x_ready = c->x_pass = false;   // a new SW batch: no exchange of it yet
     HIPCHK(hipSetDevice(c->device));
     c->cns_launched = false;
     c->iter_masked = false;
@@ -777,7 +833,12 @@ extern "C" int pr_sw_upload_gpu_seeds(pr_ctx *c, const pr_sw_batch *b) {
             return set_error(PR_ERR_ARG, "lr_seq NULL: the long reads must be those of the last pr_seed_gpu_index_build");
         dlr = c->sd[SX_LRSEQ].as<uint8_t>();
     }
-    return sw_upload_device_seeds(c, &sb, c->sd[SB_DENSE].as<pr_seed_task>(), c->seed_pre.data(), dsr, dlr);
+    c->x_ready = c->x_pass = false;   // a new SW batch: no exchange of it yet
+    const int rc = sw_upload_device_seeds(c, &sb, c->sd[SB_DENSE].as<pr_seed_task>(), c->seed_pre.data(), dsr, dlr);
+    // the seeding's short-read pool is handed over once: a later batch with the same base count
+    // (another sample, another shard) must not pick it up silently (the next map sets it again)
+    if (!rc && dsr) c->seed_sr_bases = -1;
+    return rc;
 }
 
 // the sender half of the exchange: the reported alignments of the last bwa-mode pr_sw_launch
@@ -866,7 +927,10 @@ extern "C" int pr_aln_exchange(pr_ctx *c, pr_comm *comm, int64_t sr0, const int6
         return 0;
     }
     std::vector<int64_t> nrec, nops;
-    if ((rc = xchg_pack(c, world, sr0, lr_bounds, nrec, nops))) return rc;
+    rc = xchg_pack(c, world, sr0, lr_bounds, nrec, nops);
+    // the pack is local: every rank learns whether all packed before any data moves
+    if (comm) rc = pr_comm_agree(comm, rc);
+    if (rc) return rc;
     std::vector<int64_t> sc_rec((size_t)world), sc_cig((size_t)world), rc_rec((size_t)world), rc_cig((size_t)world);
     for (int r = 0; r < world; ++r) {
         sc_rec[(size_t)r] = nrec[(size_t)r] * (int64_t)sizeof(XRec);
@@ -911,6 +975,7 @@ extern "C" int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64
     for (int k = 0; k < world; ++k) {
         if (!ctxs[k]) return set_error(PR_ERR_ARG, "null context");
         ctxs[k]->x_ready = false;
+        ctxs[k]->x_pass = false;   // the owned launch reads the records copied below
         if ((rc = xchg_pack(ctxs[k], world, sr0[k], lr_bounds, nrec[(size_t)k], nops[(size_t)k]))) return rc;
     }
     for (int k = 0; k < world; ++k) {
@@ -969,7 +1034,8 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     c->total_cols = tl;
     c->has_ref = true;
     c->pipe_ref_ascii = true;
-    c->has_qual = b->lr_qual != nullptr || b->from_set;
+    const bool from_set = (b->from_set & PR_OWN_FROM_SET) != 0, sr_res = (b->from_set & PR_OWN_RESIDENT_SR) != 0;
+    c->has_qual = b->lr_qual != nullptr || from_set;
     c->has_ign = false;
     c->lr_off_host.assign(b->lr_off, b->lr_off + n + 1);
     if (!n) c->lr_off_host.assign(1, 0);
@@ -982,7 +1048,7 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
         c->chim_off[i + 1] = c->chim_off[i] + nb / 2 + 2;
     }
     int64_t set0 = 0;   // from_set: the owned reads' first base in the set
-    if (b->from_set) {
+    if (from_set) {
         if (c->ls_n < 0) return set_error(PR_ERR_ARG, "from_set: no resident long-read set");
         if (b->lr0 < 0 || b->lr0 + n > c->ls_n) return set_error(PR_ERR_ARG, "owned long reads outside the set");
         set0 = c->ls_off[(size_t)b->lr0];
@@ -998,13 +1064,13 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     DevBuf *B = c->cb;
     const size_t n1 = (size_t)n + 1;
     if ((rc = upload(B[CB_LR_OFF], c->lr_off_host.data(), n1, s))) return rc;
-    if (!b->from_set && b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)tl, s))) return rc;
+    if (!from_set && b->lr_qual && (rc = upload(B[CB_REF_QUAL], b->lr_qual, (size_t)tl, s))) return rc;
     // ref_seq / sr_seq NULL: the resident SW batch's long reads (the owned slice, nt4: the mapping
     // reference is the consensus reference) / short reads (every short read of the task) on the device
     SwPtrs sp{};
-    if (((!b->ref_seq && !b->from_set) || !b->sr_seq) && (rc = sw_get_ptrs(c, &sp))) return rc;
-    c->own_ref_nt4 = !b->ref_seq && !b->from_set;
-    if (b->from_set) {   // the set's reads and qualities (the previous task's consensus)
+    if (((!b->ref_seq && !from_set) || (!b->sr_seq && !sr_res)) && (rc = sw_get_ptrs(c, &sp))) return rc;
+    c->own_ref_nt4 = !b->ref_seq && !from_set;
+    if (from_set) {   // the set's reads and qualities (the previous task's consensus)
         if ((rc = B[CB_REF_SEQ].ensure((size_t)tl + 1)) || (rc = B[CB_REF_QUAL].ensure((size_t)tl + 1))) return rc;
         if (tl) {
             HIPCHK(hipMemcpyAsync(B[CB_REF_SEQ].p, c->ls[LS_SEQ].as<uint8_t>() + set0, (size_t)tl, hipMemcpyDeviceToDevice, s));
@@ -1023,7 +1089,12 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
         if (tl) HIPCHK(hipMemcpyAsync(B[CB_REF_SEQ].p, sp.lr + base, (size_t)tl, hipMemcpyDeviceToDevice, s));
     }
     if ((rc = upload(c->xb[XB_SROFF], b->sr_off, (size_t)b->n_sr + 1, s))) return rc;
-    if (b->sr_seq) {
+    c->own_sr_resident = sr_res;
+    if (sr_res) {   // the resident short reads (pr_srset_load) are the task's: read in place
+        if (b->sr_seq) return set_error(PR_ERR_ARG, "PR_OWN_RESIDENT_SR: sr_seq must be NULL");
+        if (c->ss_off.size() != (size_t)b->n_sr + 1 || (b->n_sr && c->ss_off.back() != b->sr_off[b->n_sr]))
+            return set_error(PR_ERR_ARG, "PR_OWN_RESIDENT_SR: the resident short reads (pr_srset_load) differ");
+    } else if (b->sr_seq) {
         if ((rc = upload(c->xb[XB_SR], b->sr_seq, (size_t)b->sr_off[b->n_sr], s))) return rc;
     } else {
         if (sp.n_sr != b->n_sr) return set_error(PR_ERR_ARG, "sr_seq NULL: the SW batch must hold every short read");
@@ -1243,6 +1314,41 @@ extern "C" int pr_iter_download(pr_ctx *c, pr_cns_out *o) {
     HIPCHK(hipMemcpy(err.data(), c->pb[2].p, (size_t)c->n_lr * 4, hipMemcpyDeviceToHost));
     for (int i = 0; i < c->n_lr; ++i)
         if (err[(size_t)i]) return set_error(PR_ERR_CAPACITY, "hand-off of long read %d failed (code %d)", i, err[(size_t)i]);
+    return 0;
+}
+
+extern "C" int pr_iter_download_range(pr_ctx *c, int32_t first, int32_t n, pr_cns_out *o) {
+    // reads [first, first + n) of the last launch: the per-read arrays have n entries, out_off /
+    // chim_off n + 1 entries counted from the range's first read
+    if (!c || !o) return set_error(PR_ERR_ARG, "null arg");
+    if (first < 0 || n < 0 || (int64_t)first + n > c->n_lr) return set_error(PR_ERR_ARG, "read range outside the batch");
+    if (o->kept || o->bin_bases) return set_error(PR_ERR_ARG, "kept / bin_bases: pr_iter_download");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+    if (!c->cns_launched) return set_error(PR_ERR_ARG, "no consensus launch to download");
+    const size_t f = (size_t)first, m = (size_t)n;
+    const int64_t o0 = c->out_off[f], o1 = c->out_off[f + m], h0 = c->chim_off[f], h1 = c->chim_off[f + m];
+    if (o->out_off)
+        for (size_t i = 0; i <= m; ++i) o->out_off[i] = c->out_off[f + i] - o0;
+    if (o->chim_off)
+        for (size_t i = 0; i <= m; ++i) o->chim_off[i] = c->chim_off[f + i] - h0;
+    DevBuf *B = c->cb;
+    int rc;
+    if ((rc = download(o->status, B[CB_STATUS], m, s, f)) || (rc = download(o->seq_len, B[CB_SEQ_LEN], m, s, f)) ||
+        (rc = download(o->trace_len, B[CB_TRACE_LEN], m, s, f)) || (rc = download(o->ncigar, B[CB_NCIGAR], m, s, f)) ||
+        (rc = download(o->nchim, B[CB_NCHIM], m, s, f)) || (rc = download(o->seq, B[CB_O_SEQ], (size_t)(o1 - o0), s, (size_t)o0)) ||
+        (rc = download(o->qual, B[CB_O_QUAL], (size_t)(o1 - o0), s, (size_t)o0)) ||
+        (rc = download(o->trace, B[CB_O_TRACE], (size_t)(o1 - o0), s, (size_t)o0)) ||
+        (rc = download(o->cigar, B[CB_O_CIG], (size_t)(o1 - o0), s, (size_t)o0)) ||
+        (rc = download(o->chim, B[CB_O_CHIM], (size_t)(h1 - h0) * 4, s, (size_t)h0 * 4)))
+        return rc;
+    std::vector<int32_t> err(m + 1, 0);
+    if (c->pipe && m) HIPCHK(hipMemcpyAsync(err.data(), c->pb[2].as<int32_t>() + f, m * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (size_t i = 0; i < m; ++i)
+        if (err[i]) return set_error(PR_ERR_CAPACITY, "hand-off of long read %d failed (code %d)", first + (int)i, err[i]);
     return 0;
 }
 
@@ -1583,33 +1689,50 @@ extern "C" int pr_iter_upload_lrset(pr_ctx *c, const pr_sw_batch *b) {
     ib.sw.n_lr = c->ls_n;
     ib.sw.lr_off = c->ls_off.data();
     ib.sw.lr_seq = nullptr;
-    return iter_upload(c, &ib, true, b->sr_seq ? nullptr : c->sd[SB_SEQ].as<uint8_t>(), c->sd[SX_LRSEQ].as<uint8_t>(),
-                       c->ls[LS_SEQ].as<uint8_t>(), c->ls[LS_QUAL].as<uint8_t>());
+    const int rc = iter_upload(c, &ib, true, b->sr_seq ? nullptr : c->sd[SB_SEQ].as<uint8_t>(),
+                               c->sd[SX_LRSEQ].as<uint8_t>(), c->ls[LS_SEQ].as<uint8_t>(), c->ls[LS_QUAL].as<uint8_t>());
+    if (!rc && !b->sr_seq) c->seed_sr_bases = -1;   // handed over once (as pr_sw_upload_gpu_seeds)
+    return rc;
 }
 
-extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int with_mask) {
-    if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+// pr_lrset_commit's checks on this rank: the launch, the masking, every read's hand-off and
+// consensus status (as pr_iter_download: never silent); fills the per-read status and length
+static int commit_check(pr_ctx *c, int world, bool with_mask, int lr0, int n, std::vector<int32_t> &st,
+                        std::vector<int32_t> &len, std::vector<int32_t> &herr) {
     if (!c->cns_launched || !c->pipe) return set_error(PR_ERR_ARG, "no iteration launch to commit");
     if (with_mask && !c->iter_masked) return set_error(PR_ERR_ARG, "with_mask: no pr_iter_mask launch");
-    int rank = 0, world = 1, rc;
-    if (comm && (rc = pr_comm_rank(comm, &rank, &world))) return rc;
-    const int lr0 = c->own ? c->own_lr0 : 0, n = c->n_lr;
     if (world == 1 && (lr0 != 0 || n != c->ls_n)) return set_error(PR_ERR_ARG, "the batch must hold every long read");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
+    int rc;
     if (with_mask && (rc = mask_check_err(c))) return rc;
-    std::vector<int32_t> st((size_t)n + 1, 0), len((size_t)n + 1, 0), herr((size_t)n + 1, 0);
     if (n) {
         HIPCHK(hipMemcpyAsync(st.data(), c->cb[CB_STATUS].p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(len.data(), c->cb[CB_SEQ_LEN].p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
         HIPCHK(hipMemcpyAsync(herr.data(), c->pb[2].p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
     }
     HIPCHK(hipStreamSynchronize(s));
-    for (int i = 0; i < n; ++i) {   // as pr_iter_download: never silent
+    for (int i = 0; i < n; ++i) {
         if (herr[(size_t)i])
             return set_error(PR_ERR_CAPACITY, "hand-off of long read %d failed (code %d)", lr0 + i, herr[(size_t)i]);
         if (st[(size_t)i]) return set_error(st[(size_t)i], "consensus of long read %d failed (status %d)", lr0 + i, st[(size_t)i]);
     }
+    return 0;
+}
+
+extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int flags) {
+    if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+    int rank = 0, world = 1, rc;
+    if (comm && (rc = pr_comm_rank(comm, &rank, &world))) return rc;
+    if (comm && comm_ctx(comm) != c) return set_error(PR_ERR_ARG, "the communicator belongs to another context");
+    const bool dry = (flags & PR_LRSET_COMMIT_DRY) != 0, with_mask = (flags & PR_LRSET_COMMIT_MASK) != 0;
+    const int lr0 = c->own ? c->own_lr0 : 0, n = c->n_lr;
+    std::vector<int32_t> st((size_t)n + 1, 0), len((size_t)n + 1, 0), herr((size_t)n + 1, 0);
+    // local checks first; with ranks, every rank learns whether all passed before any collective
+    rc = commit_check(c, world, with_mask, lr0, n, st, len, herr);
+    if (world > 1) rc = pr_comm_agree(comm, rc);
+    if (rc) return rc;
+    hipStream_t s = c->stream;
     std::vector<int64_t> doff((size_t)n + 1, 0);
     for (int i = 0; i < n; ++i) doff[(size_t)i + 1] = doff[(size_t)i] + len[(size_t)i];
     const int64_t own = doff[(size_t)n];
@@ -1624,9 +1747,11 @@ extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int with_mask) {
     if (e) return set_error(PR_ERR_HIP, "long-read set compaction: %s", hipGetErrorString((hipError_t)e));
     std::vector<int64_t> off((size_t)c->ls_n + 1, 0);
     if (world == 1) {
-        std::swap(L[LS_SEQ], L[LS_TSEQ]);
-        std::swap(L[LS_QUAL], L[LS_TQUAL]);
-        if (with_mask) std::swap(L[LS_MAP], L[LS_TMAP]);
+        if (!dry) {
+            std::swap(L[LS_SEQ], L[LS_TSEQ]);
+            std::swap(L[LS_QUAL], L[LS_TQUAL]);
+            if (with_mask) std::swap(L[LS_MAP], L[LS_TMAP]);
+        }
         off = doff;
     } else {
         // every rank's owned reads in rank order (= global order: the owners' ranges ascend):
@@ -1649,13 +1774,16 @@ extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int with_mask) {
             k += cnt[(size_t)r];
         }
         const size_t tot = (size_t)off.back();
-        const int ids[3][2] = {{LS_TSEQ, LS_SEQ}, {LS_TQUAL, LS_QUAL}, {LS_TMAP, LS_MAP}};
+        // dry: the same all-gathers into scratch pools, the set unchanged
+        const int ids[3][2] = {{LS_TSEQ, dry ? LS_GSEQ : LS_SEQ}, {LS_TQUAL, dry ? LS_GQUAL : LS_QUAL},
+                               {LS_TMAP, dry ? LS_GMAP : LS_MAP}};
         for (int q = 0; q < (with_mask ? 3 : 2); ++q) {
             if ((rc = L[ids[q][1]].ensure(tot + 1))) return rc;
             if ((rc = pr_comm_allgatherv_dev(comm, L[ids[q][0]].p, bytes.data(), L[ids[q][1]].p))) return rc;
         }
     }
     HIPCHK(hipStreamSynchronize(s));
+    if (dry) return 0;
     c->ls_off = off;
     if (with_mask) c->ls_map_is_reads = false;
     else c->ls_map_is_reads = true;   // the finish task: the reads are their own mapping reference
@@ -2225,6 +2353,7 @@ extern "C" int pr_seed_gpu_phase_ticks(pr_ctx *c, uint64_t *ticks4) {
 SwResident &ctx_sw(pr_ctx *c) { return c->sw; }
 hipStream_t ctx_stream(pr_ctx *c) { return c->stream; }
 int ctx_device(pr_ctx *c) { return c->device; }
+void ctx_sw_batch_changed(pr_ctx *c) { c->x_ready = c->x_pass = false; }
 int ctx_ncu(pr_ctx *c) { return c->n_cu; }
 hipEvent_t ctx_event(pr_ctx *c, int i) { return c->ev[i]; }
 int pr_set_error(int code, const char *msg) { return set_error(code, "%s", msg); }

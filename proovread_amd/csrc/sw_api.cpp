@@ -16,6 +16,7 @@ using namespace prgpu;
 
 // accessors defined in prgpu_api.cpp
 SwResident &ctx_sw(pr_ctx *c);
+void ctx_sw_batch_changed(pr_ctx *c);
 hipStream_t ctx_stream(pr_ctx *c);
 int ctx_device(pr_ctx *c);
 int ctx_ncu(pr_ctx *c);
@@ -134,6 +135,7 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
     HIPCHK(hipSetDevice(ctx_device(c)));
     SwResident &r = ctx_sw(c);
     hipStream_t s = ctx_stream(c);
+    ctx_sw_batch_changed(c);   // an exchange of the previous batch must not be consumed
     int qmax = 1;
     for (int i = 0; i < b->n_sr; ++i) {
         const int64_t l = b->sr_off[i + 1] - b->sr_off[i];

@@ -204,6 +204,56 @@ class Iteration:
         rid = [ids[i] for i in np.repeat(idx, cnt).tolist()]
         return [f"{i}\t{fr}\t{to}\t{x:.15g}" for i, fr, to, x in zip(rid, r[:, 0].tolist(), r[:, 1].tolist(), ratio)]
 
+    def results_range(self, first: int, n: int) -> List[cns.ReadResult]:
+        """results() of reads [first, first + n) only (pr_iter_download_range)."""
+        L = self.L
+        L.pr_iter_download_range.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(_abi.CnsOut)]
+        oo = np.zeros(n + 1, np.int64)
+        co = np.zeros(n + 1, np.int64)
+        _abi.check(L.pr_iter_download_range(self.ctx.h, first, n, C.byref(_abi.CnsOut(out_off=_abi.ptr(oo, C.c_int64),
+                                                                                      chim_off=_abi.ptr(co, C.c_int64)))),
+                   "pr_iter_download_range")
+        cap = int(oo[-1]) + 1
+        a = dict(out_off=oo, status=np.zeros(n + 1, np.int32), seq_len=np.zeros(n + 1, np.int32),
+                 trace_len=np.zeros(n + 1, np.int32), ncigar=np.zeros(n + 1, np.int32), nchim=np.zeros(n + 1, np.int32),
+                 seq=np.zeros(cap, np.uint8), qual=np.zeros(cap, np.uint8), trace=np.zeros(cap, np.uint8),
+                 cigar=np.zeros(cap, np.uint32), chim_off=co, chim=np.zeros(4 * (int(co[-1]) + 1), np.int32))
+        o = _abi.CnsOut()
+        for k, ct in (("out_off", C.c_int64), ("status", C.c_int32), ("seq_len", C.c_int32),
+                      ("trace_len", C.c_int32), ("ncigar", C.c_int32), ("nchim", C.c_int32), ("seq", C.c_uint8),
+                      ("qual", C.c_uint8), ("trace", C.c_uint8), ("cigar", C.c_uint32), ("chim_off", C.c_int64),
+                      ("chim", C.c_int32)):
+            setattr(o, k, _abi.ptr(a[k], ct))
+        _abi.check(L.pr_iter_download_range(self.ctx.h, first, n, C.byref(o)), "pr_iter_download_range")
+        out = []
+        for k in range(n):
+            st = int(a["status"][k])
+            r = cns.ReadResult(f"lr{first + k}", st)
+            if st == 0:
+                o0 = int(oo[k])
+                sl, tl, nc = int(a["seq_len"][k]), int(a["trace_len"][k]), int(a["ncigar"][k])
+                r.seq = a["seq"][o0:o0 + sl].tobytes().decode("latin-1")
+                r.qual = a["qual"][o0:o0 + sl].tobytes().decode("latin-1")
+                r.trace = a["trace"][o0:o0 + tl].tobytes().decode("latin-1")
+                r.cigar = [(int(x >> 4), "MID"[int(x & 15)]) for x in a["cigar"][o0:o0 + nc]]
+                c0, nch = int(co[k]), int(a["nchim"][k])
+                r.chim = [tuple(int(v) for v in row) for row in a["chim"][4 * c0:4 * (c0 + nch)].reshape(-1, 4)]
+            out.append(r)
+        return out
+
+    def results_of(self, reads) -> List[cns.ReadResult]:
+        """results() of the listed reads only."""
+        return [self.results_range(int(i), 1)[0] for i in reads]
+
+    def statuses(self) -> np.ndarray:
+        """Every read's consensus status of the last launch (pr_iter_download_range)."""
+        L = self.L
+        L.pr_iter_download_range.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.POINTER(_abi.CnsOut)]
+        st = np.zeros(max(self.n_lr, 1), np.int32)
+        _abi.check(L.pr_iter_download_range(self.ctx.h, 0, self.n_lr, C.byref(_abi.CnsOut(status=_abi.ptr(st, C.c_int32)))),
+                   "pr_iter_download_range")
+        return st[:self.n_lr]
+
     def results(self) -> List[cns.ReadResult]:
         a = self.download()
         out = []
@@ -295,14 +345,15 @@ class OwnedIteration(Iteration):
 
     def __init__(self, ctx, lo: int, hi: int, lr_off: np.ndarray, ref_seq: Optional[np.ndarray],
                  ref_qual: Optional[np.ndarray], sr: Optional[np.ndarray], sr_off: np.ndarray,
-                 from_set: bool = False):
+                 from_set: bool = False, resident_sr: bool = False):
         """lr_off: every long read's offsets; ref_seq / ref_qual: the consensus reference
         (ASCII, bam2cns --ref) and qualities of all long reads in lr_off's layout (the owned
         slice is uploaded; ref_seq None: the SW batch's long reads, when the mapping reference
         is the consensus reference); sr / sr_off: every short read of the task (nt4), which
         the consensus reads by global id (sr None: the SW batch holds every short read);
         from_set: the reference and qualities are the resident long-read set's (LongReadSet;
-        ref_seq / ref_qual not used)."""
+        ref_seq / ref_qual not used); resident_sr: the short reads are the resident ones
+        (GpuStages.load_short_reads / pr_srset_load; sr must be None): read in place."""
         self.L = _abi.lib()
         _setup(self.L)
         self.ctx = ctx
@@ -326,7 +377,7 @@ class OwnedIteration(Iteration):
         ob.n_sr = len(self._sr_off) - 1
         ob.sr_off = _abi.ptr(self._sr_off, C.c_int64)
         ob.sr_seq = _abi.ptr(self._sr, C.c_uint8)
-        ob.from_set = int(from_set)
+        ob.from_set = (1 if from_set else 0) | (2 if resident_sr else 0)   # PR_OWN_FROM_SET | PR_OWN_RESIDENT_SR
         self._ob = ob
         _abi.check(self.L.pr_iter_upload_owned(ctx.h, C.byref(ob)), "pr_iter_upload_owned")
         self.d = SimpleNamespace(lr_off=self._own_off)
@@ -387,10 +438,12 @@ class LongReadSet:
         _abi.check(self.L.pr_lrset_index(self.ctx.h, int(which)), "pr_lrset_index")
         return seed._last_ms(self.L.pr_seed_gpu_index_last_ms, self.ctx)
 
-    def commit(self, comm=None, with_mask: bool = False):
+    def commit(self, comm=None, with_mask: bool = False, dry: bool = False):
         """Every read's consensus (with_mask: and its masked copy as the next mapping reference)
-        replaces the set's; comm: the owned batches of all ranks, all-gathered on the device."""
-        _abi.check(self.L.pr_lrset_commit(self.ctx.h, comm.h if comm is not None else None, int(with_mask)),
+        replaces the set's; comm: the owned batches of all ranks, all-gathered on the device.
+        dry: every step of the commit without replacing the set (PR_LRSET_COMMIT_DRY)."""
+        flags = (1 if with_mask else 0) | (2 if dry else 0)
+        _abi.check(self.L.pr_lrset_commit(self.ctx.h, comm.h if comm is not None else None, flags),
                    "pr_lrset_commit")
 
 

@@ -182,6 +182,69 @@ def simulate(seed: int, genome_len: int, n_lr: int, lr_len: int, sr_cov: float,
                    qbeg[order].astype(np.int32), rbeg[order].astype(np.int32), best_len[order].astype(np.int32))
 
 
+_SYNTH = None
+
+
+def _synth_lib():
+    """libprsynth.so (csrc/synth.c, built by build.py next to libprgpu.so): the host-thread
+    generator behind simulate_reads."""
+    global _SYNTH
+    if _SYNTH is None:
+        import ctypes as C
+        from pathlib import Path
+        p = Path(__file__).resolve().parent / "libprsynth.so"
+        if not p.exists():
+            raise RuntimeError(f"{p} not found: run __graft_entry__.build()")
+        L = C.CDLL(str(p))
+        P64, PU8 = C.POINTER(C.c_int64), C.POINTER(C.c_uint8)
+        L.prs_genome.argtypes = [C.c_uint64, C.c_int64, PU8]
+        L.prs_long_reads.argtypes = [PU8, P64, C.c_int64, C.c_int64, C.c_double, C.c_double, C.c_double, C.c_uint64,
+                                     C.c_int, P64, P64, PU8]
+        L.prs_short_reads.argtypes = [PU8, P64, PU8, C.c_int64, C.c_int64, C.c_double, C.c_uint64, C.c_int, PU8]
+        _SYNTH = L
+    return _SYNTH
+
+
+def simulate_reads(seed: int, genome_len: int, n_lr: int, lr_len: int, n_sr: int, p_ins: float = 0.09,
+                   p_del: float = 0.045, p_sub: float = 0.015, sr_len: int = 150, threads: int = 16) -> Dataset:
+    """The reads of simulate()'s model at BASELINE configs[2] / configs[3] scale (SURVEY.md §8d
+    C3 / C4: 100 k / 270 k x 10 kb long reads), generated on host threads (libprsynth.so),
+    without the simulation-truth task list (the product's seeding front end makes the tasks).
+    n_sr short reads in sequencer order -- unsorted over the genome, as a FASTQ from a
+    sequencing run is, so contiguous short-read shards hit every part of the long-read set.
+    Deterministic for a seed whatever the thread count."""
+    import ctypes as C
+    L = _synth_lib()
+    P64, PU8 = C.POINTER(C.c_int64), C.POINTER(C.c_uint8)
+    seed = int(seed) & (2 ** 64 - 1)
+    genome = np.empty(genome_len, np.uint8)
+    L.prs_genome(seed, genome_len, genome.ctypes.data_as(PU8))
+    span = min(lr_len, genome_len)
+    rp = np.random.default_rng(seed)
+    lr_start = np.ascontiguousarray(np.sort(rp.integers(0, genome_len - span + 1, n_lr)), np.int64)
+    sr_start = np.ascontiguousarray(rp.integers(0, genome_len - sr_len + 1, n_sr), np.int64)
+    sr_strand = np.ascontiguousarray(rp.integers(0, 2, n_sr), np.uint8)
+    gp = genome.ctypes.data_as(PU8)
+    lens = np.zeros(max(n_lr, 1), np.int64)
+    if L.prs_long_reads(gp, lr_start.ctypes.data_as(P64), n_lr, span, p_ins, p_del, p_sub, seed, threads,
+                        lens.ctypes.data_as(P64), None, None):
+        raise RuntimeError("prs_long_reads failed")
+    lr_off = np.zeros(n_lr + 1, np.int64)
+    np.cumsum(lens[:n_lr], out=lr_off[1:])
+    lr_seq = np.empty(int(lr_off[-1]) + 1, np.uint8)
+    if L.prs_long_reads(gp, lr_start.ctypes.data_as(P64), n_lr, span, p_ins, p_del, p_sub, seed, threads,
+                        lens.ctypes.data_as(P64), lr_off.ctypes.data_as(P64), lr_seq.ctypes.data_as(PU8)):
+        raise RuntimeError("prs_long_reads failed")
+    sr_seq = np.empty(n_sr * sr_len + 1, np.uint8)
+    if L.prs_short_reads(gp, sr_start.ctypes.data_as(P64), sr_strand.ctypes.data_as(PU8), n_sr, sr_len,
+                         0.001 * sr_len, seed, threads, sr_seq.ctypes.data_as(PU8)):
+        raise RuntimeError("prs_short_reads failed")
+    sr_off = np.arange(n_sr + 1, dtype=np.int64) * sr_len
+    z32, z8 = np.zeros(0, np.int32), np.zeros(0, np.uint8)
+    return Dataset(genome, lr_seq[:-1], lr_off, lr_start, sr_seq[:-1], sr_off, sr_start, sr_strand, z32, z32, z8, z32,
+                   z32, z32)
+
+
 def with_seeds(d: Dataset, tasks: np.ndarray) -> Dataset:
     """The same reads with the seeding front end's output (seed.TASK_DTYPE records of
     pr_seed_map / pr_seed_gpu_map: every seed of the kept chains, grouped by short read, then

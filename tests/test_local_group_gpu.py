@@ -31,6 +31,7 @@ def _ranks(world, fn):
             out[r] = fn(r, ctxs[r], cms[r])
         except BaseException as e:   # noqa: BLE001 - reported below
             err[r] = e
+            g.abort()   # the other ranks must not wait for this one in a collective
 
     th = [threading.Thread(target=run, args=(r,), daemon=True) for r in range(world)]
     for t in th:
