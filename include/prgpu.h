@@ -489,6 +489,8 @@ int pr_aln_exchange(pr_ctx *ctx, pr_comm *comm, int64_t sr0, const int64_t *lr_b
  * place of RCCL; sr0[k] is context k's first short read, n_recv[world] (may be NULL) */
 int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64_t *sr0, const int64_t *lr_bounds,
                           int64_t *n_recv);
+/* the last exchange's received records by source rank (per_rank[cap]; world = ranks) */
+int pr_aln_exchange_sources(pr_ctx *ctx, int64_t *per_rank, int cap, int *world);
 typedef struct pr_own_batch {
     int32_t lr0, n_lr;            /* owned long reads: global ids [lr0, lr0 + n_lr)          */
     const int64_t *lr_off;        /* [n_lr+1] their offsets (from 0)                          */

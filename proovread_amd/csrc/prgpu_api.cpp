@@ -244,6 +244,7 @@ struct pr_ctx {
     bool x_ready = false;        // XB_RREC / XB_RCIG hold the last exchange's records
     bool x_pass = false;         // world 1: the exchange is the identity, the owned launch reads the SW output
     int64_t x_nrecv = 0, x_nrcig = 0;
+    std::vector<int64_t> x_from;  // records of the last exchange by source rank
     // the resident long-read set (pr_lrset_*): reads, qualities, mapping reference (masked reads)
     DevBuf ls[LS_COUNT];
     std::vector<int64_t> ls_off;
@@ -923,6 +924,7 @@ extern "C" int pr_aln_exchange(pr_ctx *c, pr_comm *comm, int64_t sr0, const int6
         c->x_pass = true;
         c->x_ready = true;
         c->x_nrecv = X.n;
+        c->x_from.assign(1, X.n);
         if (n_recv) *n_recv = X.n;
         return 0;
     }
@@ -945,9 +947,11 @@ extern "C" int pr_aln_exchange(pr_ctx *c, pr_comm *comm, int64_t sr0, const int6
         rc_cig = sc_cig;
     }
     int64_t nr = 0, nc = 0;
+    c->x_from.assign((size_t)world, 0);
     for (int r = 0; r < world; ++r) {
         nr += rc_rec[(size_t)r];
         nc += rc_cig[(size_t)r];
+        c->x_from[(size_t)r] = rc_rec[(size_t)r] / (int64_t)sizeof(XRec);
     }
     if ((rc = xchg_recv_buffers(c, nr, nc))) return rc;
     DevBuf *B = c->xb;
@@ -985,9 +989,11 @@ extern "C" int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64
     for (int r = 0; r < world; ++r) {
         pr_ctx *d = ctxs[r];
         int64_t nr = 0, nc = 0;
+        d->x_from.assign((size_t)world, 0);
         for (int k = 0; k < world; ++k) {
             nr += nrec[(size_t)k][(size_t)r] * (int64_t)sizeof(XRec);
             nc += nops[(size_t)k][(size_t)r] * 4;
+            d->x_from[(size_t)k] = nrec[(size_t)k][(size_t)r];
         }
         if ((rc = xchg_recv_buffers(d, nr, nc))) return rc;
         int64_t ro = 0, co = 0;
@@ -1010,6 +1016,14 @@ extern "C" int pr_aln_exchange_local(pr_ctx *const *ctxs, int world, const int64
         d->x_ready = true;
         if (n_recv) n_recv[r] = d->x_nrecv;
     }
+    return 0;
+}
+
+extern "C" int pr_aln_exchange_sources(pr_ctx *c, int64_t *per_rank, int cap, int *world) {
+    if (!c || (cap && !per_rank)) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->x_ready) return set_error(PR_ERR_ARG, "no exchange yet");
+    for (int r = 0; r < cap && r < (int)c->x_from.size(); ++r) per_rank[r] = c->x_from[(size_t)r];
+    if (world) *world = (int)c->x_from.size();
     return 0;
 }
 

@@ -321,6 +321,16 @@ def exchange(ctx, comm, s: int, bounds: np.ndarray) -> int:
     return nr.value
 
 
+def exchange_sources(ctx) -> List[int]:
+    """Records the last exchange delivered to this rank, by source rank (pr_aln_exchange_sources)."""
+    L = _abi.lib()
+    L.pr_aln_exchange_sources.argtypes = [C.c_void_p, _abi.P64, C.c_int, _abi.P32]
+    v = np.zeros(64, np.int64)
+    w = C.c_int32()
+    _abi.check(L.pr_aln_exchange_sources(ctx.h, _abi.ptr(v, C.c_int64), 64, C.byref(w)), "pr_aln_exchange_sources")
+    return [int(x) for x in v[:w.value]]
+
+
 def exchange_local(ctxs, starts, bounds: np.ndarray) -> List[int]:
     """Step 2 among several contexts of this process (pr_aln_exchange_local: the same packs,
     device copies in place of RCCL): context k holds the shard starting at starts[k]."""

@@ -115,3 +115,76 @@ def test_local_group_exact_world1_with_comm_equals_plain():
                                                    stages=correct.GpuStages(ctx), comm=cm))[0]
     assert got.reads.seqs == want.reads.seqs and got.reads.quals == want.reads.quals
     assert got.chim == want.chim
+
+
+def _shared_task_inputs():
+    """One genome, one long-read set and one short-read run in sequencer order (unsorted over
+    the genome) -- what every rank holds in the exact layout."""
+    from proovread_amd import correct, synth
+    d = synth.simulate_reads(31, 400_000, 300, 5_000, 12_000, threads=8)
+    pool = np.frombuffer(b"ACGTN", np.uint8)[d.lr_seq]
+    reads = correct.LongReads([f"lr{i}" for i in range(d.n_lr)],
+                              pools=(pool, d.lr_off, np.full(len(pool), ord("$"), np.uint8)))
+    return d, reads
+
+
+def _task(ctx, cm, d, reads, exact):
+    from proovread_amd import cns, correct, iteration
+    st = correct.GpuStages(ctx)
+    st.load(reads)
+    params = cns.CnsParams(coverage=11.25, use_ref_qual=True, max_ins_length=0)
+    out = st.task("bwa-sr-1", d.sr_seq, d.sr_off, params, (20, 300.0), comm=cm, exact=exact,
+                  mask_cfg=("20,41,80,130,60,0.7", 150))
+    src = iteration.exchange_sources(ctx) if exact else None
+    off, seq, qual, mp = st.lrs.download(seq=True, qual=True, mapping=True)
+    return out, src, off, seq, qual, mp
+
+
+@pytest.mark.gpu
+def test_local_group_task_on_shared_genome_crosses_ranks():
+    """World 3 on ONE shared dataset (short reads in sequencer order): most alignments a rank
+    receives come from the other ranks' short-read shards (pr_aln_exchange moves them), and the
+    task's corrected reads, qualities and masked reads equal the world-1 task's byte for byte."""
+    d, reads = _shared_task_inputs()
+    from proovread_amd import _abi
+    want = _task(_abi.default_context(), None, d, reads, False)
+    got = _ranks(3, lambda r, ctx, cm: _task(ctx, cm, d, reads, True))
+    bpt = bpn = n_tasks = 0
+    for r, (out, src, off, seq, qual, mp) in enumerate(got):
+        assert np.array_equal(off, want[2])
+        assert np.array_equal(seq, want[3]) and np.array_equal(qual, want[4]) and np.array_equal(mp, want[5])
+        assert len(src) == 3 and sum(src) > 1000
+        assert sum(src) - src[r] > 0.5 * sum(src), src   # received from the other ranks' shards
+        bpt, bpn, n_tasks = bpt + out.bpt, bpn + out.bpn, n_tasks + out.n_tasks
+    assert (bpt, bpn, n_tasks) == (want[0].bpt, want[0].bpn, want[0].n_tasks)
+
+
+@pytest.mark.gpu
+def test_local_group_error_on_one_rank_returns_on_every_rank():
+    """a failure on one rank before the exchange's collectives (here rank 1's
+    long-read bounds are not ascending, so its pack fails) makes pr_aln_exchange return an
+    error on EVERY rank (pr_comm_agree) instead of leaving the others in the all-to-all."""
+    from proovread_amd import _abi, correct, exact_shard as ex, iteration, seed, sw
+    d, reads = _shared_task_inputs()
+
+    def fn(r, ctx, cm):
+        L = _abi.lib()
+        st = correct.GpuStages(ctx)
+        st.load(reads)
+        st.lrs.index(st.lrs.MAP)
+        s, e = ex.sr_range(d.n_sr, 2, r)
+        a0, a1 = int(d.sr_off[s]), int(d.sr_off[e])
+        seed._map_gpu(L, ctx, d.sr_seq[a0:a1], d.sr_off[s:e + 1] - a0, seed.default_opts(False), False,
+                      keep_on_device=True)
+        iteration.ShardSW(ctx, d.sr_seq, d.sr_off, s, e, None, d.lr_off, device_pools=True).launch(
+            sw.default_opts(finish=False))
+        bounds = ex.lr_bounds(d.lr_off, 2)
+        if r == 1:
+            bounds = np.array([0, d.n_lr, d.n_lr // 2], np.int64)   # not ascending
+        with pytest.raises(RuntimeError) as ei:
+            iteration.exchange(ctx, cm, s, bounds)
+        return str(ei.value)
+
+    msgs = _ranks(2, fn)
+    assert "ascending" in msgs[1]
+    assert "another rank failed" in msgs[0]
