@@ -246,7 +246,7 @@ struct HostScratch {
     std::vector<uint64_t> qext;
     std::vector<uint32_t> ge, hpos;
     std::vector<uint8_t> hhi;
-    std::vector<uint16_t> hml;
+    std::vector<uint16_t> hml, rmax;
     std::vector<seedc::Iv> mems, m1, curr, prev;
     std::vector<seedc::Seed> seeds;
     std::vector<int32_t> next, cnx, kept, hkey, hhead, htail;
@@ -263,6 +263,7 @@ struct HostScratch {
         codes.resize((size_t)lmax + 1);
         qext.resize((size_t)lmax + 1);
         ge.resize((size_t)lmax * seedc::HB + 1);
+        rmax.resize((size_t)lmax + 1);
         hpos.resize((size_t)hits);
         hml.resize((size_t)hits);
         mems.resize((size_t)mems_cap);
@@ -285,6 +286,7 @@ struct HostScratch {
                            prev.data(), iv,           seeds.data(), next.data(), seeds_cap,   cv.data(),
                            ch.data(),   cnx.data(),   kept.data(), hkey.data(), hhead.data(),
                            htail.data(), chains,      hs};
+        S.rmax = rmax.data();
     }
     void grow(int err) {
         if (err & seedc::SC_OVER_HITS) hits *= 2;

@@ -124,6 +124,7 @@ struct Scratch {
     int32_t *cnx, *kept;                       // [cap_chains] each; cnx: next chain of its range's list
     int32_t *hkey, *hhead, *htail;             // [hsize] range table: key (-1 free), list head / tail
     int32_t cap_chains, hsize;                 // hsize: power of two >= 2 * cap_chains
+    uint16_t *rmax;                            // [lmax + 1] per start a: the end of its longest match
 };
 
 SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
@@ -196,6 +197,68 @@ struct Occ {
         return c;
     }
 };
+
+// R_1 of every start into S.rmax (starts a0, a0 + step, ...; the device runs it a lane per
+// start): the start's longest hit, or below 12 bases the j-mer counts
+SC_HD void build_rmax(const IndexView &I, Scratch &S, const uint8_t *q, int len, const uint32_t *lc, int a0, int step);
+
+// The end of the longest match from start a that occurs >= k times in the text:
+// R_k(a) = max{e : occ(a, e) >= k} (a when even q[a] occurs fewer than k times or is N).
+// occ(a, e) never grows with e and never shrinks as a moves right (every occurrence of
+// q[a, e) contains one of q[a + 1, e)), which is what makes smem1's backward extension a
+// staircase over R_k (below).  Below 12 bases: the N-free j-mer counts.
+SC_HD int rmax_short(const Occ &occ, const uint8_t *q, int len, int a, int64_t k) {
+    int e = a;
+    while (e < len && e - a < KI - 1 && q[e] < 4 && occ(a, e + 1) >= k) ++e;
+    return e;
+}
+// R_k(a) for k > 1 (re-seeding), from the start's count row and, beyond it, its hits' lengths
+SC_HD int rmax_k(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a, int64_t k) {
+    if (k <= 1) return S.rmax[a];
+    if (q[a] > 3) return a;
+    if (a + KI <= len && S.codes[a] >= 0) {
+        const uint32_t *g = S.ge + (int64_t)a * HB;
+        if ((int64_t)g[0] >= k) {
+            if ((int64_t)g[HB - 1] < k) {   // the largest t with g[t] >= k (the row never grows with t)
+                int lo = 0, hi = HB - 2;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if ((int64_t)g[mid] >= k) lo = mid; else hi = mid - 1;
+                }
+                return a + KI + lo;
+            }
+            // >= k hits match at least KI + HB - 1 bases: the k-th largest match length
+            int lo = KI + HB - 1, hi = len - a;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                int64_t c = 0;
+                for (int32_t h = S.hoff[a]; h < S.hoff[a + 1]; ++h) c += S.hml[h] >= mid;
+                if (c >= k) lo = mid; else hi = mid - 1;
+            }
+            return a + lo;
+        }
+    }
+    return rmax_short(occ, q, len, a, k);
+}
+
+SC_HD void build_rmax(const IndexView &I, Scratch &S, const uint8_t *q, int len, const uint32_t *lc, int a0, int step) {
+    const Occ occ{&I, &S, q, len, lc};
+    for (int a = a0; a < len; a += step) {
+        int e = a;
+        if (q[a] < 4) {
+            int32_t h0 = 0, h1 = 0;
+            if (a + KI <= len && S.codes[a] >= 0) h0 = S.hoff[a], h1 = S.hoff[a + 1];
+            if (h1 > h0) {
+                int m = 0;
+                for (int32_t h = h0; h < h1; ++h) m = m > (int)S.hml[h] ? m : (int)S.hml[h];
+                e = a + m;
+            } else {
+                e = rmax_short(occ, q, len, a, 1);
+            }
+        }
+        S.rmax[a] = (uint16_t)e;
+    }
+}
 
 // -> 0 or SC_OVER_*
 SC_HD int build_occ(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
@@ -273,6 +336,7 @@ SC_HD int build_occ(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
         prev1 = nh;
     }
     for (int a = len - KI + 1 < 0 ? 0 : len - KI + 1; a <= len; ++a) S.hoff[a] = nh;
+    build_rmax(I, S, q, len, nullptr, 0, 1);
     return 0;
 }
 
@@ -351,44 +415,30 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
         if (nc >= cap) { err |= SC_OVER_IV; return len; }
         curr[nc++] = ik;
     }
-    iv_reverse(curr, nc);   // longer matches first
-    const int ret = curr[0].end;
-    {
-        Iv *t = prev;
-        prev = curr;
-        curr = t;
-        np = nc;
-    }
-    for (i = x - 1; i >= -1; --i) {
-        const int c = i < 0 ? -1 : (q[i] < 4 ? q[i] : -1);
-        nc = 0;
-        SC_STAT(17, np);
-        // the counts of this column's extensions do not depend on each other: 8 at a time
-        // (their loads in flight together), then the intervals in order as before
-        for (int k0 = 0; k0 < np; k0 += 8) {
-            int64_t ov[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) ov[u] = (c >= 0 && k0 + u < np) ? occ(i, prev[k0 + u].end) : 0;
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                if (k0 + u >= np) break;
-                const Iv p = prev[k0 + u];
-                const int64_t o = ov[u];
-                if (c < 0 || o < min_intv) {
-                    if (nc == 0 && (nmem == 0 || i + 1 < mem[nmem - 1].start)) {
-                        if (nmem >= cap) { err |= SC_OVER_IV; return len; }
-                        mem[nmem++] = Iv{i + 1, p.end, p.occ};
-                    }
-                } else if (nc == 0 || o != curr[nc - 1].occ) {
-                    curr[nc++] = Iv{i, p.end, o};   // nc <= np <= cap
-                }
-            }
+    const int ret = curr[nc - 1].end;   // the longest forward match
+    (void)prev;
+    (void)np;
+    // Backward extension.  bwa extends the forward intervals (longest end first) one column
+    // to the left at a time; an interval stops at the first column i with occ(i, end) <
+    // min_intv, and is reported as [i + 1, end) when no longer-end interval survived that
+    // column (and none was reported there).  Since occ(a, e) >= k holds for every a from x
+    // down to the stopping column (it never shrinks as a moves right), an interval's stopping
+    // start is a(e) = the lowest a <= x with R_k(a') >= e for all a' in [a, x), found by one
+    // downward sweep over R_k as the ends decrease; the reported intervals are those whose
+    // a(e) is strictly below the previous (longer-end) interval's.  Intervals bwa drops for an
+    // occurrence count equal to a longer neighbour's share that neighbour's a(e) and are never
+    // reported either.  Same SMEMs, one R_k load per column instead of one count lookup per
+    // live interval per column.
+    int a = x, last = x + 1;
+    for (int j = nc - 1; j >= 0; --j) {
+        const Iv p = curr[j];
+        SC_STAT(17, 1);
+        while (a > 0 && rmax_k(occ, S, q, len, a - 1, min_intv) >= p.end) --a;
+        if (a < last) {
+            if (nmem >= cap) { err |= SC_OVER_IV; return len; }
+            mem[nmem++] = Iv{a, p.end, a == x ? p.occ : occ(a, p.end)};
+            last = a;
         }
-        if (nc == 0) break;
-        Iv *t = prev;
-        prev = curr;
-        curr = t;
-        np = nc;
     }
     iv_reverse(mem, nmem);
     return ret;
@@ -1009,7 +1059,8 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += 2 * align8((int64_t)sizeof(Chain) * c.chains);  // cv, ch
     b += 2 * align8(4 * (int64_t)c.chains);              // cnx, kept
     b += 3 * align8(4 * (int64_t)range_table_size(c.chains));   // hkey, hhead, htail
-    if (c.hi) b += align8((int64_t)c.hits);              // hhi (last: the small-text layout is unchanged)
+    b += align8(2 * (int64_t)(c.lmax + 1));              // rmax
+    if (c.hi) b += align8((int64_t)c.hits);              // hhi (last)
     return b;
 }
 
@@ -1047,6 +1098,7 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.hhead = (int32_t *)take(4 * (int64_t)S.hsize);
     S.htail = (int32_t *)take(4 * (int64_t)S.hsize);
     S.cap_chains = c.chains;
+    S.rmax = (uint16_t *)take(2 * (int64_t)(c.lmax + 1));
     S.hhi = c.hi ? (uint8_t *)take((int64_t)c.hits) : nullptr;
     return S;
 }

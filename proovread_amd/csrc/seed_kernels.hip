@@ -173,13 +173,20 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
         wave_sync_lds();
         // the count table, a lane per start: ge[a][t] = #{hits of a with ml - KI >= t} summed
         // directly in registers (no zeroing, no atomics, no suffix pass over HBM)
+        // and R_1(a), the end of the start's longest match (seed_core.h rmax_k: smem1's backward
+        // extension sweeps it), from the same hits, or below 12 bases from the j-mer counts
+        const seedc::Occ occ{&V, &S, q, len, nullptr};
         for (int a = lane; a < len; a += 64) {
             uint32_t g[HB];
 #pragma unroll
             for (int t = 0; t < HB; ++t) g[t] = 0u;
-            if (a + KI <= len && S.codes[a] >= 0) {
+            int mmax = 0;
+            const bool has = a + KI <= len && S.codes[a] >= 0;
+            if (has) {
                 for (int h = ho[a]; h < ho[a + 1]; ++h) {
-                    const int d = (int)S.hml[h] - KI;
+                    const int ml = (int)S.hml[h];
+                    const int d = ml - KI;
+                    mmax = mmax > ml ? mmax : ml;
 #pragma unroll
                     for (int t = 0; t < HB; ++t) g[t] += d >= t ? 1u : 0u;
                 }
@@ -187,6 +194,9 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
             uint32_t *dst = S.ge + (int64_t)a * HB;
 #pragma unroll
             for (int t = 0; t < HB; ++t) dst[t] = g[t];
+            int e = a;
+            if (q[a] < 4) e = mmax > 0 ? a + mmax : seedc::rmax_short(occ, q, len, a, 1);
+            S.rmax[a] = (uint16_t)e;
         }
         __threadfence_block();
     }
