@@ -2140,7 +2140,7 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         (rc = D[SB_SCRATCH].ensure((size_t)scratch)) ||
         (rc = D[SB_OUT].ensure((size_t)(std::min<int64_t>(chunk, n_sr) * slot_bytes + 16))) ||
         (rc = D[SB_NOUT].ensure((size_t)n_sr * 4 + 16)) || (rc = D[SB_STATUS].ensure((size_t)n_sr * 4 + 16)) ||
-        (rc = D[SB_NEXT].ensure(128)) || (rc = D[SB_PRE].ensure(((size_t)n_sr + 1) * 8)) ||
+        (rc = D[SB_NEXT].ensure(256)) || (rc = D[SB_PRE].ensure(((size_t)n_sr + 1) * 8)) ||
         (rc = D[SB_DENSE].ensure(sizeof(pr_seed_task))))
         return rc;
     K.sr_seq = D[SB_SEQ].as<uint8_t>();
@@ -2150,7 +2150,7 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     K.status = D[SB_STATUS].as<int32_t>();
     K.next = D[SB_NEXT].as<int32_t>();
     K.prof = reinterpret_cast<unsigned long long *>(D[SB_NEXT].as<uint8_t>() + 64);
-    HIPCHK(hipMemsetAsync(K.next, 0, 128, s));
+    HIPCHK(hipMemsetAsync(K.next, 0, 256, s));
     HIPCHK(hipEventRecord(c->ev[8], s));
     c->seed_pass2 = 0;
     c->seed_pass3 = 0;
@@ -2301,12 +2301,7 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     if (n_sr && hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_seed = ms;
     c->ms_seed_pass2 = 0.f;   // (the passes after the first chunk's pass 1; one chunk at configs[1])
     if (n_sr && hipEventElapsedTime(&ms, c->ev[10], c->ev[9]) == hipSuccess) c->ms_seed_pass2 = ms;
-    if (getenv("PRGPU_SEED_DEBUG") && K.prof) {   // pass 1's lane phase split (lane-summed ticks)
-        unsigned long long t8[8] = {};
-        if (hipMemcpy(t8, K.prof, sizeof t8, hipMemcpyDeviceToHost) == hipSuccess)
-            fprintf(stderr, "[seed] pass-1 lane ms (summed over lanes): smems %.1f chaining %.1f filter+out %.1f\n",
-                    t8[4] / 1e5, t8[5] / 1e5, t8[6] / 1e5);
-    }
+
     // an incomplete seed set (flagged reads have no seeds) is never handed to
     // pr_iter_upload_gpu_seeds: it refuses when seed_pre does not match the reads
     if (bad) c->seed_pre.clear();
@@ -2360,6 +2355,14 @@ extern "C" int pr_seed_gpu_phase_ticks(pr_ctx *c, uint64_t *ticks4) {
     if (!c->sd[SB_NEXT].p) return set_error(PR_ERR_ARG, "no pr_seed_gpu_map launch yet");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMemcpy(ticks4, c->sd[SB_NEXT].as<uint8_t>() + 64, 32, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int pr_seed_gpu_lane_ticks(pr_ctx *c, uint64_t *ticks6) {
+    if (!c || !ticks6) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->sd[SB_NEXT].p) return set_error(PR_ERR_ARG, "no pr_seed_gpu_map launch yet");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(ticks6, c->sd[SB_NEXT].as<uint8_t>() + 64 + 4 * 8, 48, hipMemcpyDeviceToHost));
     return 0;
 }
 

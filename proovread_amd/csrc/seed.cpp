@@ -263,7 +263,7 @@ struct HostScratch {
         codes.resize((size_t)lmax + 1);
         qext.resize((size_t)lmax + 1);
         ge.resize((size_t)lmax * seedc::HB + 1);
-        rmax.resize((size_t)lmax + 1);
+        rmax.resize(((size_t)lmax + 1) * seedc::RK);
         hpos.resize((size_t)hits);
         hml.resize((size_t)hits);
         mems.resize((size_t)mems_cap);

@@ -57,6 +57,7 @@ constexpr int KX = 28;                        // bases stored after each hit
 constexpr uint64_t KX_MASK = (1ull << (2 * KX)) - 1;
 constexpr int HB = 20;                        // per-start count table width
 constexpr int CB_SHIFT = 12;                  // contig block table granularity
+constexpr int RK = 11;                        // R_k tabulated per start for k <= RK (split_width + 1)
 
 // Text positions: the text holds both strands of every long read, 2 l_pac + 2 n_lr bases, up to
 // 2^33 (l_pac < 4.29 Gb: configs[3]'s 2.7 Gb read set).  Hit positions are
@@ -124,7 +125,7 @@ struct Scratch {
     int32_t *cnx, *kept;                       // [cap_chains] each; cnx: next chain of its range's list
     int32_t *hkey, *hhead, *htail;             // [hsize] range table: key (-1 free), list head / tail
     int32_t cap_chains, hsize;                 // hsize: power of two >= 2 * cap_chains
-    uint16_t *rmax;                            // [lmax + 1] per start a: the end of its longest match
+    uint16_t *rmax;                            // [(lmax + 1) * RK] R_k(a), k = 1..RK (rmax_k)
 };
 
 SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
@@ -198,10 +199,6 @@ struct Occ {
     }
 };
 
-// R_1 of every start into S.rmax (starts a0, a0 + step, ...; the device runs it a lane per
-// start): the start's longest hit, or below 12 bases the j-mer counts
-SC_HD void build_rmax(const IndexView &I, Scratch &S, const uint8_t *q, int len, const uint32_t *lc, int a0, int step);
-
 // The end of the longest match from start a that occurs >= k times in the text:
 // R_k(a) = max{e : occ(a, e) >= k} (a when even q[a] occurs fewer than k times or is N).
 // occ(a, e) never grows with e and never shrinks as a moves right (every occurrence of
@@ -212,9 +209,45 @@ SC_HD int rmax_short(const Occ &occ, const uint8_t *q, int len, int a, int64_t k
     while (e < len && e - a < KI - 1 && q[e] < 4 && occ(a, e + 1) >= k) ++e;
     return e;
 }
-// R_k(a) for k > 1 (re-seeding), from the start's count row and, beyond it, its hits' lengths
+
+// R_1 .. R_RK of start a into S.rmax[a * RK ..]: with >= k hits of its 12-mer, a + the k-th
+// largest hit match length (occ(a, e) >= k exactly when k hits match >= e - a bases); with
+// fewer, the longest N-free j-mer (j < 12) with >= k occurrences (R_k never grows with k)
+SC_HD void fill_rk(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a) {
+    uint16_t *r = S.rmax + (int64_t)a * RK;
+    uint16_t top[RK];
+#pragma unroll
+    for (int k = 0; k < RK; ++k) top[k] = 0;
+    if (q[a] < 4 && a + KI <= len && S.codes[a] >= 0) {
+        for (int32_t h = S.hoff[a]; h < S.hoff[a + 1]; ++h) {
+            uint16_t v = S.hml[h];   // insert into the descending top list
+#pragma unroll
+            for (int k = 0; k < RK; ++k) {
+                const uint16_t t = top[k];
+                const bool gt = v > t;
+                top[k] = gt ? v : t;
+                v = gt ? t : v;
+            }
+        }
+    }
+    int e = -1;   // the short part: j-mer counts never grow with k, so its end only falls
+    for (int k = 1; k <= RK; ++k) {
+        if (top[k - 1] > 0) {
+            r[k - 1] = (uint16_t)(a + top[k - 1]);
+            continue;
+        }
+        if (e < 0) e = rmax_short(occ, q, len, a, k);
+        else
+            while (e > a && occ(a, e) < k) --e;
+        r[k - 1] = (uint16_t)e;
+    }
+}
+
+// R_k(a): tabulated for k <= RK; beyond (re-seeding with split_width >= RK), from the start's
+// count row and its hits' lengths
 SC_HD int rmax_k(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a, int64_t k) {
-    if (k <= 1) return S.rmax[a];
+    if (k < 1) k = 1;
+    if (k <= RK) return S.rmax[(int64_t)a * RK + (k - 1)];
     if (q[a] > 3) return a;
     if (a + KI <= len && S.codes[a] >= 0) {
         const uint32_t *g = S.ge + (int64_t)a * HB;
@@ -239,25 +272,6 @@ SC_HD int rmax_k(const Occ &occ, const Scratch &S, const uint8_t *q, int len, in
         }
     }
     return rmax_short(occ, q, len, a, k);
-}
-
-SC_HD void build_rmax(const IndexView &I, Scratch &S, const uint8_t *q, int len, const uint32_t *lc, int a0, int step) {
-    const Occ occ{&I, &S, q, len, lc};
-    for (int a = a0; a < len; a += step) {
-        int e = a;
-        if (q[a] < 4) {
-            int32_t h0 = 0, h1 = 0;
-            if (a + KI <= len && S.codes[a] >= 0) h0 = S.hoff[a], h1 = S.hoff[a + 1];
-            if (h1 > h0) {
-                int m = 0;
-                for (int32_t h = h0; h < h1; ++h) m = m > (int)S.hml[h] ? m : (int)S.hml[h];
-                e = a + m;
-            } else {
-                e = rmax_short(occ, q, len, a, 1);
-            }
-        }
-        S.rmax[a] = (uint16_t)e;
-    }
 }
 
 // -> 0 or SC_OVER_*
@@ -336,7 +350,8 @@ SC_HD int build_occ(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
         prev1 = nh;
     }
     for (int a = len - KI + 1 < 0 ? 0 : len - KI + 1; a <= len; ++a) S.hoff[a] = nh;
-    build_rmax(I, S, q, len, nullptr, 0, 1);
+    const Occ occ{&I, &S, q, len, nullptr};
+    for (int a = 0; a < len; ++a) fill_rk(occ, S, q, len, a);
     return 0;
 }
 
@@ -461,8 +476,27 @@ SC_HD int seed_strategy1(const Occ &occ, const uint8_t *q, int len, int x, int m
     return len;
 }
 
+// wall-clock ticks per part of a read's lane work (device, optional): [SMEM pass, re-seeding,
+// -y seeds + sort, chaining, mem_chain_flt, filter + output]
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SC_TICK(k)                                          \
+    do {                                                    \
+        if (ticks) {                                        \
+            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   \
+            ticks[k] += t_ - t_last;                        \
+            t_last = t_;                                    \
+        }                                                   \
+    } while (0)
+#else
+#define SC_TICK(k) do { (void)ticks; } while (0)
+#endif
+
 // mem_collect_intv -> S.mems[0, return) sorted by (start, end), stable
-SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const uint8_t *q, int len, int &err) {
+SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const uint8_t *q, int len, int &err,
+                       unsigned long long *ticks = nullptr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
+#endif
     int nm = 0, n1 = 0;
     auto push = [&](const Iv &v) {
         if (nm >= S.cap_mems) {
@@ -480,6 +514,7 @@ SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const 
             ++x;
         }
     }
+    SC_TICK(0);
     const int split_len = (int)(O.min_seed_len * O.split_factor + .499);
     const int nfirst = nm;
     for (int k = 0; k < nfirst && !err; ++k) {
@@ -489,6 +524,7 @@ SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const 
         for (int j = 0; j < n1; ++j)
             if (S.m1[j].end - S.m1[j].start >= O.min_seed_len) push(S.m1[j]);
     }
+    SC_TICK(1);
     if (O.max_mem_intv > 0) {
         for (int x = 0; x < len && !err;) {
             if (q[x] < 4) {
@@ -500,16 +536,42 @@ SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const 
             }
         }
     }
-    // stable insertion sort by (start, end)
-    for (int i = 1; i < nm; ++i) {
-        const Iv v = S.mems[i];
-        int j = i - 1;
-        while (j >= 0 && (S.mems[j].start > v.start || (S.mems[j].start == v.start && S.mems[j].end > v.end))) {
-            S.mems[j + 1] = S.mems[j];
-            --j;
+    // stable sort by (start, end).  The three rounds each come out sorted by start, so a
+    // counting sort by start (into the seed pool, free until mem_chain; the counts in `codes`,
+    // which nothing reads after the occurrence lookups) and an insertion sort by end inside each
+    // start's run (a few intervals) replace one insertion sort over all ~150 (quadratic moves)
+    if (nm > 1 && S.cap_seeds >= nm && !err) {
+        static_assert(sizeof(Seed) == sizeof(Iv), "the seed pool holds the sorted intervals");
+        int32_t *cnt = S.codes;
+        Iv *tmp = reinterpret_cast<Iv *>(S.seeds);
+        for (int x = 0; x <= len; ++x) cnt[x] = 0;
+        for (int i = 0; i < nm; ++i) ++cnt[S.mems[i].start + 1];
+        for (int x = 1; x <= len; ++x) cnt[x] += cnt[x - 1];
+        for (int i = 0; i < nm; ++i) {
+            const Iv v = S.mems[i];
+            tmp[cnt[v.start]++] = v;
         }
-        S.mems[j + 1] = v;
+        for (int i = 0; i < nm; ++i) {
+            const Iv v = tmp[i];
+            int j = i - 1;
+            while (j >= 0 && S.mems[j].start == v.start && S.mems[j].end > v.end) {
+                S.mems[j + 1] = S.mems[j];
+                --j;
+            }
+            S.mems[j + 1] = v;
+        }
+    } else {
+        for (int i = 1; i < nm; ++i) {
+            const Iv v = S.mems[i];
+            int j = i - 1;
+            while (j >= 0 && (S.mems[j].start > v.start || (S.mems[j].start == v.start && S.mems[j].end > v.end))) {
+                S.mems[j + 1] = S.mems[j];
+                --j;
+            }
+            S.mems[j + 1] = v;
+        }
     }
+    SC_TICK(2);
     return nm;
 }
 
@@ -679,18 +741,6 @@ SC_HD int seed_sw_score(const IndexView &I, const pr_seed_opts &O, const uint8_t
 // filter and the tasks into out[0, *n_out) (chain order after mem_chain_flt).
 // Returns 0 or an SC_OVER_* mask (then the read's output is not valid).
 // ticks (device, optional): wall-clock ticks added per part [SMEMs, chaining, filter + output]
-#if defined(__HIP_DEVICE_COMPILE__)
-#define SC_TICK(k)                                          \
-    do {                                                    \
-        if (ticks) {                                        \
-            const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();   \
-            ticks[k] += t_ - t_last;                        \
-            t_last = t_;                                    \
-        }                                                   \
-    } while (0)
-#else
-#define SC_TICK(k) do { (void)ticks; } while (0)
-#endif
 // Part 1: SMEMs, chaining and mem_chain_flt; *n_chains = the chains in S.ch (kept flags set).
 SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int *n_chains,
                      unsigned long long *ticks = nullptr, const uint32_t *lcnt = nullptr) {
@@ -700,11 +750,13 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
     unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
 #endif
     const Occ occ{&I, &S, q, len, lcnt};
-    const int nm = collect_intv(occ, S, O, q, len, err);
+    const int nm = collect_intv(occ, S, O, q, len, err, ticks);
     if (err) return err;
     SC_STAT(0, 1);
     SC_STAT(1, nm);
-    SC_TICK(0);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (ticks) t_last = __builtin_amdgcn_s_memrealtime();
+#endif
     // mem_chain
     int32_t ns = 0, ncv = 0;
     for (int k = 0; k < S.hsize; ++k) S.hkey[k] = -1;
@@ -815,7 +867,7 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
             }
         }
     }
-    SC_TICK(1);
+    SC_TICK(3);
     SC_STAT(11, ncv);
     SC_STAT(12, (unsigned long long)ncv * ncv);
     // mem_chain_flt: the weight filter, then bwa's stable sort by weight (descending) of the
@@ -870,7 +922,7 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
             if (S.ch[S.kept[k]].first >= 0) S.ch[S.ch[S.kept[k]].first].kept = 1;
     }
     *n_chains = nch;
-    SC_TICK(2);   // (mem_chain_flt: with the filter + output part, as before the split)
+    SC_TICK(4);
     return 0;
 }
 
@@ -966,7 +1018,7 @@ SC_HD int map_output(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
     *n_out = no;
     SC_STAT(14, nch);
     SC_STAT(15, no);
-    SC_TICK(2);
+    SC_TICK(5);
     return 0;
 }
 
@@ -1059,7 +1111,7 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += 2 * align8((int64_t)sizeof(Chain) * c.chains);  // cv, ch
     b += 2 * align8(4 * (int64_t)c.chains);              // cnx, kept
     b += 3 * align8(4 * (int64_t)range_table_size(c.chains));   // hkey, hhead, htail
-    b += align8(2 * (int64_t)(c.lmax + 1));              // rmax
+    b += align8(2 * (int64_t)(c.lmax + 1) * RK);         // rmax
     if (c.hi) b += align8((int64_t)c.hits);              // hhi (last)
     return b;
 }
@@ -1098,7 +1150,7 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.hhead = (int32_t *)take(4 * (int64_t)S.hsize);
     S.htail = (int32_t *)take(4 * (int64_t)S.hsize);
     S.cap_chains = c.chains;
-    S.rmax = (uint16_t *)take(2 * (int64_t)(c.lmax + 1));
+    S.rmax = (uint16_t *)take(2 * (int64_t)(c.lmax + 1) * RK);
     S.hhi = c.hi ? (uint8_t *)take((int64_t)c.hits) : nullptr;
     return S;
 }

@@ -173,20 +173,18 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
         wave_sync_lds();
         // the count table, a lane per start: ge[a][t] = #{hits of a with ml - KI >= t} summed
         // directly in registers (no zeroing, no atomics, no suffix pass over HBM)
-        // and R_1(a), the end of the start's longest match (seed_core.h rmax_k: smem1's backward
-        // extension sweeps it), from the same hits, or below 12 bases from the j-mer counts
+        // and R_1 .. R_RK(a), the ends of the start's longest matches with >= k occurrences
+        // (seed_core.h fill_rk: smem1's backward extension sweeps them), from the same hits, or
+        // below 12 bases from the j-mer counts
         const seedc::Occ occ{&V, &S, q, len, nullptr};
         for (int a = lane; a < len; a += 64) {
             uint32_t g[HB];
 #pragma unroll
             for (int t = 0; t < HB; ++t) g[t] = 0u;
-            int mmax = 0;
             const bool has = a + KI <= len && S.codes[a] >= 0;
             if (has) {
                 for (int h = ho[a]; h < ho[a + 1]; ++h) {
-                    const int ml = (int)S.hml[h];
-                    const int d = ml - KI;
-                    mmax = mmax > ml ? mmax : ml;
+                    const int d = (int)S.hml[h] - KI;
 #pragma unroll
                     for (int t = 0; t < HB; ++t) g[t] += d >= t ? 1u : 0u;
                 }
@@ -194,9 +192,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
             uint32_t *dst = S.ge + (int64_t)a * HB;
 #pragma unroll
             for (int t = 0; t < HB; ++t) dst[t] = g[t];
-            int e = a;
-            if (q[a] < 4) e = mmax > 0 ? a + mmax : seedc::rmax_short(occ, q, len, a, 1);
-            S.rmax[a] = (uint16_t)e;
+            seedc::fill_rk(occ, S, q, len, a);
         }
         __threadfence_block();
     }
@@ -217,13 +213,18 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
     seedc::Scratch S = seedc::carve(D.scratch + slot * D.stride, D.caps);
     int32_t *ho = hoff_lds[wv];
     unsigned long long pt[4] = {0ULL, 0ULL, 0ULL, 0ULL};   // lane 0: phase ticks of this wave
+    unsigned long long pl[6] = {0ULL, 0ULL, 0ULL, 0ULL, 0ULL, 0ULL};   // lane 0: seed_core.h's parts
     for (;;) {
         int j = 0;
         if (lane == 0) j = atomicAdd(D.next, 1);
         j = __shfl(j, 0, 64);
         if (j >= D.n_list) {   // every wave reaches this: the grid drains
-            if (D.prof && lane == 0)
+            if (D.prof && lane == 0) {
+                pt[1] += pl[0] + pl[1] + pl[2];
+                pt[2] += pl[3] + pl[4];
+                pt[3] += pl[5];
                 for (int k = 0; k < 4; ++k) atomicAdd(&D.prof[k], pt[k]);
+            }
             break;
         }
         const int i = D.rlist ? D.rlist[j] : j;
@@ -241,7 +242,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
         if (lane == 0) {
             if (D.prof) pt[0] += wall_clock64() - t0;
             if (len > 0 && !err) {
-                err = seedc::map_chains(D.V, D.O, S, q, len, &nch, D.prof ? pt + 1 : nullptr, lcnt);
+                err = seedc::map_chains(D.V, D.O, S, q, len, &nch, D.prof ? pl : nullptr, lcnt);
                 if (!err && seedc::seed_flt_min_score(D.O, len) >= 0 && 3 * S.cap_seeds <= S.cap_hits &&
                     2 * 201 * 64 * 2 <= 4 * S.lmax * seedc::HB)
                     nlist = seedc::flt_seed_list(S, nch, (int32_t *)S.hpos + S.cap_seeds, S.cap_seeds);
@@ -275,7 +276,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
             if (len > 0 && !err)
                 err = seedc::map_output(D.V, D.O, S, q, len, i, nch, D.out + (int64_t)(i - D.out0) * D.caps.out,
                                         D.caps.out, &n, nlist >= 0 ? (const int32_t *)S.hpos : nullptr,
-                                        D.prof ? pt + 1 : nullptr);
+                                        D.prof ? pl : nullptr);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
         }
@@ -300,7 +301,8 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
     uint8_t *base = D.scratch + slot * 64 * D.stride;
     int32_t *ho = hoff_lds[wv];
     unsigned long long pt[2] = {0ULL, 0ULL};   // wave wall-clock: occurrence tables, lane work
-    unsigned long long lt[3] = {0ULL, 0ULL, 0ULL};   // per lane: SMEMs, chaining, filter + output
+    // per lane: SMEM pass, re-seeding, -y seeds + sort, chaining, mem_chain_flt, filter + output
+    unsigned long long lt[6] = {0ULL, 0ULL, 0ULL, 0ULL, 0ULL, 0ULL};
     for (;;) {
         int b0 = 0;
         if (lane == 0) b0 = atomicAdd(D.next, 64);
@@ -309,13 +311,13 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
         if (b0 >= nlim) {   // every wave reaches this: the grid drains
             if (D.prof) {
 #pragma unroll
-                for (int k = 0; k < 3; ++k)
+                for (int k = 0; k < 6; ++k)
                     for (int o = 32; o > 0; o >>= 1) lt[k] += __shfl_xor(lt[k], o, 64);
             }
             if (D.prof && lane == 0) {
                 atomicAdd(&D.prof[0], pt[0]);
                 atomicAdd(&D.prof[1], pt[1]);
-                for (int k = 0; k < 3; ++k) atomicAdd(&D.prof[4 + k], lt[k]);   // lane-summed
+                for (int k = 0; k < 6; ++k) atomicAdd(&D.prof[4 + k], lt[k]);   // lane-summed
             }
             break;
         }

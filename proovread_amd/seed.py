@@ -203,6 +203,11 @@ def _phase_ms(L, ctx) -> dict:
     out = {k: round(float(v) / 1e5, 1) for k, v in
            zip(("occ_table", "lane_phase_and_pass2_smems", "pass2_chaining", "pass2_filter_out"), t)}
     out["pass2_reads"] = n2.value
+    lt = np.zeros(6, np.uint64)
+    L.pr_seed_gpu_lane_ticks.argtypes = [C.c_void_p, C.c_void_p]
+    _abi.check(L.pr_seed_gpu_lane_ticks(ctx.h, lt.ctypes.data), "pr_seed_gpu_lane_ticks")
+    out["pass1_lane_ms_summed"] = {k: round(float(v) / 1e5, 1) for k, v in
+                                   zip(("smem_pass", "reseeding", "y_seeds_sort", "chaining", "chain_flt", "output"), lt)}
     p2 = C.c_double()
     _abi.check(L.pr_seed_gpu_pass2_ms(ctx.h, C.byref(p2)), "pr_seed_gpu_pass2_ms")
     out["pass2_wall_ms"] = round(p2.value, 1)

@@ -97,6 +97,12 @@ def test_one_rank_share_on_one_gpu(cfg, monkeypatch):
     rec["group_peaks"] = {k: v["peak"] for k, v in mem["groups"].items()}
     rec["seeds"] = out.n_tasks
     it = st.last_iteration
+    L0 = _abi.lib()
+    rec["event_ms"] = {"index": round(seed._last_ms(L0.pr_seed_gpu_index_last_ms, ctx), 1),
+                       "seeding": round(seed._last_ms(L0.pr_seed_gpu_last_ms, ctx), 1),
+                       **{k: round(v, 1) for k, v in zip(("sw_extend", "sw_global_cigar", "exchange_handoff",
+                                                          "consensus"), it.timing())}}
+    rec["seeding_phases"] = seed._phase_ms(L0, ctx)
     rec["alignments"] = it.alignment_stats()[0]
     _log(cfg, rec)
     status = it.statuses()
