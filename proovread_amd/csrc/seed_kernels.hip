@@ -64,7 +64,7 @@ __device__ __forceinline__ uint64_t nib16(const uint64_t *w4, uint64_t x) {
 }
 
 __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, const uint8_t *q, int len, int32_t *ho,
-                              int lane, uint64_t *q4) {
+                              int lane, uint64_t *q4, const uint32_t *lc) {
     using seedc::HB;
     using seedc::KI;
     using seedc::KX;
@@ -176,7 +176,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
         // and R_1 .. R_RK(a), the ends of the start's longest matches with >= k occurrences
         // (seed_core.h fill_rk: smem1's backward extension sweeps them), from the same hits, or
         // below 12 bases from the j-mer counts
-        const seedc::Occ occ{&V, &S, q, len, nullptr};
+        const seedc::Occ occ{&V, &S, q, len, lc};
         for (int a = lane; a < len; a += 64) {
             uint32_t g[HB];
 #pragma unroll
@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
         int err = 0;
         const unsigned long long t0 = D.prof && lane == 0 ? wall_clock64() : 0ULL;
         if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
-        if (len > 0 && !err) err = build_occ_wave(D.V, S, q, len, ho, lane, q4_lds[wv]);
+        if (len > 0 && !err) err = build_occ_wave(D.V, S, q, len, ho, lane, q4_lds[wv], lcnt);
         // SMEMs and chaining on lane 0; then, for reads where bwa runs mem_flt_chained_seeds
         // (>= 440 bp), the seeds' local SW scores over all 64 lanes (a seed per lane, the rows
         // int16 and lane-interleaved in the dead count table); the output on lane 0
@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             seedc::Scratch S = seedc::carve(base + (int64_t)rd * D.stride, D.caps);
             int err = 0;
             if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
-            if (len > 0 && !err) err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv]);
+            if (len > 0 && !err) err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt);
             if (lane == rd) my_err = err;
         }
         const unsigned long long t1 = D.prof ? wall_clock64() : 0ULL;
