@@ -93,12 +93,9 @@ struct Seed {
     int32_t qbeg, len;
 };
 struct Chain {
-    int64_t pos;                  // its first seed's rbeg
-    int64_t lrb;                  // its last seed's rbeg
+    int64_t pos;
     int32_t rid, head, tail, n;   // seeds: a linked list in the pool (only ever appended)
     int32_t w, kept, first;
-    int32_t fq, lq, llen;         // first seed's qbeg, last seed's qbeg and length (kept here so
-                                  // test_and_merge reads one record, not two seeds behind it)
 };
 
 enum {
@@ -628,22 +625,21 @@ SC_HD int range_slot(const Scratch &S, int32_t key) {
 // -> 1 merged, 0 not, -1 pool full
 SC_HD int test_and_merge(const pr_seed_opts &O, int64_t l_pac, Scratch &S, int32_t &ns, Chain &c, const Seed &p,
                          int rid) {
-    const int64_t qend = (int64_t)c.lq + c.llen, rend = c.lrb + c.llen;
+    const Seed &last = S.seeds[c.tail];
+    const Seed &first = S.seeds[c.head];
+    const int64_t qend = last.qbeg + last.len, rend = last.rbeg + last.len;
     if (rid != c.rid) return 0;
-    if (p.qbeg >= c.fq && p.qbeg + p.len <= qend && p.rbeg >= c.pos && p.rbeg + p.len <= rend)
+    if (p.qbeg >= first.qbeg && p.qbeg + p.len <= qend && p.rbeg >= first.rbeg && p.rbeg + p.len <= rend)
         return 1;   // contained seed
-    if ((c.lrb < l_pac || c.pos < l_pac) && p.rbeg >= l_pac) return 0;   // other strand
-    const int64_t x = p.qbeg - c.lq, y = p.rbeg - c.lrb;
-    if (y >= 0 && x - y <= O.w && y - x <= O.w && x - c.llen < O.max_chain_gap && y - c.llen < O.max_chain_gap) {
+    if ((last.rbeg < l_pac || first.rbeg < l_pac) && p.rbeg >= l_pac) return 0;   // other strand
+    const int64_t x = p.qbeg - last.qbeg, y = p.rbeg - last.rbeg;
+    if (y >= 0 && x - y <= O.w && y - x <= O.w && x - last.len < O.max_chain_gap && y - last.len < O.max_chain_gap) {
         if (ns >= S.cap_seeds) return -1;
         S.seeds[ns] = p;
         S.next[ns] = -1;
         S.next[c.tail] = ns;
         c.tail = ns++;
         ++c.n;
-        c.lq = p.qbeg;
-        c.llen = p.len;
-        c.lrb = p.rbeg;
         return 1;
     }
     return 0;
@@ -857,14 +853,12 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
                 S.seeds[ns] = s;
                 S.next[ns] = -1;
                 Chain c;
-                c.pos = c.lrb = s.rbeg;
+                c.pos = s.rbeg;
                 c.rid = rid;
                 c.head = c.tail = ns++;
                 c.n = 1;
                 c.w = c.kept = 0;
                 c.first = -1;
-                c.fq = c.lq = s.qbeg;
-                c.llen = s.len;
                 S.cv[ncv] = c;
                 if (!found) {   // the range's first chain
                     S.hkey[hs] = key[u];
@@ -912,12 +906,12 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
         S.ch[0].kept = 3;
         for (int i = 1; i < nch; ++i) {
             int large = 0, k;
-            const int bi = S.ch[i].fq;
-            const int ei = S.ch[i].lq + S.ch[i].llen;
+            const int bi = S.seeds[S.ch[i].head].qbeg;
+            const int ei = S.seeds[S.ch[i].tail].qbeg + S.seeds[S.ch[i].tail].len;
             for (k = 0; k < nk; ++k) {
                 Chain &cj = S.ch[S.kept[k]];
-                const int bj = cj.fq;
-                const int ej = cj.lq + cj.llen;
+                const int bj = S.seeds[cj.head].qbeg;
+                const int ej = S.seeds[cj.tail].qbeg + S.seeds[cj.tail].len;
                 const int bmax = bj > bi ? bj : bi;
                 const int emin = ej < ei ? ej : ei;
                 if (emin > bmax) {
