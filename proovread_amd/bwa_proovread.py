@@ -28,8 +28,11 @@ per long read, bin = int((POS + length/2) / BIN) with Sam::Alignment's length
 rule (Alignment.pm:417-431), ncscore = AS/length * length/(40+length); a bin
 holding more than LEN bases admits a record only if it beats the bin's lowest
 ncscore, which it then evicts.  Records pass through it in output order and the
-survivors are printed in that order (parity unpinned).  Not restated:
-mem_sort_dedup_patch, bwa's MAPQ model.
+survivors are printed in that order (parity unpinned).  The rest of bwa
+mem's per-read alignment (mem_chain2aln over every seed of the kept chains,
+mem_sort_dedup_patch with mem_patch_reg, mem_mark_primary_se, mem_reg2sam's -T / -D
+filters) runs on the device (sw.run in bwa mode).  Not restated: bwa's MAPQ model
+(MAPQ is 60 for primary, 0 for secondary records).
 """
 from __future__ import annotations
 

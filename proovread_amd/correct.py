@@ -194,8 +194,13 @@ class ShortReads:
             lens = s1 - s0
             self.off = np.zeros(len(lens) + 1, np.int64)
             np.cumsum(lens, out=self.off[1:])
-            idx = np.repeat(s0 - self.off[:-1], lens) + np.arange(int(self.off[-1]), dtype=np.int64)
-            self.pool = NT4[arr[idx]]
+            # the sequence lines' bytes by a byte mask (+1 at each line start, -1 at its end,
+            # running sum > 0): ~3 bytes per input byte instead of an int64 index per base
+            d = np.zeros(len(arr) + 1, np.int8)
+            d[s0] = 1
+            d[s1] -= 1
+            self.pool = NT4[arr[np.cumsum(d[:-1], dtype=np.int8) > 0]]
+            del d
         else:
             self.pool, self.off = _pool(seqs)
             self.pool = NT4[self.pool]

@@ -65,21 +65,47 @@ __global__ void ix_text_kernel(uint8_t *lr_seq, const int64_t *lr_off, int n_lr,
   }
 }
 
-__global__ void ix_keys_kernel(const uint8_t *text, int64_t n, uint32_t *key, uint32_t *val, uint32_t *kc) {
+// the 12-mer at every text position as a sort key (NK: none), no histogram: the hits' offsets
+// come from the sorted keys (ix_koff_kernel; round 4 counted 290 M positions with global
+// atomics, 10.8 ms of the 28 ms build at configs[1]).  The 12 bases from 4 dwords (the text
+// buffer has 64 bytes of slack) aligned with v_alignbyte.
+__global__ void ix_keys_kernel(const uint8_t *text, int64_t n, uint32_t *key, uint32_t *val) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
     uint32_t code = 0;
     bool ok = p + KI <= n;
     if (ok) {
-        for (int x = 0; x < KI; ++x) {
-            const uint8_t c = text[p + x];
-            ok &= c < 4;
+        const uint32_t *tw = reinterpret_cast<const uint32_t *>(text) + (p >> 2);
+        const uint32_t sh = (uint32_t)(p & 3);
+        const uint32_t w0 = tw[0], w1 = tw[1], w2 = tw[2], w3 = tw[3];
+        const uint32_t x[3] = {__builtin_amdgcn_alignbyte(w1, w0, sh), __builtin_amdgcn_alignbyte(w2, w1, sh),
+                               __builtin_amdgcn_alignbyte(w3, w2, sh)};
+#pragma unroll
+        for (int j = 0; j < KI; ++j) {
+            const uint32_t c = (x[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            ok &= c < 4u;
             code = (code << 2) | (c & 3u);
         }
     }
     key[p] = ok ? code : NK;
     val[p] = (uint32_t)p;
-    if (ok) atomicAdd(&kc[code], 1u);
+}
+
+// koff from the sorted keys: koff[c] = the first slot with key >= c, for every c <= NK (each c
+// written once: by the slot where the key steps past it, the codes after the last key by the
+// last slot); then kc[c] = koff[c + 1] - koff[c] for the j-mer tables
+__global__ void ix_koff_kernel(const uint32_t *skey, int64_t n, uint64_t *koff) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = skey[i] < NK ? skey[i] : NK;
+    const int64_t kp = i > 0 ? (int64_t)(skey[i - 1] < NK ? skey[i - 1] : NK) : -1;
+    for (int64_t c = kp + 1; c <= (int64_t)k; ++c) koff[c] = (uint64_t)i;
+    if (i == n - 1)
+        for (int64_t c = (int64_t)k + 1; c <= (int64_t)NK; ++c) koff[c] = (uint64_t)n;
+}
+__global__ void ix_kc_kernel(const uint64_t *koff, uint32_t *kc) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < (int64_t)NK) kc[c] = (uint32_t)(koff[c + 1] - koff[c]);
 }
 
 // the KX bases after the 12-mer at text position p: the 9 dwords around them loaded at once
@@ -219,18 +245,19 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
         // one sort: 12-mer keys + histogram, koff = exclusive scan, stable sort of (key,
         // position) by key (positions ascend within a k-mer) straight into kpos, then kext
         if (n > 0) {
-            hipLaunchKernelGGL(ix_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.key0, B.val0,
-                               B.kc);
+            hipLaunchKernelGGL(ix_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.key0, B.val0);
             IXCHK(hipGetLastError());
-        }
-        size_t tb = B.temp_bytes;
-        IXCHK(rocprim::exclusive_scan(B.temp, tb, B.kc, B.koff, (uint64_t)0, (size_t)NK + 1, rocprim::plus<uint64_t>(), s));
-        if (n > 0) {
-            tb = B.temp_bytes;
+            size_t tb = B.temp_bytes;
             IXCHK(rocprim::radix_sort_pairs(B.temp, tb, B.key0, B.key1, B.val0, B.kpos, (size_t)n, 0u, 25u, s));
+            hipLaunchKernelGGL(ix_koff_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.key1, n, B.koff);
+            IXCHK(hipGetLastError());
+            hipLaunchKernelGGL(ix_kc_kernel, dim3(blocks_for((int64_t)NK, 256)), dim3(256), 0, s, B.koff, B.kc);
+            IXCHK(hipGetLastError());
             hipLaunchKernelGGL(ix_kext_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kpos, B.koff,
                                B.kext);
             IXCHK(hipGetLastError());
+        } else {
+            IXCHK(hipMemsetAsync(B.koff, 0, ((size_t)NK + 1) * 8, s));
         }
     } else {
         // chunks of B.chunk positions (a divisor of 2^32, so one starts at 2^32): the global
