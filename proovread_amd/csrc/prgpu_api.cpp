@@ -2186,20 +2186,37 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         int e = seed_batch_launch(K, (void *)s);
         if (e) return set_error(PR_ERR_HIP, "seed kernel: %s", hipGetErrorString((hipError_t)e));
         if (r0 == 0) HIPCHK(hipEventRecord(c->ev[10], s));
-        std::vector<int32_t> st1((size_t)(r1 - r0));
-        if ((rc = download(st1.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0))) return rc;
+        std::vector<int32_t> st1((size_t)(r1 - r0)), no1((size_t)(r1 - r0));
+        if ((rc = download(st1.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0)) ||
+            (rc = download(no1.data(), D[SB_NOUT], (size_t)(r1 - r0), s, (size_t)r0)))
+            return rc;
         HIPCHK(hipStreamSynchronize(s));
         std::vector<int32_t> redo;
         int32_t fl1 = 0;
+        int64_t need_hits = 0;   // the largest hit table a flagged read asked for
         for (int64_t i = r0; i < r1; ++i)
-            if (st1[(size_t)(i - r0)]) redo.push_back((int32_t)i), fl1 |= st1[(size_t)(i - r0)];
+            if (st1[(size_t)(i - r0)]) {
+                redo.push_back((int32_t)i);
+                fl1 |= st1[(size_t)(i - r0)];
+                need_hits = std::max<int64_t>(need_hits, -(int64_t)no1[(size_t)(i - r0)]);
+            }
         // many flagged reads (the finish task maps to corrected reads at 30x long-read coverage:
         // ~140 starts x 30 hits > 4096 for nearly every read): pass 1 again, lane per read, over
         // them with the arrays that overflowed grown (within the scratch already allocated),
         // instead of pass 2's one wave per read
         if (redo.size() > 4096 && !(fl1 & (seedc::SC_OVER_LEN | seedc::SC_OVER_OUT))) {
             seedc::Caps cb = small;
-            if (fl1 & seedc::SC_OVER_HITS) cb.hits *= 4;
+            // the hit tables sized for the largest flagged read (dense indexes: configs[2] /
+            // configs[3], or N > 1 ranks of the exact layout, every read overflows pass 1)
+            if (fl1 & seedc::SC_OVER_HITS) {
+                cb.hits = (int32_t)std::min<int64_t>(std::max<int64_t>(4 * (int64_t)cb.hits, (need_hits + 1023) & ~(int64_t)1023),
+                                                     (int64_t)1 << 20);
+                // their chaining never ran; random 12-mer hits become chains and seeds in
+                // proportion to the hits, so those arrays grow by the same factor
+                const int64_t f = std::min<int64_t>(16, std::max<int64_t>(1, cb.hits / small.hits));
+                cb.chains = (int32_t)(cb.chains * f);
+                cb.seeds = (int32_t)(cb.seeds * f);
+            }
             if (fl1 & seedc::SC_OVER_IV) cb.iv *= 2;
             if (fl1 & seedc::SC_OVER_MEMS) cb.mems *= 2;
             if (fl1 & seedc::SC_OVER_SEEDS) cb.seeds *= 2;

@@ -64,7 +64,7 @@ __device__ __forceinline__ uint64_t nib16(const uint64_t *w4, uint64_t x) {
 }
 
 __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, const uint8_t *q, int len, int32_t *ho,
-                              int lane, uint64_t *q4, const uint32_t *lc) {
+                              int lane, uint64_t *q4, const uint32_t *lc, int *n_hits = nullptr) {
     using seedc::HB;
     using seedc::KI;
     using seedc::KX;
@@ -119,6 +119,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
         run += __shfl(x, 63, 64);
     }
     const int nh = run;
+    if (n_hits) *n_hits = nh;
     if (nh > S.cap_hits) err = seedc::SC_OVER_HITS;
     wave_sync_lds();
     __threadfence_block();
@@ -322,17 +323,17 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             break;
         }
         const unsigned long long t0 = D.prof ? wall_clock64() : 0ULL;
-        int my_err = 0;
+        int my_err = 0, my_hits = 0;
         const int nb = (int)(nlim - b0 < 64 ? nlim - b0 : 64);
         for (int rd = 0; rd < nb; ++rd) {
             const int i = D.rlist ? D.rlist[b0 + rd] : b0 + rd;
             const int64_t o = D.sr_off[i];
             const int len = (int)(D.sr_off[i + 1] - o);
             seedc::Scratch S = seedc::carve(base + (int64_t)rd * D.stride, D.caps);
-            int err = 0;
+            int err = 0, nh = 0;
             if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
-            if (len > 0 && !err) err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt);
-            if (lane == rd) my_err = err;
+            if (len > 0 && !err) err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt, &nh);
+            if (lane == rd) my_err = err, my_hits = nh;
         }
         const unsigned long long t1 = D.prof ? wall_clock64() : 0ULL;
         if (lane < nb) {
@@ -345,7 +346,9 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
                 err = seedc::map_after_occ(D.V, D.O, S, D.sr_seq + o, len, i, D.out + (int64_t)(i - D.out0) * D.caps.out,
                                            D.caps.out, &n, D.prof ? lt : nullptr, lcnt,
                                            D.dp ? D.dp + slot * (2 * 201 * 64) + lane : nullptr);
-            D.n_out[i] = err ? 0 : n;
+            // a read whose hit table overflowed reports the hits it needs (the retry pass sizes
+            // its slices from them: texts of 1 - 3 Gb give ~20-50 k hits per 150 bp read)
+            D.n_out[i] = (my_err & seedc::SC_OVER_HITS) ? -my_hits : (err ? 0 : n);
             D.status[i] = err;
         }
         if (D.prof && lane == 0) {
