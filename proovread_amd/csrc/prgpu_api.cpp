@@ -1863,6 +1863,8 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
     const int64_t l_pac = n_lr ? lr_off[n_lr] - lr_off[0] : 0;
     if (2 * l_pac + 2 * (int64_t)n_lr > seedc::MAX_TEXT)
         return set_error(PR_ERR_CAPACITY, "long reads beyond the index's 2^33 text positions (l_pac < 4.29 Gb)");
+    if ((int64_t)n_lr >= ((int64_t)1 << seedc::FR_RID_BITS))
+        return set_error(PR_ERR_CAPACITY, "more than 2^24 long reads in one index");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
     DevBuf *D = c->sd;

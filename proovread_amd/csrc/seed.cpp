@@ -247,6 +247,7 @@ struct HostScratch {
     std::vector<uint32_t> ge, hpos;
     std::vector<uint8_t> hhi;
     std::vector<uint16_t> hml, rmax;
+    std::vector<uint64_t> hfr;
     std::vector<seedc::Iv> mems, m1, curr, prev;
     std::vector<seedc::Seed> seeds;
     std::vector<int32_t> next, cnx, kept, hkey, hhead, htail;
@@ -266,6 +267,7 @@ struct HostScratch {
         rmax.resize(((size_t)lmax + 1) * seedc::RK);
         hpos.resize((size_t)hits);
         hml.resize((size_t)hits);
+        hfr.resize((size_t)hits);
         mems.resize((size_t)mems_cap);
         m1.resize((size_t)iv);
         curr.resize((size_t)iv);
@@ -287,6 +289,7 @@ struct HostScratch {
                            ch.data(),   cnx.data(),   kept.data(), hkey.data(), hhead.data(),
                            htail.data(), chains,      hs};
         S.rmax = rmax.data();
+        S.hfr = hfr.data();
     }
     void grow(int err) {
         if (err & seedc::SC_OVER_HITS) hits *= 2;
@@ -374,6 +377,8 @@ extern "C" int pr_seed_index_build(const uint8_t *lr_seq, const int64_t *lr_off,
     const int64_t l_pac = n_lr ? lr_off[n_lr] - lr_off[0] : 0;
     if (2 * l_pac + 2 * (int64_t)n_lr > seedc::MAX_TEXT)
         return pr_set_error(PR_ERR_CAPACITY, "long reads beyond the index's 2^33 text positions (l_pac < 4.29 Gb)");
+    if ((int64_t)n_lr >= ((int64_t)1 << seedc::FR_RID_BITS))
+        return pr_set_error(PR_ERR_CAPACITY, "more than 2^24 long reads in one index");
     pr_seed_index *h = new pr_seed_index;
     Index &I = h->I;
     I.n_lr = n_lr;

@@ -126,6 +126,7 @@ struct Scratch {
     int32_t *hkey, *hhead, *htail;             // [hsize] range table: key (-1 free), list head / tail
     int32_t cap_chains, hsize;                 // hsize: power of two >= 2 * cap_chains
     uint16_t *rmax;                            // [(lmax + 1) * RK] R_k(a), k = 1..RK (rmax_k)
+    uint64_t *hfr;                             // [cap_hits] pack_fr of the hit (the chaining's coordinates)
 };
 
 SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
@@ -162,6 +163,34 @@ SC_HD uint64_t get_hpos(const Scratch &S, int64_t k) {
 SC_HD void set_hpos(const Scratch &S, int64_t k, uint64_t p) {
     S.hpos[k] = (uint32_t)p;
     if (S.hhi) S.hhi[k] = (uint8_t)(p >> 32);
+}
+
+// ---------------------------------------------------------------- text -> bwa coordinates
+SC_HD int contig_of(const IndexView &I, int64_t p) {
+    int c = I.cblk[p >> CB_SHIFT];
+    while (c + 1 < I.n_contig && I.cstart[c + 1] <= p) ++c;
+    return c;
+}
+
+SC_HD void text_to_fr(const IndexView &I, uint64_t p, int64_t &fr, int &rid) {
+    const int c = contig_of(I, p);
+    const int64_t o = (int64_t)p - I.cstart[c];
+    if (c < I.n_lr) {
+        rid = c;
+        fr = I.lr_off[c] + o;
+    } else {
+        rid = 2 * I.n_lr - 1 - c;   // the reverse half holds the long reads in reverse order
+        fr = I.l_pac + (I.l_pac - I.lr_off[rid + 1]) + o;
+    }
+}
+
+// a hit's forward-reverse coordinate and long read, packed for the chaining (rid < 2^24)
+constexpr int FR_RID_BITS = 24;
+SC_HD uint64_t pack_fr(const IndexView &I, uint64_t p) {
+    int64_t fr;
+    int rid;
+    text_to_fr(I, p, fr, rid);
+    return ((uint64_t)fr << FR_RID_BITS) | (uint64_t)rid;
 }
 
 // ---------------------------------------------------------------- occurrence table
@@ -351,6 +380,7 @@ SC_HD int build_occ(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
                         while (a + ml < len && q[a + ml] < 4 && T[p + ml] == q[a + ml]) ++ml;
                 }
                 set_hpos(S, nh, p);
+                S.hfr[nh] = pack_fr(I, p);
                 S.hml[nh] = (uint16_t)(ml < 65535 ? ml : 65535);
                 ++nh;
                 ++g[ml - KI < HB - 1 ? ml - KI : HB - 1];
@@ -587,24 +617,6 @@ SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const 
 }
 
 // ---------------------------------------------------------------- chaining
-SC_HD int contig_of(const IndexView &I, int64_t p) {
-    int c = I.cblk[p >> CB_SHIFT];
-    while (c + 1 < I.n_contig && I.cstart[c + 1] <= p) ++c;
-    return c;
-}
-
-SC_HD void text_to_fr(const IndexView &I, uint64_t p, int64_t &fr, int &rid) {
-    const int c = contig_of(I, p);
-    const int64_t o = (int64_t)p - I.cstart[c];
-    if (c < I.n_lr) {
-        rid = c;
-        fr = I.lr_off[c] + o;
-    } else {
-        rid = 2 * I.n_lr - 1 - c;   // the reverse half holds the long reads in reverse order
-        fr = I.l_pac + (I.l_pac - I.lr_off[rid + 1]) + o;
-    }
-}
-
 // ---------------------------------------------------------------- chain order
 // mem_chain keeps its chains in a btree by pos (ties: creation order) and tests every
 // occurrence against the chain with the largest pos <= its rbeg (the predecessor).
@@ -804,16 +816,14 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
                     sel[nsel++] = k;
                 }
             }
-            uint64_t hp[CB];
             int64_t rb[CB];
             int rd[CB], hsl[CB];
             int32_t key[CB];
 #pragma unroll
-            for (int u = 0; u < CB; ++u) hp[u] = u < nsel ? get_hpos(S, sel[u]) : 0ull;
-#pragma unroll
             for (int u = 0; u < CB; ++u) {
-                rb[u] = 0, rd[u] = 0;
-                if (u < nsel) text_to_fr(I, hp[u], rb[u], rd[u]);
+                const uint64_t v = u < nsel ? S.hfr[sel[u]] : 0ull;   // coordinates from the occurrence table
+                rb[u] = (int64_t)(v >> FR_RID_BITS);
+                rd[u] = (int)(v & ((1u << FR_RID_BITS) - 1u));
                 key[u] = rd[u] * 2 + (rb[u] >= I.l_pac ? 1 : 0);
             }
 #pragma unroll
@@ -1123,6 +1133,7 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += 2 * align8(4 * (int64_t)c.chains);              // cnx, kept
     b += 3 * align8(4 * (int64_t)range_table_size(c.chains));   // hkey, hhead, htail
     b += align8(2 * (int64_t)(c.lmax + 1) * RK);         // rmax
+    b += align8(8 * (int64_t)c.hits);                    // hfr
     if (c.hi) b += align8((int64_t)c.hits);              // hhi (last)
     return b;
 }
@@ -1162,6 +1173,7 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.htail = (int32_t *)take(4 * (int64_t)S.hsize);
     S.cap_chains = c.chains;
     S.rmax = (uint16_t *)take(2 * (int64_t)(c.lmax + 1) * RK);
+    S.hfr = (uint64_t *)take(8 * (int64_t)c.hits);
     S.hhi = c.hi ? (uint8_t *)take((int64_t)c.hits) : nullptr;
     return S;
 }

@@ -168,6 +168,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                 }
             }
             seedc::set_hpos(S, k, p);
+            S.hfr[k] = seedc::pack_fr(V, p);   // the chaining's coordinates, lane-parallel here
             S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
         }
         __threadfence_block();
