@@ -2091,10 +2091,12 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     for (int i = 0; i < n_sr; ++i) qmax = std::max<int>(qmax, (int)(sr_off[i + 1] - sr_off[i]));
     seedc::Caps caps = seedc::device_caps(qmax);
     caps.hi = c->seed_view.ksplit != nullptr;   // text beyond 2^32: positions carry bit 32
+    caps.nopos = 1;   // the device tables keep the chaining's coordinates only (seed_core.h Caps)
     // pass 1: 64 reads per wave, small slices sized for the batch; pass 2 (flagged reads): the
     // large slices, one wave per read
     seedc::Caps small = seedc::device_caps_small(std::min(qmax, caps.lmax));
     small.hi = caps.hi;
+    small.nopos = 1;
     if (const char *sc = getenv("PRGPU_SEED_SMALL"))   // tuning hook: hits,iv,mems,seeds,chains
         sscanf(sc, "%d,%d,%d,%d,%d", &small.hits, &small.iv, &small.mems, &small.seeds, &small.chains);
     SeedDev K{};
@@ -2114,8 +2116,16 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         const int64_t rounds = (nbatch + waves - 1) / waves;
         waves = (nbatch + rounds - 1) / rounds;
     }
-    {   // pass 1's slices within a scratch budget (long mr reads: fewer waves, ~24 GB)
-        const int64_t wmax = std::max<int64_t>(c->n_cu, ((int64_t)24 << 30) / (64 * K.stride));
+    {   // pass 1's slices within a scratch budget: 15 % of the free device memory, between 24 and
+        // 40 GB (configs[1]'s 16 waves per CU need ~32 GB; long mr reads: fewer waves).  (Round 4
+        // capped it at 24 GB, which cut configs[1] to ~3,800 of its 4,096 waves.)
+        size_t fr = 0, tot = 0;
+        (void)hipMemGetInfo(&fr, &tot);
+        (void)hipGetLastError();
+        const int64_t have = (int64_t)D[SB_SCRATCH].cap;   // (already ours: counts as free)
+        const int64_t budget = std::min<int64_t>((int64_t)40 << 30,
+                                                 std::max<int64_t>((int64_t)24 << 30, ((int64_t)fr + have) * 15 / 100));
+        const int64_t wmax = std::max<int64_t>(c->n_cu, budget / (64 * K.stride));
         if (waves > wmax) waves = wmax;
     }
     K.n_lanes = waves;

@@ -161,6 +161,7 @@ SC_HD uint64_t get_hpos(const Scratch &S, int64_t k) {
     return (uint64_t)S.hpos[k] | (S.hhi ? (uint64_t)S.hhi[k] << 32 : 0ull);
 }
 SC_HD void set_hpos(const Scratch &S, int64_t k, uint64_t p) {
+    if (!S.hpos) return;
     S.hpos[k] = (uint32_t)p;
     if (S.hhi) S.hhi[k] = (uint8_t)(p >> 32);
 }
@@ -1074,7 +1075,9 @@ namespace seedc {
 // need more are flagged with the SC_OVER_* bit of the array that overflowed.
 struct Caps {
     int32_t lmax, hits, iv, mems, seeds, chains, out;
-    int32_t hi;   // the text reaches beyond 2^32: the hit table carries bit 32 of the positions (hhi)
+    int32_t hi;      // the text reaches beyond 2^32: the hit table carries bit 32 of the positions (hhi)
+    int32_t nopos;   // no hit positions (hpos / hhi): the device's tables keep only the chaining's
+                     // coordinates (hfr); the host's build_occ follows diagonals through hpos
 };
 // output slots per read (the seeds of its kept chains): 384 for short reads, 2 per base for
 // the mr modes' 300-1000 bp reads (~300 seeds per 600 bp read at 15x long-read coverage)
@@ -1123,7 +1126,7 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += align8(8 * (int64_t)(c.lmax + 1));              // qext
     b += align8(4 * (int64_t)(c.lmax + 1));              // codes
     b += align8(4 * (int64_t)c.lmax * HB);               // ge
-    b += align8(4 * (int64_t)c.hits);                    // hpos
+    if (!c.nopos) b += align8(4 * (int64_t)c.hits);      // hpos
     b += align8(2 * (int64_t)c.hits);                    // hml
     b += align8((int64_t)sizeof(Iv) * c.mems);           // mems
     b += 3 * align8((int64_t)sizeof(Iv) * c.iv);         // m1, curr, prev
@@ -1134,7 +1137,7 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += 3 * align8(4 * (int64_t)range_table_size(c.chains));   // hkey, hhead, htail
     b += align8(2 * (int64_t)(c.lmax + 1) * RK);         // rmax
     b += align8(8 * (int64_t)c.hits);                    // hfr
-    if (c.hi) b += align8((int64_t)c.hits);              // hhi (last)
+    if (c.hi && !c.nopos) b += align8((int64_t)c.hits);  // hhi (last)
     return b;
 }
 
@@ -1151,7 +1154,7 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.qext = (uint64_t *)take(8 * (int64_t)(c.lmax + 1));
     S.codes = (int32_t *)take(4 * (int64_t)(c.lmax + 1));
     S.ge = (uint32_t *)take(4 * (int64_t)c.lmax * HB);
-    S.hpos = (uint32_t *)take(4 * (int64_t)c.hits);
+    S.hpos = c.nopos ? nullptr : (uint32_t *)take(4 * (int64_t)c.hits);
     S.hml = (uint16_t *)take(2 * (int64_t)c.hits);
     S.cap_hits = c.hits;
     S.mems = (Iv *)take((int64_t)sizeof(Iv) * c.mems);
@@ -1174,7 +1177,7 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.cap_chains = c.chains;
     S.rmax = (uint16_t *)take(2 * (int64_t)(c.lmax + 1) * RK);
     S.hfr = (uint64_t *)take(8 * (int64_t)c.hits);
-    S.hhi = c.hi ? (uint8_t *)take((int64_t)c.hits) : nullptr;
+    S.hhi = c.hi && !c.nopos ? (uint8_t *)take((int64_t)c.hits) : nullptr;
     return S;
 }
 

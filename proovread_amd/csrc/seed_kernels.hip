@@ -245,17 +245,17 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
             if (D.prof) pt[0] += wall_clock64() - t0;
             if (len > 0 && !err) {
                 err = seedc::map_chains(D.V, D.O, S, q, len, &nch, D.prof ? pl : nullptr, lcnt);
-                if (!err && seedc::seed_flt_min_score(D.O, len) >= 0 && 3 * S.cap_seeds <= S.cap_hits &&
+                if (!err && seedc::seed_flt_min_score(D.O, len) >= 0 && 3 * S.cap_seeds <= 2 * S.cap_hits &&
                     2 * 201 * 64 * 2 <= 4 * S.lmax * seedc::HB)
-                    nlist = seedc::flt_seed_list(S, nch, (int32_t *)S.hpos + S.cap_seeds, S.cap_seeds);
+                    nlist = seedc::flt_seed_list(S, nch, (int32_t *)S.hfr + S.cap_seeds, S.cap_seeds);
             }
         }
         err = __shfl(err, 0, 64);
         nlist = __shfl(nlist, 0, 64);
         if (nlist > 0) {
             __threadfence_block();
-            const int32_t *list = (const int32_t *)S.hpos + S.cap_seeds;
-            int32_t *rid = (int32_t *)S.hpos + 2 * S.cap_seeds;
+            const int32_t *list = (const int32_t *)S.hfr + S.cap_seeds;   // (the dead hit coordinates)
+            int32_t *rid = (int32_t *)S.hfr + 2 * S.cap_seeds;
             if (lane == 0) {   // each listed seed's long read (its chain's)
                 int x = 0;
                 for (int ci = 0; ci < nch; ++ci) {
@@ -265,7 +265,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
                 }
             }
             __threadfence_block();
-            int32_t *scores = (int32_t *)S.hpos;
+            int32_t *scores = (int32_t *)S.hfr;
             int16_t *H = (int16_t *)S.ge + lane, *E = H + 201 * 64;
             for (int x = lane; x < nlist; x += 64) {
                 const int32_t k = list[x];
@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
             int n = 0;
             if (len > 0 && !err)
                 err = seedc::map_output(D.V, D.O, S, q, len, i, nch, D.out + (int64_t)(i - D.out0) * D.caps.out,
-                                        D.caps.out, &n, nlist >= 0 ? (const int32_t *)S.hpos : nullptr,
+                                        D.caps.out, &n, nlist >= 0 ? (const int32_t *)S.hfr : nullptr,
                                         D.prof ? pl : nullptr);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
