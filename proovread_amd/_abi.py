@@ -148,7 +148,7 @@ class DevBuffer:
         check(lib().pr_dev_upload(self.ctx.h, self.ptr, a.ctypes.data, a.nbytes), "pr_dev_upload")
 
     def close(self):
-        if self.ptr:
+        if self.ptr and self.ctx.h:   # (never through a destroyed context's handle)
             lib().pr_dev_free(self.ctx.h, self.ptr)
             self.ptr = None
 

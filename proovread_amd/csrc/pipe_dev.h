@@ -42,6 +42,13 @@ int pipe_binfilter_launch(const PipeDev &P, int bin_size, double bin_length, int
 // dense pools of the consensus (d0), its quality (d1) and masked copy (d2) from the capacity layout
 int lr_compact_launch(const int64_t *src_off, const int32_t *len, const int64_t *dst_off, int n, const uint8_t *s0,
                       uint8_t *d0, const uint8_t *s1, uint8_t *d1, const uint8_t *s2, uint8_t *d2, void *stream);
+// the consensus input (SEQ bytes, CIGAR ops) copied into pools in the hand-off's order
+size_t cns_gather_temp_bytes(int64_t n);
+int cns_gather_offsets(const int64_t *aln_total, int64_t n, const int32_t *lseq, const int32_t *ncig, int64_t *sz_seq,
+                       int64_t *sz_cig, int64_t *nso, int64_t *nco, void *temp, size_t temp_bytes, void *stream);
+int cns_gather_copy(const int64_t *aln_total, int64_t n, const uint8_t *seq, const uint32_t *cig, int64_t *seq_off,
+                    const int32_t *lseq, int64_t *cig_off, const int32_t *ncig, const int64_t *nso, const int64_t *nco,
+                    uint8_t *gseq, uint32_t *gcig, void *stream);
 int iter_stats_launch(const int64_t *out_off, const int32_t *status, const int32_t *seq_len, const uint8_t *qual,
                       int n_lr, int min_char, unsigned long long *out, void *stream);
 

@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <rocprim/device/device_scan.hpp>
+
 #include "pipe_dev.h"
 
 namespace prgpu {
@@ -322,6 +324,90 @@ int pipe_launch(const PipeDev &P, int grid, void *stream, int lds_sort) {
     e = hipFuncSetAttribute((const void *)pipe_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds_sort);
     if (e != hipSuccess) return (int)e;
     hipLaunchKernelGGL(pipe_sort_kernel, dim3(grid), dim3(PIPE_THREADS), lds_sort, s, P);
+    return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// The consensus input in consensus order.  The hand-off lists each long read's alignments, but
+// their SEQ bytes sit in the short-read pool (sequencer order: short reads from anywhere on the
+// genome side by side) and their CIGAR ops in the SW output pool (task order); every consensus
+// phase that reads them (prep, state table, pileup windows) then touches a line per alignment
+// that holds other reads' bytes.  One pass copies them behind each other in the hand-off's order
+// (SEQ padded to dwords), and the consensus reads its alignments' inputs sequentially.
+__global__ void __launch_bounds__(256) cns_gather_sizes_kernel(const int64_t *aln_total, int64_t n, const int32_t *lseq,
+                                                               const int32_t *ncig, int64_t *sz_seq, int64_t *sz_cig) {
+    const int64_t m = *aln_total;
+    for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= n; g += (int64_t)gridDim.x * blockDim.x) {
+        const bool in = g < m;
+        sz_seq[g] = in ? (int64_t)((lseq[g] + 3) & ~3) : 0;
+        sz_cig[g] = in ? (int64_t)ncig[g] : 0;
+    }
+}
+
+__global__ void __launch_bounds__(256) cns_gather_kernel(const int64_t *aln_total, const uint8_t *seq, const uint32_t *cig,
+                                                         int64_t *seq_off, const int32_t *lseq, int64_t *cig_off,
+                                                         const int32_t *ncig, const int64_t *nso, const int64_t *nco,
+                                                         uint8_t *gseq, uint32_t *gcig) {
+    // a 16-lane group per alignment (four alignments in flight per wave: the copies are short
+    // and latency-bound); a group's lanes copy dwords k, k + 16, ... of the SEQ, then the ops
+    const int gl = threadIdx.x & 15;
+    const int64_t m = *aln_total;
+    const int64_t stride = ((int64_t)gridDim.x * blockDim.x) >> 4;
+    for (int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 4; g < m; g += stride) {
+        const int64_t so = seq_off[g], co = cig_off[g];
+        const int ls = lseq[g], nc = ncig[g];
+        const int64_t ds = nso[g], dc = nco[g];
+        uint32_t *dst = reinterpret_cast<uint32_t *>(gseq + ds);
+        const int nw = (ls + 3) >> 2;
+        const uint32_t sh = (uint32_t)(so & 3);
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(seq + (so & ~(int64_t)3));   // (64 bytes of slack)
+        for (int k = gl; k < nw; k += 16) {
+            const uint32_t lo = src[k], hi = src[k + 1];
+            dst[k] = sh ? __builtin_amdgcn_alignbyte(hi, lo, sh) : lo;
+        }
+        for (int k = gl; k < nc; k += 16) gcig[dc + k] = cig[co + k];
+        if (gl == 0) {   // (every lane of the group has read the old offsets: one instruction stream)
+            seq_off[g] = ds;
+            cig_off[g] = dc;
+        }
+    }
+}
+
+size_t cns_gather_temp_bytes(int64_t n) {
+    size_t tb = 0;
+    (void)rocprim::exclusive_scan(nullptr, tb, (int64_t *)nullptr, (int64_t *)nullptr, (int64_t)0, (size_t)(n + 1),
+                                  rocprim::plus<int64_t>());
+    return tb + 256;
+}
+
+// offsets of the gathered pools: nso / nco [n + 1] (entry n: the totals)
+int cns_gather_offsets(const int64_t *aln_total, int64_t n, const int32_t *lseq, const int32_t *ncig, int64_t *sz_seq,
+                       int64_t *sz_cig, int64_t *nso, int64_t *nco, void *temp, size_t temp_bytes, void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    int64_t blocks = (n + 256) / 256;
+    blocks = blocks < 65536 ? blocks : 65536;
+    hipLaunchKernelGGL(cns_gather_sizes_kernel, dim3((unsigned)blocks), dim3(256), 0, s, aln_total, n, lseq, ncig, sz_seq,
+                       sz_cig);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    size_t tb = temp_bytes;
+    if ((e = rocprim::exclusive_scan(temp, tb, sz_seq, nso, (int64_t)0, (size_t)(n + 1), rocprim::plus<int64_t>(), s)) !=
+        hipSuccess)
+        return (int)e;
+    tb = temp_bytes;
+    if ((e = rocprim::exclusive_scan(temp, tb, sz_cig, nco, (int64_t)0, (size_t)(n + 1), rocprim::plus<int64_t>(), s)) !=
+        hipSuccess)
+        return (int)e;
+    return 0;
+}
+
+int cns_gather_copy(const int64_t *aln_total, int64_t n, const uint8_t *seq, const uint32_t *cig, int64_t *seq_off,
+                    const int32_t *lseq, int64_t *cig_off, const int32_t *ncig, const int64_t *nso, const int64_t *nco,
+                    uint8_t *gseq, uint32_t *gcig, void *stream) {
+    int64_t blocks = (n + 15) / 16;   // 16 lanes per alignment
+    blocks = blocks < 65536 ? (blocks > 0 ? blocks : 1) : 65536;
+    hipLaunchKernelGGL(cns_gather_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, aln_total, seq, cig,
+                       seq_off, lseq, cig_off, ncig, nso, nco, gseq, gcig);
     return (int)hipGetLastError();
 }
 

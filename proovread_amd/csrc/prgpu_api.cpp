@@ -178,6 +178,7 @@ enum CnsBufId {
     CB_SORTED, CB_LST_SCORE, CB_LST_ALN, CB_KEPT, CB_BIN_OFF, CB_BIN_BASES, CB_WORK,
     CB_OUT_OFF, CB_CHIM_OFF, CB_STATUS, CB_SEQ_LEN, CB_TRACE_LEN, CB_NCIGAR, CB_NCHIM,
     CB_O_SEQ, CB_O_QUAL, CB_O_TRACE, CB_O_CIG, CB_O_CHIM, CB_PROF, CB_RETRY, CB_K,
+    CB_GSZS, CB_GSZC, CB_GSO, CB_GCO, CB_GTMP,
     CB_COUNT
 };
 
@@ -239,6 +240,7 @@ struct pr_ctx {
     int64_t seed_sr_bases = -1;   // bases of the short reads of the last pr_seed_gpu_map (SB_SEQ)
     bool iter_masked = false;
     bool cns_launched = false;   // a consensus launch filled the CB_O_* outputs
+    bool cns_gathered = false;   // the hand-off's SEQ / CIGAR offsets point into CB_SEQ / CB_CIG
     // exact-parity layout: received alignments (pr_aln_exchange) and an owned batch
     DevBuf xb[XB_COUNT];
     bool x_ready = false;        // XB_RREC / XB_RCIG hold the last exchange's records
@@ -302,6 +304,7 @@ extern "C" void pr_ctx_destroy(pr_ctx *c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     for (auto &b : c->cb) b.release();
+    for (auto &b : c->pb) b.release();
     for (auto &b : c->mb) b.release();
     for (auto &b : c->sd) b.release();
     for (auto &b : c->xb) b.release();
@@ -597,6 +600,36 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         D.seq = sp.sr;
         D.seq_nt4 = 1;
         D.cig = sp.cig;
+    }
+    if (c->pipe && c->cns_gathered) {   // a second launch on the same hand-off: already in place
+        D.seq = B[CB_SEQ].as<uint8_t>();
+        D.cig = B[CB_CIG].as<uint32_t>();
+    } else if (c->pipe && c->n_aln > 0 && !getenv("PRGPU_CNS_NOGATHER")) {
+        // the alignments' SEQ bytes and CIGAR ops in consensus order (pipe_kernels.hip cns_gather):
+        // into the standalone path's SEQ / CIGAR pools, which a pipe batch does not use
+        const int64_t na = c->n_aln;
+        const int64_t *tot = D.aln_off + c->n_lr;
+        const size_t tb = cns_gather_temp_bytes(na);
+        int rc;
+        if ((rc = B[CB_GSZS].ensure((size_t)(na + 1) * 8)) || (rc = B[CB_GSZC].ensure((size_t)(na + 1) * 8)) ||
+            (rc = B[CB_GSO].ensure((size_t)(na + 1) * 8)) || (rc = B[CB_GCO].ensure((size_t)(na + 1) * 8)) ||
+            (rc = B[CB_GTMP].ensure(tb)))
+            return rc;
+        int e = cns_gather_offsets(tot, na, D.lseq, D.ncig, B[CB_GSZS].as<int64_t>(), B[CB_GSZC].as<int64_t>(),
+                                   B[CB_GSO].as<int64_t>(), B[CB_GCO].as<int64_t>(), B[CB_GTMP].p, tb, (void *)c->stream);
+        if (e) return set_error(PR_ERR_HIP, "consensus gather: %s", hipGetErrorString((hipError_t)e));
+        int64_t tot_seq = 0, tot_cig = 0;
+        HIPCHK(hipMemcpyAsync(&tot_seq, B[CB_GSO].as<int64_t>() + na, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(&tot_cig, B[CB_GCO].as<int64_t>() + na, 8, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if ((rc = B[CB_SEQ].ensure((size_t)tot_seq + 16)) || (rc = B[CB_CIG].ensure((size_t)tot_cig * 4 + 16))) return rc;
+        e = cns_gather_copy(tot, na, D.seq, D.cig, B[CB_SEQ_OFF].as<int64_t>(), D.lseq, B[CB_CIG_OFF].as<int64_t>(), D.ncig,
+                            B[CB_GSO].as<int64_t>(),
+                            B[CB_GCO].as<int64_t>(), B[CB_SEQ].as<uint8_t>(), B[CB_CIG].as<uint32_t>(), (void *)c->stream);
+        if (e) return set_error(PR_ERR_HIP, "consensus gather: %s", hipGetErrorString((hipError_t)e));
+        D.seq = B[CB_SEQ].as<uint8_t>();
+        D.cig = B[CB_CIG].as<uint32_t>();
+        c->cns_gathered = true;   // (the offsets now point into the gathered pools)
     }
     HIPCHK(hipMemsetAsync(D.work, 0, 64, c->stream));
     HIPCHK(hipMemsetAsync(B[CB_PROF].as<unsigned long long>(), 0, CNS_NPHASE * 8, c->stream));
@@ -1314,6 +1347,7 @@ extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_param
         int e = pipe_binfilter_launch(P, o->bin_size, o->bin_length, (int)max_bins, grid_f, (void *)c->stream);
         if (e) return set_error(PR_ERR_HIP, "-b/-l filter kernel: %s", hipGetErrorString((hipError_t)e));
     }
+    c->cns_gathered = false;   // the hand-off writes offsets into the SW / short-read pools
     int e = pipe_launch(P, grid, (void *)c->stream, c->pipe_sort_cap * 8);
     if (e) return set_error(PR_ERR_HIP, "pipe kernels: %s", hipGetErrorString((hipError_t)e));
     return pr_cns_launch(c, p);
@@ -1953,6 +1987,12 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_index = ms;
+    if (chunked) {
+        // a chunked build (texts beyond 2^30 positions: configs[2] / configs[3] ranks) gives its
+        // sort buffers back (~4 x 4 GB + rocPRIM's temporaries): at configs[3] a rank's device
+        // memory peaks near the card's 288 GiB later in the task (DESIGN.md current status)
+        for (int id : {(int)SX_KEY0, (int)SX_KEY1, (int)SX_VAL0, (int)SX_VAL1, (int)SX_TEMP}) D[id].release();
+    }
     seedc::IndexView v{};
     v.text = B.text;
     v.n_text = n_text;

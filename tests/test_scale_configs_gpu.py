@@ -75,10 +75,18 @@ def test_one_rank_share_on_one_gpu(cfg, monkeypatch):
     d = synth.simulate_reads(sd, glen, n_lr, 10_000, n_sr, threads=16)
     rec["gen_s"] = round(time.perf_counter() - t, 1)
     rec["long_read_bases"] = int(d.lr_off[-1])
+    # a context of its own, destroyed at the end: the next tests get the device memory back
+    ctx = _abi.Context(int(os.environ.get("LOCAL_RANK", "-1")))
+    try:
+        _run(cfg, ctx, sd, glen, n_lr, cov, n_sr, d, rec, cpu_chain, _abi, cns, correct, seed, synth)
+    finally:
+        ctx.close()
+
+
+def _run(cfg, ctx, sd, glen, n_lr, cov, n_sr, d, rec, cpu_chain, _abi, cns, correct, seed, synth):
     ascii_pool = np.frombuffer(b"ACGTN", np.uint8)[d.lr_seq]
     reads = correct.LongReads([f"lr{i}" for i in range(n_lr)],
                               pools=(ascii_pool, d.lr_off, np.full(len(ascii_pool), ord("$"), np.uint8)))
-    ctx = _abi.default_context()
     _abi.mem_reset_peak()
     st = correct.GpuStages(ctx)
     t = time.perf_counter()
