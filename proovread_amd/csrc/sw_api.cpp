@@ -97,6 +97,11 @@ static int ensure(SwResident &r, int id, size_t bytes) {
     prgpu_mem_note("sw", id, (int64_t)want);
     return 0;
 }
+// The long-read pool starts SB_LR_FRONT bytes into its buffer: the extension kernels read
+// 16-byte reference windows that may begin up to 15 bytes before a read (reverse strand).
+static constexpr size_t SB_LR_FRONT = 64;
+static uint8_t *lr_pool(SwResident &r) { return (uint8_t *)r.buf[SB_LR] + SB_LR_FRONT; }
+
 template <class T>
 static int up(SwResident &r, int id, const T *h, size_t n, hipStream_t s) {
     int rc = ensure(r, id, n * sizeof(T));
@@ -176,13 +181,15 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
     int rc;
     if ((rc = up(r, SB_SR, dev_sr ? nullptr : b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
         (rc = up(r, SB_SR_OFF, b->sr_off, (size_t)b->n_sr + 1, s)) ||
-        (rc = up(r, SB_LR, dev_lr ? nullptr : b->lr_seq, (size_t)b->lr_off[b->n_lr], s)) ||
+        (rc = ensure(r, SB_LR, (size_t)b->lr_off[b->n_lr] + SB_LR_FRONT)) ||
         (rc = up(r, SB_LR_OFF, b->lr_off, (size_t)b->n_lr + 1, s)))
         return rc;
+    if (!dev_lr && b->lr_off[b->n_lr])
+        HIPCHK(hipMemcpyAsync(lr_pool(r), b->lr_seq, (size_t)b->lr_off[b->n_lr], hipMemcpyHostToDevice, s));
     if (dev_sr && b->sr_off[b->n_sr])
         HIPCHK(hipMemcpyAsync(r.buf[SB_SR], dev_sr, (size_t)b->sr_off[b->n_sr], hipMemcpyDeviceToDevice, s));
     if (dev_lr && b->lr_off[b->n_lr])
-        HIPCHK(hipMemcpyAsync(r.buf[SB_LR], dev_lr, (size_t)b->lr_off[b->n_lr], hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(lr_pool(r), dev_lr, (size_t)b->lr_off[b->n_lr], hipMemcpyDeviceToDevice, s));
     if (dev_tasks) {   // unpack the device seed list into the task columns, count the first seeds
         if ((rc = ensure(r, SB_T_SR, (size_t)nt * 4)) || (rc = ensure(r, SB_T_LR, (size_t)nt * 4)) ||
             (rc = ensure(r, SB_T_STRAND, (size_t)nt)) || (rc = ensure(r, SB_T_QBEG, (size_t)nt * 4)) ||
@@ -589,7 +596,7 @@ extern "C" int pr_sw_launch(pr_ctx *c, const pr_sw_opts *o) {
     D.tmax = r.qmax + (r.bwa ? 8 : 4) * o->w + 8;
     D.sr = (const uint8_t *)r.buf[SB_SR];
     D.sr_off = (const int64_t *)r.buf[SB_SR_OFF];
-    D.lr = (const uint8_t *)r.buf[SB_LR];
+    D.lr = lr_pool(r);
     D.lr_off = (const int64_t *)r.buf[SB_LR_OFF];
     D.t_sr = (const int32_t *)r.buf[SB_T_SR];
     D.t_lr = (const int32_t *)r.buf[SB_T_LR];
@@ -1045,7 +1052,7 @@ int sw_get_ptrs(pr_ctx *c, SwPtrs *p) {
     p->task_off = nullptr;
     p->max_per_lr = 0;
     p->sr = (const uint8_t *)r.buf[SB_SR];
-    p->lr = (const uint8_t *)r.buf[SB_LR];
+    p->lr = lr_pool(r);
     p->strand = (const uint8_t *)r.buf[SB_T_STRAND];
     p->pass = (const uint8_t *)r.buf[SB_PASS];
     p->sr_off = (const int64_t *)r.buf[SB_SR_OFF];

@@ -131,6 +131,30 @@ struct PkHalf {
     bool comp;          // reverse strand: complement the reference bases
 };
 
+// The reference bases of rows r .. r + 15 of a task (step ts), byte k = row r + k (not yet complemented):
+// one unaligned 16-byte load per 16 rows instead of a byte load per row.  (Per-row byte loads
+// kept one 128-B line per task live for the whole extension: 128 tasks x 8 waves per CU filled
+// each XCD's L2, so nearly every row missed it.)  The window may run up to 15 bytes past either
+// end of the read: the pools keep 64 bytes of slack on both sides, and the bytes of rows >= tlen
+// are never used.
+SW_RING_FN void pk_tref16(const uint8_t *T, int ts, int r, uint32_t w[4]) {
+    uint32_t x[4];
+    __builtin_memcpy(x, ts > 0 ? T + r : T - r - 15, 16);
+    if (ts > 0) {
+        w[0] = x[0], w[1] = x[1], w[2] = x[2], w[3] = x[3];
+    } else {
+        w[0] = __builtin_bswap32(x[3]), w[1] = __builtin_bswap32(x[2]);
+        w[2] = __builtin_bswap32(x[1]), w[3] = __builtin_bswap32(x[0]);
+    }
+}
+// the window one row on
+SW_RING_FN void pk_shr8(uint32_t w[4]) {
+    w[0] = (w[0] >> 8) | (w[1] << 24);
+    w[1] = (w[1] >> 8) | (w[2] << 24);
+    w[2] = (w[2] >> 8) | (w[3] << 24);
+    w[3] >>= 8;
+}
+
 // Query bit masks of one task: m[(bit * PK_NQW + k) * MS], bit 0 / 1 of the base code
 // at bit 64 + j of the 416-bit string; returns true if the query holds an N.
 // (The byte loads of a word are unrolled so that they are all in flight together.)
@@ -234,13 +258,20 @@ SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int n
         RH[s] = pk_dup(h);
         RE[s] = pk_dup(e);
     }
-    int tA = A.tlen > 0 ? (int)A.T[0] : 0, tB = B.tlen > 0 ? (int)B.T[0] : 0;
+    uint32_t twA[4] = {0u, 0u, 0u, 0u}, twB[4] = {0u, 0u, 0u, 0u};   // reference windows: byte 0 = row i
+    if (A.tlen > 0) pk_tref16(A.T, 1, 0, twA);
+    if (B.tlen > 0) pk_tref16(B.T, 1, 0, twB);
     int hlA = 0, hlB = 0;
     for (int i = 0; i < nrows; ++i) {
-        // reference bases of row i (prefetched one row ahead)
-        int ca = tA, cb = tB;
-        if (i + 1 < A.tlen) tA = (int)A.T[i + 1];
-        if (i + 1 < B.tlen) tB = (int)B.T[i + 1];
+        // reference bases of row i
+        int ca = (int)(twA[0] & 0xFFu), cb = (int)(twB[0] & 0xFFu);
+        if ((i & 15) == 15) {   // (wave-uniform)
+            if (i + 1 < A.tlen) pk_tref16(A.T, 1, i + 1, twA);
+            if (i + 1 < B.tlen) pk_tref16(B.T, 1, i + 1, twB);
+        } else {
+            pk_shr8(twA);
+            pk_shr8(twB);
+        }
         if (A.comp && ca < 4) ca = 3 - ca;
         if (B.comp && cb < 4) cb = 3 - cb;
         if (i < A.tlen && ca > 3) nflag |= 1;
@@ -348,6 +379,7 @@ struct PkExtOut {
     int score, qle, tle, gtle, gscore, max_off;
 };
 
+
 // SMALLH (every H <= 511: a x read length <= 511): the row maximum and its last slot as one
 // packed unsigned max of h * 128 + s instead of one h * 16 + (s & 15) per 16-slot group (one
 // accumulator, no per-row reduction over the groups)
@@ -390,20 +422,25 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
     int end[2] = {qlen, qlen}, mx[2], max_i[2] = {-1, -1}, max_j[2] = {-1, -1}, max_ie[2] = {-1, -1};
     int gscore[2] = {-1, -1}, max_off[2] = {0, 0};
     bool live[2];
-    int tc[2];
+    uint32_t tw[2][4];   // reference window: byte 0 = row i
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         mx[h] = Hh[h]->h0;
         live[h] = Hh[h]->tlen > 0;
-        tc[h] = live[h] ? (int)Hh[h]->T[0] : 0;
+        tw[h][0] = tw[h][1] = tw[h][2] = tw[h][3] = 0u;
+        if (live[h]) pk_tref16(Hh[h]->T, Hh[h]->ts, 0, tw[h]);
     }
     for (int i = 0; i < nrows; ++i) {
         int cb[2];
         uint32_t sev = 0u, bnd = 0u;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-            int c = tc[h];
-            if (i + 1 < Hh[h]->tlen) tc[h] = (int)Hh[h]->T[(long)Hh[h]->ts * (i + 1)];
+            int c = (int)(tw[h][0] & 0xFFu);
+            if ((i & 15) == 15) {   // (wave-uniform)
+                if (i + 1 < Hh[h]->tlen) pk_tref16(Hh[h]->T, Hh[h]->ts, i + 1, tw[h]);
+            } else {
+                pk_shr8(tw[h]);
+            }
             if (Hh[h]->comp && c < 4) c = 3 - c;
             if (live[h] && i >= Hh[h]->tlen) live[h] = false;
             if (live[h] && c > 3) {

@@ -67,7 +67,11 @@ extern "C" int pk_global(int a, int b, int o_del, int e_del, int o_ins, int e_in
     int qn = 0;
     if (pk_build_mask(qa, 0, 1, tla >= 0 ? qlen : 0, m[0], 1)) qn |= 1;
     if (pk_build_mask(qb, 0, 1, tlb >= 0 ? qlen : 0, m[1], 1)) qn |= 2;
-    PkHalf A{ta, tla > 0 ? tla : 0, false}, B{tb, tlb > 0 ? tlb : 0, false};
+    // the kernel reads 16-byte reference windows past the window's end: padded copies
+    std::vector<uint8_t> pa((tla > 0 ? tla : 0) + 64, 4), pb((tlb > 0 ? tlb : 0) + 64, 4);
+    if (tla > 0) std::copy(ta, ta + tla, pa.begin());
+    if (tlb > 0) std::copy(tb, tb + tlb, pb.begin());
+    PkHalf A{pa.data(), tla > 0 ? tla : 0, false}, B{pb.data(), tlb > 0 ? tlb : 0, false};
     int nrow = A.tlen > B.tlen ? A.tlen : B.tlen;
     if (nrow < nrow_min) nrow = nrow_min;   // other lanes of the wave may run longer
     const int npair = pk_npair(w);
@@ -119,7 +123,11 @@ static int pk_extend_t(int a, int b, int o_del, int e_del, int o_ins, int e_ins,
     int nflag = 0;
     if (pk_build_mask(qa, 0, 1, qlen, m[0], 1)) nflag |= 4;
     if (pk_build_mask(qb, 0, 1, qlen, m[1], 1)) nflag |= 8;
-    PkExtHalf A{ta, 1, false, tla, h0a}, B{tb, 1, false, tlb, h0b};
+    // the kernel reads 16-byte reference windows past the read's end: padded copies
+    std::vector<uint8_t> pa(tla + 64, 4), pb(tlb + 64, 4);
+    std::copy(ta, ta + tla, pa.begin());
+    std::copy(tb, tb + tlb, pb.begin());
+    PkExtHalf A{pa.data(), 1, false, tla, h0a}, B{pb.data(), 1, false, tlb, h0b};
     int nrow = tla > tlb ? tla : tlb;
     if (nrow < nrow_min) nrow = nrow_min;
     PkExtOut o[2];
