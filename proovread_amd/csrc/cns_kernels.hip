@@ -34,7 +34,15 @@ __device__ __forceinline__ double phred2freq(int p) {
     double x = __dadd_rn(__dmul_rn(__ddiv_rn(__dmul_rn((double)p, (double)p), 120.0), 100.0), 0.5);
     return __ddiv_rn((double)(long long)x, 100.0);
 }
+// int(sqrt(120 f) + 0.5) capped at 40: 40 for every f >= 14 (sqrt(1680) + 0.5 > 41); integer
+// counts below 14 from a table (their square roots are nowhere near a rounding boundary)
 __device__ __forceinline__ int freq2phred(double f) {
+    if (f >= 14.0) return 40;
+    const int m = (int)f;
+    if ((double)m == f && m >= 0) {   // 0 11 15 19 22 24 27 29 | 31 33 35 36 38 39
+        const unsigned long long t = m < 8 ? 0x1D1B1816130F0B00ULL : 0x000027262423211FULL;
+        return (int)((t >> (8 * (m & 7))) & 0xFFu);
+    }
     double x = __dadd_rn(__dsqrt_rn(__dmul_rn(f, 120.0)), 0.5);
     long long p = (long long)x;
     return p > 40 ? 40 : (int)p;
@@ -438,7 +446,10 @@ struct CnsGeo {
 // wave work is latency-bound, occupancy hides it); GeoS (more insertion states, 2 per CU)
 // stays selectable with PRGPU_CNS_GEO=S; GeoL (1 per CU) reruns the reads that overflow
 using GeoS = CnsGeo<512, 1024, 1024, 2, true>;
-using GeoM = CnsGeo<256, 1024, 512, 4, true>;
+#ifndef CNS_M_WGCU
+#define CNS_M_WGCU 4
+#endif
+using GeoM = CnsGeo<256, 1024, 512, CNS_M_WGCU, true>;
 using GeoL = CnsGeo<2048, 1024, 8192, 1, false>;
 
 // per-column descriptor: flag bits above the 12-bit state-table slot
@@ -616,6 +627,27 @@ __device__ __forceinline__ int group_incl_scan(int v) {
     return v;
 }
 
+// Lane exchanges inside a 16-lane group as DPP row operations (VALU, no LDS round trip):
+// lane l of the row gets lane l + D's value (D = 1, 2; the row's last lanes get 0), or lane F's.
+template <int D>
+__device__ __forceinline__ uint32_t row_down(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x100 + D, 0xf, 0xf, true);   // row_shl:D
+}
+template <int F>
+__device__ __forceinline__ int row_bcast(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, 0x150 + F, 0xf, 0xf, false);   // row_newbcast:F
+}
+
+// the number of the row's lanes whose v <= x (x per lane), from 16 row broadcasts
+template <int F = 0>
+__device__ __forceinline__ int row_count_le(int v, int x) {
+    if constexpr (F == 16) {
+        return 0;
+    } else {
+        return (row_bcast<F>(v) <= x ? 1 : 0) + row_count_le<F + 1>(v, x);
+    }
+}
+
 // a wave's LDS writes visible to its own later LDS reads (lanes exchange through LDS)
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -648,7 +680,7 @@ __device__ __forceinline__ int32_t kfld(int32_t kv, int g) {
 // the first one's op by a binary search over the chunk's op starts (ops: the half's LDS
 // table, 32 int4) and walks on from there.  The two halves of a wave run their own
 // alignments (their loops may differ in length: every cross-lane step stays in the half).
-template <class FS, class FC>
+template <bool COLS = true, class FS, class FC>
 __device__ __forceinline__ void group_states(const uint32_t *cg, int nop, int rp, int q0, int cmin, int cmax, int4 *ops,
                                              const uint32_t (&c_first)[CNS_OPF], FS &&special, FC &&column) {
     constexpr int GW = CNS_GW;
@@ -661,27 +693,58 @@ __device__ __forceinline__ void group_states(const uint32_t *cg, int nop, int rp
         uint32_t c = valid && k0 >= CNS_OPF * GW ? cg[k] : 0u;
 #pragma unroll
         for (int u = 0; u < CNS_OPF; ++u) c = k0 == u * GW ? c_first[u] : c;
+        // this lane's op of the next chunk (its first two are the last lanes' look-ahead below:
+        // from the caller's registers, not a dependent HBM load on every chunk)
+        uint32_t cn = 0u;
+        if (k0 + GW >= CNS_OPF * GW) {
+            if (gl < 2 && k + GW < nop) cn = cg[k + GW];
+        } else {
+#pragma unroll
+            for (int u = 0; u + 1 < CNS_OPF; ++u) cn = k0 == u * GW ? c_first[u + 1] : cn;
+        }
+        uint32_t n0, n1;
+        if constexpr (GW == 16) {
+            n0 = (uint32_t)row_bcast<0>((int)cn);
+            n1 = (uint32_t)row_bcast<1>((int)cn);
+        } else {
+            n0 = __shfl(cn, 0, GW);
+            n1 = __shfl(cn, 1, GW);
+        }
         const int n = (int)(c >> 4), code = (int)(c & 15u);
         const bool lead = k == 0 && code == 1;
         const int ncol = !valid ? 0 : (code == 0 || code == 2) ? n : (lead ? 1 : 0);
         const int qadv = valid && (code == 0 || code == 1) ? n : 0;
-        const uint32_t nx1 = __shfl_down(c, 1, GW), nx2 = __shfl_down(c, 2, GW);
+        uint32_t nx1, nx2;
+        if constexpr (GW == 16) {
+            nx1 = row_down<1>(c);
+            nx2 = row_down<2>(c);
+        } else {
+            nx1 = __shfl_down(c, 1, GW);
+            nx2 = __shfl_down(c, 2, GW);
+        }
         const int sc = group_incl_scan<GW>(ncol), sq = group_incl_scan<GW>(qadv);
         // inserted bases right after an op that owns columns (zero-length ops skipped)
         int tot = 0;
         if (ncol > 0 && k + 1 < nop) {
-            const uint32_t x1 = gl <= GW - 2 ? nx1 : cg[k + 1];
+            const uint32_t x1 = gl <= GW - 2 ? nx1 : n0;
             if ((x1 & 15u) == 1u || (x1 >> 4) == 0u) {
                 tot = (x1 & 15u) == 1u ? (int)(x1 >> 4) : 0;
                 for (int j = k + 2; j < nop; ++j) {
-                    const uint32_t x2 = (j == k + 2 && gl <= GW - 3) ? nx2 : cg[j];
+                    const uint32_t x2 = j != k + 2 ? cg[j] : gl <= GW - 3 ? nx2 : gl == GW - 2 ? n0 : n1;
                     if ((x2 & 15u) == 1u) tot += (int)(x2 >> 4);
                     else if ((x2 >> 4) != 0u) break;
                 }
             }
         }
         const int cs = col0 + sc - ncol, qs = qb + sq - qadv;
-        const int ctot = __shfl(sc, glast, 64), qtot = __shfl(sq, glast, 64);
+        int ctot, qtot;
+        if constexpr (GW == 16) {
+            ctot = row_bcast<15>(sc);
+            qtot = row_bcast<15>(sq);
+        } else {
+            ctot = __shfl(sc, glast, 64);
+            qtot = __shfl(sq, glast, 64);
+        }
         int scol = -1;
         if (ncol > 0 && (tot > 0 || lead)) {
             int sqp, slen;
@@ -690,19 +753,35 @@ __device__ __forceinline__ void group_states(const uint32_t *cg, int nop, int rp
             else { scol = cs + n - 1; sqp = qs; slen = tot; }   // D + I: the insertion replaces '-'
             if (scol >= cmin && scol < cmax) special(scol, sqp, slen);
         }
+        if (!COLS) {   // the deferred (insertion) states only
+            col0 += ctot;
+            qb += qtot;
+            continue;
+        }
         ops[gl] = make_int4(valid ? cs : 0x7fffffff, qs, code == 2 ? 1 : 0, scol);
         wave_sync();
         const int cA = col0 > cmin ? col0 : cmin, cB = col0 + ctot < cmax ? col0 + ctot : cmax;
         const int nv = nop - k0 < GW ? nop - k0 : GW;
+        const int per = cB > cA ? (cB - cA + GW - 1) / GW : 0;
+        int cc = cA + gl * per;
+        int lo_dpp = 0;
+        if constexpr (GW == 16) {   // (every lane of the group active: DPP reads the row)
+            lo_dpp = row_count_le(valid ? cs : 0x7fffffff, cc) - 1;
+            lo_dpp = lo_dpp < 0 ? 0 : lo_dpp;
+        }
         if (cB > cA) {
-            const int per = (cB - cA + GW - 1) / GW;
-            int cc = cA + gl * per;
             const int ce_ = cc + per < cB ? cc + per : cB;
             if (cc < ce_) {
-                int lo = 0, hi = nv - 1;   // the last op starting at or before cc owns it
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (ops[mid].x <= cc) lo = mid; else hi = mid - 1;
+                int lo;   // the last op starting at or before cc owns it
+                if constexpr (GW == 16) {
+                    lo = lo_dpp;
+                } else {
+                    lo = 0;
+                    int hi = nv - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (ops[mid].x <= cc) lo = mid; else hi = mid - 1;
+                    }
                 }
                 int4 o = ops[lo];
                 int nxs = lo + 1 < nv ? ops[lo + 1].x : 0x7fffffff;
@@ -720,6 +799,119 @@ __device__ __forceinline__ void group_states(const uint32_t *cg, int nop, int rp
         wave_sync();
         col0 += ctot;
         qb += qtot;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// One kept alignment as a 16-lane group sees it (its SEQ bytes in the group's LDS area when
+// they fit: `fast`)
+struct KeptView {
+    int rp, i, sb, nop, ls;
+    bool rc, fast;
+    const uint8_t *sl;   // SEQ base 0 (fast: the group's LDS copy)
+    SeqV sv;
+    int64_t cgi;         // its first CIGAR op kept
+};
+
+// Every kept alignment of K[kb, ke) that overlaps the columns [cw0, cw1) -> body(view, ops,
+// op table, first ops), by CNS_NG groups of CNS_GW lanes per wave: stream wv * CNS_NG + g takes
+// the entries kb + stream + NSTREAM j, software-pipelined (the next entry's first CIGAR ops
+// and SEQ dwords, and the K entry of the one after it, are in flight while the current one is
+// processed).  A K entry (12 ints) is held spread over lanes 0..11 of its group in one register.
+#ifndef CNS_PD_M
+#define CNS_PD_M 1
+#endif
+#ifndef CNS_PD_S
+#define CNS_PD_S 1
+#endif
+template <int PD, class Body>
+__device__ __forceinline__ void stream_kept(const CnsDev &D, const int4 *K, int kb, int ke, int cw0, int cw1,
+                                            int4 *wops, uint32_t *wseq, bool snt4, Body &&body) {
+    constexpr int NWAVE = CNS_THREADS / 64;
+    constexpr int NSTREAM = CNS_NG * NWAVE;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int g = lane / CNS_GW, gl = lane % CNS_GW;
+    const int stream = wv * CNS_NG + g;
+    int4 *gops = wops + g * CNS_GW;
+    uint32_t *gseq = wseq + g * CNS_SEQ_DW;
+    const int32_t *Ki = reinterpret_cast<const int32_t *>(K);
+    const uint32_t *gdw = reinterpret_cast<const uint32_t *>(D.seq);
+    auto ldK = [&](int kk) -> int32_t {
+        return kk < ke ? (gl < 12 ? Ki[12 * (int64_t)kk + gl] : 0) : (gl == 0 ? 0x7fffffff : 0);
+    };
+    auto overl = [&](int32_t kv) { return kfld<0>(kv, g) < cw1 && kfld<1>(kv, g) > cw0; };
+    auto ldD = [&](int32_t kv, uint32_t (&op)[CNS_OPF], uint32_t (&dw)[CNS_SEQ_PL]) {
+#pragma unroll
+        for (int u = 0; u < CNS_OPF; ++u) op[u] = 0u;
+#pragma unroll
+        for (int u = 0; u < CNS_SEQ_PL; ++u) dw[u] = 0u;
+        if (!overl(kv)) return;
+        const int64_t so = (int64_t)(uint32_t)kfld<6>(kv, g) | ((int64_t)kfld<7>(kv, g) << 32);
+        const int64_t cgi = (int64_t)(uint32_t)kfld<8>(kv, g) | ((int64_t)kfld<9>(kv, g) << 32);
+        const int nop = kfld<4>(kv, g);
+#pragma unroll
+        for (int u = 0; u < CNS_OPF; ++u)
+            if (u * CNS_GW + gl < nop) op[u] = D.cig[cgi + u * CNS_GW + gl];
+        const int ndw = ((int)(so & 3) + (kfld<2>(kv, g) & 0x7FFFFFFF) + 3) >> 2;
+        if (ndw <= CNS_SEQ_DW) {
+#pragma unroll
+            for (int u = 0; u < CNS_SEQ_PL; ++u)
+                if (u * CNS_GW + gl < ndw) dw[u] = gdw[(so >> 2) + u * CNS_GW + gl];
+        }
+    };
+    // the K entries of this stream's candidates j .. j + PD and the data of j .. j + PD - 1
+    int32_t kv[PD + 1];
+    uint32_t op[PD][CNS_OPF], dw[PD][CNS_SEQ_PL];
+#pragma unroll
+    for (int d = 0; d <= PD; ++d) kv[d] = ldK(kb + stream + d * NSTREAM);
+#pragma unroll
+    for (int d = 0; d < PD; ++d) ldD(kv[d], op[d], dw[d]);
+    for (int kk = kb + stream; kk < ke; kk += NSTREAM) {
+        uint32_t opn[CNS_OPF], dwn[CNS_SEQ_PL];
+        ldD(kv[PD], opn, dwn);
+        const int32_t kn = ldK(kk + (PD + 1) * NSTREAM);
+        const int32_t ckv = kv[0];
+        if (overl(ckv)) {
+            KeptView v;
+            v.rp = kfld<0>(ckv, g);
+            const int e0z = kfld<2>(ckv, g);
+            v.sb = kfld<3>(ckv, g);
+            v.nop = kfld<4>(ckv, g);
+            v.i = kfld<5>(ckv, g);
+            v.ls = e0z & 0x7FFFFFFF;
+            v.rc = e0z < 0;
+            const int64_t so = (int64_t)(uint32_t)kfld<6>(ckv, g) | ((int64_t)kfld<7>(ckv, g) << 32);
+            v.cgi = (int64_t)(uint32_t)kfld<8>(ckv, g) | ((int64_t)kfld<9>(ckv, g) << 32);
+            const int head = (int)(so & 3);
+            const int ndw = (head + v.ls + 3) >> 2;
+            v.fast = ndw <= CNS_SEQ_DW;
+            if (v.fast) {
+#pragma unroll
+                for (int u = 0; u < CNS_SEQ_PL; ++u)
+                    if (u * CNS_GW + gl < CNS_SEQ_DW) gseq[u * CNS_GW + gl] = dw[0][u];
+            }
+            v.sl = reinterpret_cast<const uint8_t *>(gseq) + head;
+            v.sv.p = v.fast ? v.sl : D.seq + so;   // (the insertion states' keys; the slow path's bases)
+            v.sv.n = v.ls;
+            v.sv.rc = v.rc;
+            v.sv.nt4 = snt4;
+            wave_sync();
+            body(v, gops, op[0]);
+        }
+#pragma unroll
+        for (int d = 0; d < PD; ++d) kv[d] = kv[d + 1];
+        kv[PD] = kn;
+#pragma unroll
+        for (int d = 0; d + 1 < PD; ++d) {
+#pragma unroll
+            for (int u = 0; u < CNS_OPF; ++u) op[d][u] = op[d + 1][u];
+#pragma unroll
+            for (int u = 0; u < CNS_SEQ_PL; ++u) dw[d][u] = dw[d + 1][u];
+        }
+#pragma unroll
+        for (int u = 0; u < CNS_OPF; ++u) op[PD - 1][u] = opn[u];
+#pragma unroll
+        for (int u = 0; u < CNS_SEQ_PL; ++u) dw[PD - 1][u] = dwn[u];
     }
 }
 
@@ -914,8 +1106,7 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         int32_t *wcur = reinterpret_cast<int32_t *>(B + G::B_CNT);   // per-window counters (<= 3W)
         int32_t *Kh = D.k_pool + (int64_t)blockIdx.x * D.k_cap;      // [0, nwin] window starts, then entries
         int4 *K = reinterpret_cast<int4 *>(Kh + ((nwin + 4) & ~3));
-        const int lane = tid & 63, wv = tid >> 6;
-        constexpr int NWAVE = CNS_THREADS / 64;
+        const int wv = tid >> 6;
         int4 *wops = reinterpret_cast<int4 *>(B + G::B_WAVE + wv * G::WAVE_BYTES);   // this wave's op table
         uint32_t *wseq = reinterpret_cast<uint32_t *>(B + G::B_WAVE + wv * G::WAVE_BYTES + 64 * 16);   // its SEQ dwords
         const bool snt4 = D.seq_nt4 != 0;
@@ -923,7 +1114,7 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         for (int x = tid; x <= nwin && x < 3 * G::W; x += CNS_THREADS) wcur[x] = 0;
         __syncthreads();
         if (nwin + 1 > 3 * G::W) C->flag = 1;
-        for (int i = tid; i < na; i += CNS_THREADS) {   // a thread per kept alignment
+        for (int i = tid; i < na; i += CNS_THREADS) {   // a thread per kept alignment: the window counts
             const int64_t g = a0 + i;
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
             const int rp = D.a_rpos[g], span = D.a_end[g] - rp;
@@ -931,20 +1122,6 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             atomicMax(&C->maxspan, span);
             const int win = rp / G::W;
             if (win < 3 * G::W) atomicAdd(&wcur[win], 1);
-            const SeqV sv = seq_view(D, g);
-            const int sb = D.a_sb[g];
-            const uint32_t *cg = D.cig + D.cig_off[g];
-            walk_states<true>(cg, D.a_cb[g], D.a_ce[g], rp, 0, 0x7fffffff,
-                              [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                  const uint64_t k = state_key(sv, sb + qoff, qlen);
-                                  if (qlen > 0xFFFF || sb + qoff > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
-                                  const int h = T.insert(k, ((uint64_t)qlen << 48) | ((uint64_t)(sb + qoff) << 32) |
-                                                                (uint64_t)g);
-                                  if (h < 0) { C->flag = 1; return; }
-                                  const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)sidx;
-                                  atomicMin(&T.ord_all[h], ord);
-                                  if (!(nig && in_ign(ig, nig, col))) atomicMin(&T.ord_cns[h], ord);
-                              });
         }
         __syncthreads();
         // 16-bit fixed-state counters: at most 65535 kept alignments per read
@@ -980,6 +1157,29 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         }
         __threadfence_block();
         __syncthreads();
+        // the multi-character states of every kept alignment (walk_states' semantics through
+        // group_states' deferred states: a 16-lane group per alignment, its SEQ in LDS; the
+        // state index of a column is column - rp)
+        stream_kept<G::WGCU >= 4 ? CNS_PD_M : CNS_PD_S>(D, K, 0, C->nk, -1, 0x7fffffff, wops, wseq, snt4, [&](const KeptView &v, int4 *gops, const uint32_t (&cop)[CNS_OPF]) {
+            const int64_t g = a0 + v.i;
+            group_states<false>(D.cig + v.cgi, v.nop, v.rp, v.sb, 0, 0x7fffffff, gops, cop,
+                                [&](int scol, int sqp, int slen) {
+                                    if (slen <= 1) return;
+                                    if (slen > 0xFFFF || sqp > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
+                                    const uint64_t k = state_key(v.sv, sqp, slen);
+                                    const int h = T.insert(k, ((uint64_t)slen << 48) | ((uint64_t)sqp << 32) | (uint64_t)g);
+                                    if (h < 0) { C->flag = 1; return; }
+                                    const unsigned int ord = ((unsigned int)v.i << 12) | (unsigned int)(scol - v.rp);
+                                    atomicMin(&T.ord_all[h], ord);
+                                    if (!(nig && in_ign(ig, nig, scol))) atomicMin(&T.ord_cns[h], ord);
+                                },
+                                [&](int, int) {});
+        });
+        __syncthreads();
+        if (C->flag) {
+            CNS_CAP_FAIL();
+            continue;
+        }
         const int wback = (C->maxspan + G::W - 1) / G::W;   // windows an alignment can reach back
         CNS_TICK(2);
 
@@ -997,7 +1197,6 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         uint32_t *ignb = reinterpret_cast<uint32_t *>(B + G::B_IGN);
         const bool use_rq = P.use_ref_qual && D.ref_seq && D.ref_qual;
         constexpr int CPT = G::W / CNS_THREADS;   // argmax columns per thread
-        const uint32_t *gdw = reinterpret_cast<const uint32_t *>(D.seq);
         for (int wi = 0; wi < nwin; ++wi) {
             const long w0 = (long)wi * G::W;
             const int wn = (L - w0) < G::W ? (int)(L - w0) : G::W;
@@ -1016,105 +1215,59 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             CNS_TICK(8);
             if (D.prof && tid == 0) pt[14] += 1;
             const int cw0 = (int)w0, cw1 = (int)w0 + wn;
-            // CNS_NG candidate streams per wave, one per CNS_GW-lane group (stream wv * CNS_NG + g
-            // takes the candidates kb + stream + NSTREAM j), software-pipelined: the next
-            // candidate's first CIGAR ops and SEQ dwords, and the K entry of the one after it, are
-            // in flight while the current one is processed.  A K entry (12 ints) is held spread
-            // over lanes 0..11 of its group in one register.
-            const int g = lane / CNS_GW, gl = lane % CNS_GW;
-            const int stream = wv * CNS_NG + g;
-            constexpr int NSTREAM = CNS_NG * NWAVE;
-            int4 *gops = wops + g * CNS_GW;
-            uint32_t *gseq = wseq + g * CNS_SEQ_DW;
-            const int32_t *Ki = reinterpret_cast<const int32_t *>(K);
-            auto ldK = [&](int kk) -> int32_t {
-                return kk < ke ? (gl < 12 ? Ki[12 * (int64_t)kk + gl] : 0) : (gl == 0 ? 0x7fffffff : 0);
-            };
-            auto overl = [&](int32_t kv) { return kfld<0>(kv, g) < cw1 && kfld<1>(kv, g) > cw0; };   // overlaps the window
-            auto ldD = [&](int32_t kv, uint32_t (&op)[CNS_OPF], uint32_t (&dw)[CNS_SEQ_PL]) {
-#pragma unroll
-                for (int u = 0; u < CNS_OPF; ++u) op[u] = 0u;
-#pragma unroll
-                for (int u = 0; u < CNS_SEQ_PL; ++u) dw[u] = 0u;
-                if (!overl(kv)) return;
-                const int64_t so = (int64_t)(uint32_t)kfld<6>(kv, g) | ((int64_t)kfld<7>(kv, g) << 32);
-                const int64_t cgi = (int64_t)(uint32_t)kfld<8>(kv, g) | ((int64_t)kfld<9>(kv, g) << 32);
-                const int nop = kfld<4>(kv, g);
-#pragma unroll
-                for (int u = 0; u < CNS_OPF; ++u)
-                    if (u * CNS_GW + gl < nop) op[u] = D.cig[cgi + u * CNS_GW + gl];
-                const int ndw = ((int)(so & 3) + (kfld<2>(kv, g) & 0x7FFFFFFF) + 3) >> 2;
-                if (ndw <= CNS_SEQ_DW) {
-#pragma unroll
-                    for (int u = 0; u < CNS_SEQ_PL; ++u)
-                        if (u * CNS_GW + gl < ndw) dw[u] = gdw[(so >> 2) + u * CNS_GW + gl];
-                }
-            };
-            int32_t ckv = ldK(kb + stream), nkv;
-            uint32_t cop[CNS_OPF], cdw[CNS_SEQ_PL];
-            ldD(ckv, cop, cdw);
-            nkv = ldK(kb + stream + NSTREAM);
-            for (int kk = kb + stream; kk < ke; kk += NSTREAM) {
-                uint32_t nop_[CNS_OPF], ndw_[CNS_SEQ_PL];
-                ldD(nkv, nop_, ndw_);
-                const int32_t mkv = ldK(kk + 2 * NSTREAM);
-                if (overl(ckv)) {
-                    const int rp = kfld<0>(ckv, g), e0z = kfld<2>(ckv, g), sb = kfld<3>(ckv, g), nop = kfld<4>(ckv, g);
-                    const int ls = e0z & 0x7FFFFFFF;
-                    const bool rc = e0z < 0;
-                    const int64_t so = (int64_t)(uint32_t)kfld<6>(ckv, g) | ((int64_t)kfld<7>(ckv, g) << 32);
-                    const int64_t cgi = (int64_t)(uint32_t)kfld<8>(ckv, g) | ((int64_t)kfld<9>(ckv, g) << 32);
-                    const int head = (int)(so & 3);
-                    const int ndw = (head + ls + 3) >> 2;
-                    // the alignment's SEQ in the group's LDS area (loaded ahead), when it fits
-                    const bool fast = ndw <= CNS_SEQ_DW;
-                    if (fast) {
-#pragma unroll
-                        for (int u = 0; u < CNS_SEQ_PL; ++u)
-                            if (u * CNS_GW + gl < CNS_SEQ_DW) gseq[u * CNS_GW + gl] = cdw[u];
+            stream_kept<G::WGCU >= 4 ? CNS_PD_M : CNS_PD_S>(D, K, kb, ke, cw0, cw1, wops, wseq, snt4, [&](const KeptView &v, int4 *gops, const uint32_t (&cop)[CNS_OPF]) {
+                const uint32_t lut = v.rc ? 0x50321u : 0x51230u;   // nt4 code -> fixed-state index
+                auto fixed_at = [&](int s) -> int {
+                    if (v.fast && snt4) {
+                        uint32_t c8 = v.sl[v.rc ? v.ls - 1 - s : s];
+                        c8 = c8 > 4u ? 4u : c8;
+                        return (int)((lut >> (4u * c8)) & 15u);
                     }
-                    const uint8_t *sl = reinterpret_cast<const uint8_t *>(gseq) + head;
-                    SeqV sv;   // (the insertion states' keys; the slow path's bases)
-                    sv.p = fast ? sl : D.seq + so;
-                    sv.n = ls;
-                    sv.rc = rc;
-                    sv.nt4 = snt4;
-                    const uint32_t lut = rc ? 0x50321u : 0x51230u;   // nt4 code -> fixed-state index
-                    auto fixed_at = [&](int s) -> int {
-                        if (fast && snt4) {
-                            uint32_t c8 = sl[rc ? ls - 1 - s : s];
-                            c8 = c8 > 4u ? 4u : c8;
-                            return (int)((lut >> (4u * c8)) & 15u);
-                        }
-                        return fixed_idx_at(sv, s);
-                    };
-                    auto add_fixed = [&](int cc, int fi) {
-                        const int c = cc - cw0;
-                        if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
-                        atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
-                    };
-                    wave_sync();
-                    group_states(D.cig + cgi, nop, rp, sb, cw0, cw1, gops, cop,
-                                 [&](int scol, int sqp, int slen) {
-                                     if (slen == 1) { add_fixed(scol, fixed_at(sqp)); return; }
-                                     const int c = scol - cw0;
-                                     if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
-                                     const int h = T.find(state_key(sv, sqp, slen));
-                                     if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
-                                         C->flag = 1;
-                                 },
-                                 [&](int cc, int qp) { add_fixed(cc, qp < 0 ? 4 : fixed_at(qp)); });
-                }
-                ckv = nkv;
-                nkv = mkv;
-#pragma unroll
-                for (int u = 0; u < CNS_OPF; ++u) cop[u] = nop_[u];
-#pragma unroll
-                for (int u = 0; u < CNS_SEQ_PL; ++u) cdw[u] = ndw_[u];
-            }
+                    return fixed_idx_at(v.sv, s);
+                };
+                auto add_fixed = [&](int cc, int fi) {
+                    const int c = cc - cw0;
+                    if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
+                    atomicAdd(&cnt[3 * c + (fi >> 1)], 1u << (16 * (fi & 1)));
+                };
+                group_states(D.cig + v.cgi, v.nop, v.rp, v.sb, cw0, cw1, gops, cop,
+                             [&](int scol, int sqp, int slen) {
+                                 if (slen == 1) { add_fixed(scol, fixed_at(sqp)); return; }
+                                 const int c = scol - cw0;
+                                 if (nig && ((ignb[c >> 5] >> (c & 31)) & 1u)) return;
+                                 const int h = T.find(state_key(v.sv, sqp, slen));
+                                 if (h < 0 || wtab_add<G::WCAP>(wkey, wcnt, ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)h) < 0)
+                                     C->flag = 1;
+                             },
+                             [&](int cc, int qp) { add_fixed(cc, qp < 0 ? 4 : fixed_at(qp)); });
+            });
             __syncthreads();
             CNS_TICK(3);
             if (C->flag) break;
+            // this thread's argmax columns' reference bases and qualities, loaded now (one
+            // dword each for 4 columns) and used after the best-insertion pass and its barrier
+            uint32_t rq4 = 0u, rb4 = 0u;
+            {
+                const int cth = tid * CPT;
+                const int64_t at = r0 + w0 + cth;
+                if (CPT == 4 && cth + 3 < wn) {
+                    if (use_rq) __builtin_memcpy(&rq4, D.ref_qual + at, 4);
+                    if (D.ref_seq) __builtin_memcpy(&rb4, D.ref_seq + at, 4);
+                } else {
+                    for (int k = 0; k < CPT && k < 4 && cth + k < wn; ++k) {
+                        if (use_rq) rq4 |= (uint32_t)D.ref_qual[at + k] << (8 * k);
+                        if (D.ref_seq) rb4 |= (uint32_t)D.ref_seq[at + k] << (8 * k);
+                    }
+                }
+            }
+            auto ref_at = [&](int k, long col) -> uint8_t {   // ref_base(D, r0 + col)
+                if (CPT != 4) return ref_base(D, r0 + col);
+                const uint8_t c = (uint8_t)(rb4 >> (8 * k));
+                return D.ref_nt4 ? nt4_ascii(c > 4 ? 4 : c) : c;
+            };
+            auto qual_at = [&](int k, long col) -> int {
+                return CPT != 4 ? (int)D.ref_qual[r0 + col] : (int)((rq4 >> (8 * k)) & 0xFFu);
+            };
             // best insertion state per column: highest count, then lowest first-seen order
             for (int x = tid; x < G::WCAP; x += CNS_THREADS) {
                 const uint32_t k = wkey[x];
@@ -1144,9 +1297,9 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                     int rs = -1;
                     double vref = 0.0;
                     if (use_rq) {
-                        const double fr = phred2freq((int)D.ref_qual[r0 + col] - P.ref_phred_offset);
+                        const double fr = phred2freq(qual_at(k, col) - P.ref_phred_offset);
                         if (fr != 0.0) {
-                            rs = fixed_idx(ref_base(D, r0 + col));
+                            rs = fixed_idx(ref_at(k, col));
                             vref = fr;   // ref freq is added first, then +1 per alignment
                             uint32_t n = 0;
 #pragma unroll
@@ -1169,7 +1322,7 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                         bslot = (int)(bi & SLOT_MASK);
                     }
                     if (!(maxf != 0.0)) {
-                        olen = 1; desc = DESC_FIXED | (D.ref_seq ? ref_base(D, r0 + col) : (uint8_t)'n'); ph = 0;
+                        olen = 1; desc = DESC_FIXED | (D.ref_seq ? ref_at(k, col) : (uint8_t)'n'); ph = 0;
                     } else if (idx == 4) {
                         olen = 0; desc = 0; ph = 0;
                     } else if (idx < 6) {
@@ -1222,13 +1375,22 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                         so += 1; to += 1;
                     } else {
                         const int slot = (int)(d & SLOT_MASK);
-                        const uint64_t ex = T.exem[slot];
-                        const SeqV src = seq_view(D, ex_aln(ex));
-                        const int eo = ex_off(ex);
-                        for (int q = 0; q < ol; ++q) {
-                            D.o_seq[o0 + so + q] = src[eo + q];
-                            D.o_qual[o0 + so + q] = qc;
-                            D.o_trace[o0 + to + q] = q ? 'D' : 'M';
+                        const uint64_t key = T.key[slot];
+                        if (!(key >> 63)) {   // an injective key holds the string: no exemplar SEQ loads
+                            for (int q = 0; q < ol; ++q) {
+                                D.o_seq[o0 + so + q] = (uint8_t)(0x4E544743413FULL >> (8 * ((key >> (3 * q)) & 7u)));
+                                D.o_qual[o0 + so + q] = qc;
+                                D.o_trace[o0 + to + q] = q ? 'D' : 'M';
+                            }
+                        } else {
+                            const uint64_t ex = T.exem[slot];
+                            const SeqV src = seq_view(D, ex_aln(ex));
+                            const int eo = ex_off(ex);
+                            for (int q = 0; q < ol; ++q) {
+                                D.o_seq[o0 + so + q] = src[eo + q];
+                                D.o_qual[o0 + so + q] = qc;
+                                D.o_trace[o0 + to + q] = q ? 'D' : 'M';
+                            }
                         }
                         so += ol; to += ol;
                     }
