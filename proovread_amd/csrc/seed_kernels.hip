@@ -31,6 +31,9 @@ constexpr int SEED_LMAX = SEED_LMAX_DEF;     // LDS start offsets per wave: read
 #ifndef SEED_MINB
 #define SEED_MINB 4
 #endif
+#ifndef OCC_U
+#define OCC_U 2   // hits per lane per pass of the occurrence table's hit loop
+#endif
 
 // the short j-mer count tables (j <= LC_MAX) into the workgroup's LDS: the SMEM search's
 // occurrence counts of short extensions are dependent lookups, on chip instead of L2/MALL
@@ -125,51 +128,107 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
     __threadfence_block();
     if (!err) {
         const int amax = len - KI;   // last start with a 12-mer
-        for (int k = lane; k < nh; k += 64) {
-            int lo = 0, hi = amax;   // last start whose hits begin at or before k
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (ho[mid] <= k) lo = mid; else hi = mid - 1;
-            }
-            const int a = lo;
-            const uint32_t code = (uint32_t)S.codes[a];
-            const uint64_t r = V.koff[code] + (uint64_t)(k - ho[a]);
-            const uint64_t p = seedc::hit_pos(V, code, r);
-            const uint64_t exb = V.kext[r];
-            const uint64_t qe = S.qext[a];
-            const int le = (int)(exb >> 56), lq = (int)(qe >> 56);
-            const uint64_t xd = (exb ^ qe) & seedc::KX_MASK;
-            int m = xd ? seedc::ctz64(xd) >> 1 : KX;
-            m = m < le ? m : le;
-            m = m < lq ? m : lq;
-            int ml = KI + m;
-            if (m == KX) {
-                if (V.text4) {   // 16 bases at a time: the first differing nibble, or a read N, or the read's end
-                    for (;;) {
-                        const int x = a + ml;
-                        if (x >= len) break;
-                        const uint64_t qw = nib16(q4, (uint64_t)x), tw = nib16(V.text4, p + ml);
-                        const uint64_t nq = (qw >> 2) & 0x1111111111111111ull;   // read N (code 4) or past the end (6)
-                        const uint64_t bad = (qw ^ tw) | (nq * 0xFull);
-                        const int lim = len - x;
-                        if (bad) {
-                            const int f = __builtin_ctzll(bad) >> 2;
-                            ml += f < lim ? f : lim;
-                            break;
-                        }
-                        if (lim <= 16) {
-                            ml += lim;
-                            break;
-                        }
-                        ml += 16;
-                    }
-                } else {
-                    while (a + ml < len && q[a + ml] < 4 && V.text[p + ml] == q[a + ml]) ++ml;
+        // OCC_U hits per lane per pass, their dependent load chains (start lookup -> code ->
+        // k-mer list -> position -> contig -> coordinates) interleaved: one chain's latency per
+        // OCC_U hits instead of per hit
+        constexpr int U = OCC_U;
+        for (int k0 = lane; k0 < nh; k0 += 64 * U) {
+            int aa[U];
+            bool ok[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int k = k0 + 64 * u;
+                ok[u] = k < nh;
+                int lo = 0, hi = amax;   // last start whose hits begin at or before k
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (ho[mid] <= k) lo = mid; else hi = mid - 1;
                 }
+                aa[u] = lo;
             }
-            seedc::set_hpos(S, k, p);
-            S.hfr[k] = seedc::pack_fr(V, p);   // the chaining's coordinates, lane-parallel here
-            S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
+            uint32_t code[U];
+            uint64_t qe[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                code[u] = ok[u] ? (uint32_t)S.codes[aa[u]] : 0u;
+                qe[u] = ok[u] ? S.qext[aa[u]] : 0ull;
+            }
+            uint64_t r[U], p[U], exb[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) r[u] = V.koff[code[u]] + (uint64_t)(k0 + 64 * u - ho[aa[u]]);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                p[u] = ok[u] ? seedc::hit_pos(V, code[u], r[u]) : 0ull;
+                exb[u] = ok[u] ? V.kext[r[u]] : 0ull;
+            }
+            // the contigs (seed_core.h contig_of) and bwa coordinates (pack_fr), interleaved
+            int c[U];
+            int64_t nx[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) c[u] = V.cblk[p[u] >> seedc::CB_SHIFT];
+#pragma unroll
+            for (int u = 0; u < U; ++u) nx[u] = c[u] + 1 < V.n_contig ? V.cstart[c[u] + 1] : INT64_MAX;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                while (nx[u] <= (int64_t)p[u]) {
+                    ++c[u];
+                    nx[u] = c[u] + 1 < V.n_contig ? V.cstart[c[u] + 1] : INT64_MAX;
+                }
+            int64_t cst[U], lro[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                cst[u] = V.cstart[c[u]];
+                lro[u] = c[u] < V.n_lr ? V.lr_off[c[u]] : V.lr_off[2 * V.n_lr - c[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!ok[u]) continue;
+                const int k = k0 + 64 * u, a = aa[u];
+                const int le = (int)(exb[u] >> 56), lq = (int)(qe[u] >> 56);
+                const uint64_t xd = (exb[u] ^ qe[u]) & seedc::KX_MASK;
+                int m = xd ? seedc::ctz64(xd) >> 1 : KX;
+                m = m < le ? m : le;
+                m = m < lq ? m : lq;
+                int ml = KI + m;
+                if (m == KX) {
+                    if (V.text4) {   // 16 bases at a time: the first differing nibble, or a read N, or the read's end
+                        for (;;) {
+                            const int x = a + ml;
+                            if (x >= len) break;
+                            const uint64_t qw = nib16(q4, (uint64_t)x), tw = nib16(V.text4, p[u] + ml);
+                            const uint64_t nq = (qw >> 2) & 0x1111111111111111ull;   // read N (code 4) or past the end (6)
+                            const uint64_t bad = (qw ^ tw) | (nq * 0xFull);
+                            const int lim = len - x;
+                            if (bad) {
+                                const int f = __builtin_ctzll(bad) >> 2;
+                                ml += f < lim ? f : lim;
+                                break;
+                            }
+                            if (lim <= 16) {
+                                ml += lim;
+                                break;
+                            }
+                            ml += 16;
+                        }
+                    } else {
+                        while (a + ml < len && q[a + ml] < 4 && V.text[p[u] + ml] == q[a + ml]) ++ml;
+                    }
+                }
+                seedc::set_hpos(S, k, p[u]);
+                // pack_fr: the hit's forward-reverse coordinate and long read (text_to_fr)
+                const int64_t o = (int64_t)p[u] - cst[u];
+                int64_t fr;
+                int rid;
+                if (c[u] < V.n_lr) {
+                    rid = c[u];
+                    fr = lro[u] + o;
+                } else {
+                    rid = 2 * V.n_lr - 1 - c[u];   // the reverse half holds the long reads in reverse order
+                    fr = V.l_pac + (V.l_pac - lro[u]) + o;
+                }
+                S.hfr[k] = ((uint64_t)fr << seedc::FR_RID_BITS) | (uint64_t)rid;
+                S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
+            }
         }
         __threadfence_block();
         wave_sync_lds();

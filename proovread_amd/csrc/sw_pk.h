@@ -147,6 +147,20 @@ SW_RING_FN void pk_tref16(const uint8_t *T, int ts, int r, uint32_t w[4]) {
         w[2] = __builtin_bswap32(x[1]), w[3] = __builtin_bswap32(x[0]);
     }
 }
+// 8 bases (rows r .. r + 7), as pk_tref16
+SW_RING_FN void pk_tref8(const uint8_t *T, int ts, int r, uint32_t w[2]) {
+    uint32_t x[2];
+    __builtin_memcpy(x, ts > 0 ? T + r : T - r - 7, 8);
+    if (ts > 0) {
+        w[0] = x[0], w[1] = x[1];
+    } else {
+        w[0] = __builtin_bswap32(x[1]), w[1] = __builtin_bswap32(x[0]);
+    }
+}
+SW_RING_FN void pk_shr8_2(uint32_t w[2]) {
+    w[0] = (w[0] >> 8) | (w[1] << 24);
+    w[1] >>= 8;
+}
 // the window one row on
 SW_RING_FN void pk_shr8(uint32_t w[4]) {
     w[0] = (w[0] >> 8) | (w[1] << 24);
@@ -422,13 +436,21 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
     int end[2] = {qlen, qlen}, mx[2], max_i[2] = {-1, -1}, max_j[2] = {-1, -1}, max_ie[2] = {-1, -1};
     int gscore[2] = {-1, -1}, max_off[2] = {0, 0};
     bool live[2];
-    uint32_t tw[2][4];   // reference window: byte 0 = row i
+#ifndef PK_EXT_TW
+#define PK_EXT_TW 4   // reference window of the extension: 4 dwords (16 rows) or 2 (8 rows)
+#endif
+    constexpr int TW = PK_EXT_TW, TROWS = 4 * TW;
+    uint32_t tw[2][TW];   // reference window: byte 0 = row i
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         mx[h] = Hh[h]->h0;
         live[h] = Hh[h]->tlen > 0;
-        tw[h][0] = tw[h][1] = tw[h][2] = tw[h][3] = 0u;
-        if (live[h]) pk_tref16(Hh[h]->T, Hh[h]->ts, 0, tw[h]);
+#pragma unroll
+        for (int x = 0; x < TW; ++x) tw[h][x] = 0u;
+        if (live[h]) {
+            if constexpr (TW == 4) pk_tref16(Hh[h]->T, Hh[h]->ts, 0, tw[h]);
+            else pk_tref8(Hh[h]->T, Hh[h]->ts, 0, tw[h]);
+        }
     }
     for (int i = 0; i < nrows; ++i) {
         int cb[2];
@@ -436,10 +458,14 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             int c = (int)(tw[h][0] & 0xFFu);
-            if ((i & 15) == 15) {   // (wave-uniform)
-                if (i + 1 < Hh[h]->tlen) pk_tref16(Hh[h]->T, Hh[h]->ts, i + 1, tw[h]);
+            if ((i & (TROWS - 1)) == TROWS - 1) {   // (wave-uniform)
+                if (i + 1 < Hh[h]->tlen) {
+                    if constexpr (TW == 4) pk_tref16(Hh[h]->T, Hh[h]->ts, i + 1, tw[h]);
+                    else pk_tref8(Hh[h]->T, Hh[h]->ts, i + 1, tw[h]);
+                }
             } else {
-                pk_shr8(tw[h]);
+                if constexpr (TW == 4) pk_shr8(tw[h]);
+                else pk_shr8_2(tw[h]);
             }
             if (Hh[h]->comp && c < 4) c = 3 - c;
             if (live[h] && i >= Hh[h]->tlen) live[h] = false;

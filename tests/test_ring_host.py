@@ -16,10 +16,11 @@ import oracle_bind as ob
 ROOT = Path(__file__).resolve().parents[1]
 
 
-@pytest.fixture(scope="module")
-def ring(tmp_path_factory):
-    out = tmp_path_factory.mktemp("ring") / "libring_host.so"
-    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", str(out),
+@pytest.fixture(scope="module", params=[4, 2], ids=["tw4", "tw2"])
+def ring(tmp_path_factory, request):
+    """Both reference-window widths of the packed extension (PK_EXT_TW dwords)."""
+    out = tmp_path_factory.mktemp("ring") / f"libring_host_tw{request.param}.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", f"-DPK_EXT_TW={request.param}", "-o", str(out),
                     str(ROOT / "tests" / "native" / "ring_host.cpp")], check=True)
     return C.CDLL(str(out))
 
