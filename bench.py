@@ -291,7 +291,10 @@ def main():
 
             def hbm(prefix):
                 return next((v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith(prefix)), None)
-            traffic, traffic_cns, traffic_seed = hbm("sw_global_pk_kernel<40"), hbm("cns_lr_kernel"), hbm("seed_batch")
+            traffic, traffic_cns = hbm("sw_global_pk_kernel<40"), hbm("cns_lr_kernel")
+            ts = [hbm("prgpu::seed_batch_kernel"), hbm("prgpu::seed_wave_kernel")]   # both seeding passes
+            ts = [hbm("seed_batch"), hbm("seed_wave")] if ts[0] is None else ts
+            traffic_seed = sum(x for x in ts if x is not None) if ts[0] is not None else None
             traffic_ext = {k: v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith("sw_ext_")}
         except Exception:
             traffic = traffic_cns = traffic_ext = traffic_seed = None
@@ -367,7 +370,7 @@ def main():
             "frac_of_packed_int16_peak": round(ext_tops / (2 * VALU_PEAK_TOPS), 4),
             "traffic_per_launch": traffic_ext,
         },
-        "roofline_seeding": seeding_roofline(ev[1], s1 - s0, traffic_seed),
+        "roofline_seeding": seeding_roofline(ev[1], s1 - s0, traffic_seed, n_seeds),
         "cpu_baseline": cpu,
         "cpu_baseline_reference": ref_cpu,
         "comm": "rccl" if cm is not None else "none",
@@ -394,14 +397,18 @@ def lrs_index_ms(L, ctx) -> float:
 # on 20 k reads of this workload): per 150 bp read the scratch and index accesses the algorithm
 # makes -- occurrence-table builds, SMEM steps, chaining and the filter -- in bytes.  Kept as a
 # constant measured once ("seeding roofline").
-SEED_BYTES_PER_READ = None
+# algorithmic bytes per short read of the seeding stage without its output (tools/seed_bytes.py on
+# this dataset: 150 B of bases, 16 B per start's koff pair x 139.0 starts, 32 B per occurrence-table
+# hit (kpos, kext, contig lookup) x 3200.5 hits), + 40 B per output seed (pr_seed_task)
+SEED_BYTES_PER_READ = 104789
+SEED_BYTES_PER_SEED = 40
 
 
-def seeding_roofline(kernel_ms: float, n_reads: int, traffic):
+def seeding_roofline(kernel_ms: float, n_reads: int, traffic, n_seeds: int = 0):
     if not SEED_BYTES_PER_READ or not kernel_ms:
         return {"kernel": "seed_batch_kernel + seed_wave_kernel", "bound": "hbm", "launch_ms": round(kernel_ms, 3),
                 "traffic": traffic, "note": "byte model not measured"}
-    alg = SEED_BYTES_PER_READ * n_reads
+    alg = SEED_BYTES_PER_READ * n_reads + SEED_BYTES_PER_SEED * n_seeds
     ach = alg / (kernel_ms * 1e-3) / 1e9
     return {"kernel": "seed_batch_kernel + seed_wave_kernel", "bound": "hbm", "achieved": round(ach, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes": int(alg),
