@@ -1104,16 +1104,22 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
         }
         const int nwin = (int)((L + G::W - 1) / G::W);
         int32_t *wcur = reinterpret_cast<int32_t *>(B + G::B_CNT);   // per-window counters (<= 3W)
-        int32_t *Kh = D.k_pool + (int64_t)blockIdx.x * D.k_cap;      // [0, nwin] window starts, then entries
-        int4 *K = reinterpret_cast<int4 *>(Kh + ((nwin + 4) & ~3));
+        // K pool of this workgroup: Kh[0, nwin] window starts, Ks[0, nwin) the start of each
+        // window's straddlers (alignments that run past the window's end: they sit last in their
+        // window, so the candidates of window w are the contiguous K[Ks[w - wback], Kh[w + 1])),
+        // then the entries
+        int32_t *Kh = D.k_pool + (int64_t)blockIdx.x * D.k_cap;
+        int32_t *Ks = Kh + nwin + 1;
+        int4 *K = reinterpret_cast<int4 *>(Kh + ((2 * nwin + 4) & ~3));
+        int32_t *wst = wcur + nwin + 1;   // per-window straddler counters
         const int wv = tid >> 6;
         int4 *wops = reinterpret_cast<int4 *>(B + G::B_WAVE + wv * G::WAVE_BYTES);   // this wave's op table
         uint32_t *wseq = reinterpret_cast<uint32_t *>(B + G::B_WAVE + wv * G::WAVE_BYTES + 64 * 16);   // its SEQ dwords
         const bool snt4 = D.seq_nt4 != 0;
         if (tid == 0) { C->nk = 0; C->maxspan = 0; }
-        for (int x = tid; x <= nwin && x < 3 * G::W; x += CNS_THREADS) wcur[x] = 0;
+        for (int x = tid; x < 2 * (nwin + 1) && x < 3 * G::W; x += CNS_THREADS) wcur[x] = 0;
         __syncthreads();
-        if (nwin + 1 > 3 * G::W) C->flag = 1;
+        if (2 * (nwin + 1) > 3 * G::W) C->flag = 1;
         for (int i = tid; i < na; i += CNS_THREADS) {   // a thread per kept alignment: the window counts
             const int64_t g = a0 + i;
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
@@ -1121,11 +1127,14 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             atomicAdd(&C->nk, 1);
             atomicMax(&C->maxspan, span);
             const int win = rp / G::W;
-            if (win < 3 * G::W) atomicAdd(&wcur[win], 1);
+            if (2 * (nwin + 1) <= 3 * G::W) {
+                atomicAdd(&wcur[win], 1);
+                if (D.a_end[g] > (win + 1) * G::W) atomicAdd(&wst[win], 1);
+            }
         }
         __syncthreads();
         // 16-bit fixed-state counters: at most 65535 kept alignments per read
-        if (C->flag || (int64_t)((nwin + 4) & ~3) + 12 * (int64_t)C->nk > D.k_cap || C->nk > 65535) {
+        if (C->flag || (int64_t)((2 * nwin + 4) & ~3) + 12 * (int64_t)C->nk > D.k_cap || C->nk > 65535) {
             CNS_CAP_FAIL();
             continue;
         }
@@ -1136,16 +1145,21 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             for (int w = b0; w < b1; ++w) s += w < nwin ? wcur[w] : 0;
             long long tot;
             long long base = block_scan_excl(s, scan, &tot);
-            for (int w = b0; w < b1; ++w) { Kh[w] = (int32_t)base; base += w < nwin ? wcur[w] : 0; }
+            for (int w = b0; w < b1; ++w) {
+                Kh[w] = (int32_t)base;
+                if (w < nwin) Ks[w] = (int32_t)base + wcur[w] - wst[w];
+                base += w < nwin ? wcur[w] : 0;
+            }
             __syncthreads();
-            for (int w = tid; w < nwin; w += CNS_THREADS) wcur[w] = 0;
+            for (int w = tid; w < nwin; w += CNS_THREADS) { wcur[w] = 0; wst[w] = 0; }
             __syncthreads();
         }
         for (int i = tid; i < na; i += CNS_THREADS) {
             const int64_t g = a0 + i;
             if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
             const int rp = D.a_rpos[g], win = rp / G::W;
-            const int kpos = Kh[win] + atomicAdd(&wcur[win], 1);
+            const int kpos = D.a_end[g] > (win + 1) * G::W ? Ks[win] + atomicAdd(&wst[win], 1)
+                                                           : Kh[win] + atomicAdd(&wcur[win], 1);
             // the entry carries what a window's wave needs (one 48-byte record instead of seven
             // scattered per-alignment loads per window)
             const int cbk = D.a_cb[g];
@@ -1210,7 +1224,8 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                 const long lo = s0 > w0 ? s0 : w0, hi = s1 < w0 + wn ? s1 : w0 + wn;
                 for (long col = lo; col < hi; ++col) atomicOr(&ignb[(col - w0) >> 5], 1u << ((col - w0) & 31));
             }
-            const int kb = Kh[wi - wback > 0 ? wi - wback : 0], ke = Kh[wi + 1];
+            const int wb0 = wi - wback;   // the earliest window whose straddlers can reach this one
+            const int kb = wb0 < 0 ? 0 : (wb0 < wi ? Ks[wb0] : Kh[wi]), ke = Kh[wi + 1];
             __syncthreads();
             CNS_TICK(8);
             if (D.prof && tid == 0) pt[14] += 1;
