@@ -250,7 +250,9 @@ struct HostScratch {
     std::vector<uint64_t> hfr;
     std::vector<seedc::Iv> mems, m1, curr, prev;
     std::vector<seedc::Seed> seeds;
-    std::vector<int32_t> next, cnx, kept, hkey, hhead, htail;
+    std::vector<int32_t> cnx, kept;
+    std::vector<seedc::RangeEnt> htab;
+    std::vector<seedc::RangeRec> rg;
     std::vector<seedc::Chain> cv, ch;
     std::vector<pr_seed_task> out;
     seedc::Scratch S{};
@@ -273,21 +275,19 @@ struct HostScratch {
         curr.resize((size_t)iv);
         prev.resize((size_t)iv);
         seeds.resize((size_t)seeds_cap);
-        next.resize((size_t)seeds_cap);
         cv.resize((size_t)chains);
         ch.resize((size_t)chains);
         cnx.resize((size_t)chains);
         kept.resize((size_t)chains);
         const int32_t hs = seedc::range_table_size(chains);
-        hkey.resize((size_t)hs);
-        hhead.resize((size_t)hs);
-        htail.resize((size_t)hs);
+        htab.resize((size_t)hs);
+        rg.resize((size_t)chains);
         out.resize((size_t)out_cap);
         S = seedc::Scratch{lmax,        hoff.data(),  qext.data(), codes.data(), ge.data(),   hpos.data(),
                            hi ? hhi.data() : nullptr, hml.data(),  hits, mems.data(), mems_cap, m1.data(), curr.data(),
-                           prev.data(), iv,           seeds.data(), next.data(), seeds_cap,   cv.data(),
-                           ch.data(),   cnx.data(),   kept.data(), hkey.data(), hhead.data(),
-                           htail.data(), chains,      hs};
+                           prev.data(), iv,           seeds.data(), seeds_cap,   cv.data(),
+                           ch.data(),   cnx.data(),   kept.data(), htab.data(), rg.data(),
+                           chains,      hs};
         S.rmax = rmax.data();
         S.hfr = hfr.data();
     }

@@ -90,7 +90,23 @@ struct Iv {
 };
 struct Seed {
     int64_t rbeg;   // forward-reverse coordinate (bwa): reverse strand >= l_pac
-    int32_t qbeg, len;
+    int16_t qbeg, len;   // (reads <= 1000 bp: proovread:457)
+    int32_t nx;     // the next seed of its chain (-1: the last)
+};
+// A (long read, strand) range of the chaining (map_chains): its chain list and, for the merges
+// that nearly every occurrence makes, a copy of the list's last chain's merge state (its pos,
+// first and last seed, seed count) -- one cache line per occurrence instead of the range table,
+// the chain record and two seed records.  n / last / l_idx are authoritative while the chain is
+// the range's tail and written back to it when another chain becomes the tail and at the end.
+struct RangeRec {
+    int32_t head, tail, n, l_idx;   // list head / tail (chain indices), the tail chain's seeds / last seed
+    int64_t tpos;                   // the tail chain's pos
+    int64_t f_rbeg, l_rbeg;         // its first and last seed
+    int32_t f_ql, l_ql;             // qbeg | len << 16
+    int32_t pad[4];                 // (64 bytes: one record per half cache line)
+};
+struct RangeEnt {
+    int32_t key, r;   // rid * 2 + strand (-1: free), its RangeRec
 };
 struct Chain {
     int64_t pos;
@@ -119,11 +135,11 @@ struct Scratch {
     Iv *m1, *curr, *prev;                      // [cap_iv] each
     int32_t cap_iv;
     Seed *seeds;                               // [cap_seeds]
-    int32_t *next;                             // [cap_seeds]
     int32_t cap_seeds;
     Chain *cv, *ch;                            // [cap_chains] each
     int32_t *cnx, *kept;                       // [cap_chains] each; cnx: next chain of its range's list
-    int32_t *hkey, *hhead, *htail;             // [hsize] range table: key (-1 free), list head / tail
+    RangeEnt *htab;                            // [hsize] range table (open addressing)
+    RangeRec *rg;                              // [cap_chains] the ranges, in creation order
     int32_t cap_chains, hsize;                 // hsize: power of two >= 2 * cap_chains
     uint16_t *rmax;                            // [(lmax + 1) * RK] R_k(a), k = 1..RK (rmax_k)
     uint64_t *hfr;                             // [cap_hits] pack_fr of the hit (the chaining's coordinates)
@@ -631,9 +647,10 @@ SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const 
 // one sorted array (every insert shifted ~40 entries, the seeding kernel's largest cost).
 SC_HD int range_slot(const Scratch &S, int32_t key) {
     uint32_t h = ((uint32_t)key * 0x9E3779B1u) & (uint32_t)(S.hsize - 1);
-    while (S.hkey[h] != -1 && S.hkey[h] != key) h = (h + 1) & (uint32_t)(S.hsize - 1);
+    while (S.htab[h].key != -1 && S.htab[h].key != key) h = (h + 1) & (uint32_t)(S.hsize - 1);
     return (int)h;
 }
+SC_HD int32_t pack_ql(const Seed &s) { return (int32_t)(uint16_t)s.qbeg | ((int32_t)s.len << 16); }
 
 // -> 1 merged, 0 not, -1 pool full
 SC_HD int test_and_merge(const pr_seed_opts &O, int64_t l_pac, Scratch &S, int32_t &ns, Chain &c, const Seed &p,
@@ -649,8 +666,8 @@ SC_HD int test_and_merge(const pr_seed_opts &O, int64_t l_pac, Scratch &S, int32
     if (y >= 0 && x - y <= O.w && y - x <= O.w && x - last.len < O.max_chain_gap && y - last.len < O.max_chain_gap) {
         if (ns >= S.cap_seeds) return -1;
         S.seeds[ns] = p;
-        S.next[ns] = -1;
-        S.next[c.tail] = ns;
+        S.seeds[ns].nx = -1;
+        S.seeds[c.tail].nx = ns;
         c.tail = ns++;
         ++c.n;
         return 1;
@@ -658,10 +675,38 @@ SC_HD int test_and_merge(const pr_seed_opts &O, int64_t l_pac, Scratch &S, int32
     return 0;
 }
 
+// test_and_merge against a range's tail chain through its RangeRec copy (same decisions)
+SC_HD int merge_tail(const pr_seed_opts &O, int64_t l_pac, Scratch &S, int32_t &ns, RangeRec &R, const Seed &p) {
+    const int64_t f_rbeg = R.f_rbeg, l_rbeg = R.l_rbeg;
+    const int f_q = (int16_t)(R.f_ql & 0xFFFF), l_q = (int16_t)(R.l_ql & 0xFFFF), l_len = R.l_ql >> 16;
+    const int64_t qend = l_q + l_len, rend = l_rbeg + l_len;
+    if (p.qbeg >= f_q && p.qbeg + p.len <= qend && p.rbeg >= f_rbeg && p.rbeg + p.len <= rend)
+        return 1;   // contained seed
+    if ((l_rbeg < l_pac || f_rbeg < l_pac) && p.rbeg >= l_pac) return 0;   // other strand
+    const int64_t x = p.qbeg - l_q, y = p.rbeg - l_rbeg;
+    if (y >= 0 && x - y <= O.w && y - x <= O.w && x - l_len < O.max_chain_gap && y - l_len < O.max_chain_gap) {
+        if (ns >= S.cap_seeds) return -1;
+        S.seeds[ns] = p;
+        S.seeds[ns].nx = -1;
+        S.seeds[R.l_idx].nx = ns;
+        R.l_idx = ns++;
+        R.l_rbeg = p.rbeg;
+        R.l_ql = pack_ql(p);
+        ++R.n;
+        return 1;
+    }
+    return 0;
+}
+// the tail chain's authoritative fields back into its chain record
+SC_HD void flush_tail(Scratch &S, const RangeRec &R) {
+    S.cv[R.tail].tail = R.l_idx;
+    S.cv[R.tail].n = R.n;
+}
+
 SC_HD int chain_weight(const Scratch &S, const Chain &c) {
     int64_t end = 0;
     int w = 0;
-    for (int32_t k = c.head; k >= 0; k = S.next[k]) {
+    for (int32_t k = c.head; k >= 0; k = S.seeds[k].nx) {
         const Seed &s = S.seeds[k];
         if (s.qbeg >= end) w += s.len;
         else if (s.qbeg + s.len > end) w += (int)(s.qbeg + s.len - end);
@@ -670,7 +715,7 @@ SC_HD int chain_weight(const Scratch &S, const Chain &c) {
     const int tmp = w;
     w = 0;
     end = 0;
-    for (int32_t k = c.head; k >= 0; k = S.next[k]) {
+    for (int32_t k = c.head; k >= 0; k = S.seeds[k].nx) {
         const Seed &s = S.seeds[k];
         if (s.rbeg >= end) w += s.len;
         else if (s.rbeg + s.len > end) w += (int)(s.rbeg + s.len - end);
@@ -782,8 +827,8 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
     if (ticks) t_last = __builtin_amdgcn_s_memrealtime();
 #endif
     // mem_chain
-    int32_t ns = 0, ncv = 0;
-    for (int k = 0; k < S.hsize; ++k) S.hkey[k] = -1;
+    int32_t ns = 0, ncv = 0, nrg = 0;
+    for (int k = 0; k < S.hsize; ++k) S.htab[k].key = -1;
     for (int mi = 0; mi < nm; ++mi) {
         const Iv p = S.mems[mi];
         const int slen = p.end - p.start;
@@ -793,9 +838,9 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
         const int64_t np = p.occ;
         const int64_t step = np > O.max_occ ? np / O.max_occ : 1;
         int64_t fidx = 0, take = 0, count = 0;
-        // the selected occurrences in batches of CB: their text positions, forward-reverse
-        // coordinates and range-table probes are independent loads, issued together (one
-        // latency per batch instead of ~5 dependent ones per occurrence); then each in order
+        // the selected occurrences in batches of CB: their forward-reverse coordinates and
+        // range-table probes are independent loads, issued together (one latency per batch
+        // instead of several dependent ones per occurrence); then each in order
         constexpr int CB = 8;
         int32_t k = h0;
         while (k < h1 && count < O.max_occ) {
@@ -834,61 +879,87 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
                 SC_STAT(3, 1);
                 Seed s;
                 s.rbeg = rb[u];
-                s.qbeg = p.start;
-                s.len = slen;
+                s.qbeg = (int16_t)p.start;
+                s.len = (int16_t)slen;
+                s.nx = -1;
                 const int rid = rd[u];
                 // the predecessor that can merge: the last chain of the occurrence's range with
                 // pos <= rbeg (`at`, also the insertion point); occurrences at one locus mostly
-                // come in increasing rbeg, so the list's tail first
+                // come in increasing rbeg, so the list's tail (its RangeRec copy) first
                 const int hs = opened ? range_slot(S, key[u]) : hsl[u];
-                const bool found = S.hkey[hs] == key[u];
+                const RangeEnt e = S.htab[hs];
+                const bool found = e.key == key[u];
                 int at = -1;
+                bool at_tail = false;
                 if (found) {
-                    const int tl = S.htail[hs];
+                    RangeRec &R = S.rg[e.r];
                     SC_STAT(4, 1);
-                    if (S.cv[tl].pos <= s.rbeg) at = tl;
-                    else
-                        for (int x = S.hhead[hs]; x >= 0 && S.cv[x].pos <= s.rbeg; x = S.cnx[x]) {
+                    if (R.tpos <= s.rbeg) {
+                        at = R.tail;
+                        at_tail = true;
+                    } else {
+                        for (int x = R.head; x >= 0 && S.cv[x].pos <= s.rbeg; x = S.cnx[x]) {
                             at = x;
                             SC_STAT(4, 1);
                         }
-                }
-                if (at >= 0) {
-                    const int r = test_and_merge(O, I.l_pac, S, ns, S.cv[at], s, rid);
-                    if (r < 0) return SC_OVER_SEEDS;
-                    if (r) { SC_STAT(5, 1); continue; }
+                    }
+                    if (at >= 0) {
+                        const int r = at_tail ? merge_tail(O, I.l_pac, S, ns, R, s)
+                                              : test_and_merge(O, I.l_pac, S, ns, S.cv[at], s, rid);
+                        if (r < 0) return SC_OVER_SEEDS;
+                        if (r) { SC_STAT(5, 1); continue; }
+                    }
                 }
                 SC_STAT(6, 1);
                 if (ncv >= S.cap_chains) return SC_OVER_CHAINS;
                 if (ns >= S.cap_seeds) return SC_OVER_SEEDS;
                 S.seeds[ns] = s;
-                S.next[ns] = -1;
                 Chain c;
                 c.pos = s.rbeg;
                 c.rid = rid;
-                c.head = c.tail = ns++;
+                c.head = c.tail = ns;
                 c.n = 1;
                 c.w = c.kept = 0;
                 c.first = -1;
                 S.cv[ncv] = c;
                 if (!found) {   // the range's first chain
-                    S.hkey[hs] = key[u];
-                    S.hhead[hs] = S.htail[hs] = ncv;
+                    RangeRec &R = S.rg[nrg];
+                    R.head = R.tail = ncv;
+                    R.n = 1;
+                    R.l_idx = ns;
+                    R.tpos = s.rbeg;
+                    R.f_rbeg = R.l_rbeg = s.rbeg;
+                    R.f_ql = R.l_ql = pack_ql(s);
+                    S.htab[hs].key = key[u];
+                    S.htab[hs].r = nrg++;
                     S.cnx[ncv] = -1;
                     opened = true;
-                } else if (at < 0) {   // before every chain of the range
-                    S.cnx[ncv] = S.hhead[hs];
-                    S.hhead[hs] = ncv;
-                } else {   // after `at` (and after every chain of equal pos)
-                    const int nx = S.cnx[at];
-                    S.cnx[ncv] = nx;
-                    S.cnx[at] = ncv;
-                    if (nx < 0) S.htail[hs] = ncv;
+                } else {
+                    RangeRec &R = S.rg[e.r];
+                    if (at < 0) {   // before every chain of the range
+                        S.cnx[ncv] = R.head;
+                        R.head = ncv;
+                    } else {   // after `at` (and after every chain of equal pos)
+                        const int nx = S.cnx[at];
+                        S.cnx[ncv] = nx;
+                        S.cnx[at] = ncv;
+                        if (nx < 0) {   // the new tail: the old one's fields back into its record
+                            flush_tail(S, R);
+                            R.tail = ncv;
+                            R.n = 1;
+                            R.l_idx = ns;
+                            R.tpos = s.rbeg;
+                            R.f_rbeg = R.l_rbeg = s.rbeg;
+                            R.f_ql = R.l_ql = pack_ql(s);
+                        }
+                    }
                 }
+                ++ns;
                 ++ncv;
             }
         }
     }
+    for (int r = 0; r < nrg; ++r) flush_tail(S, S.rg[r]);
     SC_TICK(3);
     SC_STAT(11, ncv);
     SC_STAT(12, (unsigned long long)ncv * ncv);
@@ -955,7 +1026,7 @@ SC_HD int flt_seed_list(const Scratch &S, int nch, int32_t *list, int cap) {
     for (int ci = 0; ci < nch; ++ci) {
         const Chain &c = S.ch[ci];
         if (c.kept == 0) continue;
-        for (int32_t k = c.head; k >= 0; k = S.next[k]) {
+        for (int32_t k = c.head; k >= 0; k = S.seeds[k].nx) {
             if (n >= cap) return -1;
             list[n++] = k;
         }
@@ -994,7 +1065,7 @@ SC_HD int map_output(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
         const int first = no;
         int idx = 0;
         int64_t r0 = INT64_MAX, r1 = INT64_MIN;
-        for (int32_t k = c.head; k >= 0; k = S.next[k]) {
+        for (int32_t k = c.head; k >= 0; k = S.seeds[k].nx) {
             const Seed &s = S.seeds[k];
             int score = s.len;
             if (flt >= 0) {
@@ -1131,14 +1202,15 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += align8((int64_t)sizeof(Iv) * c.mems);           // mems
     b += 3 * align8((int64_t)sizeof(Iv) * c.iv);         // m1, curr, prev
     b += align8((int64_t)sizeof(Seed) * c.seeds);        // seeds
-    b += align8(4 * (int64_t)c.seeds);                   // next
     b += 2 * align8((int64_t)sizeof(Chain) * c.chains);  // cv, ch
     b += 2 * align8(4 * (int64_t)c.chains);              // cnx, kept
-    b += 3 * align8(4 * (int64_t)range_table_size(c.chains));   // hkey, hhead, htail
+    b += align8((int64_t)sizeof(RangeEnt) * range_table_size(c.chains));   // htab
+    b = (b + 63) & ~(int64_t)63;                         // (rg 64-byte aligned)
+    b += align8((int64_t)sizeof(RangeRec) * c.chains);   // rg
     b += align8(2 * (int64_t)(c.lmax + 1) * RK);         // rmax
     b += align8(8 * (int64_t)c.hits);                    // hfr
     if (c.hi && !c.nopos) b += align8((int64_t)c.hits);  // hhi (last)
-    return b;
+    return (b + 63) & ~(int64_t)63;                      // (slices 64-byte aligned)
 }
 
 // lay a Scratch over an 8-byte aligned slice of scratch_bytes(c) bytes
@@ -1164,16 +1236,15 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.prev = (Iv *)take((int64_t)sizeof(Iv) * c.iv);
     S.cap_iv = c.iv;
     S.seeds = (Seed *)take((int64_t)sizeof(Seed) * c.seeds);
-    S.next = (int32_t *)take(4 * (int64_t)c.seeds);
     S.cap_seeds = c.seeds;
     S.cv = (Chain *)take((int64_t)sizeof(Chain) * c.chains);
     S.ch = (Chain *)take((int64_t)sizeof(Chain) * c.chains);
     S.cnx = (int32_t *)take(4 * (int64_t)c.chains);
     S.kept = (int32_t *)take(4 * (int64_t)c.chains);
     S.hsize = range_table_size(c.chains);
-    S.hkey = (int32_t *)take(4 * (int64_t)S.hsize);
-    S.hhead = (int32_t *)take(4 * (int64_t)S.hsize);
-    S.htail = (int32_t *)take(4 * (int64_t)S.hsize);
+    S.htab = (RangeEnt *)take((int64_t)sizeof(RangeEnt) * S.hsize);
+    p = (uint8_t *)(((uintptr_t)p + 63) & ~(uintptr_t)63);   // (scratch_bytes' alignment of rg)
+    S.rg = (RangeRec *)take((int64_t)sizeof(RangeRec) * c.chains);
     S.cap_chains = c.chains;
     S.rmax = (uint16_t *)take(2 * (int64_t)(c.lmax + 1) * RK);
     S.hfr = (uint64_t *)take(8 * (int64_t)c.hits);

@@ -320,7 +320,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
                 for (int ci = 0; ci < nch; ++ci) {
                     const seedc::Chain &c = S.ch[ci];
                     if (c.kept == 0) continue;
-                    for (int32_t k = c.head; k >= 0; k = S.next[k]) rid[x++] = c.rid;
+                    for (int32_t k = c.head; k >= 0; k = S.seeds[k].nx) rid[x++] = c.rid;
                 }
             }
             __threadfence_block();
