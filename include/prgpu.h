@@ -425,6 +425,9 @@ int pr_seed_gpu_phase_ticks(pr_ctx *ctx, uint64_t *ticks4);
 /* Diagnostics: pass 1's lane work summed over lanes (100 MHz ticks): [SMEM pass, re-seeding,
  * -y seeds + sort, chaining, mem_chain_flt, filter + output] */
 int pr_seed_gpu_lane_ticks(pr_ctx *ctx, uint64_t *ticks6);
+/* pass 1's occurrence tables (profiling): 100 MHz wave-clock ticks summed over
+   waves of the start pass, the hit pass and the count table */
+int pr_seed_gpu_occ_ticks(pr_ctx *ctx, uint64_t *ticks3);
 /* wall time of the last pr_seed_gpu_map's second pass (the reads that outgrew pass 1's slices), ms */
 int pr_seed_gpu_pass2_ms(pr_ctx *ctx, double *ms);
 /* diagnostics (tests): the device path's core and capacities (its passes included) run on the host */

@@ -2435,6 +2435,14 @@ extern "C" int pr_seed_gpu_lane_ticks(pr_ctx *c, uint64_t *ticks6) {
     return 0;
 }
 
+extern "C" int pr_seed_gpu_occ_ticks(pr_ctx *c, uint64_t *ticks3) {
+    if (!c || !ticks3) return set_error(PR_ERR_ARG, "null arg");
+    if (!c->sd[SB_NEXT].p) return set_error(PR_ERR_ARG, "no pr_seed_gpu_map launch yet");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(ticks3, c->sd[SB_NEXT].as<uint8_t>() + 64 + 10 * 8, 24, hipMemcpyDeviceToHost));
+    return 0;
+}
+
 // SW stage entry points are in sw_api.cpp (they share pr_ctx through this accessor)
 SwResident &ctx_sw(pr_ctx *c) { return c->sw; }
 hipStream_t ctx_stream(pr_ctx *c) { return c->stream; }

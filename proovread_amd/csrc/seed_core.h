@@ -264,23 +264,20 @@ SC_HD int rmax_short(const Occ &occ, const uint8_t *q, int len, int a, int64_t k
 // R_1 .. R_RK of start a into S.rmax[a * RK ..]: with >= k hits of its 12-mer, a + the k-th
 // largest hit match length (occ(a, e) >= k exactly when k hits match >= e - a bases); with
 // fewer, the longest N-free j-mer (j < 12) with >= k occurrences (R_k never grows with k)
-SC_HD void fill_rk(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a) {
-    uint16_t *r = S.rmax + (int64_t)a * RK;
-    uint16_t top[RK];
+// insert a hit's match length into a start's descending top-RK list
+SC_HD void topk_insert(uint16_t (&top)[RK], uint16_t v) {
 #pragma unroll
-    for (int k = 0; k < RK; ++k) top[k] = 0;
-    if (q[a] < 4 && a + KI <= len && S.codes[a] >= 0) {
-        for (int32_t h = S.hoff[a]; h < S.hoff[a + 1]; ++h) {
-            uint16_t v = S.hml[h];   // insert into the descending top list
-#pragma unroll
-            for (int k = 0; k < RK; ++k) {
-                const uint16_t t = top[k];
-                const bool gt = v > t;
-                top[k] = gt ? v : t;
-                v = gt ? t : v;
-            }
-        }
+    for (int k = 0; k < RK; ++k) {
+        const uint16_t t = top[k];
+        const bool gt = v > t;
+        top[k] = gt ? v : t;
+        v = gt ? t : v;
     }
+}
+// R_1 .. R_RK of start a from its top list (the RK largest hit match lengths, 0-padded; all
+// zero when the start has no 12-mer or q[a] is N)
+SC_HD void fill_rk_top(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a, const uint16_t (&top)[RK]) {
+    uint16_t *r = S.rmax + (int64_t)a * RK;
     int e = -1;   // the short part: j-mer counts never grow with k, so its end only falls
     int64_t ce = 0;
     for (int k = 1; k <= RK; ++k) {
@@ -298,6 +295,14 @@ SC_HD void fill_rk(const Occ &occ, const Scratch &S, const uint8_t *q, int len, 
         }
         r[k - 1] = (uint16_t)e;
     }
+}
+SC_HD void fill_rk(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a) {
+    uint16_t top[RK];
+#pragma unroll
+    for (int k = 0; k < RK; ++k) top[k] = 0;
+    if (q[a] < 4 && a + KI <= len && S.codes[a] >= 0)
+        for (int32_t h = S.hoff[a]; h < S.hoff[a + 1]; ++h) topk_insert(top, S.hml[h]);
+    fill_rk_top(occ, S, q, len, a, top);
 }
 
 // R_k(a): tabulated for k <= RK; beyond (re-seeding with split_width >= RK), from the start's

@@ -67,23 +67,46 @@ __device__ __forceinline__ uint64_t nib16(const uint64_t *w4, uint64_t x) {
 }
 
 __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, const uint8_t *q, int len, int32_t *ho,
-                              int lane, uint64_t *q4, const uint32_t *lc, int *n_hits = nullptr) {
+                              int lane, uint64_t *q4, const uint32_t *lc, int *n_hits = nullptr,
+                              unsigned long long *ot = nullptr) {
+    // ot (optional): wall-clock ticks of the start pass, the hit pass and the count table
+    unsigned long long t_occ = ot ? wall_clock64() : 0ULL;
+#define OCC_TICK(k)                                        \
+    do {                                                   \
+        if (ot) {                                          \
+            const unsigned long long t_ = wall_clock64();  \
+            ot[k] += t_ - t_occ;                           \
+            t_occ = t_;                                    \
+        }                                                  \
+    } while (0)
     using seedc::HB;
     using seedc::KI;
     using seedc::KX;
     int err = 0;
     int run = 0;
-    // the read 16 bases per word in LDS (past the read: 6, never a text code) for the match
-    // lengths below; visible after the wave_sync_lds that follows the start pass
-    if (V.text4)
-        for (int w = lane; w <= (len >> 4) + 1; w += 64) {
+    // the read 16 bases per word in LDS (past the read: 6, never a text code) for the start
+    // pass's codes and the match lengths below (words up to (len >> 4) + 3: a start's 12-mer and
+    // the KX bases after it, read 16 at a time)
+    if (V.text4) {
+        for (int w = lane; w <= (len >> 4) + 3; w += 64) {
+            const int x0 = w * 16;
+            uint8_t b[16];
+            if (x0 + 16 <= len) {
+                __builtin_memcpy(b, q + x0, 16);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) b[k] = x0 + k < len ? q[x0 + k] : (uint8_t)6;
+            }
             uint64_t v = 0;
+#pragma unroll
             for (int k = 0; k < 16; ++k) {
-                const int x = w * 16 + k;
-                v |= (uint64_t)(x < len ? (q[x] < 4 ? q[x] : 4) : 6) << (4 * k);
+                const uint32_t c = x0 + k < len ? (b[k] < 4 ? b[k] : 4u) : 6u;
+                v |= (uint64_t)c << (4 * k);
             }
             q4[w] = v;
         }
+        wave_sync_lds();
+    }
     for (int a0 = 0; a0 <= len; a0 += 64) {
         const int a = a0 + lane;
         int ca = 0;
@@ -93,13 +116,38 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
             if (a + KI <= len) {
                 uint32_t code = 0;
                 bool ok = true;
-                for (int x = 0; x < KI; ++x) {
-                    const uint8_t c = q[a + x];
-                    ok &= c < 4;
-                    code = (code << 2) | (c & 3u);
-                }
                 const int n = len - a - KI;
-                qe = seedc::pack_ext(q + a + KI, n < KX ? n : KX);
+                if (V.text4) {   // from the read's packed copy in LDS (4 bits a base, 6 past its end)
+                    const uint64_t w0 = nib16(q4, (uint64_t)a), w1 = nib16(q4, (uint64_t)a + 16),
+                                   w2 = nib16(q4, (uint64_t)a + 32);
+#pragma unroll
+                    for (int x = 0; x < KI; ++x) {
+                        const uint32_t c = (uint32_t)(w0 >> (4 * x)) & 15u;
+                        ok &= c < 4;
+                        code = (code << 2) | (c & 3u);
+                    }
+                    // pack_ext of the KX bases after the 12-mer: 2 bits each up to the first N
+                    const int nmax = n < KX ? n : KX;
+                    uint64_t v = 0;
+                    int k = 0;
+#pragma unroll
+                    for (int x = 0; x < KX; ++x) {
+                        const int b = KI + x;   // base a + b: word b >> 4, nibble b & 15
+                        const uint64_t wb = b < 16 ? w0 : b < 32 ? w1 : w2;
+                        const uint32_t c = (uint32_t)(wb >> (4 * (b & 15))) & 15u;
+                        const bool go = k == x && x < nmax && c < 4;
+                        v |= go ? (uint64_t)c << (2 * x) : 0ull;
+                        k += go ? 1 : 0;
+                    }
+                    qe = v | ((uint64_t)k << 56);
+                } else {
+                    for (int x = 0; x < KI; ++x) {
+                        const uint8_t c = q[a + x];
+                        ok &= c < 4;
+                        code = (code << 2) | (c & 3u);
+                    }
+                    qe = seedc::pack_ext(q + a + KI, n < KX ? n : KX);
+                }
                 if (ok) {
                     code_a = (int32_t)code;
                     ca = (int)(V.koff[code + 1] - V.koff[code]);
@@ -126,6 +174,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
     if (nh > S.cap_hits) err = seedc::SC_OVER_HITS;
     wave_sync_lds();
     __threadfence_block();
+    OCC_TICK(0);
     if (!err) {
         const int amax = len - KI;   // last start with a 12-mer
         // OCC_U hits per lane per pass, their dependent load chains (start lookup -> code ->
@@ -232,6 +281,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
         }
         __threadfence_block();
         wave_sync_lds();
+        OCC_TICK(1);
         // the count table, a lane per start: ge[a][t] = #{hits of a with ml - KI >= t} summed
         // directly in registers (no zeroing, no atomics, no suffix pass over HBM)
         // and R_1 .. R_RK(a), the ends of the start's longest matches with >= k occurrences
@@ -240,24 +290,41 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
         const seedc::Occ occ{&V, &S, q, len, lc};
         for (int a = lane; a < len; a += 64) {
             uint32_t g[HB];
+            uint16_t top[seedc::RK];   // (fill_rk's top list, from the same pass over the hits)
 #pragma unroll
             for (int t = 0; t < HB; ++t) g[t] = 0u;
-            const bool has = a + KI <= len && S.codes[a] >= 0;
-            if (has) {
-                for (int h = ho[a]; h < ho[a + 1]; ++h) {
-                    const int d = (int)S.hml[h] - KI;
 #pragma unroll
-                    for (int t = 0; t < HB; ++t) g[t] += d >= t ? 1u : 0u;
+            for (int k = 0; k < seedc::RK; ++k) top[k] = 0;
+            const bool has = a + KI <= len && S.codes[a] >= 0;
+            const bool ranked = has && q[a] < 4;
+            if (has) {
+                // the match lengths 4 at a time (one 8-byte load; the slice's hml array has room past
+                // its last hit): the count row and the top list in one pass
+                const int h0 = ho[a], h1 = ho[a + 1];
+                for (int h = h0; h < h1; h += 4) {
+                    uint64_t w4;
+                    __builtin_memcpy(&w4, S.hml + h, 8);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        if (h + j >= h1) break;
+                        const uint16_t ml = (uint16_t)(w4 >> (16 * j));
+                        const int d = (int)ml - KI;
+#pragma unroll
+                        for (int t = 0; t < HB; ++t) g[t] += d >= t ? 1u : 0u;
+                        if (ranked) seedc::topk_insert(top, ml);
+                    }
                 }
             }
             uint32_t *dst = S.ge + (int64_t)a * HB;
 #pragma unroll
             for (int t = 0; t < HB; ++t) dst[t] = g[t];
-            seedc::fill_rk(occ, S, q, len, a);
+            seedc::fill_rk_top(occ, S, q, len, a, top);
         }
         __threadfence_block();
     }
     wave_sync_lds();
+    OCC_TICK(2);
+#undef OCC_TICK
     return err;
 }
 
@@ -364,6 +431,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
     unsigned long long pt[2] = {0ULL, 0ULL};   // wave wall-clock: occurrence tables, lane work
     // per lane: SMEM pass, re-seeding, -y seeds + sort, chaining, mem_chain_flt, filter + output
     unsigned long long lt[6] = {0ULL, 0ULL, 0ULL, 0ULL, 0ULL, 0ULL};
+    unsigned long long ot[3] = {0ULL, 0ULL, 0ULL};   // occurrence table: starts, hits, count table
     for (;;) {
         int b0 = 0;
         if (lane == 0) b0 = atomicAdd(D.next, 64);
@@ -379,6 +447,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
                 atomicAdd(&D.prof[0], pt[0]);
                 atomicAdd(&D.prof[1], pt[1]);
                 for (int k = 0; k < 6; ++k) atomicAdd(&D.prof[4 + k], lt[k]);   // lane-summed
+                for (int k = 0; k < 3; ++k) atomicAdd(&D.prof[10 + k], ot[k]);
             }
             break;
         }
@@ -392,7 +461,8 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             seedc::Scratch S = seedc::carve(base + (int64_t)rd * D.stride, D.caps);
             int err = 0, nh = 0;
             if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
-            if (len > 0 && !err) err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt, &nh);
+            if (len > 0 && !err)
+                err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt, &nh, D.prof ? ot : nullptr);
             if (lane == rd) my_err = err, my_hits = nh;
         }
         const unsigned long long t1 = D.prof ? wall_clock64() : 0ULL;

@@ -208,6 +208,11 @@ def _phase_ms(L, ctx) -> dict:
     _abi.check(L.pr_seed_gpu_lane_ticks(ctx.h, lt.ctypes.data), "pr_seed_gpu_lane_ticks")
     out["pass1_lane_ms_summed"] = {k: round(float(v) / 1e5, 1) for k, v in
                                    zip(("smem_pass", "reseeding", "y_seeds_sort", "chaining", "chain_flt", "output"), lt)}
+    if hasattr(L, "pr_seed_gpu_occ_ticks"):   # (older builds of the library, PRGPU_LIB A/B runs)
+        ot = np.zeros(3, np.uint64)
+        L.pr_seed_gpu_occ_ticks.argtypes = [C.c_void_p, C.c_void_p]
+        _abi.check(L.pr_seed_gpu_occ_ticks(ctx.h, ot.ctypes.data), "pr_seed_gpu_occ_ticks")
+        out["occ_table_parts"] = {k: round(float(v) / 1e5, 1) for k, v in zip(("starts", "hits", "count_table"), ot)}
     p2 = C.c_double()
     _abi.check(L.pr_seed_gpu_pass2_ms(ctx.h, C.byref(p2)), "pr_seed_gpu_pass2_ms")
     out["pass2_wall_ms"] = round(p2.value, 1)
