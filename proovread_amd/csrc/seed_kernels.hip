@@ -107,9 +107,18 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
         }
         wave_sync_lds();
     }
+    // per-start side tables for the hit pass in the LDS area beyond the start offsets (reads of
+    // up to 170 bases: ho [L1] | code [L1] | qext [L1] u64 | koff of the code [L1] u64, L1 = len + 1
+    // rounded up to even); longer reads read S.codes / S.qext / koff from HBM
+    const int L1 = (len + 2) & ~1;
+    const bool side = 6 * L1 <= SEED_LMAX + 4;
+    int32_t *lcode = ho + L1;
+    uint64_t *lqext = reinterpret_cast<uint64_t *>(ho + 2 * L1);
+    uint64_t *lr0 = reinterpret_cast<uint64_t *>(ho + 4 * L1);
     for (int a0 = 0; a0 <= len; a0 += 64) {
         const int a = a0 + lane;
         int ca = 0;
+        uint64_t r0a = 0;
         if (a <= len) {
             int32_t code_a = -1;
             uint64_t qe = 0;
@@ -150,11 +159,17 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                 }
                 if (ok) {
                     code_a = (int32_t)code;
-                    ca = (int)(V.koff[code + 1] - V.koff[code]);
+                    r0a = V.koff[code];
+                    ca = (int)(V.koff[code + 1] - r0a);
                 }
             }
             S.codes[a] = code_a;
             S.qext[a] = qe;
+            if (side) {   // the hit pass's per-start inputs on chip
+                lcode[a] = code_a;
+                lqext[a] = qe;
+                lr0[a] = r0a;
+            }
         }
         int x = ca;
 #pragma unroll
@@ -181,6 +196,10 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
         // k-mer list -> position -> contig -> coordinates) interleaved: one chain's latency per
         // OCC_U hits instead of per hit
         constexpr int U = OCC_U;
+        // the start of a pass's first hit (wave-uniform, non-decreasing): each lane walks from it
+        // to the last start whose hits begin at or before its hit (a few steps over the LDS start
+        // offsets instead of a binary search over all of them)
+        int apos = 0;
         for (int k0 = lane; k0 < nh; k0 += 64 * U) {
             int aa[U];
             bool ok[U];
@@ -188,23 +207,27 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
             for (int u = 0; u < U; ++u) {
                 const int k = k0 + 64 * u;
                 ok[u] = k < nh;
-                int lo = 0, hi = amax;   // last start whose hits begin at or before k
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (ho[mid] <= k) lo = mid; else hi = mid - 1;
-                }
-                aa[u] = lo;
+                int a = apos;
+                if (ok[u])
+                    while (a < amax && ho[a + 1] <= k) ++a;
+                aa[u] = a;
             }
+            apos = __shfl(aa[U - 1], 63, 64);   // (the pass's last hit, or a start before nh's)
             uint32_t code[U];
-            uint64_t qe[U];
+            uint64_t qe[U], r[U], p[U], exb[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                code[u] = ok[u] ? (uint32_t)S.codes[aa[u]] : 0u;
-                qe[u] = ok[u] ? S.qext[aa[u]] : 0ull;
+                const int a = aa[u], k = k0 + 64 * u;
+                if (side) {
+                    code[u] = ok[u] ? (uint32_t)lcode[a] : 0u;
+                    qe[u] = ok[u] ? lqext[a] : 0ull;
+                    r[u] = ok[u] ? lr0[a] + (uint64_t)(k - ho[a]) : 0ull;
+                } else {
+                    code[u] = ok[u] ? (uint32_t)S.codes[a] : 0u;
+                    qe[u] = ok[u] ? S.qext[a] : 0ull;
+                    r[u] = V.koff[code[u]] + (uint64_t)(k - ho[a]);
+                }
             }
-            uint64_t r[U], p[U], exb[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) r[u] = V.koff[code[u]] + (uint64_t)(k0 + 64 * u - ho[aa[u]]);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 p[u] = ok[u] ? seedc::hit_pos(V, code[u], r[u]) : 0ull;
@@ -331,7 +354,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
 // Pass 2: one wave per read with the large scratch slice (the reads of D.rlist: those that
 // outgrew pass 1's slices), the sequential part on lane 0.
 __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(SeedDev D) {
-    __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
+    __shared__ __attribute__((aligned(16))) int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint64_t q4_lds[SEED_WAVES][SEED_LMAX / 16 + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
     load_lcnt(D.V, lcnt);
@@ -419,7 +442,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
 // (D.caps sized for the batch's read lengths); a read that outgrows its slice is flagged and
 // goes to pass 2.
 __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(SeedDev D) {
-    __shared__ int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
+    __shared__ __attribute__((aligned(16))) int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint64_t q4_lds[SEED_WAVES][SEED_LMAX / 16 + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
     load_lcnt(D.V, lcnt);
