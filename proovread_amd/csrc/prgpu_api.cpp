@@ -189,7 +189,7 @@ enum SeedBufId {
     SI_TEXT, SI_CSTART, SI_CBLK, SI_LROFF, SI_KOFF, SI_KPOS, SI_KEXT, SI_CNT0,
     SB_SEQ = SI_CNT0 + 11, SB_OFF, SB_SCRATCH, SB_OUT, SB_NOUT, SB_STATUS, SB_NEXT, SB_PRE, SB_DENSE,
     SX_LRSEQ, SX_KEY0, SX_KEY1, SX_VAL0, SX_KC, SX_CNTPTR, SX_TEMP, SI_KSPLIT, SX_VAL1, SX_KCC, SX_KOFFC, SX_KCUR,
-    SB_DP, SI_TEXT4, SB_ORDER, SD_COUNT
+    SB_DP, SI_TEXT4, SB_ORDER, SI_BLKFR, SD_COUNT
 };
 // the exact-parity layout's exchange (pr_aln_exchange, owned batches): bounds, sort keys and
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
@@ -1850,6 +1850,40 @@ static int seed_text4(pr_ctx *c, seedc::IndexView &v, hipStream_t s) {
     return 0;
 }
 
+// Per 2^CB_SHIFT text block: the contig at its start, the next two contig starts inside it and
+// the coordinate offsets of those contigs (fr = p + delta, seed_core.h text_to_fr), so the
+// seeding's hit pass computes a hit's bwa coordinate with one table load instead of the cblk ->
+// cstart -> lr_off chain.  cstart / off: host arrays of the index (off rebased to 0).
+static int upload_blk_fr(pr_ctx *c, seedc::IndexView &v, const int64_t *cstart, const int64_t *off, int n_lr,
+                         int64_t l_pac, int64_t n_text, hipStream_t s) {
+    const int64_t nb = (n_text >> seedc::CB_SHIFT) + 1;
+    const int nc = 2 * n_lr;
+    const int bs = 1 << seedc::CB_SHIFT;
+    auto delta = [&](int ci) -> int64_t {
+        if (ci < n_lr) return off[ci] - cstart[ci];
+        const int rid = 2 * n_lr - 1 - ci;   // the reverse half holds the long reads in reverse order
+        return 2 * l_pac - off[rid + 1] - cstart[ci];
+    };
+    std::vector<seedc::BlkFr> t((size_t)nb);
+    int ci = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+        const int64_t b0 = b << seedc::CB_SHIFT, b1 = b0 + bs;
+        while (ci + 1 < nc && cstart[ci + 1] <= b0) ++ci;
+        seedc::BlkFr &e = t[(size_t)b];
+        e.c0 = ci;
+        e.d0 = nc ? delta(ci) : 0;
+        e.d1 = ci + 1 < nc ? delta(ci + 1) : 0;
+        e.bnd = ci + 1 < nc && cstart[ci + 1] < b1 ? (int32_t)(cstart[ci + 1] - b0) : bs;
+        e.bnd2 = ci + 2 < nc && cstart[ci + 2] < b1 ? (int32_t)(cstart[ci + 2] - b0) : bs;
+    }
+    int rc = c->sd[SI_BLKFR].ensure(t.size() * sizeof(seedc::BlkFr));
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(c->sd[SI_BLKFR].p, t.data(), t.size() * sizeof(seedc::BlkFr), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));   // (t is a host temporary)
+    v.blkfr = c->sd[SI_BLKFR].as<seedc::BlkFr>();
+    return 0;
+}
+
 extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
     if (!c || !h) return set_error(PR_ERR_ARG, "null arg");
     HIPCHK(hipSetDevice(c->device));
@@ -1878,6 +1912,7 @@ extern "C" int pr_seed_gpu_upload(pr_ctx *c, const pr_seed_index *h) {
     v.kext = D[SI_KEXT].as<uint64_t>();
     v.ksplit = z.ksplit ? D[SI_KSPLIT].as<uint64_t>() : nullptr;
     if ((rc = seed_text4(c, v, s))) return rc;
+    if ((rc = upload_blk_fr(c, v, hv.cstart, hv.lr_off, hv.n_lr, hv.l_pac, hv.n_text, s))) return rc;
     HIPCHK(hipStreamSynchronize(s));
     c->seed_view = v;
     c->seed_loaded = true;
@@ -2008,6 +2043,7 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
     v.ksplit = B.ksplit;
     for (int j = 0; j < seedc::KI - 1; ++j) v.cnt[j] = B.cnt[j];
     if ((rc = seed_text4(c, v, s))) return rc;
+    if ((rc = upload_blk_fr(c, v, cstart.data(), off.data(), n_lr, l_pac, n_text, s))) return rc;
     c->seed_view = v;
     c->seed_loaded = true;
     c->seed_n_text = n_text;

@@ -66,6 +66,14 @@ constexpr int RK = 11;                        // R_k tabulated per start for k <
 constexpr uint64_t POS_PAGE = 1ull << 32;
 constexpr int64_t MAX_TEXT = (int64_t)1 << 33;
 
+// Per 2^CB_SHIFT text block (device index only): the contig at the block's start (c0), the
+// offsets in the block where contigs c0 + 1 and c0 + 2 start (2^CB_SHIFT: none), and the
+// coordinate offsets of c0 and c0 + 1 (fr = text position + d): text_to_fr in one load.
+struct BlkFr {
+    int64_t d0, d1;
+    int32_t c0, bnd, bnd2, pad;
+};
+
 // Device- or host-resident index, plain pointers (built by seed.cpp).
 struct IndexView {
     const uint8_t *text;       // forward long reads, then rc of their concatenation, SEP (5) after each
@@ -82,6 +90,7 @@ struct IndexView {
     const uint64_t *kext;      // per hit: KX bases after it (2 bits each) | count << 56
     const uint32_t *cnt[KI - 1];   // cnt[j-1][code]: occurrences of the j-mer `code`, j = 1..11
     const uint64_t *text4;     // device: the text 16 bases per word (4 bits each) + a padding word, or null
+    const BlkFr *blkfr;        // device: [n_text >> CB_SHIFT + 1] block coordinate table, or null
 };
 
 struct Iv {

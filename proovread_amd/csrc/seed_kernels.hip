@@ -233,24 +233,35 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                 p[u] = ok[u] ? seedc::hit_pos(V, code[u], r[u]) : 0ull;
                 exb[u] = ok[u] ? V.kext[r[u]] : 0ull;
             }
-            // the contigs (seed_core.h contig_of) and bwa coordinates (pack_fr), interleaved
+            // the contigs (seed_core.h contig_of) and bwa coordinates (pack_fr): from the block
+            // table when the hit's block has at most two contig starts after its first contig,
+            // else the cblk -> cstart walk; interleaved over the pass's hits
             int c[U];
-            int64_t nx[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) c[u] = V.cblk[p[u] >> seedc::CB_SHIFT];
-#pragma unroll
-            for (int u = 0; u < U; ++u) nx[u] = c[u] + 1 < V.n_contig ? V.cstart[c[u] + 1] : INT64_MAX;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                while (nx[u] <= (int64_t)p[u]) {
-                    ++c[u];
-                    nx[u] = c[u] + 1 < V.n_contig ? V.cstart[c[u] + 1] : INT64_MAX;
-                }
-            int64_t cst[U], lro[U];
+            int64_t dlt[U];
+            bool walk[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                cst[u] = V.cstart[c[u]];
-                lro[u] = c[u] < V.n_lr ? V.lr_off[c[u]] : V.lr_off[2 * V.n_lr - c[u]];
+                walk[u] = true;
+                if (V.blkfr && ok[u]) {
+                    const seedc::BlkFr bt = V.blkfr[p[u] >> seedc::CB_SHIFT];
+                    const int o = (int)(p[u] & ((1u << seedc::CB_SHIFT) - 1u));
+                    if (o < bt.bnd) { c[u] = bt.c0; dlt[u] = bt.d0; walk[u] = false; }
+                    else if (o < bt.bnd2) { c[u] = bt.c0 + 1; dlt[u] = bt.d1; walk[u] = false; }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!walk[u]) continue;
+                int cc = V.cblk[p[u] >> seedc::CB_SHIFT];
+                int64_t nx = cc + 1 < V.n_contig ? V.cstart[cc + 1] : INT64_MAX;
+                while (nx <= (int64_t)p[u]) {
+                    ++cc;
+                    nx = cc + 1 < V.n_contig ? V.cstart[cc + 1] : INT64_MAX;
+                }
+                c[u] = cc;
+                const int64_t cst = V.cstart[cc];
+                const int64_t lro = cc < V.n_lr ? V.lr_off[cc] : V.lr_off[2 * V.n_lr - cc];
+                dlt[u] = cc < V.n_lr ? lro - cst : 2 * V.l_pac - lro - cst;
             }
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -287,17 +298,11 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                     }
                 }
                 seedc::set_hpos(S, k, p[u]);
-                // pack_fr: the hit's forward-reverse coordinate and long read (text_to_fr)
-                const int64_t o = (int64_t)p[u] - cst[u];
-                int64_t fr;
-                int rid;
-                if (c[u] < V.n_lr) {
-                    rid = c[u];
-                    fr = lro[u] + o;
-                } else {
-                    rid = 2 * V.n_lr - 1 - c[u];   // the reverse half holds the long reads in reverse order
-                    fr = V.l_pac + (V.l_pac - lro[u]) + o;
-                }
+                // pack_fr: the hit's forward-reverse coordinate and long read (text_to_fr: fr =
+                // lr_off[c] + (p - cstart[c]) forward, l_pac + (l_pac - lr_off[rid + 1]) +
+                // (p - cstart[c]) reverse, both p + dlt)
+                const int64_t fr = (int64_t)p[u] + dlt[u];
+                const int rid = c[u] < V.n_lr ? c[u] : 2 * V.n_lr - 1 - c[u];   // (reverse half: reads in reverse order)
                 S.hfr[k] = ((uint64_t)fr << seedc::FR_RID_BITS) | (uint64_t)rid;
                 S.hml[k] = (uint16_t)(ml < 65535 ? ml : 65535);
             }
