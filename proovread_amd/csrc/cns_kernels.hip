@@ -409,7 +409,10 @@ constexpr uint32_t SLOT_MASK = (1u << SLOT_SH) - 1u;
 #endif
 constexpr int CNS_GW = CNS_GW_DEF;   // lanes per kept alignment in the pileup (16: four per wave)
 constexpr int CNS_NG = 64 / CNS_GW;  // alignments per wave
-constexpr int CNS_OPF = CNS_GW == 16 ? 3 : 2;                 // CIGAR ops per lane loaded ahead (48 / 64 ops)
+#ifndef CNS_OPF_DEF
+#define CNS_OPF_DEF 3
+#endif
+constexpr int CNS_OPF = CNS_GW == 16 ? CNS_OPF_DEF : 2;       // CIGAR ops per lane loaded ahead (16 x CNS_OPF_DEF / 64 ops)
 constexpr int CNS_SEQ_DW = CNS_GW == 16 ? 40 : 64;            // SEQ dwords a group keeps in LDS (160 / 256 bytes)
 constexpr int CNS_SEQ_PL = (CNS_SEQ_DW + CNS_GW - 1) / CNS_GW; // of them per lane
 
