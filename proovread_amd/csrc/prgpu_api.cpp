@@ -1956,9 +1956,19 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
         }
     }
     const size_t nt = (size_t)(n_text > 0 ? n_text : 1);
-    // sorts of up to 2^30 text positions (a divisor of 2^32; PRGPU_INDEX_CHUNK=k: 2^k, a test
-    // hook that sends small texts through the chunked build)
+    // sorts of up to 2^31 text positions when the device has room for their buffers (~16 bytes a
+    // position + rocPRIM's temporaries: configs[2]'s 2.1 G-position text in one sort, 293 -> 151
+    // ms), else 2^30 (a divisor of 2^32 either way; PRGPU_INDEX_CHUNK=k: 2^k, a test hook that
+    // sends small texts through the chunked build)
     int64_t chunk = (int64_t)1 << 30;
+    if (n_text > chunk) {
+        size_t fr = 0, tot = 0;
+        (void)hipMemGetInfo(&fr, &tot);
+        (void)hipGetLastError();
+        const int64_t have = (int64_t)(D[SX_KEY0].cap + D[SX_KEY1].cap + D[SX_VAL0].cap + D[SX_VAL1].cap + D[SX_TEMP].cap);
+        // (room for the bigger sort buffers with 64 GB to spare for the rest of the task)
+        if ((int64_t)fr + have >= ((int64_t)1 << 31) * 20 + ((int64_t)64 << 30)) chunk = (int64_t)1 << 31;
+    }
     if (const char *ch = getenv("PRGPU_INDEX_CHUNK")) {
         const int k = atoi(ch);
         if (k >= 16 && k <= 31) chunk = (int64_t)1 << k;
@@ -2022,10 +2032,11 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
     HIPCHK(hipStreamSynchronize(s));
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, c->ev[8], c->ev[9]) == hipSuccess) c->ms_index = ms;
-    if (chunked) {
-        // a chunked build (texts beyond 2^30 positions: configs[2] / configs[3] ranks) gives its
-        // sort buffers back (~4 x 4 GB + rocPRIM's temporaries): at configs[3] a rank's device
-        // memory peaks near the card's 288 GiB later in the task (DESIGN.md current status)
+    if (n_text > (int64_t)seedc::POS_PAGE) {
+        // a build beyond 2^32 positions (configs[3] ranks) gives its sort buffers back (4 x 4-8 GB +
+        // rocPRIM's temporaries): there a rank's device memory peaks near the card's 288 GiB later
+        // in the task (DESIGN.md current status); smaller texts keep them for the next task's
+        // build (no re-allocation inside a timed step)
         for (int id : {(int)SX_KEY0, (int)SX_KEY1, (int)SX_VAL0, (int)SX_VAL1, (int)SX_TEMP}) D[id].release();
     }
     seedc::IndexView v{};
