@@ -592,6 +592,15 @@ int pr_iter_mask(pr_ctx *ctx, const pr_mask_params *p, int64_t *dev_stats);
 int pr_iter_mask_download(pr_ctx *ctx, uint8_t *masked);
 
 /* ------------------------------------------------------------------ */
+/* short-read input (bin/proovread:1293, the short-read files as one stream): a FASTQ stream of
+   plain 4-line records ('@' first, '\n' last, no '\r', QUAL as long as SEQ) scanned natively;
+   PR_ERR_ARG for anything else (the caller's record parser takes FASTA / multi-line input).
+   scan: the record and base counts; fill: every record's start offset [n_rec], the sequence
+   offsets [n_rec + 1] and the bases through table256 (e.g. ASCII -> nt4) [n_bases] */
+int pr_fastq4_scan(const uint8_t *data, int64_t n, int64_t *n_rec, int64_t *n_bases);
+int pr_fastq4_fill(const uint8_t *data, int64_t n, const uint8_t *table256, int64_t *starts, int64_t *off,
+                   uint8_t *pool);
+
 /* final quality trimming: the windows `SeqFilter --trim-win mean,min` keeps
  * (proovread.cfg:152-155; bin/proovread:919-943), i.e. Fastq::Seq::qual_window
  * (lib/Fastq/Seq.pm:1064-1160).  Host code (once per job), threads over reads. */

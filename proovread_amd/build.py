@@ -15,7 +15,7 @@ SRC = PKG / "csrc"
 OBJ = PKG.parent / "build" / "obj"
 OUT = PKG / "libprgpu.so"
 SOURCES = ["cns_kernels.hip", "sw_kernels.hip", "pipe_kernels.hip", "xchg_kernels.hip", "mask_kernels.hip", "seed_kernels.hip", "seed_index.hip", "aln_kernels.hip",
-           "sw_api.cpp", "prgpu_api.cpp", "comm.cpp", "seed.cpp", "trim.cpp", "bam_codec.cpp"]
+           "sw_api.cpp", "prgpu_api.cpp", "comm.cpp", "seed.cpp", "trim.cpp", "bam_codec.cpp", "fastq.cpp"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-pthread",
          # exact IEEE double semantics of the reference Perl arithmetic
          "-ffp-contract=off", "-fno-fast-math",

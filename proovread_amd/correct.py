@@ -177,10 +177,9 @@ class ShortReads:
     def __init__(self, data: bytes, chunk_number: int = 1000):
         self.data = data
         total = len(data)
-        arr = np.frombuffer(data, np.uint8)
-        rec = _fastq4_records(arr)
-        if rec is not None:   # plain 4-line FASTQ: record starts and sequence lines by numpy
-            starts, s0, s1 = rec
+        rec = _fastq4_native(data)
+        if rec is not None:   # plain 4-line FASTQ: record starts, offsets and nt4 pool in one native pass
+            starts, self.off, self.pool = rec
         else:                 # FASTA (multi-line) or irregular FASTQ: the record parser
             spans = list(seqchunker.records(data))
             starts = np.array([x for x, _ in spans], np.int64)
@@ -190,18 +189,7 @@ class ShortReads:
         chunk_of = np.minimum(starts // csize, self.n_chunks - 1) if len(starts) else np.zeros(0, np.int64)
         # records of chunk k (1-based): [cfirst[k-1], cfirst[k])
         self.cfirst = np.searchsorted(chunk_of, np.arange(self.n_chunks + 1), side="left").astype(np.int64)
-        if rec is not None:
-            lens = s1 - s0
-            self.off = np.zeros(len(lens) + 1, np.int64)
-            np.cumsum(lens, out=self.off[1:])
-            # the sequence lines' bytes by a byte mask (+1 at each line start, -1 at its end,
-            # running sum > 0): ~3 bytes per input byte instead of an int64 index per base
-            d = np.zeros(len(arr) + 1, np.int8)
-            d[s0] = 1
-            d[s1] -= 1
-            self.pool = NT4[arr[np.cumsum(d[:-1], dtype=np.int8) > 0]]
-            del d
-        else:
+        if rec is None:
             self.pool, self.off = _pool(seqs)
             self.pool = NT4[self.pool]
         self.lengths = np.diff(self.off)
@@ -240,22 +228,26 @@ class ShortReads:
         return self.gather(rg), off
 
 
-def _fastq4_records(arr: np.ndarray):
-    """(record starts, sequence-line starts, sequence-line ends) of a FASTQ stream of plain
-    4-line records (no blank lines, no CR), or None."""
-    if len(arr) == 0 or arr[0] != ord("@") or arr[-1] != 10:
+def _fastq4_native(data: bytes):
+    """(record starts, sequence offsets, nt4 pool) of a FASTQ stream of plain 4-line records
+    (pr_fastq4_scan / pr_fastq4_fill: '@' first, '\n' last, no CR, quality lines as long as the
+    sequences), or None for anything else."""
+    import ctypes as C
+    from . import _abi
+    if not data:
         return None
-    nl = np.flatnonzero(arr == 10)
-    if len(nl) % 4 or (arr == 13).any():
+    L = _abi.lib()
+    L.pr_fastq4_scan.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+    L.pr_fastq4_fill.argtypes = [C.c_char_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    n_rec, n_bases = C.c_int64(), C.c_int64()
+    if L.pr_fastq4_scan(data, len(data), C.byref(n_rec), C.byref(n_bases)) != 0:
         return None
-    starts = np.concatenate([[0], nl[3::4][:-1] + 1]).astype(np.int64)
-    if not (arr[starts] == ord("@")).all() or not (arr[nl[1::4] + 1] == ord("+")).all():
-        return None
-    s0 = (nl[0::4] + 1).astype(np.int64)
-    s1 = nl[1::4].astype(np.int64)
-    if not ((nl[3::4] - nl[2::4]) == (s1 - s0) + 1).all():   # quality lines as long as the sequences
-        return None
-    return starts, s0, s1
+    starts = np.zeros(n_rec.value, np.int64)
+    off = np.zeros(n_rec.value + 1, np.int64)
+    pool = np.zeros(n_bases.value, np.uint8)
+    _abi.check(L.pr_fastq4_fill(data, len(data), NT4.ctypes.data, starts.ctypes.data, off.ctypes.data, pool.ctypes.data),
+               "pr_fastq4_fill")
+    return starts, off, pool
 
 
 # ---------------------------------------------------------------------------- device stages
