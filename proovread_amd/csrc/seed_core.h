@@ -819,6 +819,9 @@ SC_HD int seed_sw_score(const IndexView &I, const pr_seed_opts &O, const uint8_t
     return best;
 }
 
+SC_HD void chain_flt(const pr_seed_opts &O, Scratch &S, int ncv, int *n_chains);
+SC_HD int chain_seq(const IndexView &I, const pr_seed_opts &O, Scratch &S, int nm, int *n_cv);
+
 // Everything after the occurrence table (S.hoff / hpos / hml / ge of the read, built by
 // build_occ or by the device's wave-parallel equivalent): SMEMs, chaining, the chain
 // filter and the tasks into out[0, *n_out) (chain order after mem_chain_flt).
@@ -840,7 +843,20 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
 #if defined(__HIP_DEVICE_COMPILE__)
     if (ticks) t_last = __builtin_amdgcn_s_memrealtime();
 #endif
-    // mem_chain
+    int ncv = 0;
+    err = chain_seq(I, O, S, nm, &ncv);
+    if (err) return err;
+    SC_TICK(3);
+    SC_STAT(11, ncv);
+    SC_STAT(12, (unsigned long long)ncv * ncv);
+    chain_flt(O, S, ncv, n_chains);
+    SC_TICK(4);
+    return 0;
+}
+
+// mem_chain over the SMEMs S.mems[0, nm) -> the chains S.cv[0, *n_cv) in creation order
+// (one thread); 0 or SC_OVER_SEEDS / SC_OVER_CHAINS
+SC_HD int chain_seq(const IndexView &I, const pr_seed_opts &O, Scratch &S, int nm, int *n_cv) {
     int32_t ns = 0, ncv = 0, nrg = 0;
     for (int k = 0; k < S.hsize; ++k) S.htab[k].key = -1;
     for (int mi = 0; mi < nm; ++mi) {
@@ -974,11 +990,14 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
         }
     }
     for (int r = 0; r < nrg; ++r) flush_tail(S, S.rg[r]);
-    SC_TICK(3);
-    SC_STAT(11, ncv);
-    SC_STAT(12, (unsigned long long)ncv * ncv);
-    // mem_chain_flt: the weight filter, then bwa's stable sort by weight (descending) of the
-    // pos-ordered chains = a sort by (weight desc, pos, creation order = first seed's index)
+    *n_cv = ncv;
+    return 0;
+}
+
+// mem_chain_flt over the chains S.cv[0, ncv) in creation order -> S.ch[0, *n_chains) with their
+// kept flags: the weight filter, then bwa's stable sort by weight (descending) of the
+// pos-ordered chains = a sort by (weight desc, pos, creation order = first seed's index)
+SC_HD void chain_flt(const pr_seed_opts &O, Scratch &S, int ncv, int *n_chains) {
     int nch = 0;
     for (int j = 0; j < ncv; ++j) {
         Chain c = S.cv[j];
@@ -1029,8 +1048,6 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
             if (S.ch[S.kept[k]].first >= 0) S.ch[S.ch[S.kept[k]].first].kept = 1;
     }
     *n_chains = nch;
-    SC_TICK(4);
-    return 0;
 }
 
 // The seeds whose mem_flt_chained_seeds score part 2 needs (every seed of every kept chain,

@@ -356,6 +356,197 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
     return err;
 }
 
+// mem_chain of one read by the whole wave (pass 2's reads: their thousands of occurrences chained
+// on one lane were pass 2's wall time).  Chains of different (long read, strand) ranges never
+// interact (seed_core.h chain_seq), so the ranges are dealt to lanes by a hash of their key and
+// every lane chains its ranges' occurrences in the sequential order.  A seed's slot, and a new
+// chain's, is the occurrence's place in that order: creation order -- the chain sort's last
+// tie-break -- is the sequential one and no slot counter is shared.  -> the number of chains,
+// compacted into S.cv[0, n) in creation order, or -1 when the occurrences do not fit the slice
+// (the caller then chains on one lane).  lds: 66 ints of the wave's LDS.
+__device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seedc::Scratch &S, int nm, int lane,
+                          int32_t *lds) {
+    using namespace seedc;
+    // 1. the selected occurrences in chaining order (chain_seq's selection), on lane 0: (hit, SMEM)
+    int2 *ol = reinterpret_cast<int2 *>(S.ge);   // (the count table is dead after the SMEMs)
+    const int cap_ge = (int)((int64_t)S.lmax * HB * 4 / 12);   // 8 bytes an entry + a 4-byte list index
+    const int cap = cap_ge < S.cap_seeds ? (cap_ge < S.cap_chains ? cap_ge : S.cap_chains)
+                                         : (S.cap_seeds < S.cap_chains ? S.cap_seeds : S.cap_chains);
+    int n = 0;
+    if (lane == 0) {
+        for (int mi = 0; mi < nm && n >= 0; ++mi) {
+            const Iv p = S.mems[mi];
+            const int slen = p.end - p.start;
+            const int32_t h0 = S.hoff[p.start], h1 = S.hoff[p.start + 1];
+            const int64_t step = p.occ > O.max_occ ? p.occ / O.max_occ : 1;
+            int64_t fidx = 0, take = 0, count = 0;
+            for (int32_t k = h0; k < h1 && count < O.max_occ; ++k) {
+                if (S.hml[k] < slen) continue;   // text-position order: the 12-mer lists are sorted
+                const bool use = fidx == take;
+                ++fidx;
+                if (!use) continue;
+                take += step;
+                ++count;
+                if (n >= cap) { n = -1; break; }
+                ol[n++] = make_int2(k, mi);
+            }
+        }
+    }
+    n = __shfl(n, 0, 64);
+    if (n < 0) return -1;
+    int32_t *idx = reinterpret_cast<int32_t *>(ol + n);   // the lanes' lists of occurrence indices
+    int32_t *cnt = lds, *cur = lds + 64;                 // per-lane counts / cursors (LDS)
+    cnt[lane] = 0;
+    for (int e = lane; e < n; e += 64) S.cv[e].n = 0;   // (chain slots: n > 0 marks a chain)
+    for (int k = lane; k < S.hsize; k += 64) S.htab[k].key = -1;
+    if (lane == 0) lds[128] = 0;                          // ranges so far
+    __threadfence_block();
+    wave_sync_lds();
+    auto owner_of = [&](int e) -> int {
+        const uint64_t v = S.hfr[ol[e].x];
+        const int rid = (int)(v & ((1u << FR_RID_BITS) - 1u));
+        const int key = rid * 2 + ((int64_t)(v >> FR_RID_BITS) >= I.l_pac ? 1 : 0);
+        return (int)(((uint32_t)key * 0x9E3779B1u) >> 26);
+    };
+    // 2. every lane's share, 64 occurrences at a time: same-owner lanes by 6 ballots, ranks in
+    // occurrence order; counts, then the stable scatter into the lanes' lists
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1) {   // list starts: exclusive prefix of the counts over lanes
+            int x = cnt[lane];
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int y = __shfl_up(x, d, 64);
+                if (lane >= d) x += y;
+            }
+            cur[lane] = x - cnt[lane];
+            wave_sync_lds();
+        }
+        for (int e0 = 0; e0 < n; e0 += 64) {
+            const int e = e0 + lane;
+            const int own = e < n ? owner_of(e) : 64;
+            unsigned long long m = __ballot(e < n);
+#pragma unroll
+            for (int b = 0; b < 7; ++b) {
+                const bool bit = (own >> b) & 1;
+                const unsigned long long w = __ballot(bit);
+                m &= bit ? w : ~w;
+            }
+            const int rank = __popcll(m & below);
+            const bool leader = e < n && rank == 0;
+            if (pass == 0) {
+                if (leader) atomicAdd(&cnt[own], __popcll(m));
+            } else {
+                if (e < n) idx[cur[own] + rank] = e;
+                wave_sync_lds();
+                if (leader) cur[own] += __popcll(m);
+            }
+            wave_sync_lds();
+        }
+        wave_sync_lds();
+    }
+    __threadfence_block();
+    wave_sync_lds();
+    // 3. each lane chains its occurrences in order (chain_seq's decisions; slots = occurrence index)
+    const int mine = cnt[lane], first = cur[lane] - mine;
+    for (int t = 0; t < mine; ++t) {
+        const int e = idx[first + t];
+        const int2 oe = ol[e];
+        const Iv p = S.mems[oe.y];
+        const uint64_t v = S.hfr[oe.x];
+        Seed sd;
+        sd.rbeg = (int64_t)(v >> FR_RID_BITS);
+        sd.qbeg = (int16_t)p.start;
+        sd.len = (int16_t)(p.end - p.start);
+        sd.nx = -1;
+        const int rid = (int)(v & ((1u << FR_RID_BITS) - 1u));
+        const int32_t key = rid * 2 + (sd.rbeg >= I.l_pac ? 1 : 0);
+        // the range: probe, claiming a free entry with a CAS (other lanes' keys may share a probe run)
+        uint32_t h = ((uint32_t)key * 0x9E3779B1u) & (uint32_t)(S.hsize - 1);
+        bool found = false;
+        for (;;) {
+            const int32_t kk = S.htab[h].key;
+            if (kk == key) { found = true; break; }
+            if (kk == -1) {
+                const int32_t old = atomicCAS(&S.htab[h].key, -1, key);
+                if (old == -1) break;   // claimed: a new range
+                if (old == key) { found = true; break; }
+            }
+            h = (h + 1) & (uint32_t)(S.hsize - 1);
+        }
+        int at = -1;
+        bool at_tail = false;
+        int32_t ns = e;
+        if (found) {
+            RangeRec &R = S.rg[S.htab[h].r];
+            if (R.tpos <= sd.rbeg) {
+                at = R.tail;
+                at_tail = true;
+            } else {
+                for (int x = R.head; x >= 0 && S.cv[x].pos <= sd.rbeg; x = S.cnx[x]) at = x;
+            }
+            if (at >= 0) {
+                const int r = at_tail ? merge_tail(O, I.l_pac, S, ns, R, sd)
+                                      : test_and_merge(O, I.l_pac, S, ns, S.cv[at], sd, rid);
+                if (r) continue;   // merged or contained (slots < the capacities: r >= 0)
+            }
+        }
+        S.seeds[e] = sd;
+        Chain c;
+        c.pos = sd.rbeg;
+        c.rid = rid;
+        c.head = c.tail = e;
+        c.n = 1;
+        c.w = c.kept = 0;
+        c.first = -1;
+        S.cv[e] = c;
+        if (!found) {
+            const int r = atomicAdd(&lds[128], 1);
+            RangeRec &R = S.rg[r];
+            R.head = R.tail = e;
+            R.n = 1;
+            R.l_idx = e;
+            R.tpos = sd.rbeg;
+            R.f_rbeg = R.l_rbeg = sd.rbeg;
+            R.f_ql = R.l_ql = pack_ql(sd);
+            S.htab[h].r = r;
+            S.cnx[e] = -1;
+        } else {
+            RangeRec &R = S.rg[S.htab[h].r];
+            if (at < 0) {
+                S.cnx[e] = R.head;
+                R.head = e;
+            } else {
+                const int nx = S.cnx[at];
+                S.cnx[e] = nx;
+                S.cnx[at] = e;
+                if (nx < 0) {
+                    flush_tail(S, R);
+                    R.tail = e;
+                    R.n = 1;
+                    R.l_idx = e;
+                    R.tpos = sd.rbeg;
+                    R.f_rbeg = R.l_rbeg = sd.rbeg;
+                    R.f_ql = R.l_ql = pack_ql(sd);
+                }
+            }
+        }
+    }
+    __threadfence_block();
+    wave_sync_lds();
+    const int nrg = lds[128];
+    for (int r = lane; r < nrg; r += 64) flush_tail(S, S.rg[r]);
+    __threadfence_block();
+    wave_sync_lds();
+    // 4. the chains in creation order (slot order), compacted on lane 0
+    int ncv = 0;
+    if (lane == 0)
+        for (int e = 0; e < n; ++e)
+            if (S.cv[e].n > 0) S.cv[ncv++] = S.cv[e];
+    __threadfence_block();
+    return __shfl(ncv, 0, 64);
+}
+
 // Pass 2: one wave per read with the large scratch slice (the reads of D.rlist: those that
 // outgrew pass 1's slices), the sequential part on lane 0.
 __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(SeedDev D) {
@@ -394,11 +585,28 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
         // SMEMs and chaining on lane 0; then, for reads where bwa runs mem_flt_chained_seeds
         // (>= 440 bp), the seeds' local SW scores over all 64 lanes (a seed per lane, the rows
         // int16 and lane-interleaved in the dead count table); the output on lane 0
-        int nch = 0, nlist = -1;
+        int nch = 0, nlist = -1, nm = 0;
         if (lane == 0) {
             if (D.prof) pt[0] += wall_clock64() - t0;
             if (len > 0 && !err) {
-                err = seedc::map_chains(D.V, D.O, S, q, len, &nch, D.prof ? pl : nullptr, lcnt);
+                const seedc::Occ occ{&D.V, &S, q, len, lcnt};
+                nm = seedc::collect_intv(occ, S, D.O, q, len, err, D.prof ? pl : nullptr);
+            }
+        }
+        err = __shfl(err, 0, 64);
+        nm = __shfl(nm, 0, 64);
+        if (len > 0 && !err) {
+            // chaining over the wave's lanes (by range), on lane 0 when the occurrences do not fit
+            const unsigned long long tc = D.prof && lane == 0 ? wall_clock64() : 0ULL;
+            __threadfence_block();
+            int ncv = chain_wave(D.V, D.O, S, nm, lane, ho);
+            if (lane == 0) {
+                if (ncv < 0) {
+                    ncv = 0;
+                    err = seedc::chain_seq(D.V, D.O, S, nm, &ncv);
+                }
+                if (!err) seedc::chain_flt(D.O, S, ncv, &nch);
+                if (D.prof) pl[3] += wall_clock64() - tc;
                 if (!err && seedc::seed_flt_min_score(D.O, len) >= 0 && 3 * S.cap_seeds <= 2 * S.cap_hits &&
                     2 * 201 * 64 * 2 <= 4 * S.lmax * seedc::HB)
                     nlist = seedc::flt_seed_list(S, nch, (int32_t *)S.hfr + S.cap_seeds, S.cap_seeds);

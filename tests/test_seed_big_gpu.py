@@ -15,6 +15,8 @@ seed, and seeds on A's reverse strand exist.  A second test sends a small text t
 chunked device build (PRGPU_INDEX_CHUNK) and checks its tables' digests against the host
 build's.  (bwa mode's seeding order depends on global occurrence counts, so equality with the
 host path over the whole index is the bar, not equality with a smaller index.)"""
+import os
+
 import numpy as np
 import pytest
 
@@ -81,10 +83,15 @@ def test_device_index_beyond_2_32_matches_host(finish):
     hx = seed.SeedIndex(seq, off)
     want_digest = hx.digest()
     hx.close()
-    ctx = _abi.default_context()
-    ix = seed.DeviceSeedIndex(ctx, seq, off)
-    assert ix.digest() == want_digest   # every table, ksplit included
-    got, st = ix.map(sr, sr_off, seed.default_opts(finish))
+    # a context of its own, destroyed at the end: a >2^32-position index holds
+    # ~100 GB that later tests in the same process need back
+    ctx = _abi.Context(int(os.environ.get("LOCAL_RANK", "-1")))
+    try:
+        ix = seed.DeviceSeedIndex(ctx, seq, off)
+        assert ix.digest() == want_digest   # every table, ksplit included
+        got, st = ix.map(sr, sr_off, seed.default_opts(finish))
+    finally:
+        ctx.close()
     assert (st == 0).all()
     assert len(want) > d.n_sr
     for f in ("sr", "lr", "strand", "qbeg", "rbeg", "slen", "rmax0", "rmax1", "chain", "rank"):
