@@ -367,32 +367,43 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
 __device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seedc::Scratch &S, int nm, int lane,
                           int32_t *lds) {
     using namespace seedc;
-    // 1. the selected occurrences in chaining order (chain_seq's selection), on lane 0: (hit, SMEM)
+    // 1. the selected occurrences in chaining order (chain_seq's selection) over the lanes: (hit, SMEM)
     int2 *ol = reinterpret_cast<int2 *>(S.ge);   // (the count table is dead after the SMEMs)
     const int cap_ge = (int)((int64_t)S.lmax * HB * 4 / 12);   // 8 bytes an entry + a 4-byte list index
-    const int cap = cap_ge < S.cap_seeds ? (cap_ge < S.cap_chains ? cap_ge : S.cap_chains)
-                                         : (S.cap_seeds < S.cap_chains ? S.cap_seeds : S.cap_chains);
+    // chain slots run on into S.ch and S.cnx into S.kept (carve: cv|ch and cnx|kept adjacent,
+    // both dead until the filter); more than cap_chains chains or ranges -> -2 (SC_OVER_CHAINS,
+    // as the sequential chaining flags them)
+    const int cap2 = 2 * S.cap_chains;
+    const int cap = cap_ge < S.cap_seeds ? (cap_ge < cap2 ? cap_ge : cap2) : (S.cap_seeds < cap2 ? S.cap_seeds : cap2);
+    // (the 64 hits of a step filtered by match length, then every step-th of them up to max_occ:
+    // ranks from ballots keep the sequential order)
+    const unsigned long long below = (1ull << lane) - 1ull;
     int n = 0;
-    if (lane == 0) {
-        for (int mi = 0; mi < nm && n >= 0; ++mi) {
-            const Iv p = S.mems[mi];
-            const int slen = p.end - p.start;
-            const int32_t h0 = S.hoff[p.start], h1 = S.hoff[p.start + 1];
-            const int64_t step = p.occ > O.max_occ ? p.occ / O.max_occ : 1;
-            int64_t fidx = 0, take = 0, count = 0;
-            for (int32_t k = h0; k < h1 && count < O.max_occ; ++k) {
-                if (S.hml[k] < slen) continue;   // text-position order: the 12-mer lists are sorted
-                const bool use = fidx == take;
-                ++fidx;
-                if (!use) continue;
-                take += step;
-                ++count;
-                if (n >= cap) { n = -1; break; }
-                ol[n++] = make_int2(k, mi);
+    wave_sync_lds();   // (lane 0's SMEMs)
+    for (int mi = 0; mi < nm && n >= 0; ++mi) {
+        const Iv p = S.mems[mi];
+        const int slen = p.end - p.start;
+        const int32_t h0 = S.hoff[p.start], h1 = S.hoff[p.start + 1];
+        const int step = p.occ > O.max_occ ? (int)(p.occ / O.max_occ) : 1;
+        int fbase = 0, count = 0;
+        for (int32_t kb = h0; kb < h1 && count < O.max_occ; kb += 64) {
+            const int32_t k = kb + lane;
+            const bool qual = k < h1 && S.hml[k] >= slen;   // text-position order: the 12-mer lists are sorted
+            const unsigned long long qm = __ballot(qual);
+            const int f = fbase + __popcll(qm & below);
+            const bool use = qual && f % step == 0 && f / step < O.max_occ;
+            const unsigned long long um = __ballot(use);
+            const int nu = __popcll(um);
+            if (n + nu > cap) {
+                n = -1;
+                break;
             }
+            if (use) ol[n + __popcll(um & below)] = make_int2(k, mi);
+            n += nu;
+            count += nu;
+            fbase += __popcll(qm);
         }
     }
-    n = __shfl(n, 0, 64);
     if (n < 0) return -1;
     int32_t *idx = reinterpret_cast<int32_t *>(ol + n);   // the lanes' lists of occurrence indices
     int32_t *cnt = lds, *cur = lds + 64;                 // per-lane counts / cursors (LDS)
@@ -410,7 +421,6 @@ __device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seed
     };
     // 2. every lane's share, 64 occurrences at a time: same-owner lanes by 6 ballots, ranks in
     // occurrence order; counts, then the stable scatter into the lanes' lists
-    const unsigned long long below = (1ull << lane) - 1ull;
     for (int pass = 0; pass < 2; ++pass) {
         if (pass == 1) {   // list starts: exclusive prefix of the counts over lanes
             int x = cnt[lane];
@@ -477,6 +487,7 @@ __device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seed
         int at = -1;
         bool at_tail = false;
         int32_t ns = e;
+        if (found && S.htab[h].r < 0) continue;   // (a range beyond cap_chains: the read is flagged)
         if (found) {
             RangeRec &R = S.rg[S.htab[h].r];
             if (R.tpos <= sd.rbeg) {
@@ -502,6 +513,10 @@ __device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seed
         S.cv[e] = c;
         if (!found) {
             const int r = atomicAdd(&lds[128], 1);
+            if (r >= S.cap_chains) {
+                S.htab[h].r = -1;
+                continue;
+            }
             RangeRec &R = S.rg[r];
             R.head = R.tail = e;
             R.n = 1;
@@ -535,6 +550,7 @@ __device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seed
     __threadfence_block();
     wave_sync_lds();
     const int nrg = lds[128];
+    if (nrg > S.cap_chains) return -2;
     for (int r = lane; r < nrg; r += 64) flush_tail(S, S.rg[r]);
     __threadfence_block();
     wave_sync_lds();
@@ -544,7 +560,122 @@ __device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seed
         for (int e = 0; e < n; ++e)
             if (S.cv[e].n > 0) S.cv[ncv++] = S.cv[e];
     __threadfence_block();
-    return __shfl(ncv, 0, 64);
+    ncv = __shfl(ncv, 0, 64);
+    return ncv > S.cap_chains ? -2 : ncv;
+}
+
+// mem_chain_flt (seed_core.h chain_flt) of one read by the whole wave: pass 2's reads carry up to
+// 2,048 chains, and the sequential filter's kept-list scan (every chain against every kept one,
+// three dependent loads a test) was ~90 ms per read at configs[3].  The weights a chain per lane;
+// the stable sort as ranks (the keys (weight desc, pos, head) are distinct, so every chain's
+// place is the number of smaller keys: the same order as the insertion sort); the kept scan in
+// sorted order with the kept list dealt over the lanes, 64 entries a step, ended at the first
+// entry that drops the chain (a ballot: the lowest lane is the sequential loop's break).  S.ge
+// (dead after the chaining) holds the keys, then the chains' query intervals, the kept list and
+// its `first` marks.  -> false when they do not fit (the caller filters on lane 0).
+__device__ bool chain_flt_wave(const pr_seed_opts &O, seedc::Scratch &S, int ncv, int lane, int *n_chains) {
+    using namespace seedc;
+    const int64_t ge_bytes = (int64_t)S.lmax * HB * 4;
+    if ((int64_t)ncv * 36 > ge_bytes) return false;
+    struct Key { int32_t nw, head; int64_t pos; };   // nw = -weight (INT32_MAX: filtered out)
+    Key *key = reinterpret_cast<Key *>(S.ge);
+    for (int j = lane; j < ncv; j += 64) {
+        Chain &c = S.cv[j];
+        const int w = chain_weight(S, c);
+        c.w = w;
+        key[j] = Key{w >= O.min_chain_weight ? -w : INT32_MAX, c.head, c.pos};
+    }
+    __threadfence_block();
+    wave_sync_lds();
+    int nch = 0;
+    for (int ib = 0; ib < ncv; ib += 64) {
+        const int i = ib + lane;
+        const Key ki = i < ncv ? key[i] : Key{INT32_MAX, 0, 0};
+        const bool pass = ki.nw != INT32_MAX;
+        nch += __popcll(__ballot(pass));
+        int rank = 0;
+        for (int jb = 0; jb < ncv; jb += 64) {   // 64 keys a step, one coalesced load, read out by lane
+            // (a padding key -- INT32_MAX weight -- is never below a key that passes)
+            const Key kj = jb + lane < ncv ? key[jb + lane] : Key{INT32_MAX, 0, 0};
+            const int plo = (int)(uint32_t)kj.pos, phi = (int)(kj.pos >> 32);
+#pragma unroll
+            for (int t = 0; t < 64; ++t) {
+                const int nw = __builtin_amdgcn_readlane(kj.nw, t), hd = __builtin_amdgcn_readlane(kj.head, t);
+                const int64_t ps = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane(phi, t) << 32) |
+                                             (uint32_t)__builtin_amdgcn_readlane(plo, t));
+                rank += (nw < ki.nw || (nw == ki.nw && (ps < ki.pos || (ps == ki.pos && hd < ki.head)))) ? 1 : 0;
+            }
+        }
+        if (pass) S.ch[rank] = S.cv[i];
+    }
+    __threadfence_block();
+    wave_sync_lds();
+    // the sorted chains' query intervals and weights; the kept list's (KV) and its first marks (F)
+    int4 *iv = reinterpret_cast<int4 *>(S.ge);
+    int4 *kv = iv + nch;
+    int32_t *fm = reinterpret_cast<int32_t *>(kv + nch);
+    for (int i = lane; i < nch; i += 64) {
+        const Chain &c = S.ch[i];
+        const Seed &h = S.seeds[c.head], &t = S.seeds[c.tail];
+        iv[i] = make_int4(h.qbeg, t.qbeg + t.len, c.w, 0);
+        fm[i] = -1;
+    }
+    __threadfence_block();
+    wave_sync_lds();
+    if (nch > 0) {
+        int nk = 1;
+        if (lane == 0) {
+            kv[0] = iv[0];
+            S.ch[0].kept = 3;
+        }
+        __threadfence_block();
+        wave_sync_lds();
+        for (int i = 1; i < nch; ++i) {
+            const int4 ci = iv[i];
+            const int bi = ci.x, ei = ci.y;
+            bool large = false, drop = false;
+            for (int kb = 0; kb < nk && !drop; kb += 64) {
+                const int k = kb + lane;
+                bool ov = false, br = false;
+                if (k < nk) {
+                    const int4 cj = kv[k];
+                    const int bj = cj.x, ej = cj.y;
+                    const int bmax = bj > bi ? bj : bi;
+                    const int emin = ej < ei ? ej : ei;
+                    if (emin > bmax) {
+                        const int li = ei - bi, lj = ej - bj;
+                        const int minl = li < lj ? li : lj;
+                        if (emin - bmax >= minl * O.mask_level && minl < O.max_chain_gap) {
+                            ov = true;
+                            br = ci.z < cj.z * O.drop_ratio && cj.z - ci.z >= O.min_seed_len << 1;
+                        }
+                    }
+                }
+                const unsigned long long bm = __ballot(br);
+                const int last = bm ? __ffsll((long long)bm) - 1 : 63;   // the lanes the sequential loop visits
+                if (ov && lane <= last && fm[k] < 0) fm[k] = i;
+                large = large || __ballot(ov && lane <= last) != 0ull;
+                drop = bm != 0ull;
+            }
+            if (!drop) {
+                if (lane == 0) {
+                    kv[nk] = ci;
+                    S.ch[i].kept = large ? 2 : 3;
+                }
+                ++nk;
+                __threadfence_block();
+                wave_sync_lds();
+            }
+        }
+        __threadfence_block();
+        wave_sync_lds();
+        for (int k = lane; k < nk; k += 64)
+            if (fm[k] >= 0) S.ch[fm[k]].kept = 1;
+    }
+    __threadfence_block();
+    wave_sync_lds();
+    *n_chains = nch;
+    return true;
 }
 
 // Pass 2: one wave per read with the large scratch slice (the reads of D.rlist: those that
@@ -600,13 +731,34 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
             const unsigned long long tc = D.prof && lane == 0 ? wall_clock64() : 0ULL;
             __threadfence_block();
             int ncv = chain_wave(D.V, D.O, S, nm, lane, ho);
-            if (lane == 0) {
-                if (ncv < 0) {
-                    ncv = 0;
-                    err = seedc::chain_seq(D.V, D.O, S, nm, &ncv);
+            unsigned long long tf = D.prof && lane == 0 ? wall_clock64() : 0ULL;
+            if (lane == 0 && D.prof) atomicAdd(&D.prof[14 + (ncv == -1 ? 1 : 0)], tf - tc);
+            if (ncv == -2) {
+                ncv = 0;
+                err = seedc::SC_OVER_CHAINS;
+            }
+            if (lane == 0 && ncv == -1) {
+                ncv = 0;
+                err = seedc::chain_seq(D.V, D.O, S, nm, &ncv);
+                if (D.prof) {
+                    const unsigned long long t_ = wall_clock64();
+                    atomicAdd(&D.prof[13], 1ULL);
+                    atomicAdd(&D.prof[15], t_ - tf);
+                    tf = t_;
                 }
-                if (!err) seedc::chain_flt(D.O, S, ncv, &nch);
-                if (D.prof) pl[3] += wall_clock64() - tc;
+            }
+            err = __shfl(err, 0, 64);
+            ncv = __shfl(ncv, 0, 64);
+            __threadfence_block();
+            wave_sync_lds();
+            bool flt = err != 0 || chain_flt_wave(D.O, S, ncv, lane, &nch);
+            if (lane == 0) {
+                if (!flt) seedc::chain_flt(D.O, S, ncv, &nch);
+                if (D.prof) {
+                    const unsigned long long t_ = wall_clock64();
+                    pl[3] += t_ - tc;
+                    atomicAdd(&D.prof[16], t_ - tf);
+                }
                 if (!err && seedc::seed_flt_min_score(D.O, len) >= 0 && 3 * S.cap_seeds <= 2 * S.cap_hits &&
                     2 * 201 * 64 * 2 <= 4 * S.lmax * seedc::HB)
                     nlist = seedc::flt_seed_list(S, nch, (int32_t *)S.hfr + S.cap_seeds, S.cap_seeds);

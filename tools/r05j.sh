@@ -2,7 +2,7 @@
 # interleaved A/B (base,new,base,new) printing step and seeding times
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_seed_gpu.py tests/test_seed_big_gpu.py tests/test_scale_configs_gpu.py -m gpu -x -q --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/r05j_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest ${TESTS:-tests/test_seed_gpu.py tests/test_seed_big_gpu.py tests/test_scale_configs_gpu.py} -m gpu -x -q --timeout 400 --timeout-method thread -p no:cacheprovider > gpurun_out/r05j_tests.log 2>&1
 rc=$?
 echo "tests rc=$rc"; tail -3 gpurun_out/r05j_tests.log
 [ $rc -le 1 ] || exit $rc
