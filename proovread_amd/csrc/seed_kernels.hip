@@ -554,13 +554,21 @@ __device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seed
     for (int r = lane; r < nrg; r += 64) flush_tail(S, S.rg[r]);
     __threadfence_block();
     wave_sync_lds();
-    // 4. the chains in creation order (slot order), compacted on lane 0
+    // 4. the chains in creation order (slot order), compacted 64 slots a step (a chunk's chains
+    // are all loaded before any is stored: destinations are at or below their sources)
     int ncv = 0;
-    if (lane == 0)
-        for (int e = 0; e < n; ++e)
-            if (S.cv[e].n > 0) S.cv[ncv++] = S.cv[e];
-    __threadfence_block();
-    ncv = __shfl(ncv, 0, 64);
+    for (int e0 = 0; e0 < n; e0 += 64) {
+        const int e = e0 + lane;
+        Chain c{};
+        if (e < n) c = S.cv[e];
+        const bool live = e < n && c.n > 0;
+        const unsigned long long lm = __ballot(live);
+        wave_sync_lds();
+        if (live) S.cv[ncv + __popcll(lm & below)] = c;
+        ncv += __popcll(lm);
+        __threadfence_block();
+        wave_sync_lds();
+    }
     return ncv > S.cap_chains ? -2 : ncv;
 }
 
