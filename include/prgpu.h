@@ -428,10 +428,11 @@ int pr_seed_gpu_lane_ticks(pr_ctx *ctx, uint64_t *ticks6);
 /* pass 1's occurrence tables (profiling): 100 MHz wave-clock ticks summed over
    waves of the start pass, the hit pass and the count table */
 int pr_seed_gpu_occ_ticks(pr_ctx *ctx, uint64_t *ticks3);
-/* pass 2's chaining (profiling): reads chained on one lane (occurrences beyond the wave's
-   slots), then ticks summed over waves of the wave-parallel chaining, of the one-lane chaining
-   and of the chain filter */
-int pr_seed_gpu_pass2_ticks(pr_ctx *ctx, uint64_t *t4);
+/* pass 2 (profiling): reads chained on one lane (occurrences beyond the wave's slots), then
+   ticks summed over waves of the wave-parallel chaining, of the one-lane chaining and of the
+   chain filter; then the largest ticks of one read's occurrence table, of its SMEMs and of the
+   whole read (7 values) */
+int pr_seed_gpu_pass2_ticks(pr_ctx *ctx, uint64_t *t7);
 /* wall time of the last pr_seed_gpu_map's second pass (the reads that outgrew pass 1's slices), ms */
 int pr_seed_gpu_pass2_ms(pr_ctx *ctx, double *ms);
 /* diagnostics (tests): the device path's core and capacities (its passes included) run on the host */

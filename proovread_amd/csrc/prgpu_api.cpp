@@ -2482,11 +2482,11 @@ extern "C" int pr_seed_gpu_lane_ticks(pr_ctx *c, uint64_t *ticks6) {
     return 0;
 }
 
-extern "C" int pr_seed_gpu_pass2_ticks(pr_ctx *c, uint64_t *t4) {
-    if (!c || !t4) return set_error(PR_ERR_ARG, "null arg");
+extern "C" int pr_seed_gpu_pass2_ticks(pr_ctx *c, uint64_t *t7) {
+    if (!c || !t7) return set_error(PR_ERR_ARG, "null arg");
     if (!c->sd[SB_NEXT].p) return set_error(PR_ERR_ARG, "no pr_seed_gpu_map launch yet");
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipMemcpy(t4, c->sd[SB_NEXT].as<uint8_t>() + 64 + 13 * 8, 32, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(t7, c->sd[SB_NEXT].as<uint8_t>() + 64 + 13 * 8, 56, hipMemcpyDeviceToHost));
     return 0;
 }
 

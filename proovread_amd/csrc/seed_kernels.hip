@@ -725,12 +725,18 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
         // (>= 440 bp), the seeds' local SW scores over all 64 lanes (a seed per lane, the rows
         // int16 and lane-interleaved in the dead count table); the output on lane 0
         int nch = 0, nlist = -1, nm = 0;
+        unsigned long long tm = 0ULL;   // (lane 0, profiling: the read's phase boundaries)
         if (lane == 0) {
-            if (D.prof) pt[0] += wall_clock64() - t0;
+            if (D.prof) {
+                tm = wall_clock64();
+                pt[0] += tm - t0;
+                atomicMax(&D.prof[17], tm - t0);
+            }
             if (len > 0 && !err) {
                 const seedc::Occ occ{&D.V, &S, q, len, lcnt};
                 nm = seedc::collect_intv(occ, S, D.O, q, len, err, D.prof ? pl : nullptr);
             }
+            if (D.prof) atomicMax(&D.prof[18], wall_clock64() - tm);
         }
         err = __shfl(err, 0, 64);
         nm = __shfl(nm, 0, 64);
@@ -803,6 +809,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
                                         D.prof ? pl : nullptr);
             D.n_out[i] = err ? 0 : n;
             D.status[i] = err;
+            if (D.prof) atomicMax(&D.prof[19], wall_clock64() - t0);   // the slowest read
         }
         __threadfence_block();
     }

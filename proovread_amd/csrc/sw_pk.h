@@ -234,10 +234,29 @@ SW_RING_FN uint32_t bfi_b32(uint32_t mask, uint32_t v, uint32_t acc) { return (m
 #define PK_BRANCH_BARRIER() ((void)0)
 #endif
 
-// Direction words of one (row, 16-slot pair of chunks): chunk 2p in x0/y0, 2p+1 in x1/y1.
+// Direction bits of one (row, 16-slot pair of chunks), 3 bit planes (12 bytes a lane; round 4's
+// four planes D1..D4 were 16).  ksw_global2's backtrack reads at a cell either the h source
+// (state M: F if D2, else E if D1, else M), or D3 (state E) or D4 (state F), and D1 => D3, D2 => D4
+// (e0 > M => M - e0 < o_del; f > max(M, e0) => f > M - o_ins): 8 cases, 3 bits.  Planes: p3 = the
+// source is not M; p1 = source F, or (source M and D3); p2 = D3 for source F, else D4.  Each plane
+// word: byte 0 / 1 = half A / B of chunk 2p (a bit per slot), byte 2 / 3 = the same of chunk 2p+1.
 struct PkDir {
-    uint32_t x0, y0, x1, y1;
+    uint32_t p1, p2, p3;
 };
+// glob_pk's chunk words (bytes D1A, D1B, D2A, D2B and D3A, D3B, D4A, D4B) of chunks 2p / 2p+1 -> PkDir
+SW_RING_FN PkDir pk_dir_enc(uint32_t x0, uint32_t y0, uint32_t x1, uint32_t y1) {
+    const uint32_t d1 = perm_b32(x1, x0, 0x05040100u), d2 = perm_b32(x1, x0, 0x07060302u);
+    const uint32_t d3 = perm_b32(y1, y0, 0x05040100u), d4 = perm_b32(y1, y0, 0x07060302u);
+    return PkDir{d2 | (d3 & ~d1), (d2 & d3) | (d4 & ~d2), d1 | d2};
+}
+// the planes back to D1 (D1 and not D2: the backtrack never reads D1 under D2) .. D4, words in
+// the plane layout
+SW_RING_FN void pk_dir_dec(const PkDir &v, uint32_t &d1, uint32_t &d2, uint32_t &d3, uint32_t &d4) {
+    d1 = v.p3 & ~v.p1;
+    d2 = v.p3 & v.p1;
+    d3 = (v.p1 ^ v.p3) | (v.p1 & v.p2 & v.p3);
+    d4 = v.p2 | (v.p3 & v.p1);
+}
 constexpr int pk_npair(int w) { return (2 * w + 2 + 15) >> 4; }
 
 // The DP of both tasks.  mA/mB: their query masks; nrows = wave max of tlen;
@@ -276,6 +295,7 @@ SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int n
     if (A.tlen > 0) pk_tref16(A.T, 1, 0, twA);
     if (B.tlen > 0) pk_tref16(B.T, 1, 0, twB);
     int hlA = 0, hlB = 0;
+    const int tmax = A.tlen > B.tlen ? A.tlen : B.tlen;
     for (int i = 0; i < nrows; ++i) {
         // reference bases of row i
         int ca = (int)(twA[0] & 0xFFu), cb = (int)(twB[0] & 0xFFu);
@@ -336,10 +356,11 @@ SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int n
                 ax = bfi_b32(bit, perm_b32(D2, D1, 0x0B0A0908u), ax);
                 ay = bfi_b32(bit, perm_b32(D4, D3, 0x0B0A0908u), ay);
             }
+            // (rows past both of the lane's tasks are never walked: no store)
             if (c & 1) {
-                if (!(O.debug & 2)) zi[(c >> 1) * ZS] = PkDir{px, py, ax, ay};
+                if (!(O.debug & 2) && i < tmax) zi[(c >> 1) * ZS] = pk_dir_enc(px, py, ax, ay);
             } else if (c == cse || c + 1 == NCH) {
-                if (!(O.debug & 2)) zi[(c >> 1) * ZS] = PkDir{ax, ay, 0u, 0u};
+                if (!(O.debug & 2) && i < tmax) zi[(c >> 1) * ZS] = pk_dir_enc(ax, ay, 0u, 0u);
             } else {
                 px = ax, py = ay;
             }
@@ -607,10 +628,10 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
 
 // direction nibble (D1 | D2 << 1 | D3 << 2 | D4 << 3) of half hb at (row i, slot s)
 SW_RING_FN int pk_nib(const PkDir &v, int s, int hb) {
-    const uint32_t x = (s & 8) ? v.x1 : v.x0, y = (s & 8) ? v.y1 : v.y0;
-    const int bt = (s & 7) + 8 * hb;
-    return (int)(((x >> bt) & 1u) | (((x >> (bt + 16)) & 1u) << 1) | (((y >> bt) & 1u) << 2) |
-                 (((y >> (bt + 16)) & 1u) << 3));
+    uint32_t d1, d2, d3, d4;
+    pk_dir_dec(v, d1, d2, d3, d4);
+    const int bt = (s & 7) + 8 * hb + ((s & 8) ? 16 : 0);
+    return (int)(((d1 >> bt) & 1u) | (((d2 >> bt) & 1u) << 1) | (((d3 >> bt) & 1u) << 2) | (((d4 >> bt) & 1u) << 3));
 }
 // ksw_global2's state step: h source (M 0, E 1, F 2) from state 0, continue bits otherwise
 SW_RING_FN int pk_which(int which, int nib) {
@@ -687,9 +708,11 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
     };
     // the half's direction bytes of a (row, pair) word: x = D1|D2 of both chunks, y = D3|D4
     auto pick = [&](const PkDir &v, int h, uint32_t &x, uint32_t &y) {
-        const uint32_t sel = h ? 0x07050301u : 0x06040200u;
-        x = perm_b32(v.x1, v.x0, sel);
-        y = perm_b32(v.y1, v.y0, sel);
+        uint32_t d1, d2, d3, d4;
+        pk_dir_dec(v, d1, d2, d3, d4);
+        const uint32_t sel = h ? 0x07030501u : 0x06020400u;
+        x = perm_b32(d2, d1, sel);
+        y = perm_b32(d4, d3, sel);
     };
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -708,7 +731,7 @@ SW_RING_FN void pk_backtrack2(const PkDir *zl, int ZS, int npair, int nrows, con
             PkDir v[WIN];
 #pragma unroll
             for (int d = 0; d < WIN; ++d) {
-                v[d] = PkDir{0u, 0u, 0u, 0u};
+                v[d] = PkDir{0u, 0u, 0u};
                 if (live[h] && R - d >= 0 && R - d <= i[h]) {
                     const long ix = ((long)(R - d) * npair + p[h]) * ZS;
                     PK_ZCHECK(ix);

@@ -214,12 +214,13 @@ def _phase_ms(L, ctx) -> dict:
         _abi.check(L.pr_seed_gpu_occ_ticks(ctx.h, ot.ctypes.data), "pr_seed_gpu_occ_ticks")
         out["occ_table_parts"] = {k: round(float(v) / 1e5, 1) for k, v in zip(("starts", "hits", "count_table"), ot)}
     if hasattr(L, "pr_seed_gpu_pass2_ticks"):
-        t2 = np.zeros(4, np.uint64)
+        t2 = np.zeros(7, np.uint64)
         L.pr_seed_gpu_pass2_ticks.argtypes = [C.c_void_p, C.c_void_p]
         _abi.check(L.pr_seed_gpu_pass2_ticks(ctx.h, t2.ctypes.data), "pr_seed_gpu_pass2_ticks")
         out["pass2_parts"] = {"one_lane_reads": int(t2[0])}
         out["pass2_parts"].update({k: round(float(v) / 1e5, 1) for k, v in
-                                   zip(("chain_wave", "chain_one_lane", "chain_flt"), t2[1:])})
+                                   zip(("chain_wave", "chain_one_lane", "chain_flt", "max_read_occ_table",
+                                        "max_read_smems", "max_read"), t2[1:])})
     p2 = C.c_double()
     _abi.check(L.pr_seed_gpu_pass2_ms(ctx.h, C.byref(p2)), "pr_seed_gpu_pass2_ms")
     out["pass2_wall_ms"] = round(p2.value, 1)
