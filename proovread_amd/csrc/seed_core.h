@@ -1185,7 +1185,7 @@ struct Caps {
 // the mr modes' 300-1000 bp reads (~300 seeds per 600 bp read at 15x long-read coverage)
 SC_HD int device_out_cap(int qmax) { return qmax > 192 ? 2 * ((qmax + 15) & ~15) : 384; }
 SC_HD Caps device_caps(int qmax = 0) {
-    Caps c{1024, 8192, 256, 1024, 4096, 2048, 384, 0};
+    Caps c{1024, 8192, 256, 1024, 8192, 4096, 384, 0};   // (seeds / chains: pass 2 chains reads of up to ~6.8 k occurrences over the wave)
     c.out = device_out_cap(qmax);
     if (qmax > 192) {   // pass 2 for mr reads: at least twice pass 1's room (device_caps_small)
         const int l = (qmax + 15) & ~15;
