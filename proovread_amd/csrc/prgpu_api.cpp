@@ -2293,11 +2293,13 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         std::vector<int32_t> redo;
         int32_t fl1 = 0;
         int64_t need_hits = 0;   // the largest hit table a flagged read asked for
+        int64_t need_sum = 0, need_n = 0;   // (and their mean)
         for (int64_t i = r0; i < r1; ++i)
             if (st1[(size_t)(i - r0)]) {
                 redo.push_back((int32_t)i);
                 fl1 |= st1[(size_t)(i - r0)];
                 need_hits = std::max<int64_t>(need_hits, -(int64_t)no1[(size_t)(i - r0)]);
+                if (no1[(size_t)(i - r0)] < 0) need_sum -= no1[(size_t)(i - r0)], ++need_n;
             }
         // many flagged reads (the finish task maps to corrected reads at 30x long-read coverage:
         // ~140 starts x 30 hits > 4096 for nearly every read): pass 1 again, lane per read, over
@@ -2323,7 +2325,42 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
             const int64_t sb = seedc::scratch_bytes(cb);
             int64_t wb = std::min<int64_t>((int64_t)D[SB_SCRATCH].cap / (64 * sb), ((int64_t)redo.size() + 63) / 64);
             wb = std::min<int64_t>(wb, waves);   // (the filter rows' area holds `waves` waves)
-            if (wb >= c->n_cu) {
+            // reads that need more than 4x pass 1's hits on average (dense indexes: configs[2] / [3]) one wave
+            // each (seed_wave_kernel: the chaining over the lanes) with pass 2's slices grown like
+            // cb: 64 such slices per wave fit only a few hundred waves in the scratch (a configs[3]
+            // rank's seeding 17.4 -> 4.1 s, configs[2] 1.01 -> 0.82 s).  The finish task's reads
+            // (just over pass 1's hits, ~30x coverage) stay lane per read (620 vs 724 ms as waves).
+            // PRGPU_SEED_1B=wave / lane forces either.
+            const char *p1b = getenv("PRGPU_SEED_1B");
+            const bool by_wave = p1b ? !strcmp(p1b, "wave") : need_sum > 4 * (int64_t)small.hits * need_n;
+            seedc::Caps cw = caps;
+            cw.hits = std::max(caps.hits, cb.hits);
+            cw.iv = std::max(caps.iv, cb.iv);
+            cw.mems = std::max(caps.mems, cb.mems);
+            cw.seeds = std::max(caps.seeds, cb.seeds);
+            cw.chains = std::max(caps.chains, cb.chains);
+            const int64_t sw = seedc::scratch_bytes(cw);
+            const int64_t ww = std::min<int64_t>(std::min<int64_t>(lanes2, (int64_t)redo.size()), (int64_t)D[SB_SCRATCH].cap / sw);
+            if (by_wave && ww >= c->n_cu) {
+                K.caps = cw;
+                K.stride = sw;
+                K.n_lanes = ww;
+                K.rlist = D[SB_PRE].as<int32_t>();
+                K.n_list = (int64_t)redo.size();
+                HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
+                HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
+                e = seed_launch(K, (void *)s);
+                if (e) return set_error(PR_ERR_HIP, "seed kernel (pass 1b, waves): %s", hipGetErrorString((hipError_t)e));
+                std::vector<int32_t> st1b((size_t)(r1 - r0));
+                if ((rc = download(st1b.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0))) return rc;
+                HIPCHK(hipStreamSynchronize(s));
+                std::vector<int32_t> left;
+                for (int32_t i : redo)
+                    if (st1b[(size_t)(i - r0)]) left.push_back(i);
+                redo.swap(left);
+                K.rlist = nullptr;
+                K.n_list = 0;
+            } else if (wb >= c->n_cu) {
                 K.caps = cb;
                 K.stride = sb;
                 K.n_lanes = wb;
