@@ -67,7 +67,7 @@ BIN_FILTER = (20, 20.0 * 15.0)
 HCR_MASK = "20,41,80,130,60,0.7"   # hcr-mask of bwa-sr-1 (proovread.cfg:234-242)
 # HBM bytes per launch from separate FETCH_SIZE / WRITE_SIZE rocprofv3 passes over this bench
 # (tools/pmc_summary.py; MI355X_MICROARCH.md's corrections)
-PMC_FILE = "pmc_r05.json"
+PMC_FILE = "pmc_traffic.json"   # (repo root: profiles/ does not travel to the GPU box)
 _JSON_OUT = sys.stdout
 
 
@@ -284,7 +284,10 @@ def main():
     # pileup kernel: algorithmic bytes (SURVEY.md §8d model) / kernel time
     cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + own_bases * (2 + 2 + 6 * 4 * 2)
     traffic = traffic_cns = traffic_ext = traffic_seed = None
-    prof = ROOT / "profiles" / PMC_FILE
+    pmc_src = None
+    prof = ROOT / PMC_FILE   # tools/pmc_summary.py of the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+    if not prof.exists():
+        prof = ROOT / "profiles" / "pmc_r05.json"
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())
@@ -296,6 +299,8 @@ def main():
             ts = [hbm("seed_batch"), hbm("seed_wave")] if ts[0] is None else ts
             traffic_seed = sum(x for x in ts if x is not None) if ts[0] is not None else None
             traffic_ext = {k: v.get("hbm_bytes_per_launch") for k, v in pm.items() if k.startswith("sw_ext_")}
+            pmc_src = f"{prof.name}: rocprofv3 FETCH_SIZE (x2, gfx950) + WRITE_SIZE passes per launch, " \
+                      f"{pm.get('_build', 'build not recorded')}"
         except Exception:
             traffic = traffic_cns = traffic_ext = traffic_seed = None
     ref_cpu = None   # the reference's own Perl consensus, timed in the build container
@@ -347,6 +352,7 @@ def main():
                                      zip(("masks", "dp", "backtrack", "emit"), pc)},
         "consensus_phase_ms_summed_over_workgroups": {k: round(v, 1) for k, v in cns_phases.items()},
         "seeding_phase_ms_summed_over_waves": seed_phases,
+        "traffic_source": pmc_src,
         "roofline": {
             "kernel": "sw_global_pk_kernel<40> (ksw_global2 CIGAR pass + backtrack, packed int16, two tasks per lane)",
             "bound": "valu", "achieved": round(dom_tops, 3), "peak": round(VALU_PEAK_TOPS, 2), "unit": "TOP/s (int32)",

@@ -8,6 +8,7 @@ doubled to the bytes of the lines moved; WRITE_SIZE reads the written bytes exac
 """
 import csv
 import json
+import os
 import sys
 from collections import defaultdict
 from pathlib import Path
@@ -38,5 +39,6 @@ for name in vals["WRITE_SIZE"]:
         "hbm_bytes_per_launch": round(2 * fe_b + wr_b),
     }
 res["_note"] = __doc__.strip()
+res["_build"] = "build " + os.environ.get("PMC_BUILD", "not recorded")
 out.write_text(json.dumps(res, indent=1) + "\n")
 print(json.dumps(res, indent=1))

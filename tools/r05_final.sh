@@ -26,4 +26,8 @@ for c in FETCH_SIZE WRITE_SIZE; do
      > "$GRAFT_REPO_ROOT/gpurun_out/pmc_$c.log" 2>&1) || { echo "pass $c rc=$?"; exit 1; }
   echo "pass $c ok"
 done
-TAG=sq_${T} bash tools/pmc_sq.sh
+TAG=sq_${T} bash tools/pmc_sq.sh || exit 1
+# the traffic the bench line reports: this build's PMC passes, then the bench once more
+PMC_BUILD="${BUILD:-unknown}" python3 tools/pmc_summary.py pmc_traffic.json > /dev/null && cp pmc_traffic.json gpurun_out/pmc_traffic.json || exit 1
+timeout -k 10 600 python -u bench.py > gpurun_out/${T}_bench_traffic.json 2> gpurun_out/${T}_bench_traffic.err
+rc=$?; echo "bench (traffic) rc=$rc"; cut -c1-300 gpurun_out/${T}_bench_traffic.json; exit $rc
