@@ -362,8 +362,9 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
 // every lane chains its ranges' occurrences in the sequential order.  A seed's slot, and a new
 // chain's, is the occurrence's place in that order: creation order -- the chain sort's last
 // tie-break -- is the sequential one and no slot counter is shared.  -> the number of chains,
-// compacted into S.cv[0, n) in creation order, or -1 when the occurrences do not fit the slice
-// (the caller then chains on one lane).  lds: 66 ints of the wave's LDS.
+// compacted into S.cv[0, n) in creation order; -1 when the occurrences do not fit the slice
+// (the caller then chains on one lane); -2 when the chains or ranges exceed cap_chains (the
+// sequential chaining's SC_OVER_CHAINS).  lds: 129 ints of the wave's LDS.
 __device__ int chain_wave(const seedc::IndexView &I, const pr_seed_opts &O, seedc::Scratch &S, int nm, int lane,
                           int32_t *lds) {
     using namespace seedc;
