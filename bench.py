@@ -1,37 +1,38 @@
 #!/usr/bin/env python
-"""Benchmark of proovread's hot path on MI355X: one whole bwa-sr correction task per step --
-the seed index of the long reads, bwa-proovread mem seeding, seed extension + CIGAR, the
-alignments to their long reads' owners, the -b/-l filter, hand-off and bam2cns consensus, the
-masking of the corrected reads with its {bpt, bpN} statistic, and the commit of the corrected
-reads -- over a synthetic workload of BASELINE.json configs[1] size per GPU.
+"""Benchmark of proovread's hot path on MI355X: the whole sr-noccs correction run per step --
+read-long's output restored in HBM, then bwa-sr-1 .. bwa-sr-N with mask_shortcut_frac and
+bwa-sr-finish (bin/proovread:705-905, 2026-2047) -- over a synthetic workload of BASELINE.json
+configs[1] size per GPU; beside it the rate of one bwa-sr-1 task (value_task).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-One step = one bwa-sr-1 task as proovread runs it every iteration (bin/proovread:835-869:
-index 1270, mem 1313, create_sorted_bam 1330-1355, correct_sr_mt 1528-1721), in the
-correction loop's multi-GPU layout (correct.GpuStages; SURVEY.md §8e exact-parity option,
-DESIGN.md §6):
+One step = one correction run as proovread makes it (correct.run_tasks on correct.GpuStages, the
+loop's multi-GPU layout; SURVEY.md §8e exact-parity option): the long-read set back
+to read-long's output (pr_lrset_restore, device to device), then per task
 
-  index     pr_lrset_index: the seed index of ALL long reads, from the resident set in HBM
-  seeding   pr_seed_gpu_map_sampled: the rank's contiguous share of the task's short reads
-            (gathered on the device from the resident short reads), seeds left in HBM
-  SW        pr_sw_upload_gpu_seeds + pr_sw_launch: bwa mode over every seed of the kept
-            chains (extension rounds, final pass, CIGAR pass over the reported alignments)
-  exchange  pr_aln_exchange: every reported alignment to the owner of its long read (device
-            pack + one RCCL all-to-all; at N = 1 the identity)
-  consensus pr_iter_upload_owned + pr_iter_launch: the owner's -b/-l filter, hand-off and
-            consensus of its long reads
-  mask      pr_iter_mask + RCCL all-reduce of {bpt, bpN} (mask_shortcut_frac's input)
-  commit    pr_lrset_commit(DRY): the corrected and masked reads compacted and all-gathered
-            across the ranks exactly as the loop does, without replacing the set, so every
-            step repeats the same task on the same input
+  sampling  SeqChunker's chunks of the short-read stream for the task's coverage
+            (cov2seqchunker, bin/proovread:2085-2102), gathered on the device from the
+            resident short reads (every rank its contiguous share of the sample)
+  index     pr_lrset_index: the seed index of ALL long reads' mapping reference (the finish
+            task: the reads), from the resident set in HBM
+  seeding   pr_seed_gpu_map_sampled: bwa-proovread mem's seeding and chaining, seeds left in HBM
+  SW        pr_sw_upload_gpu_seeds + pr_sw_launch: bwa mode over every seed of the kept chains
+  exchange  pr_aln_exchange: every reported alignment to the owner of its long read (RCCL
+            all-to-all; at N = 1 the identity)
+  consensus pr_iter_upload_owned + pr_iter_launch: the -b/-l filter, hand-off and consensus
+  mask      pr_iter_mask + the {bpt, bpN} all-reduce -> mask_shortcut_frac (regular tasks)
+  commit    pr_lrset_commit: the corrected (and masked) reads replace the set, all-gathered
+            across the ranks
 
-Every rank generates the SAME global dataset (one genome, one long-read set, one short-read
-run in sequencer order -- unsorted over the genome): configs[1] x N (weak scaling: each rank
-owns 13,800 long reads and aligns 1/N of the short reads; at N > 1 about (N-1)/N of its
-alignments belong to another rank's long reads and cross xGMI).  Inputs are resident in HBM
-before the timed region; no torch in the process (libprgpu owns the HIP runtime and RCCL).
+`value` = the corrected long-read bases of the whole job per second of the run.  `value_task`
+repeats bwa-sr-1 alone on the raw reads (the round-5 headline's scope, commit DRY).
+
+Every rank generates the SAME global dataset (one genome, one long-read set, one 50x short-read
+run in sequencer order -- unsorted over the genome): configs[1] x N (weak scaling: each rank owns
+13,800 long reads and aligns 1/N of every task's sample; at N > 1 about (N-1)/N of its alignments
+belong to another rank's long reads and cross xGMI).  Inputs are resident in HBM before the
+timed region; no torch in the process (libprgpu owns the HIP runtime and RCCL).
 
 Prints ONE JSON line on rank 0 (see DESIGN.md §5 for every field).
 """
@@ -59,8 +60,9 @@ HBM_PEAK_GBS = 8000.0
 OPS_PER_CELL = 14   # SURVEY.md §8d canonical int ops per DP cell
 SEED = 20261015 + 2   # 20261015 + config number
 # configs[1] per GPU: 4.6 Mb genome, 13,800 x 10 kb CLR reads (30x, 15 % error), 50x 150 bp
-# short reads sampled to the iteration's 15x (cov2seqchunker, proovread:2085-2102: 6 of 20)
-GENOME, N_LR, SR_COV, SR_FRAC = 4_600_000, 13_800, 50.0, 6 / 20
+# short reads, sampled per task by SeqChunker (cov2seqchunker, proovread:2085-2102: 6 of 20
+# chunks for the regular tasks' 15x, 12 of 20 for the finish task's 30x)
+GENOME, N_LR, SR_COV = 4_600_000, 13_800, 50.0
 # bwa-proovread -b BIN -l LEN of a bwa-sr iteration: BIN = bin-size 20 (proovread.cfg:259-273),
 # LEN = BIN x min(--coverage 50, sr-coverage 15) (bin/proovread:1302-1313)
 BIN_FILTER = (20, 20.0 * 15.0)
@@ -85,6 +87,16 @@ def parse():
     return ap.parse_args()
 
 
+def host_cpu() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(d, per_worker: int):
     """The oracle chain (oracle/cpu_bench.py) on the first per_worker x workers long reads, in
     a child process; -> (cpu_baseline JSON object, per-read oracle outputs)."""
@@ -105,10 +117,12 @@ def cpu_baseline(d, per_worker: int):
                         str(BIN_FILTER[0]), str(BIN_FILTER[1])], check=True)
         r = json.loads(Path(out).read_text())
     cpu = {"value": round(r["bases"] / r["wall_s"] / 1e6, 4), "unit": "Mbases/s", "cores": r["workers"], "kind": "port",
-           "sample": f"first {r['n']} of {d.n_lr} long reads of the same workload ({r['bases']} bases; bwa mem "
-                     f"per-read alignment of every short read seeded on them, {r['tasks']} seeds), SW + consensus C "
-                     f"restatement (oracle/), {r['workers']} processes, {r['wall_s']:.1f} s; seeding and masking "
-                     f"not included"}
+           "cpu": host_cpu(), "compare_with": "value_task (one bwa-sr-1 task)",
+           "sample": f"one bwa-sr-1 task on the first {r['n']} of {d.n_lr} long reads of the same workload "
+                     f"({r['bases']} bases; bwa mem per-read alignment of every short read seeded on them, "
+                     f"{r['tasks']} seeds), SW + consensus C restatement (oracle/), {r['workers']} processes, "
+                     f"{r['wall_s']:.1f} s; the seeding, index build and masking are NOT included (the GPU "
+                     f"value_task includes them)"}
     return cpu, r["results"]
 
 
@@ -129,6 +143,23 @@ def check_parity(it, cpu_res):
                        "restatement pinned to the reference Perl engine), same seeds"}
 
 
+def reference_cpu():
+    """The reference's own Perl consensus (lib/Sam/Seq.pm), timed in the build container where
+    /root/reference exists (tools/time_reference_r03.py); the record travels with the tree."""
+    rp = ROOT / "baselines" / "reference_cpu_consensus_r03.json"
+    if not rp.exists():
+        return None
+    try:
+        r3 = json.loads(rp.read_text())
+        rpl = r3["reference_perl"]
+        return {"value": rpl["Mbases_per_s"], "unit": "Mbases/s", "cores": rpl["processes"], "kind": "reference",
+                "scope": "consensus only (bam2cns over Sam::Seq), build container", "cpu": r3["host"]["cpu"],
+                "sample": r3["workload"] + f"; {rpl['engine']}; {rpl['wall_s']} s wall",
+                "source": "baselines/reference_cpu_consensus_r03.json (tools/time_reference_r03.py)"}
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     # the contract is ONE JSON line on stdout: libraries that print there (RCCL's version
@@ -147,72 +178,108 @@ def main():
     from proovread_amd import synth
     gl = int(GENOME * args.scale * world)
     n_lr = int(N_LR * args.scale * world)
-    n_sr = int(round(SR_COV * gl / 150 * SR_FRAC))
+    n_sr = int(round(SR_COV * gl / 150))
     t = time.perf_counter()
     threads = max(1, min(16, (os.cpu_count() or 1) // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", world)))))
     d = synth.simulate_reads(SEED, gl, n_lr, 10_000, n_sr, threads=threads)   # the same on every rank
     gen_s = time.perf_counter() - t
 
-    from proovread_amd import _abi, cns, comm as comm_mod, correct, exact_shard as ex, iteration, mask, seed, sw
+    from proovread_amd import _abi, cns, comm as comm_mod, control, correct, exact_shard as ex, seed, sw
+    from proovread_amd import tasks as T
     ctx = _abi.Context(local)
     cm = comm_mod.RcclComm.from_env(ctx) if world > 1 or args.comm == "rccl" else None
     L = _abi.lib()
+    from proovread_amd import iteration
     iteration._setup(L)
     seed._setup(L)
-    # resident inputs: every long read (ASCII + '$' qualities: raw CLR reads, phred 3) and every
-    # short read of the task on every rank
+    # resident inputs: every long read (ASCII + '$' qualities: raw CLR reads, phred 3) and the
+    # whole 50x short-read run on every rank
     t_up = time.perf_counter()
-    ascii_pool = np.frombuffer(b"ACGTN", np.uint8)[d.lr_seq]
+    ascii_pool = np.frombuffer(b"ACGTN", np.uint8)[d.lr_seq[:int(d.lr_off[-1])]]
     stages = correct.GpuStages(ctx)
     stages.load(correct.LongReads([f"lr{i}" for i in range(n_lr)],
                                   pools=(ascii_pool, d.lr_off, np.full(len(ascii_pool), ord("$"), np.uint8))))
     del ascii_pool
-    _abi.check(L.pr_srset_load(ctx.h, n_sr, _abi.ptr(d.sr_off, C.c_int64), _abi.ptr(d.sr_seq, C.c_uint8)),
-               "pr_srset_load")
+    stages.snapshot()                      # read-long's output: every step restarts from it
+    srs = correct.ShortReads.from_pool(d.sr_seq[:int(d.sr_off[-1])], d.sr_off)
+    stages.load_short_reads(srs)
     upload_s = time.perf_counter() - t_up
     lrs = stages.lrs
     lr_off = d.lr_off
     bounds = ex.lr_bounds(lr_off, world)
     lo, hi = int(bounds[rank]), int(bounds[rank + 1])
-    s0, s1 = ex.sr_range(n_sr, world, rank)
-    shard_rg = np.array([[s0, s1]], np.int64)
     own_bases = int(lr_off[hi] - lr_off[lo])
-    opts = sw.default_opts(finish=False)
-    opts.bin_size, opts.bin_length = BIN_FILTER     # bwa-proovread -b 20 -l 300 (proovread:1302-1313)
+    cfg = correct.LoopConfig(coverage=50.0, exact_layout=True)
+    mode = "sr-noccs"
+    loop_tasks = list(T.MODE_TASKS[mode][1:])   # after read-long (proovread.cfg:119)
+    min_sr = 150
+
+    # ------------------------------------------------------------------ the whole run (value)
+    def loop_step():
+        stages.restore()
+        chim, _, log = correct.run_tasks(stages, srs, loop_tasks, cfg, mode, min_sr, True, cm)
+        return chim, log
+
+    def digest(chim):
+        import hashlib
+        off, sq, ql, _ = lrs.download(seq=True, qual=True)
+        h = hashlib.sha256(off.tobytes())
+        h.update(sq.tobytes())
+        h.update(ql.tobytes())
+        h.update("".join(chim).encode())
+        return h.hexdigest()
+
+    first_digest = None
+    for k in range(args.warmup):
+        chim, _ = loop_step()
+        if k == 0:
+            first_digest = digest(chim)
+    if cm is not None:
+        cm.barrier()
+    _abi.check(L.pr_ctx_sync(ctx.h), "pr_ctx_sync")
+    t0 = time.perf_counter()
+    dev0 = stages.device_ms
+    logs = []
+    for _ in range(args.steps):
+        chim, log = loop_step()
+        logs.append(log)
+    if cm is not None:
+        cm.barrier()
+    _abi.check(L.pr_ctx_sync(ctx.h), "pr_ctx_sync")
+    el = time.perf_counter() - t0
+    loop_dev_ms = (stages.device_ms - dev0) / max(args.steps, 1)
+    last_digest = digest(chim)
+    n_chim = len(chim)
+    if cm is not None:
+        el = cm.allreduce_floats([el], comm_mod.RED_MAX)[0]
+        total_bases = cm.allreduce_ints([own_bases])[0]
+    else:
+        total_bases = own_bases
+    log = logs[-1]
+    loop_rows = [{"task": e.task, "short_reads": e.n_sr, "seeds_rank": e.n_tasks, "wall_ms": e.wall_ms,
+                  "device_ms": e.device_ms, "masked_frac": None if e.masked_frac is None else round(e.masked_frac, 4),
+                  "shortcut": e.shortcut} for e in log]
+    same_tasks = all([e.task for e in lg] == [e.task for e in log] for lg in logs)
+
+    # ------------------------------------------------------------------ one bwa-sr-1 task (value_task)
+    sampler = control.Sampler(sampling=cfg.sampling)
+    rg1, off1 = srs.sample_ranges(sampler.cov2seqchunker(cfg.coverage, T.sr_coverage("bwa-sr-1")))
+    n1 = len(off1) - 1
+    s0, s1 = ex.sr_range(n1, world, rank)
+    params1 = cns.CnsParams(coverage=min(50.0, 15.0) * 0.75, use_ref_qual=True, max_ins_length=0)   # :1540-1541
     sopts = seed.default_opts(False)
-    params = cns.CnsParams(coverage=min(50.0, 15.0) * 0.75, use_ref_qual=True, max_ins_length=0)   # :1540-1541
-    mparams = mask.params(HCR_MASK, 150)
-    stats = _abi.DevBuffer(ctx, 16)
-    shard_status = np.zeros(max(1, s1 - s0), np.int32)
+    stages.restore()
     wall = {}
 
-    def tick(key, t0):
-        t1 = time.perf_counter()
-        wall[key] = wall.get(key, 0.0) + (t1 - t0)
-        return t1
-
-    def step(timed=True):
+    def task_step(dry=True):
         t0 = time.perf_counter()
-        lrs.index(lrs.MAP)                                                   # bwa-proovread index
-        t0 = tick("index", t0)
-        _abi.check(L.pr_seed_gpu_map_sampled(ctx.h, C.byref(sopts), _abi.ptr(shard_rg, C.c_int64), 1,
-                                             _abi.ptr(shard_status, C.c_int32)), "pr_seed_gpu_map_sampled")
-        t0 = tick("seeding", t0)                                             # bwa-proovread mem front end
-        iteration.ShardSW(ctx, None, d.sr_off, s0, s1, None, lr_off, device_pools=True).launch(opts)
-        iteration.exchange(ctx, cm if world > 1 else None, s0, bounds)
-        it = iteration.OwnedIteration(ctx, lo, hi, lr_off, None, None, None, d.sr_off, from_set=True,
-                                      resident_sr=True)
-        t0 = tick("sw_exchange", t0)                                         # (the owned upload waits for the SW)
-        it.launch(opts, params)
-        it.mask_to(stats.ptr, mparams)                                       # SeqFilter --phred-mask
-        if cm is not None:
-            cm.allreduce_dev(stats.ptr, 2)                                   # global bpt / bpN
-        lrs.commit(cm if world > 1 else None, with_mask=True, dry=True)      # (synchronises)
-        tick("consensus_mask_commit", t0)
-        return it
+        stages.task("bwa-sr-1", None, off1, params1, BIN_FILTER, cm, True, (HCR_MASK, min_sr), sr_ranges=rg1,
+                    dry=dry)
+        wall["task"] = wall.get("task", 0.0) + time.perf_counter() - t0
+        return stages.last_iteration
 
     for _ in range(args.warmup):
-        step()
+        task_step()
     wall.clear()
     if cm is not None:
         cm.barrier()
@@ -220,55 +287,56 @@ def main():
     t0 = time.perf_counter()
     ev = np.zeros(6)
     dom_ms = dom_cells = ext_ms = ext_cells = ext_launches = 0
+    sw_stage_ms = sw_cells = 0.0
     for _ in range(args.steps):
-        it = step()
+        it = task_step()
         ev += np.array([lrs_index_ms(L, ctx), seed._last_ms(L.pr_seed_gpu_last_ms, ctx), *it.timing()])
         dm, dom_cells = sw.dominant_kernel(ctx)
         dom_ms += dm
         xm, ext_cells, ext_launches = sw.extension_kernels(ctx)
         ext_ms += xm
+        me, mg, ce, cg = sw.last_timing(ctx)
+        sw_stage_ms += me + mg
+        sw_cells += ce + cg
     if cm is not None:
         cm.barrier()
     _abi.check(L.pr_ctx_sync(ctx.h), "pr_ctx_sync")
-    el = time.perf_counter() - t0
+    el_task = time.perf_counter() - t0
     if cm is not None:
-        el = cm.allreduce_floats([el], comm_mod.RED_MAX)[0]
-        total_bases = cm.allreduce_ints([own_bases])[0]
-    else:
-        total_bases = own_bases
+        el_task = cm.allreduce_floats([el_task], comm_mod.RED_MAX)[0]
     K = max(args.steps, 1)
     ev /= K
-    wall_ms = {k: round(v / K * 1e3, 2) for k, v in wall.items()}
     n_seeds = seed._count(L, ctx)
-    me, mg, ce, cg = sw.last_timing(ctx)
     bwa_rounds, bwa_ext, bwa_patch = sw.bwa_stats(ctx)
     pc = sw.phase_cycles(ctx)
     n_recv = it.n_task
     n_aln, sum_ncig, sum_lseq = it.alignment_stats()
-    # one more, untimed step with the consensus kernel's per-phase clock counters on
+    # one more, untimed task with the consensus kernel's per-phase clock counters on
     os.environ["PRGPU_CNS_PROF"] = "1"
-    it = step()
+    it = task_step()
     os.environ.pop("PRGPU_CNS_PROF")
     cns_phases = it.cns_phase_ms()
     seed_phases = seed._phase_ms(L, ctx)
-    bpt, bpn = (int(x) for x in stats.download(np.int64))
     status = it.statuses()
     ok = int((status == 0).sum())
     # checks outside the timed region (rank 0 at N = 1): GPU seeds = the host seeding path on
-    # 20 k reads; the CPU baseline (oracle chain) on a bounded sample, whose per-read outputs
-    # are also the parity check of the GPU task
+    # 20 k reads of the task's sample; the CPU baseline (oracle chain) on a bounded sample,
+    # whose per-read outputs are also the parity check of the GPU task
     cpu = cpu_res = parity = seed_check = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        gpu_tasks, gst = seed._map_gpu(L, ctx, d.sr_seq, d.sr_off, sopts, False)   # same device index
-        ns = min(n_sr, 20_000)
+        import dataclasses
+        sr1 = np.ascontiguousarray(srs.gather(rg1), np.uint8)
+        dt = dataclasses.replace(d, sr_seq=sr1, sr_off=np.ascontiguousarray(off1, np.int64))
+        gpu_tasks, gst = seed._map_gpu(L, ctx, sr1, off1, sopts, False)   # same device index (raw reads)
+        ns = min(n1, 20_000)
         hx = seed.SeedIndex(d.lr_seq, d.lr_off)
-        want = hx.map(d.sr_seq[:d.sr_off[ns]], d.sr_off[:ns + 1], sopts, threads=min(16, os.cpu_count() or 1))
+        want = hx.map(sr1[:off1[ns]], off1[:ns + 1], sopts, threads=min(16, os.cpu_count() or 1))
         hx.close()
         seed_check = {"reads": int(ns), "tasks": int(len(want)),
                       "equal": bool(np.array_equal(gpu_tasks[gpu_tasks["sr"] < ns], want))}
         if not seed_check["equal"]:
             raise SystemExit(f"bench: GPU seeding differs from the host path on the first {ns} reads")
-        cpu, cpu_res = cpu_baseline(synth.with_seeds(d, gpu_tasks), args.cpu_lrs_per_worker)
+        cpu, cpu_res = cpu_baseline(synth.with_seeds(dt, gpu_tasks), args.cpu_lrs_per_worker)
         del gpu_tasks
         parity = check_parity(it, cpu_res)
     if rank != 0:
@@ -277,17 +345,18 @@ def main():
         return
     value = total_bases * args.steps / el / 1e6
     step_ms = el / args.steps * 1e3
+    task_ms = el_task / args.steps * 1e3
     dom_ms /= K
     dom_tops = dom_cells * OPS_PER_CELL / (dom_ms * 1e-3) / 1e12
     ext_ms /= K
     ext_tops = ext_cells * OPS_PER_CELL / (ext_ms * 1e-3) / 1e12 if ext_ms > 0 else 0.0
+    sw_stage_ms /= K
+    sw_cells /= K
     # pileup kernel: algorithmic bytes (SURVEY.md §8d model) / kernel time
     cns_bytes = sum_lseq + 4 * sum_ncig + 16 * n_aln + own_bases * (2 + 2 + 6 * 4 * 2)
     traffic = traffic_cns = traffic_ext = traffic_seed = None
     pmc_src = None
     prof = ROOT / PMC_FILE   # tools/pmc_summary.py of the rocprofv3 FETCH_SIZE / WRITE_SIZE passes
-    if not prof.exists():
-        prof = ROOT / "profiles" / "pmc_r05.json"
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())
@@ -303,20 +372,6 @@ def main():
                       f"{pm.get('_build', 'build not recorded')}"
         except Exception:
             traffic = traffic_cns = traffic_ext = traffic_seed = None
-    ref_cpu = None   # the reference's own Perl consensus, timed in the build container
-    rp = ROOT / "profiles" / "r03_reference_cpu_consensus.json"
-    if rp.exists():
-        try:
-            r3 = json.loads(rp.read_text())
-            rpl = r3["reference_perl"]
-            ref_cpu = {"value": rpl["Mbases_per_s"], "unit": "Mbases/s", "cores": rpl["processes"], "kind": "reference",
-                       "scope": "consensus only, build container", "cpu": r3["host"]["cpu"],
-                       "sample": r3["workload"] + f"; {rpl['engine']}; {rpl['wall_s']} s wall",
-                       "source": "profiles/r03_reference_cpu_consensus.json (tools/time_reference_r03.py)"}
-        except Exception:
-            ref_cpu = None
-    # the step without the index build and the seeding (the round-4 headline's scope)
-    step_only_ms = wall_ms.get("sw_exchange", 0) + wall_ms.get("consensus_mask_commit", 0)
     out = {
         "metric": "corrected long-read Mbases/sec per node",
         "value": round(value, 3),
@@ -329,24 +384,34 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic: iid genome, CLR-like long reads (15 % error), 150 bp short reads in sequencer order; "
-                "the same dataset on every rank",
+        "data": "synthetic: iid genome, CLR-like long reads (15 % error), 50x 150 bp short reads in sequencer order, "
+                "sampled per task by SeqChunker's chunk rule; the same dataset on every rank",
         "config": {
             "workload": "configs[1] per GPU: 4.6 Mb genome, 13,800 x 10 kb long reads (30x, 15% error), "
-                        "50x 2x150 short reads sampled to 15x; one whole bwa-sr-1 task per step (index, seeding, "
-                        "SW, exchange, -b/-l, consensus, masking, commit)",
+                        "50x 2x150 short reads; one whole sr-noccs correction run per step (read-long's output "
+                        "restored in HBM, bwa-sr-1..N with mask_shortcut_frac, bwa-sr-finish)",
             "genome_bp": gl, "long_reads": n_lr, "long_read_bases": int(lr_off[-1]), "short_reads": n_sr,
-            "owned_long_reads": hi - lo, "short_read_shard": s1 - s0, "seeds": n_seeds,
-            "alignments_received": int(n_recv), "task": "bwa-sr-1", "coverage_cap": params.coverage,
+            "owned_long_reads": hi - lo, "mode": mode,
             "parallelism": f"exact-parity layout x{world}: every rank indexes all {n_lr} long reads, seeds and aligns "
-                           f"1/{world} of the short reads, alignments all-to-all to the long reads' owners over RCCL "
-                           f"(pr_aln_exchange), corrected reads all-gathered (pr_lrset_commit)",
+                           f"1/{world} of each task's short-read sample, alignments all-to-all to the long reads' "
+                           f"owners over RCCL (pr_aln_exchange), corrected reads all-gathered (pr_lrset_commit)",
         },
-        "value_step": round(total_bases / (step_only_ms * 1e-3) / 1e6, 3) if step_only_ms else None,
-        "step_wall_ms": wall_ms,
+        "loop": {"tasks": loop_rows, "device_ms": round(loop_dev_ms, 1), "chimera_lines": n_chim,
+                 "same_task_list_every_step": same_tasks,
+                 "repeat_identical": (first_digest == last_digest) if first_digest is not None else None,
+                 "final_reads_sha256": last_digest},
+        "value_task": round(total_bases / (task_ms * 1e-3) / 1e6, 3),
+        "task": {"name": "bwa-sr-1", "ms": round(task_ms, 3), "short_reads": n1, "short_read_shard": s1 - s0,
+                 "seeds": n_seeds, "alignments_received": int(n_recv), "coverage_cap": params1.coverage,
+                 "wall_ms": {k: round(v / K * 1e3, 2) for k, v in wall.items()}},
         "stage_event_ms": {k: round(v, 3) for k, v in zip(("index", "seeding", "sw_extend", "sw_global_cigar",
                                                             "exchange_handoff", "consensus"), ev)},
-        "sw_gcups": round((ce + cg) / ((me + mg) * 1e-3) / 1e9, 2) if me + mg > 0 else None,
+        "sw_gcups": round(sw_cells / (sw_stage_ms * 1e-3) / 1e9, 2) if sw_stage_ms > 0 else None,
+        "sw_gcups_note": "DP cells of every extension and CIGAR launch of the bwa-sr-1 task (unpruned band, SURVEY.md "
+                         "§8d) / the SW stage's device time (HIP events: extension rounds incl. the bwa-mode walk and "
+                         "final passes, then the CIGAR pass)",
+        "sw_gcups_kernels": round((ext_cells + dom_cells) / ((ext_ms + dom_ms) * 1e-3) / 1e9, 2)
+        if ext_ms + dom_ms > 0 else None,
         "bwa": {"rounds": bwa_rounds, "seeds_extended": bwa_ext, "patches": bwa_patch},
         "cigar_kernel_phase_share": {k: round(v / max(sum(pc), 1), 3) for k, v in
                                      zip(("masks", "dp", "backtrack", "emit"), pc)},
@@ -368,7 +433,7 @@ def main():
             "alignments": int(n_aln), "traffic": traffic_cns, "launch_ms": round(ev[5], 3),
         },
         "roofline_extension": {
-            "kernels": "every ksw_extend2 DP launch of the step (sw_ext_pk_kernel<40>, sw_ext_phase_kernel<*>, wide), "
+            "kernels": "every ksw_extend2 DP launch of the task (sw_ext_pk_kernel<40>, sw_ext_phase_kernel<*>, wide), "
                        "all bwa-mode rounds, both sides and band tries",
             "bound": "valu", "achieved": round(ext_tops, 3), "peak": round(VALU_PEAK_TOPS, 2), "unit": "TOP/s (int32)",
             "frac": round(ext_tops / VALU_PEAK_TOPS, 4), "summed_launch_ms": round(ext_ms, 3),
@@ -378,13 +443,12 @@ def main():
         },
         "roofline_seeding": seeding_roofline(ev[1], s1 - s0, traffic_seed, n_seeds),
         "cpu_baseline": cpu,
-        "cpu_baseline_reference": ref_cpu,
+        "cpu_baseline_reference": reference_cpu(),
         "comm": "rccl" if cm is not None else "none",
         "seed_parity_vs_host": seed_check,
         "gen_s": round(gen_s, 1),
         "upload_s": round(upload_s, 2),
         "reads_ok": ok,
-        "iteration_stat": {"bpt": bpt, "bpN": bpn, "masked_frac": round(bpn / bpt, 4) if bpt else None},
         "parity": parity,
     }
     print(json.dumps(out), file=_JSON_OUT, flush=True)
@@ -392,6 +456,8 @@ def main():
         cm.close()
     if parity is not None and parity["mismatches"]:
         raise SystemExit(f"bench: {parity['mismatches']} of {parity['checked_reads']} reads differ from the CPU chain")
+    if first_digest is not None and first_digest != last_digest:
+        raise SystemExit("bench: the correction run's output differs between steps")
 
 
 def lrs_index_ms(L, ctx) -> float:

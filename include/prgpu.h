@@ -514,7 +514,8 @@ typedef struct pr_own_batch {
     int32_t from_set;             /* PR_OWN_FROM_SET: reference and qualities from the resident
                                    * long-read set (pr_lrset_*; ref_seq / lr_qual ignored);
                                    * | PR_OWN_RESIDENT_SR: the short reads are the resident ones
-                                   * (pr_srset_load, sr_seq NULL; no upload per task)          */
+                                   * (pr_srset_load, or the task sample of pr_srset_sample;
+                                   * sr_seq NULL; no upload per task)                          */
 } pr_own_batch;
 enum { PR_OWN_FROM_SET = 1, PR_OWN_RESIDENT_SR = 2 };
 int pr_iter_upload_owned(pr_ctx *ctx, const pr_own_batch *b);
@@ -545,6 +546,12 @@ int pr_lrset_index(pr_ctx *ctx, int which);
 int pr_iter_upload_lrset(pr_ctx *ctx, const pr_sw_batch *b);
 int pr_lrset_commit(pr_ctx *ctx, pr_comm *comm, int flags);
 int pr_lrset_download(pr_ctx *ctx, int64_t *off, uint8_t *seq, uint8_t *qual, uint8_t *map);
+/* pr_lrset_snapshot: a device copy of the set's current reads and qualities (the read-long
+ * output); pr_lrset_restore: the set returns to it, the mapping reference to the reads -- a
+ * correction run restarted on the same input without a host round trip (bench.py: every step
+ * runs the whole loop, bin/proovread:705-905, from the raw long reads) */
+int pr_lrset_snapshot(pr_ctx *ctx);
+int pr_lrset_restore(pr_ctx *ctx);
 /* The resident short reads: the whole short-read input (nt4, in stream order) once; a task's
  * sample -- SeqChunker's chunks are contiguous record ranges (bin/proovread:2085-2102) -- is then
  * gathered on the device from ranges[2k], ranges[2k+1] (records [r0, r1)) and seeded as
@@ -552,6 +559,13 @@ int pr_lrset_download(pr_ctx *ctx, int64_t *off, uint8_t *seq, uint8_t *qual, ui
  * pr_iter_upload_lrset with sr_seq NULL takes them). */
 int pr_srset_load(pr_ctx *ctx, int64_t n_sr, const int64_t *off, const uint8_t *seq);
 int pr_seed_gpu_map_sampled(pr_ctx *ctx, const pr_seed_opts *o, const int64_t *ranges, int n_ranges, int32_t *status);
+/* The task's whole sample of the resident short reads (ranges as above), gathered on the device
+ * for the consensus of an owned batch: with ranks each seeds only its shard of the sample
+ * (pr_seed_gpu_map_sampled over the shard's ranges), while the alignments it receives name any
+ * read of the sample.  PR_OWN_RESIDENT_SR then reads this sample (its sr_off must equal the
+ * sample's offsets, checked element by element); without a sample, the whole resident set.
+ * pr_srset_load clears the sample. */
+int pr_srset_sample(pr_ctx *ctx, const int64_t *ranges, int n_ranges);
 
 /* enqueue (ctx stream) the per-iteration statistic of the resident consensus:
  * dev_out[0] = corrected bases, dev_out[1] = bases with phred >= min_phred.

@@ -251,6 +251,11 @@ def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers
     ob.aln_lib()
     workers = workers or min(16, os.cpu_count() or 1)
     lrs = list(lrs)
+    if workers > 1 and _hip_in_process():   # never fork a process that holds a HIP runtime
+        return _run_in_child(d, lrs, dict(task=task, coverage=coverage, use_ref_qual=use_ref_qual, workers=workers,
+                                          ref_seq=ref_seq, ref_qual=ref_qual, detect_chimera=detect_chimera,
+                                          full=full, bin_filter=bin_filter, drop_ratio=drop_ratio,
+                                          sam_only=sam_only))
     bases = int(sum(int(d.lr_off[i + 1] - d.lr_off[i]) for i in lrs))
     bwa = getattr(d, "t_chain", None) is not None
     _RECS = None
@@ -273,8 +278,7 @@ def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers
         if workers == 1:
             per_read = [_sr_records(r) for r in reads]
         else:
-            with mp.get_context("fork").Pool(workers, initializer=_init_worker) as pool:
-                per_read = pool.map(_sr_records, reads, chunksize=64)
+            per_read = _pool_map(_sr_records, reads, workers, 64)
         _RECS = {i: [] for i in lrs}
         for recs in per_read:   # read order, then SAM order inside a read
             for lr, rec in recs:
@@ -284,6 +288,81 @@ def run_sample(d, lrs, task="bwa-sr", coverage=11.25, use_ref_qual=True, workers
     if workers == 1:
         res = [fn(i) for i in lrs]
     else:
-        with mp.get_context("fork").Pool(workers, initializer=_init_worker) as pool:
-            res = pool.map(fn, lrs, chunksize=1)
+        res = _pool_map(fn, lrs, workers, 1)
     return time.perf_counter() - t, bases, res, workers
+
+
+def _pool_map(fn, items, workers: int, chunksize: int):
+    """fn over items on forked workers (they inherit the module's dataset).  A worker that dies
+    breaks the pool and raises here (concurrent.futures' BrokenProcessPool) instead of being
+    replaced silently.  Only called in a process without a HIP runtime (run_sample)."""
+    from concurrent.futures import ProcessPoolExecutor
+    with ProcessPoolExecutor(workers, mp_context=mp.get_context("fork"), initializer=_init_worker) as ex:
+        return list(ex.map(fn, items, chunksize=chunksize))
+
+
+def _hip_in_process() -> bool:
+    """Whether this process has loaded the HIP runtime (a GPU test's pytest process): forking it
+    is unsafe, so the worker pool then runs in a fresh child process (_run_in_child)."""
+    try:
+        with open("/proc/self/maps") as f:
+            return any("libamdhip64" in ln for ln in f)
+    except OSError:
+        return False
+
+
+_DATA_KEYS = ("lr_seq", "lr_off", "sr_seq", "sr_off", "t_sr", "t_lr", "t_strand", "t_qbeg", "t_rbeg", "t_slen",
+              "t_chain")
+
+
+def _run_in_child(d, lrs, kw):
+    """run_sample in a fresh Python process (no HIP runtime there, so it may fork its workers):
+    the dataset goes through .npy files (memory-mapped by the child), the results come back as
+    JSON."""
+    import json
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory(prefix="cpu_chain_") as td:
+        tdp = Path(td)
+        meta = {"lrs": [int(x) for x in lrs], "kw": {}, "arrays": [], "lr_names": None}
+        for k in _DATA_KEYS:
+            v = getattr(d, k, None)
+            if v is not None:
+                np.save(tdp / f"{k}.npy", np.ascontiguousarray(v))
+                meta["arrays"].append(k)
+        if hasattr(d, "lr_names"):
+            meta["lr_names"] = list(d.lr_names)
+        for k, v in kw.items():
+            if isinstance(v, np.ndarray):
+                np.save(tdp / f"kw_{k}.npy", np.ascontiguousarray(v))
+                meta["kw"][k] = {"npy": f"kw_{k}.npy"}
+            else:
+                meta["kw"][k] = {"value": list(v) if isinstance(v, tuple) else v}
+        (tdp / "meta.json").write_text(json.dumps(meta))
+        subprocess.run([sys.executable, str(Path(__file__).resolve()), "--child", td], check=True)
+        out = json.loads((tdp / "out.json").read_text())
+    res = [tuple(r) if isinstance(r, list) and not kw.get("sam_only") else r for r in out["res"]]
+    return out["wall"], out["bases"], res, out["workers"]
+
+
+def _child_main(td: str) -> None:
+    import json
+    from types import SimpleNamespace
+    tdp = Path(td)
+    meta = json.loads((tdp / "meta.json").read_text())
+    d = SimpleNamespace(**{k: np.load(tdp / f"{k}.npy", mmap_mode="r") for k in meta["arrays"]})
+    d.n_lr, d.n_sr = len(d.lr_off) - 1, len(d.sr_off) - 1
+    if meta["lr_names"] is not None:
+        d.lr_names = meta["lr_names"]
+    kw = {}
+    for k, v in meta["kw"].items():
+        if "npy" in v:
+            kw[k] = np.load(tdp / v["npy"])
+        else:
+            kw[k] = tuple(v["value"]) if k in ("task", "bin_filter") and isinstance(v["value"], list) else v["value"]
+    wall, bases, res, workers = run_sample(d, meta["lrs"], **kw)
+    (tdp / "out.json").write_text(json.dumps({"wall": wall, "bases": bases, "res": res, "workers": workers}))
+
+
+if __name__ == "__main__" and len(sys.argv) == 3 and sys.argv[1] == "--child":
+    _child_main(sys.argv[2])

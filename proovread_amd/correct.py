@@ -194,6 +194,30 @@ class ShortReads:
             self.pool = NT4[self.pool]
         self.lengths = np.diff(self.off)
 
+    @classmethod
+    def from_pool(cls, pool: np.ndarray, off: np.ndarray, chunk_number: int = 1000) -> "ShortReads":
+        """The reads of an nt4 pool as the FASTQ stream `@sr<i>` / sequence / `+` / quality
+        records would hold them (SeqChunker chunks by byte offset), without building the bytes."""
+        self = cls.__new__(cls)
+        self.data = None
+        off = np.ascontiguousarray(off, np.int64)
+        n = len(off) - 1
+        lens = np.diff(off)
+        digits = np.ones(n, np.int64)
+        for k in range(1, 20):
+            digits += np.arange(n) >= 10 ** k
+        rec = (4 + digits) + lens + 1 + 2 + lens + 1    # "@sr<i>\n" seq "\n+\n" qual "\n"
+        starts = np.zeros(n, np.int64)
+        if n:
+            np.cumsum(rec[:-1], out=starts[1:])
+        total = int(rec.sum())
+        self.n_chunks = max(1, chunk_number)
+        csize = max(1, math.ceil(total / self.n_chunks)) if total else 1
+        chunk_of = np.minimum(starts // csize, self.n_chunks - 1)
+        self.cfirst = np.searchsorted(chunk_of, np.arange(self.n_chunks + 1), side="left").astype(np.int64)
+        self.pool, self.off, self.lengths = pool, off, lens
+        return self
+
     @staticmethod
     def _seq_of(rec: bytes) -> bytes:
         if rec[:1] == b">":
@@ -284,6 +308,22 @@ class GpuStages:
         self.ids: List[str] = []
 
     device_short_reads = True   # world 1: a task's sample is gathered on the device (pr_srset_*)
+    device_short_reads_exact = True   # ... and in the exact-parity layout (pr_srset_sample)
+
+    def snapshot(self) -> None:
+        """Keep the loaded long reads on the device (pr_lrset_snapshot) for restore()."""
+        from . import _abi
+        L = _abi.lib()
+        L.pr_lrset_snapshot.argtypes = [C.c_void_p]
+        _abi.check(L.pr_lrset_snapshot(self.ctx.h), "pr_lrset_snapshot")
+
+    def restore(self) -> None:
+        """The set back to the snapshot's reads, the mapping reference to the reads
+        (pr_lrset_restore): the state right after read-long, without a host round trip."""
+        from . import _abi
+        L = _abi.lib()
+        L.pr_lrset_restore.argtypes = [C.c_void_p]
+        _abi.check(L.pr_lrset_restore(self.ctx.h), "pr_lrset_restore")
 
     def load(self, reads: LongReads) -> None:
         from . import iteration
@@ -301,7 +341,7 @@ class GpuStages:
                    "pr_srset_load")
 
     def task(self, task: str, sr: Optional[np.ndarray], sr_off: np.ndarray, params, bin_filter, comm=None,
-             exact: bool = False, mask_cfg=None, sr_ranges: Optional[np.ndarray] = None) -> TaskOut:
+             exact: bool = False, mask_cfg=None, sr_ranges: Optional[np.ndarray] = None, dry: bool = False) -> TaskOut:
         """One bwa-sr task on the resident set.  mask_cfg = (hcr-mask, min_sr_length) for the
         regular tasks, None for the finish task (which maps to the unmasked reads,
         proovread:838-850); exact: the multi-GPU exact-parity layout."""
@@ -332,13 +372,25 @@ class GpuStages:
             s, e = ex.sr_range(n_sr, world, rank)
             bounds = ex.lr_bounds(lr_off, world)
             lo, hi = int(bounds[rank]), int(bounds[rank + 1])
-            a0, a1 = int(sr_off[s]), int(sr_off[e])
-            seed._map_gpu(L, self.ctx, sr[a0:a1], np.asarray(sr_off[s:e + 1]) - a0, seed_opts, False,
-                          keep_on_device=True)
+            if sr is None:   # the resident short reads: the shard's records gathered on the device
+                rg = np.ascontiguousarray(sr_ranges, np.int64).reshape(-1, 2)
+                sub = np.ascontiguousarray(sample_subranges(rg, s, e), np.int64)
+                st = np.zeros(max(1, e - s), np.int32)
+                _abi.check(L.pr_seed_gpu_map_sampled(self.ctx.h, C.byref(seed_opts), _abi.ptr(sub, C.c_int64), len(sub),
+                                                     _abi.ptr(st, C.c_int32)), "pr_seed_gpu_map_sampled")
+            else:
+                a0, a1 = int(sr_off[s]), int(sr_off[e])
+                seed._map_gpu(L, self.ctx, sr[a0:a1], np.asarray(sr_off[s:e + 1]) - a0, seed_opts, False,
+                              keep_on_device=True)
             iteration.ShardSW(self.ctx, sr, sr_off, s, e, None, lr_off, device_pools=True).launch(opts)
             iteration.exchange(self.ctx, comm, s, bounds)
-            it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, None, None, sr if world > 1 else None, sr_off,
-                                          from_set=True)
+            if sr is None:   # the consensus reads any short read of the sample: gathered on the device once
+                _abi.check(L.pr_srset_sample(self.ctx.h, _abi.ptr(rg, C.c_int64), len(rg)), "pr_srset_sample")
+                it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, None, None, None, sr_off, from_set=True,
+                                              resident_sr=True)
+            else:
+                it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, None, None, sr if world > 1 else None, sr_off,
+                                              from_set=True)
         n_tasks = seed._count(L, self.ctx)
         self.device_ms += seed._last_ms(L.pr_seed_gpu_last_ms, self.ctx)
         it.launch(opts, params)
@@ -352,7 +404,7 @@ class GpuStages:
             st = self._stats.download(np.int64)
             out.bpt, out.bpn = int(st[0]), int(st[1])
         self.device_ms += sum(it.timing())
-        self.lrs.commit(comm if exact else None, with_mask=not finish)
+        self.lrs.commit(comm if exact else None, with_mask=not finish, dry=dry)   # dry: the set stays (bench.py)
         self.last_iteration = it   # the task's consensus outputs stay readable (tests, drivers)
         return out
 
@@ -364,6 +416,20 @@ class GpuStages:
         """The mapping reference of the next task (LR.masked.fa)."""
         off, _, _, m = self.lrs.download(seq=False, qual=False, mapping=True)
         return _split(m, off)
+
+
+def sample_subranges(ranges: np.ndarray, s: int, e: int) -> np.ndarray:
+    """The record ranges of reads [s, e) of a sample made of `ranges` ([k, 2] record ranges of
+    the whole short-read stream, in sample order)."""
+    out = []
+    at = 0
+    for a, b in np.asarray(ranges, np.int64).reshape(-1, 2).tolist():
+        n = b - a
+        lo, hi = max(s, at), min(e, at + n)
+        if hi > lo:
+            out.append((a + lo - at, a + hi - at))
+        at += n
+    return np.array(out, np.int64).reshape(-1, 2)
 
 
 def _seed_tasks(lr_map, lr_off, sr, sr_off, seed_opts, threads):
@@ -417,33 +483,49 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
     FASTQ/FASTA stream; returns the finish task's reads and chimera lines and a log per task.
     With `comm` (world > 1) every rank calls run() on the same inputs and gets the same
     result; the work is split as Comm describes.  n_tasks in the log is the rank's share."""
-    from . import cns
     cfg = cfg or LoopConfig()
     stages = stages or GpuStages()
     srs = ShortReads(sr_data)
     min_sr = cfg.min_sr_length or (int(srs.lengths.min()) if len(srs.lengths) else 200)
     stubby = cfg.lr_min_length if cfg.lr_min_length is not None else 2 * min_sr
-    sampler = control.Sampler(sampling=cfg.sampling)
     mode = cfg.mode or T.mode_for(min_sr)
     tasks = list(cfg.tasks or T.MODE_TASKS[mode])
-    fracs: List[float] = []
-    log: List[TaskLog] = []
     ids: List[str] = []
     ignored: List[str] = []
+    log: List[TaskLog] = []
+    if tasks and tasks[0] == "read-long":   # proovread:705 (the first task of every mode)
+        reads, ignored = read_long(lr_records, stubby)
+        ids = reads.ids
+        stages.load(reads)    # the mapping reference starts as the reads (.masked.fa)
+        if hasattr(stages, "load_short_reads"):
+            stages.load_short_reads(srs)
+        log.append(TaskLog("read-long"))
+        tasks = tasks[1:]
+    chim, last_masked, tlog = run_tasks(stages, srs, tasks, cfg, mode, min_sr, bool(ids), comm)
+    log += tlog
+    reads = stages.reads() if ids else LongReads([], [], [])
+    if cfg.keep_masked and last_masked is None and ids:
+        last_masked = stages.masked()
+    return LoopResult(reads, chim, ignored, log, last_masked)
+
+
+def run_tasks(stages, srs: ShortReads, tasks: List[str], cfg: LoopConfig, mode: str, min_sr: int, have_reads: bool,
+              comm=None, sampler: Optional[control.Sampler] = None) -> Tuple[List[str], Optional[List[bytes]], List[TaskLog]]:
+    """The bwa-sr / bwa-mr tasks of the loop after read-long (bin/proovread:705-905) on the
+    stages' resident long reads: per task SeqChunker sampling, the task on the stages, the
+    {bpt, bpN} statistic (all-reduced over ranks) and mask_shortcut_frac's splice of the task
+    list.  -> (chimera lines of the finish task, the masked reads kept by cfg.keep_masked or
+    None, a log per task)."""
+    from . import cns
+    sampler = sampler or control.Sampler(sampling=cfg.sampling)
+    tasks = list(tasks)
+    fracs: List[float] = []
+    log: List[TaskLog] = []
     chim: List[str] = []
     last_masked = None
     tc = 0
     while tc < len(tasks):   # proovread:705 (tasks may shrink: mask_shortcut_frac splices)
         task = tasks[tc]
-        if task == "read-long":
-            reads, ignored = read_long(lr_records, stubby)
-            ids = reads.ids
-            stages.load(reads)    # the mapping reference starts as the reads (.masked.fa)
-            if hasattr(stages, "load_short_reads"):
-                stages.load_short_reads(srs)
-            log.append(TaskLog(task))
-            tc += 1
-            continue
         if not (task.startswith("bwa-sr") or task.startswith("bwa-mr")):
             raise ValueError(f"task {task} is outside the sr / mr loops")
         finish = task.endswith("-finish")
@@ -453,8 +535,9 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         task_cov = sr_coverage_for(task)
         multi = comm is not None and comm.world > 1
         ranges, sr_off = srs.sample_ranges(sampler.cov2seqchunker(cfg.coverage, task_cov))
-        # device stages at world 1: the sample is gathered from the resident short reads on the device
-        on_dev = bool(getattr(stages, "device_short_reads", False)) and not (multi or cfg.exact_layout)
+        # device stages: the sample is gathered from the resident short reads on the device
+        on_dev = bool(getattr(stages, "device_short_reads", False)) and \
+            (not (multi or cfg.exact_layout) or bool(getattr(stages, "device_short_reads_exact", False)))
         sr = None if on_dev else srs.gather(ranges)
         ent.n_sr = len(sr_off) - 1
         max_cov = min(cfg.coverage, task_cov) * cfg.coverage_scale_factor     # proovread:1541
@@ -466,7 +549,8 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
         if finish and cfg.keep_masked:
             last_masked = stages.masked()
         r = stages.task(task, sr, sr_off, params, binf, comm, multi or cfg.exact_layout,
-                        None if finish else (hcr_mask_for(task), min_sr), sr_ranges=ranges) if ids else TaskOut(0, [])
+                        None if finish else (hcr_mask_for(task), min_sr), sr_ranges=ranges) if have_reads \
+            else TaskOut(0, [])
         ent.n_tasks = r.n_tasks
         lines, bpt, bpn = r.chim, r.bpt, r.bpn
         if multi:
@@ -485,10 +569,7 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
             ent.device_ms = round(stages.device_ms - dev0, 1)
         log.append(ent)
         tc += 1
-    reads = stages.reads() if ids else LongReads([], [], [])
-    if cfg.keep_masked and last_masked is None and ids:
-        last_masked = stages.masked()
-    return LoopResult(reads, chim, ignored, log, last_masked)
+    return chim, last_masked, log
 
 
 # ---------------------------------------------------------------------------- outputs

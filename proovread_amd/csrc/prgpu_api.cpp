@@ -195,7 +195,11 @@ enum SeedBufId {
 // indices, counts, op prefix, send / receive records and CIGAR ops, grouped hand-off inputs,
 // the task's short reads
 // the resident long-read set: pools, the dense offsets of a commit, the commit's staging pools
-enum LrSetBufId { LS_SEQ, LS_QUAL, LS_MAP, LS_OFF, LS_TSEQ, LS_TQUAL, LS_TMAP, LS_SRSEQ, LS_GSEQ, LS_GQUAL, LS_GMAP, LS_COUNT };
+// (LS_RSEQ / LS_RQUAL: pr_lrset_snapshot's raw reads; LS_SRSAMP: pr_srset_sample's task sample)
+enum LrSetBufId {
+    LS_SEQ, LS_QUAL, LS_MAP, LS_OFF, LS_TSEQ, LS_TQUAL, LS_TMAP, LS_SRSEQ, LS_GSEQ, LS_GQUAL, LS_GMAP, LS_RSEQ, LS_RQUAL,
+    LS_SRSAMP, LS_COUNT
+};
 enum XchgBufId {
     XB_BOUNDS, XB_KEY0, XB_KEY1, XB_IDX0, XB_IDX1, XB_CNT, XB_OPIN, XB_OPAT, XB_SREC, XB_SCIG, XB_TEMP,
     XB_RREC, XB_RCIG, XB_RCIGAT, XB_GCNT, XB_GCNT64, XB_TASKOFF, XB_ERR, XB_GSR, XB_GSTATUS, XB_GPOS, XB_GSCORE,
@@ -253,6 +257,8 @@ struct pr_ctx {
     int32_t ls_n = -1;
     bool ls_map_is_reads = true;
     std::vector<int64_t> ss_off;   // the resident short reads (pr_srset_load): offsets on the host
+    std::vector<int64_t> ss_samp_off;   // pr_srset_sample's task sample (LS_SRSAMP), empty: none
+    std::vector<int64_t> ls_raw_off;    // pr_lrset_snapshot's offsets, empty: none
     bool seed_sr_staged = false;   // SB_SEQ already holds the reads of the next pr_seed_gpu_map
     bool own = false;            // the resident iteration batch is an owned batch (pr_iter_upload_owned)
     bool own_ref_nt4 = false;    // its consensus reference is the SW long-read pool's slice (nt4)
@@ -575,7 +581,8 @@ extern "C" int pr_cns_launch(pr_ctx *c, const pr_cns_params *p) {
         // the received wire pool, the ASCII consensus reference of the owned reads
         D.ref_seq = B[CB_REF_SEQ].as<uint8_t>();
         D.ref_nt4 = c->own_ref_nt4 ? 1 : 0;
-        D.seq = c->own_sr_resident ? c->ls[LS_SRSEQ].as<uint8_t>() : c->xb[XB_SR].as<uint8_t>();
+        D.seq = c->own_sr_resident ? c->ls[c->ss_samp_off.empty() ? LS_SRSEQ : LS_SRSAMP].as<uint8_t>()
+                                   : c->xb[XB_SR].as<uint8_t>();
         D.seq_nt4 = 1;
         D.cig = c->xb[XB_RCIG].as<uint32_t>();
         if (c->x_pass) {   // world 1: CIGARs in place in the SW output pool
@@ -986,7 +993,11 @@ extern "C" int pr_aln_exchange(pr_ctx *c, pr_comm *comm, int64_t sr0, const int6
         nc += rc_cig[(size_t)r];
         c->x_from[(size_t)r] = rc_rec[(size_t)r] / (int64_t)sizeof(XRec);
     }
-    if ((rc = xchg_recv_buffers(c, nr, nc))) return rc;
+    rc = xchg_recv_buffers(c, nr, nc);
+    // the receive buffers are a local allocation: a rank that could not get them must not leave
+    // the others inside the all-to-all
+    if (comm) rc = pr_comm_agree(comm, rc);
+    if (rc) return rc;
     DevBuf *B = c->xb;
     if (comm) {
         if ((rc = pr_comm_alltoallv_dev(comm, B[XB_SREC].p, sc_rec.data(), B[XB_RREC].p, rc_rec.data())) ||
@@ -1137,10 +1148,14 @@ extern "C" int pr_iter_upload_owned(pr_ctx *c, const pr_own_batch *b) {
     }
     if ((rc = upload(c->xb[XB_SROFF], b->sr_off, (size_t)b->n_sr + 1, s))) return rc;
     c->own_sr_resident = sr_res;
-    if (sr_res) {   // the resident short reads (pr_srset_load) are the task's: read in place
+    if (sr_res) {   // the resident short reads (pr_srset_load, or the task sample) are the task's: read in place
         if (b->sr_seq) return set_error(PR_ERR_ARG, "PR_OWN_RESIDENT_SR: sr_seq must be NULL");
-        if (c->ss_off.size() != (size_t)b->n_sr + 1 || (b->n_sr && c->ss_off.back() != b->sr_off[b->n_sr]))
-            return set_error(PR_ERR_ARG, "PR_OWN_RESIDENT_SR: the resident short reads (pr_srset_load) differ");
+        const std::vector<int64_t> &ro = c->ss_samp_off.empty() ? c->ss_off : c->ss_samp_off;
+        // every offset, not only the count and total: a batch with another per-read layout of the
+        // same size would read the wrong bases
+        if (ro.size() != (size_t)b->n_sr + 1 || !std::equal(ro.begin(), ro.end(), b->sr_off))
+            return set_error(PR_ERR_ARG, "PR_OWN_RESIDENT_SR: sr_off differs from the resident short reads (pr_srset_load / "
+                                         "pr_srset_sample)");
     } else if (b->sr_seq) {
         if ((rc = upload(c->xb[XB_SR], b->sr_seq, (size_t)b->sr_off[b->n_sr], s))) return rc;
     } else {
@@ -1694,6 +1709,40 @@ extern "C" int pr_lrset_load(pr_ctx *c, int32_t n_lr, const int64_t *off, const 
     return 0;
 }
 
+extern "C" int pr_lrset_snapshot(pr_ctx *c) {
+    if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t nb = (size_t)c->ls_off.back();
+    int rc;
+    if ((rc = c->ls[LS_RSEQ].ensure(nb + 1)) || (rc = c->ls[LS_RQUAL].ensure(nb + 1))) return rc;
+    if (nb) {
+        HIPCHK(hipMemcpyAsync(c->ls[LS_RSEQ].p, c->ls[LS_SEQ].p, nb, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->ls[LS_RQUAL].p, c->ls[LS_QUAL].p, nb, hipMemcpyDeviceToDevice, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    c->ls_raw_off = c->ls_off;
+    return 0;
+}
+
+extern "C" int pr_lrset_restore(pr_ctx *c) {
+    if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
+    if (c->ls_raw_off.empty()) return set_error(PR_ERR_ARG, "no snapshot of the long-read set (pr_lrset_snapshot)");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    const size_t nb = (size_t)c->ls_raw_off.back();
+    int rc;
+    if ((rc = c->ls[LS_SEQ].ensure(nb + 1)) || (rc = c->ls[LS_QUAL].ensure(nb + 1))) return rc;
+    if (nb) {   // stream-ordered after every launch that read the set
+        HIPCHK(hipMemcpyAsync(c->ls[LS_SEQ].p, c->ls[LS_RSEQ].p, nb, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(c->ls[LS_QUAL].p, c->ls[LS_RQUAL].p, nb, hipMemcpyDeviceToDevice, s));
+    }
+    c->ls_off = c->ls_raw_off;
+    c->ls_n = (int32_t)c->ls_off.size() - 1;
+    c->ls_map_is_reads = true;   // read-long: the mapping reference is the reads themselves
+    return 0;
+}
+
 extern "C" int pr_lrset_info(pr_ctx *c, int32_t *n_lr, int64_t *bases) {
     if (!c || c->ls_n < 0) return set_error(PR_ERR_ARG, "no resident long-read set (pr_lrset_load)");
     if (n_lr) *n_lr = c->ls_n;
@@ -1785,14 +1834,19 @@ extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int flags) {
     for (int i = 0; i < n; ++i) doff[(size_t)i + 1] = doff[(size_t)i] + len[(size_t)i];
     const int64_t own = doff[(size_t)n];
     DevBuf *L = c->ls;
-    if ((rc = upload(L[LS_OFF], doff.data(), (size_t)n + 1, s)) || (rc = L[LS_TSEQ].ensure((size_t)own + 1)) ||
-        (rc = L[LS_TQUAL].ensure((size_t)own + 1)) || (with_mask && (rc = L[LS_TMAP].ensure((size_t)own + 1))))
-        return rc;
-    int e = lr_compact_launch(c->cb[CB_OUT_OFF].as<int64_t>(), c->cb[CB_SEQ_LEN].as<int32_t>(), L[LS_OFF].as<int64_t>(),
-                              n, c->cb[CB_O_SEQ].as<uint8_t>(), L[LS_TSEQ].as<uint8_t>(), c->cb[CB_O_QUAL].as<uint8_t>(),
-                              L[LS_TQUAL].as<uint8_t>(), with_mask ? c->mb[MB_OUT].as<uint8_t>() : nullptr,
-                              with_mask ? L[LS_TMAP].as<uint8_t>() : nullptr, (void *)s);
-    if (e) return set_error(PR_ERR_HIP, "long-read set compaction: %s", hipGetErrorString((hipError_t)e));
+    // the compaction's buffers and launch are local too: with ranks, agree again before the
+    // first collective so a rank that failed here does not leave the others inside it
+    if (!(rc = upload(L[LS_OFF], doff.data(), (size_t)n + 1, s)) && !(rc = L[LS_TSEQ].ensure((size_t)own + 1)) &&
+        !(rc = L[LS_TQUAL].ensure((size_t)own + 1)) && !(with_mask && (rc = L[LS_TMAP].ensure((size_t)own + 1)))) {
+        const int e = lr_compact_launch(c->cb[CB_OUT_OFF].as<int64_t>(), c->cb[CB_SEQ_LEN].as<int32_t>(),
+                                        L[LS_OFF].as<int64_t>(), n, c->cb[CB_O_SEQ].as<uint8_t>(), L[LS_TSEQ].as<uint8_t>(),
+                                        c->cb[CB_O_QUAL].as<uint8_t>(), L[LS_TQUAL].as<uint8_t>(),
+                                        with_mask ? c->mb[MB_OUT].as<uint8_t>() : nullptr,
+                                        with_mask ? L[LS_TMAP].as<uint8_t>() : nullptr, (void *)s);
+        if (e) rc = set_error(PR_ERR_HIP, "long-read set compaction: %s", hipGetErrorString((hipError_t)e));
+    }
+    if (world > 1) rc = pr_comm_agree(comm, rc);
+    if (rc) return rc;
     std::vector<int64_t> off((size_t)c->ls_n + 1, 0);
     if (world == 1) {
         if (!dry) {
@@ -1825,10 +1879,18 @@ extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int flags) {
         // dry: the same all-gathers into scratch pools, the set unchanged
         const int ids[3][2] = {{LS_TSEQ, dry ? LS_GSEQ : LS_SEQ}, {LS_TQUAL, dry ? LS_GQUAL : LS_QUAL},
                                {LS_TMAP, dry ? LS_GMAP : LS_MAP}};
-        for (int q = 0; q < (with_mask ? 3 : 2); ++q) {
-            if ((rc = L[ids[q][1]].ensure(tot + 1))) return rc;
-            if ((rc = pr_comm_allgatherv_dev(comm, L[ids[q][0]].p, bytes.data(), L[ids[q][1]].p))) return rc;
+        const int nq = with_mask ? 3 : 2;
+        // every gather target first, then one more agreement: no rank enters an all-gather that
+        // another cannot reach for want of memory
+        for (int q = 0; q < nq && !rc; ++q) rc = L[ids[q][1]].ensure(tot + 1);
+        rc = pr_comm_agree(comm, rc);
+        for (int q = 0; q < nq && !rc; ++q)
+            rc = pr_comm_allgatherv_dev(comm, L[ids[q][0]].p, bytes.data(), L[ids[q][1]].p);
+        if (dry) {   // the scratch pools of a dry commit are not kept (configs[3]: ~3 x 2.9 GB)
+            HIPCHK(hipStreamSynchronize(s));
+            for (int q = 0; q < nq; ++q) L[ids[q][1]].release();
         }
+        if (rc) return rc;
     }
     HIPCHK(hipStreamSynchronize(s));
     if (dry) return 0;
@@ -2121,6 +2183,34 @@ extern "C" int pr_srset_load(pr_ctx *c, int64_t n_sr, const int64_t *off, const 
     if (rc) return rc;
     HIPCHK(hipStreamSynchronize(c->stream));
     c->ss_off.assign(off, off + n_sr + 1);
+    c->ss_samp_off.clear();
+    c->ls[LS_SRSAMP].release();
+    return 0;
+}
+
+extern "C" int pr_srset_sample(pr_ctx *c, const int64_t *ranges, int n_ranges) {
+    if (!c || n_ranges < 0 || (n_ranges && !ranges)) return set_error(PR_ERR_ARG, "null arg");
+    if (c->ss_off.empty()) return set_error(PR_ERR_ARG, "no resident short reads (pr_srset_load)");
+    const int64_t N = (int64_t)c->ss_off.size() - 1;
+    std::vector<int64_t> off(1, 0);
+    for (int k = 0; k < n_ranges; ++k) {
+        const int64_t r0 = ranges[2 * k], r1 = ranges[2 * k + 1];
+        if (r0 < 0 || r1 < r0 || r1 > N) return set_error(PR_ERR_ARG, "record range outside the short reads");
+        for (int64_t i = r0; i < r1; ++i) off.push_back(off.back() + c->ss_off[(size_t)i + 1] - c->ss_off[(size_t)i]);
+    }
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    int rc = c->ls[LS_SRSAMP].ensure((size_t)off.back() + 1);
+    if (rc) return rc;
+    int64_t at = 0;
+    for (int k = 0; k < n_ranges; ++k) {
+        const int64_t b0 = c->ss_off[(size_t)ranges[2 * k]], b1 = c->ss_off[(size_t)ranges[2 * k + 1]];
+        if (b1 > b0)
+            HIPCHK(hipMemcpyAsync(c->ls[LS_SRSAMP].as<uint8_t>() + at, c->ls[LS_SRSEQ].as<uint8_t>() + b0, (size_t)(b1 - b0),
+                                  hipMemcpyDeviceToDevice, s));
+        at += b1 - b0;
+    }
+    c->ss_samp_off.swap(off);
     return 0;
 }
 

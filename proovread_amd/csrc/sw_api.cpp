@@ -907,6 +907,14 @@ extern "C" int pr_sw_run(pr_ctx *c, const pr_sw_opts *o, const pr_sw_batch *b, p
 extern "C" int pr_sw_last_timing(pr_ctx *c, double *ms_extend, double *ms_global) {
     if (!c) return pr_set_error(PR_ERR_ARG, "null ctx");
     SwResident &r = ctx_sw(c);
+    if (r.loaded && r.n_task) {   // from the launch's events (pipelines that never call pr_sw_download)
+        HIPCHK(hipSetDevice(ctx_device(c)));
+        HIPCHK(hipStreamSynchronize(ctx_stream(c)));
+        float a = 0.f, b = 0.f;
+        if (hipEventElapsedTime(&a, ctx_event(c, 2), ctx_event(c, 3)) == hipSuccess) r.ms_ext = a;
+        if (hipEventElapsedTime(&b, ctx_event(c, 3), ctx_event(c, 0)) == hipSuccess) r.ms_glob = b;
+        (void)hipGetLastError();
+    }
     if (ms_extend) *ms_extend = r.ms_ext;
     if (ms_global) *ms_global = r.ms_glob;
     return 0;

@@ -50,6 +50,9 @@ def _setup(L):
     from . import seed
     L.pr_srset_load.argtypes = [C.c_void_p, C.c_int64, _abi.P64, _abi.PU8]
     L.pr_seed_gpu_map_sampled.argtypes = [C.c_void_p, C.POINTER(seed.SeedOpts), _abi.P64, C.c_int, _abi.P32]
+    L.pr_srset_sample.argtypes = [C.c_void_p, _abi.P64, C.c_int]
+    L.pr_lrset_snapshot.argtypes = [C.c_void_p]
+    L.pr_lrset_restore.argtypes = [C.c_void_p]
     L._iter_ready = True
 
 

@@ -27,6 +27,7 @@ def fastq_bytes(seq, off):
     n = len(off) - 1
     L = int(off[1] - off[0])
     assert (np.diff(off) == L).all()
+    seq = seq[:int(off[-1])]
     heads = [b"@sr%d\n" % i for i in range(n)]
     hl = np.array([len(h) for h in heads], np.int64)
     rec = hl + L + 1 + 2 + L + 1
@@ -55,7 +56,10 @@ def main():
     scale = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
     out = sys.argv[2] if len(sys.argv) > 2 else None
     t = time.perf_counter()
-    d = synth.simulate(20261015 + 2, int(4_600_000 * scale), int(13_800 * scale), 10_000, 50.0)
+    # the bench's dataset: short reads in sequencer order (unsorted over the genome), as a FASTQ
+    # from a sequencing run is -- SeqChunker's contiguous chunks then sample the whole genome
+    gl = int(4_600_000 * scale)
+    d = synth.simulate_reads(20261015 + 2, gl, int(13_800 * scale), 10_000, int(round(50.0 * gl / 150)), threads=16)
     lrs = [(f"lr{i}", ACGT[d.lr_seq[d.lr_off[i]:d.lr_off[i + 1]]].tobytes(), None) for i in range(d.n_lr)]
     srd = fastq_bytes(d.sr_seq, d.sr_off)
     gen_s = time.perf_counter() - t

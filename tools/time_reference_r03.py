@@ -8,7 +8,7 @@ oracle chain (host seeding, oracle/aln_oracle.c + sw_oracle.c, -b 20 -l 300), co
 The worker is tests/golden/gen_cns_golden.pl (bam2cns's per-read loop over lib/Sam/Seq.pm
 without its samtools forks; Sam::Seq::alns returns arrival order for determinism).  The C
 oracle runs the same chunks and its outputs are compared with Perl's read by read.
-Needs /root/reference: build container only.  Writes profiles/r03_reference_cpu_consensus.json,
+Needs /root/reference: build container only.  Writes baselines/reference_cpu_consensus_r03.json,
 which bench.py reports as `cpu_baseline_reference`.
 
     python tools/time_reference_r03.py [n_long_reads] [workers]
@@ -45,7 +45,7 @@ def cpu_model():
 def main():
     n_lr = int(sys.argv[1]) if len(sys.argv) > 1 else 1600
     workers = int(sys.argv[2]) if len(sys.argv) > 2 else (os.cpu_count() or 1)
-    out = ROOT / "profiles" / "r03_reference_cpu_consensus.json"
+    out = ROOT / "baselines" / "reference_cpu_consensus_r03.json"
     import bench
     t = time.perf_counter()
     d = synth.simulate(20261015 + 2, 4_600_000, 13_800, 10_000, 50.0, sr_frac=0.3)   # bench.py, rank 0
