@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scale", type=float, default=1.0, help="fraction of the configs[1] workload per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--loop-only", action="store_true",
+                    help="profiling: the correction runs only (no value_task phase, no CPU baseline)")
     ap.add_argument("--cpu-lrs-per-worker", type=int, default=256)
     ap.add_argument("--comm", choices=("rccl", "none"), default="rccl",
                     help="rccl: the step all-reduces the device {bpt, bpN} statistic over an RCCL communicator at "
@@ -258,9 +260,19 @@ def main():
     log = logs[-1]
     loop_rows = [{"task": e.task, "short_reads": e.n_sr, "seeds_rank": e.n_tasks, "wall_ms": e.wall_ms,
                   "device_ms": e.device_ms, "masked_frac": None if e.masked_frac is None else round(e.masked_frac, 4),
-                  "shortcut": e.shortcut} for e in log]
+                  "shortcut": e.shortcut, "stage_event_ms": e.stage_ms} for e in log]
     same_tasks = all([e.task for e in lg] == [e.task for e in log] for lg in logs)
 
+    if args.loop_only:
+        if rank == 0:
+            print(json.dumps({"metric": "corrected long-read Mbases/sec per node", "value": round(
+                total_bases * args.steps / el / 1e6, 3), "unit": "Mbases/s", "n_gpus": world, "steps": args.steps,
+                "ms_per_step": round(el / args.steps * 1e3, 3), "loop": {"tasks": loop_rows,
+                                                                      "device_ms": round(loop_dev_ms, 1)}}),
+                  file=_JSON_OUT, flush=True)
+        if cm is not None:
+            cm.close()
+        return
     # ------------------------------------------------------------------ one bwa-sr-1 task (value_task)
     sampler = control.Sampler(sampling=cfg.sampling)
     rg1, off1 = srs.sample_ranges(sampler.cov2seqchunker(cfg.coverage, T.sr_coverage("bwa-sr-1")))
@@ -306,6 +318,7 @@ def main():
         el_task = cm.allreduce_floats([el_task], comm_mod.RED_MAX)[0]
     K = max(args.steps, 1)
     ev /= K
+    task_wall = {k: round(v / K * 1e3, 2) for k, v in wall.items()}
     n_seeds = seed._count(L, ctx)
     bwa_rounds, bwa_ext, bwa_patch = sw.bwa_stats(ctx)
     pc = sw.phase_cycles(ctx)
@@ -403,7 +416,7 @@ def main():
         "value_task": round(total_bases / (task_ms * 1e-3) / 1e6, 3),
         "task": {"name": "bwa-sr-1", "ms": round(task_ms, 3), "short_reads": n1, "short_read_shard": s1 - s0,
                  "seeds": n_seeds, "alignments_received": int(n_recv), "coverage_cap": params1.coverage,
-                 "wall_ms": {k: round(v / K * 1e3, 2) for k, v in wall.items()}},
+                 "wall_ms": task_wall},
         "stage_event_ms": {k: round(v, 3) for k, v in zip(("index", "seeding", "sw_extend", "sw_global_cigar",
                                                             "exchange_handoff", "consensus"), ev)},
         "sw_gcups": round(sw_cells / (sw_stage_ms * 1e-3) / 1e9, 2) if sw_stage_ms > 0 else None,

@@ -133,6 +133,7 @@ class TaskLog:
     shortcut: str = ""
     wall_ms: Optional[float] = None        # the task's wall time in run()
     device_ms: Optional[float] = None      # kernel time the device stages report (HIP events), if any
+    stage_ms: Optional[Dict[str, float]] = None   # ... per stage (index, seeding, SW, hand-off, consensus)
 
 
 @dataclasses.dataclass
@@ -349,7 +350,8 @@ class GpuStages:
         L = _abi.lib()
         seed._setup(L)
         finish = mask_cfg is None
-        self.device_ms += self.lrs.index(self.lrs.READS if finish else self.lrs.MAP)
+        ix_ms = self.lrs.index(self.lrs.READS if finish else self.lrs.MAP)
+        self.device_ms += ix_ms
         seed_opts, opts = T.options(task)
         if bin_filter:
             opts.bin_size, opts.bin_length = int(bin_filter[0]), float(bin_filter[1])
@@ -392,7 +394,8 @@ class GpuStages:
                 it = iteration.OwnedIteration(self.ctx, lo, hi, lr_off, None, None, sr if world > 1 else None, sr_off,
                                               from_set=True)
         n_tasks = seed._count(L, self.ctx)
-        self.device_ms += seed._last_ms(L.pr_seed_gpu_last_ms, self.ctx)
+        sd_ms = seed._last_ms(L.pr_seed_gpu_last_ms, self.ctx)
+        self.device_ms += sd_ms
         it.launch(opts, params)
         out = TaskOut(n_tasks, [])
         if finish:
@@ -403,7 +406,10 @@ class GpuStages:
             it.mask_to(self._stats.ptr, mask.params(mask_cfg[0], mask_cfg[1]))
             st = self._stats.download(np.int64)
             out.bpt, out.bpn = int(st[0]), int(st[1])
-        self.device_ms += sum(it.timing())
+        tm = it.timing()
+        self.device_ms += sum(tm)
+        self.last_stage_ms = {k: round(v, 2) for k, v in zip(("index", "seeding", "sw_extend", "sw_global_cigar",
+                                                               "exchange_handoff", "consensus"), (ix_ms, sd_ms, *tm))}
         self.lrs.commit(comm if exact else None, with_mask=not finish, dry=dry)   # dry: the set stays (bench.py)
         self.last_iteration = it   # the task's consensus outputs stay readable (tests, drivers)
         return out
@@ -567,6 +573,7 @@ def run_tasks(stages, srs: ShortReads, tasks: List[str], cfg: LoopConfig, mode: 
         ent.wall_ms = round((time.perf_counter() - t_task) * 1e3, 1)
         if dev0 is not None:
             ent.device_ms = round(stages.device_ms - dev0, 1)
+            ent.stage_ms = getattr(stages, "last_stage_ms", None)
         log.append(ent)
         tc += 1
     return chim, last_masked, log
