@@ -252,6 +252,25 @@ struct Occ {
         for (int32_t k = S->hoff[a]; k < S->hoff[a + 1]; ++k) c += S->hml[k] >= n;
         return c;
     }
+    // occ(a, a + n) for n >= KI + HB (a scan of the start's hits) and the smallest match length
+    // >= n (mn; 0 when none): occ(a, a + n') is the same for every n' in [n, mn], so a forward
+    // extension can step from n to mn at once (the finish task's near-exact reads: one scan per
+    // distinct match length instead of one per base)
+    SC_HD int64_t scan_ge(int a, int n, int &mn) const {
+        int64_t c = 0;
+        int m = 0x7fffffff;
+        SC_STAT(9, 1);
+        SC_STAT(10, S->hoff[a + 1] - S->hoff[a]);
+        for (int32_t k = S->hoff[a]; k < S->hoff[a + 1]; ++k) {
+            const int v = S->hml[k];
+            if (v >= n) {
+                ++c;
+                m = v < m ? v : m;
+            }
+        }
+        mn = c ? m : 0;
+        return c;
+    }
 };
 
 // The end of the longest match from start a that occurs >= k times in the text:
@@ -467,7 +486,12 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
         if (q[i] < 4) {
             const int n = i + 1 - x;
             int64_t o;
-            if (have && n >= 7 && n < 16) {
+            int skip = 0;   // lengths n + 1 .. n + skip have the same count (Occ::scan_ge)
+            if (have && n >= KI + HB) {
+                int mn;
+                o = occ.scan_ge(x, n, mn);
+                skip = mn > n ? mn - n : 0;   // (no read N inside a hit's match: q[x, x + mn) is N-free)
+            } else if (have && n >= 7 && n < 16) {
                 uint32_t v = pre[0];
 #pragma unroll
                 for (int t = 1; t < 9; ++t) v = n - 7 == t ? pre[t] : v;
@@ -491,6 +515,7 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
                 curr[nc++] = ik;
                 if (o < min_intv) break;
             }
+            i += skip;
             ik = Iv{x, i + 1, o};
         } else {
             if (nc >= cap) { err |= SC_OVER_IV; return len; }
@@ -538,11 +563,14 @@ SC_HD int seed_strategy1(const Occ &occ, const uint8_t *q, int len, int x, int m
     for (int i = x + 1; i < len; ++i) {
         if (q[i] > 3) return i + 1;
         if (i - x >= min_len) {
-            const int64_t o = occ(x, i + 1);
+            const int n = i + 1 - x;
+            int mn = 0;
+            const int64_t o = n >= KI + HB ? occ.scan_ge(x, n, mn) : occ(x, i + 1);
             if (o < max_intv) {
                 m = Iv{x, i + 1, o};
                 return i + 1;
             }
+            if (mn > n) i += mn - n;   // the count holds up to length mn (Occ::scan_ge; q[x, x + mn) is N-free)
         }
     }
     return len;

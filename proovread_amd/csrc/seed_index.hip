@@ -316,7 +316,9 @@ __global__ void ix_pack4_kernel(const uint8_t *text, int64_t n_text, uint64_t *t
         text4[w] = v;
     }
 }
-int64_t ix_pack4_words(int64_t n_text) { return n_text / 16 + 2; }
+// (8 padding words: the occurrence table's match-length walk loads 5 words at a time from any
+// word a match can reach, seed_kernels.hip build_occ_wave)
+int64_t ix_pack4_words(int64_t n_text) { return n_text / 16 + 8; }
 int ix_pack4_launch(const uint8_t *text, int64_t n_text, uint64_t *text4, hipStream_t s) {
     const int64_t nw = ix_pack4_words(n_text);
     int64_t blocks = (nw + 255) / 256;

@@ -276,3 +276,57 @@ def test_map_mr_reads_matches_oracle_with_seed_filter(mr_data, task, monkeypatch
         for i, r in enumerate(mr_data["srs"]):
             plain += [tuple(t[k] for k in seed.TASK_DTYPE.names) for t in so.map_read(mr_data["oidx"], oo, r, i)]
         assert len(plain) > len(want)
+
+
+@pytest.fixture(scope="module")
+def near_exact():
+    """The finish task's setting: short reads against near-exact long reads at ~30x coverage
+    (every 12-mer of a read hits ~30 copies, matches run to the read's end), so the SMEM forward
+    extension and bwt_seed_strategy1 (-y) count lengths beyond the per-start count table."""
+    rng = np.random.default_rng(11)
+    G = rng.integers(0, 4, 2400)
+    lrs = []
+    for i in range(34):
+        s = int(rng.integers(0, 900))
+        lr = _mutate(rng, G[s:s + 1500], p_ins=0.002, p_del=0.002, p_sub=0.002)
+        if i == 5:
+            lr[40] = 4   # an N inside a copy
+        lrs.append(lr)
+    srs = []
+    for i in range(24):
+        s = int(rng.integers(0, 2250))
+        r = [int(x) for x in G[s:s + 150]]
+        if i % 5 == 1:
+            r[int(rng.integers(0, 150))] = 4   # a read N
+        if rng.random() < 0.5:
+            r = [3 - x if x < 4 else 4 for x in reversed(r)]
+        srs.append(r)
+    lr_off = np.concatenate([[0], np.cumsum([len(x) for x in lrs])]).astype(np.int64)
+    sr_off = np.concatenate([[0], np.cumsum([len(x) for x in srs])]).astype(np.int64)
+    return dict(lrs=lrs, srs=srs, lr_seq=np.concatenate([np.array(x, np.uint8) for x in lrs]), lr_off=lr_off,
+                sr_seq=np.concatenate([np.array(x, np.uint8) for x in srs]), sr_off=sr_off,
+                oidx=so.Index(lrs), G=G)
+
+
+@pytest.mark.parametrize("finish", [False, True])
+def test_map_near_exact_matches_oracle(near_exact, finish):
+    ix = seed.SeedIndex(near_exact["lr_seq"], near_exact["lr_off"])
+    try:
+        tasks = _cmp(near_exact, ix, seed.default_opts(finish), so.Opts.finish() if finish else so.Opts())
+    finally:
+        ix.close()
+    assert len(tasks) > 100
+
+
+def test_smem_near_exact_matches_oracle(near_exact):
+    ix = seed.SeedIndex(near_exact["lr_seq"], near_exact["lr_off"])
+    try:
+        for r in near_exact["srs"][:10]:
+            q = np.array(r, np.uint8)
+            for x in (0, 37, 75):
+                for mi in (1, 20, 31):
+                    got = ix.smem(q, x, mi)
+                    want = so.smem1(near_exact["oidx"], r, x, mi)
+                    assert (got[0], got[1]) == (want[0], want[1]), (x, mi)
+    finally:
+        ix.close()

@@ -255,3 +255,25 @@ def test_device_index_build_equals_host_index():
             assert (st == 0).all(), name
             assert np.array_equal(got, want), name
         hx.close()
+
+
+@pytest.mark.gpu
+def test_gpu_seeding_near_exact_matches_host_path():
+    """The finish task's setting (short reads against near-exact long reads at 30x: every 12-mer
+    hits ~30 copies, matches run to the read's end, every read outgrows pass 1's hit slices):
+    the occurrence table's 64-base text walks and the SMEM / -y count jumps (seed_core.h
+    Occ::scan_ge) give the host path's seeds, for both option sets."""
+    from proovread_amd import _abi
+    d = synth.simulate(17, 150_000, 900, 5000, 40.0, p_ins=0.002, p_del=0.002, p_sub=0.002, sr_frac=0.1)
+    n = min(4000, d.n_sr)
+    ss, so_ = d.sr_seq[:d.sr_off[n]], d.sr_off[:n + 1]
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    ix.to_gpu(_abi.default_context())
+    for finish in (False, True):
+        o = seed.default_opts(finish)
+        want = ix.map(ss, so_, o, threads=8)
+        got, st = ix.map_gpu(ss, so_, o, allow_flagged=False)
+        assert (st == 0).all()
+        assert np.array_equal(got, want)
+        assert len(want) > 10 * n
+    ix.close()
