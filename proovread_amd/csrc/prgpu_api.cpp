@@ -2400,7 +2400,10 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
             // the hit tables sized for the largest flagged read (dense indexes: configs[2] /
             // configs[3], or N > 1 ranks of the exact layout, every read overflows pass 1)
             if (fl1 & seedc::SC_OVER_HITS) {
-                cb.hits = (int32_t)std::min<int64_t>(std::max<int64_t>(4 * (int64_t)cb.hits, (need_hits + 1023) & ~(int64_t)1023),
+                // the largest flagged read's hit table (+ 1/8), not a multiple of pass 1's: the finish
+                // task's reads need just over pass 1's 4096 hits, and 4x slices cut the waves in flight
+                // (the occurrence table is latency-bound: 413 -> measured in DESIGN.md §5 round 6)
+                cb.hits = (int32_t)std::min<int64_t>(std::max<int64_t>((int64_t)cb.hits + 512, (need_hits + need_hits / 8 + 511) & ~(int64_t)511),
                                                      (int64_t)1 << 20);
                 // their chaining never ran; random 12-mer hits become chains and seeds in
                 // proportion to the hits, so those arrays grow by the same factor
@@ -2413,6 +2416,20 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
             if (fl1 & seedc::SC_OVER_SEEDS) cb.seeds *= 2;
             if (fl1 & seedc::SC_OVER_CHAINS) cb.chains *= 2;
             const int64_t sb = seedc::scratch_bytes(cb);
+            {   // room for as many waves as pass 1 ran (or the flagged reads' batches), within pass 1's budget
+                size_t fr = 0, tot = 0;
+                (void)hipMemGetInfo(&fr, &tot);
+                (void)hipGetLastError();
+                const int64_t have = (int64_t)D[SB_SCRATCH].cap;
+                const int64_t budget = std::min<int64_t>((int64_t)40 << 30,
+                                                         std::max<int64_t>((int64_t)24 << 30, ((int64_t)fr + have) * 15 / 100));
+                const int64_t want = std::min<int64_t>(waves, ((int64_t)redo.size() + 63) / 64) * 64 * sb;
+                if (want > have && want <= budget) {
+                    HIPCHK(hipStreamSynchronize(s));
+                    if ((rc = D[SB_SCRATCH].ensure((size_t)want))) return rc;
+                    K.scratch = D[SB_SCRATCH].as<uint8_t>();
+                }
+            }
             int64_t wb = std::min<int64_t>((int64_t)D[SB_SCRATCH].cap / (64 * sb), ((int64_t)redo.size() + 63) / 64);
             wb = std::min<int64_t>(wb, waves);   // (the filter rows' area holds `waves` waves)
             // reads that need more than 4x pass 1's hits on average (dense indexes: configs[2] / [3]) one wave
