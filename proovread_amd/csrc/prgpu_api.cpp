@@ -2274,6 +2274,9 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
     seedc::Caps small = seedc::device_caps_small(std::min(qmax, caps.lmax));
     small.hi = caps.hi;
     small.nopos = 1;
+    // the finish tasks' near-exact mapping: pass 1's occurrence tables lazily, a start's hits on
+    // first use (seed_core.h materialize; the later passes build them eagerly, wave-parallel)
+    small.lazy = seedc::lazy_occ(*o) ? 1 : 0;
     if (const char *sc = getenv("PRGPU_SEED_SMALL"))   // tuning hook: hits,iv,mems,seeds,chains
         sscanf(sc, "%d,%d,%d,%d,%d", &small.hits, &small.iv, &small.mems, &small.seeds, &small.chains);
     SeedDev K{};

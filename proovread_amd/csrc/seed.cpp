@@ -737,6 +737,7 @@ extern "C" int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opt
     for (int i = 0; i < n_sr; ++i) qmax = std::max<int>(qmax, (int)(sr_off[i + 1] - sr_off[i]));
     seedc::Caps caps = seedc::device_caps(qmax);   // (the output slots follow the longest read, as on the device)
     caps.hi = V.ksplit != nullptr;
+    caps.lazy = seedc::lazy_occ(*o) ? 1 : 0;   // the device's pass-1 table for these options
     const int64_t bytes = seedc::scratch_bytes(caps);
     int nt = n_threads > 0 ? n_threads : (int)std::thread::hardware_concurrency();
     nt = nt < 1 ? 1 : (nt > 64 ? 64 : nt);

@@ -152,6 +152,13 @@ struct Scratch {
     int32_t cap_chains, hsize;                 // hsize: power of two >= 2 * cap_chains
     uint16_t *rmax;                            // [(lmax + 1) * RK] R_k(a), k = 1..RK (rmax_k)
     uint64_t *hfr;                             // [cap_hits] pack_fr of the hit (the chaining's coordinates)
+    // lazy occurrence table (Caps.lazy; null otherwise): a start's hits, count row and R_k are
+    // computed the first time the SMEM search or the chaining asks for them (materialize), its hits
+    // appended to a per-read pool: hits of start a at [hoff[a], hend[a])
+    int32_t *hend;                             // [lmax + 1]
+    uint8_t *ready;                            // [lmax + 1] start materialized
+    uint64_t *q4w;                             // [lmax / 16 + 4] the read 16 bases per word (4 bits each), or null
+    int32_t *lz;                               // [4] pool fill, SC_OVER_* flags, hits the read would need
 };
 
 SC_HD uint64_t pack_ext(const uint8_t *s, int n) {
@@ -219,6 +226,17 @@ SC_HD uint64_t pack_fr(const IndexView &I, uint64_t p) {
     return ((uint64_t)fr << FR_RID_BITS) | (uint64_t)rid;
 }
 
+// 16 bases from base x of a 4-bit packed sequence (a padding word after the last)
+SC_HD uint64_t nib16c(const uint64_t *w4, uint64_t x) {
+    const uint64_t w = x >> 4;
+    const int sh = (int)(x & 15) * 4;
+    const uint64_t lo = w4[w];
+    return sh ? (lo >> sh) | (w4[w + 1] << (64 - sh)) : lo;
+}
+
+// the end of start a's hits in the occurrence table
+SC_HD int32_t hit_end(const Scratch &S, int a) { return S.hend ? S.hend[a] : S.hoff[a + 1]; }
+
 // ---------------------------------------------------------------- occurrence table
 // the j-mer count tables j = 1..LC_MAX held on chip by the device kernels (5,460 entries):
 // table j at LC_OFF(j) = (4^j - 4) / 3
@@ -226,12 +244,20 @@ constexpr int LC_MAX = 6;
 SC_HD constexpr int lc_off(int j) { return ((1 << (2 * j)) - 4) / 3; }
 constexpr int LC_N = lc_off(LC_MAX + 1);   // 4 + 16 + ... + 4^LC_MAX
 
+struct Occ;
+SC_HD void materialize(const Occ &occ, int a);
+
 struct Occ {
     const IndexView *I;
     const Scratch *S;
     const uint8_t *q;
     int len;
     const uint32_t *lc = nullptr;   // LDS copy of cnt[0 .. LC_MAX-1] (device) or null
+
+    // the lazy table's start a on first use (a no-op for the eager table)
+    SC_HD void need(int a) const {
+        if (S->hend && a < len && !S->ready[a]) materialize(*this, a);
+    }
 
     SC_HD int64_t operator()(int a, int b) const {
         const int n = b - a;
@@ -245,11 +271,13 @@ struct Occ {
             if (lc && n <= LC_MAX) return lc[lc_off(n) + code];
             return I->cnt[n - 1][code];
         }
+        need(a);
         if (n - KI < HB) return S->ge[(int64_t)a * HB + (n - KI)];
         int64_t c = 0;
         SC_STAT(9, 1);
-        SC_STAT(10, S->hoff[a + 1] - S->hoff[a]);
-        for (int32_t k = S->hoff[a]; k < S->hoff[a + 1]; ++k) c += S->hml[k] >= n;
+        const int32_t h1 = hit_end(*S, a);
+        SC_STAT(10, h1 - S->hoff[a]);
+        for (int32_t k = S->hoff[a]; k < h1; ++k) c += S->hml[k] >= n;
         return c;
     }
     // occ(a, a + n) for n >= KI + HB (a scan of the start's hits) and the smallest match length
@@ -259,9 +287,11 @@ struct Occ {
     SC_HD int64_t scan_ge(int a, int n, int &mn) const {
         int64_t c = 0;
         int m = 0x7fffffff;
+        need(a);
+        const int32_t h1 = hit_end(*S, a);
         SC_STAT(9, 1);
-        SC_STAT(10, S->hoff[a + 1] - S->hoff[a]);
-        for (int32_t k = S->hoff[a]; k < S->hoff[a + 1]; ++k) {
+        SC_STAT(10, h1 - S->hoff[a]);
+        for (int32_t k = S->hoff[a]; k < h1; ++k) {
             const int v = S->hml[k];
             if (v >= n) {
                 ++c;
@@ -337,6 +367,7 @@ SC_HD void fill_rk(const Occ &occ, const Scratch &S, const uint8_t *q, int len, 
 // count row and its hits' lengths
 SC_HD int rmax_k(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a, int64_t k) {
     if (k < 1) k = 1;
+    occ.need(a);
     if (k <= RK) return S.rmax[(int64_t)a * RK + (k - 1)];
     if (q[a] > 3) return a;
     if (a + KI <= len && S.codes[a] >= 0) {
@@ -355,13 +386,143 @@ SC_HD int rmax_k(const Occ &occ, const Scratch &S, const uint8_t *q, int len, in
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 int64_t c = 0;
-                for (int32_t h = S.hoff[a]; h < S.hoff[a + 1]; ++h) c += S.hml[h] >= mid;
+                for (int32_t h = S.hoff[a]; h < hit_end(S, a); ++h) c += S.hml[h] >= mid;
                 if (c >= k) lo = mid; else hi = mid - 1;
             }
             return a + lo;
         }
     }
     return rmax_short(occ, q, len, a, k);
+}
+
+// the exact match length ml = LCP(q[a..], T[p..]) of a hit of start a: the KX bases stored after
+// the hit (ex) against the read's (qe), then the text (16 bases a step from the 4-bit copies when
+// the index and the read have them, else a base a step)
+SC_HD int hit_ml(const IndexView &I, const Scratch &S, const uint8_t *q, int len, int a, uint64_t p, uint64_t ex,
+                 uint64_t qe) {
+    const int le = (int)(ex >> 56), lq = (int)(qe >> 56);
+    const uint64_t x = (ex ^ qe) & KX_MASK;
+    int m = x ? ctz64(x) >> 1 : KX;
+    m = m < le ? m : le;
+    m = m < lq ? m : lq;
+    int ml = KI + m;
+    if (m < KX) return ml;
+    if (I.text4 && S.q4w) {
+        for (;;) {
+            const int xx = a + ml;
+            if (xx >= len) break;
+            const uint64_t qw = nib16c(S.q4w, (uint64_t)xx), tw = nib16c(I.text4, p + (uint64_t)ml);
+            const uint64_t nq = (qw >> 2) & 0x1111111111111111ull;   // read N (code 4) or past the end (6)
+            const uint64_t bad = (qw ^ tw) | (nq * 0xFull);
+            const int lim = len - xx;
+            if (bad) {
+                const int f = ctz64(bad) >> 2;
+                ml += f < lim ? f : lim;
+                break;
+            }
+            if (lim <= 16) {
+                ml += lim;
+                break;
+            }
+            ml += 16;
+        }
+    } else {
+        while (a + ml < len && q[a + ml] < 4 && I.text[p + ml] == q[a + ml]) ++ml;
+    }
+    return ml;
+}
+
+// The lazy table's start a (Scratch.hend): its hits appended to the read's pool with their match
+// lengths and coordinates, its count row and R_1 .. R_RK -- the values the eager table holds for
+// it.  A pool that would overflow flags the read (lz[1]) and records the hits it needs (lz[2]).
+SC_HD void materialize(const Occ &occ, int a) {
+    const IndexView &I = *occ.I;
+    const Scratch &S = *occ.S;
+    const uint8_t *q = occ.q;
+    const int len = occ.len;
+    S.ready[a] = 1;
+    const int32_t beg = S.lz[0];
+    uint32_t g[HB];
+    uint16_t top[RK];
+#pragma unroll
+    for (int t = 0; t < HB; ++t) g[t] = 0u;
+#pragma unroll
+    for (int k = 0; k < RK; ++k) top[k] = 0;
+    int32_t n = 0;
+    const int32_t code = a + KI <= len ? S.codes[a] : -1;
+    if (code >= 0) {
+        const uint64_t r0 = I.koff[code], r1 = I.koff[code + 1];
+        const int64_t need = (int64_t)beg + (int64_t)(r1 - r0);
+        if (need > S.cap_hits) {
+            S.lz[1] |= SC_OVER_HITS;
+            S.lz[2] = (int32_t)(need < (int64_t)1 << 30 ? need : (int64_t)1 << 30);
+        } else {
+            n = (int32_t)(r1 - r0);
+            const uint64_t qe = S.qext[a];
+            const bool ranked = q[a] < 4;
+            for (uint64_t r = r0; r < r1; ++r) {
+                const uint64_t p = hit_pos(I, (uint32_t)code, r);
+                const int ml = hit_ml(I, S, q, len, a, p, I.kext[r], qe);
+                const int32_t k = beg + (int32_t)(r - r0);
+                const uint16_t v = (uint16_t)(ml < 65535 ? ml : 65535);
+                S.hml[k] = v;
+                S.hfr[k] = pack_fr(I, p);
+                const int d = ml - KI;
+#pragma unroll
+                for (int t = 0; t < HB; ++t) g[t] += d >= t ? 1u : 0u;
+                if (ranked) topk_insert(top, v);
+            }
+        }
+    }
+    S.hoff[a] = beg;
+    S.hend[a] = beg + n;
+    S.lz[0] = beg + n;
+    uint32_t *dst = S.ge + (int64_t)a * HB;
+#pragma unroll
+    for (int t = 0; t < HB; ++t) dst[t] = g[t];
+    fill_rk_top(occ, S, q, len, a, top);
+}
+
+// The lazy table's per-start inputs of read q (the host's; the device builds them wave-parallel in
+// seed_kernels.hip): 12-mer codes, the KX bases after each start, the 4-bit copy, no start ready
+SC_HD int build_starts(const IndexView &I, Scratch &S, const uint8_t *q, int len) {
+    if (len > S.lmax) return SC_OVER_LEN;
+    for (int a = 0; a <= len; ++a) {
+        S.codes[a] = -1;
+        S.qext[a] = 0;
+        S.hoff[a] = 0;
+        S.hend[a] = 0;
+        S.ready[a] = a == len ? 1 : 0;
+    }
+    for (int a = 0; a + KI <= len; ++a) {
+        const int n = len - a - KI;
+        S.qext[a] = pack_ext(q + a + KI, n < KX ? n : KX);
+    }
+    uint32_t code = 0;
+    int run = 0;
+    for (int e = 0; e < len; ++e) {
+        if (q[e] > 3) {
+            run = 0;
+            code = 0;
+        } else {
+            code = ((code << 2) | q[e]) & (NK - 1);
+            ++run;
+        }
+        if (e - KI + 1 >= 0 && run >= KI) S.codes[e - KI + 1] = (int32_t)code;
+    }
+    if (S.q4w) {
+        for (int w = 0; w <= (len >> 4) + 3; ++w) {
+            uint64_t v = 0;
+            for (int k = 0; k < 16; ++k) {
+                const int x = w * 16 + k;
+                const uint64_t c = x < len ? (q[x] < 4 ? q[x] : 4u) : 6u;
+                v |= c << (4 * k);
+            }
+            S.q4w[w] = v;
+        }
+    }
+    S.lz[0] = S.lz[1] = S.lz[2] = 0;
+    return 0;
 }
 
 // -> 0 or SC_OVER_*
@@ -474,6 +635,7 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
     uint32_t pre[9];
     const bool have = S.codes != nullptr && x + KI <= len && S.codes[x] >= 0;
     if (have) {
+        occ.need(x);
         const uint32_t c12 = (uint32_t)S.codes[x];
 #pragma unroll
         for (int n = 7; n < KI; ++n) pre[n - 7] = occ.I->cnt[n - 1][c12 >> (2 * (KI - n))];
@@ -640,7 +802,7 @@ SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const 
     // counting sort by start (into the seed pool, free until mem_chain; the counts in `codes`,
     // which nothing reads after the occurrence lookups) and an insertion sort by end inside each
     // start's run (a few intervals) replace one insertion sort over all ~150 (quadratic moves)
-    if (nm > 1 && S.cap_seeds >= nm && !err) {
+    if (nm > 1 && S.cap_seeds >= nm && !err && !S.hend) {   // (the lazy table still needs `codes`)
         static_assert(sizeof(Seed) == sizeof(Iv), "the seed pool holds the sorted intervals");
         int32_t *cnt = S.codes;
         Iv *tmp = reinterpret_cast<Iv *>(S.seeds);
@@ -865,6 +1027,7 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
 #endif
     const Occ occ{&I, &S, q, len, lcnt};
     const int nm = collect_intv(occ, S, O, q, len, err, ticks);
+    if (S.hend) err |= S.lz[1];   // the lazy table's pool overflowed: the counts are not valid
     if (err) return err;
     SC_STAT(0, 1);
     SC_STAT(1, nm);
@@ -873,6 +1036,7 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
 #endif
     int ncv = 0;
     err = chain_seq(I, O, S, nm, &ncv);
+    if (S.hend) err |= S.lz[1];
     if (err) return err;
     SC_TICK(3);
     SC_STAT(11, ncv);
@@ -890,7 +1054,9 @@ SC_HD int chain_seq(const IndexView &I, const pr_seed_opts &O, Scratch &S, int n
     for (int mi = 0; mi < nm; ++mi) {
         const Iv p = S.mems[mi];
         const int slen = p.end - p.start;
-        const int32_t h0 = S.hoff[p.start], h1 = S.hoff[p.start + 1];
+        // (lazy table: every SMEM's start was counted by the SMEM search, so it is materialized)
+        if (S.hend && !S.ready[p.start]) return SC_OVER_HITS;
+        const int32_t h0 = S.hoff[p.start], h1 = hit_end(S, p.start);
         // the SMEM's occurrence count is the number of the start's hits with ml >= slen
         // (every interval's occ comes from the same per-start table, slen >= 12)
         const int64_t np = p.occ;
@@ -1186,14 +1352,20 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
 }
 #undef SC_TICK
 
-// The whole read: occurrence table, then map_after_occ.
+// The whole read: occurrence table (the lazy one when S has it), then map_after_occ.
 SC_HD int map_read(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
                    pr_seed_task *out, int cap_out, int *n_out) {
     *n_out = 0;
-    const int err = build_occ(I, S, q, len);
+    const int err = S.hend ? build_starts(I, S, q, len) : build_occ(I, S, q, len);
     if (err) return err;
     return map_after_occ(I, O, S, q, len, sid, out, cap_out, n_out);
 }
+
+// Whether the device path builds the lazy occurrence table for these options: the finish tasks'
+// near-exact mapping (-k >= 17: bwa-sr-finish, bwa-mr-finish) consults a few starts per read
+// (its SMEMs run to the read's end), the iterations' noisy mapping nearly every start.  Either
+// table gives the same seeds; only the cost differs.
+SC_HD bool lazy_occ(const pr_seed_opts &O) { return O.min_seed_len >= 17; }
 
 }  // namespace seedc
 }  // namespace prgpu
@@ -1208,6 +1380,7 @@ struct Caps {
     int32_t hi;      // the text reaches beyond 2^32: the hit table carries bit 32 of the positions (hhi)
     int32_t nopos;   // no hit positions (hpos / hhi): the device's tables keep only the chaining's
                      // coordinates (hfr); the host's build_occ follows diagonals through hpos
+    int32_t lazy;    // the lazy occurrence table (Scratch.hend / ready / q4w / lz)
 };
 // output slots per read (the seeds of its kept chains): 384 for short reads, 2 per base for
 // the mr modes' 300-1000 bp reads (~300 seeds per 600 bp read at 15x long-read coverage)
@@ -1268,7 +1441,13 @@ SC_HD int64_t scratch_bytes(const Caps &c) {
     b += align8((int64_t)sizeof(RangeRec) * c.chains);   // rg
     b += align8(2 * (int64_t)(c.lmax + 1) * RK);         // rmax
     b += align8(8 * (int64_t)c.hits);                    // hfr
-    if (c.hi && !c.nopos) b += align8((int64_t)c.hits);  // hhi (last)
+    if (c.hi && !c.nopos) b += align8((int64_t)c.hits);  // hhi
+    if (c.lazy) {
+        b += align8(4 * (int64_t)(c.lmax + 1));          // hend
+        b += align8((int64_t)(c.lmax + 1));              // ready
+        b += align8(8 * (int64_t)(c.lmax / 16 + 4));     // q4w
+        b += align8(16);                                 // lz
+    }
     return (b + 63) & ~(int64_t)63;                      // (slices 64-byte aligned)
 }
 
@@ -1308,6 +1487,12 @@ SC_HD Scratch carve(uint8_t *p, const Caps &c) {
     S.rmax = (uint16_t *)take(2 * (int64_t)(c.lmax + 1) * RK);
     S.hfr = (uint64_t *)take(8 * (int64_t)c.hits);
     S.hhi = c.hi && !c.nopos ? (uint8_t *)take((int64_t)c.hits) : nullptr;
+    if (c.lazy) {
+        S.hend = (int32_t *)take(4 * (int64_t)(c.lmax + 1));
+        S.ready = (uint8_t *)take((int64_t)(c.lmax + 1));
+        S.q4w = (uint64_t *)take(8 * (int64_t)(c.lmax / 16 + 4));
+        S.lz = (int32_t *)take(16);
+    }
     return S;
 }
 

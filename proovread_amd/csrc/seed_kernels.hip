@@ -31,6 +31,9 @@ constexpr int SEED_LMAX = SEED_LMAX_DEF;     // LDS start offsets per wave: read
 #ifndef SEED_MINB
 #define SEED_MINB 4
 #endif
+#ifndef NOWALK_PROBE
+#define NOWALK_PROBE 0
+#endif
 #ifndef OCC_U
 #define OCC_U 2   // hits per lane per pass of the occurrence table's hit loop
 #endif
@@ -68,7 +71,7 @@ __device__ __forceinline__ uint64_t nib16(const uint64_t *w4, uint64_t x) {
 
 __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, const uint8_t *q, int len, int32_t *ho,
                               int lane, uint64_t *q4, const uint32_t *lc, int *n_hits = nullptr,
-                              unsigned long long *ot = nullptr) {
+                              unsigned long long *ot = nullptr, bool lazy = false) {
     // ot (optional): wall-clock ticks of the start pass, the hit pass and the count table
     unsigned long long t_occ = ot ? wall_clock64() : 0ULL;
 #define OCC_TICK(k)                                        \
@@ -159,12 +162,20 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                 }
                 if (ok) {
                     code_a = (int32_t)code;
-                    r0a = V.koff[code];
-                    ca = (int)(V.koff[code + 1] - r0a);
+                    if (!lazy) {
+                        r0a = V.koff[code];
+                        ca = (int)(V.koff[code + 1] - r0a);
+                    }
                 }
             }
             S.codes[a] = code_a;
             S.qext[a] = qe;
+            if (lazy) {   // the lazy table: no start ready, the hits come on first use (seed_core.h materialize)
+                S.ready[a] = a == len ? 1 : 0;
+                S.hoff[a] = 0;
+                S.hend[a] = 0;
+                ca = 0;
+            }
             if (side) {   // the hit pass's per-start inputs on chip
                 lcode[a] = code_a;
                 lqext[a] = qe;
@@ -183,6 +194,29 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
             S.hoff[a] = ex;
         }
         run += __shfl(x, 63, 64);
+    }
+    if (lazy) {   // the read's 4-bit copy for materialize's text walks, an empty pool
+        if (S.q4w) {
+            if (V.text4) {
+                for (int w = lane; w <= (len >> 4) + 3; w += 64) S.q4w[w] = q4[w];
+            } else {
+                for (int w = lane; w <= (len >> 4) + 3; w += 64) {
+                    uint64_t v = 0;
+                    for (int k = 0; k < 16; ++k) {
+                        const int x = w * 16 + k;
+                        const uint64_t c = x < len ? (q[x] < 4 ? q[x] : 4u) : 6u;
+                        v |= c << (4 * k);
+                    }
+                    S.q4w[w] = v;
+                }
+            }
+        }
+        if (lane == 0) S.lz[0] = S.lz[1] = S.lz[2] = 0;
+        if (n_hits) *n_hits = 0;
+        __threadfence_block();
+        wave_sync_lds();
+        OCC_TICK(0);
+        return 0;
     }
     const int nh = run;
     if (n_hits) *n_hits = nh;
@@ -278,7 +312,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                         // the text words of 64 bases are loaded together (5 independent loads, the text
                         // has 8 padding words) and compared from registers: one memory round trip per
                         // 64 bases instead of one per 16 (the finish task's near-exact reads walk ~110)
-                        bool go = a + ml < len;
+                        bool go = a + ml < len && !NOWALK_PROBE;
                         while (go) {
                             const uint64_t tp = p[u] + (uint64_t)ml;
                             const uint64_t* tw4 = V.text4 + (tp >> 4);
@@ -880,7 +914,8 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             int err = 0, nh = 0;
             if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
             if (len > 0 && !err)
-                err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt, &nh, D.prof ? ot : nullptr);
+                err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt, &nh, D.prof ? ot : nullptr,
+                                     D.caps.lazy != 0);
             if (lane == rd) my_err = err, my_hits = nh;
         }
         const unsigned long long t1 = D.prof ? wall_clock64() : 0ULL;
@@ -896,7 +931,9 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
                                            D.dp ? D.dp + slot * (2 * 201 * 64) + lane : nullptr);
             // a read whose hit table overflowed reports the hits it needs (the retry pass sizes
             // its slices from them: texts of 1 - 3 Gb give ~20-50 k hits per 150 bp read)
-            D.n_out[i] = (my_err & seedc::SC_OVER_HITS) ? -my_hits : (err ? 0 : n);
+            D.n_out[i] = (my_err & seedc::SC_OVER_HITS) ? -my_hits
+                         : (D.caps.lazy && (err & seedc::SC_OVER_HITS)) ? -S.lz[2]   // (the lazy pool's need)
+                                                                        : (err ? 0 : n);
             D.status[i] = err;
         }
         if (D.prof && lane == 0) {

@@ -330,3 +330,24 @@ def test_smem_near_exact_matches_oracle(near_exact):
                     assert (got[0], got[1]) == (want[0], want[1]), (x, mi)
     finally:
         ix.close()
+
+
+@pytest.mark.parametrize("finish", [False, True])
+def test_device_caps_near_exact_equals_host(near_exact, finish):
+    """The device path's core on the host (finish options: the lazy occurrence table, a start's
+    hits on first use) gives the host path's seeds on near-exact reads, whatever the scratch held."""
+    import os
+    ix = seed.SeedIndex(near_exact["lr_seq"], near_exact["lr_off"])
+    try:
+        o = seed.default_opts(finish)
+        want = ix.map(near_exact["sr_seq"], near_exact["sr_off"], o, threads=2)
+        for fill in (None, "0xA5"):
+            if fill:
+                os.environ["PRGPU_SCRATCH_FILL"] = fill
+            try:
+                got, st = ix.map_device_caps(near_exact["sr_seq"], near_exact["sr_off"], o, threads=2)
+            finally:
+                os.environ.pop("PRGPU_SCRATCH_FILL", None)
+            assert (st == 0).all() and np.array_equal(got, want), fill
+    finally:
+        ix.close()
