@@ -31,9 +31,6 @@ constexpr int SEED_LMAX = SEED_LMAX_DEF;     // LDS start offsets per wave: read
 #ifndef SEED_MINB
 #define SEED_MINB 4
 #endif
-#ifndef NOWALK_PROBE
-#define NOWALK_PROBE 0
-#endif
 #ifndef OCC_U
 #define OCC_U 2   // hits per lane per pass of the occurrence table's hit loop
 #endif
@@ -312,7 +309,7 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                         // the text words of 64 bases are loaded together (5 independent loads, the text
                         // has 8 padding words) and compared from registers: one memory round trip per
                         // 64 bases instead of one per 16 (the finish task's near-exact reads walk ~110)
-                        bool go = a + ml < len && !NOWALK_PROBE;
+                        bool go = a + ml < len;
                         while (go) {
                             const uint64_t tp = p[u] + (uint64_t)ml;
                             const uint64_t* tw4 = V.text4 + (tp >> 4);
