@@ -317,6 +317,28 @@ int pr_sw_download(pr_ctx *ctx, pr_sw_out *out);      /* syncs               */
 int pr_sw_cigar_total(pr_ctx *ctx, int64_t *total, int64_t *n_overflow);
 /* bwa mode: reported alignments of the last launch (syncs) */
 int pr_sw_aln_count(pr_ctx *ctx, int64_t *n_aln);
+/* bwa-proovread mem's output stage on the last bwa-mode launch (the `mem` drop-in, replacing
+ * bwa-proovread's mem_reg2sam printing and its proovread.[ch] bin filter, bin/proovread:1302-1313).
+ * pr_sw_binfilter: the -b BIN -l LEN score binning on the device (pipe_binfilter_kernel, the
+ * same filter as pr_iter_launch's) -> keep[pr_sw_aln_count] in SAM order (1 = printed).
+ * pr_sw_sam: the SAM records (QNAME FLAG RNAME POS MAPQ CIGAR * 0 0 SEQ QUAL AS:i) of the
+ * reported alignments that passed -T (and keep, when given), in SAM order, formatted on host
+ * threads into one library-allocated text (pr_buffer_free).  SEQ: the read as given, upper
+ * case, or its reverse complement (N for non-ACGT) on the reverse strand; QUAL reversed there,
+ * '*' without qualities.  MAPQ 60 primary, 0 secondary (bwa's MAPQ model is not restated). */
+typedef struct pr_sam_in {
+    const int64_t *sr_off;        /* [n_sr+1] the batch's short reads (pr_sw_batch.sr_off)      */
+    const uint8_t *sr_text;       /* the reads as given (ASCII, sr_off layout)                  */
+    const uint8_t *sr_qual;       /* phred+33 (sr_off layout), or NULL                          */
+    const char *sr_names;         /* names pool: read i at [sr_name_off[i], sr_name_off[i+1])   */
+    const int64_t *sr_name_off;
+    const char *lr_names;         /* long-read names pool (RNAME)                               */
+    const int64_t *lr_name_off;
+    const uint8_t *keep;          /* [pr_sw_aln_count] from pr_sw_binfilter, or NULL            */
+    int32_t n_threads;            /* <= 0: all cores                                            */
+} pr_sam_in;
+int pr_sw_binfilter(pr_ctx *ctx, int32_t bin_size, double bin_length, uint8_t *keep);
+int pr_sw_sam(pr_ctx *ctx, const pr_sam_in *in, char **text, int64_t *len, int64_t *n_records);
 /* bwa mode diagnostics of the last launch: extension rounds, seeds extended, mem_patch_reg
  * global scores computed */
 int pr_sw_bwa_stats(pr_ctx *ctx, int32_t *rounds, int64_t *n_extended, int64_t *n_patch);

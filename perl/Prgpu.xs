@@ -195,6 +195,51 @@ static void fill_sw_batch(pTHX_ HV *batch, pr_sw_batch *b) {
     b->read_id0 = (int64_t)num(aTHX_ batch, "read_id0", 0);
 }
 
+/* bwa mem seeding + chaining options (bin/proovread:1313, proovread.cfg:318-333) */
+static void fill_seed_opts(pTHX_ HV *opts, pr_seed_opts *o) {
+    pr_seed_opts_default(o, inum(aTHX_ opts, "finish", 0));
+    o->min_seed_len = inum(aTHX_ opts, "min_seed_len", o->min_seed_len);
+    o->min_chain_weight = inum(aTHX_ opts, "min_chain_weight", o->min_chain_weight);
+    o->w = inum(aTHX_ opts, "w", o->w);
+    o->split_factor = num(aTHX_ opts, "split_factor", o->split_factor);
+    o->split_width = inum(aTHX_ opts, "split_width", o->split_width);
+    o->max_mem_intv = inum(aTHX_ opts, "max_mem_intv", o->max_mem_intv);
+    o->max_occ = inum(aTHX_ opts, "max_occ", o->max_occ);
+    o->drop_ratio = num(aTHX_ opts, "drop_ratio", o->drop_ratio);
+    o->a = inum(aTHX_ opts, "a", o->a);
+    o->o_del = inum(aTHX_ opts, "o_del", o->o_del);
+    o->e_del = inum(aTHX_ opts, "e_del", o->e_del);
+    o->o_ins = inum(aTHX_ opts, "o_ins", o->o_ins);
+    o->e_ins = inum(aTHX_ opts, "e_ins", o->e_ins);
+    o->b = inum(aTHX_ opts, "b", o->b);
+}
+
+/* the seed index of the batch's long reads built in HBM and its short reads seeded there, the
+   seeds left in HBM (pr_seed_gpu_index_build + pr_seed_gpu_map(out = NULL)): bwa-proovread
+   index / mem's front end on the device */
+static void gpu_seed(pTHX_ pr_ctx *cx, HV *seed_opts, const pr_sw_batch *b) {
+    pr_seed_opts so;
+    int rc;
+    fill_seed_opts(aTHX_ seed_opts, &so);
+    if ((rc = pr_seed_gpu_index_build(cx, b->lr_seq, b->lr_off, b->n_lr)) != 0)
+        croak("Prgpu: pr_seed_gpu_index_build: %s (%d)", pr_last_error(), rc);
+    if ((rc = pr_seed_gpu_map(cx, &so, b->sr_seq, b->sr_off, b->n_sr, NULL, NULL)) != 0)
+        croak("Prgpu: pr_seed_gpu_map: %s (%d)", pr_last_error(), rc);
+}
+
+static void pools_batch(pTHX_ HV *batch, pr_sw_batch *b) {
+    STRLEN lss = 0, lso = 0, lls = 0, llo = 0;
+    const char *ss = field(aTHX_ batch, "sr_seq", 0, 0, &lss), *so = field(aTHX_ batch, "sr_off", 8, 0, &lso);
+    const char *ls_ = field(aTHX_ batch, "lr_seq", 0, 0, &lls), *lo_ = field(aTHX_ batch, "lr_off", 8, 0, &llo);
+    memset(b, 0, sizeof *b);
+    b->n_sr = (int32_t)check_off(aTHX_ so, lso, lss, "sr_off");
+    b->n_lr = (int32_t)check_off(aTHX_ lo_, llo, lls, "lr_off");
+    b->sr_seq = (const uint8_t *)ss;
+    b->sr_off = (const int64_t *)so;
+    b->lr_seq = (const uint8_t *)ls_;
+    b->lr_off = (const int64_t *)lo_;
+}
+
 MODULE = Prgpu  PACKAGE = Prgpu
 
 PROTOTYPES: DISABLE
@@ -340,21 +385,7 @@ seed_map(IV ix, HV *opts, SV *sr_seq, SV *sr_off, int threads)
     const int64_t n = check_off(aTHX_ off, lo, ls, "sr_off");
     int rc;
     if (!ix) croak("Prgpu::seed_map: no index");
-    pr_seed_opts_default(&o, inum(aTHX_ opts, "finish", 0));
-    o.min_seed_len = inum(aTHX_ opts, "min_seed_len", o.min_seed_len);
-    o.min_chain_weight = inum(aTHX_ opts, "min_chain_weight", o.min_chain_weight);
-    o.w = inum(aTHX_ opts, "w", o.w);
-    o.split_factor = num(aTHX_ opts, "split_factor", o.split_factor);
-    o.split_width = inum(aTHX_ opts, "split_width", o.split_width);
-    o.max_mem_intv = inum(aTHX_ opts, "max_mem_intv", o.max_mem_intv);
-    o.max_occ = inum(aTHX_ opts, "max_occ", o.max_occ);
-    o.drop_ratio = num(aTHX_ opts, "drop_ratio", o.drop_ratio);
-    o.a = inum(aTHX_ opts, "a", o.a);
-    o.o_del = inum(aTHX_ opts, "o_del", o.o_del);
-    o.e_del = inum(aTHX_ opts, "e_del", o.e_del);
-    o.o_ins = inum(aTHX_ opts, "o_ins", o.o_ins);
-    o.e_ins = inum(aTHX_ opts, "e_ins", o.e_ins);
-    o.b = inum(aTHX_ opts, "b", o.b);
+    fill_seed_opts(aTHX_ opts, &o);
     rc = pr_seed_map(INT2PTR(const pr_seed_index *, ix), &o, (const uint8_t *)seq, (const int64_t *)off, (int)n,
                      threads, &t);
     if (rc != 0) croak("Prgpu: pr_seed_map: %s (%d)", pr_last_error(), rc);
@@ -422,6 +453,108 @@ sw_run(IV ctx, HV *opts, HV *batch)
         hv_store(res, "n", 1, newSViv((IV)nt), 0);
     }
     RETVAL = newRV_noinc((SV *)res);
+  OUTPUT:
+    RETVAL
+
+SV *
+mem_gpu(IV ctx, HV *seed_opts, HV *sw_opts, HV *in)
+  CODE:
+    /* bwa-proovread mem on the device end to end: the index and the seeds in HBM, bwa mode on
+       them, the -b/-l filter on the device (pr_sw_binfilter), the SAM records formatted natively
+       (pr_sw_sam) -> the record text.  in: the pools of pools_batch (nt4 codes) plus sr_text,
+       sr_qual (optional), sr_names / sr_name_off, lr_names / lr_name_off, b, l, threads. */
+    pr_ctx *cx = INT2PTR(pr_ctx *, ctx);
+    pr_sw_batch b, ub;
+    pr_sw_opts o;
+    pr_sam_in si;
+    STRLEN lt = 0, lq = 0, lsn = 0, lln = 0;
+    const char *text, *qual;
+    char *sam = NULL;
+    int64_t len = 0, nrec = 0, n_aln = 0;
+    int32_t bs;
+    double bl;
+    SV *keep = NULL;
+    int rc;
+    pools_batch(aTHX_ in, &b);
+    fill_sw_opts(aTHX_ sw_opts, &o);
+    text = field(aTHX_ in, "sr_text", (size_t)i64_at((const char *)b.sr_off, b.n_sr), 0, &lt);
+    qual = field(aTHX_ in, "sr_qual", (size_t)i64_at((const char *)b.sr_off, b.n_sr), 1, &lq);
+    memset(&si, 0, sizeof si);
+    si.sr_off = b.sr_off;
+    si.sr_text = (const uint8_t *)text;
+    si.sr_qual = (const uint8_t *)qual;
+    si.sr_names = field(aTHX_ in, "sr_names", 0, 0, &lsn);
+    si.sr_name_off = (const int64_t *)field(aTHX_ in, "sr_name_off", 8 * ((size_t)b.n_sr + 1), 0, NULL);
+    si.lr_names = field(aTHX_ in, "lr_names", 0, 0, &lln);
+    si.lr_name_off = (const int64_t *)field(aTHX_ in, "lr_name_off", 8 * ((size_t)b.n_lr + 1), 0, NULL);
+    if (i64_at((const char *)si.sr_name_off, b.n_sr) > (int64_t)lsn ||
+        i64_at((const char *)si.lr_name_off, b.n_lr) > (int64_t)lln)
+        croak("Prgpu::mem_gpu: name offsets beyond their pools");
+    si.n_threads = inum(aTHX_ in, "threads", 0);
+    bs = inum(aTHX_ in, "b", 0);
+    bl = num(aTHX_ in, "l", 0);
+    gpu_seed(aTHX_ cx, seed_opts, &b);
+    ub = b;
+    ub.sr_seq = NULL;   /* the seeding's device copies */
+    ub.lr_seq = NULL;
+    if ((rc = pr_sw_upload_gpu_seeds(cx, &ub)) != 0) croak("Prgpu: pr_sw_upload_gpu_seeds: %s (%d)", pr_last_error(), rc);
+    if ((rc = pr_sw_launch(cx, &o)) != 0) croak("Prgpu: pr_sw_launch: %s (%d)", pr_last_error(), rc);
+    if ((rc = pr_sw_aln_count(cx, &n_aln)) != 0) croak("Prgpu: pr_sw_aln_count: %s (%d)", pr_last_error(), rc);
+    if (bs > 0 && bl > 0) {
+        keep = newSV((STRLEN)n_aln + 1);
+        SvPOK_on(keep);
+        SvCUR_set(keep, (STRLEN)n_aln);
+        if ((rc = pr_sw_binfilter(cx, bs, bl, (uint8_t *)SvPVX(keep))) != 0) {
+            SvREFCNT_dec(keep);
+            croak("Prgpu: pr_sw_binfilter: %s (%d)", pr_last_error(), rc);
+        }
+        si.keep = (const uint8_t *)SvPVX(keep);
+    }
+    rc = pr_sw_sam(cx, &si, &sam, &len, &nrec);
+    if (keep) SvREFCNT_dec(keep);
+    if (rc != 0) croak("Prgpu: pr_sw_sam: %s (%d)", pr_last_error(), rc);
+    RETVAL = newSVpvn(len ? sam : "", (STRLEN)len);
+    pr_buffer_free(sam);
+  OUTPUT:
+    RETVAL
+
+SV *
+iter_run_gpu(IV ctx, HV *seed_opts, HV *sw_opts, HV *params, HV *batch)
+  CODE:
+    /* one correction iteration with the seeding on the device too: the index and the bwa-mode
+       seeds in HBM (gpu_seed), then pr_iter_upload_gpu_seeds + pr_iter_launch as iter_run */
+    pr_ctx *cx = INT2PTR(pr_ctx *, ctx);
+    pr_sw_opts o;
+    pr_cns_params p;
+    pr_iter_batch ib;
+    pr_cns_bounds bd;
+    pr_cns_out out;
+    int32_t n_lr = 0;
+    int64_t n_task = 0, nbases;
+    int rc;
+    fill_sw_opts(aTHX_ sw_opts, &o);
+    fill_cns_params(aTHX_ params, &p);
+    memset(&ib, 0, sizeof ib);
+    pools_batch(aTHX_ batch, &ib.sw);
+    nbases = i64_at((const char *)ib.sw.lr_off, ib.sw.n_lr);
+    ib.lr_qual = (const uint8_t *)field(aTHX_ batch, "lr_qual", (size_t)nbases, 1, NULL);
+    ib.ref_seq = (const uint8_t *)field(aTHX_ batch, "ref_seq", (size_t)nbases, 1, NULL);
+    gpu_seed(aTHX_ cx, seed_opts, &ib.sw);
+    if ((rc = pr_iter_upload_gpu_seeds(cx, &ib)) != 0)
+        croak("Prgpu: pr_iter_upload_gpu_seeds: %s (%d)", pr_last_error(), rc);
+    if ((rc = pr_iter_bounds(cx, &n_lr, &n_task, &bd)) != 0) croak("Prgpu: pr_iter_bounds: %s (%d)", pr_last_error(), rc);
+    if ((rc = pr_iter_launch(cx, &o, &p)) != 0) croak("Prgpu: pr_iter_launch: %s (%d)", pr_last_error(), rc);
+    {
+        SV *all[CNS_NOUT];
+        unsigned k;
+        cns_out_alloc(aTHX_ n_lr, n_task, &bd, all, &out);
+        rc = pr_iter_download(cx, &out);
+        if (rc != 0) {
+            for (k = 0; k < CNS_NOUT; ++k) SvREFCNT_dec(all[k]);
+            croak("Prgpu: pr_iter_download: %s (%d)", pr_last_error(), rc);
+        }
+        RETVAL = cns_out_hash(aTHX_ all);
+    }
   OUTPUT:
     RETVAL
 

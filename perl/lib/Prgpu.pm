@@ -288,10 +288,20 @@ sub seed_batch {
                       slen => \@t_slen, chain => \@t_chain});
 }
 
+# names -> (concatenated names, packed int64 offsets)
+sub names_pool {
+    my ($names) = @_;
+    my @off = (0);
+    push @off, $off[-1] + length $_ for @$names;
+    return (join('', @$names), pack('q<*', @off));
+}
+
 # mem(%a) -> (header lines, record lines): the output of `bwa-proovread mem`.
-#   ctx        Prgpu::Context (or a sw_runner coderef taking the seed batch hash and returning
+#   ctx        Prgpu::Context: the whole of mem on the device (mem_gpu: the index and the seeds in
+#              HBM, bwa mode, the -b/-l filter on the device, the records formatted in the
+#              library); or a sw_runner coderef taking the host seeding's batch hash and returning
 #              {pos, score, pass, status, cigar, task, flag} arrays per reported alignment in SAM
-#              order — the tests inject the oracle)
+#              order — the tests inject the oracle; the records are then formatted here)
 #   seed_opts, sw_opts  option hashes for seed_map / sw_run ({finish => 0|1, ...})
 #   b, l       the -b/-l bin filter (0: off)
 #   threads    host seeding threads
@@ -299,6 +309,23 @@ sub seed_batch {
 #   cl         the command line for @PG
 sub mem {
     my (%a) = @_;
+    if (ref $a{ctx} ne 'CODE') {
+        my @head = ("\@HD\tVN:1.5\tSO:unsorted\n");
+        push @head, "\@SQ\tSN:$a{lr_names}[$_]\tLN:" . length($a{lr_seqs}[$_]) . "\n" for 0 .. $#{$a{lr_names}};
+        push @head, "\@PG\tID:bwa-proovread\tPN:bwa-proovread\tVN:prgpu\tCL:bwa-proovread mem " . ($a{cl} // '') . "\n";
+        my ($lr_pool, $lr_off) = pool($a{lr_seqs});
+        my ($sr_pool, $sr_off) = pool($a{sr_seqs});
+        my ($srn, $srn_off) = names_pool($a{sr_names});
+        my ($lrn, $lrn_off) = names_pool($a{lr_names});
+        my %in = (sr_seq => $sr_pool, sr_off => $sr_off, lr_seq => $lr_pool, lr_off => $lr_off,
+                  sr_text => join('', @{$a{sr_seqs}}), sr_names => $srn, sr_name_off => $srn_off, lr_names => $lrn,
+                  lr_name_off => $lrn_off, b => $a{b} || 0, l => $a{l} || 0, threads => $a{threads} || 0);
+        my $quals = $a{sr_quals} || [];
+        $in{sr_qual} = join('', @$quals) if @$quals == @{$a{sr_seqs}} && !grep { !defined } @$quals;
+        my $text = mem_gpu(ref $a{ctx} ? $a{ctx}->handle : $a{ctx}, $a{seed_opts} || {}, $a{sw_opts} || {}, \%in);
+        my @rec = split /(?<=\n)/, $text;
+        return (\@head, \@rec);
+    }
     my ($bt, $tc) = seed_batch(%a);
     my %batch = %$bt;
     my $nt = $batch{n_task};
@@ -387,6 +414,19 @@ sub mem {
 #   reference, the previous task's unmasked .fq; default lr_seqs), sr_seqs
 sub iteration {
     my (%a) = @_;
+    if (ref $a{ctx} ne 'CODE') {   # the seeding on the device too (iter_run_gpu)
+        my ($lr_pool, $lr_off) = pool($a{lr_seqs});
+        my ($sr_pool, $sr_off) = pool($a{sr_seqs});
+        my %batch = (sr_seq => $sr_pool, sr_off => $sr_off, lr_seq => $lr_pool, lr_off => $lr_off);
+        $batch{lr_qual} = join '', map {
+            my $q = $a{lr_quals} ? $a{lr_quals}[$_] : undef;
+            defined $q ? $q : '$' x length $a{lr_seqs}[$_]
+        } 0 .. $#{$a{lr_seqs}};
+        $batch{ref_seq} = join '', @{$a{ref_seqs}} if $a{ref_seqs};
+        my $o = iter_run_gpu(ref $a{ctx} ? $a{ctx}->handle : $a{ctx}, $a{seed_opts} || {}, $a{sw_opts} || {},
+                             $a{params} || {}, \%batch);
+        return cns_results($o, $a{lr_ids});
+    }
     my ($bt, $tc) = seed_batch(%a);
     my %batch = %$bt;   # bwa mode: the seeds as pr_seed_map returns them, grouped on the device
     $batch{lr_qual} = join '', map {

@@ -8,11 +8,13 @@ proovread calls (bin/proovread:1270, 1313; options from proovread.cfg:318-333):
 
 `index` checks the long-read file and records it (the seed index is rebuilt in
 memory by `mem`, in about a second per 15 Mb).  `mem` reads the long reads
-(FASTA/FASTQ), the short reads (FASTA/FASTQ, a file, `-` or /dev/fd/0), seeds and
-chains them on the host (libprgpu.so pr_seed_map, restating bwa's
-mem_collect_intv / mem_chain / mem_chain_flt), runs seed extension + CIGAR on
-the GPU (pr_sw_run: ksw_extend2 / ksw_global2 / mem_reg2aln, bit-exact to the
-SW oracle) and prints SAM: `QNAME FLAG RNAME POS MAPQ CIGAR * 0 0 SEQ QUAL
+(FASTA/FASTQ), the short reads (FASTA/FASTQ, a file, `-` or /dev/fd/0), builds the
+seed index in HBM and seeds and chains them on the GPU (pr_seed_gpu_index_build /
+pr_seed_gpu_map, restating bwa's mem_collect_intv / mem_chain / mem_chain_flt), runs
+bwa mode's seed extension + CIGAR on the seeds left in HBM (pr_sw_upload_gpu_seeds +
+pr_sw_launch: ksw_extend2 / ksw_global2 / mem_reg2aln, bit-exact to the SW oracle),
+applies -b/-l on the device (pr_sw_binfilter) and prints SAM formatted in native code
+(pr_sw_sam): `QNAME FLAG RNAME POS MAPQ CIGAR * 0 0 SEQ QUAL
 AS:i:score` for every chain whose alignment passes -T (AS >= T * aligned query
 length, cfg:324 "per-base-score"), with SEQ/QUAL printed for secondary hits too
 (bam2cns:347 needs them).  Per read the best AS is primary (MAPQ 60), others
@@ -37,6 +39,7 @@ filters) runs on the device (sw.run in bwa mode).  Not restated: bwa's MAPQ mode
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import re
 import gzip
 import os
@@ -200,7 +203,93 @@ class BinFilter:
         return rid
 
 
-def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=None) -> int:
+class SamIn(C.Structure):
+    _fields_ = [("sr_off", C.c_void_p), ("sr_text", C.c_void_p), ("sr_qual", C.c_void_p), ("sr_names", C.c_void_p),
+                ("sr_name_off", C.c_void_p), ("lr_names", C.c_void_p), ("lr_name_off", C.c_void_p),
+                ("keep", C.c_void_p), ("n_threads", C.c_int32)]
+
+
+def _name_pool(names: List[str]) -> Tuple[np.ndarray, np.ndarray]:
+    enc = [n.encode() for n in names]
+    off = np.zeros(len(enc) + 1, np.int64)
+    np.cumsum([len(x) for x in enc], out=off[1:])
+    return np.frombuffer(b"".join(enc) + b"\0", np.uint8).copy(), off
+
+
+def _header(out, lr_names, lr_seqs, argv) -> None:
+    out.write("@HD\tVN:1.5\tSO:unsorted\n")
+    for n, s in zip(lr_names, lr_seqs):
+        out.write(f"@SQ\tSN:{n}\tLN:{len(s)}\n")
+    out.write("@PG\tID:bwa-proovread\tPN:bwa-proovread\tVN:prgpu\tCL:bwa-proovread mem " + " ".join(argv) + "\n")
+
+
+def _mem_gpu(a, so, wo, argv, lr_names, lr_seqs, sr_names, sr_seqs, sr_quals, lr_pool, lr_off, sr_pool, sr_off, out,
+             log, ctx=None) -> int:
+    """The product path: the seed index built in HBM (pr_seed_gpu_index_build), the seeds kept
+    there (pr_seed_gpu_map), bwa mode on them (pr_sw_upload_gpu_seeds + pr_sw_launch), the
+    -b/-l filter on the device (pr_sw_binfilter) and the SAM text formatted natively
+    (pr_sw_sam): nothing per record in Python."""
+    from . import _abi, iteration
+    ctx = ctx or _abi.default_context()
+    L = _abi.lib()
+    seed._setup(L)
+    iteration._setup(L)
+    L.pr_sw_binfilter.argtypes = [C.c_void_p, C.c_int32, C.c_double, C.c_void_p]
+    L.pr_sw_sam.argtypes = [C.c_void_p, C.POINTER(SamIn), C.POINTER(C.c_void_p), C.POINTER(C.c_int64),
+                            C.POINTER(C.c_int64)]
+    L.pr_buffer_free.argtypes = [C.c_void_p]
+    L.pr_buffer_free.restype = None
+    n_lr, n_sr = len(lr_seqs), len(sr_seqs)
+    _abi.check(L.pr_seed_gpu_index_build(ctx.h, lr_pool.ctypes.data, lr_off.ctypes.data, n_lr),
+               "pr_seed_gpu_index_build")
+    st = np.zeros(max(1, n_sr), np.int32)
+    _abi.check(L.pr_seed_gpu_map(ctx.h, C.byref(so), sr_pool.ctypes.data, sr_off.ctypes.data, n_sr, None,
+                                 st.ctypes.data), "pr_seed_gpu_map")
+    n_seeds = C.c_int64()
+    _abi.check(L.pr_seed_gpu_seed_count(ctx.h, C.byref(n_seeds)), "pr_seed_gpu_seed_count")
+    print(f"[bwa-proovread] {n_sr} reads, {n_lr} long reads, {n_seeds.value} seeds (GPU)", file=log)
+    iteration.ShardSW(ctx, None, sr_off, 0, n_sr, None, lr_off, device_pools=True).launch(wo)
+    n_aln = C.c_int64()
+    _abi.check(L.pr_sw_aln_count(ctx.h, C.byref(n_aln)), "pr_sw_aln_count")
+    keep = None
+    if a.b > 0 and a.l > 0:
+        keep = np.zeros(max(1, n_aln.value), np.uint8)
+        _abi.check(L.pr_sw_binfilter(ctx.h, int(a.b), float(a.l), keep.ctypes.data), "pr_sw_binfilter")
+    text = np.frombuffer(b"".join(sr_seqs) + b"\0", np.uint8)
+    quals = None
+    if sr_quals and all(q is not None for q in sr_quals):
+        quals = np.frombuffer(b"".join(sr_quals) + b"\0", np.uint8)
+        if len(quals) != len(text):
+            raise ValueError("quality lines differ in length from their sequences")
+    srn, srn_off = _name_pool(sr_names)
+    lrn, lrn_off = _name_pool(lr_names)
+    si = SamIn(sr_off.ctypes.data, text.ctypes.data, None if quals is None else quals.ctypes.data, srn.ctypes.data,
+               srn_off.ctypes.data, lrn.ctypes.data, lrn_off.ctypes.data, None if keep is None else keep.ctypes.data,
+               int(a.t) if a.t and a.t > 1 else 0)
+    buf, ln, nrec = C.c_void_p(), C.c_int64(), C.c_int64()
+    _abi.check(L.pr_sw_sam(ctx.h, C.byref(si), C.byref(buf), C.byref(ln), C.byref(nrec)), "pr_sw_sam")
+    try:
+        _header(out, lr_names, lr_seqs, argv)
+        data = C.string_at(buf.value, ln.value) if ln.value else b""
+        if hasattr(out, "buffer"):
+            out.flush()
+            out.buffer.write(data)
+            out.buffer.flush()
+        else:
+            out.write(data.decode())
+    finally:
+        if buf.value:
+            L.pr_buffer_free(buf)
+    if keep is not None:
+        print(f"[bwa-proovread] -b {a.b} -l {a.l}: {nrec.value} of {int(n_aln.value)} alignments kept (device filter)",
+              file=log)
+    return 0
+
+
+def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=None, ctx=None) -> int:
+    """bwa-proovread mem.  Product path: seeding, SW, -b/-l and SAM on the device and in native
+    code (_mem_gpu).  sw_runner (tests): the host seeding front end (pr_seed_map) with that SW
+    runner in place of the device, records formatted here."""
     out = out or sys.stdout
     log = log or sys.stderr
     a = parse_mem(argv)
@@ -209,6 +298,9 @@ def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=Non
     sr_names, sr_seqs, sr_quals = read_fastx(a.reads)
     lr_pool, lr_off = _pool(lr_seqs)
     sr_pool, sr_off = _pool(sr_seqs)
+    if sw_runner is None:
+        return _mem_gpu(a, so, wo, argv, lr_names, lr_seqs, sr_names, sr_seqs, sr_quals, lr_pool, lr_off, sr_pool,
+                        sr_off, out, log, ctx)
     ix = seed.SeedIndex(lr_pool, lr_off)
     tasks = ix.map(sr_pool, sr_off, so, threads=a.t)
     ix.close()
@@ -220,11 +312,8 @@ def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=Non
                      tasks["strand"].astype(np.uint8), tasks["qbeg"].astype(np.int32),
                      tasks["rbeg"].astype(np.int32), tasks["slen"].astype(np.int32),
                      tasks["chain"].astype(np.int32))
-    res = (sw_runner or sw.run)(inp, wo)
-    out.write("@HD\tVN:1.5\tSO:unsorted\n")
-    for n, s in zip(lr_names, lr_seqs):
-        out.write(f"@SQ\tSN:{n}\tLN:{len(s)}\n")
-    out.write("@PG\tID:bwa-proovread\tPN:bwa-proovread\tVN:prgpu\tCL:bwa-proovread mem " + " ".join(argv) + "\n")
+    res = sw_runner(inp, wo)
+    _header(out, lr_names, lr_seqs, argv)
     filt = BinFilter(a.b, a.l) if a.b > 0 and a.l > 0 else None
     records = []
     for i in range(res.n):

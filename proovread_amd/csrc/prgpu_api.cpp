@@ -1368,6 +1368,68 @@ extern "C" int pr_iter_launch(pr_ctx *c, const pr_sw_opts *o, const pr_cns_param
     return pr_cns_launch(c, p);
 }
 
+int sw_keep_to_sam(pr_ctx *c, const uint8_t *keep_grouped, uint8_t *keep_sam);
+
+// bwa-proovread -b/-l on the last bwa-mode SW launch alone (the `mem` drop-in): the hand-off's
+// grouping by long read and pipe_binfilter_kernel, as pr_iter_launch runs them
+extern "C" int pr_sw_binfilter(pr_ctx *c, int32_t bin_size, double bin_length, uint8_t *keep) {
+    if (!c || !keep) return set_error(PR_ERR_ARG, "null arg");
+    if (bin_size <= 0 || !(bin_length > 0)) return set_error(PR_ERR_ARG, "-b / -l must be positive");
+    HIPCHK(hipSetDevice(c->device));
+    SwPtrs sp;
+    int rc;
+    if ((rc = sw_get_pipe_ptrs(c, &sp, true))) return rc;
+    if (!sp.task_off) return set_error(PR_ERR_ARG, "pr_sw_binfilter: bwa mode only");
+    const int n_lr = sp.n_lr;
+    if (n_lr == 0 || sp.n_task == 0) return 0;
+    std::vector<int64_t> lo((size_t)n_lr + 1);
+    HIPCHK(hipMemcpyAsync(lo.data(), sp.lr_off, ((size_t)n_lr + 1) * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int64_t lmax = 0;
+    for (int i = 0; i < n_lr; ++i) lmax = std::max(lmax, lo[(size_t)i + 1] - lo[(size_t)i]);
+    const int64_t max_bins = (lmax + 1024) / bin_size + 2;
+    if ((2 * max_bins + 256) * 4 > 160 * 1024)
+        return set_error(PR_ERR_CAPACITY, "-b/-l filter: %lld bins per long read exceed the LDS layout", (long long)max_bins);
+    const size_t nt1 = (size_t)sp.n_task + 1;
+    if ((rc = c->pb[2].ensure(((size_t)n_lr + 1) * 4)) || (rc = c->pb[3].ensure(nt1)) || (rc = c->pb[4].ensure(nt1 * 4)) ||
+        (rc = c->pb[5].ensure(nt1 * 4)) || (rc = c->pb[6].ensure(nt1 * 8)) || (rc = c->pb[7].ensure(nt1 * 4)) ||
+        (rc = c->pb[8].ensure(nt1 * 8)) || (rc = c->pb[9].ensure(nt1 * 4)))
+        return rc;
+    PipeDev P;
+    std::memset(&P, 0, sizeof P);
+    P.n_lr = n_lr;
+    P.task_off = sp.task_off;
+    P.t_sr = sp.t_sr;
+    P.strand = sp.strand;
+    P.pass = sp.pass;
+    P.status = sp.status;
+    P.pos = sp.pos;
+    P.score = sp.score;
+    P.ncig = sp.ncig;
+    P.sr_off = sp.sr_off;
+    P.cig_at = sp.cig_at;
+    P.lr_off = sp.lr_off;
+    P.cig = sp.cig;
+    P.err = c->pb[2].as<int32_t>();
+    P.keep = c->pb[3].as<uint8_t>();
+    P.fsorted = c->pb[4].as<int32_t>();
+    P.fbin = c->pb[5].as<int32_t>();
+    P.fnc = c->pb[6].as<double>();
+    P.flen = c->pb[7].as<int32_t>();
+    P.flst = c->pb[8].as<double>();
+    P.flsti = c->pb[9].as<int32_t>();
+    HIPCHK(hipMemsetAsync(c->pb[2].p, 0, (size_t)n_lr * 4, c->stream));
+    const int grid_f = n_lr < c->n_cu * 8 ? n_lr : c->n_cu * 8;
+    const int e = pipe_binfilter_launch(P, bin_size, bin_length, (int)max_bins, grid_f, (void *)c->stream);
+    if (e) return set_error(PR_ERR_HIP, "-b/-l filter kernel: %s", hipGetErrorString((hipError_t)e));
+    std::vector<int32_t> err((size_t)n_lr);
+    HIPCHK(hipMemcpyAsync(err.data(), c->pb[2].p, (size_t)n_lr * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < n_lr; ++i)
+        if (err[(size_t)i]) return set_error(PR_ERR_CAPACITY, "-b/-l filter of long read %d failed (code %d)", i, err[(size_t)i]);
+    return sw_keep_to_sam(c, c->pb[3].as<uint8_t>(), keep);
+}
+
 extern "C" int pr_iter_download(pr_ctx *c, pr_cns_out *o) {
     if (!c) return set_error(PR_ERR_ARG, "null ctx");
     int rc = pr_cns_download(c, o);

@@ -244,10 +244,13 @@ constexpr int LC_MAX = 6;
 SC_HD constexpr int lc_off(int j) { return ((1 << (2 * j)) - 4) / 3; }
 constexpr int LC_N = lc_off(LC_MAX + 1);   // 4 + 16 + ... + 4^LC_MAX
 
-struct Occ;
-SC_HD void materialize(const Occ &occ, int a);
+template <bool LZ> struct OccB;
+SC_HD void materialize(const OccB<true> &occ, int a);
 
-struct Occ {
+// The occurrence counts of read q's substrings.  LZ: the lazy table (Scratch.hend), a start
+// materialized on first use; the eager table's code (LZ = false) has no trace of it.
+template <bool LZ>
+struct OccB {
     const IndexView *I;
     const Scratch *S;
     const uint8_t *q;
@@ -256,21 +259,27 @@ struct Occ {
 
     // the lazy table's start a on first use (a no-op for the eager table)
     SC_HD void need(int a) const {
-        if (S->hend && a < len && !S->ready[a]) materialize(*this, a);
+        if constexpr (LZ) {
+            if (a < len && !S->ready[a]) materialize(*this, a);
+        }
+    }
+
+    // occ(a, b) for b - a < KI: the j-mer count tables (no occurrence-table access)
+    SC_HD int64_t jmer(int a, int b) const {
+        const int n = b - a;
+        uint32_t code = 0;
+        const int32_t c12 = a + KI <= len ? S->codes[a] : -1;
+        if (c12 >= 0) code = (uint32_t)c12 >> (2 * (KI - n));   // the start's 12-mer code, truncated
+        else
+            for (int x = a; x < b; ++x) code = (code << 2) | q[x];
+        if (lc && n <= LC_MAX) return lc[lc_off(n) + code];
+        return I->cnt[n - 1][code];
     }
 
     SC_HD int64_t operator()(int a, int b) const {
         const int n = b - a;
         SC_STAT(8, 1);
-        if (n < KI) {
-            uint32_t code = 0;
-            const int32_t c12 = a + KI <= len ? S->codes[a] : -1;
-            if (c12 >= 0) code = (uint32_t)c12 >> (2 * (KI - n));   // the start's 12-mer code, truncated
-            else
-                for (int x = a; x < b; ++x) code = (code << 2) | q[x];
-            if (lc && n <= LC_MAX) return lc[lc_off(n) + code];
-            return I->cnt[n - 1][code];
-        }
+        if (n < KI) return jmer(a, b);
         need(a);
         if (n - KI < HB) return S->ge[(int64_t)a * HB + (n - KI)];
         int64_t c = 0;
@@ -302,6 +311,8 @@ struct Occ {
         return c;
     }
 };
+using Occ = OccB<false>;
+using OccLazy = OccB<true>;
 
 // The end of the longest match from start a that occurs >= k times in the text:
 // R_k(a) = max{e : occ(a, e) >= k} (a when even q[a] occurs fewer than k times or is N).
@@ -313,9 +324,10 @@ SC_HD int short_limit(const uint8_t *q, int len, int a) {   // the N-free bases 
     while (e < len && e - a < KI - 1 && q[e] < 4) ++e;
     return e;
 }
-SC_HD int rmax_short(const Occ &occ, const uint8_t *q, int len, int a, int64_t k) {
+template <class OccT>
+SC_HD int rmax_short(const OccT &occ, const uint8_t *q, int len, int a, int64_t k) {
     int e = short_limit(q, len, a);   // from the longest down: one lookup when it qualifies
-    while (e > a && occ(a, e) < k) --e;
+    while (e > a && occ.jmer(a, e) < k) --e;
     return e;
 }
 
@@ -334,7 +346,8 @@ SC_HD void topk_insert(uint16_t (&top)[RK], uint16_t v) {
 }
 // R_1 .. R_RK of start a from its top list (the RK largest hit match lengths, 0-padded; all
 // zero when the start has no 12-mer or q[a] is N)
-SC_HD void fill_rk_top(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a, const uint16_t (&top)[RK]) {
+template <class OccT>
+SC_HD void fill_rk_top(const OccT &occ, const Scratch &S, const uint8_t *q, int len, int a, const uint16_t (&top)[RK]) {
     uint16_t *r = S.rmax + (int64_t)a * RK;
     int e = -1;   // the short part: j-mer counts never grow with k, so its end only falls
     int64_t ce = 0;
@@ -345,16 +358,17 @@ SC_HD void fill_rk_top(const Occ &occ, const Scratch &S, const uint8_t *q, int l
         }
         if (e < 0) {
             e = short_limit(q, len, a);
-            ce = e > a ? occ(a, e) : 0;
+            ce = e > a ? occ.jmer(a, e) : 0;
         }
         while (e > a && ce < k) {
             --e;
-            ce = e > a ? occ(a, e) : 0;
+            ce = e > a ? occ.jmer(a, e) : 0;
         }
         r[k - 1] = (uint16_t)e;
     }
 }
-SC_HD void fill_rk(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a) {
+template <class OccT>
+SC_HD void fill_rk(const OccT &occ, const Scratch &S, const uint8_t *q, int len, int a) {
     uint16_t top[RK];
 #pragma unroll
     for (int k = 0; k < RK; ++k) top[k] = 0;
@@ -365,7 +379,8 @@ SC_HD void fill_rk(const Occ &occ, const Scratch &S, const uint8_t *q, int len, 
 
 // R_k(a): tabulated for k <= RK; beyond (re-seeding with split_width >= RK), from the start's
 // count row and its hits' lengths
-SC_HD int rmax_k(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int a, int64_t k) {
+template <class OccT>
+SC_HD int rmax_k(const OccT &occ, const Scratch &S, const uint8_t *q, int len, int a, int64_t k) {
     if (k < 1) k = 1;
     occ.need(a);
     if (k <= RK) return S.rmax[(int64_t)a * RK + (k - 1)];
@@ -435,7 +450,10 @@ SC_HD int hit_ml(const IndexView &I, const Scratch &S, const uint8_t *q, int len
 // The lazy table's start a (Scratch.hend): its hits appended to the read's pool with their match
 // lengths and coordinates, its count row and R_1 .. R_RK -- the values the eager table holds for
 // it.  A pool that would overflow flags the read (lz[1]) and records the hits it needs (lz[2]).
-SC_HD void materialize(const Occ &occ, int a) {
+#if defined(__HIPCC__)
+__attribute__((noinline))   // (out of line: the eager table's kernels only test S.hend)
+#endif
+SC_HD void materialize(const OccLazy &occ, int a) {
     const IndexView &I = *occ.I;
     const Scratch &S = *occ.S;
     const uint8_t *q = occ.q;
@@ -618,7 +636,8 @@ SC_HD void iv_reverse(Iv *v, int n) {
 
 // bwt_smem1a (max_intv = 0): SMEMs covering x with >= min_intv occurrences, sorted by
 // start, into mem[0, *nmem); returns the end of the longest forward match from x.
-SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int x, int64_t min_intv, Iv *mem,
+template <class OccT>
+SC_HD int smem1(const OccT &occ, const Scratch &S, const uint8_t *q, int len, int x, int64_t min_intv, Iv *mem,
                 int &nmem, int &err) {
     nmem = 0;
     if (q[x] > 3) return x + 1;
@@ -719,7 +738,8 @@ SC_HD int smem1(const Occ &occ, const Scratch &S, const uint8_t *q, int len, int
 }
 
 // bwt_seed_strategy1: the shortest match from x longer than min_len with < max_intv hits
-SC_HD int seed_strategy1(const Occ &occ, const uint8_t *q, int len, int x, int min_len, int64_t max_intv, Iv &m) {
+template <class OccT>
+SC_HD int seed_strategy1(const OccT &occ, const uint8_t *q, int len, int x, int min_len, int64_t max_intv, Iv &m) {
     m = Iv{0, 0, 0};
     if (q[x] > 3) return x + 1;
     for (int i = x + 1; i < len; ++i) {
@@ -754,7 +774,8 @@ SC_HD int seed_strategy1(const Occ &occ, const uint8_t *q, int len, int x, int m
 #endif
 
 // mem_collect_intv -> S.mems[0, return) sorted by (start, end), stable
-SC_HD int collect_intv(const Occ &occ, Scratch &S, const pr_seed_opts &O, const uint8_t *q, int len, int &err,
+template <class OccT>
+SC_HD int collect_intv(const OccT &occ, Scratch &S, const pr_seed_opts &O, const uint8_t *q, int len, int &err,
                        unsigned long long *ticks = nullptr) {
 #if defined(__HIP_DEVICE_COMPILE__)
     unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
@@ -1018,6 +1039,7 @@ SC_HD int chain_seq(const IndexView &I, const pr_seed_opts &O, Scratch &S, int n
 // Returns 0 or an SC_OVER_* mask (then the read's output is not valid).
 // ticks (device, optional): wall-clock ticks added per part [SMEMs, chaining, filter + output]
 // Part 1: SMEMs, chaining and mem_chain_flt; *n_chains = the chains in S.ch (kept flags set).
+template <bool LZ = false>
 SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int *n_chains,
                      unsigned long long *ticks = nullptr, const uint32_t *lcnt = nullptr) {
     *n_chains = 0;
@@ -1025,9 +1047,9 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
 #if defined(__HIP_DEVICE_COMPILE__)
     unsigned long long t_last = ticks ? __builtin_amdgcn_s_memrealtime() : 0ULL;
 #endif
-    const Occ occ{&I, &S, q, len, lcnt};
+    const OccB<LZ> occ{&I, &S, q, len, lcnt};
     const int nm = collect_intv(occ, S, O, q, len, err, ticks);
-    if (S.hend) err |= S.lz[1];   // the lazy table's pool overflowed: the counts are not valid
+    if (LZ) err |= S.lz[1];   // the lazy table's pool overflowed: the counts are not valid
     if (err) return err;
     SC_STAT(0, 1);
     SC_STAT(1, nm);
@@ -1036,7 +1058,7 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
 #endif
     int ncv = 0;
     err = chain_seq(I, O, S, nm, &ncv);
-    if (S.hend) err |= S.lz[1];
+    if (LZ) err |= S.lz[1];
     if (err) return err;
     SC_TICK(3);
     SC_STAT(11, ncv);
@@ -1341,12 +1363,13 @@ SC_HD int map_output(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
 }
 
 // Everything after the occurrence table: parts 1 and 2 on one thread.
+template <bool LZ = false>
 SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
                         pr_seed_task *out, int cap_out, int *n_out, unsigned long long *ticks = nullptr,
                         const uint32_t *lcnt = nullptr, int16_t *dp16 = nullptr) {
     *n_out = 0;
     int nch = 0;
-    const int err = map_chains(I, O, S, q, len, &nch, ticks, lcnt);
+    const int err = map_chains<LZ>(I, O, S, q, len, &nch, ticks, lcnt);
     if (err) return err;
     return map_output(I, O, S, q, len, sid, nch, out, cap_out, n_out, nullptr, ticks, dp16);
 }
@@ -1356,9 +1379,12 @@ SC_HD int map_after_occ(const IndexView &I, const pr_seed_opts &O, Scratch &S, c
 SC_HD int map_read(const IndexView &I, const pr_seed_opts &O, Scratch &S, const uint8_t *q, int len, int sid,
                    pr_seed_task *out, int cap_out, int *n_out) {
     *n_out = 0;
-    const int err = S.hend ? build_starts(I, S, q, len) : build_occ(I, S, q, len);
-    if (err) return err;
-    return map_after_occ(I, O, S, q, len, sid, out, cap_out, n_out);
+    if (S.hend) {
+        const int err = build_starts(I, S, q, len);
+        return err ? err : map_after_occ<true>(I, O, S, q, len, sid, out, cap_out, n_out);
+    }
+    const int err = build_occ(I, S, q, len);
+    return err ? err : map_after_occ<false>(I, O, S, q, len, sid, out, cap_out, n_out);
 }
 
 // Whether the device path builds the lazy occurrence table for these options: the finish tasks'

@@ -867,6 +867,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
 // with 64 reads' loads in flight per wave instead of one.  Scratch: 64 small slices per wave
 // (D.caps sized for the batch's read lengths); a read that outgrows its slice is flagged and
 // goes to pass 2.
+template <bool LZ>   // LZ: the lazy occurrence table (D.caps.lazy), a separate kernel so the eager one carries none of it
 __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(SeedDev D) {
     __shared__ __attribute__((aligned(16))) int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint64_t q4_lds[SEED_WAVES][SEED_LMAX / 16 + 4];
@@ -912,7 +913,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
             if (len > 0 && !err)
                 err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt, &nh, D.prof ? ot : nullptr,
-                                     D.caps.lazy != 0);
+                                     LZ);
             if (lane == rd) my_err = err, my_hits = nh;
         }
         const unsigned long long t1 = D.prof ? wall_clock64() : 0ULL;
@@ -923,13 +924,13 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             seedc::Scratch S = seedc::carve(base + (int64_t)lane * D.stride, D.caps);
             int n = 0, err = my_err;
             if (len > 0 && !err)
-                err = seedc::map_after_occ(D.V, D.O, S, D.sr_seq + o, len, i, D.out + (int64_t)(i - D.out0) * D.caps.out,
+                err = seedc::map_after_occ<LZ>(D.V, D.O, S, D.sr_seq + o, len, i, D.out + (int64_t)(i - D.out0) * D.caps.out,
                                            D.caps.out, &n, D.prof ? lt : nullptr, lcnt,
                                            D.dp ? D.dp + slot * (2 * 201 * 64) + lane : nullptr);
             // a read whose hit table overflowed reports the hits it needs (the retry pass sizes
             // its slices from them: texts of 1 - 3 Gb give ~20-50 k hits per 150 bp read)
             D.n_out[i] = (my_err & seedc::SC_OVER_HITS) ? -my_hits
-                         : (D.caps.lazy && (err & seedc::SC_OVER_HITS)) ? -S.lz[2]   // (the lazy pool's need)
+                         : (LZ && (err & seedc::SC_OVER_HITS)) ? -S.lz[2]   // (the lazy pool's need)
                                                                         : (err ? 0 : n);
             D.status[i] = err;
         }
@@ -1014,7 +1015,10 @@ int seed_launch(const SeedDev &D, void *stream) {
 int seed_batch_launch(const SeedDev &D, void *stream) {
     if (D.n_sr <= 0) return 0;
     const int64_t blocks = (D.n_lanes + SEED_WAVES - 1) / SEED_WAVES;
-    hipLaunchKernelGGL(seed_batch_kernel, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
+    if (D.caps.lazy)
+        hipLaunchKernelGGL(seed_batch_kernel<true>, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
+    else
+        hipLaunchKernelGGL(seed_batch_kernel<false>, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
     return (int)hipGetLastError();
 }
 

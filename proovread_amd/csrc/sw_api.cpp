@@ -4,6 +4,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/prgpu.h"
@@ -730,18 +732,21 @@ struct BwaRows {
     int32_t *qb, *qe, *rb, *re, *score, *truesc, *pos, *ncig, *status, *task;
     int64_t *cig_at;
     uint8_t *pass;
+    int32_t *sr, *lr;   // the alignment's short read, long read and strand (its seed task's)
+    uint8_t *strand;
 };
 static int bwa_gather(pr_ctx *c, SwResident &r, BwaRows &g) {
     hipStream_t s = ctx_stream(c);
     const int64_t n = r.n_aln;
     const size_t n1 = (size_t)n + 1;
     int rc;
-    if ((rc = ensure(r, SB_GDOWN, n1 * (10 * 4 + 8 + 1) + 64))) return rc;
+    if ((rc = ensure(r, SB_GDOWN, n1 * (12 * 4 + 8 + 2) + 64))) return rc;
     char *b = (char *)r.buf[SB_GDOWN];
-    int32_t **f[10] = {&g.qb, &g.qe, &g.rb, &g.re, &g.score, &g.truesc, &g.pos, &g.ncig, &g.status, &g.task};
-    for (int k = 0; k < 10; ++k) *f[k] = (int32_t *)(b + (size_t)k * n1 * 4);
-    g.cig_at = (int64_t *)(b + ((10 * n1 * 4 + 7) & ~(size_t)7));
+    int32_t **f[12] = {&g.qb, &g.qe, &g.rb, &g.re, &g.score, &g.truesc, &g.pos, &g.ncig, &g.status, &g.task, &g.sr, &g.lr};
+    for (int k = 0; k < 12; ++k) *f[k] = (int32_t *)(b + (size_t)k * n1 * 4);
+    g.cig_at = (int64_t *)(b + ((12 * n1 * 4 + 7) & ~(size_t)7));
     g.pass = (uint8_t *)(g.cig_at + n1);
+    g.strand = g.pass + n1;
     SwGather G;
     std::memset(&G, 0, sizeof G);
     G.list = (const int32_t *)r.buf[SB_ALIST];
@@ -762,6 +767,8 @@ static int bwa_gather(pr_ctx *c, SwResident &r, BwaRows &g) {
     G.o_qb = g.qb; G.o_qe = g.qe; G.o_rb = g.rb; G.o_re = g.re; G.o_score = g.score; G.o_truesc = g.truesc;
     G.o_pos = g.pos; G.o_ncig = g.ncig; G.o_status = g.status; G.o_task = g.task; G.o_cig_at = g.cig_at;
     G.o_pass = g.pass;
+    G.strand = (const uint8_t *)r.buf[SB_T_STRAND];
+    G.o_sr = g.sr; G.o_lr = g.lr; G.o_strand = g.strand;
     const int e = sw_launch_gather(G, (void *)s);
     if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     return 0;
@@ -885,6 +892,159 @@ extern "C" int pr_sw_aln_count(pr_ctx *c, int64_t *n_aln) {
     HIPCHK(hipSetDevice(ctx_device(c)));
     HIPCHK(hipStreamSynchronize(ctx_stream(c)));
     *n_aln = r.bwa ? r.n_aln : r.n_task;
+    return 0;
+}
+
+// pr_sw_binfilter's keep flags (computed per alignment in the long-read grouping of bwa_group,
+// on the device) into SAM order: the grouping lists the alignments' tasks (SB_GLIST), SAM order
+// lists them too (SB_ALIST), and a task reports at most one alignment
+int sw_keep_to_sam(pr_ctx *c, const uint8_t *keep_grouped, uint8_t *keep_sam) {
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded || !r.bwa) return pr_set_error(PR_ERR_ARG, "no resident bwa-mode SW batch");
+    hipStream_t s = ctx_stream(c);
+    const size_t n = (size_t)r.n_aln;
+    std::vector<int32_t> gl(n + 1), al(n + 1);
+    std::vector<uint8_t> kg(n + 1);
+    if (n) {
+        HIPCHK(hipMemcpyAsync(gl.data(), r.buf[SB_GLIST], n * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(al.data(), r.buf[SB_ALIST], n * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(kg.data(), keep_grouped, n, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<uint8_t> by_task((size_t)r.n_task + 1, 0);
+    for (size_t j = 0; j < n; ++j) {
+        if (gl[j] < 0 || gl[j] >= r.n_task) return pr_set_error(PR_ERR_ARG, "alignment grouping out of range");
+        by_task[(size_t)gl[j]] = kg[j];
+    }
+    for (size_t i = 0; i < n; ++i) keep_sam[i] = by_task[(size_t)al[i]];
+    return 0;
+}
+
+extern "C" int pr_sw_sam(pr_ctx *c, const pr_sam_in *in, char **text, int64_t *len, int64_t *n_records) {
+    if (!c || !in || !text || !len || !in->sr_off || !in->sr_text || !in->sr_names || !in->sr_name_off ||
+        !in->lr_names || !in->lr_name_off)
+        return pr_set_error(PR_ERR_ARG, "null arg");
+    *text = nullptr;
+    *len = 0;
+    SwResident &r = ctx_sw(c);
+    if (!r.loaded || !r.bwa) return pr_set_error(PR_ERR_ARG, "no resident bwa-mode SW batch (pr_sw_launch first)");
+    HIPCHK(hipSetDevice(ctx_device(c)));
+    hipStream_t s = ctx_stream(c);
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipGetLastError());
+    const size_t n = (size_t)r.n_aln;
+    BwaRows g;
+    int rc;
+    if ((rc = bwa_gather(c, r, g))) return rc;
+    std::vector<int32_t> pos(n + 1), score(n + 1), ncig(n + 1), st(n + 1), sr(n + 1), lr(n + 1), flag(n + 1);
+    std::vector<uint8_t> pass(n + 1), strand(n + 1);
+    auto d32 = [&](std::vector<int32_t> &h, const void *dv) -> int {
+        if (n) HIPCHK(hipMemcpyAsync(h.data(), dv, n * 4, hipMemcpyDeviceToHost, s));
+        return 0;
+    };
+    if ((rc = d32(pos, g.pos)) || (rc = d32(score, g.score)) || (rc = d32(ncig, g.ncig)) || (rc = d32(st, g.status)) ||
+        (rc = d32(sr, g.sr)) || (rc = d32(lr, g.lr)) || (rc = d32(flag, r.buf[SB_AFLAG])))
+        return rc;
+    if (n) {
+        HIPCHK(hipMemcpyAsync(pass.data(), g.pass, n, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(strand.data(), g.strand, n, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    // the printed alignments' CIGARs, compacted on the device
+    std::vector<int64_t> off(n + 1, 0);
+    for (size_t t = 0; t < n; ++t) {
+        const bool pr = st[t] == 0 && pass[t] && (!in->keep || in->keep[t]);
+        off[t + 1] = off[t] + (pr ? ncig[t] : 0);
+        if (!pr) ncig[t] = -1;
+    }
+    std::vector<uint32_t> cig((size_t)off[n] + 1);
+    if (off[n]) {
+        std::vector<int32_t> nc_dev(n);
+        for (size_t t = 0; t < n; ++t) nc_dev[t] = ncig[t] < 0 ? 0 : ncig[t];
+        if ((rc = up(r, SB_CIGOFF, off.data(), n + 1, s)) || (rc = ensure(r, SB_CIGOUT, (size_t)off[n] * 4))) return rc;
+        // the compaction reads its op counts from the device: the printed ones, 0 for the rest
+        HIPCHK(hipMemcpyAsync(g.ncig, nc_dev.data(), n * 4, hipMemcpyHostToDevice, s));
+        const int e = sw_launch_cig_compact((const uint32_t *)r.buf[SB_CIG], g.cig_at, g.ncig,
+                                            (const int64_t *)r.buf[SB_CIGOFF], (int64_t)n, (uint32_t *)r.buf[SB_CIGOUT],
+                                            (void *)s);
+        if (e) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipMemcpyAsync(cig.data(), r.buf[SB_CIGOUT], (size_t)off[n] * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+    }
+    const int64_t n_sr = r.n_sr, n_lr = r.n_lr;
+    for (size_t t = 0; t < n; ++t)
+        if (ncig[t] >= 0 && (sr[t] < 0 || sr[t] >= n_sr || lr[t] < 0 || lr[t] >= n_lr))
+            return pr_set_error(PR_ERR_ARG, "pr_sw_sam: an alignment names a read outside the batch");
+    // the records, formatted in parallel over ranges of alignments (SAM order kept)
+    int nt = in->n_threads > 0 ? in->n_threads : (int)std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : (nt > 64 ? 64 : nt);
+    if ((size_t)nt > n / 1024 + 1) nt = (int)(n / 1024 + 1);
+    std::vector<std::string> parts((size_t)nt);
+    std::vector<int64_t> nrec((size_t)nt, 0);
+    static const char OPS[] = "MIDNSHP=X";
+    static const char CMP[] = "TGCAN";   // reverse complement of nt4 codes A0 C1 G2 T3 N4
+    auto work = [&](int k) {
+        const size_t t0 = n * (size_t)k / (size_t)nt, t1 = n * (size_t)(k + 1) / (size_t)nt;
+        std::string &o = parts[(size_t)k];
+        char num[32];
+        for (size_t t = t0; t < t1; ++t) {
+            if (ncig[t] < 0) continue;
+            const int64_t q0 = in->sr_off[sr[t]], q1 = in->sr_off[sr[t] + 1];
+            o.append(in->sr_names + in->sr_name_off[sr[t]], (size_t)(in->sr_name_off[sr[t] + 1] - in->sr_name_off[sr[t]]));
+            o += '\t';
+            o += std::to_string(flag[t]);
+            o += '\t';
+            o.append(in->lr_names + in->lr_name_off[lr[t]], (size_t)(in->lr_name_off[lr[t] + 1] - in->lr_name_off[lr[t]]));
+            std::snprintf(num, sizeof num, "\t%d\t%d\t", pos[t] + 1, (flag[t] & 0x100) ? 0 : 60);
+            o += num;
+            for (int64_t x = off[t]; x < off[t + 1]; ++x) {
+                o += std::to_string(cig[(size_t)x] >> 4);
+                o += OPS[cig[(size_t)x] & 15u];
+            }
+            o += "\t*\t0\t0\t";
+            if (strand[t]) {
+                for (int64_t x = q1 - 1; x >= q0; --x) {
+                    const uint8_t b = in->sr_text[x] | 0x20;
+                    o += CMP[b == 'a' ? 0 : b == 'c' ? 1 : b == 'g' ? 2 : b == 't' ? 3 : 4];
+                }
+            } else {
+                for (int64_t x = q0; x < q1; ++x) {
+                    const uint8_t b = in->sr_text[x];
+                    o += (char)(b >= 'a' && b <= 'z' ? b - 32 : b);
+                }
+            }
+            o += '\t';
+            if (!in->sr_qual) o += '*';
+            else if (strand[t])
+                for (int64_t x = q1 - 1; x >= q0; --x) o += (char)in->sr_qual[x];
+            else
+                o.append((const char *)in->sr_qual + q0, (size_t)(q1 - q0));
+            o += "\tAS:i:";
+            o += std::to_string(score[t]);
+            o += '\n';
+            ++nrec[(size_t)k];
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int k = 1; k < nt; ++k) th.emplace_back(work, k);
+        work(0);
+        for (auto &x : th) x.join();
+    }
+    size_t tot = 0;
+    int64_t nr = 0;
+    for (int k = 0; k < nt; ++k) tot += parts[(size_t)k].size(), nr += nrec[(size_t)k];
+    char *buf = (char *)std::malloc(tot + 1);
+    if (!buf) return pr_set_error(PR_ERR_ARG, "pr_sw_sam: out of host memory for the SAM text");
+    size_t at = 0;
+    for (int k = 0; k < nt; ++k) {
+        std::memcpy(buf + at, parts[(size_t)k].data(), parts[(size_t)k].size());
+        at += parts[(size_t)k].size();
+    }
+    buf[tot] = 0;
+    *text = buf;
+    *len = (int64_t)tot;
+    if (n_records) *n_records = nr;
     return 0;
 }
 
