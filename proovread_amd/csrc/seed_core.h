@@ -234,9 +234,6 @@ SC_HD uint64_t nib16c(const uint64_t *w4, uint64_t x) {
     return sh ? (lo >> sh) | (w4[w + 1] << (64 - sh)) : lo;
 }
 
-// the end of start a's hits in the occurrence table
-SC_HD int32_t hit_end(const Scratch &S, int a) { return S.hend ? S.hend[a] : S.hoff[a + 1]; }
-
 // ---------------------------------------------------------------- occurrence table
 // the j-mer count tables j = 1..LC_MAX held on chip by the device kernels (5,460 entries):
 // table j at LC_OFF(j) = (4^j - 4) / 3
@@ -263,6 +260,11 @@ struct OccB {
             if (a < len && !S->ready[a]) materialize(*this, a);
         }
     }
+    // the end of start a's hits (the eager table: the next start's offset)
+    SC_HD int32_t end_of(int a) const {
+        if constexpr (LZ) return S->hend[a];
+        else return S->hoff[a + 1];
+    }
 
     // occ(a, b) for b - a < KI: the j-mer count tables (no occurrence-table access)
     SC_HD int64_t jmer(int a, int b) const {
@@ -284,7 +286,7 @@ struct OccB {
         if (n - KI < HB) return S->ge[(int64_t)a * HB + (n - KI)];
         int64_t c = 0;
         SC_STAT(9, 1);
-        const int32_t h1 = hit_end(*S, a);
+        const int32_t h1 = end_of(a);
         SC_STAT(10, h1 - S->hoff[a]);
         for (int32_t k = S->hoff[a]; k < h1; ++k) c += S->hml[k] >= n;
         return c;
@@ -297,7 +299,7 @@ struct OccB {
         int64_t c = 0;
         int m = 0x7fffffff;
         need(a);
-        const int32_t h1 = hit_end(*S, a);
+        const int32_t h1 = end_of(a);
         SC_STAT(9, 1);
         SC_STAT(10, h1 - S->hoff[a]);
         for (int32_t k = S->hoff[a]; k < h1; ++k) {
@@ -401,7 +403,8 @@ SC_HD int rmax_k(const OccT &occ, const Scratch &S, const uint8_t *q, int len, i
             while (lo < hi) {
                 const int mid = (lo + hi + 1) >> 1;
                 int64_t c = 0;
-                for (int32_t h = S.hoff[a]; h < hit_end(S, a); ++h) c += S.hml[h] >= mid;
+                const int32_t h1 = occ.end_of(a);
+                for (int32_t h = S.hoff[a]; h < h1; ++h) c += S.hml[h] >= mid;
                 if (c >= k) lo = mid; else hi = mid - 1;
             }
             return a + lo;
@@ -1031,6 +1034,7 @@ SC_HD int seed_sw_score(const IndexView &I, const pr_seed_opts &O, const uint8_t
 }
 
 SC_HD void chain_flt(const pr_seed_opts &O, Scratch &S, int ncv, int *n_chains);
+template <bool LZ = false>
 SC_HD int chain_seq(const IndexView &I, const pr_seed_opts &O, Scratch &S, int nm, int *n_cv);
 
 // Everything after the occurrence table (S.hoff / hpos / hml / ge of the read, built by
@@ -1057,7 +1061,7 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
     if (ticks) t_last = __builtin_amdgcn_s_memrealtime();
 #endif
     int ncv = 0;
-    err = chain_seq(I, O, S, nm, &ncv);
+    err = chain_seq<LZ>(I, O, S, nm, &ncv);
     if (LZ) err |= S.lz[1];
     if (err) return err;
     SC_TICK(3);
@@ -1070,6 +1074,7 @@ SC_HD int map_chains(const IndexView &I, const pr_seed_opts &O, Scratch &S, cons
 
 // mem_chain over the SMEMs S.mems[0, nm) -> the chains S.cv[0, *n_cv) in creation order
 // (one thread); 0 or SC_OVER_SEEDS / SC_OVER_CHAINS
+template <bool LZ>
 SC_HD int chain_seq(const IndexView &I, const pr_seed_opts &O, Scratch &S, int nm, int *n_cv) {
     int32_t ns = 0, ncv = 0, nrg = 0;
     for (int k = 0; k < S.hsize; ++k) S.htab[k].key = -1;
@@ -1077,8 +1082,8 @@ SC_HD int chain_seq(const IndexView &I, const pr_seed_opts &O, Scratch &S, int n
         const Iv p = S.mems[mi];
         const int slen = p.end - p.start;
         // (lazy table: every SMEM's start was counted by the SMEM search, so it is materialized)
-        if (S.hend && !S.ready[p.start]) return SC_OVER_HITS;
-        const int32_t h0 = S.hoff[p.start], h1 = hit_end(S, p.start);
+        if (LZ && !S.ready[p.start]) return SC_OVER_HITS;
+        const int32_t h0 = S.hoff[p.start], h1 = LZ ? S.hend[p.start] : S.hoff[p.start + 1];
         // the SMEM's occurrence count is the number of the start's hits with ml >= slen
         // (every interval's occ comes from the same per-start table, slen >= 12)
         const int64_t np = p.occ;
