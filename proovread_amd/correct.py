@@ -516,12 +516,15 @@ def run(lr_records: Sequence[Tuple[str, bytes, Optional[bytes]]], sr_data: bytes
 
 
 def run_tasks(stages, srs: ShortReads, tasks: List[str], cfg: LoopConfig, mode: str, min_sr: int, have_reads: bool,
-              comm=None, sampler: Optional[control.Sampler] = None) -> Tuple[List[str], Optional[List[bytes]], List[TaskLog]]:
+              comm=None, sampler: Optional[control.Sampler] = None, sample_shard: Optional[Tuple[int, int]] = None,
+              on_task=None) -> Tuple[List[str], Optional[List[bytes]], List[TaskLog]]:
     """The bwa-sr / bwa-mr tasks of the loop after read-long (bin/proovread:705-905) on the
     stages' resident long reads: per task SeqChunker sampling, the task on the stages, the
     {bpt, bpN} statistic (all-reduced over ranks) and mask_shortcut_frac's splice of the task
     list.  -> (chimera lines of the finish task, the masked reads kept by cfg.keep_masked or
-    None, a log per task)."""
+    None, a log per task).  sample_shard (rank, world) (tests): every task sees only that
+    rank's contiguous share of its sample -- one rank's seeding and SW of an N-rank run, at
+    world 1; on_task(task) (tests): called before each task."""
     from . import cns
     sampler = sampler or control.Sampler(sampling=cfg.sampling)
     tasks = list(tasks)
@@ -541,6 +544,13 @@ def run_tasks(stages, srs: ShortReads, tasks: List[str], cfg: LoopConfig, mode: 
         task_cov = sr_coverage_for(task)
         multi = comm is not None and comm.world > 1
         ranges, sr_off = srs.sample_ranges(sampler.cov2seqchunker(cfg.coverage, task_cov))
+        if sample_shard is not None:
+            from .exact_shard import sr_range
+            s0, s1 = sr_range(len(sr_off) - 1, sample_shard[1], sample_shard[0])
+            ranges = sample_subranges(ranges, s0, s1)
+            sr_off = np.ascontiguousarray(sr_off[s0:s1 + 1] - sr_off[s0], np.int64)
+        if on_task is not None:
+            on_task(task)
         # device stages: the sample is gathered from the resident short reads on the device
         on_dev = bool(getattr(stages, "device_short_reads", False)) and \
             (not (multi or cfg.exact_layout) or bool(getattr(stages, "device_short_reads_exact", False)))

@@ -161,3 +161,124 @@ def _run(cfg, ctx, sd, glen, n_lr, cov, n_sr, d, rec, cpu_chain, _abi, cns, corr
         assert ch == "" and not g.chim, i
     rec["oracle_reads"] = sample_lrs
     _log(cfg, rec)
+
+
+def test_configs2_loop_one_rank_share(monkeypatch):
+    """configs[2] as BASELINE states it, an iterative loop, at one rank's
+    share on one GPU: the index of ALL 100 k long reads every task, each task's SeqChunker sample
+    cut to rank 0's 1/8 (correct.run_tasks sample_shard), bwa-sr-1 .. bwa-sr-6 with
+    mask_shortcut_frac, then bwa-sr-finish (the lazy occurrence table at 1 Gb).  Checked: every
+    task commits (every read's status 0), the masked fractions never fall, GPU seeds = the host
+    path on finish-task reads, and 6 spread long reads' finish consensus and chimera lines = the
+    oracle chain over the pre-finish reads.  A rank's consensus sees 1/8 of the coverage here, so
+    the masked fractions stay far below a real run's (the shortcut fires on the 3 % gain rule)."""
+    import cpu_chain
+    from proovread_amd import _abi, correct, seed, synth
+    from proovread_amd import tasks as T
+    monkeypatch.setenv("PRGPU_XCHG_FORCE", "1")
+    sd, glen, n_lr, cov = CONFIGS["configs2"]
+    n_sr = int(round(cov * glen / 150))
+    rec = {"config": "configs2-loop", "long_reads": n_lr, "short_reads_total": n_sr, "ranks": RANKS}
+    t = time.perf_counter()
+    d = synth.simulate_reads(sd, glen, n_lr, 10_000, n_sr, threads=16)
+    rec["gen_s"] = round(time.perf_counter() - t, 1)
+    ctx = _abi.Context(int(os.environ.get("LOCAL_RANK", "-1")))
+    try:
+        ascii_pool = np.frombuffer(b"ACGTN", np.uint8)[d.lr_seq[:int(d.lr_off[-1])]]
+        reads = correct.LongReads([f"lr{i}" for i in range(n_lr)],
+                                  pools=(ascii_pool, d.lr_off, np.full(len(ascii_pool), ord("$"), np.uint8)))
+        _abi.mem_reset_peak()
+        st = correct.GpuStages(ctx)
+        st.load(reads)
+        del ascii_pool, reads
+        srs = correct.ShortReads.from_pool(d.sr_seq[:int(d.sr_off[-1])], d.sr_off)
+        st.load_short_reads(srs)
+        cfg = correct.LoopConfig(coverage=cov, exact_layout=True)
+        pre_finish = {}
+        peaks = []
+
+        def on_task(task):
+            m = _abi.mem_stats()
+            peaks.append(m["peak"])
+            _abi.mem_reset_peak()
+            if task.endswith("finish"):
+                off, seq, qual, _ = st.lrs.download(seq=True, qual=True)
+                pre_finish.update(off=off, seq=seq, qual=qual)
+
+        t = time.perf_counter()
+        chim, _, log = correct.run_tasks(st, srs, list(T.MODE_TASKS["sr-noccs"][1:]), cfg, "sr-noccs", 150, True,
+                                         None, sample_shard=(0, RANKS), on_task=on_task)
+        rec["loop_s"] = round(time.perf_counter() - t, 1)
+        peaks.append(_abi.mem_stats()["peak"])
+        rec["tasks"] = [{"task": e.task, "short_reads": e.n_sr, "seeds": e.n_tasks, "wall_ms": e.wall_ms,
+                         "masked_frac": e.masked_frac, "shortcut": e.shortcut, "stage_event_ms": e.stage_ms}
+                        for e in log]
+        rec["peak_device_bytes_per_task"] = peaks[1:]
+        rec["chimera_lines"] = len(chim)
+        _log("configs2_loop", rec)
+        assert log[-1].task == "bwa-sr-finish" and len(log) >= 2
+        fr = [e.masked_frac for e in log if e.masked_frac is not None]
+        assert all(0.0 <= f < 1.0 for f in fr) and all(b >= a for a, b in zip(fr, fr[1:])), fr
+        it = st.last_iteration
+        status = it.statuses()
+        assert len(status) == n_lr and (status == 0).all()
+        sample_lrs = [int(x) for x in np.linspace(0, n_lr - 1, 6).astype(np.int64)]
+        got = it.results_of(sample_lrs)   # (before the seed checks reuse the seeding buffers)
+
+        # the finish task's seeds: GPU (the lazy occurrence table) = the host path, on a sample
+        L = _abi.lib()
+        fo = seed.default_opts(True)
+        sampler = correct.control.Sampler()
+        for e in log:   # replay the samples to the finish task's
+            rg, off = srs.sample_ranges(sampler.cov2seqchunker(cov, T.sr_coverage(e.task)))
+        from proovread_amd.exact_shard import sr_range
+        s0, s1 = sr_range(len(off) - 1, RANKS, 0)
+        rg = correct.sample_subranges(rg, s0, s1)
+        f_seq = np.ascontiguousarray(srs.gather(rg), np.uint8)
+        f_off = np.ascontiguousarray(off[s0:s1 + 1] - off[s0], np.int64)
+        assert len(f_off) - 1 == log[-1].n_sr
+        rng = np.random.default_rng(sd + 1)
+        pick = np.sort(rng.choice(len(f_off) - 1, 20_000, replace=False))
+        p_off = np.zeros(len(pick) + 1, np.int64)
+        p_off[1:] = np.cumsum(f_off[pick + 1] - f_off[pick])
+        p_seq = np.concatenate([f_seq[f_off[i]:f_off[i + 1]] for i in pick])
+        gpu, gst = seed._map_gpu(L, ctx, p_seq, p_off, fo, False)   # the finish index (the pre-finish reads)
+        nt4 = correct.NT4[pre_finish["seq"]]
+        hx = seed.SeedIndex(nt4, pre_finish["off"])
+        host = hx.map(p_seq, p_off, fo, threads=16)
+        hx.close()
+        assert (gst == 0).all() and np.array_equal(gpu, host) and len(host) > 20_000
+        rec["finish_seed_check"] = {"reads": int(len(pick)), "seeds": int(len(host))}
+
+        # 6 spread long reads: finish consensus + chimera lines = the oracle chain (over the GPU
+        # seeds of the finish shard, which equal the host path's on the sample above)
+        ft, fst = seed._map_gpu(L, ctx, f_seq, f_off, fo, False)
+        assert (fst == 0).all()
+        on = np.isin(ft["lr"], sample_lrs)
+        keep_sr = np.zeros(len(f_off) - 1, bool)
+        keep_sr[ft["sr"][on]] = True
+        ft = ft[keep_sr[ft["sr"]]]
+        dd = synth.with_seeds(dataclasses_replace(d, lr_seq=nt4, lr_off=pre_finish["off"], sr_seq=f_seq,
+                                                  sr_off=f_off), ft)
+        o = ob.sw_opts("bwa-sr-finish")
+        swt = (o.a, o.b, o.o_del, o.o_ins, o.e_del, o.e_ins, o.w, o.pen_clip5, o.pen_clip3, o.zdrop,
+               o.min_score_per_base)
+        capf = min(cov, T.sr_coverage("bwa-sr-finish")) * 0.75
+        _, _, want, _ = cpu_chain.run_sample(dd, sample_lrs, task=swt, coverage=capf, use_ref_qual=False,
+                                             detect_chimera=True, workers=16, full=True,
+                                             bin_filter=(20, 20.0 * min(cov, T.sr_coverage("bwa-sr-finish"))),
+                                             drop_ratio=0.75, ref_seq=pre_finish["seq"], ref_qual=pre_finish["qual"])
+        for i, g, (rc, fq, trace, ch) in zip(sample_lrs, got, want):
+            assert rc == 0 and g.status == 0, (i, rc, g.status)
+            assert g.fastq == fq, i
+            assert g.trace == trace, i
+            assert "".join(x + "\n" for x in g.chim_lines()) == ch, i
+        rec["oracle_reads"] = sample_lrs
+        _log("configs2_loop", rec)
+    finally:
+        ctx.close()
+
+
+def dataclasses_replace(d, **kw):
+    import dataclasses
+    return dataclasses.replace(d, **kw)
