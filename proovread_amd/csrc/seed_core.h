@@ -217,6 +217,10 @@ SC_HD void text_to_fr(const IndexView &I, uint64_t p, int64_t &fr, int &rid) {
     }
 }
 
+// pack_fr through the device's block coordinate table when the hit's block has at most two
+// contig starts after its first contig (one load), else the cblk -> cstart walk
+SC_HD uint64_t pack_fr_blk(const IndexView &I, uint64_t p);
+
 // a hit's forward-reverse coordinate and long read, packed for the chaining (rid < 2^24)
 constexpr int FR_RID_BITS = 24;
 SC_HD uint64_t pack_fr(const IndexView &I, uint64_t p) {
@@ -224,6 +228,22 @@ SC_HD uint64_t pack_fr(const IndexView &I, uint64_t p) {
     int rid;
     text_to_fr(I, p, fr, rid);
     return ((uint64_t)fr << FR_RID_BITS) | (uint64_t)rid;
+}
+
+SC_HD uint64_t pack_fr_blk(const IndexView &I, uint64_t p) {
+    if (I.blkfr) {
+        const BlkFr bt = I.blkfr[p >> CB_SHIFT];
+        const int o = (int)(p & ((1u << CB_SHIFT) - 1u));
+        int c = -1;
+        int64_t d = 0;
+        if (o < bt.bnd) c = bt.c0, d = bt.d0;
+        else if (o < bt.bnd2) c = bt.c0 + 1, d = bt.d1;
+        if (c >= 0) {
+            const int rid = c < I.n_lr ? c : 2 * I.n_lr - 1 - c;   // (reverse half: reads in reverse order)
+            return ((uint64_t)((int64_t)p + d) << FR_RID_BITS) | (uint64_t)rid;
+        }
+    }
+    return pack_fr(I, p);
 }
 
 // 16 bases from base x of a 4-bit packed sequence (a padding word after the last)
@@ -425,24 +445,35 @@ SC_HD int hit_ml(const IndexView &I, const Scratch &S, const uint8_t *q, int len
     m = m < lq ? m : lq;
     int ml = KI + m;
     if (m < KX) return ml;
-    if (I.text4 && S.q4w) {
-        for (;;) {
-            const int xx = a + ml;
-            if (xx >= len) break;
-            const uint64_t qw = nib16c(S.q4w, (uint64_t)xx), tw = nib16c(I.text4, p + (uint64_t)ml);
-            const uint64_t nq = (qw >> 2) & 0x1111111111111111ull;   // read N (code 4) or past the end (6)
-            const uint64_t bad = (qw ^ tw) | (nq * 0xFull);
-            const int lim = len - xx;
-            if (bad) {
-                const int f = ctz64(bad) >> 2;
-                ml += f < lim ? f : lim;
-                break;
+    if (I.text4 && S.q4w) {   // 64 bases a round trip: 5 text words loaded together (8 padding words)
+        bool go = a + ml < len;
+        while (go) {
+            const uint64_t tp = p + (uint64_t)ml;
+            const uint64_t *tw4 = I.text4 + (tp >> 4);
+            const int sh = (int)(tp & 15) * 4;
+            uint64_t w5[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) w5[j] = tw4[j];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!go) break;
+                const int xx = a + ml;
+                const uint64_t tw = sh ? (w5[j] >> sh) | (w5[j + 1] << (64 - sh)) : w5[j];
+                const uint64_t qw = nib16c(S.q4w, (uint64_t)xx);
+                const uint64_t nq = (qw >> 2) & 0x1111111111111111ull;   // read N (code 4) or past the end (6)
+                const uint64_t bad = (qw ^ tw) | (nq * 0xFull);
+                const int lim = len - xx;
+                if (bad) {
+                    const int f = ctz64(bad) >> 2;
+                    ml += f < lim ? f : lim;
+                    go = false;
+                } else if (lim <= 16) {
+                    ml += lim;
+                    go = false;
+                } else {
+                    ml += 16;
+                }
             }
-            if (lim <= 16) {
-                ml += lim;
-                break;
-            }
-            ml += 16;
         }
     } else {
         while (a + ml < len && q[a + ml] < 4 && I.text[p + ml] == q[a + ml]) ++ml;
@@ -481,17 +512,32 @@ SC_HD void materialize(const OccLazy &occ, int a) {
             n = (int32_t)(r1 - r0);
             const uint64_t qe = S.qext[a];
             const bool ranked = q[a] < 4;
-            for (uint64_t r = r0; r < r1; ++r) {
-                const uint64_t p = hit_pos(I, (uint32_t)code, r);
-                const int ml = hit_ml(I, S, q, len, a, p, I.kext[r], qe);
-                const int32_t k = beg + (int32_t)(r - r0);
-                const uint16_t v = (uint16_t)(ml < 65535 ? ml : 65535);
-                S.hml[k] = v;
-                S.hfr[k] = pack_fr(I, p);
-                const int d = ml - KI;
+            // 4 hits at a time: their position, extension and block-table loads are independent
+            // (one latency per batch, not per hit), then each hit's match length and coordinate
+            constexpr int MB = 4;
+            for (uint64_t r = r0; r < r1; r += MB) {
+                uint64_t pp[MB], ex[MB], fr[MB];
 #pragma unroll
-                for (int t = 0; t < HB; ++t) g[t] += d >= t ? 1u : 0u;
-                if (ranked) topk_insert(top, v);
+                for (int u = 0; u < MB; ++u) {
+                    const bool ok = r + u < r1;
+                    pp[u] = ok ? hit_pos(I, (uint32_t)code, r + u) : 0ull;
+                    ex[u] = ok ? I.kext[r + u] : 0ull;
+                }
+#pragma unroll
+                for (int u = 0; u < MB; ++u) fr[u] = r + u < r1 ? pack_fr_blk(I, pp[u]) : 0ull;
+#pragma unroll
+                for (int u = 0; u < MB; ++u) {
+                    if (r + u >= r1) break;
+                    const int ml = hit_ml(I, S, q, len, a, pp[u], ex[u], qe);
+                    const int32_t k = beg + (int32_t)(r + u - r0);
+                    const uint16_t v = (uint16_t)(ml < 65535 ? ml : 65535);
+                    S.hml[k] = v;
+                    S.hfr[k] = fr[u];
+                    const int d = ml - KI;
+#pragma unroll
+                    for (int t = 0; t < HB; ++t) g[t] += d >= t ? 1u : 0u;
+                    if (ranked) topk_insert(top, v);
+                }
             }
         }
     }
