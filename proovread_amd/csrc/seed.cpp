@@ -732,9 +732,21 @@ extern "C" int pr_seed_map_device_caps(const pr_seed_index *h, const pr_seed_opt
     if (o->min_seed_len < KI) return pr_set_error(PR_ERR_UNSUPPORTED, "min seed length below the 12-mer index");
     out->n = 0;
     out->t = nullptr;
-    const seedc::IndexView V = view_of(h->I);
+    seedc::IndexView V = view_of(h->I);
     int qmax = 1;
     for (int i = 0; i < n_sr; ++i) qmax = std::max<int>(qmax, (int)(sr_off[i + 1] - sr_off[i]));
+    // the device's 4-bit text (16 bases a word, SEP past the end, 8 padding words), so the lazy
+    // table's 64-base text walks run here as on the device
+    std::vector<uint64_t> text4((size_t)(V.n_text / 16 + 8), 0);
+    for (size_t w = 0; w < text4.size(); ++w) {
+        uint64_t v = 0;
+        for (int k = 0; k < 16; ++k) {
+            const int64_t x = (int64_t)w * 16 + k;
+            v |= (uint64_t)(x < V.n_text ? V.text[x] : SEP) << (4 * k);
+        }
+        text4[w] = v;
+    }
+    V.text4 = text4.data();
     seedc::Caps caps = seedc::device_caps(qmax);   // (the output slots follow the longest read, as on the device)
     caps.hi = V.ksplit != nullptr;
     caps.lazy = seedc::lazy_occ(*o) ? 1 : 0;   // the device's pass-1 table for these options
