@@ -515,7 +515,6 @@ SC_HD void materialize(const OccLazy &occ, int a) {
             // 4 hits at a time: their position, extension and block-table loads are independent
             // (one latency per batch, not per hit), then each hit's match length and coordinate
             constexpr int MB = 4;
-            static_assert(MB == 4, "the walk loop below tests four lanes of go[]");
             for (uint64_t r = r0; r < r1; r += MB) {
                 uint64_t pp[MB], ex[MB], fr[MB];
 #pragma unroll
@@ -526,60 +525,10 @@ SC_HD void materialize(const OccLazy &occ, int a) {
                 }
 #pragma unroll
                 for (int u = 0; u < MB; ++u) fr[u] = r + u < r1 ? pack_fr_blk(I, pp[u]) : 0ull;
-                int mlb[MB];
-                if (I.text4 && S.q4w) {   // the batch's text walks in lock-step: one round trip a round
-                    bool go[MB];
-#pragma unroll
-                    for (int u = 0; u < MB; ++u) {
-                        const int le = (int)(ex[u] >> 56), lq = (int)(qe >> 56);
-                        const uint64_t x = (ex[u] ^ qe) & KX_MASK;
-                        int m = x ? ctz64(x) >> 1 : KX;
-                        m = m < le ? m : le;
-                        m = m < lq ? m : lq;
-                        mlb[u] = KI + m;
-                        go[u] = r + u < r1 && m == KX && a + mlb[u] < len;
-                    }
-                    while (go[0] || go[1] || go[2] || go[3]) {
-                        uint64_t w5[MB][5];
-#pragma unroll
-                        for (int u = 0; u < MB; ++u) {
-                            const uint64_t *tw4 = I.text4 + ((pp[u] + (uint64_t)mlb[u]) >> 4);
-#pragma unroll
-                            for (int j = 0; j < 5; ++j) w5[u][j] = go[u] ? tw4[j] : 0ull;
-                        }
-#pragma unroll
-                        for (int u = 0; u < MB; ++u) {
-                            const int sh = (int)((pp[u] + (uint64_t)mlb[u]) & 15) * 4;
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                if (!go[u]) break;
-                                const int xx = a + mlb[u];
-                                const uint64_t tw = sh ? (w5[u][j] >> sh) | (w5[u][j + 1] << (64 - sh)) : w5[u][j];
-                                const uint64_t qw = nib16c(S.q4w, (uint64_t)xx);
-                                const uint64_t nq = (qw >> 2) & 0x1111111111111111ull;   // read N or past the end
-                                const uint64_t bad = (qw ^ tw) | (nq * 0xFull);
-                                const int lim = len - xx;
-                                if (bad) {
-                                    const int f = ctz64(bad) >> 2;
-                                    mlb[u] += f < lim ? f : lim;
-                                    go[u] = false;
-                                } else if (lim <= 16) {
-                                    mlb[u] += lim;
-                                    go[u] = false;
-                                } else {
-                                    mlb[u] += 16;
-                                }
-                            }
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int u = 0; u < MB; ++u) mlb[u] = r + u < r1 ? hit_ml(I, S, q, len, a, pp[u], ex[u], qe) : 0;
-                }
 #pragma unroll
                 for (int u = 0; u < MB; ++u) {
                     if (r + u >= r1) break;
-                    const int ml = mlb[u];
+                    const int ml = hit_ml(I, S, q, len, a, pp[u], ex[u], qe);
                     const int32_t k = beg + (int32_t)(r + u - r0);
                     const uint16_t v = (uint16_t)(ml < 65535 ? ml : 65535);
                     S.hml[k] = v;
