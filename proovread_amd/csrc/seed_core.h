@@ -371,26 +371,22 @@ SC_HD void topk_insert(uint16_t (&top)[RK], uint16_t v) {
 template <class OccT>
 SC_HD void fill_rk_top(const OccT &occ, const Scratch &S, const uint8_t *q, int len, int a, const uint16_t (&top)[RK]) {
     uint16_t *r = S.rmax + (int64_t)a * RK;
-    // the short part (fewer than k hits of the 12-mer): the longest N-free j-mer from a with >= k
-    // occurrences.  The j-mer counts never grow with j and the end only falls as k grows; all of
-    // the start's counts are loaded together (independent loads: one latency instead of a chain
-    // of up to 11 -- the masked iterations' reads, whose 12-mers mostly have no hits, take it
-    // at nearly every start)
-    int jm = -1;
-    uint32_t cj[KI];
+    int e = -1;   // the short part: j-mer counts never grow with k, so its end only falls
+    int64_t ce = 0;
     for (int k = 1; k <= RK; ++k) {
         if (top[k - 1] > 0) {
             r[k - 1] = (uint16_t)(a + top[k - 1]);
             continue;
         }
-        if (jm < 0) {
-            jm = short_limit(q, len, a) - a;
-            cj[0] = 0u;
-#pragma unroll
-            for (int j = 1; j < KI; ++j) cj[j] = j <= jm ? (uint32_t)occ.jmer(a, a + j) : 0u;
+        if (e < 0) {
+            e = short_limit(q, len, a);
+            ce = e > a ? occ.jmer(a, e) : 0;
         }
-        while (jm > 0 && (int64_t)cj[jm] < k) --jm;
-        r[k - 1] = (uint16_t)(a + jm);
+        while (e > a && ce < k) {
+            --e;
+            ce = e > a ? occ.jmer(a, e) : 0;
+        }
+        r[k - 1] = (uint16_t)e;
     }
 }
 template <class OccT>
