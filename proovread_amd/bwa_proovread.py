@@ -44,6 +44,7 @@ import re
 import gzip
 import os
 import sys
+import time
 from typing import Callable, List, Optional, Tuple
 
 import numpy as np
@@ -230,6 +231,7 @@ def _mem_gpu(a, so, wo, argv, lr_names, lr_seqs, sr_names, sr_seqs, sr_quals, lr
     -b/-l filter on the device (pr_sw_binfilter) and the SAM text formatted natively
     (pr_sw_sam): nothing per record in Python."""
     from . import _abi, iteration
+    t0 = time.perf_counter()
     ctx = ctx or _abi.default_context()
     L = _abi.lib()
     seed._setup(L)
@@ -266,23 +268,29 @@ def _mem_gpu(a, so, wo, argv, lr_names, lr_seqs, sr_names, sr_seqs, sr_quals, lr
     si = SamIn(sr_off.ctypes.data, text.ctypes.data, None if quals is None else quals.ctypes.data, srn.ctypes.data,
                srn_off.ctypes.data, lrn.ctypes.data, lrn_off.ctypes.data, None if keep is None else keep.ctypes.data,
                int(a.t) if a.t and a.t > 1 else 0)
+    t1 = time.perf_counter()
     buf, ln, nrec = C.c_void_p(), C.c_int64(), C.c_int64()
     _abi.check(L.pr_sw_sam(ctx.h, C.byref(si), C.byref(buf), C.byref(ln), C.byref(nrec)), "pr_sw_sam")
+    t2 = time.perf_counter()
     try:
         _header(out, lr_names, lr_seqs, argv)
-        data = C.string_at(buf.value, ln.value) if ln.value else b""
+        # a view of the native buffer (ctypes.string_at takes a C int size: SAM text passes 2 GiB)
+        data = memoryview((C.c_ubyte * ln.value).from_address(buf.value)) if ln.value else memoryview(b"")
         if hasattr(out, "buffer"):
             out.flush()
             out.buffer.write(data)
             out.buffer.flush()
         else:
-            out.write(data.decode())
+            out.write(bytes(data).decode())
+        del data
     finally:
         if buf.value:
             L.pr_buffer_free(buf)
     if keep is not None:
         print(f"[bwa-proovread] -b {a.b} -l {a.l}: {nrec.value} of {int(n_aln.value)} alignments kept (device filter)",
               file=log)
+    print(f"[bwa-proovread] device stages {t1 - t0:.3f} s, SAM formatting {t2 - t1:.3f} s ({ln.value} bytes), "
+          f"write {time.perf_counter() - t2:.3f} s", file=log)
     return 0
 
 
@@ -294,11 +302,13 @@ def mem(argv: List[str], out=None, sw_runner: Optional[SwRunner] = None, log=Non
     log = log or sys.stderr
     a = parse_mem(argv)
     so, wo = options(a)
+    t0 = time.perf_counter()
     lr_names, lr_seqs, _ = read_fastx(a.ref)
     sr_names, sr_seqs, sr_quals = read_fastx(a.reads)
     lr_pool, lr_off = _pool(lr_seqs)
     sr_pool, sr_off = _pool(sr_seqs)
     if sw_runner is None:
+        print(f"[bwa-proovread] inputs read in {time.perf_counter() - t0:.3f} s", file=log)
         return _mem_gpu(a, so, wo, argv, lr_names, lr_seqs, sr_names, sr_seqs, sr_quals, lr_pool, lr_off, sr_pool,
                         sr_off, out, log, ctx)
     ix = seed.SeedIndex(lr_pool, lr_off)

@@ -975,72 +975,120 @@ extern "C" int pr_sw_sam(pr_ctx *c, const pr_sam_in *in, char **text, int64_t *l
     for (size_t t = 0; t < n; ++t)
         if (ncig[t] >= 0 && (sr[t] < 0 || sr[t] >= n_sr || lr[t] < 0 || lr[t] >= n_lr))
             return pr_set_error(PR_ERR_ARG, "pr_sw_sam: an alignment names a read outside the batch");
-    // the records, formatted in parallel over ranges of alignments (SAM order kept)
+    // the records, formatted in parallel over ranges of alignments (SAM order kept): each
+    // record's exact length first, then every thread writes its range straight into the one
+    // output buffer at its prefix-summed offset (no growing strings, no serial concatenation)
     int nt = in->n_threads > 0 ? in->n_threads : (int)std::thread::hardware_concurrency();
     nt = nt < 1 ? 1 : (nt > 64 ? 64 : nt);
     if ((size_t)nt > n / 1024 + 1) nt = (int)(n / 1024 + 1);
-    std::vector<std::string> parts((size_t)nt);
-    std::vector<int64_t> nrec((size_t)nt, 0);
     static const char OPS[] = "MIDNSHP=X";
     static const char CMP[] = "TGCAN";   // reverse complement of nt4 codes A0 C1 G2 T3 N4
-    auto work = [&](int k) {
-        const size_t t0 = n * (size_t)k / (size_t)nt, t1 = n * (size_t)(k + 1) / (size_t)nt;
-        std::string &o = parts[(size_t)k];
-        char num[32];
+    auto ndig = [](int64_t v) -> int64_t {
+        int64_t d = v < 0 ? 2 : 1;
+        uint64_t u = v < 0 ? (uint64_t)(-v) : (uint64_t)v;
+        while (u >= 10) u /= 10, ++d;
+        return d;
+    };
+    auto put = [](char *p, int64_t v) -> char * {
+        if (v < 0) *p++ = '-', v = -v;
+        char tmp[24];
+        int k = 0;
+        do tmp[k++] = (char)('0' + v % 10), v /= 10; while (v);
+        while (k) *p++ = tmp[--k];
+        return p;
+    };
+    std::vector<int64_t> rlen(n + 1, 0), part((size_t)nt + 1, 0), nrec((size_t)nt, 0);
+    auto range = [&](int k, size_t &t0, size_t &t1) {
+        t0 = n * (size_t)k / (size_t)nt;
+        t1 = n * (size_t)(k + 1) / (size_t)nt;
+    };
+    auto measure = [&](int k) {
+        size_t t0, t1;
+        range(k, t0, t1);
+        int64_t sum = 0, nr = 0;
         for (size_t t = t0; t < t1; ++t) {
             if (ncig[t] < 0) continue;
+            const int64_t ql = in->sr_off[sr[t] + 1] - in->sr_off[sr[t]];
+            int64_t L = (in->sr_name_off[sr[t] + 1] - in->sr_name_off[sr[t]]) + 1 + ndig(flag[t]) + 1 +
+                        (in->lr_name_off[lr[t] + 1] - in->lr_name_off[lr[t]]) + 1 + ndig((int64_t)pos[t] + 1) + 1 +
+                        ((flag[t] & 0x100) ? 1 : 2) + 1;
+            for (int64_t x = off[t]; x < off[t + 1]; ++x) L += ndig(cig[(size_t)x] >> 4) + 1;
+            L += 7 + ql + 1 + (in->sr_qual ? ql : 1) + 6 + ndig(score[t]) + 1;
+            rlen[t] = L;
+            sum += L;
+            ++nr;
+        }
+        part[(size_t)k + 1] = sum;
+        nrec[(size_t)k] = nr;
+    };
+    char *buf = nullptr;
+    auto write = [&](int k) {
+        size_t t0, t1;
+        range(k, t0, t1);
+        char *p = buf + part[(size_t)k];
+        for (size_t t = t0; t < t1; ++t) {
+            if (ncig[t] < 0) continue;
+            char *const rec = p;
             const int64_t q0 = in->sr_off[sr[t]], q1 = in->sr_off[sr[t] + 1];
-            o.append(in->sr_names + in->sr_name_off[sr[t]], (size_t)(in->sr_name_off[sr[t] + 1] - in->sr_name_off[sr[t]]));
-            o += '\t';
-            o += std::to_string(flag[t]);
-            o += '\t';
-            o.append(in->lr_names + in->lr_name_off[lr[t]], (size_t)(in->lr_name_off[lr[t] + 1] - in->lr_name_off[lr[t]]));
-            std::snprintf(num, sizeof num, "\t%d\t%d\t", pos[t] + 1, (flag[t] & 0x100) ? 0 : 60);
-            o += num;
+            const int64_t sn = in->sr_name_off[sr[t] + 1] - in->sr_name_off[sr[t]];
+            std::memcpy(p, in->sr_names + in->sr_name_off[sr[t]], (size_t)sn);
+            p += sn;
+            *p++ = '\t';
+            p = put(p, flag[t]);
+            *p++ = '\t';
+            const int64_t ln = in->lr_name_off[lr[t] + 1] - in->lr_name_off[lr[t]];
+            std::memcpy(p, in->lr_names + in->lr_name_off[lr[t]], (size_t)ln);
+            p += ln;
+            *p++ = '\t';
+            p = put(p, (int64_t)pos[t] + 1);
+            *p++ = '\t';
+            p = put(p, (flag[t] & 0x100) ? 0 : 60);
+            *p++ = '\t';
             for (int64_t x = off[t]; x < off[t + 1]; ++x) {
-                o += std::to_string(cig[(size_t)x] >> 4);
-                o += OPS[cig[(size_t)x] & 15u];
+                p = put(p, cig[(size_t)x] >> 4);
+                *p++ = OPS[cig[(size_t)x] & 15u];
             }
-            o += "\t*\t0\t0\t";
+            std::memcpy(p, "\t*\t0\t0\t", 7);
+            p += 7;
             if (strand[t]) {
                 for (int64_t x = q1 - 1; x >= q0; --x) {
                     const uint8_t b = in->sr_text[x] | 0x20;
-                    o += CMP[b == 'a' ? 0 : b == 'c' ? 1 : b == 'g' ? 2 : b == 't' ? 3 : 4];
+                    *p++ = CMP[b == 'a' ? 0 : b == 'c' ? 1 : b == 'g' ? 2 : b == 't' ? 3 : 4];
                 }
             } else {
                 for (int64_t x = q0; x < q1; ++x) {
                     const uint8_t b = in->sr_text[x];
-                    o += (char)(b >= 'a' && b <= 'z' ? b - 32 : b);
+                    *p++ = (char)(b >= 'a' && b <= 'z' ? b - 32 : b);
                 }
             }
-            o += '\t';
-            if (!in->sr_qual) o += '*';
+            *p++ = '\t';
+            if (!in->sr_qual) *p++ = '*';
             else if (strand[t])
-                for (int64_t x = q1 - 1; x >= q0; --x) o += (char)in->sr_qual[x];
-            else
-                o.append((const char *)in->sr_qual + q0, (size_t)(q1 - q0));
-            o += "\tAS:i:";
-            o += std::to_string(score[t]);
-            o += '\n';
-            ++nrec[(size_t)k];
+                for (int64_t x = q1 - 1; x >= q0; --x) *p++ = (char)in->sr_qual[x];
+            else {
+                std::memcpy(p, in->sr_qual + q0, (size_t)(q1 - q0));
+                p += q1 - q0;
+            }
+            std::memcpy(p, "\tAS:i:", 6);
+            p += 6;
+            p = put(p, score[t]);
+            *p++ = '\n';
+            if (p - rec != rlen[t]) std::abort();   // measure and write disagree: a bug here, never data
         }
     };
-    {
+    auto run = [&](auto &&fn) {
         std::vector<std::thread> th;
-        for (int k = 1; k < nt; ++k) th.emplace_back(work, k);
-        work(0);
+        for (int k = 1; k < nt; ++k) th.emplace_back(fn, k);
+        fn(0);
         for (auto &x : th) x.join();
-    }
-    size_t tot = 0;
+    };
+    run(measure);
     int64_t nr = 0;
-    for (int k = 0; k < nt; ++k) tot += parts[(size_t)k].size(), nr += nrec[(size_t)k];
-    char *buf = (char *)std::malloc(tot + 1);
+    for (int k = 0; k < nt; ++k) part[(size_t)k + 1] += part[(size_t)k], nr += nrec[(size_t)k];
+    const size_t tot = (size_t)part[(size_t)nt];
+    buf = (char *)std::malloc(tot + 1);
     if (!buf) return pr_set_error(PR_ERR_ARG, "pr_sw_sam: out of host memory for the SAM text");
-    size_t at = 0;
-    for (int k = 0; k < nt; ++k) {
-        std::memcpy(buf + at, parts[(size_t)k].data(), parts[(size_t)k].size());
-        at += parts[(size_t)k].size();
-    }
+    run(write);
     buf[tot] = 0;
     *text = buf;
     *len = (int64_t)tot;
