@@ -46,23 +46,26 @@ AL_HD uint64_t hash_64(uint64_t key) {
 // ---------------------------------------------------------------- klib ks_introsort
 // over an index array into the read's regions (the permutation klib's element moves make)
 struct LtEnd {   // alnreg_slt2 (mem_ars2)
-    AL_HD bool operator()(const AlnReg &a, const AlnReg &b) const { return a.re < b.re; }
+    template <class Reg>
+    AL_HD bool operator()(const Reg &a, const Reg &b) const { return a.re < b.re; }
 };
 struct LtScore {   // alnreg_slt (mem_ars)
-    AL_HD bool operator()(const AlnReg &a, const AlnReg &b) const {
+    template <class Reg>
+    AL_HD bool operator()(const Reg &a, const Reg &b) const {
         return a.score > b.score || (a.score == b.score && (a.rb < b.rb || (a.rb == b.rb && a.qb < b.qb)));
     }
 };
 struct LtHash {   // alnreg_hlt (mem_ars_hash)
-    AL_HD bool operator()(const AlnReg &a, const AlnReg &b) const {
+    template <class Reg>
+    AL_HD bool operator()(const Reg &a, const Reg &b) const {
         return a.score > b.score || (a.score == b.score && a.hash < b.hash);
     }
 };
 
 // klib ks_introsort (ksort.h as vendored by bwa) over an index array into the read's
 // regions, written with integer positions (the permutation klib's element moves make)
-template <class Lt>
-AL_HD void insertsort(int32_t *a, int s, int t, const AlnReg *R, Lt lt) {   // [s, t)
+template <class Lt, class Reg>
+AL_HD void insertsort(int32_t *a, int s, int t, const Reg *R, Lt lt) {   // [s, t)
     for (int i = s + 1; i < t; ++i)
         for (int j = i; j > s && lt(R[a[j]], R[a[j - 1]]); --j) {
             const int32_t x = a[j];
@@ -70,8 +73,8 @@ AL_HD void insertsort(int32_t *a, int s, int t, const AlnReg *R, Lt lt) {   // [
             a[j - 1] = x;
         }
 }
-template <class Lt>
-AL_HD void combsort(int32_t *a, int s, int n, const AlnReg *R, Lt lt) {   // [s, s + n)
+template <class Lt, class Reg>
+AL_HD void combsort(int32_t *a, int s, int n, const Reg *R, Lt lt) {   // [s, s + n)
     const double shrink_factor = 1.2473309501039786540366528676643;
     int do_swap;
     int gap = n;
@@ -93,8 +96,8 @@ AL_HD void combsort(int32_t *a, int s, int n, const AlnReg *R, Lt lt) {   // [s,
     } while (do_swap || gap > 2);
     if (gap != 1) insertsort(a, s, s + n, R, lt);
 }
-template <class Lt>
-AL_HD void introsort(int n, int32_t *a, const AlnReg *R, Lt lt) {
+template <class Lt, class Reg>
+AL_HD void introsort(int n, int32_t *a, const Reg *R, Lt lt) {
     int st_l[64], st_r[64], st_d[64];
     int top = 0, d;
     if (n < 1) return;
@@ -210,16 +213,12 @@ AL_HD void aln_heads_read(const AlnDev &A, int64_t r) {
     }
 }
 
-// is seed (slr, sst, srb, sqb, slen) "around" region i (mem_chain2aln's containment test)?
-AL_HD bool aln_around(const AlnDev &A, int64_t i, int64_t srb, int sqb, int slen, int lq) {
-    AlnBox bx;
-    if (A.box) bx = A.box[i];
-    else bx = AlnBox{A.o_qb[i], A.o_qe[i], A.o_rb[i], A.o_re[i], A.t_slen[i], A.o_w[i], 0, 0};
-    const int pqb = bx.qb, pqe = bx.qe;
-    const int64_t prb = bx.rb, pre = bx.re;
+// is a seed (srb, sqb, slen) "around" the region (pqb, pqe, prb, pre) extended from a seed of
+// length pslen with band pw (mem_chain2aln's containment test)
+AL_HD bool around_f(const AlnDev &A, int pqb, int pqe, int64_t prb, int64_t pre, int pslen, int pw, int64_t srb,
+                    int sqb, int slen, int lq) {
     if (srb < prb || srb + slen > pre || sqb < pqb || sqb + slen > pqe) return false;   // not contained
-    if ((double)(slen - bx.slen) > .1 * lq) return false;   // may give a better alignment
-    const int pw = bx.w;
+    if ((double)(slen - pslen) > .1 * lq) return false;   // may give a better alignment
     int64_t qd = sqb - pqb, rd = srb - prb;
     int mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
     int w = mg < pw ? mg : pw;
@@ -229,6 +228,22 @@ AL_HD bool aln_around(const AlnDev &A, int64_t i, int64_t srb, int sqb, int slen
     mg = cal_max_gap_a(A, (int)(qd < rd ? qd : rd));
     w = mg < pw ? mg : pw;
     return qd - rd < w && rd - qd < w;
+}
+
+// is seed (slr, sst, srb, sqb, slen) "around" region i?
+AL_HD bool aln_around(const AlnDev &A, int64_t i, int64_t srb, int sqb, int slen, int lq) {
+    AlnBox bx;
+    if (A.box) bx = A.box[i];
+    else bx = AlnBox{A.o_qb[i], A.o_qe[i], A.o_rb[i], A.o_re[i], A.t_slen[i], A.o_w[i], 0, 0};
+    return around_f(A, bx.qb, bx.qe, bx.rb, bx.re, bx.slen, bx.w, srb, sqb, slen, lq);
+}
+
+// mem_chain2aln's exception for a seed (srb, sqb, slen) inside a region: an earlier seed of its
+// chain (tr, tq, tl), >= 95 % of its length, overlapping it on the query on another diagonal
+AL_HD bool other_diag(int64_t srb, int sqb, int slen, int64_t tr, int tq, int tl) {
+    if (tl < slen * .95) return false;
+    if (sqb <= tq && sqb + slen - tq >= slen >> 2 && (int64_t)(tq - sqb) != tr - srb) return true;
+    return tq <= sqb && tq + tl - sqb >= slen >> 2 && (int64_t)(sqb - tq) != srb - tr;
 }
 
 // any region made before seed k (dec == 1) that seed k is around?  Regions on another long
@@ -263,11 +278,7 @@ AL_HD bool aln_maybe_other(const AlnDev &A, int64_t c0, int64_t k) {
     const int sqb = A.t_qbeg[k], slen = A.t_slen[k];
     for (int64_t j = c0; j < k; ++j) {
         if (A.dec[j] == 2) continue;
-        const int tl = A.t_slen[j], tq = A.t_qbeg[j];
-        const int64_t tr = A.t_rbeg[j];
-        if (tl < slen * .95) continue;
-        if (sqb <= tq && sqb + slen - tq >= slen >> 2 && (int64_t)(tq - sqb) != tr - srb) return true;
-        if (tq <= sqb && tq + tl - sqb >= slen >> 2 && (int64_t)(sqb - tq) != srb - tr) return true;
+        if (other_diag(srb, sqb, slen, A.t_rbeg[j], A.t_qbeg[j], A.t_slen[j])) return true;
     }
     return false;
 }
@@ -318,9 +329,7 @@ AL_HD int aln_walk_read(const AlnDev &A, int64_t r, Push push) {
                 } else {
                     tl = A.t_slen[j], tq = A.t_qbeg[j], tr = A.t_rbeg[j];
                 }
-                if (tl < slen * .95) continue;
-                if (sqb <= tq && sqb + slen - tq >= slen >> 2 && (int64_t)(tq - sqb) != tr - srb) { other = true; break; }
-                if (tq <= sqb && tq + tl - sqb >= slen >> 2 && (int64_t)(sqb - tq) != srb - tr) { other = true; break; }
+                if (other_diag(srb, sqb, slen, tr, tq, tl)) { other = true; break; }
             }
             if (!other) {
                 A.dec[k] = 2;
@@ -351,6 +360,101 @@ AL_HD int aln_walk_read(const AlnDev &A, int64_t r, Push push) {
     }
     A.resume[r] = (int32_t)s1;
     return 0;
+}
+
+// mem_sort_dedup_patch's redundancy test and colinear merges (mem_patch_reg) over the regions
+// sorted by end (ix): -> 1 when a patch's global score is not known yet (*req filled; the read
+// is replayed once it is), 0 done
+template <class Reg>
+AL_HD int dedup_patch(const AlnDev &A, int64_t r, int64_t s0, Reg *R, const int32_t *ix, int n, AlnPatch *req) {
+    const int64_t l_pac = A.lr_off[A.n_lr];
+    int m_patch = 0;
+    for (int i = 1; i < n; ++i) {
+        Reg &p = R[ix[i]];
+        const Reg &pv = R[ix[i - 1]];
+        if (p.lr != pv.lr || p.rb >= pv.re + A.max_chain_gap) continue;
+        for (int j = i - 1; j >= 0 && p.lr == R[ix[j]].lr && p.rb < R[ix[j]].re + A.max_chain_gap; --j) {
+            Reg &q = R[ix[j]];
+            if (q.qe == q.qb) continue;   // excluded
+            const int64_t orr = q.re - p.rb;
+            const int64_t oq = q.qb < p.qb ? q.qe - p.qb : p.qe - q.qb;
+            const int64_t mr = q.re - q.rb < p.re - p.rb ? q.re - q.rb : p.re - p.rb;
+            const int64_t mq = q.qe - q.qb < p.qe - p.qb ? q.qe - q.qb : p.qe - p.qb;
+            if (orr > A.mask_level_redun * mr && oq > A.mask_level_redun * mq) {   // one is redundant
+                if (p.score < q.score) {
+                    p.qe = p.qb;
+                    break;
+                }
+                q.qe = q.qb;
+                continue;
+            }
+            if (!(q.rb < p.rb)) continue;
+            // mem_patch_reg(q, p)
+            if (q.rb < l_pac && p.rb >= l_pac) continue;   // different strands
+            if (q.qb >= p.qb || q.qe >= p.qe || q.re >= p.re) continue;   // not colinear
+            int w = (int)((q.re - p.rb) - (q.qe - p.qb));
+            w = w > 0 ? w : -w;
+            double rr = (double)(q.re - p.rb) / (double)(p.re - q.rb) - (double)(q.qe - p.qb) / (double)(p.qe - q.qb);
+            rr = rr > 0. ? rr : -rr;
+            if (q.re < p.rb || q.qe < p.qb) {
+                if (w > A.w << 1 || rr >= 0.05) continue;
+            } else if (w > A.w << 2 || rr >= 0.05 * 2) {
+                continue;
+            }
+            w += q.w + p.w;
+            w = w < A.w << 2 ? w : A.w << 2;
+            int score;
+            if (m_patch < A.npk[r]) {
+                score = A.pscore[s0 + m_patch];
+            } else {   // the global score is not known yet: request it, replay the read later
+                const int64_t base = fr_of(A, q.lr, q.strand, 0);
+                req->read = (int32_t)r;
+                req->m = m_patch;
+                req->lr = q.lr;
+                req->strand = q.strand;
+                req->qb = q.qb;
+                req->qe = p.qe;
+                req->rb = (int32_t)(q.rb - base);
+                req->re = (int32_t)(p.re - base);
+                req->w = w;
+                req->pad = 0;
+                return 1;
+            }
+            ++m_patch;
+            const int q_s = (int)((double)(p.qe - q.qb) / ((p.qe - p.qb) + (q.qe - q.qb)) * (p.score + q.score) + .5);
+            const int r_s = (int)((double)(p.re - q.rb) / (double)((p.re - p.rb) + (q.re - q.rb)) * (p.score + q.score) + .5);
+            if (score <= 0 || (double)score / (q_s > r_s ? q_s : r_s) < 0.90) continue;
+            p.qb = q.qb, p.rb = q.rb;
+            p.truesc = p.score = score;
+            p.w = w;
+            p.patched = 1;
+            q.qb = q.qe;
+        }
+    }
+    return 0;
+}
+
+// the regions left (qe > qb), in place -> their count
+template <class Reg>
+AL_HD int compact_live(int n, int32_t *ix, const Reg *R) {
+    int m = 0;
+    for (int i = 0; i < n; ++i)
+        if (R[ix[i]].qe > R[ix[i]].qb) ix[m++] = ix[i];
+    return m;
+}
+
+// after the (score, rb, qb) sort: identical hits after the first removed -> the regions left
+template <class Reg>
+AL_HD int drop_identical(int n, int32_t *ix, Reg *R) {
+    for (int i = 1; i < n; ++i) {
+        Reg &a = R[ix[i]];
+        const Reg &b = R[ix[i - 1]];
+        if (a.score == b.score && a.rb == b.rb && a.qb == b.qb) a.qe = a.qb;
+    }
+    int m = n > 0 ? 1 : 0;
+    for (int i = 1; i < n; ++i)
+        if (R[ix[i]].qe > R[ix[i]].qb) ix[m++] = ix[i];
+    return m;
 }
 
 // the final pass of read r -> 0 done, 1: the global score of patch *req is needed first
@@ -388,86 +492,12 @@ AL_HD int aln_final_read(const AlnDev &A, int64_t r, AlnPatch *req) {
         ++n;
       }
     }
-    const int64_t l_pac = A.lr_off[A.n_lr];
-    int m_patch = 0;
     if (n > 1) {
         introsort(n, ix, R, LtEnd());
-        for (int i = 1; i < n; ++i) {
-            AlnReg &p = R[ix[i]];
-            const AlnReg &pv = R[ix[i - 1]];
-            if (p.lr != pv.lr || p.rb >= pv.re + A.max_chain_gap) continue;
-            for (int j = i - 1; j >= 0 && p.lr == R[ix[j]].lr && p.rb < R[ix[j]].re + A.max_chain_gap; --j) {
-                AlnReg &q = R[ix[j]];
-                if (q.qe == q.qb) continue;   // excluded
-                const int64_t orr = q.re - p.rb;
-                const int64_t oq = q.qb < p.qb ? q.qe - p.qb : p.qe - q.qb;
-                const int64_t mr = q.re - q.rb < p.re - p.rb ? q.re - q.rb : p.re - p.rb;
-                const int64_t mq = q.qe - q.qb < p.qe - p.qb ? q.qe - q.qb : p.qe - p.qb;
-                if (orr > A.mask_level_redun * mr && oq > A.mask_level_redun * mq) {   // one is redundant
-                    if (p.score < q.score) {
-                        p.qe = p.qb;
-                        break;
-                    }
-                    q.qe = q.qb;
-                    continue;
-                }
-                if (!(q.rb < p.rb)) continue;
-                // mem_patch_reg(q, p)
-                if (q.rb < l_pac && p.rb >= l_pac) continue;   // different strands
-                if (q.qb >= p.qb || q.qe >= p.qe || q.re >= p.re) continue;   // not colinear
-                int w = (int)((q.re - p.rb) - (q.qe - p.qb));
-                w = w > 0 ? w : -w;
-                double rr = (double)(q.re - p.rb) / (double)(p.re - q.rb) - (double)(q.qe - p.qb) / (double)(p.qe - q.qb);
-                rr = rr > 0. ? rr : -rr;
-                if (q.re < p.rb || q.qe < p.qb) {
-                    if (w > A.w << 1 || rr >= 0.05) continue;
-                } else if (w > A.w << 2 || rr >= 0.05 * 2) {
-                    continue;
-                }
-                w += q.w + p.w;
-                w = w < A.w << 2 ? w : A.w << 2;
-                int score;
-                if (m_patch < A.npk[r]) {
-                    score = A.pscore[s0 + m_patch];
-                } else {   // the global score is not known yet: request it, replay the read later
-                    const int64_t base = fr_of(A, q.lr, q.strand, 0);
-                    req->read = (int32_t)r;
-                    req->m = m_patch;
-                    req->lr = q.lr;
-                    req->strand = q.strand;
-                    req->qb = q.qb;
-                    req->qe = p.qe;
-                    req->rb = (int32_t)(q.rb - base);
-                    req->re = (int32_t)(p.re - base);
-                    req->w = w;
-                    req->pad = 0;
-                    return 1;
-                }
-                ++m_patch;
-                const int q_s = (int)((double)(p.qe - q.qb) / ((p.qe - p.qb) + (q.qe - q.qb)) * (p.score + q.score) + .5);
-                const int r_s = (int)((double)(p.re - q.rb) / (double)((p.re - p.rb) + (q.re - q.rb)) * (p.score + q.score) + .5);
-                if (score <= 0 || (double)score / (q_s > r_s ? q_s : r_s) < 0.90) continue;
-                p.qb = q.qb, p.rb = q.rb;
-                p.truesc = p.score = score;
-                p.w = w;
-                p.patched = 1;
-                q.qb = q.qe;
-            }
-        }
-        int m = 0;
-        for (int i = 0; i < n; ++i)
-            if (R[ix[i]].qe > R[ix[i]].qb) ix[m++] = ix[i];
-        n = m;
+        if (dedup_patch(A, r, s0, R, ix, n, req)) return 1;
+        n = compact_live(n, ix, R);
         introsort(n, ix, R, LtScore());
-        for (int i = 1; i < n; ++i) {
-            AlnReg &a = R[ix[i]];
-            const AlnReg &b = R[ix[i - 1]];
-            if (a.score == b.score && a.rb == b.rb && a.qb == b.qb) a.qe = a.qb;
-        }
-        m = n > 0 ? 1 : 0;
-        for (int i = 1; i < n; ++i)
-            if (R[ix[i]].qe > R[ix[i]].qb) ix[m++] = ix[i];
-        n = m;
+        n = drop_identical(n, ix, R);
     }
     // mem_mark_primary_se
     for (int i = 0; i < n; ++i) R[ix[i]].hash = hash_64((uint64_t)(A.read_id0 + r + i));

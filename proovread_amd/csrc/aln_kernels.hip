@@ -34,6 +34,9 @@ namespace prgpu {
 
 using namespace alnc;
 
+// the largest read (seeds) the wave-per-read kernels take (below)
+constexpr int WAVE_SEEDS = 128;
+
 // ---------------------------------------------------------------- round 0
 __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
     // (the round-0 list -- every chain's first seed, sel = SEL_EXT -- is made by aln_list_kernel)
@@ -105,10 +108,12 @@ __global__ void __launch_bounds__(256) aln_heads_kernel(AlnDev A, int cap) {
 }
 
 // ---------------------------------------------------------------- mem_chain2aln
-__global__ void __launch_bounds__(256, 8) aln_walk_kernel(AlnDev A) {
+__global__ void __launch_bounds__(256, 8) aln_walk_kernel(AlnDev A, int big_only) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n_sr) return;
+    if (big_only && A.seed_off[r + 1] - A.seed_off[r] <= WAVE_SEEDS) return;   // the wave kernel's
     // requested seeds carry SEL_EXT; aln_list_kernel lists them
-    if (r < A.n_sr) aln_walk_read(A, r, [](int64_t) {});
+    aln_walk_read(A, r, [](int64_t) {});
 }
 
 // The seeds flagged SEL_EXT -> tlist (any order: the extension kernels order their tasks
@@ -159,7 +164,8 @@ __global__ void __launch_bounds__(256) aln_list_kernel(AlnDev A) {
 // complement: the reads the early pass does NOT take (still walking at the snapshot), run on the
 // main stream beside the early pass once every walk is done (disjoint reads); no patch requests
 // are recorded there either (the late pass replays what is left)
-__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t *snap, int32_t *next, int complement) {
+__global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t *snap, int32_t *next, int complement,
+                                                        int big_only) {
     const int lane = threadIdx.x & 63;
     const bool early = snap != nullptr;
     for (;;) {
@@ -170,11 +176,379 @@ __global__ void __launch_bounds__(256) aln_final_kernel(AlnDev A, const int32_t 
         const int64_t r = (int64_t)c * 64 + lane;
         if (r >= A.n_sr) continue;
         if (early && (snap[r] < A.seed_off[r + 1]) != (complement != 0)) continue;   // (not) walking at the snapshot
+        if (big_only && A.seed_off[r + 1] - A.seed_off[r] <= WAVE_SEEDS) continue;   // the wave kernel's
         AlnPatch req;
         if (aln_final_read(A, r, &req) && !early) {   // a patch score is needed: the read is replayed later
             const int slot = atomicAdd(&A.counter[1], 1);
             if (slot < A.preq_cap) A.preq[slot] = req;
         }
+    }
+}
+
+// ---------------------------------------------------------------- the wave-per-read paths
+// A read of at most WAVE_SEEDS seeds (at configs[1]'s bwa-sr-1: 75 on average, 104 at the 99th
+// percentile, 132 at most in a 20 k-read sample) is walked and finalised by ONE wave, its
+// seeds / regions staged in LDS: every containment test of a seed against the read's regions,
+// every rank of a sort and every secondary test runs lane-parallel over LDS, where the lane
+// kernels above made each of them a chain of dependent HBM/L2 loads of one lane (measured
+// waiting 94 % of their cycles).  The decisions are the lane path's, statement for statement:
+// the sequential parts (mem_sort_dedup_patch's redundancy / patch loop, and a sort whose keys
+// tie, where klib's introsort order decides) run on lane 0 through the same aln_core.h code.
+// Larger reads keep the lane kernels (big_only), so mr-mode reads lose nothing.
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct WalkLds {   // one read's seeds (5.6 KB)
+    int32_t key[WAVE_SEEDS], hk[WAVE_SEEDS], qbeg[WAVE_SEEDS], rbeg[WAVE_SEEDS], slen[WAVE_SEEDS];
+    int32_t bqb[WAVE_SEEDS], bqe[WAVE_SEEDS], brb[WAVE_SEEDS], bre[WAVE_SEEDS], bw[WAVE_SEEDS];   // regions
+    int16_t cst[WAVE_SEEDS];   // first seed of the seed's chain
+    uint8_t dec[WAVE_SEEDS], ext[WAVE_SEEDS];
+};
+
+// aln_walk_read for read r (s0, ns seeds, resumed at local seed kl) by the calling wave.  The
+// walk's per-seed test (around a region before it and no longer chain mate on another
+// diagonal) only changes when a region is made, so every lane keeps the test's two parts for
+// its two seeds (`around`, `other`) and updates them when one is: the next seed to decide is the
+// first open seed whose test fails (a ballot), the open seeds before it are skipped (dec 2) --
+// the order-by-order walk's decisions, at one round of LDS work per region instead of per seed.
+__device__ void walk_wave_read(const AlnDev &A, WalkLds &L, int64_t r, int64_t s0, int ns, int kl, int lane) {
+    const int lq = (int)(A.sr_off[r + 1] - A.sr_off[r]);
+    for (int j = lane; j < ns; j += 64) {   // the last round's results, the seeds, the regions
+        const int64_t t = s0 + j;
+        uint8_t e = A.ext[t];
+        if (A.sel[t] & SEL_EXT) {
+            e = 1;
+            A.ext[t] = 1;
+            A.sel[t] = 0;
+        }
+        L.dec[j] = A.dec[t];
+        L.ext[j] = e;
+        L.key[j] = A.t_lr[t] * 2 + (A.t_strand[t] ? 1 : 0);
+        L.qbeg[j] = A.t_qbeg[t];
+        L.rbeg[j] = A.t_rbeg[t];
+        L.slen[j] = A.t_slen[t];
+        if (e) {
+            L.bqb[j] = A.o_qb[t];
+            L.bqe[j] = A.o_qe[t];
+            L.brb[j] = A.o_rb[t];
+            L.bre[j] = A.o_re[t];
+            L.bw[j] = A.o_w[t];
+        }
+    }
+    int carry = 0;   // chain starts: a ballot of the starts, the last one at or before each seed
+    for (int b = 0; b < ns; b += 64) {
+        const int j = b + lane;
+        const bool st = j < ns && (j == 0 || A.t_chain[s0 + j] != A.t_chain[s0 + j - 1]);
+        const uint64_t m = __ballot(st) & ((2ull << lane) - 1);
+        const int c = m ? b + 63 - __builtin_clzll(m) : carry;
+        if (j < ns) L.cst[j] = (int16_t)c;
+        carry = __shfl(c, 63, 64);
+    }
+    wsync();
+    for (int j = lane; j < ns; j += 64) L.hk[j] = L.key[L.cst[j]];
+    wsync();
+    // the lane's seeds j0 = lane, j1 = lane + 64
+    const int j0 = lane, j1 = lane + 64;
+    const bool v0 = j0 < ns, v1 = j1 < ns;
+    int64_t rb0 = 0, rb1 = 0;
+    int qb0 = 0, qb1 = 0, sl0 = 0, sl1 = 0, cs0 = 0, cs1 = 0, hk0 = 0, hk1 = 0;
+    if (v0) rb0 = L.rbeg[j0], qb0 = L.qbeg[j0], sl0 = L.slen[j0], cs0 = L.cst[j0], hk0 = L.hk[j0];
+    if (v1) rb1 = L.rbeg[j1], qb1 = L.qbeg[j1], sl1 = L.slen[j1], cs1 = L.cst[j1], hk1 = L.hk[j1];
+    bool ar0 = false, ot0 = false, ar1 = false, ot1 = false;
+    // region i (dec 1) against the lane's seeds after it: aln_around_any's set (the seed's chain
+    // mates, and the earlier chains whose head has its chain head's long read and strand) and
+    // the walk's "longer chain mate on another diagonal"
+    auto add_region = [&](int i) {
+        const int pqb = L.bqb[i], pqe = L.bqe[i], prb = L.brb[i], pre = L.bre[i], psl = L.slen[i], pw = L.bw[i];
+        const int hki = L.hk[i], iq = L.qbeg[i];
+        const int64_t ir = L.rbeg[i];
+        if (v0 && i < j0) {
+            if (!ar0 && (i >= cs0 || hki == hk0)) ar0 = around_f(A, pqb, pqe, prb, pre, psl, pw, rb0, qb0, sl0, lq);
+            if (!ot0 && i >= cs0) ot0 = other_diag(rb0, qb0, sl0, ir, iq, psl);
+        }
+        if (v1 && i < j1) {
+            if (!ar1 && (i >= cs1 || hki == hk1)) ar1 = around_f(A, pqb, pqe, prb, pre, psl, pw, rb1, qb1, sl1, lq);
+            if (!ot1 && i >= cs1) ot1 = other_diag(rb1, qb1, sl1, ir, iq, psl);
+        }
+    };
+    {   // the regions made in earlier rounds
+        const uint64_t m0 = __ballot(v0 && L.dec[j0] == 1), m1 = __ballot(v1 && L.dec[j1] == 1);
+        for (uint64_t m = m0; m; m &= m - 1) add_region(__builtin_ctzll(m));
+        for (uint64_t m = m1; m; m &= m - 1) add_region(64 + __builtin_ctzll(m));
+    }
+    const int k_first = kl;
+    for (;;) {
+        // the next seed to decide: the first open one from kl whose test fails
+        const bool c0f = v0 && j0 >= kl && L.dec[j0] == 0 && !(ar0 && !ot0);
+        const bool c1f = v1 && j1 >= kl && L.dec[j1] == 0 && !(ar1 && !ot1);
+        const uint64_t m0 = __ballot(c0f), m1 = __ballot(c1f);
+        const int ks = m0 ? __builtin_ctzll(m0) : (m1 ? 64 + __builtin_ctzll(m1) : ns);
+        if (v0 && j0 >= kl && j0 < ks && L.dec[j0] == 0) L.dec[j0] = 2;   // inside a region: skipped
+        if (v1 && j1 >= kl && j1 < ks && L.dec[j1] == 0) L.dec[j1] = 2;
+        wsync();
+        if (ks >= ns) break;
+        if (!L.ext[ks]) {   // extension needed: request it and the likely ones after it, resume here
+            // a later open seed is requested with it unless it is inside a region and no chain
+            // mate that is not skipped (>= 95 % of its length, another diagonal) could save it
+            auto spec = [&](int kk, bool ar, int cs, int64_t rb, int qb, int sl) {
+                if (kk <= ks || L.dec[kk] || L.ext[kk]) return;
+                if (ar) {
+                    bool mo = false;   // aln_maybe_other
+                    for (int j = cs; j < kk && !mo; ++j)
+                        mo = L.dec[j] != 2 && other_diag(rb, qb, sl, L.rbeg[j], L.qbeg[j], L.slen[j]);
+                    if (!mo) return;
+                }
+                A.sel[s0 + kk] = SEL_EXT;
+            };
+            if (v0) spec(j0, ar0, cs0, rb0, qb0, sl0);
+            if (v1) spec(j1, ar1, cs1, rb1, qb1, sl1);
+            if (lane == 0) {
+                A.sel[s0 + ks] = SEL_EXT;
+                A.resume[r] = (int32_t)(s0 + ks);
+            }
+            for (int j = k_first + lane; j < ks; j += 64) A.dec[s0 + j] = L.dec[j];
+            return;
+        }
+        if (lane == 0) L.dec[ks] = 1;
+        add_region(ks);
+        wsync();
+        kl = ks + 1;
+    }
+    if (lane == 0) A.resume[r] = (int32_t)(s0 + ns);
+    for (int j = k_first + lane; j < ns; j += 64) A.dec[s0 + j] = L.dec[j];
+}
+
+// a wave per 64 consecutive reads: the ones still walking (and small enough) one after another
+__global__ void __launch_bounds__(256) aln_walk_wave_kernel(AlnDev A) {
+    __shared__ WalkLds sh[4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int64_t base = ((int64_t)blockIdx.x * 4 + wv) * 64;
+    if (base >= A.n_sr) return;
+    const int64_t r = base + lane;
+    long long s0 = 0;
+    int ns = 0, kl = 0;
+    bool act = false;
+    if (r < A.n_sr) {
+        s0 = A.seed_off[r];
+        const int64_t s1 = A.seed_off[r + 1], k = A.resume[r];
+        ns = (int)(s1 - s0);
+        kl = (int)(k - s0);
+        act = k < s1 && ns <= WAVE_SEEDS;
+    }
+    for (uint64_t m = __ballot(act); m; m &= m - 1) {
+        const int l = __builtin_ctzll(m);
+        walk_wave_read(A, sh[wv], base + l, (int64_t)__shfl(s0, l, 64), __shfl(ns, l, 64), __shfl(kl, l, 64), lane);
+        wsync();   // the LDS is the next read's
+    }
+}
+
+struct RegW {   // a region of the wave final pass (LDS)
+    int64_t rb, re;
+    uint64_t hash;
+    int32_t qb, qe, score, truesc, w, lr;
+    int16_t task, secondary;   // task: the seed's index in the read; secondary: an ix position or -1
+    uint8_t strand, patched, pad[2];
+};
+
+struct FinalLds {   // one read's regions (7.7 KB)
+    RegW R[WAVE_SEEDS];
+    int32_t ix[WAVE_SEEDS];
+    uint8_t pass[WAVE_SEEDS];
+};
+
+// ix[0, n) sorted by lt, lane-parallel: every element's rank is the number of elements before
+// it; -> false (ix untouched) when two keys tie, where klib's order decides (the caller then
+// runs introsort on lane 0)
+template <class Lt>
+__device__ bool rank_sort(FinalLds &L, int n, int lane, Lt lt) {
+    const int e0 = lane < n ? L.ix[lane] : 0, e1 = lane + 64 < n ? L.ix[lane + 64] : 0;
+    const RegW a0 = L.R[e0], a1 = L.R[e1];
+    int r0 = 0, r1 = 0;
+    bool tie = false;
+    for (int j = 0; j < n; ++j) {
+        const RegW &b = L.R[L.ix[j]];
+        if (lt(b, a0)) ++r0;
+        else if (j != lane && !lt(a0, b)) tie = true;
+        if (lt(b, a1)) ++r1;
+        else if (j != lane + 64 && !lt(a1, b) && lane + 64 < n) tie = true;
+    }
+    if (__ballot(tie && lane < n)) return false;
+    wsync();   // every lane has read ix
+    if (lane < n) L.ix[r0] = e0;
+    if (lane + 64 < n) L.ix[r1] = e1;
+    wsync();
+    return true;
+}
+
+// aln_final_read for read r by the calling wave -> 1: the global score of patch *req (lane 0's)
+// is needed first
+__device__ int final_wave_read(const AlnDev &A, FinalLds &L, int64_t r, int64_t s0, int ns, int lane, AlnPatch *req) {
+    int n = 0;
+    for (int b = 0; b < ns; b += 64) {   // the regions, in seed order
+        const int j = b + lane;
+        const int64_t t = s0 + j;
+        const bool reg = j < ns && A.dec[t] == 1;
+        const uint64_t m = __ballot(reg);
+        if (reg) {
+            const int pos = n + __popcll(m & ((1ull << lane) - 1));
+            RegW &g = L.R[pos];
+            const int lr = A.t_lr[t], st = A.t_strand[t];
+            const int64_t base = fr_of(A, lr, st, 0);
+            g.rb = base + A.o_rb[t];
+            g.re = base + A.o_re[t];
+            g.qb = A.o_qb[t];
+            g.qe = A.o_qe[t];
+            g.score = A.o_score[t];
+            g.truesc = A.o_truesc[t];
+            g.w = A.o_w[t];
+            g.lr = lr;
+            g.strand = (uint8_t)st;
+            g.task = (int16_t)j;
+            g.secondary = -1;
+            g.patched = 0;
+            L.ix[pos] = pos;
+        }
+        n += __popcll(m);
+    }
+    wsync();
+    if (n > 1) {
+        if (!rank_sort(L, n, lane, LtEnd())) {
+            if (lane == 0) introsort(n, L.ix, L.R, LtEnd());
+            wsync();
+        }
+        int need = 0;
+        if (lane == 0) need = dedup_patch(A, r, s0, L.R, L.ix, n, req);
+        need = __shfl(need, 0, 64);
+        wsync();
+        if (need) return 1;
+        int m = 0;   // the regions left, in order
+        for (int b = 0; b < n; b += 64) {
+            const int i = b + lane;
+            const int e = i < n ? L.ix[i] : 0;
+            const bool live = i < n && L.R[e].qe > L.R[e].qb;
+            const uint64_t mk = __ballot(live);
+            wsync();
+            if (live) L.ix[m + __popcll(mk & ((1ull << lane) - 1))] = e;
+            m += __popcll(mk);
+            wsync();
+        }
+        n = m;
+        if (!rank_sort(L, n, lane, LtScore())) {   // a tie is an identical hit: klib's order keeps one
+            int nn = 0;
+            if (lane == 0) {
+                introsort(n, L.ix, L.R, LtScore());
+                nn = drop_identical(n, L.ix, L.R);
+            }
+            n = __shfl(nn, 0, 64);
+            wsync();
+        }
+    }
+    // mem_mark_primary_se: hash_64 is a bijection, so (score, hash) never ties
+    for (int i = lane; i < n; i += 64) L.R[L.ix[i]].hash = hash_64((uint64_t)(A.read_id0 + r + i));
+    wsync();
+    if (n > 1 && !rank_sort(L, n, lane, LtHash())) {
+        if (lane == 0) introsort(n, L.ix, L.R, LtHash());
+        wsync();
+    }
+    for (int i = 1; i < n; ++i) {   // secondaries: the first earlier primary a region overlaps
+        const RegW ai = L.R[L.ix[i]];
+        int first = -1;
+        for (int b = 0; b < i; b += 64) {
+            const int j = b + lane;
+            bool c = false;
+            if (j < i) {
+                const RegW &aj = L.R[L.ix[j]];
+                if (aj.secondary < 0) {
+                    const int b_max = aj.qb > ai.qb ? aj.qb : ai.qb;
+                    const int e_min = aj.qe < ai.qe ? aj.qe : ai.qe;
+                    if (e_min > b_max) {
+                        const int min_l = ai.qe - ai.qb < aj.qe - aj.qb ? ai.qe - ai.qb : aj.qe - aj.qb;
+                        c = e_min - b_max >= min_l * A.mask_level;
+                    }
+                }
+            }
+            const uint64_t mk = __ballot(c);
+            if (mk) {
+                first = b + __builtin_ctzll(mk);
+                break;
+            }
+        }
+        if (first >= 0) {
+            if (lane == 0) L.R[L.ix[i]].secondary = (int16_t)first;
+            wsync();
+        }
+    }
+    // mem_reg2sam: -T per aligned base, -D for secondaries; SAM order; mark for the CIGAR pass
+    for (int j = lane; j < ns; j += 64) L.pass[j] = 0;
+    wsync();
+    int no = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int k = b + lane;
+        bool ok = false;
+        RegW p;
+        if (k < n) {
+            p = L.R[L.ix[k]];
+            ok = (double)p.score >= A.min_score_per_base * (double)(p.qe - p.qb);
+            if (ok && p.secondary >= 0 && p.score < L.R[L.ix[p.secondary]].score * A.drop_ratio) ok = false;
+        }
+        const uint64_t mk = __ballot(ok);
+        if (ok) {
+            const int o = no + __popcll(mk & ((1ull << lane) - 1));
+            const int64_t t = s0 + p.task;
+            const int64_t base = fr_of(A, p.lr, p.strand, 0);
+            A.o_qb[t] = p.qb;
+            A.o_rb[t] = (int32_t)(p.rb - base);
+            A.o_score[t] = p.score;
+            A.o_truesc[t] = p.truesc;
+            A.o_w[t] = p.w;
+            L.pass[p.task] = 1;
+            A.olist[s0 + o] = (int32_t)t;
+            A.oflag[s0 + o] = (p.strand ? 0x10 : 0) | (p.secondary >= 0 ? 0x100 : (o > 0 ? 0x800 : 0));
+        }
+        no += __popcll(mk);
+    }
+    wsync();
+    for (int j = lane; j < ns; j += 64) {
+        const uint8_t pm = L.pass[j];
+        A.o_pass[s0 + j] = pm;
+        A.sel[s0 + j] = pm ? SEL_CIG : 0;
+    }
+    if (lane == 0) {
+        A.nout[r] = no;
+        A.fdone[r] = 1;
+    }
+    return 0;
+}
+
+// a wave per 64 consecutive reads; snap / complement as aln_final_kernel's
+__global__ void __launch_bounds__(128) aln_final_wave_kernel(AlnDev A, const int32_t *snap, int complement) {
+    __shared__ FinalLds sh[2];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const bool early = snap != nullptr;
+    const int64_t base = ((int64_t)blockIdx.x * 2 + wv) * 64;
+    if (base >= A.n_sr) return;
+    const int64_t r = base + lane;
+    long long s0 = 0;
+    int ns = 0;
+    bool act = false;
+    if (r < A.n_sr) {
+        s0 = A.seed_off[r];
+        const int64_t s1 = A.seed_off[r + 1];
+        ns = (int)(s1 - s0);
+        act = ns <= WAVE_SEEDS && !A.fdone[r] && (!early || (snap[r] < s1) == (complement != 0));
+    }
+    for (uint64_t m = __ballot(act); m; m &= m - 1) {
+        const int l = __builtin_ctzll(m);
+        AlnPatch req;
+        const int need = final_wave_read(A, sh[wv], base + l, (int64_t)__shfl(s0, l, 64), __shfl(ns, l, 64), lane, &req);
+        if (need && !early && lane == 0) {   // replayed once the score is there
+            const int slot = atomicAdd(&A.counter[1], 1);
+            if (slot < A.preq_cap) A.preq[slot] = req;
+        }
+        wsync();
     }
 }
 
@@ -305,11 +679,24 @@ int aln_launch_list(const AlnDev &A, void *stream) {
     hipLaunchKernelGGL(aln_list_kernel, dim3((unsigned)grid_of(A.n_task, 2048)), dim3(256), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
+// PRGPU_ALN_LANE=1: every read on the lane kernels (the wave kernels off)
+static bool aln_lane_only() {
+    static const int v = getenv("PRGPU_ALN_LANE") ? atoi(getenv("PRGPU_ALN_LANE")) : 0;
+    return v != 0;
+}
 int aln_launch_walk(const AlnDev &A, void *stream) {
     if (A.n_sr <= 0) return 0;
     static const int wgcu = getenv("PRGPU_ALN_WALK_WG") ? atoi(getenv("PRGPU_ALN_WALK_WG")) : 0;
     const unsigned lds = wgcu > 0 ? (unsigned)(160 * 1024 / wgcu) & ~255u : 0u;
-    hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A);
+    const bool wave = !aln_lane_only();
+    if (wave) {
+        hipLaunchKernelGGL(aln_walk_wave_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), 0,
+                           (hipStream_t)stream, A);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return (int)e;
+    }
+    hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A,
+                       wave ? 1 : 0);
     return (int)hipGetLastError();
 }
 int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap, bool complement) {
@@ -335,8 +722,14 @@ int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap, b
     int64_t grid = (int64_t)n_cu * (wgcu > 0 ? wgcu : 8);
     if (grid > (chunks + 3) / 4) grid = (chunks + 3) / 4;
     if (grid < 1) grid = 1;
+    const bool wave = !aln_lane_only();
+    if (wave) {
+        hipLaunchKernelGGL(aln_final_wave_kernel, dim3((unsigned)((A.n_sr + 127) / 128)), dim3(128), 0,
+                           (hipStream_t)stream, A, early_snap, complement ? 1 : 0);
+        if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+    }
     hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)grid), dim3(256), lds, (hipStream_t)stream, A, early_snap, next,
-                       complement ? 1 : 0);
+                       complement ? 1 : 0, wave ? 1 : 0);
     return (int)hipGetLastError();
 }
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, void *stream) {
