@@ -268,7 +268,9 @@ def main():
             print(json.dumps({"metric": "corrected long-read Mbases/sec per node", "value": round(
                 total_bases * args.steps / el / 1e6, 3), "unit": "Mbases/s", "n_gpus": world, "steps": args.steps,
                 "ms_per_step": round(el / args.steps * 1e3, 3), "loop": {"tasks": loop_rows,
-                                                                      "device_ms": round(loop_dev_ms, 1)},
+                                                                      "device_ms": round(loop_dev_ms, 1),
+                                                                      "chimera_lines": n_chim,
+                                                                      "final_reads_sha256": last_digest},
                 "last_task_seeding_phases": seed._phase_ms(L, ctx)}),
                   file=_JSON_OUT, flush=True)
         if cm is not None:

@@ -383,6 +383,165 @@ __device__ bool rank_sort(FinalLds &L, int n, int lane, Lt lt) {
     return true;
 }
 
+__device__ __forceinline__ int64_t rl64(int64_t v, int l) {   // lane l's 64-bit value (l uniform)
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), l);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// The final pass of a read with at most 64 regions (every read at configs[1]): lane i holds
+// the region at position i in registers, a sort's ranks come from readlane broadcasts, the
+// regions move to their ranks through LDS (L.R is kept in position order with L.ix the
+// identity, so the lane-0 fallbacks -- a tie under a sort key, a region that may be redundant
+// or merged -- run aln_core.h's code on it unchanged).
+__device__ int final_wave_small(const AlnDev &A, FinalLds &L, int64_t r, int64_t s0, int ns, int n, int lane,
+                                AlnPatch *req) {
+    RegW e;
+    bool v = lane < n;
+    if (v) e = L.R[lane];
+    auto place = [&](int rank) {   // every region to its rank
+        wsync();
+        if (v) L.R[rank] = e;
+        wsync();
+        if (v) e = L.R[lane];
+    };
+    auto adopt = [&](int m) {   // L.R in L.ix[0, m)'s order (after a lane-0 sort), L.ix the identity
+        wsync();
+        RegW t;
+        if (lane < m) t = L.R[L.ix[lane]];
+        wsync();
+        if (lane < m) L.R[lane] = t;
+        L.ix[lane] = lane;
+        L.ix[lane + 64] = lane + 64;
+        n = m;
+        v = lane < n;
+        if (v) e = t;
+        wsync();
+    };
+    if (n > 1) {
+        int rk = 0;   // alnreg_slt2: by end
+        bool tie = false;
+        for (int j = 0; j < n; ++j) {
+            const int64_t re = rl64(e.re, j);
+            rk += re < e.re;
+            tie |= j != lane && re == e.re;
+        }
+        if (__ballot(v && tie)) {
+            if (lane == 0) introsort(n, L.ix, L.R, LtEnd());
+            adopt(n);
+        } else {
+            place(rk);
+        }
+        // redundant / colinear regions: only where a region starts within max_chain_gap of its
+        // predecessor's end on the same long read does mem_sort_dedup_patch's loop do anything
+        const int plr = __shfl(e.lr, lane > 0 ? lane - 1 : 0, 64);
+        const int64_t pre = (int64_t)__shfl((long long)e.re, lane > 0 ? lane - 1 : 0, 64);
+        if (__ballot(v && lane > 0 && e.lr == plr && e.rb < pre + A.max_chain_gap)) {
+            int need = 0;
+            if (lane == 0) need = dedup_patch(A, r, s0, L.R, L.ix, n, req);
+            need = __shfl(need, 0, 64);
+            wsync();
+            if (need) return 1;
+            if (v) e = L.R[lane];
+        }
+        const bool live = v && e.qe > e.qb;
+        const uint64_t lm = __ballot(live);
+        if (lm != __ballot(v)) {   // the regions left, in order
+            wsync();
+            if (live) L.R[__popcll(lm & ((1ull << lane) - 1))] = e;
+            n = __popcll(lm);
+            v = lane < n;
+            wsync();
+            if (v) e = L.R[lane];
+        }
+        rk = 0;   // alnreg_slt: score, then rb, then qb
+        tie = false;
+        for (int j = 0; j < n; ++j) {
+            const int sc = __builtin_amdgcn_readlane(e.score, j), qb = __builtin_amdgcn_readlane(e.qb, j);
+            const int64_t rb = rl64(e.rb, j);
+            rk += sc > e.score || (sc == e.score && (rb < e.rb || (rb == e.rb && qb < e.qb)));
+            tie |= j != lane && sc == e.score && rb == e.rb && qb == e.qb;
+        }
+        if (__ballot(v && tie)) {   // identical hits: klib's order decides which one stays
+            int nn = 0;
+            if (lane == 0) {
+                introsort(n, L.ix, L.R, LtScore());
+                nn = drop_identical(n, L.ix, L.R);
+            }
+            adopt(__shfl(nn, 0, 64));
+        } else {
+            place(rk);
+        }
+    }
+    // mem_mark_primary_se: hash_64 is a bijection, so (score, hash) never ties
+    if (v) e.hash = hash_64((uint64_t)(A.read_id0 + r + lane));
+    if (n > 1) {
+        int rk = 0;
+        bool tie = false;
+        for (int j = 0; j < n; ++j) {
+            const int sc = __builtin_amdgcn_readlane(e.score, j);
+            const uint64_t h = (uint64_t)rl64((int64_t)e.hash, j);
+            rk += sc > e.score || (sc == e.score && h < e.hash);
+            tie |= j != lane && sc == e.score && h == e.hash;
+        }
+        if (__ballot(v && tie)) {
+            wsync();
+            if (v) L.R[lane] = e;
+            wsync();
+            if (lane == 0) introsort(n, L.ix, L.R, LtHash());
+            adopt(n);
+        } else {
+            place(rk);
+        }
+    }
+    int sec = -1;   // the first earlier primary the region overlaps (mem_mark_primary_se_core)
+    for (int i = 1; i < n; ++i) {
+        const int aqb = __builtin_amdgcn_readlane(e.qb, i), aqe = __builtin_amdgcn_readlane(e.qe, i);
+        bool c = false;
+        if (lane < i && sec < 0) {
+            const int b_max = e.qb > aqb ? e.qb : aqb;
+            const int e_min = e.qe < aqe ? e.qe : aqe;
+            if (e_min > b_max) {
+                const int min_l = aqe - aqb < e.qe - e.qb ? aqe - aqb : e.qe - e.qb;
+                c = e_min - b_max >= min_l * A.mask_level;
+            }
+        }
+        const uint64_t mk = __ballot(c);
+        if (mk && lane == i) sec = __builtin_ctzll(mk);
+    }
+    // mem_reg2sam: -T per aligned base, -D for secondaries; SAM order; mark for the CIGAR pass
+    for (int j = lane; j < ns; j += 64) L.pass[j] = 0;
+    wsync();
+    const int sec_score = __shfl(e.score, sec >= 0 ? sec : lane, 64);
+    bool ok = v && (double)e.score >= A.min_score_per_base * (double)(e.qe - e.qb);
+    if (ok && sec >= 0 && e.score < sec_score * A.drop_ratio) ok = false;
+    const uint64_t mk = __ballot(ok);
+    if (ok) {
+        const int o = __popcll(mk & ((1ull << lane) - 1));
+        const int64_t t = s0 + e.task;
+        const int64_t base = fr_of(A, e.lr, e.strand, 0);
+        A.o_qb[t] = e.qb;
+        A.o_rb[t] = (int32_t)(e.rb - base);
+        A.o_score[t] = e.score;
+        A.o_truesc[t] = e.truesc;
+        A.o_w[t] = e.w;
+        L.pass[e.task] = 1;
+        A.olist[s0 + o] = (int32_t)t;
+        A.oflag[s0 + o] = (e.strand ? 0x10 : 0) | (sec >= 0 ? 0x100 : (o > 0 ? 0x800 : 0));
+    }
+    wsync();
+    for (int j = lane; j < ns; j += 64) {
+        const uint8_t pm = L.pass[j];
+        A.o_pass[s0 + j] = pm;
+        A.sel[s0 + j] = pm ? SEL_CIG : 0;
+    }
+    if (lane == 0) {
+        A.nout[r] = __popcll(mk);
+        A.fdone[r] = 1;
+    }
+    return 0;
+}
+
 // aln_final_read for read r by the calling wave -> 1: the global score of patch *req (lane 0's)
 // is needed first
 __device__ int final_wave_read(const AlnDev &A, FinalLds &L, int64_t r, int64_t s0, int ns, int lane, AlnPatch *req) {
@@ -414,6 +573,7 @@ __device__ int final_wave_read(const AlnDev &A, FinalLds &L, int64_t r, int64_t 
         n += __popcll(m);
     }
     wsync();
+    if (n <= 64) return final_wave_small(A, L, r, s0, ns, n, lane, req);
     if (n > 1) {
         if (!rank_sort(L, n, lane, LtEnd())) {
             if (lane == 0) introsort(n, L.ix, L.R, LtEnd());
@@ -549,6 +709,125 @@ __global__ void __launch_bounds__(128) aln_final_wave_kernel(AlnDev A, const int
             if (slot < A.preq_cap) A.preq[slot] = req;
         }
         wsync();
+    }
+}
+
+// mem_patch_reg's global score (bwa_gen_cigar2's ksw_global2, score only) with one wave per
+// patch: lane l owns CB consecutive query columns, row i runs on lane l at step i + l (an
+// anti-diagonal wavefront), F(i, first column) and H(i-1, first column - 1) come from the lane
+// to the left through shuffles, and the band's outside reads as the very negative values the
+// row-by-row kernel leaves there.  aln_patch_kernel (one lane per patch, H/E rows in HBM) walked
+// every cell with a dependent global load: 6.5 ms at configs[1] bwa-sr-2 for its longest patch.
+constexpr int PATCH_REF_MAX = 2048;
+
+template <int CB>
+__device__ int patch_wave_score(const AlnDev &A, const AlnPatch &P, int lq, int rlen, int w, const uint8_t *sref,
+                                int lane) {
+    constexpr int NEG = -0x40000000;
+    const uint8_t *Q = A.sr + A.sr_off[P.read] + P.qb;
+    const int cb = (lq + 63) / 64, nl = (lq + cb - 1) / cb, c0 = lane * cb;
+    const int oe_del = A.o_del + A.e_del, oe_ins = A.o_ins + A.e_ins;
+    int8_t qv[CB];
+    int hp[CB], ev[CB];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+        const int j = c0 + c;
+        const bool in = c < cb && j < lq;
+        qv[c] = in ? (int8_t)(P.strand ? Q[lq - 1 - j] : Q[j]) : (int8_t)4;
+        hp[c] = in && j + 1 <= w ? -(A.o_ins + A.e_ins * (j + 1)) : NEG;   // H(-1, j)
+        ev[c] = NEG;
+    }
+    int pub_f = NEG, pub_hd = NEG, score = NEG;
+    const int nsteps = rlen + nl - 1;
+    for (int st = 0; st < nsteps; ++st) {
+        const int fin = __shfl_up(pub_f, 1, 64), hdin = __shfl_up(pub_hd, 1, 64);
+        const int i = st - lane;
+        if (lane < nl && i >= 0 && i < rlen) {
+            int f, dg;
+            if (lane == 0) {
+                f = NEG;
+                dg = i == 0 ? 0 : (i - 1 <= w ? -(A.o_del + A.e_del * i) : NEG);   // H(i-1, -1)
+            } else {
+                f = fin;
+                dg = hdin;
+            }
+            const int tb = sref[i];
+            const int beg = i > w ? i - w : 0, end = i + w + 1 < lq ? i + w + 1 : lq;
+            int hlast = NEG;   // H(i-1, last column), for the right lane
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+                if (c == cb - 1) hlast = hp[c];
+#pragma unroll
+            for (int c = 0; c < CB; ++c) {
+                if (c >= cb) break;
+                const int j = c0 + c;
+                const int old = hp[c];
+                if (j >= beg && j < end) {
+                    const int qb = qv[c];
+                    const int m = dg + ((tb > 3 || qb > 3) ? -1 : (tb == qb ? A.a : -A.b));
+                    int h = m >= ev[c] ? m : ev[c];
+                    h = h >= f ? h : f;
+                    hp[c] = h;
+                    int t = m - oe_del;
+                    const int e = ev[c] - A.e_del;
+                    ev[c] = e > t ? e : t;
+                    t = m - oe_ins;
+                    f -= A.e_ins;
+                    f = f > t ? f : t;
+                } else {
+                    hp[c] = NEG;
+                    ev[c] = NEG;
+                    f = NEG;
+                }
+                dg = old;
+            }
+            pub_f = f;
+            pub_hd = hlast;
+            if (i == rlen - 1 && lq - 1 >= c0 && lq - 1 < c0 + cb) {
+#pragma unroll
+                for (int c = 0; c < CB; ++c)
+                    if (c0 + c == lq - 1) score = hp[c];
+            }
+        }
+    }
+    return __shfl(score, (lq - 1) / cb, 64);
+}
+
+__global__ void __launch_bounds__(256) aln_patch_wave_kernel(AlnDev A, int n_req, int32_t *pool, int64_t stride) {
+    __shared__ uint8_t sref[4][PATCH_REF_MAX];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int k = blockIdx.x * 4 + wv;
+    if (k >= n_req) return;
+    const AlnPatch P = A.preq[k];
+    const int lq = P.qe - P.qb, rlen = P.re - P.rb;
+    int score;
+    if (lq <= 0 || rlen <= 0 || (lq == rlen && P.w == 0) || lq > 64 * 16 || rlen > PATCH_REF_MAX) {
+        if (lane == 0) score = aln_patch_score(A, P, pool + (int64_t)k * stride, stride);   // aln_patch_kernel's way
+    } else {
+        const uint8_t *Lr = A.lr + A.lr_off[P.lr];
+        const int L = (int)(A.lr_off[P.lr + 1] - A.lr_off[P.lr]);
+        for (int i = lane; i < rlen; i += 64) {   // the strand reference row, reversed on the reverse strand
+            const int x = P.strand ? P.re - 1 - i : P.rb + i;
+            int c = P.strand ? Lr[L - 1 - x] : Lr[x];
+            if (P.strand && c < 4) c = 3 - c;
+            sref[wv][i] = (uint8_t)c;
+        }
+        wsync();
+        const int mn = lq < rlen ? lq : rlen;   // the band, as aln_patch_score's
+        const int max_ins = (int)((double)(mn * A.a - A.o_ins) / A.e_ins + 1.);
+        const int max_del = (int)((double)(mn * A.a - A.o_del) / A.e_del + 1.);
+        int max_gap = max_ins > max_del ? max_ins : max_del;
+        max_gap = max_gap > 1 ? max_gap : 1;
+        const int dl = rlen > lq ? rlen - lq : lq - rlen;
+        int w = (max_gap + dl + 1) >> 1;
+        w = w < P.w ? w : P.w;
+        w = w > dl + 3 ? w : dl + 3;
+        score = lq <= 64 * 4 ? patch_wave_score<4>(A, P, lq, rlen, w, sref[wv], lane)
+                             : patch_wave_score<16>(A, P, lq, rlen, w, sref[wv], lane);
+    }
+    if (lane == 0) {
+        A.pscore[A.seed_off[P.read] + P.m] = score;
+        A.npk[P.read] = P.m + 1;
     }
 }
 
@@ -734,8 +1013,12 @@ int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap, b
 }
 int aln_launch_patch(const AlnDev &A, int n_req, int32_t *pool, int64_t stride, void *stream) {
     if (n_req <= 0) return 0;
-    hipLaunchKernelGGL(aln_patch_kernel, dim3((unsigned)((n_req + 63) / 64)), dim3(64), 0, (hipStream_t)stream, A, n_req,
-                       pool, stride);
+    if (aln_lane_only())
+        hipLaunchKernelGGL(aln_patch_kernel, dim3((unsigned)((n_req + 63) / 64)), dim3(64), 0, (hipStream_t)stream, A,
+                           n_req, pool, stride);
+    else
+        hipLaunchKernelGGL(aln_patch_wave_kernel, dim3((unsigned)((n_req + 3) / 4)), dim3(256), 0, (hipStream_t)stream, A,
+                           n_req, pool, stride);
     return (int)hipGetLastError();
 }
 

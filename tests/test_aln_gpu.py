@@ -46,6 +46,7 @@ def test_bwa_mode_matches_oracle(finish, err):
     ctx = _abi.default_context()
     res = sw.run(d.sw_input(), sw.default_opts(finish), ctx=ctx)
     rounds, n_ext, n_patch = sw.bwa_stats(ctx)
+    print(f"rounds {rounds} extended {n_ext} patches {n_patch}")
     want = cpu_chain.bwa_alignments(d, task)
     got = _by_read(res, d)
     n = 0
@@ -148,3 +149,35 @@ def test_bwa_mode_mr_reads_match_oracle(task, sr_len):
         assert got.get(r, []) == want[r], r
         n += len(want[r])
     assert n == res.n and n > 2 * d.n_lr
+
+
+@pytest.mark.parametrize("err", [0.05, 0.15])
+def test_bwa_mode_patches_match_oracle(err):
+    """mem_patch_reg's global scores (aln_patch_wave_kernel, a wave per patch): long reads with
+    N windows (a short read across one is extended up to it from each side: two colinear
+    regions the final pass merges through a patch); the
+    device = the oracle read by read, and patches were scored."""
+    import cpu_chain
+    from proovread_amd import _abi, seed, sw, synth
+    f = err / 0.15
+    d = synth.simulate(97 + int(err * 100), 40000, 40, 2500, 15, p_ins=0.09 * f, p_del=0.045 * f, p_sub=0.015 * f)
+    rng = np.random.default_rng(5)
+    lr = d.lr_seq.copy()
+    for i in range(len(d.lr_off) - 1):   # a 10-110 bp N window every ~300 bp
+        a, b = int(d.lr_off[i]), int(d.lr_off[i + 1])
+        for x in range(a + 100, b - 200, 300):
+            x += int(rng.integers(0, 100))
+            lr[x:x + int(rng.integers(10, 111))] = 4
+    d.lr_seq = lr
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    d = synth.with_seeds(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=4))
+    ix.close()
+    ctx = _abi.default_context()
+    res = sw.run(d.sw_input(), sw.default_opts(False), ctx=ctx)
+    rounds, n_ext, n_patch = sw.bwa_stats(ctx)
+    print(f"rounds {rounds} extended {n_ext} patches {n_patch}")
+    want = cpu_chain.bwa_alignments(d, "bwa-sr")
+    got = _by_read(res, d)
+    assert all(got.get(r, []) == want[r] for r in range(d.n_sr))
+    assert res.n == sum(len(v) for v in want) > 0
+    assert n_patch > 0

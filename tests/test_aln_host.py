@@ -84,3 +84,29 @@ def test_device_logic_on_host_matches_oracle(host, finish, err):
     assert sum(map(len, got)) > 2 * d.n_lr
     n_chain = len(np.unique(d.t_sr.astype(np.int64) * 65536 + d.t_chain))
     assert stats[0] >= 1 and stats[1] >= n_chain
+
+
+def test_device_logic_patches_on_host_match_oracle(host):
+    """N windows in the long reads split short reads' alignments into colinear regions that
+    mem_sort_dedup_patch merges through mem_patch_reg (aln_patch_score in extra rounds)."""
+    import cpu_chain
+    from proovread_amd import seed, synth
+    f = 0.05 / 0.15
+    d = synth.simulate(97, 30000, 30, 2500, 15, p_ins=0.09 * f, p_del=0.045 * f, p_sub=0.015 * f)
+    rng = np.random.default_rng(5)
+    lr = d.lr_seq.copy()
+    for i in range(len(d.lr_off) - 1):   # a 10-110 bp N window every ~300 bp
+        a, b = int(d.lr_off[i]), int(d.lr_off[i + 1])
+        for x in range(a + 100, b - 200, 300):
+            x += int(rng.integers(0, 100))
+            lr[x:x + int(rng.integers(10, 111))] = 4
+    d.lr_seq = lr
+    ix = seed.SeedIndex(d.lr_seq, d.lr_off)
+    d = synth.with_seeds(d, ix.map(d.sr_seq, d.sr_off, seed.default_opts(False), threads=4))
+    ix.close()
+    got, stats = _run_host(host, d, "bwa-sr")
+    want = cpu_chain.bwa_alignments(d, "bwa-sr")
+    for r in range(d.n_sr):
+        w = [(a[0], a[1], a[5], a[6], a[7], a[8], a[9], a[4], a[10], a[11]) for a in want[r]]
+        assert got[r] == w, r
+    assert stats[2] > 0
