@@ -10,6 +10,10 @@
 
 namespace prgpu {
 
+// the largest read (seeds) the wave-per-read walk and final kernels take; larger reads go to
+// the lane-per-read kernels
+constexpr int ALN_WAVE_SEEDS = 128;
+
 // one region of a read in the final pass (per-read scratch, in HBM)
 struct AlnReg {
     int64_t rb, re;        // bwa's forward-reverse coordinates
@@ -48,6 +52,7 @@ struct AlnDev {
     int32_t *tlist;            // [n_task] the seeds to extend in the next round (their count in counter)
     int32_t *cnext;            // [n_task] of a chain's first seed: the next chain's first seed
     int32_t cnext_ready;       // cnext already written (aln_unpack_kernel, from the seeds' ranks)
+    int64_t n_big;             // reads of more than ALN_WAVE_SEEDS seeds (0: no lane-kernel launches)
     AlnBox *box;               // [n_task] the extended seeds' regions, packed by the walk (null: the field arrays)
     int32_t *hprev;            // [n_task] of a chain head: the read's previous head on the same long read and strand (or -1); null: scan every head
     AlnReg *R;                 // [n_task] region scratch (read r: from seed_off[r])

@@ -34,8 +34,7 @@ namespace prgpu {
 
 using namespace alnc;
 
-// the largest read (seeds) the wave-per-read kernels take (below)
-constexpr int WAVE_SEEDS = 128;
+constexpr int WAVE_SEEDS = ALN_WAVE_SEEDS;
 
 // ---------------------------------------------------------------- round 0
 __global__ void __launch_bounds__(256) aln_init_kernel(AlnDev A) {
@@ -938,6 +937,11 @@ static int grid_of(int64_t n, int cap = 8192) {
     return (int)(g < 1 ? 1 : (g > cap ? cap : g));
 }
 
+// PRGPU_ALN_LANE=1: every read on the lane kernels (the wave kernels off)
+static bool aln_lane_only() {
+    static const int v = getenv("PRGPU_ALN_LANE") ? atoi(getenv("PRGPU_ALN_LANE")) : 0;
+    return v != 0;
+}
 int aln_launch_init(const AlnDev &A, void *stream) {
     const int64_t n = A.n_task > A.n_sr ? A.n_task : A.n_sr;
     hipLaunchKernelGGL(aln_init_kernel, dim3(grid_of(n)), dim3(256), 0, (hipStream_t)stream, A);
@@ -945,6 +949,7 @@ int aln_launch_init(const AlnDev &A, void *stream) {
 }
 int aln_launch_heads(const AlnDev &A, void *stream) {
     if (A.n_sr <= 0) return 0;
+    if (!aln_lane_only() && A.n_big == 0) return 0;   // hprev only feeds the lane walk
     const int64_t blocks = (A.n_sr + 3) / 4;   // a wave per read (grid-stride beyond 16 k workgroups)
     // PRGPU_HEADS_CAP (tests): a smaller LDS list, so that reads take the lane-0 path sooner
     const int cap_env = getenv("PRGPU_HEADS_CAP") ? atoi(getenv("PRGPU_HEADS_CAP")) : HEADS_CAP;
@@ -958,11 +963,6 @@ int aln_launch_list(const AlnDev &A, void *stream) {
     hipLaunchKernelGGL(aln_list_kernel, dim3((unsigned)grid_of(A.n_task, 2048)), dim3(256), 0, (hipStream_t)stream, A);
     return (int)hipGetLastError();
 }
-// PRGPU_ALN_LANE=1: every read on the lane kernels (the wave kernels off)
-static bool aln_lane_only() {
-    static const int v = getenv("PRGPU_ALN_LANE") ? atoi(getenv("PRGPU_ALN_LANE")) : 0;
-    return v != 0;
-}
 int aln_launch_walk(const AlnDev &A, void *stream) {
     if (A.n_sr <= 0) return 0;
     static const int wgcu = getenv("PRGPU_ALN_WALK_WG") ? atoi(getenv("PRGPU_ALN_WALK_WG")) : 0;
@@ -974,6 +974,7 @@ int aln_launch_walk(const AlnDev &A, void *stream) {
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return (int)e;
     }
+    if (wave && A.n_big == 0) return 0;
     hipLaunchKernelGGL(aln_walk_kernel, dim3((unsigned)((A.n_sr + 255) / 256)), dim3(256), lds, (hipStream_t)stream, A,
                        wave ? 1 : 0);
     return (int)hipGetLastError();
@@ -1006,6 +1007,7 @@ int aln_launch_final(const AlnDev &A, void *stream, const int32_t *early_snap, b
         hipLaunchKernelGGL(aln_final_wave_kernel, dim3((unsigned)((A.n_sr + 127) / 128)), dim3(128), 0,
                            (hipStream_t)stream, A, early_snap, complement ? 1 : 0);
         if ((e = hipGetLastError()) != hipSuccess) return (int)e;
+        if (A.n_big == 0) return 0;
     }
     hipLaunchKernelGGL(aln_final_kernel, dim3((unsigned)grid), dim3(256), lds, (hipStream_t)stream, A, early_snap, next,
                        complement ? 1 : 0, wave ? 1 : 0);

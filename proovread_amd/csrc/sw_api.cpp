@@ -180,6 +180,9 @@ static int sw_upload_impl(pr_ctx *c, const pr_sw_batch *b, const pr_seed_task *d
         for (int64_t t = 0; t < nt; ++t)
             r.n_rank0 += (t == 0 || b->t_sr[t] != b->t_sr[t - 1] || b->t_chain[t] != b->t_chain[t - 1]) ? 1 : 0;
     }
+    r.n_big = 0;
+    if (bwa)
+        for (int i = 0; i < b->n_sr; ++i) r.n_big += seed_off[(size_t)i + 1] - seed_off[(size_t)i] > ALN_WAVE_SEEDS;
     int rc;
     if ((rc = up(r, SB_SR, dev_sr ? nullptr : b->sr_seq, (size_t)b->sr_off[b->n_sr], s)) ||
         (rc = up(r, SB_SR_OFF, b->sr_off, (size_t)b->n_sr + 1, s)) ||
@@ -295,6 +298,7 @@ static AlnDev aln_dev(SwResident &r, const SwDev &D, const pr_sw_opts *o) {
     A.n_sr = (int32_t)r.n_sr;
     A.n_lr = (int32_t)r.n_lr;
     A.read_id0 = r.read_id0;
+    A.n_big = r.n_big;
     A.seed_off = (const int64_t *)r.buf[SB_SEEDOFF];
     A.t_sr = D.t_sr;
     A.t_lr = D.t_lr;

@@ -112,6 +112,7 @@ struct SwResident {
     int64_t n_ext = 0;          // seeds extended
     int64_t n_rank0 = 0;        // first seeds of the chains (the first round)
     bool cnext_ready = false;   // cnext written by the device-seed unpack (seed ranks)
+    int64_t n_big = 0;          // bwa mode: reads of more than ALN_WAVE_SEEDS seeds (the lane kernels')
     void *side = nullptr;       // hipStream_t: the early final pass beside the later extension rounds
     void *side_ev[3] = {nullptr, nullptr, nullptr};   // hipEvent_t
     int64_t n_patch = 0;        // mem_patch_reg global scores computed
