@@ -2446,6 +2446,10 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
             return rc;
         HIPCHK(hipStreamSynchronize(s));
         std::vector<int32_t> redo;
+        // pass 2's slices; after the by-wave pass 1b they are that pass's (its leftovers overflowed
+        // them), so pass 2 is skipped and the later passes grow from them
+        seedc::Caps p2caps = caps;
+        bool p2_ran = false;
         int32_t fl1 = 0;
         int64_t need_hits = 0;   // the largest hit table a flagged read asked for
         int64_t need_sum = 0, need_n = 0;   // (and their mean)
@@ -2523,6 +2527,8 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
                 HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
                 e = seed_launch(K, (void *)s);
                 if (e) return set_error(PR_ERR_HIP, "seed kernel (pass 1b, waves): %s", hipGetErrorString((hipError_t)e));
+                p2caps = cw;
+                p2_ran = true;
                 std::vector<int32_t> st1b((size_t)(r1 - r0));
                 if ((rc = download(st1b.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0))) return rc;
                 HIPCHK(hipStreamSynchronize(s));
@@ -2555,20 +2561,22 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         }
         c->seed_pass2 += (int64_t)redo.size();
         if (!redo.empty()) {   // pass 2 over the flagged reads (rlist in SB_PRE)
-            HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
-            HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
-            K.caps = caps;
-            K.stride = seedc::scratch_bytes(caps);
-            K.n_lanes = std::min<int64_t>(lanes2, (int64_t)redo.size());
             K.rlist = D[SB_PRE].as<int32_t>();
-            K.n_list = (int64_t)redo.size();
-            e = seed_launch(K, (void *)s);
-            if (e) return set_error(PR_ERR_HIP, "seed kernel (pass 2): %s", hipGetErrorString((hipError_t)e));
-            HIPCHK(hipStreamSynchronize(s));
+            if (!p2_ran) {
+                HIPCHK(hipMemcpyAsync(D[SB_PRE].p, redo.data(), redo.size() * 4, hipMemcpyHostToDevice, s));
+                HIPCHK(hipMemsetAsync(K.next, 0, 4, s));
+                K.caps = caps;
+                K.stride = seedc::scratch_bytes(caps);
+                K.n_lanes = std::min<int64_t>(lanes2, (int64_t)redo.size());
+                K.n_list = (int64_t)redo.size();
+                e = seed_launch(K, (void *)s);
+                if (e) return set_error(PR_ERR_HIP, "seed kernel (pass 2): %s", hipGetErrorString((hipError_t)e));
+                HIPCHK(hipStreamSynchronize(s));
+            }
             // later passes: the reads that outgrew the large slices too (e.g. the finish task's
             // near-exact reads at 30-60x long-read coverage: every 12-mer hits every copy, > 8192
             // hits per read) again, with the arrays that overflowed grown, up to 4 times
-            seedc::Caps cg = caps;
+            seedc::Caps cg = p2caps;
             for (int pass = 3; pass <= 6; ++pass) {
                 std::vector<int32_t> st2((size_t)(r1 - r0));
                 if ((rc = download(st2.data(), D[SB_STATUS], (size_t)(r1 - r0), s, (size_t)r0))) return rc;

@@ -138,6 +138,38 @@ static int pk_extend_t(int a, int b, int o_del, int e_del, int o_ins, int e_ins,
     }
     return nflag;
 }
+// the same pair with both references walked backwards (ts = -1), as the kernel reads a reverse-strand
+// window: each target stored reversed behind 64 bytes of front slack (SB_LR_FRONT), T at its last
+// byte, so row r is T[-r] = the target's base r; the 16- / 8-byte windows load T - r - 15 (- 7)
+static int pk_extend_rev_t(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int zdrop, int qlen, int w,
+                           const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb,
+                           const uint8_t *tb, int h0a, int h0b, int nrow_min, int *out) {
+    SwOptsDev O{};
+    O.a = a; O.b = b; O.o_del = o_del; O.e_del = e_del; O.o_ins = o_ins; O.e_ins = e_ins; O.zdrop = zdrop;
+    uint32_t m[2][2 * PK_NQW];
+    int nflag = 0;
+    if (pk_build_mask(qa, 0, 1, qlen, m[0], 1)) nflag |= 4;
+    if (pk_build_mask(qb, 0, 1, qlen, m[1], 1)) nflag |= 8;
+    std::vector<uint8_t> pa(64 + tla + 64, 4), pb(64 + tlb + 64, 4);
+    for (int r = 0; r < tla; ++r) pa[64 + tla - 1 - r] = ta[r];
+    for (int r = 0; r < tlb; ++r) pb[64 + tlb - 1 - r] = tb[r];
+    PkExtHalf A{pa.data() + 64 + tla - 1, -1, false, tla, h0a}, B{pb.data() + 64 + tlb - 1, -1, false, tlb, h0b};
+    int nrow = tla > tlb ? tla : tlb;
+    if (nrow < nrow_min) nrow = nrow_min;
+    PkExtOut o[2];
+    ext_pk<40, false>(A, B, qlen, w, nrow, O, m[0], m[1], 1, o, nflag);
+    for (int h = 0; h < 2; ++h) {
+        out[6 * h + 0] = o[h].score; out[6 * h + 1] = o[h].qle; out[6 * h + 2] = o[h].tle;
+        out[6 * h + 3] = o[h].gtle; out[6 * h + 4] = o[h].gscore; out[6 * h + 5] = o[h].max_off;
+    }
+    return nflag;
+}
+extern "C" int pk_extend_rev(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int zdrop, int qlen, int w,
+                             const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb,
+                             const uint8_t *tb, int h0a, int h0b, int nrow_min, int *out) {
+    return pk_extend_rev_t(a, b, o_del, e_del, o_ins, e_ins, zdrop, qlen, w, qa, qb, tla, ta, tlb, tb, h0a, h0b,
+                           nrow_min, out);
+}
 extern "C" int pk_extend(int a, int b, int o_del, int e_del, int o_ins, int e_ins, int zdrop, int qlen, int w,
                          const uint8_t *qa, const uint8_t *qb, int tla, const uint8_t *ta, int tlb,
                          const uint8_t *tb, int h0a, int h0b, int nrow_min, int *out) {

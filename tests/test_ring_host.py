@@ -225,6 +225,37 @@ def test_extend_pk_matches_oracle(ring, seed):
     assert n == 1000
 
 
+@pytest.mark.parametrize("seed", [31, 32])
+def test_extend_pk_reverse_window_matches_oracle(ring, seed):
+    """The packed extension reading its references backwards (ts = -1: a reverse-strand window,
+    16- or 8-byte loads at T - r - 15 / T - r - 7 byte-swapped, the 64-byte front slack the pools
+    keep) against osw_extend on the same targets read forwards; both PK_EXT_TW builds."""
+    rng = random.Random(seed)
+    n = 0
+    for _ in range(150):
+        L = rng.choice([1, 5, 16, 17, 40, 75, 100, 150])
+        qs = ["".join(rng.choice("ACGT") for _ in range(L)) for _ in range(2)]
+        ts = []
+        for q in qs:
+            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])).replace("N", "C") + \
+                "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 60)))
+            ts.append(t[:250])
+        h0s = [rng.choice([0, 5, 30, 100, 400]) for _ in range(2)]
+        eb = rng.choice([30, 0, 5])
+        for a, b, od, ed, oi, ei, zd in SCORING[:2]:
+            w = _band_w(L, a, od, ed, oi, ei, eb, 40)
+            out = (C.c_int * 12)()
+            fl = ring.pk_extend_rev(a, b, od, ed, oi, ei, zd, L, w, _nt4(qs[0]), _nt4(qs[1]), len(ts[0]),
+                                    _nt4(ts[0] or "A"), len(ts[1]), _nt4(ts[1] or "A"), h0s[0], h0s[1], 0, out)
+            assert fl == 0
+            for h in range(2):
+                sc, outs = ob.sw_extend(qs[h], ts[h], h0s[h], w=w, a=a, b=b, o_del=od, e_del=ed, o_ins=oi,
+                                        e_ins=ei, end_bonus=eb, zdrop=zd)
+                assert list(out[6 * h:6 * h + 6]) == [sc] + list(outs), (h, qs[h], ts[h], w, h0s[h], eb)
+                n += 1
+    assert n == 600
+
+
 def test_global_pk_cigar_cap(ring):
     """The packed backtrack's op cap: a CIGAR of N ops fits max_cigar = N and reports -1
     (the task goes to the overflow pass) at N - 1, for both halves."""
