@@ -260,7 +260,7 @@ def main():
     log = logs[-1]
     loop_rows = [{"task": e.task, "short_reads": e.n_sr, "seeds_rank": e.n_tasks, "wall_ms": e.wall_ms,
                   "device_ms": e.device_ms, "masked_frac": None if e.masked_frac is None else round(e.masked_frac, 4),
-                  "shortcut": e.shortcut, "stage_event_ms": e.stage_ms} for e in log]
+                  "shortcut": e.shortcut, "stage_event_ms": e.stage_ms, "part_wall_ms": e.part_ms} for e in log]
     same_tasks = all([e.task for e in lg] == [e.task for e in log] for lg in logs)
 
     if args.loop_only:
@@ -271,7 +271,10 @@ def main():
                                                                       "device_ms": round(loop_dev_ms, 1),
                                                                       "chimera_lines": n_chim,
                                                                       "final_reads_sha256": last_digest},
-                "last_task_seeding_phases": seed._phase_ms(L, ctx)}),
+                "last_task_seeding_phases": seed._phase_ms(L, ctx),
+                # (with PRGPU_CNS_PROF=1 in the environment: the finish task's consensus phases)
+                "last_task_consensus_phases": stages.last_iteration.cns_phase_ms()
+                if os.environ.get("PRGPU_CNS_PROF") else None}),
                   file=_JSON_OUT, flush=True)
         if cm is not None:
             cm.close()
@@ -303,6 +306,7 @@ def main():
     ev = np.zeros(6)
     dom_ms = dom_cells = ext_ms = ext_cells = ext_launches = 0
     sw_stage_ms = sw_cells = 0.0
+    bwa_ms = np.zeros(3)   # walk, main-stream final passes, early final pass (HIP events)
     for _ in range(args.steps):
         it = task_step()
         ev += np.array([lrs_index_ms(L, ctx), seed._last_ms(L.pr_seed_gpu_last_ms, ctx), *it.timing()])
@@ -313,6 +317,7 @@ def main():
         me, mg, ce, cg = sw.last_timing(ctx)
         sw_stage_ms += me + mg
         sw_cells += ce + cg
+        bwa_ms += np.array(sw.bwa_timing(ctx))
     if cm is not None:
         cm.barrier()
     _abi.check(L.pr_ctx_sync(ctx.h), "pr_ctx_sync")
@@ -324,6 +329,9 @@ def main():
     task_wall = {k: round(v / K * 1e3, 2) for k, v in wall.items()}
     n_seeds = seed._count(L, ctx)
     bwa_rounds, bwa_ext, bwa_patch = sw.bwa_stats(ctx)
+    bwa_ms /= K
+    na_rep = C.c_int64()
+    _abi.check(L.pr_sw_aln_count(ctx.h, C.byref(na_rep)), "pr_sw_aln_count")
     pc = sw.phase_cycles(ctx)
     n_recv = it.n_task
     n_aln, sum_ncig, sum_lseq = it.alignment_stats()
@@ -458,6 +466,7 @@ def main():
             "traffic_per_launch": traffic_ext,
         },
         "roofline_seeding": seeding_roofline(ev[1], s1 - s0, traffic_seed, n_seeds),
+        "roofline_bwa_rounds": bwa_rounds_roofline(bwa_ms, n_seeds, bwa_ext, int(na_rep.value), bwa_rounds),
         "cpu_baseline": cpu,
         "cpu_baseline_reference": reference_cpu(),
         "comm": "rccl" if cm is not None else "none",
@@ -501,6 +510,28 @@ def seeding_roofline(kernel_ms: float, n_reads: int, traffic, n_seeds: int = 0):
     return {"kernel": "seed_batch_kernel + seed_wave_kernel", "bound": "hbm", "achieved": round(ach, 2),
             "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes": int(alg),
             "bytes_per_read": SEED_BYTES_PER_READ, "traffic": traffic, "launch_ms": round(kernel_ms, 3)}
+
+
+# bwa mode's bookkeeping kernels (aln_walk_*_kernel, aln_final_*_kernel: mem_chain2aln's walk,
+# mem_sort_dedup_patch .. mem_reg2sam) per task, in algorithmic bytes: every seed's task record
+# read once by the walk (40 B, pr_seed_task's fields), every extended seed's result read by the
+# walk and again by the final pass as a region (2 x 32 B: score, query / reference ends, true
+# score, band, global score, flags), every reported alignment written once (32 B)
+BWA_BYTES_PER_SEED, BWA_BYTES_PER_EXT, BWA_BYTES_PER_ALN = 40, 64, 32
+
+
+def bwa_rounds_roofline(ms, n_seeds: int, n_ext: int, n_aln: int, rounds: int):
+    walk, final, early = (float(x) for x in ms)
+    alg = BWA_BYTES_PER_SEED * n_seeds + BWA_BYTES_PER_EXT * n_ext + BWA_BYTES_PER_ALN * n_aln
+    t = walk + final + early
+    ach = alg / (t * 1e-3) / 1e9 if t > 0 else 0.0
+    return {"kernels": "aln_walk_wave_kernel / aln_walk_kernel (every round) + aln_final_wave_kernel / aln_final_kernel "
+                       "(early pass on the side stream, complement and late passes on the main stream)",
+            "bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes": int(alg), "summed_launch_ms": round(t, 3),
+            "walk_ms": round(walk, 3), "final_main_ms": round(final, 3), "final_early_side_ms": round(early, 3),
+            "critical_path_ms": round(walk + final, 3), "rounds": rounds, "seeds": n_seeds, "extended": n_ext,
+            "reported": n_aln}
 
 
 if __name__ == "__main__":

@@ -342,6 +342,10 @@ int pr_sw_sam(pr_ctx *ctx, const pr_sam_in *in, char **text, int64_t *len, int64
 /* bwa mode diagnostics of the last launch: extension rounds, seeds extended, mem_patch_reg
  * global scores computed */
 int pr_sw_bwa_stats(pr_ctx *ctx, int32_t *rounds, int64_t *n_extended, int64_t *n_patch);
+/* bwa mode's bookkeeping kernels of the last launch (HIP events): the walks summed over the
+ * extension rounds and the main-stream final passes (the complement and the late passes), both
+ * on the critical path, and the early final pass on the side stream beside the later rounds */
+int pr_sw_bwa_timing(pr_ctx *ctx, float *walk_ms, float *final_ms, float *early_final_ms);
 /* kernel milliseconds of the last launch (HIP events on the ctx stream) */
 int pr_sw_last_timing(pr_ctx *ctx, double *ms_extend, double *ms_global);
 /* canonical DP cells of the last launch (unpruned band, final width) */
@@ -483,6 +487,13 @@ int pr_iter_upload(pr_ctx *ctx, const pr_iter_batch *b);
 int pr_iter_upload_gpu_seeds(pr_ctx *ctx, const pr_iter_batch *b);
 int pr_iter_launch(pr_ctx *ctx, const pr_sw_opts *o, const pr_cns_params *p);   /* async */
 int pr_iter_download(pr_ctx *ctx, pr_cns_out *out);   /* consensus outputs, syncs */
+/* bam2cns's chimera lines (bam2cns:488: "ID\tFROM\tTO\tRATIO\n", RATIO = npos / ntot printed as
+ * Perl prints a number, %.15g) of every read with nchim > 0, reads in order, each read's rows in
+ * order -- from pr_iter_download's nchim / chim_off / chim rows ([from, to, npos, ntot] int32) and
+ * the reads' names (pool + [n_lr+1] offsets).  Host only; one library-allocated text
+ * (pr_buffer_free).  Replaces the finish task's per-line formatting in the host language. */
+int pr_fmt_chim_lines(int32_t n_lr, const char *names, const int64_t *name_off, const int32_t *nchim,
+                      const int64_t *chim_off, const int32_t *chim, char **text, int64_t *len, int64_t *n_lines);
 /* the outputs of reads [first, first + n) only (one bam2cns chunk's FASTQ, bam2cns:332-365;
  * a sample of a configs[3]-size batch): per-read arrays of n entries, out_off / chim_off of
  * n + 1 counted from the range's first read, pools sized by them; kept / bin_bases NULL */

@@ -134,6 +134,7 @@ class TaskLog:
     wall_ms: Optional[float] = None        # the task's wall time in run()
     device_ms: Optional[float] = None      # kernel time the device stages report (HIP events), if any
     stage_ms: Optional[Dict[str, float]] = None   # ... per stage (index, seeding, SW, hand-off, consensus)
+    part_ms: Optional[Dict[str, float]] = None    # host wall clock per part of the device task (GpuStages)
 
 
 @dataclasses.dataclass
@@ -350,7 +351,9 @@ class GpuStages:
         L = _abi.lib()
         seed._setup(L)
         finish = mask_cfg is None
+        tp = [time.perf_counter()]   # host clock at the parts' ends (last_part_ms)
         ix_ms = self.lrs.index(self.lrs.READS if finish else self.lrs.MAP)
+        tp.append(time.perf_counter())
         self.device_ms += ix_ms
         seed_opts, opts = T.options(task)
         if bin_filter:
@@ -396,7 +399,9 @@ class GpuStages:
         n_tasks = seed._count(L, self.ctx)
         sd_ms = seed._last_ms(L.pr_seed_gpu_last_ms, self.ctx)
         self.device_ms += sd_ms
+        tp.append(time.perf_counter())
         it.launch(opts, params)
+        tp.append(time.perf_counter())
         out = TaskOut(n_tasks, [])
         if finish:
             out.chim = it.chim_lines(self.ids[lo:hi])
@@ -410,7 +415,13 @@ class GpuStages:
         self.device_ms += sum(tm)
         self.last_stage_ms = {k: round(v, 2) for k, v in zip(("index", "seeding", "sw_extend", "sw_global_cigar",
                                                                "exchange_handoff", "consensus"), (ix_ms, sd_ms, *tm))}
+        tp.append(time.perf_counter())
         self.lrs.commit(comm if exact else None, with_mask=not finish, dry=dry)   # dry: the set stays (bench.py)
+        tp.append(time.perf_counter())
+        # wall clock per part (ms, device work included): index; seeding + SW + exchange; the
+        # iteration launch (hand-off, consensus; waits for it); chimera lines or masking; commit
+        self.last_part_ms = {k: round((b - a) * 1e3, 2) for k, a, b in
+                             zip(("index", "seed_sw_exchange", "consensus_launch", "chim_or_mask", "commit"), tp, tp[1:])}
         self.last_iteration = it   # the task's consensus outputs stay readable (tests, drivers)
         return out
 
@@ -584,6 +595,7 @@ def run_tasks(stages, srs: ShortReads, tasks: List[str], cfg: LoopConfig, mode: 
         if dev0 is not None:
             ent.device_ms = round(stages.device_ms - dev0, 1)
             ent.stage_ms = getattr(stages, "last_stage_ms", None)
+            ent.part_ms = getattr(stages, "last_part_ms", None)
         log.append(ent)
         tc += 1
     return chim, last_masked, log

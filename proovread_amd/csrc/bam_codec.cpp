@@ -4,6 +4,9 @@
 // (sam_to_record, BgzfWriter): same record layout (SAM/BAM spec), smallest-fitting
 // integer tag type in the order c, C, s, S, i, I, and the same zlib raw-deflate
 // parameters per 0xFF00-byte block.
+#include <charconv>
+#include <cmath>
+#include <cstdio>
 #include <stdint.h>
 #include <zlib.h>
 
@@ -788,3 +791,54 @@ extern "C" int pr_bam_index(const uint8_t *data, int64_t len, int n_threads, uin
 }
 
 extern "C" void pr_buffer_free(void *p) { std::free(p); }
+
+// bam2cns:488's chimera lines (include/prgpu.h pr_fmt_chim_lines), each line written once into a
+// growing buffer.  RATIO as Perl (and Python's '%.15g') prints it: std::to_chars(general, 15) is
+// printf's %.15g (correctly rounded) without its per-call cost; nan / inf spelled as Python does.
+extern "C" int pr_fmt_chim_lines(int32_t n_lr, const char *names, const int64_t *name_off, const int32_t *nchim,
+                                 const int64_t *chim_off, const int32_t *chim, char **text, int64_t *len,
+                                 int64_t *n_lines) {
+    if (!text || !len || !n_lines || n_lr < 0 || (n_lr && (!names || !name_off || !nchim || !chim_off || !chim)))
+        return -1;
+    *text = nullptr;
+    *len = 0;
+    *n_lines = 0;
+    int64_t lines = 0, cap = 1;
+    for (int32_t i = 0; i < n_lr; ++i)
+        if (nchim[i] > 0) lines += nchim[i], cap += (int64_t)nchim[i] * (name_off[i + 1] - name_off[i] + 48);
+    char *out = static_cast<char *>(std::malloc((size_t)cap));
+    if (!out) return -1;
+    char *w = out;
+    for (int32_t i = 0; i < n_lr; ++i) {
+        const int32_t n = nchim[i];
+        if (n <= 0) continue;
+        const int64_t nl = name_off[i + 1] - name_off[i];
+        for (int32_t j = 0; j < n; ++j) {
+            const int32_t *r = chim + 4 * (chim_off[i] + j);
+            std::memcpy(w, names + name_off[i], (size_t)nl);
+            w += nl;
+            *w++ = '\t';
+            w = std::to_chars(w, w + 12, r[0]).ptr;
+            *w++ = '\t';
+            w = std::to_chars(w, w + 12, r[1]).ptr;
+            *w++ = '\t';
+            const double x = (double)r[2] / (double)r[3];
+            if (std::isnan(x)) {
+                std::memcpy(w, "nan", 3);
+                w += 3;
+            } else if (std::isinf(x)) {
+                const int k = x > 0 ? 3 : 4;
+                std::memcpy(w, x > 0 ? "inf" : "-inf", (size_t)k);
+                w += k;
+            } else {
+                w = std::to_chars(w, w + 24, x, std::chars_format::general, 15).ptr;
+            }
+            *w++ = '\n';
+        }
+    }
+    *w = 0;
+    *text = out;
+    *len = (int64_t)(w - out);
+    *n_lines = lines;
+    return 0;
+}

@@ -428,6 +428,19 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
     r.n_patch = 0;
     r.n_aln = 0;
     HIPCHK(hipEventRecord(ctx_event(c, 2), s));
+    if (!r.bt_ev[0])
+        for (void *&ev : r.bt_ev) {
+            hipEvent_t x;
+            HIPCHK(hipEventCreate(&x));
+            ev = (void *)x;
+        }
+    hipEvent_t *bt = reinterpret_cast<hipEvent_t *>(r.bt_ev);
+    r.ms_walk = r.ms_final = r.ms_final_early = 0.f;
+    auto bt_add = [&](float &acc, int k) {   // (after a sync that follows event bt[k + 1])
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, bt[k], bt[k + 1]) == hipSuccess) acc += ms;
+        (void)hipGetLastError();
+    };
     HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
     if ((e = aln_launch_init(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
     if ((e = aln_launch_list(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
@@ -456,10 +469,13 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
             HIPCHK(hipStreamWaitEvent(s, (hipEvent_t)r.side_ev[2], 0));
             heads_side = false;
         }
+        HIPCHK(hipEventRecord(bt[0], s));
         if ((e = aln_launch_walk(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipEventRecord(bt[1], s));
         if ((e = aln_launch_list(A, (void *)s))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
         HIPCHK(hipMemcpyAsync(cnt, A.counter, 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        bt_add(r.ms_walk, 0);
         ++r.ext_rounds;
         r.n_ext += cnt[0];
         // after the first resumed walk most reads are decided: their final pass runs on a side
@@ -474,7 +490,9 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
             HIPCHK(hipMemcpyAsync(snap, A.resume, (size_t)r.n_sr * 4, hipMemcpyDeviceToDevice, s));
             HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[0], s));
             HIPCHK(hipStreamWaitEvent((hipStream_t)r.side, (hipEvent_t)r.side_ev[0], 0));
+            HIPCHK(hipEventRecord(bt[4], (hipStream_t)r.side));
             if ((e = aln_launch_final(A, r.side, snap))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+            HIPCHK(hipEventRecord(bt[5], (hipStream_t)r.side));
             HIPCHK(hipEventRecord((hipEvent_t)r.side_ev[1], (hipStream_t)r.side));
             early = true;
         }
@@ -484,17 +502,29 @@ static int bwa_launch(pr_ctx *c, SwResident &r, SwDev &D, const SwOptsDev &O, co
         n_list = cnt[0];
     }
     D.tsel = nullptr;
+    bool comp_timed = false;
     if (early) {   // the reads the early pass skips, beside it (disjoint reads), then join it
+        HIPCHK(hipEventRecord(bt[6], s));
         if (!getenv("PRGPU_BWA_NO_COMPLEMENT") &&
             (e = aln_launch_final(A, (void *)s, (const int32_t *)r.buf[SB_RSNAP], true)))
             return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipEventRecord(bt[7], s));
         HIPCHK(hipStreamWaitEvent(s, (hipEvent_t)r.side_ev[1], 0));
+        comp_timed = true;
     }
     for (int round = 0;; ++round) {   // final pass; mem_patch_reg global scores in extra rounds
         HIPCHK(hipMemsetAsync(A.counter, 0, 16, s));
+        HIPCHK(hipEventRecord(bt[2], s));
         if ((e = aln_launch_final(A, (void *)s, nullptr))) return pr_set_error(PR_ERR_HIP, hipGetErrorString((hipError_t)e));
+        HIPCHK(hipEventRecord(bt[3], s));
         HIPCHK(hipMemcpyAsync(cnt, A.counter, 16, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
+        bt_add(r.ms_final, 2);
+        if (comp_timed) {   // (the side stream joined before this sync)
+            bt_add(r.ms_final, 6);
+            bt_add(r.ms_final_early, 4);
+            comp_timed = false;
+        }
         if (getenv("PRGPU_BWA_DEBUG")) fprintf(stderr, "[bwa] final round %d: %d patch requests\n", round, cnt[1]);
         if (cnt[1] == 0) break;
         if (round > r.n_task + 2) return pr_set_error(PR_ERR_HIP, "bwa mode: patch rounds do not converge");
@@ -1097,6 +1127,15 @@ extern "C" int pr_sw_sam(pr_ctx *c, const pr_sam_in *in, char **text, int64_t *l
     *text = buf;
     *len = (int64_t)tot;
     if (n_records) *n_records = nr;
+    return 0;
+}
+
+extern "C" int pr_sw_bwa_timing(pr_ctx *c, float *walk_ms, float *final_ms, float *early_final_ms) {
+    if (!c) return pr_set_error(PR_ERR_ARG, "null ctx");
+    SwResident &r = ctx_sw(c);
+    if (walk_ms) *walk_ms = r.ms_walk;
+    if (final_ms) *final_ms = r.ms_final;
+    if (early_final_ms) *early_final_ms = r.ms_final_early;
     return 0;
 }
 

@@ -116,6 +116,11 @@ struct SwResident {
     void *side = nullptr;       // hipStream_t: the early final pass beside the later extension rounds
     void *side_ev[3] = {nullptr, nullptr, nullptr};   // hipEvent_t
     int64_t n_patch = 0;        // mem_patch_reg global scores computed
+    // bwa mode's bookkeeping kernels of the last launch (timing events, created on first use):
+    // [0, 1] each round's walk, [2, 3] each late final pass, [4, 5] the early final pass (side
+    // stream), [6, 7] its complement on the main stream
+    void *bt_ev[8] = {};
+    float ms_walk = 0.f, ms_final = 0.f, ms_final_early = 0.f;
     int64_t cig_slots = 0;      // ops in the slots (= first spill op)
     int64_t n_overflow = 0;     // tasks of the last launch whose CIGAR went to the spill area
     float ms_ext = 0.f, ms_glob = 0.f;

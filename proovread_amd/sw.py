@@ -175,6 +175,16 @@ def bwa_stats(ctx: _abi.Context):
     return r.value, n.value, p.value
 
 
+def bwa_timing(ctx: _abi.Context):
+    """bwa mode: (walk ms summed over rounds, main-stream final passes ms, early final pass ms)
+    of the last launch (pr_sw_bwa_timing)."""
+    L = _abi.lib()
+    L.pr_sw_bwa_timing.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_float), C.POINTER(C.c_float)]
+    w, f, e = C.c_float(), C.c_float(), C.c_float()
+    _abi.check(L.pr_sw_bwa_timing(ctx.h, C.byref(w), C.byref(f), C.byref(e)), "pr_sw_bwa_timing")
+    return w.value, f.value, e.value
+
+
 def last_timing(ctx: _abi.Context):
     L = _abi.lib()
     _setup(L)
