@@ -1965,10 +1965,10 @@ extern "C" int pr_lrset_commit(pr_ctx *c, pr_comm *comm, int flags) {
 // ---------------------------------------------------------------------------
 // seeding on the device (seed_kernels.hip over seed_core.h)
 // the index text 16 bases per word (IndexView.text4) for the occurrence table's match lengths
-static int seed_text4(pr_ctx *c, seedc::IndexView &v, hipStream_t s, bool packed = false) {
+static int seed_text4(pr_ctx *c, seedc::IndexView &v, hipStream_t s) {
     int rc = c->sd[SI_TEXT4].ensure((size_t)ix_pack4_words(v.n_text) * 8);
     if (rc) return rc;
-    const int e = packed ? 0 : ix_pack4_launch(v.text, v.n_text, c->sd[SI_TEXT4].as<uint64_t>(), s);
+    const int e = ix_pack4_launch(v.text, v.n_text, c->sd[SI_TEXT4].as<uint64_t>(), s);
     if (e) return set_error(PR_ERR_HIP, "text packing: %s", hipGetErrorString((hipError_t)e));
     v.text4 = c->sd[SI_TEXT4].as<uint64_t>();
     return 0;
@@ -2109,8 +2109,7 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
         (rc = D[SX_KEY0].ensure(ns * 4)) || (rc = D[SX_KEY1].ensure(ns * 4)) || (rc = D[SX_VAL0].ensure(ns * 4)) ||
         (rc = D[SX_KC].ensure(nk1 * 4)) || (rc = D[SI_KOFF].ensure(nk1 * 8)) ||
         (rc = D[SI_KPOS].ensure(nt * 4)) || (rc = D[SI_KEXT].ensure(nt * 8)) || (rc = D[SX_TEMP].ensure(temp)) ||
-        (rc = D[SX_CNTPTR].ensure(sizeof(uint32_t *) * (seedc::KI - 1))) ||
-        (rc = D[SI_TEXT4].ensure((size_t)ix_pack4_words(n_text) * 8)))
+        (rc = D[SX_CNTPTR].ensure(sizeof(uint32_t *) * (seedc::KI - 1))))
         return rc;
     if (chunked && ((rc = D[SX_VAL1].ensure(ns * 4)) || (rc = D[SX_KCC].ensure(nk1 * 4)) ||
                     (rc = D[SX_KOFFC].ensure(nk1 * 4)) || (rc = D[SX_KCUR].ensure(nk1 * 8))))
@@ -2132,7 +2131,6 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
     B.cstart = D[SI_CSTART].as<int64_t>();
     B.n_text = n_text;
     B.text = D[SI_TEXT].as<uint8_t>();
-    B.text4 = D[SI_TEXT4].as<uint64_t>();   // packed inside the build (its kext pass reads it)
     B.chunk = chunk;
     B.key0 = D[SX_KEY0].as<uint32_t>();
     B.key1 = D[SX_KEY1].as<uint32_t>();
@@ -2179,7 +2177,7 @@ static int index_build(pr_ctx *c, const uint8_t *lr_seq, const int64_t *lr_off, 
     v.kext = B.kext;
     v.ksplit = B.ksplit;
     for (int j = 0; j < seedc::KI - 1; ++j) v.cnt[j] = B.cnt[j];
-    if ((rc = seed_text4(c, v, s, true))) return rc;
+    if ((rc = seed_text4(c, v, s))) return rc;
     if ((rc = upload_blk_fr(c, v, cstart.data(), off.data(), n_lr, l_pac, n_text, s))) return rc;
     c->seed_view = v;
     c->seed_loaded = true;

@@ -141,40 +141,6 @@ __global__ void ix_kext_kernel(const uint8_t *text, int64_t n, const uint32_t *k
     kext[r] = kext_at(text, n, (int64_t)kpos[r]);
 }
 
-// kext_at from the 4-bit text (IndexView.text4, 16 bases a word, SEP past the text): the KX
-// bases after the 12-mer are nibbles x .. x + 27 of two shifted word pairs.  The packed text is
-// half the byte text's size (145 MB at configs[1]: it stays in the MALL), and a hit's random
-// access is 3 words instead of 9 dwords over up to two 128-byte lines (the byte-text gather was
-// 6.6 ms of the 18.8 ms build at configs[1]).  Same values: a nibble > 3 (N, SEP -- also every
-// position at or past the text's end) stops the run.
-__device__ __forceinline__ uint64_t nib_to_2bit(uint64_t x) {   // 16 nibbles' low 2 bits -> 32 bits
-    x &= 0x3333333333333333ull;
-    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
-    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
-    x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
-    return x;
-}
-__device__ __forceinline__ uint64_t kext_at4(const uint64_t *text4, int64_t p12) {
-    const int64_t x = p12 + KI;
-    const uint64_t *w = text4 + (x >> 4);
-    const int sh = (int)(x & 15) * 4;
-    const uint64_t a = w[0], b = w[1], c = w[2];
-    const uint64_t lo = sh ? (a >> sh) | (b << (64 - sh)) : a;   // nibbles x .. x + 15
-    const uint64_t hi = sh ? (b >> sh) | (c << (64 - sh)) : b;   // nibbles x + 16 .. x + 31
-    // a code > 3 has bit 2 set (codes are 0 .. 5)
-    const uint64_t blo = (lo >> 2) & 0x1111111111111111ull, bhi = (hi >> 2) & 0x0000111111111111ull;   // (12 nibbles)
-    const int m = blo ? __builtin_ctzll(blo) >> 2 : bhi ? 16 + (__builtin_ctzll(bhi) >> 2) : KX;
-    uint64_t v = nib_to_2bit(lo) | (nib_to_2bit(hi) << 32);
-    v &= m >= 32 ? ~0ull : ((1ull << (2 * m)) - 1ull);
-    return v | ((uint64_t)m << 56);
-}
-__global__ void ix_kext4_kernel(const uint64_t *text4, const uint32_t *kpos, const uint64_t *koff, uint64_t *kext) {
-    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= (int64_t)koff[NK]) return;
-    kext[r] = kext_at4(text4, (int64_t)kpos[r]);
-}
-
 // chunked build (texts beyond one sort): the 12-mer histogram of the whole text
 __global__ void ix_count_kernel(const uint8_t *text, int64_t n, uint32_t *kc) {
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p + KI <= n; p += (int64_t)gridDim.x * blockDim.x) {
@@ -275,7 +241,6 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
         IXCHK(hipGetLastError());
     }
     IXCHK(hipMemsetAsync(B.kc, 0, ((size_t)NK + 1) * 4, s));
-    if (B.text4) IXCHK((hipError_t)ix_pack4_launch(B.text, n, B.text4, s));
     if (n <= B.chunk) {
         // one sort: 12-mer keys + histogram, koff = exclusive scan, stable sort of (key,
         // position) by key (positions ascend within a k-mer) straight into kpos, then kext
@@ -288,13 +253,8 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
             IXCHK(hipGetLastError());
             hipLaunchKernelGGL(ix_kc_kernel, dim3(blocks_for((int64_t)NK, 256)), dim3(256), 0, s, B.koff, B.kc);
             IXCHK(hipGetLastError());
-            if (B.text4) {   // (packed behind the text kernel, below)
-                hipLaunchKernelGGL(ix_kext4_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text4, B.kpos, B.koff,
-                                   B.kext);
-            } else {
-                hipLaunchKernelGGL(ix_kext_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kpos, B.koff,
-                                   B.kext);
-            }
+            hipLaunchKernelGGL(ix_kext_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kpos, B.koff,
+                               B.kext);
             IXCHK(hipGetLastError());
         } else {
             IXCHK(hipMemsetAsync(B.koff, 0, ((size_t)NK + 1) * 8, s));

@@ -16,8 +16,6 @@ struct SeedIndexBuild {
     const int64_t *cstart;        // [2 n_lr] text offset of every contig
     int64_t n_text;               // 2 l_pac + 2 n_lr (<= seedc::MAX_TEXT)
     uint8_t *text;                // [n_text]
-    uint64_t *text4;              // [ix_pack4_words(n_text)] the 4-bit copy (IndexView.text4), packed
-                                  // by the build and read by its kext pass; null: neither
     // the 12-mer lists are sorted in chunks of `chunk` text positions (a divisor of 2^32); one
     // chunk (the text fits): the sort writes kpos directly
     int64_t chunk;
