@@ -98,6 +98,7 @@ int cns_k_header();      // ints of window starts reserved at the head of a K po
 constexpr int CNS_THREADS = 256;
 constexpr int CHIM_MAXCOLS = 128;
 constexpr int CHIM_TCAP = 256;
+constexpr int CHIM_CL = 8;   // insertion states a column's chimera entry list holds (more: the table scan)
 // per-phase wall-clock ticks: prep, binning, state table, scatter, argmax+write, cigar, chimera,
 // idle; scatter detail: zero+ignore, group select, staging, walks; counts: groups, items, windows
 constexpr int CNS_NPHASE = 24;

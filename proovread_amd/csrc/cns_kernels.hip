@@ -436,7 +436,8 @@ struct CnsGeo {
     static constexpr int WAVE_BYTES = 64 * 16 + (64 / CNS_GW) * CNS_SEQ_DW * 4;   // per wave: op tables int4[NG][GW], SEQ dwords u32[NG][SEQ_DW]
     static constexpr int B_WAVE = (B_IGN + W / 8 + 15) & ~15;
     static constexpr int SZ_WIN = B_WAVE + (CNS_THREADS / 64) * WAVE_BYTES;
-    static constexpr int SZ_CHIM = (CHIM_MAXCOLS * 13 + CHIM_TCAP * 4 + 16) * 4;
+    static constexpr int SZ_CHIM = (CHIM_MAXCOLS * 13 + CHIM_TCAP * 4 + 16) * 4 +
+                                   CHIM_MAXCOLS * (4 + CHIM_CL * 12);   // + the per-column entry lists
     static constexpr int SZ_B = ((SZ_WIN > SZ_CHIM ? SZ_WIN : SZ_CHIM) + 15) & ~15;
     static constexpr int LDS = OFF_B + SZ_B;
     static constexpr int MAX_BINS = (SZ_A + SZ_B - CNS_THREADS * 4) / 8;
@@ -601,6 +602,43 @@ __device__ double chim_hx(int side, int c, const uint32_t *f6l, const uint32_t *
             first = false;
         }
     }
+    return h;
+}
+
+// chim_hx over a column's merged entry list (chim_cols): n insertion states sorted by their
+// chimera-table order (ok: order << SLOT_SH | slot), each with its left / right counts (cnt: l | r
+// << 16).  The same additions in the same order as chim_hx's selection over the whole tables (a
+// state absent from a side has count 0 there and adds nothing), so the same doubles.
+__device__ double chim_hx_list(int side, int c, const uint32_t *f6l, const uint32_t *f6r, const unsigned long long *ok,
+                               const uint32_t *cnt, int n) {
+    const double l2 = log(2.0);
+    double total = 0.0;
+    for (int s = 0; s < 6; ++s) {
+        const uint32_t v = (side != 1 ? f6l[c * 6 + s] : 0u) + (side != 0 ? f6r[c * 6 + s] : 0u);
+        if (v) total += (double)v;
+    }
+    auto ins = [&](int k) -> uint32_t {
+        const uint32_t x = cnt[k];
+        return side == 0 ? (x & 0xFFFFu) : side == 1 ? (x >> 16) : (x & 0xFFFFu) + (x >> 16);
+    };
+    for (int k = 0; k < n; ++k) {
+        const uint32_t v = ins(k);
+        if (v) total += (double)v;
+    }
+    double h = 0.0;
+    for (int s = 0; s < 6; ++s) {
+        const uint32_t v = (side != 1 ? f6l[c * 6 + s] : 0u) + (side != 0 ? f6r[c * 6 + s] : 0u);
+        if (!v) continue;
+        const double p = (double)v / total;
+        h -= p * (log(p) / l2);
+    }
+    for (int k = 0; k < n; ++k) {
+        const uint32_t v = ins(k);
+        if (!v) continue;
+        const double p = (double)v / total;
+        h -= p * (log(p) / l2);
+    }
+    (void)ok;
     return h;
 }
 
@@ -1517,66 +1555,133 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                 for (int x = tid; x < CHIM_MAXCOLS * 13; x += CNS_THREADS) f6a[x] = 0u;
                 for (int x = tid; x < CHIM_TCAP * 4; x += CNS_THREADS) tkl[x] = 0u;
                 __syncthreads();
-                for (int i = tid; i < na; i += CNS_THREADS) {
-                    const int64_t g = a0 + i;
-                    if (!D.kept[g] || (D.a_st[g] & ST_SMSKIP)) continue;
-                    const int rp = D.a_rpos[g];
-                    if (rp > mt || D.a_end[g] <= mf) continue;
-                    const int bin = D.a_bin[g];
+                // the kept alignments that can overlap [mf, mt]: the pileup's K pool range of the
+                // windows mf .. mt touch (those starting there, and the straddlers of the wback
+                // windows before), not every alignment of the read
+                const int kw0 = mf / G::W, kw1 = mt / G::W, kwb = kw0 - wback;
+                const int kb = kwb < 0 ? 0 : (kwb < kw0 ? Ks[kwb] : Kh[kw0]), ke = Kh[kw1 + 1];
+                // a kept alignment's states in [mf, mt] by a 16-lane group, op-parallel (the pileup's
+                // stream_kept / group_states: its SEQ in the group's LDS area), not a thread walking
+                // its CIGAR; each state counted into the side tables of the bins the alignment is in
+                stream_kept<G::WGCU >= 4 ? CNS_PD_M : CNS_PD_S>(D, K, kb, ke, mf, mt + 1, wops, wseq, snt4, [&](const KeptView &v, int4 *gops, const uint32_t (&cop)[CNS_OPF]) {
+                    const int bin = D.a_bin[a0 + v.i];
                     const bool inl = bin >= fl && bin <= tl, inr = bin >= fr && bin <= tr;
-                    const SeqV sv = seq_view(D, g);
-                    const int sb = D.a_sb[g];
-                    const uint32_t *cg = D.cig + D.cig_off[g];
-                    walk_states<false>(cg, D.a_cb[g], D.a_ce[g], rp, mf, mt + 1,
-                                       [&](int col, int sidx, int kind, int qoff, int qlen) {
-                                           const int c = col - mf;
-                                           f6a[c] = 1u;
-                                           int fi = -1, slot = -1;
-                                           if (kind == 1) fi = 4;
-                                           else if (qlen == 1) fi = fixed_idx(sv[sb + qoff]);
-                                           else slot = T.find(state_key(sv, sb + qoff, qlen));
-                                           for (int side = 0; side < 2; ++side) {
-                                               if (side == 0 ? !inl : !inr) continue;
-                                               uint32_t *f6 = side == 0 ? f6l : f6r;
-                                               uint32_t *tk = side == 0 ? tkl : tkr;
-                                               uint32_t *tc = side == 0 ? tcl : tcr;
-                                               if (fi >= 0) { atomicAdd(&f6[c * 6 + fi], 1u); continue; }
-                                               if (slot < 0) { C->flag = 1; continue; }
-                                               const uint32_t key = ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)slot;
-                                               uint32_t h = (key * 2654435761u) >> 24;
-                                               int p = 0;
-                                               for (; p < CHIM_TCAP; ++p) {
-                                                   const uint32_t x = tk[h];
-                                                   if (x == key) break;
-                                                   if (x == 0u) {
-                                                       const uint32_t o = atomicCAS(&tk[h], 0u, key);
-                                                       if (o == 0u || o == key) break;
-                                                   }
-                                                   h = (h + 1) & (CHIM_TCAP - 1);
-                                               }
-                                               if (p == CHIM_TCAP) C->flag = 1;
-                                               else atomicAdd(&tc[h], 1u);
-                                           }
-                                       });
-                }
+                    const uint32_t lut = v.rc ? 0x50321u : 0x51230u;   // nt4 code -> fixed-state index
+                    auto fixed_at = [&](int sq) -> int {
+                        if (v.fast && snt4) {
+                            uint32_t c8 = v.sl[v.rc ? v.ls - 1 - sq : sq];
+                            c8 = c8 > 4u ? 4u : c8;
+                            return (int)((lut >> (4u * c8)) & 15u);
+                        }
+                        return fixed_idx_at(v.sv, sq);
+                    };
+                    auto add = [&](int col, int fi, int slot) {
+                        const int c = col - mf;
+                        f6a[c] = 1u;
+                        for (int side = 0; side < 2; ++side) {
+                            if (side == 0 ? !inl : !inr) continue;
+                            uint32_t *f6 = side == 0 ? f6l : f6r;
+                            uint32_t *tk = side == 0 ? tkl : tkr;
+                            uint32_t *tc = side == 0 ? tcl : tcr;
+                            if (fi >= 0) { atomicAdd(&f6[c * 6 + fi], 1u); continue; }
+                            if (slot < 0) { C->flag = 1; continue; }
+                            const uint32_t key = ((uint32_t)(c + 1) << SLOT_SH) | (uint32_t)slot;
+                            uint32_t h = (key * 2654435761u) >> 24;
+                            int p = 0;
+                            for (; p < CHIM_TCAP; ++p) {
+                                const uint32_t x = tk[h];
+                                if (x == key) break;
+                                if (x == 0u) {
+                                    const uint32_t o = atomicCAS(&tk[h], 0u, key);
+                                    if (o == 0u || o == key) break;
+                                }
+                                h = (h + 1) & (CHIM_TCAP - 1);
+                            }
+                            if (p == CHIM_TCAP) C->flag = 1;
+                            else atomicAdd(&tc[h], 1u);
+                        }
+                    };
+                    group_states(D.cig + v.cgi, v.nop, v.rp, v.sb, mf, mt + 1, gops, cop,
+                                 [&](int scol, int sqp, int slen) {
+                                     if (slen == 1) add(scol, fixed_at(sqp), -1);
+                                     else add(scol, -1, (inl || inr) ? T.find(state_key(v.sv, sqp, slen)) : -1);
+                                 },
+                                 [&](int cc, int qp) { add(cc, qp < 0 ? 4 : fixed_at(qp), -1); });
+                });
                 __syncthreads();
+                CNS_TICK(9);   // (the candidate's side tables)
                 // skip if any column of [mf, mt] is empty in the full recompute (Seq.pm:808)
                 int empty = 0;
                 for (int c = tid; c < ncol; c += CNS_THREADS) if (!f6a[c]) empty = 1;
                 empty = block_or(empty, ired);
                 if (empty) continue;
+                // every column's insertion-state entries of both side tables, listed once (an entry a
+                // thread) and merged per state in chimera-table order, so the three Hx of a column
+                // visit its few states instead of selecting each from both whole tables (the
+                // selection was ~2/3 of the finish task's consensus kernel); a column with more than
+                // CHIM_CL states keeps the table selection
+                uint32_t *cln = reinterpret_cast<uint32_t *>(ired + 16);            // [CHIM_MAXCOLS]
+                unsigned long long *clk = reinterpret_cast<unsigned long long *>(cln + CHIM_MAXCOLS);   // [.. x CHIM_CL]
+                uint32_t *clc = reinterpret_cast<uint32_t *>(clk + CHIM_MAXCOLS * CHIM_CL);             // [.. x CHIM_CL]
+                for (int c = tid; c < CHIM_MAXCOLS; c += CNS_THREADS) cln[c] = 0u;
+                __syncthreads();
+                for (int e = tid; e < 2 * CHIM_TCAP; e += CNS_THREADS) {
+                    const int side = e >= CHIM_TCAP ? 1 : 0, x = e - side * CHIM_TCAP;
+                    const uint32_t k = side ? tkr[x] : tkl[x];
+                    if (!k) continue;
+                    const int c = (int)(k >> SLOT_SH) - 1;
+                    if (c < 0 || c >= CHIM_MAXCOLS) continue;
+                    const uint32_t at = atomicAdd(&cln[c], 1u);
+                    // (raw entries first: the table index and its side)
+                    if (at < (uint32_t)CHIM_CL) clc[c * CHIM_CL + (int)at] = (uint32_t)e;
+                }
+                __syncthreads();
                 int npos = 0, ntot = 0;
                 for (int c = tid; c < ncol; c += CNS_THREADS) {
                     bool nel = false, ner = false;
                     for (int s = 0; s < 6; ++s) { nel |= f6l[c * 6 + s] != 0u; ner |= f6r[c * 6 + s] != 0u; }
-                    for (int e = 0; e < CHIM_TCAP; ++e) {
-                        nel |= tkl[e] != 0u && (int)(tkl[e] >> SLOT_SH) - 1 == c;
-                        ner |= tkr[e] != 0u && (int)(tkr[e] >> SLOT_SH) - 1 == c;
+                    const int ne = (int)cln[c];
+                    const bool listed = ne <= CHIM_CL;
+                    int nm = 0;   // merged states of the column
+                    unsigned long long *mk = clk + c * CHIM_CL;
+                    uint32_t *mc = clc + c * CHIM_CL;
+                    if (listed) {
+                        // (in place: the merged list's writes stay at or below entry k, read first)
+                        for (int k = 0; k < ne; ++k) {
+                            const int e = (int)mc[k], side = e >= CHIM_TCAP ? 1 : 0, x = e - side * CHIM_TCAP;
+                            const uint32_t key = side ? tkr[x] : tkl[x], v = side ? tcr[x] : tcl[x];
+                            nel |= side == 0;
+                            ner |= side == 1;
+                            const int slot = (int)(key & SLOT_MASK);
+                            const unsigned long long o = (T.chim_order(slot) << SLOT_SH) | (unsigned long long)slot;
+                            int j = 0;
+                            while (j < nm && mk[j] != o) ++j;
+                            if (j == nm) {   // insert in order
+                                int i = nm++;
+                                while (i > 0 && mk[i - 1] > o) { mk[i] = mk[i - 1]; mc[i] = mc[i - 1]; --i; }
+                                mk[i] = o;
+                                mc[i] = side ? v << 16 : v;
+                            } else {
+                                mc[j] += side ? v << 16 : v;
+                            }
+                        }
+                    } else {
+                        for (int e = 0; e < CHIM_TCAP; ++e) {
+                            nel |= tkl[e] != 0u && (int)(tkl[e] >> SLOT_SH) - 1 == c;
+                            ner |= tkr[e] != 0u && (int)(tkr[e] >> SLOT_SH) - 1 == c;
+                        }
                     }
                     if (!nel || !ner) continue;
-                    const double hr = chim_hx(1, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
-                    const double hl = chim_hx(0, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
-                    const double hc = chim_hx(2, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
+                    double hr, hl, hc;
+                    if (listed) {
+                        hr = chim_hx_list(1, c, f6l, f6r, mk, mc, nm);
+                        hl = chim_hx_list(0, c, f6l, f6r, mk, mc, nm);
+                        hc = chim_hx_list(2, c, f6l, f6r, mk, mc, nm);
+                    } else {
+                        hr = chim_hx(1, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
+                        hl = chim_hx(0, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
+                        hc = chim_hx(2, c, f6l, f6r, tkl, tcl, tkr, tcr, T);
+                    }
                     const double hgt = hr > hl ? hr : hl;
                     ++ntot;
                     if (hc - hgt > 0.7) ++npos;
@@ -1584,6 +1689,7 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
                 long long tp, tt;
                 block_scan_excl(npos, scan, &tp);
                 block_scan_excl(ntot, scan, &tt);
+                CNS_TICK(10);   // (its column entropies)
                 if (tid == 0 && tt > 0 && C->nchim >= (int)(D.chim_off[lr + 1] - c_off)) C->flag = 1;
                 else if (tid == 0 && tt > 0) {
                     int32_t *rec = D.o_chim + 4 * (c_off + C->nchim);

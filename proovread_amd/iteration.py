@@ -175,7 +175,7 @@ class Iteration:
         t = (C.c_uint64 * 24)()
         _abi.check(self.L.pr_cns_phase_ticks(self.ctx.h, t, 24), "pr_cns_phase_ticks")
         names = ["prep", "binning", "state_table", "scatter", "argmax_write", "cigar", "chimera", "idle",
-                 "scatter_zero", "scatter_select", "scatter_stage", "scatter_walk"]
+                 "scatter_zero", "chimera_tables", "chimera_entropy", "scatter_walk"]
         out = {k: t[i] / 1e5 for i, k in enumerate(names)}
         out.update(groups=int(t[12]), items=int(t[13]), windows=int(t[14]), scatter_prepass=t[15] / 1e5,
                    scatter_ins=t[16] / 1e5, visits=int(t[17]), runs=int(t[18]), ins_states=int(t[19]),
