@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--loop-only", action="store_true",
                     help="profiling: the correction runs only (no value_task phase, no CPU baseline)")
+    ap.add_argument("--task-only", action="store_true",
+                    help="profiling: one untimed correction run, then the timed bwa-sr-1 tasks (value_task, rooflines); "
+                         "value is then not a measurement (rocprof / PMC passes of the roofline kernels)")
     ap.add_argument("--cpu-lrs-per-worker", type=int, default=256)
     ap.add_argument("--comm", choices=("rccl", "none"), default="rccl",
                     help="rccl: the step all-reduces the device {bpt, bpN} statistic over an RCCL communicator at "
@@ -232,7 +235,7 @@ def main():
         return h.hexdigest()
 
     first_digest = None
-    for k in range(args.warmup):
+    for k in range(0 if args.task_only else args.warmup):
         chim, _ = loop_step()
         if k == 0:
             first_digest = digest(chim)
@@ -242,15 +245,17 @@ def main():
     t0 = time.perf_counter()
     dev0 = stages.device_ms
     logs = []
-    for _ in range(args.steps):
+    chim = []
+    for _ in range(0 if args.task_only else args.steps):   # (task-only: no correction run at all)
         chim, log = loop_step()
         logs.append(log)
+    logs = logs or [[]]
     if cm is not None:
         cm.barrier()
     _abi.check(L.pr_ctx_sync(ctx.h), "pr_ctx_sync")
     el = time.perf_counter() - t0
     loop_dev_ms = (stages.device_ms - dev0) / max(args.steps, 1)
-    last_digest = digest(chim)
+    last_digest = digest(chim) if not args.task_only else None
     n_chim = len(chim)
     if cm is not None:
         el = cm.allreduce_floats([el], comm_mod.RED_MAX)[0]
@@ -367,8 +372,8 @@ def main():
         if cm is not None:
             cm.close()
         return
-    value = total_bases * args.steps / el / 1e6
-    step_ms = el / args.steps * 1e3
+    value = total_bases * args.steps / el / 1e6 if not args.task_only else None
+    step_ms = el / args.steps * 1e3 if not args.task_only else None
     task_ms = el_task / args.steps * 1e3
     dom_ms /= K
     dom_tops = dom_cells * OPS_PER_CELL / (dom_ms * 1e-3) / 1e12
@@ -398,12 +403,12 @@ def main():
             traffic = traffic_cns = traffic_ext = traffic_seed = None
     out = {
         "metric": "corrected long-read Mbases/sec per node",
-        "value": round(value, 3),
+        "value": round(value, 3) if value is not None else None,
         "unit": "Mbases/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(step_ms, 3),
+        "ms_per_step": round(step_ms, 3) if step_ms is not None else None,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
