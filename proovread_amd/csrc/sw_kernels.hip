@@ -30,6 +30,35 @@ __device__ __forceinline__ int sw_score(int t, int q, int a, int b) {
     return (t > 3 || q > 3) ? -1 : (t == q ? a : -b);
 }
 
+// bwa_gen_cigar2's gap-free score (query length == reference length, no DP): the scores of query
+// base qbase + qstep * i against reference row i (complemented on the reverse strand), 16 rows a
+// step from two 16-byte windows -- the query read forward from its first base, the reference
+// forward or, on the reverse strand, backwards from its last row (pk_tref16; the pools' 64 bytes
+// of slack on both sides cover the windows' overhang) -- instead of two byte loads per row (the
+// finish task's near-exact alignments are nearly all gap-free: ~16 ms of its CIGAR pass)
+__device__ int nogap_score(const uint8_t *Q, int qbase, int qstep, const uint8_t *Lr, long tb, bool rev, int n,
+                           const SwOptsDev &O) {
+    const int q0 = qstep > 0 ? qbase : qbase - n + 1;   // the query's first base
+    // pair u: query q0 + u with row i = (qstep > 0 ? u : n - 1 - u)
+    const uint8_t *T = qstep > 0 ? Lr + tb : Lr + tb + n - 1;
+    const int ts = qstep > 0 ? 1 : -1;
+    int sc = 0;
+    for (int u0 = 0; u0 < n; u0 += 16) {
+        uint32_t qw[4], tw[4];
+        __builtin_memcpy(qw, Q + q0 + u0, 16);
+        pk_tref16(T, ts, u0, tw);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (u0 + k >= n) break;
+            int tc = (int)((tw[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+            if (rev && tc < 4) tc = 3 - tc;
+            const int qc = (int)((qw[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+            sc += sw_score(tc, qc, O.a, O.b);
+        }
+    }
+    return sc;
+}
+
 // ---- extension: packed LDS word = h[0,13) | e[13,26) | 8*q[26,32)
 // (H and E of ksw_extend2 are >= 0 and bounded by a * read length < 8192;
 // the query base is stored pre-multiplied by 8 to index the row score table)
@@ -1063,14 +1092,7 @@ __global__ void __launch_bounds__(SW_WAVE) sw_global_ring_kernel(SwDev D, SwOpts
         int gsc = glob_ring<WB>(Q, qbase, qstep, dp ? lqq : 0, Lr, tb, 1, rev, dp ? rlen : 0, O, dp ? ww : 0, zl, SW_WAVE);
         if (t < 0) continue;
         if (ww < 0) gsc = 0;
-        if (nogap) {
-            gsc = 0;
-            for (int i = 0; i < lqq; ++i) {
-                int tc = (int)Lr[tb + i];
-                if (rev && tc < 4) tc = 3 - tc;
-                gsc += sw_score(tc, (int)Q[qbase + qstep * i], O.a, O.b);
-            }
-        }
+        if (nogap) gsc = nogap_score(Q, qbase, qstep, Lr, tb, rev, lqq, O);
         // bwa_gen_cigar2's loop after pass 1: stop when w2 hit its cap or the score is close
         // enough; otherwise the LDS kernel reruns the whole loop for this task
         if (dp && w2 != O.w << 2 && gsc < truesc - O.a) {
