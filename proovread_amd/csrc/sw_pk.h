@@ -261,8 +261,8 @@ constexpr int pk_npair(int w) { return (2 * w + 2 + 15) >> 4; }
 
 // The DP of both tasks.  mA/mB: their query masks; nrows = wave max of tlen;
 // z: direction words of this lane, (row, pair) at z[(i * npair + p) * ZS];
-// scA/scB: ksw_global2 scores; nflag gets bit 0 / 1 set if task A / B met an N
-// in its reference window.  w and qlen must be wave-uniform.
+// scA/scB: ksw_global2 scores (reference N rows scored as bwa does, -1 a cell; the caller flags
+// queries with an N).  w and qlen must be wave-uniform.
 template <int WB>
 SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int nrows, const SwOptsDev &O,
                         const uint32_t *mA, const uint32_t *mB, int MS, PkDir *z, int ZS, int &scA, int &scB,
@@ -274,6 +274,7 @@ SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int n
     const int npair = pk_npair(w);
     const uint32_t NEG = pk_dup(PK_NEG);
     const uint32_t NAB = pk_dup(-(O.a + b));               // m = -1 on a match: M = Hd + (a + b)
+    const uint32_t NB1 = pk_dup(-(b - 1));                 // a reference N row: M = Hd + (b - 1)
     const uint32_t cE = pk_dup(O.e_del - b);               // E' = e0 - e_del (+ b: next row's bias)
     const uint32_t cT1 = pk_dup(O.o_del + O.e_del - b);    // t1 = M - oe_del (+ b)
     const uint32_t cD3 = pk_dup(O.o_del);                  // t1 - E' = D1 - o_del
@@ -308,17 +309,21 @@ SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int n
         }
         if (A.comp && ca < 4) ca = 3 - ca;
         if (B.comp && cb < 4) cb = 3 - cb;
-        if (i < A.tlen && ca > 3) nflag |= 1;
-        if (i < B.tlen && cb > 3) nflag |= 2;
         // match groups: slot s <-> bit s & 15 of G[s >> 4] (low half A, high half B)
         uint32_t wa[3], wb[3], G[6];
         pk_window(mA, MS, i - w + 64, ca & 3, wa);
         pk_window(mB, MS, i - w + 64, cb & 3, wb);
+        // a reference N row scores -1 in every column (bwa_fill_scmat): with the row bias b that is
+        // + (b - 1) on every slot -- all bits set and the row's step (b - 1) for that half
+        const bool na = ca > 3, nb = cb > 3;
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
+            wa[g] = na ? 0xFFFFFFFFu : wa[g];
+            wb[g] = nb ? 0xFFFFFFFFu : wb[g];
             G[2 * g] = perm_b32(wb[g], wa[g], 0x05040100u);
             G[2 * g + 1] = perm_b32(wb[g], wa[g], 0x07060302u);
         }
+        const uint32_t NABr = (na || nb) ? ((na ? NB1 : NAB) & 0xFFFFu) | ((nb ? NB1 : NAB) & 0xFFFF0000u) : NAB;
         const int beta = (i + 1) * b;
         uint32_t h1 = i == w ? pk_dup(-(O.o_del + O.e_del * (i + 1)) + beta) : NEG;
         uint32_t f = NEG;
@@ -337,7 +342,7 @@ SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int n
                 const uint32_t Hd = s + 1 < NS ? RH[s + 1] : NEG;
                 const uint32_t e0 = s + 1 < NS ? RE[s + 1] : NEG;
                 const uint32_t mm = pk_asr15(pk_shl(G[s >> 4], 15 - (s & 15)));
-                const uint32_t M = pk_mad(mm, NAB, Hd);
+                const uint32_t M = pk_mad(mm, NABr, Hd);
                 const uint32_t hme = pk_max(M, e0);
                 const uint32_t h = pk_max(hme, f);
                 const uint32_t D1 = pk_sub(M, e0);
@@ -402,7 +407,8 @@ SW_RING_FN void glob_pk(const PkHalf &A, const PkHalf &B, int qlen, int w, int n
 // h * 16 + (s & 15) (h <= 2047 for the routed tasks).  Pruned end: the last
 // word eh[j] != 0 is one past the last column with H > 0 (E(i+1,j) > 0 implies
 // H(i,j) > 0), tracked as a packed max of [h > 0] * (s + 1).
-// Tasks that meet an N are flagged for the exact kernel.
+// Reference N rows are scored as bwa does (-1 a cell); tasks whose query holds an N are flagged
+// by the caller for the exact kernel.
 struct PkExtHalf {
     const uint8_t *T;   // first reference base of the side's window
     int ts;             // +1 / -1: reference step
@@ -475,6 +481,7 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
     }
     for (int i = 0; i < nrows; ++i) {
         int cb[2];
+        bool rn[2];
         uint32_t sev = 0u, bnd = 0u;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -490,10 +497,7 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
             }
             if (Hh[h]->comp && c < 4) c = 3 - c;
             if (live[h] && i >= Hh[h]->tlen) live[h] = false;
-            if (live[h] && c > 3) {
-                nflag |= 1 << h;
-                live[h] = false;
-            }
+            rn[h] = c > 3;   // a reference N row: -1 in every column (below)
             cb[h] = c & 3;
             if (end[h] > i + w + 1) end[h] = i + w + 1;
             if (end[h] > qlen) end[h] = qlen;
@@ -504,11 +508,16 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
         uint32_t wa[3], wb[3], G[6];
         pk_window(mA, MS, i - w + 64, cb[0], wa);
         pk_window(mB, MS, i - w + 64, cb[1], wb);
+        // a reference N row (bwa_fill_scmat: -1 against every query base): no match bits and the
+        // mismatch step 1 instead of b for that half -- M = max(Hd - 1, 0) where Hd > 0
 #pragma unroll
         for (int g = 0; g < 3; ++g) {
+            wa[g] = rn[0] ? 0u : wa[g];
+            wb[g] = rn[1] ? 0u : wb[g];
             G[2 * g] = perm_b32(wb[g], wa[g], 0x05040100u);
             G[2 * g + 1] = perm_b32(wb[g], wa[g], 0x07060302u);
         }
+        const uint32_t BDr = (rn[0] || rn[1]) ? ((rn[0] ? 1u : BD & 0xFFFFu) | (rn[1] ? 0x10000u : BD & 0xFFFF0000u)) : BD;
         // the column entering at the top slot still holds its row -1 word (H only)
         uint32_t qin = 0u;
         {
@@ -545,7 +554,7 @@ SW_RING_FN void ext_pk(const PkExtHalf &A, const PkExtHalf &B, int qlen, int w, 
                 // M = H(i-1,j-1) ? H(i-1,j-1) + S : 0, clamped at 0 (a negative M acts as 0 in
                 // every use: h = max(M, e, f) with e, f >= 0, and the gap openings max(M - oe, 0)),
                 // so the unsigned saturating subtracts replace the max-with-0 steps
-                const uint32_t M = pk_min(pk_shl(Hd, 4), pk_subs(pk_mad(mm, NAB, Hd), BD));
+                const uint32_t M = pk_min(pk_shl(Hd, 4), pk_subs(pk_mad(mm, NAB, Hd), BDr));
                 const uint32_t h = pk_max(pk_max(M, e0), f);
                 const uint32_t en = pk_max(pk_subs(e0, cED), pk_subs(M, cOD));
                 const uint32_t fn = pk_max(pk_subs(f, cEI), pk_subs(M, cOI));

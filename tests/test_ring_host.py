@@ -112,7 +112,7 @@ def test_global_pk_matches_oracle(ring, seed):
     for _ in range(300):
         lq = rng.choice([1, 2, 5, 10, 30, 60, 100, 149, 150, 151, 200, 255])
         qs = ["".join(rng.choice("ACGT") for _ in range(lq)) for _ in range(2)]
-        ts = [(_mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])).replace("N", "A") or "A") for q in qs]
+        ts = [(_mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])) or "A") for q in qs]   # (N in targets: scored)
         if rng.random() < 0.15:
             ts[1] = ""      # empty partner half
         dls = [abs(len(t) - lq) for t in ts if t]
@@ -140,12 +140,20 @@ def test_global_pk_matches_oracle(ring, seed):
 
 
 def test_global_pk_flags_n(ring):
-    """An N in the query or the target window is flagged (the task goes to the exact kernel)."""
+    """An N in the query is flagged (the task goes to the exact kernel); an N in the target
+    window is scored in the packed kernel (-1 against every query base, bwa_fill_scmat), so the
+    half with the target N is not flagged and matches osw_global."""
     q, t = "ACGTNACGTA", "ACGTAACGTA"
     sc, nc, cig = (C.c_int * 2)(), (C.c_int * 2)(), (C.c_uint32 * 256)()
     fl = ring.pk_global(5, 11, 2, 4, 1, 3, 10, 5, _nt4(q), _nt4(t), 10, _nt4(t), 10, _nt4("ACGTANCGTA"),
                         sc, nc, cig, 128, 0)
-    assert fl == (1 << 2) | 2
+    assert fl == (1 << 2)
+    L = ob.sw_lib()
+    mat = (C.c_int8 * 25)()
+    L.osw_fill_scmat(5, 11, mat)
+    nco, cigo = C.c_int(), (C.c_uint32 * 128)()
+    so = L.osw_global(10, _nt4(t), 10, _nt4("ACGTANCGTA"), 5, mat, 2, 4, 1, 3, 5, C.byref(nco), cigo, 128)
+    assert (sc[1], list(cig[128:128 + nc[1]])) == (so, list(cigo[:nco.value]))
 
 
 def _band_w(lq, a, od, ed, oi, ei, eb, w):
@@ -167,7 +175,7 @@ def test_extend_pk_small_h_matches_oracle(ring, seed):
         qs = ["".join(rng.choice("ACGT") for _ in range(L)) for _ in range(2)]
         ts = []
         for q in qs:
-            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])).replace("N", "C") + \
+            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])) + \
                 "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 60)))
             if rng.random() < 0.2:
                 t = "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 200)))
@@ -204,7 +212,7 @@ def test_extend_pk_matches_oracle(ring, seed):
         qs = ["".join(rng.choice("ACGT") for _ in range(L)) for _ in range(2)]
         ts = []
         for q in qs:
-            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])).replace("N", "C") + \
+            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])) + \
                 "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 60)))
             if rng.random() < 0.2:
                 t = "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 200)))
@@ -237,7 +245,7 @@ def test_extend_pk_reverse_window_matches_oracle(ring, seed):
         qs = ["".join(rng.choice("ACGT") for _ in range(L)) for _ in range(2)]
         ts = []
         for q in qs:
-            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])).replace("N", "C") + \
+            t = _mutate(q, rng, rng.choice([0, 0.05, 0.15, 0.3])) + \
                 "".join(rng.choice("ACGT") for _ in range(rng.randint(0, 60)))
             ts.append(t[:250])
         h0s = [rng.choice([0, 5, 30, 100, 400]) for _ in range(2)]
