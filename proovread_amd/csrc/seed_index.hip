@@ -195,7 +195,15 @@ __global__ void ix_chunk_advance_kernel(uint64_t *kcur, const uint32_t *kcc) {
 
 // run ends: one thread per text position holding N / SEP; the j-mers (j < 12) that end
 // just before it inside the run of bases are counted into cnt[j - 1]
-__global__ void ix_tail_kernel(const uint8_t *text, int64_t n, uint32_t *const *cnt) {
+// The j-mers of length j <= TAIL_LDS_J have 4^j <= 1024 counters, which every N / SEP position
+// of a masked text hits (bwa-sr-2's mapping reference is ~70 % N: 3.3 ms of global atomics on a
+// few addresses); they are counted in the workgroup's LDS and added to HBM once per block.
+constexpr int TAIL_LDS_J = 5;
+constexpr int TAIL_LDS_N = ((1 << (2 * (TAIL_LDS_J + 1))) - 4) / 3;   // 4 + 16 + ... + 4^TAIL_LDS_J
+__global__ void __launch_bounds__(256) ix_tail_kernel(const uint8_t *text, int64_t n, uint32_t *const *cnt) {
+    __shared__ uint32_t lc[TAIL_LDS_N];
+    for (int k = threadIdx.x; k < TAIL_LDS_N; k += blockDim.x) lc[k] = 0u;
+    __syncthreads();
     for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (int64_t)gridDim.x * blockDim.x) {
         if (text[p] <= 3) continue;
         uint32_t code = 0;
@@ -204,8 +212,17 @@ __global__ void ix_tail_kernel(const uint8_t *text, int64_t n, uint32_t *const *
             const uint8_t c = text[p - j];
             if (c > 3) break;
             code |= (uint32_t)c << (2 * (j - 1));   // T[p-j] is the first base of the j-mer
-            atomicAdd(&cnt[j - 1][code], 1u);
+            if (j <= TAIL_LDS_J) atomicAdd(&lc[((1 << (2 * j)) - 4) / 3 + code], 1u);
+            else atomicAdd(&cnt[j - 1][code], 1u);
         }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < TAIL_LDS_N; k += blockDim.x) {
+        const uint32_t v = lc[k];
+        if (!v) continue;
+        int j = 1;
+        while (k >= ((1 << (2 * (j + 1))) - 4) / 3) ++j;   // table j holds [(4^j - 4) / 3, (4^(j+1) - 4) / 3)
+        atomicAdd(&cnt[j - 1][k - ((1 << (2 * j)) - 4) / 3], v);
     }
 }
 
@@ -291,7 +308,9 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
     // j-mer count tables: run ends first, then the children's sums from j = 11 down
     for (int j = 1; j < KI; ++j) IXCHK(hipMemsetAsync(B.cnt[j - 1], 0, ((size_t)1 << (2 * j)) * 4, s));
     if (n > 0) {
-        hipLaunchKernelGGL(ix_tail_kernel, dim3(blocks_capped(n, 256)), dim3(256), 0, s, B.text, n, B.cnt_dev);
+        // (a grid of 8192 blocks striding over the text: each block's LDS counts flushed once)
+        const unsigned tb = blocks_capped(n, 256) < 8192u ? blocks_capped(n, 256) : 8192u;
+        hipLaunchKernelGGL(ix_tail_kernel, dim3(tb), dim3(256), 0, s, B.text, n, B.cnt_dev);
         IXCHK(hipGetLastError());
     }
     for (int j = KI - 1; j >= 1; --j) {
