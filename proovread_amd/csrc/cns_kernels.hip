@@ -1209,27 +1209,25 @@ __global__ void __launch_bounds__(CNS_THREADS, G::WGCU) cns_lr_kernel(CnsDev D, 
             Ke[0] = make_int4(rp, D.a_end[g], D.lseq[g] | ((D.aflags[g] & 8) ? (int)0x80000000 : 0), D.a_sb[g]);
             Ke[1] = make_int4(D.a_ce[g] - cbk, i, (int)(uint32_t)(so & 0xFFFFFFFFLL), (int)(so >> 32));
             Ke[2] = make_int4((int)(uint32_t)(cgi & 0xFFFFFFFFLL), (int)(cgi >> 32), 0, 0);
+            // its multi-character states (walk_states: the thread walks its own ops, a kept
+            // alignment per thread -- every thread busy, ~700 independent walks in flight per
+            // read, where a 16-lane group per alignment kept 16 in flight); the state index of
+            // a column is column - rp
+            const SeqV sv = seq_view(D, g);
+            const int sbg = D.a_sb[g];
+            walk_states<true>(D.cig + D.cig_off[g], cbk, D.a_ce[g], rp, 0, 0x7fffffff,
+                              [&](int scol, int, int, int qoff, int slen) {
+                                  const int sqp = sbg + qoff;
+                                  if (slen > 0xFFFF || sqp > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
+                                  const uint64_t k = state_key(sv, sqp, slen);
+                                  const int h = T.insert(k, ((uint64_t)slen << 48) | ((uint64_t)sqp << 32) | (uint64_t)g);
+                                  if (h < 0) { C->flag = 1; return; }
+                                  const unsigned int ord = ((unsigned int)i << 12) | (unsigned int)(scol - rp);
+                                  atomicMin(&T.ord_all[h], ord);
+                                  if (!(nig && in_ign(ig, nig, scol))) atomicMin(&T.ord_cns[h], ord);
+                              });
         }
         __threadfence_block();
-        __syncthreads();
-        // the multi-character states of every kept alignment (walk_states' semantics through
-        // group_states' deferred states: a 16-lane group per alignment, its SEQ in LDS; the
-        // state index of a column is column - rp)
-        stream_kept<G::WGCU >= 4 ? CNS_PD_M : CNS_PD_S>(D, K, 0, C->nk, -1, 0x7fffffff, wops, wseq, snt4, [&](const KeptView &v, int4 *gops, const uint32_t (&cop)[CNS_OPF]) {
-            const int64_t g = a0 + v.i;
-            group_states<false>(D.cig + v.cgi, v.nop, v.rp, v.sb, 0, 0x7fffffff, gops, cop,
-                                [&](int scol, int sqp, int slen) {
-                                    if (slen <= 1) return;
-                                    if (slen > 0xFFFF || sqp > 0xFFFF || g > 0xFFFFFFFFLL) { C->flag = 1; return; }
-                                    const uint64_t k = state_key(v.sv, sqp, slen);
-                                    const int h = T.insert(k, ((uint64_t)slen << 48) | ((uint64_t)sqp << 32) | (uint64_t)g);
-                                    if (h < 0) { C->flag = 1; return; }
-                                    const unsigned int ord = ((unsigned int)v.i << 12) | (unsigned int)(scol - v.rp);
-                                    atomicMin(&T.ord_all[h], ord);
-                                    if (!(nig && in_ign(ig, nig, scol))) atomicMin(&T.ord_cns[h], ord);
-                                },
-                                [&](int, int) {});
-        });
         __syncthreads();
         if (C->flag) {
             CNS_CAP_FAIL();
