@@ -265,7 +265,7 @@ def main():
     log = logs[-1]
     loop_rows = [{"task": e.task, "short_reads": e.n_sr, "seeds_rank": e.n_tasks, "wall_ms": e.wall_ms,
                   "device_ms": e.device_ms, "masked_frac": None if e.masked_frac is None else round(e.masked_frac, 4),
-                  "shortcut": e.shortcut, "stage_event_ms": e.stage_ms, "part_wall_ms": e.part_ms} for e in log]
+                  "shortcut": e.shortcut, "stage_event_ms": e.stage_ms, "part_wall_ms": e.part_ms, "pre_ms": e.pre_ms} for e in log]
     same_tasks = all([e.task for e in lg] == [e.task for e in log] for lg in logs)
 
     if args.loop_only:

@@ -135,6 +135,7 @@ class TaskLog:
     device_ms: Optional[float] = None      # kernel time the device stages report (HIP events), if any
     stage_ms: Optional[Dict[str, float]] = None   # ... per stage (index, seeding, SW, hand-off, consensus)
     part_ms: Optional[Dict[str, float]] = None    # host wall clock per part of the device task (GpuStages)
+    pre_ms: Optional[float] = None         # the task's host time before the stages are called
 
 
 @dataclasses.dataclass
@@ -575,6 +576,7 @@ def run_tasks(stages, srs: ShortReads, tasks: List[str], cfg: LoopConfig, mode: 
         binf = (bsz, bsz * min(cfg.coverage, task_cov)) if cfg.bin_filter else None
         if finish and cfg.keep_masked:
             last_masked = stages.masked()
+        ent.pre_ms = round((time.perf_counter() - t_task) * 1e3, 2)   # (host: sampling and set-up)
         r = stages.task(task, sr, sr_off, params, binf, comm, multi or cfg.exact_layout,
                         None if finish else (hcr_mask_for(task), min_sr), sr_ranges=ranges) if have_reads \
             else TaskOut(0, [])
