@@ -24,6 +24,7 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include "seed_core.h"
 #include "seed_index_dev.h"
@@ -139,6 +140,24 @@ __global__ void ix_kext_kernel(const uint8_t *text, int64_t n, const uint32_t *k
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= (int64_t)koff[NK]) return;   // the hits: the sorted pairs with a valid key
     kext[r] = kext_at(text, n, (int64_t)kpos[r]);
+}
+
+// The positions whose 12 bases are all A/C/G/T, compacted in text order before the sort: the
+// sort then takes 24 key bits (3 onesweep passes instead of 4 for 25, the 25th bit only ever
+// separated the positions without a 12-mer) over fewer pairs (bwa-sr-2's mapping reference is
+// ~70 % N).  off = exclusive scan of the valid flags; ckey / cval: the compacted pairs.
+struct IxValid {
+    __host__ __device__ uint32_t operator()(uint32_t k) const { return k < NK ? 1u : 0u; }
+};
+__global__ void ix_compact_kernel(const uint32_t *key, const uint32_t *off, int64_t n, uint32_t *ckey, uint32_t *cval) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t k = key[p];
+    if (k < NK) {
+        const uint32_t o = off[p];
+        ckey[o] = k;
+        cval[o] = (uint32_t)p;
+    }
 }
 
 // chunked build (texts beyond one sort): the 12-mer histogram of the whole text
@@ -264,10 +283,27 @@ int seed_index_device_build(const SeedIndexBuild &B, hipStream_t s) {
         if (n > 0) {
             hipLaunchKernelGGL(ix_keys_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.key0, B.val0);
             IXCHK(hipGetLastError());
+            // the valid pairs compacted (keys into the kext buffer, free until the kext pass), then
+            // sorted by their 24 key bits into key0 / kpos
             size_t tb = B.temp_bytes;
-            IXCHK(rocprim::radix_sort_pairs(B.temp, tb, B.key0, B.key1, B.val0, B.kpos, (size_t)n, 0u, 25u, s));
-            hipLaunchKernelGGL(ix_koff_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.key1, n, B.koff);
+            auto vit = rocprim::make_transform_iterator(B.key0, IxValid{});
+            IXCHK(rocprim::exclusive_scan(B.temp, tb, vit, B.key1, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+            uint32_t *ckey = reinterpret_cast<uint32_t *>(B.kext);
+            hipLaunchKernelGGL(ix_compact_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.key0, B.key1, n, ckey, B.val0);
             IXCHK(hipGetLastError());
+            uint32_t last[2] = {0u, 0u};   // the scan's last entry and the last key: the valid count
+            IXCHK(hipMemcpyAsync(&last[0], B.key1 + (n - 1), 4, hipMemcpyDeviceToHost, s));
+            IXCHK(hipMemcpyAsync(&last[1], B.key0 + (n - 1), 4, hipMemcpyDeviceToHost, s));
+            IXCHK(hipStreamSynchronize(s));
+            const int64_t nv = (int64_t)last[0] + (last[1] < NK ? 1 : 0);
+            tb = B.temp_bytes;
+            if (nv > 0) IXCHK(rocprim::radix_sort_pairs(B.temp, tb, ckey, B.key0, B.val0, B.kpos, (size_t)nv, 0u, 24u, s));
+            if (nv > 0) {
+                hipLaunchKernelGGL(ix_koff_kernel, dim3(blocks_for(nv, 256)), dim3(256), 0, s, B.key0, nv, B.koff);
+                IXCHK(hipGetLastError());
+            } else {
+                IXCHK(hipMemsetAsync(B.koff, 0, ((size_t)NK + 1) * 8, s));
+            }
             hipLaunchKernelGGL(ix_kc_kernel, dim3(blocks_for((int64_t)NK, 256)), dim3(256), 0, s, B.koff, B.kc);
             IXCHK(hipGetLastError());
             hipLaunchKernelGGL(ix_kext_kernel, dim3(blocks_for(n, 256)), dim3(256), 0, s, B.text, n, B.kpos, B.koff,
@@ -355,7 +391,10 @@ size_t seed_index_temp_bytes(int64_t chunk) {
                                   rocprim::plus<uint32_t>());
     (void)rocprim::radix_sort_pairs(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                     (uint32_t *)nullptr, (size_t)(chunk > 0 ? chunk : 1), 0u, 25u);
-    return std::max(a, std::max(b, c)) + 256;
+    size_t d = 0;   // the valid-position scan of the one-sort build
+    (void)rocprim::exclusive_scan(nullptr, d, rocprim::make_transform_iterator((uint32_t *)nullptr, IxValid{}),
+                                  (uint32_t *)nullptr, 0u, (size_t)(chunk > 0 ? chunk : 1), rocprim::plus<uint32_t>());
+    return std::max(std::max(a, d), std::max(b, c)) + 256;
 }
 
 }  // namespace prgpu
