@@ -1971,6 +1971,10 @@ static int seed_text4(pr_ctx *c, seedc::IndexView &v, hipStream_t s) {
     const int e = ix_pack4_launch(v.text, v.n_text, c->sd[SI_TEXT4].as<uint64_t>(), s);
     if (e) return set_error(PR_ERR_HIP, "text packing: %s", hipGetErrorString((hipError_t)e));
     v.text4 = c->sd[SI_TEXT4].as<uint64_t>();
+    // dense indexes (> 64 hits per 12-mer on average: configs[2] / [3] at one rank's share): the
+    // by-wave pass walks 16 bases per text round trip (seed_wave_kernel<1>: no 5-word buffers,
+    // more waves resident), the others 64 (tools/ab_scale.sh: profiles/r06_walk_ab.txt)
+    v.walk_nw = v.n_text > ((int64_t)64 << 24) ? 1 : 4;
     return 0;
 }
 
@@ -2378,7 +2382,7 @@ extern "C" int pr_seed_gpu_map(pr_ctx *c, const pr_seed_opts *o, const uint8_t *
         if (rc0) return rc0;
         K.dp = D[SB_DP].as<int16_t>();
     }
-    int64_t lanes2 = (int64_t)c->n_cu * seed_slots_per_cu();
+    int64_t lanes2 = (int64_t)c->n_cu * seed_slots_per_cu(c->seed_view.walk_nw);
     const int64_t scratch = std::max<int64_t>(waves * 64 * K.stride, lanes2 * seedc::scratch_bytes(caps));
     const int64_t nb = n_sr ? sr_off[n_sr] : 0;
     // reads are mapped in chunks whose output slabs (caps.out seeds per read) fit a budget

@@ -55,6 +55,9 @@ constexpr int KI = 12;                        // indexed k-mer length
 constexpr uint32_t NK = 1u << (2 * KI);       // 4^12
 constexpr int KX = 28;                        // bases stored after each hit
 constexpr uint64_t KX_MASK = (1ull << (2 * KX)) - 1;
+#ifndef SC_SCANGE   // count jumps past the per-start table (Occ::scan_ge) in smem1 / seed_strategy1
+#define SC_SCANGE 1
+#endif
 constexpr int HB = 20;                        // per-start count table width
 constexpr int CB_SHIFT = 12;                  // contig block table granularity
 constexpr int RK = 11;                        // R_k tabulated per start for k <= RK (split_width + 1)
@@ -91,6 +94,7 @@ struct IndexView {
     const uint32_t *cnt[KI - 1];   // cnt[j-1][code]: occurrences of the j-mer `code`, j = 1..11
     const uint64_t *text4;     // device: the text 16 bases per word (4 bits each) + a padding word, or null
     const BlkFr *blkfr;        // device: [n_text >> CB_SHIFT + 1] block coordinate table, or null
+    int32_t walk_nw = 4;       // device: the match-length walk's 16-base compares per text round trip
 };
 
 struct Iv {
@@ -717,7 +721,7 @@ SC_HD int smem1(const OccT &occ, const Scratch &S, const uint8_t *q, int len, in
             const int n = i + 1 - x;
             int64_t o;
             int skip = 0;   // lengths n + 1 .. n + skip have the same count (Occ::scan_ge)
-            if (have && n >= KI + HB) {
+            if (SC_SCANGE && have && n >= KI + HB) {
                 int mn;
                 o = occ.scan_ge(x, n, mn);
                 skip = mn > n ? mn - n : 0;   // (no read N inside a hit's match: q[x, x + mn) is N-free)
@@ -796,7 +800,7 @@ SC_HD int seed_strategy1(const OccT &occ, const uint8_t *q, int len, int x, int 
         if (i - x >= min_len) {
             const int n = i + 1 - x;
             int mn = 0;
-            const int64_t o = n >= KI + HB ? occ.scan_ge(x, n, mn) : occ(x, i + 1);
+            const int64_t o = SC_SCANGE && n >= KI + HB ? occ.scan_ge(x, n, mn) : occ(x, i + 1);
             if (o < max_intv) {
                 m = Iv{x, i + 1, o};
                 return i + 1;

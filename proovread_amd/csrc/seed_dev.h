@@ -39,7 +39,7 @@ int seed_batch_launch(const SeedDev &D, void *stream);   // pass 1: 64 reads per
 size_t seed_order_bytes(int64_t n);
 int seed_order_launch(const SeedDev &D, int64_t r0, int64_t n, void *buf, int32_t **order, void *stream);
 // resident waves per CU of the seeding kernel (= scratch slots per CU)
-int seed_slots_per_cu();
+int seed_slots_per_cu(int walk_nw);   // pass 2's resident waves per CU (seed_wave_kernel<walk_nw>)
 // dense task list: out[pre[i] + j] = slots[i * cap + j] for j < n_out[i]
 int seed_compact_launch(const pr_seed_task *slots, const int32_t *n_out, const int64_t *pre, int64_t n_sr, int cap,
                         pr_seed_task *out, void *stream);

@@ -66,6 +66,7 @@ __device__ __forceinline__ uint64_t nib16(const uint64_t *w4, uint64_t x) {
     return sh ? (lo >> sh) | (w4[w + 1] << (64 - sh)) : lo;
 }
 
+template <int NW>   // the match-length walk's 16-base compares per text round trip (1 or 4)
 __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, const uint8_t *q, int len, int32_t *ho,
                               int lane, uint64_t *q4, const uint32_t *lc, int *n_hits = nullptr,
                               unsigned long long *ot = nullptr, bool lazy = false) {
@@ -306,20 +307,23 @@ __device__ int build_occ_wave(const seedc::IndexView &V, seedc::Scratch &S, cons
                 int ml = KI + m;
                 if (m == KX) {
                     if (V.text4) {   // 16 bases at a time: the first differing nibble, or a read N, or the read's end
-                        // the text words of 64 bases are loaded together (5 independent loads, the text
-                        // has 8 padding words) and compared from registers: one memory round trip per
-                        // 64 bases instead of one per 16 (the finish task's near-exact reads walk ~110)
+                        // the text words of up to 64 bases are loaded together (5 independent loads, the
+                        // text has 8 padding words) and compared from registers: one memory round trip
+                        // per 64 bases instead of one per 16 (the finish task's near-exact reads walk ~110)
                         bool go = a + ml < len;
+                        // (NW compares per round trip: 1 for dense indexes' by-wave pass, where the
+                        // 5-word buffers cost occupancy, V.walk_nw)
+                        constexpr int nw = NW;
                         while (go) {
                             const uint64_t tp = p[u] + (uint64_t)ml;
                             const uint64_t* tw4 = V.text4 + (tp >> 4);
                             const int sh = (int)(tp & 15) * 4;
                             uint64_t w5[5];
 #pragma unroll
-                            for (int j = 0; j < 5; ++j) w5[j] = tw4[j];
+                            for (int j = 0; j < 5; ++j) w5[j] = j <= nw ? tw4[j] : 0ull;
 #pragma unroll
                             for (int j = 0; j < 4; ++j) {
-                                if (!go) break;
+                                if (!go || j >= nw) break;
                                 const int x = a + ml;
                                 const uint64_t tw = sh ? (w5[j] >> sh) | (w5[j + 1] << (64 - sh)) : w5[j];
                                 const uint64_t qw = nib16(q4, (uint64_t)x);
@@ -734,6 +738,7 @@ __device__ bool chain_flt_wave(const pr_seed_opts &O, seedc::Scratch &S, int ncv
 
 // Pass 2: one wave per read with the large scratch slice (the reads of D.rlist: those that
 // outgrew pass 1's slices), the sequential part on lane 0.
+template <int NW>
 __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(SeedDev D) {
     __shared__ __attribute__((aligned(16))) int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint64_t q4_lds[SEED_WAVES][SEED_LMAX / 16 + 4];
@@ -766,7 +771,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(S
         int err = 0;
         const unsigned long long t0 = D.prof && lane == 0 ? wall_clock64() : 0ULL;
         if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
-        if (len > 0 && !err) err = build_occ_wave(D.V, S, q, len, ho, lane, q4_lds[wv], lcnt);
+        if (len > 0 && !err) err = build_occ_wave<NW>(D.V, S, q, len, ho, lane, q4_lds[wv], lcnt);
         // SMEMs and chaining on lane 0; then, for reads where bwa runs mem_flt_chained_seeds
         // (>= 440 bp), the seeds' local SW scores over all 64 lanes (a seed per lane, the rows
         // int16 and lane-interleaved in the dead count table); the output on lane 0
@@ -912,7 +917,7 @@ __global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_batch_kernel(
             int err = 0, nh = 0;
             if (len > S.lmax || len > SEED_LMAX - 1) err = seedc::SC_OVER_LEN;
             if (len > 0 && !err)
-                err = build_occ_wave(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt, &nh, D.prof ? ot : nullptr,
+                err = build_occ_wave<4>(D.V, S, D.sr_seq + o, len, ho, lane, q4_lds[wv], lcnt, &nh, D.prof ? ot : nullptr,
                                      LZ);
             if (lane == rd) my_err = err, my_hits = nh;
         }
@@ -998,9 +1003,11 @@ int seed_order_launch(const SeedDev &D, int64_t r0, int64_t n, void *buf, int32_
     return 0;
 }
 
-int seed_slots_per_cu() {
+int seed_slots_per_cu(int walk_nw) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, seed_wave_kernel, 64 * SEED_WAVES, 0) != hipSuccess || nb < 1)
+    const hipError_t e = walk_nw == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, seed_wave_kernel<1>, 64 * SEED_WAVES, 0)
+                                      : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, seed_wave_kernel<4>, 64 * SEED_WAVES, 0);
+    if (e != hipSuccess || nb < 1)
         nb = 2;
     return nb * SEED_WAVES;
 }
@@ -1008,7 +1015,10 @@ int seed_slots_per_cu() {
 int seed_launch(const SeedDev &D, void *stream) {
     if (D.n_list <= 0) return 0;
     const int64_t blocks = (D.n_lanes + SEED_WAVES - 1) / SEED_WAVES;
-    hipLaunchKernelGGL(seed_wave_kernel, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
+    if (D.V.walk_nw == 1)
+        hipLaunchKernelGGL(seed_wave_kernel<1>, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
+    else
+        hipLaunchKernelGGL(seed_wave_kernel<4>, dim3((unsigned)blocks), dim3(64 * SEED_WAVES), 0, (hipStream_t)stream, D);
     return (int)hipGetLastError();
 }
 
