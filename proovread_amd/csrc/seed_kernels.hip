@@ -31,6 +31,9 @@ constexpr int SEED_LMAX = SEED_LMAX_DEF;     // LDS start offsets per wave: read
 #ifndef SEED_MINB
 #define SEED_MINB 4
 #endif
+#ifndef SEED_WAVE_MINB   // the by-wave kernel's workgroups per CU (register budget)
+#define SEED_WAVE_MINB SEED_MINB
+#endif
 #ifndef OCC_U
 #define OCC_U 2   // hits per lane per pass of the occurrence table's hit loop
 #endif
@@ -739,7 +742,7 @@ __device__ bool chain_flt_wave(const pr_seed_opts &O, seedc::Scratch &S, int ncv
 // Pass 2: one wave per read with the large scratch slice (the reads of D.rlist: those that
 // outgrew pass 1's slices), the sequential part on lane 0.
 template <int NW>
-__global__ void __launch_bounds__(64 * SEED_WAVES, SEED_MINB) seed_wave_kernel(SeedDev D) {
+__global__ void __launch_bounds__(64 * SEED_WAVES, SEED_WAVE_MINB) seed_wave_kernel(SeedDev D) {
     __shared__ __attribute__((aligned(16))) int32_t hoff_lds[SEED_WAVES][SEED_LMAX + 4];
     __shared__ uint64_t q4_lds[SEED_WAVES][SEED_LMAX / 16 + 4];
     __shared__ uint32_t lcnt[seedc::LC_N];
