@@ -1975,6 +1975,8 @@ static int seed_text4(pr_ctx *c, seedc::IndexView &v, hipStream_t s) {
     // by-wave pass walks 16 bases per text round trip (seed_wave_kernel<1>: no 5-word buffers,
     // more waves resident), the others 64 (tools/ab_scale.sh: profiles/r06_walk_ab.txt)
     v.walk_nw = v.n_text > ((int64_t)64 << 24) ? 1 : 4;
+    if (const char *w = getenv("PRGPU_SEED_WALK_NW"))   // tuning hook: 1 or 4
+        v.walk_nw = atoi(w) == 1 ? 1 : 4;
     return 0;
 }
 
